@@ -1,0 +1,158 @@
+"""Numerics of every native HIP kernel vs a plain PyTorch fp32/fp64 reference (GPU only)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    import torch_distributed_sandbox_amd as tds
+
+    return tds._ext.ops()
+
+
+def _close(a, b, rtol=1e-4, atol=1e-5):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    scale = b.abs().max().item() + 1e-12
+    err = (a - b).abs().max().item()
+    assert err <= atol + rtol * scale, f"max abs err {err:.3e} vs scale {scale:.3e}"
+
+
+def test_relu(gpu):
+    x = torch.randn(3, 5, 33, 17, device=gpu)
+    y = _ops().relu_fwd(x)
+    _close(y, F.relu(x), 0, 0)
+    g = torch.randn_like(x)
+    _close(_ops().relu_bwd(g, y), g * (x > 0), 0, 0)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 8, 8), (1, 4, 37, 70), (3, 2, 5, 9)])
+def test_maxpool(gpu, shape):
+    x = torch.randn(*shape, device=gpu)
+    y, idx = _ops().maxpool2_fwd(x)
+    ref, ref_idx = F.max_pool2d(x, 2, 2, return_indices=True)
+    _close(y, ref, 0, 0)
+    gy = torch.randn_like(y)
+    gx = _ops().maxpool2_bwd(gy, idx, shape[2], shape[3])
+    xr = x.clone().requires_grad_(True)
+    F.max_pool2d(xr, 2, 2).backward(gy)
+    _close(gx, xr.grad, 0, 0)
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(1, 16, 40, 70), (16, 32, 23, 131), (3, 5, 9, 9), (16, 32, 64, 64)])
+def test_conv_fwd_bwd(gpu, cin, cout, h, w):
+    torch.manual_seed(0)
+    x = torch.randn(2, cin, h, w, device=gpu)
+    wt = torch.randn(cout, cin, 5, 5, device=gpu) * 0.1
+    b = torch.randn(cout, device=gpu)
+    y = _ops().conv2d_fwd(x, wt, b, 2)
+    ref = F.conv2d(x.double().cpu(), wt.double().cpu(), b.double().cpu(), padding=2)
+    _close(y, ref, 1e-5, 1e-5)
+    gy = torch.randn_like(y)
+    xr = x.double().cpu().requires_grad_(True)
+    wr = wt.double().cpu().requires_grad_(True)
+    br = b.double().cpu().requires_grad_(True)
+    F.conv2d(xr, wr, br, padding=2).backward(gy.double().cpu())
+    dx = _ops().conv2d_dgrad(gy, wt, 2)
+    _close(dx, xr.grad, 1e-5, 1e-5)
+    dw, db = _ops().conv2d_wgrad(x, gy, 5, 2, True)
+    _close(dw, wr.grad, 1e-5, 1e-4)
+    _close(db, br.grad, 1e-5, 1e-4)
+
+
+def test_batchnorm_train(gpu):
+    torch.manual_seed(0)
+    x = torch.randn(4, 6, 19, 23, device=gpu) * 3 + 1.5
+    g = torch.rand(6, device=gpu) + 0.5
+    be = torch.randn(6, device=gpu)
+    rm, rv = torch.zeros(6, device=gpu), torch.ones(6, device=gpu)
+    nb = torch.zeros((), dtype=torch.long, device=gpu)
+    y, mean, invstd = _ops().bn_fwd_train(x, g, be, rm, rv, nb, 0.1, 1e-5, False)
+    rm2, rv2 = torch.zeros(6, dtype=torch.float64), torch.ones(6, dtype=torch.float64)
+    xr = x.double().cpu().requires_grad_(True)
+    gr = g.double().cpu().requires_grad_(True)
+    br = be.double().cpu().requires_grad_(True)
+    ref = F.batch_norm(xr, rm2, rv2, gr, br, True, 0.1, 1e-5)
+    _close(y, ref, 1e-5, 1e-5)
+    _close(rm, rm2, 1e-5, 1e-6)
+    _close(rv, rv2, 1e-5, 1e-6)
+    assert int(nb.item()) == 1
+    gy = torch.randn_like(x)
+    ref.backward(gy.double().cpu())
+    dx, dg, db = _ops().bn_bwd(gy, x, g, mean, invstd, True)
+    _close(dx, xr.grad, 1e-4, 1e-5)
+    _close(dg, gr.grad, 1e-5, 1e-4)
+    _close(db, br.grad, 1e-5, 1e-4)
+    # eval
+    ye = _ops().bn_fwd_eval(x, g, be, rm, rv, 1e-5, True)
+    _close(ye, F.relu(F.batch_norm(x, rm, rv, g, be, False, 0.1, 1e-5)), 1e-5, 1e-5)
+
+
+@pytest.mark.parametrize("m,n,k", [(5, 10, 4096 * 3 + 4), (3, 7, 1001), (8, 16, 100000)])
+def test_linear(gpu, m, n, k):
+    torch.manual_seed(0)
+    x = torch.randn(m, k, device=gpu)
+    w = torch.randn(n, k, device=gpu) * 0.01
+    b = torch.randn(n, device=gpu)
+    y = _ops().linear_fwd(x, w, b)
+    _close(y, F.linear(x.double(), w.double(), b.double()), 1e-5, 1e-5)
+    gy = torch.randn(m, n, device=gpu)
+    dw = torch.empty_like(w)
+    db = torch.empty_like(b)
+    dx = _ops().linear_bwd_into(gy, x, w, dw, db, 1.0, False, True)
+    _close(dx, gy.double() @ w.double(), 1e-5, 1e-5)
+    _close(dw, gy.double().t() @ x.double(), 1e-5, 1e-5)
+    _close(db, gy.double().sum(0), 1e-5, 1e-6)
+    # scaled accumulate into existing buffer
+    dw2 = dw.clone()
+    _ops().linear_bwd_into(gy, x, w, dw2, None, 0.5, True, False)
+    _close(dw2, dw.double() * 1.5, 1e-5, 1e-5)
+
+
+def test_cross_entropy(gpu):
+    torch.manual_seed(0)
+    z = torch.randn(5, 10, device=gpu) * 3
+    lab = torch.tensor([1, 0, 9, -100, 4], device=gpu)
+    loss, dz = _ops().cross_entropy(z, lab, -100, 0.0)
+    zr = z.double().cpu().requires_grad_(True)
+    ref = F.cross_entropy(zr, lab.cpu())
+    ref.backward()
+    _close(loss, ref, 1e-6, 1e-6)
+    _close(dz, zr.grad, 1e-6, 1e-6)
+    loss2, dz2 = _ops().cross_entropy(z, lab, -100, 0.1)
+    zr2 = z.double().cpu().requires_grad_(True)
+    ref2 = F.cross_entropy(zr2, lab.cpu(), label_smoothing=0.1)
+    ref2.backward()
+    _close(loss2, ref2, 1e-6, 1e-6)
+    _close(dz2, zr2.grad, 1e-6, 1e-6)
+
+
+def test_sgd(gpu):
+    ps = [torch.randn(n, device=gpu) for n in (7, 1000, 33)]
+    gs = [torch.randn_like(p) for p in ps]
+    ref = [p - 0.1 * g for p, g in zip(ps, gs)]
+    _ops().sgd_step_(ps, gs, [], 0.1, 0.0, 0.0, 0.0, False, False)
+    for a, b in zip(ps, ref):
+        _close(a, b, 1e-6, 1e-7)
+    ms = [torch.zeros_like(p) for p in ps]
+    p2 = [p.clone() for p in ps]
+    _ops().sgd_step_(ps, gs, ms, 0.1, 0.01, 0.9, 0.0, False, True)
+    tp = [p.cpu().clone().requires_grad_(False) for p in p2]
+    opt = torch.optim.SGD(tp, lr=0.1, momentum=0.9, weight_decay=0.01)
+    for t, g in zip(tp, gs):
+        t.grad = g.cpu()
+    opt.step()
+    for a, b in zip(ps, tp):
+        _close(a, b, 1e-6, 1e-6)
+
+
+def test_upsample(gpu):
+    src = torch.randint(0, 256, (3, 28, 28), dtype=torch.uint8, device=gpu)
+    y = _ops().upsample_bilinear_u8(src, 300, 301)
+    ref = F.interpolate(src.float().unsqueeze(1).cpu().double(), size=(300, 301), mode="bilinear",
+                        align_corners=False).round().clamp(0, 255) / 255.0
+    # bilinear weights in fp32 vs fp64 may round a half differently: <= 1 LSB
+    assert (y.double().cpu() - ref).abs().max().item() <= 1.0 / 255 + 1e-6
+    assert ((y.double().cpu() - ref).abs() > 1e-6).float().mean().item() < 1e-3

@@ -1,0 +1,75 @@
+// Shared device helpers for the gfx950 (MI355X, CDNA4) kernels.
+//
+// Everything here assumes wave64: lane = threadIdx.x & 63, 64-bit ballots,
+// shuffles over 64 lanes.  No CUDA spellings, no dual paths.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TDS_WAVE 64
+
+namespace tds {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (TDS_WAVE - 1); }
+__device__ __forceinline__ int wave_id() { return threadIdx.x / TDS_WAVE; }
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, TDS_WAVE);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    T o = __shfl_xor(v, off, TDS_WAVE);
+    v = v > o ? v : o;
+  }
+  return v;
+}
+
+// Block-wide sum of one value per thread; result valid in every thread.
+// `scratch` must hold blockDim.x / 64 elements.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+  v = wave_sum(v);
+  const int nw = blockDim.x / TDS_WAVE;
+  __syncthreads();
+  if (lane_id() == 0) scratch[wave_id()] = v;
+  __syncthreads();
+  T r = 0;
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  return r;
+}
+
+// Round-to-nearest-even f32 -> bf16 bits (finite inputs; NaN stays NaN via cast path).
+__device__ __forceinline__ unsigned short f32_to_bf16_bits(float f) {
+  unsigned int u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+__device__ __forceinline__ float bf16_bits_to_f32(unsigned short h) {
+  return __uint_as_float(((unsigned int)h) << 16);
+}
+
+// XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): consecutive logical tiles land on the same XCD so neighbours
+// share that XCD's L2.  Speed only; correctness never depends on placement.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int nx = 8;
+  if (nwg < nx) return orig;
+  const int q = nwg / nx, r = nwg % nx;
+  const int x = orig % nx;
+  const int base = (x < r) ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+  return base + orig / nx;
+}
+
+}  // namespace tds

@@ -1,0 +1,56 @@
+// Host-side launch entry points of the gfx950 kernels.  Plain C++ (pointers +
+// hipStream_t), no torch types, so the .hip translation units build without
+// torch headers and the binding layer (csrc/ops.cpp) owns all tensor checks.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// ---- elementwise.hip
+void tds_relu_fwd(const float* x, float* y, int64_t n, hipStream_t st);
+void tds_relu_bwd(const float* g, const float* out, float* dx, int64_t n, hipStream_t st);
+void tds_maxpool2_fwd(const float* x, float* y, uint8_t* idx, int64_t planes, int H, int W, hipStream_t st);
+void tds_maxpool2_bwd(const float* gy, const uint8_t* idx, float* gx, int64_t planes, int H, int W, hipStream_t st);
+void tds_upsample_bilinear_u8(const uint8_t* src, float* dst, int B, int h, int w, int H, int W, hipStream_t st);
+
+#define TDS_SGD_MAX_TENSORS 48
+struct SgdChunkTable {
+  float* param[TDS_SGD_MAX_TENSORS];
+  const float* grad[TDS_SGD_MAX_TENSORS];
+  float* mom[TDS_SGD_MAX_TENSORS];
+  int64_t numel[TDS_SGD_MAX_TENSORS];
+  int n;
+};
+void tds_sgd_multi(const SgdChunkTable& tab, float lr, float wd, float momentum, float dampening, int nesterov,
+                   int first_step, int64_t max_numel, hipStream_t st);
+void tds_cross_entropy(const float* logits, const int64_t* labels, float* row_loss, float* dlogits, float* loss,
+                       float* inv_count, int M, int N, int64_t ignore_index, float label_smoothing, hipStream_t st);
+void tds_scale_by_device_scalar(const float* in, const float* s, float* out, int64_t n, hipStream_t st);
+
+// ---- conv_generic.hip (NCHW fp32, stride 1, square kernel)
+int tds_conv2d_fwd_f32(const float* in, const float* w, const float* bias, float* out, int B, int Cin, int Cout, int H,
+                       int W, int KS, int P, hipStream_t st);
+void tds_conv2d_flip_weights(const float* w, float* wt, int Cout, int Cin, int KS, hipStream_t st);
+int64_t tds_conv2d_wgrad_f32(const float* in, const float* g, float* dw, float* db, float* slab, int B, int Cin,
+                             int Cout, int H, int W, int KS, int P, float scale, int accumulate, int num_wg,
+                             hipStream_t st);
+
+// ---- batchnorm.hip (NCHW fp32)
+int tds_bn_num_chunks(int B, int C, int64_t HW);
+void tds_bn_fwd_train(const float* x, int B, int C, int64_t HW, float eps, float momentum, const float* gamma,
+                      const float* beta, float* save_mean, float* save_invstd, float* running_mean, float* running_var,
+                      int64_t* num_batches, float* aff_a, float* aff_b, double* partial, int nchunk, hipStream_t st);
+void tds_bn_eval_affine(const float* rm, const float* rv, int C, float eps, const float* gamma, const float* beta,
+                        float* aff_a, float* aff_b, hipStream_t st);
+void tds_bn_apply(const float* x, const float* aff_a, const float* aff_b, float* y, int B, int C, int64_t HW, int relu,
+                  hipStream_t st);
+void tds_bn_bwd(const float* dy, const float* x, int B, int C, int64_t HW, const float* gamma, const float* mean,
+                const float* invstd, float* dx, float* dgamma, float* dbeta, float* kbuf, double* partial, int nchunk,
+                hipStream_t st);
+
+// ---- linear.hip (skinny M<=8, N<=16)
+int tds_linear_fwd_nblk(int64_t K);
+int tds_linear_fwd_skinny(const float* x, const float* W, const float* bias, float* out, float* partial, int M, int N,
+                          int64_t K, int nblk, hipStream_t st);
+int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float* dx, float* dW, float* db, int M,
+                          int N, int64_t K, float scale, int acc_w, hipStream_t st);

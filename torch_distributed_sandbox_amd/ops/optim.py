@@ -1,0 +1,91 @@
+"""SGD with a multi-tensor gfx950 kernel (``torch.optim.SGD(params, lr)``, mnist_onegpu.py:49).
+
+One launch updates every parameter (tensor table in the kernel arguments,
+SURVEY.md §2.4 K26).  When the parameters live in one flat buffer (as laid
+out by ``parallel.ddp.DistributedDataParallel``), the update is a single
+contiguous sweep over that buffer and its flat gradient bucket.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import _ext
+
+
+class SGD(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False):
+        if lr < 0.0:
+            raise ValueError(f"Invalid learning rate: {lr}")
+        if nesterov and (momentum <= 0 or dampening != 0):
+            raise ValueError("Nesterov momentum requires a momentum and zero dampening")
+        defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay, nesterov=nesterov)
+        super().__init__(params, defaults)
+        self._flat = None  # (flat_param, flat_grad) when installed by DDP
+
+    def set_flat_buffers(self, flat_param: torch.Tensor, flat_grad: torch.Tensor, params):
+        """Declare that ``params`` are views of ``flat_param`` with grads in ``flat_grad``."""
+        ids = {id(p) for g in self.param_groups for p in g["params"]}
+        if ids == {id(p) for p in params} and len(self.param_groups) == 1:
+            self._flat = (flat_param, flat_grad, list(params))
+        else:
+            self._flat = None
+
+    def _flat_ok(self):
+        if self._flat is None:
+            return False
+        fp, fg, params = self._flat
+        for p in params:
+            if p.grad is None:
+                return False
+            # grads must still be views of the flat bucket
+            if p.grad.untyped_storage().data_ptr() != fg.untyped_storage().data_ptr():
+                return False
+        return True
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        for group in self.param_groups:
+            lr, mom, damp = group["lr"], group["momentum"], group["dampening"]
+            wd, nest = group["weight_decay"], group["nesterov"]
+            if (self._flat is not None and mom == 0.0 and wd == 0.0 and self._flat_ok() and self._flat[0].is_cuda):
+                fp, fg, _ = self._flat
+                _ext.ops().sgd_step_([fp], [fg], [], lr, 0.0, 0.0, 0.0, False, False)
+                continue
+            params, grads, bufs, first = [], [], [], False
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                params.append(p)
+                grads.append(p.grad)
+                if mom != 0.0:
+                    st = self.state[p]
+                    if "momentum_buffer" not in st:
+                        st["momentum_buffer"] = torch.zeros_like(p)
+                        first = True
+                    bufs.append(st["momentum_buffer"])
+            if not params:
+                continue
+            if params[0].is_cuda:
+                ok = all(p.is_contiguous() and g.is_contiguous() and p.dtype == torch.float32 for p, g in
+                         zip(params, grads))
+                if ok:
+                    _ext.ops().sgd_step_(params, grads, bufs, lr, wd, mom, damp, nest, first)
+                    continue
+            # CPU / non-contiguous reference path (torch.optim.SGD semantics)
+            for i, p in enumerate(params):
+                d = grads[i]
+                if wd != 0.0:
+                    d = d.add(p, alpha=wd)
+                if mom != 0.0:
+                    b = bufs[i]
+                    if first:
+                        b.copy_(d)
+                    else:
+                        b.mul_(mom).add_(d, alpha=1.0 - damp)
+                    d = d.add(b, alpha=mom) if nest else b
+                p.add_(d, alpha=-lr)
+        return loss

@@ -1,0 +1,265 @@
+"""DistributedDataParallel for one-process-per-GPU training over RCCL/xGMI.
+
+API mirrors ``torch.nn.parallel.DistributedDataParallel(model, device_ids=[gpu])``
+(mnist_distributed.py:67) and reproduces its semantics:
+rank-0 parameter/buffer broadcast at construction (C5), rank-0 buffer
+broadcast before every forward when ``broadcast_buffers`` (C6), gradients
+averaged over ranks with bucketed asynchronous all-reduce overlapped with the
+backward (C7/C8), ``no_sync()`` for accumulation.
+
+What is different (MI355X-first):
+
+* **Flat parameter + gradient buffers.**  Parameters are re-homed into one
+  flat buffer (``param.data`` becomes a view; the Parameter objects — and so
+  optimizer references and state_dict names — are unchanged) and gradients
+  live in a flat bucket buffer with the same layout.  Broadcast at
+  construction is one call, the optimizer step is one sweep
+  (``ops.optim.SGD``), and there is no copy-in/copy-out of gradients
+  (torch's reducer does ``grad * 1/W`` into the bucket and copies back,
+  SURVEY.md §2.4 K15).
+* **Gradient sinks.**  Backward kernels that support it (the skinny Linear and
+  the fused ConvNet plan) write weight gradients straight into their bucket
+  slot (``ops/grad_sink.py``).
+* **Averaging in the collective.**  Buckets are all-reduced with ``AVG``
+  (``ncclAvg`` in RCCL) instead of being pre-scaled by 1/W in a separate pass.
+* **Static bucket order** = reverse parameter order (the order gradients
+  become ready), so there is no iteration-0 single-bucket pass and no bucket
+  rebuild.
+* Buckets follow torch's size rule (add a tensor, close the bucket once it
+  reaches ``bucket_cap_mb``, default 25), which for the ConvNet gives the
+  measured reference layout ``[[fc.bias, fc.weight], [8 conv/BN tensors]]``:
+  the 720 MB fc gradient goes out as soon as the fc backward finishes and
+  overlaps the whole conv backward.
+"""
+from __future__ import annotations
+
+import contextlib
+import hashlib
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from ..ops import grad_sink
+from . import distributed as tdist
+
+_ALIGN_ELEMS = 64  # 256-byte alignment of every parameter slot in the flat buffers
+
+
+def _align(n: int) -> int:
+    return (n + _ALIGN_ELEMS - 1) // _ALIGN_ELEMS * _ALIGN_ELEMS
+
+
+class _Bucket:
+    __slots__ = ("index", "params", "offset", "numel", "pending", "work", "ready")
+
+    def __init__(self, index, offset):
+        self.index, self.params, self.offset, self.numel = index, [], offset, 0
+        self.pending, self.work, self.ready = 0, None, False
+
+
+class DistributedDataParallel(nn.Module):
+    def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
+                 process_group=None, bucket_cap_mb: Optional[float] = None, find_unused_parameters: bool = False,
+                 gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False):
+        super().__init__()
+        self.module = module
+        self.device_ids = device_ids
+        self.broadcast_buffers = broadcast_buffers
+        self.process_group = process_group
+        self.find_unused_parameters = find_unused_parameters
+        self.world_size = tdist.get_world_size(process_group)
+        self.rank = tdist.get_rank(process_group)
+        self.require_backward_grad_sync = True
+        self._params: List[nn.Parameter] = [p for p in module.parameters() if p.requires_grad]
+        if not self._params:
+            raise RuntimeError("DistributedDataParallel: module has no parameters that require grad")
+        dev = self._params[0].device
+        dtype = self._params[0].dtype
+        for p in self._params:
+            if p.device != dev or p.dtype != dtype:
+                raise RuntimeError("DistributedDataParallel: all parameters must share one device and dtype")
+        self.device = dev
+        self._verify_param_shapes()
+
+        # ---- flat layout in gradient-ready order (reverse definition order)
+        order = list(reversed(self._params))
+        cap_mb = 25.0 if bucket_cap_mb is None else float(bucket_cap_mb)
+        limit = max(1, int(cap_mb * 1024 * 1024 // self._params[0].element_size()))
+        self._slots = {}  # id(param) -> (offset, numel)
+        self._buckets: List[_Bucket] = []
+        off = 0
+        cur = _Bucket(0, 0)
+        for p in order:
+            # torch's _compute_bucket_assignment_by_size: add, then close once >= cap
+            n = p.numel()
+            self._slots[id(p)] = (off, n)
+            cur.params.append(p)
+            off += _align(n)
+            cur.numel = off - cur.offset
+            if cur.numel >= limit:
+                self._buckets.append(cur)
+                cur = _Bucket(len(self._buckets), off)
+        if cur.params:
+            self._buckets.append(cur)
+        self._total = off
+        self._bucket_of = {id(p): b for b in self._buckets for p in b.params}
+
+        with torch.no_grad():
+            self.flat_grad = torch.zeros(self._total, device=dev, dtype=dtype)
+            if flat_params:
+                self.flat_param = torch.zeros(self._total, device=dev, dtype=dtype)
+                for p in order:
+                    o, n = self._slots[id(p)]
+                    self.flat_param[o:o + n].copy_(p.detach().reshape(-1))
+                    p.data = self.flat_param[o:o + n].view_as(p)
+            else:
+                self.flat_param = None
+
+        # ---- rank-0 state broadcast: one call for all params
+        self._sync_module_states()
+
+        # ---- gradient sinks + readiness hooks
+        for p in self._params:
+            grad_sink.register(p, self._make_view_fn(p))
+        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self._params]
+        self._callback_queued = False
+
+    # ------------------------------------------------------------------ setup helpers
+    def _make_view_fn(self, p):
+        o, n = self._slots[id(p)]
+        shape = p.shape
+        flat = self.flat_grad
+
+        def view():
+            return flat.narrow(0, o, n).view(shape)
+
+        return view
+
+    def grad_view(self, p):
+        o, n = self._slots[id(p)]
+        return self.flat_grad.narrow(0, o, n).view(p.shape)
+
+    def _verify_param_shapes(self):
+        """Same check as torch's _verify_param_shape_across_processes (C4): a hash
+        of every parameter shape, compared with MAX/MIN all-reduces."""
+        if self.world_size == 1:
+            return
+        h = hashlib.sha1(repr([tuple(p.shape) for p in self._params]).encode()).digest()
+        v = int.from_bytes(h[:7], "little")
+        dev = self.device if self.device.type == "cuda" else torch.device("cpu")
+        t = torch.tensor([v, -v], dtype=torch.int64, device=dev)
+        tdist.all_reduce(t, tdist.ReduceOp.MAX, group=self.process_group)
+        if int(t[0].item()) != v or int(t[1].item()) != -v:
+            raise RuntimeError("DistributedDataParallel: parameter shapes differ across ranks")
+
+    def _sync_module_states(self):
+        if self.world_size == 1:
+            return
+        with torch.no_grad():
+            if self.flat_param is not None:
+                tdist.broadcast(self.flat_param, 0, group=self.process_group)
+            else:
+                for p in self._params:
+                    tdist.broadcast(p.data, 0, group=self.process_group)
+            self._broadcast_buffers_now()
+
+    def _broadcast_buffers_now(self):
+        bufs = [b for b in self.module.buffers() if b is not None]
+        if not bufs:
+            return
+        by_dtype = {}
+        for b in bufs:
+            by_dtype.setdefault((b.dtype, b.device), []).append(b)
+        for (_, _), group in by_dtype.items():
+            flat = torch.cat([b.reshape(-1) for b in group])
+            tdist.broadcast(flat, 0, group=self.process_group)
+            o = 0
+            for b in group:
+                n = b.numel()
+                b.copy_(flat[o:o + n].view_as(b))
+                o += n
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, *args, **kwargs):
+        if self.broadcast_buffers and self.world_size > 1:
+            with torch.no_grad():
+                self._broadcast_buffers_now()  # C6: rank-0 BN running stats each forward
+        self._reset_bucket_state()
+        return self.module(*args, **kwargs)
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.require_backward_grad_sync
+        self.require_backward_grad_sync = False
+        try:
+            yield
+        finally:
+            self.require_backward_grad_sync = old
+
+    # ------------------------------------------------------------------ backward
+    def _reset_bucket_state(self):
+        for b in self._buckets:
+            b.pending = len(b.params)
+            b.work = None
+            b.ready = False
+        self._callback_queued = False
+
+    def _on_grad_ready(self, p):
+        o, n = self._slots[id(p)]
+        view = self.flat_grad.narrow(0, o, n)
+        g = p.grad
+        if g is None:
+            return
+        if not (g.data_ptr() == view.data_ptr() and g.is_contiguous()):
+            # a producer without a sink: copy into the bucket once and re-point .grad
+            with torch.no_grad():
+                view.copy_(g.reshape(-1))
+            p.grad = view.view(p.shape)
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+        b = self._bucket_of[id(p)]
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch(b)
+
+    def _launch(self, b: _Bucket):
+        b.ready = True
+        if self.world_size == 1 or not self.require_backward_grad_sync:
+            return
+        seg = self.flat_grad.narrow(0, b.offset, b.numel)
+        b.work = tdist.all_reduce(seg, tdist.ReduceOp.AVG, group=self.process_group, async_op=True)
+
+    def _finalize_backward(self):
+        for b in self._buckets:
+            if not b.ready:
+                if not self.find_unused_parameters:
+                    missing = [i for i, p in enumerate(b.params) if p.grad is None]
+                    raise RuntimeError(
+                        f"DistributedDataParallel: bucket {b.index} never became ready ({len(missing)} params got no "
+                        "gradient); pass find_unused_parameters=True if parts of the model are unused")
+                # unused params: their slots hold zeros / stale values -> zero and launch
+                for p in b.params:
+                    if p.grad is None:
+                        v = self.grad_view(p)
+                        v.zero_()
+                        p.grad = v
+                self._launch(b)
+        for b in self._buckets:
+            if b.work is not None:
+                b.work.wait()
+                b.work = None
+        self._callback_queued = False
+
+    # ------------------------------------------------------------------ misc
+    def bucket_layout(self):
+        """[(bucket index, bytes, [param shapes])] — for tests and logs."""
+        return [(b.index, b.numel * self.flat_grad.element_size(), [tuple(p.shape) for p in b.params])
+                for b in self._buckets]
+
+    def attach_optimizer(self, optimizer):
+        """Let ``ops.optim.SGD`` update the flat buffer in one sweep."""
+        if self.flat_param is not None and hasattr(optimizer, "set_flat_buffers"):
+            optimizer.set_flat_buffers(self.flat_param, self.flat_grad, self._params)
+        return optimizer

@@ -1,0 +1,218 @@
+"""torch.distributed-style process-group API.
+
+Same call surface the reference uses — ``init_process_group``, ``new_group``,
+``all_reduce``, ``barrier``, ``destroy_process_group``, ``ReduceOp`` — plus the
+collectives DDP needs (``broadcast``, ``all_gather``, ``reduce_scatter``).
+
+Backends
+--------
+``"rccl"`` / ``"nccl"``  device collectives over RCCL/xGMI (torch's ProcessGroupNCCL
+                         *is* RCCL on ROCm).  One process per GPU.
+``"gloo"``               CPU collectives (tests / CPU rehearsals).
+``"host"``               this package's C++ TCP ring backend (``csrc/comm``),
+                         registered with torch.distributed as a custom backend.
+``None``                 ``rccl`` when a GPU is visible, else ``gloo``
+                         (the reference's auto-switch, test_init.py:84-88).
+
+Fixes vs the reference (documented deviations):
+
+* ``new_group(ranks)`` is cached by (ranks, backend): the reference creates a
+  new communicator every step (allreduce_toy.py:26-27, mnist_distributed.py:99-100);
+  we keep its semantics (all ranks must call it) without the per-step init.
+* ``init_method`` / ``MASTER_ADDR`` / ``MASTER_PORT`` are honoured for
+  multi-node (the reference hard-codes loopback, mnist_distributed.py:124-125).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+DEFAULT_TIMEOUT = datetime.timedelta(minutes=10)  # torch's default_pg_nccl_timeout
+
+
+class ReduceOp:
+    SUM = dist.ReduceOp.SUM
+    AVG = dist.ReduceOp.AVG
+    MAX = dist.ReduceOp.MAX
+    MIN = dist.ReduceOp.MIN
+    PRODUCT = dist.ReduceOp.PRODUCT
+
+
+_state = {
+    "backend": None,  # normalised backend name
+    "groups": {},  # (ranks tuple, backend) -> ProcessGroup
+}
+
+
+def _normalise_backend(backend: Optional[str]) -> str:
+    if backend is None or backend == "auto":
+        return "rccl" if torch.cuda.is_available() else "gloo"
+    b = backend.lower()
+    if b in ("nccl", "rccl", "cuda", "hip"):
+        return "rccl"
+    if b in ("gloo", "cpu"):
+        return "gloo"
+    if b == "host":
+        return "host"
+    raise ValueError(f"unknown backend {backend!r} (expected rccl|nccl|gloo|host)")
+
+
+def _torch_backend(b: str) -> str:
+    if b == "rccl":
+        return "nccl"
+    if b == "host":
+        from . import host_backend
+
+        host_backend.register()
+        return host_backend.BACKEND_NAME
+    return b
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def init_process_group(backend: Optional[str] = None, init_method: Optional[str] = None, rank: Optional[int] = None,
+                       world_size: Optional[int] = None, timeout: datetime.timedelta = DEFAULT_TIMEOUT,
+                       device_id: Optional[int] = None, store=None) -> None:
+    """Initialise the default group.  ``rank``/``world_size`` default to the
+    ``RANK``/``WORLD_SIZE`` environment (torchrun); ``init_method`` defaults to
+    ``env://`` (``MASTER_ADDR``/``MASTER_PORT``)."""
+    b = _normalise_backend(backend)
+    if rank is None:
+        rank = int(os.environ.get("RANK", "0"))
+    if world_size is None:
+        world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    kwargs = dict(backend=_torch_backend(b), rank=rank, world_size=world_size, timeout=timeout)
+    if store is not None:
+        kwargs["store"] = store
+    else:
+        if init_method is None:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            init_method = "env://"
+        kwargs["init_method"] = init_method
+    if b == "rccl":
+        if device_id is None:
+            device_id = int(os.environ.get("LOCAL_RANK", rank % max(1, torch.cuda.device_count())))
+        torch.cuda.set_device(device_id)
+        # eager communicator init (bound to this GPU) instead of lazy first-collective init
+        kwargs["device_id"] = torch.device("cuda", device_id)
+    dist.init_process_group(**kwargs)
+    _state["backend"] = b
+    _state["groups"] = {}
+
+
+def destroy_process_group(group=None) -> None:
+    if not is_initialized():
+        return
+    if group is None:
+        _state["groups"] = {}
+        _state["backend"] = None
+        dist.destroy_process_group()
+    else:
+        for k, g in list(_state["groups"].items()):
+            if g is group:
+                del _state["groups"][k]
+        dist.destroy_process_group(group)
+
+
+def get_rank(group=None) -> int:
+    return dist.get_rank(group) if is_initialized() else 0
+
+
+def get_world_size(group=None) -> int:
+    return dist.get_world_size(group) if is_initialized() else 1
+
+
+def get_backend(group=None) -> Optional[str]:
+    return _state["backend"] if is_initialized() else None
+
+
+def new_group(ranks: Optional[Sequence[int]] = None, backend: Optional[str] = None, timeout=DEFAULT_TIMEOUT):
+    """Collective over the default group (like torch), cached by (ranks, backend)."""
+    world = get_world_size()
+    key_ranks = tuple(sorted(ranks)) if ranks is not None else tuple(range(world))
+    b = _normalise_backend(backend) if backend is not None else _state["backend"]
+    key = (key_ranks, b)
+    g = _state["groups"].get(key)
+    if g is None:
+        if key_ranks == tuple(range(world)) and b == _state["backend"]:
+            g = dist.group.WORLD
+        else:
+            g = dist.new_group(ranks=list(key_ranks), backend=_torch_backend(b), timeout=timeout)
+        _state["groups"][key] = g
+    return g
+
+
+def _needs_avg_emulation(group) -> bool:
+    b = dist.get_backend(group)
+    return b != "nccl"
+
+
+def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool = False):
+    """In-place all-reduce.  AVG is native on RCCL (ncclAvg) and emulated as
+    SUM + divide elsewhere (gloo has no AVG)."""
+    if op == ReduceOp.AVG and _needs_avg_emulation(group):
+        work = dist.all_reduce(tensor, op=ReduceOp.SUM, group=group, async_op=async_op)
+        n = get_world_size(group)
+        if async_op:
+            return _PostOpWork(work, lambda: _div_(tensor, n))
+        _div_(tensor, n)
+        return None
+    return dist.all_reduce(tensor, op=op, group=group, async_op=async_op)
+
+
+def _div_(t: torch.Tensor, n: int):
+    if t.is_floating_point():
+        t.div_(n)
+    else:
+        t.floor_divide_(n)
+
+
+class _PostOpWork:
+    def __init__(self, work, fn):
+        self._work, self._fn, self._done = work, fn, False
+
+    def wait(self, timeout=None):
+        if timeout is None:
+            self._work.wait()
+        else:
+            self._work.wait(timeout)
+        if not self._done:
+            self._fn()
+            self._done = True
+        return True
+
+    def is_completed(self):
+        return self._work.is_completed()
+
+
+def broadcast(tensor: torch.Tensor, src: int = 0, group=None, async_op: bool = False):
+    return dist.broadcast(tensor, src=src, group=group, async_op=async_op)
+
+
+def all_gather(tensor_list, tensor, group=None, async_op: bool = False):
+    return dist.all_gather(tensor_list, tensor, group=group, async_op=async_op)
+
+
+def all_gather_into_tensor(output, input, group=None, async_op: bool = False):
+    return dist.all_gather_into_tensor(output, input, group=group, async_op=async_op)
+
+
+def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op: bool = False):
+    return dist.reduce_scatter_tensor(output, input, op=op, group=group, async_op=async_op)
+
+
+def barrier(group=None) -> None:
+    """Barrier.  On RCCL this is a 1-element all-reduce plus a stream sync
+    (ProcessGroupNCCL semantics)."""
+    if not is_initialized():
+        return
+    if dist.get_backend(group) == "nccl":
+        dist.barrier(group=group, device_ids=[torch.cuda.current_device()])
+    else:
+        dist.barrier(group=group)

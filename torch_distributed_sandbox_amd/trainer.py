@@ -1,0 +1,150 @@
+"""Training loops behind ``mnist_onegpu.py`` and ``mnist_distributed.py``.
+
+Reference loops: mnist_onegpu.py:34-84 (single GPU) and
+mnist_distributed.py:48-109 (DDP); SURVEY.md §3.3-§3.4.  Kept: seed 0 before
+model construction, ConvNet topology, bs=5, SGD(lr=1e-4), CE loss,
+``zero_grad -> backward -> step`` order, the log lines (every 100 steps on
+local GPU 0, rank-local loss) and ``Training complete in: ...``.  Added:
+images/sec, peak memory, ``--max-steps``, synthetic on-device data, optional
+global-average loss (the reference's commented-out ``all_reduce(AVG)``,
+mnist_distributed.py:102), checkpoint/resume, fault injection.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from datetime import datetime
+
+import torch
+
+from . import _ext
+from .data import DeviceUpsampleLoader, SyntheticMNIST
+from .models import ConvNet
+from .ops import CrossEntropyLoss, SGD
+from .parallel import DistributedDataParallel, DistributedSampler
+from .parallel import distributed as tdist
+from .utils import checkpoint, fault
+from .utils.timing import nvtx_range
+
+
+def add_common_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
+    p.add_argument("--epochs", default=2, type=int, metavar="N", help="number of total epochs to run")
+    p.add_argument("--image-size", default=3000, type=int, help="square image edge (reference: 3000)")
+    p.add_argument("--batch-size", default=5, type=int, help="per-GPU batch size (reference: 5)")
+    p.add_argument("--lr", default=1e-4, type=float)
+    p.add_argument("--max-steps", default=0, type=int, help="stop after this many steps per epoch (0 = full epoch)")
+    p.add_argument("--dataset-size", default=60000, type=int, help="synthetic MNIST size (reference: 60000)")
+    p.add_argument("--log-interval", default=100, type=int)
+    p.add_argument("--mode", default="auto", choices=["auto", "fused", "layers"], help="ConvNet execution plan")
+    p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
+    p.add_argument("--checkpoint", default="", help="save a checkpoint here at the end (rank 0)")
+    p.add_argument("--resume", default="", help="resume from this checkpoint")
+    p.add_argument("--json", action="store_true", help="print a JSON summary line at the end")
+    return p
+
+
+def _device(args, gpu: int) -> torch.device:
+    want = args.device
+    if want == "auto":
+        want = "cuda" if torch.cuda.is_available() else "cpu"
+    if want == "cuda":
+        torch.cuda.set_device(gpu)
+        _ext.ops()  # fail loudly if the native extension is missing on a GPU box
+        return torch.device("cuda", gpu)
+    return torch.device("cpu")
+
+
+def train(gpu: int, args, distributed: bool = False) -> dict:
+    rank = 0
+    world = 1
+    if distributed:
+        rank = args.nr * args.gpus + gpu
+        world = args.world_size
+        backend = args.backend
+        if backend in (None, "auto"):
+            backend = "rccl" if (args.device != "cpu" and torch.cuda.is_available()) else "gloo"
+        tdist.init_process_group(backend=backend, world_size=world, rank=rank,
+                                 device_id=gpu if tdist._normalise_backend(backend) == "rccl" else None)
+    device = _device(args, gpu)
+    torch.manual_seed(0)
+    H = W = args.image_size
+    model = ConvNet(image_shape=(H, W), device=device, mode=args.mode)
+    batch_size = args.batch_size
+    criterion = CrossEntropyLoss()
+    optimizer = SGD(model.parameters(), args.lr)
+    if distributed:
+        model = DistributedDataParallel(model, device_ids=[gpu] if device.type == "cuda" else None)
+        model.attach_optimizer(optimizer)
+    start_epoch = 0
+    if args.resume:
+        _, start_epoch, _ = checkpoint.load(args.resume, model, optimizer, map_location=device)
+    dataset = SyntheticMNIST(size=args.dataset_size)
+    if distributed:
+        sampler = DistributedSampler(len(dataset), num_replicas=world, rank=rank)
+        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, sampler=sampler)
+    else:
+        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, shuffle=True)
+
+    start = datetime.now()
+    total_step = len(loader)
+    if args.max_steps:
+        total_step = min(total_step, args.max_steps)
+    steps_done = 0
+    t_first = None
+    loss = None
+    for epoch in range(start_epoch, args.epochs):
+        loader.set_epoch(epoch)
+        for i, (images, labels) in enumerate(loader):
+            if args.max_steps and i >= args.max_steps:
+                break
+            fault.maybe_inject(rank, steps_done)
+            with nvtx_range("forward"):
+                outputs = model(images)
+                loss = criterion(outputs, labels)
+            optimizer.zero_grad()
+            with nvtx_range("backward"):
+                loss.backward()
+            with nvtx_range("optimizer"):
+                optimizer.step()
+            if distributed:
+                # the reference builds a group every step (mnist_distributed.py:99-100); cached here
+                tdist.new_group(ranks=list(range(args.gpus)) if args.nodes == 1 else None)
+            steps_done += 1
+            if steps_done == 1 and device.type == "cuda":
+                torch.cuda.synchronize()
+                t_first = time.perf_counter()
+            if (i + 1) % args.log_interval == 0 and gpu == 0:
+                shown = loss.detach()
+                if distributed and getattr(args, "avg_loss", False):
+                    shown = shown.clone()
+                    tdist.all_reduce(shown, tdist.ReduceOp.AVG)
+                if distributed:
+                    print("Rank [{}], Epoch [{}/{}], Step [{}/{}], Loss: {:.4f}".format(
+                        rank, epoch + 1, args.epochs, i + 1, total_step, shown.item()), flush=True)
+                else:
+                    print("Epoch [{}/{}], Step [{}/{}], Loss: {:.4f}".format(
+                        epoch + 1, args.epochs, i + 1, total_step, shown.item()), flush=True)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t_end = time.perf_counter()
+    summary = {"rank": rank, "world_size": world, "steps": steps_done, "batch_size": batch_size,
+               "image_size": H, "final_loss": float(loss.item()) if loss is not None else None}
+    if t_first is not None and steps_done > 1:
+        dt = t_end - t_first
+        summary["images_per_sec_per_rank"] = (steps_done - 1) * batch_size / dt
+        summary["images_per_sec_global"] = summary["images_per_sec_per_rank"] * world
+        summary["ms_per_step"] = 1e3 * dt / (steps_done - 1)
+    if device.type == "cuda":
+        summary["peak_mem_gb"] = torch.cuda.max_memory_allocated(device) / 1e9
+    if gpu == 0:
+        print("Training complete in: " + str(datetime.now() - start), flush=True)
+        if args.json:
+            print(json.dumps(summary), flush=True)
+    if args.checkpoint:
+        checkpoint.save(args.checkpoint, model, optimizer, step=steps_done, epoch=args.epochs, rank=rank)
+    if distributed:
+        tdist.barrier()
+        tdist.destroy_process_group()
+    return summary
