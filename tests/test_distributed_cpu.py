@@ -1,0 +1,194 @@
+"""Multi-process CPU tests (gloo, world_size 2-4) of the process-group API, DDP,
+sampler, launcher fail-fast and fault injection."""
+import copy
+import os
+
+import pytest
+import torch
+
+from torch_distributed_sandbox_amd.parallel import launch
+
+
+def _init(rank, world, port, backend="gloo"):
+    from torch_distributed_sandbox_amd.parallel import distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    return dist
+
+
+# ---------------------------------------------------------------- collectives
+def _w_collectives(rank, world, port):
+    dist = _init(rank, world, port)
+    t = torch.tensor(rank + 1, dtype=torch.int32)
+    g = dist.new_group(list(range(world)))
+    assert g is dist.new_group(list(range(world)))  # cached, no per-step re-init
+    dist.all_reduce(t, dist.ReduceOp.SUM, group=g)
+    assert t.item() == world * (world + 1) // 2
+    f = torch.full((5,), float(rank))
+    dist.all_reduce(f, dist.ReduceOp.AVG)
+    assert torch.allclose(f, torch.full((5,), (world - 1) / 2))
+    m = torch.tensor([float(rank)])
+    dist.all_reduce(m, dist.ReduceOp.MAX)
+    assert m.item() == world - 1
+    w = dist.all_reduce(torch.ones(3), dist.ReduceOp.AVG, async_op=True)
+    w.wait()
+    b = torch.tensor([rank * 10.0])
+    dist.broadcast(b, src=world - 1)
+    assert b.item() == (world - 1) * 10.0
+    out = [torch.zeros(2) for _ in range(world)]
+    dist.all_gather(out, torch.full((2,), float(rank)))
+    assert [o[0].item() for o in out] == list(range(world))
+    if world > 2:
+        sub = dist.new_group([0, 1])
+        if rank in (0, 1):
+            s = torch.tensor([1.0])
+            dist.all_reduce(s, group=sub)
+            assert s.item() == 2.0
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_collectives_gloo(world):
+    launch.spawn(_w_collectives, args=(world, launch.find_free_port()), nprocs=world, timeout=180)
+
+
+# ---------------------------------------------------------------- DDP equivalence
+def _w_ddp(rank, world, port, H, B):
+    dist = _init(rank, world, port)
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    base = ConvNet(image_shape=(H, H))
+    ref = copy.deepcopy(base)  # rank-0 init (all ranks seeded 0)
+    torch.manual_seed(100 + rank)
+    model = ConvNet(image_shape=(H, H))  # different init per rank -> must be overwritten by rank 0
+    model.load_state_dict(base.state_dict()) if rank == 0 else None
+    ddp = DistributedDataParallel(model)
+    assert [b[2][0] for b in ddp.bucket_layout()][0] == (10,)  # fc.bias first (gradient-ready order)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.equal(p.data, q.data), "rank-0 broadcast at construction failed"
+    opt = ddp.attach_optimizer(SGD(model.parameters(), 0.05))
+    ropt = torch.optim.SGD(ref.parameters(), 0.05)
+    crit = CrossEntropyLoss()
+    g = torch.Generator().manual_seed(7)
+    for step in range(3):
+        xs = torch.rand(world, B, 1, H, H, generator=g)
+        ys = torch.randint(0, 10, (world, B), generator=g)
+        loss = crit(ddp(xs[rank]), ys[rank])
+        opt.zero_grad()
+        loss.backward()
+        # reference: average of per-rank gradients (per-rank BN stats), one process
+        ropt.zero_grad()
+        grads = None
+        for r in range(world):
+            rr = copy.deepcopy(ref)
+            rl = torch.nn.functional.cross_entropy(rr(xs[r]), ys[r])
+            rl.backward()
+            gg = [p.grad.clone() for p in rr.parameters()]
+            grads = gg if grads is None else [a + b for a, b in zip(grads, gg)]
+            if r == 0:
+                ref_buffers = [b.clone() for b in rr.buffers()]
+        for p, gsum in zip(ref.parameters(), grads):
+            p.grad = gsum / world
+        for (n, p), q in zip(model.named_parameters(), ref.parameters()):
+            assert torch.allclose(p.grad, q.grad, rtol=1e-4, atol=1e-6), (step, n)
+        opt.step()
+        ropt.step()
+        with torch.no_grad():
+            for b, rb in zip(ref.buffers(), ref_buffers):
+                b.copy_(rb)  # buffers follow rank 0 (broadcast_buffers=True)
+    for p, q in zip(model.parameters(), ref.parameters()):
+        assert torch.allclose(p, q, rtol=1e-4, atol=1e-6)
+    dist.destroy_process_group()
+
+
+def test_ddp_matches_single_process_average():
+    launch.spawn(_w_ddp, args=(2, launch.find_free_port(), 32, 2), nprocs=2, timeout=300)
+
+
+def _w_no_sync(rank, world, port):
+    dist = _init(rank, world, port)
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(4, 3)
+    ddp = DistributedDataParallel(lin)
+    x = torch.full((2, 4), float(rank + 1))
+    with ddp.no_sync():
+        ddp(x).sum().backward()
+    local = lin.weight.grad.clone()
+    ddp(x).sum().backward()  # accumulates + syncs
+    t = local * 2
+    dist.all_reduce(t, dist.ReduceOp.AVG)
+    assert torch.allclose(lin.weight.grad, t), (lin.weight.grad, t)
+    dist.destroy_process_group()
+
+
+def test_ddp_no_sync_accumulation():
+    launch.spawn(_w_no_sync, args=(2, launch.find_free_port()), nprocs=2, timeout=120)
+
+
+# ---------------------------------------------------------------- sampler
+def test_distributed_sampler_matches_torch():
+    from torch.utils.data.distributed import DistributedSampler as TorchDS
+
+    from torch_distributed_sandbox_amd.parallel import DistributedSampler
+
+    ds = list(range(23))
+    for W in (1, 2, 3, 4):
+        for r in range(W):
+            for drop in (False, True):
+                ours = DistributedSampler(len(ds), num_replicas=W, rank=r, drop_last=drop)
+                theirs = TorchDS(ds, num_replicas=W, rank=r, drop_last=drop)
+                for ep in (0, 1):
+                    ours.set_epoch(ep)
+                    theirs.set_epoch(ep)
+                    assert list(ours) == list(theirs)
+                    assert len(ours) == len(theirs)
+
+
+# ---------------------------------------------------------------- launcher / faults
+def _w_fault(rank, world, port, mode):
+    os.environ.update({"TDS_FAULT_RANK": "1", "TDS_FAULT_STEP": "2", "TDS_FAULT_MODE": mode,
+                       "TDS_FAULT_HANG_S": "60"})
+    from torch_distributed_sandbox_amd.utils import fault
+
+    dist = _init(rank, world, port)
+    for step in range(5):
+        fault.maybe_inject(rank, step)
+        t = torch.ones(1)
+        dist.all_reduce(t)
+
+
+@pytest.mark.parametrize("mode", ["raise", "exit"])
+def test_fail_fast_on_rank_fault(mode):
+    with pytest.raises((launch.ProcessRaisedException, launch.ProcessExitedException)) as ei:
+        launch.spawn(_w_fault, args=(2, launch.find_free_port(), mode), nprocs=2, timeout=120)
+    assert ei.value.error_index == 1
+    if mode == "raise":
+        assert "injected fault on rank 1 at step 2" in str(ei.value)
+
+
+def test_spawn_timeout_on_hang():
+    with pytest.raises(TimeoutError):
+        launch.spawn(_w_fault, args=(2, launch.find_free_port(), "hang"), nprocs=2, timeout=15)
+
+
+def _w_ok(i, path):
+    with open(os.path.join(path, f"r{i}"), "w") as f:
+        f.write(str(i))
+
+
+def test_spawn_runs_all(tmp_path):
+    launch.spawn(_w_ok, args=(str(tmp_path),), nprocs=3, timeout=60)
+    assert sorted(os.listdir(tmp_path)) == ["r0", "r1", "r2"]
+
+
+def test_find_free_port():
+    p = int(launch.find_free_port())
+    assert 0 < p < 65536

@@ -48,8 +48,12 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
         for n, p in ours.named_parameters():
             g, rg = p.grad.double().cpu(), rp[n].grad
             err = (g - rg).abs().max().item()
-            scale = rg.abs().max().item() + 1e-12
-            assert err <= 2e-3 * scale + 1e-6, f"step {s} {n}: {err:.3e} vs {scale:.3e}"
+            scale = rg.abs().max().item()
+            if n.endswith("0.bias"):
+                # conv bias before BN: analytically zero gradient; compare against the
+                # magnitude of the conv weight gradient (pure rounding noise either way)
+                scale = max(scale, rp[n.replace("bias", "weight")].grad.abs().max().item() * 1e-3)
+            assert err <= 2e-3 * scale + 1e-9, f"step {s} {n}: {err:.3e} vs {scale:.3e}"
         opt.step()
         ropt.step()
     rb = dict(ref.named_buffers())

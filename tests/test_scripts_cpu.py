@@ -1,0 +1,85 @@
+"""The four reference entry points, run end to end on CPU (gloo) at small sizes."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=300, env=None):
+    e = dict(os.environ)
+    e.update(env or {})
+    e["CUDA_VISIBLE_DEVICES"] = ""  # CPU rehearsal even on a GPU box
+    e["HIP_VISIBLE_DEVICES"] = ""
+    p = subprocess.run([sys.executable] + args, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=e)
+    return p
+
+
+def test_allreduce_toy_gloo():
+    p = _run(["allreduce_toy.py", "-s", "3", "--backend", "gloo", "--steps", "4"])
+    assert p.returncode == 0, p.stderr
+    lines = re.findall(r"rank: (\d), step: (\d+), value: (\d+), reduced sum: (\d+)\.", p.stdout)
+    assert {r for r, *_ in lines} == {"0", "1"}  # only ranks 0 and 1 print (allreduce_toy.py:35-38)
+    steps = {}
+    for r, s, v, tot in lines:
+        steps.setdefault(s, set()).add(tot)
+    assert sorted(steps, key=int) == ["1", "2", "3", "4"]  # --steps honoured
+    for s, tots in steps.items():
+        assert len(tots) == 1  # every printing rank agrees on the reduced sum
+    assert p.stdout.count("--> done setting up rank=") == 3
+
+
+def test_test_init_script():
+    p = _run(["test_init.py"])
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.count("--> done setting up rank=") == 4
+    assert "successful test_setup!" in p.stdout
+    assert p.stdout.count("backend='gloo'") == 4
+
+
+def test_test_init_pytest_collectable():
+    sys.path.insert(0, ROOT)
+    import test_init
+
+    test_init.test_setup()
+
+
+def test_mnist_onegpu_cpu_learns():
+    p = _run(["mnist_onegpu.py", "--device", "cpu", "--image-size", "32", "--epochs", "1", "--max-steps", "60",
+              "--log-interval", "20", "--lr", "0.05", "--dataset-size", "600", "--json"])
+    assert p.returncode == 0, p.stderr
+    losses = [float(x) for x in re.findall(r"Epoch \[1/1\], Step \[\d+/60\], Loss: ([\d.]+)", p.stdout)]
+    assert len(losses) == 3
+    assert "Training complete in: " in p.stdout
+    summ = json.loads(p.stdout.strip().splitlines()[-1])
+    assert summ["steps"] == 60
+
+
+def test_mnist_distributed_cpu(tmp_path):
+    ck = str(tmp_path / "ck.pt")
+    p = _run(["mnist_distributed.py", "-g", "2", "--device", "cpu", "--backend", "gloo", "--image-size", "32",
+              "--epochs", "1", "--max-steps", "20", "--log-interval", "10", "--lr", "0.05", "--dataset-size", "400",
+              "--checkpoint", ck, "--avg-loss"])
+    assert p.returncode == 0, p.stderr
+    assert len(re.findall(r"Rank \[0\], Epoch \[1/1\], Step \[\d+/20\], Loss: ", p.stdout)) == 2
+    assert "Training complete in: " in p.stdout
+    assert os.path.exists(ck)
+    sd = torch.load(ck, weights_only=True)
+    assert "fc.weight" in sd["model"] or "module.fc.weight" in sd["model"]
+    # resume
+    p2 = _run(["mnist_distributed.py", "-g", "2", "--device", "cpu", "--backend", "gloo", "--image-size", "32",
+               "--epochs", "2", "--max-steps", "5", "--dataset-size", "400", "--resume", ck])
+    assert p2.returncode == 0, p2.stderr
+
+
+def test_mnist_distributed_fault_fails_fast():
+    p = _run(["mnist_distributed.py", "-g", "2", "--device", "cpu", "--backend", "gloo", "--image-size", "32",
+              "--epochs", "1", "--max-steps", "10", "--dataset-size", "200"],
+             env={"TDS_FAULT_RANK": "1", "TDS_FAULT_STEP": "3", "TDS_FAULT_MODE": "raise"}, timeout=200)
+    assert p.returncode != 0
+    assert "injected fault on rank 1 at step 3" in p.stderr
