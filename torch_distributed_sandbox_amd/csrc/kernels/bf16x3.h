@@ -1,0 +1,56 @@
+// bf16x3 split-precision MFMA helpers (gfx950, v_mfma_f32_16x16x32_bf16).
+//
+// An fp32 operand x is carried as hi = bf16(x), lo = bf16(x - hi); a product is
+// formed as hi*hi + hi*lo + lo*hi with fp32 accumulation (the lo*lo term,
+// ~2^-16 relative, is dropped).  Per-product relative error ~2^-16 (≈1.5e-5),
+// i.e. ~30x tighter than the TF32 (10-bit mantissa) convolutions cuDNN runs by
+// default for the reference on Ampere; accumulation and all I/O stay fp32.
+// Cost: 3 bf16 MFMAs = 3/16 of the f32-MFMA time (5.3x faster than exact
+// v_mfma_f32_16x16x4_f32 at the same FLOPs).
+#pragma once
+
+#include "common.h"
+
+namespace tds {
+
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ f32x4 mfma_bf16(const s16x8& a, const s16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c,
+                                                 0, 0, 0);
+}
+
+// c += a*b with a = ahi+alo, b = bhi+blo (small terms first)
+__device__ __forceinline__ f32x4 mfma_bf16x3(const s16x8& ahi, const s16x8& alo, const s16x8& bhi, const s16x8& blo,
+                                             f32x4 c) {
+  c = mfma_bf16(alo, bhi, c);
+  c = mfma_bf16(ahi, blo, c);
+  c = mfma_bf16(ahi, bhi, c);
+  return c;
+}
+
+__device__ __forceinline__ unsigned short bf16_rne(float f) {
+  unsigned int u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (unsigned short)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));  // inf/nan
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (unsigned short)(u >> 16);
+}
+
+__device__ __forceinline__ void split_bf16(float x, unsigned short& hi, unsigned short& lo) {
+  hi = bf16_rne(x);
+  const float h = __uint_as_float(((unsigned int)hi) << 16);
+  lo = bf16_rne(x - h);
+}
+
+__device__ __forceinline__ float bf16_to_f32(unsigned short h) { return __uint_as_float(((unsigned int)h) << 16); }
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of row q,
+// columns 4p..4p+3; lane i gets column i of the 4 rows (element q = row q).
+__device__ __forceinline__ s16x4 ds_read_tr16(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(lds_ptr));
+}
+
+}  // namespace tds

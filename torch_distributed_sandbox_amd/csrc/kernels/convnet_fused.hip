@@ -1,0 +1,873 @@
+// Fused ConvNet kernels (everything except conv2, see conv2_bf16x3.hip).
+// Reference model: mnist_onegpu.py:11-31; SURVEY.md §2.4 K1-K4, K6-K18, K22-K25.
+//
+// Forward
+//   l1_conv<STATS>  : conv1 (exact fp32, v_mfma_f32_16x16x4_f32) -> per-channel sum / sumsq
+//                     of y1 - b1 (shifted for stability); y1 is never written (2.88 GB saved).
+//   x_autocorr      : 9x9 autocorrelation + border strips of x -> Gram G = sum xpatch xpatch^T
+//                     and S = sum xpatch, used by the closed-form conv1 weight gradient.
+//   l1_conv<APPLY>  : conv1 recomputed, BN1 affine, ReLU, 2x2 max-pool -> p1 (bf16 hi|lo NHWC)
+//                     and a 1-byte argmax per pooled value.
+//   [conv2 fwd + BN2 stats]
+//   head_fwd        : BN2 affine + ReLU + 2x2 pool + fc, one pass over y2 and W (p2 never stored).
+// Backward
+//   head_bwd        : recomputes p2; dW = dlogits^T p2 straight into the DDP bucket, g2 =
+//                     dlogits W masked by ReLU (pooled grad), BN2 reductions sum dz, sum dz*y.
+//   dy2_build       : max-pool/ReLU/BN2 backward -> dy2 = k1*dz + k2*y2 + k3 as bf16 hi|lo.
+//   [conv2 dgrad, conv2 wgrad]
+//   l1_bwd          : sparse layer-1 backward: dz1 is non-zero only at the argmax of each
+//                     pooled window with p1 > 0, so per (pooled pixel, channel) one y1 value
+//                     (25 FMA) and one rank-1 update of sum dz1 x xpatch (25 FMA).
+//   l1_finalize     : dW1 = a1*sum(dz1 xpatch) + a2*(W1 G + b1 S) + a3*S, db1, dgamma1, dbeta1.
+#include "bf16x3.h"
+#include "launchers.h"
+
+namespace tds {
+
+// ============================================================================ layer 1 conv
+constexpr int L1_TR = 16;           // conv1 output rows per tile
+constexpr int L1_TC = 64;           // conv1 output cols per tile
+constexpr int L1_XR = L1_TR + 4;
+constexpr int L1_XS = 80;           // LDS row stride (floats): 16 mod 32 -> paired taps hit disjoint banks
+
+__device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// K index k -> tap (ky = k % 5, kx = k / 5): consecutive k step down a column so the
+// two 16-lane groups of a 32-lane half read rows 80 floats apart (disjoint banks).
+__device__ __forceinline__ int l1_koff(int k) {
+  if (k >= 25) k = 0;
+  return (k % 5) * L1_XS + (k / 5);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+                                                      const float* __restrict__ b1, const float* __restrict__ aff,
+                                                      double* __restrict__ partial, uint4* __restrict__ p1,
+                                                      uint8_t* __restrict__ idx1, int B, int H, int W) {
+  __shared__ __attribute__((aligned(16))) float xs[L1_XR * L1_XS];
+  __shared__ double red[4][16][2];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int P = H / 2, PW = W / 2;
+  const int tiles_c = (W + L1_TC - 1) / L1_TC, tiles_r = (H + L1_TR - 1) / L1_TR;
+  const int per_img = tiles_c * tiles_r, total = per_img * B;
+
+  // A operand (weights) in registers: lane -> co = li, k = 4s + g
+  float wa[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) {
+    const int k = 4 * s + g;
+    wa[s] = k < 25 ? w1[li * 25 + (k % 5) * 5 + (k / 5)] : 0.f;
+  }
+  int koff[7];
+#pragma unroll
+  for (int s = 0; s < 7; ++s) koff[s] = l1_koff(4 * s + g);
+
+  // per-lane epilogue constants for co = 4g + r
+  float bia[4], ea[4], eb[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    bia[r] = b1[4 * g + r];
+    ea[r] = MODE == 1 ? aff[4 * g + r] : 0.f;
+    eb[r] = MODE == 1 ? aff[16 + 4 * g + r] : 0.f;
+  }
+  float s_acc[4] = {0.f, 0.f, 0.f, 0.f}, q_acc[4] = {0.f, 0.f, 0.f, 0.f};
+
+  for (int t = xcd_remap(blockIdx.x, gridDim.x); t < total; t += gridDim.x) {
+    const int b = t / per_img, rem = t - b * per_img;
+    const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
+    const float* xb = x + (int64_t)b * H * W;
+    __syncthreads();
+    for (int e = tid; e < L1_XR * (L1_TC + 4); e += 256) {
+      const int rr = e / (L1_TC + 4), cc = e - rr * (L1_TC + 4);
+      const int gr = r0 - 2 + rr, gc = c0 - 2 + cc;
+      xs[rr * L1_XS + cc] = (gr >= 0 && gr < H && gc >= 0 && gc < W) ? xb[(int64_t)gr * W + gc] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rp = 0; rp < 2; ++rp) {
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        // 4 tiles: rows (4wv + 2rp + {0,1}) x segments (2sp + {0,1}) of 16 pixels
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < 7; ++s) {
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const int row = 4 * wv + 2 * rp + a, seg = 2 * sp + c;
+              const float bv = xs[row * L1_XS + seg * 16 + li + koff[s]];
+              acc[a][c] = mfma16x4(wa[s], bv, acc[a][c]);
+            }
+        }
+        if (MODE == 0) {
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+              const int row = r0 + 4 * wv + 2 * rp + a, col = c0 + (2 * sp + c) * 16 + li;
+              if (row < H && col < W) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const float v = acc[a][c][r];  // y1 - b1 (shifted statistics)
+                  s_acc[r] += v;
+                  q_acc[r] += v * v;
+                }
+              }
+            }
+        } else {
+          // BN1 affine -> 2x2 max-pool (first max in scan order, NaN wins) -> ReLU
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int col = c0 + (2 * sp + c) * 16 + li;     // conv column of this lane
+            const int prow = (r0 + 4 * wv + 2 * rp) >> 1;    // pooled row
+            const int pcol = col >> 1;
+            uint16_t hi[4], lo[4];
+            uint8_t ix[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float z0 = ea[r] * (acc[0][c][r] + bia[r]) + eb[r];
+              const float z1 = ea[r] * (acc[1][c][r] + bia[r]) + eb[r];
+              const float z0n = __shfl_xor(z0, 1, 64);
+              const float z1n = __shfl_xor(z1, 1, 64);
+              float m = z0;
+              int a = 0;
+              if (z0n > m || isnan(z0n)) { m = z0n; a = 1; }
+              if (z1 > m || isnan(z1)) { m = z1; a = 2; }
+              if (z1n > m || isnan(z1n)) { m = z1n; a = 3; }
+              const float p = m > 0.f ? m : (isnan(m) ? m : 0.f);
+              unsigned short h, l;
+              split_bf16(p, h, l);
+              hi[r] = h;
+              lo[r] = l;
+              ix[r] = (uint8_t)a;
+            }
+            if ((li & 1) == 0 && prow < P && pcol < PW) {
+              const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
+              uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
+              dst[g] = make_uint2(hi[0] | ((uint32_t)hi[1] << 16), hi[2] | ((uint32_t)hi[3] << 16));
+              dst[4 + g] = make_uint2(lo[0] | ((uint32_t)lo[1] << 16), lo[2] | ((uint32_t)lo[3] << 16));
+              reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] =
+                  ix[0] | ((uint32_t)ix[1] << 8) | ((uint32_t)ix[2] << 16) | ((uint32_t)ix[3] << 24);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (MODE == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        s_acc[r] += __shfl_xor(s_acc[r], off, 64);
+        q_acc[r] += __shfl_xor(q_acc[r], off, 64);
+      }
+    }
+    if (li == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[wv][4 * g + r][0] = s_acc[r];
+        red[wv][4 * g + r][1] = q_acc[r];
+      }
+    }
+    __syncthreads();
+    if (tid < 32) {
+      const int co = tid >> 1, k = tid & 1;
+      const double v = red[0][co][k] + red[1][co][k] + red[2][co][k] + red[3][co][k];
+      partial[((int64_t)co * gridDim.x + blockIdx.x) * 2 + k] = v;
+    }
+  }
+}
+
+// Shifted BN finalize: statistics were accumulated on (y - shift[c]).
+__global__ void bn_finalize_shifted_kernel(const double* __restrict__ partial, int C, int nchunk, int64_t n,
+                                           const float* __restrict__ shift, float eps, float momentum,
+                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                           float* __restrict__ stats /* mean[C], invstd[C] */,
+                                           float* __restrict__ running_mean, float* __restrict__ running_var,
+                                           int64_t* __restrict__ num_batches, float* __restrict__ aff /* a[C], b[C] */) {
+  const int c = threadIdx.x;
+  if (c == 0 && num_batches) num_batches[0] += 1;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    s += partial[((int64_t)c * nchunk + k) * 2];
+    ss += partial[((int64_t)c * nchunk + k) * 2 + 1];
+  }
+  const double m0 = s / (double)n;
+  double var = ss / (double)n - m0 * m0;
+  if (var < 0.0) var = 0.0;
+  const double mean = m0 + (shift ? (double)shift[c] : 0.0);
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  stats[c] = (float)mean;
+  stats[C + c] = invstd;
+  if (running_mean) {
+    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+  }
+  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
+  aff[c] = gm * invstd;
+  aff[C + c] = bt - (float)mean * gm * invstd;
+}
+
+// ============================================================================ x autocorrelation (Gram of conv1 patches)
+// full[b][dy+4][dx+4] = sum_u x(u) x(u+d) over the image (0 outside), d in [-4,4]^2 with
+// (dy > 0) or (dy == 0 and dx >= 0) computed, the rest by symmetry in the finalize.
+// A thread owns 4 consecutive pixels of a row; a workgroup a 16 x 64 tile (+4 halo right/below, +4 left).
+constexpr int AC_TR = 16, AC_TC = 64;
+__global__ __launch_bounds__(256) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
+                                                         int B, int H, int W) {
+  __shared__ __attribute__((aligned(16))) float xs[(AC_TR + 4) * (AC_TC + 8 + 4)];
+  __shared__ double red[4][41];
+  constexpr int XS = AC_TC + 12;  // cols c0-4 .. c0+TC+4 (+pad)
+  const int tid = threadIdx.x;
+  const int tiles_c = (W + AC_TC - 1) / AC_TC, tiles_r = (H + AC_TR - 1) / AC_TR;
+  const int total = tiles_c * tiles_r * B;
+  float acc[41];
+#pragma unroll
+  for (int i = 0; i < 41; ++i) acc[i] = 0.f;
+  const int tr = tid >> 4, tc = (tid & 15) * 4;  // thread: row tr, cols tc..tc+3
+  for (int t = blockIdx.x; t < total; t += gridDim.x) {
+    const int b = t / (tiles_c * tiles_r), rem = t % (tiles_c * tiles_r);
+    const int r0 = (rem / tiles_c) * AC_TR, c0 = (rem % tiles_c) * AC_TC;
+    const float* xb = x + (int64_t)b * H * W;
+    __syncthreads();
+    for (int e = tid; e < (AC_TR + 4) * XS; e += 256) {
+      const int rr = e / XS, cc = e - rr * XS;
+      const int gr = r0 + rr, gc = c0 - 4 + cc;
+      xs[e] = (gr < H && gc >= 0 && gc < W && cc < AC_TC + 8 + 4) ? xb[(int64_t)gr * W + gc] : 0.f;
+    }
+    __syncthreads();
+    // own pixels: xs[tr][tc+4 .. tc+7]; window rows tr..tr+4, cols tc .. tc+11
+    float w[5][12];
+#pragma unroll
+    for (int dy = 0; dy < 5; ++dy)
+#pragma unroll
+      for (int c = 0; c < 12; ++c) w[dy][c] = xs[(tr + dy) * XS + tc + c];
+    const bool valid_row = (r0 + tr) < H;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const float u = (valid_row && c0 + tc + p < W) ? w[0][4 + p] : 0.f;
+      int i = 0;
+#pragma unroll
+      for (int dx = 0; dx <= 4; ++dx) acc[i++] += u * w[0][4 + p + dx];
+#pragma unroll
+      for (int dy = 1; dy <= 4; ++dy)
+#pragma unroll
+        for (int dx = -4; dx <= 4; ++dx) acc[i++] += u * w[dy][4 + p + dx];
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < 41; ++i) {
+    const float s = wave_sum(acc[i]);
+    if (lane == 0) red[wv][i] = s;
+  }
+  __syncthreads();
+  if (tid < 41) partial[(int64_t)blockIdx.x * 41 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+// Border strips: for each image, line L in {row 0,1,H-2,H-1, col 0,1,W-2,W-1} and d in
+// [-4,4]^2: strip[L][d] = sum_{u on line L} x(u) x(u+d); also plain line sums (d = "none").
+// grid: (82 (81 d + 1 plain), 9 lines; line 8 = whole-image plain sum), block reduces over
+// B images and the line.
+__global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__ x, double* __restrict__ strips,
+                                                       int B, int H, int W) {
+  __shared__ double sh[8];
+  const int di = blockIdx.x, L = blockIdx.y;
+  const int dy = di / 9 - 4, dx = di % 9 - 4;
+  const bool plain = di == 81;
+  if (L == 8) {  // whole-image plain sum (only slot 81 is meaningful)
+    double s = 0.0;
+    if (plain)
+      for (int64_t i = threadIdx.x; i < (int64_t)B * H * W; i += blockDim.x) s += x[i];
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) strips[8 * 82 + di] = s;
+    return;
+  }
+  const bool is_row = L < 4;
+  const int fixed = is_row ? (L < 2 ? L : H - 4 + L) : (L < 6 ? L - 4 : W - 8 + L);
+  const int len = is_row ? W : H;
+  double s = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const float* xb = x + (int64_t)b * H * W;
+    for (int i = threadIdx.x; i < len; i += blockDim.x) {
+      const int r = is_row ? fixed : i, c = is_row ? i : fixed;
+      if (r < 0 || r >= H || c < 0 || c >= W) continue;
+      const float u = xb[(int64_t)r * W + c];
+      if (plain) {
+        s += u;
+      } else {
+        const int r2 = r + dy, c2 = c + dx;
+        if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) s += (double)u * xb[(int64_t)r2 * W + c2];
+      }
+    }
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) strips[L * 82 + di] = s;
+}
+
+// ============================================================================ head: BN2 + ReLU + pool + fc
+// One thread per pooled position (py, px): loops channels in groups of 4 and all
+// images, so W (fc weight, [NC][32][Q][Q] in reference flatten order) is read once.
+template <int MAXB>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
+                                                       const float* __restrict__ aff2, float* __restrict__ partial,
+                                                       int B, int P, int Q, int NC) {
+  __shared__ float red[4][MAXB * 10];
+  const int tid = threadIdx.x;
+  const int64_t QQ = (int64_t)Q * Q;
+  float acc[MAXB][10];
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) acc[b][j] = 0.f;
+  for (int64_t pos = (int64_t)blockIdx.x * blockDim.x + tid; pos < QQ; pos += (int64_t)gridDim.x * blockDim.x) {
+    const int py = (int)(pos / Q), px = (int)(pos - (int64_t)py * Q);
+#pragma unroll 1
+    for (int c4 = 0; c4 < 8; ++c4) {
+      float wj[10][4];
+#pragma unroll
+      for (int j = 0; j < 10; ++j)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc)
+          wj[j][cc] = j < NC ? Wfc[((int64_t)j * 32 + 4 * c4 + cc) * QQ + pos] : 0.f;
+      float a[4], bb[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        a[cc] = aff2[4 * c4 + cc];
+        bb[cc] = aff2[32 + 4 * c4 + cc];
+      }
+#pragma unroll
+      for (int b = 0; b < MAXB; ++b) {
+        if (b < B) {
+          const int64_t base = (((int64_t)b * P + 2 * py) * P + 2 * px) * 8 + c4;  // float4 index
+          const float4 v00 = y2[base], v01 = y2[base + 8], v10 = y2[base + (int64_t)P * 8], v11 = y2[base + (int64_t)P * 8 + 8];
+          const float y[4][4] = {{v00.x, v00.y, v00.z, v00.w}, {v01.x, v01.y, v01.z, v01.w},
+                                 {v10.x, v10.y, v10.z, v10.w}, {v11.x, v11.y, v11.z, v11.w}};
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) {
+            float m = a[cc] * y[0][cc] + bb[cc];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) {
+              const float z = a[cc] * y[q][cc] + bb[cc];
+              if (z > m || isnan(z)) m = z;
+            }
+            const float p = m > 0.f ? m : (isnan(m) ? m : 0.f);
+#pragma unroll
+            for (int j = 0; j < 10; ++j) acc[b][j] += p * wj[j][cc];
+          }
+        }
+      }
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int b = 0; b < MAXB; ++b)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const float s = wave_sum(acc[b][j]);
+      if (lane == 0) red[wv][b * 10 + j] = s;
+    }
+  __syncthreads();
+  for (int i = tid; i < B * NC; i += blockDim.x) {
+    const int b = i / NC, j = i % NC;
+    partial[(int64_t)blockIdx.x * B * NC + i] =
+        red[0][b * 10 + j] + red[1][b * 10 + j] + red[2][b * 10 + j] + red[3][b * 10 + j];
+  }
+}
+
+__global__ void head_logits_reduce_kernel(const float* __restrict__ partial, const float* __restrict__ bias,
+                                          float* __restrict__ logits, int nblk, int BN, int NC) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= BN) return;
+  double s = 0.0;
+  for (int k = 0; k < nblk; ++k) s += partial[(int64_t)k * BN + i];
+  logits[i] = (float)s + (bias ? bias[i % NC] : 0.f);
+}
+
+// Backward of the head.  dl = dlogits [B][NC].
+//   dW[j][c][pos] = scale * sum_b dl[b][j] p2[b][c][pos]   (written into dW_out, e.g. the DDP bucket)
+//   g2m[b][pos][c] = (sum_j dl[b][j] W[j][c][pos]) * [p2 > 0]     (NHWC, fp32)
+//   red partial per block: [c][0] += g2m (= sum dz2), [c][1] += g2m * y2(argmax)
+template <int MAXB>
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
+                                                       const float* __restrict__ aff2, const float* __restrict__ dl,
+                                                       float* __restrict__ dW, float4* __restrict__ g2m,
+                                                       double* __restrict__ partial, int B, int P, int Q, int NC,
+                                                       float scale) {
+  __shared__ float red[4][64];
+  const int tid = threadIdx.x;
+  const int64_t QQ = (int64_t)Q * Q;
+  float sdz[32], sdy[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) sdz[c] = sdy[c] = 0.f;
+  for (int64_t pos = (int64_t)blockIdx.x * blockDim.x + tid; pos < QQ; pos += (int64_t)gridDim.x * blockDim.x) {
+    const int py = (int)(pos / Q), px = (int)(pos - (int64_t)py * Q);
+#pragma unroll
+    for (int c4 = 0; c4 < 8; ++c4) {
+      float wj[10][4], dwa[10][4];
+#pragma unroll
+      for (int j = 0; j < 10; ++j)
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          wj[j][cc] = j < NC ? Wfc[((int64_t)j * 32 + 4 * c4 + cc) * QQ + pos] : 0.f;
+          dwa[j][cc] = 0.f;
+        }
+      float a[4], bb[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        a[cc] = aff2[4 * c4 + cc];
+        bb[cc] = aff2[32 + 4 * c4 + cc];
+      }
+#pragma unroll 1
+      for (int b = 0; b < MAXB && b < B; ++b) {
+        const int64_t base = (((int64_t)b * P + 2 * py) * P + 2 * px) * 8 + c4;
+        const float4 v00 = y2[base], v01 = y2[base + 8], v10 = y2[base + (int64_t)P * 8], v11 = y2[base + (int64_t)P * 8 + 8];
+        const float y[4][4] = {{v00.x, v00.y, v00.z, v00.w}, {v01.x, v01.y, v01.z, v01.w},
+                               {v10.x, v10.y, v10.z, v10.w}, {v11.x, v11.y, v11.z, v11.w}};
+        float gout[4];
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          float m = a[cc] * y[0][cc] + bb[cc], ya = y[0][cc];
+#pragma unroll
+          for (int q = 1; q < 4; ++q) {
+            const float z = a[cc] * y[q][cc] + bb[cc];
+            if (z > m || isnan(z)) { m = z; ya = y[q][cc]; }
+          }
+          const float p = m > 0.f ? m : 0.f;
+          float gsum = 0.f;
+#pragma unroll
+          for (int j = 0; j < 10; ++j) {
+            const float d = j < NC ? dl[b * NC + j] : 0.f;
+            gsum += d * wj[j][cc];
+            dwa[j][cc] += d * p;
+          }
+          const float gm = m > 0.f ? gsum : 0.f;
+          gout[cc] = gm;
+          sdz[4 * c4 + cc] += gm;
+          sdy[4 * c4 + cc] += gm * ya;
+        }
+        g2m[((int64_t)b * QQ + pos) * 8 + c4] = make_float4(gout[0], gout[1], gout[2], gout[3]);
+      }
+#pragma unroll
+      for (int j = 0; j < 10; ++j)
+        if (j < NC)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) dW[((int64_t)j * 32 + 4 * c4 + cc) * QQ + pos] = scale * dwa[j][cc];
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    const float s0 = wave_sum(sdz[c]);
+    const float s1 = wave_sum(sdy[c]);
+    if (lane == 0) {
+      red[wv][2 * c] = s0;
+      red[wv][2 * c + 1] = s1;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int c = tid >> 1, k = tid & 1;
+    partial[((int64_t)c * gridDim.x + blockIdx.x) * 2 + k] =
+        (double)red[0][tid] + (double)red[1][tid] + (double)red[2][tid] + (double)red[3][tid];
+  }
+}
+
+// BN backward finalize from (sum dz, sum dz*y) partials:
+//   dgamma = invstd*(sdzy - mean*sdz), dbeta = sdz,
+//   dy = k1*dz + k2*y + k3,  k1 = g*is, k2 = -g*is^3*(sdzy - mean*sdz)/n, k3 = -g*is*sdz/n - k2*mean
+__global__ void bn_bwd_finalize2_kernel(const double* __restrict__ partial, int C, int nchunk, int64_t n,
+                                        const float* __restrict__ gamma, const float* __restrict__ stats,
+                                        float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ kbuf,
+                                        double* __restrict__ sums_out) {
+  const int c = threadIdx.x;
+  if (c >= C) return;
+  double sdz = 0.0, sdzy = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    sdz += partial[((int64_t)c * nchunk + k) * 2];
+    sdzy += partial[((int64_t)c * nchunk + k) * 2 + 1];
+  }
+  const double mean = stats[c], is = stats[C + c];
+  const double gm = gamma ? gamma[c] : 1.0;
+  const double sdxh = sdzy - mean * sdz;  // sum dz*(y-mean)
+  if (dgamma) dgamma[c] = (float)(is * sdxh);
+  if (dbeta) dbeta[c] = (float)sdz;
+  const double k1 = gm * is;
+  const double k2 = -gm * is * is * is * sdxh / (double)n;
+  const double k3 = -gm * is * sdz / (double)n - k2 * mean;
+  kbuf[c] = (float)k1;
+  kbuf[C + c] = (float)k2;
+  kbuf[2 * C + c] = (float)k3;
+  if (sums_out) {
+    sums_out[c * 2] = sdz;
+    sums_out[c * 2 + 1] = sdzy;
+  }
+}
+
+// ============================================================================ dy2 build
+// thread = (pooled window, 4 channels).  dz = g2m at the window's argmax (of the BN2
+// output z, first max in scan order), dy2 = k1*dz + k2*y2 + k3 for all 4 pixels,
+// written as bf16 hi|lo (64-channel records).  Pixels of an unpooled last row/col
+// (odd P) get dz = 0.
+__global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict__ y2, const float4* __restrict__ g2m,
+                                                        const float* __restrict__ aff2, const float* __restrict__ kbuf,
+                                                        uint2* __restrict__ dy2, int B, int P, int Q) {
+  const int PH = (P + 1) / 2;
+  const int64_t total = (int64_t)B * PH * PH * 8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c4 = (int)(e & 7);
+    const int64_t w = e >> 3;
+    const int wx = (int)(w % PH);
+    const int64_t t = w / PH;
+    const int wy = (int)(t % PH);
+    const int b = (int)(t / PH);
+    const bool pooled = wy < Q && wx < Q;
+    float a[4], bb[4], k1[4], k2[4], k3[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      const int c = 4 * c4 + cc;
+      a[cc] = aff2[c];
+      bb[cc] = aff2[32 + c];
+      k1[cc] = kbuf[c];
+      k2[cc] = kbuf[32 + c];
+      k3[cc] = kbuf[64 + c];
+    }
+    float y[4][4];
+    bool inb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = 2 * wy + (q >> 1), cidx = 2 * wx + (q & 1);
+      inb[q] = r < P && cidx < P;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (inb[q]) v = y2[(((int64_t)b * P + r) * P + cidx) * 8 + c4];
+      y[q][0] = v.x; y[q][1] = v.y; y[q][2] = v.z; y[q][3] = v.w;
+    }
+    float gv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (pooled) {
+      const float4 gg = g2m[(((int64_t)b * Q + wy) * Q + wx) * 8 + c4];
+      gv[0] = gg.x; gv[1] = gg.y; gv[2] = gg.z; gv[3] = gg.w;
+    }
+    int am[4];
+#pragma unroll
+    for (int cc = 0; cc < 4; ++cc) {
+      float m = a[cc] * y[0][cc] + bb[cc];
+      int ai = 0;
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        const float z = a[cc] * y[q][cc] + bb[cc];
+        if (z > m || isnan(z)) { m = z; ai = q; }
+      }
+      am[cc] = pooled ? ai : -1;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!inb[q]) continue;
+      uint16_t hi[4], lo[4];
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const float dz = am[cc] == q ? gv[cc] : 0.f;
+        const float d = k1[cc] * dz + k2[cc] * y[q][cc] + k3[cc];
+        unsigned short h, l;
+        split_bf16(d, h, l);
+        hi[cc] = h;
+        lo[cc] = l;
+      }
+      const int r = 2 * wy + (q >> 1), cidx = 2 * wx + (q & 1);
+      uint2* rec = dy2 + (((int64_t)b * P + r) * P + cidx) * 16;  // 128-B record = 16 x 8 B
+      rec[c4] = make_uint2(hi[0] | ((uint32_t)hi[1] << 16), hi[2] | ((uint32_t)hi[3] << 16));
+      rec[8 + c4] = make_uint2(lo[0] | ((uint32_t)lo[1] << 16), lo[2] | ((uint32_t)lo[3] << 16));
+    }
+  }
+}
+
+// ============================================================================ layer-1 backward (sparse)
+// Workgroup tile: 8 x 32 pooled pixels (x tile 20 x 68 in LDS).  Thread (c = tid & 15,
+// slot = tid >> 4) owns channel c for pooled pixels slot, slot+16, ... of the tile and
+// accumulates: sdz, sdzy (dz * y1 at the argmax), sdzx[25] (dz * xpatch).
+constexpr int LB_PR = 8, LB_PC = 32;
+constexpr int LB_XR = 2 * LB_PR + 4, LB_XC = 2 * LB_PC + 4;
+constexpr int LB_NACC = 27;
+__global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dp1,
+                                                     const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
+                                                     const float* __restrict__ w1, const float* __restrict__ b1,
+                                                     double* __restrict__ partial, int B, int H, int W) {
+  __shared__ float xs[LB_XR * LB_XC];
+  __shared__ float red[16][16][LB_NACC + 1];
+  const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
+  const int P = H / 2, PW = W / 2;
+  const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
+  const int per_img = tiles_c * tiles_r, total = per_img * B;
+  float wr[25];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) wr[k] = w1[c * 25 + k];
+  const float bc = b1[c];
+  float acc[LB_NACC];
+#pragma unroll
+  for (int i = 0; i < LB_NACC; ++i) acc[i] = 0.f;
+
+  for (int t = xcd_remap(blockIdx.x, gridDim.x); t < total; t += gridDim.x) {
+    const int b = t / per_img, rem = t - b * per_img;
+    const int pr0 = (rem / tiles_c) * LB_PR, pc0 = (rem % tiles_c) * LB_PC;
+    const float* xb = x + (int64_t)b * H * W;
+    __syncthreads();
+    for (int e = tid; e < LB_XR * LB_XC; e += 256) {
+      const int rr = e / LB_XC, cc = e - rr * LB_XC;
+      const int gr = 2 * pr0 - 2 + rr, gc = 2 * pc0 - 2 + cc;
+      xs[e] = (gr >= 0 && gr < H && gc >= 0 && gc < W) ? xb[(int64_t)gr * W + gc] : 0.f;
+    }
+    __syncthreads();
+    for (int pp = slot; pp < LB_PR * LB_PC; pp += 16) {
+      const int pr = pp / LB_PC, pc = pp - (pp / LB_PC) * LB_PC;
+      const int gpr = pr0 + pr, gpc = pc0 + pc;
+      if (gpr >= P || gpc >= PW) continue;
+      const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
+      const unsigned short ph = reinterpret_cast<const unsigned short*>(p1 + rec * 4)[c];
+      const float phf = bf16_to_f32(ph);
+      if (!(phf > 0.f)) continue;
+      const float dz = dp1[rec * 16 + c];
+      const int a = idx1[rec * 16 + c];
+      const int lr = 2 * pr + (a >> 1), lc = 2 * pc + (a & 1);  // conv1 pixel in tile coords
+      const float* xp = xs + lr * LB_XC + lc;                      // patch origin (halo offset built in)
+      float y = bc;
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 5; ++kx) {
+          const float xv = xp[ky * LB_XC + kx];
+          y += wr[ky * 5 + kx] * xv;
+          acc[2 + ky * 5 + kx] += dz * xv;
+        }
+      acc[0] += dz;
+      acc[1] += dz * y;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < LB_NACC; ++i) red[slot][c][i] = acc[i];
+  __syncthreads();
+  for (int e = tid; e < 16 * LB_NACC; e += 256) {
+    const int cc = e / LB_NACC, i = e - cc * LB_NACC;
+    double s = 0.0;
+    for (int k = 0; k < 16; ++k) s += red[k][cc][i];
+    partial[((int64_t)blockIdx.x * 16 + cc) * LB_NACC + i] = s;
+  }
+}
+
+// Closed-form layer-1 gradients (one workgroup).  Inputs: l1_bwd partials, x
+// autocorrelation partials + border strips, BN1 stats/params, conv1 params.
+//   G[k][j] = Full(d) - sum_{excluded rows of k} R(d,row) - sum_{excluded cols} C(d,col)
+//             + sum corners,  d = o_j - o_k  (see x_autocorr / x_border)
+//   dw1[c][j] = a1 sdzx[c][j] + a2 (sum_k w1[c][k] G[k][j] + b1[c] S[j]) + a3 S[j]
+__global__ void l1_finalize_kernel(const double* __restrict__ bwd_partial, int nbwd,
+                                   const double* __restrict__ ac_partial, int nac,
+                                   const double* __restrict__ strips, const float* __restrict__ x, int B, int H, int W,
+                                   const float* __restrict__ w1, const float* __restrict__ b1,
+                                   const float* __restrict__ gamma1, const float* __restrict__ stats1,
+                                   float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dgamma1,
+                                   float* __restrict__ dbeta1, float scale) {
+  __shared__ double full[81];
+  __shared__ double G[25][25];
+  __shared__ double S[25];
+  __shared__ double acc[16][LB_NACC];
+  const int tid = threadIdx.x;
+  // fold l1_bwd partials
+  for (int e = tid; e < 16 * LB_NACC; e += blockDim.x) {
+    double s = 0.0;
+    for (int k = 0; k < nbwd; ++k) s += bwd_partial[(int64_t)k * 16 * LB_NACC + e];
+    acc[e / LB_NACC][e % LB_NACC] = s;
+  }
+  // fold autocorrelation partials into the 81 offsets
+  if (tid < 81) {
+    const int dy = tid / 9 - 4, dx = tid % 9 - 4;
+    int sy = dy, sx = dx;
+    if (dy < 0 || (dy == 0 && dx < 0)) { sy = -dy; sx = -dx; }
+    const int i = sy == 0 ? sx : 5 + (sy - 1) * 9 + (sx + 4);
+    double s = 0.0;
+    for (int k = 0; k < nac; ++k) s += ac_partial[(int64_t)k * 41 + i];
+    full[tid] = s;
+  }
+  __syncthreads();
+  // corner products (and plain corner values) computed directly from x (16 px per image)
+  for (int e = tid; e < 625 + 25; e += blockDim.x) {
+    const bool isS = e >= 625;
+    const int k = isS ? e - 625 : e / 25, j = isS ? e - 625 : e % 25;
+    const int oky = k / 5 - 2, okx = k % 5 - 2, ojy = j / 5 - 2, ojx = j % 5 - 2;
+    const int dy = ojy - oky, dx = ojx - okx;
+    const int di = (dy + 4) * 9 + (dx + 4);
+    // excluded rows / cols of U_k (u = px + o_k must map back into the image)
+    int er[2], ne = 0, ec[2], nc = 0;
+    const int ak = isS ? ojy : oky, bk = isS ? ojx : okx;
+    if (ak > 0) { for (int i = 0; i < ak; ++i) er[ne++] = i; }
+    if (ak < 0) { for (int i = 0; i < -ak; ++i) er[ne++] = H - 1 - i; }
+    if (bk > 0) { for (int i = 0; i < bk; ++i) ec[nc++] = i; }
+    if (bk < 0) { for (int i = 0; i < -bk; ++i) ec[nc++] = W - 1 - i; }
+    auto line_index_row = [&](int r) { return r < 2 ? r : (r - (H - 4)); };       // 0,1,2,3
+    auto line_index_col = [&](int cidx) { return 4 + (cidx < 2 ? cidx : (cidx - (W - 4))); };
+    double v;
+    if (!isS) {
+      v = full[di];
+      for (int i = 0; i < ne; ++i) v -= strips[line_index_row(er[i]) * 82 + di];
+      for (int i = 0; i < nc; ++i) v -= strips[line_index_col(ec[i]) * 82 + di];
+      for (int i = 0; i < ne; ++i)
+        for (int q = 0; q < nc; ++q) {
+          const int r = er[i], cc = ec[q], r2 = r + dy, c2 = cc + dx;
+          if (r2 < 0 || r2 >= H || c2 < 0 || c2 >= W) continue;
+          for (int b = 0; b < B; ++b) {
+            const float* xb = x + (int64_t)b * H * W;
+            v += (double)xb[(int64_t)r * W + cc] * xb[(int64_t)r2 * W + c2];
+          }
+        }
+      G[k][j] = v;
+    } else {
+      // S[j] = sum over U_j of x = total - excluded row sums - excluded col sums + corners
+      v = 0.0;
+      for (int i = 0; i < ne; ++i) v -= strips[line_index_row(er[i]) * 82 + 81];
+      for (int i = 0; i < nc; ++i) v -= strips[line_index_col(ec[i]) * 82 + 81];
+      for (int i = 0; i < ne; ++i)
+        for (int q = 0; q < nc; ++q)
+          for (int b = 0; b < B; ++b) v += x[(int64_t)b * H * W + (int64_t)er[i] * W + ec[q]];
+      S[j] = v;  // total added below
+    }
+  }
+  __syncthreads();
+  if (tid < 25) S[tid] += strips[8 * 82 + 81];  // total sum of x (line 8 = whole image)
+  __syncthreads();
+  // gradients per channel
+  if (tid < 16) {
+    const int c = tid;
+    const int64_t n = (int64_t)B * H * W;
+    const double mean = stats1[c], is = stats1[16 + c];
+    const double gm = gamma1 ? gamma1[c] : 1.0;
+    const double sdz = acc[c][0], sdzy = acc[c][1];
+    const double sdxh = sdzy - mean * sdz;
+    if (dgamma1) dgamma1[c] = (float)(is * sdxh);
+    if (dbeta1) dbeta1[c] = (float)sdz;
+    const double a1 = gm * is;
+    const double a2 = -gm * is * is * is * sdxh / (double)n;
+    const double a3 = -gm * is * sdz / (double)n - a2 * mean;
+    // db1 = sum dy1 = a1 sdz + a2 sum y1 + a3 n  (sum y1 = n*mean)
+    if (db1) db1[c] = (float)(scale * (a1 * sdz + a2 * (double)n * mean + a3 * (double)n));
+    for (int j = 0; j < 25; ++j) {
+      double h = (double)b1[c] * S[j];
+      for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k][j];
+      const double v = a1 * acc[c][2 + j] + a2 * h + a3 * S[j];
+      dw1[c * 25 + j] = (float)(scale * v);
+    }
+  }
+}
+
+}  // namespace tds
+
+using namespace tds;
+
+int tds_fused_num_wg(int per_cu) {
+  int dev = 0, n = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) n = prop.multiProcessorCount;
+  }
+  return n * per_cu;
+}
+
+void tds_l1_stats(const float* x, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(l1_conv_kernel<0>, dim3(nwg), dim3(256), 0, st, x, w1, b1, nullptr, partial, nullptr, nullptr, B,
+                     H, W);
+}
+
+void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
+                  int B, int H, int W, hipStream_t st) {
+  hipLaunchKernelGGL(l1_conv_kernel<1>, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, nullptr,
+                     reinterpret_cast<uint4*>(p1), idx1, B, H, W);
+}
+
+void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
+                             float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
+                             float* running_var, int64_t* num_batches, float* aff, hipStream_t st) {
+  hipLaunchKernelGGL(bn_finalize_shifted_kernel, dim3(1), dim3(64), 0, st, partial, C, nchunk, n, shift, eps, momentum,
+                     gamma, beta, stats, running_mean, running_var, num_batches, aff);
+}
+
+void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
+  hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
+  hipLaunchKernelGGL(x_border_kernel, dim3(82, 9), dim3(256), 0, st, x, strips, B, H, W);
+}
+
+int tds_head_fwd_nblk(int Q) {
+  int64_t nb = ((int64_t)Q * Q + 255) / 256;
+  if (nb > 2048) nb = 2048;
+  return (int)(nb < 1 ? 1 : nb);
+}
+
+int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, float* partial, float* logits,
+                 int nblk, int B, int P, int NC, hipStream_t st) {
+  const int Q = P / 2;
+  if (B > 8 || NC > 10) return -1;
+#define TDS_HF(MB)                                                                                                   \
+  hipLaunchKernelGGL((head_fwd_kernel<MB>), dim3(nblk), dim3(256), 0, st, reinterpret_cast<const float4*>(y2), Wfc, \
+                     aff2, partial, B, P, Q, NC)
+  if (B <= 1) TDS_HF(1);
+  else if (B <= 2) TDS_HF(2);
+  else if (B <= 4) TDS_HF(4);
+  else TDS_HF(8);
+#undef TDS_HF
+  hipLaunchKernelGGL(head_logits_reduce_kernel, dim3((B * NC + 63) / 64), dim3(64), 0, st, partial, bias, logits, nblk,
+                     B * NC, NC);
+  return 0;
+}
+
+int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
+                 double* partial, int nblk, int B, int P, int NC, float scale, hipStream_t st) {
+  const int Q = P / 2;
+  if (B > 8 || NC > 10) return -1;
+#define TDS_HB(MB)                                                                                                   \
+  hipLaunchKernelGGL((head_bwd_kernel<MB>), dim3(nblk), dim3(256), 0, st, reinterpret_cast<const float4*>(y2), Wfc, \
+                     aff2, dlogits, dW, reinterpret_cast<float4*>(g2m), partial, B, P, Q, NC, scale)
+  if (B <= 1) TDS_HB(1);
+  else if (B <= 2) TDS_HB(2);
+  else if (B <= 4) TDS_HB(4);
+  else TDS_HB(8);
+#undef TDS_HB
+  return 0;
+}
+
+void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
+                          float* dgamma, float* dbeta, float* kbuf, hipStream_t st) {
+  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(1), dim3(64), 0, st, partial, C, nchunk, n, gamma, stats, dgamma,
+                     dbeta, kbuf, nullptr);
+}
+
+void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const float* kbuf, void* dy2, int B, int P,
+                   hipStream_t st) {
+  const int Q = P / 2, PH = (P + 1) / 2;
+  const int64_t total = (int64_t)B * PH * PH * 8;
+  int64_t g = (total + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(dy2_build_kernel, dim3((unsigned)g), dim3(256), 0, st, reinterpret_cast<const float4*>(y2),
+                     reinterpret_cast<const float4*>(g2m), aff2, kbuf, reinterpret_cast<uint2*>(dy2), B, P, Q);
+}
+
+void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
+                double* partial, int nwg, int B, int H, int W, hipStream_t st) {
+  hipLaunchKernelGGL(l1_bwd_kernel, dim3(nwg), dim3(256), 0, st, x, dp1, reinterpret_cast<const uint4*>(p1), idx1, w1,
+                     b1, partial, B, H, W);
+}
+
+void tds_l1_finalize(const double* bwd_partial, int nbwd, const double* ac_partial, int nac, const double* strips,
+                     const float* x, int B, int H, int W, const float* w1, const float* b1, const float* gamma1,
+                     const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1, float scale,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(l1_finalize_kernel, dim3(1), dim3(256), 0, st, bwd_partial, nbwd, ac_partial, nac, strips, x, B, H,
+                     W, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+}

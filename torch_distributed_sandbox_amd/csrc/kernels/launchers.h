@@ -54,3 +54,39 @@ int tds_linear_fwd_skinny(const float* x, const float* W, const float* bias, flo
                           int64_t K, int nblk, hipStream_t st);
 int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float* dx, float* dW, float* db, int M,
                           int N, int64_t K, float scale, int acc_w, hipStream_t st);
+
+// ---- conv2_bf16x3.hip (NHWC, bf16x3 split MFMA)
+void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t st);
+int tds_conv2_num_wg();
+void tds_conv2_fwd_bf16x3(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg,
+                          int B, int P, hipStream_t st);
+void tds_conv2_dgrad_bf16x3(const void* dy2, const short* wd, float* dp1, int nwg, int B, int P, hipStream_t st);
+void tds_conv2_wgrad_bf16x3(const void* dy2, const void* p1, float* slab, float* dw, float* db, float scale, int nwg,
+                            int B, int P, hipStream_t st);
+int tds_conv2_lds_bytes(int which);
+
+// ---- convnet_fused.hip
+int tds_fused_num_wg(int per_cu);
+void tds_l1_stats(const float* x, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
+                  hipStream_t st);
+void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
+                  int B, int H, int W, hipStream_t st);
+void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
+                             float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
+                             float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
+void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
+int tds_head_fwd_nblk(int Q);
+int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, float* partial, float* logits,
+                 int nblk, int B, int P, int NC, hipStream_t st);
+int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
+                 double* partial, int nblk, int B, int P, int NC, float scale, hipStream_t st);
+void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
+                          float* dgamma, float* dbeta, float* kbuf, hipStream_t st);
+void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const float* kbuf, void* dy2, int B, int P,
+                   hipStream_t st);
+void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
+                double* partial, int nwg, int B, int H, int W, hipStream_t st);
+void tds_l1_finalize(const double* bwd_partial, int nbwd, const double* ac_partial, int nac, const double* strips,
+                     const float* x, int B, int H, int W, const float* w1, const float* b1, const float* gamma1,
+                     const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1, float scale,
+                     hipStream_t st);
