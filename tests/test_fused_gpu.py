@@ -53,7 +53,8 @@ def test_layer1_forward(gpu):
     z = F.batch_norm(y, rmr, rvr, g1.double().cpu(), be1.double().cpu(), True, 0.1, 1e-5)
     ref, ridx = F.max_pool2d(F.relu(z), 2, 2, return_indices=True)
     got = unpack_hilo(p1, 16).permute(0, 3, 1, 2)
-    _check(got, ref, 2e-6, "p1")
+    # p1 is stored as bf16 hi+lo (16 significant bits): <= 2^-16 relative representation error
+    _check(got, ref, 2e-5, "p1")
     _check(rm, rmr, 1e-5, "running_mean")
     _check(rv, rvr, 1e-5, "running_var")
     assert int(nbt.item()) == 1

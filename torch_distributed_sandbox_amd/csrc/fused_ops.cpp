@@ -66,16 +66,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   auto partial = at::empty({16 * nwg * 2}, fo.dtype(at::kDouble));
   tds_l1_stats(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg,
                (int)B, (int)H, (int)W, st);
+  auto sums = at::empty({32}, fo.dtype(at::kDouble));
+  tds_reduce_partials(partial.data_ptr<double>(), sums.data_ptr<double>(), 32, nwg, 2, (int64_t)nwg * 2, 2, st);
   auto stats = at::empty({32}, fo);
   auto aff = at::empty({32}, fo);
-  tds_bn_finalize_shifted(partial.data_ptr<double>(), 16, nwg, B * H * W, b1.data_ptr<float>(), (float)eps,
+  tds_bn_finalize_shifted(sums.data_ptr<double>(), 16, 1, B * H * W, b1.data_ptr<float>(), (float)eps,
                           (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   auto p1 = at::empty({B, P, P, 16}, fo);  // carrier of bf16 [B,P,P,32]
   auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
   tds_l1_apply(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(), p1.data_ptr(),
                idx1.data_ptr<uint8_t>(), nwg, (int)B, (int)H, (int)W, st);
   const int nac = ac_wg();
-  auto ac = at::empty({nac * 41}, fo.dtype(at::kDouble));
+  auto ac = at::empty({nac * 42}, fo.dtype(at::kDouble));
   auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
   tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
                  st);
@@ -134,15 +136,19 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
   const float* bf = optf(bfc, NC, "fc.bias");
   c10::DeviceGuard guard(y2.device());
   hipStream_t st = stream_of(y2);
+  auto sums2 = at::empty({64}, y2.options().dtype(at::kDouble));
+  tds_reduce_partials(partial2.data_ptr<double>(), sums2.data_ptr<double>(), 64, nch, 2, (int64_t)nch * 2, 2, st);
   auto stats = at::empty({64}, y2.options());
   auto aff = at::empty({64}, y2.options());
-  tds_bn_finalize_shifted(partial2.data_ptr<double>(), 32, nch, B * P * P, b2.data_ptr<float>(), (float)eps,
+  tds_bn_finalize_shifted(sums2.data_ptr<double>(), 32, 1, B * P * P, b2.data_ptr<float>(), (float)eps,
                           (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   const int nblk = tds_head_fwd_nblk((int)Q);
-  auto part = at::empty({nblk * B * NC}, y2.options());
+  auto part = at::empty({(int64_t)nblk * B * NC}, y2.options().dtype(at::kDouble));
+  auto lsum = at::empty({B * NC}, y2.options().dtype(at::kDouble));
   auto logits = at::empty({B, NC}, y2.options());
   const int rc = tds_head_fwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
-                              part.data_ptr<float>(), logits.data_ptr<float>(), nblk, (int)B, (int)P, (int)NC, st);
+                              part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), (int)B,
+                              (int)P, (int)NC, st);
   TORCH_CHECK(rc == 0, "fused_head_forward: unsupported B/NC");
   return {logits, stats, aff};
 }
@@ -171,15 +177,17 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   }
   auto g2m = at::empty({B, Q, Q, 32}, y2.options());
   const int nblk = tds_head_fwd_nblk((int)Q);
-  auto partial = at::empty({32 * nblk * 2}, y2.options().dtype(at::kDouble));
+  auto partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
   const int rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
                               dlogits.data_ptr<float>(), dW.data_ptr<float>(), g2m.data_ptr<float>(),
-                              partial.data_ptr<double>(), nblk, (int)B, (int)P, (int)NC, (float)scale, st);
+                              partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported B/NC");
+  auto sums = at::empty({64}, y2.options().dtype(at::kDouble));
+  tds_reduce_partials(partial.data_ptr<double>(), sums.data_ptr<double>(), 64, nblk, 2, (int64_t)nblk * 2, 2, st);
   auto dgamma = at::empty({32}, y2.options());
   auto dbeta = at::empty({32}, y2.options());
   auto kbuf = at::empty({96}, y2.options());
-  tds_bn_bwd_finalize2(partial.data_ptr<double>(), 32, nblk, B * P * P, g, stats2.data_ptr<float>(),
+  tds_bn_bwd_finalize2(sums.data_ptr<double>(), 32, 1, B * P * P, g, stats2.data_ptr<float>(),
                        dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), st);
   auto dy2 = at::empty({B, P, P, 32}, y2.options());  // carrier of bf16 [B,P,P,64]
   tds_dy2_build(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
@@ -224,7 +232,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   need(b1, at::kFloat, {16}, "conv1.bias");
   need(stats1, at::kFloat, {32}, "stats1");
   need(strips, at::kDouble, {9 * 82}, "strips");
-  TORCH_CHECK(ac.is_cuda() && ac.scalar_type() == at::kDouble && ac.numel() % 41 == 0, "ac partial");
+  TORCH_CHECK(ac.is_cuda() && ac.scalar_type() == at::kDouble && ac.numel() % 42 == 0, "ac partial");
   const float* g = optf(gamma1, 16, "bn1.weight");
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
@@ -232,11 +240,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   auto partial = at::empty({(int64_t)nwg * 16 * 27}, x.options().dtype(at::kDouble));
   tds_l1_bwd(x.data_ptr<float>(), dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(), w1.data_ptr<float>(),
              b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
+  const int nac = (int)(ac.numel() / 42);
+  auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
+  auto asum = at::empty({42}, x.options().dtype(at::kDouble));
+  tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, nwg, 16 * 27, 0, 16 * 27, st);
+  tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
   auto dw1 = at::empty({16, 1, 5, 5}, x.options());
   auto db1 = at::empty({16}, x.options());
   auto dg = at::empty({16}, x.options());
   auto dbe = at::empty({16}, x.options());
-  tds_l1_finalize(partial.data_ptr<double>(), nwg, ac.data_ptr<double>(), (int)(ac.numel() / 41),
+  tds_l1_finalize(bsum.data_ptr<double>(), 1, asum.data_ptr<double>(), 1,
                   strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W, w1.data_ptr<float>(),
                   b1.data_ptr<float>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(), db1.data_ptr<float>(),
                   dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale, st);

@@ -227,14 +227,14 @@ constexpr int AC_TR = 16, AC_TC = 64;
 __global__ __launch_bounds__(256) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
                                                          int B, int H, int W) {
   __shared__ __attribute__((aligned(16))) float xs[(AC_TR + 4) * (AC_TC + 8 + 4)];
-  __shared__ double red[4][41];
+  __shared__ double red[4][42];
   constexpr int XS = AC_TC + 12;  // cols c0-4 .. c0+TC+4 (+pad)
   const int tid = threadIdx.x;
   const int tiles_c = (W + AC_TC - 1) / AC_TC, tiles_r = (H + AC_TR - 1) / AC_TR;
   const int total = tiles_c * tiles_r * B;
-  float acc[41];
+  float acc[42];
 #pragma unroll
-  for (int i = 0; i < 41; ++i) acc[i] = 0.f;
+  for (int i = 0; i < 42; ++i) acc[i] = 0.f;
   const int tr = tid >> 4, tc = (tid & 15) * 4;  // thread: row tr, cols tc..tc+3
   for (int t = blockIdx.x; t < total; t += gridDim.x) {
     const int b = t / (tiles_c * tiles_r), rem = t % (tiles_c * tiles_r);
@@ -264,36 +264,28 @@ __global__ __launch_bounds__(256) void x_autocorr_kernel(const float* __restrict
       for (int dy = 1; dy <= 4; ++dy)
 #pragma unroll
         for (int dx = -4; dx <= 4; ++dx) acc[i++] += u * w[dy][4 + p + dx];
+      acc[41] += u;
     }
   }
   const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
-  for (int i = 0; i < 41; ++i) {
+  for (int i = 0; i < 42; ++i) {
     const float s = wave_sum(acc[i]);
     if (lane == 0) red[wv][i] = s;
   }
   __syncthreads();
-  if (tid < 41) partial[(int64_t)blockIdx.x * 41 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+  if (tid < 42) partial[(int64_t)blockIdx.x * 42 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
 }
 
 // Border strips: for each image, line L in {row 0,1,H-2,H-1, col 0,1,W-2,W-1} and d in
 // [-4,4]^2: strip[L][d] = sum_{u on line L} x(u) x(u+d); also plain line sums (d = "none").
-// grid: (82 (81 d + 1 plain), 9 lines; line 8 = whole-image plain sum), block reduces over
-// B images and the line.
+// grid: (82 (81 d + 1 plain), 8 lines), block reduces over B images and the line.
 __global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__ x, double* __restrict__ strips,
                                                        int B, int H, int W) {
   __shared__ double sh[8];
   const int di = blockIdx.x, L = blockIdx.y;
   const int dy = di / 9 - 4, dx = di % 9 - 4;
   const bool plain = di == 81;
-  if (L == 8) {  // whole-image plain sum (only slot 81 is meaningful)
-    double s = 0.0;
-    if (plain)
-      for (int64_t i = threadIdx.x; i < (int64_t)B * H * W; i += blockDim.x) s += x[i];
-    s = block_sum(s, sh);
-    if (threadIdx.x == 0) strips[8 * 82 + di] = s;
-    return;
-  }
   const bool is_row = L < 4;
   const int fixed = is_row ? (L < 2 ? L : H - 4 + L) : (L < 6 ? L - 4 : W - 8 + L);
   const int len = is_row ? W : H;
@@ -317,60 +309,91 @@ __global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__
 }
 
 // ============================================================================ head: BN2 + ReLU + pool + fc
-// One thread per pooled position (py, px): loops channels in groups of 4 and all
-// images, so W (fc weight, [NC][32][Q][Q] in reference flatten order) is read once.
+// Workgroup = one pooled row py x 64 pooled columns, all images, all channels.
+// Lane = pooled column, wave w = channels 8w..8w+7.  The fc weights of the
+// tile (W[j][c][py][px0..px0+63], coalesced over lanes) stay in registers for
+// all images; per image the two y2 rows (2 x 128 NHWC records) are staged into
+// LDS with coalesced 16-B loads (record stride padded to 144 B).
+constexpr int HD_PX = 64;
+constexpr int HD_REC = 144;                 // padded LDS record stride (bytes)
+constexpr int HD_LDS = 2 * 2 * HD_PX * HD_REC;
+
+__device__ __forceinline__ void head_stage(const float4* __restrict__ y2, char* lds, int b, int py, int px0, int P,
+                                           int Q) {
+  // 2 rows x 128 records x 8 float4
+  for (int e = threadIdx.x; e < 2 * 2 * HD_PX * 8; e += blockDim.x) {
+    const int chunk = e & 7, rec = (e >> 3) & 127, row = e >> 10;
+    const int col = 2 * px0 + rec;
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (col < 2 * Q) v = y2[(((int64_t)b * P + 2 * py + row) * P + col) * 8 + chunk];
+    *reinterpret_cast<float4*>(lds + (row * 2 * HD_PX + rec) * HD_REC + chunk * 16) = v;
+  }
+}
+
+// z = a*y + b for the 4 pixels of this lane's window, channels 8w..8w+7
+__device__ __forceinline__ void head_window(const char* lds, int lane, int wv, const float* a, const float* bb,
+                                            float* p, float* yarg, bool* pos) {
+  float y[4][8];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = q >> 1, rec = 2 * lane + (q & 1);
+    const float4 u0 = *reinterpret_cast<const float4*>(lds + (row * 2 * HD_PX + rec) * HD_REC + wv * 32);
+    const float4 u1 = *reinterpret_cast<const float4*>(lds + (row * 2 * HD_PX + rec) * HD_REC + wv * 32 + 16);
+    y[q][0] = u0.x; y[q][1] = u0.y; y[q][2] = u0.z; y[q][3] = u0.w;
+    y[q][4] = u1.x; y[q][5] = u1.y; y[q][6] = u1.z; y[q][7] = u1.w;
+  }
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float m = a[c] * y[0][c] + bb[c], ya = y[0][c];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float z = a[c] * y[q][c] + bb[c];
+      if (z > m || isnan(z)) { m = z; ya = y[q][c]; }
+    }
+    pos[c] = m > 0.f;
+    p[c] = m > 0.f ? m : (isnan(m) ? m : 0.f);
+    yarg[c] = ya;
+  }
+}
+
 template <int MAXB>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
-                                                       const float* __restrict__ aff2, float* __restrict__ partial,
+                                                       const float* __restrict__ aff2, double* __restrict__ partial,
                                                        int B, int P, int Q, int NC) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ float red[4][MAXB * 10];
-  const int tid = threadIdx.x;
-  const int64_t QQ = (int64_t)Q * Q;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int py = blockIdx.y, px0 = blockIdx.x * HD_PX, px = px0 + lane;
+  const bool valid = px < Q;
+  const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)py * Q + px;
+  float w[10][8], a[8], bb[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    a[c] = aff2[8 * wv + c];
+    bb[c] = aff2[32 + 8 * wv + c];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) w[j][c] = (valid && j < NC) ? Wfc[((int64_t)j * 32 + 8 * wv + c) * QQ + pos] : 0.f;
+  }
   float acc[MAXB][10];
 #pragma unroll
   for (int b = 0; b < MAXB; ++b)
 #pragma unroll
     for (int j = 0; j < 10; ++j) acc[b][j] = 0.f;
-  for (int64_t pos = (int64_t)blockIdx.x * blockDim.x + tid; pos < QQ; pos += (int64_t)gridDim.x * blockDim.x) {
-    const int py = (int)(pos / Q), px = (int)(pos - (int64_t)py * Q);
-#pragma unroll 1
-    for (int c4 = 0; c4 < 8; ++c4) {
-      float wj[10][4];
 #pragma unroll
-      for (int j = 0; j < 10; ++j)
+  for (int b = 0; b < MAXB; ++b) {
+    if (b < B) {
+      __syncthreads();
+      head_stage(y2, smem, b, py, px0, P, Q);
+      __syncthreads();
+      float p[8], ya[8];
+      bool ps[8];
+      head_window(smem, lane, wv, a, bb, p, ya, ps);
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc)
-          wj[j][cc] = j < NC ? Wfc[((int64_t)j * 32 + 4 * c4 + cc) * QQ + pos] : 0.f;
-      float a[4], bb[4];
+      for (int c = 0; c < 8; ++c)
 #pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        a[cc] = aff2[4 * c4 + cc];
-        bb[cc] = aff2[32 + 4 * c4 + cc];
-      }
-#pragma unroll
-      for (int b = 0; b < MAXB; ++b) {
-        if (b < B) {
-          const int64_t base = (((int64_t)b * P + 2 * py) * P + 2 * px) * 8 + c4;  // float4 index
-          const float4 v00 = y2[base], v01 = y2[base + 8], v10 = y2[base + (int64_t)P * 8], v11 = y2[base + (int64_t)P * 8 + 8];
-          const float y[4][4] = {{v00.x, v00.y, v00.z, v00.w}, {v01.x, v01.y, v01.z, v01.w},
-                                 {v10.x, v10.y, v10.z, v10.w}, {v11.x, v11.y, v11.z, v11.w}};
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) {
-            float m = a[cc] * y[0][cc] + bb[cc];
-#pragma unroll
-            for (int q = 1; q < 4; ++q) {
-              const float z = a[cc] * y[q][cc] + bb[cc];
-              if (z > m || isnan(z)) m = z;
-            }
-            const float p = m > 0.f ? m : (isnan(m) ? m : 0.f);
-#pragma unroll
-            for (int j = 0; j < 10; ++j) acc[b][j] += p * wj[j][cc];
-          }
-        }
-      }
+        for (int j = 0; j < 10; ++j) acc[b][j] += p[c] * w[j][c];
     }
   }
-  const int lane = tid & 63, wv = tid >> 6;
 #pragma unroll
   for (int b = 0; b < MAXB; ++b)
 #pragma unroll
@@ -379,109 +402,112 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const float4* __restrict_
       if (lane == 0) red[wv][b * 10 + j] = s;
     }
   __syncthreads();
-  for (int i = tid; i < B * NC; i += blockDim.x) {
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  for (int i = threadIdx.x; i < B * NC; i += blockDim.x) {
     const int b = i / NC, j = i % NC;
-    partial[(int64_t)blockIdx.x * B * NC + i] =
-        red[0][b * 10 + j] + red[1][b * 10 + j] + red[2][b * 10 + j] + red[3][b * 10 + j];
+    partial[(int64_t)blk * B * NC + i] = (double)red[0][b * 10 + j] + (double)red[1][b * 10 + j] +
+                                         (double)red[2][b * 10 + j] + (double)red[3][b * 10 + j];
   }
 }
 
-__global__ void head_logits_reduce_kernel(const float* __restrict__ partial, const float* __restrict__ bias,
-                                          float* __restrict__ logits, int nblk, int BN, int NC) {
+// logits[i] = sums[i] + bias[i % NC]
+__global__ void head_logits_kernel(const double* __restrict__ sums, const float* __restrict__ bias,
+                                   float* __restrict__ logits, int BN, int NC) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= BN) return;
-  double s = 0.0;
-  for (int k = 0; k < nblk; ++k) s += partial[(int64_t)k * BN + i];
-  logits[i] = (float)s + (bias ? bias[i % NC] : 0.f);
+  if (i < BN) logits[i] = (float)sums[i] + (bias ? bias[i % NC] : 0.f);
 }
 
 // Backward of the head.  dl = dlogits [B][NC].
 //   dW[j][c][pos] = scale * sum_b dl[b][j] p2[b][c][pos]   (written into dW_out, e.g. the DDP bucket)
 //   g2m[b][pos][c] = (sum_j dl[b][j] W[j][c][pos]) * [p2 > 0]     (NHWC, fp32)
-//   red partial per block: [c][0] += g2m (= sum dz2), [c][1] += g2m * y2(argmax)
+//   partial[c][blk][2] = { sum g2m (= sum dz2), sum g2m * y2(argmax) }
 template <int MAXB>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
                                                        const float* __restrict__ aff2, const float* __restrict__ dl,
                                                        float* __restrict__ dW, float4* __restrict__ g2m,
                                                        double* __restrict__ partial, int B, int P, int Q, int NC,
                                                        float scale) {
-  __shared__ float red[4][64];
-  const int tid = threadIdx.x;
-  const int64_t QQ = (int64_t)Q * Q;
-  float sdz[32], sdy[32];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float dls[MAXB * 10];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int py = blockIdx.y, px0 = blockIdx.x * HD_PX, px = px0 + lane;
+  const bool valid = px < Q;
+  const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)py * Q + px;
+  if (threadIdx.x < MAXB * 10) {
+    const int b = threadIdx.x / 10, j = threadIdx.x % 10;
+    dls[threadIdx.x] = (b < B && j < NC) ? dl[b * NC + j] : 0.f;
+  }
+  float w[10][8], dwa[10][8], a[8], bb[8], sdz[8], sdy[8];
 #pragma unroll
-  for (int c = 0; c < 32; ++c) sdz[c] = sdy[c] = 0.f;
-  for (int64_t pos = (int64_t)blockIdx.x * blockDim.x + tid; pos < QQ; pos += (int64_t)gridDim.x * blockDim.x) {
-    const int py = (int)(pos / Q), px = (int)(pos - (int64_t)py * Q);
+  for (int c = 0; c < 8; ++c) {
+    a[c] = aff2[8 * wv + c];
+    bb[c] = aff2[32 + 8 * wv + c];
+    sdz[c] = sdy[c] = 0.f;
 #pragma unroll
-    for (int c4 = 0; c4 < 8; ++c4) {
-      float wj[10][4], dwa[10][4];
-#pragma unroll
-      for (int j = 0; j < 10; ++j)
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          wj[j][cc] = j < NC ? Wfc[((int64_t)j * 32 + 4 * c4 + cc) * QQ + pos] : 0.f;
-          dwa[j][cc] = 0.f;
-        }
-      float a[4], bb[4];
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        a[cc] = aff2[4 * c4 + cc];
-        bb[cc] = aff2[32 + 4 * c4 + cc];
-      }
-#pragma unroll 1
-      for (int b = 0; b < MAXB && b < B; ++b) {
-        const int64_t base = (((int64_t)b * P + 2 * py) * P + 2 * px) * 8 + c4;
-        const float4 v00 = y2[base], v01 = y2[base + 8], v10 = y2[base + (int64_t)P * 8], v11 = y2[base + (int64_t)P * 8 + 8];
-        const float y[4][4] = {{v00.x, v00.y, v00.z, v00.w}, {v01.x, v01.y, v01.z, v01.w},
-                               {v10.x, v10.y, v10.z, v10.w}, {v11.x, v11.y, v11.z, v11.w}};
-        float gout[4];
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          float m = a[cc] * y[0][cc] + bb[cc], ya = y[0][cc];
-#pragma unroll
-          for (int q = 1; q < 4; ++q) {
-            const float z = a[cc] * y[q][cc] + bb[cc];
-            if (z > m || isnan(z)) { m = z; ya = y[q][cc]; }
-          }
-          const float p = m > 0.f ? m : 0.f;
-          float gsum = 0.f;
-#pragma unroll
-          for (int j = 0; j < 10; ++j) {
-            const float d = j < NC ? dl[b * NC + j] : 0.f;
-            gsum += d * wj[j][cc];
-            dwa[j][cc] += d * p;
-          }
-          const float gm = m > 0.f ? gsum : 0.f;
-          gout[cc] = gm;
-          sdz[4 * c4 + cc] += gm;
-          sdy[4 * c4 + cc] += gm * ya;
-        }
-        g2m[((int64_t)b * QQ + pos) * 8 + c4] = make_float4(gout[0], gout[1], gout[2], gout[3]);
-      }
-#pragma unroll
-      for (int j = 0; j < 10; ++j)
-        if (j < NC)
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) dW[((int64_t)j * 32 + 4 * c4 + cc) * QQ + pos] = scale * dwa[j][cc];
+    for (int j = 0; j < 10; ++j) {
+      w[j][c] = (valid && j < NC) ? Wfc[((int64_t)j * 32 + 8 * wv + c) * QQ + pos] : 0.f;
+      dwa[j][c] = 0.f;
     }
   }
-  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll 1
+  for (int b = 0; b < B && b < MAXB; ++b) {
+    __syncthreads();
+    head_stage(y2, smem, b, py, px0, P, Q);
+    __syncthreads();
+    float p[8], ya[8];
+    bool ps[8];
+    head_window(smem, lane, wv, a, bb, p, ya, ps);
+    float gm[8];
 #pragma unroll
-  for (int c = 0; c < 32; ++c) {
+    for (int c = 0; c < 8; ++c) {
+      float g = 0.f;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const float d = dls[b * 10 + j];
+        g += d * w[j][c];
+        dwa[j][c] += d * p[c];
+      }
+      gm[c] = ps[c] ? g : 0.f;
+      if (valid) {
+        sdz[c] += gm[c];
+        sdy[c] += gm[c] * ya[c];
+      }
+    }
+    if (valid) {
+      float4* dst = g2m + ((int64_t)b * QQ + pos) * 8 + 2 * wv;
+      dst[0] = make_float4(gm[0], gm[1], gm[2], gm[3]);
+      dst[1] = make_float4(gm[4], gm[5], gm[6], gm[7]);
+    }
+  }
+  if (valid) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (j < NC)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) dW[((int64_t)j * 32 + 8 * wv + c) * QQ + pos] = scale * dwa[j][c];
+  }
+  const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
     const float s0 = wave_sum(sdz[c]);
     const float s1 = wave_sum(sdy[c]);
     if (lane == 0) {
-      red[wv][2 * c] = s0;
-      red[wv][2 * c + 1] = s1;
+      partial[((int64_t)(8 * wv + c) * nblk + blk) * 2 + 0] = s0;
+      partial[((int64_t)(8 * wv + c) * nblk + blk) * 2 + 1] = s1;
     }
   }
-  __syncthreads();
-  if (tid < 64) {
-    const int c = tid >> 1, k = tid & 1;
-    partial[((int64_t)c * gridDim.x + blockIdx.x) * 2 + k] =
-        (double)red[0][tid] + (double)red[1][tid] + (double)red[2][tid] + (double)red[3][tid];
-  }
+}
+
+// out[e] = sum_k in[(e / inner) * ostride + (e % inner) + k * kstride]  (one workgroup per output, fp64)
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __restrict__ in, double* __restrict__ out,
+                                                              int nchunk, int inner, int64_t ostride, int64_t kstride) {
+  __shared__ double sh[8];
+  const int e = blockIdx.x;
+  const int64_t base = (int64_t)(e / inner) * ostride + (e % inner);
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += in[base + (int64_t)k * kstride];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) out[e] = s;
 }
 
 // BN backward finalize from (sum dz, sum dz*y) partials:
@@ -694,7 +720,7 @@ __global__ void l1_finalize_kernel(const double* __restrict__ bwd_partial, int n
     if (dy < 0 || (dy == 0 && dx < 0)) { sy = -dy; sx = -dx; }
     const int i = sy == 0 ? sx : 5 + (sy - 1) * 9 + (sx + 4);
     double s = 0.0;
-    for (int k = 0; k < nac; ++k) s += ac_partial[(int64_t)k * 41 + i];
+    for (int k = 0; k < nac; ++k) s += ac_partial[(int64_t)k * 42 + i];
     full[tid] = s;
   }
   __syncthreads();
@@ -741,7 +767,11 @@ __global__ void l1_finalize_kernel(const double* __restrict__ bwd_partial, int n
     }
   }
   __syncthreads();
-  if (tid < 25) S[tid] += strips[8 * 82 + 81];  // total sum of x (line 8 = whole image)
+  if (tid < 25) {
+    double tot = 0.0;  // whole-image sum of x (autocorrelation slot 41)
+    for (int k = 0; k < nac; ++k) tot += ac_partial[(int64_t)k * 42 + 41];
+    S[tid] += tot;
+  }
   __syncthreads();
   // gradients per channel
   if (tid < 16) {
@@ -801,38 +831,40 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
 
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
   hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
-  hipLaunchKernelGGL(x_border_kernel, dim3(82, 9), dim3(256), 0, st, x, strips, B, H, W);
+  hipLaunchKernelGGL(x_border_kernel, dim3(82, 8), dim3(256), 0, st, x, strips, B, H, W);
 }
 
-int tds_head_fwd_nblk(int Q) {
-  int64_t nb = ((int64_t)Q * Q + 255) / 256;
-  if (nb > 2048) nb = 2048;
-  return (int)(nb < 1 ? 1 : nb);
-}
+int tds_head_fwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
 
-int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, float* partial, float* logits,
-                 int nblk, int B, int P, int NC, hipStream_t st) {
+// partial: double [nblk][B*NC]; sums: double [B*NC] workspace
+int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
+                 float* logits, int B, int P, int NC, hipStream_t st) {
   const int Q = P / 2;
-  if (B > 8 || NC > 10) return -1;
-#define TDS_HF(MB)                                                                                                   \
-  hipLaunchKernelGGL((head_fwd_kernel<MB>), dim3(nblk), dim3(256), 0, st, reinterpret_cast<const float4*>(y2), Wfc, \
+  if (B > 8 || NC > 10 || Q < 1) return -1;
+  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
+#define TDS_HF(MB)                                                                                                 \
+  hipLaunchKernelGGL((head_fwd_kernel<MB>), grid, dim3(256), HD_LDS, st, reinterpret_cast<const float4*>(y2), Wfc, \
                      aff2, partial, B, P, Q, NC)
   if (B <= 1) TDS_HF(1);
   else if (B <= 2) TDS_HF(2);
   else if (B <= 4) TDS_HF(4);
   else TDS_HF(8);
 #undef TDS_HF
-  hipLaunchKernelGGL(head_logits_reduce_kernel, dim3((B * NC + 63) / 64), dim3(64), 0, st, partial, bias, logits, nblk,
-                     B * NC, NC);
+  const int nblk = grid.x * grid.y, BN = B * NC;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(BN), dim3(256), 0, st, partial, sums, nblk, BN, (int64_t)0,
+                     (int64_t)BN);
+  hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);
   return 0;
 }
 
+// partial: double [32][nblk][2]
 int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
-                 double* partial, int nblk, int B, int P, int NC, float scale, hipStream_t st) {
+                 double* partial, int B, int P, int NC, float scale, hipStream_t st) {
   const int Q = P / 2;
-  if (B > 8 || NC > 10) return -1;
-#define TDS_HB(MB)                                                                                                   \
-  hipLaunchKernelGGL((head_bwd_kernel<MB>), dim3(nblk), dim3(256), 0, st, reinterpret_cast<const float4*>(y2), Wfc, \
+  if (B > 8 || NC > 10 || Q < 1) return -1;
+  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
+#define TDS_HB(MB)                                                                                                 \
+  hipLaunchKernelGGL((head_bwd_kernel<MB>), grid, dim3(256), HD_LDS, st, reinterpret_cast<const float4*>(y2), Wfc, \
                      aff2, dlogits, dW, reinterpret_cast<float4*>(g2m), partial, B, P, Q, NC, scale)
   if (B <= 1) TDS_HB(1);
   else if (B <= 2) TDS_HB(2);
@@ -840,6 +872,11 @@ int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const flo
   else TDS_HB(8);
 #undef TDS_HB
   return 0;
+}
+
+void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(n), dim3(256), 0, st, in, out, nchunk, inner, ostride, kstride);
 }
 
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,

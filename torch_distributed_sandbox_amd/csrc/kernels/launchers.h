@@ -76,10 +76,12 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
                              float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
 int tds_head_fwd_nblk(int Q);
-int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, float* partial, float* logits,
-                 int nblk, int B, int P, int NC, hipStream_t st);
+int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
+                 float* logits, int B, int P, int NC, hipStream_t st);
 int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
-                 double* partial, int nblk, int B, int P, int NC, float scale, hipStream_t st);
+                 double* partial, int B, int P, int NC, float scale, hipStream_t st);
+void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
+                         hipStream_t st);
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
                           float* dgamma, float* dbeta, float* kbuf, hipStream_t st);
 void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const float* kbuf, void* dy2, int B, int P,
