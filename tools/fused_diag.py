@@ -1,5 +1,6 @@
 """Per-parameter gradient error of the fused plan (and the exact layers plan) vs an fp64 reference."""
-import sys
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
