@@ -36,9 +36,10 @@ def unpack_hilo(carrier, C):
     return b[..., :C].float() + b[..., C:2 * C].float()
 
 
-def test_layer1_forward(gpu):
+@pytest.mark.parametrize("H", [68, 256, 264])
+def test_layer1_forward(gpu, H):
     torch.manual_seed(0)
-    B, H = 3, 68
+    B = 3
     x = torch.rand(B, 1, H, H, device=gpu)
     w1 = torch.randn(16, 1, 5, 5, device=gpu) * 0.2
     b1 = torch.randn(16, device=gpu) * 0.1
@@ -84,7 +85,39 @@ def test_conv2_forward(gpu):
     _check(s[:, 1], (yc * yc).sum((0, 2, 3)), 1e-4, "sumsq")
 
 
-@pytest.mark.parametrize("P", [40, 37])
+@pytest.mark.parametrize("P", [64, 128, 200])
+def test_head_fwd_bwd(gpu, P):
+    """BN2(batch stats) + ReLU + pool + fc forward/backward, incl. the dy2 build, vs fp64 autograd."""
+    torch.manual_seed(P)
+    B, NC = 3, 10
+    Q = P // 2
+    y2 = torch.randn(B, P, P, 32, device=gpu)
+    b2 = torch.randn(32, device=gpu) * 0.1
+    g2 = torch.rand(32, device=gpu) + 0.5
+    be2 = torch.randn(32, device=gpu) * 0.1
+    wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
+    bfc = torch.randn(NC, device=gpu)
+    yc = (y2 - b2).double()
+    partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()  # [32][1][2]
+    logits, stats2, aff2 = _ops().fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc)
+    yr = y2.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
+    gr = g2.double().cpu().requires_grad_(True)
+    ber = be2.double().cpu().requires_grad_(True)
+    wr = wfc.double().cpu().requires_grad_(True)
+    z = F.batch_norm(yr, None, None, gr, ber, True, 0.1, 1e-5)
+    pz = F.max_pool2d(F.relu(z), 2, 2)
+    ref = F.linear(pz.reshape(B, -1), wr, bfc.double().cpu())
+    _check(logits, ref, 1e-5, "logits")
+    dl = torch.randn(B, NC, device=gpu)
+    ref.backward(dl.double().cpu())
+    dW, dbfc, dg2, dbe2, dy2 = _ops().fused_head_backward(dl, y2, stats2, aff2, g2, wfc, None, 1.0)
+    _check(dW, wr.grad, 1e-5, "dW")
+    _check(dg2, gr.grad, 1e-5, "dgamma2")
+    _check(dbe2, ber.grad, 1e-5, "dbeta2")
+    _check(unpack_hilo(dy2, 32).permute(0, 3, 1, 2), yr.grad, 1e-4, "dy2")
+
+
+@pytest.mark.parametrize("P", [40, 37, 128, 200])
 def test_conv2_backward(gpu, P):
     torch.manual_seed(0)
     B = 2
@@ -139,12 +172,14 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
         assert abs(loss.item() - rl.item()) <= 2e-4 * max(1.0, abs(rl.item())), (loss.item(), rl.item())
         rp = dict(ref.named_parameters())
         for n, p in ours.named_parameters():
-            e, sc = _err(p.grad, rp[n].grad)
+            g, rg = p.grad.double().cpu(), rp[n].grad
             if n.endswith("0.bias"):  # analytically zero (bias before BN): rounding noise both sides
                 wsc = rp[n.replace("bias", "weight")].grad.abs().max().item()
-                assert e <= 1e-3 * wsc + 1e-6, f"step {s} {n}: {e:.3e} vs weight grad {wsc:.3e}"
+                assert (g - rg).abs().max().item() <= 1e-3 * wsc + 1e-6, f"step {s} {n}"
                 continue
-            assert e <= 2e-3 * sc + 1e-9, f"step {s} {n}: err {e:.3e} vs {sc:.3e}"
+            # relative L2 (robust to rare argmax flips on near-tied pool windows)
+            rel = ((g - rg).norm() / rg.norm().clamp_min(1e-30)).item()
+            assert rel <= 1e-3, f"step {s} {n}: rel L2 err {rel:.3e}"
         opt.step()
         ropt.step()
     rb = dict(ref.named_buffers())

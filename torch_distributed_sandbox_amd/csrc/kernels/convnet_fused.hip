@@ -75,17 +75,43 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
   }
   float s_acc[4] = {0.f, 0.f, 0.f, 0.f}, q_acc[4] = {0.f, 0.f, 0.f, 0.f};
 
-  for (int t = xcd_remap(blockIdx.x, gridDim.x); t < total; t += gridDim.x) {
+  // x tile staging: LDS column 0 <-> global column c0-4 (16-B aligned since W % 4 == 0),
+  // 20 rows x 18 float4; the next tile's loads are issued before this tile's MFMAs.
+  constexpr int NV = L1_XR * 18;
+  constexpr int PER = (NV + 255) / 256;
+  float4 pre[PER];
+  auto load_tile = [&](int t) {
     const int b = t / per_img, rem = t - b * per_img;
     const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
     const float* xb = x + (int64_t)b * H * W;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < NV) {
+        const int rr = e / 18, cv = e - rr * 18;
+        const int gr = r0 - 2 + rr, gc = c0 - 4 + 4 * cv;
+        if (gr >= 0 && gr < H && gc >= 0 && gc < W) v = *reinterpret_cast<const float4*>(xb + (int64_t)gr * W + gc);
+      }
+      pre[u] = v;
+    }
+  };
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (t < total) load_tile(t);
+  for (; t < total; t += gridDim.x) {
+    const int b = t / per_img, rem = t - b * per_img;
+    const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
     __syncthreads();
-    for (int e = tid; e < L1_XR * (L1_TC + 4); e += 256) {
-      const int rr = e / (L1_TC + 4), cc = e - rr * (L1_TC + 4);
-      const int gr = r0 - 2 + rr, gc = c0 - 2 + cc;
-      xs[rr * L1_XS + cc] = (gr >= 0 && gr < H && gc >= 0 && gc < W) ? xb[(int64_t)gr * W + gc] : 0.f;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u;
+      if (e < NV) {
+        const int rr = e / 18, cv = e - rr * 18;
+        *reinterpret_cast<float4*>(xs + rr * L1_XS + 4 * cv) = pre[u];
+      }
     }
     __syncthreads();
+    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
 #pragma unroll
     for (int rp = 0; rp < 2; ++rp) {
 #pragma unroll
@@ -103,7 +129,7 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
 #pragma unroll
             for (int c = 0; c < 2; ++c) {
               const int row = 4 * wv + 2 * rp + a, seg = 2 * sp + c;
-              const float bv = xs[row * L1_XS + seg * 16 + li + koff[s]];
+              const float bv = xs[row * L1_XS + 2 + seg * 16 + li + koff[s]];  // +2: tile origin is c0-4
               acc[a][c] = mfma16x4(wa[s], bv, acc[a][c]);
             }
         }
@@ -308,195 +334,7 @@ __global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__
   if (threadIdx.x == 0) strips[L * 82 + di] = s;
 }
 
-// ============================================================================ head: BN2 + ReLU + pool + fc
-// Workgroup = one pooled row py x 64 pooled columns, all images, all channels.
-// Lane = pooled column, wave w = channels 8w..8w+7.  The fc weights of the
-// tile (W[j][c][py][px0..px0+63], coalesced over lanes) stay in registers for
-// all images; per image the two y2 rows (2 x 128 NHWC records) are staged into
-// LDS with coalesced 16-B loads (record stride padded to 144 B).
-constexpr int HD_PX = 64;
-constexpr int HD_REC = 144;                 // padded LDS record stride (bytes)
-constexpr int HD_LDS = 2 * 2 * HD_PX * HD_REC;
-
-__device__ __forceinline__ void head_stage(const float4* __restrict__ y2, char* lds, int b, int py, int px0, int P,
-                                           int Q) {
-  // 2 rows x 128 records x 8 float4
-  for (int e = threadIdx.x; e < 2 * 2 * HD_PX * 8; e += blockDim.x) {
-    const int chunk = e & 7, rec = (e >> 3) & 127, row = e >> 10;
-    const int col = 2 * px0 + rec;
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (col < 2 * Q) v = y2[(((int64_t)b * P + 2 * py + row) * P + col) * 8 + chunk];
-    *reinterpret_cast<float4*>(lds + (row * 2 * HD_PX + rec) * HD_REC + chunk * 16) = v;
-  }
-}
-
-// z = a*y + b for the 4 pixels of this lane's window, channels 8w..8w+7
-__device__ __forceinline__ void head_window(const char* lds, int lane, int wv, const float* a, const float* bb,
-                                            float* p, float* yarg, bool* pos) {
-  float y[4][8];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int row = q >> 1, rec = 2 * lane + (q & 1);
-    const float4 u0 = *reinterpret_cast<const float4*>(lds + (row * 2 * HD_PX + rec) * HD_REC + wv * 32);
-    const float4 u1 = *reinterpret_cast<const float4*>(lds + (row * 2 * HD_PX + rec) * HD_REC + wv * 32 + 16);
-    y[q][0] = u0.x; y[q][1] = u0.y; y[q][2] = u0.z; y[q][3] = u0.w;
-    y[q][4] = u1.x; y[q][5] = u1.y; y[q][6] = u1.z; y[q][7] = u1.w;
-  }
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    float m = a[c] * y[0][c] + bb[c], ya = y[0][c];
-#pragma unroll
-    for (int q = 1; q < 4; ++q) {
-      const float z = a[c] * y[q][c] + bb[c];
-      if (z > m || isnan(z)) { m = z; ya = y[q][c]; }
-    }
-    pos[c] = m > 0.f;
-    p[c] = m > 0.f ? m : (isnan(m) ? m : 0.f);
-    yarg[c] = ya;
-  }
-}
-
-template <int MAXB>
-__global__ __launch_bounds__(256) void head_fwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
-                                                       const float* __restrict__ aff2, double* __restrict__ partial,
-                                                       int B, int P, int Q, int NC) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float red[4][MAXB * 10];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int py = blockIdx.y, px0 = blockIdx.x * HD_PX, px = px0 + lane;
-  const bool valid = px < Q;
-  const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)py * Q + px;
-  float w[10][8], a[8], bb[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    a[c] = aff2[8 * wv + c];
-    bb[c] = aff2[32 + 8 * wv + c];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) w[j][c] = (valid && j < NC) ? Wfc[((int64_t)j * 32 + 8 * wv + c) * QQ + pos] : 0.f;
-  }
-  float acc[MAXB][10];
-#pragma unroll
-  for (int b = 0; b < MAXB; ++b)
-#pragma unroll
-    for (int j = 0; j < 10; ++j) acc[b][j] = 0.f;
-#pragma unroll
-  for (int b = 0; b < MAXB; ++b) {
-    if (b < B) {
-      __syncthreads();
-      head_stage(y2, smem, b, py, px0, P, Q);
-      __syncthreads();
-      float p[8], ya[8];
-      bool ps[8];
-      head_window(smem, lane, wv, a, bb, p, ya, ps);
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-#pragma unroll
-        for (int j = 0; j < 10; ++j) acc[b][j] += p[c] * w[j][c];
-    }
-  }
-#pragma unroll
-  for (int b = 0; b < MAXB; ++b)
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      const float s = wave_sum(acc[b][j]);
-      if (lane == 0) red[wv][b * 10 + j] = s;
-    }
-  __syncthreads();
-  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-  for (int i = threadIdx.x; i < B * NC; i += blockDim.x) {
-    const int b = i / NC, j = i % NC;
-    partial[(int64_t)blk * B * NC + i] = (double)red[0][b * 10 + j] + (double)red[1][b * 10 + j] +
-                                         (double)red[2][b * 10 + j] + (double)red[3][b * 10 + j];
-  }
-}
-
-// logits[i] = sums[i] + bias[i % NC]
-__global__ void head_logits_kernel(const double* __restrict__ sums, const float* __restrict__ bias,
-                                   float* __restrict__ logits, int BN, int NC) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < BN) logits[i] = (float)sums[i] + (bias ? bias[i % NC] : 0.f);
-}
-
-// Backward of the head.  dl = dlogits [B][NC].
-//   dW[j][c][pos] = scale * sum_b dl[b][j] p2[b][c][pos]   (written into dW_out, e.g. the DDP bucket)
-//   g2m[b][pos][c] = (sum_j dl[b][j] W[j][c][pos]) * [p2 > 0]     (NHWC, fp32)
-//   partial[c][blk][2] = { sum g2m (= sum dz2), sum g2m * y2(argmax) }
-template <int MAXB>
-__global__ __launch_bounds__(256) void head_bwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
-                                                       const float* __restrict__ aff2, const float* __restrict__ dl,
-                                                       float* __restrict__ dW, float4* __restrict__ g2m,
-                                                       double* __restrict__ partial, int B, int P, int Q, int NC,
-                                                       float scale) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float dls[MAXB * 10];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int py = blockIdx.y, px0 = blockIdx.x * HD_PX, px = px0 + lane;
-  const bool valid = px < Q;
-  const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)py * Q + px;
-  if (threadIdx.x < MAXB * 10) {
-    const int b = threadIdx.x / 10, j = threadIdx.x % 10;
-    dls[threadIdx.x] = (b < B && j < NC) ? dl[b * NC + j] : 0.f;
-  }
-  float w[10][8], dwa[10][8], a[8], bb[8], sdz[8], sdy[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    a[c] = aff2[8 * wv + c];
-    bb[c] = aff2[32 + 8 * wv + c];
-    sdz[c] = sdy[c] = 0.f;
-#pragma unroll
-    for (int j = 0; j < 10; ++j) {
-      w[j][c] = (valid && j < NC) ? Wfc[((int64_t)j * 32 + 8 * wv + c) * QQ + pos] : 0.f;
-      dwa[j][c] = 0.f;
-    }
-  }
-#pragma unroll 1
-  for (int b = 0; b < B && b < MAXB; ++b) {
-    __syncthreads();
-    head_stage(y2, smem, b, py, px0, P, Q);
-    __syncthreads();
-    float p[8], ya[8];
-    bool ps[8];
-    head_window(smem, lane, wv, a, bb, p, ya, ps);
-    float gm[8];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      float g = 0.f;
-#pragma unroll
-      for (int j = 0; j < 10; ++j) {
-        const float d = dls[b * 10 + j];
-        g += d * w[j][c];
-        dwa[j][c] += d * p[c];
-      }
-      gm[c] = ps[c] ? g : 0.f;
-      if (valid) {
-        sdz[c] += gm[c];
-        sdy[c] += gm[c] * ya[c];
-      }
-    }
-    if (valid) {
-      float4* dst = g2m + ((int64_t)b * QQ + pos) * 8 + 2 * wv;
-      dst[0] = make_float4(gm[0], gm[1], gm[2], gm[3]);
-      dst[1] = make_float4(gm[4], gm[5], gm[6], gm[7]);
-    }
-  }
-  if (valid) {
-#pragma unroll
-    for (int j = 0; j < 10; ++j)
-      if (j < NC)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) dW[((int64_t)j * 32 + 8 * wv + c) * QQ + pos] = scale * dwa[j][c];
-  }
-  const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const float s0 = wave_sum(sdz[c]);
-    const float s1 = wave_sum(sdy[c]);
-    if (lane == 0) {
-      partial[((int64_t)(8 * wv + c) * nblk + blk) * 2 + 0] = s0;
-      partial[((int64_t)(8 * wv + c) * nblk + blk) * 2 + 1] = s1;
-    }
-  }
-}
+// head kernels: see head_fused.hip
 
 // out[e] = sum_k in[(e / inner) * ostride + (e % inner) + k * kstride]  (one workgroup per output, fp64)
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __restrict__ in, double* __restrict__ out,
@@ -629,7 +467,7 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
                                                      const float* __restrict__ w1, const float* __restrict__ b1,
                                                      double* __restrict__ partial, int B, int H, int W) {
   __shared__ float xs[LB_XR * LB_XC];
-  __shared__ float red[16][16][LB_NACC + 1];
+  __shared__ float red[4][16][LB_NACC + 1];
   const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
   const int P = H / 2, PW = W / 2;
   const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
@@ -680,12 +518,18 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < LB_NACC; ++i) red[slot][c][i] = acc[i];
+  for (int i = 0; i < LB_NACC; ++i) {
+    // lanes l, l+16, l+32, l+48 of a wave hold the same channel
+    float v = acc[i];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if ((tid & 63) < 16) red[tid >> 6][c][i] = v;
+  }
   __syncthreads();
   for (int e = tid; e < 16 * LB_NACC; e += 256) {
     const int cc = e / LB_NACC, i = e - cc * LB_NACC;
     double s = 0.0;
-    for (int k = 0; k < 16; ++k) s += red[k][cc][i];
+    for (int k = 0; k < 4; ++k) s += red[k][cc][i];
     partial[((int64_t)blockIdx.x * 16 + cc) * LB_NACC + i] = s;
   }
 }
@@ -832,46 +676,6 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
   hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
   hipLaunchKernelGGL(x_border_kernel, dim3(82, 8), dim3(256), 0, st, x, strips, B, H, W);
-}
-
-int tds_head_fwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
-
-// partial: double [nblk][B*NC]; sums: double [B*NC] workspace
-int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
-                 float* logits, int B, int P, int NC, hipStream_t st) {
-  const int Q = P / 2;
-  if (B > 8 || NC > 10 || Q < 1) return -1;
-  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
-#define TDS_HF(MB)                                                                                                 \
-  hipLaunchKernelGGL((head_fwd_kernel<MB>), grid, dim3(256), HD_LDS, st, reinterpret_cast<const float4*>(y2), Wfc, \
-                     aff2, partial, B, P, Q, NC)
-  if (B <= 1) TDS_HF(1);
-  else if (B <= 2) TDS_HF(2);
-  else if (B <= 4) TDS_HF(4);
-  else TDS_HF(8);
-#undef TDS_HF
-  const int nblk = grid.x * grid.y, BN = B * NC;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(BN), dim3(256), 0, st, partial, sums, nblk, BN, (int64_t)0,
-                     (int64_t)BN);
-  hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);
-  return 0;
-}
-
-// partial: double [32][nblk][2]
-int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
-                 double* partial, int B, int P, int NC, float scale, hipStream_t st) {
-  const int Q = P / 2;
-  if (B > 8 || NC > 10 || Q < 1) return -1;
-  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
-#define TDS_HB(MB)                                                                                                 \
-  hipLaunchKernelGGL((head_bwd_kernel<MB>), grid, dim3(256), HD_LDS, st, reinterpret_cast<const float4*>(y2), Wfc, \
-                     aff2, dlogits, dW, reinterpret_cast<float4*>(g2m), partial, B, P, Q, NC, scale)
-  if (B <= 1) TDS_HB(1);
-  else if (B <= 2) TDS_HB(2);
-  else if (B <= 4) TDS_HB(4);
-  else TDS_HB(8);
-#undef TDS_HB
-  return 0;
 }
 
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,

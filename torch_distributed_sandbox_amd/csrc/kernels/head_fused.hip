@@ -1,0 +1,269 @@
+// Fused ConvNet head: BN2 affine + ReLU + 2x2 max-pool + fc, forward and backward
+// (reference: mnist_onegpu.py:21-24,29-30 -> native_batch_norm, clamp_min,
+// max_pool2d_with_indices, addmm and their backward ops; SURVEY.md §2.4 K6-K9,
+// K12-K18).  p2 (the pooled activation, 360 MB at 3000^2) is never stored:
+// both directions recompute it from y2 while streaming the fc weight once.
+//
+// Workgroup = one pooled row py x 64 pooled columns, every image, every channel:
+// 8 waves, wave w owns channels 4w..4w+3, lane = pooled column.  The tile's fc
+// weights W[j][c][py][px0..px0+63] (coalesced over lanes) stay in registers for
+// all images; per image the two y2 rows (2 x 128 NHWC records of 128 B) are
+// staged through LDS with coalesced 16-B loads, the next image's loads issued
+// into registers before the current image is processed.
+#include "common.h"
+#include "launchers.h"
+
+namespace tds {
+
+constexpr int HD_PX = 64;
+constexpr int HD_REC = 144;  // padded LDS record stride (bytes): 128 B of y2 + 16 B
+constexpr int HD_LDS = 2 * 2 * HD_PX * HD_REC;
+
+template <int NW>  // waves per workgroup; wave w owns channels CPW*w .. CPW*w+CPW-1
+struct HeadTile {
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int PER = (2 * 2 * HD_PX * 8) / THREADS;  // float4 per thread per image
+  const float4* y2;
+  int P, Q, py, px0;
+  __device__ void load(int b, float4 (&pre)[PER]) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = threadIdx.x + u * THREADS;
+      const int chunk = e & 7, rec = (e >> 3) & 127, row = e >> 10;
+      const int col = 2 * px0 + rec;
+      pre[u] = col < 2 * Q ? y2[(((int64_t)b * P + 2 * py + row) * P + col) * 8 + chunk] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ static void store(char* lds, const float4 (&pre)[PER]) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = threadIdx.x + u * THREADS;
+      const int chunk = e & 7, rec = (e >> 3) & 127, row = e >> 10;
+      *reinterpret_cast<float4*>(lds + (row * 2 * HD_PX + rec) * HD_REC + chunk * 16) = pre[u];
+    }
+  }
+};
+
+// BN2 affine + max-pool over this lane's 2x2 window for its CPW channels.
+template <int CPW>
+__device__ __forceinline__ void head_window(const char* lds, int lane, int wv, const float (&a)[CPW],
+                                            const float (&bb)[CPW], float (&p)[CPW], float (&yarg)[CPW],
+                                            bool (&pos)[CPW]) {
+  float y[4][CPW];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = q >> 1, rec = 2 * lane + (q & 1);
+    const char* src = lds + (row * 2 * HD_PX + rec) * HD_REC + wv * CPW * 4;
+    if constexpr (CPW == 4) {
+      const float4 u = *reinterpret_cast<const float4*>(src);
+      y[q][0] = u.x; y[q][1] = u.y; y[q][2] = u.z; y[q][3] = u.w;
+    } else {
+      const float2 u = *reinterpret_cast<const float2*>(src);
+      y[q][0] = u.x; y[q][1] = u.y;
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    float m = a[c] * y[0][c] + bb[c], ya = y[0][c];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const float z = a[c] * y[q][c] + bb[c];
+      if (z > m || isnan(z)) { m = z; ya = y[q][c]; }  // first max in scan order, NaN wins
+    }
+    pos[c] = m > 0.f;
+    p[c] = m > 0.f ? m : (isnan(m) ? m : 0.f);
+    yarg[c] = ya;
+  }
+}
+
+// partial[blk][b*NC + j] (fp64) = sum over the tile of p2[b][c][pos] * W[j][c][pos]
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void head_fwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
+                                                           const float* __restrict__ aff2,
+                                                           double* __restrict__ partial, int B, int P, int Q, int NC) {
+  constexpr int CPW = 32 / NW;
+  using Tile = HeadTile<NW>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float red[NW][8 * 10];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const Tile tile{y2, P, Q, (int)blockIdx.y, (int)blockIdx.x * HD_PX};
+  const int px = tile.px0 + lane;
+  const bool valid = px < Q;
+  const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)tile.py * Q + px;
+  float w[10][CPW], a[CPW], bb[CPW];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    a[c] = aff2[CPW * wv + c];
+    bb[c] = aff2[32 + CPW * wv + c];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) w[j][c] = (valid && j < NC) ? Wfc[((int64_t)j * 32 + CPW * wv + c) * QQ + pos] : 0.f;
+  }
+  float4 pre[Tile::PER];
+  tile.load(0, pre);
+#pragma unroll 1
+  for (int b = 0; b < B; ++b) {
+    __syncthreads();
+    Tile::store(smem, pre);
+    __syncthreads();
+    if (b + 1 < B) tile.load(b + 1, pre);
+    float p[CPW], ya[CPW];
+    bool ps[CPW];
+    head_window<CPW>(smem, lane, wv, a, bb, p, ya, ps);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) s += p[c] * w[j][c];
+      s = wave_sum(s);
+      if (lane == 0) red[wv][b * 10 + j] = s;
+    }
+  }
+  __syncthreads();
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  for (int i = threadIdx.x; i < B * NC; i += blockDim.x) {
+    const int b = i / NC, j = i % NC;
+    double s = 0.0;
+#pragma unroll
+    for (int w8 = 0; w8 < NW; ++w8) s += (double)red[w8][b * 10 + j];
+    partial[(int64_t)blk * B * NC + i] = s;
+  }
+}
+
+// logits[i] = sums[i] + bias[i % NC]
+__global__ void head_logits_kernel(const double* __restrict__ sums, const float* __restrict__ bias,
+                                   float* __restrict__ logits, int BN, int NC) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < BN) logits[i] = (float)sums[i] + (bias ? bias[i % NC] : 0.f);
+}
+
+// Backward.  dl = dlogits [B][NC].
+//   dW[j][c][pos]  = scale * sum_b dl[b][j] p2[b][c][pos]      (e.g. straight into the DDP bucket)
+//   g2m[b][pos][c] = (sum_j dl[b][j] W[j][c][pos]) * [p2 > 0]   (NHWC pooled gradient, fp32)
+//   partial[c][blk][2] = { sum g2m (= sum dz2), sum g2m * y2(argmax) }   (BN2 backward reductions)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
+                                                           const float* __restrict__ aff2, const float* __restrict__ dl,
+                                                           float* __restrict__ dW, float* __restrict__ g2m,
+                                                           double* __restrict__ partial, int B, int P, int Q, int NC,
+                                                           float scale) {
+  constexpr int CPW = 32 / NW;
+  using Tile = HeadTile<NW>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float dls[8 * 10];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const Tile tile{y2, P, Q, (int)blockIdx.y, (int)blockIdx.x * HD_PX};
+  const int px = tile.px0 + lane;
+  const bool valid = px < Q;
+  const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)tile.py * Q + px;
+  if (threadIdx.x < 80) {
+    const int b = threadIdx.x / 10, j = threadIdx.x % 10;
+    dls[threadIdx.x] = (b < B && j < NC) ? dl[b * NC + j] : 0.f;
+  }
+  float w[10][CPW], dwa[10][CPW], a[CPW], bb[CPW], sdz[CPW], sdy[CPW];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    a[c] = aff2[CPW * wv + c];
+    bb[c] = aff2[32 + CPW * wv + c];
+    sdz[c] = sdy[c] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      w[j][c] = (valid && j < NC) ? Wfc[((int64_t)j * 32 + CPW * wv + c) * QQ + pos] : 0.f;
+      dwa[j][c] = 0.f;
+    }
+  }
+  float4 pre[Tile::PER];
+  tile.load(0, pre);
+#pragma unroll 1
+  for (int b = 0; b < B; ++b) {
+    __syncthreads();
+    Tile::store(smem, pre);
+    __syncthreads();
+    if (b + 1 < B) tile.load(b + 1, pre);
+    float p[CPW], ya[CPW];
+    bool ps[CPW];
+    head_window<CPW>(smem, lane, wv, a, bb, p, ya, ps);
+    float gm[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      float g = 0.f;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const float d = dls[b * 10 + j];
+        g += d * w[j][c];
+        dwa[j][c] += d * p[c];
+      }
+      gm[c] = ps[c] ? g : 0.f;
+      sdz[c] += valid ? gm[c] : 0.f;
+      sdy[c] += valid ? gm[c] * ya[c] : 0.f;
+    }
+    if (valid) {
+      float* dst = g2m + ((int64_t)b * QQ + pos) * 32 + CPW * wv;
+      if constexpr (CPW == 4) *reinterpret_cast<float4*>(dst) = make_float4(gm[0], gm[1], gm[2], gm[3]);
+      else *reinterpret_cast<float2*>(dst) = make_float2(gm[0], gm[1]);
+    }
+  }
+  if (valid) {
+    float* dst = dW + (int64_t)(CPW * wv) * QQ + pos;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (j < NC)
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) __builtin_nontemporal_store(scale * dwa[j][c], dst + ((int64_t)j * 32 + c) * QQ);
+  }
+  const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    const float s0 = wave_sum(sdz[c]);
+    const float s1 = wave_sum(sdy[c]);
+    if (lane == 0) {
+      partial[((int64_t)(CPW * wv + c) * nblk + blk) * 2 + 0] = s0;
+      partial[((int64_t)(CPW * wv + c) * nblk + blk) * 2 + 1] = s1;
+    }
+  }
+}
+
+constexpr int HD_FWD_NW = 8;
+constexpr int HD_BWD_NW = 16;
+
+static void head_lds_limits() {
+  static bool done = false;
+  if (done) return;
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_fwd_kernel<HD_FWD_NW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, HD_LDS);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_bwd_kernel<HD_BWD_NW>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, HD_LDS);
+  done = true;
+}
+
+}  // namespace tds
+
+using namespace tds;
+
+int tds_head_fwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
+
+// partial: double [nblk][B*NC]; sums: double [B*NC] workspace
+int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
+                 float* logits, int B, int P, int NC, hipStream_t st) {
+  const int Q = P / 2;
+  if (B > 8 || NC > 10 || Q < 1) return -1;
+  head_lds_limits();
+  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
+  hipLaunchKernelGGL(head_fwd_kernel<HD_FWD_NW>, grid, dim3(64 * HD_FWD_NW), HD_LDS, st,
+                     reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, B, P, Q, NC);
+  const int nblk = grid.x * grid.y, BN = B * NC;
+  tds_reduce_partials(partial, sums, BN, nblk, BN, 0, BN, st);
+  hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);
+  return 0;
+}
+
+// partial: double [32][nblk][2]
+int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
+                 double* partial, int B, int P, int NC, float scale, hipStream_t st) {
+  const int Q = P / 2;
+  if (B > 8 || NC > 10 || Q < 1) return -1;
+  head_lds_limits();
+  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
+  hipLaunchKernelGGL(head_bwd_kernel<HD_BWD_NW>, grid, dim3(64 * HD_BWD_NW), HD_LDS, st,
+                     reinterpret_cast<const float4*>(y2), Wfc, aff2, dlogits, dW, g2m, partial, B, P, Q, NC, scale);
+  return 0;
+}
