@@ -34,7 +34,7 @@ const float* optf(const c10::optional<Tensor>& t, int64_t n, const char* name) {
 }
 
 int l1_wg() { return tds_fused_num_wg(4); }
-int ac_wg() { return tds_fused_num_wg(2); }
+int ac_wg() { return tds_fused_num_wg(4); }
 
 // ---------------------------------------------------------------- layer 1 forward
 // returns (p1 carrier, idx1, stats1[mean16|invstd16], ac_partial, strips)

@@ -252,7 +252,7 @@ __global__ void bn_finalize_shifted_kernel(const double* __restrict__ partial, i
 constexpr int AC_TR = 16, AC_TC = 64;
 __global__ __launch_bounds__(256) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
                                                          int B, int H, int W) {
-  __shared__ __attribute__((aligned(16))) float xs[(AC_TR + 4) * (AC_TC + 8 + 4)];
+  __shared__ __attribute__((aligned(16))) float xs[(AC_TR + 4) * (AC_TC + 12)];
   __shared__ double red[4][42];
   constexpr int XS = AC_TC + 12;  // cols c0-4 .. c0+TC+4 (+pad)
   const int tid = threadIdx.x;
@@ -262,17 +262,41 @@ __global__ __launch_bounds__(256) void x_autocorr_kernel(const float* __restrict
 #pragma unroll
   for (int i = 0; i < 42; ++i) acc[i] = 0.f;
   const int tr = tid >> 4, tc = (tid & 15) * 4;  // thread: row tr, cols tc..tc+3
-  for (int t = blockIdx.x; t < total; t += gridDim.x) {
+  // staging: rows r0..r0+19, cols c0-4 .. c0+71 as 19 float4 per row (W % 4 == 0), next tile prefetched
+  constexpr int NV = (AC_TR + 4) * 19;
+  constexpr int PER = (NV + 255) / 256;
+  float4 pre[PER];
+  auto load_tile = [&](int t) {
     const int b = t / (tiles_c * tiles_r), rem = t % (tiles_c * tiles_r);
     const int r0 = (rem / tiles_c) * AC_TR, c0 = (rem % tiles_c) * AC_TC;
-    const float* xb = x + (int64_t)b * H * W;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < NV) {
+        const int rr = e / 19, cv = e - rr * 19;
+        const int gr = r0 + rr, gc = c0 - 4 + 4 * cv;
+        if (gr < H && gc >= 0 && gc < W) v = *reinterpret_cast<const float4*>(x + ((int64_t)b * H + gr) * W + gc);
+      }
+      pre[u] = v;
+    }
+  };
+  int t = blockIdx.x;
+  if (t < total) load_tile(t);
+  for (; t < total; t += gridDim.x) {
+    const int rem = t % (tiles_c * tiles_r);
+    const int r0 = (rem / tiles_c) * AC_TR, c0 = (rem % tiles_c) * AC_TC;
     __syncthreads();
-    for (int e = tid; e < (AC_TR + 4) * XS; e += 256) {
-      const int rr = e / XS, cc = e - rr * XS;
-      const int gr = r0 + rr, gc = c0 - 4 + cc;
-      xs[e] = (gr < H && gc >= 0 && gc < W && cc < AC_TC + 8 + 4) ? xb[(int64_t)gr * W + gc] : 0.f;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u;
+      if (e < NV) {
+        const int rr = e / 19, cv = e - rr * 19;
+        *reinterpret_cast<float4*>(xs + rr * XS + 4 * cv) = pre[u];
+      }
     }
     __syncthreads();
+    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
     // own pixels: xs[tr][tc+4 .. tc+7]; window rows tr..tr+4, cols tc .. tc+11
     float w[5][12];
 #pragma unroll
@@ -460,14 +484,24 @@ __global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict
 // slot = tid >> 4) owns channel c for pooled pixels slot, slot+16, ... of the tile and
 // accumulates: sdz, sdzy (dz * y1 at the argmax), sdzx[25] (dz * xpatch).
 constexpr int LB_PR = 8, LB_PC = 32;
-constexpr int LB_XR = 2 * LB_PR + 4, LB_XC = 2 * LB_PC + 4;
+constexpr int LB_XR = 2 * LB_PR + 4;
+constexpr int LB_XS = 76;  // LDS x row stride (floats); column 0 <-> global column 2*pc0 - 4
 constexpr int LB_NACC = 27;
+constexpr int LB_NP = LB_PR * LB_PC;                     // pooled pixels per tile
+constexpr int LB_V_DP = LB_NP * 4, LB_V_PH = LB_NP * 2, LB_V_ID = LB_NP, LB_V_X = LB_XR * 18;
+constexpr int LB_V = LB_V_DP + LB_V_PH + LB_V_ID + LB_V_X;  // 16-B vectors staged per tile
+constexpr int LB_PER = (LB_V + 255) / 256;
 __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dp1,
                                                      const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
                                                      const float* __restrict__ w1, const float* __restrict__ b1,
                                                      double* __restrict__ partial, int B, int H, int W) {
-  __shared__ float xs[LB_XR * LB_XC];
+  // LDS: dp1 tile [256][16] f32 | p1-hi tile [256][16] bf16 | argmax tile [256][16] u8 | x tile
+  __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 32 + LB_NP * 16 + LB_XR * LB_XS * 4];
   __shared__ float red[4][16][LB_NACC + 1];
+  float* dps = reinterpret_cast<float*>(lds);
+  unsigned short* phs = reinterpret_cast<unsigned short*>(lds + LB_NP * 64);
+  uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 96);
+  float* xs = reinterpret_cast<float*>(lds + LB_NP * 112);
   const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
   const int P = H / 2, PW = W / 2;
   const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
@@ -480,35 +514,72 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
 #pragma unroll
   for (int i = 0; i < LB_NACC; ++i) acc[i] = 0.f;
 
-  for (int t = xcd_remap(blockIdx.x, gridDim.x); t < total; t += gridDim.x) {
+  uint4 pre[LB_PER];
+  auto load_tile = [&](int t) {
     const int b = t / per_img, rem = t - b * per_img;
     const int pr0 = (rem / tiles_c) * LB_PR, pc0 = (rem % tiles_c) * LB_PC;
-    const float* xb = x + (int64_t)b * H * W;
-    __syncthreads();
-    for (int e = tid; e < LB_XR * LB_XC; e += 256) {
-      const int rr = e / LB_XC, cc = e - rr * LB_XC;
-      const int gr = 2 * pr0 - 2 + rr, gc = 2 * pc0 - 2 + cc;
-      xs[e] = (gr >= 0 && gr < H && gc >= 0 && gc < W) ? xb[(int64_t)gr * W + gc] : 0.f;
+#pragma unroll
+    for (int u = 0; u < LB_PER; ++u) {
+      int e = tid + 256 * u;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (e < LB_V_DP + LB_V_PH + LB_V_ID) {
+        int q, nq;
+        if (e < LB_V_DP) { q = e & 3; nq = 4; e >>= 2; }
+        else if (e < LB_V_DP + LB_V_PH) { e -= LB_V_DP; q = e & 1; nq = 2; e >>= 1; }
+        else { e -= LB_V_DP + LB_V_PH; q = 0; nq = 1; }
+        const int gpr = pr0 + e / LB_PC, gpc = pc0 + e % LB_PC;
+        if (gpr < P && gpc < PW) {
+          const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
+          if (nq == 4) v = reinterpret_cast<const uint4*>(dp1)[rec * 4 + q];
+          else if (nq == 2) v = p1[rec * 4 + q];
+          else v = reinterpret_cast<const uint4*>(idx1)[rec];
+        }
+      } else if (e < LB_V) {
+        e -= LB_V_DP + LB_V_PH + LB_V_ID;
+        const int rr = e / 18, cv = e - rr * 18;
+        const int gr = 2 * pr0 - 2 + rr, gc = 2 * pc0 - 4 + 4 * cv;
+        if (gr >= 0 && gr < H && gc >= 0 && gc < W)
+          v = *reinterpret_cast<const uint4*>(x + ((int64_t)b * H + gr) * W + gc);
+      }
+      pre[u] = v;
     }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int u = 0; u < LB_PER; ++u) {
+      int e = tid + 256 * u;
+      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[e] = pre[u];
+      else if (e < LB_V_DP + LB_V_PH) reinterpret_cast<uint4*>(phs)[e - LB_V_DP] = pre[u];
+      else if (e < LB_V_DP + LB_V_PH + LB_V_ID) reinterpret_cast<uint4*>(ids)[e - LB_V_DP - LB_V_PH] = pre[u];
+      else if (e < LB_V) {
+        e -= LB_V_DP + LB_V_PH + LB_V_ID;
+        const int rr = e / 18, cv = e - rr * 18;
+        *reinterpret_cast<uint4*>(xs + rr * LB_XS + 4 * cv) = pre[u];
+      }
+    }
+  };
+
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (t < total) load_tile(t);
+  for (; t < total; t += gridDim.x) {
     __syncthreads();
-    for (int pp = slot; pp < LB_PR * LB_PC; pp += 16) {
+    store_tile();
+    __syncthreads();
+    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
+    for (int pp = slot; pp < LB_NP; pp += 16) {
+      const float phf = bf16_to_f32(phs[pp * 16 + c]);
+      if (!(phf > 0.f)) continue;  // pooled value 0 (or out of range): ReLU blocks the gradient
+      const float dz = dps[pp * 16 + c];
+      const int a = ids[pp * 16 + c];
       const int pr = pp / LB_PC, pc = pp - (pp / LB_PC) * LB_PC;
-      const int gpr = pr0 + pr, gpc = pc0 + pc;
-      if (gpr >= P || gpc >= PW) continue;
-      const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
-      const unsigned short ph = reinterpret_cast<const unsigned short*>(p1 + rec * 4)[c];
-      const float phf = bf16_to_f32(ph);
-      if (!(phf > 0.f)) continue;
-      const float dz = dp1[rec * 16 + c];
-      const int a = idx1[rec * 16 + c];
-      const int lr = 2 * pr + (a >> 1), lc = 2 * pc + (a & 1);  // conv1 pixel in tile coords
-      const float* xp = xs + lr * LB_XC + lc;                      // patch origin (halo offset built in)
+      const int lr = 2 * pr + (a >> 1), lc = 2 * pc + (a & 1) + 2;  // patch origin in the x tile
+      const float* xp = xs + lr * LB_XS + lc;
       float y = bc;
 #pragma unroll
       for (int ky = 0; ky < 5; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 5; ++kx) {
-          const float xv = xp[ky * LB_XC + kx];
+          const float xv = xp[ky * LB_XS + kx];
           y += wr[ky * 5 + kx] * xv;
           acc[2 + ky * 5 + kx] += dz * xv;
         }
