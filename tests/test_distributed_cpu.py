@@ -19,8 +19,8 @@ def _init(rank, world, port, backend="gloo"):
 
 
 # ---------------------------------------------------------------- collectives
-def _w_collectives(rank, world, port):
-    dist = _init(rank, world, port)
+def _w_collectives(rank, world, port, backend="gloo"):
+    dist = _init(rank, world, port, backend)
     t = torch.tensor(rank + 1, dtype=torch.int32)
     g = dist.new_group(list(range(world)))
     assert g is dist.new_group(list(range(world)))  # cached, no per-step re-init
@@ -50,14 +50,15 @@ def _w_collectives(rank, world, port):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("backend", ["gloo", "host"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_collectives_gloo(world):
-    launch.spawn(_w_collectives, args=(world, launch.find_free_port()), nprocs=world, timeout=180)
+def test_collectives(world, backend):
+    launch.spawn(_w_collectives, args=(world, launch.find_free_port(), backend), nprocs=world, timeout=180)
 
 
 # ---------------------------------------------------------------- DDP equivalence
-def _w_ddp(rank, world, port, H, B):
-    dist = _init(rank, world, port)
+def _w_ddp(rank, world, port, H, B, backend="gloo"):
+    dist = _init(rank, world, port, backend)
     from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
@@ -107,8 +108,9 @@ def _w_ddp(rank, world, port, H, B):
     dist.destroy_process_group()
 
 
-def test_ddp_matches_single_process_average():
-    launch.spawn(_w_ddp, args=(2, launch.find_free_port(), 32, 2), nprocs=2, timeout=300)
+@pytest.mark.parametrize("backend", ["gloo", "host"])
+def test_ddp_matches_single_process_average(backend):
+    launch.spawn(_w_ddp, args=(2, launch.find_free_port(), 32, 2, backend), nprocs=2, timeout=300)
 
 
 def _w_no_sync(rank, world, port):

@@ -81,12 +81,23 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
                        device_id: Optional[int] = None, store=None) -> None:
     """Initialise the default group.  ``rank``/``world_size`` default to the
     ``RANK``/``WORLD_SIZE`` environment (torchrun); ``init_method`` defaults to
-    ``env://`` (``MASTER_ADDR``/``MASTER_PORT``)."""
+    ``env://`` (``MASTER_ADDR``/``MASTER_PORT``).  ``store="native"`` (or
+    ``TDS_STORE=native``) rendezvouses through this package's C++ TCP store
+    (parallel/store.py) instead of c10d's."""
     b = _normalise_backend(backend)
     if rank is None:
         rank = int(os.environ.get("RANK", "0"))
     if world_size is None:
         world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if store is None and init_method is None and os.environ.get("TDS_STORE", "") == "native":
+        store = "native"
+    if isinstance(store, str):
+        if store != "native":
+            raise ValueError(f"unknown store {store!r} (expected 'native' or a torch.distributed.Store)")
+        from .store import create_store
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        store = create_store(rank, world_size, timeout=timeout)
     kwargs = dict(backend=_torch_backend(b), rank=rank, world_size=world_size, timeout=timeout)
     if store is not None:
         kwargs["store"] = store
@@ -150,12 +161,12 @@ def new_group(ranks: Optional[Sequence[int]] = None, backend: Optional[str] = No
 
 def _needs_avg_emulation(group) -> bool:
     b = dist.get_backend(group)
-    return b != "nccl"
+    return b not in ("nccl", "tds_host")
 
 
 def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool = False):
-    """In-place all-reduce.  AVG is native on RCCL (ncclAvg) and emulated as
-    SUM + divide elsewhere (gloo has no AVG)."""
+    """In-place all-reduce.  AVG is native on RCCL (ncclAvg) and on the host ring
+    backend, and emulated as SUM + divide on gloo (which has no AVG)."""
     if op == ReduceOp.AVG and _needs_avg_emulation(group):
         work = dist.all_reduce(tensor, op=ReduceOp.SUM, group=group, async_op=async_op)
         n = get_world_size(group)

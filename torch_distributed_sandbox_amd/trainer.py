@@ -115,12 +115,15 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
             if steps_done == 1 and device.type == "cuda":
                 torch.cuda.synchronize()
                 t_first = time.perf_counter()
-            if (i + 1) % args.log_interval == 0 and gpu == 0:
+            if (i + 1) % args.log_interval == 0:
                 shown = loss.detach()
                 if distributed and getattr(args, "avg_loss", False):
+                    # collective: every rank joins, rank 0 prints
                     shown = shown.clone()
                     tdist.all_reduce(shown, tdist.ReduceOp.AVG)
-                if distributed:
+                if gpu != 0:
+                    pass
+                elif distributed:
                     print("Rank [{}], Epoch [{}/{}], Step [{}/{}], Loss: {:.4f}".format(
                         rank, epoch + 1, args.epochs, i + 1, total_step, shown.item()), flush=True)
                 else:
