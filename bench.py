@@ -36,6 +36,8 @@ def main(argv=None):
     ap.add_argument("--batch-size", type=int, default=5, help="per-rank batch (reference: 5)")
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "layers"])
     ap.add_argument("--bucket-mb", type=float, default=None)
+    ap.add_argument("--backend", default=os.environ.get("TDS_BENCH_BACKEND", "rccl"),
+                    help="rccl (torch ProcessGroupNCCL = RCCL) | rccl-native (this package's C++ communicator)")
     ap.add_argument("--profile-phases", action="store_true", help="also report per-phase GPU times (adds events)")
     args = ap.parse_args(argv)
 
@@ -61,7 +63,7 @@ def main(argv=None):
     tds._ext.ops()  # native extension must be loaded (fails loudly otherwise)
     device = torch.device("cuda", local_rank)
     if world > 1:
-        tdist.init_process_group("rccl", rank=rank, world_size=world, device_id=local_rank)
+        tdist.init_process_group(args.backend, rank=rank, world_size=world, device_id=local_rank)
 
     H = W = args.image_size
     B = args.batch_size
@@ -131,6 +133,8 @@ def main(argv=None):
                 "image_size": [H, W],
                 "parallelism": f"dp{world}",
                 "mode": args.mode,
+                "backend": args.backend if world > 1 else None,
+                "reducer": ddp.reducer_kind,
                 "optimizer": "SGD(lr=1e-4)",
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3),
                 "final_loss": final_loss,

@@ -70,6 +70,8 @@ def _w_ddp(rank, world, port, H, B, backend="gloo"):
     model = ConvNet(image_shape=(H, H))  # different init per rank -> must be overwritten by rank 0
     model.load_state_dict(base.state_dict()) if rank == 0 else None
     ddp = DistributedDataParallel(model)
+    # this package's host ring backend drives the C++ reducer; torch's gloo the Python hooks
+    assert ddp.reducer_kind == ("native" if backend == "host" else "python")
     assert [b[2][0] for b in ddp.bucket_layout()][0] == (10,)  # fc.bias first (gradient-ready order)
     for p, q in zip(model.parameters(), ref.parameters()):
         assert torch.equal(p.data, q.data), "rank-0 broadcast at construction failed"
@@ -113,8 +115,8 @@ def test_ddp_matches_single_process_average(backend):
     launch.spawn(_w_ddp, args=(2, launch.find_free_port(), 32, 2, backend), nprocs=2, timeout=300)
 
 
-def _w_no_sync(rank, world, port):
-    dist = _init(rank, world, port)
+def _w_no_sync(rank, world, port, backend="gloo"):
+    dist = _init(rank, world, port, backend)
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
 
     torch.manual_seed(0)
@@ -131,8 +133,44 @@ def _w_no_sync(rank, world, port):
     dist.destroy_process_group()
 
 
-def test_ddp_no_sync_accumulation():
-    launch.spawn(_w_no_sync, args=(2, launch.find_free_port()), nprocs=2, timeout=120)
+@pytest.mark.parametrize("backend", ["gloo", "host"])
+def test_ddp_no_sync_accumulation(backend):
+    launch.spawn(_w_no_sync, args=(2, launch.find_free_port(), backend), nprocs=2, timeout=120)
+
+
+def _w_unused(rank, world, port, find_unused):
+    dist = _init(rank, world, port, "host")
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+
+    class Two(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = torch.nn.Linear(4, 3)
+            self.b = torch.nn.Linear(4, 3)  # never used in forward
+
+        def forward(self, x):
+            return self.a(x)
+
+    m = Two()
+    ddp = DistributedDataParallel(m, find_unused_parameters=find_unused, bucket_cap_mb=1e-5)
+    assert ddp.reducer_kind == "native"
+    x = torch.full((2, 4), float(rank + 1))
+    if find_unused:
+        ddp(x).sum().backward()
+        assert torch.equal(m.b.weight.grad, torch.zeros_like(m.b.weight))
+        expect = torch.full((3, 4), 2.0 * (1 + 2) / 2)  # d(sum)/dW = sum_b x, averaged over ranks
+        assert torch.allclose(m.a.weight.grad, expect)
+    else:
+        with pytest.raises(RuntimeError, match="never became ready"):
+            ddp(x).sum().backward()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("find_unused", [True, False])
+def test_native_reducer_unused_parameters(find_unused):
+    launch.spawn(_w_unused, args=(2, launch.find_free_port(), find_unused), nprocs=2, timeout=120)
 
 
 # ---------------------------------------------------------------- sampler

@@ -1,0 +1,412 @@
+// Native RCCL communicator for device tensors (SURVEY.md §2.3 N1 — the role
+// ProcessGroupNCCL plays for the reference's init_process_group('nccl'),
+// mnist_distributed.py:50, allreduce_toy.py:44).
+//
+// One communicator per process/GPU over xGMI, created eagerly from a unique id
+// the Python side exchanges through the rendezvous store.  Collectives run on a
+// dedicated high-priority HIP stream (so the big gradient all-reduce is
+// scheduled ahead of compute work when both are ready):
+//
+//   caller stream --event--> comm stream: ncclX(...) --done event--> Work
+//
+// Work::wait() makes the caller's current stream wait on the done event (the host
+// never blocks); Work::synchronize() blocks the host.  Buffers are registered with
+// the caching allocator on the comm stream (recordStream) so they are not reused
+// while the collective is in flight.
+//
+// A watchdog thread polls outstanding collectives and the communicator's async
+// error state; a collective older than the timeout, or an RCCL async error,
+// aborts the communicator (ncclCommAbort) and — by default — terminates the
+// process so a launcher's fail-fast tears the job down (the same policy as
+// torch's TORCH_NCCL_ASYNC_ERROR_HANDLING).  TDS_RCCL_ERROR_HANDLING=raise keeps
+// the process alive and rethrows from the next wait/collective instead.
+//
+// Links against torch's bundled librccl (one RCCL per process; see _build.py).
+#pragma once
+#include <ATen/ATen.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPGuard.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <torch/custom_class.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "comm/comm.h"
+
+namespace tds_comm {
+
+#define TDS_RCCL(cmd)                                                                   \
+  do {                                                                                  \
+    ncclResult_t r_ = (cmd);                                                            \
+    TORCH_CHECK(r_ == ncclSuccess, "RCCL error '", ncclGetErrorString(r_), "' in ", #cmd); \
+  } while (0)
+#define TDS_HIP(cmd)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (cmd);                                                             \
+    TORCH_CHECK(e_ == hipSuccess, "HIP error '", hipGetErrorString(e_), "' in ", #cmd); \
+  } while (0)
+
+inline ncclDataType_t nccl_dtype(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kDouble: return ncclFloat64;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kChar: return ncclInt8;
+    case at::kByte:
+    case at::kBool: return ncclUint8;
+    default: TORCH_CHECK(false, "rccl: unsupported dtype ", t);
+  }
+}
+
+inline ncclRedOp_t nccl_op(int64_t op) {
+  switch (op) {
+    case R_SUM: return ncclSum;
+    case R_AVG: return ncclAvg;
+    case R_MAX: return ncclMax;
+    case R_MIN: return ncclMin;
+    case R_PROD: return ncclProd;
+    default: TORCH_CHECK(false, "rccl: unsupported reduce op ", op);
+  }
+}
+
+// State shared by the communicator, its works and the watchdog.
+struct RcclState {
+  ncclComm_t comm = nullptr;
+  int device = 0;
+  int64_t rank = 0, world = 1, timeout_ms = 600000;
+  bool exit_on_error = true;
+  std::atomic<bool> aborted{false};
+  std::mutex mu;
+  std::string error;  // guarded by mu
+  std::condition_variable cv;
+  bool stop = false;  // guarded by mu
+
+  struct Pending {
+    hipEvent_t done;
+    std::chrono::steady_clock::time_point start;
+    std::string what;
+  };
+  std::deque<Pending> pending;  // guarded by mu
+
+  void check_ok() {
+    if (aborted.load()) {
+      std::lock_guard<std::mutex> g(mu);
+      TORCH_CHECK(false, "rccl communicator (rank ", rank, ") was aborted: ", error);
+    }
+  }
+
+  // Abort once; called from the watchdog (or a failing wait).
+  void fail(const std::string& why) {
+    bool expected = false;
+    if (!aborted.compare_exchange_strong(expected, true)) return;
+    {
+      std::lock_guard<std::mutex> g(mu);
+      error = why;
+    }
+    std::fprintf(stderr, "[tds rccl] rank %lld: %s -- aborting communicator\n", (long long)rank, why.c_str());
+    std::fflush(stderr);
+    if (comm) ncclCommAbort(comm);
+    comm = nullptr;
+    if (exit_on_error) {
+      std::fprintf(stderr, "[tds rccl] rank %lld: terminating process (TDS_RCCL_ERROR_HANDLING=raise to disable)\n",
+                   (long long)rank);
+      std::fflush(stderr);
+      std::_Exit(70);
+    }
+  }
+};
+
+struct RcclWork : CommWork {
+  std::shared_ptr<RcclState> st;
+  hipEvent_t done = nullptr;
+  int device = 0;
+
+  RcclWork(std::shared_ptr<RcclState> s, hipEvent_t e) : st(std::move(s)), done(e), device(st->device) {}
+  ~RcclWork() override {
+    if (done) (void)hipEventDestroy(done);
+  }
+
+  void wait() override {
+    st->check_ok();
+    c10::hip::HIPGuard g((c10::DeviceIndex)device);
+    TDS_HIP(hipStreamWaitEvent(c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream(), done, 0));
+  }
+  bool is_completed() override {
+    st->check_ok();
+    return hipEventQuery(done) == hipSuccess;
+  }
+  void synchronize() override {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (true) {
+      st->check_ok();
+      hipError_t e = hipEventQuery(done);
+      if (e == hipSuccess) return;
+      TORCH_CHECK(e == hipErrorNotReady, "rccl work: ", hipGetErrorString(e));
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(st->timeout_ms)) {
+        st->fail("collective did not finish within the timeout (host wait)");
+        st->check_ok();
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+  }
+};
+
+class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
+ public:
+  static at::Tensor unique_id() {
+    ncclUniqueId id;
+    TDS_RCCL(ncclGetUniqueId(&id));
+    auto t = at::empty({(int64_t)sizeof(id)}, at::TensorOptions().dtype(at::kByte));
+    std::memcpy(t.data_ptr(), &id, sizeof(id));
+    return t;
+  }
+
+  RcclComm(int64_t rank, int64_t world, int64_t device, at::Tensor id, int64_t timeout_ms)
+      : st_(std::make_shared<RcclState>()),
+        stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device)) {
+    TORCH_CHECK(id.numel() == (int64_t)sizeof(ncclUniqueId) && id.scalar_type() == at::kByte,
+                "RcclComm: bad unique id");
+    st_->rank = rank;
+    st_->world = world;
+    st_->device = (int)device;
+    st_->timeout_ms = timeout_ms;
+    const char* eh = std::getenv("TDS_RCCL_ERROR_HANDLING");
+    st_->exit_on_error = !(eh && std::string(eh) == "raise");
+    ncclUniqueId uid;
+    auto idc = id.contiguous().cpu();
+    std::memcpy(&uid, idc.data_ptr(), sizeof(uid));
+    c10::hip::HIPGuard g((c10::DeviceIndex)device);
+    TDS_RCCL(ncclCommInitRank(&st_->comm, (int)world, uid, (int)rank));
+    TDS_HIP(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+    watchdog_ = std::thread([s = st_] { watchdog_loop(s); });
+  }
+
+  ~RcclComm() override { shutdown(); }
+
+  void shutdown() {
+    if (watchdog_.joinable()) {
+      {
+        std::lock_guard<std::mutex> g(st_->mu);
+        st_->stop = true;
+      }
+      st_->cv.notify_all();
+      watchdog_.join();
+    }
+    if (st_->comm && !st_->aborted.load()) {
+      c10::hip::HIPGuard g((c10::DeviceIndex)st_->device);
+      (void)hipStreamSynchronize(stream_.stream());
+      ncclCommDestroy(st_->comm);
+      st_->comm = nullptr;
+    }
+    if (ready_) {
+      (void)hipEventDestroy(ready_);
+      ready_ = nullptr;
+    }
+  }
+
+  void abort(const std::string& why) {
+    const bool keep = st_->exit_on_error;
+    st_->exit_on_error = false;  // an explicit abort never terminates the process
+    st_->fail(why.empty() ? "aborted by user" : why);
+    st_->exit_on_error = keep;
+  }
+
+  int64_t comm_rank() const override { return st_->rank; }
+  int64_t comm_world() const override { return st_->world; }
+  int64_t rank() const { return st_->rank; }
+  int64_t world_size() const { return st_->world; }
+  int64_t device() const { return st_->device; }
+  int64_t pending() {
+    std::lock_guard<std::mutex> g(st_->mu);
+    return (int64_t)st_->pending.size();
+  }
+
+  // ---------------------------------------------------------------- collectives
+  c10::intrusive_ptr<CommWork> allreduce_async(at::Tensor t, int64_t op) override {
+    check_dev(t);
+    return run({t}, "allreduce", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), nccl_op(op), c, s));
+    });
+  }
+  c10::intrusive_ptr<CommWork> allreduce(at::Tensor t, int64_t op) { return allreduce_async(t, op); }
+
+  c10::intrusive_ptr<CommWork> broadcast(at::Tensor t, int64_t root) {
+    check_dev(t);
+    return run({t}, "broadcast", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)root, c, s));
+    });
+  }
+
+  // One grouped launch for many tensors (DDP's coalesced state/buffer broadcast, N5).
+  c10::intrusive_ptr<CommWork> broadcast_coalesced(std::vector<at::Tensor> ts, int64_t root) {
+    for (auto& t : ts) check_dev(t);
+    return run(ts, "broadcast_coalesced", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclGroupStart());
+      for (auto& t : ts)
+        TDS_RCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)root, c, s));
+      TDS_RCCL(ncclGroupEnd());
+    });
+  }
+
+  c10::intrusive_ptr<CommWork> reduce(at::Tensor t, int64_t root, int64_t op) {
+    check_dev(t);
+    return run({t}, "reduce", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), nccl_op(op), (int)root,
+                          c, s));
+    });
+  }
+
+  c10::intrusive_ptr<CommWork> allgather(at::Tensor out, at::Tensor in) {
+    check_dev(out);
+    check_dev(in);
+    TORCH_CHECK(out.numel() == in.numel() * st_->world && out.scalar_type() == in.scalar_type(),
+                "rccl allgather: output must hold world_size x input elements");
+    return run({out, in}, "allgather", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in.scalar_type()), c, s));
+    });
+  }
+
+  c10::intrusive_ptr<CommWork> reduce_scatter(at::Tensor out, at::Tensor in, int64_t op) {
+    check_dev(out);
+    check_dev(in);
+    TORCH_CHECK(in.numel() == out.numel() * st_->world && out.scalar_type() == in.scalar_type(),
+                "rccl reduce_scatter: input must hold world_size x output elements");
+    return run({out, in}, "reduce_scatter", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in.scalar_type()),
+                                 nccl_op(op), c, s));
+    });
+  }
+
+  // equal splits: in/out are [world * n]
+  c10::intrusive_ptr<CommWork> alltoall(at::Tensor out, at::Tensor in) {
+    check_dev(out);
+    check_dev(in);
+    TORCH_CHECK(in.numel() == out.numel() && in.numel() % st_->world == 0, "rccl alltoall: bad sizes");
+    const int64_t n = in.numel() / st_->world, esz = in.element_size();
+    return run({out, in}, "alltoall", [&](ncclComm_t c, hipStream_t s) {
+      const auto dt = nccl_dtype(in.scalar_type());
+      TDS_RCCL(ncclGroupStart());
+      for (int64_t r = 0; r < st_->world; ++r) {
+        TDS_RCCL(ncclSend(static_cast<char*>(in.data_ptr()) + r * n * esz, n, dt, (int)r, c, s));
+        TDS_RCCL(ncclRecv(static_cast<char*>(out.data_ptr()) + r * n * esz, n, dt, (int)r, c, s));
+      }
+      TDS_RCCL(ncclGroupEnd());
+    });
+  }
+
+  c10::intrusive_ptr<CommWork> send(at::Tensor t, int64_t peer) {
+    check_dev(t);
+    return run({t}, "send", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclSend(t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)peer, c, s));
+    });
+  }
+
+  c10::intrusive_ptr<CommWork> recv(at::Tensor t, int64_t peer) {
+    check_dev(t);
+    return run({t}, "recv", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclRecv(t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)peer, c, s));
+    });
+  }
+
+  // ProcessGroupNCCL semantics: a 1-element all-reduce, then the host waits for it.
+  void barrier() {
+    c10::hip::HIPGuard g((c10::DeviceIndex)st_->device);
+    if (!barrier_buf_.defined())
+      barrier_buf_ = at::zeros({1}, at::TensorOptions().dtype(at::kInt).device(at::kCUDA, st_->device));
+    auto w = allreduce_async(barrier_buf_, R_SUM);
+    w->synchronize();
+  }
+
+ private:
+  std::shared_ptr<RcclState> st_;
+  c10::hip::HIPStream stream_;
+  hipEvent_t ready_ = nullptr;
+  std::thread watchdog_;
+  at::Tensor barrier_buf_;
+  std::mutex run_mu_;  // the caller (main thread) and the reducer (autograd thread) may both enqueue
+
+  void check_dev(const at::Tensor& t) const {
+    TORCH_CHECK(t.is_cuda() && t.get_device() == st_->device, "rccl: tensor must be on cuda:", st_->device);
+    TORCH_CHECK(t.is_contiguous(), "rccl: tensor must be contiguous");
+  }
+
+  template <class F>
+  c10::intrusive_ptr<CommWork> run(const std::vector<at::Tensor>& ts, const char* what, F&& fn) {
+    st_->check_ok();
+    std::lock_guard<std::mutex> run_lock(run_mu_);
+    c10::hip::HIPGuard g((c10::DeviceIndex)st_->device);
+    hipStream_t cur = c10::hip::getCurrentHIPStream((c10::DeviceIndex)st_->device).stream();
+    hipStream_t cs = stream_.stream();
+    // comm stream waits for the producer work already queued on the caller's stream
+    TDS_HIP(hipEventRecord(ready_, cur));
+    TDS_HIP(hipStreamWaitEvent(cs, ready_, 0));
+    fn(st_->comm, cs);
+    for (const auto& t : ts) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
+    hipEvent_t done;
+    TDS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    TDS_HIP(hipEventRecord(done, cs));
+    // the watchdog tracks its own event (the Work may be dropped before completion)
+    hipEvent_t wd;
+    TDS_HIP(hipEventCreateWithFlags(&wd, hipEventDisableTiming));
+    TDS_HIP(hipEventRecord(wd, cs));
+    {
+      std::lock_guard<std::mutex> gl(st_->mu);
+      st_->pending.push_back({wd, std::chrono::steady_clock::now(), what});
+    }
+    return c10::make_intrusive<RcclWork>(st_, done);
+  }
+
+  static void watchdog_loop(std::shared_ptr<RcclState> s) {
+    (void)hipSetDevice(s->device);
+    std::unique_lock<std::mutex> lk(s->mu);
+    while (!s->stop) {
+      s->cv.wait_for(lk, std::chrono::milliseconds(100));
+      if (s->stop || s->aborted.load()) break;
+      const auto now = std::chrono::steady_clock::now();
+      std::string why;
+      while (!s->pending.empty()) {
+        auto& p = s->pending.front();
+        hipError_t e = hipEventQuery(p.done);
+        if (e == hipSuccess) {
+          (void)hipEventDestroy(p.done);
+          s->pending.pop_front();
+          continue;
+        }
+        if (e != hipErrorNotReady) {
+          why = std::string("HIP error on the comm stream: ") + hipGetErrorString(e);
+        } else if (now - p.start > std::chrono::milliseconds(s->timeout_ms)) {
+          why = "collective '" + p.what + "' did not complete within " + std::to_string(s->timeout_ms) + " ms";
+        }
+        break;  // collectives complete in order on the comm stream
+      }
+      if (why.empty() && s->comm) {
+        ncclResult_t ae = ncclSuccess;
+        if (ncclCommGetAsyncError(s->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+          why = std::string("RCCL async error: ") + ncclGetErrorString(ae);
+      }
+      if (!why.empty()) {
+        lk.unlock();
+        s->fail(why);
+        lk.lock();
+        break;
+      }
+    }
+  }
+};
+
+}  // namespace tds_comm

@@ -25,6 +25,12 @@ What is different (MI355X-first):
 * **Static bucket order** = reverse parameter order (the order gradients
   become ready), so there is no iteration-0 single-bucket pass and no bucket
   rebuild.
+* **Native reducer.**  With this package's communicators (``rccl-native``,
+  ``host``) — or at world size 1 — bucket bookkeeping runs in C++
+  (``csrc/comm/reducer.cpp``): AccumulateGrad post-hooks, per-bucket ready
+  counters, all-reduce launch on the comm stream and the end-of-backward
+  stream fence, with no Python on the backward path.  With torch's own
+  process groups (``nccl``/``gloo``) the same logic runs from Python hooks.
 * Buckets follow torch's size rule (add a tensor, close the bucket once it
   reaches ``bucket_cap_mb``, default 25), which for the ConvNet gives the
   measured reference layout ``[[fc.bias, fc.weight], [8 conv/BN tensors]]``:
@@ -61,7 +67,8 @@ class _Bucket:
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  process_group=None, bucket_cap_mb: Optional[float] = None, find_unused_parameters: bool = False,
-                 gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False):
+                 gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False,
+                 reducer: str = "auto"):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -122,8 +129,49 @@ class DistributedDataParallel(nn.Module):
         # ---- gradient sinks + readiness hooks
         for p in self._params:
             grad_sink.register(p, self._make_view_fn(p))
-        self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self._params]
         self._callback_queued = False
+        self._native = self._make_native_reducer(reducer)
+        if self._native is None:
+            self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self._params]
+        else:
+            self._hooks = []
+            self._native.attach(self._params)
+
+    def _make_native_reducer(self, mode: str):
+        if mode not in ("auto", "native", "python"):
+            raise ValueError(f"reducer must be auto|native|python, got {mode!r}")
+        if mode == "python":
+            return None
+        from .. import _ext
+        from .rccl_backend import native_comm_of
+
+        comm, kind = native_comm_of(self.process_group) if self.world_size > 1 else (None, None)
+        if self.world_size > 1 and comm is None:
+            if mode == "native":
+                raise RuntimeError("reducer='native' needs a native process group (backend rccl-native or host)")
+            return None  # torch's own PG (nccl/gloo): Python hooks drive it
+        if not _ext.load():
+            if mode == "native" or self.device.type == "cuda":
+                _ext.ops()  # raises with the load error
+            return None
+        idx = {id(p): i for i, p in enumerate(self._params)}
+        ps = torch.zeros(len(self._params), 3, dtype=torch.int64)
+        for b in self._buckets:
+            for p in b.params:
+                o, n = self._slots[id(p)]
+                ps[idx[id(p)]] = torch.tensor([o, n, b.index])
+        bs = torch.tensor([[b.offset, b.numel] for b in self._buckets], dtype=torch.int64)
+        r = _ext.classes().Reducer(self.flat_grad, ps, bs, bool(self.find_unused_parameters))
+        if kind == "rccl":
+            r.set_rccl_comm(comm)
+            self._rccl_comm = comm
+        elif kind == "host":
+            r.set_host_comm(comm)
+        return r
+
+    @property
+    def reducer_kind(self) -> str:
+        return "native" if self._native is not None else "python"
 
     # ------------------------------------------------------------------ setup helpers
     def _make_view_fn(self, p):
@@ -168,6 +216,11 @@ class DistributedDataParallel(nn.Module):
         bufs = [b for b in self.module.buffers() if b is not None]
         if not bufs:
             return
+        comm = getattr(self, "_rccl_comm", None)
+        if comm is not None and all(b.is_contiguous() and b.is_cuda for b in bufs):
+            # one grouped RCCL launch, no flatten/copy-back
+            comm.broadcast_coalesced(bufs, 0).wait()
+            return
         by_dtype = {}
         for b in bufs:
             by_dtype.setdefault((b.dtype, b.device), []).append(b)
@@ -185,7 +238,10 @@ class DistributedDataParallel(nn.Module):
         if self.broadcast_buffers and self.world_size > 1:
             with torch.no_grad():
                 self._broadcast_buffers_now()  # C6: rank-0 BN running stats each forward
-        self._reset_bucket_state()
+        if self._native is not None:
+            self._native.prepare_for_backward(bool(self.require_backward_grad_sync))
+        else:
+            self._reset_bucket_state()
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager

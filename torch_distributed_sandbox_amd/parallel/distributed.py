@@ -11,6 +11,8 @@ Backends
 ``"gloo"``               CPU collectives (tests / CPU rehearsals).
 ``"host"``               this package's C++ TCP ring backend (``csrc/comm``),
                          registered with torch.distributed as a custom backend.
+``"rccl-native"``        this package's C++ RCCL communicator (own comm stream,
+                         event works, watchdog/abort; ``parallel/rccl_backend.py``).
 ``None``                 ``rccl`` when a GPU is visible, else ``gloo``
                          (the reference's auto-switch, test_init.py:84-88).
 
@@ -58,7 +60,9 @@ def _normalise_backend(backend: Optional[str]) -> str:
         return "gloo"
     if b == "host":
         return "host"
-    raise ValueError(f"unknown backend {backend!r} (expected rccl|nccl|gloo|host)")
+    if b in ("rccl-native", "rccl_native", "tds_rccl", "native"):
+        return "rccl-native"
+    raise ValueError(f"unknown backend {backend!r} (expected rccl|nccl|gloo|host|rccl-native)")
 
 
 def _torch_backend(b: str) -> str:
@@ -69,6 +73,10 @@ def _torch_backend(b: str) -> str:
 
         host_backend.register()
         return host_backend.BACKEND_NAME
+    if b == "rccl-native":
+        from . import rccl_backend
+
+        return rccl_backend.register()
     return b
 
 
@@ -106,12 +114,14 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             init_method = "env://"
         kwargs["init_method"] = init_method
-    if b == "rccl":
+    if b in ("rccl", "rccl-native"):
         if device_id is None:
             device_id = int(os.environ.get("LOCAL_RANK", rank % max(1, torch.cuda.device_count())))
         torch.cuda.set_device(device_id)
-        # eager communicator init (bound to this GPU) instead of lazy first-collective init
-        kwargs["device_id"] = torch.device("cuda", device_id)
+        if b == "rccl":
+            # eager communicator init (bound to this GPU) instead of lazy first-collective init
+            kwargs["device_id"] = torch.device("cuda", device_id)
+        # (rccl-native always creates its communicator eagerly in the backend constructor)
     dist.init_process_group(**kwargs)
     _state["backend"] = b
     _state["groups"] = {}
@@ -161,7 +171,7 @@ def new_group(ranks: Optional[Sequence[int]] = None, backend: Optional[str] = No
 
 def _needs_avg_emulation(group) -> bool:
     b = dist.get_backend(group)
-    return b not in ("nccl", "tds_host")
+    return b not in ("nccl", "tds_host", "tds_rccl")
 
 
 def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool = False):
