@@ -47,7 +47,7 @@ def test_layer1_forward(gpu, H):
     be1 = torch.randn(16, device=gpu) * 0.1
     rm, rv = torch.zeros(16, device=gpu), torch.ones(16, device=gpu)
     nbt = torch.zeros((), dtype=torch.long, device=gpu)
-    p1, idx1, stats, ac, strips = _ops().fused_l1_forward(x, w1, b1, g1, be1, rm, rv, nbt, 0.1, 1e-5)
+    p1, idx1, stats, gram = _ops().fused_l1_forward(x, w1, b1, g1, be1, rm, rv, nbt, 0.1, 1e-5)
     xd = x.double().cpu()
     y = F.conv2d(xd, w1.double().cpu(), b1.double().cpu(), padding=2)
     rmr, rvr = torch.zeros(16, dtype=torch.float64), torch.ones(16, dtype=torch.float64)
@@ -66,6 +66,12 @@ def test_layer1_forward(gpu, H):
     mine = idx1.permute(0, 3, 1, 2).long().cpu()
     pos = ref > 1e-6
     assert (mine[pos] == rr[pos]).float().mean().item() > 0.999
+    # Gram of the zero-padded 5x5 patches and the patch sums (fp64 reference)
+    pat = F.unfold(xd, 5, padding=2)  # [B, 25, H*W]
+    G = torch.einsum("bkp,bjp->kj", pat, pat)
+    S = pat.sum((0, 2))
+    _check(gram[:625].view(25, 25), G, 2e-6, "G")
+    _check(gram[625:], S, 2e-6, "S")
 
 
 def test_conv2_forward(gpu):

@@ -41,7 +41,7 @@ def main(H, B):
     dl = torch.randn(B, 10, device=dev)
     logits_r.backward(dl.double().cpu())
     # fused
-    p1, idx1, st1, ac, strips = ops.fused_l1_forward(x, w1, b1, g1, be1, None, None, None, 0.1, 1e-5)
+    p1, idx1, st1, gram = ops.fused_l1_forward(x, w1, b1, g1, be1, None, None, None, 0.1, 1e-5)
     print(f"H={H} B={B}")
     print("  p1      ", rel(unpack(p1, 16).permute(0, 3, 1, 2), p1r))
     wp, wd = ops.conv2_pack(w2)
@@ -55,7 +55,7 @@ def main(H, B):
     dp1, dw2, db2 = ops.fused_conv2_backward(dy2, p1, wd, True, 1.0)
     print("  dp1     ", rel(dp1.permute(0, 3, 1, 2), p1r.grad))
     print("  dw2     ", rel(dw2, P[4].grad))
-    dw1, db1, dg1, dbe1 = ops.fused_l1_backward(dp1, x, p1, idx1, w1, b1, g1, st1, ac, strips, 1.0)
+    dw1, db1, dg1, dbe1 = ops.fused_l1_backward(dp1, x, p1, idx1, w1, b1, g1, st1, gram, 1.0)
     print("  dw1     ", rel(dw1, P[0].grad), " dg1", rel(dg1, P[2].grad), " dbe1", rel(dbe1, P[3].grad))
     # conv2 backward fed with the exact fp64 dy2 / p1 (isolates the kernels from upstream error)
     def pack(t):

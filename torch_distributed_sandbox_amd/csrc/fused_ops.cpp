@@ -38,7 +38,7 @@ int ac_wg() { return tds_fused_num_wg(4); }
 
 // ---------------------------------------------------------------- layer 1 forward
 // returns (p1 carrier, idx1, stats1[mean16|invstd16], ac_partial, strips)
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
+std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     const Tensor& x, const Tensor& w1, const Tensor& b1, const c10::optional<Tensor>& gamma1,
     const c10::optional<Tensor>& beta1, const c10::optional<Tensor>& rm1, const c10::optional<Tensor>& rv1,
     const c10::optional<Tensor>& nbt1, double momentum, double eps) {
@@ -62,26 +62,28 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   hipStream_t st = stream_of(x);
   const int64_t P = H / 2;
   auto fo = x.options();
-  const int nwg = l1_wg();
-  auto partial = at::empty({16 * nwg * 2}, fo.dtype(at::kDouble));
-  tds_l1_stats(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg,
-               (int)B, (int)H, (int)W, st);
-  auto sums = at::empty({32}, fo.dtype(at::kDouble));
-  tds_reduce_partials(partial.data_ptr<double>(), sums.data_ptr<double>(), 32, nwg, 2, (int64_t)nwg * 2, 2, st);
-  auto stats = at::empty({32}, fo);
-  auto aff = at::empty({32}, fo);
-  tds_bn_finalize_shifted(sums.data_ptr<double>(), 16, 1, B * H * W, b1.data_ptr<float>(), (float)eps,
-                          (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
-  auto p1 = at::empty({B, P, P, 16}, fo);  // carrier of bf16 [B,P,P,32]
-  auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
-  tds_l1_apply(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(), p1.data_ptr(),
-               idx1.data_ptr<uint8_t>(), nwg, (int)B, (int)H, (int)W, st);
+  // x autocorrelation + border strips -> Gram G / patch sums S -> BN1 statistics in closed form
   const int nac = ac_wg();
   auto ac = at::empty({nac * 42}, fo.dtype(at::kDouble));
   auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
   tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
                  st);
-  return {p1, idx1, stats, ac, strips};
+  auto asum = at::empty({42}, fo.dtype(at::kDouble));
+  tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
+  auto gram = at::empty({650}, fo.dtype(at::kDouble));
+  auto sums = at::empty({32}, fo.dtype(at::kDouble));
+  tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W,
+              w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), st);
+  auto stats = at::empty({32}, fo);
+  auto aff = at::empty({32}, fo);
+  tds_bn_finalize_shifted(sums.data_ptr<double>(), 16, 1, B * H * W, b1.data_ptr<float>(), (float)eps,
+                          (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+  // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1, argmax
+  auto p1 = at::empty({B, P, P, 16}, fo);  // carrier of bf16 [B,P,P,32]
+  auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
+  tds_l1_apply(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(), p1.data_ptr(),
+               idx1.data_ptr<uint8_t>(), l1_wg(), (int)B, (int)H, (int)W, st);
+  return {p1, idx1, stats, gram};
 }
 
 // ---------------------------------------------------------------- conv2 forward
@@ -221,7 +223,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward(const Tensor& dy2, const
 std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, const Tensor& x, const Tensor& p1,
                                                              const Tensor& idx1, const Tensor& w1, const Tensor& b1,
                                                              const c10::optional<Tensor>& gamma1, const Tensor& stats1,
-                                                             const Tensor& ac, const Tensor& strips, double scale) {
+                                                             const Tensor& gram, double scale) {
   TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, "fused_l1_backward: x");
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3), P = H / 2;
   need(x, at::kFloat, {B, 1, H, W}, "x");
@@ -231,8 +233,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   need(w1, at::kFloat, {16, 1, 5, 5}, "conv1.weight");
   need(b1, at::kFloat, {16}, "conv1.bias");
   need(stats1, at::kFloat, {32}, "stats1");
-  need(strips, at::kDouble, {9 * 82}, "strips");
-  TORCH_CHECK(ac.is_cuda() && ac.scalar_type() == at::kDouble && ac.numel() % 42 == 0, "ac partial");
+  need(gram, at::kDouble, {650}, "gram");
   const float* g = optf(gamma1, 16, "bn1.weight");
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
@@ -240,17 +241,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   auto partial = at::empty({(int64_t)nwg * 16 * 27}, x.options().dtype(at::kDouble));
   tds_l1_bwd(x.data_ptr<float>(), dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(), w1.data_ptr<float>(),
              b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
-  const int nac = (int)(ac.numel() / 42);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
-  auto asum = at::empty({42}, x.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, nwg, 16 * 27, 0, 16 * 27, st);
-  tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
   auto dw1 = at::empty({16, 1, 5, 5}, x.options());
   auto db1 = at::empty({16}, x.options());
   auto dg = at::empty({16}, x.options());
   auto dbe = at::empty({16}, x.options());
-  tds_l1_finalize(bsum.data_ptr<double>(), 1, asum.data_ptr<double>(), 1,
-                  strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W, w1.data_ptr<float>(),
+  tds_l1_finalize(bsum.data_ptr<double>(), gram.data_ptr<double>(), B * H * W, w1.data_ptr<float>(),
                   b1.data_ptr<float>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(), db1.data_ptr<float>(),
                   dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale, st);
   return {dw1, db1, dg, dbe};
@@ -261,7 +258,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
 TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
-      "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor, Tensor)",
+      "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_forward);
   m.def("conv2_pack(Tensor w2) -> (Tensor, Tensor)", &conv2_pack);
   m.def("fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2) -> (Tensor, Tensor)", &fused_conv2_forward);
@@ -278,6 +275,6 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
         &fused_conv2_backward);
   m.def(
       "fused_l1_backward(Tensor dp1, Tensor x, Tensor p1, Tensor idx1, Tensor w1, Tensor b1, Tensor? gamma1, "
-      "Tensor stats1, Tensor ac, Tensor strips, float scale) -> (Tensor, Tensor, Tensor, Tensor)",
+      "Tensor stats1, Tensor gram, float scale) -> (Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_backward);
 }

@@ -2,12 +2,13 @@
 // Reference model: mnist_onegpu.py:11-31; SURVEY.md §2.4 K1-K4, K6-K18, K22-K25.
 //
 // Forward
-//   l1_conv<STATS>  : conv1 (exact fp32, v_mfma_f32_16x16x4_f32) -> per-channel sum / sumsq
-//                     of y1 - b1 (shifted for stability); y1 is never written (2.88 GB saved).
 //   x_autocorr      : 9x9 autocorrelation + border strips of x -> Gram G = sum xpatch xpatch^T
-//                     and S = sum xpatch, used by the closed-form conv1 weight gradient.
-//   l1_conv<APPLY>  : conv1 recomputed, BN1 affine, ReLU, 2x2 max-pool -> p1 (bf16 hi|lo NHWC)
-//                     and a 1-byte argmax per pooled value.
+//                     and S = sum xpatch (l1_gram).  BN1 statistics follow in closed form
+//                     (sum y1 - b1 = w1.S, sum (y1 - b1)^2 = w1^T G w1), so conv1 runs ONCE;
+//                     G and S are reused by the closed-form conv1 weight gradient.
+//   l1_conv         : conv1 (exact fp32, v_mfma_f32_16x16x4_f32), BN1 affine, ReLU, 2x2 max-pool
+//                     -> p1 (bf16 hi|lo NHWC) and a 1-byte argmax per pooled value; y1 is never
+//                     written (2.88 GB saved).
 //   [conv2 fwd + BN2 stats]
 //   head_fwd        : BN2 affine + ReLU + 2x2 pool + fc, one pass over y2 and W (p2 never stored).
 // Backward
@@ -41,13 +42,11 @@ __device__ __forceinline__ int l1_koff(int k) {
   return (k % 5) * L1_XS + (k / 5);
 }
 
-template <int MODE>
 __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ x, const float* __restrict__ w1,
                                                       const float* __restrict__ b1, const float* __restrict__ aff,
-                                                      double* __restrict__ partial, uint4* __restrict__ p1,
-                                                      uint8_t* __restrict__ idx1, int B, int H, int W) {
+                                                      uint4* __restrict__ p1, uint8_t* __restrict__ idx1, int B,
+                                                      int H, int W) {
   __shared__ __attribute__((aligned(16))) float xs[L1_XR * L1_XS];
-  __shared__ double red[4][16][2];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int P = H / 2, PW = W / 2;
@@ -70,10 +69,9 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     bia[r] = b1[4 * g + r];
-    ea[r] = MODE == 1 ? aff[4 * g + r] : 0.f;
-    eb[r] = MODE == 1 ? aff[16 + 4 * g + r] : 0.f;
+    ea[r] = aff[4 * g + r];
+    eb[r] = aff[16 + 4 * g + r];
   }
-  float s_acc[4] = {0.f, 0.f, 0.f, 0.f}, q_acc[4] = {0.f, 0.f, 0.f, 0.f};
 
   // x tile staging: LDS column 0 <-> global column c0-4 (16-B aligned since W % 4 == 0),
   // 20 rows x 18 float4; the next tile's loads are issued before this tile's MFMAs.
@@ -133,22 +131,7 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
               acc[a][c] = mfma16x4(wa[s], bv, acc[a][c]);
             }
         }
-        if (MODE == 0) {
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              const int row = r0 + 4 * wv + 2 * rp + a, col = c0 + (2 * sp + c) * 16 + li;
-              if (row < H && col < W) {
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                  const float v = acc[a][c][r];  // y1 - b1 (shifted statistics)
-                  s_acc[r] += v;
-                  q_acc[r] += v * v;
-                }
-              }
-            }
-        } else {
+        {
           // BN1 affine -> 2x2 max-pool (first max in scan order, NaN wins) -> ReLU
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
@@ -186,29 +169,6 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
           }
         }
       }
-    }
-  }
-  if (MODE == 0) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) {
-        s_acc[r] += __shfl_xor(s_acc[r], off, 64);
-        q_acc[r] += __shfl_xor(q_acc[r], off, 64);
-      }
-    }
-    if (li == 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        red[wv][4 * g + r][0] = s_acc[r];
-        red[wv][4 * g + r][1] = q_acc[r];
-      }
-    }
-    __syncthreads();
-    if (tid < 32) {
-      const int co = tid >> 1, k = tid & 1;
-      const double v = red[0][co][k] + red[1][co][k] + red[2][co][k] + red[3][co][k];
-      partial[((int64_t)co * gridDim.x + blockIdx.x) * 2 + k] = v;
     }
   }
 }
@@ -605,41 +565,22 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
   }
 }
 
-// Closed-form layer-1 gradients (one workgroup).  Inputs: l1_bwd partials, x
-// autocorrelation partials + border strips, BN1 stats/params, conv1 params.
+// Gram of the conv1 patches from the x autocorrelation (one workgroup):
 //   G[k][j] = Full(d) - sum_{excluded rows of k} R(d,row) - sum_{excluded cols} C(d,col)
 //             + sum corners,  d = o_j - o_k  (see x_autocorr / x_border)
-//   dw1[c][j] = a1 sdzx[c][j] + a2 (sum_k w1[c][k] G[k][j] + b1[c] S[j]) + a3 S[j]
-__global__ void l1_finalize_kernel(const double* __restrict__ bwd_partial, int nbwd,
-                                   const double* __restrict__ ac_partial, int nac,
-                                   const double* __restrict__ strips, const float* __restrict__ x, int B, int H, int W,
-                                   const float* __restrict__ w1, const float* __restrict__ b1,
-                                   const float* __restrict__ gamma1, const float* __restrict__ stats1,
-                                   float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dgamma1,
-                                   float* __restrict__ dbeta1, float scale) {
-  __shared__ double full[81];
-  __shared__ double G[25][25];
-  __shared__ double S[25];
-  __shared__ double acc[16][LB_NACC];
+//   S[j]    = sum of x over the pixels tap j sees (total - excluded lines + corners)
+// ac_sum: reduced autocorrelation [42] (slot 41 = plain sum).
+__device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips,
+                              const float* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
+                              double* full) {
   const int tid = threadIdx.x;
-  // fold l1_bwd partials
-  for (int e = tid; e < 16 * LB_NACC; e += blockDim.x) {
-    double s = 0.0;
-    for (int k = 0; k < nbwd; ++k) s += bwd_partial[(int64_t)k * 16 * LB_NACC + e];
-    acc[e / LB_NACC][e % LB_NACC] = s;
-  }
-  // fold autocorrelation partials into the 81 offsets
   if (tid < 81) {
     const int dy = tid / 9 - 4, dx = tid % 9 - 4;
     int sy = dy, sx = dx;
     if (dy < 0 || (dy == 0 && dx < 0)) { sy = -dy; sx = -dx; }
-    const int i = sy == 0 ? sx : 5 + (sy - 1) * 9 + (sx + 4);
-    double s = 0.0;
-    for (int k = 0; k < nac; ++k) s += ac_partial[(int64_t)k * 42 + i];
-    full[tid] = s;
+    full[tid] = ac_sum[sy == 0 ? sx : 5 + (sy - 1) * 9 + (sx + 4)];
   }
   __syncthreads();
-  // corner products (and plain corner values) computed directly from x (16 px per image)
   for (int e = tid; e < 625 + 25; e += blockDim.x) {
     const bool isS = e >= 625;
     const int k = isS ? e - 625 : e / 25, j = isS ? e - 625 : e % 25;
@@ -671,44 +612,80 @@ __global__ void l1_finalize_kernel(const double* __restrict__ bwd_partial, int n
         }
       G[k][j] = v;
     } else {
-      // S[j] = sum over U_j of x = total - excluded row sums - excluded col sums + corners
-      v = 0.0;
+      v = ac_sum[41];
       for (int i = 0; i < ne; ++i) v -= strips[line_index_row(er[i]) * 82 + 81];
       for (int i = 0; i < nc; ++i) v -= strips[line_index_col(ec[i]) * 82 + 81];
       for (int i = 0; i < ne; ++i)
         for (int q = 0; q < nc; ++q)
           for (int b = 0; b < B; ++b) v += x[(int64_t)b * H * W + (int64_t)er[i] * W + ec[q]];
-      S[j] = v;  // total added below
+      S[j] = v;
     }
   }
   __syncthreads();
-  if (tid < 25) {
-    double tot = 0.0;  // whole-image sum of x (autocorrelation slot 41)
-    for (int k = 0; k < nac; ++k) tot += ac_partial[(int64_t)k * 42 + 41];
-    S[tid] += tot;
+}
+
+// Forward: Gram + patch sums (kept for the backward) and the BN1 statistics they
+// imply, so conv1 never runs a separate statistics pass:
+//   sum_px (y1 - b1)[c]   = w1[c] . S
+//   sum_px (y1 - b1)^2[c] = w1[c]^T G w1[c]
+// gram = G[625] | S[25] (fp64); sums = [c][sum, sumsq] in the bn_finalize_shifted layout.
+__global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__ ac_sum,
+                                                      const double* __restrict__ strips, const float* __restrict__ x,
+                                                      int B, int H, int W, const float* __restrict__ w1,
+                                                      double* __restrict__ gram, double* __restrict__ sums) {
+  __shared__ double full[81];
+  __shared__ double G[25][25];
+  __shared__ double S[25];
+  __shared__ double Gw[16][25];
+  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full);
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
+  for (int e = tid; e < 16 * 25; e += blockDim.x) {
+    const int c = e / 25, j = e % 25;
+    double h = 0.0;
+    for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k][j];
+    Gw[c][j] = h * (double)w1[c * 25 + j];
   }
   __syncthreads();
-  // gradients per channel
   if (tid < 16) {
-    const int c = tid;
-    const int64_t n = (int64_t)B * H * W;
-    const double mean = stats1[c], is = stats1[16 + c];
-    const double gm = gamma1 ? gamma1[c] : 1.0;
-    const double sdz = acc[c][0], sdzy = acc[c][1];
-    const double sdxh = sdzy - mean * sdz;
-    if (dgamma1) dgamma1[c] = (float)(is * sdxh);
-    if (dbeta1) dbeta1[c] = (float)sdz;
-    const double a1 = gm * is;
-    const double a2 = -gm * is * is * is * sdxh / (double)n;
-    const double a3 = -gm * is * sdz / (double)n - a2 * mean;
-    // db1 = sum dy1 = a1 sdz + a2 sum y1 + a3 n  (sum y1 = n*mean)
-    if (db1) db1[c] = (float)(scale * (a1 * sdz + a2 * (double)n * mean + a3 * (double)n));
+    double s = 0.0, q = 0.0;
     for (int j = 0; j < 25; ++j) {
-      double h = (double)b1[c] * S[j];
-      for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k][j];
-      const double v = a1 * acc[c][2 + j] + a2 * h + a3 * S[j];
-      dw1[c * 25 + j] = (float)(scale * v);
+      s += (double)w1[tid * 25 + j] * S[j];
+      q += Gw[tid][j];
     }
+    sums[tid * 2] = s;
+    sums[tid * 2 + 1] = q;
+  }
+}
+
+// Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
+//   dw1[c][j] = a1 sdzx[c][j] + a2 (sum_k w1[c][k] G[k][j] + b1[c] S[j]) + a3 S[j]
+__global__ void l1_finalize_kernel(const double* __restrict__ bwd_sum, const double* __restrict__ gram,
+                                   int64_t n, const float* __restrict__ w1, const float* __restrict__ b1,
+                                   const float* __restrict__ gamma1, const float* __restrict__ stats1,
+                                   float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dgamma1,
+                                   float* __restrict__ dbeta1, float scale) {
+  const int c = threadIdx.x;
+  if (c >= 16) return;
+  const double* acc = bwd_sum + c * LB_NACC;
+  const double* G = gram;
+  const double* S = gram + 625;
+  const double mean = stats1[c], is = stats1[16 + c];
+  const double gm = gamma1 ? gamma1[c] : 1.0;
+  const double sdz = acc[0], sdzy = acc[1];
+  const double sdxh = sdzy - mean * sdz;
+  if (dgamma1) dgamma1[c] = (float)(is * sdxh);
+  if (dbeta1) dbeta1[c] = (float)sdz;
+  const double a1 = gm * is;
+  const double a2 = -gm * is * is * is * sdxh / (double)n;
+  const double a3 = -gm * is * sdz / (double)n - a2 * mean;
+  // db1 = sum dy1 = a1 sdz + a2 sum y1 + a3 n  (sum y1 = n*mean)
+  if (db1) db1[c] = (float)(scale * (a1 * sdz + a2 * (double)n * mean + a3 * (double)n));
+  for (int j = 0; j < 25; ++j) {
+    double h = (double)b1[c] * S[j];
+    for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k * 25 + j];
+    const double v = a1 * acc[2 + j] + a2 * h + a3 * S[j];
+    dw1[c * 25 + j] = (float)(scale * v);
   }
 }
 
@@ -725,16 +702,15 @@ int tds_fused_num_wg(int per_cu) {
   return n * per_cu;
 }
 
-void tds_l1_stats(const float* x, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
-                  hipStream_t st) {
-  hipLaunchKernelGGL(l1_conv_kernel<0>, dim3(nwg), dim3(256), 0, st, x, w1, b1, nullptr, partial, nullptr, nullptr, B,
-                     H, W);
+void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
+                 double* gram, double* sums, hipStream_t st) {
+  hipLaunchKernelGGL(l1_gram_kernel, dim3(1), dim3(256), 0, st, ac_sum, strips, x, B, H, W, w1, gram, sums);
 }
 
 void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
                   int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(l1_conv_kernel<1>, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, nullptr,
-                     reinterpret_cast<uint4*>(p1), idx1, B, H, W);
+  hipLaunchKernelGGL(l1_conv_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
+                     idx1, B, H, W);
 }
 
 void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
@@ -776,10 +752,9 @@ void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t*
                      b1, partial, B, H, W);
 }
 
-void tds_l1_finalize(const double* bwd_partial, int nbwd, const double* ac_partial, int nac, const double* strips,
-                     const float* x, int B, int H, int W, const float* w1, const float* b1, const float* gamma1,
-                     const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1, float scale,
-                     hipStream_t st) {
-  hipLaunchKernelGGL(l1_finalize_kernel, dim3(1), dim3(256), 0, st, bwd_partial, nbwd, ac_partial, nac, strips, x, B, H,
-                     W, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
+                     const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
+                     float scale, hipStream_t st) {
+  hipLaunchKernelGGL(l1_finalize_kernel, dim3(1), dim3(64), 0, st, bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1,
+                     dgamma1, dbeta1, scale);
 }

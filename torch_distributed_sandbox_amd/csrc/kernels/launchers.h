@@ -67,8 +67,8 @@ int tds_conv2_lds_bytes(int which);
 
 // ---- convnet_fused.hip
 int tds_fused_num_wg(int per_cu);
-void tds_l1_stats(const float* x, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
-                  hipStream_t st);
+void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
+                 double* gram, double* sums, hipStream_t st);
 void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
                   int B, int H, int W, hipStream_t st);
 void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
@@ -88,7 +88,6 @@ void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const f
                    hipStream_t st);
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
                 double* partial, int nwg, int B, int H, int W, hipStream_t st);
-void tds_l1_finalize(const double* bwd_partial, int nbwd, const double* ac_partial, int nac, const double* strips,
-                     const float* x, int B, int H, int W, const float* w1, const float* b1, const float* gamma1,
-                     const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1, float scale,
-                     hipStream_t st);
+void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
+                     const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
+                     float scale, hipStream_t st);

@@ -52,16 +52,15 @@ class _Layer1(torch.autograd.Function):
     def forward(ctx, x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps):
         ops = _ext.ops()
         x = x.contiguous()
-        p1, idx1, stats1, ac, strips = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps)
-        ctx.save_for_backward(x, p1, idx1, w1, b1, g1, stats1, ac, strips)
+        p1, idx1, stats1, gram = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps)
+        ctx.save_for_backward(x, p1, idx1, w1, b1, g1, stats1, gram)
         ctx.mark_non_differentiable(idx1)
         return p1
 
     @staticmethod
     def backward(ctx, dp1):
-        x, p1, idx1, w1, b1, g1, stats1, ac, strips = ctx.saved_tensors
-        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1.contiguous(), x, p1, idx1, w1, b1, g1, stats1, ac,
-                                                           strips, 1.0)
+        x, p1, idx1, w1, b1, g1, stats1, gram = ctx.saved_tensors
+        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1.contiguous(), x, p1, idx1, w1, b1, g1, stats1, gram, 1.0)
         return None, dw1, db1, dg1, dbe1, None, None, None, None, None
 
 
