@@ -45,6 +45,23 @@ __device__ __forceinline__ void split_bf16(float x, unsigned short& hi, unsigned
   lo = bf16_rne(x - h);
 }
 
+// Hardware RNE conversion (v_cvt_pk_bf16_f32) of two floats -> packed hi pair and lo pair
+// (element 0 in the low half).  NaN stays NaN.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split2_bf16(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const bf16x2_t h = __builtin_convertvector((f32x2_t){a, b}, bf16x2_t);
+  const f32x2_t hf = __builtin_convertvector(h, f32x2_t);
+  const bf16x2_t l = __builtin_convertvector((f32x2_t){a - hf.x, b - hf.y}, bf16x2_t);
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
+// lane ^ 1 (within each quad) through DPP quad_perm [1,0,3,2]: no LDS crossbar traffic
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+
 __device__ __forceinline__ float bf16_to_f32(unsigned short h) { return __uint_as_float(((unsigned int)h) << 16); }
 
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of row q,

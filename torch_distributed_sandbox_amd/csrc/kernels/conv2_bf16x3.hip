@@ -156,29 +156,36 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_fwd_bf16x3_kernel(const uint
 #pragma unroll
       for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#pragma unroll
-    for (int s = 0; s < 13; ++s) {
+    // operands of k-step s+1 are read from LDS while the MFMAs of step s run
+    s16x8 ahi[2][2], alo[2][2], bhi[2][2], blo[2][2];  // [buffer][m | n]
+    auto load_ops = [&](int s, int buf) {
       int tap = 2 * s + (g >> 1);
       if (tap > 24) tap = 0;  // zero-weight padding tap: any valid address
       const int ky = tap / 5, kx = tap - 5 * (tap / 5);
       const int rec = (wv + ky) * C2_IC + kx + li;
       const int boff = (g & 1) * 16;
-      s16x8 ahi[2], alo[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        ahi[m] = *reinterpret_cast<const s16x8*>(in_l + (rec + 16 * m) * 32 + boff);
-        alo[m] = *reinterpret_cast<const s16x8*>(in_l + F_PLANE + (rec + 16 * m) * 32 + boff);
+        ahi[buf][m] = *reinterpret_cast<const s16x8*>(in_l + (rec + 16 * m) * 32 + boff);
+        alo[buf][m] = *reinterpret_cast<const s16x8*>(in_l + F_PLANE + (rec + 16 * m) * 32 + boff);
       }
-      s16x8 bhi[2], blo[2];
 #pragma unroll
       for (int n = 0; n < 2; ++n) {
-        bhi[n] = *reinterpret_cast<const s16x8*>(w_l + ((s * 2 + n) * 64 + lane) * 16);
-        blo[n] = *reinterpret_cast<const s16x8*>(w_l + 13 * 2 * 1024 + ((s * 2 + n) * 64 + lane) * 16);
+        bhi[buf][n] = *reinterpret_cast<const s16x8*>(w_l + ((s * 2 + n) * 64 + lane) * 16);
+        blo[buf][n] = *reinterpret_cast<const s16x8*>(w_l + 13 * 2 * 1024 + ((s * 2 + n) * 64 + lane) * 16);
       }
+    };
+    load_ops(0, 0);
+#pragma unroll
+    for (int s = 0; s < 13; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < 13) load_ops(s + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
 #pragma unroll
       for (int m = 0; m < 2; ++m)
 #pragma unroll
-        for (int n = 0; n < 2; ++n) acc[m][n] = mfma_bf16x3(ahi[m], alo[m], bhi[n], blo[n], acc[m][n]);
+        for (int n = 0; n < 2; ++n)
+          acc[m][n] = mfma_bf16x3(ahi[cur][m], alo[cur][m], bhi[cur][n], blo[cur][n], acc[m][n]);
     }
     // epilogue: lane holds co = 16n + li, pixels col = c0 + 16m + 4g + r of row r0 + wv
     const int row = r0 + wv;
@@ -293,20 +300,26 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_dgrad_bf16x3_kernel(const ui
     // k-step s = flipped tap t' (ky', kx'); lane group g -> co 8g..8g+7 (plane g>>1, +16 B if g odd)
     const int hp = (g >> 1) * D_PLANE + (g & 1) * 16;
     const int lp = (2 + (g >> 1)) * D_PLANE + (g & 1) * 16;
-#pragma unroll
-    for (int s = 0; s < 25; ++s) {
+    s16x8 ahi[2][2], alo[2][2], bhi[2], blo[2];  // [buffer][m], [buffer]
+    auto load_ops = [&](int s, int buf) {
       const int ky = s / 5, kx = s % 5;
       const int rec = (wv + ky) * C2_IC + kx + li;
-      s16x8 ahi[2], alo[2];
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
-        ahi[m] = *reinterpret_cast<const s16x8*>(in_l + hp + (rec + 16 * m) * 32);
-        alo[m] = *reinterpret_cast<const s16x8*>(in_l + lp + (rec + 16 * m) * 32);
+        ahi[buf][m] = *reinterpret_cast<const s16x8*>(in_l + hp + (rec + 16 * m) * 32);
+        alo[buf][m] = *reinterpret_cast<const s16x8*>(in_l + lp + (rec + 16 * m) * 32);
       }
-      const s16x8 bhi = *reinterpret_cast<const s16x8*>(w_l + (s * 64 + lane) * 16);
-      const s16x8 blo = *reinterpret_cast<const s16x8*>(w_l + 25 * 1024 + (s * 64 + lane) * 16);
+      bhi[buf] = *reinterpret_cast<const s16x8*>(w_l + (s * 64 + lane) * 16);
+      blo[buf] = *reinterpret_cast<const s16x8*>(w_l + 25 * 1024 + (s * 64 + lane) * 16);
+    };
+    load_ops(0, 0);
 #pragma unroll
-      for (int m = 0; m < 2; ++m) acc[m] = mfma_bf16x3(ahi[m], alo[m], bhi, blo, acc[m]);
+    for (int s = 0; s < 25; ++s) {
+      const int cur = s & 1;
+      if (s + 1 < 25) load_ops(s + 1, cur ^ 1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+#pragma unroll
+      for (int m = 0; m < 2; ++m) acc[m] = mfma_bf16x3(ahi[cur][m], alo[cur][m], bhi[cur], blo[cur], acc[m]);
     }
     const int row = r0 + wv;
     if (row < P) {
@@ -420,10 +433,10 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_wgrad_bf16x3_kernel(const ui
     __syncthreads();
     if (t + (int)gridDim.x < it.total) load_tile(t + gridDim.x);
 
-#pragma unroll 1
-    for (int row = 0; row < C2_TH; ++row) {
+    // transposed operand reads of row+1 are issued while row's MFMAs run
+    s16x8 ahi[2][2], alo[2][2], bhi[2][4], blo[2][4];  // [buffer][co half | tap slot]
+    auto load_row = [&](int row, int buf) {
       // A = dy2[px = 8g+j of this row][co]: two transposed reads (4 px each) per plane
-      s16x8 ahi[2], alo[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int r_a = row * C2_TC + 8 * g + q4;
@@ -431,31 +444,46 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_wgrad_bf16x3_kernel(const ui
         const s16x4 x1 = ds_read_tr16(d_l + h * W_DPLANE + wswz(r_a + 4) * 32 + p4 * 8);
         const s16x4 y0 = ds_read_tr16(d_l + (2 + h) * W_DPLANE + wswz(r_a) * 32 + p4 * 8);
         const s16x4 y1 = ds_read_tr16(d_l + (2 + h) * W_DPLANE + wswz(r_a + 4) * 32 + p4 * 8);
-        ahi[h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-        alo[h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+        ahi[buf][h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        alo[buf][h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        if (k < ntap) {
-          const int tap = wv + 8 * k;
-          s16x8 bhi, blo;
-          if (tap < 25) {
-            const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-            const int r_b = (row + ky) * C2_IC + kx + 8 * g + q4;
-            const s16x4 x0 = ds_read_tr16(p_l + wswz(r_b) * 32 + p4 * 8);
-            const s16x4 x1 = ds_read_tr16(p_l + wswz(r_b + 4) * 32 + p4 * 8);
-            const s16x4 y0 = ds_read_tr16(p_l + W_PPLANE + wswz(r_b) * 32 + p4 * 8);
-            const s16x4 y1 = ds_read_tr16(p_l + W_PPLANE + wswz(r_b + 4) * 32 + p4 * 8);
-            bhi = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-            blo = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
-          } else {
-            bhi = ones_hi;
-            blo = zero8;
-          }
-#pragma unroll
-          for (int h = 0; h < 2; ++h) acc[k][h] = mfma_bf16x3(ahi[h], alo[h], bhi, blo, acc[k][h]);
+        const int tap = wv + 8 * k;
+        if (k < ntap && tap < 25) {
+          const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+          const int r_b = (row + ky) * C2_IC + kx + 8 * g + q4;
+          const s16x4 x0 = ds_read_tr16(p_l + wswz(r_b) * 32 + p4 * 8);
+          const s16x4 x1 = ds_read_tr16(p_l + wswz(r_b + 4) * 32 + p4 * 8);
+          const s16x4 y0 = ds_read_tr16(p_l + W_PPLANE + wswz(r_b) * 32 + p4 * 8);
+          const s16x4 y1 = ds_read_tr16(p_l + W_PPLANE + wswz(r_b + 4) * 32 + p4 * 8);
+          bhi[buf][k] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+          blo[buf][k] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+        } else {
+          bhi[buf][k] = ones_hi;  // tap 25: ones column -> bias gradient
+          blo[buf][k] = zero8;
         }
       }
+    };
+    auto mma_row = [&](int cur) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k < ntap) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            acc[k][h] = mfma_bf16x3(ahi[cur][h], alo[cur][h], bhi[cur][k], blo[cur][k], acc[k][h]);
+        }
+      }
+    };
+    load_row(0, 0);
+#pragma unroll 1
+    for (int row = 0; row < C2_TH; row += 2) {
+      load_row(row + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this row's MFMAs
+      mma_row(0);
+      if (row + 2 < C2_TH) load_row(row + 2, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mma_row(1);
     }
   }
   // slab[wg][tap(26)][co(32)][ci(16)]: lane holds C[row = co 4g+r][col = ci li] for co half h

@@ -64,13 +64,12 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
 #pragma unroll
   for (int s = 0; s < 7; ++s) koff[s] = l1_koff(4 * s + g);
 
-  // per-lane epilogue constants for co = 4g + r
-  float bia[4], ea[4], eb[4];
+  // per-lane epilogue constants for co = 4g + r: z = ea * (acc + b1) + eb = ea * acc + ebb
+  float ea[4], ebb[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    bia[r] = b1[4 * g + r];
     ea[r] = aff[4 * g + r];
-    eb[r] = aff[16 + 4 * g + r];
+    ebb[r] = fmaf(ea[r], b1[4 * g + r], aff[16 + 4 * g + r]);
   }
 
   // x tile staging: LDS column 0 <-> global column c0-4 (16-B aligned since W % 4 == 0),
@@ -132,39 +131,56 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
             }
         }
         {
-          // BN1 affine -> 2x2 max-pool (first max in scan order, NaN wins) -> ReLU
+          // BN1 affine -> 2x2 max-pool (first max in scan order; torch's NaN rule on the
+          // rare NaN window) -> ReLU -> bf16 hi|lo record + 1-byte argmax
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
             const int col = c0 + (2 * sp + c) * 16 + li;     // conv column of this lane
             const int prow = (r0 + 4 * wv + 2 * rp) >> 1;    // pooled row
             const int pcol = col >> 1;
-            uint16_t hi[4], lo[4];
-            uint8_t ix[4];
+            float pv[4], zz[4][4];
+            uint32_t ixw = 0;
+            float nsum = 0.f;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float z0 = ea[r] * (acc[0][c][r] + bia[r]) + eb[r];
-              const float z1 = ea[r] * (acc[1][c][r] + bia[r]) + eb[r];
-              const float z0n = __shfl_xor(z0, 1, 64);
-              const float z1n = __shfl_xor(z1, 1, 64);
+              const float z0 = fmaf(ea[r], acc[0][c][r], ebb[r]);
+              const float z1 = fmaf(ea[r], acc[1][c][r], ebb[r]);
+              const float z0n = dpp_xor1(z0);
+              const float z1n = dpp_xor1(z1);
+              zz[r][0] = z0; zz[r][1] = z0n; zz[r][2] = z1; zz[r][3] = z1n;
               float m = z0;
-              int a = 0;
-              if (z0n > m || isnan(z0n)) { m = z0n; a = 1; }
-              if (z1 > m || isnan(z1)) { m = z1; a = 2; }
-              if (z1n > m || isnan(z1n)) { m = z1n; a = 3; }
-              const float p = m > 0.f ? m : (isnan(m) ? m : 0.f);
-              unsigned short h, l;
-              split_bf16(p, h, l);
-              hi[r] = h;
-              lo[r] = l;
-              ix[r] = (uint8_t)a;
+              uint32_t a = 0;
+              if (z0n > m) { m = z0n; a = 1; }
+              if (z1 > m) { m = z1; a = 2; }
+              if (z1n > m) { m = z1n; a = 3; }
+              pv[r] = fmaxf(m, 0.f);
+              ixw |= a << (8 * r);
+              nsum += (z0 + z0n) + (z1 + z1n);
             }
+            if (__builtin_amdgcn_ballot_w64(isnan(nsum)) != 0) {
+              // rare NaN window (wave-uniform branch): torch's rule, update when
+              // (v > max || isnan(v)) in scan order; relu(NaN) = NaN
+              ixw = 0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float m = zz[r][0];
+                uint32_t a = 0;
+#pragma unroll
+                for (int q = 1; q < 4; ++q)
+                  if (zz[r][q] > m || isnan(zz[r][q])) { m = zz[r][q]; a = q; }
+                pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
+                ixw |= a << (8 * r);
+              }
+            }
+            uint32_t h01, l01, h23, l23;
+            split2_bf16(pv[0], pv[1], h01, l01);
+            split2_bf16(pv[2], pv[3], h23, l23);
             if ((li & 1) == 0 && prow < P && pcol < PW) {
               const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
               uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
-              dst[g] = make_uint2(hi[0] | ((uint32_t)hi[1] << 16), hi[2] | ((uint32_t)hi[3] << 16));
-              dst[4 + g] = make_uint2(lo[0] | ((uint32_t)lo[1] << 16), lo[2] | ((uint32_t)lo[3] << 16));
-              reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] =
-                  ix[0] | ((uint32_t)ix[1] << 8) | ((uint32_t)ix[2] << 16) | ((uint32_t)ix[3] << 24);
+              dst[g] = make_uint2(h01, h23);
+              dst[4 + g] = make_uint2(l01, l23);
+              reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] = ixw;
             }
           }
         }
@@ -421,20 +437,19 @@ __global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       if (!inb[q]) continue;
-      uint16_t hi[4], lo[4];
+      float d[4];
 #pragma unroll
       for (int cc = 0; cc < 4; ++cc) {
         const float dz = am[cc] == q ? gv[cc] : 0.f;
-        const float d = k1[cc] * dz + k2[cc] * y[q][cc] + k3[cc];
-        unsigned short h, l;
-        split_bf16(d, h, l);
-        hi[cc] = h;
-        lo[cc] = l;
+        d[cc] = fmaf(k1[cc], dz, fmaf(k2[cc], y[q][cc], k3[cc]));
       }
+      uint32_t h01, l01, h23, l23;
+      split2_bf16(d[0], d[1], h01, l01);
+      split2_bf16(d[2], d[3], h23, l23);
       const int r = 2 * wy + (q >> 1), cidx = 2 * wx + (q & 1);
       uint2* rec = dy2 + (((int64_t)b * P + r) * P + cidx) * 16;  // 128-B record = 16 x 8 B
-      rec[c4] = make_uint2(hi[0] | ((uint32_t)hi[1] << 16), hi[2] | ((uint32_t)hi[3] << 16));
-      rec[8 + c4] = make_uint2(lo[0] | ((uint32_t)lo[1] << 16), lo[2] | ((uint32_t)lo[3] << 16));
+      rec[c4] = make_uint2(h01, h23);
+      rec[8 + c4] = make_uint2(l01, l23);
     }
   }
 }
@@ -442,7 +457,7 @@ __global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict
 // ============================================================================ layer-1 backward (sparse)
 // Workgroup tile: 8 x 32 pooled pixels (x tile 20 x 68 in LDS).  Thread (c = tid & 15,
 // slot = tid >> 4) owns channel c for pooled pixels slot, slot+16, ... of the tile and
-// accumulates: sdz, sdzy (dz * y1 at the argmax), sdzx[25] (dz * xpatch).
+// accumulates: sdz and sdzx[25] (dz * xpatch); sum dz*y1 follows in closed form.
 constexpr int LB_PR = 8, LB_PC = 32;
 constexpr int LB_XR = 2 * LB_PR + 4;
 constexpr int LB_XS = 76;  // LDS x row stride (floats); column 0 <-> global column 2*pc0 - 4
@@ -466,11 +481,7 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
   const int P = H / 2, PW = W / 2;
   const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
   const int per_img = tiles_c * tiles_r, total = per_img * B;
-  float wr[25];
-#pragma unroll
-  for (int k = 0; k < 25; ++k) wr[k] = w1[c * 25 + k];
-  const float bc = b1[c];
-  float acc[LB_NACC];
+  float acc[LB_NACC];  // [0] sum dz, [1] unused (sum dz*y1 = w1 . sum dz*x + b1 sum dz, in l1_finalize), [2..] sum dz*x
 #pragma unroll
   for (int i = 0; i < LB_NACC; ++i) acc[i] = 0.f;
 
@@ -534,17 +545,11 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
       const int pr = pp / LB_PC, pc = pp - (pp / LB_PC) * LB_PC;
       const int lr = 2 * pr + (a >> 1), lc = 2 * pc + (a & 1) + 2;  // patch origin in the x tile
       const float* xp = xs + lr * LB_XS + lc;
-      float y = bc;
 #pragma unroll
       for (int ky = 0; ky < 5; ++ky)
 #pragma unroll
-        for (int kx = 0; kx < 5; ++kx) {
-          const float xv = xp[ky * LB_XS + kx];
-          y += wr[ky * 5 + kx] * xv;
-          acc[2 + ky * 5 + kx] += dz * xv;
-        }
+        for (int kx = 0; kx < 5; ++kx) acc[2 + ky * 5 + kx] += dz * xp[ky * LB_XS + kx];
       acc[0] += dz;
-      acc[1] += dz * y;
     }
   }
   __syncthreads();
@@ -672,7 +677,10 @@ __global__ void l1_finalize_kernel(const double* __restrict__ bwd_sum, const dou
   const double* S = gram + 625;
   const double mean = stats1[c], is = stats1[16 + c];
   const double gm = gamma1 ? gamma1[c] : 1.0;
-  const double sdz = acc[0], sdzy = acc[1];
+  const double sdz = acc[0];
+  // sum dz1 * y1 = w1[c] . sum dz1 xpatch + b1[c] sum dz1  (y1 = w1 . xpatch + b1)
+  double sdzy = (double)b1[c] * sdz;
+  for (int j = 0; j < 25; ++j) sdzy += (double)w1[c * 25 + j] * acc[2 + j];
   const double sdxh = sdzy - mean * sdz;
   if (dgamma1) dgamma1[c] = (float)(is * sdxh);
   if (dbeta1) dbeta1[c] = (float)sdz;
