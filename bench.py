@@ -38,6 +38,9 @@ def main(argv=None):
     ap.add_argument("--bucket-mb", type=float, default=None)
     ap.add_argument("--backend", default=os.environ.get("TDS_BENCH_BACKEND", "rccl"),
                     help="rccl (torch ProcessGroupNCCL = RCCL) | rccl-native (this package's C++ communicator)")
+    ap.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations"],
+                    help="fc gradient path under DDP: auto picks the activation exchange when it moves fewer "
+                         "bytes per rank than the ring all-reduce (parallel/factored.py)")
     ap.add_argument("--profile-phases", action="store_true", help="also report per-phase GPU times (adds events)")
     args = ap.parse_args(argv)
 
@@ -62,7 +65,10 @@ def main(argv=None):
     torch.cuda.set_device(local_rank)
     tds._ext.ops()  # native extension must be loaded (fails loudly otherwise)
     device = torch.device("cuda", local_rank)
-    if world > 1:
+    if world > 1 or args.grad_exchange == "activations":
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
         tdist.init_process_group(args.backend, rank=rank, world_size=world, device_id=local_rank)
 
     H = W = args.image_size
@@ -71,7 +77,8 @@ def main(argv=None):
     model = ConvNet(image_shape=(H, W), device=device, mode=args.mode)
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), 1e-4)
-    ddp = DistributedDataParallel(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_mb)
+    ddp = DistributedDataParallel(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_mb,
+                                  grad_exchange=args.grad_exchange)
     ddp.attach_optimizer(optimizer)
 
     # a pool of synthetic 28x28 sources; each step upsamples a different slice on device
@@ -135,13 +142,15 @@ def main(argv=None):
                 "mode": args.mode,
                 "backend": args.backend if world > 1 else None,
                 "reducer": ddp.reducer_kind,
+                "fc_grad": ("activation-exchange" if any(e.steps_exchanged for e in ddp.exchanges)
+                            else "allreduce" if world > 1 else "local"),
                 "optimizer": "SGD(lr=1e-4)",
                 "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3),
                 "final_loss": final_loss,
             },
         }
         print(json.dumps(rec), flush=True)
-    if world > 1:
+    if tdist.is_initialized():
         tdist.barrier()
         tdist.destroy_process_group()
 

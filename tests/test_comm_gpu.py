@@ -108,3 +108,58 @@ def test_native_reducer_ddp_on_rccl(pg, gpu):
             for p, q in zip(m.parameters(), ref.parameters()):
                 q.copy_(p)
     assert ddp._native.ready_order()[0] == 0  # the fc bucket is reduced first
+
+
+def test_linear_dw_kernel(gpu):
+    import torch_distributed_sandbox_amd as tds
+
+    torch.manual_seed(0)
+    for M, N, K in ((10, 10, 100_003), (15, 10, 4096), (40, 16, 777), (1, 3, 33)):
+        dy = torch.randn(M, N, device=gpu)
+        x = torch.randn(M, K, device=gpu)
+        dw = torch.empty(N, K, device=gpu)
+        db = torch.empty(N, device=gpu)
+        tds._ext.ops().linear_dw(dy, x, dw, db, 0.5, False)
+        ref = (dy.double().t() @ x.double()) * 0.5
+        assert ((dw.double() - ref).abs().max() / ref.abs().max()).item() < 1e-6, (M, N, K)
+        assert torch.allclose(db.double(), dy.double().sum(0) * 0.5, rtol=1e-6, atol=1e-6)
+        tds._ext.ops().linear_dw(dy, x, dw, db, 0.5, True)  # accumulate
+        assert ((dw.double() - 2 * ref).abs().max() / ref.abs().max()).item() < 1e-6
+
+
+def test_activation_exchange_fused_convnet(pg, gpu):
+    """Forced activation exchange at world size 1 runs the whole GPU path (head
+    forward writing the fc input rows, head backward without dW, linear_dw into
+    the bucket) and must reproduce the plain fused gradients."""
+    import copy
+
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    H = 256  # fc: 10 x 131072 (exchange candidate)
+    m = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    ref = copy.deepcopy(m)
+    ddp = DistributedDataParallel(m, grad_exchange="activations")
+    assert len(ddp.exchanges) == 1
+    opt = ddp.attach_optimizer(SGD(m.parameters(), 0.01))
+    x = torch.rand(3, 1, H, H, device=gpu)
+    y = torch.tensor([1, 2, 3], device=gpu)
+    for step in range(2):
+        loss = CrossEntropyLoss()(ddp(x), y)
+        opt.zero_grad()
+        loss.backward()
+        ref.zero_grad()
+        CrossEntropyLoss()(ref(x), y).backward()
+        for (n, p), q in zip(m.named_parameters(), ref.parameters()):
+            if n.endswith("0.bias"):
+                continue
+            rel = ((p.grad - q.grad).norm() / q.grad.norm().clamp_min(1e-30)).item()
+            assert rel < 1e-5, (step, n, rel)
+        assert m.fc.weight.grad.data_ptr() == ddp.grad_view(m.fc.weight).data_ptr()
+        opt.step()
+        with torch.no_grad():
+            for p, q in zip(m.parameters(), ref.parameters()):
+                q.copy_(p)
+    assert ddp.exchanges[0].steps_exchanged == 2

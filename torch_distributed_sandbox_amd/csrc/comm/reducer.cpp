@@ -71,6 +71,7 @@ class Reducer : public torch::CustomClassHolder {
     }
     pending_ = b_count_;
     b_ready_.assign(b_off_.size(), false);
+    b_skip_.assign(b_off_.size(), false);
     works_.resize(b_off_.size());
   }
 
@@ -118,6 +119,14 @@ class Reducer : public torch::CustomClassHolder {
     ready_order_.clear();
   }
 
+  // A skipped bucket's gradients are produced outside the hook/all-reduce path this
+  // step (DDP's activation exchange, parallel/factored.py): no hooks are expected,
+  // no all-reduce is launched.
+  void set_bucket_skip(int64_t b, bool skip) {
+    TORCH_CHECK(b >= 0 && b < (int64_t)b_skip_.size(), "Reducer.set_bucket_skip: bad bucket");
+    b_skip_[b] = skip;
+  }
+
   void on_ready(int64_t i) {
     auto& p = params_[i];
     at::Tensor& g = p.mutable_grad();
@@ -138,12 +147,13 @@ class Reducer : public torch::CustomClassHolder {
       });
     }
     const int64_t b = p_bucket_[i];
+    if (b_skip_[b]) return;
     if (--pending_[b] == 0) launch(b);
   }
 
   void finalize() {
     for (size_t b = 0; b < b_off_.size(); ++b) {
-      if (b_ready_[b]) continue;
+      if (b_ready_[b] || b_skip_[b]) continue;
       std::vector<int64_t> missing;
       for (size_t i = 0; i < params_.size(); ++i)
         if (p_bucket_[i] == (int64_t)b && !params_[i].grad().defined()) missing.push_back((int64_t)i);
@@ -174,7 +184,7 @@ class Reducer : public torch::CustomClassHolder {
   bool find_unused_;
   std::shared_ptr<std::atomic<Reducer*>> self_;
   std::vector<int64_t> p_off_, p_num_, p_bucket_, b_off_, b_num_, b_count_, pending_, ready_order_;
-  std::vector<bool> b_ready_;
+  std::vector<bool> b_ready_, b_skip_;
   std::vector<c10::intrusive_ptr<CommWork>> works_;
   std::vector<at::Tensor> params_;
   std::vector<std::shared_ptr<torch::autograd::Node>> accs_;
@@ -211,6 +221,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       .def("detach", &tds_comm::Reducer::detach)
       .def("prepare_for_backward", &tds_comm::Reducer::prepare_for_backward)
       .def("finalize", &tds_comm::Reducer::finalize)
+      .def("set_bucket_skip", &tds_comm::Reducer::set_bucket_skip)
       .def("ready_order", &tds_comm::Reducer::ready_order)
       .def("num_buckets", &tds_comm::Reducer::num_buckets);
 }

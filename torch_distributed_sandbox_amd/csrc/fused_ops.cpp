@@ -116,7 +116,8 @@ std::tuple<Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& w
 std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
     const Tensor& y2, const Tensor& partial2, const Tensor& b2, const c10::optional<Tensor>& gamma2,
     const c10::optional<Tensor>& beta2, const c10::optional<Tensor>& rm2, const c10::optional<Tensor>& rv2,
-    const c10::optional<Tensor>& nbt2, double momentum, double eps, const Tensor& wfc, const c10::optional<Tensor>& bfc) {
+    const c10::optional<Tensor>& nbt2, double momentum, double eps, const Tensor& wfc, const c10::optional<Tensor>& bfc,
+    const c10::optional<Tensor>& x_out) {
   TORCH_CHECK(y2.dim() == 4 && y2.size(3) == 32 && y2.size(1) == y2.size(2), "fused_head_forward: y2");
   const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
@@ -136,6 +137,11 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
   const int64_t NC = wfc.size(0);
   need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
   const float* bf = optf(bfc, NC, "fc.bias");
+  float* xo = nullptr;
+  if (x_out.has_value() && x_out->defined()) {
+    need(*x_out, at::kFloat, {B, 32 * Q * Q}, "x_out (fc input rows)");
+    xo = x_out->data_ptr<float>();
+  }
   c10::DeviceGuard guard(y2.device());
   hipStream_t st = stream_of(y2);
   auto sums2 = at::empty({64}, y2.options().dtype(at::kDouble));
@@ -149,17 +155,18 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
   auto lsum = at::empty({B * NC}, y2.options().dtype(at::kDouble));
   auto logits = at::empty({B, NC}, y2.options());
   const int rc = tds_head_fwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
-                              part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), (int)B,
+                              part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
                               (int)P, (int)NC, st);
   TORCH_CHECK(rc == 0, "fused_head_forward: unsupported B/NC");
   return {logits, stats, aff};
 }
 
 // ---------------------------------------------------------------- head backward
-// returns (dW [written into dw_out if given], db_fc, dgamma2, dbeta2, dy2 carrier)
+// returns (dW [written into dw_out if given; empty when !compute_dw], db_fc, dgamma2, dbeta2, dy2 carrier)
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
-    const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale) {
+    const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
+    bool compute_dw) {
   const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
   const int64_t NC = wfc.size(0);
@@ -171,7 +178,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   c10::DeviceGuard guard(y2.device());
   hipStream_t st = stream_of(y2);
   Tensor dW;
-  if (dw_out.has_value() && dw_out->defined()) {
+  if (!compute_dw) {
+    dW = at::empty({0}, wfc.options());
+  } else if (dw_out.has_value() && dw_out->defined()) {
     need(*dw_out, at::kFloat, {NC, 32 * Q * Q}, "dW_out");
     dW = *dw_out;
   } else {
@@ -181,7 +190,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   const int nblk = tds_head_fwd_nblk((int)Q);
   auto partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
   const int rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
-                              dlogits.data_ptr<float>(), dW.data_ptr<float>(), g2m.data_ptr<float>(),
+                              dlogits.data_ptr<float>(), compute_dw ? dW.data_ptr<float>() : nullptr,
+                              g2m.data_ptr<float>(),
                               partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported B/NC");
   auto sums = at::empty({64}, y2.options().dtype(at::kDouble));
@@ -264,12 +274,12 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2) -> (Tensor, Tensor)", &fused_conv2_forward);
   m.def(
       "fused_head_forward(Tensor y2, Tensor partial2, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
-      "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc) -> (Tensor, Tensor, "
-      "Tensor)",
+      "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc, Tensor(d!)? x_out=None) "
+      "-> (Tensor, Tensor, Tensor)",
       &fused_head_forward);
   m.def(
       "fused_head_backward(Tensor dlogits, Tensor y2, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor wfc, "
-      "Tensor(a!)? dw_out, float scale) -> (Tensor, Tensor, Tensor, Tensor, Tensor)",
+      "Tensor(a!)? dw_out, float scale, bool compute_dw=True) -> (Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
   m.def("fused_conv2_backward(Tensor dy2, Tensor p1, Tensor wd, bool need_dp1, float scale) -> (Tensor, Tensor, Tensor)",
         &fused_conv2_backward);

@@ -77,10 +77,13 @@ __device__ __forceinline__ void head_window(const char* lds, int lane, int wv, c
 }
 
 // partial[blk][b*NC + j] (fp64) = sum over the tile of p2[b][c][pos] * W[j][c][pos]
+// xout (optional): p2 itself, [B][32*Q*Q] in torch's flatten order (c, py, px) — the fc
+// input rows that DDP's activation exchange all-gathers (parallel/factored.py).
 template <int NW>
 __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
                                                            const float* __restrict__ aff2,
-                                                           double* __restrict__ partial, int B, int P, int Q, int NC) {
+                                                           double* __restrict__ partial, float* __restrict__ xout,
+                                                           int B, int P, int Q, int NC) {
   constexpr int CPW = 32 / NW;
   using Tile = HeadTile<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -109,6 +112,10 @@ __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(const float4* __restr
     float p[CPW], ya[CPW];
     bool ps[CPW];
     head_window<CPW>(smem, lane, wv, a, bb, p, ya, ps);
+    if (xout != nullptr && valid) {
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) xout[((int64_t)b * 32 + CPW * wv + c) * QQ + pos] = p[c];
+    }
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
       float s = 0.f;
@@ -140,7 +147,7 @@ __global__ void head_logits_kernel(const double* __restrict__ sums, const float*
 //   dW[j][c][pos]  = scale * sum_b dl[b][j] p2[b][c][pos]      (e.g. straight into the DDP bucket)
 //   g2m[b][pos][c] = (sum_j dl[b][j] W[j][c][pos]) * [p2 > 0]   (NHWC pooled gradient, fp32)
 //   partial[c][blk][2] = { sum g2m (= sum dz2), sum g2m * y2(argmax) }   (BN2 backward reductions)
-template <int NW>
+template <int NW, bool WITH_DW>
 __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
                                                            const float* __restrict__ aff2, const float* __restrict__ dl,
                                                            float* __restrict__ dW, float* __restrict__ g2m,
@@ -190,7 +197,7 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restr
       for (int j = 0; j < 10; ++j) {
         const float d = dls[b * 10 + j];
         g += d * w[j][c];
-        dwa[j][c] += d * p[c];
+        if constexpr (WITH_DW) dwa[j][c] += d * p[c];
       }
       gm[c] = ps[c] ? g : 0.f;
       sdz[c] += valid ? gm[c] : 0.f;
@@ -202,7 +209,7 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restr
       else *reinterpret_cast<float2*>(dst) = make_float2(gm[0], gm[1]);
     }
   }
-  if (valid) {
+  if (WITH_DW && valid) {
     float* dst = dW + (int64_t)(CPW * wv) * QQ + pos;
 #pragma unroll
     for (int j = 0; j < 10; ++j)
@@ -230,7 +237,9 @@ static void head_lds_limits() {
   if (done) return;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_fwd_kernel<HD_FWD_NW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, HD_LDS);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_bwd_kernel<HD_BWD_NW>),
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_bwd_kernel<HD_BWD_NW, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, HD_LDS);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_bwd_kernel<HD_BWD_NW, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, HD_LDS);
   done = true;
 }
@@ -243,13 +252,13 @@ int tds_head_fwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
 
 // partial: double [nblk][B*NC]; sums: double [B*NC] workspace
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
-                 float* logits, int B, int P, int NC, hipStream_t st) {
+                 float* logits, float* xout, int B, int P, int NC, hipStream_t st) {
   const int Q = P / 2;
   if (B > 8 || NC > 10 || Q < 1) return -1;
   head_lds_limits();
   const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
   hipLaunchKernelGGL(head_fwd_kernel<HD_FWD_NW>, grid, dim3(64 * HD_FWD_NW), HD_LDS, st,
-                     reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, B, P, Q, NC);
+                     reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, xout, B, P, Q, NC);
   const int nblk = grid.x * grid.y, BN = B * NC;
   tds_reduce_partials(partial, sums, BN, nblk, BN, 0, BN, st);
   hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);
@@ -263,7 +272,12 @@ int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const flo
   if (B > 8 || NC > 10 || Q < 1) return -1;
   head_lds_limits();
   const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
-  hipLaunchKernelGGL(head_bwd_kernel<HD_BWD_NW>, grid, dim3(64 * HD_BWD_NW), HD_LDS, st,
-                     reinterpret_cast<const float4*>(y2), Wfc, aff2, dlogits, dW, g2m, partial, B, P, Q, NC, scale);
+  // dW == nullptr: the fc weight gradient is formed elsewhere (activation exchange)
+  if (dW)
+    hipLaunchKernelGGL((head_bwd_kernel<HD_BWD_NW, true>), grid, dim3(64 * HD_BWD_NW), HD_LDS, st,
+                       reinterpret_cast<const float4*>(y2), Wfc, aff2, dlogits, dW, g2m, partial, B, P, Q, NC, scale);
+  else
+    hipLaunchKernelGGL((head_bwd_kernel<HD_BWD_NW, false>), grid, dim3(64 * HD_BWD_NW), HD_LDS, st,
+                       reinterpret_cast<const float4*>(y2), Wfc, aff2, dlogits, dW, g2m, partial, B, P, Q, NC, scale);
   return 0;
 }

@@ -50,6 +50,8 @@ void tds_bn_bwd(const float* dy, const float* x, int B, int C, int64_t HW, const
 
 // ---- linear.hip (skinny M<=8, N<=16)
 int tds_linear_fwd_nblk(int64_t K);
+int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, int N, int64_t K, float scale, int acc,
+                  hipStream_t st);
 int tds_linear_fwd_skinny(const float* x, const float* W, const float* bias, float* out, float* partial, int M, int N,
                           int64_t K, int nblk, hipStream_t st);
 int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float* dx, float* dW, float* db, int M,
@@ -77,7 +79,7 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
 int tds_head_fwd_nblk(int Q);
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
-                 float* logits, int B, int P, int NC, hipStream_t st);
+                 float* logits, float* xout, int B, int P, int NC, hipStream_t st);
 int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
                  double* partial, int B, int P, int NC, float scale, hipStream_t st);
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,

@@ -174,6 +174,55 @@ __global__ __launch_bounds__(256) void linear_bwd_skinny_kernel(const float* __r
   }
 }
 
+// Weight gradient of a linear layer from (grad_output, input) rows:
+//   dW[n][k] (= or +=) scale * sum_m g[m][n] x[m][k],  db[n] (= or +=) scale * sum_m g[m][n]
+// M <= 64 rows (e.g. the all-gathered rows of every rank), N <= 16 outputs, any K.
+// Exact fp32 on v_mfma_f32_16x16x4_f32: A[n][m] = g[m][n] stays in registers, B = 4 rows x
+// 16 columns of x per step; memory-bound on reading x and writing dW.
+__global__ __launch_bounds__(256) void linear_dw_mfma_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                                             float* __restrict__ dW, float* __restrict__ db, int M,
+                                                             int N, int64_t K, float scale, int acc) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int li = lane & 15, gq = lane >> 4;
+  const int steps = (M + 3) / 4;
+  float a[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int m = 4 * s + gq;
+    a[s] = (m < M && li < N) ? g[m * N + li] : 0.f;
+  }
+  if (db && blockIdx.x == 0 && threadIdx.x < N) {
+    float t = 0.f;
+    for (int m = 0; m < M; ++m) t += g[m * N + threadIdx.x];
+    db[threadIdx.x] = acc ? db[threadIdx.x] + scale * t : scale * t;
+  }
+  const int64_t ncb = (K + 15) / 16;
+  for (int64_t cb = (int64_t)blockIdx.x * 4 + wv; cb < ncb; cb += (int64_t)gridDim.x * 4) {
+    const int64_t col = cb * 16 + li;
+    const bool cv = col < K;
+    f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      if (s < steps) {
+        const int m = 4 * s + gq;
+        const float bv = (m < M && cv) ? x[(int64_t)m * K + col] : 0.f;
+        d = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bv, d, 0, 0, 0);
+      }
+    }
+    if (cv) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = 4 * gq + r;
+        if (n < N) {
+          float* ptr = dW + (int64_t)n * K + col;
+          const float v = scale * d[r];
+          *ptr = acc ? *ptr + v : v;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace tds
 
 using namespace tds;
@@ -217,5 +266,16 @@ int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float
   else if (M <= 4) TDS_LB(4);
   else TDS_LB(8);
 #undef TDS_LB
+  return 0;
+}
+
+int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, int N, int64_t K, float scale, int acc,
+                  hipStream_t st) {
+  if (M > 64 || N > 16 || M < 1) return -1;
+  int64_t ncb = (K + 15) / 16;
+  int64_t grid = (ncb + 3) / 4;
+  if (grid > 8192) grid = 8192;
+  hipLaunchKernelGGL(linear_dw_mfma_kernel, dim3((unsigned)grid), dim3(256), 0, st, dy, x, dW, db, M, N, K, scale,
+                     acc);
   return 0;
 }

@@ -348,6 +348,23 @@ Tensor linear_bwd_into(const Tensor& dy, const Tensor& x, const Tensor& w, const
   return dx;
 }
 
+// dW (= or +=) scale * dy^T x, db (= or +=) scale * sum_rows dy   (dy [M,N], x [M,K], M <= 64, N <= 16)
+void linear_dw(const Tensor& dy, const Tensor& x, const Tensor& dw, const c10::optional<Tensor>& db, double scale,
+               bool accumulate) {
+  check_f32_dev(dy, "grad_output");
+  check_f32_dev(x, "input");
+  check_f32_dev(dw, "dW");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dw.dim() == 2 && dy.size(0) == x.size(0) && dw.size(0) == dy.size(1) &&
+                  dw.size(1) == x.size(1),
+              "tdsa.linear_dw: shape mismatch");
+  check_opt(db, "db", dw.size(0));
+  c10::DeviceGuard g(x.device());
+  const int rc = tds_linear_dw(dy.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(), opt_mut_ptr(db),
+                               (int)dy.size(0), (int)dy.size(1), x.size(1), (float)scale, accumulate ? 1 : 0,
+                               cur_stream(x));
+  TORCH_CHECK(rc == 0, "tdsa.linear_dw: needs rows <= 64 and outputs <= 16");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tdsa, m) {
@@ -381,4 +398,6 @@ TORCH_LIBRARY(tdsa, m) {
       "linear_bwd_into(Tensor dy, Tensor x, Tensor w, Tensor(a!)? dw_out, Tensor(b!)? db_out, float scale, "
       "bool accumulate, bool need_dx) -> Tensor",
       &linear_bwd_into);
+  m.def("linear_dw(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db, float scale, bool accumulate) -> ()",
+        &linear_dw);
 }

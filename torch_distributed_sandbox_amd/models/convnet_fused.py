@@ -25,6 +25,7 @@ import torch
 
 from .. import _ext
 from ..ops import grad_sink
+from ..parallel import factored
 
 
 def supported(model, x) -> bool:
@@ -83,21 +84,35 @@ class _Conv2(torch.autograd.Function):
 
 class _Head(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc):
+    def forward(ctx, y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex):
         ops = _ext.ops()
+        x_out = None
+        if ex is not None:
+            B, P = y2.shape[0], y2.shape[1]
+            x_out = torch.empty((B, wfc.shape[1]), device=y2.device, dtype=torch.float32)
         logits, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
-                                                      bfc)
+                                                      bfc, x_out)
+        if ex is not None and not ex.begin(x_out):
+            raise RuntimeError("activation exchange refused to start after ready() agreed")
         ctx.save_for_backward(y2, stats2, aff2, g2, wfc)
         ctx.wfc_param = wfc
+        ctx.ex = ex
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         y2, stats2, aff2, g2, wfc = ctx.saved_tensors
+        dlogits = dlogits.contiguous().float()
+        ex = ctx.ex
+        if ex is not None:
+            # fc gradients come from the activation exchange (parallel/factored.py)
+            _, _, dg2, dbe2, dy2 = _ext.ops().fused_head_backward(dlogits, y2, stats2, aff2, g2, wfc, None, 1.0,
+                                                                  False)
+            ex.defer(dlogits)
+            return dy2, None, None, dg2, dbe2, None, None, None, None, None, None, None, None
         dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[10] else None, wfc.shape, wfc)
-        dW, dbfc, dg2, dbe2, dy2 = _ext.ops().fused_head_backward(dlogits.contiguous().float(), y2, stats2, aff2, g2,
-                                                                  wfc, dw_out, 1.0)
-        return dy2, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc
+        dW, dbfc, dg2, dbe2, dy2 = _ext.ops().fused_head_backward(dlogits, y2, stats2, aff2, g2, wfc, dw_out, 1.0)
+        return dy2, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None
 
 
 def forward(model, x):
@@ -107,5 +122,8 @@ def forward(model, x):
     p1 = _Layer1.apply(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
                        bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps))
     y2, partial2 = _Conv2.apply(p1, conv2.weight, conv2.bias)
+    ex = factored.get(fc.weight)
+    if ex is not None and not ex.ready(x.shape[0]):
+        ex = None
     return _Head.apply(y2, partial2, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
-                       bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias)
+                       bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias, ex)

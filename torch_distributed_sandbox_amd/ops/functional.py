@@ -170,7 +170,41 @@ class _LinearSkinny(torch.autograd.Function):
         return (dx if need_dx else None, dw_out, db_out)
 
 
+class _ExchangedLinear(torch.autograd.Function):
+    """Linear whose weight/bias gradients come from DDP's activation exchange
+    (parallel/factored.py): backward returns only dX and hands dY to the exchange."""
+
+    @staticmethod
+    def forward(ctx, x2, w, b, ex):
+        ctx.save_for_backward(x2, w)
+        ctx.ex = ex
+        if x2.is_cuda and x2.shape[0] <= 8 and w.shape[0] <= 16:
+            return _ext.ops().linear_fwd(x2, w.contiguous(), b)
+        return F.linear(x2, w, b)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        gy = gy.contiguous()
+        ctx.ex.defer(gy)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if gy.is_cuda and x2.shape[0] <= 8 and w.shape[0] <= 16:
+                dx = _ext.ops().linear_bwd_into(gy, x2, w.contiguous(), None, None, 1.0, False, True)
+            else:
+                dx = gy.mm(w)
+        return dx, None, None, None
+
+
 def linear(x, weight, bias=None):
+    from ..parallel import factored
+
+    ex = factored.get(weight)
+    if ex is not None and torch.is_grad_enabled() and weight.requires_grad:
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        if ex.begin(x2):
+            y = _ExchangedLinear.apply(x2, weight, bias, ex)
+            return y.reshape(*x.shape[:-1], weight.shape[0])
     if not x.is_cuda:
         return F.linear(x, weight, bias)
     if x.dim() == 2 and x.shape[0] <= 8 and weight.shape[0] <= 16:

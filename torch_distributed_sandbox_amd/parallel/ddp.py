@@ -48,6 +48,7 @@ import torch.nn as nn
 
 from ..ops import grad_sink
 from . import distributed as tdist
+from . import factored
 
 _ALIGN_ELEMS = 64  # 256-byte alignment of every parameter slot in the flat buffers
 
@@ -57,18 +58,18 @@ def _align(n: int) -> int:
 
 
 class _Bucket:
-    __slots__ = ("index", "params", "offset", "numel", "pending", "work", "ready")
+    __slots__ = ("index", "params", "offset", "numel", "pending", "work", "ready", "skip")
 
     def __init__(self, index, offset):
         self.index, self.params, self.offset, self.numel = index, [], offset, 0
-        self.pending, self.work, self.ready = 0, None, False
+        self.pending, self.work, self.ready, self.skip = 0, None, False, False
 
 
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  process_group=None, bucket_cap_mb: Optional[float] = None, find_unused_parameters: bool = False,
                  gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False,
-                 reducer: str = "auto"):
+                 reducer: str = "auto", grad_exchange: str = "auto"):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -90,16 +91,40 @@ class DistributedDataParallel(nn.Module):
         self._verify_param_shapes()
 
         # ---- flat layout in gradient-ready order (reverse definition order)
+        if grad_exchange not in ("auto", "allreduce", "activations"):
+            raise ValueError(f"grad_exchange must be auto|allreduce|activations, got {grad_exchange!r}")
+        self.grad_exchange = grad_exchange
+        exch_layers = self._exchange_candidates(module) if grad_exchange != "allreduce" else []
+        layer_of = {id(p): lyr for lyr in exch_layers for p in (lyr.weight, lyr.bias) if p is not None}
         order = list(reversed(self._params))
         cap_mb = 25.0 if bucket_cap_mb is None else float(bucket_cap_mb)
         limit = max(1, int(cap_mb * 1024 * 1024 // self._params[0].element_size()))
         self._slots = {}  # id(param) -> (offset, numel)
         self._buckets: List[_Bucket] = []
+        self._layer_bucket = {}  # id(exchange-candidate layer) -> bucket
         off = 0
         cur = _Bucket(0, 0)
         for p in order:
-            # torch's _compute_bucket_assignment_by_size: add, then close once >= cap
             n = p.numel()
+            lyr = layer_of.get(id(p))
+            if lyr is not None:
+                # an activation-exchange candidate gets a bucket of its own (weight + bias only)
+                lb = self._layer_bucket.get(id(lyr))
+                if lb is None:
+                    if cur.params:
+                        self._buckets.append(cur)
+                        cur = _Bucket(len(self._buckets), off)
+                    lb = cur
+                    self._layer_bucket[id(lyr)] = lb
+                self._slots[id(p)] = (off, n)
+                lb.params.append(p)
+                off += _align(n)
+                lb.numel = off - lb.offset
+                if len(lb.params) == sum(q is not None for q in (lyr.weight, lyr.bias)):
+                    self._buckets.append(lb)
+                    cur = _Bucket(len(self._buckets), off)
+                continue
+            # torch's _compute_bucket_assignment_by_size: add, then close once >= cap
             self._slots[id(p)] = (off, n)
             cur.params.append(p)
             off += _align(n)
@@ -136,6 +161,16 @@ class DistributedDataParallel(nn.Module):
         else:
             self._hooks = []
             self._native.attach(self._params)
+
+        # ---- activation exchange for huge skinny Linear layers (parallel/factored.py)
+        self._exchanges = []
+        if exch_layers and (self.world_size > 1 or (grad_exchange == "activations" and tdist.is_initialized())):
+            for lyr in exch_layers:
+                b = self._layer_bucket[id(lyr)]
+                self._exchanges.append(factored.ActivationExchange(
+                    lyr.weight, lyr.bias, process_group, self.world_size, grad_exchange,
+                    self._make_skip_fn(b), self._make_view_fn(lyr.weight),
+                    self._make_view_fn(lyr.bias) if lyr.bias is not None else None))
 
     def _make_native_reducer(self, mode: str):
         if mode not in ("auto", "native", "python"):
@@ -174,6 +209,34 @@ class DistributedDataParallel(nn.Module):
         return "native" if self._native is not None else "python"
 
     # ------------------------------------------------------------------ setup helpers
+    @staticmethod
+    def _exchange_candidates(module):
+        """This package's Linear layers (their forward routes through ops.functional.linear /
+        the fused head, which implement the exchange) big enough that exchanging activations
+        can beat all-reducing the weight gradient; the decision itself is made per step
+        from the batch rows."""
+        from ..ops.modules import Linear as TdsLinear
+
+        out = []
+        for m in module.modules():
+            if isinstance(m, TdsLinear):
+                w, b = m.weight, m.bias
+                if w.requires_grad and w.numel() >= (1 << 20) and w.shape[0] <= 16 and (b is None or b.requires_grad):
+                    out.append(m)
+        return out
+
+    def _make_skip_fn(self, b: _Bucket):
+        def set_skip(flag: bool):
+            b.skip = bool(flag)
+            if self._native is not None:
+                self._native.set_bucket_skip(b.index, bool(flag))
+
+        return set_skip
+
+    @property
+    def exchanges(self):
+        return list(self._exchanges)
+
     def _make_view_fn(self, p):
         o, n = self._slots[id(p)]
         shape = p.shape
@@ -242,6 +305,9 @@ class DistributedDataParallel(nn.Module):
             self._native.prepare_for_backward(bool(self.require_backward_grad_sync))
         else:
             self._reset_bucket_state()
+        sync = bool(self.require_backward_grad_sync) and torch.is_grad_enabled()
+        for ex in self._exchanges:
+            ex.arm(sync)
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
@@ -276,6 +342,8 @@ class DistributedDataParallel(nn.Module):
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
         b = self._bucket_of[id(p)]
+        if b.skip:
+            return
         b.pending -= 1
         if b.pending == 0:
             self._launch(b)
@@ -289,7 +357,7 @@ class DistributedDataParallel(nn.Module):
 
     def _finalize_backward(self):
         for b in self._buckets:
-            if not b.ready:
+            if not b.ready and not b.skip:
                 if not self.find_unused_parameters:
                     missing = [i for i, p in enumerate(b.params) if p.grad is None]
                     raise RuntimeError(
