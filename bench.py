@@ -41,6 +41,8 @@ def main(argv=None):
     ap.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations"],
                     help="fc gradient path under DDP: auto picks the activation exchange when it moves fewer "
                          "bytes per rank than the ring all-reduce (parallel/factored.py)")
+    ap.add_argument("--overlap-optimizer", action=argparse.BooleanOptionalAction, default=True,
+                    help="finish the fc bucket (collective + SGD) on a side stream under the next forward's convs")
     ap.add_argument("--profile-phases", action="store_true", help="also report per-phase GPU times (adds events)")
     args = ap.parse_args(argv)
 
@@ -78,7 +80,7 @@ def main(argv=None):
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), 1e-4)
     ddp = DistributedDataParallel(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_mb,
-                                  grad_exchange=args.grad_exchange)
+                                  grad_exchange=args.grad_exchange, overlap_optimizer=args.overlap_optimizer)
     ddp.attach_optimizer(optimizer)
 
     # a pool of synthetic 28x28 sources; each step upsamples a different slice on device
@@ -142,6 +144,7 @@ def main(argv=None):
                 "mode": args.mode,
                 "backend": args.backend if world > 1 else None,
                 "reducer": ddp.reducer_kind,
+                "overlap_optimizer": ddp.overlap_optimizer,
                 "fc_grad": ("activation-exchange" if any(e.steps_exchanged for e in ddp.exchanges)
                             else "allreduce" if world > 1 else "local"),
                 "optimizer": "SGD(lr=1e-4)",

@@ -163,3 +163,40 @@ def test_activation_exchange_fused_convnet(pg, gpu):
             for p, q in zip(m.parameters(), ref.parameters()):
                 q.copy_(p)
     assert ddp.exchanges[0].steps_exchanged == 2
+
+
+@pytest.mark.parametrize("exchange", ["allreduce", "activations"])
+def test_overlap_optimizer_matches_sequential(pg, gpu, exchange):
+    """overlap_optimizer: the fc bucket's collective + SGD update run on a side stream
+    and the next forward's head waits on a parameter fence; the trajectory must be
+    identical to the sequential step."""
+    import copy
+
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss, param_fence
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    H = 256
+    m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    m2 = copy.deepcopy(m1)
+    d1 = DistributedDataParallel(m1, grad_exchange=exchange, overlap_optimizer=True)
+    d2 = DistributedDataParallel(m2, grad_exchange=exchange)
+    assert d1.overlap_optimizer and len(d1._deferred) == 1
+    o1 = d1.attach_optimizer(SGD(m1.parameters(), 1e-4))
+    o2 = d2.attach_optimizer(SGD(m2.parameters(), 1e-4))
+    crit = CrossEntropyLoss()
+    g = torch.Generator(device=gpu).manual_seed(5)
+    for step in range(4):
+        x = torch.rand(3, 1, H, H, device=gpu, generator=g)
+        y = torch.randint(0, 10, (3,), device=gpu, generator=g)
+        for d, o in ((d1, o1), (d2, o2)):
+            loss = crit(d(x), y)
+            o.zero_grad()
+            loss.backward()
+            o.step()
+        assert param_fence.pending(m1.fc.weight)
+    d1.wait_pending_updates()
+    torch.cuda.synchronize()
+    for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+        assert torch.equal(p, q), n

@@ -72,7 +72,9 @@ class Reducer : public torch::CustomClassHolder {
     pending_ = b_count_;
     b_ready_.assign(b_off_.size(), false);
     b_skip_.assign(b_off_.size(), false);
+    b_defer_.assign(b_off_.size(), false);
     works_.resize(b_off_.size());
+    taken_.resize(b_off_.size());
   }
 
   ~Reducer() override {
@@ -127,6 +129,22 @@ class Reducer : public torch::CustomClassHolder {
     b_skip_[b] = skip;
   }
 
+  // A deferred bucket's collective is NOT waited at the end of backward; DDP takes
+  // the work (take_work) and finishes it on a side stream together with the
+  // optimizer update of that bucket (DistributedDataParallel(overlap_optimizer=True)).
+  void set_bucket_deferred(int64_t b, bool deferred) {
+    TORCH_CHECK(b >= 0 && b < (int64_t)b_defer_.size(), "Reducer.set_bucket_deferred: bad bucket");
+    b_defer_[b] = deferred;
+  }
+
+  c10::optional<c10::intrusive_ptr<CommWork>> take_work(int64_t b) {
+    TORCH_CHECK(b >= 0 && b < (int64_t)taken_.size(), "Reducer.take_work: bad bucket");
+    auto w = taken_[b];
+    taken_[b].reset();
+    if (!w) return c10::nullopt;
+    return w;
+  }
+
   void on_ready(int64_t i) {
     auto& p = params_[i];
     at::Tensor& g = p.mutable_grad();
@@ -169,8 +187,13 @@ class Reducer : public torch::CustomClassHolder {
       }
       launch((int64_t)b);
     }
-    for (auto& w : works_) {
-      if (w) w->wait();  // caller stream waits on the collective (device-side)
+    for (size_t b = 0; b < works_.size(); ++b) {
+      auto& w = works_[b];
+      if (w && b_defer_[b]) {
+        taken_[b] = w;  // finished later on DDP's side stream
+      } else if (w) {
+        w->wait();  // caller stream waits on the collective (device-side)
+      }
       w.reset();
     }
     callback_queued_ = false;
@@ -184,8 +207,8 @@ class Reducer : public torch::CustomClassHolder {
   bool find_unused_;
   std::shared_ptr<std::atomic<Reducer*>> self_;
   std::vector<int64_t> p_off_, p_num_, p_bucket_, b_off_, b_num_, b_count_, pending_, ready_order_;
-  std::vector<bool> b_ready_, b_skip_;
-  std::vector<c10::intrusive_ptr<CommWork>> works_;
+  std::vector<bool> b_ready_, b_skip_, b_defer_;
+  std::vector<c10::intrusive_ptr<CommWork>> works_, taken_;
   std::vector<at::Tensor> params_;
   std::vector<std::shared_ptr<torch::autograd::Node>> accs_;
   std::vector<uintptr_t> keys_;
@@ -222,6 +245,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       .def("prepare_for_backward", &tds_comm::Reducer::prepare_for_backward)
       .def("finalize", &tds_comm::Reducer::finalize)
       .def("set_bucket_skip", &tds_comm::Reducer::set_bucket_skip)
+      .def("set_bucket_deferred", &tds_comm::Reducer::set_bucket_deferred)
+      .def("take_work", &tds_comm::Reducer::take_work)
       .def("ready_order", &tds_comm::Reducer::ready_order)
       .def("num_buckets", &tds_comm::Reducer::num_buckets);
 }

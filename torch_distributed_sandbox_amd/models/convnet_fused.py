@@ -24,7 +24,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
-from ..ops import grad_sink
+from ..ops import grad_sink, param_fence
 from ..parallel import factored
 
 
@@ -122,6 +122,10 @@ def forward(model, x):
     p1 = _Layer1.apply(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
                        bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps))
     y2, partial2 = _Conv2.apply(p1, conv2.weight, conv2.bias)
+    # the fc update may still be running on DDP's side stream (overlap_optimizer): wait here,
+    # after the convolutions were queued, not before
+    param_fence.wait(fc.weight)
+    param_fence.wait(fc.bias)
     ex = factored.get(fc.weight)
     if ex is not None and not ex.ready(x.shape[0]):
         ex = None

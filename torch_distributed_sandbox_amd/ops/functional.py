@@ -198,7 +198,11 @@ class _ExchangedLinear(torch.autograd.Function):
 
 def linear(x, weight, bias=None):
     from ..parallel import factored
+    from . import param_fence
 
+    if x.is_cuda:  # a deferred (side-stream) optimizer update of this layer must land first
+        param_fence.wait(weight)
+        param_fence.wait(bias)
     ex = factored.get(weight)
     if ex is not None and torch.is_grad_enabled() and weight.requires_grad:
         x2 = x.reshape(-1, x.shape[-1]).contiguous()

@@ -21,6 +21,7 @@ class SGD(torch.optim.Optimizer):
         defaults = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay, nesterov=nesterov)
         super().__init__(params, defaults)
         self._flat = None  # (flat_param, flat_grad) when installed by DDP
+        self._deferred = None  # ([(offset, numel)], runner) when DDP overlaps part of the update
 
     def set_flat_buffers(self, flat_param: torch.Tensor, flat_grad: torch.Tensor, params):
         """Declare that ``params`` are views of ``flat_param`` with grads in ``flat_grad``."""
@@ -29,6 +30,11 @@ class SGD(torch.optim.Optimizer):
             self._flat = (flat_param, flat_grad, list(params))
         else:
             self._flat = None
+
+    def set_deferred(self, ranges, runner):
+        """DDP(overlap_optimizer=True): the flat ranges in ``ranges`` are updated by
+        ``runner(update_fn)`` on DDP's side stream; the rest here, on the current stream."""
+        self._deferred = (sorted(ranges), runner) if ranges else None
 
     def _flat_ok(self):
         if self._flat is None:
@@ -53,7 +59,20 @@ class SGD(torch.optim.Optimizer):
             wd, nest = group["weight_decay"], group["nesterov"]
             if (self._flat is not None and mom == 0.0 and wd == 0.0 and self._flat_ok() and self._flat[0].is_cuda):
                 fp, fg, _ = self._flat
-                _ext.ops().sgd_step_([fp], [fg], [], lr, 0.0, 0.0, 0.0, False, False)
+                if self._deferred is None:
+                    _ext.ops().sgd_step_([fp], [fg], [], lr, 0.0, 0.0, 0.0, False, False)
+                    continue
+                ranges, runner = self._deferred
+                ps, gs, pos = [], [], 0
+                for off, n in ranges + [(fp.numel(), 0)]:
+                    if off > pos:
+                        ps.append(fp[pos:off])
+                        gs.append(fg[pos:off])
+                    pos = off + n
+                if ps:
+                    _ext.ops().sgd_step_(ps, gs, [], lr, 0.0, 0.0, 0.0, False, False)
+                runner(lambda off, n, _lr=lr: _ext.ops().sgd_step_([fp[off:off + n]], [fg[off:off + n]], [], _lr,
+                                                                   0.0, 0.0, 0.0, False, False))
                 continue
             params, grads, bufs, first = [], [], [], False
             for p in group["params"]:

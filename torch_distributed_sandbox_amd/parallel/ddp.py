@@ -69,7 +69,7 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  process_group=None, bucket_cap_mb: Optional[float] = None, find_unused_parameters: bool = False,
                  gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False,
-                 reducer: str = "auto", grad_exchange: str = "auto"):
+                 reducer: str = "auto", grad_exchange: str = "auto", overlap_optimizer: bool = False):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -94,8 +94,9 @@ class DistributedDataParallel(nn.Module):
         if grad_exchange not in ("auto", "allreduce", "activations"):
             raise ValueError(f"grad_exchange must be auto|allreduce|activations, got {grad_exchange!r}")
         self.grad_exchange = grad_exchange
-        exch_layers = self._exchange_candidates(module) if grad_exchange != "allreduce" else []
-        layer_of = {id(p): lyr for lyr in exch_layers for p in (lyr.weight, lyr.bias) if p is not None}
+        big_layers = self._exchange_candidates(module)
+        exch_layers = big_layers if grad_exchange != "allreduce" else []
+        layer_of = {id(p): lyr for lyr in big_layers for p in (lyr.weight, lyr.bias) if p is not None}
         order = list(reversed(self._params))
         cap_mb = 25.0 if bucket_cap_mb is None else float(bucket_cap_mb)
         limit = max(1, int(cap_mb * 1024 * 1024 // self._params[0].element_size()))
@@ -171,6 +172,21 @@ class DistributedDataParallel(nn.Module):
                     lyr.weight, lyr.bias, process_group, self.world_size, grad_exchange,
                     self._make_skip_fn(b), self._make_view_fn(lyr.weight),
                     self._make_view_fn(lyr.bias) if lyr.bias is not None else None))
+
+        # ---- overlapped optimizer: the big layers' buckets finish (collective + SGD
+        # update) on a side stream while the next forward's convolutions run
+        self.overlap_optimizer = bool(overlap_optimizer) and dev.type == "cuda" and self.flat_param is not None
+        self._deferred: List[_Bucket] = []
+        self._deferred_works = {}
+        self._side = None
+        if self.overlap_optimizer and big_layers:
+            self._side = torch.cuda.Stream(device=dev)
+            self._deferred = [self._layer_bucket[id(lyr)] for lyr in big_layers]
+            for b in self._deferred:
+                if self._native is not None:
+                    self._native.set_bucket_deferred(b.index, True)
+            for ex in self._exchanges:
+                ex.side_stream = self._side
 
     def _make_native_reducer(self, mode: str):
         if mode not in ("auto", "native", "python"):
@@ -370,9 +386,13 @@ class DistributedDataParallel(nn.Module):
                         v.zero_()
                         p.grad = v
                 self._launch(b)
+        deferred = {id(b) for b in self._deferred}
         for b in self._buckets:
             if b.work is not None:
-                b.work.wait()
+                if id(b) in deferred:
+                    self._deferred_works[b.index] = b.work  # finished on the side stream (optimizer step)
+                else:
+                    b.work.wait()
                 b.work = None
         self._callback_queued = False
 
@@ -383,7 +403,43 @@ class DistributedDataParallel(nn.Module):
                 for b in self._buckets]
 
     def attach_optimizer(self, optimizer):
-        """Let ``ops.optim.SGD`` update the flat buffer in one sweep."""
+        """Let ``ops.optim.SGD`` update the flat buffer in one sweep (and, with
+        ``overlap_optimizer``, hand the deferred buckets' update to the side stream)."""
         if self.flat_param is not None and hasattr(optimizer, "set_flat_buffers"):
             optimizer.set_flat_buffers(self.flat_param, self.flat_grad, self._params)
+            if self._deferred and hasattr(optimizer, "set_deferred"):
+                optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred], self._run_deferred_update)
         return optimizer
+
+    def _run_deferred_update(self, update_fn):
+        """Finish the deferred buckets on the side stream: wait for this step's
+        backward (compute stream) and the bucket collective, apply ``update_fn(offset,
+        numel)`` (the optimizer's flat-slice update), then fence the parameters so
+        their first reader in the next forward waits (ops/param_fence.py)."""
+        from ..ops import param_fence
+
+        cur = torch.cuda.current_stream(self.device)
+        side = self._side
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            for b in self._deferred:
+                w = self._deferred_works.pop(b.index, None)
+                if w is None and self._native is not None:
+                    w = self._native.take_work(b.index)
+                if w is not None:
+                    w.wait()  # side stream waits for the bucket all-reduce
+                update_fn(b.offset, b.numel)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for b in self._deferred:
+            for p in b.params:
+                param_fence.set(p, ev)
+
+    def wait_pending_updates(self):
+        """Order the current stream after any deferred parameter update (call before
+        reading the parameters outside the model's forward, e.g. checkpointing)."""
+        from ..ops import param_fence
+
+        for b in self._deferred:
+            for p in b.params:
+                param_fence.wait(p)

@@ -60,6 +60,7 @@ class ActivationExchange:
         self.active = False
         self.steps_exchanged = 0
         self._x_all = self._x_work = self._dy = None
+        self.side_stream = None  # set by DDP(overlap_optimizer=True): dW is formed off the compute stream
         setattr(weight, _ATTR, self)
 
     def detach(self):
@@ -109,6 +110,20 @@ class ActivationExchange:
         torch.autograd.Variable._execution_engine.queue_callback(self.finalize)
 
     def finalize(self):
+        side = self.side_stream if (self.side_stream is not None and self._dy.is_cuda) else None
+        if side is None:
+            self._finish()
+            return
+        # the dy gather queues behind the big x gather on the comm stream: issue both
+        # waits and the dW GEMM from the side stream so the compute stream runs on
+        cur = torch.cuda.current_stream(self._dy.device)
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._finish()
+            for t in (self._dy, self._x_all, self._x_local):
+                t.record_stream(side)
+
+    def _finish(self):
         from .. import _ext
         from . import distributed as tdist
 

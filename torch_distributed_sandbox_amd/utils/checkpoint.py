@@ -17,6 +17,8 @@ def _unwrap(model):
 
 
 def save(path: str, model, optimizer=None, step: int = 0, epoch: int = 0, rank: int = 0, extra=None) -> None:
+    if hasattr(model, "wait_pending_updates"):
+        model.wait_pending_updates()  # DDP(overlap_optimizer=True) side-stream updates land first
     if rank != 0:
         return
     state = {
