@@ -118,10 +118,11 @@ class ActivationExchange:
         # waits and the dW GEMM from the side stream so the compute stream runs on
         cur = torch.cuda.current_stream(self._dy.device)
         side.wait_stream(cur)
+        keep = (self._dy, self._x_all, self._x_local)  # used on the side stream
         with torch.cuda.stream(side):
-            self._finish()
-            for t in (self._dy, self._x_all, self._x_local):
+            for t in keep:
                 t.record_stream(side)
+            self._finish()
 
     def _finish(self):
         from .. import _ext
