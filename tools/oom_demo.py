@@ -1,0 +1,121 @@
+"""The reference's "OOM workaround" story (README.md:9-15),
+re-sized for 288 GB of HBM3E per MI355X.
+
+The reference: at 3000x3000 a per-GPU batch of 10 does not fit one 24 GB A5000,
+a batch of 5 does, so DDP with 5 per rank x N ranks gives an effective batch
+of 5N.  Our fused ConvNet plan needs far less memory per image (no y1, no p2,
+1-byte argmax, NHWC bf16 hi|lo activations), so the edge where batch 10 stops
+fitting 288 GB is much larger.  This script:
+
+1. prints the memory model of the fused plan and the predicted OOM edge,
+2. tries ONE training step at batch 10 on this GPU at --image-size and reports
+   the out-of-memory error (expected),
+3. runs --steps steps at batch 5 on the same image size (fits) and reports
+   peak memory and images/sec,
+4. under torchrun with N ranks: step 3 is the DDP run, effective batch 5N.
+
+    python tools/oom_demo.py --image-size 18000
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/oom_demo.py --image-size 18000
+"""
+import argparse
+import gc
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+# bytes per input pixel per image in the fused plan (x 4, p1 16, idx1 4, y2 32, dy2 32,
+# dp1 16, g2m 8, upsample/out 4) measured as 96 B/px at 3000^2 (peak 5.77 GB at B=5
+# incl. 1.44 GB of fc weight + gradient); fc weight+grad = 2 * 10 * 32 * (H/4)^2 * 4 B
+ACT_BYTES_PER_PX = 96.0
+FC_BYTES_PER_PX = 160.0 / 1.0  # weight + gradient, per input pixel of ONE image edge^2
+
+
+def predicted_bytes(H, B):
+    return B * ACT_BYTES_PER_PX * H * H + FC_BYTES_PER_PX * H * H
+
+
+def run(H, B, steps, device, world, rank):
+    from torch_distributed_sandbox_amd.data import synthetic_batch
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
+    from torch_distributed_sandbox_amd.ops import functional as TF
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.cuda.reset_peak_memory_stats(device)
+    torch.manual_seed(0)
+    model = ConvNet(image_shape=(H, H), device=device)
+    opt = SGD(model.parameters(), 1e-4)
+    ddp = DistributedDataParallel(model, device_ids=[device.index])
+    ddp.attach_optimizer(opt)
+    crit = CrossEntropyLoss()
+    src, lab = synthetic_batch(B, (H, H), device, seed=7 + rank)
+    t0 = None
+    for i in range(steps):
+        images = TF.upsample_bilinear_u8(src, H, H)
+        loss = crit(ddp(images), lab)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        if i == 0:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / max(1, steps - 1) if steps > 1 else None
+    peak = torch.cuda.max_memory_allocated(device)
+    del ddp, model, opt, images, loss
+    gc.collect()
+    torch.cuda.empty_cache()
+    return {"batch_per_rank": B, "peak_gb": round(peak / 1e9, 2),
+            "ms_per_step": round(dt * 1e3, 2) if dt else None,
+            "images_per_sec_node": round(world * B / dt, 2) if dt else None}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--image-size", type=int, default=18000)
+    ap.add_argument("--bs-fail", type=int, default=10)
+    ap.add_argument("--bs-fit", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=3)
+    args = ap.parse_args()
+    from torch_distributed_sandbox_amd.parallel import distributed as tdist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        tdist.init_process_group("rccl", rank=rank, world_size=world, device_id=local)
+    H = args.image_size
+    total = torch.cuda.get_device_properties(device).total_memory
+    rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1), "world_size": world,
+           "model": {"act_bytes_per_px_per_image": ACT_BYTES_PER_PX, "fc_bytes_per_px": FC_BYTES_PER_PX,
+                     "predicted_gb": {str(b): round(predicted_bytes(H, b) / 1e9, 1)
+                                      for b in (args.bs_fit, args.bs_fail)},
+                     "predicted_oom_edge_bs%d" % args.bs_fail:
+                         int((total / (args.bs_fail * ACT_BYTES_PER_PX + FC_BYTES_PER_PX)) ** 0.5)}}
+    # 1) batch 10 on one GPU (every rank tries it alone: no collective inside)
+    try:
+        r = run(H, args.bs_fail, 1, device, 1, rank) if world == 1 else None
+        rec["bs_fail_result"] = {"oom": False, **(r or {})}
+    except torch.cuda.OutOfMemoryError as e:
+        msg = str(e).split("\n")[0]
+        rec["bs_fail_result"] = {"oom": True, "error": msg[:300]}
+    gc.collect()
+    torch.cuda.empty_cache()
+    # 2) batch 5 per rank (DDP over all ranks when launched with torchrun)
+    rec["bs_fit_result"] = run(H, args.bs_fit, args.steps, device, world, rank)
+    rec["effective_batch"] = args.bs_fit * world
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -46,7 +46,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, "fused_l1_forward: x must be [B,1,H,W]");
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
   TORCH_CHECK(H == W && H >= 8, "fused_l1_forward: square images with H >= 8");
-  TORCH_CHECK(B >= 1 && B <= 8, "fused_l1_forward: 1 <= B <= 8 per rank");
+  TORCH_CHECK(B >= 1 && B <= 32, "fused_l1_forward: 1 <= B <= 32 per rank");
   need(w1, at::kFloat, {16, 1, 5, 5}, "conv1.weight");
   need(b1, at::kFloat, {16}, "conv1.bias");
   const float* g = optf(gamma1, 16, "bn1.weight");
@@ -63,8 +63,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   const int64_t P = H / 2;
   auto fo = x.options();
   // x autocorrelation + border strips -> Gram G / patch sums S -> BN1 statistics in closed form
-  const int nac = ac_wg();
-  auto ac = at::empty({nac * 42}, fo.dtype(at::kDouble));
+  // enough workgroups that each thread's fp32 partial covers <= ~32 products (fp64 beyond)
+  const int64_t ac_tiles = B * ((H + 15) / 16) * ((W + 63) / 64);
+  const int nac = (int)std::max<int64_t>(ac_wg(), (ac_tiles + 7) / 8);
+  auto ac = at::empty({(int64_t)nac * 42}, fo.dtype(at::kDouble));
   auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
   tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
                  st);

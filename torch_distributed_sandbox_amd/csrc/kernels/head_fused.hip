@@ -16,6 +16,7 @@
 namespace tds {
 
 constexpr int HD_PX = 64;
+constexpr int HD_MAXB = 32;  // images per rank (per-image partial sums live in LDS)
 constexpr int HD_REC = 144;  // padded LDS record stride (bytes): 128 B of y2 + 16 B
 constexpr int HD_LDS = 2 * 2 * HD_PX * HD_REC;
 
@@ -87,7 +88,7 @@ __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(const float4* __restr
   constexpr int CPW = 32 / NW;
   using Tile = HeadTile<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float red[NW][8 * 10];
+  __shared__ float red[NW][HD_MAXB * 10];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const Tile tile{y2, P, Q, (int)blockIdx.y, (int)blockIdx.x * HD_PX};
   const int px = tile.px0 + lane;
@@ -156,15 +157,15 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restr
   constexpr int CPW = 32 / NW;
   using Tile = HeadTile<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float dls[8 * 10];
+  __shared__ float dls[HD_MAXB * 10];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const Tile tile{y2, P, Q, (int)blockIdx.y, (int)blockIdx.x * HD_PX};
   const int px = tile.px0 + lane;
   const bool valid = px < Q;
   const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)tile.py * Q + px;
-  if (threadIdx.x < 80) {
-    const int b = threadIdx.x / 10, j = threadIdx.x % 10;
-    dls[threadIdx.x] = (b < B && j < NC) ? dl[b * NC + j] : 0.f;
+  for (int i = threadIdx.x; i < HD_MAXB * 10; i += blockDim.x) {
+    const int b = i / 10, j = i % 10;
+    dls[i] = (b < B && j < NC) ? dl[b * NC + j] : 0.f;
   }
   float w[10][CPW], dwa[10][CPW], a[CPW], bb[CPW], sdz[CPW], sdy[CPW];
 #pragma unroll
@@ -254,7 +255,7 @@ int tds_head_fwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
                  float* logits, float* xout, int B, int P, int NC, hipStream_t st) {
   const int Q = P / 2;
-  if (B > 8 || NC > 10 || Q < 1) return -1;
+  if (B > HD_MAXB || NC > 10 || Q < 1) return -1;
   head_lds_limits();
   const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
   hipLaunchKernelGGL(head_fwd_kernel<HD_FWD_NW>, grid, dim3(64 * HD_FWD_NW), HD_LDS, st,
@@ -269,7 +270,7 @@ int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const flo
 int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
                  double* partial, int B, int P, int NC, float scale, hipStream_t st) {
   const int Q = P / 2;
-  if (B > 8 || NC > 10 || Q < 1) return -1;
+  if (B > HD_MAXB || NC > 10 || Q < 1) return -1;
   head_lds_limits();
   const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
   // dW == nullptr: the fc weight gradient is formed elsewhere (activation exchange)

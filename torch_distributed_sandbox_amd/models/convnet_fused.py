@@ -34,7 +34,7 @@ def supported(model, x) -> bool:
     if x.dim() != 4 or x.shape[1] != 1 or x.dtype != torch.float32:
         return False
     B, _, H, W = x.shape
-    if H != W or H < 8 or B > 8 or H % 4 != 0:
+    if H != W or H < 8 or B > 32 or H % 4 != 0:
         return False
     bn1, bn2 = model.layer1[1], model.layer2[1]
     for bn in (bn1, bn2):

@@ -42,6 +42,11 @@ def add_common_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--checkpoint", default="", help="save a checkpoint here at the end (rank 0)")
     p.add_argument("--resume", default="", help="resume from this checkpoint")
     p.add_argument("--json", action="store_true", help="print a JSON summary line at the end")
+    p.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations"],
+                   help="DDP gradient path of the big fc layer (parallel/factored.py)")
+    p.add_argument("--overlap-optimizer", action=argparse.BooleanOptionalAction, default=True,
+                   help="finish the fc bucket (collective + SGD) on a side stream under the next forward")
+    p.add_argument("--bucket-mb", default=None, type=float, help="DDP bucket cap (MB, default 25 like torch)")
     return p
 
 
@@ -75,7 +80,10 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), args.lr)
     if distributed:
-        model = DistributedDataParallel(model, device_ids=[gpu] if device.type == "cuda" else None)
+        model = DistributedDataParallel(model, device_ids=[gpu] if device.type == "cuda" else None,
+                                        bucket_cap_mb=getattr(args, "bucket_mb", None),
+                                        grad_exchange=getattr(args, "grad_exchange", "auto"),
+                                        overlap_optimizer=getattr(args, "overlap_optimizer", True))
         model.attach_optimizer(optimizer)
     start_epoch = 0
     if args.resume:
