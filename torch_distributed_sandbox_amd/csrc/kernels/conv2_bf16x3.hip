@@ -38,7 +38,9 @@ constexpr int C2_IC = C2_TC + 4;
 constexpr int C2_THREADS = 512;
 
 // ---------------------------------------------------------------------------- weight packing
-// fwd : wp[hl][s<13][nt<2][g<4][co16][j8], k = 32s+8g+j -> tap = 2s+(g>>1), ci = 8(g&1)+j  (tap 25 = 0)
+// fwd : wp[hl][s<13][nt<2][g<4][co16][j8], k = 32s+8g+j, ci = 8(g&1)+j, taps paired so that one
+//       input-row A fragment serves every output row:  s < 10: (ky = s>>1, kx = 2(s&1) + (g>>1));
+//       s = 10 + kp: (ky = 2kp + (g>>1), kx = 4)  (ky = 5 -> zero)
 // dgrad: wd[hl][s<25][g<4][ci16][j8],      k = 32s+8g+j -> tap' = s, co = 8g+j; w = w2[co][ci][24-tap']
 __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* __restrict__ wp,
                                           short* __restrict__ wd) {
@@ -47,8 +49,10 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < FW + DW; e += gridDim.x * blockDim.x) {
     if (e < FW) {
       const int j = e & 7, co_in = (e >> 3) & 15, g = (e >> 7) & 3, nt = (e >> 9) & 1, s = e >> 10;
-      const int tap = 2 * s + (g >> 1), ci = 8 * (g & 1) + j, co = nt * 16 + co_in;
-      const float v = tap < 25 ? w2[(co * 16 + ci) * 25 + tap] : 0.f;
+      const int ky = s < 10 ? (s >> 1) : 2 * (s - 10) + (g >> 1);
+      const int kx = s < 10 ? 2 * (s & 1) + (g >> 1) : 4;
+      const int ci = 8 * (g & 1) + j, co = nt * 16 + co_in;
+      const float v = ky < 5 ? w2[(co * 16 + ci) * 25 + ky * 5 + kx] : 0.f;
       unsigned short hi, lo;
       split_bf16(v, hi, lo);
       wp[e] = (short)hi;
@@ -83,12 +87,21 @@ struct TileIter {
 };
 
 // ---------------------------------------------------------------------------- forward
-// LDS: weights (2 x 13 x 2 x 1 KiB = 53248 B) + input planes (2 x 12 x 36 x 32 B = 27648 B)
+// Tile: 8 output rows x 64 output cols.  Wave w owns output rows 4*(w>>2) .. +3 and columns
+// 16*(w&3) .. +15 (four M tiles stacked vertically), N = 32 output channels (two N tiles).
+// K steps pair taps so that an input row's A fragment serves every output row it reaches:
+//   (ky, kx in {2a, 2a+1}) for a = 0, 1  -> A = input row R, output row o = R - ky
+//   (ky in {2kp, 2kp+1}, kx = 4)         -> A = input rows R (lane groups 0-1) and R+1 (2-3),
+//                                           output row o = R - 2kp
+// Per wave-tile: 100 ds_read_b128 for 104 MFMA triples (the row-per-wave layout needed 208).
+// LDS: weights (2 x 13 x 2 x 1 KiB) + p1 planes (2 x 12 x 68 x 32 B).
+constexpr int FW_TH = 8, FW_TC = 64;
+constexpr int FW_IR = FW_TH + 4, FW_IC = FW_TC + 4;
 constexpr int F_WBYTES = 2 * 13 * 2 * 1024;
-constexpr int F_PLANE = C2_IR * C2_IC * 32;
-constexpr int F_LDS = F_WBYTES + 2 * F_PLANE;
-constexpr int F_CHUNKS = C2_IR * C2_IC * 4;  // 16-byte chunks per staged tile
-constexpr int F_PER_THREAD = (F_CHUNKS + C2_THREADS - 1) / C2_THREADS;
+constexpr int F_PLANE = FW_IR * FW_IC * 32;                              // 26112 B
+constexpr int F_LDS = F_WBYTES + 2 * F_PLANE;                            // 105472 B
+constexpr int F_CHUNKS = FW_IR * FW_IC * 4;                               // 16-byte chunks per staged tile
+constexpr int F_PER_THREAD = (F_CHUNKS + C2_THREADS - 1) / C2_THREADS;   // 7
 
 __global__ __launch_bounds__(C2_THREADS) void conv2_fwd_bf16x3_kernel(const uint4* __restrict__ p1,
                                                                       const uint4* __restrict__ wpack,
@@ -100,7 +113,9 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_fwd_bf16x3_kernel(const uint
   char* in_l = smem + F_WBYTES;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
-  const TileIter it(B, P);
+  const int rg = wv >> 2, cg = wv & 3;
+  const int tiles_c = (P + FW_TC - 1) / FW_TC, tiles_r = (P + FW_TH - 1) / FW_TH;
+  const int per_img = tiles_c * tiles_r, total = per_img * B;
   const int vid = xcd_remap(blockIdx.x, gridDim.x);
 
   // weights -> LDS once (persistent workgroup)
@@ -111,17 +126,23 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_fwd_bf16x3_kernel(const uint
   bco[1] = bias[16 + li];
   float s_acc[2] = {0.f, 0.f}, q_acc[2] = {0.f, 0.f};
 
+  auto decode = [&](int t, int& b, int& r0, int& c0) {
+    b = t / per_img;
+    const int rem = t - b * per_img;
+    r0 = (rem / tiles_c) * FW_TH;
+    c0 = (rem % tiles_c) * FW_TC;
+  };
   uint4 pre[F_PER_THREAD];
   auto load_tile = [&](int t) {
     int b, r0, c0;
-    it.decode(t, b, r0, c0);
+    decode(t, b, r0, c0);
 #pragma unroll
     for (int u = 0; u < F_PER_THREAD; ++u) {
       const int e = tid + u * C2_THREADS;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (e < F_CHUNKS) {
         const int px = e >> 2, q = e & 3;
-        const int rr = px / C2_IC, cc = px - rr * C2_IC;
+        const int rr = px / FW_IC, cc = px - rr * FW_IC;
         const int gr = r0 - 2 + rr, gc = c0 - 2 + cc;
         if (gr >= 0 && gr < P && gc >= 0 && gc < P)
           v = p1[(((int64_t)b * P + gr) * P + gc) * 4 + q];
@@ -139,73 +160,112 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_fwd_bf16x3_kernel(const uint
       }
     }
   };
+  auto ldb = [&](int s, int n, int hl) -> s16x8 {
+    return *reinterpret_cast<const s16x8*>(w_l + hl * 13 * 2 * 1024 + ((s * 2 + n) * 64 + lane) * 16);
+  };
 
+  const int boff = (g & 1) * 16;  // ci half of the 32-B record
   int t = vid;
-  if (t < it.total) load_tile(t);
-  for (; t < it.total; t += gridDim.x) {
+  if (t < total) load_tile(t);
+  for (; t < total; t += gridDim.x) {
     __syncthreads();  // previous tile's readers are done
     store_tile();
     __syncthreads();
     int b, r0, c0;
-    it.decode(t, b, r0, c0);
-    if (t + (int)gridDim.x < it.total) load_tile(t + gridDim.x);  // prefetch next tile into registers
+    decode(t, b, r0, c0);
+    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);  // prefetch next tile into registers
 
-    f32x4 acc[2][2];
+    f32x4 acc[4][2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int o = 0; o < 4; ++o) acc[o][0] = acc[o][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    s16x8 ah[2], al[2];
+    // ---- kx pairs (0,1) and (2,3): A = input row R at column offset 2a + (g>>1)
 #pragma unroll
-      for (int n = 0; n < 2; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-    // operands of k-step s+1 are read from LDS while the MFMAs of step s run
-    s16x8 ahi[2][2], alo[2][2], bhi[2][2], blo[2][2];  // [buffer][m | n]
-    auto load_ops = [&](int s, int buf) {
-      int tap = 2 * s + (g >> 1);
-      if (tap > 24) tap = 0;  // zero-weight padding tap: any valid address
-      const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-      const int rec = (wv + ky) * C2_IC + kx + li;
-      const int boff = (g & 1) * 16;
+    for (int a = 0; a < 2; ++a) {
+      s16x8 bh[5][2], bl[5][2];
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        ahi[buf][m] = *reinterpret_cast<const s16x8*>(in_l + (rec + 16 * m) * 32 + boff);
-        alo[buf][m] = *reinterpret_cast<const s16x8*>(in_l + F_PLANE + (rec + 16 * m) * 32 + boff);
+      for (int ky = 0; ky < 5; ++ky)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          bh[ky][n] = ldb(2 * ky + a, n, 0);
+          bl[ky][n] = ldb(2 * ky + a, n, 1);
+        }
+      auto load_a = [&](int R, int buf) {
+        const int rec = (4 * rg + R) * FW_IC + 16 * cg + li + 2 * a + (g >> 1);
+        ah[buf] = *reinterpret_cast<const s16x8*>(in_l + rec * 32 + boff);
+        al[buf] = *reinterpret_cast<const s16x8*>(in_l + F_PLANE + rec * 32 + boff);
+      };
+      load_a(0, 0);
+#pragma unroll
+      for (int R = 0; R < 8; ++R) {
+        const int cur = R & 1;
+        if (R + 1 < 8) load_a(R + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ky = 0; ky < 5; ++ky) {
+          const int o = R - ky;
+          if (o >= 0 && o < 4) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+              acc[o][n] = mfma_bf16x3(ah[cur], al[cur], bh[ky][n], bl[ky][n], acc[o][n]);
+          }
+        }
       }
-#pragma unroll
-      for (int n = 0; n < 2; ++n) {
-        bhi[buf][n] = *reinterpret_cast<const s16x8*>(w_l + ((s * 2 + n) * 64 + lane) * 16);
-        blo[buf][n] = *reinterpret_cast<const s16x8*>(w_l + 13 * 2 * 1024 + ((s * 2 + n) * 64 + lane) * 16);
-      }
-    };
-    load_ops(0, 0);
-#pragma unroll
-    for (int s = 0; s < 13; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < 13) load_ops(s + 1, cur ^ 1);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[m][n] = mfma_bf16x3(ahi[cur][m], alo[cur][m], bhi[cur][n], blo[cur][n], acc[m][n]);
     }
-    // epilogue: lane holds co = 16n + li, pixels col = c0 + 16m + 4g + r of row r0 + wv
-    const int row = r0 + wv;
-    if (row < P) {
-      float* yrow = y2 + ((int64_t)b * P + row) * P * 32;
+    // ---- column kx = 4, ky pairs (2kp, 2kp+1): lane groups 2-3 read input row R+1
+    {
+      s16x8 bh[3][2], bl[3][2];
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+      for (int kp = 0; kp < 3; ++kp)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) {
+          bh[kp][n] = ldb(10 + kp, n, 0);
+          bl[kp][n] = ldb(10 + kp, n, 1);
+        }
+      auto load_a = [&](int R, int buf) {
+        int row = 4 * rg + R + (g >> 1);
+        if (row > FW_IR - 1) row = FW_IR - 1;  // only reached with a zero weight (ky = 5): any staged row
+        const int rec = row * FW_IC + 16 * cg + li + 4;
+        ah[buf] = *reinterpret_cast<const s16x8*>(in_l + rec * 32 + boff);
+        al[buf] = *reinterpret_cast<const s16x8*>(in_l + F_PLANE + rec * 32 + boff);
+      };
+      load_a(0, 0);
+#pragma unroll
+      for (int R = 0; R < 8; ++R) {
+        const int cur = R & 1;
+        if (R + 1 < 8) load_a(R + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kp = 0; kp < 3; ++kp) {
+          const int o = R - 2 * kp;
+          if (o >= 0 && o < 4) {
+#pragma unroll
+            for (int n = 0; n < 2; ++n)
+              acc[o][n] = mfma_bf16x3(ah[cur], al[cur], bh[kp][n], bl[kp][n], acc[o][n]);
+          }
+        }
+      }
+    }
+    // epilogue: lane holds co = 16n + li for pixels col = c0 + 16cg + 4g + r of row 4rg + o
+#pragma unroll
+    for (int o = 0; o < 4; ++o) {
+      const int row = r0 + 4 * rg + o;
+      if (row < P) {
+        float* yrow = y2 + ((int64_t)b * P + row) * P * 32;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int col = c0 + 16 * m + 4 * g + r;
+          const int col = c0 + 16 * cg + 4 * g + r;
           if (col < P) {
 #pragma unroll
             for (int n = 0; n < 2; ++n) {
-              const float v = acc[m][n][r];  // y2 - b2: statistics shifted by the bias
+              const float v = acc[o][n][r];  // y2 - b2: statistics shifted by the bias
               yrow[(int64_t)col * 32 + 16 * n + li] = v + bco[n];
               s_acc[n] += v;
               q_acc[n] += v * v;
             }
           }
         }
+      }
     }
   }
   // BN2 batch-stat partials: reduce the 4 lane groups, then the 8 waves
@@ -235,12 +295,19 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_fwd_bf16x3_kernel(const uint
 }
 
 // ---------------------------------------------------------------------------- data gradient
-// LDS: weights (2 x 25 x 1 KiB = 51200 B) + dy2 planes (4 x 12 x 36 x 32 B = 55296 B)
+// Tile: 8 output rows x 64 output cols.  Wave w owns output rows 4*(w>>2) .. +3 and
+// columns 16*(w&3) .. +15: four 16-pixel M tiles stacked vertically, N = 16 input channels,
+// K = (flipped tap, 32 output channels).  An input row R of the wave's 8-row window serves
+// every output row it reaches (o = R - ky), so per kx the 5 weight fragments (ky = 0..4)
+// stay in registers and each input row's A fragment is read from LDS once:
+// 26 ds_read_b128 per 20 MFMA triples (the row-per-wave layout needed 60).
+constexpr int DG_TH = 8, DG_TC = 64;
+constexpr int DG_IR = DG_TH + 4, DG_IC = DG_TC + 4;
 constexpr int D_WBYTES = 2 * 25 * 1024;
-constexpr int D_PLANE = C2_IR * C2_IC * 32;
-constexpr int D_LDS = D_WBYTES + 4 * D_PLANE;
-constexpr int D_CHUNKS = C2_IR * C2_IC * 8;
-constexpr int D_PER_THREAD = (D_CHUNKS + C2_THREADS - 1) / C2_THREADS;
+constexpr int D_PLANE = DG_IR * DG_IC * 32;                            // 26112 B
+constexpr int D_LDS = D_WBYTES + 4 * D_PLANE;                          // 155648 B (< 160 KiB)
+constexpr int D_CHUNKS = DG_IR * DG_IC * 8;                             // 16-B chunks per staged tile
+constexpr int D_PER_THREAD = (D_CHUNKS + C2_THREADS - 1) / C2_THREADS;  // 13
 
 __global__ __launch_bounds__(C2_THREADS) void conv2_dgrad_bf16x3_kernel(const uint4* __restrict__ dy2,
                                                                         const uint4* __restrict__ wdpack,
@@ -250,21 +317,29 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_dgrad_bf16x3_kernel(const ui
   char* in_l = smem + D_WBYTES;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
-  const TileIter it(B, P);
+  const int rg = wv >> 2, cg = wv & 3;
+  const int tiles_c = (P + DG_TC - 1) / DG_TC, tiles_r = (P + DG_TH - 1) / DG_TH;
+  const int per_img = tiles_c * tiles_r, total = per_img * B;
   const int vid = xcd_remap(blockIdx.x, gridDim.x);
   for (int e = tid; e < D_WBYTES / 16; e += C2_THREADS) reinterpret_cast<uint4*>(w_l)[e] = wdpack[e];
 
+  auto decode = [&](int t, int& b, int& r0, int& c0) {
+    b = t / per_img;
+    const int rem = t - b * per_img;
+    r0 = (rem / tiles_c) * DG_TH;
+    c0 = (rem % tiles_c) * DG_TC;
+  };
   uint4 pre[D_PER_THREAD];
   auto load_tile = [&](int t) {
     int b, r0, c0;
-    it.decode(t, b, r0, c0);
+    decode(t, b, r0, c0);
 #pragma unroll
     for (int u = 0; u < D_PER_THREAD; ++u) {
       const int e = tid + u * C2_THREADS;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (e < D_CHUNKS) {
         const int px = e >> 3, q = e & 7;
-        const int rr = px / C2_IC, cc = px - rr * C2_IC;
+        const int rr = px / DG_IC, cc = px - rr * DG_IC;
         const int gr = r0 - 2 + rr, gc = c0 - 2 + cc;
         if (gr >= 0 && gr < P && gc >= 0 && gc < P)
           v = dy2[(((int64_t)b * P + gr) * P + gc) * 8 + q];
@@ -284,53 +359,62 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_dgrad_bf16x3_kernel(const ui
     }
   };
 
+  // lane group g -> output channels 8g..8g+7: plane g>>1 (+16 B if g odd), hi planes 0-1, lo 2-3
+  const int hp = (g >> 1) * D_PLANE + (g & 1) * 16;
+  const int lp = (2 + (g >> 1)) * D_PLANE + (g & 1) * 16;
   int t = vid;
-  if (t < it.total) load_tile(t);
-  for (; t < it.total; t += gridDim.x) {
+  if (t < total) load_tile(t);
+  for (; t < total; t += gridDim.x) {
     __syncthreads();
     store_tile();
     __syncthreads();
     int b, r0, c0;
-    it.decode(t, b, r0, c0);
-    if (t + (int)gridDim.x < it.total) load_tile(t + gridDim.x);
+    decode(t, b, r0, c0);
+    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
 
-    f32x4 acc[2];
-    acc[0] = f32x4{0.f, 0.f, 0.f, 0.f};
-    acc[1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // k-step s = flipped tap t' (ky', kx'); lane group g -> co 8g..8g+7 (plane g>>1, +16 B if g odd)
-    const int hp = (g >> 1) * D_PLANE + (g & 1) * 16;
-    const int lp = (2 + (g >> 1)) * D_PLANE + (g & 1) * 16;
-    s16x8 ahi[2][2], alo[2][2], bhi[2], blo[2];  // [buffer][m], [buffer]
-    auto load_ops = [&](int s, int buf) {
-      const int ky = s / 5, kx = s % 5;
-      const int rec = (wv + ky) * C2_IC + kx + li;
+    f32x4 acc[4];
 #pragma unroll
-      for (int m = 0; m < 2; ++m) {
-        ahi[buf][m] = *reinterpret_cast<const s16x8*>(in_l + hp + (rec + 16 * m) * 32);
-        alo[buf][m] = *reinterpret_cast<const s16x8*>(in_l + lp + (rec + 16 * m) * 32);
+    for (int o = 0; o < 4; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kx = 0; kx < 5; ++kx) {
+      s16x8 bh[5], bl[5];
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky) {
+        const int s = ky * 5 + kx;
+        bh[ky] = *reinterpret_cast<const s16x8*>(w_l + (s * 64 + lane) * 16);
+        bl[ky] = *reinterpret_cast<const s16x8*>(w_l + 25 * 1024 + (s * 64 + lane) * 16);
       }
-      bhi[buf] = *reinterpret_cast<const s16x8*>(w_l + (s * 64 + lane) * 16);
-      blo[buf] = *reinterpret_cast<const s16x8*>(w_l + 25 * 1024 + (s * 64 + lane) * 16);
-    };
-    load_ops(0, 0);
+      s16x8 ah[2], al[2];
+      auto load_a = [&](int R, int buf) {
+        const int rec = (4 * rg + R) * DG_IC + 16 * cg + kx + li;
+        ah[buf] = *reinterpret_cast<const s16x8*>(in_l + hp + rec * 32);
+        al[buf] = *reinterpret_cast<const s16x8*>(in_l + lp + rec * 32);
+      };
+      load_a(0, 0);
 #pragma unroll
-    for (int s = 0; s < 25; ++s) {
-      const int cur = s & 1;
-      if (s + 1 < 25) load_ops(s + 1, cur ^ 1);
-      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of this step's MFMAs
+      for (int R = 0; R < 8; ++R) {
+        const int cur = R & 1;
+        if (R + 1 < 8) load_a(R + 1, cur ^ 1);
+        __builtin_amdgcn_sched_barrier(0);  // next input row's reads ahead of this row's MFMAs
 #pragma unroll
-      for (int m = 0; m < 2; ++m) acc[m] = mfma_bf16x3(ahi[cur][m], alo[cur][m], bhi[cur], blo[cur], acc[m]);
+        for (int ky = 0; ky < 5; ++ky) {
+          const int o = R - ky;
+          if (o >= 0 && o < 4) acc[o] = mfma_bf16x3(ah[cur], al[cur], bh[ky], bl[ky], acc[o]);
+        }
+      }
     }
-    const int row = r0 + wv;
-    if (row < P) {
-      float* orow = dp1 + ((int64_t)b * P + row) * P * 16;
+    // lane holds C[px = 4g + r][ci = li] of output row 4rg + o
 #pragma unroll
-      for (int m = 0; m < 2; ++m)
+    for (int o = 0; o < 4; ++o) {
+      const int row = r0 + 4 * rg + o;
+      if (row < P) {
+        float* orow = dp1 + ((int64_t)b * P + row) * P * 16;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int col = c0 + 16 * m + 4 * g + r;
-          if (col < P) orow[(int64_t)col * 16 + li] = acc[m][r];
+          const int col = c0 + 16 * cg + 4 * g + r;
+          if (col < P) orow[(int64_t)col * 16 + li] = acc[o][r];
         }
+      }
     }
   }
 }
