@@ -304,12 +304,12 @@ def _w_exchange_policy(rank, world, port):
     lin = Linear(1 << 17, 10)
     d = DistributedDataParallel(lin)
     ex = d.exchanges[0]
-    # bytes per rank: exchange (W-1)*B*in vs ring all-reduce 2(W-1)/W*in*out  ->  B*W < 2*out
-    assert ex.worthwhile(4) == (4 * world < 20)
+    # bytes per rank: exchange (W-1)*B*in vs ring all-reduce 2(W-1)/W*in*out  ->  B*W <= 2*out
+    assert ex.worthwhile(5) == (5 * world <= 20)
     assert ex.worthwhile(16) is False
-    x = torch.randn(3, 1 << 17)
+    x = torch.randn(6, 1 << 17)
     d(x).sum().backward()
-    assert ex.steps_exchanged == (1 if 3 * world < 20 else 0)
+    assert ex.steps_exchanged == (1 if 6 * world <= 20 else 0)
     dist.destroy_process_group()
 
 

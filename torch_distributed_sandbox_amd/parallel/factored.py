@@ -15,8 +15,9 @@ moves ``(W-1) × B × in × 4`` bytes per rank instead — 360 MB instead of 720
 at W = 2 — and the exchange can start as soon as the FORWARD has produced
 ``X_r``, so it overlaps the entire backward instead of only the part after the
 fc gradient exists.  Per rank the bytes favour the exchange when
-``B·W < 2·out_features`` (W = 2, 3 for the ConvNet: B = 5, 10 classes); at
-larger W the ring all-reduce is cheaper and is used.
+``B·W ≤ 2·out_features`` (W = 2, 3, 4 for the ConvNet: B = 5, 10 classes; at
+equal bytes the exchange still wins because it starts a whole backward earlier);
+at larger W the ring all-reduce is cheaper and is used.
 
 The result is the same average DDP produces (floating-point summation order
 differs, as it does between all-reduce algorithms), identical on every rank.
@@ -72,7 +73,8 @@ class ActivationExchange:
         if self.mode == "activations":
             return True
         out_f = self.weight.shape[0]
-        return self.world > 1 and rows * self.world < 2 * out_f
+        # equal bytes (B*W == 2*out) still favour the exchange: it starts a whole backward earlier
+        return self.world > 1 and rows * self.world <= 2 * out_f
 
     def arm(self, sync: bool):
         self.armed = bool(sync)
