@@ -218,3 +218,35 @@ def test_fused_grads_land_in_ddp_bucket(gpu):
     loss.backward()
     v = d.grad_view(m.fc.weight)
     assert m.fc.weight.grad.data_ptr() == v.data_ptr()
+
+
+@pytest.mark.parametrize("P", [37, 40, 130])
+def test_conv2_backward_fused_with_bn2_pool(gpu, P):
+    """fused_conv2_backward_y2 (dy2 rebuilt in LDS from y2 + g2m) vs the unfused path
+    (dy2_build -> dy2 in HBM -> conv2 dgrad + wgrad)."""
+    torch.manual_seed(P)
+    B, NC = 2, 10
+    Q = P // 2
+    ops = _ops()
+    y2 = torch.randn(B, P, P, 32, device=gpu)
+    b2 = torch.randn(32, device=gpu) * 0.1
+    g2 = torch.rand(32, device=gpu) + 0.5
+    be2 = torch.randn(32, device=gpu) * 0.1
+    wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
+    bfc = torch.randn(NC, device=gpu)
+    yc = (y2 - b2).double()
+    partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()
+    _, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc)
+    dl = torch.randn(B, NC, device=gpu)
+    _, _, _, _, dy2 = ops.fused_head_backward(dl, y2, stats2, aff2, g2, wfc, None, 1.0)
+    _, _, _, _, g2m, kbuf = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, None, 1.0)
+    p = torch.relu(torch.randn(B, P, P, 16, device=gpu))
+    w2 = torch.randn(32, 16, 5, 5, device=gpu) * 0.05
+    _, wd = ops.conv2_pack(w2)
+    p1 = pack_hilo(p)
+    dp1_r, dw2_r, db2_r = ops.fused_conv2_backward(dy2, p1, wd, True, 1.0)
+    dp1, dw2, db2 = ops.fused_conv2_backward_y2(y2, g2m, aff2, kbuf, p1, wd, 1.0)
+    _check(dp1, dp1_r, 1e-6, "dp1")
+    _check(dw2, dw2_r, 1e-5, "dw2")
+    # conv bias before BN: sum(dy2) is analytically zero, both sides are rounding noise
+    assert (db2 - db2_r).abs().max().item() <= 1e-4 * dw2_r.abs().max().item()

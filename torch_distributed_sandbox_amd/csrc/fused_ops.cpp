@@ -164,11 +164,15 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
 }
 
 // ---------------------------------------------------------------- head backward
-// returns (dW [written into dw_out if given; empty when !compute_dw], db_fc, dgamma2, dbeta2, dy2 carrier)
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
-    const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
-    const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
-    bool compute_dw) {
+struct HeadBwd {
+  Tensor dW, dbfc, dgamma, dbeta, g2m, kbuf;
+};
+
+// fc / pool2 / ReLU / BN2 backward up to the pooled gradient g2m and the BN2 backward
+// constants kbuf = [k1|k2|k3] (dy2 = k1*dz + k2*y2 + k3)
+static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
+                                  const c10::optional<Tensor>& gamma2, const Tensor& wfc,
+                                  const c10::optional<Tensor>& dw_out, double scale, bool compute_dw) {
   const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
   const int64_t NC = wfc.size(0);
@@ -177,37 +181,59 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   need(stats2, at::kFloat, {64}, "stats2");
   need(aff2, at::kFloat, {64}, "aff2");
   const float* g = optf(gamma2, 32, "bn2.weight");
-  c10::DeviceGuard guard(y2.device());
   hipStream_t st = stream_of(y2);
-  Tensor dW;
+  HeadBwd r;
   if (!compute_dw) {
-    dW = at::empty({0}, wfc.options());
+    r.dW = at::empty({0}, wfc.options());
   } else if (dw_out.has_value() && dw_out->defined()) {
     need(*dw_out, at::kFloat, {NC, 32 * Q * Q}, "dW_out");
-    dW = *dw_out;
+    r.dW = *dw_out;
   } else {
-    dW = at::empty_like(wfc);
+    r.dW = at::empty_like(wfc);
   }
-  auto g2m = at::empty({B, Q, Q, 32}, y2.options());
+  r.g2m = at::empty({B, Q, Q, 32}, y2.options());
   const int nblk = tds_head_fwd_nblk((int)Q);
   auto partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
   const int rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
-                              dlogits.data_ptr<float>(), compute_dw ? dW.data_ptr<float>() : nullptr,
-                              g2m.data_ptr<float>(),
-                              partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale, st);
+                              dlogits.data_ptr<float>(), compute_dw ? r.dW.data_ptr<float>() : nullptr,
+                              r.g2m.data_ptr<float>(), partial.data_ptr<double>(), (int)B, (int)P, (int)NC,
+                              (float)scale, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported B/NC");
   auto sums = at::empty({64}, y2.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), sums.data_ptr<double>(), 64, nblk, 2, (int64_t)nblk * 2, 2, st);
-  auto dgamma = at::empty({32}, y2.options());
-  auto dbeta = at::empty({32}, y2.options());
-  auto kbuf = at::empty({96}, y2.options());
+  r.dgamma = at::empty({32}, y2.options());
+  r.dbeta = at::empty({32}, y2.options());
+  r.kbuf = at::empty({96}, y2.options());
   tds_bn_bwd_finalize2(sums.data_ptr<double>(), 32, 1, B * P * P, g, stats2.data_ptr<float>(),
-                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), st);
+                       r.dgamma.data_ptr<float>(), r.dbeta.data_ptr<float>(), r.kbuf.data_ptr<float>(), st);
+  r.dbfc = dlogits.sum(0).mul_(scale);
+  return r;
+}
+
+// returns (dW [written into dw_out if given; empty when !compute_dw], db_fc, dgamma2, dbeta2, dy2 carrier)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
+    const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
+    const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
+    bool compute_dw) {
+  c10::DeviceGuard guard(y2.device());
+  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw);
+  const int64_t B = y2.size(0), P = y2.size(1);
   auto dy2 = at::empty({B, P, P, 32}, y2.options());  // carrier of bf16 [B,P,P,64]
-  tds_dy2_build(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
-                dy2.data_ptr(), (int)B, (int)P, st);
-  auto dbfc = dlogits.sum(0).mul_(scale);
-  return {dW, dbfc, dgamma, dbeta, dy2};
+  tds_dy2_build(y2.data_ptr<float>(), r.g2m.data_ptr<float>(), aff2.data_ptr<float>(), r.kbuf.data_ptr<float>(),
+                dy2.data_ptr(), (int)B, (int)P, stream_of(y2));
+  return {r.dW, r.dbfc, r.dgamma, r.dbeta, dy2};
+}
+
+// Head backward up to the pooled gradient: returns (dW, db_fc, dgamma2, dbeta2, g2m, kbuf).
+// The conv2 backward then runs fused with the BN2/pool backward (fused_conv2_backward_y2),
+// so dy2 is never materialised.
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward_g2m(
+    const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
+    const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
+    bool compute_dw) {
+  c10::DeviceGuard guard(y2.device());
+  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw);
+  return {r.dW, r.dbfc, r.dgamma, r.dbeta, r.g2m, r.kbuf};
 }
 
 // ---------------------------------------------------------------- conv2 backward
@@ -228,6 +254,30 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward(const Tensor& dy2, const
   auto db2 = at::empty({32}, p1.options());
   tds_conv2_wgrad_bf16x3(dy2.data_ptr(), p1.data_ptr(), slab.data_ptr<float>(), dw2.data_ptr<float>(),
                          db2.data_ptr<float>(), (float)scale, nwg, (int)B, (int)P, st);
+  return {dp1, dw2, db2};
+}
+
+// BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2, g2m, aff2, kbuf, p1) -> (dp1, dw2, db2)
+std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& g2m, const Tensor& aff2,
+                                                           const Tensor& kbuf, const Tensor& p1, const Tensor& wd,
+                                                           double scale) {
+  const int64_t B = p1.size(0), P = p1.size(1), Q = P / 2;
+  need(p1, at::kFloat, {B, P, P, 16}, "p1");
+  need(y2, at::kFloat, {B, P, P, 32}, "y2");
+  need(g2m, at::kFloat, {B, Q, Q, 32}, "g2m");
+  need(aff2, at::kFloat, {64}, "aff2");
+  need(kbuf, at::kFloat, {96}, "kbuf");
+  need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
+  c10::DeviceGuard guard(p1.device());
+  hipStream_t st = stream_of(p1);
+  const int nwg = tds_conv2_num_wg();
+  auto dp1 = at::empty({B, P, P, 16}, p1.options());
+  auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options());
+  auto dw2 = at::empty({32, 16, 5, 5}, p1.options());
+  auto db2 = at::empty({32}, p1.options());
+  tds_conv2_bwd_fused(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
+                      p1.data_ptr(), wd.data_ptr<int16_t>(), dp1.data_ptr<float>(), slab.data_ptr<float>(),
+                      dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, nwg, (int)B, (int)P, st);
   return {dp1, dw2, db2};
 }
 
@@ -285,6 +335,14 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       &fused_head_backward);
   m.def("fused_conv2_backward(Tensor dy2, Tensor p1, Tensor wd, bool need_dp1, float scale) -> (Tensor, Tensor, Tensor)",
         &fused_conv2_backward);
+  m.def(
+      "fused_head_backward_g2m(Tensor dlogits, Tensor y2, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor wfc, "
+      "Tensor(a!)? dw_out, float scale, bool compute_dw=True) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
+      &fused_head_backward_g2m);
+  m.def(
+      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale) -> "
+      "(Tensor, Tensor, Tensor)",
+      &fused_conv2_backward_y2);
   m.def(
       "fused_l1_backward(Tensor dp1, Tensor x, Tensor p1, Tensor idx1, Tensor w1, Tensor b1, Tensor? gamma1, "
       "Tensor stats1, Tensor gram, float scale) -> (Tensor, Tensor, Tensor, Tensor)",

@@ -62,6 +62,9 @@ void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t s
 int tds_conv2_num_wg();
 void tds_conv2_fwd_bf16x3(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg,
                           int B, int P, hipStream_t st);
+void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
+                         const short* wd, float* dp1, float* slab, float* dw, float* db, float scale, int nwg, int B,
+                         int P, hipStream_t st);
 void tds_conv2_dgrad_bf16x3(const void* dy2, const short* wd, float* dp1, int nwg, int B, int P, hipStream_t st);
 void tds_conv2_wgrad_bf16x3(const void* dy2, const void* p1, float* slab, float* dw, float* db, float scale, int nwg,
                             int B, int P, hipStream_t st);

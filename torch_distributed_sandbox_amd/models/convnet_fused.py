@@ -6,7 +6,8 @@ autograd Functions over NHWC/bf16x3 activations (kernels in
 ``csrc/kernels/convnet_fused.hip`` and ``conv2_bf16x3.hip``):
 
 ``_Layer1``  x -> p1            conv1 + BN1(batch stats) + ReLU + pool, conv1 never stored
-``_Conv2``   p1 -> y2           conv2 (bf16x3 MFMA) with BN2 batch-stat partials fused
+``_Conv2``   p1 -> y2           conv2 (bf16x3 MFMA) with BN2 batch-stat partials fused; its
+                                backward rebuilds dy2 from y2 in LDS (BN2/pool backward fused)
 ``_Head``    y2 -> logits       BN2 + ReLU + pool + fc in one pass; fc grads into the DDP bucket
 
 Autograd runs the backward head -> conv2 -> layer1, so the fc gradient (the
@@ -65,26 +66,39 @@ class _Layer1(torch.autograd.Function):
         return None, dw1, db1, dg1, dbe1, None, None, None, None, None
 
 
+class _Layer2Link:
+    """Carries the head backward's pooled gradient (g2m) and BN2 backward constants to the
+    conv2 backward, which rebuilds dy2 tile by tile in LDS (never in HBM).  The two stay
+    separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
+    all-reduce — fires before the conv2 backward runs."""
+
+    __slots__ = ("g2m", "kbuf", "aff2")
+
+
 class _Conv2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, p1, w2, b2):
+    def forward(ctx, p1, w2, b2, link):
         ops = _ext.ops()
         wp, wd = ops.conv2_pack(w2.contiguous())
         y2, partial2 = ops.fused_conv2_forward(p1, wp, b2)
-        ctx.save_for_backward(p1, wd)
+        ctx.save_for_backward(p1, wd, y2)
+        ctx.link = link
         ctx.mark_non_differentiable(partial2)
         return y2, partial2
 
     @staticmethod
-    def backward(ctx, dy2, _unused):
-        p1, wd = ctx.saved_tensors
-        dp1, dw2, db2 = _ext.ops().fused_conv2_backward(dy2.contiguous(), p1, wd, ctx.needs_input_grad[0], 1.0)
-        return (dp1 if ctx.needs_input_grad[0] else None), dw2, db2
+    def backward(ctx, _dy2_placeholder, _unused):
+        p1, wd, y2 = ctx.saved_tensors
+        link = ctx.link
+        # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
+        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, p1, wd, 1.0)
+        link.g2m = link.kbuf = link.aff2 = None
+        return (dp1 if ctx.needs_input_grad[0] else None), dw2, db2, None
 
 
 class _Head(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex):
+    def forward(ctx, y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex, link):
         ops = _ext.ops()
         x_out = None
         if ex is not None:
@@ -97,6 +111,7 @@ class _Head(torch.autograd.Function):
         ctx.save_for_backward(y2, stats2, aff2, g2, wfc)
         ctx.wfc_param = wfc
         ctx.ex = ex
+        ctx.link = link
         return logits
 
     @staticmethod
@@ -104,15 +119,22 @@ class _Head(torch.autograd.Function):
         y2, stats2, aff2, g2, wfc = ctx.saved_tensors
         dlogits = dlogits.contiguous().float()
         ex = ctx.ex
+        ops = _ext.ops()
         if ex is not None:
             # fc gradients come from the activation exchange (parallel/factored.py)
-            _, _, dg2, dbe2, dy2 = _ext.ops().fused_head_backward(dlogits, y2, stats2, aff2, g2, wfc, None, 1.0,
-                                                                  False)
+            _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, None, 1.0,
+                                                                     False)
             ex.defer(dlogits)
-            return dy2, None, None, dg2, dbe2, None, None, None, None, None, None, None, None
-        dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[10] else None, wfc.shape, wfc)
-        dW, dbfc, dg2, dbe2, dy2 = _ext.ops().fused_head_backward(dlogits, y2, stats2, aff2, g2, wfc, dw_out, 1.0)
-        return dy2, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None
+            dW = dbfc = None
+        else:
+            dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[10] else None, wfc.shape, wfc)
+            dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, dw_out,
+                                                                         1.0)
+        link = ctx.link
+        link.g2m, link.kbuf, link.aff2 = g2m, kbuf, aff2
+        # y2's gradient is carried by the link; autograd gets a zero-stride placeholder
+        dy2 = torch.zeros((), device=y2.device, dtype=y2.dtype).expand(y2.shape)
+        return dy2, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None, None
 
 
 def forward(model, x):
@@ -121,7 +143,8 @@ def forward(model, x):
     fc = model.fc
     p1 = _Layer1.apply(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
                        bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps))
-    y2, partial2 = _Conv2.apply(p1, conv2.weight, conv2.bias)
+    link = _Layer2Link()
+    y2, partial2 = _Conv2.apply(p1, conv2.weight, conv2.bias, link)
     # the fc update may still be running on DDP's side stream (overlap_optimizer): wait here,
     # after the convolutions were queued, not before
     param_fence.wait(fc.weight)
@@ -130,4 +153,4 @@ def forward(model, x):
     if ex is not None and not ex.ready(x.shape[0]):
         ex = None
     return _Head.apply(y2, partial2, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
-                       bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias, ex)
+                       bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias, ex, link)
