@@ -49,7 +49,25 @@ def main():
         res[f"diag{diag}"] = times
         print(diag, times, flush=True)
     os.environ["TDS_CONV2_DIAG"] = "0"
-    print(json.dumps({"B": B, "P": P, "ms": res}))
+    # A/B of the fused backward designs (TDS_CONV2_BWD: 1 = one 8-wave WG per CU, 2 = two 4-wave WGs)
+    fn = lambda: ops.fused_conv2_backward_y2(dy2, g2m, aff2, kbuf, p1, wd, 1.0)  # noqa: E731
+    ab = {}
+    for rep in range(3):
+        for ver in ("1", "2"):
+            os.environ["TDS_CONV2_BWD"] = ver
+            for _ in range(2):
+                fn()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            ab.setdefault(f"bwd_v{ver}", []).append(round(s.elapsed_time(e) / 10, 4))
+    os.environ.pop("TDS_CONV2_BWD")
+    print("fused backward A/B (ms):", ab, flush=True)
+    print(json.dumps({"B": B, "P": P, "ms": res, "bwd_ab": ab}))
 
 
 if __name__ == "__main__":

@@ -270,7 +270,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
   c10::DeviceGuard guard(p1.device());
   hipStream_t st = stream_of(p1);
-  const int nwg = tds_conv2_num_wg();
+  const int nwg = tds_conv2_bwd_fused_num_wg();
   auto dp1 = at::empty({B, P, P, 16}, p1.options());
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options());
   auto dw2 = at::empty({32, 16, 5, 5}, p1.options());

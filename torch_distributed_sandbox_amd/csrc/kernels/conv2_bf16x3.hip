@@ -28,7 +28,7 @@
 // registers before the current tile's MFMAs and written to LDS after them.
 #include <cstdlib>
 
-#include "bf16x3.h"
+#include "conv2_common.h"
 #include "launchers.h"
 
 namespace tds {
@@ -38,38 +38,6 @@ constexpr int C2_TC = 32;  // tile cols   (two 16-pixel M tiles per wave)
 constexpr int C2_IR = C2_TH + 4;
 constexpr int C2_IC = C2_TC + 4;
 constexpr int C2_THREADS = 512;
-
-// ---------------------------------------------------------------------------- diagnostics
-// DIAG = 0: the real kernel.  Timing-only builds (tools/conv2_diag.py, TDS_CONV2_DIAG):
-//   1: no MFMAs (operand reads kept alive by one VALU op),  2: no LDS operand reads
-//   (register constants), 3: no global tile loads (LDS holds whatever it held).
-template <int DIAG>
-__device__ __forceinline__ f32x4 mma3(const s16x8& ah, const s16x8& al, const s16x8& bh, const s16x8& bl, f32x4 c) {
-  if constexpr (DIAG == 1) {
-    c[0] += (float)((int)(ah[0] ^ al[1] ^ bh[2] ^ bl[3]) & 1);
-    return c;
-  } else {
-    return mfma_bf16x3(ah, al, bh, bl, c);
-  }
-}
-template <int DIAG>
-__device__ __forceinline__ s16x8 lds8(const void* p) {
-  if constexpr (DIAG == 2) {
-    const short v = (short)(threadIdx.x & 7);
-    return s16x8{v, v, v, v, v, v, v, v};
-  } else {
-    return *reinterpret_cast<const s16x8*>(p);
-  }
-}
-template <int DIAG>
-__device__ __forceinline__ s16x4 ldtr(const void* p) {
-  if constexpr (DIAG == 2) {
-    const short v = (short)(threadIdx.x & 7);
-    return s16x4{v, v, v, v};
-  } else {
-    return ds_read_tr16(p);
-  }
-}
 
 // ---------------------------------------------------------------------------- weight packing
 // fwd : wp[hl][s<13][nt<2][g<4][co16][j8], k = 32s+8g+j, ci = 8(g&1)+j, taps paired so that one
@@ -1029,11 +997,28 @@ void tds_conv2_wgrad_bf16x3(const void* dy2, const void* p1, float* slab, float*
 
 int tds_conv2_lds_bytes(int which) { return which == 0 ? F_LDS : (which == 1 ? D_LDS : W_LDS); }
 
+// Which fused backward kernel runs: 2 = conv2_bwd2_kernel (two 4-wave workgroups per CU,
+// conv2_bwd2.hip; default), 1 = conv2_bwd_fused_kernel (one 8-wave workgroup per CU).
+// TDS_CONV2_BWD selects (A/B timing, tools/conv2_diag.py).
+int tds_conv2_bwd_version() {
+  const char* e = std::getenv("TDS_CONV2_BWD");
+  return (e && std::atoi(e) == 1) ? 1 : 2;
+}
+int tds_conv2_bwd_fused_num_wg() {
+  return tds_conv2_bwd_version() == 2 ? tds_conv2_bwd2_num_wg() : tds_conv2_num_wg();
+}
+
 // fused BN2/pool backward + conv2 dgrad + wgrad: y2 [B,P,P,32] f32, g2m [B,Q,Q,32] f32,
 // aff2 [a32|b32], kbuf [k1|k2|k3]; dp1 [B,P,P,16] f32; slab [nwg][26][512]
 void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
                          const short* wd, float* dp1, float* slab, float* dw, float* db, float scale, int nwg, int B,
                          int P, hipStream_t st) {
+  if (tds_conv2_bwd_version() == 2) {
+    tds_conv2_bwd2(y2, g2m, aff2, kbuf, p1, wd, dp1, slab, nwg, B, P, st);
+    hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((26 * 512 + 255) / 256), dim3(256), 0, st, slab, nwg, dw, db,
+                       scale);
+    return;
+  }
   set_lds_limits();
   const int Q = P / 2;
   TDS_C2_DISPATCH(conv2_bwd_fused_kernel, dim3(nwg), dim3(C2_THREADS), BW_LDS, st,

@@ -1,0 +1,70 @@
+// Shared pieces of the conv2 kernels (conv2_bf16x3.hip, conv2_bwd2.hip): the timing-only
+// diagnostic operand/MFMA wrappers (tools/conv2_diag.py, TDS_CONV2_DIAG).
+#pragma once
+
+#include "bf16x3.h"
+
+namespace tds {
+
+// ---------------------------------------------------------------------------- diagnostics
+// DIAG = 0: the real kernel.  Timing-only builds (tools/conv2_diag.py, TDS_CONV2_DIAG):
+//   1: no MFMAs (operand reads kept alive by one VALU op),  2: no LDS operand reads
+//   (register constants), 3: no global tile loads (LDS holds whatever it held).
+template <int DIAG>
+__device__ __forceinline__ f32x4 mma3(const s16x8& ah, const s16x8& al, const s16x8& bh, const s16x8& bl, f32x4 c) {
+  if constexpr (DIAG == 1) {
+    c[0] += (float)((int)(ah[0] ^ al[1] ^ bh[2] ^ bl[3]) & 1);
+    return c;
+  } else {
+    return mfma_bf16x3(ah, al, bh, bl, c);
+  }
+}
+template <int DIAG>
+__device__ __forceinline__ s16x8 lds8(const void* p) {
+  if constexpr (DIAG == 2) {
+    const short v = (short)(threadIdx.x & 7);
+    return s16x8{v, v, v, v, v, v, v, v};
+  } else {
+    return *reinterpret_cast<const s16x8*>(p);
+  }
+}
+template <int DIAG>
+__device__ __forceinline__ s16x4 ldtr(const void* p) {
+  if constexpr (DIAG == 2) {
+    const short v = (short)(threadIdx.x & 7);
+    return s16x4{v, v, v, v};
+  } else {
+    return ds_read_tr16(p);
+  }
+}
+
+// ---------------------------------------------------------------------------- tile order
+// L2-blocked tile order for the persistent conv kernels.  xcd_remap hands each XCD a
+// contiguous run of 64 work indices per round (grid = 512 = 8 XCDs x 64 workgroups), and
+// t -> t + grid is the same workgroup's next tile.  A plain row-major order makes those 64
+// tiles a 1-D strip, so the 2-pixel halo above/below each tile (a third of the staged rows)
+// is fetched again a round later, long after it left the XCD's 4 MiB L2.  Here work index
+// t walks, per image, bands of BC tile-columns; each band in row groups of GR tile-rows;
+// each row group in column groups of GC:  one XCD round = one GR x GC block of tiles (its
+// halos are fetched once, concurrently, into one L2), the 8 XCDs take the 8 blocks of a
+// band row side by side, and the next round is the block right below (its top halo still
+// in L2).  Bijective for any tiles_r x tiles_c (edge groups are simply smaller).
+template <int BC, int GR, int GC>
+__device__ __forceinline__ void blocked_tile(int t, int per_img, int tiles_r, int tiles_c, int& b, int& tr, int& tc) {
+  b = t / per_img;
+  int off = t - b * per_img;
+  const int band = off / (BC * tiles_r);  // every band before the last is full width
+  off -= band * BC * tiles_r;
+  const int wj = min(BC, tiles_c - band * BC);
+  const int gr = off / (GR * wj);
+  off -= gr * GR * wj;
+  const int hg = min(GR, tiles_r - gr * GR);
+  const int cg = off / (GC * hg);
+  off -= cg * GC * hg;
+  const int wc = min(GC, wj - cg * GC);
+  const int r = off / wc;
+  tr = gr * GR + r;
+  tc = band * BC + cg * GC + (off - r * wc);
+}
+
+}  // namespace tds

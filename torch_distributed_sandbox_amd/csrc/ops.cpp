@@ -87,6 +87,9 @@ Tensor maxpool2_bwd(const Tensor& gy, const Tensor& idx, int64_t H, int64_t W) {
 Tensor upsample_bilinear_u8(const Tensor& src, int64_t H, int64_t W) {
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.is_contiguous() && src.dim() == 3,
               "tdsa.upsample_bilinear_u8: expected contiguous uint8 [B,h,w] on GPU");
+  TORCH_CHECK(src.size(1) >= 1 && src.size(2) >= 1 && src.size(2) <= 256 && src.size(0) <= 65535 && H >= 1 &&
+                  W >= 1 && H <= INT32_MAX && W <= INT32_MAX,
+              "tdsa.upsample_bilinear_u8: source width must be 1..256 and batch <= 65535");
   c10::DeviceGuard g(src.device());
   auto dst = at::empty({src.size(0), 1, H, W}, src.options().dtype(at::kFloat));
   tds_upsample_bilinear_u8(src.data_ptr<uint8_t>(), dst.data_ptr<float>(), (int)src.size(0), (int)src.size(1),
