@@ -123,6 +123,47 @@ def test_head_fwd_bwd(gpu, P):
     _check(unpack_hilo(dy2, 32).permute(0, 3, 1, 2), yr.grad, 1e-4, "dy2")
 
 
+@pytest.mark.parametrize("P", [64, 130])
+def test_head_backward_from_saved_argmax(gpu, P):
+    """head backward from the saved argmax values ya (head_bwd_ya_kernel) == the y2 path,
+    and dW / dgamma / dbeta vs fp64 autograd."""
+    torch.manual_seed(P + 1)
+    B, NC = 5, 10
+    Q = P // 2
+    ops = _ops()
+    y2 = torch.randn(B, P, P, 32, device=gpu)
+    b2 = torch.randn(32, device=gpu) * 0.1
+    g2 = torch.rand(32, device=gpu) + 0.5
+    be2 = torch.randn(32, device=gpu) * 0.1
+    wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
+    bfc = torch.randn(NC, device=gpu)
+    yc = (y2 - b2).double()
+    partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()
+    ya = torch.empty(B, 32 * Q * Q, device=gpu)
+    logits, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc,
+                                                  None, ya)
+    # ya is y2 at the window argmax of the BN2 output: relu(a*ya + b) is the pooled activation
+    yr = y2.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
+    gr = g2.double().cpu().requires_grad_(True)
+    ber = be2.double().cpu().requires_grad_(True)
+    wr = wfc.double().cpu().requires_grad_(True)
+    z = F.batch_norm(yr, None, None, gr, ber, True, 0.1, 1e-5)
+    pz = F.max_pool2d(F.relu(z), 2, 2)
+    a, b = aff2[:32].double().cpu(), aff2[32:].double().cpu()
+    p_from_ya = torch.relu(a.view(1, 32, 1, 1) * ya.view(B, 32, Q, Q).double().cpu() + b.view(1, 32, 1, 1))
+    _check(p_from_ya, pz, 1e-5, "relu(a*ya+b) vs pooled")
+    ref = F.linear(pz.reshape(B, -1), wr, bfc.double().cpu())
+    dl = torch.randn(B, NC, device=gpu)
+    ref.backward(dl.double().cpu())
+    r_y2 = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, None, 1.0, True)
+    r_ya = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, None, 1.0, True, ya)
+    for name, u, v in zip(("dW", "dbfc", "dgamma2", "dbeta2", "g2m", "kbuf"), r_ya, r_y2):
+        _check(u, v, 1e-6, name + " (ya vs y2 path)")
+    _check(r_ya[0], wr.grad, 1e-5, "dW")
+    _check(r_ya[2], gr.grad, 1e-5, "dgamma2")
+    _check(r_ya[3], ber.grad, 1e-5, "dbeta2")
+
+
 @pytest.mark.parametrize("P", [40, 37, 128, 200])
 def test_conv2_backward(gpu, P):
     torch.manual_seed(0)

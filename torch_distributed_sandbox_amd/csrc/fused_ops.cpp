@@ -119,7 +119,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
     const Tensor& y2, const Tensor& partial2, const Tensor& b2, const c10::optional<Tensor>& gamma2,
     const c10::optional<Tensor>& beta2, const c10::optional<Tensor>& rm2, const c10::optional<Tensor>& rv2,
     const c10::optional<Tensor>& nbt2, double momentum, double eps, const Tensor& wfc, const c10::optional<Tensor>& bfc,
-    const c10::optional<Tensor>& x_out) {
+    const c10::optional<Tensor>& x_out, const c10::optional<Tensor>& ya_out) {
   TORCH_CHECK(y2.dim() == 4 && y2.size(3) == 32 && y2.size(1) == y2.size(2), "fused_head_forward: y2");
   const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
@@ -144,6 +144,11 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
     need(*x_out, at::kFloat, {B, 32 * Q * Q}, "x_out (fc input rows)");
     xo = x_out->data_ptr<float>();
   }
+  float* yo = nullptr;
+  if (ya_out.has_value() && ya_out->defined()) {
+    need(*ya_out, at::kFloat, {B, 32 * Q * Q}, "ya_out (y2 at the pooling argmax)");
+    yo = ya_out->data_ptr<float>();
+  }
   c10::DeviceGuard guard(y2.device());
   hipStream_t st = stream_of(y2);
   auto sums2 = at::empty({64}, y2.options().dtype(at::kDouble));
@@ -157,7 +162,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
   auto lsum = at::empty({B * NC}, y2.options().dtype(at::kDouble));
   auto logits = at::empty({B, NC}, y2.options());
   const int rc = tds_head_fwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
-                              part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
+                              part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, yo, (int)B,
                               (int)P, (int)NC, st);
   TORCH_CHECK(rc == 0, "fused_head_forward: unsupported B/NC");
   return {logits, stats, aff};
@@ -172,7 +177,8 @@ struct HeadBwd {
 // constants kbuf = [k1|k2|k3] (dy2 = k1*dz + k2*y2 + k3)
 static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
                                   const c10::optional<Tensor>& gamma2, const Tensor& wfc,
-                                  const c10::optional<Tensor>& dw_out, double scale, bool compute_dw) {
+                                  const c10::optional<Tensor>& dw_out, double scale, bool compute_dw,
+                                  const c10::optional<Tensor>& ya = c10::nullopt) {
   const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
   const int64_t NC = wfc.size(0);
@@ -192,12 +198,24 @@ static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const
     r.dW = at::empty_like(wfc);
   }
   r.g2m = at::empty({B, Q, Q, 32}, y2.options());
-  const int nblk = tds_head_fwd_nblk((int)Q);
+  const bool use_ya = ya.has_value() && ya->defined() && tds_head_bwd_ya_supported((int)B, (int)P, (int)NC);
+  const int nblk = use_ya ? tds_head_bwd_ya_nblk((int)Q) : tds_head_fwd_nblk((int)Q);
   auto partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
-  const int rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
-                              dlogits.data_ptr<float>(), compute_dw ? r.dW.data_ptr<float>() : nullptr,
-                              r.g2m.data_ptr<float>(), partial.data_ptr<double>(), (int)B, (int)P, (int)NC,
-                              (float)scale, st);
+  int rc;
+  rc = -1;
+  if (use_ya) {
+    // saved argmax values: stream ya (B*32*Q*Q floats) instead of y2
+    need(*ya, at::kFloat, {B, 32 * Q * Q}, "ya");
+    rc = tds_head_bwd_ya(ya->data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
+                         dlogits.data_ptr<float>(), compute_dw ? r.dW.data_ptr<float>() : nullptr,
+                         r.g2m.data_ptr<float>(), partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale,
+                         st);
+  }
+  if (rc != 0) {
+    rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(), dlogits.data_ptr<float>(),
+                      compute_dw ? r.dW.data_ptr<float>() : nullptr, r.g2m.data_ptr<float>(),
+                      partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale, st);
+  }
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported B/NC");
   auto sums = at::empty({64}, y2.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), sums.data_ptr<double>(), 64, nblk, 2, (int64_t)nblk * 2, 2, st);
@@ -230,9 +248,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward_g2m(
     const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
     const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
-    bool compute_dw) {
+    bool compute_dw, const c10::optional<Tensor>& ya) {
   c10::DeviceGuard guard(y2.device());
-  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw);
+  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw, ya);
   return {r.dW, r.dbfc, r.dgamma, r.dbeta, r.g2m, r.kbuf};
 }
 
@@ -326,7 +344,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2) -> (Tensor, Tensor)", &fused_conv2_forward);
   m.def(
       "fused_head_forward(Tensor y2, Tensor partial2, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
-      "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc, Tensor(d!)? x_out=None) "
+      "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc, Tensor(d!)? x_out=None, "
+      "Tensor(e!)? ya_out=None) "
       "-> (Tensor, Tensor, Tensor)",
       &fused_head_forward);
   m.def(
@@ -337,7 +356,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
         &fused_conv2_backward);
   m.def(
       "fused_head_backward_g2m(Tensor dlogits, Tensor y2, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor wfc, "
-      "Tensor(a!)? dw_out, float scale, bool compute_dw=True) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
+      "Tensor(a!)? dw_out, float scale, bool compute_dw=True, Tensor? ya=None) -> "
+      "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward_g2m);
   m.def(
       "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale) -> "

@@ -906,18 +906,36 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_bwd_fused_kernel(
   }
 }
 
-// dw2[co][ci][tap] = sum_wg slab (fixed order, fp64), db2[co] = sum_wg slab[tap 25][co][0]
-__global__ void conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nwg, float* __restrict__ dw,
-                                          float* __restrict__ db, float scale) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;  // over 26*32*16
-  if (e >= 26 * 512) return;
-  const int tap = e / 512, co = (e / 16) & 31, ci = e & 15;
-  if (tap == 25 && ci != 0) return;
+// dw2[co][ci][tap] = sum_wg slab (fixed order, fp64), db2[co] = sum_wg slab[tap 25][co][0].
+// A block owns 64 consecutive slab elements; its 4 waves sum interleaved quarters of the
+// workgroup rows (w = 4j + wave, 8 loads in flight per lane), then wave 0 adds the four
+// partials in a fixed order: deterministic, and 4x the parallelism of one lane per element.
+__global__ __launch_bounds__(256) void conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nwg,
+                                                                 float* __restrict__ dw, float* __restrict__ db,
+                                                                 float scale) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;  // over 26*32*16
   double s = 0.0;
-  for (int w = 0; w < nwg; ++w) s += slab[(int64_t)w * 26 * 512 + e];
-  const float v = (float)s * scale;
+  if (e < 26 * 512) {
+    int w = wv;
+    for (; w + 28 < nwg; w += 32) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = slab[(int64_t)(w + 4 * k) * 26 * 512 + e];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += (double)v[k];
+    }
+    for (; w < nwg; w += 4) s += (double)slab[(int64_t)w * 26 * 512 + e];
+  }
+  part[wv][lane] = s;
+  __syncthreads();
+  if (wv != 0 || e >= 26 * 512) return;
+  const double tot = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  const int tap = e / 512, co = (e / 16) & 31, ci = e & 15;
+  const float v = (float)tot * scale;
   if (tap < 25) dw[(co * 16 + ci) * 25 + tap] = v;
-  else if (db) db[co] = v;
+  else if (db && ci == 0) db[co] = v;
 }
 
 }  // namespace tds
@@ -991,7 +1009,7 @@ void tds_conv2_wgrad_bf16x3(const void* dy2, const void* p1, float* slab, float*
   set_lds_limits();
   TDS_C2_DISPATCH(conv2_wgrad_bf16x3_kernel, dim3(nwg), dim3(C2_THREADS), W_LDS, st,
                   reinterpret_cast<const uint4*>(dy2), reinterpret_cast<const uint4*>(p1), slab, B, P);
-  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((26 * 512 + 255) / 256), dim3(256), 0, st, slab, nwg, dw, db,
+  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db,
                      scale);
 }
 
@@ -1015,7 +1033,7 @@ void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, c
                          int P, hipStream_t st) {
   if (tds_conv2_bwd_version() == 2) {
     tds_conv2_bwd2(y2, g2m, aff2, kbuf, p1, wd, dp1, slab, nwg, B, P, st);
-    hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((26 * 512 + 255) / 256), dim3(256), 0, st, slab, nwg, dw, db,
+    hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db,
                        scale);
     return;
   }
@@ -1024,6 +1042,6 @@ void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, c
   TDS_C2_DISPATCH(conv2_bwd_fused_kernel, dim3(nwg), dim3(C2_THREADS), BW_LDS, st,
                   reinterpret_cast<const float4*>(y2), reinterpret_cast<const float4*>(g2m), aff2, kbuf,
                   reinterpret_cast<const uint4*>(p1), reinterpret_cast<const uint4*>(wd), dp1, slab, B, P, Q);
-  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3((26 * 512 + 255) / 256), dim3(256), 0, st, slab, nwg, dw, db,
+  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db,
                      scale);
 }

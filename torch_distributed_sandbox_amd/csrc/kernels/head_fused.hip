@@ -10,6 +10,8 @@
 // all images; per image the two y2 rows (2 x 128 NHWC records of 128 B) are
 // staged through LDS with coalesced 16-B loads, the next image's loads issued
 // into registers before the current image is processed.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -17,6 +19,7 @@ namespace tds {
 
 constexpr int HD_PX = 64;
 constexpr int HD_MAXB = 32;  // images per rank (per-image partial sums live in LDS)
+constexpr int HD_MAXB_YA = 8;  // images per rank on the ya backward path (per-lane registers)
 constexpr int HD_REC = 144;  // padded LDS record stride (bytes): 128 B of y2 + 16 B
 constexpr int HD_LDS = 2 * 2 * HD_PX * HD_REC;
 
@@ -65,10 +68,10 @@ __device__ __forceinline__ void head_window(const char* lds, int lane, int wv, c
   }
 #pragma unroll
   for (int c = 0; c < CPW; ++c) {
-    float m = a[c] * y[0][c] + bb[c], ya = y[0][c];
+    float m = fmaf(a[c], y[0][c], bb[c]), ya = y[0][c];
 #pragma unroll
     for (int q = 1; q < 4; ++q) {
-      const float z = a[c] * y[q][c] + bb[c];
+      const float z = fmaf(a[c], y[q][c], bb[c]);
       if (z > m || isnan(z)) { m = z; ya = y[q][c]; }  // first max in scan order, NaN wins
     }
     pos[c] = m > 0.f;
@@ -84,7 +87,7 @@ template <int NW>
 __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
                                                            const float* __restrict__ aff2,
                                                            double* __restrict__ partial, float* __restrict__ xout,
-                                                           int B, int P, int Q, int NC) {
+                                                           float* __restrict__ yaout, int B, int P, int Q, int NC) {
   constexpr int CPW = 32 / NW;
   using Tile = HeadTile<NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -116,6 +119,10 @@ __global__ __launch_bounds__(64 * NW) void head_fwd_kernel(const float4* __restr
     if (xout != nullptr && valid) {
 #pragma unroll
       for (int c = 0; c < CPW; ++c) xout[((int64_t)b * 32 + CPW * wv + c) * QQ + pos] = p[c];
+    }
+    if (yaout != nullptr && valid) {
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) yaout[((int64_t)b * 32 + CPW * wv + c) * QQ + pos] = ya[c];
     }
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
@@ -230,6 +237,88 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restr
   }
 }
 
+// Backward from the saved argmax values ya = y2 at each pooled window's argmax, [B][32][Q][Q]
+// in the fc's flatten order (written by head_fwd).  p2 = relu(a*ya + b) is recomputed
+// bit-exactly (same fmaf as head_window), so the kernel streams only ya (360 MB at 3000^2)
+// and W instead of y2 (1.44 GB) through an LDS transpose.  Tile: one pooled row py x 64
+// columns (lane = column), wave w owns channels 4w..4w+3; every load of a lane is issued
+// before any use (60 x 4 B in flight per lane).
+// (A persistent two-register-set pipelined variant ran out of SGPRs for its 100 plane
+// offsets and was slower; see docs/KERNELS.md.)  Outputs as head_bwd_kernel.
+template <bool WITH_DW, int NB>  // NB = images per rank (compile-time: exact register footprint)
+__global__ __launch_bounds__(512, 2) void head_bwd_ya_kernel(const float* __restrict__ ya, const float* __restrict__ Wfc,
+                                                             const float* __restrict__ aff2, const float* __restrict__ dl,
+                                                             float* __restrict__ dW, float* __restrict__ g2m,
+                                                             double* __restrict__ partial, int Q, int NC, float scale) {
+  constexpr int CPW = 4;
+  __shared__ float dls[NB * 10];  // dlogits: broadcast LDS reads (as scalars they cost ~50 SGPRs and spill)
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x < NB * 10) dls[threadIdx.x] = (int)threadIdx.x % 10 < NC ? dl[(threadIdx.x / 10) * NC + threadIdx.x % 10] : 0.f;
+  const int px = blockIdx.x * HD_PX + lane;
+  const bool valid = px < Q;
+  const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)blockIdx.y * Q + (valid ? px : 0);
+  const int c0 = CPW * wv;
+  float w[10][CPW], y[NB][CPW];
+#pragma unroll
+  for (int j = 0; j < 10; ++j)
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) w[j][c] = (valid && j < NC) ? Wfc[((int64_t)j * 32 + c0 + c) * QQ + pos] : 0.f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) y[b][c] = valid ? ya[((int64_t)b * 32 + c0 + c) * QQ + pos] : 0.f;
+  float a[CPW], bb[CPW], sdz[CPW], sdy[CPW], dwa[10][CPW];
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    a[c] = aff2[c0 + c];
+    bb[c] = aff2[32 + c0 + c];
+    sdz[c] = sdy[c] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 10; ++j) dwa[j][c] = 0.f;
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    float gm[CPW];
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const float m = fmaf(a[c], y[b][c], bb[c]);  // == head_window's max of the window
+      const bool ps = m > 0.f;
+      const float p = ps ? m : (isnan(m) ? m : 0.f);
+      float g = 0.f;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        const float d = dls[b * 10 + j];
+        g += d * w[j][c];
+        if constexpr (WITH_DW) dwa[j][c] += d * p;
+      }
+      gm[c] = ps ? g : 0.f;
+      sdz[c] += valid ? gm[c] : 0.f;
+      sdy[c] += valid ? gm[c] * y[b][c] : 0.f;
+    }
+    if (valid)
+      *reinterpret_cast<float4*>(g2m + ((int64_t)b * QQ + pos) * 32 + c0) = make_float4(gm[0], gm[1], gm[2], gm[3]);
+  }
+  if (WITH_DW && valid) {
+    float* dst = dW + (int64_t)c0 * QQ + pos;
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (j < NC)
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) __builtin_nontemporal_store(scale * dwa[j][c], dst + ((int64_t)j * 32 + c) * QQ);
+  }
+  const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    const float s0 = wave_sum(sdz[c]);
+    const float s1 = wave_sum(sdy[c]);
+    if (lane == 0) {
+      partial[((int64_t)(c0 + c) * nblk + blk) * 2 + 0] = s0;
+      partial[((int64_t)(c0 + c) * nblk + blk) * 2 + 1] = s1;
+    }
+  }
+}
+
 constexpr int HD_FWD_NW = 8;
 constexpr int HD_BWD_NW = 16;
 
@@ -253,13 +342,13 @@ int tds_head_fwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
 
 // partial: double [nblk][B*NC]; sums: double [B*NC] workspace
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
-                 float* logits, float* xout, int B, int P, int NC, hipStream_t st) {
+                 float* logits, float* xout, float* yaout, int B, int P, int NC, hipStream_t st) {
   const int Q = P / 2;
   if (B > HD_MAXB || NC > 10 || Q < 1) return -1;
   head_lds_limits();
   const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
   hipLaunchKernelGGL(head_fwd_kernel<HD_FWD_NW>, grid, dim3(64 * HD_FWD_NW), HD_LDS, st,
-                     reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, xout, B, P, Q, NC);
+                     reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, xout, yaout, B, P, Q, NC);
   const int nblk = grid.x * grid.y, BN = B * NC;
   tds_reduce_partials(partial, sums, BN, nblk, BN, 0, BN, st);
   hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);
@@ -281,4 +370,30 @@ int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const flo
     hipLaunchKernelGGL((head_bwd_kernel<HD_BWD_NW, false>), grid, dim3(64 * HD_BWD_NW), HD_LDS, st,
                        reinterpret_cast<const float4*>(y2), Wfc, aff2, dlogits, dW, g2m, partial, B, P, Q, NC, scale);
   return 0;
+}
+
+int tds_head_bwd_ya_max_batch() { return HD_MAXB_YA; }
+
+// backward from saved argmax values (head_bwd_ya_kernel); partial: double [32][nblk][2]
+int tds_head_bwd_ya_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
+
+bool tds_head_bwd_ya_supported(int B, int P, int NC) { return B >= 1 && B <= HD_MAXB_YA && NC <= 10 && P >= 2; }
+
+int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
+                    double* partial, int B, int P, int NC, float scale, hipStream_t st) {
+  const int Q = P / 2;
+  if (!tds_head_bwd_ya_supported(B, P, NC)) return -1;
+  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
+#define TDS_HBY(NB)                                                                                                \
+  case NB:                                                                                                         \
+    if (dW)                                                                                                        \
+      hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW, g2m,  \
+                         partial, Q, NC, scale);                                                                   \
+    else                                                                                                           \
+      hipLaunchKernelGGL((head_bwd_ya_kernel<false, NB>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW, g2m, \
+                         partial, Q, NC, scale);                                                                   \
+    return 0;
+  switch (B) { TDS_HBY(1) TDS_HBY(2) TDS_HBY(3) TDS_HBY(4) TDS_HBY(5) TDS_HBY(6) TDS_HBY(7) TDS_HBY(8) default: break; }
+#undef TDS_HBY
+  return -1;
 }

@@ -87,7 +87,12 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
 int tds_head_fwd_nblk(int Q);
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
-                 float* logits, float* xout, int B, int P, int NC, hipStream_t st);
+                 float* logits, float* xout, float* yaout, int B, int P, int NC, hipStream_t st);
+int tds_head_bwd_ya_max_batch();
+int tds_head_bwd_ya_nblk(int Q);
+bool tds_head_bwd_ya_supported(int B, int P, int NC);
+int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
+                    double* partial, int B, int P, int NC, float scale, hipStream_t st);
 int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
                  double* partial, int B, int P, int NC, float scale, hipStream_t st);
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,

@@ -104,11 +104,14 @@ class _Head(torch.autograd.Function):
         if ex is not None:
             B, P = y2.shape[0], y2.shape[1]
             x_out = torch.empty((B, wfc.shape[1]), device=y2.device, dtype=torch.float32)
+        # y2 at each pooling window's argmax, in the fc's flatten order: the backward
+        # streams it (360 MB at 3000^2) instead of y2 (1.44 GB)
+        ya = torch.empty((y2.shape[0], wfc.shape[1]), device=y2.device, dtype=torch.float32)
         logits, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
-                                                      bfc, x_out)
+                                                      bfc, x_out, ya)
         if ex is not None and not ex.begin(x_out):
             raise RuntimeError("activation exchange refused to start after ready() agreed")
-        ctx.save_for_backward(y2, stats2, aff2, g2, wfc)
+        ctx.save_for_backward(y2, stats2, aff2, g2, wfc, ya)
         ctx.wfc_param = wfc
         ctx.ex = ex
         ctx.link = link
@@ -116,20 +119,20 @@ class _Head(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dlogits):
-        y2, stats2, aff2, g2, wfc = ctx.saved_tensors
+        y2, stats2, aff2, g2, wfc, ya = ctx.saved_tensors
         dlogits = dlogits.contiguous().float()
         ex = ctx.ex
         ops = _ext.ops()
         if ex is not None:
             # fc gradients come from the activation exchange (parallel/factored.py)
             _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, None, 1.0,
-                                                                     False)
+                                                                     False, ya)
             ex.defer(dlogits)
             dW = dbfc = None
         else:
             dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[10] else None, wfc.shape, wfc)
             dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, dw_out,
-                                                                         1.0)
+                                                                         1.0, True, ya)
         link = ctx.link
         link.g2m, link.kbuf, link.aff2 = g2m, kbuf, aff2
         # y2's gradient is carried by the link; autograd gets a zero-stride placeholder
