@@ -1,5 +1,5 @@
 """Timing-only variants of the conv2 kernels (conv2_bf16x3.hip, TDS_CONV2_DIAG):
-0 real, 1 no MFMA, 2 no LDS operand reads, 3 no global tile loads.
+0 real, 1 no MFMA, 2 no LDS operand reads, 3 no global tile loads, 4 (forward v2 only) no y2 stores.
 Tells which resource bounds each kernel at the bench shape (B=5, P=1500).
 Outputs of variants 1-3 are garbage by design."""
 import json
@@ -27,7 +27,7 @@ def main():
     aff2 = torch.cat([torch.rand(32, device=dev) + 0.5, torch.randn(32, device=dev)])
     kbuf = torch.randn(96, device=dev)
     res = {}
-    for diag in (0, 1, 2, 3):
+    for diag in (0, 1, 2, 3, 4):
         os.environ["TDS_CONV2_DIAG"] = str(diag)
         times = {}
         for name, fn in (("fwd", lambda: ops.fused_conv2_forward(p1, wp, b2)),
@@ -67,6 +67,24 @@ def main():
             ab.setdefault(f"bwd_v{ver}", []).append(round(s.elapsed_time(e) / 10, 4))
     os.environ.pop("TDS_CONV2_BWD")
     print("fused backward A/B (ms):", ab, flush=True)
+    fab = {}
+    fwd = lambda: ops.fused_conv2_forward(p1, wp, b2)  # noqa: E731
+    for rep in range(3):
+        for ver in ("1", "2"):
+            os.environ["TDS_CONV2_FWD"] = ver
+            for _ in range(2):
+                fwd()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                fwd()
+            e.record()
+            torch.cuda.synchronize()
+            fab.setdefault(f"fwd_v{ver}", []).append(round(s.elapsed_time(e) / 10, 4))
+    os.environ.pop("TDS_CONV2_FWD")
+    print("forward A/B (ms):", fab, flush=True)
+    ab.update(fab)
     print(json.dumps({"B": B, "P": P, "ms": res, "bwd_ab": ab}))
 
 

@@ -104,8 +104,9 @@ std::tuple<Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& w
   need(p1, at::kFloat, {B, P, P, 16}, "p1");
   need(wp, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
   need(b2, at::kFloat, {32}, "conv2.bias");
+  TORCH_CHECK(B <= 255 && P <= 32760, "fused_conv2_forward: batch <= 255 and P <= 32760 (tile-order table packing)");
   c10::DeviceGuard guard(p1.device());
-  const int nwg = tds_conv2_num_wg();
+  const int nwg = tds_conv2_fwd_num_wg();
   auto y2 = at::empty({B, P, P, 32}, p1.options());
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
   tds_conv2_fwd_bf16x3(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), y2.data_ptr<float>(),
@@ -286,6 +287,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
   need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
+  TORCH_CHECK(B <= 255 && P <= 32760, "fused_conv2_backward_y2: batch <= 255 and P <= 32760 (tile-order table packing)");
   c10::DeviceGuard guard(p1.device());
   hipStream_t st = stream_of(p1);
   const int nwg = tds_conv2_bwd_fused_num_wg();

@@ -991,8 +991,20 @@ static int conv2_diag() {
     default: hipLaunchKernelGGL(KERNEL<0>, __VA_ARGS__); break;                       \
   }
 
+// Which conv2 forward runs: 2 = conv2_fwd2_kernel (several 4-wave workgroups per CU, weights in
+// registers, LDS-DMA staging; conv2_fwd2.hip; default), 1 = conv2_fwd_bf16x3_kernel below.
+int tds_conv2_fwd_version() {
+  const char* e = std::getenv("TDS_CONV2_FWD");
+  return (e && std::atoi(e) == 1) ? 1 : 2;
+}
+int tds_conv2_fwd_num_wg() { return tds_conv2_fwd_version() == 2 ? tds_conv2_fwd2_num_wg() : tds_conv2_num_wg(); }
+
 void tds_conv2_fwd_bf16x3(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg,
                           int B, int P, hipStream_t st) {
+  if (tds_conv2_fwd_version() == 2) {
+    tds_conv2_fwd2(p1, wp, bias, y2, partial, nwg, B, P, st);
+    return;
+  }
   set_lds_limits();
   TDS_C2_DISPATCH(conv2_fwd_bf16x3_kernel, dim3(nwg), dim3(C2_THREADS), F_LDS, st,
                   reinterpret_cast<const uint4*>(p1), reinterpret_cast<const uint4*>(wp), bias, y2, partial, B, P);

@@ -200,6 +200,7 @@ struct B2Args {
   const uint4* __restrict__ p1;
   float* __restrict__ dp1;
   float* __restrict__ slab;
+  const int* __restrict__ order;  // blocked tile order (tds_tile_order)
   int B, P, Q, tiles_r, tiles_c, per_img, total;
 };
 
@@ -211,7 +212,7 @@ struct B2Tile {
 __device__ __forceinline__ B2Tile b2_decode(const B2Args& a, int t) {
   B2Tile x;
   int tr, tc;
-  blocked_tile<32, 16, 4>(t, a.per_img, a.tiles_r, a.tiles_c, x.b, tr, tc);
+  tile_from_order(a.order, t, x.b, tr, tc);
   x.r0 = tr * B2_TH;
   x.c0 = tc * B2_TC;
   x.interior = x.r0 >= 2 && x.c0 >= 2 && x.r0 + B2_SR - 2 <= 2 * a.Q && x.c0 + B2_SC - 2 <= 2 * a.Q;
@@ -525,12 +526,12 @@ template <int DIAG>
 __global__ __launch_bounds__(B2_THREADS, 2) void conv2_bwd2_kernel(
     const float4* __restrict__ y2, const float4* __restrict__ g2m, const float* __restrict__ aff2,
     const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
-    float* __restrict__ dp1, float* __restrict__ slab, int B, int P, int Q) {
+    float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ order, int B, int P, int Q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform role: scalar branches
   B2Args a;
-  a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab;
+  a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.order = order;
   a.B = B; a.P = P; a.Q = Q;
   a.tiles_c = (P + B2_TC - 1) / B2_TC;
   a.tiles_r = (P + B2_TH - 1) / B2_TH;
@@ -582,10 +583,12 @@ void tds_conv2_bwd2(const float* y2, const float* g2m, const float* aff2, const 
   const float4* gm = reinterpret_cast<const float4*>(g2m);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wd);
+  const int* order = tds_tile_order(B, (P + B2_TH - 1) / B2_TH, (P + B2_TC - 1) / B2_TC);
+  if (!order) return;  // shape beyond the table's packing (B > 255 or > 4095 tiles per side)
   switch (conv2_diag_env()) {
-    case 1: hipLaunchKernelGGL(conv2_bwd2_kernel<1>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, B, P, Q); break;
-    case 2: hipLaunchKernelGGL(conv2_bwd2_kernel<2>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, B, P, Q); break;
-    case 3: hipLaunchKernelGGL(conv2_bwd2_kernel<3>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, B, P, Q); break;
-    default: hipLaunchKernelGGL(conv2_bwd2_kernel<0>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, B, P, Q); break;
+    case 1: hipLaunchKernelGGL(conv2_bwd2_kernel<1>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
+    case 2: hipLaunchKernelGGL(conv2_bwd2_kernel<2>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
+    case 3: hipLaunchKernelGGL(conv2_bwd2_kernel<3>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
+    default: hipLaunchKernelGGL(conv2_bwd2_kernel<0>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
   }
 }

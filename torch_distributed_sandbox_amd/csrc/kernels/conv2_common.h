@@ -68,3 +68,20 @@ __device__ __forceinline__ void blocked_tile(int t, int per_img, int tiles_r, in
 }
 
 }  // namespace tds
+
+namespace tds {
+
+// Device table of the blocked tile order (blocked_tile<32, 16, 4>), one int per work index:
+// b << 24 | tile_row << 12 | tile_col.  A decode is then one scalar load instead of six
+// runtime integer divisions on the scalar unit (≈400 SALU instructions per tile per wave,
+// measured with SQ_INSTS_SALU).  Built on the host once per shape and cached.
+const int* tds_tile_order(int B, int tiles_r, int tiles_c);
+
+__device__ __forceinline__ void tile_from_order(const int* __restrict__ order, int t, int& b, int& tr, int& tc) {
+  const int v = order[t];
+  b = v >> 24;
+  tr = (v >> 12) & 4095;
+  tc = v & 4095;
+}
+
+}  // namespace tds

@@ -1,0 +1,267 @@
+// conv2 forward v2 (Conv2d(16, 32, 5, pad 2), mnist_onegpu.py:20):
+// y2 = conv(p1) + b2 in NHWC fp32, plus BN2 batch-statistic partials, on
+// v_mfma_f32_16x16x32_bf16 with the bf16x3 split, laid out for SEVERAL small workgroups
+// per CU (the design of conv2_bwd2.hip):
+//   * 4 waves per workgroup, output tile 8 rows x 16 columns (staged p1: 12 x 20 records);
+//   * weights in REGISTERS: wave w owns co half nt = w & 1 and output rows 4(w>>1) .. +3,
+//     all 13 K-steps of its half (13 x (hi, lo) fragments = 104 VGPRs), loaded once;
+//   * p1 staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs, no VALU), double-buffered:
+//     tile t+1 streams in while tile t is on the MFMAs;
+//   * the epilogue of tile t (y2 stores + statistics) runs after tile t+1's DMA is issued,
+//     from a second accumulator set, so the stores drain under the next MFMAs.
+// K order and input-row sharing as conv2_fwd_bf16x3_kernel: K-step s < 10 pairs taps
+// (ky = s>>1, kx = 2(s&1) + (g>>1)) so one staged input row R serves output rows R - ky;
+// s = 10 + kp pairs (ky = 2kp + (g>>1), kx = 4) with lane groups 2-3 reading row R+1.
+#include "conv2_common.h"
+#include "launchers.h"
+
+namespace tds {
+
+constexpr int F2_TH = 8, F2_TC = 16;
+constexpr int F2_SR = F2_TH + 4, F2_SC = F2_TC + 4;  // 12 x 20 staged records
+constexpr int F2_REC = F2_SR * F2_SC;                  // 240
+constexpr int F2_THREADS = 256;
+constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records per plane
+constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records, 240 used)
+constexpr int F2_PBUF = 2 * F2_PPLANE;                 // hi + lo
+constexpr int F2_STAGE = F2_TH * F2_TC * 32 * 4;        // finished tile: 8 x 16 px x 32 co fp32 = 16 KiB
+constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
+constexpr int F2_LDS = F2_OFF_S + 2 * F2_STAGE;        // + double-buffered output staging: 64 KiB
+constexpr int F2_DMA_PER_WAVE = 2 * F2_PGROUPS / (F2_THREADS / 64);  // 4
+static_assert(F2_LDS % 16 == 0, "LDS carve");
+
+// 16 zero bytes: the DMA source of staged records outside the image
+__device__ __attribute__((aligned(16))) uint32_t g_f2_zero[4] = {0u, 0u, 0u, 0u};
+
+struct F2Tile {
+  int b, r0, c0;
+};
+
+template <int DIAG, int WV>
+__device__ __forceinline__ void f2_dma(const uint4* __restrict__ p1, const F2Tile& x, int P, char* buf, int lane) {
+  if constexpr (DIAG == 3) return;
+  const char* base = reinterpret_cast<const char*>(p1) + (((int64_t)x.b * P + x.r0 - 2) * P + (x.c0 - 2)) * 64;
+#pragma unroll
+  for (int j = 0; j < F2_DMA_PER_WAVE; ++j) {
+    const int k = WV * F2_DMA_PER_WAVE + j;
+    const int pl = k / F2_PGROUPS, rg = k - pl * F2_PGROUPS;
+    const int px = rg * 32 + (lane >> 1), half = lane & 1;
+    const int rr = px / F2_SC, cc = px - rr * F2_SC;
+    const int gr = x.r0 - 2 + rr, gc = x.c0 - 2 + cc;
+    const bool ok = px < F2_REC && gr >= 0 && gr < P && gc >= 0 && gc < P;
+    const char* src = ok ? base + ((int64_t)rr * P + cc) * 64 + pl * 32 + half * 16
+                         : reinterpret_cast<const char*>(g_f2_zero);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + pl * F2_PPLANE + rg * 1024),
+                                     16, 0, 0);
+  }
+}
+
+// One wave's MFMAs for one tile: rows 4RH .. 4RH+3 of the tile, co half NT (weights in W).
+// The 24 A-fragment row loads (3 tap groups x 8 staged rows) form one sequence read through
+// a 4-deep register ring, 3 rows ahead of the MFMAs that use them: the rows at a group's
+// edges feed only 1-2 MFMA triples, too few to hide an LDS round trip one row ahead.
+template <int DIAG>
+__device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13][2], f32x4 (&acc)[4], int RH, int lane) {
+  constexpr int DEPTH = 4;
+  const int li = lane & 15, g = lane >> 4;
+  const int boff = (g & 1) * 16;  // ci half of the 32-B record
+  const char* ph = buf;
+  const char* pl = buf + F2_PPLANE;
+#pragma unroll
+  for (int o = 0; o < 4; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 ah[DEPTH], al[DEPTH];
+  // load i: group i / 8 (0, 1: kx pairs 2a + (g>>1); 2: kx = 4 with lane groups 2-3 one row down)
+  auto load_a = [&](int i) {
+    const int grp = i >> 3, R = i & 7;
+    int rec;
+    if (grp < 2) {
+      rec = (4 * RH + R) * F2_SC + li + 2 * grp + (g >> 1);
+    } else {
+      int row = 4 * RH + R + (g >> 1);
+      if (row > F2_SR - 1) row = F2_SR - 1;  // only reached with a zero weight (ky = 5)
+      rec = row * F2_SC + li + 4;
+    }
+    ah[i % DEPTH] = lds8<DIAG>(ph + rec * 32 + boff);
+    al[i % DEPTH] = lds8<DIAG>(pl + rec * 32 + boff);
+  };
+#pragma unroll
+  for (int i = 0; i < DEPTH - 1; ++i) load_a(i);
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    if (i + DEPTH - 1 < 24) load_a(i + DEPTH - 1);
+    __builtin_amdgcn_sched_barrier(0);  // keep the ring's loads ahead of this row's MFMAs
+    const int grp = i >> 3, R = i & 7, cur = i % DEPTH;
+    if (grp < 2) {
+#pragma unroll
+      for (int ky = 0; ky < 5; ++ky) {
+        const int o = R - ky;
+        if (o >= 0 && o < 4)
+          acc[o] = mma3<DIAG>(ah[cur], al[cur], __builtin_bit_cast(s16x8, W[2 * ky + grp][0]),
+                              __builtin_bit_cast(s16x8, W[2 * ky + grp][1]), acc[o]);
+      }
+    } else {
+#pragma unroll
+      for (int kp = 0; kp < 3; ++kp) {
+        const int o = R - 2 * kp;
+        if (o >= 0 && o < 4)
+          acc[o] = mma3<DIAG>(ah[cur], al[cur], __builtin_bit_cast(s16x8, W[10 + kp][0]),
+                              __builtin_bit_cast(s16x8, W[10 + kp][1]), acc[o]);
+      }
+    }
+  }
+}
+
+// A finished tile goes to LDS first ([row][px][32 co], 16-B chunks XOR-swizzled by px & 7 so
+// the MFMA-layout writes are conflict-free), then the workgroup stores it as full 128-B
+// pixel records, 1 KiB contiguous per wave-instruction.  (Stored straight from the MFMA
+// layout, each wave wrote 64-B halves of lines whose other half came from another wave:
+// the y2 writes then cost ~0.3 ms more, TDS_CONV2_DIAG=4.)
+__device__ __forceinline__ int f2_stage_off(int row, int px, int chunk) {
+  return ((row * F2_TC + px) * 8 + (chunk ^ (px & 7))) * 16;
+}
+
+// stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li]
+__device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, int P, int RH, int NT,
+                                         int lane, float bco, float& s_acc, float& q_acc) {
+  const int li = lane & 15, g = lane >> 4;
+  const int co = 16 * NT + li;
+#pragma unroll
+  for (int o = 0; o < 4; ++o) {
+    const int row = 4 * RH + o;
+    const bool rok = x.r0 + row < P;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int px = 4 * g + r;
+      const float v = acc[o][r];  // y2 - b2: statistics shifted by the bias
+      if (rok && x.c0 + px < P) {
+        s_acc += v;
+        q_acc += v * v;
+      }
+      *reinterpret_cast<float*>(stage + f2_stage_off(row, px, co >> 2) + (co & 3) * 4) = v + bco;
+    }
+  }
+}
+
+// the whole workgroup stores a staged tile: thread e, i -> float4 q = e + 256 i of
+// [row 8][px 16][chunk 8]: a wave-instruction writes 1 KiB of one y2 row
+template <int DIAG>
+__device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, float* __restrict__ y2, int P) {
+  if constexpr (DIAG == 4) return;  // timing-only: no y2
+  const int e = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < F2_STAGE / 16 / F2_THREADS; ++i) {
+    const int q = e + F2_THREADS * i;
+    const int row = q >> 7, px = (q >> 3) & 15, chunk = q & 7;
+    const int gr = x.r0 + row, gc = x.c0 + px;
+    const float4 v = *reinterpret_cast<const float4*>(stage + f2_stage_off(row, px, chunk));
+    if (gr < P && gc < P) *reinterpret_cast<float4*>(y2 + (((int64_t)x.b * P + gr) * P + gc) * 32 + chunk * 4) = v;
+  }
+}
+
+template <int DIAG, int WV>
+__device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
+                                       const float* __restrict__ bias, float* __restrict__ y2,
+                                       double* __restrict__ partial, const int* __restrict__ order, int B, int P,
+                                       char* smem) {
+  constexpr int NT = WV & 1, RH = WV >> 1;
+  const int lane = threadIdx.x & 63, li = lane & 15;
+  const int tiles_c = (P + F2_TC - 1) / F2_TC, tiles_r = (P + F2_TH - 1) / F2_TH;
+  const int per_img = tiles_c * tiles_r, total = per_img * B;
+  auto decode = [&](int t) {
+    F2Tile x;
+    int tr, tc;
+    tile_from_order(order, t, x.b, tr, tc);
+    x.r0 = tr * F2_TH;
+    x.c0 = tc * F2_TC;
+    return x;
+  };
+  // weights: fwd pack wp[hl][s][nt][g][co16][j8] -> uint4 index ((hl*13 + s)*2 + nt)*64 + lane
+  f32x4 W[13][2];
+#pragma unroll
+  for (int s = 0; s < 13; ++s)
+#pragma unroll
+    for (int hl = 0; hl < 2; ++hl) W[s][hl] = __builtin_bit_cast(f32x4, wpack[((hl * 13 + s) * 2 + NT) * 64 + lane]);
+  const float bco = bias[16 * NT + li];
+  float s_acc = 0.f, q_acc = 0.f;
+  f32x4 acc[4];
+  F2Tile prev{0, 0, 0};
+  bool have_prev = false;
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (t < total) f2_dma<DIAG, WV>(p1, decode(t), P, smem, lane);
+  int kk = 0;
+  for (; t < total; t += gridDim.x, ++kk) {
+    const F2Tile cur = decode(t);
+    // tile t's DMA landed (vmcnt(0) + barrier); p1 buffer (kk+1)&1 is free; the staged
+    // tile t-1 (stage (kk+1)&1) is complete
+    __syncthreads();
+    if (t + (int)gridDim.x < total) f2_dma<DIAG, WV>(p1, decode(t + gridDim.x), P, smem + ((kk + 1) & 1) * F2_PBUF, lane);
+    if (have_prev) f2_store<DIAG>(smem + F2_OFF_S + ((kk + 1) & 1) * F2_STAGE, prev, y2, P);
+    f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
+    f2_stage(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, P, RH, NT, lane, bco, s_acc, q_acc);
+    prev = cur;
+    have_prev = true;
+  }
+  __syncthreads();
+  if (have_prev) f2_store<DIAG>(smem + F2_OFF_S + ((kk - 1) & 1) * F2_STAGE, prev, y2, P);
+  // BN2 partials: reduce the 4 lane groups, then the two row-halves of this co half
+  s_acc += __shfl_xor(s_acc, 16, 64);
+  s_acc += __shfl_xor(s_acc, 32, 64);
+  q_acc += __shfl_xor(q_acc, 16, 64);
+  q_acc += __shfl_xor(q_acc, 32, 64);
+  __syncthreads();  // all operand reads done: reuse the LDS for the reduction
+  double* red = reinterpret_cast<double*>(smem);  // [4 waves][16 co][2]
+  if (lane < 16) {
+    red[(WV * 16 + li) * 2 + 0] = (double)s_acc;
+    red[(WV * 16 + li) * 2 + 1] = (double)q_acc;
+  }
+  __syncthreads();
+  if (WV == 0 && lane < 64) {
+    const int co = lane >> 1, k = lane & 1, nt = co >> 4, c16 = co & 15;
+    // waves with this co half: nt (rows 0-3) and nt + 2 (rows 4-7)
+    const double v = red[(nt * 16 + c16) * 2 + k] + red[((nt + 2) * 16 + c16) * 2 + k];
+    partial[((int64_t)co * gridDim.x + blockIdx.x) * 2 + k] = v;
+  }
+}
+
+template <int DIAG>
+__global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* __restrict__ p1,
+                                                                   const uint4* __restrict__ wpack,
+                                                                   const float* __restrict__ bias,
+                                                                   float* __restrict__ y2,
+                                                                   double* __restrict__ partial,
+                                                                   const int* __restrict__ order, int B, int P) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
+  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, y2, partial, order, B, P, smem);
+  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, y2, partial, order, B, P, smem);
+  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, y2, partial, order, B, P, smem);
+  else f2_run<DIAG, 3>(p1, wpack, bias, y2, partial, order, B, P, smem);
+}
+
+}  // namespace tds
+
+using namespace tds;
+
+// workgroups the v2 forward launches (BN2 partial rows): 2 per CU
+int tds_conv2_fwd2_num_wg() { return 2 * tds_conv2_num_wg(); }
+
+static int f2_diag_env() {
+  const char* e = std::getenv("TDS_CONV2_DIAG");
+  return e ? std::atoi(e) : 0;
+}
+
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg, int B,
+                    int P, hipStream_t st) {
+  const dim3 grid(nwg), block(F2_THREADS);
+  const uint4* pp = reinterpret_cast<const uint4*>(p1);
+  const uint4* w = reinterpret_cast<const uint4*>(wp);
+  const int* order = tds_tile_order(B, (P + F2_TH - 1) / F2_TH, (P + F2_TC - 1) / F2_TC);
+  if (!order) return;  // shape beyond the table's packing (B > 255 or > 4095 tiles per side)
+  switch (f2_diag_env()) {
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
+  }
+}

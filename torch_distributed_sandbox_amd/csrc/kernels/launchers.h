@@ -65,6 +65,11 @@ void tds_conv2_fwd_bf16x3(const void* p1, const short* wp, const float* bias, fl
 void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
                          const short* wd, float* dp1, float* slab, float* dw, float* db, float scale, int nwg, int B,
                          int P, hipStream_t st);
+int tds_conv2_fwd_version();
+int tds_conv2_fwd_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
+int tds_conv2_fwd2_num_wg();
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg, int B,
+                    int P, hipStream_t st);
 int tds_conv2_bwd_version();
 int tds_conv2_bwd_fused_num_wg();  // slab rows the fused backward needs (workgroups it launches)
 int tds_conv2_bwd2_num_wg();
