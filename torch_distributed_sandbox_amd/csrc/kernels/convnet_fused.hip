@@ -20,6 +20,8 @@
 //                     pooled window with p1 > 0, so per (pooled pixel, channel) one y1 value
 //                     (25 FMA) and one rank-1 update of sum dz1 x xpatch (25 FMA).
 //   l1_finalize     : dW1 = a1*sum(dz1 xpatch) + a2*(W1 G + b1 S) + a3*S, db1, dgamma1, dbeta1.
+#include <cstdlib>
+
 #include "bf16x3.h"
 #include "launchers.h"
 
@@ -130,6 +132,182 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
               acc[a][c] = mfma16x4(wa[s], bv, acc[a][c]);
             }
         }
+        {
+          // BN1 affine -> 2x2 max-pool (first max in scan order; torch's NaN rule on the
+          // rare NaN window) -> ReLU -> bf16 hi|lo record + 1-byte argmax
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            const int col = c0 + (2 * sp + c) * 16 + li;     // conv column of this lane
+            const int prow = (r0 + 4 * wv + 2 * rp) >> 1;    // pooled row
+            const int pcol = col >> 1;
+            float pv[4], zz[4][4];
+            uint32_t ixw = 0;
+            float nsum = 0.f;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float z0 = fmaf(ea[r], acc[0][c][r], ebb[r]);
+              const float z1 = fmaf(ea[r], acc[1][c][r], ebb[r]);
+              const float z0n = dpp_xor1(z0);
+              const float z1n = dpp_xor1(z1);
+              zz[r][0] = z0; zz[r][1] = z0n; zz[r][2] = z1; zz[r][3] = z1n;
+              float m = z0;
+              uint32_t a = 0;
+              if (z0n > m) { m = z0n; a = 1; }
+              if (z1 > m) { m = z1; a = 2; }
+              if (z1n > m) { m = z1n; a = 3; }
+              pv[r] = fmaxf(m, 0.f);
+              ixw |= a << (8 * r);
+              nsum += (z0 + z0n) + (z1 + z1n);
+            }
+            if (__builtin_amdgcn_ballot_w64(isnan(nsum)) != 0) {
+              // rare NaN window (wave-uniform branch): torch's rule, update when
+              // (v > max || isnan(v)) in scan order; relu(NaN) = NaN
+              ixw = 0;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                float m = zz[r][0];
+                uint32_t a = 0;
+#pragma unroll
+                for (int q = 1; q < 4; ++q)
+                  if (zz[r][q] > m || isnan(zz[r][q])) { m = zz[r][q]; a = q; }
+                pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
+                ixw |= a << (8 * r);
+              }
+            }
+            uint32_t h01, l01, h23, l23;
+            split2_bf16(pv[0], pv[1], h01, l01);
+            split2_bf16(pv[2], pv[3], h23, l23);
+            if ((li & 1) == 0 && prow < P && pcol < PW) {
+              const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
+              uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
+              dst[g] = make_uint2(h01, h23);
+              dst[4 + g] = make_uint2(l01, l23);
+              reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] = ixw;
+            }
+          }
+        }
+      }
+    }
+  }
+}
+
+// conv1 on v_mfma_f32_16x16x32_bf16 with the bf16x3 split (bf16x3.h): K = 32 slots per lane
+// group g: taps (ky = g, kx = 0..4) and the row-4 taps spread over g = 0 (kx 0..2) and g = 1
+// (kx 3, 4); the rest are zero-weight pads.  x is staged in LDS as one word per value
+// (bf16 hi << 16 | bf16 lo), so a lane's 8 taps are 8 ds_read_b32 + 8 v_perm; 3 MFMAs per
+// 16 px x 16 co replace 7 v_mfma_f32_16x16x4_f32 (4.7x fewer MFMA cycles).
+__device__ __forceinline__ int l1b_tap(int g, int j) {
+  if (j < 5) return g * 5 + j;
+  if (g == 0) return 20 + (j - 5);           // (4, 0..2)
+  if (g == 1 && j < 7) return 23 + (j - 5);  // (4, 3..4)
+  return -1;
+}
+
+__global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+                                                      const float* __restrict__ b1, const float* __restrict__ aff,
+                                                      uint4* __restrict__ p1, uint8_t* __restrict__ idx1, int B,
+                                                      int H, int W) {
+  __shared__ __attribute__((aligned(16))) uint32_t xs[L1_XR * L1_XS];  // x as (bf16 hi << 16 | bf16 lo)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int P = H / 2, PW = W / 2;
+  const int tiles_c = (W + L1_TC - 1) / L1_TC, tiles_r = (H + L1_TR - 1) / L1_TR;
+  const int per_img = tiles_c * tiles_r, total = per_img * B;
+
+  // A operand (weights) in registers as bf16 hi / lo: lane -> co = li, k = 8g + j -> tap
+  // l1b_tap(g, j) (rows ky = g plus row 4 spread over g = 0, 1; pads carry weight 0)
+  s16x8 wah, wal;
+  int koff[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int tp = l1b_tap(g, j);
+    const float wv = tp >= 0 ? w1[li * 25 + tp] : 0.f;
+    unsigned short h, l;
+    split_bf16(wv, h, l);
+    wah[j] = (short)h;
+    wal[j] = (short)l;
+    koff[j] = tp >= 0 ? (tp / 5) * L1_XS + (tp % 5) : 0;
+  }
+
+  // per-lane epilogue constants for co = 4g + r: z = ea * (acc + b1) + eb = ea * acc + ebb
+  float ea[4], ebb[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ea[r] = aff[4 * g + r];
+    ebb[r] = fmaf(ea[r], b1[4 * g + r], aff[16 + 4 * g + r]);
+  }
+
+  // x tile staging: LDS column 0 <-> global column c0-4 (16-B aligned since W % 4 == 0),
+  // 20 rows x 18 float4; the next tile's loads are issued before this tile's MFMAs.
+  constexpr int NV = L1_XR * 18;
+  constexpr int PER = (NV + 255) / 256;
+  float4 pre[PER];
+  auto load_tile = [&](int t) {
+    const int b = t / per_img, rem = t - b * per_img;
+    const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
+    const float* xb = x + (int64_t)b * H * W;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e < NV) {
+        const int rr = e / 18, cv = e - rr * 18;
+        const int gr = r0 - 2 + rr, gc = c0 - 4 + 4 * cv;
+        if (gr >= 0 && gr < H && gc >= 0 && gc < W) v = *reinterpret_cast<const float4*>(xb + (int64_t)gr * W + gc);
+      }
+      pre[u] = v;
+    }
+  };
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (t < total) load_tile(t);
+  for (; t < total; t += gridDim.x) {
+    const int b = t / per_img, rem = t - b * per_img;
+    const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = tid + 256 * u;
+      if (e < NV) {
+        const int rr = e / 18, cv = e - rr * 18;
+        uint32_t h01, l01, h23, l23;
+        split2_bf16(pre[u].x, pre[u].y, h01, l01);
+        split2_bf16(pre[u].z, pre[u].w, h23, l23);
+        uint4 v;  // per value: hi in the upper half, lo in the lower half
+        v.x = __builtin_amdgcn_perm(h01, l01, 0x05040100u);
+        v.y = __builtin_amdgcn_perm(h01, l01, 0x07060302u);
+        v.z = __builtin_amdgcn_perm(h23, l23, 0x05040100u);
+        v.w = __builtin_amdgcn_perm(h23, l23, 0x07060302u);
+        *reinterpret_cast<uint4*>(xs + rr * L1_XS + 4 * cv) = v;
+      }
+    }
+    __syncthreads();
+    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
+#pragma unroll
+    for (int rp = 0; rp < 2; ++rp) {
+#pragma unroll
+      for (int sp = 0; sp < 2; ++sp) {
+        // 4 tiles: rows (4wv + 2rp + {0,1}) x segments (2sp + {0,1}) of 16 pixels
+        f32x4 acc[2][2];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int c = 0; c < 2; ++c) {
+            // B = x patches: lane (px = li, g) gathers its 8 taps as packed hi|lo words
+            const int row = 4 * wv + 2 * rp + a, seg = 2 * sp + c;
+            const uint32_t* src = xs + row * L1_XS + 2 + seg * 16 + li;  // +2: tile origin is c0-4
+            uint32_t u[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) u[j] = src[koff[j]];
+            s16x8 bh, bl;
+            uint32_t* hp = reinterpret_cast<uint32_t*>(&bh);
+            uint32_t* lp = reinterpret_cast<uint32_t*>(&bl);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
+              lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+            }
+            acc[a][c] = mfma_bf16x3(wah, wal, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
+          }
         {
           // BN1 affine -> 2x2 max-pool (first max in scan order; torch's NaN rule on the
           // rare NaN window) -> ReLU -> bf16 hi|lo record + 1-byte argmax
@@ -715,10 +893,16 @@ void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int
   hipLaunchKernelGGL(l1_gram_kernel, dim3(1), dim3(256), 0, st, ac_sum, strips, x, B, H, W, w1, gram, sums);
 }
 
+// TDS_L1_CONV=1 selects the exact-fp32 MFMA conv1 (l1_conv_kernel); default: bf16x3 (l1_conv_bf3_kernel)
 void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
                   int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(l1_conv_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
-                     idx1, B, H, W);
+  const char* e = std::getenv("TDS_L1_CONV");
+  if (e && std::atoi(e) == 1)
+    hipLaunchKernelGGL(l1_conv_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
+                       idx1, B, H, W);
+  else
+    hipLaunchKernelGGL(l1_conv_bf3_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
+                       idx1, B, H, W);
 }
 
 void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
