@@ -49,6 +49,11 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal only (tools/steps_multirank_rehearsal.txt): several ranks on one GPU with a
+    # host-side backend (gloo), to exercise the multi-rank code path where RCCL refuses a
+    # shared device.  Never set by the driver.
+    if os.environ.get("TDS_BENCH_SHARED_DEVICE") is not None:
+        local_rank = int(os.environ["TDS_BENCH_SHARED_DEVICE"])
     if world != args.gpus:
         print(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}; launch N>1 with torch.distributed.run",
               file=sys.stderr)
