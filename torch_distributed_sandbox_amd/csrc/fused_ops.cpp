@@ -179,7 +179,7 @@ struct HeadBwd {
 static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
                                   const c10::optional<Tensor>& gamma2, const Tensor& wfc,
                                   const c10::optional<Tensor>& dw_out, double scale, bool compute_dw,
-                                  const c10::optional<Tensor>& ya = c10::nullopt) {
+                                  const c10::optional<Tensor>& ya = c10::nullopt, double update_lr = 0.0) {
   const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
   const int64_t NC = wfc.size(0);
@@ -207,11 +207,15 @@ static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const
   if (use_ya) {
     // saved argmax values: stream ya (B*32*Q*Q floats) instead of y2
     need(*ya, at::kFloat, {B, 32 * Q * Q}, "ya");
+    // update_lr > 0: also apply SGD to wfc in place (optimizer step fused into the backward)
     rc = tds_head_bwd_ya(ya->data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
                          dlogits.data_ptr<float>(), compute_dw ? r.dW.data_ptr<float>() : nullptr,
                          r.g2m.data_ptr<float>(), partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale,
-                         st);
+                         (update_lr > 0.0 && compute_dw) ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr,
+                         (float)update_lr, st);
   }
+  TORCH_CHECK(update_lr <= 0.0 || (use_ya && rc == 0 && compute_dw),
+              "fused_head_backward_g2m: update_lr needs the saved-argmax (ya) path with compute_dw");
   if (rc != 0) {
     rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(), dlogits.data_ptr<float>(),
                       compute_dw ? r.dW.data_ptr<float>() : nullptr, r.g2m.data_ptr<float>(),
@@ -249,9 +253,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward_g2m(
     const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
     const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
-    bool compute_dw, const c10::optional<Tensor>& ya) {
+    bool compute_dw, const c10::optional<Tensor>& ya, double update_lr) {
   c10::DeviceGuard guard(y2.device());
-  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw, ya);
+  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw, ya, update_lr);
   return {r.dW, r.dbfc, r.dgamma, r.dbeta, r.g2m, r.kbuf};
 }
 
@@ -358,7 +362,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
         &fused_conv2_backward);
   m.def(
       "fused_head_backward_g2m(Tensor dlogits, Tensor y2, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor wfc, "
-      "Tensor(a!)? dw_out, float scale, bool compute_dw=True, Tensor? ya=None) -> "
+      "Tensor(a!)? dw_out, float scale, bool compute_dw=True, Tensor? ya=None, float update_lr=0.0) -> "
       "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward_g2m);
   m.def(

@@ -245,11 +245,14 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restr
 // before any use (60 x 4 B in flight per lane).
 // (A persistent two-register-set pipelined variant ran out of SGPRs for its 100 plane
 // offsets and was slower; see docs/KERNELS.md.)  Outputs as head_bwd_kernel.
-template <bool WITH_DW, int NB>  // NB = images per rank (compile-time: exact register footprint)
-__global__ __launch_bounds__(512, 2) void head_bwd_ya_kernel(const float* __restrict__ ya, const float* __restrict__ Wfc,
+// With UPD (optimizer step fused into the backward, world size 1 only: ops/fused_update.py)
+// the kernel also writes W - lr * dW over W (each element read and written by one lane).
+template <bool WITH_DW, int NB, bool UPD>  // NB = images per rank (compile-time: exact register footprint)
+__global__ __launch_bounds__(512, 2) void head_bwd_ya_kernel(const float* __restrict__ ya, const float* Wfc,
                                                              const float* __restrict__ aff2, const float* __restrict__ dl,
                                                              float* __restrict__ dW, float* __restrict__ g2m,
-                                                             double* __restrict__ partial, int Q, int NC, float scale) {
+                                                             double* __restrict__ partial, int Q, int NC, float scale,
+                                                             float* Wupd, float lr) {
   constexpr int CPW = 4;
   __shared__ float dls[NB * 10];  // dlogits: broadcast LDS reads (as scalars they cost ~50 SGPRs and spill)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -305,7 +308,11 @@ __global__ __launch_bounds__(512, 2) void head_bwd_ya_kernel(const float* __rest
     for (int j = 0; j < 10; ++j)
       if (j < NC)
 #pragma unroll
-        for (int c = 0; c < CPW; ++c) __builtin_nontemporal_store(scale * dwa[j][c], dst + ((int64_t)j * 32 + c) * QQ);
+        for (int c = 0; c < CPW; ++c) {
+          const float gd = scale * dwa[j][c];
+          __builtin_nontemporal_store(gd, dst + ((int64_t)j * 32 + c) * QQ);
+          if constexpr (UPD) Wupd[((int64_t)j * 32 + c0 + c) * QQ + pos] = w[j][c] - lr * gd;  // torch SGD: p -= lr*g
+        }
   }
   const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
 #pragma unroll
@@ -380,18 +387,22 @@ int tds_head_bwd_ya_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
 bool tds_head_bwd_ya_supported(int B, int P, int NC) { return B >= 1 && B <= HD_MAXB_YA && NC <= 10 && P >= 2; }
 
 int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
-                    double* partial, int B, int P, int NC, float scale, hipStream_t st) {
+                    double* partial, int B, int P, int NC, float scale, float* Wupd, float lr, hipStream_t st) {
   const int Q = P / 2;
   if (!tds_head_bwd_ya_supported(B, P, NC)) return -1;
+  if (Wupd && !dW) return -1;
   const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
-#define TDS_HBY(NB)                                                                                                \
-  case NB:                                                                                                         \
-    if (dW)                                                                                                        \
-      hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW, g2m,  \
-                         partial, Q, NC, scale);                                                                   \
-    else                                                                                                           \
-      hipLaunchKernelGGL((head_bwd_ya_kernel<false, NB>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW, g2m, \
-                         partial, Q, NC, scale);                                                                   \
+#define TDS_HBY(NB)                                                                                                 \
+  case NB:                                                                                                          \
+    if (Wupd)                                                                                                       \
+      hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB, true>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW,  \
+                         g2m, partial, Q, NC, scale, Wupd, lr);                                                     \
+    else if (dW)                                                                                                    \
+      hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB, false>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW, \
+                         g2m, partial, Q, NC, scale, Wupd, lr);                                                     \
+    else                                                                                                            \
+      hipLaunchKernelGGL((head_bwd_ya_kernel<false, NB, false>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits,    \
+                         dW, g2m, partial, Q, NC, scale, Wupd, lr);                                                 \
     return 0;
   switch (B) { TDS_HBY(1) TDS_HBY(2) TDS_HBY(3) TDS_HBY(4) TDS_HBY(5) TDS_HBY(6) TDS_HBY(7) TDS_HBY(8) default: break; }
 #undef TDS_HBY

@@ -97,7 +97,7 @@ int tds_head_bwd_ya_max_batch();
 int tds_head_bwd_ya_nblk(int Q);
 bool tds_head_bwd_ya_supported(int B, int P, int NC);
 int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
-                    double* partial, int B, int P, int NC, float scale, hipStream_t st);
+                    double* partial, int B, int P, int NC, float scale, float* Wupd, float lr, hipStream_t st);
 int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
                  double* partial, int B, int P, int NC, float scale, hipStream_t st);
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,

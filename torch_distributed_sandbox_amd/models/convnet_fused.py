@@ -25,7 +25,7 @@ from __future__ import annotations
 import torch
 
 from .. import _ext
-from ..ops import grad_sink, param_fence
+from ..ops import fused_update, grad_sink, param_fence
 from ..parallel import factored
 
 
@@ -131,8 +131,15 @@ class _Head(torch.autograd.Function):
             dW = dbfc = None
         else:
             dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[10] else None, wfc.shape, wfc)
+            # world size 1 under DDP(overlap_optimizer): the SGD step of the fc weight runs in
+            # this same kernel (ops/fused_update.py)
+            lr = None
+            if ctx.needs_input_grad[10] and y2.shape[0] <= 8 and wfc.shape[0] <= 10:  # head_bwd_ya_kernel shapes
+                lr = fused_update.take(ctx.wfc_param)
             dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, dw_out,
-                                                                         1.0, True, ya)
+                                                                         1.0, True, ya, float(lr or 0.0))
+            if lr:
+                fused_update.applied(ctx.wfc_param)
         link = ctx.link
         link.g2m, link.kbuf, link.aff2 = g2m, kbuf, aff2
         # y2's gradient is carried by the link; autograd gets a zero-stride placeholder

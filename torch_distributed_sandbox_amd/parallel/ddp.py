@@ -69,7 +69,8 @@ class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  process_group=None, bucket_cap_mb: Optional[float] = None, find_unused_parameters: bool = False,
                  gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False,
-                 reducer: str = "auto", grad_exchange: str = "auto", overlap_optimizer: bool = False):
+                 reducer: str = "auto", grad_exchange: str = "auto", overlap_optimizer: bool = False,
+                 fuse_update_in_backward: bool = True):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -176,6 +177,8 @@ class DistributedDataParallel(nn.Module):
         # ---- overlapped optimizer: the big layers' buckets finish (collective + SGD
         # update) on a side stream while the next forward's convolutions run
         self.overlap_optimizer = bool(overlap_optimizer) and dev.type == "cuda" and self.flat_param is not None
+        self.fuse_update_in_backward = bool(fuse_update_in_backward)
+        self._fused_done = set()  # ids of params whose step ran inside their backward kernel
         self._deferred: List[_Bucket] = []
         self._deferred_works = {}
         self._side = None
@@ -404,12 +407,46 @@ class DistributedDataParallel(nn.Module):
 
     def attach_optimizer(self, optimizer):
         """Let ``ops.optim.SGD`` update the flat buffer in one sweep (and, with
-        ``overlap_optimizer``, hand the deferred buckets' update to the side stream)."""
+        ``overlap_optimizer``, hand the deferred buckets' update to the side stream).
+        At world size 1 the deferred big weights' plain-SGD step is fused into their
+        backward kernel instead (ops/fused_update.py): nothing to average, and the
+        kernel already holds the weight and its gradient."""
         if self.flat_param is not None and hasattr(optimizer, "set_flat_buffers"):
             optimizer.set_flat_buffers(self.flat_param, self.flat_grad, self._params)
             if self._deferred and hasattr(optimizer, "set_deferred"):
                 optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred], self._run_deferred_update)
+                if self.world_size == 1 and self.fuse_update_in_backward:
+                    self._register_fused_updates(optimizer)
         return optimizer
+
+    def _register_fused_updates(self, optimizer):
+        from ..ops import fused_update
+
+        def plain_sgd_lr():
+            if len(optimizer.param_groups) != 1:
+                return None
+            g = optimizer.param_groups[0]
+            if g.get("momentum", 0.0) != 0.0 or g.get("weight_decay", 0.0) != 0.0 or g.get("nesterov", False):
+                return None
+            if g.get("maximize", False):
+                return None
+            return float(g["lr"])
+
+        for b in self._deferred:
+            for p in b.params:
+                if p.dim() < 2:
+                    continue  # biases: tiny, updated by the optimizer as usual
+
+                def provider(what, p=p):
+                    if what == "applied":
+                        self._fused_done.add(id(p))
+                        return None
+                    # only a plain synchronised step whose gradient lands straight in the bucket
+                    if not self.require_backward_grad_sync or p.grad is not None or id(p) in self._fused_done:
+                        return None
+                    return plain_sgd_lr()
+
+                fused_update.register(p, provider)
 
     def _run_deferred_update(self, update_fn):
         """Finish the deferred buckets on the side stream: wait for this step's
@@ -421,6 +458,7 @@ class DistributedDataParallel(nn.Module):
         cur = torch.cuda.current_stream(self.device)
         side = self._side
         side.wait_stream(cur)
+        done, self._fused_done = self._fused_done, set()
         with torch.cuda.stream(side):
             for b in self._deferred:
                 w = self._deferred_works.pop(b.index, None)
@@ -428,7 +466,13 @@ class DistributedDataParallel(nn.Module):
                     w = self._native.take_work(b.index)
                 if w is not None:
                     w.wait()  # side stream waits for the bucket all-reduce
-                update_fn(b.offset, b.numel)
+                if not done:
+                    update_fn(b.offset, b.numel)
+                    continue
+                for p in b.params:  # the backward already stepped some of them
+                    if id(p) not in done:
+                        off, n = self._slots[id(p)]
+                        update_fn(off, n)
             ev = torch.cuda.Event()
             ev.record(side)
         for b in self._deferred:
