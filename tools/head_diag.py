@@ -42,15 +42,17 @@ def main():
                                                        bfc, None, ya))
     _, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, None, ya)
     res["bwd_y2"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True))
-    for vx in ("1",):
-        os.environ["TDS_HEAD_BWD_VX"] = vx
-        res[f"bwd_ya_vx{vx}"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True,
+    for nw in ("8", "4"):
+        os.environ["TDS_HEAD_BWD_NW"] = nw
+        res[f"bwd_ya_nw{nw}"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True,
                                                                            ya))
-    os.environ.pop("TDS_HEAD_BWD_VX")
+        res[f"bwd_ya_upd_nw{nw}"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0,
+                                                                               True, ya, 1e-12))
+    os.environ.pop("TDS_HEAD_BWD_NW")
     gb_fwd = (y2.numel() + wfc.numel() + ya.numel()) * 4 / 1e9
     gb_bwd = (ya.numel() + 2 * wfc.numel() + B * Q * Q * 32) * 4 / 1e9
     res["fwd_TBps"] = round(gb_fwd / res["fwd"], 3)
-    res["bwd_ya_TBps"] = round(gb_bwd / res["bwd_ya_vx1"], 3)
+    res["bwd_ya_TBps"] = round(gb_bwd / min(res["bwd_ya_nw8"], res["bwd_ya_nw4"]), 3)
     print(res, flush=True)
 
 

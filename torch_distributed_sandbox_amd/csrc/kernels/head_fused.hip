@@ -247,8 +247,11 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restr
 // offsets and was slower; see docs/KERNELS.md.)  Outputs as head_bwd_kernel.
 // With UPD (optimizer step fused into the backward, world size 1 only: ops/fused_update.py)
 // the kernel also writes W - lr * dW over W (each element read and written by one lane).
-template <bool WITH_DW, int NB, bool UPD>  // NB = images per rank (compile-time: exact register footprint)
-__global__ __launch_bounds__(512, 2) void head_bwd_ya_kernel(const float* __restrict__ ya, const float* Wfc,
+// NW = 8: one workgroup per tile and all 32 channels; NW = 4: two workgroups per tile (channel
+// halves, consecutive block ids) so up to three fit a CU and one's loads overlap another's
+// stores (TDS_HEAD_BWD_NW selects).
+template <bool WITH_DW, int NB, bool UPD, int NW = 8>  // NB = images per rank (compile-time: exact register footprint)
+__global__ __launch_bounds__(64 * NW, 2) void head_bwd_ya_kernel(const float* __restrict__ ya, const float* Wfc,
                                                              const float* __restrict__ aff2, const float* __restrict__ dl,
                                                              float* __restrict__ dW, float* __restrict__ g2m,
                                                              double* __restrict__ partial, int Q, int NC, float scale,
@@ -257,10 +260,12 @@ __global__ __launch_bounds__(512, 2) void head_bwd_ya_kernel(const float* __rest
   __shared__ float dls[NB * 10];  // dlogits: broadcast LDS reads (as scalars they cost ~50 SGPRs and spill)
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (threadIdx.x < NB * 10) dls[threadIdx.x] = (int)threadIdx.x % 10 < NC ? dl[(threadIdx.x / 10) * NC + threadIdx.x % 10] : 0.f;
-  const int px = blockIdx.x * HD_PX + lane;
+  const int half = NW == 8 ? 0 : (int)(blockIdx.x & 1);
+  const int pxb = NW == 8 ? (int)blockIdx.x : (int)(blockIdx.x >> 1);
+  const int px = pxb * HD_PX + lane;
   const bool valid = px < Q;
   const int64_t QQ = (int64_t)Q * Q, pos = (int64_t)blockIdx.y * Q + (valid ? px : 0);
-  const int c0 = CPW * wv;
+  const int c0 = 16 * half + CPW * wv;
   float w[10][CPW], y[NB][CPW];
 #pragma unroll
   for (int j = 0; j < 10; ++j)
@@ -314,7 +319,8 @@ __global__ __launch_bounds__(512, 2) void head_bwd_ya_kernel(const float* __rest
           if constexpr (UPD) Wupd[((int64_t)j * 32 + c0 + c) * QQ + pos] = w[j][c] - lr * gd;  // torch SGD: p -= lr*g
         }
   }
-  const int nblk = gridDim.x * gridDim.y, blk = blockIdx.y * gridDim.x + blockIdx.x;
+  const int tiles_c = NW == 8 ? (int)gridDim.x : (int)(gridDim.x >> 1);
+  const int nblk = tiles_c * gridDim.y, blk = blockIdx.y * tiles_c + pxb;
 #pragma unroll
   for (int c = 0; c < CPW; ++c) {
     const float s0 = wave_sum(sdz[c]);
@@ -391,20 +397,29 @@ int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const 
   const int Q = P / 2;
   if (!tds_head_bwd_ya_supported(B, P, NC)) return -1;
   if (Wupd && !dW) return -1;
-  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
-#define TDS_HBY(NB)                                                                                                 \
-  case NB:                                                                                                          \
-    if (Wupd)                                                                                                       \
-      hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB, true>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW,  \
-                         g2m, partial, Q, NC, scale, Wupd, lr);                                                     \
-    else if (dW)                                                                                                    \
-      hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB, false>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits, dW, \
-                         g2m, partial, Q, NC, scale, Wupd, lr);                                                     \
-    else                                                                                                            \
-      hipLaunchKernelGGL((head_bwd_ya_kernel<false, NB, false>), grid, dim3(512), 0, st, ya, Wfc, aff2, dlogits,    \
-                         dW, g2m, partial, Q, NC, scale, Wupd, lr);                                                 \
+  const char* nwe = std::getenv("TDS_HEAD_BWD_NW");
+  const bool half = !(nwe && std::atoi(nwe) == 8);
+  const dim3 grid(((Q + HD_PX - 1) / HD_PX) * (half ? 2 : 1), Q);
+#define TDS_HBY_NW(NB, NW)                                                                                              \
+  if (Wupd)                                                                                                            \
+    hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB, true, NW>), grid, dim3(64 * NW), 0, st, ya, Wfc, aff2, dlogits,   \
+                       dW, g2m, partial, Q, NC, scale, Wupd, lr);                                                      \
+  else if (dW)                                                                                                         \
+    hipLaunchKernelGGL((head_bwd_ya_kernel<true, NB, false, NW>), grid, dim3(64 * NW), 0, st, ya, Wfc, aff2, dlogits,  \
+                       dW, g2m, partial, Q, NC, scale, Wupd, lr);                                                      \
+  else                                                                                                                 \
+    hipLaunchKernelGGL((head_bwd_ya_kernel<false, NB, false, NW>), grid, dim3(64 * NW), 0, st, ya, Wfc, aff2, dlogits, \
+                       dW, g2m, partial, Q, NC, scale, Wupd, lr);
+#define TDS_HBY(NB)            \
+  case NB:                     \
+    if (half) {                \
+      TDS_HBY_NW(NB, 4)        \
+    } else {                   \
+      TDS_HBY_NW(NB, 8)        \
+    }                          \
     return 0;
   switch (B) { TDS_HBY(1) TDS_HBY(2) TDS_HBY(3) TDS_HBY(4) TDS_HBY(5) TDS_HBY(6) TDS_HBY(7) TDS_HBY(8) default: break; }
+#undef TDS_HBY_NW
 #undef TDS_HBY
   return -1;
 }
