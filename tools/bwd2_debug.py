@@ -22,7 +22,7 @@ def main():
         torch.manual_seed(P)
         B, Q = 2, P // 2
         y2 = torch.randn(B, P, P, 32, device=dev)
-        g2m = torch.randn(B, Q, Q, 32, device=dev)
+        g2m = torch.randn(B, 32, Q, Q, device=dev)
         aff2 = torch.cat([torch.rand(32, device=dev) + 0.5, torch.randn(32, device=dev)])
         kbuf = torch.randn(96, device=dev)
         p1 = pack_hilo(torch.relu(torch.randn(B, P, P, 16, device=dev)))

@@ -23,7 +23,7 @@ def main():
     b2 = torch.zeros(32, device=dev)
     wp, wd = ops.conv2_pack(w2)
     Q = P // 2
-    g2m = torch.randn(B, Q, Q, 32, device=dev)
+    g2m = torch.randn(B, 32, Q, Q, device=dev)
     aff2 = torch.cat([torch.rand(32, device=dev) + 0.5, torch.randn(32, device=dev)])
     kbuf = torch.randn(96, device=dev)
     res = {}

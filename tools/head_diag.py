@@ -1,5 +1,5 @@
 """A/B timing of the fused head kernels at the bench shape (B=5, P=1500): forward, backward
-from y2 (LDS transpose) and backward from the saved argmax values ya (TDS_HEAD_BWD_VX=1|2)."""
+from y2 (LDS transpose) and backward from the saved argmax values ya (TDS_HEAD_BWD_NW=8|4 lane-per-column, 0 streaming)."""
 import os
 import sys
 
@@ -42,17 +42,34 @@ def main():
                                                        bfc, None, ya))
     _, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, None, ya)
     res["bwd_y2"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True))
-    for nw in ("8", "4"):
+    outs = {}
+    for nw in ("8", "4", "0"):
         os.environ["TDS_HEAD_BWD_NW"] = nw
         res[f"bwd_ya_nw{nw}"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True,
                                                                            ya))
+        r = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True, ya)
+        outs[nw] = [t.clone() for t in r]
+        w0 = wfc.clone()
         res[f"bwd_ya_upd_nw{nw}"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0,
                                                                                True, ya, 1e-12))
+        wfc.copy_(w0)
+    os.environ.pop("TDS_HEAD_BWD_NW")
+    names = ["dW", "dbfc", "dg2", "dbe2", "g2m", "kbuf"]
+    for nw in ("4", "0"):
+        res[f"maxdiff_nw{nw}_vs_nw8"] = {n: float((a - b).abs().max()) for n, a, b in zip(names, outs[nw], outs["8"])}
+    # update path: W - lr*dW once, compare against the unfused result
+    os.environ["TDS_HEAD_BWD_NW"] = "0"
+    w0 = wfc.clone()
+    r = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True, ya, 0.5)
+    res["upd_maxdiff"] = float((wfc - (w0 - 0.5 * r[0])).abs().max())
+    wfc.copy_(w0)
     os.environ.pop("TDS_HEAD_BWD_NW")
     gb_fwd = (y2.numel() + wfc.numel() + ya.numel()) * 4 / 1e9
     gb_bwd = (ya.numel() + 2 * wfc.numel() + B * Q * Q * 32) * 4 / 1e9
     res["fwd_TBps"] = round(gb_fwd / res["fwd"], 3)
-    res["bwd_ya_TBps"] = round(gb_bwd / min(res["bwd_ya_nw8"], res["bwd_ya_nw4"]), 3)
+    res["bwd_ya_TBps"] = {nw: round(gb_bwd / res[f"bwd_ya_nw{nw}"], 3) for nw in ("8", "4", "0")}
+    res["bwd_ya_upd_TBps"] = {nw: round((gb_bwd + wfc.numel() * 4 / 1e9) / res[f"bwd_ya_upd_nw{nw}"], 3)
+                              for nw in ("8", "4", "0")}
     print(res, flush=True)
 
 

@@ -198,9 +198,9 @@ static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const
   } else {
     r.dW = at::empty_like(wfc);
   }
-  r.g2m = at::empty({B, Q, Q, 32}, y2.options());
+  r.g2m = at::empty({B, 32, Q, Q}, y2.options());  // planar (fc flatten order)
   const bool use_ya = ya.has_value() && ya->defined() && tds_head_bwd_ya_supported((int)B, (int)P, (int)NC);
-  const int nblk = use_ya ? tds_head_bwd_ya_nblk((int)Q) : tds_head_fwd_nblk((int)Q);
+  int nblk = use_ya ? tds_head_bwd_ya_nblk((int)B, (int)P, (int)NC) : tds_head_fwd_nblk((int)Q);
   auto partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
   int rc;
   rc = -1;
@@ -217,6 +217,10 @@ static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const
   TORCH_CHECK(update_lr <= 0.0 || (use_ya && rc == 0 && compute_dw),
               "fused_head_backward_g2m: update_lr needs the saved-argmax (ya) path with compute_dw");
   if (rc != 0) {
+    if (nblk != tds_head_fwd_nblk((int)Q)) {
+      nblk = tds_head_fwd_nblk((int)Q);
+      partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
+    }
     rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(), dlogits.data_ptr<float>(),
                       compute_dw ? r.dW.data_ptr<float>() : nullptr, r.g2m.data_ptr<float>(),
                       partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale, st);
@@ -287,7 +291,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   const int64_t B = p1.size(0), P = p1.size(1), Q = P / 2;
   need(p1, at::kFloat, {B, P, P, 16}, "p1");
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
-  need(g2m, at::kFloat, {B, Q, Q, 32}, "g2m");
+  need(g2m, at::kFloat, {B, 32, Q, Q}, "g2m");
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
   need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");

@@ -72,4 +72,13 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + orig / nx;
 }
 
+// The head backward's pooled gradient g2m is PLANAR, [B][32][Q][Q] (the fc flatten order):
+// its producer streams the fc weight planes and writes g2m in the same long per-channel runs
+// (head_bwd_stream_kernel).  Channels 4*c4 .. 4*c4+3 of pooled position (py, px) of image b:
+__device__ __forceinline__ float4 g2m_planar4(const float* __restrict__ g2m, int b, int c4, int py, int px, int Q) {
+  const int64_t QQ = (int64_t)Q * Q;
+  const float* g = g2m + ((int64_t)b * 32 + 4 * c4) * QQ + (int64_t)py * Q + px;
+  return make_float4(g[0], g[QQ], g[2 * QQ], g[3 * QQ]);
+}
+
 }  // namespace tds

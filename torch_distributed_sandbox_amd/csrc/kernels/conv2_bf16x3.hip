@@ -652,7 +652,7 @@ constexpr int BW_PPER = (BW_PCHUNKS + C2_THREADS - 1) / C2_THREADS;     // 4
 
 template <int DIAG>
 __global__ __launch_bounds__(C2_THREADS) void conv2_bwd_fused_kernel(
-    const float4* __restrict__ y2, const float4* __restrict__ g2m, const float* __restrict__ aff2,
+    const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
     const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
     float* __restrict__ dp1, float* __restrict__ slab, int B, int P, int Q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -696,7 +696,7 @@ __global__ __launch_bounds__(C2_THREADS) void conv2_bwd_fused_kernel(
       }
       const int py = gy >> 1, px = gx >> 1;  // pooled coordinates (arithmetic shift: -1 for gy = -2)
       gv[u] = (DIAG != 3 && it < BW_ITEMS && gy >= 0 && gx >= 0 && py < Q && px < Q)
-                  ? g2m[(((int64_t)b * Q + py) * Q + px) * 8 + c4]
+                  ? g2m_planar4(g2m, b, c4, py, px, Q)
                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
@@ -1038,7 +1038,7 @@ int tds_conv2_bwd_fused_num_wg() {
   return tds_conv2_bwd_version() == 2 ? tds_conv2_bwd2_num_wg() : tds_conv2_num_wg();
 }
 
-// fused BN2/pool backward + conv2 dgrad + wgrad: y2 [B,P,P,32] f32, g2m [B,Q,Q,32] f32,
+// fused BN2/pool backward + conv2 dgrad + wgrad: y2 [B,P,P,32] f32, g2m [B,32,Q,Q] f32 (planar),
 // aff2 [a32|b32], kbuf [k1|k2|k3]; dp1 [B,P,P,16] f32; slab [nwg][26][512]
 void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
                          const short* wd, float* dp1, float* slab, float* dw, float* db, float scale, int nwg, int B,
@@ -1052,7 +1052,7 @@ void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, c
   set_lds_limits();
   const int Q = P / 2;
   TDS_C2_DISPATCH(conv2_bwd_fused_kernel, dim3(nwg), dim3(C2_THREADS), BW_LDS, st,
-                  reinterpret_cast<const float4*>(y2), reinterpret_cast<const float4*>(g2m), aff2, kbuf,
+                  reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf,
                   reinterpret_cast<const uint4*>(p1), reinterpret_cast<const uint4*>(wd), dp1, slab, B, P, Q);
   hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db,
                      scale);

@@ -196,7 +196,7 @@ __device__ __forceinline__ void b2_wgrad(const char* d_l, const char* p_l, f32x4
 // in registers (loaded under the current tile's MFMAs), then BN2 backward -> LDS.
 struct B2Args {
   const float4* __restrict__ y2;
-  const float4* __restrict__ g2m;
+  const float* __restrict__ g2m;  // planar [B][32][Q][Q]
   const uint4* __restrict__ p1;
   float* __restrict__ dp1;
   float* __restrict__ slab;
@@ -264,7 +264,7 @@ struct B2Stager {
       int wy, wx;
       item_geom(tid, u, wy, wx);
       yoff[u] = (uint32_t)(((2 * wy) * a.P + 2 * wx) * 128 + c4 * 16);
-      goff[u] = (uint32_t)((wy * a.Q + wx) * 128 + c4 * 16);
+      goff[u] = (uint32_t)((wy * a.Q + wx) * 4 + (int64_t)c4 * 16 * a.Q * a.Q);  // planar: channel 4*c4
       drec[u] = ((2 * wy) * B2_SC + 2 * wx) * 32 + (c4 & 3) * 8;
     }
 #pragma unroll
@@ -293,7 +293,8 @@ struct B2Stager {
     const __amdgpu_buffer_rsrc_t ry =
         b2_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 128);
     const __amdgpu_buffer_rsrc_t rg = b2_rsrc(reinterpret_cast<const char*>(a.g2m) +
-                                              (((int64_t)x.b * Q + (x.r0 - 2) / 2) * Q + (x.c0 - 2) / 2) * 128);
+                                              ((int64_t)x.b * 32 * Q * Q + (int64_t)((x.r0 - 2) / 2) * Q + (x.c0 - 2) / 2) * 4);
+    const uint32_t gplane = (uint32_t)(Q * Q * 4);
     const char* pbase = reinterpret_cast<const char*>(a.p1) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 64;
     uint32_t oy[B2_IPER][4], og[B2_IPER];
 #pragma unroll
@@ -351,7 +352,13 @@ struct B2Stager {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         yv[u][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy[u][q], 0, 0));
-      gv[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, og[u], 0, 0));
+      // four channel planes; an out-of-image lane stays at kB2Oob for all four (zeros)
+      float g4[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        g4[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                              rg, og[u] == kB2Oob ? kB2Oob : og[u] + k * gplane, 0, 0));
+      gv[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
     }
   }
 
@@ -524,7 +531,7 @@ __device__ __forceinline__ void b2_run(const B2Args& a, const uint4* __restrict_
 
 template <int DIAG>
 __global__ __launch_bounds__(B2_THREADS, 2) void conv2_bwd2_kernel(
-    const float4* __restrict__ y2, const float4* __restrict__ g2m, const float* __restrict__ aff2,
+    const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
     const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
     float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ order, int B, int P, int Q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -580,7 +587,7 @@ void tds_conv2_bwd2(const float* y2, const float* g2m, const float* aff2, const 
     lds_set = lds;
   }
   const float4* y = reinterpret_cast<const float4*>(y2);
-  const float4* gm = reinterpret_cast<const float4*>(g2m);
+  const float* gm = g2m;
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wd);
   const int* order = tds_tile_order(B, (P + B2_TH - 1) / B2_TH, (P + B2_TC - 1) / B2_TC);

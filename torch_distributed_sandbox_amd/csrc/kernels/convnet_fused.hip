@@ -562,7 +562,7 @@ __global__ void bn_bwd_finalize2_kernel(const double* __restrict__ partial, int 
 // output z, first max in scan order), dy2 = k1*dz + k2*y2 + k3 for all 4 pixels,
 // written as bf16 hi|lo (64-channel records).  Pixels of an unpooled last row/col
 // (odd P) get dz = 0.
-__global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict__ y2, const float4* __restrict__ g2m,
+__global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict__ y2, const float* __restrict__ g2m,
                                                         const float* __restrict__ aff2, const float* __restrict__ kbuf,
                                                         uint2* __restrict__ dy2, int B, int P, int Q) {
   const int PH = (P + 1) / 2;
@@ -597,7 +597,7 @@ __global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict
     }
     float gv[4] = {0.f, 0.f, 0.f, 0.f};
     if (pooled) {
-      const float4 gg = g2m[(((int64_t)b * Q + wy) * Q + wx) * 8 + c4];
+      const float4 gg = g2m_planar4(g2m, b, c4, wy, wx, Q);
       gv[0] = gg.x; gv[1] = gg.y; gv[2] = gg.z; gv[3] = gg.w;
     }
     int am[4];
@@ -935,7 +935,7 @@ void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const f
   int64_t g = (total + 255) / 256;
   if (g > 8192) g = 8192;
   hipLaunchKernelGGL(dy2_build_kernel, dim3((unsigned)g), dim3(256), 0, st, reinterpret_cast<const float4*>(y2),
-                     reinterpret_cast<const float4*>(g2m), aff2, kbuf, reinterpret_cast<uint2*>(dy2), B, P, Q);
+                     g2m, aff2, kbuf, reinterpret_cast<uint2*>(dy2), B, P, Q);
 }
 
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,

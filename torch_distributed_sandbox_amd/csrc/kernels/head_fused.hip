@@ -153,7 +153,7 @@ __global__ void head_logits_kernel(const double* __restrict__ sums, const float*
 
 // Backward.  dl = dlogits [B][NC].
 //   dW[j][c][pos]  = scale * sum_b dl[b][j] p2[b][c][pos]      (e.g. straight into the DDP bucket)
-//   g2m[b][pos][c] = (sum_j dl[b][j] W[j][c][pos]) * [p2 > 0]   (NHWC pooled gradient, fp32)
+//   g2m[b][c][pos] = (sum_j dl[b][j] W[j][c][pos]) * [p2 > 0]   (planar pooled gradient, fp32)
 //   partial[c][blk][2] = { sum g2m (= sum dz2), sum g2m * y2(argmax) }   (BN2 backward reductions)
 template <int NW, bool WITH_DW>
 __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
@@ -212,9 +212,8 @@ __global__ __launch_bounds__(64 * NW) void head_bwd_kernel(const float4* __restr
       sdy[c] += valid ? gm[c] * ya[c] : 0.f;
     }
     if (valid) {
-      float* dst = g2m + ((int64_t)b * QQ + pos) * 32 + CPW * wv;
-      if constexpr (CPW == 4) *reinterpret_cast<float4*>(dst) = make_float4(gm[0], gm[1], gm[2], gm[3]);
-      else *reinterpret_cast<float2*>(dst) = make_float2(gm[0], gm[1]);
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) g2m[((int64_t)b * 32 + CPW * wv + c) * QQ + pos] = gm[c];  // planar
     }
   }
   if (WITH_DW && valid) {
@@ -304,8 +303,10 @@ __global__ __launch_bounds__(64 * NW, 2) void head_bwd_ya_kernel(const float* __
       sdz[c] += valid ? gm[c] : 0.f;
       sdy[c] += valid ? gm[c] * y[b][c] : 0.f;
     }
-    if (valid)
-      *reinterpret_cast<float4*>(g2m + ((int64_t)b * QQ + pos) * 32 + c0) = make_float4(gm[0], gm[1], gm[2], gm[3]);
+    if (valid) {
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) g2m[((int64_t)b * 32 + c0 + c) * QQ + pos] = gm[c];  // planar
+    }
   }
   if (WITH_DW && valid) {
     float* dst = dW + (int64_t)c0 * QQ + pos;
@@ -329,6 +330,123 @@ __global__ __launch_bounds__(64 * NW, 2) void head_bwd_ya_kernel(const float* __
       partial[((int64_t)(c0 + c) * nblk + blk) * 2 + 0] = s0;
       partial[((int64_t)(c0 + c) * nblk + blk) * 2 + 1] = s1;
     }
+  }
+}
+
+// Streaming form of the ya backward (the default).  Workgroup = one channel c x HS_RUN
+// consecutive pooled positions; thread = 4 positions (dwordx4).  Every plane it touches
+// (ya[b][c], W[j][c] in; dW[j][c], the updated W[j][c], g2m[b][c] out) is read or written as
+// one contiguous 4 KB run: tools/micro/runlen_bw.hip measured this plane mix at 4.5-5 TB/s
+// with >= 1 KB runs against 2-2.4 TB/s for the 128 B runs of a 32-channel x 32-position
+// block, and plain stores beat nontemporal ones.  That is why g2m is planar (an NHWC g2m
+// needs all 32 channels of a position in one workgroup; a channel-quad layout with a 1 KB-run
+// LDS transpose measured 0.67 ms against 0.52 ms for this kernel).  Per-channel BN2 sums: one
+// (sum dz, sum dz*y) pair per workgroup, partial[c][run][2].  Planes are addressed through one
+// buffer descriptor per tensor (plane base = scalar soffset, lane offset = voffset).
+// Requires QQ % 4 == 0 and every tensor < 2 GiB (tds_head_bwd_ya falls back otherwise).
+constexpr int HS_RUN = 1024;
+typedef unsigned int hs_u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hs_rsrc(const void* base) {
+  const uint64_t v = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7FFFFFF0, 0x00020000);
+}
+
+__device__ __forceinline__ float4 hs_ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));
+}
+
+__device__ __forceinline__ void hs_st(float4 v, __amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(hs_u32x4, v), r, vo, so, 0);
+}
+
+__device__ __forceinline__ float hs_relu(float m) { return m > 0.f ? m : (isnan(m) ? m : 0.f); }
+
+template <bool WITH_DW, int NB, bool UPD>
+__global__ __launch_bounds__(256) void head_bwd_stream_kernel(
+    const float* __restrict__ ya, const float* Wfc, const float* __restrict__ aff2, const float* __restrict__ dl,
+    float* __restrict__ dW, float* __restrict__ g2m, double* __restrict__ partial, int64_t QQ, int NC, float scale,
+    float* Wupd, float lr) {
+  __shared__ float dls[NB * 10];
+  __shared__ float red[2][4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int nrun = (int)((QQ + HS_RUN - 1) / HS_RUN);
+  const int c = (int)blockIdx.x / nrun, run = (int)blockIdx.x - c * nrun;  // channel-major: neighbours share planes
+  if (t < NB * 10) dls[t] = t % 10 < NC ? dl[(t / 10) * NC + t % 10] : 0.f;
+  const float a = aff2[c], bb = aff2[32 + c];
+  const __amdgpu_buffer_rsrc_t ry = hs_rsrc(ya), rw = hs_rsrc(Wfc), rd = hs_rsrc(dW), ru = hs_rsrc(Wupd),
+                               rg = hs_rsrc(g2m);
+  const uint32_t plane = (uint32_t)(32 * QQ * 4);  // bytes between consecutive b (ya, g2m) / j (W, dW)
+  const int64_t pos = (int64_t)run * HS_RUN + 4 * t;
+  const bool valid = pos < QQ;  // QQ % 4 == 0: a thread's 4 positions are all in or all out
+  const uint32_t vo = valid ? (uint32_t)(((int64_t)c * QQ + pos) * 4) : 0u;
+  float4 y[NB], w[10];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) y[b] = hs_ld(ry, vo, b * plane);
+#pragma unroll
+  for (int j = 0; j < 10; ++j) w[j] = hs_ld(rw, vo, (j < NC ? j : 0) * plane);  // rows >= NC: reload row 0
+#pragma unroll
+  for (int b = 0; b < NB; ++b) y[b] = valid ? y[b] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int j = 0; j < 10; ++j) w[j] = (valid && j < NC) ? w[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();  // dls
+  float sdz = 0.f, sdy = 0.f;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const float d = dls[b * 10 + j];
+      g.x += d * w[j].x;
+      g.y += d * w[j].y;
+      g.z += d * w[j].z;
+      g.w += d * w[j].w;
+    }
+    // same fmaf as head_window: bit-exact recomputation of the pooled pre-activation
+    float4 gm;
+    gm.x = fmaf(a, y[b].x, bb) > 0.f ? g.x : 0.f;
+    gm.y = fmaf(a, y[b].y, bb) > 0.f ? g.y : 0.f;
+    gm.z = fmaf(a, y[b].z, bb) > 0.f ? g.z : 0.f;
+    gm.w = fmaf(a, y[b].w, bb) > 0.f ? g.w : 0.f;
+    // invalid positions hold zeros: w = 0 -> gm = 0, y = 0 -> no contribution
+    sdz += (gm.x + gm.y) + (gm.z + gm.w);
+    sdy += (gm.x * y[b].x + gm.y * y[b].y) + (gm.z * y[b].z + gm.w * y[b].w);
+    if (valid) hs_st(gm, rg, vo, b * plane);
+  }
+  if constexpr (WITH_DW) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        const float d = dls[b * 10 + j];
+        s.x += d * hs_relu(fmaf(a, y[b].x, bb));
+        s.y += d * hs_relu(fmaf(a, y[b].y, bb));
+        s.z += d * hs_relu(fmaf(a, y[b].z, bb));
+        s.w += d * hs_relu(fmaf(a, y[b].w, bb));
+      }
+      s = make_float4(scale * s.x, scale * s.y, scale * s.z, scale * s.w);
+      if (valid && j < NC) {
+        hs_st(s, rd, vo, j * plane);
+        if constexpr (UPD)  // torch SGD: p -= lr * g
+          hs_st(make_float4(w[j].x - lr * s.x, w[j].y - lr * s.y, w[j].z - lr * s.z, w[j].w - lr * s.w), ru, vo,
+                j * plane);
+      }
+    }
+  }
+  sdz = wave_sum(sdz);
+  sdy = wave_sum(sdy);
+  if (lane == 0) {
+    red[0][wv] = sdz;
+    red[1][wv] = sdy;
+  }
+  __syncthreads();
+  if (t < 2) {
+    const double s = ((double)red[t][0] + (double)red[t][1]) + ((double)red[t][2] + (double)red[t][3]);
+    partial[((int64_t)c * nrun + run) * 2 + t] = s;
   }
 }
 
@@ -388,7 +506,27 @@ int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const flo
 int tds_head_bwd_ya_max_batch() { return HD_MAXB_YA; }
 
 // backward from saved argmax values (head_bwd_ya_kernel); partial: double [32][nblk][2]
-int tds_head_bwd_ya_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
+// TDS_HEAD_BWD_NW = 4 / 8 select the lane-per-column head_bwd_ya_kernel (A/B); default: streaming
+static int head_bwd_ya_form() {
+  const char* e = std::getenv("TDS_HEAD_BWD_NW");  // read per call: in-process A/B (tools/head_diag.py)
+  const int v = e ? std::atoi(e) : 0;
+  return (v == 4 || v == 8) ? v : 0;
+}
+
+static int head_bwd_stream_nrun(int Q) { return (int)(((int64_t)Q * Q + HS_RUN - 1) / HS_RUN); }
+
+// the streaming kernel's buffer descriptors cover 2 GiB and its dwordx4 plane accesses need QQ % 4 == 0
+static bool head_bwd_use_stream(int B, int P, int NC) {
+  const int64_t QQ = (int64_t)(P / 2) * (P / 2);
+  const int64_t big = (int64_t)(B > NC ? B : NC) * 32 * QQ * 4;
+  return head_bwd_ya_form() == 0 && QQ % 4 == 0 && big < 0x7FFFFFF0LL;
+}
+
+int tds_head_bwd_ya_nblk(int B, int P, int NC) {
+  const int Q = P / 2;
+  if (head_bwd_use_stream(B, P, NC)) return head_bwd_stream_nrun(Q);
+  return ((Q + HD_PX - 1) / HD_PX) * Q;
+}
 
 bool tds_head_bwd_ya_supported(int B, int P, int NC) { return B >= 1 && B <= HD_MAXB_YA && NC <= 10 && P >= 2; }
 
@@ -397,8 +535,26 @@ int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const 
   const int Q = P / 2;
   if (!tds_head_bwd_ya_supported(B, P, NC)) return -1;
   if (Wupd && !dW) return -1;
-  const char* nwe = std::getenv("TDS_HEAD_BWD_NW");
-  const bool half = !(nwe && std::atoi(nwe) == 8);
+  if (head_bwd_use_stream(B, P, NC)) {
+    const dim3 grid(32 * head_bwd_stream_nrun(Q));
+    const int64_t QQ = (int64_t)Q * Q;
+#define TDS_HBS(NB)                                                                                                    \
+  case NB:                                                                                                             \
+    if (Wupd)                                                                                                          \
+      hipLaunchKernelGGL((head_bwd_stream_kernel<true, NB, true>), grid, dim3(256), 0, st, ya, Wfc, aff2, dlogits, dW, \
+                         g2m, partial, QQ, NC, scale, Wupd, lr);                                                       \
+    else if (dW)                                                                                                       \
+      hipLaunchKernelGGL((head_bwd_stream_kernel<true, NB, false>), grid, dim3(256), 0, st, ya, Wfc, aff2, dlogits,    \
+                         dW, g2m, partial, QQ, NC, scale, Wupd, lr);                                                   \
+    else                                                                                                               \
+      hipLaunchKernelGGL((head_bwd_stream_kernel<false, NB, false>), grid, dim3(256), 0, st, ya, Wfc, aff2, dlogits,   \
+                         dW, g2m, partial, QQ, NC, scale, Wupd, lr);                                                   \
+    return 0;
+    switch (B) { TDS_HBS(1) TDS_HBS(2) TDS_HBS(3) TDS_HBS(4) TDS_HBS(5) TDS_HBS(6) TDS_HBS(7) TDS_HBS(8) default: break; }
+#undef TDS_HBS
+    return -1;
+  }
+  const bool half = head_bwd_ya_form() != 8;
   const dim3 grid(((Q + HD_PX - 1) / HD_PX) * (half ? 2 : 1), Q);
 #define TDS_HBY_NW(NB, NW)                                                                                              \
   if (Wupd)                                                                                                            \

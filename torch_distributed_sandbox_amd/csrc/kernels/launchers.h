@@ -94,7 +94,7 @@ int tds_head_fwd_nblk(int Q);
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
                  float* logits, float* xout, float* yaout, int B, int P, int NC, hipStream_t st);
 int tds_head_bwd_ya_max_batch();
-int tds_head_bwd_ya_nblk(int Q);
+int tds_head_bwd_ya_nblk(int B, int P, int NC);
 bool tds_head_bwd_ya_supported(int B, int P, int NC);
 int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
                     double* partial, int B, int P, int NC, float scale, float* Wupd, float lr, hipStream_t st);
