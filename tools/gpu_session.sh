@@ -1,6 +1,6 @@
 #!/bin/bash
 # Runs a list of GPU steps (one per line in $1), each under its own timeout.
-# Test failures (exit 1) continue; faults / aborts / timeouts (124,134,137,139, >128) stop the session.
+# Any nonzero exit stops the session (a pytest failure can be a GPU memory fault: nothing more runs on the GPU after it).
 # Usage: bash tools/gpu_session.sh steps.txt   (lines: "<timeout_s> <logname> <command...>")
 set -u
 mkdir -p gpurun_out
@@ -18,8 +18,8 @@ while IFS= read -r line || [ -n "$line" ]; do
   end=$(date +%s)
   echo "=== [$name] rc=$rc in $((end-start))s"
   tail -n 25 "gpurun_out/$name.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ] && [ $rc -ne 2 ]; then
-    echo "=== stopping: step $name ended with rc=$rc (fault/timeout/abort)"
+  if [ $rc -ne 0 ]; then
+    echo "=== stopping: step $name ended with rc=$rc"
     exit $rc
   fi
 done < "$1"

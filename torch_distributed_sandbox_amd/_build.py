@@ -41,6 +41,12 @@ ARCH = os.environ.get("TDS_OFFLOAD_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
+# per-file device-compiler flags.  x_autocorr.hip: the SLP vectorizer pairs the 41 shift
+# accumulators into v_pk_fma_f32 whose misaligned operand pairs cost ~4 v_mov per FMA pair
+# (322 moves against 80 packed FMAs per row); scalar v_fmac needs none.
+HIP_FILE_FLAGS = {"x_autocorr.hip": ["-fno-slp-vectorize"]}
+
+
 def _torch_paths():
     import torch
     from torch.utils import cpp_extension as ce
@@ -139,6 +145,9 @@ def write_ninja(debug: bool = False, host_sanitize: bool = False) -> str:
         o = os.path.join(BUILD_DIR, rel + ".o")
         rule = "hip" if s.endswith(".hip") else "host"
         lines.append(f"build {_ninja_escape(o)}: {rule} {_ninja_escape(s)}")
+        extra = HIP_FILE_FLAGS.get(os.path.basename(s))
+        if extra:
+            lines.append(f"  hipflags = $hipflags {' '.join(shlex.quote(f) for f in extra)}")
         objs.append(o)
     lines.append(f"build {_ninja_escape(OUT_SO)}: link {' '.join(_ninja_escape(o) for o in objs)}")
     lines.append(f"default {_ninja_escape(OUT_SO)}")

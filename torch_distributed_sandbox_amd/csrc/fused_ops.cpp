@@ -34,7 +34,6 @@ const float* optf(const c10::optional<Tensor>& t, int64_t n, const char* name) {
 }
 
 int l1_wg() { return tds_fused_num_wg(4); }
-int ac_wg() { return tds_fused_num_wg(4); }
 
 // ---------------------------------------------------------------- layer 1 forward
 // returns (p1 carrier, idx1, stats1[mean16|invstd16], ac_partial, strips)
@@ -63,9 +62,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   const int64_t P = H / 2;
   auto fo = x.options();
   // x autocorrelation + border strips -> Gram G / patch sums S -> BN1 statistics in closed form
-  // enough workgroups that each thread's fp32 partial covers <= ~32 products (fp64 beyond)
-  const int64_t ac_tiles = B * ((H + 15) / 16) * ((W + 63) / 64);
-  const int nac = (int)std::max<int64_t>(ac_wg(), (ac_tiles + 7) / 8);
+  // one thread per 4 x 8 pixel block: each fp32 partial covers 32 products (fp64 beyond)
+  const int nac = tds_x_autocorr_num_wg((int)B, (int)H, (int)W);
+  TORCH_CHECK(nac > 0, "fused_l1_forward: x must be < 2 GiB with W % 4 == 0 (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo.dtype(at::kDouble));
   auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
   tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,

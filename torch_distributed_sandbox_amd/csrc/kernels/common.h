@@ -72,6 +72,19 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + orig / nx;
 }
 
+// Wave-uniform raw buffer descriptor over [base, base + bytes): lanes whose voffset is past
+// `bytes` read zeros / drop stores (hardware range check).  The two readfirstlane halves are
+// widened as UNSIGNED: readfirstlane returns int, and OR-ing a sign-extended low word into the
+// address corrupts the high word whenever bit 31 of the base is set (an allocation-dependent
+// memory fault).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t tds_buffer_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t v = reinterpret_cast<uint64_t>(base);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | (uint64_t)lo), (short)0,
+                                           (int)bytes, 0x00020000);
+}
+
 // The head backward's pooled gradient g2m is PLANAR, [B][32][Q][Q] (the fc flatten order):
 // its producer streams the fc weight planes and writes g2m in the same long per-channel runs
 // (head_bwd_stream_kernel).  Channels 4*c4 .. 4*c4+3 of pooled position (py, px) of image b:

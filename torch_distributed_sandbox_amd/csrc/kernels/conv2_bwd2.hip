@@ -222,13 +222,7 @@ __device__ __forceinline__ B2Tile b2_decode(const B2Args& a, int t) {
 // wave-uniform buffer descriptor over [base, base + 2 GiB): per-lane byte offsets in voffset,
 // an invalid lane gets kB2Oob and reads zeros (hardware range check, no exec masking)
 constexpr uint32_t kB2Oob = 0xFFFFFFF0u;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t b2_rsrc(const void* base) {
-  const uint64_t v = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7FFFFFF0, 0x00020000);
-}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t b2_rsrc(const void* base) { return tds_buffer_rsrc(base, 0x7FFFFFF0u); }
 
 // 16 zero bytes: the LDS-DMA source of staged p1 records outside the image
 __device__ __attribute__((aligned(16))) uint32_t g_b2_zero[4] = {0u, 0u, 0u, 0u};

@@ -399,88 +399,6 @@ __global__ void bn_finalize_shifted_kernel(const double* __restrict__ partial, i
   aff[C + c] = bt - (float)mean * gm * invstd;
 }
 
-// ============================================================================ x autocorrelation (Gram of conv1 patches)
-// full[b][dy+4][dx+4] = sum_u x(u) x(u+d) over the image (0 outside), d in [-4,4]^2 with
-// (dy > 0) or (dy == 0 and dx >= 0) computed, the rest by symmetry in the finalize.
-// A thread owns 4 consecutive pixels of a row; a workgroup a 16 x 64 tile (+4 halo right/below, +4 left).
-constexpr int AC_TR = 16, AC_TC = 64;
-__global__ __launch_bounds__(256) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
-                                                         int B, int H, int W) {
-  __shared__ __attribute__((aligned(16))) float xs[(AC_TR + 4) * (AC_TC + 12)];
-  __shared__ double red[4][42];
-  constexpr int XS = AC_TC + 12;  // cols c0-4 .. c0+TC+4 (+pad)
-  const int tid = threadIdx.x;
-  const int tiles_c = (W + AC_TC - 1) / AC_TC, tiles_r = (H + AC_TR - 1) / AC_TR;
-  const int total = tiles_c * tiles_r * B;
-  float acc[42];
-#pragma unroll
-  for (int i = 0; i < 42; ++i) acc[i] = 0.f;
-  const int tr = tid >> 4, tc = (tid & 15) * 4;  // thread: row tr, cols tc..tc+3
-  // staging: rows r0..r0+19, cols c0-4 .. c0+71 as 19 float4 per row (W % 4 == 0), next tile prefetched
-  constexpr int NV = (AC_TR + 4) * 19;
-  constexpr int PER = (NV + 255) / 256;
-  float4 pre[PER];
-  auto load_tile = [&](int t) {
-    const int b = t / (tiles_c * tiles_r), rem = t % (tiles_c * tiles_r);
-    const int r0 = (rem / tiles_c) * AC_TR, c0 = (rem % tiles_c) * AC_TC;
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = tid + 256 * u;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < NV) {
-        const int rr = e / 19, cv = e - rr * 19;
-        const int gr = r0 + rr, gc = c0 - 4 + 4 * cv;
-        if (gr < H && gc >= 0 && gc < W) v = *reinterpret_cast<const float4*>(x + ((int64_t)b * H + gr) * W + gc);
-      }
-      pre[u] = v;
-    }
-  };
-  int t = blockIdx.x;
-  if (t < total) load_tile(t);
-  for (; t < total; t += gridDim.x) {
-    const int rem = t % (tiles_c * tiles_r);
-    const int r0 = (rem / tiles_c) * AC_TR, c0 = (rem % tiles_c) * AC_TC;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = tid + 256 * u;
-      if (e < NV) {
-        const int rr = e / 19, cv = e - rr * 19;
-        *reinterpret_cast<float4*>(xs + rr * XS + 4 * cv) = pre[u];
-      }
-    }
-    __syncthreads();
-    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
-    // own pixels: xs[tr][tc+4 .. tc+7]; window rows tr..tr+4, cols tc .. tc+11
-    float w[5][12];
-#pragma unroll
-    for (int dy = 0; dy < 5; ++dy)
-#pragma unroll
-      for (int c = 0; c < 12; ++c) w[dy][c] = xs[(tr + dy) * XS + tc + c];
-    const bool valid_row = (r0 + tr) < H;
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      const float u = (valid_row && c0 + tc + p < W) ? w[0][4 + p] : 0.f;
-      int i = 0;
-#pragma unroll
-      for (int dx = 0; dx <= 4; ++dx) acc[i++] += u * w[0][4 + p + dx];
-#pragma unroll
-      for (int dy = 1; dy <= 4; ++dy)
-#pragma unroll
-        for (int dx = -4; dx <= 4; ++dx) acc[i++] += u * w[dy][4 + p + dx];
-      acc[41] += u;
-    }
-  }
-  const int lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-  for (int i = 0; i < 42; ++i) {
-    const float s = wave_sum(acc[i]);
-    if (lane == 0) red[wv][i] = s;
-  }
-  __syncthreads();
-  if (tid < 42) partial[(int64_t)blockIdx.x * 42 + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
-}
-
 // Border strips: for each image, line L in {row 0,1,H-2,H-1, col 0,1,W-2,W-1} and d in
 // [-4,4]^2: strip[L][d] = sum_{u on line L} x(u) x(u+d); also plain line sums (d = "none").
 // grid: (82 (81 d + 1 plain), 8 lines), block reduces over B images and the line.
@@ -912,8 +830,7 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
                      gamma, beta, stats, running_mean, running_var, num_batches, aff);
 }
 
-void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
+void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st) {
   hipLaunchKernelGGL(x_border_kernel, dim3(82, 8), dim3(256), 0, st, x, strips, B, H, W);
 }
 

@@ -347,13 +347,7 @@ __global__ __launch_bounds__(64 * NW, 2) void head_bwd_ya_kernel(const float* __
 constexpr int HS_RUN = 1024;
 typedef unsigned int hs_u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t hs_rsrc(const void* base) {
-  const uint64_t v = reinterpret_cast<uint64_t>(base);
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
-  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, 0x7FFFFFF0, 0x00020000);
-}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t hs_rsrc(const void* base) { return tds_buffer_rsrc(base, 0x7FFFFFF0u); }
 
 __device__ __forceinline__ float4 hs_ld(__amdgpu_buffer_rsrc_t r, uint32_t vo, uint32_t so) {
   return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, vo, so, 0));

@@ -89,6 +89,8 @@ void tds_l1_apply(const float* x, const float* w1, const float* b1, const float*
 void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
                              float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
                              float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
+int tds_x_autocorr_num_wg(int B, int H, int W);  // partial rows tds_x_autocorr writes
+void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st);
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
 int tds_head_fwd_nblk(int Q);
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,

@@ -1,0 +1,102 @@
+// x autocorrelation for the closed-form BN1 statistics (the conv1
+// batch-norm moments come from the Gram of the 5x5 input patches instead of a pass over the
+// 16-channel conv1 output).  Built with -fno-slp-vectorize (_build.HIP_FILE_FLAGS).
+#include "common.h"
+#include "launchers.h"
+
+namespace tds {
+
+// ============================================================================ x autocorrelation (Gram of conv1 patches)
+// full[b][dy+4][dx+4] = sum_u x(u) x(u+d) over the image (0 outside), d in [-4,4]^2 with
+// (dy > 0) or (dy == 0 and dx >= 0) computed, the rest by symmetry in the finalize.
+// A thread owns a 4-column x AC_RB-row block of pixels and keeps the rows it multiplies
+// (AC_RB + 4 rows x 12 columns: cols c-4 .. c+7) in registers: no LDS, no barriers (the
+// LDS-tiled form with two barriers per 16 x 64 tile ran at 0.19 ms, latency bound).  A wave
+// covers 256 consecutive columns, so every row load is a 1 KB run; neighbours' halo reloads hit
+// L2.  Requires B*H*W*4 < 2^31 (tds_x_autocorr_num_wg returns 0 beyond).  Each fp32 accumulator sums 4 * AC_RB = 32 products; waves reduce in fp32, the workgroup
+// in fp64 (partial[wg][42], slot 41 = plain sum).  Requires W % 4 == 0.
+constexpr int AC_RB = 8;
+
+static int x_autocorr_num_wg(int B, int H, int W) {
+  if ((int64_t)B * H * W * 4 >= 0x7FFFFFF0LL || W % 4 != 0) return 0;
+  const int64_t threads = (int64_t)B * ((H + AC_RB - 1) / AC_RB) * (W / 4);
+  return (int)((threads + 255) / 256);
+}
+
+__global__ __launch_bounds__(256, 3) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
+                                                         int B, int H, int W) {
+  __shared__ double red[4][42];
+  const int tid = threadIdx.x;
+  const int ncg = W / 4, nband = (H + AC_RB - 1) / AC_RB;
+  const int64_t gt = (int64_t)blockIdx.x * 256 + tid;
+  float acc[42];
+#pragma unroll
+  for (int i = 0; i < 42; ++i) acc[i] = 0.f;
+  if (gt < (int64_t)B * nband * ncg) {
+    const int cg = (int)(gt % ncg);
+    const int64_t rest = gt / ncg;
+    const int band = (int)(rest % nband), b = (int)(rest / nband);
+    const int c = 4 * cg, r0 = band * AC_RB;
+    // one buffer descriptor over x: lanes outside the image read zeros by the range check
+    const __amdgpu_buffer_rsrc_t rx = tds_buffer_rsrc(x, (uint32_t)((int64_t)B * H * W * 4));
+    constexpr uint32_t kOob = 0xFFFFFFF0u;
+    const uint32_t base = (uint32_t)(((int64_t)b * H * W + c) * 4);
+    const bool has_l = c >= 4, has_r = c + 4 < W;
+    auto ld_row = [&](int r, float (&row)[12]) {
+      const uint32_t o = base + (uint32_t)r * (uint32_t)W * 4u;
+      const bool in = r < H;
+      const float4 v0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, in && has_l ? o - 16 : kOob, 0, 0));
+      const float4 v1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, in ? o : kOob, 0, 0));
+      const float4 v2 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rx, in && has_r ? o + 16 : kOob, 0, 0));
+      row[0] = v0.x; row[1] = v0.y; row[2] = v0.z; row[3] = v0.w;
+      row[4] = v1.x; row[5] = v1.y; row[6] = v1.z; row[7] = v1.w;
+      row[8] = v2.x; row[9] = v2.y; row[10] = v2.z; row[11] = v2.w;
+    };
+    // 5-row ring (own row + 4 below) plus the next row in flight
+    float w[5][12], nx[12];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) ld_row(r0 + i, w[i]);
+#pragma unroll 1
+    for (int i = 0; i < AC_RB; ++i) {
+      if (i + 1 < AC_RB) ld_row(r0 + i + 5, nx);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const float u = w[0][4 + p];  // rows >= H loaded as zeros
+        int k = 0;
+#pragma unroll
+        for (int dx = 0; dx <= 4; ++dx) acc[k++] += u * w[0][4 + p + dx];
+#pragma unroll
+        for (int dy = 1; dy <= 4; ++dy)
+#pragma unroll
+          for (int dx = -4; dx <= 4; ++dx) acc[k++] += u * w[dy][4 + p + dx];
+        acc[41] += u;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int q = 0; q < 12; ++q) w[k][q] = w[k + 1][q];
+#pragma unroll
+      for (int q = 0; q < 12; ++q) w[4][q] = nx[q];
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < 42; ++i) {
+    const float s = wave_sum(acc[i]);
+    if (lane == 0) red[wv][i] = s;
+  }
+  __syncthreads();
+  if (tid < 42) partial[(int64_t)blockIdx.x * 42 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
+}  // namespace tds
+
+using namespace tds;
+
+int tds_x_autocorr_num_wg(int B, int H, int W) { return x_autocorr_num_wg(B, H, W); }
+
+void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
+  if (nwg != x_autocorr_num_wg(B, H, W)) return;  // the partial buffer is sized by tds_x_autocorr_num_wg
+  hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
+  tds_x_border(x, strips, B, H, W, st);
+}
