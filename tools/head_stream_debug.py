@@ -35,6 +35,19 @@ def run(P, B=5, NC=10, timing=False):
     partial2 = torch.stack([y2.double().sum((0, 1, 2)), (y2.double() ** 2).sum((0, 1, 2))], 1).contiguous()
     ya = torch.empty(B, 32 * Q * Q, device=dev)
     _, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, None, ya)
+    fw = {}
+    for f in ("1", "0"):
+        os.environ["TDS_HEAD_FWD"] = f
+        ya_f = torch.empty_like(ya)
+        xo = torch.empty_like(ya)
+        r = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, xo, ya_f)
+        fw[f] = [t.clone() for t in r] + [ya_f, xo]
+        if timing:
+            fw["ms" + f] = timeit(lambda: ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5,
+                                                                 wfc, bfc, None, ya_f))
+    os.environ.pop("TDS_HEAD_FWD")
+    print(P, "fwd wide vs narrow maxdiff", [float((u - v).abs().max()) for u, v in zip(fw["0"], fw["1"])],
+          {k: v for k, v in fw.items() if k.startswith("ms")}, flush=True)
     dl = torch.randn(B, NC, device=dev)
     ref = [t.clone() for t in ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, None, 1.0, True)]
     out = {}

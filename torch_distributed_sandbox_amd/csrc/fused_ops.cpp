@@ -199,7 +199,7 @@ static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const
   }
   r.g2m = at::empty({B, 32, Q, Q}, y2.options());  // planar (fc flatten order)
   const bool use_ya = ya.has_value() && ya->defined() && tds_head_bwd_ya_supported((int)B, (int)P, (int)NC);
-  int nblk = use_ya ? tds_head_bwd_ya_nblk((int)B, (int)P, (int)NC) : tds_head_fwd_nblk((int)Q);
+  int nblk = use_ya ? tds_head_bwd_ya_nblk((int)B, (int)P, (int)NC) : tds_head_bwd_nblk((int)Q);
   auto partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
   int rc;
   rc = -1;
@@ -216,8 +216,8 @@ static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const
   TORCH_CHECK(update_lr <= 0.0 || (use_ya && rc == 0 && compute_dw),
               "fused_head_backward_g2m: update_lr needs the saved-argmax (ya) path with compute_dw");
   if (rc != 0) {
-    if (nblk != tds_head_fwd_nblk((int)Q)) {
-      nblk = tds_head_fwd_nblk((int)Q);
+    if (nblk != tds_head_bwd_nblk((int)Q)) {
+      nblk = tds_head_bwd_nblk((int)Q);
       partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
     }
     rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(), dlogits.data_ptr<float>(),

@@ -444,6 +444,149 @@ __global__ __launch_bounds__(256) void head_bwd_stream_kernel(
   }
 }
 
+// Forward, wide tiles (the default; TDS_HEAD_FWD=1 selects head_fwd_kernel): workgroup = one
+// pooled row x 128 pooled columns, 16 waves x 2 channels, lane = columns l and l + 64.  A wave's
+// fc-weight loads and ya stores for a channel are two back-to-back 256 B runs (512 B
+// contiguous) instead of one: tools/micro/runlen_bw.hip puts 256 B runs at ~2.9 TB/s and
+// 512 B runs at ~3.8 TB/s for this plane mix.  The y2 rows are staged as in head_fwd_kernel
+// (2 rows x 256 NHWC records, 72 KB LDS, one workgroup per CU); the next image's records are
+// prefetched into registers while the current one is reduced.
+template <int NW, int PXL>
+struct HeadTile2 {
+  static constexpr int THREADS = 64 * NW;
+  static constexpr int PX = 64 * PXL;                        // pooled columns per tile
+  static constexpr int PER = (2 * 2 * PX * 8) / THREADS;     // float4 per thread per image
+  static constexpr int LDS = 2 * 2 * PX * HD_REC;
+  const float4* y2;
+  int P, Q, py, px0;
+  __device__ void load(int b, float4 (&pre)[PER]) const {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = threadIdx.x + u * THREADS;
+      const int chunk = e & 7, rec = (e >> 3) % (2 * PX), row = (e >> 3) / (2 * PX);
+      const int col = 2 * px0 + rec;
+      pre[u] = col < 2 * Q ? y2[(((int64_t)b * P + 2 * py + row) * P + col) * 8 + chunk] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  __device__ static void store(char* lds, const float4 (&pre)[PER]) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = threadIdx.x + u * THREADS;
+      const int chunk = e & 7, rec = (e >> 3) % (2 * PX), row = (e >> 3) / (2 * PX);
+      *reinterpret_cast<float4*>(lds + (row * 2 * PX + rec) * HD_REC + chunk * 16) = pre[u];
+    }
+  }
+};
+
+template <int NW, int PXL>
+__global__ __launch_bounds__(64 * NW) void head_fwd2_kernel(const float4* __restrict__ y2, const float* __restrict__ Wfc,
+                                                            const float* __restrict__ aff2, double* __restrict__ partial,
+                                                            float* __restrict__ xout, float* __restrict__ yaout, int B,
+                                                            int P, int Q, int NC) {
+  constexpr int CPW = 32 / NW;
+  using Tile = HeadTile2<NW, PXL>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float red[NW][HD_MAXB * 10];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const Tile tile{y2, P, Q, (int)blockIdx.y, (int)blockIdx.x * Tile::PX};
+  const int64_t QQ = (int64_t)Q * Q;
+  bool valid[PXL];
+  int64_t pos[PXL];
+#pragma unroll
+  for (int k = 0; k < PXL; ++k) {
+    const int px = tile.px0 + lane + 64 * k;
+    valid[k] = px < Q;
+    pos[k] = (int64_t)tile.py * Q + px;
+  }
+  float w[10][PXL][CPW], a[CPW], bb[CPW];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    a[c] = aff2[CPW * wv + c];
+    bb[c] = aff2[32 + CPW * wv + c];
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+#pragma unroll
+      for (int k = 0; k < PXL; ++k)
+        w[j][k][c] = (valid[k] && j < NC) ? Wfc[((int64_t)j * 32 + CPW * wv + c) * QQ + pos[k]] : 0.f;
+  }
+  float4 pre[Tile::PER];
+  tile.load(0, pre);
+#pragma unroll 1
+  for (int b = 0; b < B; ++b) {
+    __syncthreads();
+    Tile::store(smem, pre);
+    __syncthreads();
+    if (b + 1 < B) tile.load(b + 1, pre);
+    float s[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) s[j] = 0.f;
+#pragma unroll
+    for (int k = 0; k < PXL; ++k) {
+      // BN2 affine + max-pool over the 2x2 window of column lane + 64k (same fmaf / scan
+      // order / NaN rule as head_window)
+      float y[4][CPW];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int row = q >> 1, rec = 2 * (lane + 64 * k) + (q & 1);
+        const char* src = smem + (row * 2 * Tile::PX + rec) * HD_REC + wv * CPW * 4;
+        if constexpr (CPW == 2) {
+          const float2 u = *reinterpret_cast<const float2*>(src);
+          y[q][0] = u.x; y[q][1] = u.y;
+        } else {
+          const float4 u = *reinterpret_cast<const float4*>(src);
+          y[q][0] = u.x; y[q][1] = u.y; y[q][2] = u.z; y[q][3] = u.w;
+        }
+      }
+      float p[CPW], ya[CPW];
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) {
+        float m = fmaf(a[c], y[0][c], bb[c]), yv = y[0][c];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) {
+          const float z = fmaf(a[c], y[q][c], bb[c]);
+          if (z > m || isnan(z)) { m = z; yv = y[q][c]; }
+        }
+        p[c] = m > 0.f ? m : (isnan(m) ? m : 0.f);
+        ya[c] = yv;
+      }
+      if (valid[k]) {
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+          const int64_t o = ((int64_t)b * 32 + CPW * wv + c) * QQ + pos[k];
+          if (xout != nullptr) xout[o] = p[c];
+          if (yaout != nullptr) yaout[o] = ya[c];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 10; ++j)
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) s[j] += p[c] * w[j][k][c];
+    }
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const float t = wave_sum(s[j]);
+      if (lane == 0) red[wv][b * 10 + j] = t;
+    }
+  }
+  __syncthreads();
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  for (int i = threadIdx.x; i < B * NC; i += blockDim.x) {
+    const int b = i / NC, j = i % NC;
+    double t = 0.0;
+#pragma unroll
+    for (int w8 = 0; w8 < NW; ++w8) t += (double)red[w8][b * 10 + j];
+    partial[(int64_t)blk * B * NC + i] = t;
+  }
+}
+
+constexpr int HF2_NW = 16, HF2_PXL = 2;
+using HF2Tile = HeadTile2<HF2_NW, HF2_PXL>;
+
+static bool head_fwd_wide() {
+  const char* e = std::getenv("TDS_HEAD_FWD");  // per call: in-process A/B
+  return !(e && std::atoi(e) == 1);
+}
+
 constexpr int HD_FWD_NW = 8;
 constexpr int HD_BWD_NW = 16;
 
@@ -452,6 +595,8 @@ static void head_lds_limits() {
   if (done) return;
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_fwd_kernel<HD_FWD_NW>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, HD_LDS);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_fwd2_kernel<HF2_NW, HF2_PXL>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, HF2Tile::LDS);
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_bwd_kernel<HD_BWD_NW, true>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, HD_LDS);
   (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_bwd_kernel<HD_BWD_NW, false>),
@@ -463,7 +608,12 @@ static void head_lds_limits() {
 
 using namespace tds;
 
-int tds_head_fwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }
+int tds_head_bwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }  // head_bwd_kernel (y2 path)
+
+int tds_head_fwd_nblk(int Q) {
+  const int px = head_fwd_wide() ? HF2Tile::PX : HD_PX;
+  return ((Q + px - 1) / px) * Q;
+}
 
 // partial: double [nblk][B*NC]; sums: double [B*NC] workspace
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
@@ -471,9 +621,15 @@ int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const flo
   const int Q = P / 2;
   if (B > HD_MAXB || NC > 10 || Q < 1) return -1;
   head_lds_limits();
-  const dim3 grid((Q + HD_PX - 1) / HD_PX, Q);
-  hipLaunchKernelGGL(head_fwd_kernel<HD_FWD_NW>, grid, dim3(64 * HD_FWD_NW), HD_LDS, st,
-                     reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, xout, yaout, B, P, Q, NC);
+  const bool wide = head_fwd_wide();
+  const int px = wide ? HF2Tile::PX : HD_PX;
+  const dim3 grid((Q + px - 1) / px, Q);
+  if (wide)
+    hipLaunchKernelGGL((head_fwd2_kernel<HF2_NW, HF2_PXL>), grid, dim3(64 * HF2_NW), HF2Tile::LDS, st,
+                       reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, xout, yaout, B, P, Q, NC);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<HD_FWD_NW>, grid, dim3(64 * HD_FWD_NW), HD_LDS, st,
+                       reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, xout, yaout, B, P, Q, NC);
   const int nblk = grid.x * grid.y, BN = B * NC;
   tds_reduce_partials(partial, sums, BN, nblk, BN, 0, BN, st);
   hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);

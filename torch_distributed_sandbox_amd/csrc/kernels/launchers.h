@@ -93,6 +93,7 @@ int tds_x_autocorr_num_wg(int B, int H, int W);  // partial rows tds_x_autocorr 
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st);
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
 int tds_head_fwd_nblk(int Q);
+int tds_head_bwd_nblk(int Q);  // partial rows of tds_head_bwd (y2 path)
 int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
                  float* logits, float* xout, float* yaout, int B, int P, int NC, hipStream_t st);
 int tds_head_bwd_ya_max_batch();
