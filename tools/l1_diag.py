@@ -40,6 +40,17 @@ def main():
             res.setdefault(f"l1_fwd_v{ver}", []).append(
                 timeit(lambda: ops.fused_l1_forward(x, w1, b1, g1, be1, None, None, None, 0.1, 1e-5)))
     os.environ.pop("TDS_L1_CONV")
+    # backward: sparse VALU (TDS_L1_BWD=1) vs MFMA (default) on the forward's saved tensors
+    p1, idx1, stats1, gram = ops.fused_l1_forward(x, w1, b1, g1, be1, None, None, None, 0.1, 1e-5)
+    dp1 = torch.randn(B, H // 2, H // 2, 16, device=dev) * 1e-3
+    outs = {}
+    for ver in ("1", "0"):
+        os.environ["TDS_L1_BWD"] = ver
+        outs[ver] = [t.clone() for t in ops.fused_l1_backward(dp1, x, p1, idx1, w1, b1, g1, stats1, gram, 1.0)]
+        res[f"l1_bwd_{'sparse' if ver == '1' else 'mfma'}"] = timeit(
+            lambda: ops.fused_l1_backward(dp1, x, p1, idx1, w1, b1, g1, stats1, gram, 1.0))
+    os.environ.pop("TDS_L1_BWD")
+    res["l1_bwd_rel_err"] = [float((u - v).norm() / v.norm().clamp_min(1e-30)) for u, v in zip(outs["0"], outs["1"])]
     print(res, flush=True)
 
 

@@ -326,12 +326,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   const float* g = optf(gamma1, 16, "bn1.weight");
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
-  const int nwg = l1_wg();
-  auto partial = at::empty({(int64_t)nwg * 16 * 27}, x.options().dtype(at::kDouble));
+  const int nwg = tds_fused_num_wg(3), rows = tds_l1_bwd_rows(nwg);  // 3 workgroups fit a CU (156 VGPRs)
+  auto partial = at::empty({(int64_t)rows * 16 * 27}, x.options().dtype(at::kDouble));
   tds_l1_bwd(x.data_ptr<float>(), dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(), w1.data_ptr<float>(),
              b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
-  tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, nwg, 16 * 27, 0, 16 * 27, st);
+  tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);
   auto dw1 = at::empty({16, 1, 5, 5}, x.options());
   auto db1 = at::empty({16}, x.options());
   auto dg = at::empty({16}, x.options());

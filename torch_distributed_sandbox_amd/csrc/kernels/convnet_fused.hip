@@ -156,7 +156,7 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
               if (z1 > m) { m = z1; a = 2; }
               if (z1n > m) { m = z1n; a = 3; }
               pv[r] = fmaxf(m, 0.f);
-              ixw |= a << (8 * r);
+              ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);  // bit 2: ReLU passes the gradient
               nsum += (z0 + z0n) + (z1 + z1n);
             }
             if (__builtin_amdgcn_ballot_w64(isnan(nsum)) != 0) {
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ 
                 for (int q = 1; q < 4; ++q)
                   if (zz[r][q] > m || isnan(zz[r][q])) { m = zz[r][q]; a = q; }
                 pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
-                ixw |= a << (8 * r);
+                ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);
               }
             }
             uint32_t h01, l01, h23, l23;
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
               if (z1 > m) { m = z1; a = 2; }
               if (z1n > m) { m = z1n; a = 3; }
               pv[r] = fmaxf(m, 0.f);
-              ixw |= a << (8 * r);
+              ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);  // bit 2: ReLU passes the gradient
               nsum += (z0 + z0n) + (z1 + z1n);
             }
             if (__builtin_amdgcn_ballot_w64(isnan(nsum)) != 0) {
@@ -347,7 +347,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
                 for (int q = 1; q < 4; ++q)
                   if (zz[r][q] > m || isnan(zz[r][q])) { m = zz[r][q]; a = q; }
                 pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
-                ixw |= a << (8 * r);
+                ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);
               }
             }
             uint32_t h01, l01, h23, l23;
@@ -559,20 +559,22 @@ constexpr int LB_XR = 2 * LB_PR + 4;
 constexpr int LB_XS = 76;  // LDS x row stride (floats); column 0 <-> global column 2*pc0 - 4
 constexpr int LB_NACC = 27;
 constexpr int LB_NP = LB_PR * LB_PC;                     // pooled pixels per tile
-constexpr int LB_V_DP = LB_NP * 4, LB_V_PH = LB_NP * 2, LB_V_ID = LB_NP, LB_V_X = LB_XR * 18;
+constexpr int LB_V_DP = LB_NP * 4, LB_V_PH = 0, LB_V_ID = LB_NP, LB_V_X = LB_XR * 18;
 constexpr int LB_V = LB_V_DP + LB_V_PH + LB_V_ID + LB_V_X;  // 16-B vectors staged per tile
+// The argmax byte carries the ReLU mask in bit 2 (set by l1_conv: pooled max > 0), so the
+// backward never reads p1 (720 MB of 64-B hi|lo records at the bench shape).
 constexpr int LB_PER = (LB_V + 255) / 256;
 __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dp1,
                                                      const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
                                                      const float* __restrict__ w1, const float* __restrict__ b1,
                                                      double* __restrict__ partial, int B, int H, int W) {
-  // LDS: dp1 tile [256][16] f32 | p1-hi tile [256][16] bf16 | argmax tile [256][16] u8 | x tile
-  __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 32 + LB_NP * 16 + LB_XR * LB_XS * 4];
+  // LDS: dp1 tile [256][16] f32 | argmax tile [256][16] u8 (bit 2 = ReLU mask) | x tile
+  __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LB_XR * LB_XS * 4];
   __shared__ float red[4][16][LB_NACC + 1];
   float* dps = reinterpret_cast<float*>(lds);
-  unsigned short* phs = reinterpret_cast<unsigned short*>(lds + LB_NP * 64);
-  uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 96);
-  float* xs = reinterpret_cast<float*>(lds + LB_NP * 112);
+  unsigned short* phs = nullptr;
+  uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 64);
+  float* xs = reinterpret_cast<float*>(lds + LB_NP * 80);
   const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
   const int P = H / 2, PW = W / 2;
   const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
@@ -634,10 +636,10 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
     __syncthreads();
     if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
     for (int pp = slot; pp < LB_NP; pp += 16) {
-      const float phf = bf16_to_f32(phs[pp * 16 + c]);
-      if (!(phf > 0.f)) continue;  // pooled value 0 (or out of range): ReLU blocks the gradient
+      const int ab = ids[pp * 16 + c];
+      if (!(ab & 4)) continue;  // pooled value <= 0 (or out of range): ReLU blocks the gradient
       const float dz = dps[pp * 16 + c];
-      const int a = ids[pp * 16 + c];
+      const int a = ab & 3;
       const int pr = pp / LB_PC, pc = pp - (pp / LB_PC) * LB_PC;
       const int lr = 2 * pr + (a >> 1), lc = 2 * pc + (a & 1) + 2;  // patch origin in the x tile
       const float* xp = xs + lr * LB_XS + lc;
@@ -663,6 +665,179 @@ __global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x
     double s = 0.0;
     for (int k = 0; k < 4; ++k) s += red[k][cc][i];
     partial[((int64_t)blockIdx.x * 16 + cc) * LB_NACC + i] = s;
+  }
+}
+
+// ============================================================================ layer-1 backward (MFMA)
+// The sums the sparse kernel above forms with 25 VALU FMAs per active (pooled pixel,
+// channel) as one matrix product on v_mfma_f32_16x16x32_bf16 (bf16x3 split):
+//   D[co][n] = sum_pixels dz1[co][pix] * X[pix][n],  X[pix][n] = x(pix + tap n) for n < 25,
+//   X[pix][25] = 1 (-> sum dz1), n = 26..31 zero pads;
+// dz1[co][pix] = dp1 at the pooled window's argmax when the pooled value is > 0, else 0 (the
+// dense full-resolution form of the sparse routing).  M = 16 channels, K = 32 pixels (2 rows
+// x 16 columns), N = 32 taps in two MFMA blocks.  Tile = 16 x 64 conv1 pixels = 8 x 32 pooled
+// (the sparse kernel's tile); 4 waves, wave w = row pairs 2w, 2w+1 x 4 column segments.  The
+// dp1 / argmax tile and the x tile (packed bf16 hi|lo words, as l1_conv_bf3 stages it)
+// go through LDS; fp32 MFMA accumulation per tile (256 pixels), fp64 across tiles.
+// partial[wg*4 + wave][16][27] in the sparse kernel's layout ([0] sum dz, [1] 0, [2+j] taps).
+constexpr int LM_XS = 80;  // x tile row stride (words): 20 rows x (72 staged + pad) columns
+__global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restrict__ x, const float* __restrict__ dp1,
+                                                          const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
+                                                          double* __restrict__ partial, int B, int H, int W) {
+  __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LB_XR * LM_XS * 4];
+  float* dps = reinterpret_cast<float*>(lds);
+  unsigned short* phs = nullptr;
+  uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 64);
+  uint32_t* xs = reinterpret_cast<uint32_t*>(lds + LB_NP * 80);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 15, g = lane >> 4, dr = g >> 1, gc = g & 1;
+  const int P = H / 2, PW = W / 2;
+  const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
+  const int per_img = tiles_c * tiles_r, total = per_img * B;
+
+  // B-operand geometry of this lane's tap in each N block: x tile word offset (tile origin:
+  // row r0 - 2, column c0 - 4) relative to the K-step base 2*rp*XS + 16*s
+  int boff[2];
+  uint32_t bconst[2];  // taps >= 25: the constant packed word (1.0 for n = 25, else 0)
+  bool bdata[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int n = 16 * blk + li;
+    bdata[blk] = n < 25;
+    const int ky = n < 25 ? n / 5 : 0, kx = n < 25 ? n % 5 : 0;
+    boff[blk] = (dr + ky) * LM_XS + 8 * gc + kx + 2;
+    bconst[blk] = n == 25 ? 0x3F800000u : 0u;  // bf16(1.0) = 0x3F80 in the hi half, lo = 0
+  }
+
+  uint4 pre[LB_PER];
+  auto load_tile = [&](int t) {
+    const int b = t / per_img, rem = t - b * per_img;
+    const int pr0 = (rem / tiles_c) * LB_PR, pc0 = (rem % tiles_c) * LB_PC;
+#pragma unroll
+    for (int u = 0; u < LB_PER; ++u) {
+      int e = tid + 256 * u;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (e < LB_V_DP + LB_V_PH + LB_V_ID) {
+        int q, nq;
+        if (e < LB_V_DP) { q = e & 3; nq = 4; e >>= 2; }
+        else if (e < LB_V_DP + LB_V_PH) { e -= LB_V_DP; q = e & 1; nq = 2; e >>= 1; }
+        else { e -= LB_V_DP + LB_V_PH; q = 0; nq = 1; }
+        const int gpr = pr0 + e / LB_PC, gpc = pc0 + e % LB_PC;
+        if (gpr < P && gpc < PW) {
+          const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
+          if (nq == 4) v = reinterpret_cast<const uint4*>(dp1)[rec * 4 + q];
+          else if (nq == 2) v = p1[rec * 4 + q];
+          else v = reinterpret_cast<const uint4*>(idx1)[rec];
+        }
+      } else if (e < LB_V) {
+        e -= LB_V_DP + LB_V_PH + LB_V_ID;
+        const int rr = e / 18, cv = e - rr * 18;
+        const int gr = 2 * pr0 - 2 + rr, gcol = 2 * pc0 - 4 + 4 * cv;
+        if (gr >= 0 && gr < H && gcol >= 0 && gcol < W)
+          v = *reinterpret_cast<const uint4*>(x + ((int64_t)b * H + gr) * W + gcol);
+      }
+      pre[u] = v;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int u = 0; u < LB_PER; ++u) {
+      int e = tid + 256 * u;
+      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[e] = pre[u];
+      else if (e < LB_V_DP + LB_V_PH) reinterpret_cast<uint4*>(phs)[e - LB_V_DP] = pre[u];
+      else if (e < LB_V_DP + LB_V_PH + LB_V_ID) reinterpret_cast<uint4*>(ids)[e - LB_V_DP - LB_V_PH] = pre[u];
+      else if (e < LB_V) {
+        e -= LB_V_DP + LB_V_PH + LB_V_ID;
+        const int rr = e / 18, cv = e - rr * 18;
+        const float4 f = __builtin_bit_cast(float4, pre[u]);
+        uint32_t h01, l01, h23, l23;
+        split2_bf16(f.x, f.y, h01, l01);
+        split2_bf16(f.z, f.w, h23, l23);
+        uint4 v;  // per value: hi in the upper half, lo in the lower half
+        v.x = __builtin_amdgcn_perm(h01, l01, 0x05040100u);
+        v.y = __builtin_amdgcn_perm(h01, l01, 0x07060302u);
+        v.z = __builtin_amdgcn_perm(h23, l23, 0x05040100u);
+        v.w = __builtin_amdgcn_perm(h23, l23, 0x07060302u);
+        *reinterpret_cast<uint4*>(xs + rr * LM_XS + 4 * cv) = v;
+      }
+    }
+  };
+
+  double dacc[2][4];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) dacc[blk][r] = 0.0;
+
+  int t = xcd_remap(blockIdx.x, gridDim.x);
+  if (t < total) load_tile(t);
+  for (; t < total; t += gridDim.x) {
+    __syncthreads();
+    store_tile();
+    __syncthreads();
+    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
+    f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int rp = 2 * wv + h;
+#pragma unroll
+      for (int sg = 0; sg < 4; ++sg) {
+        // A = dz1 for (co = li, pixels row dr, columns 8*gc + j): pooled pp = rp*32 + 8*sg + 4*gc + j/2
+        float dz[8];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int pp = rp * LB_PC + 8 * sg + 4 * gc + m;
+          const float dp = dps[pp * 16 + li];
+          const int ab = ids[pp * 16 + li], am = ab & 3;
+          const float d = (ab & 4) ? dp : 0.f;  // ReLU: a pooled value <= 0 blocks the gradient
+          dz[2 * m] = am == 2 * dr ? d : 0.f;
+          dz[2 * m + 1] = am == 2 * dr + 1 ? d : 0.f;
+        }
+        s16x8 ah, al;
+        {
+          uint32_t* hp = reinterpret_cast<uint32_t*>(&ah);
+          uint32_t* lp = reinterpret_cast<uint32_t*>(&al);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) split2_bf16(dz[2 * j], dz[2 * j + 1], hp[j], lp[j]);
+        }
+        const int base = 2 * rp * LM_XS + 16 * sg;
+#pragma unroll
+        for (int blk = 0; blk < 2; ++blk) {
+          uint32_t u[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const uint32_t w = xs[base + boff[blk] + j];
+            u[j] = bdata[blk] ? w : bconst[blk];
+          }
+          s16x8 bh, bl;
+          uint32_t* hp = reinterpret_cast<uint32_t*>(&bh);
+          uint32_t* lp = reinterpret_cast<uint32_t*>(&bl);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
+            lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+          }
+          acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
+        }
+      }
+    }
+#pragma unroll
+    for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dacc[blk][r] += (double)acc[blk][r];
+  }
+  // D layout: lane holds column n = 16*blk + li, rows co = 4*g + r
+  double* out = partial + ((int64_t)blockIdx.x * 4 + wv) * 16 * LB_NACC;
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int n = 16 * blk + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 4 * g + r;
+      if (n < 25) out[co * LB_NACC + 2 + n] = dacc[blk][r];
+      else if (n == 25) out[co * LB_NACC + 0] = dacc[blk][r];
+      else if (n == 26) out[co * LB_NACC + 1] = 0.0;
+    }
   }
 }
 
@@ -855,8 +1030,21 @@ void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const f
                      g2m, aff2, kbuf, reinterpret_cast<uint2*>(dy2), B, P, Q);
 }
 
+// TDS_L1_BWD=1 selects the sparse VALU kernel (l1_bwd_kernel); default: l1_bwd_mfma_kernel
+static bool l1_bwd_sparse() {
+  const char* e = std::getenv("TDS_L1_BWD");  // per call: in-process A/B
+  return e && std::atoi(e) == 1;
+}
+
+int tds_l1_bwd_rows(int nwg) { return l1_bwd_sparse() ? nwg : 4 * nwg; }
+
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
                 double* partial, int nwg, int B, int H, int W, hipStream_t st) {
+  if (!l1_bwd_sparse()) {
+    hipLaunchKernelGGL(l1_bwd_mfma_kernel, dim3(nwg), dim3(256), 0, st, x, dp1, reinterpret_cast<const uint4*>(p1),
+                       idx1, partial, B, H, W);
+    return;
+  }
   hipLaunchKernelGGL(l1_bwd_kernel, dim3(nwg), dim3(256), 0, st, x, dp1, reinterpret_cast<const uint4*>(p1), idx1, w1,
                      b1, partial, B, H, W);
 }

@@ -109,6 +109,7 @@ void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, c
                           float* dgamma, float* dbeta, float* kbuf, hipStream_t st);
 void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const float* kbuf, void* dy2, int B, int P,
                    hipStream_t st);
+int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
                 double* partial, int nwg, int B, int H, int W, hipStream_t st);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
