@@ -1030,12 +1030,14 @@ int tds_conv2_lds_bytes(int which) { return which == 0 ? F_LDS : (which == 1 ? D
 // Which fused backward kernel runs: 2 = conv2_bwd2_kernel (two 4-wave workgroups per CU,
 // conv2_bwd2.hip; default), 1 = conv2_bwd_fused_kernel (one 8-wave workgroup per CU).
 // TDS_CONV2_BWD selects (A/B timing, tools/conv2_diag.py).
-int tds_conv2_bwd_version() {
+int tds_conv2_bwd_version() {  // TDS_CONV2_BWD = 1 / 2 / 3 (default 3: producer/consumer waves)
   const char* e = std::getenv("TDS_CONV2_BWD");
-  return (e && std::atoi(e) == 1) ? 1 : 2;
+  const int v = e ? std::atoi(e) : 3;
+  return (v == 1 || v == 2) ? v : 3;
 }
 int tds_conv2_bwd_fused_num_wg() {
-  return tds_conv2_bwd_version() == 2 ? tds_conv2_bwd2_num_wg() : tds_conv2_num_wg();
+  const int v = tds_conv2_bwd_version();
+  return v == 2 ? tds_conv2_bwd2_num_wg() : v == 3 ? tds_conv2_bwd3_num_wg() : tds_conv2_num_wg();
 }
 
 // fused BN2/pool backward + conv2 dgrad + wgrad: y2 [B,P,P,32] f32, g2m [B,32,Q,Q] f32 (planar),
@@ -1043,8 +1045,10 @@ int tds_conv2_bwd_fused_num_wg() {
 void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
                          const short* wd, float* dp1, float* slab, float* dw, float* db, float scale, int nwg, int B,
                          int P, hipStream_t st) {
-  if (tds_conv2_bwd_version() == 2) {
-    tds_conv2_bwd2(y2, g2m, aff2, kbuf, p1, wd, dp1, slab, nwg, B, P, st);
+  const int ver = tds_conv2_bwd_version();
+  if (ver == 2 || ver == 3) {
+    if (ver == 3) tds_conv2_bwd3(y2, g2m, aff2, kbuf, p1, wd, dp1, slab, nwg, B, P, st);
+    else tds_conv2_bwd2(y2, g2m, aff2, kbuf, p1, wd, dp1, slab, nwg, B, P, st);
     hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db,
                        scale);
     return;

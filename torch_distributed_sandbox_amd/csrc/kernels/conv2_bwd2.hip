@@ -548,6 +548,147 @@ __global__ __launch_bounds__(B2_THREADS, 2) void conv2_bwd2_kernel(
   else b2_run<3, DIAG>(a, wdpack, smem, t0);
 }
 
+// ============================================================================ v3: producer/consumer waves
+// Counters on v2 (rocprofv3 --pmc, docs/KERNELS.md): MFMA busy ~41% of the kernel, ~725 VALU
+// instructions per wave per tile against ~312 MFMAs, and every wave alternating staging and
+// MFMA phases between two barriers, so with two waves per SIMD the MFMA pipe idles whenever
+// both sit in the same phase.  v3 splits the roles: one 8-wave workgroup per CU, waves 0-3 run
+// ONLY the dgrad/wgrad MFMA loops of v2 (one per SIMD), waves 4-7 ONLY stage (BN2/ReLU/pool
+// backward -> dy2 hi|lo planes; p1 by LDS-DMA).  Staging runs one tile ahead into double-
+// buffered dy2 planes, the p1 DMA two tiles ahead into triple-buffered planes, the dgrad
+// exchange slots are double-buffered, so ONE barrier per tile separates producer and
+// consumer.  The barrier is a bare s_barrier after lgkmcnt(0): a producer's register loads
+// for the tile after next stay in flight across it (its DMA is issued before those loads, so
+// the vmcnt wait the next staging pass needs for its registers also retires the DMA).
+constexpr int B3_THREADS = 512;
+constexpr int B3_DBUF = 4 * B2_DPLANE;                      // dy2 hi/lo planes of one tile
+constexpr int B3_OFF_P = 2 * B3_DBUF;                       // 61696: 3 x p1 buffers
+constexpr int B3_OFF_X = B3_OFF_P + 3 * B2_PBUF;            // 110848: 2 x exchange slots
+constexpr int B3_OFF_K = B3_OFF_X + 2 * B2_XCHG;            // 127232
+constexpr int B3_LDS = B3_OFF_K + 5 * 32 * 4;               // 127872
+static_assert(B3_LDS <= 160 * 1024 && B3_OFF_P % 16 == 0 && B3_OFF_X % 16 == 0 && B3_OFF_K % 16 == 0, "v3 LDS carve");
+
+__device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int ROLE, int DIAG>  // ROLE 0/1 = dgrad wave D, 2/3 = wgrad
+__device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict__ wdpack, char* smem, int first_t) {
+  const int lane = threadIdx.x & 63;
+  const int li = lane & 15, g = lane >> 4;
+  f32x4 R[13][2];
+#pragma unroll
+  for (int k = 0; k < 13; ++k) R[k][0] = R[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc[8];
+#pragma unroll
+  for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (ROLE < 2) b2_load_w<ROLE>(wdpack, R, lane);
+  s16x8 ones_hi, zero8;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    ones_hi[j] = (short)(li == 0 ? 0x3f80 : 0);
+    zero8[j] = 0;
+  }
+  const int hp = (g >> 1) * B2_DPLANE + (g & 1) * 16;
+  const int lp = (2 + (g >> 1)) * B2_DPLANE + (g & 1) * 16;
+  B2Tile prev{0, 0, 0, false};
+  bool have_prev = false;
+  int t = first_t;
+  for (int kk = 0; t < a.total; t += gridDim.x, ++kk) {
+    const B2Tile cur = b2_decode(a, t);
+    char* d_cur = smem + (kk & 1) * B3_DBUF;
+    char* p_cur = smem + B3_OFF_P + (kk % 3) * B2_PBUF;
+    b3_barrier();  // tile t staged; the partner's exchange slot of tile t-1 is written
+    if constexpr (ROLE < 2) {
+      if (have_prev)
+        b2_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk + 1) & 1) * B2_XCHG), acc, a.dp1,
+                             lane, prev.b, prev.r0, prev.c0, a.P);
+      b2_dgrad<ROLE, DIAG>(d_cur, R, acc, hp, lp, li);
+      b2_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + B3_OFF_X + (kk & 1) * B2_XCHG), acc, lane);
+    } else {
+      b2_wgrad<ROLE - 2, DIAG>(d_cur, p_cur, R, lane, ones_hi, zero8);
+    }
+    prev = cur;
+    have_prev = true;
+  }
+  // kk == number of tiles here; the last put went to slot (kk - 1) & 1
+  int kk_end = 0;
+  for (int tt = first_t; tt < a.total; tt += gridDim.x) ++kk_end;
+  b3_barrier();
+  if constexpr (ROLE < 2) {
+    if (have_prev)
+      b2_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk_end - 1) & 1) * B2_XCHG), acc, a.dp1,
+                           lane, prev.b, prev.r0, prev.c0, a.P);
+  } else {
+    float* out = a.slab + (int64_t)blockIdx.x * 26 * 512;
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      const int tap = 13 * (ROLE - 2) + k;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(tap * 32 + 16 * h + 4 * g + r) * 16 + li] = R[k][h][r];
+    }
+  }
+}
+
+template <int WV, int DIAG>  // staging wave WV (0..3) = workgroup wave 4 + WV
+__device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_t) {
+  if constexpr (DIAG == 5) {  // timing only: no staging at all (consumers read stale LDS)
+    for (int t = first_t; t < a.total; t += gridDim.x) b3_barrier();
+    b3_barrier();
+    return;
+  }
+  const int tid = threadIdx.x - 256;
+  const float* kc = reinterpret_cast<const float*>(smem + B3_OFF_K);
+  B2Stager<DIAG, WV> st;
+  st.init(a, tid);
+  const int G = gridDim.x;
+  int t = first_t;
+  // prologue: tile 0 staged into dy2 buffer 0 (p1 -> buffer 0), tile 1 loaded (p1 -> buffer 1)
+  if (t < a.total) {
+    const B2Tile x0 = b2_decode(a, t);
+    st.load(a, x0, tid, smem + B3_OFF_P);
+    st.store(a, x0, tid, smem, kc);
+  }
+  if (t + G < a.total) st.load(a, b2_decode(a, t + G), tid, smem + B3_OFF_P + B2_PBUF);
+  for (int kk = 0; t < a.total; t += G, ++kk) {
+    b3_barrier();  // consumers start tile kk
+    if (t + G < a.total) st.store(a, b2_decode(a, t + G), tid, smem + ((kk + 1) & 1) * B3_DBUF, kc);
+    if (t + 2 * G < a.total) st.load(a, b2_decode(a, t + 2 * G), tid, smem + B3_OFF_P + ((kk + 2) % 3) * B2_PBUF);
+  }
+  b3_barrier();
+}
+
+template <int DIAG>
+__global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
+    const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
+    const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
+    float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ order, int B, int P, int Q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  B2Args a;
+  a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.order = order;
+  a.B = B; a.P = P; a.Q = Q;
+  a.tiles_c = (P + B2_TC - 1) / B2_TC;
+  a.tiles_r = (P + B2_TH - 1) / B2_TH;
+  a.per_img = a.tiles_c * a.tiles_r;
+  a.total = a.per_img * B;
+  float* kc = reinterpret_cast<float*>(smem + B3_OFF_K);
+  if (tid < 160) kc[tid] = (tid < 64) ? aff2[tid] : kbuf[tid - 64];
+  __syncthreads();  // kc visible to the staging waves
+  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
+  switch (wv) {
+    case 0: b3_mfma<0, DIAG>(a, wdpack, smem, t0); break;
+    case 1: b3_mfma<1, DIAG>(a, wdpack, smem, t0); break;
+    case 2: b3_mfma<2, DIAG>(a, wdpack, smem, t0); break;
+    case 3: b3_mfma<3, DIAG>(a, wdpack, smem, t0); break;
+    case 4: b3_stage<0, DIAG>(a, smem, t0); break;
+    case 5: b3_stage<1, DIAG>(a, smem, t0); break;
+    case 6: b3_stage<2, DIAG>(a, smem, t0); break;
+    default: b3_stage<3, DIAG>(a, smem, t0); break;
+  }
+}
+
 }  // namespace tds
 
 using namespace tds;
@@ -558,6 +699,36 @@ static int conv2_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
   return e ? std::atoi(e) : 0;
 }
+
+int tds_conv2_bwd3_num_wg() { return tds_conv2_num_wg(); }  // one 8-wave workgroup per CU
+
+void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
+                    const short* wd, float* dp1, float* slab, int nwg, int B, int P, hipStream_t st) {
+  const int Q = P / 2;
+  const int* order = tds_tile_order(B, (P + B2_TH - 1) / B2_TH, (P + B2_TC - 1) / B2_TC);
+  if (!order) return;
+  // TDS_CONV2_DIAG (timing only): 1 no MFMAs, 3 no global tile loads, 5 no staging
+#define TDS_B3_LAUNCH(D)                                                                                               \
+  {                                                                                                                    \
+    static bool set = false;                                                                                           \
+    if (!set) {                                                                                                        \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd3_kernel<D>),                                   \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, B3_LDS);                                   \
+      set = true;                                                                                                      \
+    }                                                                                                                  \
+    hipLaunchKernelGGL(conv2_bwd3_kernel<D>, dim3(nwg), dim3(B3_THREADS), B3_LDS, st,                                  \
+                       reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, reinterpret_cast<const uint4*>(p1),       \
+                       reinterpret_cast<const uint4*>(wd), dp1, slab, order, B, P, Q);                                  \
+  }
+  switch (conv2_diag_env()) {
+    case 1: TDS_B3_LAUNCH(1) break;
+    case 3: TDS_B3_LAUNCH(3) break;
+    case 5: TDS_B3_LAUNCH(5) break;
+    default: TDS_B3_LAUNCH(0) break;
+  }
+#undef TDS_B3_LAUNCH
+}
+
 
 template <int DIAG>
 static void b2_set_lds_limit(int bytes) {

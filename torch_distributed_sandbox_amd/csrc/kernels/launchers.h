@@ -73,6 +73,9 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, float* y
 int tds_conv2_bwd_version();
 int tds_conv2_bwd_fused_num_wg();  // slab rows the fused backward needs (workgroups it launches)
 int tds_conv2_bwd2_num_wg();
+int tds_conv2_bwd3_num_wg();
+void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
+                    const short* wd, float* dp1, float* slab, int nwg, int B, int P, hipStream_t st);
 void tds_conv2_bwd2(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
                     const short* wd, float* dp1, float* slab, int nwg, int B, int P, hipStream_t st);
 void tds_conv2_dgrad_bf16x3(const void* dy2, const short* wd, float* dp1, int nwg, int B, int P, hipStream_t st);
