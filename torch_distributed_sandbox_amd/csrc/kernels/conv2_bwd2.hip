@@ -227,9 +227,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t b2_rsrc(const void* base) { re
 // 16 zero bytes: the LDS-DMA source of staged p1 records outside the image
 __device__ __attribute__((aligned(16))) uint32_t g_b2_zero[4] = {0u, 0u, 0u, 0u};
 
-template <int DIAG, int WV>  // WV: the wave (= role) this staging code runs in
+// REGP1 (v3): p1 records go global -> registers -> ds_write in store() instead of LDS-DMA.
+// The compiler cannot tell an LDS-DMA's destination from later LDS accesses, so every ds_read /
+// ds_write after one waits vmcnt(0) -- which drains the register loads issued for LATER
+// tiles too and defeats a multi-tile lookahead.
+template <int DIAG, int WV, bool REGP1 = false>  // WV: the wave (= role) this staging code runs in
 struct B2Stager {
   float4 yv[B2_IPER][4], gv[B2_IPER];
+  uint4 pr[REGP1 ? B2_DMA_PER_WAVE : 1];
   // per-thread byte offsets (fixed for the kernel): global, relative to the tile's
   // descriptor bases, and LDS, of each staging item (window x 4 channels); p1 DMA sources
   uint32_t yoff[B2_IPER], goff[B2_IPER], doff[B2_DMA_PER_WAVE];
@@ -334,12 +339,19 @@ struct B2Stager {
         if (px >= B2_REC) psrc[j] = reinterpret_cast<const char*>(g_b2_zero);
       }
     }
+    const __amdgpu_buffer_rsrc_t rp = b2_rsrc(pbase);
 #pragma unroll
     for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
-      int pl, rgp, px, half;
-      dma_geom(WV, j, 0, pl, rgp, px, half);
-      __builtin_amdgcn_global_load_lds(psrc[j], (__attribute__((address_space(3))) void*)(pbuf + pl * B2_PPLANE + rgp * 1024),
-                                       16, 0, 0);
+      if constexpr (REGP1) {
+        // buffer loads (not flat: a flat load makes every later wait a full vmcnt(0) drain)
+        const uint32_t po = psrc[j] == reinterpret_cast<const char*>(g_b2_zero) ? kB2Oob : doff[j];
+        pr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, po, 0, 0));
+      } else {
+        int pl, rgp, px, half;
+        dma_geom(WV, j, 0, pl, rgp, px, half);
+        __builtin_amdgcn_global_load_lds(psrc[j], (__attribute__((address_space(3))) void*)(pbuf + pl * B2_PPLANE + rgp * 1024),
+                                         16, 0, 0);
+      }
     }
 #pragma unroll
     for (int u = 0; u < B2_IPER; ++u) {
@@ -361,6 +373,18 @@ struct B2Stager {
   // Interior tiles take a short path: every window pooled, every pixel inside the image,
   // argmax by max3 + first-equal (torch's scan-order tie rule); a NaN anywhere in the
   // thread's windows sends the wave to the general path (torch's NaN-wins rule).
+  // REGP1: the tile's p1 records -> plane buffer pbuf (same layout the DMA writes)
+  __device__ __forceinline__ void store_p1(char* pbuf, int tid) {
+    if constexpr (REGP1) {
+#pragma unroll
+      for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
+        int pl, rgp, px, half;
+        dma_geom(WV, j, tid & 63, pl, rgp, px, half);
+        *reinterpret_cast<uint4*>(pbuf + pl * B2_PPLANE + rgp * 1024 + (tid & 63) * 16) = pr[j];
+      }
+    }
+  }
+
   __device__ __forceinline__ void store(const B2Args& a, const B2Tile& x, int tid, char* d_l, const float* kc) {
     const int c4 = tid & 7;
     const int P = a.P, Q = a.Q;
@@ -555,20 +579,128 @@ __global__ __launch_bounds__(B2_THREADS, 2) void conv2_bwd2_kernel(
 // both sit in the same phase.  v3 splits the roles: one 8-wave workgroup per CU, waves 0-3 run
 // ONLY the dgrad/wgrad MFMA loops of v2 (one per SIMD), waves 4-7 ONLY stage (BN2/ReLU/pool
 // backward -> dy2 hi|lo planes; p1 by LDS-DMA).  Staging runs one tile ahead into double-
-// buffered dy2 planes, the p1 DMA two tiles ahead into triple-buffered planes, the dgrad
+// buffered dy2 / p1 planes; its y2 / g2m / p1 register loads run three tiles ahead (two
+// register sets: staging alone was memory-latency bound; no LDS-DMA, see B2Stager), the dgrad
 // exchange slots are double-buffered, so ONE barrier per tile separates producer and
 // consumer.  The barrier is a bare s_barrier after lgkmcnt(0): a producer's register loads
-// for the tile after next stay in flight across it (its DMA is issued before those loads, so
-// the vmcnt wait the next staging pass needs for its registers also retires the DMA).
+// for later tiles stay in flight across it.
 constexpr int B3_THREADS = 512;
 constexpr int B3_DBUF = 4 * B2_DPLANE;                      // dy2 hi/lo planes of one tile
 constexpr int B3_OFF_P = 2 * B3_DBUF;                       // 61696: 3 x p1 buffers
-constexpr int B3_OFF_X = B3_OFF_P + 3 * B2_PBUF;            // 110848: 2 x exchange slots
-constexpr int B3_OFF_K = B3_OFF_X + 2 * B2_XCHG;            // 127232
-constexpr int B3_LDS = B3_OFF_K + 5 * 32 * 4;               // 127872
+constexpr int B3_NP = 2;                                   // p1 buffers (staged with dy2, one tile ahead)
+constexpr int B3_OFF_X = B3_OFF_P + B3_NP * B2_PBUF;        // 127232: 2 x exchange slots
+constexpr int B3_OFF_K = B3_OFF_X + 2 * B2_XCHG;            // 143616
+constexpr int B3_LDS = B3_OFF_K + 5 * 32 * 4;               // 144256
 static_assert(B3_LDS <= 160 * 1024 && B3_OFF_P % 16 == 0 && B3_OFF_X % 16 == 0 && B3_OFF_K % 16 == 0, "v3 LDS carve");
 
 __device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// v3 MFMA loops: the v2 loops (b2_dgrad, b2_wgrad) prefetch operands one step ahead and
+// restart the pipeline at every kx group / K-step; with ONE MFMA wave per SIMD nothing hides
+// those bubbles (v3 with staging disabled ran at ~67% MFMA utilisation).  Here each role's
+// tile is one flat, fully unrolled sequence with operands fetched two steps ahead across
+// group / K-step boundaries.
+template <int D>
+struct DgSeq {
+  static constexpr int n(int i) { return 8 + (i < 2 ? 5 : (D == 0 ? 3 : 2)) - 1; }  // rows of group i
+  static constexpr int S = n(0) + n(1) + n(2);
+  static constexpr int grp(int s) { return s < n(0) ? 0 : s < n(0) + n(1) ? 1 : 2; }
+  static constexpr int row(int s) { return s < n(0) ? s : s < n(0) + n(1) ? s - n(0) : s - n(0) - n(1); }
+  static constexpr int kx(int i) { return D == 0 ? (i == 0 ? 0 : i == 1 ? 1 : 4) : (i == 0 ? 2 : i == 1 ? 3 : 4); }
+  static constexpr int ky0(int i) { return i < 2 ? 0 : (D == 0 ? 0 : 3); }
+  static constexpr int nky(int i) { return i < 2 ? 5 : (D == 0 ? 3 : 2); }
+};
+
+template <int D, int DIAG>
+__device__ __forceinline__ void b3_dgrad(const char* d_l, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int lp,
+                                         int li) {
+  using Q = DgSeq<D>;
+#pragma unroll
+  for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
+  s16x8 ah[3], al[3];
+  auto load_a = [&](int s, int buf) {
+    const int i = Q::grp(s), r = Q::row(s);
+    const int rec = (Q::ky0(i) + r) * B2_SC + Q::kx(i) + li;
+    ah[buf] = lds8<DIAG>(d_l + hp + rec * 32);
+    al[buf] = lds8<DIAG>(d_l + lp + rec * 32);
+  };
+  load_a(0, 0);
+  load_a(1, 1);
+#pragma unroll
+  for (int s = 0; s < Q::S; ++s) {
+    if (s + 2 < Q::S) load_a(s + 2, (s + 2) % 3);
+    __builtin_amdgcn_sched_barrier(0);
+    const int i = Q::grp(s), r = Q::row(s);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int o = r - k;
+      if (k < Q::nky(i) && o >= 0 && o < 8)
+        acc[o] = mma3<DIAG>(ah[s % 3], al[s % 3], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
+                            __builtin_bit_cast(s16x8, R[5 * i + k][1]), acc[o]);
+    }
+  }
+}
+
+template <int E, int DIAG>
+__device__ __forceinline__ void b3_wgrad(const char* d_l, const char* p_l, f32x4 (&wacc)[13][2], int lane,
+                                         const s16x8& ones_hi, const s16x8& zero8) {
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  s16x8 ahi[2][2], alo[2][2], bhi[3], blo[3];
+  auto load_a = [&](int m, int slot) {
+    const int ra = (2 * m + 2) * B2_SC + 2 + 4 * g + q4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const s16x4 x0 = ldtr<DIAG>(d_l + h * B2_DPLANE + ra * 32 + p4 * 8);
+      const s16x4 x1 = ldtr<DIAG>(d_l + h * B2_DPLANE + (ra + B2_SC) * 32 + p4 * 8);
+      const s16x4 y0 = ldtr<DIAG>(d_l + (2 + h) * B2_DPLANE + ra * 32 + p4 * 8);
+      const s16x4 y1 = ldtr<DIAG>(d_l + (2 + h) * B2_DPLANE + (ra + B2_SC) * 32 + p4 * 8);
+      ahi[slot][h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      alo[slot][h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+    }
+  };
+  auto load_b = [&](int s, int buf) {
+    const int m = s / 13, tap = 13 * E + s % 13;
+    if (tap < 25) {
+      const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+      const int rb = (2 * m + ky) * B2_SC + kx + 4 * g + q4;
+      const s16x4 x0 = ldtr<DIAG>(p_l + rb * 32 + p4 * 8);
+      const s16x4 x1 = ldtr<DIAG>(p_l + (rb + B2_SC) * 32 + p4 * 8);
+      const s16x4 y0 = ldtr<DIAG>(p_l + B2_PPLANE + rb * 32 + p4 * 8);
+      const s16x4 y1 = ldtr<DIAG>(p_l + B2_PPLANE + (rb + B2_SC) * 32 + p4 * 8);
+      bhi[buf] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+      blo[buf] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+    } else {
+      bhi[buf] = ones_hi;  // bias gradient column
+      blo[buf] = zero8;
+    }
+  };
+  // K-steps m in a rolled loop (static buffer indices inside), operands rotated at the end
+  load_a(0, 0);
+  load_b(0, 0);
+  load_b(1, 1);
+#pragma unroll 1
+  for (int m = 0; m < 4; ++m) {
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      if (k + 2 < 13) load_b(13 * m + k + 2, (k + 2) % 3);
+      else if (m + 1 < 4) load_b(13 * (m + 1) + k + 2 - 13, (k + 2) % 3);  // next K-step's first taps
+      if (k == 10 && m + 1 < 4) load_a(m + 1, 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) wacc[k][h] = mma3<DIAG>(ahi[0][h], alo[0][h], bhi[k % 3], blo[k % 3], wacc[k][h]);
+    }
+    // taps 0, 1 of the next K-step sit in buffers 1, 2 (13 % 3 == 1), its A in slot 1
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      ahi[0][h] = ahi[1][h];
+      alo[0][h] = alo[1][h];
+    }
+    bhi[0] = bhi[1];
+    blo[0] = blo[1];
+    bhi[1] = bhi[2];
+    blo[1] = blo[2];
+  }
+}
 
 template <int ROLE, int DIAG>  // ROLE 0/1 = dgrad wave D, 2/3 = wgrad
 __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict__ wdpack, char* smem, int first_t) {
@@ -595,16 +727,16 @@ __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict
   for (int kk = 0; t < a.total; t += gridDim.x, ++kk) {
     const B2Tile cur = b2_decode(a, t);
     char* d_cur = smem + (kk & 1) * B3_DBUF;
-    char* p_cur = smem + B3_OFF_P + (kk % 3) * B2_PBUF;
+    char* p_cur = smem + B3_OFF_P + (kk % B3_NP) * B2_PBUF;
     b3_barrier();  // tile t staged; the partner's exchange slot of tile t-1 is written
     if constexpr (ROLE < 2) {
       if (have_prev)
         b2_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk + 1) & 1) * B2_XCHG), acc, a.dp1,
                              lane, prev.b, prev.r0, prev.c0, a.P);
-      b2_dgrad<ROLE, DIAG>(d_cur, R, acc, hp, lp, li);
+      b3_dgrad<ROLE, DIAG>(d_cur, R, acc, hp, lp, li);
       b2_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + B3_OFF_X + (kk & 1) * B2_XCHG), acc, lane);
     } else {
-      b2_wgrad<ROLE - 2, DIAG>(d_cur, p_cur, R, lane, ones_hi, zero8);
+      b3_wgrad<ROLE - 2, DIAG>(d_cur, p_cur, R, lane, ones_hi, zero8);
     }
     prev = cur;
     have_prev = true;
@@ -639,21 +771,37 @@ __device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_
   }
   const int tid = threadIdx.x - 256;
   const float* kc = reinterpret_cast<const float*>(smem + B3_OFF_K);
-  B2Stager<DIAG, WV> st;
-  st.init(a, tid);
+  // two register sets: tile j's y2 / g2m registers are loaded two iterations before they are
+  // staged (set j & 1), its p1 DMA lands in buffer j % 4
+  B2Stager<DIAG, WV, true> st0, st1;
+  st0.init(a, tid);
+  st1.init(a, tid);
   const int G = gridDim.x;
-  int t = first_t;
-  // prologue: tile 0 staged into dy2 buffer 0 (p1 -> buffer 0), tile 1 loaded (p1 -> buffer 1)
-  if (t < a.total) {
-    const B2Tile x0 = b2_decode(a, t);
-    st.load(a, x0, tid, smem + B3_OFF_P);
-    st.store(a, x0, tid, smem, kc);
+  auto tile = [&](int j) { return first_t + j * G; };
+  auto pbuf = [&](int j) { return smem + B3_OFF_P + (j % B3_NP) * B2_PBUF; };  // written in store(j)
+  auto dbuf = [&](int j) { return smem + (j & 1) * B3_DBUF; };
+  if (tile(0) < a.total) {
+    st0.load(a, b2_decode(a, tile(0)), tid, nullptr);
+    st0.store(a, b2_decode(a, tile(0)), tid, dbuf(0), kc);
+    st0.store_p1(pbuf(0), tid);
   }
-  if (t + G < a.total) st.load(a, b2_decode(a, t + G), tid, smem + B3_OFF_P + B2_PBUF);
-  for (int kk = 0; t < a.total; t += G, ++kk) {
+  if (tile(1) < a.total) st1.load(a, b2_decode(a, tile(1)), tid, nullptr);
+  if (tile(2) < a.total) st0.load(a, b2_decode(a, tile(2)), tid, nullptr);
+  // iteration kk stages tile kk+1 and loads tile kk+3 (both in set (kk+1) & 1)
+  for (int kk = 0; tile(kk) < a.total; kk += 2) {
     b3_barrier();  // consumers start tile kk
-    if (t + G < a.total) st.store(a, b2_decode(a, t + G), tid, smem + ((kk + 1) & 1) * B3_DBUF, kc);
-    if (t + 2 * G < a.total) st.load(a, b2_decode(a, t + 2 * G), tid, smem + B3_OFF_P + ((kk + 2) % 3) * B2_PBUF);
+    if (tile(kk + 1) < a.total) {
+      st1.store(a, b2_decode(a, tile(kk + 1)), tid, dbuf(kk + 1), kc);
+      st1.store_p1(pbuf(kk + 1), tid);
+    }
+    if (tile(kk + 3) < a.total) st1.load(a, b2_decode(a, tile(kk + 3)), tid, nullptr);
+    if (tile(kk + 1) >= a.total) break;
+    b3_barrier();  // consumers start tile kk + 1
+    if (tile(kk + 2) < a.total) {
+      st0.store(a, b2_decode(a, tile(kk + 2)), tid, dbuf(kk + 2), kc);
+      st0.store_p1(pbuf(kk + 2), tid);
+    }
+    if (tile(kk + 4) < a.total) st0.load(a, b2_decode(a, tile(kk + 4)), tid, nullptr);
   }
   b3_barrier();
 }
