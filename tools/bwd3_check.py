@@ -59,7 +59,8 @@ def main():
     for B, P in ((2, 37), (2, 40), (1, 128), (3, 200)):
         case(ops, dev, B, P)
     case(ops, dev, 5, 1500, timing=True)
-    # where v3's time goes (timing-only builds): 1 = no MFMAs, 3 = no global loads, 5 = no staging
+    # where v3's time goes (timing-only builds): 1 = no MFMAs, 3 = no global loads, 5 = no staging,
+    # 6 = no g2m loads, 7 = no y2 loads
     B, P = 5, 1500
     Q = P // 2
     y2 = torch.randn(B, P, P, 32, device=dev)
@@ -70,7 +71,7 @@ def main():
     _, wd = ops.conv2_pack(torch.randn(32, 16, 5, 5, device=dev) * 0.05)
     os.environ["TDS_CONV2_BWD"] = "3"
     res = {}
-    for d in ("0", "1", "3", "5"):
+    for d in ("0", "1", "3", "5", "6", "7"):
         os.environ["TDS_CONV2_DIAG"] = d
         res["diag" + d] = timeit(lambda: ops.fused_conv2_backward_y2(y2, g2m, aff2, kbuf, p1, wd, 1.0))
     os.environ.pop("TDS_CONV2_DIAG")

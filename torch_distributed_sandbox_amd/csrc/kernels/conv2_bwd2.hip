@@ -357,13 +357,15 @@ struct B2Stager {
     for (int u = 0; u < B2_IPER; ++u) {
 #pragma unroll
       for (int q = 0; q < 4; ++q)
-        yv[u][q] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy[u][q], 0, 0));
+        yv[u][q] = DIAG == 7 ? make_float4(1.f, 0.f, 0.f, 0.f)  // timing only: no y2 loads
+                             : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy[u][q], 0, 0));
       // four channel planes; an out-of-image lane stays at kB2Oob for all four (zeros)
       float g4[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        g4[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                              rg, og[u] == kB2Oob ? kB2Oob : og[u] + k * gplane, 0, 0));
+        g4[k] = DIAG == 6 ? 0.f  // timing only: no g2m loads
+                          : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                rg, og[u] == kB2Oob ? kB2Oob : og[u] + k * gplane, 0, 0));
       gv[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
     }
   }
@@ -855,7 +857,8 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
   const int Q = P / 2;
   const int* order = tds_tile_order(B, (P + B2_TH - 1) / B2_TH, (P + B2_TC - 1) / B2_TC);
   if (!order) return;
-  // TDS_CONV2_DIAG (timing only): 1 no MFMAs, 3 no global tile loads, 5 no staging
+  // TDS_CONV2_DIAG (timing only): 1 no MFMAs, 3 no global tile loads, 5 no staging, 6 no g2m loads,
+  // 7 no y2 loads
 #define TDS_B3_LAUNCH(D)                                                                                               \
   {                                                                                                                    \
     static bool set = false;                                                                                           \
@@ -872,6 +875,8 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
     case 1: TDS_B3_LAUNCH(1) break;
     case 3: TDS_B3_LAUNCH(3) break;
     case 5: TDS_B3_LAUNCH(5) break;
+    case 6: TDS_B3_LAUNCH(6) break;
+    case 7: TDS_B3_LAUNCH(7) break;
     default: TDS_B3_LAUNCH(0) break;
   }
 #undef TDS_B3_LAUNCH
