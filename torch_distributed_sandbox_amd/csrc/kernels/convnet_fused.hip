@@ -236,6 +236,10 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
     ea[r] = aff[4 * g + r];
     ebb[r] = fmaf(ea[r], b1[4 * g + r], aff[16 + 4 * g + r]);
   }
+  bool fin = true;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) fin = fin && __builtin_isfinite(ea[r]) && __builtin_isfinite(ebb[r]) && ea[r] != 0.f;
+  const bool fast_ok = __builtin_amdgcn_ballot_w64(!fin) == 0 && __syncthreads_and(fin) != 0;
 
   // x tile staging: LDS column 0 <-> global column c0-4 (16-B aligned since W % 4 == 0),
   // 20 rows x 18 float4; the next tile's loads are issued before this tile's MFMAs.
@@ -264,11 +268,13 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
     const int b = t / per_img, rem = t - b * per_img;
     const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
     __syncthreads();
+    bool nonfinite = false;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = tid + 256 * u;
       if (e < NV) {
         const int rr = e / 18, cv = e - rr * 18;
+        nonfinite |= !__builtin_isfinite((pre[u].x + pre[u].y) + (pre[u].z + pre[u].w));
         uint32_t h01, l01, h23, l23;
         split2_bf16(pre[u].x, pre[u].y, h01, l01);
         split2_bf16(pre[u].z, pre[u].w, h23, l23);
@@ -280,21 +286,24 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
         *reinterpret_cast<uint4*>(xs + rr * L1_XS + 4 * cv) = v;
       }
     }
-    __syncthreads();
+    // a non-finite x anywhere in the tile (or a degenerate BN1 affine) sends the whole tile to
+    // the general epilogue (torch's NaN rules); otherwise no window can hold a NaN
+    const bool slow = __syncthreads_or(nonfinite) != 0 || !fast_ok;
     if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
 #pragma unroll
     for (int rp = 0; rp < 2; ++rp) {
 #pragma unroll
       for (int sp = 0; sp < 2; ++sp) {
-        // 4 tiles: rows (4wv + 2rp + {0,1}) x segments (2sp + {0,1}) of 16 pixels
+        // rows (4wv + 2rp + a), 32-pixel span sp; MFMA c takes the pixels 2*li + c of the
+        // span, so a lane's two columns ARE the two columns of pooling window li: the 2x2
+        // window is acc[0..1][0..1][r] of one lane (no cross-lane exchange, no duplicate work)
         f32x4 acc[2][2];
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
           for (int c = 0; c < 2; ++c) {
-            // B = x patches: lane (px = li, g) gathers its 8 taps as packed hi|lo words
-            const int row = 4 * wv + 2 * rp + a, seg = 2 * sp + c;
-            const uint32_t* src = xs + row * L1_XS + 2 + seg * 16 + li;  // +2: tile origin is c0-4
+            const int row = 4 * wv + 2 * rp + a;
+            const uint32_t* src = xs + row * L1_XS + 2 + 32 * sp + 2 * li + c;  // +2: tile origin is c0-4
             uint32_t u[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) u[j] = src[koff[j]];
@@ -308,59 +317,41 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
             }
             acc[a][c] = mfma_bf16x3(wah, wal, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
           }
-        {
-          // BN1 affine -> 2x2 max-pool (first max in scan order; torch's NaN rule on the
-          // rare NaN window) -> ReLU -> bf16 hi|lo record + 1-byte argmax
+        // BN1 affine -> 2x2 max-pool (first max in scan order) -> ReLU -> bf16 hi|lo record +
+        // argmax byte (bit 2 = ReLU passes the gradient) for channels 4g .. 4g+3
+        const int prow = (r0 + 4 * wv + 2 * rp) >> 1;
+        const int pcol = (c0 >> 1) + 16 * sp + li;
+        float pv[4];
+        uint32_t ixw = 0;
 #pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int col = c0 + (2 * sp + c) * 16 + li;     // conv column of this lane
-            const int prow = (r0 + 4 * wv + 2 * rp) >> 1;    // pooled row
-            const int pcol = col >> 1;
-            float pv[4], zz[4][4];
-            uint32_t ixw = 0;
-            float nsum = 0.f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float z0 = fmaf(ea[r], acc[0][c][r], ebb[r]);
-              const float z1 = fmaf(ea[r], acc[1][c][r], ebb[r]);
-              const float z0n = dpp_xor1(z0);
-              const float z1n = dpp_xor1(z1);
-              zz[r][0] = z0; zz[r][1] = z0n; zz[r][2] = z1; zz[r][3] = z1n;
-              float m = z0;
-              uint32_t a = 0;
-              if (z0n > m) { m = z0n; a = 1; }
-              if (z1 > m) { m = z1; a = 2; }
-              if (z1n > m) { m = z1n; a = 3; }
-              pv[r] = fmaxf(m, 0.f);
-              ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);  // bit 2: ReLU passes the gradient
-              nsum += (z0 + z0n) + (z1 + z1n);
-            }
-            if (__builtin_amdgcn_ballot_w64(isnan(nsum)) != 0) {
-              // rare NaN window (wave-uniform branch): torch's rule, update when
-              // (v > max || isnan(v)) in scan order; relu(NaN) = NaN
-              ixw = 0;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                float m = zz[r][0];
-                uint32_t a = 0;
-#pragma unroll
-                for (int q = 1; q < 4; ++q)
-                  if (zz[r][q] > m || isnan(zz[r][q])) { m = zz[r][q]; a = q; }
-                pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
-                ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);
-              }
-            }
-            uint32_t h01, l01, h23, l23;
-            split2_bf16(pv[0], pv[1], h01, l01);
-            split2_bf16(pv[2], pv[3], h23, l23);
-            if ((li & 1) == 0 && prow < P && pcol < PW) {
-              const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
-              uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
-              dst[g] = make_uint2(h01, h23);
-              dst[4 + g] = make_uint2(l01, l23);
-              reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] = ixw;
-            }
+        for (int r = 0; r < 4; ++r) {
+          // scan order: (row 0, col 0), (row 0, col 1), (row 1, col 0), (row 1, col 1)
+          const float z0 = fmaf(ea[r], acc[0][0][r], ebb[r]), z1 = fmaf(ea[r], acc[0][1][r], ebb[r]);
+          const float z2 = fmaf(ea[r], acc[1][0][r], ebb[r]), z3 = fmaf(ea[r], acc[1][1][r], ebb[r]);
+          float m;
+          uint32_t am;
+          if (!slow) {  // every z finite (tile-uniform)
+            m = fmaxf(fmaxf(z0, z1), fmaxf(z2, z3));
+            am = z0 == m ? 0u : z1 == m ? 1u : z2 == m ? 2u : 3u;  // first max
+          } else {      // torch's rule: update when (v > max || isnan(v)), relu(NaN) = NaN
+            m = z0;
+            am = 0;
+            if (z1 > m || isnan(z1)) { m = z1; am = 1; }
+            if (z2 > m || isnan(z2)) { m = z2; am = 2; }
+            if (z3 > m || isnan(z3)) { m = z3; am = 3; }
           }
+          pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
+          ixw |= (am | (m > 0.f ? 4u : 0u)) << (8 * r);
+        }
+        uint32_t h01, l01, h23, l23;
+        split2_bf16(pv[0], pv[1], h01, l01);
+        split2_bf16(pv[2], pv[3], h23, l23);
+        if (prow < P && pcol < PW) {
+          const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
+          uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
+          dst[g] = make_uint2(h01, h23);
+          dst[4 + g] = make_uint2(l01, l23);
+          reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] = ixw;
         }
       }
     }
