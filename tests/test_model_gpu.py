@@ -22,6 +22,17 @@ class RefConvNet(nn.Module):
         return self.fc(out.reshape(out.size(0), -1))
 
 
+def near_tie_windows(a, rel=1e-5):
+    """2x2 max-pool windows of the (post-ReLU, fp64) pooling input whose two largest values
+    differ by less than rel x the layer's largest activation: windows an fp32 forward
+    (relative rounding ~1e-6 of the activation scale) may resolve the other way."""
+    B, C, H, W = a.shape
+    w = a[:, :, : H // 2 * 2, : W // 2 * 2].reshape(B, C, H // 2, 2, W // 2, 2).permute(0, 1, 2, 4, 3, 5)
+    top = w.reshape(B, C, H // 2, W // 2, 4).topk(2, dim=-1).values
+    gap = top[..., 0] - top[..., 1]
+    return int(((top[..., 0] > 0) & (gap <= rel * a.abs().max())).sum())
+
+
 def _compare(mode, gpu, H=64, B=3, steps=2):
     from torch_distributed_sandbox_amd.models import ConvNet, fc_in_features
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
@@ -34,13 +45,26 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
     opt = SGD(ours.parameters(), 0.05)
     ropt = torch.optim.SGD(ref.parameters(), 0.05)
     crit = CrossEntropyLoss()
+    pool_in = []
+    for pool in (ref.layer1[3], ref.layer2[3]):
+        pool.register_forward_hook(lambda mod, inp, out: pool_in.append(inp[0].detach()))
     for s in range(steps):
+        # Re-sync the reference to our parameters every step: each step's gradients are then
+        # checked on identical weights.  Free-running fp32 and fp64 trajectories drift apart
+        # after one SGD step (at lr 0.05 a 1e-6 weight difference flips near-tied max-pool
+        # windows), which made a multi-step comparison measure chaos, not kernel error.  The
+        # update itself is pinned below against p - lr * p.grad.
+        with torch.no_grad():
+            for (n, p), q in zip(ours.named_parameters(), ref.parameters()):
+                q.copy_(p.detach().double().cpu())
         x = torch.rand(B, 1, H, H, device=gpu)
         y = torch.randint(0, 10, (B,), device=gpu)
         loss = crit(ours(x), y)
         opt.zero_grad()
         loss.backward()
+        pool_in.clear()
         rloss = nn.functional.cross_entropy(ref(x.double().cpu()), y.cpu())
+        ties = sum(near_tie_windows(a) for a in pool_in)
         ropt.zero_grad()
         rloss.backward()
         assert abs(loss.item() - rloss.item()) < 1e-4 * max(1, abs(rloss.item())), (loss.item(), rloss.item())
@@ -53,12 +77,23 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
                 wg = rp[n.replace("bias", "weight")].grad.abs().max().item()
                 assert (g - rg).abs().max().item() <= 1e-3 * wg + 1e-5, f"step {s} {n}"
                 continue
-            # relative L2 error: robust to the rare max-pool argmax flips that any
-            # non-fp64 arithmetic produces on near-tied windows
+            # relative L2 error.  A non-fp64 forward can flip a near-tied max-pool window
+            # against the fp64 reference; one flip reroutes one pooled gradient and moves a conv
+            # weight gradient by ~1/sqrt(#windows) (5.6e-3 for one layer-2 flip at H=128, B=2,
+            # tools/model_grad_check.py).  The wider bound applies only when the fp64 forward
+            # itself shows a window tied to within fp32 rounding (near_tie_windows), and only to
+            # the parameters a rerouted window reaches through a different input patch (conv
+            # weights, BN1); BN2 and fc see the same tied value either way and stay at 2e-3.
             rel = ((g - rg).norm() / rg.norm().clamp_min(1e-30)).item()
-            assert rel <= 2e-3, f"step {s} {n}: rel L2 err {rel:.3e}"
+            flip_reach = n.startswith("layer1.") or n.startswith("layer2.0.")
+            tol = 2e-2 if ties and flip_reach else 2e-3
+            assert rel <= tol, f"step {s} {n}: rel L2 err {rel:.3e} (near-tied windows: {ties})"
+        before = {n: (p.detach().clone(), p.grad.detach().clone()) for n, p in ours.named_parameters()}
         opt.step()
         ropt.step()
+        for n, p in ours.named_parameters():
+            w0, g0 = before[n]
+            assert torch.allclose(p.detach(), w0 - 0.05 * g0, rtol=1e-6, atol=1e-7), f"step {s} {n}: SGD update"
     rb = dict(ref.named_buffers())
     for n, b in ours.named_buffers():
         if b.is_floating_point():

@@ -681,25 +681,33 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
   uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 64);
   uint32_t* xs = reinterpret_cast<uint32_t*>(lds + LB_NP * 80);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int li = lane & 15, g = lane >> 4, dr = g >> 1, gc = g & 1;
+  const int li = lane & 15, g = lane >> 4;
   const int P = H / 2, PW = W / 2;
   const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
   const int per_img = tiles_c * tiles_r, total = per_img * B;
 
-  // B-operand geometry of this lane's tap in each N block: x tile word offset (tile origin:
-  // row r0 - 2, column c0 - 4) relative to the K-step base 2*rp*XS + 16*s
+  // K ordering of a K-step (2 rows x 16 columns = 8 pooling windows): k = 4*w + 2*dr + dc, so
+  // lane group g holds windows 2g, 2g+1 whole -- dz1 of a window is one pooled value placed
+  // at its argmax slot (a 64-bit shift), no per-pixel selects.
+  // B-operand geometry: x tile word offset (tile origin row r0 - 2, column c0 - 4) of this
+  // lane's tap relative to the K-step base 2*rp*XS + 16*s; slot j adds koffB(j).  Taps >= 25
+  // read a constant block kept in the tile's padding columns 72..75 (rows 0-1: bf16 1.0 for
+  // the sum-dz column n = 25; rows 2-3: zeros).
   int boff[2];
-  uint32_t bconst[2];  // taps >= 25: the constant packed word (1.0 for n = 25, else 0)
   bool bdata[2];
+  int bcst[2];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int n = 16 * blk + li;
     bdata[blk] = n < 25;
     const int ky = n < 25 ? n / 5 : 0, kx = n < 25 ? n % 5 : 0;
-    boff[blk] = (dr + ky) * LM_XS + 8 * gc + kx + 2;
-    bconst[blk] = n == 25 ? 0x3F800000u : 0u;  // bf16(1.0) = 0x3F80 in the hi half, lo = 0
+    boff[blk] = ky * LM_XS + kx + 2 + 4 * g;
+    bcst[blk] = (n == 25 ? 0 : 2 * LM_XS) + 72;
   }
-
+  if (tid < 16) {  // constant blocks (never overwritten: the x tile uses columns 0..71)
+    const int r = tid >> 2, c = tid & 3;
+    xs[r * LM_XS + 72 + c] = r < 2 ? 0x3F800000u : 0u;
+  }
   uint4 pre[LB_PER];
   auto load_tile = [&](int t) {
     const int b = t / per_img, rem = t - b * per_img;
@@ -773,32 +781,36 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
       const int rp = 2 * wv + h;
 #pragma unroll
       for (int sg = 0; sg < 4; ++sg) {
-        // A = dz1 for (co = li, pixels row dr, columns 8*gc + j): pooled pp = rp*32 + 8*sg + 4*gc + j/2
-        float dz[8];
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int pp = rp * LB_PC + 8 * sg + 4 * gc + m;
-          const float dp = dps[pp * 16 + li];
-          const int ab = ids[pp * 16 + li], am = ab & 3;
-          const float d = (ab & 4) ? dp : 0.f;  // ReLU: a pooled value <= 0 blocks the gradient
-          dz[2 * m] = am == 2 * dr ? d : 0.f;
-          dz[2 * m + 1] = am == 2 * dr + 1 ? d : 0.f;
-        }
+        // A = dz1 for (co = li, windows 2g, 2g+1 of the K-step): pooled pp = rp*32 + 8*sg + w
         s16x8 ah, al;
         {
           uint32_t* hp = reinterpret_cast<uint32_t*>(&ah);
           uint32_t* lp = reinterpret_cast<uint32_t*>(&al);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) split2_bf16(dz[2 * j], dz[2 * j + 1], hp[j], lp[j]);
+          for (int wi = 0; wi < 2; ++wi) {
+            const int pp = rp * LB_PC + 8 * sg + 2 * g + wi;
+            const float dp = dps[pp * 16 + li];
+            const uint32_t ab = ids[pp * 16 + li];
+            const float d = (ab & 4u) ? dp : 0.f;  // ReLU: a pooled value <= 0 blocks the gradient
+            uint32_t h, l;
+            split2_bf16(d, 0.f, h, l);             // low halves: bf16 hi / lo of d
+            const uint32_t sh = 16u * (ab & 3u);  // argmax slot (dr, dc) of the window
+            const uint64_t h64 = (uint64_t)(h & 0xFFFFu) << sh, l64 = (uint64_t)(l & 0xFFFFu) << sh;
+            hp[2 * wi] = (uint32_t)h64;
+            hp[2 * wi + 1] = (uint32_t)(h64 >> 32);
+            lp[2 * wi] = (uint32_t)l64;
+            lp[2 * wi + 1] = (uint32_t)(l64 >> 32);
+          }
         }
         const int base = 2 * rp * LM_XS + 16 * sg;
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
+          const int bo = bdata[blk] ? base + boff[blk] : bcst[blk];
           uint32_t u[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const uint32_t w = xs[base + boff[blk] + j];
-            u[j] = bdata[blk] ? w : bconst[blk];
+            const int wi = j >> 2, dr2 = (j >> 1) & 1, dc = j & 1;  // slot j = (window wi, row dr2, col dc)
+            u[j] = xs[bo + dr2 * LM_XS + 2 * wi + dc];
           }
           s16x8 bh, bl;
           uint32_t* hp = reinterpret_cast<uint32_t*>(&bh);
