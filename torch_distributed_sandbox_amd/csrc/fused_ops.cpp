@@ -33,6 +33,19 @@ const float* optf(const c10::optional<Tensor>& t, int64_t n, const char* name) {
   return t->data_ptr<float>();
 }
 
+// Gradient sink: a caller-provided destination (the parameter's slot in the DDP bucket,
+// ops/grad_sink.py) or a fresh tensor -- the small parameter gradients land in the bucket
+// straight from their finalize kernels instead of one copy kernel each.
+Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shape, const Tensor& like,
+                     const char* name) {
+  if (out.has_value() && out->defined()) {
+    need(*out, at::kFloat, shape, name);
+    TORCH_CHECK(out->device() == like.device(), "tdsa fused: ", name, " on the wrong device");
+    return *out;
+  }
+  return at::empty(shape, like.options().dtype(at::kFloat));
+}
+
 int l1_wg() { return tds_fused_num_wg(4); }
 
 // ---------------------------------------------------------------- layer 1 forward
@@ -178,7 +191,10 @@ struct HeadBwd {
 static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
                                   const c10::optional<Tensor>& gamma2, const Tensor& wfc,
                                   const c10::optional<Tensor>& dw_out, double scale, bool compute_dw,
-                                  const c10::optional<Tensor>& ya = c10::nullopt, double update_lr = 0.0) {
+                                  const c10::optional<Tensor>& ya = c10::nullopt, double update_lr = 0.0,
+                                  const c10::optional<Tensor>& dbfc_out = c10::nullopt,
+                                  const c10::optional<Tensor>& dg_out = c10::nullopt,
+                                  const c10::optional<Tensor>& dbe_out = c10::nullopt) {
   const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
   const int64_t NC = wfc.size(0);
@@ -227,12 +243,14 @@ static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported B/NC");
   auto sums = at::empty({64}, y2.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), sums.data_ptr<double>(), 64, nblk, 2, (int64_t)nblk * 2, 2, st);
-  r.dgamma = at::empty({32}, y2.options());
-  r.dbeta = at::empty({32}, y2.options());
+  r.dgamma = sink_or_empty(dg_out, {32}, y2, "dgamma2_out");
+  r.dbeta = sink_or_empty(dbe_out, {32}, y2, "dbeta2_out");
   r.kbuf = at::empty({96}, y2.options());
   tds_bn_bwd_finalize2(sums.data_ptr<double>(), 32, 1, B * P * P, g, stats2.data_ptr<float>(),
                        r.dgamma.data_ptr<float>(), r.dbeta.data_ptr<float>(), r.kbuf.data_ptr<float>(), st);
-  r.dbfc = dlogits.sum(0).mul_(scale);
+  r.dbfc = sink_or_empty(dbfc_out, {NC}, y2, "dbfc_out");
+  at::sum_out(r.dbfc, dlogits, {0});
+  if (scale != 1.0) r.dbfc.mul_(scale);
   return r;
 }
 
@@ -256,9 +274,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward_g2m(
     const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
     const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
-    bool compute_dw, const c10::optional<Tensor>& ya, double update_lr) {
+    bool compute_dw, const c10::optional<Tensor>& ya, double update_lr, const c10::optional<Tensor>& dbfc_out,
+    const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out) {
   c10::DeviceGuard guard(y2.device());
-  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw, ya, update_lr);
+  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw, ya, update_lr,
+                                 dbfc_out, dg_out, dbe_out);
   return {r.dW, r.dbfc, r.dgamma, r.dbeta, r.g2m, r.kbuf};
 }
 
@@ -286,7 +306,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward(const Tensor& dy2, const
 // BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2, g2m, aff2, kbuf, p1) -> (dp1, dw2, db2)
 std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& g2m, const Tensor& aff2,
                                                            const Tensor& kbuf, const Tensor& p1, const Tensor& wd,
-                                                           double scale) {
+                                                           double scale, const c10::optional<Tensor>& dw_out,
+                                                           const c10::optional<Tensor>& db_out) {
   const int64_t B = p1.size(0), P = p1.size(1), Q = P / 2;
   need(p1, at::kFloat, {B, P, P, 16}, "p1");
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
@@ -300,8 +321,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   const int nwg = tds_conv2_bwd_fused_num_wg();
   auto dp1 = at::empty({B, P, P, 16}, p1.options());
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options());
-  auto dw2 = at::empty({32, 16, 5, 5}, p1.options());
-  auto db2 = at::empty({32}, p1.options());
+  auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
+  auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
   tds_conv2_bwd_fused(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
                       p1.data_ptr(), wd.data_ptr<int16_t>(), dp1.data_ptr<float>(), slab.data_ptr<float>(),
                       dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, nwg, (int)B, (int)P, st);
@@ -312,7 +333,11 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
 std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, const Tensor& x, const Tensor& p1,
                                                              const Tensor& idx1, const Tensor& w1, const Tensor& b1,
                                                              const c10::optional<Tensor>& gamma1, const Tensor& stats1,
-                                                             const Tensor& gram, double scale) {
+                                                             const Tensor& gram, double scale,
+                                                             const c10::optional<Tensor>& dw_out,
+                                                             const c10::optional<Tensor>& db_out,
+                                                             const c10::optional<Tensor>& dg_out,
+                                                             const c10::optional<Tensor>& dbe_out) {
   TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, "fused_l1_backward: x");
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3), P = H / 2;
   need(x, at::kFloat, {B, 1, H, W}, "x");
@@ -332,10 +357,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
              b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);
-  auto dw1 = at::empty({16, 1, 5, 5}, x.options());
-  auto db1 = at::empty({16}, x.options());
-  auto dg = at::empty({16}, x.options());
-  auto dbe = at::empty({16}, x.options());
+  auto dw1 = sink_or_empty(dw_out, {16, 1, 5, 5}, x, "dw1_out");
+  auto db1 = sink_or_empty(db_out, {16}, x, "db1_out");
+  auto dg = sink_or_empty(dg_out, {16}, x, "dgamma1_out");
+  auto dbe = sink_or_empty(dbe_out, {16}, x, "dbeta1_out");
   tds_l1_finalize(bsum.data_ptr<double>(), gram.data_ptr<double>(), B * H * W, w1.data_ptr<float>(),
                   b1.data_ptr<float>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(), db1.data_ptr<float>(),
                   dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale, st);
@@ -365,15 +390,17 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
         &fused_conv2_backward);
   m.def(
       "fused_head_backward_g2m(Tensor dlogits, Tensor y2, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor wfc, "
-      "Tensor(a!)? dw_out, float scale, bool compute_dw=True, Tensor? ya=None, float update_lr=0.0) -> "
+      "Tensor(a!)? dw_out, float scale, bool compute_dw=True, Tensor? ya=None, float update_lr=0.0, "
+      "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None) -> "
       "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward_g2m);
   m.def(
-      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale) -> "
-      "(Tensor, Tensor, Tensor)",
+      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale, "
+      "Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
       &fused_conv2_backward_y2);
   m.def(
       "fused_l1_backward(Tensor dp1, Tensor x, Tensor p1, Tensor idx1, Tensor w1, Tensor b1, Tensor? gamma1, "
-      "Tensor stats1, Tensor gram, float scale) -> (Tensor, Tensor, Tensor, Tensor)",
+      "Tensor stats1, Tensor gram, float scale, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
+      "Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None) -> (Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_backward);
 }

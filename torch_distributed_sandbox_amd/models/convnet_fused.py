@@ -49,6 +49,27 @@ def supported(model, x) -> bool:
     return True
 
 
+def _sinks(ctx, params, first):
+    """Gradient destinations for ``params`` (bucket views when DDP registered sinks,
+    ops/grad_sink.py; None for parameters that need no gradient).  ``first`` is the
+    forward-input index of params[0], or a tuple of indices."""
+    idx = first if isinstance(first, tuple) else tuple(range(first, first + len(params)))
+    return [grad_sink.acquire(p, p.shape, p) if p is not None and ctx.needs_input_grad[i] else None
+            for p, i in zip(params, idx)]
+
+
+_ZERO = {}
+
+
+def _zero_scalar(like):
+    """Cached 0-d zero per (device, dtype): the y2 gradient placeholder costs no fill kernel."""
+    key = (like.device, like.dtype)
+    z = _ZERO.get(key)
+    if z is None:
+        z = _ZERO[key] = torch.zeros((), device=like.device, dtype=like.dtype)
+    return z
+
+
 class _Layer1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps):
@@ -56,13 +77,16 @@ class _Layer1(torch.autograd.Function):
         x = x.contiguous()
         p1, idx1, stats1, gram = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps)
         ctx.save_for_backward(x, p1, idx1, w1, b1, g1, stats1, gram)
+        ctx.params = (w1, b1, g1, be1)
         ctx.mark_non_differentiable(idx1)
         return p1
 
     @staticmethod
     def backward(ctx, dp1):
         x, p1, idx1, w1, b1, g1, stats1, gram = ctx.saved_tensors
-        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1.contiguous(), x, p1, idx1, w1, b1, g1, stats1, gram, 1.0)
+        outs = _sinks(ctx, ctx.params, 1)
+        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1.contiguous(), x, p1, idx1, w1, b1, g1, stats1, gram, 1.0,
+                                                           *outs)
         return None, dw1, db1, dg1, dbe1, None, None, None, None, None
 
 
@@ -82,6 +106,7 @@ class _Conv2(torch.autograd.Function):
         wp, wd = ops.conv2_pack(w2.contiguous())
         y2, partial2 = ops.fused_conv2_forward(p1, wp, b2)
         ctx.save_for_backward(p1, wd, y2)
+        ctx.params = (w2, b2)
         ctx.link = link
         ctx.mark_non_differentiable(partial2)
         return y2, partial2
@@ -91,7 +116,8 @@ class _Conv2(torch.autograd.Function):
         p1, wd, y2 = ctx.saved_tensors
         link = ctx.link
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
-        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, p1, wd, 1.0)
+        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, p1, wd, 1.0,
+                                                           *_sinks(ctx, ctx.params, 1))
         link.g2m = link.kbuf = link.aff2 = None
         return (dp1 if ctx.needs_input_grad[0] else None), dw2, db2, None
 
@@ -113,6 +139,7 @@ class _Head(torch.autograd.Function):
             raise RuntimeError("activation exchange refused to start after ready() agreed")
         ctx.save_for_backward(y2, stats2, aff2, g2, wfc, ya)
         ctx.wfc_param = wfc
+        ctx.small = (bfc, g2, be2)
         ctx.ex = ex
         ctx.link = link
         return logits
@@ -136,14 +163,16 @@ class _Head(torch.autograd.Function):
             lr = None
             if ctx.needs_input_grad[10] and y2.shape[0] <= 8 and wfc.shape[0] <= 10:  # head_bwd_ya_kernel shapes
                 lr = fused_update.take(ctx.wfc_param)
+            dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (11, 3, 4))
             dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, dw_out,
-                                                                         1.0, True, ya, float(lr or 0.0))
+                                                                         1.0, True, ya, float(lr or 0.0), dbfc_o, dg_o,
+                                                                         dbe_o)
             if lr:
                 fused_update.applied(ctx.wfc_param)
         link = ctx.link
         link.g2m, link.kbuf, link.aff2 = g2m, kbuf, aff2
         # y2's gradient is carried by the link; autograd gets a zero-stride placeholder
-        dy2 = torch.zeros((), device=y2.device, dtype=y2.dtype).expand(y2.shape)
+        dy2 = _zero_scalar(y2).expand(y2.shape)
         return dy2, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None, None
 
 
