@@ -40,6 +40,17 @@ def main():
     res = {}
     res["fwd"] = timeit(lambda: ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc,
                                                        bfc, None, ya))
+    fo = {}
+    for mode in ("2", "1"):
+        os.environ["TDS_HEAD_FWD"] = mode
+        res[f"fwd_mode{mode}"] = timeit(lambda: ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1,
+                                                                       1e-5, wfc, bfc, None, ya))
+        lg = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, None, ya)[0]
+        fo[mode] = (lg.clone(), ya.clone())
+    os.environ.pop("TDS_HEAD_FWD")
+    for mode in ("1",):
+        res[f"fwd_mode{mode}_vs_2"] = {"logits_rel": float((fo[mode][0] - fo["2"][0]).norm() / fo["2"][0].norm()),
+                                       "ya_maxdiff": float((fo[mode][1] - fo["2"][1]).abs().max())}
     _, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, None, ya)
     res["bwd_y2"] = timeit(lambda: ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, dW, 1.0, True))
     outs = {}

@@ -486,8 +486,20 @@ __global__ __launch_bounds__(64 * NW) void head_fwd2_kernel(const float4* __rest
   constexpr int CPW = 32 / NW;
   using Tile = HeadTile2<NW, PXL>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __shared__ float red[NW][HD_MAXB * 10];
+  // per-image wave sums, reduced (fixed order) by threads < NC after the next barrier: 640 B
+  // of static LDS instead of NW x HD_MAXB x 10 floats, so two workgroups share a CU
+  // (2 x 73 KB) and one's weight prologue / tail overlaps the other's streaming
+  __shared__ float red[NW][10];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  auto flush = [&](int b) {  // after a barrier that follows image b's red[] writes
+    if ((int)threadIdx.x < NC) {
+      double t = 0.0;
+#pragma unroll
+      for (int w8 = 0; w8 < NW; ++w8) t += (double)red[w8][threadIdx.x];
+      partial[((int64_t)blk * B + b) * NC + threadIdx.x] = t;
+    }
+  };
   const Tile tile{y2, P, Q, (int)blockIdx.y, (int)blockIdx.x * Tile::PX};
   const int64_t QQ = (int64_t)Q * Q;
   bool valid[PXL];
@@ -514,6 +526,7 @@ __global__ __launch_bounds__(64 * NW) void head_fwd2_kernel(const float4* __rest
 #pragma unroll 1
   for (int b = 0; b < B; ++b) {
     __syncthreads();
+    if (b > 0) flush(b - 1);
     Tile::store(smem, pre);
     __syncthreads();
     if (b + 1 < B) tile.load(b + 1, pre);
@@ -565,27 +578,24 @@ __global__ __launch_bounds__(64 * NW) void head_fwd2_kernel(const float4* __rest
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
       const float t = wave_sum(s[j]);
-      if (lane == 0) red[wv][b * 10 + j] = t;
+      if (lane == 0) red[wv][j] = t;
     }
   }
   __syncthreads();
-  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-  for (int i = threadIdx.x; i < B * NC; i += blockDim.x) {
-    const int b = i / NC, j = i % NC;
-    double t = 0.0;
-#pragma unroll
-    for (int w8 = 0; w8 < NW; ++w8) t += (double)red[w8][b * 10 + j];
-    partial[(int64_t)blk * B * NC + i] = t;
-  }
+  flush(B - 1);
 }
 
 constexpr int HF2_NW = 16, HF2_PXL = 2;
 using HF2Tile = HeadTile2<HF2_NW, HF2_PXL>;
 
-static bool head_fwd_wide() {
-  const char* e = std::getenv("TDS_HEAD_FWD");  // per call: in-process A/B
-  return !(e && std::atoi(e) == 1);
+// TDS_HEAD_FWD (read per call: in-process A/B): 1 = head_fwd_kernel (64 columns), otherwise
+// head_fwd2_kernel<16, 2> (128 columns).  <16, 4> (256 columns, 1 KB plane runs, 144 KB LDS)
+// measured 1.26 ms against 0.66 (tools/head_diag.py): 80 weight registers per lane.
+static int head_fwd_mode() {
+  const char* e = std::getenv("TDS_HEAD_FWD");
+  return (e && std::atoi(e) == 1) ? 1 : 2;
 }
+static int head_fwd_px(int mode) { return mode == 1 ? HD_PX : 64 * mode; }
 
 constexpr int HD_FWD_NW = 8;
 constexpr int HD_BWD_NW = 16;
@@ -611,7 +621,7 @@ using namespace tds;
 int tds_head_bwd_nblk(int Q) { return ((Q + HD_PX - 1) / HD_PX) * Q; }  // head_bwd_kernel (y2 path)
 
 int tds_head_fwd_nblk(int Q) {
-  const int px = head_fwd_wide() ? HF2Tile::PX : HD_PX;
+  const int px = head_fwd_px(head_fwd_mode());
   return ((Q + px - 1) / px) * Q;
 }
 
@@ -621,10 +631,10 @@ int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const flo
   const int Q = P / 2;
   if (B > HD_MAXB || NC > 10 || Q < 1) return -1;
   head_lds_limits();
-  const bool wide = head_fwd_wide();
-  const int px = wide ? HF2Tile::PX : HD_PX;
+  const int mode = head_fwd_mode();
+  const int px = head_fwd_px(mode);
   const dim3 grid((Q + px - 1) / px, Q);
-  if (wide)
+  if (mode == 2)
     hipLaunchKernelGGL((head_fwd2_kernel<HF2_NW, HF2_PXL>), grid, dim3(64 * HF2_NW), HF2Tile::LDS, st,
                        reinterpret_cast<const float4*>(y2), Wfc, aff2, partial, xout, yaout, B, P, Q, NC);
   else
