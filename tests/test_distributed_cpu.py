@@ -316,3 +316,15 @@ def _w_exchange_policy(rank, world, port):
 @pytest.mark.parametrize("world", [2, 4])
 def test_activation_exchange_policy(world):
     launch.spawn(_w_exchange_policy, args=(world, launch.find_free_port()), nprocs=world, timeout=120)
+
+
+# ---------------------------------------------------------------- TDS_DEBUG_SYNC
+def test_debug_sync_mode_collectives_and_ddp(monkeypatch):
+    """Stream-ordering assertion mode (every collective waited + device synced on issue)
+    must not change results: collectives and the DDP equivalence check pass under it."""
+    from torch_distributed_sandbox_amd.parallel import distributed as dist
+
+    monkeypatch.setenv("TDS_DEBUG_SYNC", "1")
+    assert dist.debug_sync_enabled()
+    launch.spawn(_w_collectives, args=(2, launch.find_free_port(), "gloo"), nprocs=2, timeout=180)
+    launch.spawn(_w_ddp, args=(2, launch.find_free_port(), 32, 2, "gloo"), nprocs=2, timeout=300)

@@ -21,6 +21,11 @@
 // torch's TORCH_NCCL_ASYNC_ERROR_HANDLING).  TDS_RCCL_ERROR_HANDLING=raise keeps
 // the process alive and rethrows from the next wait/collective instead.
 //
+// TDS_DEBUG_SYNC=1 is the stream-ordering assertion mode: every collective is
+// followed by a host wait on the comm stream and a check of the HIP and RCCL
+// async error state, so a fault, a hang or a missing event fence shows up at
+// the collective that caused it (named in the error), not steps later.
+//
 // Links against torch's bundled librccl (one RCCL per process; see _build.py).
 #pragma once
 #include <ATen/ATen.h>
@@ -90,6 +95,7 @@ struct RcclState {
   int device = 0;
   int64_t rank = 0, world = 1, timeout_ms = 600000;
   bool exit_on_error = true;
+  bool debug_sync = false;  // TDS_DEBUG_SYNC=1
   std::atomic<bool> aborted{false};
   std::mutex mu;
   std::string error;  // guarded by mu
@@ -187,6 +193,8 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     st_->timeout_ms = timeout_ms;
     const char* eh = std::getenv("TDS_RCCL_ERROR_HANDLING");
     st_->exit_on_error = !(eh && std::string(eh) == "raise");
+    const char* ds = std::getenv("TDS_DEBUG_SYNC");
+    st_->debug_sync = ds && std::atoi(ds) != 0;
     ncclUniqueId uid;
     auto idc = id.contiguous().cpu();
     std::memcpy(&uid, idc.data_ptr(), sizeof(uid));
@@ -368,7 +376,20 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
       std::lock_guard<std::mutex> gl(st_->mu);
       st_->pending.push_back({wd, std::chrono::steady_clock::now(), what});
     }
+    if (st_->debug_sync) debug_sync_check(cs, what);
     return c10::make_intrusive<RcclWork>(st_, done);
+  }
+
+  // TDS_DEBUG_SYNC: block until this collective has finished and surface any error here
+  void debug_sync_check(hipStream_t cs, const char* what) {
+    const hipError_t he = hipStreamSynchronize(cs);
+    TORCH_CHECK(he == hipSuccess, "TDS_DEBUG_SYNC: ", what, " on rank ", st_->rank, ": HIP error ",
+                hipGetErrorString(he));
+    ncclResult_t ae = ncclSuccess;
+    if (st_->comm) TDS_RCCL(ncclCommGetAsyncError(st_->comm, &ae));
+    TORCH_CHECK(ae == ncclSuccess, "TDS_DEBUG_SYNC: ", what, " on rank ", st_->rank, ": RCCL async error ",
+                ncclGetErrorString(ae));
+    st_->check_ok();
   }
 
   static void watchdog_loop(std::shared_ptr<RcclState> s) {

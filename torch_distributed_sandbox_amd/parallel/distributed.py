@@ -181,10 +181,32 @@ def all_reduce(tensor: torch.Tensor, op=ReduceOp.SUM, group=None, async_op: bool
         work = dist.all_reduce(tensor, op=ReduceOp.SUM, group=group, async_op=async_op)
         n = get_world_size(group)
         if async_op:
-            return _PostOpWork(work, lambda: _div_(tensor, n))
+            return _debug_sync(_PostOpWork(work, lambda: _div_(tensor, n)), "all_reduce", tensor)
         _div_(tensor, n)
-        return None
-    return dist.all_reduce(tensor, op=op, group=group, async_op=async_op)
+        return _debug_sync(None, "all_reduce", tensor)
+    return _debug_sync(dist.all_reduce(tensor, op=op, group=group, async_op=async_op), "all_reduce", tensor)
+
+
+def debug_sync_enabled() -> bool:
+    """TDS_DEBUG_SYNC=1: stream-ordering assertion mode.  Every collective
+    issued through this module is waited for and the device synchronised right after it
+    is enqueued, so an async fault or a missing stream fence surfaces at the collective that
+    caused it.  The native RCCL communicator honours the same variable in C++
+    (csrc/comm/rccl_comm.h), which also covers the C++ reducer's bucket all-reduces."""
+    return os.environ.get("TDS_DEBUG_SYNC", "0") not in ("", "0")
+
+
+def _debug_sync(work, what: str, tensor: torch.Tensor):
+    if not debug_sync_enabled():
+        return work
+    if work is not None:
+        work.wait()
+    if tensor.is_cuda:
+        try:
+            torch.cuda.synchronize(tensor.device)
+        except RuntimeError as e:
+            raise RuntimeError(f"TDS_DEBUG_SYNC: {what} on rank {get_rank()}: {e}") from e
+    return work
 
 
 def _div_(t: torch.Tensor, n: int):
@@ -213,19 +235,21 @@ class _PostOpWork:
 
 
 def broadcast(tensor: torch.Tensor, src: int = 0, group=None, async_op: bool = False):
-    return dist.broadcast(tensor, src=src, group=group, async_op=async_op)
+    return _debug_sync(dist.broadcast(tensor, src=src, group=group, async_op=async_op), "broadcast", tensor)
 
 
 def all_gather(tensor_list, tensor, group=None, async_op: bool = False):
-    return dist.all_gather(tensor_list, tensor, group=group, async_op=async_op)
+    return _debug_sync(dist.all_gather(tensor_list, tensor, group=group, async_op=async_op), "all_gather", tensor)
 
 
 def all_gather_into_tensor(output, input, group=None, async_op: bool = False):
-    return dist.all_gather_into_tensor(output, input, group=group, async_op=async_op)
+    return _debug_sync(dist.all_gather_into_tensor(output, input, group=group, async_op=async_op),
+                       "all_gather_into_tensor", output)
 
 
 def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op: bool = False):
-    return dist.reduce_scatter_tensor(output, input, op=op, group=group, async_op=async_op)
+    return _debug_sync(dist.reduce_scatter_tensor(output, input, op=op, group=group, async_op=async_op),
+                       "reduce_scatter_tensor", output)
 
 
 def barrier(group=None) -> None:
