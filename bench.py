@@ -2,17 +2,28 @@
 
 BASELINE.json metric/config: ConvNet (mnist_onegpu.py:11-31), 3000x3000 inputs,
 per-rank batch 5, SGD(lr=1e-4), CrossEntropy, one process per MI355X over
-RCCL/xGMI, synthetic data + random init (no network for MNIST), fp32.
+RCCL/xGMI, synthetic data + random init (no network for MNIST).
 
     python bench.py                                  # 1 GPU, default steps
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+    python bench.py --gpus 8 --steps 20 --warmup 5   # spawns 8 ranks itself
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
+
+Launch: like the reference (``mp.spawn(train, nprocs=args.gpus)``,
+mnist_distributed.py:123-127) ``--gpus N`` with no ``WORLD_SIZE`` in the
+environment starts N rank processes itself (spawn start method) before the
+parent touches the GPU, and exits with the first failing rank's status.  Under
+torchrun (``WORLD_SIZE`` set) it runs as that rank.
 
 A timed step is the full training step: on-device data generation (28x28
 uint8 -> 3000x3000 bilinear upsample), forward, loss, zero_grad, backward
-(with the bucketed gradient all-reduce), optimizer step.  W untimed warmup
-steps, then exactly K steps bracketed by barrier + synchronize; the elapsed
-time is the MAX over ranks.  Rank 0 prints one JSON line.
+(with the gradient exchange), optimizer step.  W untimed warmup steps, then
+exactly K steps bracketed by barrier + synchronize; the elapsed time is the
+MAX over ranks.  Rank 0 prints one JSON line.
+
+Default multi-GPU stack: this package's RCCL communicator (``rccl-native``:
+own comm stream, non-blocking init with a bounded wait, watchdog) and the C++
+gradient reducer; ``--backend rccl`` selects torch's ProcessGroupNCCL instead.
 """
 from __future__ import annotations
 
@@ -25,9 +36,11 @@ import time
 import torch
 
 METRIC = "images/sec (whole node), 3000x3000 MNIST ConvNet DDP at 1/2/4/8 MI355X"
+DTYPE = ("fp32 (conv1/conv2 fwd+dgrad+wgrad: bf16x3 split-precision MFMA with fp32 accumulate; "
+         "BN, fc, CE, SGD: fp32)")
 
 
-def main(argv=None):
+def _parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -36,29 +49,71 @@ def main(argv=None):
     ap.add_argument("--batch-size", type=int, default=5, help="per-rank batch (reference: 5)")
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "layers"])
     ap.add_argument("--bucket-mb", type=float, default=None)
-    ap.add_argument("--backend", default=os.environ.get("TDS_BENCH_BACKEND", "rccl"),
-                    help="rccl (torch ProcessGroupNCCL = RCCL) | rccl-native (this package's C++ communicator)")
-    ap.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations"],
-                    help="fc gradient path under DDP: auto picks the activation exchange when it moves fewer "
-                         "bytes per rank than the ring all-reduce (parallel/factored.py)")
+    ap.add_argument("--backend", default=os.environ.get("TDS_BENCH_BACKEND"),
+                    help="rccl-native (default on GPU: this package's C++ RCCL communicator + C++ reducer) | "
+                         "rccl (torch ProcessGroupNCCL = RCCL) | gloo | host")
+    ap.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations", "sharded"],
+                    help="fc gradient path under DDP (parallel/factored.py); auto picks by the xGMI byte model")
     ap.add_argument("--overlap-optimizer", action=argparse.BooleanOptionalAction, default=True,
                     help="finish the fc bucket (collective + SGD) on a side stream under the next forward's convs")
-    ap.add_argument("--profile-phases", action="store_true", help="also report per-phase GPU times (adds events)")
-    args = ap.parse_args(argv)
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: rehearsal of the launch/exchange path on the torch-ops plan (small --image-size)")
+    ap.add_argument("--shared-device", action="store_true",
+                    help="rehearsal only: every rank uses cuda:0 (needs --backend gloo); recorded in the JSON")
+    ap.add_argument("--spawn-timeout", type=float, default=1800.0,
+                    help="self-spawn: terminate all ranks if the job runs longer than this (s)")
+    return ap
 
+
+def _rank_entry(i: int, argv, world: int, master_addr: str, master_port: str):
+    os.environ.update({"RANK": str(i), "LOCAL_RANK": str(i), "WORLD_SIZE": str(world),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": master_addr, "MASTER_PORT": master_port})
+    run(argv)
+
+
+def _spawn_ranks(args, argv) -> int:
+    """One process per GPU, started here (no GPU call happens in this parent)."""
+    from torch_distributed_sandbox_amd.parallel import launch
+
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = os.environ.get("MASTER_PORT") or launch.find_free_port(addr)
+    try:
+        launch.spawn(_rank_entry, args=(list(argv), args.gpus, addr, str(port)), nprocs=args.gpus,
+                     timeout=args.spawn_timeout)
+    except launch.ProcessRaisedException as e:
+        print(f"bench.py: rank {e.error_index} failed:{e}", file=sys.stderr, flush=True)
+        return 1
+    except launch.ProcessExitedException as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        return e.exit_code if e.exit_code and e.exit_code > 0 else 1
+    except TimeoutError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        return 124
+    return 0
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = _parser().parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return _spawn_ranks(args, argv)
+    run(argv)
+    return 0
+
+
+def run(argv) -> None:
+    args = _parser().parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # rehearsal only (tools/steps_multirank_rehearsal.txt): several ranks on one GPU with a
-    # host-side backend (gloo), to exercise the multi-rank code path where RCCL refuses a
-    # shared device.  Never set by the driver.
-    if os.environ.get("TDS_BENCH_SHARED_DEVICE") is not None:
-        local_rank = int(os.environ["TDS_BENCH_SHARED_DEVICE"])
     if world != args.gpus:
-        print(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}; launch N>1 with torch.distributed.run",
-              file=sys.stderr)
-        if world == 1 and args.gpus > 1:
-            sys.exit(2)
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}")
+    on_gpu = args.device == "cuda"
+    backend = args.backend or ("rccl-native" if on_gpu else "gloo")
+    if args.shared_device:
+        if backend != "gloo":
+            raise SystemExit("bench.py: --shared-device is a rehearsal mode and needs --backend gloo")
+        local_rank = 0
 
     import torch_distributed_sandbox_amd as tds
     from torch_distributed_sandbox_amd.data import synthetic_batch
@@ -67,16 +122,32 @@ def main(argv=None):
     from torch_distributed_sandbox_amd.ops import functional as TF
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
     from torch_distributed_sandbox_amd.parallel import distributed as tdist
+    from torch_distributed_sandbox_amd.parallel.rccl_backend import native_comm_of
 
-    assert torch.cuda.is_available(), "bench.py needs a GPU"
-    torch.cuda.set_device(local_rank)
-    tds._ext.ops()  # native extension must be loaded (fails loudly otherwise)
-    device = torch.device("cuda", local_rank)
-    if world > 1 or args.grad_exchange == "activations":
+    if on_gpu:
+        assert torch.cuda.is_available(), "bench.py needs a GPU (use --device cpu for a CPU rehearsal)"
+        torch.cuda.set_device(local_rank)
+        tds._ext.ops()  # native extension must be loaded (fails loudly otherwise)
+        device = torch.device("cuda", local_rank)
+    else:
+        device = torch.device("cpu")
+    if world > 1 or args.grad_exchange in ("activations", "sharded"):
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
-        tdist.init_process_group(args.backend, rank=rank, world_size=world, device_id=local_rank)
+        tdist.init_process_group(backend, rank=rank, world_size=world,
+                                 device_id=local_rank if on_gpu and backend != "gloo" else None)
+    rccl_ranks = None
+    if tdist.is_initialized():
+        comm, kind = native_comm_of(None)
+        if kind == "rccl":
+            rccl_ranks = int(comm.comm_count())
+            # sanity: one collective over the live communicator before anything is timed
+            t = torch.full((1,), float(rank + 1), device=device)
+            tdist.all_reduce(t)
+            want = world * (world + 1) / 2
+            if float(t.item()) != want:
+                raise RuntimeError(f"rccl-native sanity all-reduce gave {float(t.item())}, expected {want}")
 
     H = W = args.image_size
     B = args.batch_size
@@ -84,7 +155,7 @@ def main(argv=None):
     model = ConvNet(image_shape=(H, W), device=device, mode=args.mode)
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), 1e-4)
-    ddp = DistributedDataParallel(model, device_ids=[local_rank], bucket_cap_mb=args.bucket_mb,
+    ddp = DistributedDataParallel(model, device_ids=[local_rank] if on_gpu else None, bucket_cap_mb=args.bucket_mb,
                                   grad_exchange=args.grad_exchange, overlap_optimizer=args.overlap_optimizer)
     ddp.attach_optimizer(optimizer)
 
@@ -107,7 +178,8 @@ def main(argv=None):
     def sync_all():
         if world > 1:
             tdist.barrier()
-        torch.cuda.synchronize()
+        if on_gpu:
+            torch.cuda.synchronize()
 
     loss = None
     for i in range(args.warmup):
@@ -126,6 +198,26 @@ def main(argv=None):
     ms = 1e3 * elapsed / max(1, args.steps)
     imgs_per_sec = world * B * args.steps / elapsed
     if rank == 0:
+        config = {
+            "model": "ConvNet(conv5x5 1->16+BN+ReLU+pool2, conv5x5 16->32+BN+ReLU+pool2, fc 32*(H/4)^2->10)",
+            "global_batch": world * B,
+            "per_rank_batch": B,
+            "seq_len": None,
+            "image_size": [H, W],
+            "parallelism": f"dp{world}",
+            "mode": args.mode,
+            "device": args.device,
+            "backend": backend if world > 1 else None,
+            "rccl_ranks": rccl_ranks,
+            "reducer": ddp.reducer_kind,
+            "overlap_optimizer": ddp.overlap_optimizer,
+            "fc_grad": ddp.fc_grad_path(),
+            "optimizer": "SGD(lr=1e-4)",
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3) if on_gpu else None,
+            "final_loss": final_loss,
+        }
+        if args.shared_device:
+            config["shared_device"] = True  # rehearsal: all ranks on one GPU, not a multi-GPU number
         rec = {
             "metric": METRIC,
             "value": round(imgs_per_sec, 3),
@@ -137,25 +229,9 @@ def main(argv=None):
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": DTYPE,
             "data": "synthetic (seeded 28x28 uint8 sources upsampled on device to HxW; random labels; random init)",
-            "config": {
-                "model": "ConvNet(conv5x5 1->16+BN+ReLU+pool2, conv5x5 16->32+BN+ReLU+pool2, fc 32*(H/4)^2->10)",
-                "global_batch": world * B,
-                "per_rank_batch": B,
-                "seq_len": None,
-                "image_size": [H, W],
-                "parallelism": f"dp{world}",
-                "mode": args.mode,
-                "backend": args.backend if world > 1 else None,
-                "reducer": ddp.reducer_kind,
-                "overlap_optimizer": ddp.overlap_optimizer,
-                "fc_grad": ("activation-exchange" if any(e.steps_exchanged for e in ddp.exchanges)
-                            else "allreduce" if world > 1 else "local"),
-                "optimizer": "SGD(lr=1e-4)",
-                "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3),
-                "final_loss": final_loss,
-            },
+            "config": config,
         }
         print(json.dumps(rec), flush=True)
     if tdist.is_initialized():
@@ -164,4 +240,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -1,0 +1,34 @@
+"""bench.py on the GPU box: the 1-GPU headline path at a small image size, and the
+self-spawned multi-rank path rehearsed with gloo ranks sharing cuda:0 (the only
+multi-rank GPU run a one-GPU box allows; RCCL refuses two ranks on one device)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, timeout=240):
+    p = subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, capture_output=True, text=True,
+                       timeout=timeout)
+    assert p.returncode == 0, p.stderr[-4000:]
+    recs = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 1, p.stdout
+    return recs[0]
+
+
+def test_bench_one_gpu_small(gpu):
+    r = _bench(["--image-size", "512", "--steps", "3", "--warmup", "1"])
+    assert r["n_gpus"] == 1 and r["config"]["fc_grad"] == "local" and r["value"] > 0
+
+
+@pytest.mark.parametrize("exchange", ["auto", "allreduce"])
+def test_bench_self_spawn_shared_device(gpu, exchange):
+    r = _bench(["--gpus", "2", "--backend", "gloo", "--shared-device", "--image-size", "512", "--steps", "2",
+                "--warmup", "1", "--grad-exchange", exchange])
+    assert r["n_gpus"] == 2 and r["config"]["shared_device"] is True
+    assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 10

@@ -206,3 +206,20 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
             assert torch.allclose(p, q, rtol=1e-6, atol=1e-9), n
         else:
             assert torch.equal(p, q), n
+
+
+def test_rccl_native_count_and_sendrecv(pg, gpu):
+    """ncclCommCount of the live communicator, and the grouped point-to-point
+    primitive (self-exchange at world 1; strided row slices as sources)."""
+    from torch_distributed_sandbox_amd.parallel.rccl_backend import native_comm_of
+    import torch.distributed as tdist
+
+    comm, _ = native_comm_of(tdist.group.WORLD)
+    assert comm.comm_count() == 1
+    x = torch.arange(40.0, device=gpu).view(4, 10)
+    out = torch.zeros(4, 3, device=gpu)
+    sends = [x[b, 2:5] for b in range(4)]
+    recvs = [out[b] for b in range(4)]
+    comm.sendrecv(sends, [0] * 4, recvs, [0] * 4).wait()
+    torch.cuda.synchronize()
+    assert torch.equal(out, x[:, 2:5])

@@ -83,3 +83,38 @@ def test_mnist_distributed_fault_fails_fast():
              env={"TDS_FAULT_RANK": "1", "TDS_FAULT_STEP": "3", "TDS_FAULT_MODE": "raise"}, timeout=200)
     assert p.returncode != 0
     assert "injected fault on rank 1 at step 3" in p.stderr
+
+
+def _json_lines(out):
+    return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
+
+
+def test_bench_self_spawns_ranks_cpu():
+    """`python bench.py --gpus 2` with no external launcher starts both ranks itself
+    (reference: mp.spawn(train, nprocs=args.gpus), mnist_distributed.py:127) and rank 0
+    prints exactly one JSON line for the whole job."""
+    p = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "32", "--steps", "2", "--warmup", "1"])
+    assert p.returncode == 0, p.stderr
+    recs = _json_lines(p.stdout)
+    assert len(recs) == 1
+    r = recs[0]
+    assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
+    assert r["config"]["global_batch"] == 10 and r["config"]["parallelism"] == "dp2"
+    assert r["config"]["backend"] == "gloo" and r["value"] > 0
+    assert "bf16x3" in r["dtype"]
+
+
+def test_bench_self_spawn_native_host_backend_cpu():
+    p = _run(["bench.py", "--gpus", "3", "--device", "cpu", "--image-size", "32", "--steps", "1", "--warmup", "1",
+              "--backend", "host"])
+    assert p.returncode == 0, p.stderr
+    (r,) = _json_lines(p.stdout)
+    assert r["n_gpus"] == 3 and r["config"]["reducer"] == "native"
+
+
+def test_bench_spawn_failure_propagates_cpu():
+    # --shared-device refuses a non-gloo backend inside every rank: the parent must fail, not hang
+    p = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "32", "--steps", "1", "--warmup", "0",
+              "--backend", "host", "--shared-device"], timeout=200)
+    assert p.returncode != 0
+    assert not _json_lines(p.stdout)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Runs a list of GPU steps (one per line in $1), each under its own timeout.
 # Any nonzero exit stops the session (a pytest failure can be a GPU memory fault: nothing more runs on the GPU after it).
-# Usage: bash tools/gpu_session.sh steps.txt   (lines: "<timeout_s> <logname> <command...>")
+# Usage: bash tools/gpu_sessions/run.sh tools/gpu_sessions/<steps>.txt   (lines: "<timeout_s> <logname> <command...>")
 set -u
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0

@@ -15,6 +15,10 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       .def("world_size", &tds_comm::RcclComm::world_size)
       .def("device", &tds_comm::RcclComm::device)
       .def("pending", &tds_comm::RcclComm::pending)
+      .def("comm_count", &tds_comm::RcclComm::comm_count)
+      .def("cta_budget_min", &tds_comm::RcclComm::cta_budget_min)
+      .def("cta_budget_max", &tds_comm::RcclComm::cta_budget_max)
+      .def("sendrecv", &tds_comm::RcclComm::sendrecv)
       .def("allreduce", &tds_comm::RcclComm::allreduce)
       .def("broadcast", &tds_comm::RcclComm::broadcast)
       .def("broadcast_coalesced", &tds_comm::RcclComm::broadcast_coalesced)

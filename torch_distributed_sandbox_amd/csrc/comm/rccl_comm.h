@@ -57,6 +57,25 @@ namespace tds_comm {
     ncclResult_t r_ = (cmd);                                                            \
     TORCH_CHECK(r_ == ncclSuccess, "RCCL error '", ncclGetErrorString(r_), "' in ", #cmd); \
   } while (0)
+// A communicator created non-blocking may return ncclInProgress from any call;
+// the call has then been accepted and finishes asynchronously.  Poll the async
+// state until it settles (bounded), then check it like a blocking result.
+inline ncclResult_t nccl_settle(ncclResult_t r, ncclComm_t c, int64_t timeout_ms) {
+  if (r != ncclInProgress || c == nullptr) return r;
+  const auto t0 = std::chrono::steady_clock::now();
+  ncclResult_t st = ncclInProgress;
+  while (true) {
+    if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return ncclInternalError;
+    if (st != ncclInProgress) return st;
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return ncclInProgress;
+    std::this_thread::yield();
+  }
+}
+#define TDS_RCCL_C(c, cmd)                                                                   \
+  do {                                                                                       \
+    ncclResult_t r_ = nccl_settle((cmd), (c), st_->timeout_ms);                              \
+    TORCH_CHECK(r_ == ncclSuccess, "RCCL error '", ncclGetErrorString(r_), "' in ", #cmd);  \
+  } while (0)
 #define TDS_HIP(cmd)                                                                   \
   do {                                                                                 \
     hipError_t e_ = (cmd);                                                             \
@@ -91,7 +110,11 @@ inline ncclRedOp_t nccl_op(int64_t op) {
 
 // State shared by the communicator, its works and the watchdog.
 struct RcclState {
+  // comm is read by the main thread (collectives, TDS_DEBUG_SYNC checks) and the
+  // watchdog, and freed by fail(): every use after construction holds comm_mu, and
+  // fail() clears it under the same lock before the communicator is aborted.
   ncclComm_t comm = nullptr;
+  std::mutex comm_mu;
   int device = 0;
   int64_t rank = 0, world = 1, timeout_ms = 600000;
   bool exit_on_error = true;
@@ -126,8 +149,12 @@ struct RcclState {
     }
     std::fprintf(stderr, "[tds rccl] rank %lld: %s -- aborting communicator\n", (long long)rank, why.c_str());
     std::fflush(stderr);
-    if (comm) ncclCommAbort(comm);
-    comm = nullptr;
+    {
+      std::lock_guard<std::mutex> g(comm_mu);
+      ncclComm_t c = comm;
+      comm = nullptr;
+      if (c) ncclCommAbort(c);
+    }
     if (exit_on_error) {
       std::fprintf(stderr, "[tds rccl] rank %lld: terminating process (TDS_RCCL_ERROR_HANDLING=raise to disable)\n",
                    (long long)rank);
@@ -193,13 +220,12 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     st_->timeout_ms = timeout_ms;
     const char* eh = std::getenv("TDS_RCCL_ERROR_HANDLING");
     st_->exit_on_error = !(eh && std::string(eh) == "raise");
-    const char* ds = std::getenv("TDS_DEBUG_SYNC");
-    st_->debug_sync = ds && std::atoi(ds) != 0;
+    st_->debug_sync = env_flag("TDS_DEBUG_SYNC");
     ncclUniqueId uid;
     auto idc = id.contiguous().cpu();
     std::memcpy(&uid, idc.data_ptr(), sizeof(uid));
     c10::hip::HIPGuard g((c10::DeviceIndex)device);
-    TDS_RCCL(ncclCommInitRank(&st_->comm, (int)world, uid, (int)rank));
+    init_comm(uid);
     TDS_HIP(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
     watchdog_ = std::thread([s = st_] { watchdog_loop(s); });
   }
@@ -215,11 +241,15 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
       st_->cv.notify_all();
       watchdog_.join();
     }
-    if (st_->comm && !st_->aborted.load()) {
-      c10::hip::HIPGuard g((c10::DeviceIndex)st_->device);
-      (void)hipStreamSynchronize(stream_.stream());
-      ncclCommDestroy(st_->comm);
-      st_->comm = nullptr;
+    if (!st_->aborted.load()) {
+      std::lock_guard<std::mutex> cl(st_->comm_mu);
+      if (st_->comm) {
+        c10::hip::HIPGuard g((c10::DeviceIndex)st_->device);
+        (void)hipStreamSynchronize(stream_.stream());
+        ncclComm_t c = st_->comm;
+        st_->comm = nullptr;
+        ncclCommDestroy(c);
+      }
     }
     if (ready_) {
       (void)hipEventDestroy(ready_);
@@ -239,6 +269,17 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
   int64_t rank() const { return st_->rank; }
   int64_t world_size() const { return st_->world; }
   int64_t device() const { return st_->device; }
+  // ncclCommCount of the live communicator (the bench reports it as rccl_ranks)
+  int64_t comm_count() {
+    std::lock_guard<std::mutex> g(st_->comm_mu);
+    st_->check_ok();
+    int n = 0;
+    TORCH_CHECK(st_->comm != nullptr, "rccl: communicator is gone");
+    TDS_RCCL(ncclCommCount(st_->comm, &n));
+    return n;
+  }
+  int64_t cta_budget_min() const { return min_ctas_; }
+  int64_t cta_budget_max() const { return max_ctas_; }
   int64_t pending() {
     std::lock_guard<std::mutex> g(st_->mu);
     return (int64_t)st_->pending.size();
@@ -248,7 +289,7 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
   c10::intrusive_ptr<CommWork> allreduce_async(at::Tensor t, int64_t op) override {
     check_dev(t);
     return run({t}, "allreduce", [&](ncclComm_t c, hipStream_t s) {
-      TDS_RCCL(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), nccl_op(op), c, s));
+      TDS_RCCL_C(c, ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), nccl_op(op), c, s));
     });
   }
   c10::intrusive_ptr<CommWork> allreduce(at::Tensor t, int64_t op) { return allreduce_async(t, op); }
@@ -256,7 +297,7 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
   c10::intrusive_ptr<CommWork> broadcast(at::Tensor t, int64_t root) {
     check_dev(t);
     return run({t}, "broadcast", [&](ncclComm_t c, hipStream_t s) {
-      TDS_RCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)root, c, s));
+      TDS_RCCL_C(c, ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)root, c, s));
     });
   }
 
@@ -266,15 +307,15 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     return run(ts, "broadcast_coalesced", [&](ncclComm_t c, hipStream_t s) {
       TDS_RCCL(ncclGroupStart());
       for (auto& t : ts)
-        TDS_RCCL(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)root, c, s));
-      TDS_RCCL(ncclGroupEnd());
+        TDS_RCCL_C(c, ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)root, c, s));
+      TDS_RCCL_C(c, ncclGroupEnd());
     });
   }
 
   c10::intrusive_ptr<CommWork> reduce(at::Tensor t, int64_t root, int64_t op) {
     check_dev(t);
     return run({t}, "reduce", [&](ncclComm_t c, hipStream_t s) {
-      TDS_RCCL(ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), nccl_op(op), (int)root,
+      TDS_RCCL_C(c, ncclReduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), nccl_op(op), (int)root,
                           c, s));
     });
   }
@@ -285,7 +326,7 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     TORCH_CHECK(out.numel() == in.numel() * st_->world && out.scalar_type() == in.scalar_type(),
                 "rccl allgather: output must hold world_size x input elements");
     return run({out, in}, "allgather", [&](ncclComm_t c, hipStream_t s) {
-      TDS_RCCL(ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in.scalar_type()), c, s));
+      TDS_RCCL_C(c, ncclAllGather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dtype(in.scalar_type()), c, s));
     });
   }
 
@@ -295,7 +336,7 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     TORCH_CHECK(in.numel() == out.numel() * st_->world && out.scalar_type() == in.scalar_type(),
                 "rccl reduce_scatter: input must hold world_size x output elements");
     return run({out, in}, "reduce_scatter", [&](ncclComm_t c, hipStream_t s) {
-      TDS_RCCL(ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in.scalar_type()),
+      TDS_RCCL_C(c, ncclReduceScatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dtype(in.scalar_type()),
                                  nccl_op(op), c, s));
     });
   }
@@ -310,24 +351,50 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
       const auto dt = nccl_dtype(in.scalar_type());
       TDS_RCCL(ncclGroupStart());
       for (int64_t r = 0; r < st_->world; ++r) {
-        TDS_RCCL(ncclSend(static_cast<char*>(in.data_ptr()) + r * n * esz, n, dt, (int)r, c, s));
-        TDS_RCCL(ncclRecv(static_cast<char*>(out.data_ptr()) + r * n * esz, n, dt, (int)r, c, s));
+        TDS_RCCL_C(c, ncclSend(static_cast<char*>(in.data_ptr()) + r * n * esz, n, dt, (int)r, c, s));
+        TDS_RCCL_C(c, ncclRecv(static_cast<char*>(out.data_ptr()) + r * n * esz, n, dt, (int)r, c, s));
       }
-      TDS_RCCL(ncclGroupEnd());
+      TDS_RCCL_C(c, ncclGroupEnd());
     });
   }
 
   c10::intrusive_ptr<CommWork> send(at::Tensor t, int64_t peer) {
     check_dev(t);
     return run({t}, "send", [&](ncclComm_t c, hipStream_t s) {
-      TDS_RCCL(ncclSend(t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)peer, c, s));
+      TDS_RCCL_C(c, ncclSend(t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)peer, c, s));
     });
   }
 
   c10::intrusive_ptr<CommWork> recv(at::Tensor t, int64_t peer) {
     check_dev(t);
     return run({t}, "recv", [&](ncclComm_t c, hipStream_t s) {
-      TDS_RCCL(ncclRecv(t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)peer, c, s));
+      TDS_RCCL_C(c, ncclRecv(t.data_ptr(), t.numel(), nccl_dtype(t.scalar_type()), (int)peer, c, s));
+    });
+  }
+
+  // Grouped point-to-point exchange: every (tensor, peer) pair in `sends` is sent and
+  // every pair in `recvs` received inside one ncclGroupStart/End, so each peer pair
+  // uses its own xGMI link concurrently.  The building block of the sharded fc
+  // exchange (parallel/factored.py): strided all-to-all of activation shards and the
+  // all-gather of gradient shards, uneven splits included.
+  c10::intrusive_ptr<CommWork> sendrecv(std::vector<at::Tensor> sends, std::vector<int64_t> send_peers,
+                                        std::vector<at::Tensor> recvs, std::vector<int64_t> recv_peers) {
+    TORCH_CHECK(sends.size() == send_peers.size() && recvs.size() == recv_peers.size(),
+                "rccl sendrecv: tensors and peers must pair up");
+    std::vector<at::Tensor> all;
+    for (auto& t : sends) { check_dev(t); all.push_back(t); }
+    for (auto& t : recvs) { check_dev(t); all.push_back(t); }
+    for (auto p : send_peers) TORCH_CHECK(p >= 0 && p < st_->world, "rccl sendrecv: bad peer ", p);
+    for (auto p : recv_peers) TORCH_CHECK(p >= 0 && p < st_->world, "rccl sendrecv: bad peer ", p);
+    return run(all, "sendrecv", [&](ncclComm_t c, hipStream_t s) {
+      TDS_RCCL(ncclGroupStart());
+      for (size_t i = 0; i < sends.size(); ++i)
+        TDS_RCCL_C(c, ncclSend(sends[i].data_ptr(), sends[i].numel(), nccl_dtype(sends[i].scalar_type()),
+                               (int)send_peers[i], c, s));
+      for (size_t i = 0; i < recvs.size(); ++i)
+        TDS_RCCL_C(c, ncclRecv(recvs[i].data_ptr(), recvs[i].numel(), nccl_dtype(recvs[i].scalar_type()),
+                               (int)recv_peers[i], c, s));
+      TDS_RCCL_C(c, ncclGroupEnd());
     });
   }
 
@@ -347,6 +414,59 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
   std::thread watchdog_;
   at::Tensor barrier_buf_;
   std::mutex run_mu_;  // the caller (main thread) and the reducer (autograd thread) may both enqueue
+  int64_t min_ctas_ = 0, max_ctas_ = 0;  // 0 = RCCL's own choice
+
+  static bool env_flag(const char* name) {
+    const char* v = std::getenv(name);
+    return v && *v && std::string(v) != "0";  // same rule as parallel/distributed.py
+  }
+  static int64_t env_int(const char* name, int64_t dflt) {
+    const char* v = std::getenv(name);
+    return (v && *v) ? std::atoll(v) : dflt;
+  }
+
+  // Communicator creation.  Default: ncclCommInitRankConfig with blocking=0, then a
+  // bounded poll of the async state, so a rank that never joins turns into an error
+  // (and an aborted communicator) after TDS_RCCL_INIT_TIMEOUT_MS instead of hanging
+  // the others forever (the watchdog only exists once init has returned).
+  // TDS_RCCL_MIN_CTAS / TDS_RCCL_MAX_CTAS bound the workgroups (CUs) RCCL's kernels
+  // take from the compute kernels they overlap with.
+  void init_comm(const ncclUniqueId& uid) {
+    min_ctas_ = env_int("TDS_RCCL_MIN_CTAS", 0);
+    max_ctas_ = env_int("TDS_RCCL_MAX_CTAS", 0);
+    if (env_flag("TDS_RCCL_BLOCKING_INIT")) {
+      TORCH_CHECK(min_ctas_ == 0 && max_ctas_ == 0, "TDS_RCCL_*_CTAS needs the config (non-blocking) init");
+      TDS_RCCL(ncclCommInitRank(&st_->comm, (int)st_->world, uid, (int)st_->rank));
+      return;
+    }
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    if (min_ctas_ > 0) cfg.minCTAs = (int)min_ctas_;
+    if (max_ctas_ > 0) cfg.maxCTAs = (int)max_ctas_;
+    const int64_t limit_ms = env_int("TDS_RCCL_INIT_TIMEOUT_MS", st_->timeout_ms);
+    ncclComm_t c = nullptr;
+    ncclResult_t r = ncclCommInitRankConfig(&c, (int)st_->world, uid, (int)st_->rank, &cfg);
+    TORCH_CHECK(r == ncclSuccess || r == ncclInProgress, "RCCL error '", ncclGetErrorString(r),
+                "' in ncclCommInitRankConfig (rank ", st_->rank, " of ", st_->world, ")");
+    const auto t0 = std::chrono::steady_clock::now();
+    ncclResult_t state = r;
+    while (state == ncclInProgress) {
+      if (ncclCommGetAsyncError(c, &state) != ncclSuccess) state = ncclInternalError;
+      if (state != ncclInProgress) break;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(limit_ms)) {
+        ncclCommAbort(c);
+        TORCH_CHECK(false, "rccl: communicator init did not complete within ", limit_ms, " ms on rank ", st_->rank,
+                    " of ", st_->world, " (a rank did not join?)");
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if (state != ncclSuccess) {
+      ncclCommAbort(c);
+      TORCH_CHECK(false, "RCCL error '", ncclGetErrorString(state), "' during communicator init (rank ", st_->rank,
+                  ")");
+    }
+    st_->comm = c;
+  }
 
   void check_dev(const at::Tensor& t) const {
     TORCH_CHECK(t.is_cuda() && t.get_device() == st_->device, "rccl: tensor must be on cuda:", st_->device);
@@ -363,7 +483,11 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     // comm stream waits for the producer work already queued on the caller's stream
     TDS_HIP(hipEventRecord(ready_, cur));
     TDS_HIP(hipStreamWaitEvent(cs, ready_, 0));
-    fn(st_->comm, cs);
+    {
+      std::lock_guard<std::mutex> cl(st_->comm_mu);
+      st_->check_ok();
+      fn(st_->comm, cs);
+    }
     for (const auto& t : ts) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
     hipEvent_t done;
     TDS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
@@ -385,8 +509,12 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     const hipError_t he = hipStreamSynchronize(cs);
     TORCH_CHECK(he == hipSuccess, "TDS_DEBUG_SYNC: ", what, " on rank ", st_->rank, ": HIP error ",
                 hipGetErrorString(he));
+    st_->check_ok();  // a watchdog abort is reported as such, never as a use of a freed communicator
     ncclResult_t ae = ncclSuccess;
-    if (st_->comm) TDS_RCCL(ncclCommGetAsyncError(st_->comm, &ae));
+    {
+      std::lock_guard<std::mutex> cl(st_->comm_mu);
+      if (st_->comm) TDS_RCCL(ncclCommGetAsyncError(st_->comm, &ae));
+    }
     TORCH_CHECK(ae == ncclSuccess, "TDS_DEBUG_SYNC: ", what, " on rank ", st_->rank, ": RCCL async error ",
                 ncclGetErrorString(ae));
     st_->check_ok();
@@ -415,9 +543,11 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
         }
         break;  // collectives complete in order on the comm stream
       }
-      if (why.empty() && s->comm) {
+      if (why.empty()) {
+        std::lock_guard<std::mutex> cl(s->comm_mu);
         ncclResult_t ae = ncclSuccess;
-        if (ncclCommGetAsyncError(s->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+        if (s->comm && ncclCommGetAsyncError(s->comm, &ae) == ncclSuccess && ae != ncclSuccess &&
+            ae != ncclInProgress)
           why = std::string("RCCL async error: ") + ncclGetErrorString(ae);
       }
       if (!why.empty()) {

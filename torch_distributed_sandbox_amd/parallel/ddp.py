@@ -227,6 +227,13 @@ class DistributedDataParallel(nn.Module):
     def reducer_kind(self) -> str:
         return "native" if self._native is not None else "python"
 
+    def fc_grad_path(self) -> str:
+        """How the big fc layer's gradient was averaged in the steps run so far."""
+        if self.world_size == 1:
+            return "local"
+        used = sorted({ex.last_path for ex in self._exchanges if ex.last_path})
+        return "+".join(used) if used else "allreduce"
+
     # ------------------------------------------------------------------ setup helpers
     @staticmethod
     def _exchange_candidates(module):

@@ -60,6 +60,7 @@ class ActivationExchange:
         self.armed = False
         self.active = False
         self.steps_exchanged = 0
+        self.last_path = None  # "activation-exchange" once a step used it
         self._x_all = self._x_work = self._dy = None
         self.side_stream = None  # set by DDP(overlap_optimizer=True): dW is formed off the compute stream
         setattr(weight, _ATTR, self)
@@ -166,3 +167,4 @@ class ActivationExchange:
         self._x_all = self._x_work = self._dy = self._x_local = None
         self.active = False
         self.steps_exchanged += 1
+        self.last_path = "activation-exchange"
