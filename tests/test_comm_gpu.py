@@ -125,9 +125,18 @@ def test_linear_dw_kernel(gpu):
         assert torch.allclose(db.double(), dy.double().sum(0) * 0.5, rtol=1e-6, atol=1e-6)
         tds._ext.ops().linear_dw(dy, x, dw, db, 0.5, True)  # accumulate
         assert ((dw.double() - 2 * ref).abs().max() / ref.abs().max()).item() < 1e-6
+    # column shard written in place into a wider matrix (row stride > K), > 64 rows in passes
+    dy = torch.randn(100, 10, device=gpu)
+    x = torch.randn(100, 3000, device=gpu)
+    full = torch.full((10, 9000), 7.0, device=gpu)
+    tds._ext.ops().linear_dw(dy, x, full[:, 3000:6000], None, 0.25, False)
+    ref = (dy.double().t() @ x.double()) * 0.25
+    assert ((full[:, 3000:6000].double() - ref).abs().max() / ref.abs().max()).item() < 1e-6
+    assert (full[:, :3000] == 7).all() and (full[:, 6000:] == 7).all()
 
 
-def test_activation_exchange_fused_convnet(pg, gpu):
+@pytest.mark.parametrize("mode", ["activations", "sharded"])
+def test_activation_exchange_fused_convnet(pg, gpu, mode):
     """Forced activation exchange at world size 1 runs the whole GPU path (head
     forward writing the fc input rows, head backward without dW, linear_dw into
     the bucket) and must reproduce the plain fused gradients."""
@@ -141,7 +150,7 @@ def test_activation_exchange_fused_convnet(pg, gpu):
     H = 256  # fc: 10 x 131072 (exchange candidate)
     m = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
     ref = copy.deepcopy(m)
-    ddp = DistributedDataParallel(m, grad_exchange="activations")
+    ddp = DistributedDataParallel(m, grad_exchange=mode)
     assert len(ddp.exchanges) == 1
     opt = ddp.attach_optimizer(SGD(m.parameters(), 0.01))
     x = torch.rand(3, 1, H, H, device=gpu)
@@ -165,7 +174,8 @@ def test_activation_exchange_fused_convnet(pg, gpu):
     assert ddp.exchanges[0].steps_exchanged == 2
 
 
-@pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("allreduce", True)])
+@pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("sharded", False),
+                                           ("allreduce", True)])
 def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     """overlap_optimizer: the fc bucket's collective + SGD update run on a side stream
     and the next forward's head waits on a parameter fence; the trajectory must be

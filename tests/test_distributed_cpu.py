@@ -235,7 +235,7 @@ def test_find_free_port():
 
 
 # ---------------------------------------------------------------- activation exchange (parallel/factored.py)
-def _w_exchange(rank, world, port, backend, H, B):
+def _w_exchange(rank, world, port, backend, H, B, mode="auto"):
     dist = _init(rank, world, port, backend)
     from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
@@ -244,7 +244,7 @@ def _w_exchange(rank, world, port, backend, H, B):
     torch.manual_seed(0)
     m_ex = ConvNet(image_shape=(H, H))
     m_ar = copy.deepcopy(m_ex)
-    d_ex = DistributedDataParallel(m_ex, grad_exchange="auto")
+    d_ex = DistributedDataParallel(m_ex, grad_exchange=mode)
     d_ar = DistributedDataParallel(m_ar, grad_exchange="allreduce")
     assert len(d_ex.exchanges) == 1 and not d_ar.exchanges
     # the fc layer owns bucket 0 alone in both layouts
@@ -270,6 +270,7 @@ def _w_exchange(rank, world, port, backend, H, B):
         o_ex.step()
         o_ar.step()
     assert d_ex.exchanges[0].steps_exchanged == 3
+    assert d_ex.fc_grad_path() == ("sharded-exchange" if mode == "sharded" else "activation-exchange")
     # accumulation: a no_sync step, then a synced step: the locally accumulated fc
     # gradient is all-reduced as it is and this step's exchanged average added
     with torch.no_grad():  # re-align the replicas (3 updates of a chaotic model drift at 1e-5)
@@ -296,20 +297,47 @@ def test_activation_exchange_matches_allreduce(backend):
     launch.spawn(_w_exchange, args=(2, launch.find_free_port(), backend, 232, 2), nprocs=2, timeout=300)
 
 
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("host", 3), ("gloo", 4)])
+def test_sharded_exchange_matches_allreduce(backend, world):
+    """Column-sharded fc gradient (all-to-all of X shards, per-shard dW, all-gather of the
+    shards) equals the bucket all-reduce average, including no_sync accumulation; gloo uses
+    batched isend/irecv, the ring-only host backend the packed all-gather fallback."""
+    launch.spawn(_w_exchange, args=(world, launch.find_free_port(), backend, 232, 2, "sharded"), nprocs=world,
+                 timeout=300)
+
+
+def test_exchange_byte_model():
+    from torch_distributed_sandbox_amd.parallel import factored as F
+
+    K, N, B = 18_000_000, 10, 5
+    mb = lambda p, w: F.link_bytes(p, B, N, K, w) / 1e6  # noqa: E731
+    assert (round(mb("allreduce", 2)), round(mb("activations", 2)), round(mb("sharded", 2))) == (720, 360, 540)
+    assert (round(mb("allreduce", 8)), round(mb("activations", 8)), round(mb("sharded", 8))) == (180, 360, 135)
+    assert [F.choose_path(B, N, K, w) for w in (2, 3, 4, 8)] == ["activations", "activations", "sharded", "sharded"]
+    assert F.choose_path(16, 10, K, 8) == "allreduce"  # more rows than outputs: the dense gradient is smaller
+    for w in (1, 2, 3, 7, 8):
+        b = F.shard_bounds(K, w)
+        assert b[0][0] == 0 and b[-1][1] == K and all(b[i][1] == b[i + 1][0] for i in range(w - 1))
+        assert all(a % 64 == 0 for a, _ in b)
+
+
 def _w_exchange_policy(rank, world, port):
     dist = _init(rank, world, port, "host")
     from torch_distributed_sandbox_amd.ops import Linear
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+    from torch_distributed_sandbox_amd.parallel import factored as F
 
     lin = Linear(1 << 17, 10)
     d = DistributedDataParallel(lin)
     ex = d.exchanges[0]
-    # bytes per rank: exchange (W-1)*B*in vs ring all-reduce 2(W-1)/W*in*out  ->  B*W <= 2*out
-    assert ex.worthwhile(5) == (5 * world <= 20)
-    assert ex.worthwhile(16) is False
+    for rows in (5, 6, 16):
+        want = F.choose_path(rows, 10, 1 << 17, world)
+        assert ex.path(rows) == (None if want == "allreduce" else want)
+    assert ex.worthwhile(16) is False  # 16 rows > 10 outputs: all-reduce of dW is cheapest
     x = torch.randn(6, 1 << 17)
     d(x).sum().backward()
-    assert ex.steps_exchanged == (1 if 6 * world <= 20 else 0)
+    assert ex.steps_exchanged == 1
+    assert d.fc_grad_path() == ("activation-exchange" if world == 2 else "sharded-exchange")
     dist.destroy_process_group()
 
 

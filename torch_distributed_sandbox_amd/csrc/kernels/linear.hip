@@ -176,12 +176,14 @@ __global__ __launch_bounds__(256) void linear_bwd_skinny_kernel(const float* __r
 
 // Weight gradient of a linear layer from (grad_output, input) rows:
 //   dW[n][k] (= or +=) scale * sum_m g[m][n] x[m][k],  db[n] (= or +=) scale * sum_m g[m][n]
-// M <= 64 rows (e.g. the all-gathered rows of every rank), N <= 16 outputs, any K.
+// M <= 64 rows (e.g. the all-gathered rows of every rank), N <= 16 outputs, any K; dW rows
+// are ldw apart (ldw = K for a dense matrix, > K for a column shard written in place into
+// the full [N, ldw] gradient, parallel/factored.py sharded path).
 // Exact fp32 on v_mfma_f32_16x16x4_f32: A[n][m] = g[m][n] stays in registers, B = 4 rows x
 // 16 columns of x per step; memory-bound on reading x and writing dW.
 __global__ __launch_bounds__(256) void linear_dw_mfma_kernel(const float* __restrict__ g, const float* __restrict__ x,
                                                              float* __restrict__ dW, float* __restrict__ db, int M,
-                                                             int N, int64_t K, float scale, int acc) {
+                                                             int N, int64_t K, int64_t ldw, float scale, int acc) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int li = lane & 15, gq = lane >> 4;
   const int steps = (M + 3) / 4;
@@ -214,7 +216,7 @@ __global__ __launch_bounds__(256) void linear_dw_mfma_kernel(const float* __rest
       for (int r = 0; r < 4; ++r) {
         const int n = 4 * gq + r;
         if (n < N) {
-          float* ptr = dW + (int64_t)n * K + col;
+          float* ptr = dW + (int64_t)n * ldw + col;
           const float v = scale * d[r];
           *ptr = acc ? *ptr + v : v;
         }
@@ -269,13 +271,13 @@ int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float
   return 0;
 }
 
-int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, int N, int64_t K, float scale, int acc,
-                  hipStream_t st) {
-  if (M > 64 || N > 16 || M < 1) return -1;
+int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, int N, int64_t K, int64_t ldw,
+                  float scale, int acc, hipStream_t st) {
+  if (M > 64 || N > 16 || M < 1 || ldw < K) return -1;
   int64_t ncb = (K + 15) / 16;
   int64_t grid = (ncb + 3) / 4;
   if (grid > 8192) grid = 8192;
-  hipLaunchKernelGGL(linear_dw_mfma_kernel, dim3((unsigned)grid), dim3(256), 0, st, dy, x, dW, db, M, N, K, scale,
-                     acc);
+  hipLaunchKernelGGL(linear_dw_mfma_kernel, dim3((unsigned)grid), dim3(256), 0, st, dy, x, dW, db, M, N, K, ldw,
+                     scale, acc);
   return 0;
 }

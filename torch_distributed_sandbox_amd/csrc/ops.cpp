@@ -351,21 +351,30 @@ Tensor linear_bwd_into(const Tensor& dy, const Tensor& x, const Tensor& w, const
   return dx;
 }
 
-// dW (= or +=) scale * dy^T x, db (= or +=) scale * sum_rows dy   (dy [M,N], x [M,K], M <= 64, N <= 16)
+// dW (= or +=) scale * dy^T x, db (= or +=) scale * sum_rows dy   (dy [M,N], x [M,K], N <= 16).
+// dW may be a column slice of a wider row-major matrix (unit column stride, any row stride):
+// the sharded fc exchange writes its shard straight into the full gradient.  More than 64
+// rows run as 64-row passes that accumulate.
 void linear_dw(const Tensor& dy, const Tensor& x, const Tensor& dw, const c10::optional<Tensor>& db, double scale,
                bool accumulate) {
   check_f32_dev(dy, "grad_output");
   check_f32_dev(x, "input");
-  check_f32_dev(dw, "dW");
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat, "tdsa.linear_dw: dW must be a float32 GPU tensor");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dw.dim() == 2 && dy.size(0) == x.size(0) && dw.size(0) == dy.size(1) &&
                   dw.size(1) == x.size(1),
               "tdsa.linear_dw: shape mismatch");
+  TORCH_CHECK(dw.stride(1) == 1 && dw.stride(0) >= dw.size(1), "tdsa.linear_dw: dW rows must be unit-stride");
+  TORCH_CHECK(dy.size(1) <= 16 && dy.size(0) >= 1, "tdsa.linear_dw: needs 1 <= rows and outputs <= 16");
   check_opt(db, "db", dw.size(0));
   c10::DeviceGuard g(x.device());
-  const int rc = tds_linear_dw(dy.data_ptr<float>(), x.data_ptr<float>(), dw.data_ptr<float>(), opt_mut_ptr(db),
-                               (int)dy.size(0), (int)dy.size(1), x.size(1), (float)scale, accumulate ? 1 : 0,
-                               cur_stream(x));
-  TORCH_CHECK(rc == 0, "tdsa.linear_dw: needs rows <= 64 and outputs <= 16");
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  for (int64_t m0 = 0; m0 < M; m0 += 64) {
+    const int64_t mc = std::min<int64_t>(64, M - m0);
+    const int rc = tds_linear_dw(dy.data_ptr<float>() + m0 * N, x.data_ptr<float>() + m0 * K, dw.data_ptr<float>(),
+                                 opt_mut_ptr(db), (int)mc, (int)N, K, dw.stride(0), (float)scale,
+                                 (accumulate || m0 > 0) ? 1 : 0, cur_stream(x));
+    TORCH_CHECK(rc == 0, "tdsa.linear_dw: bad launch shape");
+  }
 }
 
 }  // namespace

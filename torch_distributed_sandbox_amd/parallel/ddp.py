@@ -92,8 +92,8 @@ class DistributedDataParallel(nn.Module):
         self._verify_param_shapes()
 
         # ---- flat layout in gradient-ready order (reverse definition order)
-        if grad_exchange not in ("auto", "allreduce", "activations"):
-            raise ValueError(f"grad_exchange must be auto|allreduce|activations, got {grad_exchange!r}")
+        if grad_exchange not in ("auto", "allreduce", "activations", "sharded"):
+            raise ValueError(f"grad_exchange must be auto|allreduce|activations|sharded, got {grad_exchange!r}")
         self.grad_exchange = grad_exchange
         big_layers = self._exchange_candidates(module)
         exch_layers = big_layers if grad_exchange != "allreduce" else []
@@ -166,7 +166,8 @@ class DistributedDataParallel(nn.Module):
 
         # ---- activation exchange for huge skinny Linear layers (parallel/factored.py)
         self._exchanges = []
-        if exch_layers and (self.world_size > 1 or (grad_exchange == "activations" and tdist.is_initialized())):
+        forced = grad_exchange in ("activations", "sharded")
+        if exch_layers and (self.world_size > 1 or (forced and tdist.is_initialized())):
             for lyr in exch_layers:
                 b = self._layer_bucket[id(lyr)]
                 self._exchanges.append(factored.ActivationExchange(

@@ -252,6 +252,125 @@ def reduce_scatter_tensor(output, input, op=ReduceOp.SUM, group=None, async_op: 
                        "reduce_scatter_tensor", output)
 
 
+class _DoneWork:
+    def wait(self, timeout=None):
+        return True
+
+    def is_completed(self):
+        return True
+
+
+class _Works:
+    def __init__(self, works):
+        self._works = [w for w in works if w is not None]
+
+    def wait(self, timeout=None):
+        for w in self._works:
+            w.wait()
+        return True
+
+    def is_completed(self):
+        return all(w.is_completed() for w in self._works)
+
+
+def sendrecv(sends, recvs, group=None, async_op: bool = True):
+    """Grouped point-to-point exchange: ``sends``/``recvs`` are lists of
+    ``(tensor, peer)``; chunks between one pair of ranks are matched in list order.
+    Pairs with ``peer == rank`` are local copies.
+
+    * ``rccl-native``: one ncclGroupStart/End of ncclSend/ncclRecv on the comm
+      stream (``RcclComm.sendrecv``): every peer pair streams over its own xGMI link.
+    * torch's ``nccl`` and ``gloo`` (CPU tensors): ``batch_isend_irecv``.
+    * anything else (the ring-only ``host`` backend, gloo with GPU tensors in the
+      one-GPU rehearsal): an all-gather of per-destination packed buffers — same
+      result, more bytes; rehearsal paths only.
+    """
+    me = get_rank(group)
+    local_s = [(t, p) for t, p in sends if p == me]
+    local_r = [(t, p) for t, p in recvs if p == me]
+    if len(local_s) != len(local_r):
+        raise ValueError("sendrecv: self-sends and self-receives must pair up")
+    for (src, _), (dst, _) in zip(local_s, local_r):
+        dst.copy_(src)
+    sends = [(t, p) for t, p in sends if p != me]
+    recvs = [(t, p) for t, p in recvs if p != me]
+    debug = debug_sync_enabled()
+    from .rccl_backend import native_comm_of
+
+    comm, kind = native_comm_of(group)
+    if kind == "rccl":
+        w = comm.sendrecv([t for t, _ in sends], [p for _, p in sends], [t for t, _ in recvs],
+                          [p for _, p in recvs])
+        w = _NativeWork(w)
+        if debug or not async_op:
+            w.wait()
+            if debug:
+                torch.cuda.synchronize()
+        return w if async_op else None
+    backend = dist.get_backend(group)
+    all_cpu = all(t.device.type == "cpu" for t, _ in sends + recvs)
+    if backend == "nccl" or (backend == "gloo" and all_cpu):
+        ops = []
+        tags = {}
+        for t, p in sends:
+            k = ("s", p)
+            tags[k] = tags.get(k, -1) + 1
+            ops.append(dist.P2POp(dist.isend, t.contiguous(), p, group=group, tag=tags[k]))
+        for t, p in recvs:
+            k = ("r", p)
+            tags[k] = tags.get(k, -1) + 1
+            ops.append(dist.P2POp(dist.irecv, t, p, group=group, tag=tags[k]))
+        works = dist.batch_isend_irecv(ops) if ops else []
+        w = _Works(works)
+        if not async_op or debug:
+            w.wait()
+        return w if async_op else None
+    _sendrecv_packed(sends, recvs, group, me)
+    return _DoneWork() if async_op else None
+
+
+class _NativeWork:
+    def __init__(self, native):
+        self._native = native
+
+    def wait(self, timeout=None):
+        self._native.wait()
+        return True
+
+    def is_completed(self):
+        return self._native.is_completed()
+
+
+def _sendrecv_packed(sends, recvs, group, me):
+    world = get_world_size(group)
+    dtypes = {t.dtype for t, _ in sends + recvs}
+    if len(dtypes) > 1:
+        raise ValueError("sendrecv (packed fallback): all chunks must share one dtype")
+    ref = (sends + recvs)[0][0] if sends or recvs else None
+    dev = ref.device if ref is not None else torch.device("cpu")
+    dt = ref.dtype if ref is not None else torch.float32
+    per_dst = [[] for _ in range(world)]
+    for t, p in sends:
+        per_dst[p].append(t.reshape(-1))
+    sizes = [sum(t.numel() for t in lst) for lst in per_dst]
+    mx = torch.tensor([max(sizes) if sizes else 0], dtype=torch.int64, device=dev)
+    all_reduce(mx, ReduceOp.MAX, group=group)
+    n = int(mx.item())
+    if n == 0:
+        return
+    buf = torch.zeros((world, n), dtype=dt, device=dev)
+    for p, lst in enumerate(per_dst):
+        if lst:
+            buf[p, :sizes[p]] = torch.cat(lst)
+    out = torch.empty((world, world, n), dtype=dt, device=dev)
+    all_gather_into_tensor(out.view(-1), buf.view(-1), group=group)
+    offs = [0] * world
+    for t, p in recvs:
+        k = t.numel()
+        t.copy_(out[p, me, offs[p]:offs[p] + k].view_as(t))
+        offs[p] += k
+
+
 def barrier(group=None) -> None:
     """Barrier.  On RCCL this is a 1-element all-reduce plus a stream sync
     (ProcessGroupNCCL semantics)."""

@@ -1,67 +1,109 @@
-"""Activation exchange: exact data-parallel gradients for a huge, skinny Linear
-layer without all-reducing its weight gradient.
+"""Exact data-parallel gradients for a huge, skinny Linear layer without a plain
+all-reduce of its weight gradient.
 
 Data parallelism averages ``dW = dYᵀX`` over ranks.  The reference's DDP
 (mnist_distributed.py:67) all-reduces the full gradient: for the 3000² ConvNet's
-fc layer that is 720 MB per step for a matrix of rank ≤ 5
-per rank.  Over xGMI — point-to-point links of ≈77 GB/s per direction — a ring
-all-reduce moves ``2(W-1)/W × 720 MB`` per GPU, which at W = 2 means ≈9 ms on
-the single link joining the pair: more than the whole compute step.
+fc layer that is 720 MB per step for a matrix of rank ≤ B
+per rank.  The gradient can instead be formed from its factors — each rank's
+fc input rows ``X_r`` [B, K] and output gradients ``dY_r`` [B, N] — and the
+factors can be exchanged in two ways:
 
-The same average can be formed from the factors: each rank contributes its
-``B`` input rows ``X_r`` and output gradients ``dY_r``, and every rank computes
-``dW = (1/W) Σ_r dY_rᵀ X_r`` locally (one skinny GEMM with ``W·B`` rows).  That
-moves ``(W-1) × B × in × 4`` bytes per rank instead — 360 MB instead of 720 MB
-at W = 2 — and the exchange can start as soon as the FORWARD has produced
-``X_r``, so it overlaps the entire backward instead of only the part after the
-fc gradient exists.  Per rank the bytes favour the exchange when
-``B·W ≤ 2·out_features`` (W = 2, 3, 4 for the ConvNet: B = 5, 10 classes; at
-equal bytes the exchange still wins because it starts a whole backward earlier);
-at larger W the ring all-reduce is cheaper and is used.
+``activations``  all-gather X (and dY); every rank forms the whole averaged dW
+                 locally (one skinny GEMM with W·B rows, ``ops.linear_dw``).
+``sharded``      K is split into W contiguous column shards.  An all-to-all
+                 sends each rank's X columns of shard s to rank s, which forms
+                 ``dW[:, shard s]`` from every rank's rows; an all-gather of the
+                 shards (grouped point-to-point, one xGMI link per peer pair)
+                 then gives every rank the full averaged gradient.
 
-The result is the same average DDP produces (floating-point summation order
-differs, as it does between all-reduce algorithms), identical on every rank.
+Bytes each rank puts on each of its W-1 links per step (fully connected xGMI,
+one link per peer pair; B rows, N outputs, K inputs, 4-byte floats):
+
+    all-reduce (ring/tree)      2·N·K/W
+    activations                 B·K
+    sharded                     (B + N)·K/W
+
+For the ConvNet (B = 5, N = 10, K = 18e6: 360 MB of X per rank, 720 MB of dW):
+W = 2 → 720 / 360 / 540 MB;  W = 4 → 360 / 360 / 270 MB;  W = 8 → 180 / 360 / 135 MB.
+``auto`` takes the cheapest, preferring ``activations`` on a tie (one phase, it
+starts as soon as the forward has produced X).  Both exchanges start in the
+forward, so they overlap the whole backward (and, with DDP's overlapped
+optimizer, the next forward's convolutions) instead of only the conv backward.
+
+The result is the average DDP produces (floating-point summation order differs,
+as it does between all-reduce algorithms), bit-identical on every rank.
 
 Protocol (driven by ``parallel/ddp.py``):
 
 * ``arm(sync)`` each DDP forward: the exchange may run this step.
-* the layer's forward calls ``begin(x)``; if the exchange is worthwhile it
-  starts an async all-gather of ``x`` and tells DDP to leave this layer's bucket
-  out of the bucket all-reduce; the layer then returns no weight/bias gradient.
+* the layer's forward calls ``begin(x)``; if an exchange is chosen it starts the
+  async all-gather / all-to-all of ``x`` and tells DDP to leave this layer's
+  bucket out of the bucket all-reduce; the layer then returns no weight/bias
+  gradient.
 * the layer's backward calls ``defer(dy)``: ``dy`` is kept and a callback is
   queued on the autograd engine.
 * at the end of backward the callback all-gathers ``dy`` (a few hundred bytes),
   waits for ``x`` and writes ``dW``/``db`` straight into the bucket slots
-  (``ops.linear_dw`` on the GPU: exact-fp32 MFMA, memory-bound).  Gradients
+  (``ops.linear_dw`` on the GPU: exact-fp32 MFMA, memory-bound; the sharded path
+  writes its column shard in place and all-gathers the others).  Gradients
   accumulated locally under ``no_sync()`` are averaged with one all-reduce and
   this step's exchanged average is added, matching DDP's accumulation semantics.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import List, Optional, Tuple
 
 import torch
 
 _ATTR = "_tds_activation_exchange"
+_SHARD_ALIGN = 64  # shard boundaries on 256-byte multiples
 
 
 def get(weight) -> Optional["ActivationExchange"]:
     return getattr(weight, _ATTR, None) if weight is not None else None
 
 
+def link_bytes(path: str, rows: int, out_f: int, in_f: int, world: int, elem: int = 4) -> float:
+    """Bytes one rank sends over each of its links per step for ``path`` (model above)."""
+    if world <= 1:
+        return 0.0
+    if path == "allreduce":
+        return 2.0 * out_f * in_f * elem / world
+    if path == "activations":
+        return float(rows * in_f * elem)
+    if path == "sharded":
+        return float((rows + out_f) * in_f * elem) / world
+    raise ValueError(path)
+
+
+def choose_path(rows: int, out_f: int, in_f: int, world: int) -> str:
+    """Cheapest of allreduce / activations / sharded by per-link bytes (ties: earlier start)."""
+    order = ("activations", "sharded", "allreduce")
+    costs = {p: link_bytes(p, rows, out_f, in_f, world) for p in order}
+    return min(order, key=lambda p: (costs[p], order.index(p)))
+
+
+def shard_bounds(in_f: int, world: int) -> List[Tuple[int, int]]:
+    per = -(-in_f // world)
+    per = -(-per // _SHARD_ALIGN) * _SHARD_ALIGN
+    return [(min(in_f, r * per), min(in_f, (r + 1) * per)) for r in range(world)]
+
+
 class ActivationExchange:
+    """One exchange-capable Linear layer under DDP (see the module docstring)."""
+
     def __init__(self, weight: torch.nn.Parameter, bias: Optional[torch.nn.Parameter], group, world: int,
                  mode: str, set_skip, weight_view, bias_view):
-        if mode not in ("auto", "activations"):
-            raise ValueError(f"ActivationExchange mode must be auto|activations, got {mode!r}")
+        if mode not in ("auto", "activations", "sharded"):
+            raise ValueError(f"ActivationExchange mode must be auto|activations|sharded, got {mode!r}")
         self.weight, self.bias = weight, bias
         self.group, self.world, self.mode = group, world, mode
         self._set_skip, self._wview, self._bview = set_skip, weight_view, bias_view
         self.armed = False
-        self.active = False
+        self.active = None  # the path running this step, or None
         self.steps_exchanged = 0
-        self.last_path = None  # "activation-exchange" once a step used it
-        self._x_all = self._x_work = self._dy = None
+        self.last_path = None  # "activation-exchange" | "sharded-exchange" once a step used it
+        self._x_buf = self._x_work = self._dy = self._x_local = None
         self.side_stream = None  # set by DDP(overlap_optimizer=True): dW is formed off the compute stream
         setattr(weight, _ATTR, self)
 
@@ -70,40 +112,58 @@ class ActivationExchange:
             delattr(self.weight, _ATTR)
 
     # ---------------------------------------------------------------- policy
+    def path(self, rows: int) -> Optional[str]:
+        """"activations" | "sharded" for a step with ``rows`` local rows, or None (bucket all-reduce)."""
+        if self.mode != "auto":
+            return self.mode
+        if self.world <= 1:
+            return None
+        out_f, in_f = self.weight.shape
+        p = choose_path(rows, out_f, in_f, self.world)
+        return None if p == "allreduce" else p
+
     def worthwhile(self, rows: int) -> bool:
-        if self.mode == "activations":
-            return True
-        out_f = self.weight.shape[0]
-        # equal bytes (B*W == 2*out) still favour the exchange: it starts a whole backward earlier
-        return self.world > 1 and rows * self.world <= 2 * out_f
+        return self.path(rows) is not None
 
     def arm(self, sync: bool):
         self.armed = bool(sync)
-        self.active = False
+        self.active = None
         self._set_skip(False)
 
     # ---------------------------------------------------------------- forward
-    def _eligible(self, rows: int) -> bool:
-        if not self.armed or self.active:
-            return False
-        return self.worthwhile(rows)
+    def _eligible(self, rows: int) -> Optional[str]:
+        if not self.armed or self.active is not None:
+            return None
+        return self.path(rows)
 
     def ready(self, rows: int) -> bool:
-        """Would a forward with ``rows`` input rows (grad mode on) run the exchange?"""
-        return torch.is_grad_enabled() and self._eligible(rows)
+        """Would a forward with ``rows`` input rows (grad mode on) run an exchange?"""
+        return torch.is_grad_enabled() and self._eligible(rows) is not None
 
     def begin(self, x2d: torch.Tensor) -> bool:
         """Called from the layer's forward (possibly inside an autograd Function,
-        i.e. under no_grad) with its [rows, in] input."""
-        if not self._eligible(x2d.shape[0]):
+        i.e. under no_grad) with its [rows, in] input.  Every rank has the same rows."""
+        path = self._eligible(x2d.shape[0])
+        if path is None:
             return False
         from . import distributed as tdist
 
         x2d = x2d.detach().contiguous()
-        self._x_all = torch.empty((self.world * x2d.shape[0], x2d.shape[1]), device=x2d.device, dtype=x2d.dtype)
-        self._x_work = tdist.all_gather_into_tensor(self._x_all, x2d, group=self.group, async_op=True)
-        self._x_local = x2d  # keep alive until the gather completes
-        self.active = True
+        rows, in_f = x2d.shape
+        if path == "activations":
+            self._x_buf = torch.empty((self.world * rows, in_f), device=x2d.device, dtype=x2d.dtype)
+            self._x_work = tdist.all_gather_into_tensor(self._x_buf, x2d, group=self.group, async_op=True)
+        else:
+            # all-to-all of column shards: rank s receives every rank's rows of shard s
+            bounds = shard_bounds(in_f, self.world)
+            me = tdist.get_rank(self.group)
+            k0, k1 = bounds[me]
+            self._x_buf = torch.empty((self.world, rows, k1 - k0), device=x2d.device, dtype=x2d.dtype)
+            sends = [(x2d[b, a:e], s) for s, (a, e) in enumerate(bounds) if e > a for b in range(rows)]
+            recvs = [(self._x_buf[s, b], s) for s in range(self.world) if k1 > k0 for b in range(rows)]
+            self._x_work = tdist.sendrecv(sends, recvs, group=self.group, async_op=True)
+        self._x_local = x2d  # keep alive until the exchange completes
+        self.active = path
         self._set_skip(True)
         return True
 
@@ -117,18 +177,33 @@ class ActivationExchange:
         if side is None:
             self._finish()
             return
-        # the dy gather queues behind the big x gather on the comm stream: issue both
+        # the dy gather queues behind the big x exchange on the comm stream: issue the
         # waits and the dW GEMM from the side stream so the compute stream runs on
         cur = torch.cuda.current_stream(self._dy.device)
         side.wait_stream(cur)
-        keep = (self._dy, self._x_all, self._x_local)  # used on the side stream
+        keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
         with torch.cuda.stream(side):
             for t in keep:
                 t.record_stream(side)
             self._finish()
 
+    def _targets(self):
+        """(dW, accumulate_w), (db, accumulate_b) — gradients accumulated under no_sync()
+        are averaged first (one all-reduce), this step's exchanged average is added."""
+        from . import distributed as tdist
+
+        out = []
+        for p, view_fn in ((self.weight, self._wview), (self.bias, self._bview)):
+            if p is None:
+                out.append((None, False))
+            elif p.grad is not None:
+                tdist.all_reduce(p.grad, tdist.ReduceOp.AVG, group=self.group)
+                out.append((p.grad, True))
+            else:
+                out.append((view_fn(), False))
+        return out
+
     def _finish(self):
-        from .. import _ext
         from . import distributed as tdist
 
         dy = self._dy
@@ -136,35 +211,42 @@ class ActivationExchange:
         dy_all = torch.empty((self.world * rows, dy.shape[1]), device=dy.device, dtype=dy.dtype)
         tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
         self._x_work.wait()
-        x_all = self._x_all
         scale = 1.0 / self.world
         with torch.no_grad():
-            # gradients accumulated locally under no_sync() are averaged as they are
-            # (one all-reduce), then this step's exchanged average is added
-            grads = []
-            for p, view_fn in ((self.weight, self._wview), (self.bias, self._bview)):
-                if p is None:
-                    grads.append(None)
-                    continue
-                if p.grad is not None:
-                    tdist.all_reduce(p.grad, tdist.ReduceOp.AVG, group=self.group)
-                    grads.append((p.grad, True))
-                else:
-                    grads.append((view_fn(), False))
-            (dw, acc_w) = grads[0]
-            db, acc_b = grads[1] if grads[1] is not None else (None, False)
-            if dy.is_cuda and acc_w == acc_b:
-                _ext.ops().linear_dw(dy_all, x_all, dw, db, scale, acc_w)
+            (dw, acc_w), (db, acc_b) = self._targets()
+            if self.active == "activations":
+                _dw_rows(dy_all, self._x_buf, dw, db, scale, acc_w, acc_b)
             else:
-                upd = torch.mm(dy_all.t(), x_all).mul_(scale)
-                dw.add_(upd) if acc_w else dw.copy_(upd)
-                if db is not None:
-                    s_b = dy_all.sum(0).mul_(scale)
-                    db.add_(s_b) if acc_b else db.copy_(s_b)
+                bounds = shard_bounds(dw.shape[1], self.world)
+                me = tdist.get_rank(self.group)
+                k0, k1 = bounds[me]
+                x_rows = self._x_buf.view(self.world * rows, k1 - k0)
+                _dw_rows(dy_all, x_rows, dw[:, k0:k1], db, scale, acc_w, acc_b)
+                # all-gather of the column shards: N row pieces per peer, straight into dW
+                n_out = dw.shape[0]
+                sends = [(dw[c, k0:k1], s) for s in range(self.world) if s != me and k1 > k0 for c in range(n_out)]
+                recvs = [(dw[c, a:e], s) for s, (a, e) in enumerate(bounds) if s != me and e > a
+                         for c in range(n_out)]
+                w = tdist.sendrecv(sends, recvs, group=self.group, async_op=True)
+                w.wait()
         self.weight.grad = dw
         if self.bias is not None:
             self.bias.grad = db
-        self._x_all = self._x_work = self._dy = self._x_local = None
-        self.active = False
+        self.last_path = "activation-exchange" if self.active == "activations" else "sharded-exchange"
+        self._x_buf = self._x_work = self._dy = self._x_local = None
+        self.active = None
         self.steps_exchanged += 1
-        self.last_path = "activation-exchange"
+
+
+def _dw_rows(dy_all, x_rows, dw, db, scale: float, acc_w: bool, acc_b: bool):
+    """dW (=/+=) scale·dy_allᵀ·x_rows, db (=/+=) scale·Σ dy_all; dw may be a column slice."""
+    from .. import _ext
+
+    if dy_all.is_cuda and (db is None or acc_w == acc_b):
+        _ext.ops().linear_dw(dy_all, x_rows, dw, db, scale, acc_w)
+        return
+    upd = torch.mm(dy_all.t(), x_rows).mul_(scale)
+    dw.add_(upd) if acc_w else dw.copy_(upd)
+    if db is not None:
+        s_b = dy_all.sum(0).mul_(scale)
+        db.add_(s_b) if acc_b else db.copy_(s_b)
