@@ -1,4 +1,5 @@
-"""Numerics of the fused ConvNet plan (NHWC, bf16x3 conv2) vs fp64 PyTorch references."""
+"""Numerics of the fused ConvNet plan (NHWC, bf16x3 convs, pooled-blocked ya/g2m) vs fp64
+PyTorch references of the same ops."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -34,6 +35,33 @@ def pack_hilo(x_nhwc):
 def unpack_hilo(carrier, C):
     b = carrier.contiguous().view(torch.bfloat16)
     return b[..., :C].float() + b[..., C:2 * C].float()
+
+
+def pb_dims(Q):
+    return (Q + 3) // 4, (Q + 7) // 8
+
+
+def pb_to_planar(t, Q):
+    """[B, 32, Q4*Q8*32] pooled-blocked (csrc/kernels/pooled_layout.h) -> [B, 32, Q, Q]."""
+    B = t.shape[0]
+    Q4, Q8 = pb_dims(Q)
+    v = t.reshape(B, 32, Q4, Q8, 4, 8).permute(0, 1, 2, 4, 3, 5).reshape(B, 32, Q4 * 4, Q8 * 8)
+    return v[:, :, :Q, :Q]
+
+
+def planar_to_pb(x):
+    B, C, Q, _ = x.shape
+    Q4, Q8 = pb_dims(Q)
+    pad = torch.zeros(B, C, Q4 * 4, Q8 * 8, dtype=x.dtype, device=x.device)
+    pad[:, :, :Q, :Q] = x
+    return pad.reshape(B, C, Q4, 4, Q8, 8).permute(0, 1, 2, 4, 3, 5).reshape(B, C, Q4 * Q8 * 32).contiguous()
+
+
+def window_extreme(y2_nchw, neg):
+    """per 2x2 window: max (neg False) or min (neg True) per channel; [B,32,Q,Q]"""
+    mx = F.max_pool2d(y2_nchw, 2, 2)
+    mn = -F.max_pool2d(-y2_nchw, 2, 2)
+    return torch.where(neg.view(1, -1, 1, 1), mn, mx)
 
 
 @pytest.mark.parametrize("H", [68, 256, 264])
@@ -76,14 +104,18 @@ def test_layer1_forward(gpu, H):
     _check(gram[625:], S, 2e-6, "S")
 
 
-def test_conv2_forward(gpu):
-    torch.manual_seed(0)
-    B, P = 2, 40
+@pytest.mark.parametrize("P", [40, 38, 37])
+def test_conv2_forward(gpu, P):
+    """y2, the BN2 partial sums, and ya = window max / min of y2 by the sign of gamma2
+    (pooled-blocked), vs fp64; P = 38 gives an odd pooled size, P = 37 an unpooled last row."""
+    torch.manual_seed(P)
+    B = 2
     p = torch.relu(torch.randn(B, P, P, 16, device=gpu))
     w2 = torch.randn(32, 16, 5, 5, device=gpu) * 0.05
     b2 = torch.randn(32, device=gpu)
+    g2 = torch.randn(32, device=gpu)  # mixed signs: max and min windows
     wp, wd = _ops().conv2_pack(w2)
-    y2, partial = _ops().fused_conv2_forward(pack_hilo(p), wp, b2)
+    y2, partial, ya = _ops().fused_conv2_forward(pack_hilo(p), wp, b2, g2)
     ref = F.conv2d(p.permute(0, 3, 1, 2).double().cpu(), w2.double().cpu(), b2.double().cpu(), padding=2)
     _check(y2.permute(0, 3, 1, 2), ref, 5e-5, "y2")
     # BN2 partials: sum over workgroups of (sum, sumsq) of y2 - b2
@@ -91,97 +123,101 @@ def test_conv2_forward(gpu):
     yc = ref - b2.double().cpu().view(1, 32, 1, 1)
     _check(s[:, 0], yc.sum((0, 2, 3)), 1e-4, "sum")
     _check(s[:, 1], (yc * yc).sum((0, 2, 3)), 1e-4, "sumsq")
+    # ya: extremes of the kernel's own y2 (exact selection, no rounding involved)
+    Q = P // 2
+    want = window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q].float(), (g2 < 0))
+    got = pb_to_planar(ya, Q)
+    assert torch.equal(got, want), (got - want).abs().max()
 
 
-@pytest.mark.parametrize("P", [64, 128, 200])
-def test_head_fwd_bwd(gpu, P):
-    """BN2(batch stats) + ReLU + pool + fc forward/backward, incl. the dy2 build, vs fp64 autograd."""
-    torch.manual_seed(P)
-    B, NC = 3, 10
+def _head_case(gpu, P, B, seed):
+    torch.manual_seed(seed)
+    NC = 10
     Q = P // 2
     y2 = torch.randn(B, P, P, 32, device=gpu)
     b2 = torch.randn(32, device=gpu) * 0.1
-    g2 = torch.rand(32, device=gpu) + 0.5
+    g2 = torch.randn(32, device=gpu)  # negative gammas exercise the min windows
     be2 = torch.randn(32, device=gpu) * 0.1
     wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
     bfc = torch.randn(NC, device=gpu)
     yc = (y2 - b2).double()
     partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()  # [32][1][2]
-    logits, stats2, aff2 = _ops().fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc)
+    ya = planar_to_pb(window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q], g2 < 0))
+    return y2, b2, g2, be2, wfc, bfc, partial2, ya
+
+
+@pytest.mark.parametrize("P,B", [(64, 3), (200, 5), (38, 2), (130, 11)])
+def test_head_forward_backward(gpu, P, B):
+    """BN2(batch stats) + ReLU + pool + fc forward/backward over ya vs fp64 autograd: logits,
+    dW, dgamma2, dbeta2, g2m (the ReLU-masked pooled gradient, pooled-blocked) and the fused SGD
+    step.  P = 38: odd pooled size (rows 1, 3, ... start off the 16-B grid); B = 11: two image
+    passes."""
+    y2, b2, g2, be2, wfc, bfc, partial2, ya = _head_case(gpu, P, B, P + B)
+    Q, NC = P // 2, wfc.shape[0]
+    ops = _ops()
+    xo = torch.empty(B, 32 * Q * Q, device=gpu)
+    logits, stats2, aff2 = ops.fused_head_forward(ya, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, P,
+                                                  xo)
     yr = y2.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
     gr = g2.double().cpu().requires_grad_(True)
     ber = be2.double().cpu().requires_grad_(True)
     wr = wfc.double().cpu().requires_grad_(True)
     z = F.batch_norm(yr, None, None, gr, ber, True, 0.1, 1e-5)
     pz = F.max_pool2d(F.relu(z), 2, 2)
+    pz.retain_grad()
     ref = F.linear(pz.reshape(B, -1), wr, bfc.double().cpu())
     _check(logits, ref, 1e-5, "logits")
+    _check(xo.view(B, 32, Q, Q), pz, 1e-5, "x_out (fc input rows)")
     dl = torch.randn(B, NC, device=gpu)
     ref.backward(dl.double().cpu())
-    dW, dbfc, dg2, dbe2, dy2 = _ops().fused_head_backward(dl, y2, stats2, aff2, g2, wfc, None, 1.0)
+    dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, True)
+    assert g2m.shape == (B, 32, Q, Q)
     _check(dW, wr.grad, 1e-5, "dW")
+    _check(dbfc, dl.double().sum(0), 1e-6, "dbfc")
     _check(dg2, gr.grad, 1e-5, "dgamma2")
     _check(dbe2, ber.grad, 1e-5, "dbeta2")
-    _check(unpack_hilo(dy2, 32).permute(0, 3, 1, 2), yr.grad, 1e-4, "dy2")
+    mask = (pz > 0).double()
+    _check(g2m, pz.grad * mask, 1e-5, "g2m")
+    # no-dW form (activation exchange) leaves the same g2m / BN2 gradients
+    _, _, dg2b, dbe2b, g2mb, kbufb = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, False)
+    assert torch.equal(g2mb, g2m) and torch.equal(kbufb, kbuf) and torch.equal(dg2b, dg2)
+    if B <= 8:
+        # SGD step fused into the backward: W <- W - lr dW (in place), dW still written
+        w0 = wfc.clone()
+        dW2 = torch.empty_like(wfc)
+        ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, dW2, 1.0, True, 0.5)
+        assert torch.equal(dW2, dW)
+        assert torch.allclose(wfc, w0 - 0.5 * dW, rtol=0, atol=1e-6)
 
 
-@pytest.mark.parametrize("P", [64, 130])
-def test_head_backward_from_saved_argmax(gpu, P):
-    """head backward from the saved argmax values ya (head_bwd_ya_kernel) == the y2 path,
-    and dW / dgamma / dbeta vs fp64 autograd."""
-    torch.manual_seed(P + 1)
-    B, NC = 5, 10
-    Q = P // 2
-    ops = _ops()
-    y2 = torch.randn(B, P, P, 32, device=gpu)
-    b2 = torch.randn(32, device=gpu) * 0.1
-    g2 = torch.rand(32, device=gpu) + 0.5
-    be2 = torch.randn(32, device=gpu) * 0.1
-    wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
-    bfc = torch.randn(NC, device=gpu)
-    yc = (y2 - b2).double()
-    partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()
-    ya = torch.empty(B, 32 * Q * Q, device=gpu)
-    logits, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc,
-                                                  None, ya)
-    # ya is y2 at the window argmax of the BN2 output: relu(a*ya + b) is the pooled activation
-    yr = y2.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
-    gr = g2.double().cpu().requires_grad_(True)
-    ber = be2.double().cpu().requires_grad_(True)
-    wr = wfc.double().cpu().requires_grad_(True)
-    z = F.batch_norm(yr, None, None, gr, ber, True, 0.1, 1e-5)
-    pz = F.max_pool2d(F.relu(z), 2, 2)
-    a, b = aff2[:32].double().cpu(), aff2[32:].double().cpu()
-    p_from_ya = torch.relu(a.view(1, 32, 1, 1) * ya.view(B, 32, Q, Q).double().cpu() + b.view(1, 32, 1, 1))
-    _check(p_from_ya, pz, 1e-5, "relu(a*ya+b) vs pooled")
-    ref = F.linear(pz.reshape(B, -1), wr, bfc.double().cpu())
-    dl = torch.randn(B, NC, device=gpu)
-    ref.backward(dl.double().cpu())
-    r_y2 = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, None, 1.0, True)
-    r_ya = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, None, 1.0, True, ya)
-    for name, u, v in zip(("dW", "dbfc", "dgamma2", "dbeta2", "g2m", "kbuf"), r_ya, r_y2):
-        _check(u, v, 1e-6, name + " (ya vs y2 path)")
-    _check(r_ya[0], wr.grad, 1e-5, "dW")
-    _check(r_ya[2], gr.grad, 1e-5, "dgamma2")
-    _check(r_ya[3], ber.grad, 1e-5, "dbeta2")
-
-
-@pytest.mark.parametrize("P", [40, 37, 128, 200])
-def test_conv2_backward(gpu, P):
-    torch.manual_seed(0)
+@pytest.mark.parametrize("P", [37, 40, 130])
+def test_conv2_backward_fused_with_bn2_pool(gpu, P):
+    """fused_conv2_backward_y2 (dy2 rebuilt in LDS from y2 + g2m + the BN2 constants) vs the fp64
+    chain BN2 -> ReLU -> pool -> fc backward -> conv2 data and weight gradients."""
     B = 2
+    y2, b2, g2, be2, wfc, bfc, partial2, ya = _head_case(gpu, P, B, 7 * P)
+    ops = _ops()
+    _, stats2, aff2 = ops.fused_head_forward(ya, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, P)
+    dl = torch.randn(B, wfc.shape[0], device=gpu)
+    _, _, _, _, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, True)
     p = torch.relu(torch.randn(B, P, P, 16, device=gpu))
     w2 = torch.randn(32, 16, 5, 5, device=gpu) * 0.05
-    dy = torch.randn(B, P, P, 32, device=gpu)
-    wp, wd = _ops().conv2_pack(w2)
-    dp1, dw2, db2 = _ops().fused_conv2_backward(pack_hilo(dy), pack_hilo(p), wd, True, 1.0)
+    _, wd = ops.conv2_pack(w2)
+    dp1, dw2, db2 = ops.fused_conv2_backward_y2(y2, g2m, aff2, kbuf, pack_hilo(p), wd, 1.0)
+    # fp64 reference: dy2 from the head chain, then the conv2 backward with that dy2
+    yr = y2.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
+    z = F.batch_norm(yr, None, None, g2.double().cpu(), be2.double().cpu(), True, 0.1, 1e-5)
+    pz = F.max_pool2d(F.relu(z), 2, 2)
+    F.linear(pz.reshape(B, -1), wfc.double().cpu(), bfc.double().cpu()).backward(dl.double().cpu())
+    dy2 = yr.grad
     pr = p.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
     wr = w2.double().cpu().requires_grad_(True)
     br = torch.zeros(32, dtype=torch.float64, requires_grad=True)
-    F.conv2d(pr, wr, br, padding=2).backward(dy.permute(0, 3, 1, 2).double().cpu())
+    F.conv2d(pr, wr, br, padding=2).backward(dy2)
     _check(dp1.permute(0, 3, 1, 2), pr.grad, 5e-5, "dp1")
     _check(dw2, wr.grad, 5e-5, "dw2")
-    _check(db2, br.grad, 5e-5, "db2")
+    # conv bias before BN: sum(dy2) is analytically zero, both sides are rounding noise
+    assert (db2.double().cpu() - br.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item()
 
 
 def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
@@ -203,6 +239,8 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
 
     torch.manual_seed(0)
     ours = ConvNet(image_shape=(H, H), mode="fused")
+    with torch.no_grad():
+        ours.layer2[1].weight[::3].neg_()  # some negative BN2 gammas: min-pooled windows
     ref = Ref(fc_in_features((H, H))).double()
     ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in ours.state_dict().items()})
     ours = ours.to(gpu)
@@ -245,7 +283,7 @@ def test_fused_model_matches_reference(gpu):
 
 
 def test_fused_model_matches_reference_odd_pool(gpu):
-    # P = 38 (not a multiple of the 32-column conv2 tile), Q = 19
+    # P = 38 (not a multiple of the 16-column conv2 tile), Q = 19 (odd: scalar fc-weight path)
     _fused_vs_ref(gpu, B=2, H=76, steps=1)
 
 
@@ -263,33 +301,15 @@ def test_fused_grads_land_in_ddp_bucket(gpu):
     assert m.fc.weight.grad.data_ptr() == v.data_ptr()
 
 
-@pytest.mark.parametrize("P", [37, 40, 130])
-def test_conv2_backward_fused_with_bn2_pool(gpu, P):
-    """fused_conv2_backward_y2 (dy2 rebuilt in LDS from y2 + g2m) vs the unfused path
-    (dy2_build -> dy2 in HBM -> conv2 dgrad + wgrad)."""
-    torch.manual_seed(P)
-    B, NC = 2, 10
-    Q = P // 2
+def test_bad_launch_raises(gpu):
+    """A launch the hardware refuses (dynamic LDS above 160 KiB, a 2048-thread block) surfaces
+    as a Python exception from the op, and the next good launch is unaffected."""
     ops = _ops()
-    y2 = torch.randn(B, P, P, 32, device=gpu)
-    b2 = torch.randn(32, device=gpu) * 0.1
-    g2 = torch.rand(32, device=gpu) + 0.5
-    be2 = torch.randn(32, device=gpu) * 0.1
-    wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
-    bfc = torch.randn(NC, device=gpu)
-    yc = (y2 - b2).double()
-    partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()
-    _, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc)
-    dl = torch.randn(B, NC, device=gpu)
-    _, _, _, _, dy2 = ops.fused_head_backward(dl, y2, stats2, aff2, g2, wfc, None, 1.0)
-    _, _, _, _, g2m, kbuf = ops.fused_head_backward_g2m(dl, y2, stats2, aff2, g2, wfc, None, 1.0)
-    p = torch.relu(torch.randn(B, P, P, 16, device=gpu))
-    w2 = torch.randn(32, 16, 5, 5, device=gpu) * 0.05
-    _, wd = ops.conv2_pack(w2)
-    p1 = pack_hilo(p)
-    dp1_r, dw2_r, db2_r = ops.fused_conv2_backward(dy2, p1, wd, True, 1.0)
-    dp1, dw2, db2 = ops.fused_conv2_backward_y2(y2, g2m, aff2, kbuf, p1, wd, 1.0)
-    _check(dp1, dp1_r, 1e-6, "dp1")
-    _check(dw2, dw2_r, 1e-5, "dw2")
-    # conv bias before BN: sum(dy2) is analytically zero, both sides are rounding noise
-    assert (db2 - db2_r).abs().max().item() <= 1e-4 * dw2_r.abs().max().item()
+    like = torch.empty(1, device=gpu)
+    ops.launch_probe(like, 4096, 256)
+    with pytest.raises(RuntimeError, match="launch"):
+        ops.launch_probe(like, 200 * 1024, 256)
+    with pytest.raises(RuntimeError, match="launch"):
+        ops.launch_probe(like, 0, 2048)
+    ops.launch_probe(like, 1024, 64)
+    torch.cuda.synchronize()

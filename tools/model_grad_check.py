@@ -1,6 +1,6 @@
 """Model vs fp64 reference (tests/test_model_gpu.py setup) reporting EVERY parameter's relative
 gradient error per step (the test stops at the first).  Env switches pass through, so the
-same script A/Bs kernel variants: TDS_CONV2_BWD=2, TDS_L1_BWD=1, TDS_HEAD_BWD_NW=8 ...
+(kernel variant A/B switches were removed; a -DTDS_DIAG build keeps the timing-only conv2 variants)
 Usage: python tools/model_grad_check.py [H] [B] [steps]"""
 import os
 import sys

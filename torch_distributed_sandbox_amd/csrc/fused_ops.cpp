@@ -4,18 +4,25 @@
 // to autograd as float32 tensors of the same byte size, so that gradients line
 // up shape-for-shape:
 //   p1 carrier  [B,P,P,16] f32  == bytes of bf16 [B,P,P,32] (hi16|lo16)   <-> dp1  [B,P,P,16] f32
-//   y2          [B,P,P,32] f32                                           <-> dy2 carrier [B,P,P,32] f32
-//                                                                            == bytes of bf16 [B,P,P,64]
+//   y2          [B,P,P,32] f32
+//   ya          [B,32,PB] f32: pooled-blocked planes (kernels/pooled_layout.h)
+//   g2m         [B,32,Q,Q] f32: planar pooled gradient
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <map>
+#include <mutex>
+#include <tuple>
+
 #include "kernels/launchers.h"
+#include "launch_check.h"
 
 namespace {
 
 using at::Tensor;
+using tds_bind::check_launches;
 
 hipStream_t stream_of(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
@@ -48,6 +55,26 @@ Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shap
 
 int l1_wg() { return tds_fused_num_wg(4); }
 
+// Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
+// torch caching allocator, built once.  The map is never destroyed (no frees at process exit).
+const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c) {
+  static std::mutex mu;
+  static auto* cache = new std::map<std::tuple<int, int, int, int>, Tensor>();
+  const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache->find(key);
+  if (it != cache->end()) return it->second.data_ptr<int>();
+  auto host = at::empty({(int64_t)B * tiles_r * tiles_c}, at::TensorOptions().dtype(at::kInt));
+  const int rc = tds_tile_order_fill(host.data_ptr<int>(), B, tiles_r, tiles_c);
+  TORCH_CHECK(rc == 0, "tdsa fused: tile order table needs B <= 255 and <= 4095 tiles per side (B=", B,
+              ", tiles ", tiles_r, " x ", tiles_c, ")");
+  Tensor dev = host.to(like.device());
+  (*cache)[key] = dev;
+  return dev.data_ptr<int>();
+}
+
+int64_t pb_plane(int64_t P) { return tds_pb_plane((int)(P / 2)); }
+
 // ---------------------------------------------------------------- layer 1 forward
 // returns (p1 carrier, idx1, stats1[mean16|invstd16], ac_partial, strips)
 std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
@@ -77,7 +104,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   // x autocorrelation + border strips -> Gram G / patch sums S -> BN1 statistics in closed form
   // one thread per 4 x 8 pixel block: each fp32 partial covers 32 products (fp64 beyond)
   const int nac = tds_x_autocorr_num_wg((int)B, (int)H, (int)W);
-  TORCH_CHECK(nac > 0, "fused_l1_forward: x must be < 2 GiB with W % 4 == 0 (autocorrelation kernel)");
+  TORCH_CHECK(nac > 0, "fused_l1_forward: W % 4 == 0 required (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo.dtype(at::kDouble));
   auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
   tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
@@ -97,6 +124,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
   tds_l1_apply(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(), p1.data_ptr(),
                idx1.data_ptr<uint8_t>(), l1_wg(), (int)B, (int)H, (int)W, st);
+  check_launches("fused_l1_forward");
   return {p1, idx1, stats, gram};
 }
 
@@ -107,35 +135,46 @@ std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2) {
   auto wp = at::empty({2 * 13 * 2 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
   auto wd = at::empty({2 * 25 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
   tds_conv2_pack_weights(w2.data_ptr<float>(), wp.data_ptr<int16_t>(), wd.data_ptr<int16_t>(), stream_of(w2));
+  check_launches("conv2_pack");
   return {wp, wd};
 }
 
-std::tuple<Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& wp, const Tensor& b2) {
+// returns (y2 [B,P,P,32], BN2 partials, ya [B,32,PB]: y2 at each 2x2 window's argmax of the BN2
+// output, resolved by the sign of gamma2)
+std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& wp, const Tensor& b2,
+                                                       const c10::optional<Tensor>& gamma2) {
   TORCH_CHECK(p1.dim() == 4 && p1.size(1) == p1.size(2) && p1.size(3) == 16, "fused_conv2_forward: p1 carrier");
   const int64_t B = p1.size(0), P = p1.size(1);
   need(p1, at::kFloat, {B, P, P, 16}, "p1");
   need(wp, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
   need(b2, at::kFloat, {32}, "conv2.bias");
-  TORCH_CHECK(B <= 255 && P <= 32760, "fused_conv2_forward: batch <= 255 and P <= 32760 (tile-order table packing)");
+  const float* g = optf(gamma2, 32, "bn2.weight");
+  TORCH_CHECK(B <= 255 && P >= 2, "fused_conv2_forward: 1 <= batch <= 255 and P >= 2");
   c10::DeviceGuard guard(p1.device());
-  const int nwg = tds_conv2_fwd_num_wg();
+  const int nwg = tds_conv2_fwd2_num_wg();
+  int tr = 0, tc = 0;
+  tds_conv2_fwd2_tiles((int)P, &tr, &tc);
+  const int* order = tile_order(p1, (int)B, tr, tc);
   auto y2 = at::empty({B, P, P, 32}, p1.options());
+  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options());
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
-  tds_conv2_fwd_bf16x3(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), y2.data_ptr<float>(),
-                       partial.data_ptr<double>(), nwg, (int)B, (int)P, stream_of(p1));
-  return {y2, partial};
+  tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr<float>(),
+                 ya.data_ptr<float>(), partial.data_ptr<double>(), order, nwg, (int)B, (int)P, stream_of(p1));
+  check_launches("fused_conv2_forward");
+  return {y2, partial, ya};
 }
 
 // ---------------------------------------------------------------- head forward (BN2 finalize + fc)
 // returns (logits, stats2 [mean32|invstd32], aff2 [a32|b32])
 std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
-    const Tensor& y2, const Tensor& partial2, const Tensor& b2, const c10::optional<Tensor>& gamma2,
+    const Tensor& ya, const Tensor& partial2, const Tensor& b2, const c10::optional<Tensor>& gamma2,
     const c10::optional<Tensor>& beta2, const c10::optional<Tensor>& rm2, const c10::optional<Tensor>& rv2,
     const c10::optional<Tensor>& nbt2, double momentum, double eps, const Tensor& wfc, const c10::optional<Tensor>& bfc,
-    const c10::optional<Tensor>& x_out, const c10::optional<Tensor>& ya_out) {
-  TORCH_CHECK(y2.dim() == 4 && y2.size(3) == 32 && y2.size(1) == y2.size(2), "fused_head_forward: y2");
-  const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
-  need(y2, at::kFloat, {B, P, P, 32}, "y2");
+    int64_t P, const c10::optional<Tensor>& x_out) {
+  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward: ya must be [B,32,PB]");
+  const int64_t B = ya.size(0), Q = P / 2;
+  TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_forward: needs P/2 >= 4 pooled columns and B >= 1");
+  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
   TORCH_CHECK(partial2.is_cuda() && partial2.scalar_type() == at::kDouble && partial2.numel() % 64 == 0, "partial2");
   const int nch = (int)(partial2.numel() / 64);
   need(b2, at::kFloat, {32}, "conv2.bias");
@@ -148,7 +187,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
     TORCH_CHECK(nbt2->is_cuda() && nbt2->scalar_type() == at::kLong && nbt2->numel() == 1, "bn2.num_batches_tracked");
     nb = nbt2->data_ptr<int64_t>();
   }
-  TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) <= 10, "fc.weight must be [<=10, 32*Q*Q]");
+  TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
+              "fc.weight must be [<=10, 32*Q*Q]");
   const int64_t NC = wfc.size(0);
   need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
   const float* bf = optf(bfc, NC, "fc.bias");
@@ -157,176 +197,120 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
     need(*x_out, at::kFloat, {B, 32 * Q * Q}, "x_out (fc input rows)");
     xo = x_out->data_ptr<float>();
   }
-  float* yo = nullptr;
-  if (ya_out.has_value() && ya_out->defined()) {
-    need(*ya_out, at::kFloat, {B, 32 * Q * Q}, "ya_out (y2 at the pooling argmax)");
-    yo = ya_out->data_ptr<float>();
-  }
-  c10::DeviceGuard guard(y2.device());
-  hipStream_t st = stream_of(y2);
-  auto sums2 = at::empty({64}, y2.options().dtype(at::kDouble));
+  c10::DeviceGuard guard(ya.device());
+  hipStream_t st = stream_of(ya);
+  auto sums2 = at::empty({64}, ya.options().dtype(at::kDouble));
   tds_reduce_partials(partial2.data_ptr<double>(), sums2.data_ptr<double>(), 64, nch, 2, (int64_t)nch * 2, 2, st);
-  auto stats = at::empty({64}, y2.options());
-  auto aff = at::empty({64}, y2.options());
+  auto stats = at::empty({64}, ya.options());
+  auto aff = at::empty({64}, ya.options());
   tds_bn_finalize_shifted(sums2.data_ptr<double>(), 32, 1, B * P * P, b2.data_ptr<float>(), (float)eps,
                           (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
-  const int nblk = tds_head_fwd_nblk((int)Q);
-  auto part = at::empty({(int64_t)nblk * B * NC}, y2.options().dtype(at::kDouble));
-  auto lsum = at::empty({B * NC}, y2.options().dtype(at::kDouble));
-  auto logits = at::empty({B, NC}, y2.options());
-  const int rc = tds_head_fwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
-                              part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, yo, (int)B,
-                              (int)P, (int)NC, st);
-  TORCH_CHECK(rc == 0, "fused_head_forward: unsupported B/NC");
+  const int nblk = 32 * tds_head_pb_nblk((int)Q);
+  auto part = at::empty({(int64_t)nblk * B * NC}, ya.options().dtype(at::kDouble));
+  auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
+  auto logits = at::empty({B, NC}, ya.options());
+  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
+                                 part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
+                                 (int)Q, (int)NC, st);
+  TORCH_CHECK(rc == 0, "fused_head_forward: unsupported shape");
+  check_launches("fused_head_forward");
   return {logits, stats, aff};
 }
 
 // ---------------------------------------------------------------- head backward
-struct HeadBwd {
-  Tensor dW, dbfc, dgamma, dbeta, g2m, kbuf;
-};
-
-// fc / pool2 / ReLU / BN2 backward up to the pooled gradient g2m and the BN2 backward
-// constants kbuf = [k1|k2|k3] (dy2 = k1*dz + k2*y2 + k3)
-static HeadBwd head_backward_core(const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
-                                  const c10::optional<Tensor>& gamma2, const Tensor& wfc,
-                                  const c10::optional<Tensor>& dw_out, double scale, bool compute_dw,
-                                  const c10::optional<Tensor>& ya = c10::nullopt, double update_lr = 0.0,
-                                  const c10::optional<Tensor>& dbfc_out = c10::nullopt,
-                                  const c10::optional<Tensor>& dg_out = c10::nullopt,
-                                  const c10::optional<Tensor>& dbe_out = c10::nullopt) {
-  const int64_t B = y2.size(0), P = y2.size(1), Q = P / 2;
-  need(y2, at::kFloat, {B, P, P, 32}, "y2");
+// fc / pool / ReLU / BN2 backward up to the pooled gradient g2m and the BN2 backward constants
+// kbuf = [k1|k2|k3] (dy2 = k1*dz + k2*y2 + k3, rebuilt tile by tile inside the conv2 backward).
+// update_lr > 0: the plain-SGD step of fc.weight runs in the same pass (W -= lr * dW).
+// returns (dW [into dw_out if given; empty when !compute_dw], db_fc, dgamma2, dbeta2, g2m, kbuf)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
+    const Tensor& dlogits, const Tensor& ya, const Tensor& stats2, const Tensor& aff2,
+    const c10::optional<Tensor>& gamma2, const Tensor& wfc, int64_t P, const c10::optional<Tensor>& dw_out,
+    double scale, bool compute_dw, double update_lr, const c10::optional<Tensor>& dbfc_out,
+    const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out) {
+  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_backward: ya must be [B,32,PB]");
+  const int64_t B = ya.size(0), Q = P / 2;
+  TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_backward: needs P/2 >= 4 pooled columns and B >= 1");
+  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
   const int64_t NC = wfc.size(0);
   need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
   need(dlogits, at::kFloat, {B, NC}, "dlogits");
   need(stats2, at::kFloat, {64}, "stats2");
   need(aff2, at::kFloat, {64}, "aff2");
   const float* g = optf(gamma2, 32, "bn2.weight");
-  hipStream_t st = stream_of(y2);
-  HeadBwd r;
+  c10::DeviceGuard guard(ya.device());
+  hipStream_t st = stream_of(ya);
+  Tensor dW;
   if (!compute_dw) {
-    r.dW = at::empty({0}, wfc.options());
+    dW = at::empty({0}, wfc.options());
   } else if (dw_out.has_value() && dw_out->defined()) {
     need(*dw_out, at::kFloat, {NC, 32 * Q * Q}, "dW_out");
-    r.dW = *dw_out;
+    dW = *dw_out;
   } else {
-    r.dW = at::empty_like(wfc);
+    dW = at::empty_like(wfc);
   }
-  r.g2m = at::empty({B, 32, Q, Q}, y2.options());  // planar (fc flatten order)
-  const bool use_ya = ya.has_value() && ya->defined() && tds_head_bwd_ya_supported((int)B, (int)P, (int)NC);
-  int nblk = use_ya ? tds_head_bwd_ya_nblk((int)B, (int)P, (int)NC) : tds_head_bwd_nblk((int)Q);
-  auto partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
-  int rc;
-  rc = -1;
-  if (use_ya) {
-    // saved argmax values: stream ya (B*32*Q*Q floats) instead of y2
-    need(*ya, at::kFloat, {B, 32 * Q * Q}, "ya");
-    // update_lr > 0: also apply SGD to wfc in place (optimizer step fused into the backward)
-    rc = tds_head_bwd_ya(ya->data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
-                         dlogits.data_ptr<float>(), compute_dw ? r.dW.data_ptr<float>() : nullptr,
-                         r.g2m.data_ptr<float>(), partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale,
-                         (update_lr > 0.0 && compute_dw) ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr,
-                         (float)update_lr, st);
-  }
-  TORCH_CHECK(update_lr <= 0.0 || (use_ya && rc == 0 && compute_dw),
-              "fused_head_backward_g2m: update_lr needs the saved-argmax (ya) path with compute_dw");
-  if (rc != 0) {
-    if (nblk != tds_head_bwd_nblk((int)Q)) {
-      nblk = tds_head_bwd_nblk((int)Q);
-      partial = at::empty({(int64_t)32 * nblk * 2}, y2.options().dtype(at::kDouble));
-    }
-    rc = tds_head_bwd(y2.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(), dlogits.data_ptr<float>(),
-                      compute_dw ? r.dW.data_ptr<float>() : nullptr, r.g2m.data_ptr<float>(),
-                      partial.data_ptr<double>(), (int)B, (int)P, (int)NC, (float)scale, st);
-  }
-  TORCH_CHECK(rc == 0, "fused_head_backward: unsupported B/NC");
-  auto sums = at::empty({64}, y2.options().dtype(at::kDouble));
-  tds_reduce_partials(partial.data_ptr<double>(), sums.data_ptr<double>(), 64, nblk, 2, (int64_t)nblk * 2, 2, st);
-  r.dgamma = sink_or_empty(dg_out, {32}, y2, "dgamma2_out");
-  r.dbeta = sink_or_empty(dbe_out, {32}, y2, "dbeta2_out");
-  r.kbuf = at::empty({96}, y2.options());
-  tds_bn_bwd_finalize2(sums.data_ptr<double>(), 32, 1, B * P * P, g, stats2.data_ptr<float>(),
-                       r.dgamma.data_ptr<float>(), r.dbeta.data_ptr<float>(), r.kbuf.data_ptr<float>(), st);
-  r.dbfc = sink_or_empty(dbfc_out, {NC}, y2, "dbfc_out");
-  at::sum_out(r.dbfc, dlogits, {0});
-  if (scale != 1.0) r.dbfc.mul_(scale);
-  return r;
-}
-
-// returns (dW [written into dw_out if given; empty when !compute_dw], db_fc, dgamma2, dbeta2, dy2 carrier)
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
-    const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
-    const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
-    bool compute_dw) {
-  c10::DeviceGuard guard(y2.device());
-  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw);
-  const int64_t B = y2.size(0), P = y2.size(1);
-  auto dy2 = at::empty({B, P, P, 32}, y2.options());  // carrier of bf16 [B,P,P,64]
-  tds_dy2_build(y2.data_ptr<float>(), r.g2m.data_ptr<float>(), aff2.data_ptr<float>(), r.kbuf.data_ptr<float>(),
-                dy2.data_ptr(), (int)B, (int)P, stream_of(y2));
-  return {r.dW, r.dbfc, r.dgamma, r.dbeta, dy2};
-}
-
-// Head backward up to the pooled gradient: returns (dW, db_fc, dgamma2, dbeta2, g2m, kbuf).
-// The conv2 backward then runs fused with the BN2/pool backward (fused_conv2_backward_y2),
-// so dy2 is never materialised.
-std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward_g2m(
-    const Tensor& dlogits, const Tensor& y2, const Tensor& stats2, const Tensor& aff2,
-    const c10::optional<Tensor>& gamma2, const Tensor& wfc, const c10::optional<Tensor>& dw_out, double scale,
-    bool compute_dw, const c10::optional<Tensor>& ya, double update_lr, const c10::optional<Tensor>& dbfc_out,
-    const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out) {
-  c10::DeviceGuard guard(y2.device());
-  HeadBwd r = head_backward_core(dlogits, y2, stats2, aff2, gamma2, wfc, dw_out, scale, compute_dw, ya, update_lr,
-                                 dbfc_out, dg_out, dbe_out);
-  return {r.dW, r.dbfc, r.dgamma, r.dbeta, r.g2m, r.kbuf};
+  const bool upd = update_lr > 0.0;
+  TORCH_CHECK(!upd || (compute_dw && tds_head_bwd_pb_npass((int)B) == 1),
+              "fused_head_backward: update_lr needs compute_dw and a batch of <= 8 images");
+  auto g2m = at::empty({B, 32, Q, Q}, ya.options());  // planar (the fc flatten order)
+  const int nblk = tds_head_pb_nblk((int)Q), npass = tds_head_bwd_pb_npass((int)B);
+  auto partial = at::empty({(int64_t)32 * npass * nblk * 2}, ya.options().dtype(at::kDouble));
+  const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
+                                 dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
+                                 compute_dw ? dW.data_ptr<float>() : nullptr,
+                                 upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
+                                 (float)scale, (float)update_lr, st);
+  TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
+  auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
+  auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");
+  auto kbuf = at::empty({96}, ya.options());
+  tds_bn_bwd_finalize2(partial.data_ptr<double>(), 32, npass * nblk, B * P * P, g, stats2.data_ptr<float>(),
+                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), st);
+  auto dbfc = sink_or_empty(dbfc_out, {NC}, ya, "dbfc_out");
+  at::sum_out(dbfc, dlogits, {0});
+  if (scale != 1.0) dbfc.mul_(scale);
+  check_launches("fused_head_backward");
+  return {dW, dbfc, dgamma, dbeta, g2m, kbuf};
 }
 
 // ---------------------------------------------------------------- conv2 backward
-std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward(const Tensor& dy2, const Tensor& p1, const Tensor& wd,
-                                                        bool need_dp1, double scale) {
-  const int64_t B = p1.size(0), P = p1.size(1);
-  need(p1, at::kFloat, {B, P, P, 16}, "p1");
-  need(dy2, at::kFloat, {B, P, P, 32}, "dy2 carrier");
-  need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
-  c10::DeviceGuard guard(p1.device());
-  hipStream_t st = stream_of(p1);
-  const int nwg = tds_conv2_num_wg();
-  Tensor dp1 = need_dp1 ? at::empty({B, P, P, 16}, p1.options()) : at::empty({0}, p1.options());
-  if (need_dp1) tds_conv2_dgrad_bf16x3(dy2.data_ptr(), wd.data_ptr<int16_t>(), dp1.data_ptr<float>(), nwg, (int)B,
-                                       (int)P, st);
-  auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options());
-  auto dw2 = at::empty({32, 16, 5, 5}, p1.options());
-  auto db2 = at::empty({32}, p1.options());
-  tds_conv2_wgrad_bf16x3(dy2.data_ptr(), p1.data_ptr(), slab.data_ptr<float>(), dw2.data_ptr<float>(),
-                         db2.data_ptr<float>(), (float)scale, nwg, (int)B, (int)P, st);
-  return {dp1, dw2, db2};
-}
-
 // BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2, g2m, aff2, kbuf, p1) -> (dp1, dw2, db2)
 std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& g2m, const Tensor& aff2,
                                                            const Tensor& kbuf, const Tensor& p1, const Tensor& wd,
                                                            double scale, const c10::optional<Tensor>& dw_out,
                                                            const c10::optional<Tensor>& db_out) {
-  const int64_t B = p1.size(0), P = p1.size(1), Q = P / 2;
+  const int64_t B = p1.size(0), P = p1.size(1);
   need(p1, at::kFloat, {B, P, P, 16}, "p1");
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
-  need(g2m, at::kFloat, {B, 32, Q, Q}, "g2m");
+  need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
   need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
-  TORCH_CHECK(B <= 255 && P <= 32760, "fused_conv2_backward_y2: batch <= 255 and P <= 32760 (tile-order table packing)");
+  TORCH_CHECK(B <= 255 && P >= 2, "fused_conv2_backward_y2: 1 <= batch <= 255 and P >= 2");
   c10::DeviceGuard guard(p1.device());
   hipStream_t st = stream_of(p1);
-  const int nwg = tds_conv2_bwd_fused_num_wg();
+  const int nwg = tds_conv2_bwd3_num_wg();
+  int tr = 0, tc = 0;
+  tds_conv2_bwd3_tiles((int)P, &tr, &tc);
+  const int* order = tile_order(p1, (int)B, tr, tc);
   auto dp1 = at::empty({B, P, P, 16}, p1.options());
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options());
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
-  tds_conv2_bwd_fused(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
-                      p1.data_ptr(), wd.data_ptr<int16_t>(), dp1.data_ptr<float>(), slab.data_ptr<float>(),
-                      dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, nwg, (int)B, (int)P, st);
+  tds_conv2_bwd3(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
+                 p1.data_ptr(), wd.data_ptr<int16_t>(), dp1.data_ptr<float>(), slab.data_ptr<float>(), order, nwg,
+                 (int)B, (int)P, st);
+  tds_conv2_wgrad_reduce(slab.data_ptr<float>(), nwg, dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, st);
+  check_launches("fused_conv2_backward_y2");
   return {dp1, dw2, db2};
+}
+
+// test hook: one launch of a trivial kernel with the given dynamic LDS / block size (a request
+// beyond the hardware limits must surface as an exception through check_launches)
+void launch_probe(const Tensor& like, int64_t lds_bytes, int64_t threads) {
+  TORCH_CHECK(like.is_cuda(), "launch_probe: needs a GPU tensor");
+  c10::DeviceGuard guard(like.device());
+  tds_launch_probe(nullptr, (int)lds_bytes, (int)threads, stream_of(like));
+  check_launches("launch_probe");
 }
 
 // ---------------------------------------------------------------- layer 1 backward
@@ -364,6 +348,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   tds_l1_finalize(bsum.data_ptr<double>(), gram.data_ptr<double>(), B * H * W, w1.data_ptr<float>(),
                   b1.data_ptr<float>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(), db1.data_ptr<float>(),
                   dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale, st);
+  check_launches("fused_l1_backward");
   return {dw1, db1, dg, dbe};
 }
 
@@ -375,25 +360,19 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_forward);
   m.def("conv2_pack(Tensor w2) -> (Tensor, Tensor)", &conv2_pack);
-  m.def("fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2) -> (Tensor, Tensor)", &fused_conv2_forward);
+  m.def("fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2) -> (Tensor, Tensor, Tensor)",
+        &fused_conv2_forward);
   m.def(
-      "fused_head_forward(Tensor y2, Tensor partial2, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
-      "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc, Tensor(d!)? x_out=None, "
-      "Tensor(e!)? ya_out=None) "
-      "-> (Tensor, Tensor, Tensor)",
+      "fused_head_forward(Tensor ya, Tensor partial2, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
+      "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc, int P, "
+      "Tensor(d!)? x_out=None) -> (Tensor, Tensor, Tensor)",
       &fused_head_forward);
   m.def(
-      "fused_head_backward(Tensor dlogits, Tensor y2, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor wfc, "
-      "Tensor(a!)? dw_out, float scale, bool compute_dw=True) -> (Tensor, Tensor, Tensor, Tensor, Tensor)",
-      &fused_head_backward);
-  m.def("fused_conv2_backward(Tensor dy2, Tensor p1, Tensor wd, bool need_dp1, float scale) -> (Tensor, Tensor, Tensor)",
-        &fused_conv2_backward);
-  m.def(
-      "fused_head_backward_g2m(Tensor dlogits, Tensor y2, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor wfc, "
-      "Tensor(a!)? dw_out, float scale, bool compute_dw=True, Tensor? ya=None, float update_lr=0.0, "
+      "fused_head_backward(Tensor dlogits, Tensor ya, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor(e!) wfc, "
+      "int P, Tensor(a!)? dw_out, float scale, bool compute_dw=True, float update_lr=0.0, "
       "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None) -> "
       "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
-      &fused_head_backward_g2m);
+      &fused_head_backward);
   m.def(
       "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale, "
       "Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
@@ -403,4 +382,5 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor stats1, Tensor gram, float scale, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
       "Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None) -> (Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_backward);
+  m.def("launch_probe(Tensor like, int lds_bytes, int threads) -> ()", &launch_probe);
 }

@@ -221,29 +221,37 @@ void tds_bn_fwd_train(const float* x, int B, int C, int64_t HW, float eps, float
                       int64_t* num_batches, float* aff_a, float* aff_b, double* partial, int nchunk, hipStream_t st) {
   hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(nchunk, C), dim3(256), 0, st, x, nullptr, nullptr, partial, B, C, HW,
                      nchunk);
+  TDS_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, st, partial, C, nchunk,
                      (int64_t)B * HW, eps, momentum, gamma, beta, save_mean, save_invstd, running_mean, running_var,
                      num_batches, aff_a, aff_b);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_bn_eval_affine(const float* rm, const float* rv, int C, float eps, const float* gamma, const float* beta,
                         float* aff_a, float* aff_b, hipStream_t st) {
   hipLaunchKernelGGL(bn_eval_affine_kernel, dim3((C + 63) / 64), dim3(64), 0, st, rm, rv, C, eps, gamma, beta, aff_a,
                      aff_b);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_bn_apply(const float* x, const float* aff_a, const float* aff_b, float* y, int B, int C, int64_t HW, int relu,
                   hipStream_t st) {
   hipLaunchKernelGGL(bn_apply_kernel, plane_grid(HW, (int64_t)B * C), dim3(256), 0, st, x, aff_a, aff_b, y, C, HW, relu);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_bn_bwd(const float* dy, const float* x, int B, int C, int64_t HW, const float* gamma, const float* mean,
                 const float* invstd, float* dx, float* dgamma, float* dbeta, float* kbuf /*3*C*/, double* partial,
                 int nchunk, hipStream_t st) {
   hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(nchunk, C), dim3(256), 0, st, x, dy, mean, partial, B, C, HW, nchunk);
+  TDS_LAUNCH_CHECK();
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0, st, partial, C, nchunk, (int64_t)B * HW,
                      gamma, mean, invstd, dgamma, dbeta, kbuf, kbuf + C, kbuf + 2 * C);
-  if (dx)
+  TDS_LAUNCH_CHECK();
+  if (dx) {
     hipLaunchKernelGGL(bn_bwd_apply_kernel, plane_grid(HW, (int64_t)B * C), dim3(256), 0, st, dy, x, kbuf, kbuf + C,
                        kbuf + 2 * C, dx, C, HW);
+    TDS_LAUNCH_CHECK();
+  }
 }

@@ -9,6 +9,15 @@
 
 #define TDS_WAVE 64
 
+// Launch-status plumbing (launch_status.hip): every host launcher calls TDS_LAUNCH_CHECK()
+// right after its hipLaunchKernelGGL, which records the first failed launch of the calling
+// thread (bad grid / block / LDS size, missing code object ...); launchers that refuse a shape
+// record it with tds_launch_fail().  The binding layer (csrc/*.cpp) takes the record after every
+// op and raises, so a bad launch is a Python exception, never silently skipped work.
+void tds_note_launch(hipError_t e, const char* where, int line);
+void tds_launch_fail(const char* what);
+#define TDS_LAUNCH_CHECK() tds_note_launch(hipGetLastError(), __func__, __LINE__)
+
 namespace tds {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));

@@ -23,8 +23,11 @@
 //              the persistent workgroup; slab[wg][26][32][16] reduced in fp64 afterwards.
 // LDS (72 448 B): dy2 planes (hi co0-15, hi co16-31, lo co0-15, lo co16-31) | 2 x p1 planes
 // (hi, lo; LDS-DMA, double-buffered) | dgrad exchange | BN2 backward constants.
+#include <cstdlib>
+
 #include "conv2_common.h"
 #include "launchers.h"
+#include "pooled_layout.h"
 
 namespace tds {
 
@@ -79,44 +82,6 @@ __device__ __forceinline__ void b2_load_w(const uint4* __restrict__ wd, f32x4 (&
   b2_load_w_group<D, 2>(wd, R, lane);
 }
 
-// One kx group: staged input rows R = KY0 .. KY0 + NKY + 6; A(R) serves o = R - ky.
-template <int D, int I, int DIAG>
-__device__ __forceinline__ void b2_dgrad_group(const char* d_l, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp,
-                                               int lp, int li) {
-  using G = DgGroup<D, I>;
-  constexpr int NR = 8 + G::NKY - 1;
-  s16x8 ah[2], al[2];
-  auto load_a = [&](int r, int buf) {
-    const int rec = (G::KY0 + r) * B2_SC + G::KX + li;
-    ah[buf] = lds8<DIAG>(d_l + hp + rec * 32);
-    al[buf] = lds8<DIAG>(d_l + lp + rec * 32);
-  };
-  load_a(0, 0);
-#pragma unroll
-  for (int r = 0; r < NR; ++r) {
-    const int cur = r & 1;
-    if (r + 1 < NR) load_a(r + 1, cur ^ 1);
-    __builtin_amdgcn_sched_barrier(0);  // next row's operand reads ahead of this row's MFMAs
-#pragma unroll
-    for (int k = 0; k < G::NKY; ++k) {
-      const int o = r - k;
-      if (o >= 0 && o < 8)
-        acc[o] = mma3<DIAG>(ah[cur], al[cur], __builtin_bit_cast(s16x8, R[5 * I + k][0]),
-                            __builtin_bit_cast(s16x8, R[5 * I + k][1]), acc[o]);
-    }
-  }
-}
-
-template <int D, int DIAG>
-__device__ __forceinline__ void b2_dgrad(const char* d_l, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int lp,
-                                         int li) {
-#pragma unroll
-  for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  b2_dgrad_group<D, 0, DIAG>(d_l, R, acc, hp, lp, li);
-  b2_dgrad_group<D, 1, DIAG>(d_l, R, acc, hp, lp, li);
-  b2_dgrad_group<D, 2, DIAG>(d_l, R, acc, hp, lp, li);
-}
-
 // Wave D hands the partner's rows (4(1-D) .. +3) to the exchange slot 1-D.
 template <int D>
 __device__ __forceinline__ void b2_xchg_put(f32x4* xs, const f32x4 (&acc)[8], int lane) {
@@ -144,64 +109,17 @@ __device__ __forceinline__ void b2_xchg_finish(const f32x4* xs, const f32x4 (&ac
   }
 }
 
-// wgrad of one tile: K-step m = output rows 2m, 2m+1 (k = 8g + j <-> row 2m + (j >> 2), col 4g + (j & 3)).
-template <int E, int DIAG>
-__device__ __forceinline__ void b2_wgrad(const char* d_l, const char* p_l, f32x4 (&wacc)[13][2], int lane,
-                                         const s16x8& ones_hi, const s16x8& zero8) {
-  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-  s16x8 ahi[2], alo[2], bhi[2], blo[2];
-  auto load_a = [&](int m) {
-    const int ra = (2 * m + 2) * B2_SC + 2 + 4 * g + q4;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const s16x4 x0 = ldtr<DIAG>(d_l + h * B2_DPLANE + ra * 32 + p4 * 8);
-      const s16x4 x1 = ldtr<DIAG>(d_l + h * B2_DPLANE + (ra + B2_SC) * 32 + p4 * 8);
-      const s16x4 y0 = ldtr<DIAG>(d_l + (2 + h) * B2_DPLANE + ra * 32 + p4 * 8);
-      const s16x4 y1 = ldtr<DIAG>(d_l + (2 + h) * B2_DPLANE + (ra + B2_SC) * 32 + p4 * 8);
-      ahi[h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      alo[h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
-    }
-  };
-  auto load_b = [&](int m, int k, int buf) {
-    const int tap = 13 * E + k;
-    if (tap < 25) {
-      const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-      const int rb = (2 * m + ky) * B2_SC + kx + 4 * g + q4;
-      const s16x4 x0 = ldtr<DIAG>(p_l + rb * 32 + p4 * 8);
-      const s16x4 x1 = ldtr<DIAG>(p_l + (rb + B2_SC) * 32 + p4 * 8);
-      const s16x4 y0 = ldtr<DIAG>(p_l + B2_PPLANE + rb * 32 + p4 * 8);
-      const s16x4 y1 = ldtr<DIAG>(p_l + B2_PPLANE + (rb + B2_SC) * 32 + p4 * 8);
-      bhi[buf] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      blo[buf] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
-    } else {
-      bhi[buf] = ones_hi;  // bias gradient column
-      blo[buf] = zero8;
-    }
-  };
-#pragma unroll 1
-  for (int m = 0; m < B2_TH / 2; ++m) {
-    load_a(m);
-    load_b(m, 0, 0);
-#pragma unroll
-    for (int k = 0; k < 13; ++k) {
-      if (k + 1 < 13) load_b(m, k + 1, (k + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);  // next tap's operand reads ahead of this tap's MFMAs
-#pragma unroll
-      for (int h = 0; h < 2; ++h) wacc[k][h] = mma3<DIAG>(ahi[h], alo[h], bhi[k & 1], blo[k & 1], wacc[k][h]);
-    }
-  }
-}
-
 // Per-thread staging state: the next tile's y2 windows, pooled gradients and p1 records
 // in registers (loaded under the current tile's MFMAs), then BN2 backward -> LDS.
 struct B2Args {
   const float4* __restrict__ y2;
-  const float* __restrict__ g2m;  // planar [B][32][Q][Q]
+  const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
   const uint4* __restrict__ p1;
   float* __restrict__ dp1;
   float* __restrict__ slab;
   const int* __restrict__ order;  // blocked tile order (tds_tile_order)
   int B, P, Q, tiles_r, tiles_c, per_img, total;
+  PBGeom pg;
 };
 
 struct B2Tile {
@@ -237,7 +155,7 @@ struct B2Stager {
   uint4 pr[REGP1 ? B2_DMA_PER_WAVE : 1];
   // per-thread byte offsets (fixed for the kernel): global, relative to the tile's
   // descriptor bases, and LDS, of each staging item (window x 4 channels); p1 DMA sources
-  uint32_t yoff[B2_IPER], goff[B2_IPER], doff[B2_DMA_PER_WAVE];
+  uint32_t yoff[B2_IPER], doff[B2_DMA_PER_WAVE];
   int drec[B2_IPER];
 
   // staging item u of this thread: window (wy, wx)
@@ -263,7 +181,6 @@ struct B2Stager {
       int wy, wx;
       item_geom(tid, u, wy, wx);
       yoff[u] = (uint32_t)(((2 * wy) * a.P + 2 * wx) * 128 + c4 * 16);
-      goff[u] = (uint32_t)((wy * a.Q + wx) * 4 + (int64_t)c4 * 16 * a.Q * a.Q);  // planar: channel 4*c4
       drec[u] = ((2 * wy) * B2_SC + 2 * wx) * 32 + (c4 & 3) * 8;
     }
 #pragma unroll
@@ -291,16 +208,22 @@ struct B2Stager {
     const int64_t img = (int64_t)x.b * P;
     const __amdgpu_buffer_rsrc_t ry =
         b2_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 128);
-    const __amdgpu_buffer_rsrc_t rg = b2_rsrc(reinterpret_cast<const char*>(a.g2m) +
-                                              ((int64_t)x.b * 32 * Q * Q + (int64_t)((x.r0 - 2) / 2) * Q + (x.c0 - 2) / 2) * 4);
-    const uint32_t gplane = (uint32_t)(Q * Q * 4);
     const char* pbase = reinterpret_cast<const char*>(a.p1) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 64;
-    uint32_t oy[B2_IPER][4], og[B2_IPER];
+    uint32_t oy[B2_IPER][4];
+    // pooled gradients: window (wy, wx) is pooled position (r0/2 - 1 + wy, c0/2 - 1 + wx); four
+    // channel planes of the planar g2m, 64-bit addressed (no 2 GiB descriptor range)
+    const float* gp[B2_IPER];
+    bool gok[B2_IPER];
+    const int64_t gplane = (int64_t)Q * Q;
 #pragma unroll
     for (int u = 0; u < B2_IPER; ++u) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) oy[u][q] = yoff[u] + (uint32_t)(((q >> 1) * P + (q & 1)) * 128);
-      og[u] = goff[u];
+      int wy, wx;
+      item_geom(tid, u, wy, wx);
+      const int py = x.r0 / 2 - 1 + wy, px = x.c0 / 2 - 1 + wx;
+      gok[u] = tid + u * B2_THREADS < B2_ITEMS && py >= 0 && py < Q && px >= 0 && px < Q;
+      gp[u] = a.g2m + (gok[u] ? ((int64_t)x.b * 32 + 4 * (tid & 7)) * gplane + (int64_t)py * Q + px : 0);
     }
     const char* psrc[B2_DMA_PER_WAVE];
 #pragma unroll
@@ -309,8 +232,6 @@ struct B2Stager {
       // edge tile: lanes outside the image (or past the item count) read zeros
       const int lo_r = max(0, 2 - x.r0), hi_r = min(B2_SR, P - x.r0 + 2);
       const int lo_c = max(0, 2 - x.c0), hi_c = min(B2_SC, P - x.c0 + 2);
-      const int plo_r = lo_r >> 1, phi_r = min(B2_SR / 2, Q - (x.r0 - 2) / 2);
-      const int plo_c = lo_c >> 1, phi_c = min(B2_SC / 2, Q - (x.c0 - 2) / 2);
 #pragma unroll
       for (int u = 0; u < B2_IPER; ++u) {
         int wy, wx;
@@ -321,7 +242,6 @@ struct B2Stager {
           const int lr = 2 * wy + (q >> 1), lc = 2 * wx + (q & 1);
           if (!(item && lr >= lo_r && lr < hi_r && lc >= lo_c && lc < hi_c)) oy[u][q] = kB2Oob;
         }
-        if (!(item && wy >= plo_r && wy < phi_r && wx >= plo_c && wx < phi_c)) og[u] = kB2Oob;
       }
 #pragma unroll
       for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
@@ -359,13 +279,9 @@ struct B2Stager {
       for (int q = 0; q < 4; ++q)
         yv[u][q] = DIAG == 7 ? make_float4(1.f, 0.f, 0.f, 0.f)  // timing only: no y2 loads
                              : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy[u][q], 0, 0));
-      // four channel planes; an out-of-image lane stays at kB2Oob for all four (zeros)
       float g4[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k)
-        g4[k] = DIAG == 6 ? 0.f  // timing only: no g2m loads
-                          : __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                rg, og[u] == kB2Oob ? kB2Oob : og[u] + k * gplane, 0, 0));
+      for (int k = 0; k < 4; ++k) g4[k] = gok[u] ? gp[u][k * gplane] : 0.f;
       gv[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
     }
   }
@@ -471,108 +387,6 @@ struct B2Stager {
     }
   }
 };
-
-// The tile loop of one role, hoisted out of the role branch (wave specialization): each
-// wave runs its own copy with the same barrier sequence, so role state that another
-// role never touches is not kept alive across it.  ROLE 0/1 = dgrad wave D, 2/3 = wgrad.
-template <int ROLE, int DIAG>
-__device__ __forceinline__ void b2_run(const B2Args& a, const uint4* __restrict__ wdpack, char* smem, int first_t) {
-  char* d_l = smem;
-  char* p_l = smem + B2_OFF_P;
-  f32x4* xs = reinterpret_cast<f32x4*>(smem + B2_OFF_X);
-  const float* kc = reinterpret_cast<const float*>(smem + B2_OFF_K);
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int li = lane & 15, g = lane >> 4;
-  B2Stager<DIAG, ROLE> st;
-
-  // R: dgrad = (hi, lo) weight fragments of the wave's flipped taps; wgrad = accumulators
-  f32x4 R[13][2];
-#pragma unroll
-  for (int k = 0; k < 13; ++k) R[k][0] = R[k][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 acc[8];  // dgrad: partial dp1 of the tile's 8 rows
-#pragma unroll
-  for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (ROLE < 2) b2_load_w<ROLE>(wdpack, R, lane);
-  s16x8 ones_hi, zero8;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ones_hi[j] = (short)(li == 0 ? 0x3f80 : 0);  // bf16 1.0 in column n = 0
-    zero8[j] = 0;
-  }
-  const int hp = (g >> 1) * B2_DPLANE + (g & 1) * 16;  // dgrad A: co 8g .. 8g+7 (hi planes)
-  const int lp = (2 + (g >> 1)) * B2_DPLANE + (g & 1) * 16;
-
-  B2Tile prev{0, 0, 0, false}, nxt{0, 0, 0, false};
-  bool have_prev = false;
-  st.init(a, tid);
-  int t = first_t;
-  if (t < a.total) {
-    nxt = b2_decode(a, t);
-    st.load(a, nxt, tid, p_l);
-  }
-  for (int kk = 0; t < a.total; t += gridDim.x, ++kk) {
-    const B2Tile cur = nxt;
-    char* p_cur = p_l + (kk & 1) * B2_PBUF;  // p1 of tile t (DMA'd one iteration earlier)
-    __syncthreads();  // (A) previous tile's operand readers are done; exchange slots are full
-    if constexpr (ROLE < 2) {
-      if (have_prev) b2_xchg_finish<ROLE>(xs, acc, a.dp1, lane, prev.b, prev.r0, prev.c0, a.P);
-    }
-    st.store(a, cur, tid, d_l, kc);
-    __syncthreads();  // (B) tile t staged
-    if (t + (int)gridDim.x < a.total) {
-      nxt = b2_decode(a, t + gridDim.x);
-      st.load(a, nxt, tid, p_l + ((kk + 1) & 1) * B2_PBUF);  // its readers finished before (A)
-    }
-    if constexpr (ROLE < 2) {
-      b2_dgrad<ROLE, DIAG>(d_l, R, acc, hp, lp, li);
-      b2_xchg_put<ROLE>(xs, acc, lane);
-    } else {
-      b2_wgrad<ROLE - 2, DIAG>(d_l, p_cur, R, lane, ones_hi, zero8);
-    }
-    prev = cur;
-    have_prev = true;
-  }
-  __syncthreads();
-  if constexpr (ROLE < 2) {
-    if (have_prev) b2_xchg_finish<ROLE>(xs, acc, a.dp1, lane, prev.b, prev.r0, prev.c0, a.P);
-  } else {
-    // slab[wg][tap(26)][co(32)][ci(16)]: lane holds C[co = 16h + 4g + r][ci = li]
-    float* out = a.slab + (int64_t)blockIdx.x * 26 * 512;
-#pragma unroll
-    for (int k = 0; k < 13; ++k) {
-      const int tap = 13 * (ROLE - 2) + k;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) out[(tap * 32 + 16 * h + 4 * g + r) * 16 + li] = R[k][h][r];
-    }
-  }
-}
-
-template <int DIAG>
-__global__ __launch_bounds__(B2_THREADS, 2) void conv2_bwd2_kernel(
-    const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
-    const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
-    float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ order, int B, int P, int Q) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x;
-  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform role: scalar branches
-  B2Args a;
-  a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.order = order;
-  a.B = B; a.P = P; a.Q = Q;
-  a.tiles_c = (P + B2_TC - 1) / B2_TC;
-  a.tiles_r = (P + B2_TH - 1) / B2_TH;
-  a.per_img = a.tiles_c * a.tiles_r;
-  a.total = a.per_img * B;
-  float* kc = reinterpret_cast<float*>(smem + B2_OFF_K);  // [5][32]: a | b | k1 | k2 | k3
-  if (tid < 160) kc[tid] = (tid < 64) ? aff2[tid] : kbuf[tid - 64];  // visible after barrier (A)
-  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
-  // wave-uniform role branch; every role executes the same sequence of barriers
-  if (wv == 0) b2_run<0, DIAG>(a, wdpack, smem, t0);
-  else if (wv == 1) b2_run<1, DIAG>(a, wdpack, smem, t0);
-  else if (wv == 2) b2_run<2, DIAG>(a, wdpack, smem, t0);
-  else b2_run<3, DIAG>(a, wdpack, smem, t0);
-}
 
 // ============================================================================ v3: producer/consumer waves
 // Counters on v2 (rocprofv3 --pmc, docs/KERNELS.md): MFMA busy ~41% of the kernel, ~725 VALU
@@ -823,6 +637,7 @@ __global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
   a.tiles_r = (P + B2_TH - 1) / B2_TH;
   a.per_img = a.tiles_c * a.tiles_r;
   a.total = a.per_img * B;
+  a.pg = pb_geom(Q);
   float* kc = reinterpret_cast<float*>(smem + B3_OFF_K);
   if (tid < 160) kc[tid] = (tid < 64) ? aff2[tid] : kbuf[tid - 64];
   __syncthreads();  // kc visible to the staging waves
@@ -843,22 +658,29 @@ __global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
 
 using namespace tds;
 
-int tds_conv2_bwd2_num_wg() { return 2 * tds_conv2_num_wg(); }
+int tds_conv2_bwd3_num_wg() { return tds_conv2_num_wg(); }  // one 8-wave workgroup per CU
 
-static int conv2_diag_env() {
+void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c) {
+  *tiles_r = (P + B2_TH - 1) / B2_TH;
+  *tiles_c = (P + B2_TC - 1) / B2_TC;
+}
+
+#ifdef TDS_DIAG
+// timing-only variants (tools/conv2_diag.py): 1 no MFMAs, 3 no global tile loads, 5 no staging,
+// 7 no y2 loads.  Compiled only into a -DTDS_DIAG build.
+static int b3_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
   return e ? std::atoi(e) : 0;
 }
+#else
+static int b3_diag_env() { return 0; }
+#endif
 
-int tds_conv2_bwd3_num_wg() { return tds_conv2_num_wg(); }  // one 8-wave workgroup per CU
-
+// g2m: planar [B][32][Q][Q]; order: the blocked tile order table (tds_tile_order_fill) from the caller
 void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, int nwg, int B, int P, hipStream_t st) {
+                    const short* wd, float* dp1, float* slab, const int* order, int nwg, int B, int P,
+                    hipStream_t st) {
   const int Q = P / 2;
-  const int* order = tds_tile_order(B, (P + B2_TH - 1) / B2_TH, (P + B2_TC - 1) / B2_TC);
-  if (!order) return;
-  // TDS_CONV2_DIAG (timing only): 1 no MFMAs, 3 no global tile loads, 5 no staging, 6 no g2m loads,
-  // 7 no y2 loads
 #define TDS_B3_LAUNCH(D)                                                                                               \
   {                                                                                                                    \
     static bool set = false;                                                                                           \
@@ -870,50 +692,16 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
     hipLaunchKernelGGL(conv2_bwd3_kernel<D>, dim3(nwg), dim3(B3_THREADS), B3_LDS, st,                                  \
                        reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, reinterpret_cast<const uint4*>(p1),       \
                        reinterpret_cast<const uint4*>(wd), dp1, slab, order, B, P, Q);                                  \
+    TDS_LAUNCH_CHECK();                                                                                                \
   }
-  switch (conv2_diag_env()) {
+  switch (b3_diag_env()) {
+#ifdef TDS_DIAG
     case 1: TDS_B3_LAUNCH(1) break;
     case 3: TDS_B3_LAUNCH(3) break;
     case 5: TDS_B3_LAUNCH(5) break;
-    case 6: TDS_B3_LAUNCH(6) break;
     case 7: TDS_B3_LAUNCH(7) break;
+#endif
     default: TDS_B3_LAUNCH(0) break;
   }
 #undef TDS_B3_LAUNCH
-}
-
-
-template <int DIAG>
-static void b2_set_lds_limit(int bytes) {
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd2_kernel<DIAG>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-}
-
-void tds_conv2_bwd2(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, int nwg, int B, int P, hipStream_t st) {
-  const int Q = P / 2;
-  const dim3 grid(nwg), block(B2_THREADS);
-  // TDS_B2_LDS_PAD (debug): extra dynamic LDS per workgroup, e.g. 20000 forces one workgroup per CU
-  const char* pad_env = std::getenv("TDS_B2_LDS_PAD");
-  const int lds = B2_LDS + (pad_env ? std::atoi(pad_env) : 0);
-  static int lds_set = 0;
-  if (lds_set != lds) {
-    b2_set_lds_limit<0>(lds);
-    b2_set_lds_limit<1>(lds);
-    b2_set_lds_limit<2>(lds);
-    b2_set_lds_limit<3>(lds);
-    lds_set = lds;
-  }
-  const float4* y = reinterpret_cast<const float4*>(y2);
-  const float* gm = g2m;
-  const uint4* pp = reinterpret_cast<const uint4*>(p1);
-  const uint4* w = reinterpret_cast<const uint4*>(wd);
-  const int* order = tds_tile_order(B, (P + B2_TH - 1) / B2_TH, (P + B2_TC - 1) / B2_TC);
-  if (!order) return;  // shape beyond the table's packing (B > 255 or > 4095 tiles per side)
-  switch (conv2_diag_env()) {
-    case 1: hipLaunchKernelGGL(conv2_bwd2_kernel<1>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
-    case 2: hipLaunchKernelGGL(conv2_bwd2_kernel<2>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
-    case 3: hipLaunchKernelGGL(conv2_bwd2_kernel<3>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
-    default: hipLaunchKernelGGL(conv2_bwd2_kernel<0>, grid, block, lds, st, y, gm, aff2, kbuf, pp, w, dp1, slab, order, B, P, Q); break;
-  }
 }

@@ -1,5 +1,6 @@
-// Shared pieces of the conv2 kernels (conv2_bf16x3.hip, conv2_bwd2.hip): the timing-only
-// diagnostic operand/MFMA wrappers (tools/conv2_diag.py, TDS_CONV2_DIAG).
+// Shared pieces of the conv2 kernels (conv2_fwd2.hip, conv2_bwd.hip): the operand / MFMA
+// wrappers, parameterised by a timing-only diagnostic variant that only a -DTDS_DIAG build
+// can select (tools/conv2_diag.py, TDS_CONV2_DIAG); production builds instantiate DIAG = 0.
 #pragma once
 
 #include "bf16x3.h"
@@ -39,44 +40,18 @@ __device__ __forceinline__ s16x4 ldtr(const void* p) {
 }
 
 // ---------------------------------------------------------------------------- tile order
-// L2-blocked tile order for the persistent conv kernels.  xcd_remap hands each XCD a
-// contiguous run of 64 work indices per round (grid = 512 = 8 XCDs x 64 workgroups), and
-// t -> t + grid is the same workgroup's next tile.  A plain row-major order makes those 64
-// tiles a 1-D strip, so the 2-pixel halo above/below each tile (a third of the staged rows)
-// is fetched again a round later, long after it left the XCD's 4 MiB L2.  Here work index
-// t walks, per image, bands of BC tile-columns; each band in row groups of GR tile-rows;
-// each row group in column groups of GC:  one XCD round = one GR x GC block of tiles (its
-// halos are fetched once, concurrently, into one L2), the 8 XCDs take the 8 blocks of a
-// band row side by side, and the next round is the block right below (its top halo still
-// in L2).  Bijective for any tiles_r x tiles_c (edge groups are simply smaller).
-template <int BC, int GR, int GC>
-__device__ __forceinline__ void blocked_tile(int t, int per_img, int tiles_r, int tiles_c, int& b, int& tr, int& tc) {
-  b = t / per_img;
-  int off = t - b * per_img;
-  const int band = off / (BC * tiles_r);  // every band before the last is full width
-  off -= band * BC * tiles_r;
-  const int wj = min(BC, tiles_c - band * BC);
-  const int gr = off / (GR * wj);
-  off -= gr * GR * wj;
-  const int hg = min(GR, tiles_r - gr * GR);
-  const int cg = off / (GC * hg);
-  off -= cg * GC * hg;
-  const int wc = min(GC, wj - cg * GC);
-  const int r = off / wc;
-  tr = gr * GR + r;
-  tc = band * BC + cg * GC + (off - r * wc);
-}
-
-}  // namespace tds
-
-namespace tds {
-
-// Device table of the blocked tile order (blocked_tile<32, 16, 4>), one int per work index:
-// b << 24 | tile_row << 12 | tile_col.  A decode is then one scalar load instead of six
-// runtime integer divisions on the scalar unit (≈400 SALU instructions per tile per wave,
-// measured with SQ_INSTS_SALU).  Built on the host once per shape and cached.
-const int* tds_tile_order(int B, int tiles_r, int tiles_c);
-
+// L2-blocked tile order for the persistent conv kernels (built on the host by
+// tds_tile_order_fill, conv2_pack.hip; device table from the torch caching allocator, one int
+// per work index: b << 24 | tile_row << 12 | tile_col).  xcd_remap hands each XCD a contiguous
+// run of 64 work indices per round (grid = 512 = 8 XCDs x 64 workgroups), and t -> t + grid is
+// the same workgroup's next tile.  A plain row-major order makes those 64 tiles a 1-D strip,
+// so the 2-pixel halo above/below each tile (a third of the staged rows) is fetched again a
+// round later, long after it left the XCD's 4 MiB L2.  The table walks, per image, bands of 32
+// tile-columns; each band in row groups of 16 tile-rows; each row group in column groups of 4:
+// one XCD round = one 16 x 4 block of tiles (its halos fetched once, concurrently, into one
+// L2), the 8 XCDs take the 8 blocks of a band row side by side, and the next round is the
+// block right below (its top halo still in L2).  A decode is one scalar load instead of six
+// runtime integer divisions on the scalar unit.
 __device__ __forceinline__ void tile_from_order(const int* __restrict__ order, int t, int& b, int& tr, int& tc) {
   const int v = order[t];
   b = v >> 24;

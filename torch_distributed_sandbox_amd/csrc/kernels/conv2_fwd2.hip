@@ -8,12 +8,21 @@
 //   * p1 staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs, no VALU), double-buffered:
 //     tile t+1 streams in while tile t is on the MFMAs;
 //   * the epilogue of tile t (y2 stores + statistics) runs after tile t+1's DMA is issued,
-//     from a second accumulator set, so the stores drain under the next MFMAs.
+//     from a second accumulator set, so the stores drain under the next MFMAs;
+//   * the epilogue also resolves the 2x2 max-pool of the BN2 output: BN2's affine a*y + b is
+//     monotone per channel with the sign of gamma (a = gamma * invstd), so the window's
+//     argmax value is max(y2) (gamma >= 0) or min(y2) (gamma < 0) -- known before the batch
+//     statistics are.  Every lane holds whole windows of its channel, the 4 x 8 pooled block
+//     of the tile is staged in LDS and stored as ya (pooled_layout.h): one 128-B line per
+//     channel.  The head then streams ya (72 MB per image at 3000^2) instead of y2 (288 MB).
 // K order and input-row sharing as conv2_fwd_bf16x3_kernel: K-step s < 10 pairs taps
 // (ky = s>>1, kx = 2(s&1) + (g>>1)) so one staged input row R serves output rows R - ky;
 // s = 10 + kp pairs (ky = 2kp + (g>>1), kx = 4) with lane groups 2-3 reading row R+1.
+#include <cstdlib>
+
 #include "conv2_common.h"
 #include "launchers.h"
+#include "pooled_layout.h"
 
 namespace tds {
 
@@ -26,9 +35,12 @@ constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records, 2
 constexpr int F2_PBUF = 2 * F2_PPLANE;                 // hi + lo
 constexpr int F2_STAGE = F2_TH * F2_TC * 32 * 4;        // finished tile: 8 x 16 px x 32 co fp32 = 16 KiB
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
-constexpr int F2_LDS = F2_OFF_S + 2 * F2_STAGE;        // + double-buffered output staging: 64 KiB
+constexpr int F2_YSTAGE = 32 * 32 * 4;                 // pooled block: 32 co x 4 x 8 fp32 = 4 KiB
+constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
+constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging: 72 KiB
 constexpr int F2_DMA_PER_WAVE = 2 * F2_PGROUPS / (F2_THREADS / 64);  // 4
 static_assert(F2_LDS % 16 == 0, "LDS carve");
+static_assert(2 * F2_LDS <= 160 * 1024, "two workgroups per CU");
 
 // 16 zero bytes: the DMA source of staged records outside the image
 __device__ __attribute__((aligned(16))) uint32_t g_f2_zero[4] = {0u, 0u, 0u, 0u};
@@ -120,9 +132,17 @@ __device__ __forceinline__ int f2_stage_off(int row, int px, int chunk) {
   return ((row * F2_TC + px) * 8 + (chunk ^ (px & 7))) * 16;
 }
 
+// pooled block staging: channel co's 32 floats [prow 4][pcol 8], float4 chunks XOR-swizzled by co
+__device__ __forceinline__ int f2_ystage_off(int co, int e) { return co * 32 + ((((e >> 2) ^ co) & 7) << 2) + (e & 3); }
+
+// window extreme in the direction of BN2's affine; a NaN anywhere wins (torch's max-pool rule)
+__device__ __forceinline__ float f2_ext(float p, float q, bool neg) {
+  return (isnan(q) || (neg ? q < p : q > p)) ? q : p;
+}
+
 // stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li]
-__device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, int P, int RH, int NT,
-                                         int lane, float bco, float& s_acc, float& q_acc) {
+__device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
+                                         int RH, int NT, int lane, float bco, bool neg, float& s_acc, float& q_acc) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
 #pragma unroll
@@ -140,6 +160,28 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
       *reinterpret_cast<float*>(stage + f2_stage_off(row, px, co >> 2) + (co & 3) * 4) = v + bco;
     }
   }
+  // pooled windows (rows 4RH + 2i + {0,1}, columns 4g + 2j + {0,1}) -> ya block entry
+  // (prow 2RH + i, pcol 2g + j); fp32 addition is monotone, so max(v) + b2 == max(v + b2)
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float e = acc[2 * i][2 * j];
+      e = f2_ext(e, acc[2 * i][2 * j + 1], neg);
+      e = f2_ext(e, acc[2 * i + 1][2 * j], neg);
+      e = f2_ext(e, acc[2 * i + 1][2 * j + 1], neg);
+      ystage[f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g + j)] = e + bco;
+    }
+}
+
+// the workgroup stores the staged pooled block: thread e -> channel e / 8, float4 e % 8
+__device__ __forceinline__ void f2_store_ya(const float* ystage, const F2Tile& x, float* __restrict__ ya,
+                                            const PBGeom& pg) {
+  const int tr = x.r0 / F2_TH, tc = x.c0 / F2_TC;  // = the tile's pooled block
+  if (tr >= pg.Q4 || tc >= pg.Q8) return;          // (odd P: a last tile row beyond the pooled image)
+  const int e = threadIdx.x, co = e >> 3, part = e & 7;
+  const float4 v = *reinterpret_cast<const float4*>(ystage + f2_ystage_off(co, part * 4));
+  *reinterpret_cast<float4*>(ya + ((((int64_t)x.b * 32 + co) * pg.Q4 + tr) * pg.Q8 + tc) * 32 + part * 4) = v;
 }
 
 // the whole workgroup stores a staged tile: thread e, i -> float4 q = e + 256 i of
@@ -160,9 +202,9 @@ __device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, flo
 
 template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
-                                       const float* __restrict__ bias, float* __restrict__ y2,
-                                       double* __restrict__ partial, const int* __restrict__ order, int B, int P,
-                                       char* smem) {
+                                       const float* __restrict__ bias, const float* __restrict__ gamma,
+                                       float* __restrict__ y2, float* __restrict__ ya, double* __restrict__ partial,
+                                       const int* __restrict__ order, int B, int P, char* smem) {
   constexpr int NT = WV & 1, RH = WV >> 1;
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int tiles_c = (P + F2_TC - 1) / F2_TC, tiles_r = (P + F2_TH - 1) / F2_TH;
@@ -182,6 +224,9 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
 #pragma unroll
     for (int hl = 0; hl < 2; ++hl) W[s][hl] = __builtin_bit_cast(f32x4, wpack[((hl * 13 + s) * 2 + NT) * 64 + lane]);
   const float bco = bias[16 * NT + li];
+  const bool neg = gamma != nullptr && gamma[16 * NT + li] < 0.f;
+  const PBGeom pg = pb_geom(P / 2);
+  float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
   float s_acc = 0.f, q_acc = 0.f;
   f32x4 acc[4];
   F2Tile prev{0, 0, 0};
@@ -195,14 +240,21 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     // tile t-1 (stage (kk+1)&1) is complete
     __syncthreads();
     if (t + (int)gridDim.x < total) f2_dma<DIAG, WV>(p1, decode(t + gridDim.x), P, smem + ((kk + 1) & 1) * F2_PBUF, lane);
-    if (have_prev) f2_store<DIAG>(smem + F2_OFF_S + ((kk + 1) & 1) * F2_STAGE, prev, y2, P);
+    if (have_prev) {
+      f2_store<DIAG>(smem + F2_OFF_S + ((kk + 1) & 1) * F2_STAGE, prev, y2, P);
+      f2_store_ya(ys + ((kk + 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
+    }
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
-    f2_stage(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, P, RH, NT, lane, bco, s_acc, q_acc);
+    f2_stage(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane, bco,
+             neg, s_acc, q_acc);
     prev = cur;
     have_prev = true;
   }
   __syncthreads();
-  if (have_prev) f2_store<DIAG>(smem + F2_OFF_S + ((kk - 1) & 1) * F2_STAGE, prev, y2, P);
+  if (have_prev) {
+    f2_store<DIAG>(smem + F2_OFF_S + ((kk - 1) & 1) * F2_STAGE, prev, y2, P);
+    f2_store_ya(ys + ((kk - 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
+  }
   // BN2 partials: reduce the 4 lane groups, then the two row-halves of this co half
   s_acc += __shfl_xor(s_acc, 16, 64);
   s_acc += __shfl_xor(s_acc, 32, 64);
@@ -227,41 +279,67 @@ template <int DIAG>
 __global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* __restrict__ p1,
                                                                    const uint4* __restrict__ wpack,
                                                                    const float* __restrict__ bias,
-                                                                   float* __restrict__ y2,
+                                                                   const float* __restrict__ gamma,
+                                                                   float* __restrict__ y2, float* __restrict__ ya,
                                                                    double* __restrict__ partial,
                                                                    const int* __restrict__ order, int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
-  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, y2, partial, order, B, P, smem);
-  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, y2, partial, order, B, P, smem);
-  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, y2, partial, order, B, P, smem);
-  else f2_run<DIAG, 3>(p1, wpack, bias, y2, partial, order, B, P, smem);
+  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
+  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
+  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
+  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
 }
 
 }  // namespace tds
 
 using namespace tds;
 
-// workgroups the v2 forward launches (BN2 partial rows): 2 per CU
+// workgroups the forward launches (BN2 partial rows): 2 per CU
 int tds_conv2_fwd2_num_wg() { return 2 * tds_conv2_num_wg(); }
 
+void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c) {
+  *tiles_r = (P + F2_TH - 1) / F2_TH;
+  *tiles_c = (P + F2_TC - 1) / F2_TC;
+}
+
+#ifdef TDS_DIAG
+// timing-only variants (tools/conv2_diag.py): 1 no MFMAs, 2 no LDS operand reads, 3 no global
+// tile loads, 4 no y2 stores.  Compiled only into a -DTDS_DIAG build.
 static int f2_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
   return e ? std::atoi(e) : 0;
 }
+#else
+static int f2_diag_env() { return 0; }
+#endif
 
-void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg, int B,
-                    int P, hipStream_t st) {
+// order: the blocked tile order table (tds_tile_order_fill), allocated by the caller
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
+                    double* partial, const int* order, int nwg, int B, int P, hipStream_t st) {
   const dim3 grid(nwg), block(F2_THREADS);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wp);
-  const int* order = tds_tile_order(B, (P + F2_TH - 1) / F2_TH, (P + F2_TC - 1) / F2_TC);
-  if (!order) return;  // shape beyond the table's packing (B > 255 or > 4095 tiles per side)
-  switch (f2_diag_env()) {
-    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
-    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
-    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
-    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
-    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, y2, partial, order, B, P); break;
+  static bool lds_set = false;
+  if (!lds_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_fwd2_kernel<0>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+#ifdef TDS_DIAG
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_fwd2_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_fwd2_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_fwd2_kernel<3>), hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_fwd2_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize, F2_LDS);
+#endif
+    lds_set = true;
   }
+  switch (f2_diag_env()) {
+#ifdef TDS_DIAG
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
+#endif
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
+  }
+  TDS_LAUNCH_CHECK();
 }

@@ -1,0 +1,130 @@
+// conv2 of the ConvNet (Conv2d(16, 32, 5, stride 1, pad 2), mnist_onegpu.py:20): shared host
+// pieces of the bf16x3 MFMA kernels (conv2_fwd2.hip, conv2_bwd.hip) -- the on-device weight
+// packing into MFMA fragment order, the deterministic fp64 reduction of the per-workgroup weight
+// gradient slabs, and the blocked tile order table.  SURVEY.md §2.4 K5 / K19 / K20.
+//
+// Activation formats (produced/consumed by convnet_fused.hip and the conv2 kernels):
+//   p1  [B][P][P][32] bf16 : ch 0-15 = hi(ci), 16-31 = lo(ci)      (pooled layer-1 output)
+//   y2  [B][P][P][32] fp32                                          (conv2 output, incl. bias)
+//   dp1 [B][P][P][16] fp32                                          (grad wrt p1)
+// MFMA mapping (v_mfma_f32_16x16x32_bf16, lane l: i = l&15, g = l>>4):
+//   A[i][k = 8g+j] (8 consecutive k per lane), B[k = 8g+j][n = i], C row = 4g+r, col = i.
+#include <vector>
+
+#include "conv2_common.h"
+#include "launchers.h"
+
+namespace tds {
+
+// ---------------------------------------------------------------------------- weight packing
+// fwd : wp[hl][s<13][nt<2][g<4][co16][j8], k = 32s+8g+j, ci = 8(g&1)+j, taps paired so that one
+//       input-row A fragment serves every output row:  s < 10: (ky = s>>1, kx = 2(s&1) + (g>>1));
+//       s = 10 + kp: (ky = 2kp + (g>>1), kx = 4)  (ky = 5 -> zero)
+// dgrad: wd[hl][s<25][g<4][ci16][j8],      k = 32s+8g+j -> tap' = s, co = 8g+j; w = w2[co][ci][24-tap']
+__global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* __restrict__ wp,
+                                          short* __restrict__ wd) {
+  const int FW = 13 * 2 * 4 * 16 * 8;  // per hl plane (fwd)
+  const int DW = 25 * 4 * 16 * 8;      // per hl plane (dgrad)
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < FW + DW; e += gridDim.x * blockDim.x) {
+    if (e < FW) {
+      const int j = e & 7, co_in = (e >> 3) & 15, g = (e >> 7) & 3, nt = (e >> 9) & 1, s = e >> 10;
+      const int ky = s < 10 ? (s >> 1) : 2 * (s - 10) + (g >> 1);
+      const int kx = s < 10 ? 2 * (s & 1) + (g >> 1) : 4;
+      const int ci = 8 * (g & 1) + j, co = nt * 16 + co_in;
+      const float v = ky < 5 ? w2[(co * 16 + ci) * 25 + ky * 5 + kx] : 0.f;
+      unsigned short hi, lo;
+      split_bf16(v, hi, lo);
+      wp[e] = (short)hi;
+      wp[FW + e] = (short)lo;
+    } else {
+      const int f = e - FW;
+      const int j = f & 7, ci = (f >> 3) & 15, g = (f >> 7) & 3, s = f >> 9;
+      const int co = 8 * g + j;
+      const float v = w2[(co * 16 + ci) * 25 + (24 - s)];
+      unsigned short hi, lo;
+      split_bf16(v, hi, lo);
+      wd[f] = (short)hi;
+      wd[DW + f] = (short)lo;
+    }
+  }
+}
+
+// dw2[co][ci][tap] = sum_wg slab (fixed order, fp64), db2[co] = sum_wg slab[tap 25][co][0].
+// A block owns 64 consecutive slab elements; its 4 waves sum interleaved quarters of the
+// workgroup rows (w = 4j + wave, 8 loads in flight per lane), then wave 0 adds the four
+// partials in a fixed order: deterministic, and 4x the parallelism of one lane per element.
+__global__ __launch_bounds__(256) void conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nwg,
+                                                                 float* __restrict__ dw, float* __restrict__ db,
+                                                                 float scale) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;  // over 26*32*16
+  double s = 0.0;
+  if (e < 26 * 512) {
+    int w = wv;
+    for (; w + 28 < nwg; w += 32) {
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = slab[(int64_t)(w + 4 * k) * 26 * 512 + e];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += (double)v[k];
+    }
+    for (; w < nwg; w += 4) s += (double)slab[(int64_t)w * 26 * 512 + e];
+  }
+  part[wv][lane] = s;
+  __syncthreads();
+  if (wv != 0 || e >= 26 * 512) return;
+  const double tot = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  const int tap = e / 512, co = (e / 16) & 31, ci = e & 15;
+  const float v = (float)tot * scale;
+  if (tap < 25) dw[(co * 16 + ci) * 25 + tap] = v;
+  else if (db && ci == 0) db[co] = v;
+}
+
+}  // namespace tds
+
+using namespace tds;
+
+void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t st) {
+  hipLaunchKernelGGL(conv2_pack_weights_kernel, dim3(64), dim3(256), 0, st, w2, wp, wd);
+  TDS_LAUNCH_CHECK();
+}
+
+int tds_conv2_num_wg() {
+  int dev = 0, n = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) n = prop.multiProcessorCount;
+  }
+  return n;
+}
+
+void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db, scale);
+  TDS_LAUNCH_CHECK();
+}
+
+// Blocked tile order (blocked_tile<32, 16, 4>, conv2_common.h) into a host array of
+// B * tiles_r * tiles_c ints: b << 24 | tile_row << 12 | tile_col.  The binding layer copies it
+// to a device tensor from the torch caching allocator and caches it per shape.
+int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c) {
+  if (B < 1 || B > 255 || tiles_r < 1 || tiles_r > 4095 || tiles_c < 1 || tiles_c > 4095) return -1;
+  constexpr int BC = 32, GR = 16, GC = 4;
+  const int per_img = tiles_r * tiles_c, total = per_img * B;
+  for (int t = 0; t < total; ++t) {
+    const int b = t / per_img;
+    int off = t - b * per_img;
+    const int band = off / (BC * tiles_r);
+    off -= band * BC * tiles_r;
+    const int wj = std::min(BC, tiles_c - band * BC);
+    const int gr = off / (GR * wj);
+    off -= gr * GR * wj;
+    const int hg = std::min(GR, tiles_r - gr * GR);
+    const int cg = off / (GC * hg);
+    off -= cg * GC * hg;
+    const int wc = std::min(GC, wj - cg * GC);
+    const int r = off / wc;
+    out[t] = (b << 24) | ((gr * GR + r) << 12) | (band * BC + cg * GC + (off - r * wc));
+  }
+  return 0;
+}

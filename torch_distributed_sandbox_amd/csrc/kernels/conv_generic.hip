@@ -322,6 +322,7 @@ static void launch_fwd(const float* in, const float* w, const float* bias, float
   dim3 grid((W + FWD_TW - 1) / FWD_TW, (H + FWD_TH - 1) / FWD_TH, B * ((Cout + C::COB - 1) / C::COB));
   const size_t lds = sizeof(float) * C::LDS_FLOATS;
   hipLaunchKernelGGL((conv_fwd_f32_kernel<KS, CIC, MT>), grid, dim3(256), lds, st, in, w, bias, out, Cin, Cout, H, W, P);
+  TDS_LAUNCH_CHECK();
 }
 
 template <int KS>
@@ -349,6 +350,7 @@ static void launch_wgrad(const float* in, const float* g, float* slab, int nwg, 
   if (red > lds) lds = red;
   hipLaunchKernelGGL((conv_wgrad_f32_kernel<KS, CINP, MT, NT>), dim3(nwg, ny, nz), dim3(256), lds, st, in, g, slab, B,
                      Cin, Cout, H, W, P, ncols, 0);
+  TDS_LAUNCH_CHECK();
 }
 
 }  // namespace tds
@@ -369,6 +371,7 @@ int tds_conv2d_fwd_f32(const float* in, const float* w, const float* bias, float
 void tds_conv2d_flip_weights(const float* w, float* wt, int Cout, int Cin, int KS, hipStream_t st) {
   const int total = Cout * Cin * KS * KS;
   hipLaunchKernelGGL(conv_flip_weights_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, wt, Cout, Cin, KS);
+  TDS_LAUNCH_CHECK();
 }
 
 // Returns the slab size (floats) needed, or launches when slab != nullptr.
@@ -410,5 +413,6 @@ int64_t tds_conv2d_wgrad_f32(const float* in, const float* g, float* dw, float* 
   const int total = Cout * ncols;
   hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, dw, db, num_wg, ny, nz,
                      COB, RW, Cin, Cout, KK, scale, accumulate);
+  TDS_LAUNCH_CHECK();
   return 0;
 }

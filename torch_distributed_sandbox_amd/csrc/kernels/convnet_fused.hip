@@ -44,153 +44,6 @@ __device__ __forceinline__ int l1_koff(int k) {
   return (k % 5) * L1_XS + (k / 5);
 }
 
-__global__ __launch_bounds__(256) void l1_conv_kernel(const float* __restrict__ x, const float* __restrict__ w1,
-                                                      const float* __restrict__ b1, const float* __restrict__ aff,
-                                                      uint4* __restrict__ p1, uint8_t* __restrict__ idx1, int B,
-                                                      int H, int W) {
-  __shared__ __attribute__((aligned(16))) float xs[L1_XR * L1_XS];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int li = lane & 15, g = lane >> 4;
-  const int P = H / 2, PW = W / 2;
-  const int tiles_c = (W + L1_TC - 1) / L1_TC, tiles_r = (H + L1_TR - 1) / L1_TR;
-  const int per_img = tiles_c * tiles_r, total = per_img * B;
-
-  // A operand (weights) in registers: lane -> co = li, k = 4s + g
-  float wa[7];
-#pragma unroll
-  for (int s = 0; s < 7; ++s) {
-    const int k = 4 * s + g;
-    wa[s] = k < 25 ? w1[li * 25 + (k % 5) * 5 + (k / 5)] : 0.f;
-  }
-  int koff[7];
-#pragma unroll
-  for (int s = 0; s < 7; ++s) koff[s] = l1_koff(4 * s + g);
-
-  // per-lane epilogue constants for co = 4g + r: z = ea * (acc + b1) + eb = ea * acc + ebb
-  float ea[4], ebb[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    ea[r] = aff[4 * g + r];
-    ebb[r] = fmaf(ea[r], b1[4 * g + r], aff[16 + 4 * g + r]);
-  }
-
-  // x tile staging: LDS column 0 <-> global column c0-4 (16-B aligned since W % 4 == 0),
-  // 20 rows x 18 float4; the next tile's loads are issued before this tile's MFMAs.
-  constexpr int NV = L1_XR * 18;
-  constexpr int PER = (NV + 255) / 256;
-  float4 pre[PER];
-  auto load_tile = [&](int t) {
-    const int b = t / per_img, rem = t - b * per_img;
-    const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
-    const float* xb = x + (int64_t)b * H * W;
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = tid + 256 * u;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < NV) {
-        const int rr = e / 18, cv = e - rr * 18;
-        const int gr = r0 - 2 + rr, gc = c0 - 4 + 4 * cv;
-        if (gr >= 0 && gr < H && gc >= 0 && gc < W) v = *reinterpret_cast<const float4*>(xb + (int64_t)gr * W + gc);
-      }
-      pre[u] = v;
-    }
-  };
-  int t = xcd_remap(blockIdx.x, gridDim.x);
-  if (t < total) load_tile(t);
-  for (; t < total; t += gridDim.x) {
-    const int b = t / per_img, rem = t - b * per_img;
-    const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int e = tid + 256 * u;
-      if (e < NV) {
-        const int rr = e / 18, cv = e - rr * 18;
-        *reinterpret_cast<float4*>(xs + rr * L1_XS + 4 * cv) = pre[u];
-      }
-    }
-    __syncthreads();
-    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
-#pragma unroll
-    for (int rp = 0; rp < 2; ++rp) {
-#pragma unroll
-      for (int sp = 0; sp < 2; ++sp) {
-        // 4 tiles: rows (4wv + 2rp + {0,1}) x segments (2sp + {0,1}) of 16 pixels
-        f32x4 acc[2][2];
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-          for (int c = 0; c < 2; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int s = 0; s < 7; ++s) {
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int c = 0; c < 2; ++c) {
-              const int row = 4 * wv + 2 * rp + a, seg = 2 * sp + c;
-              const float bv = xs[row * L1_XS + 2 + seg * 16 + li + koff[s]];  // +2: tile origin is c0-4
-              acc[a][c] = mfma16x4(wa[s], bv, acc[a][c]);
-            }
-        }
-        {
-          // BN1 affine -> 2x2 max-pool (first max in scan order; torch's NaN rule on the
-          // rare NaN window) -> ReLU -> bf16 hi|lo record + 1-byte argmax
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            const int col = c0 + (2 * sp + c) * 16 + li;     // conv column of this lane
-            const int prow = (r0 + 4 * wv + 2 * rp) >> 1;    // pooled row
-            const int pcol = col >> 1;
-            float pv[4], zz[4][4];
-            uint32_t ixw = 0;
-            float nsum = 0.f;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float z0 = fmaf(ea[r], acc[0][c][r], ebb[r]);
-              const float z1 = fmaf(ea[r], acc[1][c][r], ebb[r]);
-              const float z0n = dpp_xor1(z0);
-              const float z1n = dpp_xor1(z1);
-              zz[r][0] = z0; zz[r][1] = z0n; zz[r][2] = z1; zz[r][3] = z1n;
-              float m = z0;
-              uint32_t a = 0;
-              if (z0n > m) { m = z0n; a = 1; }
-              if (z1 > m) { m = z1; a = 2; }
-              if (z1n > m) { m = z1n; a = 3; }
-              pv[r] = fmaxf(m, 0.f);
-              ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);  // bit 2: ReLU passes the gradient
-              nsum += (z0 + z0n) + (z1 + z1n);
-            }
-            if (__builtin_amdgcn_ballot_w64(isnan(nsum)) != 0) {
-              // rare NaN window (wave-uniform branch): torch's rule, update when
-              // (v > max || isnan(v)) in scan order; relu(NaN) = NaN
-              ixw = 0;
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                float m = zz[r][0];
-                uint32_t a = 0;
-#pragma unroll
-                for (int q = 1; q < 4; ++q)
-                  if (zz[r][q] > m || isnan(zz[r][q])) { m = zz[r][q]; a = q; }
-                pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
-                ixw |= (a | (m > 0.f ? 4u : 0u)) << (8 * r);
-              }
-            }
-            uint32_t h01, l01, h23, l23;
-            split2_bf16(pv[0], pv[1], h01, l01);
-            split2_bf16(pv[2], pv[3], h23, l23);
-            if ((li & 1) == 0 && prow < P && pcol < PW) {
-              const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
-              uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
-              dst[g] = make_uint2(h01, h23);
-              dst[4 + g] = make_uint2(l01, l23);
-              reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] = ixw;
-            }
-          }
-        }
-      }
-    }
-  }
-}
-
 // conv1 on v_mfma_f32_16x16x32_bf16 with the bf16x3 split (bf16x3.h): K = 32 slots per lane
 // group g: taps (ky = g, kx = 0..4) and the row-4 taps spread over g = 0 (kx 0..2) and g = 1
 // (kx 3, 4); the rest are zero-weight pads.  x is staged in LDS as one word per value
@@ -466,85 +319,8 @@ __global__ void bn_bwd_finalize2_kernel(const double* __restrict__ partial, int 
   }
 }
 
-// ============================================================================ dy2 build
-// thread = (pooled window, 4 channels).  dz = g2m at the window's argmax (of the BN2
-// output z, first max in scan order), dy2 = k1*dz + k2*y2 + k3 for all 4 pixels,
-// written as bf16 hi|lo (64-channel records).  Pixels of an unpooled last row/col
-// (odd P) get dz = 0.
-__global__ __launch_bounds__(256) void dy2_build_kernel(const float4* __restrict__ y2, const float* __restrict__ g2m,
-                                                        const float* __restrict__ aff2, const float* __restrict__ kbuf,
-                                                        uint2* __restrict__ dy2, int B, int P, int Q) {
-  const int PH = (P + 1) / 2;
-  const int64_t total = (int64_t)B * PH * PH * 8;
-  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
-    const int c4 = (int)(e & 7);
-    const int64_t w = e >> 3;
-    const int wx = (int)(w % PH);
-    const int64_t t = w / PH;
-    const int wy = (int)(t % PH);
-    const int b = (int)(t / PH);
-    const bool pooled = wy < Q && wx < Q;
-    float a[4], bb[4], k1[4], k2[4], k3[4];
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      const int c = 4 * c4 + cc;
-      a[cc] = aff2[c];
-      bb[cc] = aff2[32 + c];
-      k1[cc] = kbuf[c];
-      k2[cc] = kbuf[32 + c];
-      k3[cc] = kbuf[64 + c];
-    }
-    float y[4][4];
-    bool inb[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int r = 2 * wy + (q >> 1), cidx = 2 * wx + (q & 1);
-      inb[q] = r < P && cidx < P;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (inb[q]) v = y2[(((int64_t)b * P + r) * P + cidx) * 8 + c4];
-      y[q][0] = v.x; y[q][1] = v.y; y[q][2] = v.z; y[q][3] = v.w;
-    }
-    float gv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (pooled) {
-      const float4 gg = g2m_planar4(g2m, b, c4, wy, wx, Q);
-      gv[0] = gg.x; gv[1] = gg.y; gv[2] = gg.z; gv[3] = gg.w;
-    }
-    int am[4];
-#pragma unroll
-    for (int cc = 0; cc < 4; ++cc) {
-      float m = a[cc] * y[0][cc] + bb[cc];
-      int ai = 0;
-#pragma unroll
-      for (int q = 1; q < 4; ++q) {
-        const float z = a[cc] * y[q][cc] + bb[cc];
-        if (z > m || isnan(z)) { m = z; ai = q; }
-      }
-      am[cc] = pooled ? ai : -1;
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (!inb[q]) continue;
-      float d[4];
-#pragma unroll
-      for (int cc = 0; cc < 4; ++cc) {
-        const float dz = am[cc] == q ? gv[cc] : 0.f;
-        d[cc] = fmaf(k1[cc], dz, fmaf(k2[cc], y[q][cc], k3[cc]));
-      }
-      uint32_t h01, l01, h23, l23;
-      split2_bf16(d[0], d[1], h01, l01);
-      split2_bf16(d[2], d[3], h23, l23);
-      const int r = 2 * wy + (q >> 1), cidx = 2 * wx + (q & 1);
-      uint2* rec = dy2 + (((int64_t)b * P + r) * P + cidx) * 16;  // 128-B record = 16 x 8 B
-      rec[c4] = make_uint2(h01, h23);
-      rec[8 + c4] = make_uint2(l01, l23);
-    }
-  }
-}
 
-// ============================================================================ layer-1 backward (sparse)
-// Workgroup tile: 8 x 32 pooled pixels (x tile 20 x 68 in LDS).  Thread (c = tid & 15,
-// slot = tid >> 4) owns channel c for pooled pixels slot, slot+16, ... of the tile and
-// accumulates: sdz and sdzx[25] (dz * xpatch); sum dz*y1 follows in closed form.
+// layer-1 backward tile: 8 pooled rows x 32 pooled columns (x tile 20 rows incl. the halo)
 constexpr int LB_PR = 8, LB_PC = 32;
 constexpr int LB_XR = 2 * LB_PR + 4;
 constexpr int LB_XS = 76;  // LDS x row stride (floats); column 0 <-> global column 2*pc0 - 4
@@ -555,109 +331,6 @@ constexpr int LB_V = LB_V_DP + LB_V_PH + LB_V_ID + LB_V_X;  // 16-B vectors stag
 // The argmax byte carries the ReLU mask in bit 2 (set by l1_conv: pooled max > 0), so the
 // backward never reads p1 (720 MB of 64-B hi|lo records at the bench shape).
 constexpr int LB_PER = (LB_V + 255) / 256;
-__global__ __launch_bounds__(256) void l1_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dp1,
-                                                     const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
-                                                     const float* __restrict__ w1, const float* __restrict__ b1,
-                                                     double* __restrict__ partial, int B, int H, int W) {
-  // LDS: dp1 tile [256][16] f32 | argmax tile [256][16] u8 (bit 2 = ReLU mask) | x tile
-  __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LB_XR * LB_XS * 4];
-  __shared__ float red[4][16][LB_NACC + 1];
-  float* dps = reinterpret_cast<float*>(lds);
-  unsigned short* phs = nullptr;
-  uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 64);
-  float* xs = reinterpret_cast<float*>(lds + LB_NP * 80);
-  const int tid = threadIdx.x, c = tid & 15, slot = tid >> 4;
-  const int P = H / 2, PW = W / 2;
-  const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
-  const int per_img = tiles_c * tiles_r, total = per_img * B;
-  float acc[LB_NACC];  // [0] sum dz, [1] unused (sum dz*y1 = w1 . sum dz*x + b1 sum dz, in l1_finalize), [2..] sum dz*x
-#pragma unroll
-  for (int i = 0; i < LB_NACC; ++i) acc[i] = 0.f;
-
-  uint4 pre[LB_PER];
-  auto load_tile = [&](int t) {
-    const int b = t / per_img, rem = t - b * per_img;
-    const int pr0 = (rem / tiles_c) * LB_PR, pc0 = (rem % tiles_c) * LB_PC;
-#pragma unroll
-    for (int u = 0; u < LB_PER; ++u) {
-      int e = tid + 256 * u;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < LB_V_DP + LB_V_PH + LB_V_ID) {
-        int q, nq;
-        if (e < LB_V_DP) { q = e & 3; nq = 4; e >>= 2; }
-        else if (e < LB_V_DP + LB_V_PH) { e -= LB_V_DP; q = e & 1; nq = 2; e >>= 1; }
-        else { e -= LB_V_DP + LB_V_PH; q = 0; nq = 1; }
-        const int gpr = pr0 + e / LB_PC, gpc = pc0 + e % LB_PC;
-        if (gpr < P && gpc < PW) {
-          const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
-          if (nq == 4) v = reinterpret_cast<const uint4*>(dp1)[rec * 4 + q];
-          else if (nq == 2) v = p1[rec * 4 + q];
-          else v = reinterpret_cast<const uint4*>(idx1)[rec];
-        }
-      } else if (e < LB_V) {
-        e -= LB_V_DP + LB_V_PH + LB_V_ID;
-        const int rr = e / 18, cv = e - rr * 18;
-        const int gr = 2 * pr0 - 2 + rr, gc = 2 * pc0 - 4 + 4 * cv;
-        if (gr >= 0 && gr < H && gc >= 0 && gc < W)
-          v = *reinterpret_cast<const uint4*>(x + ((int64_t)b * H + gr) * W + gc);
-      }
-      pre[u] = v;
-    }
-  };
-  auto store_tile = [&]() {
-#pragma unroll
-    for (int u = 0; u < LB_PER; ++u) {
-      int e = tid + 256 * u;
-      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[e] = pre[u];
-      else if (e < LB_V_DP + LB_V_PH) reinterpret_cast<uint4*>(phs)[e - LB_V_DP] = pre[u];
-      else if (e < LB_V_DP + LB_V_PH + LB_V_ID) reinterpret_cast<uint4*>(ids)[e - LB_V_DP - LB_V_PH] = pre[u];
-      else if (e < LB_V) {
-        e -= LB_V_DP + LB_V_PH + LB_V_ID;
-        const int rr = e / 18, cv = e - rr * 18;
-        *reinterpret_cast<uint4*>(xs + rr * LB_XS + 4 * cv) = pre[u];
-      }
-    }
-  };
-
-  int t = xcd_remap(blockIdx.x, gridDim.x);
-  if (t < total) load_tile(t);
-  for (; t < total; t += gridDim.x) {
-    __syncthreads();
-    store_tile();
-    __syncthreads();
-    if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
-    for (int pp = slot; pp < LB_NP; pp += 16) {
-      const int ab = ids[pp * 16 + c];
-      if (!(ab & 4)) continue;  // pooled value <= 0 (or out of range): ReLU blocks the gradient
-      const float dz = dps[pp * 16 + c];
-      const int a = ab & 3;
-      const int pr = pp / LB_PC, pc = pp - (pp / LB_PC) * LB_PC;
-      const int lr = 2 * pr + (a >> 1), lc = 2 * pc + (a & 1) + 2;  // patch origin in the x tile
-      const float* xp = xs + lr * LB_XS + lc;
-#pragma unroll
-      for (int ky = 0; ky < 5; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 5; ++kx) acc[2 + ky * 5 + kx] += dz * xp[ky * LB_XS + kx];
-      acc[0] += dz;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < LB_NACC; ++i) {
-    // lanes l, l+16, l+32, l+48 of a wave hold the same channel
-    float v = acc[i];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if ((tid & 63) < 16) red[tid >> 6][c][i] = v;
-  }
-  __syncthreads();
-  for (int e = tid; e < 16 * LB_NACC; e += 256) {
-    const int cc = e / LB_NACC, i = e - cc * LB_NACC;
-    double s = 0.0;
-    for (int k = 0; k < 4; ++k) s += red[k][cc][i];
-    partial[((int64_t)blockIdx.x * 16 + cc) * LB_NACC + i] = s;
-  }
-}
 
 // ============================================================================ layer-1 backward (MFMA)
 // The sums the sparse kernel above forms with 25 VALU FMAs per active (pooled pixel,
@@ -987,18 +660,14 @@ int tds_fused_num_wg(int per_cu) {
 void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
                  double* gram, double* sums, hipStream_t st) {
   hipLaunchKernelGGL(l1_gram_kernel, dim3(1), dim3(256), 0, st, ac_sum, strips, x, B, H, W, w1, gram, sums);
+  TDS_LAUNCH_CHECK();
 }
 
-// TDS_L1_CONV=1 selects the exact-fp32 MFMA conv1 (l1_conv_kernel); default: bf16x3 (l1_conv_bf3_kernel)
 void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
                   int B, int H, int W, hipStream_t st) {
-  const char* e = std::getenv("TDS_L1_CONV");
-  if (e && std::atoi(e) == 1)
-    hipLaunchKernelGGL(l1_conv_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
-                       idx1, B, H, W);
-  else
-    hipLaunchKernelGGL(l1_conv_bf3_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
-                       idx1, B, H, W);
+  hipLaunchKernelGGL(l1_conv_bf3_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
+                     idx1, B, H, W);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
@@ -1006,50 +675,36 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
                              float* running_var, int64_t* num_batches, float* aff, hipStream_t st) {
   hipLaunchKernelGGL(bn_finalize_shifted_kernel, dim3(1), dim3(64), 0, st, partial, C, nchunk, n, shift, eps, momentum,
                      gamma, beta, stats, running_mean, running_var, num_batches, aff);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st) {
   hipLaunchKernelGGL(x_border_kernel, dim3(82, 8), dim3(256), 0, st, x, strips, B, H, W);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
                          hipStream_t st) {
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(n), dim3(256), 0, st, in, out, nchunk, inner, ostride, kstride);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
                           float* dgamma, float* dbeta, float* kbuf, hipStream_t st) {
   hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(1), dim3(64), 0, st, partial, C, nchunk, n, gamma, stats, dgamma,
                      dbeta, kbuf, nullptr);
+  TDS_LAUNCH_CHECK();
 }
 
-void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const float* kbuf, void* dy2, int B, int P,
-                   hipStream_t st) {
-  const int Q = P / 2, PH = (P + 1) / 2;
-  const int64_t total = (int64_t)B * PH * PH * 8;
-  int64_t g = (total + 255) / 256;
-  if (g > 8192) g = 8192;
-  hipLaunchKernelGGL(dy2_build_kernel, dim3((unsigned)g), dim3(256), 0, st, reinterpret_cast<const float4*>(y2),
-                     g2m, aff2, kbuf, reinterpret_cast<uint2*>(dy2), B, P, Q);
-}
-
-// TDS_L1_BWD=1 selects the sparse VALU kernel (l1_bwd_kernel); default: l1_bwd_mfma_kernel
-static bool l1_bwd_sparse() {
-  const char* e = std::getenv("TDS_L1_BWD");  // per call: in-process A/B
-  return e && std::atoi(e) == 1;
-}
-
-int tds_l1_bwd_rows(int nwg) { return l1_bwd_sparse() ? nwg : 4 * nwg; }
+int tds_l1_bwd_rows(int nwg) { return 4 * nwg; }
 
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
                 double* partial, int nwg, int B, int H, int W, hipStream_t st) {
-  if (!l1_bwd_sparse()) {
-    hipLaunchKernelGGL(l1_bwd_mfma_kernel, dim3(nwg), dim3(256), 0, st, x, dp1, reinterpret_cast<const uint4*>(p1),
-                       idx1, partial, B, H, W);
-    return;
-  }
-  hipLaunchKernelGGL(l1_bwd_kernel, dim3(nwg), dim3(256), 0, st, x, dp1, reinterpret_cast<const uint4*>(p1), idx1, w1,
-                     b1, partial, B, H, W);
+  (void)w1;
+  (void)b1;
+  hipLaunchKernelGGL(l1_bwd_mfma_kernel, dim3(nwg), dim3(256), 0, st, x, dp1, reinterpret_cast<const uint4*>(p1), idx1,
+                     partial, B, H, W);
+  TDS_LAUNCH_CHECK();
 }
 
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
@@ -1057,4 +712,5 @@ void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const
                      float scale, hipStream_t st) {
   hipLaunchKernelGGL(l1_finalize_kernel, dim3(1), dim3(64), 0, st, bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1,
                      dgamma1, dbeta1, scale);
+  TDS_LAUNCH_CHECK();
 }

@@ -265,24 +265,32 @@ using namespace tds;
 
 void tds_relu_fwd(const float* x, float* y, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(relu_fwd_kernel, dim3(grid_for(n, 256, 16)), dim3(256), 0, st, x, y, n);
+  TDS_LAUNCH_CHECK();
 }
 void tds_relu_bwd(const float* g, const float* out, float* dx, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(n, 256, 16)), dim3(256), 0, st, g, out, dx, n);
+  TDS_LAUNCH_CHECK();
 }
 void tds_maxpool2_fwd(const float* x, float* y, uint8_t* idx, int64_t planes, int H, int W, hipStream_t st) {
   const int64_t total = planes * (H / 2) * (int64_t)(W / 2);
   if (total == 0) return;
   hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(total, 256, 4)), dim3(256), 0, st, x, y, idx, planes, H, W);
+  TDS_LAUNCH_CHECK();
 }
 void tds_maxpool2_bwd(const float* gy, const uint8_t* idx, float* gx, int64_t planes, int H, int W, hipStream_t st) {
   const int64_t total = planes * H * (int64_t)W;
   if (total == 0) return;
   hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(total, 256, 4)), dim3(256), 0, st, gy, idx, gx, planes, H, W);
+  TDS_LAUNCH_CHECK();
 }
 void tds_upsample_bilinear_u8(const uint8_t* src, float* dst, int B, int h, int w, int H, int W, hipStream_t st) {
   if ((int64_t)B * H * W == 0) return;
-  if (w > kUpsMaxW || h < 1 || B > 65535) return;  // the op wrapper rejects these shapes (ops.cpp)
+  if (w > kUpsMaxW || h < 1 || B > 65535) {  // the op wrapper rejects these shapes first (ops.cpp)
+    tds_launch_fail("upsample_bilinear_u8: unsupported shape");
+    return;
+  }
   hipLaunchKernelGGL(upsample_bilinear_u8_kernel, dim3(H, B), dim3(256), 0, st, src, dst, B, h, w, H, W);
+  TDS_LAUNCH_CHECK();
 }
 void tds_sgd_multi(const SgdChunkTable& tab, float lr, float wd, float momentum, float dampening, int nesterov,
                    int first_step, int64_t max_numel, hipStream_t st) {
@@ -291,15 +299,19 @@ void tds_sgd_multi(const SgdChunkTable& tab, float lr, float wd, float momentum,
   if (gx > 1024) gx = 1024;
   hipLaunchKernelGGL(sgd_multi_kernel, dim3(gx, tab.n), dim3(256), 0, st, tab, lr, wd, momentum, dampening,
                      nesterov, first_step);
+  TDS_LAUNCH_CHECK();
 }
 void tds_cross_entropy(const float* logits, const int64_t* labels, float* row_loss, float* dlogits, float* loss,
                        float* inv_count, int M, int N, int64_t ignore_index, float label_smoothing, hipStream_t st) {
   const int rows_per_block = 4;
   hipLaunchKernelGGL(ce_rows_kernel, dim3((M + rows_per_block - 1) / rows_per_block), dim3(64 * rows_per_block), 0, st,
                      logits, labels, row_loss, dlogits, M, N, ignore_index, label_smoothing);
+  TDS_LAUNCH_CHECK();
   hipLaunchKernelGGL(ce_finalize_kernel, dim3(1), dim3(256), 0, st, row_loss, labels, dlogits, loss, inv_count, M, N,
                      ignore_index);
+  TDS_LAUNCH_CHECK();
 }
 void tds_scale_by_device_scalar(const float* in, const float* s, float* out, int64_t n, hipStream_t st) {
   hipLaunchKernelGGL(scale_by_device_scalar_kernel, dim3(grid_for(n, 256, 4)), dim3(256), 0, st, in, s, out, n);
+  TDS_LAUNCH_CHECK();
 }

@@ -1,0 +1,424 @@
+// Fused ConvNet head on the pooled-blocked ya / g2m layout (pooled_layout.h): BN2 affine + ReLU
+// + fc forward, and the fc / ReLU backward up to the pooled gradient g2m with the BN2 backward
+// sums (reference: mnist_onegpu.py:21-24,29-30 -> native_batch_norm, clamp_min,
+// max_pool2d_with_indices, addmm and their backward ops).
+//
+// The max-pool itself is resolved by the conv2 forward: it writes ya = y2 at each window's
+// argmax (conv2_fwd2.hip), so the head streams ya (B x 72 MB at 3000^2) instead of y2 (B x
+// 288 MB) and both directions are pure streams over the fc weight (720 MB):
+//
+//   forward : X = relu(a*ya + b);  logits[b][j] = sum X[b][k] W[j][k]           (+ X rows for
+//             DDP's activation exchange when asked)
+//   backward: g = dl W, g2m = g [z > 0] (planar, for the conv2 backward), BN2 sums
+//             (sum g2m, sum g2m*ya) per channel, dW = scale dl^T X and/or W -= lr dW (SGD
+//             step fused into the backward at world size 1)
+//
+// Workgroup: one channel c and a band of HP_BAND block rows (4 pooled rows each) over the FULL
+// pooled width: the fc weight of (class j, channel c, 4 pooled rows) is then one contiguous run
+// of 4Q floats (12 KiB at 3000^2) and ya of (image, channel, block row) one run of Q8 blocks
+// (12 KiB), walked front to back (256-column spans with 1 KiB weight runs streamed at 2.7 TB/s).
+// 256 threads sweep a block row in chunks of 32 blocks (256 pooled columns): wave w takes
+// pooled row w of the block row, lane l block l/2 of the chunk, columns 4*(l%2) .. +3.  Per chunk
+// and thread:
+//   ya  : one float4 per image (the 4 waves together read one 4 KiB run per image),
+//   W   : one 4-float group per class from the fc's own (c, h, w) layout at the same row and
+//         columns -- a wave-instruction covers one 1 KiB row run.  A row starts at a 16-B boundary
+//         only when (c*Q*Q + y*Q) % 4 == 0 (for Q = 750 every odd row is 8 B off): the group is
+//         then moved as two float2 (or four floats), picked per wave, so no access straddles a
+//         16-B granule -- misaligned dwordx4 stores of the weight update cost 14% of the backward,
+//   g2m : one float4 per image (same index as ya), dW / updated W: one 4-float group per class.
+// No LDS and no barriers in the stream: the next chunk's loads are issued before the current
+// one is reduced.  64-bit indexing throughout (no buffer descriptors).
+#include "common.h"
+#include "launchers.h"
+#include "pooled_layout.h"
+
+namespace tds {
+
+constexpr int HP_THREADS = 256;
+constexpr int HP_BAND = 4;                  // block rows per workgroup
+constexpr int HP_MAXB = 8;                  // images per pass (larger batches run in passes)
+
+struct HPGrid {
+  int nband;
+  __host__ __device__ int per_channel() const { return nband; }
+};
+
+__host__ __device__ inline HPGrid hp_grid(const PBGeom& g) { return HPGrid{(g.Q4 + HP_BAND - 1) / HP_BAND}; }
+
+__device__ __forceinline__ float hp_relu(float z) { return z > 0.f ? z : (isnan(z) ? z : 0.f); }
+
+struct HPThread {
+  int blk, prow, half, part;  // block, pooled row in the block (= wave), column half, float4 in the block
+  __device__ HPThread(int chunk) {
+    const int lane = threadIdx.x & 63;
+    prow = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    blk = chunk * 32 + (lane >> 1);
+    half = lane & 1;
+    part = prow * 2 + half;
+  }
+};
+
+// 4 consecutive floats of a weight row at p; al = (element index of p) % 4, wave-uniform
+__device__ __forceinline__ void hp_st4(float* p, int al, float4 v) {
+  if (al == 0) {
+    *reinterpret_cast<float4*>(p) = v;
+  } else if (al == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y);
+    *reinterpret_cast<float2*>(p + 2) = make_float2(v.z, v.w);
+  } else {
+    p[0] = v.x;
+    p[1] = v.y;
+    p[2] = v.z;
+    p[3] = v.w;
+  }
+}
+
+// this thread's weight-row geometry for block row R: element offset of column px0 of row py in
+// plane (j = 0, c) and its wave-uniform alignment class; nvalid = columns px0 .. px0+nvalid-1
+// inside the image.  Loads never branch per lane: a group crossing the row end is read at the
+// row's last 4 columns (shifted by sh, values re-aligned with selects), rows past the image at
+// row Q-1 (masked), so every lane of a wave issues the same access form.
+struct HPRow {
+  int64_t off, ldoff;
+  int al, nvalid, sh;
+  __device__ HPRow(const PBGeom& g, const HPThread& th, int c, int R) {
+    const int Q = g.Q;
+    const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
+    const int64_t rowbase = (int64_t)c * Q * Q + (int64_t)(py < Q ? py : Q - 1) * Q;
+    nvalid = (py < Q && th.blk < g.Q8) ? max(0, min(4, Q - px0)) : 0;
+    al = __builtin_amdgcn_readfirstlane((int)(rowbase & 3));  // j*32*Q*Q % 4 == 0 for every class
+    off = rowbase + px0;
+    const int pxl = min(px0, max(0, Q - 4));  // Q >= 4 (supported(): H >= 16)
+    sh = px0 - pxl;
+    ldoff = rowbase + pxl;
+  }
+};
+
+template <int AL>
+__device__ __forceinline__ float4 hp_ld4a(const float* p) {
+  if constexpr (AL == 0) return *reinterpret_cast<const float4*>(p);
+  if constexpr (AL == 2) {
+    const float2 u = *reinterpret_cast<const float2*>(p), v = *reinterpret_cast<const float2*>(p + 2);
+    return make_float4(u.x, u.y, v.x, v.y);
+  }
+  return make_float4(p[0], p[1], p[2], p[3]);
+}
+
+// loads of one chunk: ya float4 per image, weight 4-groups per class (zeros outside the image)
+template <int NB>
+struct HPLoad {
+  float4 y[NB], w[10];
+  template <int AL>
+  __device__ __forceinline__ void issue_w(const float* W, int64_t QQ, const HPRow& rw, int NC) {
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+      if (j < NC) w[j] = hp_ld4a<AL>(W + (int64_t)j * 32 * QQ + rw.ldoff);
+  }
+  __device__ __forceinline__ void issue(const float* __restrict__ ya, const float* W, const PBGeom& g, const HPThread& th,
+                                        int c, int R, int b0, int NC) {
+    const int64_t plane = g.plane(), QQ = (int64_t)g.Q * g.Q;
+    const int bc = th.blk < g.Q8 ? th.blk : g.Q8 - 1;  // idle lanes of the last chunk: a valid block
+    const int64_t yi = (((int64_t)c * g.Q4 + R) * g.Q8 + bc) * 32 + th.part * 4;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) y[b] = *reinterpret_cast<const float4*>(ya + (int64_t)(b0 + b) * 32 * plane + yi);
+    const HPRow rw(g, th, c, R);
+    if (rw.al == 0) issue_w<0>(W, QQ, rw, NC);
+    else if (rw.al == 2) issue_w<2>(W, QQ, rw, NC);
+    else issue_w<1>(W, QQ, rw, NC);
+    // re-align the shifted edge groups, zero what lies outside the image (and classes >= NC)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const float e[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
+      float o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float v = e[k];
+        if (rw.sh > 0) v = (k + rw.sh < 4) ? e[(k + rw.sh) & 3] : 0.f;
+        o[k] = (j < NC && k < rw.nvalid) ? v : 0.f;
+      }
+      w[j] = make_float4(o[0], o[1], o[2], o[3]);
+    }
+  }
+};
+
+// store a 4-group of class j of the weight layout at this thread's (row, 4 columns), inside the image only
+__device__ __forceinline__ void hp_store4(float* out, const PBGeom& g, const HPRow& rw, int j, float4 v) {
+  if (rw.nvalid == 0) return;
+  float* p = out + (int64_t)j * 32 * g.Q * (int64_t)g.Q + rw.off;
+  if (rw.nvalid == 4) {
+    hp_st4(p, rw.al, v);
+  } else {
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < rw.nvalid) p[k] = e[k];
+  }
+}
+
+// Forward.  partial[blk][B*NC] (fp64): this workgroup's share of logits[b][j] for images
+// b0 .. b0+NB-1; xout (optional): X in the fc's flatten order, [B][32*Q*Q].
+template <int NB>
+__global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __restrict__ ya,
+                                                                 const float* __restrict__ W,
+                                                                 const float* __restrict__ aff2,
+                                                                 double* __restrict__ partial,
+                                                                 float* __restrict__ xout, PBGeom g, int Btot, int b0,
+                                                                 int NC) {
+  __shared__ float red[HP_THREADS / 64][HP_MAXB * 10];
+  const HPGrid hg = hp_grid(g);
+  const int wg = blockIdx.x;
+  const int c = wg / hg.per_channel(), band = wg - c * hg.per_channel();
+  const float a = aff2[c], bb = aff2[32 + c];
+  const int Q = g.Q;
+  const int64_t QQ = (int64_t)Q * Q, K = 32 * QQ;
+  float acc[NB][10];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) acc[b][j] = 0.f;
+  // iteration i: block row R0 + i / nch, chunk (32 blocks) i % nch of the row
+  const int nch = (g.Q8 + 31) / 32;
+  const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
+  HPLoad<NB> cur, nxt;
+  if (nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
+#pragma unroll 1
+  for (int i = 0; i < nit; ++i) {
+    const int R = R0 + i / nch;
+    const HPThread th(i % nch);
+    if (i + 1 < nit)  // next chunk in flight
+      nxt.issue(ya, W, g, HPThread((i + 1) % nch), c, R0 + (i + 1) / nch, b0, NC);
+    const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
+    const bool rok = th.blk < g.Q8 && py < Q;
+    float x[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float yy[4] = {cur.y[b].x, cur.y[b].y, cur.y[b].z, cur.y[b].w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) x[b][k] = (rok && px0 + k < Q) ? hp_relu(fmaf(a, yy[k], bb)) : 0.f;
+    }
+    if (xout != nullptr && rok) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (px0 + k < Q) xout[(int64_t)(b0 + b) * K + c * QQ + (int64_t)py * Q + px0 + k] = x[b][k];
+    }
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      const float4 w4 = cur.w[j];
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        acc[b][j] = fmaf(x[b][0], w4.x, fmaf(x[b][1], w4.y, fmaf(x[b][2], w4.z, fmaf(x[b][3], w4.w, acc[b][j]))));
+    }
+    cur = nxt;
+  }
+  // deterministic workgroup reduction: waves (DPP), then 4 wave partials in fixed order
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      if (j < NC) {
+        const float s = wave_sum(acc[b][j]);
+        if (lane == 0) red[wv][b * 10 + j] = s;
+      }
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NB * NC; i += HP_THREADS) {
+    const int b = i / NC, j = i - b * NC;
+    const double s = (((double)red[0][b * 10 + j] + (double)red[1][b * 10 + j]) + (double)red[2][b * 10 + j]) +
+                     (double)red[3][b * 10 + j];
+    partial[(int64_t)wg * Btot * NC + (b0 + b) * NC + j] = s;
+  }
+}
+
+// logits[i] = sums[i] + bias[i % NC]
+__global__ void head_logits_kernel(const double* __restrict__ sums, const float* __restrict__ bias,
+                                   float* __restrict__ logits, int BN, int NC) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < BN) logits[i] = (float)sums[i] + (bias ? bias[i % NC] : 0.f);
+}
+
+// Backward for images b0 .. b0+NB-1.
+//   g2m[b][c][py][px] = (sum_j dl[b][j] W[j][c][py][px]) * [a*ya + b > 0]   (planar [B][32][Q][Q])
+//   partial[c][pass*nblk + blk][2] = { sum g2m, sum g2m * ya }       (BN2 backward sums)
+//   dW[j][c][pos] (= or +=) scale * sum_b dl[b][j] X[b][c][pos]      (WITH_DW; ACC adds)
+//   Wupd = W - lr * dW                                               (UPD: SGD step fused)
+template <int NB, bool WITH_DW, bool ACC, bool UPD>
+__global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
+    const float* __restrict__ ya, const float* W, const float* __restrict__ aff2, const float* __restrict__ dl,
+    float* __restrict__ g2m, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass, int npass,
+    int NC, float scale, float lr) {
+  __shared__ float red[2][HP_THREADS / 64];
+  const HPGrid hg = hp_grid(g);
+  const int wg = blockIdx.x;
+  const int c = wg / hg.per_channel(), band = wg - c * hg.per_channel();
+  float dls[NB * 10];  // dlogits of this pass: wave-uniform, scalar loads
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int j = 0; j < 10; ++j) dls[b * 10 + j] = j < NC ? dl[(b0 + b) * NC + j] : 0.f;
+  const float a = aff2[c], bb = aff2[32 + c];
+  const int Q = g.Q;
+  const int64_t plane = g.plane();
+  float sdz = 0.f, sdy = 0.f;
+  const int nch = (g.Q8 + 31) / 32;
+  const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
+  HPLoad<NB> cur, nxt;
+  if (nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
+#pragma unroll 1
+  for (int i = 0; i < nit; ++i) {
+    const int R = R0 + i / nch;
+    const HPThread th(i % nch);
+    if (i + 1 < nit)  // next chunk in flight
+      nxt.issue(ya, W, g, HPThread((i + 1) % nch), c, R0 + (i + 1) / nch, b0, NC);
+    const bool bok = th.blk < g.Q8;
+    const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
+    const bool rok = bok && py < Q;
+    const HPRow rwg(g, th, c, R);
+    float x[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float yy[4] = {cur.y[b].x, cur.y[b].y, cur.y[b].z, cur.y[b].w};
+      float gm[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const bool ok = rok && px0 + k < Q;
+        const float z = fmaf(a, yy[k], bb);
+        float gs = 0.f;
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          const float wk = k == 0 ? cur.w[j].x : k == 1 ? cur.w[j].y : k == 2 ? cur.w[j].z : cur.w[j].w;
+          gs = fmaf(dls[b * 10 + j], wk, gs);
+        }
+        gm[k] = (ok && z > 0.f) ? gs : 0.f;
+        x[b][k] = ok ? hp_relu(z) : 0.f;
+        sdz += gm[k];
+        sdy = fmaf(gm[k], ok ? yy[k] : 0.f, sdy);
+      }
+      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]));  // planar, like a weight plane
+    }
+    if constexpr (WITH_DW) {
+      const HPRow& rw = rwg;
+#pragma unroll
+      for (int j = 0; j < 10; ++j) {
+        if (j < NC) {
+          float s[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float v = 0.f;
+#pragma unroll
+            for (int b = 0; b < NB; ++b) v = fmaf(dls[b * 10 + j], x[b][k], v);
+            s[k] = scale * v;
+          }
+          float4 d = make_float4(s[0], s[1], s[2], s[3]);
+          if constexpr (ACC) {  // later image passes add to the stored dW
+            if (rw.nvalid > 0) {
+              float* p = dW + (int64_t)j * 32 * Q * (int64_t)Q + rw.off;
+#pragma unroll
+              for (int k = 0; k < 4; ++k)
+                if (k < rw.nvalid) p[k] += s[k];
+            }
+          } else {
+            hp_store4(dW, g, rw, j, d);
+            if constexpr (UPD) {  // torch SGD: p -= lr * g
+              const float4 w = cur.w[j];
+              hp_store4(Wupd, g, rw, j, make_float4(w.x - lr * d.x, w.y - lr * d.y, w.z - lr * d.z, w.w - lr * d.w));
+            }
+          }
+        }
+      }
+    }
+    cur = nxt;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  sdz = wave_sum(sdz);
+  sdy = wave_sum(sdy);
+  if (lane == 0) {
+    red[0][wv] = sdz;
+    red[1][wv] = sdy;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int k = threadIdx.x;
+    const double s = (((double)red[k][0] + (double)red[k][1]) + (double)red[k][2]) + (double)red[k][3];
+    const int64_t nblk = (int64_t)hg.per_channel();
+    partial[(((int64_t)c * npass + pass) * nblk + band) * 2 + k] = s;
+  }
+}
+
+}  // namespace tds
+
+using namespace tds;
+
+int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // workgroups per channel
+int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
+
+// partial: double [32 * nblk][B*NC]; sums: double [B*NC]
+int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
+                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st) {
+  if (B < 1 || NC < 1 || NC > 10 || Q < 1) return -1;
+  const PBGeom g = pb_geom(Q);
+  const int nwg = 32 * hp_grid(g).per_channel();
+  for (int b0 = 0; b0 < B; b0 += HP_MAXB) {
+    const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
+#define TDS_HPF(NBV)                                                                                                   \
+  case NBV:                                                                                                            \
+    hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
+                       B, b0, NC);                                                                                     \
+    TDS_LAUNCH_CHECK();                                                                                                \
+    break;
+    switch (nb) {
+      TDS_HPF(1) TDS_HPF(2) TDS_HPF(3) TDS_HPF(4) TDS_HPF(5) TDS_HPF(6) TDS_HPF(7) TDS_HPF(8)
+      default: return -1;
+    }
+#undef TDS_HPF
+  }
+  const int BN = B * NC;
+  tds_reduce_partials(partial, sums, BN, nwg, BN, 0, BN, st);
+  hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);
+  TDS_LAUNCH_CHECK();
+  return 0;
+}
+
+// partial: double [32][npass * nblk][2], npass = ceil(B / 8)
+int tds_head_bwd_pb_npass(int B) { return (B + HP_MAXB - 1) / HP_MAXB; }
+
+int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
+                    double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr,
+                    hipStream_t st) {
+  if (B < 1 || NC < 1 || NC > 10 || Q < 1) return -1;
+  const int npass = tds_head_bwd_pb_npass(B);
+  if (Wupd && (!dW || npass != 1)) return -2;  // the fused SGD step needs the whole dW in one pass
+  const PBGeom g = pb_geom(Q);
+  const int nwg = 32 * hp_grid(g).per_channel();
+  for (int pass = 0; pass < npass; ++pass) {
+    const int b0 = pass * HP_MAXB;
+    const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
+    const bool acc = pass > 0;
+#define TDS_HPB_E(NBV, WD, AC, UP)                                                                                 \
+  hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2,     \
+                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr);
+#define TDS_HPB(NBV)                                   \
+  case NBV:                                            \
+    if (!dW) {                                         \
+      TDS_HPB_E(NBV, false, false, false)              \
+    } else if (acc) {                                  \
+      TDS_HPB_E(NBV, true, true, false)                \
+    } else if (Wupd) {                                 \
+      TDS_HPB_E(NBV, true, false, true)                \
+    } else {                                           \
+      TDS_HPB_E(NBV, true, false, false)               \
+    }                                                  \
+    TDS_LAUNCH_CHECK();                                \
+    break;
+    switch (nb) {
+      TDS_HPB(1) TDS_HPB(2) TDS_HPB(3) TDS_HPB(4) TDS_HPB(5) TDS_HPB(6) TDS_HPB(7) TDS_HPB(8)
+      default: return -1;
+    }
+#undef TDS_HPB
+#undef TDS_HPB_E
+  }
+  return 0;
+}

@@ -57,31 +57,24 @@ int tds_linear_fwd_skinny(const float* x, const float* W, const float* bias, flo
 int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float* dx, float* dW, float* db, int M,
                           int N, int64_t K, float scale, int acc_w, hipStream_t st);
 
-// ---- conv2_bf16x3.hip (NHWC, bf16x3 split MFMA)
+// ---- launch_status.hip (TDS_LAUNCH_CHECK, common.h)
+int tds_take_launch_error(char* buf, int n);  // 1 (and the message) if a launch failed since the last call
+void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  // test hook: a launch of any config
+
+// ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, bf16x3 split MFMA)
 void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t st);
-int tds_conv2_num_wg();
-void tds_conv2_fwd_bf16x3(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg,
-                          int B, int P, hipStream_t st);
-void tds_conv2_bwd_fused(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                         const short* wd, float* dp1, float* slab, float* dw, float* db, float scale, int nwg, int B,
-                         int P, hipStream_t st);
-int tds_conv2_fwd_version();
-int tds_conv2_fwd_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
-int tds_conv2_fwd2_num_wg();
-void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, float* y2, double* partial, int nwg, int B,
-                    int P, hipStream_t st);
-int tds_conv2_bwd_version();
-int tds_conv2_bwd_fused_num_wg();  // slab rows the fused backward needs (workgroups it launches)
-int tds_conv2_bwd2_num_wg();
-int tds_conv2_bwd3_num_wg();
+int tds_conv2_num_wg();  // CUs
+int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c);  // host: blocked tile order table
+void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st);
+int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
+void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
+// y2 [B,P,P,32]; ya pooled-blocked (pooled_layout.h), max/min of each 2x2 window by sign(gamma2)
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
+                    double* partial, const int* order, int nwg, int B, int P, hipStream_t st);
+int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
+void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, int nwg, int B, int P, hipStream_t st);
-void tds_conv2_bwd2(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, int nwg, int B, int P, hipStream_t st);
-void tds_conv2_dgrad_bf16x3(const void* dy2, const short* wd, float* dp1, int nwg, int B, int P, hipStream_t st);
-void tds_conv2_wgrad_bf16x3(const void* dy2, const void* p1, float* slab, float* dw, float* db, float scale, int nwg,
-                            int B, int P, hipStream_t st);
-int tds_conv2_lds_bytes(int which);
+                    const short* wd, float* dp1, float* slab, const int* order, int nwg, int B, int P, hipStream_t st);
 
 // ---- convnet_fused.hip
 int tds_fused_num_wg(int per_cu);
@@ -95,26 +88,23 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
 int tds_x_autocorr_num_wg(int B, int H, int W);  // partial rows tds_x_autocorr writes
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st);
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
-int tds_head_fwd_nblk(int Q);
-int tds_head_bwd_nblk(int Q);  // partial rows of tds_head_bwd (y2 path)
-int tds_head_fwd(const float* y2, const float* Wfc, const float* bias, const float* aff2, double* partial, double* sums,
-                 float* logits, float* xout, float* yaout, int B, int P, int NC, hipStream_t st);
-int tds_head_bwd_ya_max_batch();
-int tds_head_bwd_ya_nblk(int B, int P, int NC);
-bool tds_head_bwd_ya_supported(int B, int P, int NC);
-int tds_head_bwd_ya(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
-                    double* partial, int B, int P, int NC, float scale, float* Wupd, float lr, hipStream_t st);
-int tds_head_bwd(const float* y2, const float* Wfc, const float* aff2, const float* dlogits, float* dW, float* g2m,
-                 double* partial, int B, int P, int NC, float scale, hipStream_t st);
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
                          hipStream_t st);
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
                           float* dgamma, float* dbeta, float* kbuf, hipStream_t st);
-void tds_dy2_build(const float* y2, const float* g2m, const float* aff2, const float* kbuf, void* dy2, int B, int P,
-                   hipStream_t st);
 int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
                 double* partial, int nwg, int B, int H, int W, hipStream_t st);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);
+
+// ---- head_pb.hip (fc head on the pooled-blocked ya / g2m, pooled_layout.h)
+int64_t tds_pb_plane(int Q);  // floats per (image, channel) plane
+int tds_head_pb_nblk(int Q);  // workgroups per channel
+int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
+                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st);
+int tds_head_bwd_pb_npass(int B);
+int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
+                    double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr,
+                    hipStream_t st);

@@ -248,9 +248,11 @@ int tds_linear_fwd_skinny(const float* x, const float* W, const float* bias, flo
   else if (M <= 2) TDS_LF(2);
   else if (M <= 4) TDS_LF(4);
   else TDS_LF(8);
+  TDS_LAUNCH_CHECK();
 #undef TDS_LF
   hipLaunchKernelGGL(linear_fwd_reduce_kernel, dim3((M * N + 255) / 256), dim3(256), 0, st, partial, bias, out, M, N,
                      nblk);
+  TDS_LAUNCH_CHECK();
   return 0;
 }
 
@@ -267,6 +269,7 @@ int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float
   else if (M <= 2) TDS_LB(2);
   else if (M <= 4) TDS_LB(4);
   else TDS_LB(8);
+  TDS_LAUNCH_CHECK();
 #undef TDS_LB
   return 0;
 }
@@ -279,5 +282,6 @@ int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, 
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(linear_dw_mfma_kernel, dim3((unsigned)grid), dim3(256), 0, st, dy, x, dW, db, M, N, K, ldw,
                      scale, acc);
+  TDS_LAUNCH_CHECK();
   return 0;
 }

@@ -13,12 +13,16 @@ namespace tds {
 // (AC_RB + 4 rows x 12 columns: cols c-4 .. c+7) in registers: no LDS, no barriers (the
 // LDS-tiled form with two barriers per 16 x 64 tile ran at 0.19 ms, latency bound).  A wave
 // covers 256 consecutive columns, so every row load is a 1 KB run; neighbours' halo reloads hit
-// L2.  Requires B*H*W*4 < 2^31 (tds_x_autocorr_num_wg returns 0 beyond).  Each fp32 accumulator sums 4 * AC_RB = 32 products; waves reduce in fp32, the workgroup
-// in fp64 (partial[wg][42], slot 41 = plain sum).  Requires W % 4 == 0.
+// L2.  Loads go through one buffer descriptor per wave, based at the wave's first image: a
+// wave's lanes span at most two images of any size that matters, so lane offsets stay under
+// 4 GiB for images up to 2^29 pixels (23170^2) whatever the batch; lanes outside the image read
+// zeros by the descriptor's range check.  Each fp32
+// accumulator sums 4 * AC_RB = 32 products; waves reduce in fp32, the workgroup in fp64
+// (partial[wg][42], slot 41 = plain sum).  Requires W % 4 == 0.
 constexpr int AC_RB = 8;
 
 static int x_autocorr_num_wg(int B, int H, int W) {
-  if ((int64_t)B * H * W * 4 >= 0x7FFFFFF0LL || W % 4 != 0) return 0;
+  if (W % 4 != 0 || B < 1 || H < 1) return 0;
   const int64_t threads = (int64_t)B * ((H + AC_RB - 1) / AC_RB) * (W / 4);
   return (int)((threads + 255) / 256);
 }
@@ -37,10 +41,13 @@ __global__ __launch_bounds__(256, 3) void x_autocorr_kernel(const float* __restr
     const int64_t rest = gt / ncg;
     const int band = (int)(rest % nband), b = (int)(rest / nband);
     const int c = 4 * cg, r0 = band * AC_RB;
-    // one buffer descriptor over x: lanes outside the image read zeros by the range check
-    const __amdgpu_buffer_rsrc_t rx = tds_buffer_rsrc(x, (uint32_t)((int64_t)B * H * W * 4));
+    const int b0 = __builtin_amdgcn_readfirstlane(b);  // first active lane: the wave's lowest image
+    const int64_t img = (int64_t)H * W;
+    const int64_t span = (int64_t)(B - b0) * img * 4;
+    const __amdgpu_buffer_rsrc_t rx =
+        tds_buffer_rsrc(x + (int64_t)b0 * img, (uint32_t)(span < 0xFFFFFFF0LL ? span : 0xFFFFFFF0LL));
     constexpr uint32_t kOob = 0xFFFFFFF0u;
-    const uint32_t base = (uint32_t)(((int64_t)b * H * W + c) * 4);
+    const uint32_t base = (uint32_t)(((int64_t)(b - b0) * img + c) * 4);
     const bool has_l = c >= 4, has_r = c + 4 < W;
     auto ld_row = [&](int r, float (&row)[12]) {
       const uint32_t o = base + (uint32_t)r * (uint32_t)W * 4u;
@@ -96,7 +103,11 @@ using namespace tds;
 int tds_x_autocorr_num_wg(int B, int H, int W) { return x_autocorr_num_wg(B, H, W); }
 
 void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
-  if (nwg != x_autocorr_num_wg(B, H, W)) return;  // the partial buffer is sized by tds_x_autocorr_num_wg
+  if (nwg < 1 || nwg != x_autocorr_num_wg(B, H, W)) {  // the partial buffer is sized by tds_x_autocorr_num_wg
+    tds_launch_fail("x_autocorr: workgroup count does not match the shape (needs W % 4 == 0)");
+    return;
+  }
   hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
+  TDS_LAUNCH_CHECK();
   tds_x_border(x, strips, B, H, W, st);
 }

@@ -14,10 +14,12 @@
 #include <vector>
 
 #include "kernels/launchers.h"
+#include "launch_check.h"
 
 namespace {
 
 using at::Tensor;
+using tds_bind::check_launches;
 
 hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
 
@@ -47,6 +49,7 @@ Tensor relu_fwd(const Tensor& x) {
   c10::DeviceGuard g(x.device());
   auto y = at::empty_like(x);
   tds_relu_fwd(x.data_ptr<float>(), y.data_ptr<float>(), x.numel(), cur_stream(x));
+  check_launches("relu_fwd");
   return y;
 }
 
@@ -57,6 +60,7 @@ Tensor relu_bwd(const Tensor& grad, const Tensor& out) {
   c10::DeviceGuard g(grad.device());
   auto dx = at::empty_like(grad);
   tds_relu_bwd(grad.data_ptr<float>(), out.data_ptr<float>(), dx.data_ptr<float>(), grad.numel(), cur_stream(grad));
+  check_launches("relu_bwd");
   return dx;
 }
 
@@ -69,6 +73,7 @@ std::tuple<Tensor, Tensor> maxpool2_fwd(const Tensor& x) {
   auto idx = at::empty({B, C, H / 2, W / 2}, x.options().dtype(at::kByte));
   tds_maxpool2_fwd(x.data_ptr<float>(), y.data_ptr<float>(), idx.data_ptr<uint8_t>(), B * C, (int)H, (int)W,
                    cur_stream(x));
+  check_launches("maxpool2_fwd");
   return {y, idx};
 }
 
@@ -81,6 +86,7 @@ Tensor maxpool2_bwd(const Tensor& gy, const Tensor& idx, int64_t H, int64_t W) {
   auto gx = at::empty({gy.size(0), gy.size(1), H, W}, gy.options());
   tds_maxpool2_bwd(gy.data_ptr<float>(), idx.data_ptr<uint8_t>(), gx.data_ptr<float>(), gy.size(0) * gy.size(1),
                    (int)H, (int)W, cur_stream(gy));
+  check_launches("maxpool2_bwd");
   return gx;
 }
 
@@ -94,6 +100,7 @@ Tensor upsample_bilinear_u8(const Tensor& src, int64_t H, int64_t W) {
   auto dst = at::empty({src.size(0), 1, H, W}, src.options().dtype(at::kFloat));
   tds_upsample_bilinear_u8(src.data_ptr<uint8_t>(), dst.data_ptr<float>(), (int)src.size(0), (int)src.size(1),
                            (int)src.size(2), (int)H, (int)W, cur_stream(src));
+  check_launches("upsample_bilinear_u8");
   return dst;
 }
 
@@ -123,6 +130,7 @@ void sgd_step_(at::TensorList params, at::TensorList grads, at::TensorList moms,
     tds_sgd_multi(tab, (float)lr, (float)wd, (float)momentum, (float)dampening, nesterov ? 1 : 0, first_step ? 1 : 0,
                   maxn, st);
   }
+  check_launches("sgd_step_");
 }
 
 std::tuple<Tensor, Tensor> cross_entropy(const Tensor& logits, const Tensor& labels, int64_t ignore_index,
@@ -141,6 +149,7 @@ std::tuple<Tensor, Tensor> cross_entropy(const Tensor& logits, const Tensor& lab
   tds_cross_entropy(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), row_loss.data_ptr<float>(),
                     dlogits.data_ptr<float>(), loss.data_ptr<float>(), inv.data_ptr<float>(), M, N, ignore_index,
                     (float)label_smoothing, cur_stream(logits));
+  check_launches("cross_entropy");
   return {loss, dlogits};
 }
 
@@ -151,6 +160,7 @@ Tensor scale_by_scalar(const Tensor& x, const Tensor& s) {
   c10::DeviceGuard g(x.device());
   auto y = at::empty_like(x);
   tds_scale_by_device_scalar(x.data_ptr<float>(), s.data_ptr<float>(), y.data_ptr<float>(), x.numel(), cur_stream(x));
+  check_launches("scale_by_scalar");
   return y;
 }
 
@@ -177,6 +187,7 @@ Tensor conv2d_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
   const int rc = tds_conv2d_fwd_f32(x.data_ptr<float>(), w.data_ptr<float>(), opt_ptr(bias), out.data_ptr<float>(), B,
                                     Cin, Cout, H, W, KS, (int)pad, cur_stream(x));
   TORCH_CHECK(rc == 0, "tdsa.conv2d_fwd: unsupported configuration (rc=", rc, ")");
+  check_launches("conv2d_fwd");
   return out;
 }
 
@@ -198,6 +209,7 @@ Tensor conv2d_dgrad(const Tensor& gy, const Tensor& w, int64_t pad) {
   const int rc = tds_conv2d_fwd_f32(gy.data_ptr<float>(), wt.data_ptr<float>(), nullptr, dx.data_ptr<float>(), B, Cout,
                                     Cin, H, W, KS, (int)(KS - 1 - pad), st);
   TORCH_CHECK(rc == 0, "tdsa.conv2d_dgrad: unsupported configuration (rc=", rc, ")");
+  check_launches("conv2d_dgrad");
   return dx;
 }
 
@@ -223,6 +235,7 @@ std::tuple<Tensor, Tensor> conv2d_wgrad(const Tensor& x, const Tensor& gy, int64
                                           need_bias ? db.data_ptr<float>() : nullptr, slab.data_ptr<float>(), B, Cin,
                                           Cout, H, W, (int)ks, (int)pad, 1.f, 0, num_wg, cur_stream(x));
   TORCH_CHECK(rc == 0, "tdsa.conv2d_wgrad: launch failed (rc=", rc, ")");
+  check_launches("conv2d_wgrad");
   return {dw, db};
 }
 
@@ -260,6 +273,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_fwd_train(const Tensor& x, const c10::opti
   auto y = at::empty_like(x);
   tds_bn_apply(x.data_ptr<float>(), aff.data_ptr<float>(), aff.data_ptr<float>() + C, y.data_ptr<float>(), B, C, HW,
                relu ? 1 : 0, st);
+  check_launches("bn_fwd_train");
   return {y, mean, invstd};
 }
 
@@ -281,6 +295,7 @@ Tensor bn_fwd_eval(const Tensor& x, const c10::optional<Tensor>& gamma, const c1
   auto y = at::empty_like(x);
   tds_bn_apply(x.data_ptr<float>(), aff.data_ptr<float>(), aff.data_ptr<float>() + C, y.data_ptr<float>(), B, C, HW,
                relu ? 1 : 0, st);
+  check_launches("bn_fwd_eval");
   return y;
 }
 
@@ -305,6 +320,7 @@ std::tuple<Tensor, Tensor, Tensor> bn_bwd(const Tensor& dy, const Tensor& x, con
   tds_bn_bwd(dy.data_ptr<float>(), x.data_ptr<float>(), B, C, HW, opt_ptr(gamma), mean.data_ptr<float>(),
              invstd.data_ptr<float>(), need_dx ? dx.data_ptr<float>() : nullptr, dgamma.data_ptr<float>(),
              dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), partial.data_ptr<double>(), nchunk, st);
+  check_launches("bn_bwd");
   return {dx, dgamma, dbeta};
 }
 
@@ -324,6 +340,7 @@ Tensor linear_fwd(const Tensor& x, const Tensor& w, const c10::optional<Tensor>&
   const int rc = tds_linear_fwd_skinny(x.data_ptr<float>(), w.data_ptr<float>(), opt_ptr(b), out.data_ptr<float>(),
                                        partial.data_ptr<float>(), M, N, K, nblk, cur_stream(x));
   TORCH_CHECK(rc == 0, "tdsa.linear_fwd: unsupported shape");
+  check_launches("linear_fwd");
   return out;
 }
 
@@ -348,6 +365,7 @@ Tensor linear_bwd_into(const Tensor& dy, const Tensor& x, const Tensor& w, const
                                        need_dx ? dx.data_ptr<float>() : nullptr, opt_mut_ptr(dw_out),
                                        opt_mut_ptr(db_out), M, N, K, (float)scale, accumulate ? 1 : 0, cur_stream(x));
   TORCH_CHECK(rc == 0, "tdsa.linear_bwd_into: unsupported shape");
+  check_launches("linear_bwd_into");
   return dx;
 }
 
@@ -375,6 +393,7 @@ void linear_dw(const Tensor& dy, const Tensor& x, const Tensor& dw, const c10::o
                                  (accumulate || m0 > 0) ? 1 : 0, cur_stream(x));
     TORCH_CHECK(rc == 0, "tdsa.linear_dw: bad launch shape");
   }
+  check_launches("linear_dw");
 }
 
 }  // namespace

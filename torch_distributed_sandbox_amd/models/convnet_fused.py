@@ -3,19 +3,24 @@
 The reference runs 13 ATen kernels forward and ~20 backward per step on
 fp32 NCHW tensors.  This plan runs the network as three
 autograd Functions over NHWC/bf16x3 activations (kernels in
-``csrc/kernels/convnet_fused.hip`` and ``conv2_bf16x3.hip``):
+``csrc/kernels/convnet_fused.hip``, ``conv2_fwd2.hip``, ``conv2_bwd.hip``, ``head_pb.hip``):
 
 ``_Layer1``  x -> p1            conv1 + BN1(batch stats) + ReLU + pool, conv1 never stored
-``_Conv2``   p1 -> y2           conv2 (bf16x3 MFMA) with BN2 batch-stat partials fused; its
-                                backward rebuilds dy2 from y2 in LDS (BN2/pool backward fused)
-``_Head``    y2 -> logits       BN2 + ReLU + pool + fc in one pass; fc grads into the DDP bucket
+``_Conv2``   p1 -> y2, ya       conv2 (bf16x3 MFMA) with BN2 batch-stat partials and the 2x2
+                                max-pool (ya = y2 at each window's argmax, resolved by the sign
+                                of BN2's gamma) fused; its backward rebuilds dy2 from y2 in LDS
+                                (BN2/pool backward fused)
+``_Head``    ya -> logits       BN2 affine + ReLU + fc streamed over ya and the fc weight; fc
+                                grads into the DDP bucket (or the SGD step fused in)
 
-Autograd runs the backward head -> conv2 -> layer1, so the fc gradient (the
-720 MB DDP bucket) is complete — and its all-reduce launched — before the
-conv backward starts (SURVEY.md §3.4 overlap property).
+ya and the pooled gradient g2m use the pooled-blocked layout of
+``csrc/kernels/pooled_layout.h``.  Autograd runs the backward head -> conv2 ->
+layer1, so the fc gradient (the 720 MB DDP bucket) is complete — and its
+collective launched — before the conv backward starts (SURVEY.md §3.4 overlap
+property).
 
-Numerics: conv1, BN, pooling, fc and the loss are exact fp32; conv2
-(fwd/dgrad/wgrad) uses the bf16x3 split (hi*hi + hi*lo + lo*hi, fp32
+Numerics: BN, pooling, fc, the loss and SGD are exact fp32; conv1 and conv2
+(fwd/dgrad/wgrad) use the bf16x3 split (hi*hi + hi*lo + lo*hi, fp32
 accumulate): ~2^-16 relative error per product, tighter than the TF32
 convolutions cuDNN runs for the reference by default.  ``mode='layers'`` is
 the exact-fp32 generic path.
@@ -35,7 +40,10 @@ def supported(model, x) -> bool:
     if x.dim() != 4 or x.shape[1] != 1 or x.dtype != torch.float32:
         return False
     B, _, H, W = x.shape
-    if H != W or H < 8 or B > 32 or H % 4 != 0:
+    # H % 4: conv2 runs on the pooled P = H/2 grid and pools again; H >= 16: the head's 4-column
+    # weight groups fit in a pooled row (Q >= 4); H <= 65520: the conv2 tile
+    # order table packs tile rows/columns in 12 bits (P/8 <= 4095); B <= 32: layer-1 partials
+    if H != W or H < 16 or B > 32 or H % 4 != 0 or H > 65520:
         return False
     bn1, bn2 = model.layer1[1], model.layer2[1]
     for bn in (bn1, bn2):
@@ -61,12 +69,12 @@ def _sinks(ctx, params, first):
 _ZERO = {}
 
 
-def _zero_scalar(like):
+def _zero_scalar(device, dtype):
     """Cached 0-d zero per (device, dtype): the y2 gradient placeholder costs no fill kernel."""
-    key = (like.device, like.dtype)
+    key = (device, dtype)
     z = _ZERO.get(key)
     if z is None:
-        z = _ZERO[key] = torch.zeros((), device=like.device, dtype=like.dtype)
+        z = _ZERO[key] = torch.zeros((), device=device, dtype=dtype)
     return z
 
 
@@ -101,43 +109,46 @@ class _Layer2Link:
 
 class _Conv2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, p1, w2, b2, link):
+    def forward(ctx, p1, w2, b2, g2, link):
         ops = _ext.ops()
         wp, wd = ops.conv2_pack(w2.contiguous())
-        y2, partial2 = ops.fused_conv2_forward(p1, wp, b2)
+        y2, partial2, ya = ops.fused_conv2_forward(p1, wp, b2, g2)
         ctx.save_for_backward(p1, wd, y2)
         ctx.params = (w2, b2)
         ctx.link = link
-        ctx.mark_non_differentiable(partial2)
-        return y2, partial2
+        ctx.mark_non_differentiable(partial2, ya)
+        return y2, partial2, ya
 
     @staticmethod
-    def backward(ctx, _dy2_placeholder, _unused):
+    def backward(ctx, _dy2_placeholder, _unused, _unused_ya):
         p1, wd, y2 = ctx.saved_tensors
         link = ctx.link
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
         dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, p1, wd, 1.0,
                                                            *_sinks(ctx, ctx.params, 1))
         link.g2m = link.kbuf = link.aff2 = None
-        return (dp1 if ctx.needs_input_grad[0] else None), dw2, db2, None
+        return (dp1 if ctx.needs_input_grad[0] else None), dw2, db2, None, None
 
 
 class _Head(torch.autograd.Function):
+    """BN2 finalize + affine + ReLU + fc over ya.  y2 is an input only so that autograd routes
+    the conv2 backward through this node: its gradient travels in the link (g2m, BN2 backward
+    constants), autograd gets a zero-stride placeholder."""
+
     @staticmethod
-    def forward(ctx, y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex, link):
+    def forward(ctx, y2, ya, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex, link):
         ops = _ext.ops()
+        P = y2.shape[1]
         x_out = None
         if ex is not None:
-            B, P = y2.shape[0], y2.shape[1]
-            x_out = torch.empty((B, wfc.shape[1]), device=y2.device, dtype=torch.float32)
-        # y2 at each pooling window's argmax, in the fc's flatten order: the backward
-        # streams it (360 MB at 3000^2) instead of y2 (1.44 GB)
-        ya = torch.empty((y2.shape[0], wfc.shape[1]), device=y2.device, dtype=torch.float32)
-        logits, stats2, aff2 = ops.fused_head_forward(y2, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
-                                                      bfc, x_out, ya)
+            x_out = torch.empty((ya.shape[0], wfc.shape[1]), device=ya.device, dtype=torch.float32)
+        logits, stats2, aff2 = ops.fused_head_forward(ya, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
+                                                      bfc, P, x_out)
         if ex is not None and not ex.begin(x_out):
             raise RuntimeError("activation exchange refused to start after ready() agreed")
-        ctx.save_for_backward(y2, stats2, aff2, g2, wfc, ya)
+        ctx.save_for_backward(ya, stats2, aff2, g2, wfc)
+        ctx.P = P
+        ctx.y2_meta = (y2.shape, y2.dtype, y2.device)
         ctx.wfc_param = wfc
         ctx.small = (bfc, g2, be2)
         ctx.ex = ex
@@ -146,34 +157,35 @@ class _Head(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dlogits):
-        y2, stats2, aff2, g2, wfc, ya = ctx.saved_tensors
+        ya, stats2, aff2, g2, wfc = ctx.saved_tensors
         dlogits = dlogits.contiguous().float()
         ex = ctx.ex
         ops = _ext.ops()
+        P = ctx.P
         if ex is not None:
             # fc gradients come from the activation exchange (parallel/factored.py)
-            _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, None, 1.0,
-                                                                     False, ya)
+            _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, None, 1.0,
+                                                                 False)
             ex.defer(dlogits)
             dW = dbfc = None
         else:
-            dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[10] else None, wfc.shape, wfc)
+            dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[11] else None, wfc.shape, wfc)
             # world size 1 under DDP(overlap_optimizer): the SGD step of the fc weight runs in
             # this same kernel (ops/fused_update.py)
             lr = None
-            if ctx.needs_input_grad[10] and y2.shape[0] <= 8 and wfc.shape[0] <= 10:  # head_bwd_ya_kernel shapes
+            if ctx.needs_input_grad[11] and ya.shape[0] <= 8:  # one pass of head_bwd_pb_kernel
                 lr = fused_update.take(ctx.wfc_param)
-            dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (11, 3, 4))
-            dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward_g2m(dlogits, y2, stats2, aff2, g2, wfc, dw_out,
-                                                                         1.0, True, ya, float(lr or 0.0), dbfc_o, dg_o,
-                                                                         dbe_o)
+            dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (12, 4, 5))
+            dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, dw_out,
+                                                                     1.0, True, float(lr or 0.0), dbfc_o, dg_o,
+                                                                     dbe_o)
             if lr:
                 fused_update.applied(ctx.wfc_param)
         link = ctx.link
         link.g2m, link.kbuf, link.aff2 = g2m, kbuf, aff2
-        # y2's gradient is carried by the link; autograd gets a zero-stride placeholder
-        dy2 = _zero_scalar(y2).expand(y2.shape)
-        return dy2, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None, None
+        shape, dtype, device = ctx.y2_meta
+        dy2 = _zero_scalar(device, dtype).expand(shape)
+        return (dy2, None, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None, None)
 
 
 def forward(model, x):
@@ -183,7 +195,7 @@ def forward(model, x):
     p1 = _Layer1.apply(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
                        bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps))
     link = _Layer2Link()
-    y2, partial2 = _Conv2.apply(p1, conv2.weight, conv2.bias, link)
+    y2, partial2, ya = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, link)
     # the fc update may still be running on DDP's side stream (overlap_optimizer): wait here,
     # after the convolutions were queued, not before
     param_fence.wait(fc.weight)
@@ -191,5 +203,5 @@ def forward(model, x):
     ex = factored.get(fc.weight)
     if ex is not None and not ex.ready(x.shape[0]):
         ex = None
-    return _Head.apply(y2, partial2, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
+    return _Head.apply(y2, ya, partial2, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
                        bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias, ex, link)

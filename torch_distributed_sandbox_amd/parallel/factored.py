@@ -104,7 +104,8 @@ class ActivationExchange:
         self.steps_exchanged = 0
         self.last_path = None  # "activation-exchange" | "sharded-exchange" once a step used it
         self._x_buf = self._x_work = self._dy = self._x_local = None
-        self.side_stream = None  # set by DDP(overlap_optimizer=True): dW is formed off the compute stream
+        self.side_stream = None  # DDP(overlap_optimizer=True): its update stream, which also finishes the exchange
+        self._own_stream = None  # otherwise (GPU): a private side stream
         setattr(weight, _ATTR, self)
 
     def detach(self):
@@ -169,23 +170,32 @@ class ActivationExchange:
 
     # ---------------------------------------------------------------- backward
     def defer(self, dy: torch.Tensor):
+        """Called from the layer's backward with dY.  On the GPU the rest of the exchange
+        (dY gather, dW formation, shard all-gather) is issued right here on a side stream,
+        so it overlaps the rest of the backward; the compute stream only waits for it at
+        the end of backward (or, under DDP's overlapped optimizer, the optimizer's side
+        stream does).  On the CPU it runs from an end-of-backward callback."""
         self._dy = dy.detach().contiguous()
-        torch.autograd.Variable._execution_engine.queue_callback(self.finalize)
-
-    def finalize(self):
-        side = self.side_stream if (self.side_stream is not None and self._dy.is_cuda) else None
-        if side is None:
-            self._finish()
+        if not self._dy.is_cuda:
+            torch.autograd.Variable._execution_engine.queue_callback(self._finish)
             return
-        # the dy gather queues behind the big x exchange on the comm stream: issue the
-        # waits and the dW GEMM from the side stream so the compute stream runs on
-        cur = torch.cuda.current_stream(self._dy.device)
+        dev = self._dy.device
+        side = self.side_stream
+        join = side is None
+        if side is None:
+            if self._own_stream is None:
+                self._own_stream = torch.cuda.Stream(device=dev)
+            side = self._own_stream
+        cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
         keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
         with torch.cuda.stream(side):
             for t in keep:
                 t.record_stream(side)
             self._finish()
+        if join:
+            torch.autograd.Variable._execution_engine.queue_callback(
+                lambda: torch.cuda.current_stream(dev).wait_stream(side))
 
     def _targets(self):
         """(dW, accumulate_w), (db, accumulate_b) — gradients accumulated under no_sync()
