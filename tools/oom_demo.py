@@ -28,15 +28,22 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-# bytes per input pixel per image in the fused plan (x 4, p1 16, idx1 4, y2 32, dy2 32,
-# dp1 16, g2m 8, upsample/out 4) measured as 96 B/px at 3000^2 (peak 5.77 GB at B=5
-# incl. 1.44 GB of fc weight + gradient); fc weight+grad = 2 * 10 * 32 * (H/4)^2 * 4 B
-ACT_BYTES_PER_PX = 96.0
-FC_BYTES_PER_PX = 160.0 / 1.0  # weight + gradient, per input pixel of ONE image edge^2
+# Memory model of the fused plan at HEAD, peak(H, B) = (act * B + fixed) * H^2 bytes, calibrated on
+# this GPU by two short runs at --calib-size (batch 1 and 2): act = bytes per input pixel per image
+# (x, p1 hi|lo, argmax, y2, ya, g2m, dp1, ...), fixed = per-pixel bytes that do not scale with the
+# batch (fc weight + gradient = 2 * 10 * 32 * (H/4)^2 * 4 B = 80 B/px, DDP flat buffers, ...).
 
 
-def predicted_bytes(H, B):
-    return B * ACT_BYTES_PER_PX * H * H + FC_BYTES_PER_PX * H * H
+def calibrate(H, device):
+    a = run(H, 1, 1, device, 1, 0)["peak_gb"] * 1e9
+    b = run(H, 2, 1, device, 1, 0)["peak_gb"] * 1e9
+    act = (b - a) / (H * H)
+    fixed = a / (H * H) - act
+    return act, fixed
+
+
+def predicted_bytes(H, B, act, fixed):
+    return (B * act + fixed) * H * H
 
 
 def run(H, B, steps, device, world, rank):
@@ -81,6 +88,7 @@ def main():
     ap.add_argument("--bs-fail", type=int, default=10)
     ap.add_argument("--bs-fit", type=int, default=5)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--calib-size", type=int, default=3000)
     args = ap.parse_args()
     from torch_distributed_sandbox_amd.parallel import distributed as tdist
 
@@ -93,12 +101,16 @@ def main():
         tdist.init_process_group("rccl", rank=rank, world_size=world, device_id=local)
     H = args.image_size
     total = torch.cuda.get_device_properties(device).total_memory
+    act, fixed = calibrate(args.calib_size, device)
+    gc.collect()
+    torch.cuda.empty_cache()
     rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1), "world_size": world,
-           "model": {"act_bytes_per_px_per_image": ACT_BYTES_PER_PX, "fc_bytes_per_px": FC_BYTES_PER_PX,
-                     "predicted_gb": {str(b): round(predicted_bytes(H, b) / 1e9, 1)
+           "model": {"calibrated_at": args.calib_size, "act_bytes_per_px_per_image": round(act, 1),
+                     "fixed_bytes_per_px": round(fixed, 1),
+                     "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed) / 1e9, 1)
                                       for b in (args.bs_fit, args.bs_fail)},
                      "predicted_oom_edge_bs%d" % args.bs_fail:
-                         int((total / (args.bs_fail * ACT_BYTES_PER_PX + FC_BYTES_PER_PX)) ** 0.5)}}
+                         int((total / (args.bs_fail * act + fixed)) ** 0.5)}}
     # 1) batch 10 on one GPU (every rank tries it alone: no collective inside)
     try:
         r = run(H, args.bs_fail, 1, device, 1, rank) if world == 1 else None

@@ -119,7 +119,7 @@ struct B2Args {
   float* __restrict__ slab;
   const int* __restrict__ order;  // blocked tile order (tds_tile_order)
   int B, P, Q, tiles_r, tiles_c, per_img, total;
-  PBGeom pg;
+  bool g2m_big;  // 32 g2m planes exceed a 4 GiB buffer-descriptor range: 64-bit loads
 };
 
 struct B2Tile {
@@ -155,7 +155,7 @@ struct B2Stager {
   uint4 pr[REGP1 ? B2_DMA_PER_WAVE : 1];
   // per-thread byte offsets (fixed for the kernel): global, relative to the tile's
   // descriptor bases, and LDS, of each staging item (window x 4 channels); p1 DMA sources
-  uint32_t yoff[B2_IPER], doff[B2_DMA_PER_WAVE];
+  uint32_t yoff[B2_IPER], goff[B2_IPER], doff[B2_DMA_PER_WAVE];
   int drec[B2_IPER];
 
   // staging item u of this thread: window (wy, wx)
@@ -181,6 +181,7 @@ struct B2Stager {
       int wy, wx;
       item_geom(tid, u, wy, wx);
       yoff[u] = (uint32_t)(((2 * wy) * a.P + 2 * wx) * 128 + c4 * 16);
+      goff[u] = a.g2m_big ? 0u : (uint32_t)(((int64_t)c4 * 4 * a.Q * a.Q + (int64_t)wy * a.Q + wx) * 4);
       drec[u] = ((2 * wy) * B2_SC + 2 * wx) * 32 + (c4 & 3) * 8;
     }
 #pragma unroll
@@ -210,20 +211,30 @@ struct B2Stager {
         b2_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 128);
     const char* pbase = reinterpret_cast<const char*>(a.p1) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 64;
     uint32_t oy[B2_IPER][4];
-    // pooled gradients: window (wy, wx) is pooled position (r0/2 - 1 + wy, c0/2 - 1 + wx); four
-    // channel planes of the planar g2m, 64-bit addressed (no 2 GiB descriptor range)
-    const float* gp[B2_IPER];
-    bool gok[B2_IPER];
+    // pooled gradients: window (wy, wx) is pooled position (r0/2 - 1 + wy, c0/2 - 1 + wx), four
+    // channel planes of the planar g2m.  One buffer descriptor per tile (base: the tile's pooled
+    // origin in channel 0 of its image) while 32 planes fit a 4 GiB range (H < 23170); beyond
+    // that, 64-bit addresses.
     const int64_t gplane = (int64_t)Q * Q;
+    const __amdgpu_buffer_rsrc_t rg =
+        tds_buffer_rsrc(a.g2m + (int64_t)x.b * 32 * gplane + (int64_t)(x.r0 / 2 - 1) * Q + (x.c0 / 2 - 1), 0xFFFFFFF0u);
+    uint32_t og[B2_IPER];
 #pragma unroll
     for (int u = 0; u < B2_IPER; ++u) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) oy[u][q] = yoff[u] + (uint32_t)(((q >> 1) * P + (q & 1)) * 128);
-      int wy, wx;
-      item_geom(tid, u, wy, wx);
-      const int py = x.r0 / 2 - 1 + wy, px = x.c0 / 2 - 1 + wx;
-      gok[u] = tid + u * B2_THREADS < B2_ITEMS && py >= 0 && py < Q && px >= 0 && px < Q;
-      gp[u] = a.g2m + (gok[u] ? ((int64_t)x.b * 32 + 4 * (tid & 7)) * gplane + (int64_t)py * Q + px : 0);
+      og[u] = goff[u];
+    }
+    if (!x.interior || a.g2m_big) {
+      // edge tile: pooled windows outside the image read zeros (big: og only flags validity)
+#pragma unroll
+      for (int u = 0; u < B2_IPER; ++u) {
+        int wy, wx;
+        item_geom(tid, u, wy, wx);
+        const int py = x.r0 / 2 - 1 + wy, px = x.c0 / 2 - 1 + wx;
+        const bool ok = tid + u * B2_THREADS < B2_ITEMS && py >= 0 && py < Q && px >= 0 && px < Q;
+        if (!ok) og[u] = kB2Oob;
+      }
     }
     const char* psrc[B2_DMA_PER_WAVE];
 #pragma unroll
@@ -280,8 +291,20 @@ struct B2Stager {
         yv[u][q] = DIAG == 7 ? make_float4(1.f, 0.f, 0.f, 0.f)  // timing only: no y2 loads
                              : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy[u][q], 0, 0));
       float g4[4];
+      if (!a.g2m_big) {
+        const uint32_t gstep = (uint32_t)(gplane * 4);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) g4[k] = gok[u] ? gp[u][k * gplane] : 0.f;
+        for (int k = 0; k < 4; ++k)
+          g4[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                rg, og[u] == kB2Oob ? kB2Oob : og[u] + k * gstep, 0, 0));
+      } else {
+        int wy, wx;
+        item_geom(tid, u, wy, wx);
+        const float* gp = a.g2m + ((int64_t)x.b * 32 + 4 * (tid & 7)) * gplane +
+                          (int64_t)(x.r0 / 2 - 1 + wy) * Q + (x.c0 / 2 - 1 + wx);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g4[k] = og[u] == kB2Oob ? 0.f : gp[k * gplane];
+      }
       gv[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
     }
   }
@@ -637,7 +660,7 @@ __global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
   a.tiles_r = (P + B2_TH - 1) / B2_TH;
   a.per_img = a.tiles_c * a.tiles_r;
   a.total = a.per_img * B;
-  a.pg = pb_geom(Q);
+  a.g2m_big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;
   float* kc = reinterpret_cast<float*>(smem + B3_OFF_K);
   if (tid < 160) kc[tid] = (tid < 64) ? aff2[tid] : kbuf[tid - 64];
   __syncthreads();  // kc visible to the staging waves

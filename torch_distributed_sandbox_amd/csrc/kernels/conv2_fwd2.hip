@@ -135,9 +135,12 @@ __device__ __forceinline__ int f2_stage_off(int row, int px, int chunk) {
 // pooled block staging: channel co's 32 floats [prow 4][pcol 8], float4 chunks XOR-swizzled by co
 __device__ __forceinline__ int f2_ystage_off(int co, int e) { return co * 32 + ((((e >> 2) ^ co) & 7) << 2) + (e & 3); }
 
-// window extreme in the direction of BN2's affine; a NaN anywhere wins (torch's max-pool rule)
-__device__ __forceinline__ float f2_ext(float p, float q, bool neg) {
-  return (isnan(q) || (neg ? q < p : q > p)) ? q : p;
+// window extreme in the direction of BN2's affine; a NaN anywhere wins (torch's max-pool rule):
+// v_maximum3_f32 / v_minimum3_f32 (IEEE maximum/minimum, NaN-propagating) on gfx950
+__device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, bool neg) {
+  const float mx = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), __builtin_elementwise_maximum(c, d));
+  const float mn = __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), __builtin_elementwise_minimum(c, d));
+  return neg ? mn : mx;
 }
 
 // stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li]
@@ -163,15 +166,15 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
   // pooled windows (rows 4RH + 2i + {0,1}, columns 4g + 2j + {0,1}) -> ya block entry
   // (prow 2RH + i, pcol 2g + j); fp32 addition is monotone, so max(v) + b2 == max(v + b2)
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    float e[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      float e = acc[2 * i][2 * j];
-      e = f2_ext(e, acc[2 * i][2 * j + 1], neg);
-      e = f2_ext(e, acc[2 * i + 1][2 * j], neg);
-      e = f2_ext(e, acc[2 * i + 1][2 * j + 1], neg);
-      ystage[f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g + j)] = e + bco;
-    }
+    for (int j = 0; j < 2; ++j)
+      e[j] = f2_ext4(acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], acc[2 * i + 1][2 * j + 1], neg) +
+             bco;
+    // pcols 2g, 2g+1 are adjacent floats of one swizzled chunk: one ds_write_b64
+    *reinterpret_cast<float2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_float2(e[0], e[1]);
+  }
 }
 
 // the workgroup stores the staged pooled block: thread e -> channel e / 8, float4 e % 8
