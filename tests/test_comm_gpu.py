@@ -218,6 +218,46 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
             assert torch.equal(p, q), n
 
 
+@pytest.mark.parametrize("keep", [False, True])
+def test_fused_update_grad_semantics(pg, gpu, keep):
+    """World-1 fc SGD step inside the head backward: by default the weight's gradient is never
+    materialised (.grad None after backward, torch's optimizer-in-backward semantics, update-only
+    kernel); keep_fused_grads=True also writes it.  Either way the update equals p - lr * g of
+    an unfused twin."""
+    import copy
+
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    H = 256  # fc weight >= 1 Mi elements: a deferred (overlapped) bucket
+    m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    m2 = copy.deepcopy(m1)
+    d1 = DistributedDataParallel(m1, overlap_optimizer=True, keep_fused_grads=keep)
+    assert d1._deferred
+    d2 = DistributedDataParallel(m2)
+    o1 = d1.attach_optimizer(SGD(m1.parameters(), 1e-3))
+    o2 = d2.attach_optimizer(SGD(m2.parameters(), 1e-3))
+    crit = CrossEntropyLoss()
+    x = torch.rand(2, 1, H, H, device=gpu)
+    y = torch.tensor([3, 7], device=gpu)
+    for d, o in ((d1, o1), (d2, o2)):
+        o.zero_grad()
+        crit(d(x), y).backward()
+    if keep:
+        torch.testing.assert_close(m1.fc.weight.grad, m2.fc.weight.grad, rtol=1e-5, atol=1e-9)
+    else:
+        assert m1.fc.weight.grad is None
+    assert m1.fc.bias.grad is not None
+    o1.step()
+    o2.step()
+    d1.wait_pending_updates()
+    torch.cuda.synchronize()
+    for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+        torch.testing.assert_close(p, q, rtol=1e-6, atol=1e-9, msg=n)
+
+
 def test_rccl_native_count_and_sendrecv(pg, gpu):
     """ncclCommCount of the live communicator, and the grouped point-to-point
     primitive (self-exchange at world 1; strided row slices as sources)."""

@@ -1,0 +1,103 @@
+"""Per-op timing of the fused ConvNet step at the bench shape (3000x3000, B=5), each op run in
+isolation on the tensors a real step produces (CUDA events, median of 5 rounds x N iterations).
+Usage: python tools/micro/step_ops_timing.py [--iters 20] [--only conv2_bwd,...]
+With TDS_SO_VARIANT=<name> it times the side build _C_<name>.so (A/B experiments)."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+
+import torch_distributed_sandbox_amd as tds  # noqa: E402
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(iters):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        out.append(a.elapsed_time(b) / iters)
+    return statistics.median(out)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--image-size", type=int, default=3000)
+    ap.add_argument("--batch-size", type=int, default=5)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    ops = tds._ext.ops()
+    from torch_distributed_sandbox_amd.data import synthetic_batch
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import functional as TF
+
+    dev = torch.device("cuda", 0)
+    H, B = a.image_size, a.batch_size
+    P = H // 2
+    torch.manual_seed(0)
+    m = ConvNet(image_shape=(H, H), device=dev)
+    c1, n1, c2, n2, fc = m.layer1[0], m.layer1[1], m.layer2[0], m.layer2[1], m.fc
+    src, _ = synthetic_batch(B, (H, H), dev, seed=7)
+    x = TF.upsample_bilinear_u8(src, H, H)
+    with torch.no_grad():
+        st = {}
+
+        def l1f():
+            st["l1"] = ops.fused_l1_forward(x, c1.weight, c1.bias, n1.weight, n1.bias, n1.running_mean,
+                                            n1.running_var, n1.num_batches_tracked, 0.1, 1e-5)
+
+        def pack():
+            st["pack"] = ops.conv2_pack(c2.weight)
+
+        def c2f():
+            st["c2"] = ops.fused_conv2_forward(st["l1"][0], st["pack"][0], c2.bias, n2.weight)
+
+        def hf():
+            y2, partial2, ya = st["c2"]
+            st["hf"] = ops.fused_head_forward(ya, partial2, c2.bias, n2.weight, n2.bias, n2.running_mean,
+                                              n2.running_var, n2.num_batches_tracked, 0.1, 1e-5, fc.weight,
+                                              fc.bias, P, None)
+
+        dl = torch.randn(B, 10, device=dev) * 0.1
+        dw = torch.empty_like(fc.weight)
+
+        def hb():
+            _, stats2, aff2 = st["hf"]
+            st["hb"] = ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, n2.weight, fc.weight, P, dw, 1.0, True)
+
+        def c2b():
+            y2 = st["c2"][0]
+            g2m, kbuf = st["hb"][4], st["hb"][5]
+            st["c2b"] = ops.fused_conv2_backward_y2(y2, g2m, st["hf"][2], kbuf, st["l1"][0], st["pack"][1], 1.0)
+
+        def l1b():
+            p1, idx1, stats1, gram = st["l1"]
+            ops.fused_l1_backward(st["c2b"][0], x, p1, idx1, c1.weight, c1.bias, n1.weight, stats1, gram, 1.0)
+
+        seq = [("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
+               ("conv2_bwd", c2b), ("l1_bwd", l1b)]
+        for _, fn in seq:
+            fn()
+        only = set(a.only.split(",")) if a.only else None
+        res = {}
+        for name, fn in seq:
+            if only and name not in only:
+                continue
+            res[name] = round(timeit(fn, a.iters), 4)
+            print(f"{name:11s} {res[name]:.4f} ms", flush=True)
+        print(json.dumps({"variant": os.environ.get("TDS_SO_VARIANT", ""), "ms": res,
+                          "sum_ms": round(sum(res.values()), 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

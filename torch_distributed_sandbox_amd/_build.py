@@ -21,6 +21,11 @@ Usage::
 
     python -m torch_distributed_sandbox_amd._build          # incremental
     python -m torch_distributed_sandbox_amd._build --clean  # from scratch
+
+A/B kernel experiments build side variants with extra defines into ``_C_<name>.so`` (their
+own object directory), loaded instead of ``_C.so`` when ``TDS_SO_VARIANT=<name>`` is set::
+
+    python -m torch_distributed_sandbox_amd._build --variant prio -D TDS_B3_MFMA_PRIO=2
 """
 from __future__ import annotations
 
@@ -66,7 +71,15 @@ def _ninja_escape(p: str) -> str:
     return p.replace("$", "$$").replace(" ", "$ ").replace(":", "$:")
 
 
-def write_ninja(debug: bool = False, host_sanitize: bool = False) -> str:
+def _paths(variant: str | None):
+    if not variant:
+        return BUILD_DIR, OUT_SO
+    return BUILD_DIR + "_" + variant, os.path.join(PKG_DIR, f"_C_{variant}.so")
+
+
+def write_ninja(debug: bool = False, host_sanitize: bool = False, variant: str | None = None,
+                defines=()) -> str:
+    build_dir, out_so = _paths(variant)
     incs, libdir, abi = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
     hipcc = os.path.join(ROCM, "bin", "hipcc")
@@ -81,7 +94,7 @@ def write_ninja(debug: bool = False, host_sanitize: bool = False) -> str:
         f"-I{os.path.join(ROCM, 'include')}",
         "-Wno-unused-result",
         "-Wno-unused-command-line-argument",
-    ]
+    ] + [f"-D{d}" for d in defines]
     # Device code: gfx950 only.  -munsafe-fp-atomics lets float atomicAdd lower
     # to global_atomic_add_f32 (no CAS loop) for the few reductions that use it.
     hip_flags = common + [
@@ -142,17 +155,17 @@ def write_ninja(debug: bool = False, host_sanitize: bool = False) -> str:
     objs = []
     for s in hip_srcs + cpp_srcs:
         rel = os.path.relpath(s, CSRC).replace(os.sep, "_")
-        o = os.path.join(BUILD_DIR, rel + ".o")
+        o = os.path.join(build_dir, rel + ".o")
         rule = "hip" if s.endswith(".hip") else "host"
         lines.append(f"build {_ninja_escape(o)}: {rule} {_ninja_escape(s)}")
         extra = HIP_FILE_FLAGS.get(os.path.basename(s))
         if extra:
             lines.append(f"  hipflags = $hipflags {' '.join(shlex.quote(f) for f in extra)}")
         objs.append(o)
-    lines.append(f"build {_ninja_escape(OUT_SO)}: link {' '.join(_ninja_escape(o) for o in objs)}")
-    lines.append(f"default {_ninja_escape(OUT_SO)}")
-    os.makedirs(BUILD_DIR, exist_ok=True)
-    path = os.path.join(BUILD_DIR, "build.ninja")
+    lines.append(f"build {_ninja_escape(out_so)}: link {' '.join(_ninja_escape(o) for o in objs)}")
+    lines.append(f"default {_ninja_escape(out_so)}")
+    os.makedirs(build_dir, exist_ok=True)
+    path = os.path.join(build_dir, "build.ninja")
     text = "\n".join(lines) + "\n"
     old = open(path).read() if os.path.exists(path) else None
     if old != text:
@@ -163,17 +176,18 @@ def write_ninja(debug: bool = False, host_sanitize: bool = False) -> str:
 
 
 def build(clean: bool = False, jobs: int | None = None, verbose: bool = False, debug: bool = False,
-          host_sanitize: bool = False) -> str:
-    if clean and os.path.isdir(BUILD_DIR):
-        shutil.rmtree(BUILD_DIR)
-    ninja_file = write_ninja(debug=debug, host_sanitize=host_sanitize)
+          host_sanitize: bool = False, variant: str | None = None, defines=()) -> str:
+    build_dir, out_so = _paths(variant)
+    if clean and os.path.isdir(build_dir):
+        shutil.rmtree(build_dir)
+    ninja_file = write_ninja(debug=debug, host_sanitize=host_sanitize, variant=variant, defines=defines)
     ninja = shutil.which("ninja") or os.path.join(os.path.dirname(sys.executable), "ninja")
     jobs = jobs or min(16, os.cpu_count() or 4)
     cmd = [ninja, "-f", ninja_file, "-j", str(jobs)]
     if verbose:
         cmd.append("-v")
-    subprocess.run(cmd, check=True, cwd=BUILD_DIR)
-    return OUT_SO
+    subprocess.run(cmd, check=True, cwd=build_dir)
+    return out_so
 
 
 def main(argv=None):
@@ -184,8 +198,12 @@ def main(argv=None):
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("--host-sanitize", action="store_true",
                     help="ASan+UBSan on host C++ (store/backends); never on device code")
+    ap.add_argument("--variant", default=None, help="side build _C_<variant>.so (A/B experiments)")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for a variant")
     a = ap.parse_args(argv)
-    print(build(a.clean, a.jobs, a.verbose, a.debug, a.host_sanitize))
+    if a.defines and not a.variant:
+        ap.error("-D needs --variant (the default _C.so is always built without extra defines)")
+    print(build(a.clean, a.jobs, a.verbose, a.debug, a.host_sanitize, a.variant, a.defines))
 
 
 if __name__ == "__main__":

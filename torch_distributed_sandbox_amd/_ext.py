@@ -17,7 +17,9 @@ import threading
 import torch
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-SO_PATH = os.path.join(_PKG_DIR, "_C.so")
+# TDS_SO_VARIANT=<name> loads the side build _C_<name>.so (_build.py --variant; A/B experiments)
+_VARIANT = os.environ.get("TDS_SO_VARIANT", "")
+SO_PATH = os.path.join(_PKG_DIR, f"_C_{_VARIANT}.so" if _VARIANT else "_C.so")
 
 _lock = threading.Lock()
 _loaded = False

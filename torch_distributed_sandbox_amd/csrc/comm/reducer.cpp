@@ -156,6 +156,17 @@ class Reducer : public torch::CustomClassHolder {
       view.copy_(g.reshape({-1}));
       g = view.view(p.sizes());
     }
+    count_ready(i);
+  }
+
+  // A parameter whose optimizer step ran inside its backward kernel without materialising
+  // the gradient (ops/fused_update.py, optimizer-in-backward semantics): ready, no .grad.
+  void mark_ready(int64_t i) {
+    TORCH_CHECK(i >= 0 && i < (int64_t)p_bucket_.size(), "Reducer.mark_ready: bad parameter index");
+    count_ready(i);
+  }
+
+  void count_ready(int64_t i) {
     if (!callback_queued_) {
       callback_queued_ = true;
       std::weak_ptr<std::atomic<Reducer*>> w = self_;
@@ -247,6 +258,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       .def("set_bucket_skip", &tds_comm::Reducer::set_bucket_skip)
       .def("set_bucket_deferred", &tds_comm::Reducer::set_bucket_deferred)
       .def("take_work", &tds_comm::Reducer::take_work)
+      .def("mark_ready", &tds_comm::Reducer::mark_ready)
       .def("ready_order", &tds_comm::Reducer::ready_order)
       .def("num_buckets", &tds_comm::Reducer::num_buckets);
 }

@@ -226,7 +226,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     const Tensor& dlogits, const Tensor& ya, const Tensor& stats2, const Tensor& aff2,
     const c10::optional<Tensor>& gamma2, const Tensor& wfc, int64_t P, const c10::optional<Tensor>& dw_out,
     double scale, bool compute_dw, double update_lr, const c10::optional<Tensor>& dbfc_out,
-    const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out) {
+    const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out, bool keep_dw) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_backward: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_backward: needs P/2 >= 4 pooled columns and B >= 1");
@@ -239,16 +239,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   const float* g = optf(gamma2, 32, "bn2.weight");
   c10::DeviceGuard guard(ya.device());
   hipStream_t st = stream_of(ya);
-  Tensor dW;
+  const bool upd = update_lr > 0.0;
+  TORCH_CHECK(keep_dw || upd, "fused_head_backward: keep_dw=False needs update_lr > 0 (update-only step)");
+  Tensor dW;  // undefined (None) for an update-only step
   if (!compute_dw) {
     dW = at::empty({0}, wfc.options());
+  } else if (!keep_dw) {
   } else if (dw_out.has_value() && dw_out->defined()) {
     need(*dw_out, at::kFloat, {NC, 32 * Q * Q}, "dW_out");
     dW = *dw_out;
   } else {
     dW = at::empty_like(wfc);
   }
-  const bool upd = update_lr > 0.0;
   TORCH_CHECK(!upd || (compute_dw && tds_head_bwd_pb_npass((int)B) == 1),
               "fused_head_backward: update_lr needs compute_dw and a batch of <= 8 images");
   auto g2m = at::empty({B, 32, Q, Q}, ya.options());  // planar (the fc flatten order)
@@ -256,7 +258,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   auto partial = at::empty({(int64_t)32 * npass * nblk * 2}, ya.options().dtype(at::kDouble));
   const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
                                  dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
-                                 compute_dw ? dW.data_ptr<float>() : nullptr,
+                                 compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                  upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
                                  (float)scale, (float)update_lr, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
@@ -370,7 +372,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def(
       "fused_head_backward(Tensor dlogits, Tensor ya, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor(e!) wfc, "
       "int P, Tensor(a!)? dw_out, float scale, bool compute_dw=True, float update_lr=0.0, "
-      "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None) -> "
+      "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None, bool keep_dw=True) -> "
       "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
   m.def(

@@ -543,6 +543,9 @@ __device__ __forceinline__ void b3_wgrad(const char* d_l, const char* p_l, f32x4
 
 template <int ROLE, int DIAG>  // ROLE 0/1 = dgrad wave D, 2/3 = wgrad
 __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict__ wdpack, char* smem, int first_t) {
+#ifdef TDS_B3_MFMA_PRIO
+  __builtin_amdgcn_s_setprio(TDS_B3_MFMA_PRIO);
+#endif
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   f32x4 R[13][2];
@@ -608,6 +611,9 @@ __device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_
     b3_barrier();
     return;
   }
+#ifdef TDS_B3_STAGE_PRIO
+  __builtin_amdgcn_s_setprio(TDS_B3_STAGE_PRIO);
+#endif
   const int tid = threadIdx.x - 256;
   const float* kc = reinterpret_cast<const float*>(smem + B3_OFF_K);
   // two register sets: tile j's y2 / g2m registers are loaded two iterations before they are

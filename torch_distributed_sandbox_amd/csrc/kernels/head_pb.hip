@@ -245,7 +245,9 @@ __global__ void head_logits_kernel(const double* __restrict__ sums, const float*
 //   partial[c][pass*nblk + blk][2] = { sum g2m, sum g2m * ya }       (BN2 backward sums)
 //   dW[j][c][pos] (= or +=) scale * sum_b dl[b][j] X[b][c][pos]      (WITH_DW; ACC adds)
 //   Wupd = W - lr * dW                                               (UPD: SGD step fused)
-template <int NB, bool WITH_DW, bool ACC, bool UPD>
+// KEEP: dW is also stored (UPD without KEEP: the update only -- optimizer-in-backward semantics,
+// the gradient itself is never materialised, 720 MB less written at 3000^2).
+template <int NB, bool WITH_DW, bool ACC, bool UPD, bool KEEP = true>
 __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     const float* __restrict__ ya, const float* W, const float* __restrict__ aff2, const float* __restrict__ dl,
     float* __restrict__ g2m, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass, int npass,
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
                 if (k < rw.nvalid) p[k] += s[k];
             }
           } else {
-            hp_store4(dW, g, rw, j, d);
+            if constexpr (KEEP) hp_store4(dW, g, rw, j, d);
             if constexpr (UPD) {  // torch SGD: p -= lr * g
               const float4 w = cur.w[j];
               hp_store4(Wupd, g, rw, j, make_float4(w.x - lr * d.x, w.y - lr * d.y, w.z - lr * d.z, w.w - lr * d.w));
@@ -390,26 +392,28 @@ int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const 
                     hipStream_t st) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1) return -1;
   const int npass = tds_head_bwd_pb_npass(B);
-  if (Wupd && (!dW || npass != 1)) return -2;  // the fused SGD step needs the whole dW in one pass
+  if (Wupd && npass != 1) return -2;  // the fused SGD step needs the whole dW in one pass
   const PBGeom g = pb_geom(Q);
   const int nwg = 32 * hp_grid(g).per_channel();
   for (int pass = 0; pass < npass; ++pass) {
     const int b0 = pass * HP_MAXB;
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
     const bool acc = pass > 0;
-#define TDS_HPB_E(NBV, WD, AC, UP)                                                                                 \
-  hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2,     \
+#define TDS_HPB_E(NBV, WD, AC, UP, KP)                                                                             \
+  hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, \
                      dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr);
 #define TDS_HPB(NBV)                                   \
   case NBV:                                            \
-    if (!dW) {                                         \
-      TDS_HPB_E(NBV, false, false, false)              \
+    if (!dW && Wupd) {                                 \
+      TDS_HPB_E(NBV, true, false, true, false)         \
+    } else if (!dW) {                                  \
+      TDS_HPB_E(NBV, false, false, false, true)        \
     } else if (acc) {                                  \
-      TDS_HPB_E(NBV, true, true, false)                \
+      TDS_HPB_E(NBV, true, true, false, true)          \
     } else if (Wupd) {                                 \
-      TDS_HPB_E(NBV, true, false, true)                \
+      TDS_HPB_E(NBV, true, false, true, true)          \
     } else {                                           \
-      TDS_HPB_E(NBV, true, false, false)               \
+      TDS_HPB_E(NBV, true, false, false, true)         \
     }                                                  \
     TDS_LAUNCH_CHECK();                                \
     break;

@@ -117,6 +117,8 @@ class _Conv2(torch.autograd.Function):
         ctx.params = (w2, b2)
         ctx.link = link
         ctx.mark_non_differentiable(partial2, ya)
+        # no zero-filled gradients for partial2 / ya (a 360 MB fill per step at the bench shape)
+        ctx.set_materialize_grads(False)
         return y2, partial2, ya
 
     @staticmethod
@@ -175,12 +177,15 @@ class _Head(torch.autograd.Function):
             lr = None
             if ctx.needs_input_grad[11] and ya.shape[0] <= 8:  # one pass of head_bwd_pb_kernel
                 lr = fused_update.take(ctx.wfc_param)
+            keep = not lr or fused_update.keep_grad(ctx.wfc_param)
             dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (12, 4, 5))
-            dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, dw_out,
-                                                                     1.0, True, float(lr or 0.0), dbfc_o, dg_o,
-                                                                     dbe_o)
+            dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P,
+                                                                     dw_out if keep else None, 1.0, True,
+                                                                     float(lr or 0.0), dbfc_o, dg_o, dbe_o, keep)
             if lr:
-                fused_update.applied(ctx.wfc_param)
+                # update-only step: no gradient for the weight (dW is None), as in torch's
+                # optimizer-in-backward; the owner marks the parameter ready
+                fused_update.applied(ctx.wfc_param, grad_written=keep)
         link = ctx.link
         link.g2m, link.kbuf, link.aff2 = g2m, kbuf, aff2
         shape, dtype, device = ctx.y2_meta

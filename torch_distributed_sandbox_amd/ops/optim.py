@@ -22,6 +22,7 @@ class SGD(torch.optim.Optimizer):
         super().__init__(params, defaults)
         self._flat = None  # (flat_param, flat_grad) when installed by DDP
         self._deferred = None  # ([(offset, numel)], runner) when DDP overlaps part of the update
+        self._stepped = None  # predicate: parameter already stepped inside its backward (no .grad)
 
     def set_flat_buffers(self, flat_param: torch.Tensor, flat_grad: torch.Tensor, params):
         """Declare that ``params`` are views of ``flat_param`` with grads in ``flat_grad``."""
@@ -31,10 +32,13 @@ class SGD(torch.optim.Optimizer):
         else:
             self._flat = None
 
-    def set_deferred(self, ranges, runner):
+    def set_deferred(self, ranges, runner, stepped=None):
         """DDP(overlap_optimizer=True): the flat ranges in ``ranges`` are updated by
-        ``runner(update_fn)`` on DDP's side stream; the rest here, on the current stream."""
+        ``runner(update_fn)`` on DDP's side stream; the rest here, on the current stream.
+        ``stepped(p)``: True for a parameter whose update already ran inside its backward
+        kernel without a gradient (ops/fused_update.py); the runner skips it."""
         self._deferred = (sorted(ranges), runner) if ranges else None
+        self._stepped = stepped
 
     def _flat_ok(self):
         if self._flat is None:
@@ -42,6 +46,8 @@ class SGD(torch.optim.Optimizer):
         fp, fg, params = self._flat
         for p in params:
             if p.grad is None:
+                if self._deferred is not None and self._stepped is not None and self._stepped(p):
+                    continue
                 return False
             # grads must still be views of the flat bucket
             if p.grad.untyped_storage().data_ptr() != fg.untyped_storage().data_ptr():

@@ -70,7 +70,7 @@ class DistributedDataParallel(nn.Module):
                  process_group=None, bucket_cap_mb: Optional[float] = None, find_unused_parameters: bool = False,
                  gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False,
                  reducer: str = "auto", grad_exchange: str = "auto", overlap_optimizer: bool = False,
-                 fuse_update_in_backward: bool = True):
+                 fuse_update_in_backward: bool = True, keep_fused_grads: bool = False):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -179,6 +179,10 @@ class DistributedDataParallel(nn.Module):
         # update) on a side stream while the next forward's convolutions run
         self.overlap_optimizer = bool(overlap_optimizer) and dev.type == "cuda" and self.flat_param is not None
         self.fuse_update_in_backward = bool(fuse_update_in_backward)
+        # a parameter updated inside its backward kernel gets no .grad unless asked (torch's
+        # optimizer-in-backward semantics; ops/fused_update.py)
+        self.keep_fused_grads = bool(keep_fused_grads)
+        self._param_index = {id(p): i for i, p in enumerate(self._params)}
         self._fused_done = set()  # ids of params whose step ran inside their backward kernel
         self._deferred: List[_Bucket] = []
         self._deferred_works = {}
@@ -422,7 +426,8 @@ class DistributedDataParallel(nn.Module):
         if self.flat_param is not None and hasattr(optimizer, "set_flat_buffers"):
             optimizer.set_flat_buffers(self.flat_param, self.flat_grad, self._params)
             if self._deferred and hasattr(optimizer, "set_deferred"):
-                optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred], self._run_deferred_update)
+                optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred], self._run_deferred_update,
+                                       lambda p: id(p) in self._fused_done)
                 if self.world_size == 1 and self.fuse_update_in_backward:
                     self._register_fused_updates(optimizer)
         return optimizer
@@ -446,8 +451,12 @@ class DistributedDataParallel(nn.Module):
                     continue  # biases: tiny, updated by the optimizer as usual
 
                 def provider(what, p=p):
-                    if what == "applied":
+                    if what == "keep_grad":
+                        return self.keep_fused_grads
+                    if what in ("applied", "applied_no_grad"):
                         self._fused_done.add(id(p))
+                        if what == "applied_no_grad":
+                            self._mark_ready_without_grad(p)
                         return None
                     # only a plain synchronised step whose gradient lands straight in the bucket
                     if not self.require_backward_grad_sync or p.grad is not None or id(p) in self._fused_done:
@@ -455,6 +464,22 @@ class DistributedDataParallel(nn.Module):
                     return plain_sgd_lr()
 
                 fused_update.register(p, provider)
+
+    def _mark_ready_without_grad(self, p):
+        """Count ``p`` as ready for its bucket although autograd produced no gradient for it
+        (its update ran in the backward kernel, ops/fused_update.py)."""
+        if self._native is not None:
+            self._native.mark_ready(self._param_index[id(p)])
+            return
+        if not self._callback_queued:
+            self._callback_queued = True
+            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
+        b = self._bucket_of[id(p)]
+        if b.skip:
+            return
+        b.pending -= 1
+        if b.pending == 0:
+            self._launch(b)
 
     def _run_deferred_update(self, update_fn):
         """Finish the deferred buckets on the side stream: wait for this step's
