@@ -52,8 +52,15 @@ def _parser():
     ap.add_argument("--backend", default=os.environ.get("TDS_BENCH_BACKEND"),
                     help="rccl-native (default on GPU: this package's C++ RCCL communicator + C++ reducer) | "
                          "rccl (torch ProcessGroupNCCL = RCCL) | gloo | host")
-    ap.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations", "sharded"],
+    ap.add_argument("--grad-exchange", default="auto",
+                    choices=["auto", "allreduce", "activations", "sharded", "chunked"],
                     help="fc gradient path under DDP (parallel/factored.py); auto picks by the xGMI byte model")
+    ap.add_argument("--allreduce-chunks", type=int, default=None,
+                    help="K-chunks of the fc weight gradient in the all-reduce regime (default 4 on GPU)")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="keep N CUs out of the compute (CU-masked stream) for RCCL's kernels (utils/streams.py)")
+    ap.add_argument("--rccl-max-ctas", type=int, default=0,
+                    help="bound RCCL's workgroups per collective (ncclConfig maxCTAs; TDS_RCCL_MAX_CTAS)")
     ap.add_argument("--overlap-optimizer", action=argparse.BooleanOptionalAction, default=True,
                     help="finish the fc bucket (collective + SGD) on a side stream under the next forward's convs")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -131,7 +138,9 @@ def run(argv) -> None:
         device = torch.device("cuda", local_rank)
     else:
         device = torch.device("cpu")
-    if world > 1 or args.grad_exchange in ("activations", "sharded"):
+    if args.rccl_max_ctas > 0:
+        os.environ["TDS_RCCL_MAX_CTAS"] = str(args.rccl_max_ctas)
+    if world > 1 or args.grad_exchange in ("activations", "sharded", "chunked"):
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
@@ -149,6 +158,11 @@ def run(argv) -> None:
             if float(t.item()) != want:
                 raise RuntimeError(f"rccl-native sanity all-reduce gave {float(t.item())}, expected {want}")
 
+    if on_gpu and args.reserve_cus > 0:
+        # CU-masked compute stream, current for everything below (utils/streams.py)
+        from torch_distributed_sandbox_amd.utils.streams import reserve_cus_for_comm
+
+        torch.cuda.set_stream(reserve_cus_for_comm(args.reserve_cus, device))
     H = W = args.image_size
     B = args.batch_size
     torch.manual_seed(0)
@@ -156,7 +170,9 @@ def run(argv) -> None:
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), 1e-4)
     ddp = DistributedDataParallel(model, device_ids=[local_rank] if on_gpu else None, bucket_cap_mb=args.bucket_mb,
-                                  grad_exchange=args.grad_exchange, overlap_optimizer=args.overlap_optimizer)
+                                  grad_exchange=args.grad_exchange, overlap_optimizer=args.overlap_optimizer,
+                                  allreduce_chunks=args.allreduce_chunks)
+
     ddp.attach_optimizer(optimizer)
 
     # a pool of synthetic 28x28 sources; each step upsamples a different slice on device
@@ -212,6 +228,9 @@ def run(argv) -> None:
             "reducer": ddp.reducer_kind,
             "overlap_optimizer": ddp.overlap_optimizer,
             "fc_grad": ddp.fc_grad_path(),
+            "allreduce_chunks": ddp.allreduce_chunks,
+            "reserve_cus": args.reserve_cus,
+            "rccl_max_ctas": args.rccl_max_ctas or None,
             "optimizer": "SGD(lr=1e-4)",
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3) if on_gpu else None,
             "final_loss": final_loss,

@@ -135,7 +135,7 @@ def test_linear_dw_kernel(gpu):
     assert (full[:, :3000] == 7).all() and (full[:, 6000:] == 7).all()
 
 
-@pytest.mark.parametrize("mode", ["activations", "sharded"])
+@pytest.mark.parametrize("mode", ["activations", "sharded", "chunked"])
 def test_activation_exchange_fused_convnet(pg, gpu, mode):
     """Forced activation exchange at world size 1 runs the whole GPU path (head
     forward writing the fc input rows, head backward without dW, linear_dw into
@@ -175,6 +175,7 @@ def test_activation_exchange_fused_convnet(pg, gpu, mode):
 
 
 @pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("sharded", False),
+                                           ("chunked", False),
                                            ("allreduce", True)])
 def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     """overlap_optimizer: the fc bucket's collective + SGD update run on a side stream
@@ -273,3 +274,38 @@ def test_rccl_native_count_and_sendrecv(pg, gpu):
     comm.sendrecv(sends, [0] * 4, recvs, [0] * 4).wait()
     torch.cuda.synchronize()
     assert torch.equal(out, x[:, 2:5])
+
+
+def test_cu_reserve_and_masked_stream(gpu):
+    """utils/streams.py: a CU-masked compute stream with 16 CUs left to communication kernels;
+    the persistent kernels size their grids to the remaining CUs and the step matches the
+    full-chip one (summation order of the per-workgroup partials differs)."""
+    import copy
+
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import CrossEntropyLoss
+    from torch_distributed_sandbox_amd.utils.streams import compute_cus, reserve_cus_for_comm
+
+    torch.manual_seed(0)
+    H = 128
+    m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    m2 = copy.deepcopy(m1)
+    x = torch.rand(2, 1, H, H, device=gpu)
+    y = torch.tensor([1, 8], device=gpu)
+    full = compute_cus()
+    CrossEntropyLoss()(m1(x), y).backward()
+    try:
+        s = reserve_cus_for_comm(16, gpu)
+        assert compute_cus() == full - 16
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            CrossEntropyLoss()(m2(x), y).backward()
+        torch.cuda.current_stream().wait_stream(s)
+    finally:
+        reserve_cus_for_comm(0)
+    assert compute_cus() == full
+    torch.cuda.synchronize()
+    for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
+        if n.endswith("0.bias"):
+            continue
+        torch.testing.assert_close(q.grad, p.grad, rtol=1e-4, atol=1e-7, msg=n)

@@ -244,7 +244,7 @@ def _w_exchange(rank, world, port, backend, H, B, mode="auto"):
     torch.manual_seed(0)
     m_ex = ConvNet(image_shape=(H, H))
     m_ar = copy.deepcopy(m_ex)
-    d_ex = DistributedDataParallel(m_ex, grad_exchange=mode)
+    d_ex = DistributedDataParallel(m_ex, grad_exchange=mode, allreduce_chunks=3 if mode == "chunked" else None)
     d_ar = DistributedDataParallel(m_ar, grad_exchange="allreduce")
     assert len(d_ex.exchanges) == 1 and not d_ar.exchanges
     # the fc layer owns bucket 0 alone in both layouts
@@ -270,7 +270,8 @@ def _w_exchange(rank, world, port, backend, H, B, mode="auto"):
         o_ex.step()
         o_ar.step()
     assert d_ex.exchanges[0].steps_exchanged == 3
-    assert d_ex.fc_grad_path() == ("sharded-exchange" if mode == "sharded" else "activation-exchange")
+    assert d_ex.fc_grad_path() == {"sharded": "sharded-exchange", "chunked": "chunked-allreduce"}.get(
+        mode, "activation-exchange")
     # accumulation: a no_sync step, then a synced step: the locally accumulated fc
     # gradient is all-reduced as it is and this step's exchanged average added
     with torch.no_grad():  # re-align the replicas (3 updates of a chaotic model drift at 1e-5)
@@ -303,6 +304,14 @@ def test_sharded_exchange_matches_allreduce(backend, world):
     shards) equals the bucket all-reduce average, including no_sync accumulation; gloo uses
     batched isend/irecv, the ring-only host backend the packed all-gather fallback."""
     launch.spawn(_w_exchange, args=(world, launch.find_free_port(), backend, 232, 2, "sharded"), nprocs=world,
+                 timeout=300)
+
+
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("host", 4)])
+def test_chunked_allreduce_matches_allreduce(backend, world):
+    """K-chunked fc weight gradient (column chunks formed one by one, each chunk's row
+    segments all-reduced as soon as it exists) equals the bucket all-reduce average."""
+    launch.spawn(_w_exchange, args=(world, launch.find_free_port(), backend, 232, 2, "chunked"), nprocs=world,
                  timeout=300)
 
 

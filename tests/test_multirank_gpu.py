@@ -81,7 +81,7 @@ def _ref_step(params, bufs, x, y):
 
 
 @pytest.mark.parametrize("overlap", [True, False])
-@pytest.mark.parametrize("mode", ["allreduce", "activations", "sharded"])
+@pytest.mark.parametrize("mode", ["allreduce", "activations", "sharded", "chunked"])
 def test_fused_ddp_two_ranks_matches_fp64_average(gpu, tmp_path, mode, overlap):
     from torch_distributed_sandbox_amd.parallel import launch
 
@@ -90,7 +90,7 @@ def test_fused_ddp_two_ranks_matches_fp64_average(gpu, tmp_path, mode, overlap):
                  timeout=240)
     recs = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
     assert recs[0]["fc_grad"] == {"allreduce": "allreduce", "activations": "activation-exchange",
-                                  "sharded": "sharded-exchange"}[mode]
+                                  "sharded": "sharded-exchange", "chunked": "chunked-allreduce"}[mode]
     xs, ys = _data(world)
     params, bufs0 = recs[0]["p0"], recs[0]["b0"]
     for s in range(STEPS):

@@ -222,14 +222,25 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
 // kbuf = [k1|k2|k3] (dy2 = k1*dz + k2*y2 + k3, rebuilt tile by tile inside the conv2 backward).
 // update_lr > 0: the plain-SGD step of fc.weight runs in the same pass (W -= lr * dW).
 // returns (dW [into dw_out if given; empty when !compute_dw], db_fc, dgamma2, dbeta2, g2m, kbuf)
+// BN2 partial-sum workspace (doubles) of the head backward for B images at pooled size P/2
+int64_t head_bwd_workspace(int64_t B, int64_t P) {
+  const int Q = (int)(P / 2);
+  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_pb_nblk(Q) * 2;
+}
+
+// Channels [c_begin, c_end) of the head backward (K-chunked fc gradient): the caller passes the
+// same g2m_out / partial_out to every chunk and finalize=True on the last one, which then runs
+// the BN2 backward finalize and the bias gradient (outputs 1-3 and 5 are empty before that).
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     const Tensor& dlogits, const Tensor& ya, const Tensor& stats2, const Tensor& aff2,
     const c10::optional<Tensor>& gamma2, const Tensor& wfc, int64_t P, const c10::optional<Tensor>& dw_out,
     double scale, bool compute_dw, double update_lr, const c10::optional<Tensor>& dbfc_out,
-    const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out, bool keep_dw) {
+    const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out, bool keep_dw, int64_t c_begin,
+    int64_t c_end, bool finalize, const c10::optional<Tensor>& g2m_out, const c10::optional<Tensor>& partial_out) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_backward: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_backward: needs P/2 >= 4 pooled columns and B >= 1");
+  TORCH_CHECK(0 <= c_begin && c_begin < c_end && c_end <= 32, "fused_head_backward: bad channel range");
   need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
   const int64_t NC = wfc.size(0);
   need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
@@ -241,6 +252,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   hipStream_t st = stream_of(ya);
   const bool upd = update_lr > 0.0;
   TORCH_CHECK(keep_dw || upd, "fused_head_backward: keep_dw=False needs update_lr > 0 (update-only step)");
+  const bool whole = c_begin == 0 && c_end == 32;
+  TORCH_CHECK(whole || !upd, "fused_head_backward: the fused SGD step runs on the whole weight only");
   Tensor dW;  // undefined (None) for an update-only step
   if (!compute_dw) {
     dW = at::empty({0}, wfc.options());
@@ -249,19 +262,39 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     need(*dw_out, at::kFloat, {NC, 32 * Q * Q}, "dW_out");
     dW = *dw_out;
   } else {
+    TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into dw_out");
     dW = at::empty_like(wfc);
   }
   TORCH_CHECK(!upd || (compute_dw && tds_head_bwd_pb_npass((int)B) == 1),
               "fused_head_backward: update_lr needs compute_dw and a batch of <= 8 images");
-  auto g2m = at::empty({B, 32, Q, Q}, ya.options());  // planar (the fc flatten order)
+  Tensor g2m;
+  if (g2m_out.has_value() && g2m_out->defined()) {
+    need(*g2m_out, at::kFloat, {B, 32, Q, Q}, "g2m_out");
+    g2m = *g2m_out;
+  } else {
+    TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into g2m_out");
+    g2m = at::empty({B, 32, Q, Q}, ya.options());  // planar (the fc flatten order)
+  }
   const int nblk = tds_head_pb_nblk((int)Q), npass = tds_head_bwd_pb_npass((int)B);
-  auto partial = at::empty({(int64_t)32 * npass * nblk * 2}, ya.options().dtype(at::kDouble));
+  Tensor partial;
+  if (partial_out.has_value() && partial_out->defined()) {
+    need(*partial_out, at::kDouble, {head_bwd_workspace(B, P)}, "partial_out");
+    partial = *partial_out;
+  } else {
+    TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into partial_out");
+    partial = at::empty({(int64_t)32 * npass * nblk * 2}, ya.options().dtype(at::kDouble));
+  }
   const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
                                  dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
                                  compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                  upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
-                                 (float)scale, (float)update_lr, st);
+                                 (float)scale, (float)update_lr, (int)c_begin, (int)c_end, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
+  if (!finalize) {
+    check_launches("fused_head_backward");
+    const Tensor none = at::empty({0}, ya.options());
+    return {dW, none, none, none, g2m, none};
+  }
   auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
   auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");
   auto kbuf = at::empty({96}, ya.options());
@@ -304,6 +337,19 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   tds_conv2_wgrad_reduce(slab.data_ptr<float>(), nwg, dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, st);
   check_launches("fused_conv2_backward_y2");
   return {dp1, dw2, db2};
+}
+
+// CU budget (cu_budget.hip): reserve CUs for RCCL's kernels; persistent kernels size their
+// grids to the rest; a CU-masked stream for the compute (returned as a raw handle, wrapped in
+// torch.cuda.ExternalStream by utils/streams.py)
+void set_cu_reserve(int64_t n) { tds_set_cu_reserve((int)n); }
+int64_t cu_reserve() { return tds_cu_reserve(); }
+int64_t device_cus() { return tds_device_cus(); }
+int64_t cu_masked_stream(int64_t device, int64_t reserve) {
+  hipStream_t s = tds_cu_masked_stream((int)device, (int)reserve);
+  TORCH_CHECK(s != nullptr, "cu_masked_stream: hipExtStreamCreateWithCUMask failed (device ", device, ", reserve ",
+              reserve, ")");
+  return (int64_t)reinterpret_cast<intptr_t>(s);
 }
 
 // test hook: one launch of a trivial kernel with the given dynamic LDS / block size (a request
@@ -372,9 +418,11 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def(
       "fused_head_backward(Tensor dlogits, Tensor ya, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor(e!) wfc, "
       "int P, Tensor(a!)? dw_out, float scale, bool compute_dw=True, float update_lr=0.0, "
-      "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None, bool keep_dw=True) -> "
+      "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None, bool keep_dw=True, "
+      "int c_begin=0, int c_end=32, bool finalize=True, Tensor(f!)? g2m_out=None, Tensor(g!)? partial_out=None) -> "
       "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
+  m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
   m.def(
       "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale, "
       "Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
@@ -385,4 +433,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None) -> (Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_backward);
   m.def("launch_probe(Tensor like, int lds_bytes, int threads) -> ()", &launch_probe);
+  m.def("set_cu_reserve(int n) -> ()", &set_cu_reserve);
+  m.def("cu_reserve() -> int", &cu_reserve);
+  m.def("device_cus() -> int", &device_cus);
+  m.def("cu_masked_stream(int device, int reserve) -> int", &cu_masked_stream);
 }

@@ -357,7 +357,12 @@ struct B2Stager {
       }
       const float gg[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
       float d[4][4];
-      if (fast) {
+      if constexpr (DIAG == 9) {  // timing only: no BN2 / pool backward math (dy2 := y2 + g)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) d[q][cc] = y[q][cc] + gg[cc];
+      } else if (fast) {
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
           float z[4];
@@ -695,8 +700,9 @@ void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c) {
 }
 
 #ifdef TDS_DIAG
-// timing-only variants (tools/conv2_diag.py): 1 no MFMAs, 3 no global tile loads, 5 no staging,
-// 7 no y2 loads.  Compiled only into a -DTDS_DIAG build.
+// timing-only variants: 1 no MFMAs, 3 no global tile loads, 5 no staging, 7 no y2 loads, 9 no
+// BN2 / pool backward math in the staging.  Compiled only into a -DTDS_DIAG build
+// (python -m torch_distributed_sandbox_amd._build --variant diag -D TDS_DIAG; TDS_CONV2_DIAG=N).
 static int b3_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
   return e ? std::atoi(e) : 0;
@@ -729,6 +735,7 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
     case 3: TDS_B3_LAUNCH(3) break;
     case 5: TDS_B3_LAUNCH(5) break;
     case 7: TDS_B3_LAUNCH(7) break;
+    case 9: TDS_B3_LAUNCH(9) break;
 #endif
     default: TDS_B3_LAUNCH(0) break;
   }

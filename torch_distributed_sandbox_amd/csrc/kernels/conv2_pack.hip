@@ -90,14 +90,7 @@ void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t s
   TDS_LAUNCH_CHECK();
 }
 
-int tds_conv2_num_wg() {
-  int dev = 0, n = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) n = prop.multiProcessorCount;
-  }
-  return n;
-}
+int tds_conv2_num_wg() { return tds_device_cus(); }
 
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st) {
   hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db, scale);

@@ -648,14 +648,7 @@ __global__ void l1_finalize_kernel(const double* __restrict__ bwd_sum, const dou
 
 using namespace tds;
 
-int tds_fused_num_wg(int per_cu) {
-  int dev = 0, n = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) n = prop.multiProcessorCount;
-  }
-  return n * per_cu;
-}
+int tds_fused_num_wg(int per_cu) { return tds_device_cus() * per_cu; }
 
 void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
                  double* gram, double* sums, hipStream_t st) {

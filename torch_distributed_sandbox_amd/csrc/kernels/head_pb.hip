@@ -251,11 +251,11 @@ template <int NB, bool WITH_DW, bool ACC, bool UPD, bool KEEP = true>
 __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     const float* __restrict__ ya, const float* W, const float* __restrict__ aff2, const float* __restrict__ dl,
     float* __restrict__ g2m, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass, int npass,
-    int NC, float scale, float lr) {
+    int NC, float scale, float lr, int c0) {
   __shared__ float red[2][HP_THREADS / 64];
   const HPGrid hg = hp_grid(g);
   const int wg = blockIdx.x;
-  const int c = wg / hg.per_channel(), band = wg - c * hg.per_channel();
+  const int c = c0 + wg / hg.per_channel(), band = wg - (c - c0) * hg.per_channel();
   float dls[NB * 10];  // dlogits of this pass: wave-uniform, scalar loads
 #pragma unroll
   for (int b = 0; b < NB; ++b)
@@ -388,20 +388,20 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 int tds_head_bwd_pb_npass(int B) { return (B + HP_MAXB - 1) / HP_MAXB; }
 
 int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
-                    double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr,
-                    hipStream_t st) {
-  if (B < 1 || NC < 1 || NC > 10 || Q < 1) return -1;
+                    double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
+                    int c1, hipStream_t st) {
+  if (B < 1 || NC < 1 || NC > 10 || Q < 1 || c0 < 0 || c1 > 32 || c0 >= c1) return -1;
   const int npass = tds_head_bwd_pb_npass(B);
   if (Wupd && npass != 1) return -2;  // the fused SGD step needs the whole dW in one pass
   const PBGeom g = pb_geom(Q);
-  const int nwg = 32 * hp_grid(g).per_channel();
+  const int nwg = (c1 - c0) * hp_grid(g).per_channel();
   for (int pass = 0; pass < npass; ++pass) {
     const int b0 = pass * HP_MAXB;
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
     const bool acc = pass > 0;
 #define TDS_HPB_E(NBV, WD, AC, UP, KP)                                                                             \
   hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, \
-                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr);
+                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0);
 #define TDS_HPB(NBV)                                   \
   case NBV:                                            \
     if (!dW && Wupd) {                                 \

@@ -63,7 +63,13 @@ void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  //
 
 // ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, bf16x3 split MFMA)
 void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t st);
-int tds_conv2_num_wg();  // CUs
+int tds_conv2_num_wg();  // CUs (tds_device_cus)
+// ---- cu_budget.hip: CUs the persistent kernels may use (all minus a reserve for RCCL) and
+// CU-masked compute streams
+int tds_device_cus();
+void tds_set_cu_reserve(int n);
+int tds_cu_reserve();
+hipStream_t tds_cu_masked_stream(int device, int reserve);
 int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c);  // host: blocked tile order table
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st);
 int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
@@ -105,6 +111,8 @@ int tds_head_pb_nblk(int Q);  // workgroups per channel
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st);
 int tds_head_bwd_pb_npass(int B);
+// channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
+// soon as its launch lands; the BN2 partials of the other channels are left untouched)
 int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
-                    double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr,
-                    hipStream_t st);
+                    double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
+                    int c1, hipStream_t st);

@@ -142,12 +142,12 @@ class _Head(torch.autograd.Function):
         ops = _ext.ops()
         P = y2.shape[1]
         x_out = None
-        if ex is not None:
+        if ex is not None and ex.planned(ya.shape[0]) in ("activations", "sharded"):
             x_out = torch.empty((ya.shape[0], wfc.shape[1]), device=ya.device, dtype=torch.float32)
         logits, stats2, aff2 = ops.fused_head_forward(ya, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
                                                       bfc, P, x_out)
-        if ex is not None and not ex.begin(x_out):
-            raise RuntimeError("activation exchange refused to start after ready() agreed")
+        if ex is not None and not ex.begin(x_out, rows=ya.shape[0]):
+            raise RuntimeError("fc gradient exchange refused to start after ready() agreed")
         ctx.save_for_backward(ya, stats2, aff2, g2, wfc)
         ctx.P = P
         ctx.y2_meta = (y2.shape, y2.dtype, y2.device)
@@ -164,7 +164,31 @@ class _Head(torch.autograd.Function):
         ex = ctx.ex
         ops = _ext.ops()
         P = ctx.P
-        if ex is not None:
+        if ex is not None and ex.active == "chunked":
+            # K-chunked fc gradient (parallel/factored.py): one launch per channel group, each
+            # group's dW columns all-reduced as soon as it lands; grads published by the exchange
+            (dw, acc_w), (db, acc_b) = ex.chunk_targets()
+            B, Q = ya.shape[0], P // 2
+            g2m_buf = torch.empty((B, 32, Q, Q), device=ya.device, dtype=torch.float32)
+            part = torch.empty(ops.head_bwd_workspace(B, P), device=ya.device, dtype=torch.float64)
+            _, dg_o, dbe_o = _sinks(ctx, ctx.small, (12, 4, 5))
+            # accumulating under no_sync(): this step's chunk goes to a scratch dW, then is added
+            dst = torch.empty_like(dw) if acc_w else dw
+            chunks = ex.column_chunks(wfc.shape[1], planes=32)
+            for i, (k0, k1) in enumerate(chunks):
+                last = i == len(chunks) - 1
+                res = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, dst, 1.0, True, 0.0,
+                                              None, dg_o if last else None, dbe_o if last else None, True,
+                                              k0 // (Q * Q), k1 // (Q * Q), last, g2m_buf, part)
+                if acc_w:
+                    dw[:, k0:k1].add_(dst[:, k0:k1])
+                ex.chunk_ready(dw, k0, k1)
+            _, dbfc_c, dg2, dbe2, g2m, kbuf = res
+            if db is not None:
+                db.add_(dbfc_c) if acc_b else db.copy_(dbfc_c)
+            ex.chunked_done(dw, db)
+            dW = dbfc = None
+        elif ex is not None:
             # fc gradients come from the activation exchange (parallel/factored.py)
             _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, None, 1.0,
                                                                  False)

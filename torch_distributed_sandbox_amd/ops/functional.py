@@ -186,7 +186,7 @@ class _ExchangedLinear(torch.autograd.Function):
     def backward(ctx, gy):
         x2, w = ctx.saved_tensors
         gy = gy.contiguous()
-        ctx.ex.defer(gy)
+        ctx.ex.defer(gy, x2)
         dx = None
         if ctx.needs_input_grad[0]:
             if gy.is_cuda and x2.shape[0] <= 8 and w.shape[0] <= 16:

@@ -70,7 +70,8 @@ class DistributedDataParallel(nn.Module):
                  process_group=None, bucket_cap_mb: Optional[float] = None, find_unused_parameters: bool = False,
                  gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False,
                  reducer: str = "auto", grad_exchange: str = "auto", overlap_optimizer: bool = False,
-                 fuse_update_in_backward: bool = True, keep_fused_grads: bool = False):
+                 fuse_update_in_backward: bool = True, keep_fused_grads: bool = False,
+                 allreduce_chunks: Optional[int] = None):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -92,11 +93,18 @@ class DistributedDataParallel(nn.Module):
         self._verify_param_shapes()
 
         # ---- flat layout in gradient-ready order (reverse definition order)
-        if grad_exchange not in ("auto", "allreduce", "activations", "sharded"):
-            raise ValueError(f"grad_exchange must be auto|allreduce|activations|sharded, got {grad_exchange!r}")
+        if grad_exchange not in ("auto", "allreduce", "activations", "sharded", "chunked"):
+            raise ValueError(f"grad_exchange must be auto|allreduce|activations|sharded|chunked, got {grad_exchange!r}")
         self.grad_exchange = grad_exchange
+        # K-chunked all-reduce of a big layer's weight gradient (parallel/factored.py, "chunked"):
+        # default 4 chunks on the GPU, off on the CPU
+        if allreduce_chunks is None:
+            allreduce_chunks = 4 if dev.type == "cuda" else 1
+        self.allreduce_chunks = max(1, int(allreduce_chunks))
+        if grad_exchange == "chunked" and self.allreduce_chunks < 2:
+            raise ValueError("grad_exchange='chunked' needs allreduce_chunks >= 2")
         big_layers = self._exchange_candidates(module)
-        exch_layers = big_layers if grad_exchange != "allreduce" else []
+        exch_layers = big_layers if grad_exchange != "allreduce" else []  # "allreduce": the plain bucket path
         layer_of = {id(p): lyr for lyr in big_layers for p in (lyr.weight, lyr.bias) if p is not None}
         order = list(reversed(self._params))
         cap_mb = 25.0 if bucket_cap_mb is None else float(bucket_cap_mb)
@@ -166,14 +174,14 @@ class DistributedDataParallel(nn.Module):
 
         # ---- activation exchange for huge skinny Linear layers (parallel/factored.py)
         self._exchanges = []
-        forced = grad_exchange in ("activations", "sharded")
+        forced = grad_exchange in ("activations", "sharded", "chunked")
         if exch_layers and (self.world_size > 1 or (forced and tdist.is_initialized())):
             for lyr in exch_layers:
                 b = self._layer_bucket[id(lyr)]
                 self._exchanges.append(factored.ActivationExchange(
                     lyr.weight, lyr.bias, process_group, self.world_size, grad_exchange,
                     self._make_skip_fn(b), self._make_view_fn(lyr.weight),
-                    self._make_view_fn(lyr.bias) if lyr.bias is not None else None))
+                    self._make_view_fn(lyr.bias) if lyr.bias is not None else None, chunks=self.allreduce_chunks))
 
         # ---- overlapped optimizer: the big layers' buckets finish (collective + SGD
         # update) on a side stream while the next forward's convolutions run

@@ -30,6 +30,16 @@ starts as soon as the forward has produced X).  Both exchanges start in the
 forward, so they overlap the whole backward (and, with DDP's overlapped
 optimizer, the next forward's convolutions) instead of only the conv backward.
 
+In the all-reduce regime (more rows than outputs, e.g. large per-rank batches) the
+dense gradient is the smallest message, and a third mode shortens its critical path:
+
+``chunked``      the layer's weight gradient is produced in C column chunks (the fused
+                 head: channel groups, one kernel launch each) and each chunk's N row
+                 segments are all-reduced (AVG) the moment its launch lands, instead of
+                 one 720 MB bucket all-reduce after the whole head backward.  Same bytes
+                 as the all-reduce; the first chunk's collective starts (C-1)/C of the
+                 head backward earlier and the chunks pipeline over the xGMI links.
+
 The result is the average DDP produces (floating-point summation order differs,
 as it does between all-reduce algorithms), bit-identical on every rank.
 
@@ -93,11 +103,13 @@ class ActivationExchange:
     """One exchange-capable Linear layer under DDP (see the module docstring)."""
 
     def __init__(self, weight: torch.nn.Parameter, bias: Optional[torch.nn.Parameter], group, world: int,
-                 mode: str, set_skip, weight_view, bias_view):
-        if mode not in ("auto", "activations", "sharded"):
-            raise ValueError(f"ActivationExchange mode must be auto|activations|sharded, got {mode!r}")
+                 mode: str, set_skip, weight_view, bias_view, chunks: int = 1):
+        if mode not in ("auto", "activations", "sharded", "chunked", "allreduce"):
+            raise ValueError(f"ActivationExchange mode must be auto|activations|sharded|chunked|allreduce, got {mode!r}")
         self.weight, self.bias = weight, bias
         self.group, self.world, self.mode = group, world, mode
+        self.chunks = max(1, int(chunks))
+        self._works = []  # chunked: the per-chunk all-reduce works of this step
         self._set_skip, self._wview, self._bview = set_skip, weight_view, bias_view
         self.armed = False
         self.active = None  # the path running this step, or None
@@ -114,14 +126,98 @@ class ActivationExchange:
 
     # ---------------------------------------------------------------- policy
     def path(self, rows: int) -> Optional[str]:
-        """"activations" | "sharded" for a step with ``rows`` local rows, or None (bucket all-reduce)."""
-        if self.mode != "auto":
+        """"activations" | "sharded" | "chunked" for a step with ``rows`` local rows, or None
+        (plain bucket all-reduce)."""
+        if self.mode in ("activations", "sharded"):
             return self.mode
+        if self.mode == "chunked":
+            return "chunked" if self.chunks > 1 else None
         if self.world <= 1:
             return None
-        out_f, in_f = self.weight.shape
-        p = choose_path(rows, out_f, in_f, self.world)
-        return None if p == "allreduce" else p
+        p = "allreduce"
+        if self.mode == "auto":
+            out_f, in_f = self.weight.shape
+            p = choose_path(rows, out_f, in_f, self.world)
+        if p == "allreduce":
+            return "chunked" if self.chunks > 1 else None
+        return p
+
+    def needs_rows(self) -> bool:
+        """Does the running exchange need the layer's input rows (X) from its forward?"""
+        return self.active in ("activations", "sharded")
+
+    # ---------------------------------------------------------------- chunked all-reduce
+    def column_chunks(self, in_f: int, planes: int = 0):
+        """The [k0, k1) column ranges of the chunked weight gradient: whole planes of
+        in_f / planes columns when ``planes`` (the fused head: channels) else 64-aligned."""
+        if planes:
+            per = in_f // planes
+            n = min(self.chunks, planes)
+            cuts = [round(i * planes / n) for i in range(n + 1)]
+            return [(cuts[i] * per, cuts[i + 1] * per) for i in range(n) if cuts[i + 1] > cuts[i]]
+        return [(a, e) for a, e in shard_bounds(in_f, self.chunks) if e > a]
+
+    def chunk_ready(self, dw: torch.Tensor, k0: int, k1: int):
+        """Columns [k0, k1) of ``dw`` are final on the current stream: all-reduce their N row
+        segments now (async AVG; the collective's stream waits for the producer)."""
+        from . import distributed as tdist
+
+        for j in range(dw.shape[0]):
+            self._works.append(tdist.all_reduce(dw[j, k0:k1], tdist.ReduceOp.AVG, group=self.group, async_op=True))
+
+    def chunked_done(self, dw: torch.Tensor, db: Optional[torch.Tensor]):
+        """All chunks issued: all-reduce the bias, then (end of backward) order the consumer
+        stream after every chunk and publish the gradients."""
+        from . import distributed as tdist
+
+        if db is not None:
+            self._works.append(tdist.all_reduce(db, tdist.ReduceOp.AVG, group=self.group, async_op=True))
+        works, self._works = self._works, []
+
+        def finish():
+            side = self.side_stream
+            if side is not None and dw.is_cuda:
+                with torch.cuda.stream(side):  # DDP's overlapped optimizer consumes them there
+                    for w in works:
+                        w.wait()
+            else:
+                for w in works:
+                    w.wait()
+            self.weight.grad = dw
+            if self.bias is not None:
+                self.bias.grad = db
+            self.last_path = "chunked-allreduce"
+            self.active = None
+            self.steps_exchanged += 1
+
+        torch.autograd.Variable._execution_engine.queue_callback(finish)
+
+    def chunk_targets(self):
+        """(dW, accumulate), (db, accumulate) for the chunked path: the bucket slots, or the
+        gradients accumulated locally under no_sync() -- this step's chunk is added and the
+        chunk of the sum all-reduced, which is what DDP's bucket all-reduce averages."""
+        out = []
+        for p, view_fn in ((self.weight, self._wview), (self.bias, self._bview)):
+            if p is None:
+                out.append((None, False))
+            elif p.grad is not None:
+                out.append((p.grad, True))
+            else:
+                out.append((view_fn(), False))
+        return out
+
+    def chunked_linear_backward(self, dy: torch.Tensor, x2: torch.Tensor):
+        """Generic layer (ops.functional.linear): dW = dYᵀX column chunk by column chunk into
+        the bucket slot, each chunk all-reduced as soon as it is formed."""
+        (dw, acc_w), (db, acc_b) = self.chunk_targets()
+        with torch.no_grad():
+            for k0, k1 in self.column_chunks(dw.shape[1]):
+                _dw_rows(dy, x2[:, k0:k1].contiguous(), dw[:, k0:k1], None, 1.0, acc_w, False)
+                self.chunk_ready(dw, k0, k1)
+            if db is not None:
+                s_b = dy.sum(0)
+                db.add_(s_b) if acc_b else db.copy_(s_b)
+        self.chunked_done(dw, db)
 
     def worthwhile(self, rows: int) -> bool:
         return self.path(rows) is not None
@@ -137,18 +233,27 @@ class ActivationExchange:
             return None
         return self.path(rows)
 
+    def planned(self, rows: int) -> Optional[str]:
+        """The path a forward with ``rows`` rows would start now (None: plain bucket all-reduce)."""
+        return self._eligible(rows)
+
     def ready(self, rows: int) -> bool:
         """Would a forward with ``rows`` input rows (grad mode on) run an exchange?"""
         return torch.is_grad_enabled() and self._eligible(rows) is not None
 
-    def begin(self, x2d: torch.Tensor) -> bool:
+    def begin(self, x2d: Optional[torch.Tensor], rows: Optional[int] = None) -> bool:
         """Called from the layer's forward (possibly inside an autograd Function,
-        i.e. under no_grad) with its [rows, in] input.  Every rank has the same rows."""
-        path = self._eligible(x2d.shape[0])
+        i.e. under no_grad) with its [rows, in] input (None with ``rows`` when the chunked
+        path, which needs no X, was agreed by ``ready``).  Every rank has the same rows."""
+        path = self._eligible(x2d.shape[0] if x2d is not None else int(rows))
         if path is None:
             return False
         from . import distributed as tdist
 
+        if path == "chunked":
+            self.active = path
+            self._set_skip(True)
+            return True
         x2d = x2d.detach().contiguous()
         rows, in_f = x2d.shape
         if path == "activations":
@@ -169,12 +274,16 @@ class ActivationExchange:
         return True
 
     # ---------------------------------------------------------------- backward
-    def defer(self, dy: torch.Tensor):
+    def defer(self, dy: torch.Tensor, x2: Optional[torch.Tensor] = None):
         """Called from the layer's backward with dY.  On the GPU the rest of the exchange
         (dY gather, dW formation, shard all-gather) is issued right here on a side stream,
         so it overlaps the rest of the backward; the compute stream only waits for it at
         the end of backward (or, under DDP's overlapped optimizer, the optimizer's side
-        stream does).  On the CPU it runs from an end-of-backward callback."""
+        stream does).  On the CPU it runs from an end-of-backward callback.  ``chunked``: the
+        weight gradient is formed here from ``x2`` chunk by chunk, each chunk all-reduced."""
+        if self.active == "chunked":
+            self.chunked_linear_backward(dy.detach().contiguous(), x2.detach())
+            return
         self._dy = dy.detach().contiguous()
         if not self._dy.is_cuda:
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
