@@ -118,3 +118,14 @@ def test_bench_spawn_failure_propagates_cpu():
               "--backend", "host", "--shared-device"], timeout=200)
     assert p.returncode != 0
     assert not _json_lines(p.stdout)
+
+
+def test_bench_allreduce_cpu_rehearsal():
+    """tools/bench_allreduce.py end to end on 2 gloo ranks (tiny sizes): the all-reduce sweep
+    and the fc-gradient exchange paths it times on the 8-GPU node."""
+    p = _run(["tools/bench_allreduce.py", "--gpus", "2", "--device", "cpu", "--backend", "gloo", "--max-bytes", "4096",
+              "--iters", "2", "--warmup", "1", "--no-ddp-sizes", "--exchanges", "--rows", "2", "--in-features", "4096"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+    assert rec["world"] == 2 and len(rec["rows"]) == 6
+    assert [r["path"].split()[0] for r in rec["exchanges"]] == ["activations", "sharded", "chunked", "allreduce"]
