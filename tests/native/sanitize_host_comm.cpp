@@ -48,14 +48,20 @@ void rank_main(int rank, int world, int port, std::string* err) {
       store.wait("val/" + std::to_string(r), 20000);
       check(tensor_str(store.get("val/" + std::to_string(r))) == "v" + std::to_string(r * 7), "store get");
     }
-    // exactly one rank wins the CAS from "" to its own id
-    auto got = store.compare_set("owner", str_tensor(""), str_tensor(std::to_string(rank)));
-    (void)got;
+    // exactly one rank wins the CAS from "" to its own id: a winner sees its own id come back
+    // (compare_set returns the value now stored) and counts itself
+    const std::string me = std::to_string(rank);
+    const std::string got = tensor_str(store.compare_set("owner", str_tensor(""), str_tensor(me)));
+    const bool won = got == me;
+    if (won) store.add("cas_wins", 1);
     store.add("arrive", 1);
     while (store.add("arrive", 0) < world) std::this_thread::sleep_for(std::chrono::milliseconds(1));
     check(store.add("ctr", 0) == 200 * world, "store counter");
     const std::string owner = tensor_str(store.get("owner"));
     check(!owner.empty() && std::stoi(owner) >= 0 && std::stoi(owner) < world, "store CAS owner");
+    check(store.add("cas_wins", 0) == 1, "store CAS: exactly one winner");
+    check(won == (owner == me), "store CAS: the winner is the stored owner");
+    check(got == owner, "store CAS: every loser sees the winner's id");
 
     // ---- ring backend
     HostComm comm(rank, world, 20000);

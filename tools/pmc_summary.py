@@ -15,19 +15,26 @@ import os
 import sys
 
 
+def _pass_key(d):
+    """A pass is named by its full (normalised) path: two passes may share a leaf name."""
+    return os.path.normpath(os.path.abspath(d))
+
+
 def read_pass(d):
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     spans = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
             vals[r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            spans[r["Dispatch_Id"]] = (r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            # dispatch ids restart per process / agent: key by (file, agent, dispatch)
+            key = (path, r.get("Agent_Id", ""), r["Dispatch_Id"])
+            spans[key] = (r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     # profiled (serialised) kernel time of this pass, us per dispatch
     per_k = collections.defaultdict(list)
     for k, ns in spans.values():
         per_k[k].append(ns / 1e3)
     for k, v in per_k.items():
-        vals[k]["_time_us:" + os.path.basename(d.rstrip("/"))] = v
+        vals[k]["_time_us:" + _pass_key(d)] = v
     return vals
 
 
@@ -60,7 +67,7 @@ def main():
             derived = []
             def pass_time(counter):
                 for d in dirs:
-                    name = os.path.basename(d.rstrip("/"))
+                    name = _pass_key(d)
                     if name in pt and counter in read_cache[d].get(k, {}):
                         return pt[name]
                 return t_us
@@ -71,10 +78,17 @@ def main():
                 derived.append(("HBM write GB/s (WRITE_SIZE KB / profiled time)",
                                 cs["WRITE_SIZE"] * 1024 / (pass_time("WRITE_SIZE") * 1e3)))
             if "SQ_VALU_MFMA_BUSY_CYCLES" in cs:
-                # summed over the 1024 SIMDs; cycles at an assumed 2.4 GHz shader clock
+                # summed over the SIMDs (ASSUMED 1024 = 256 CUs x 4).  Clock: measured from
+                # GRBM_GUI_ACTIVE (summed over the 8 XCDs) when that counter was collected,
+                # otherwise an ASSUMED 2.4 GHz -- the label says which
                 tm = pass_time("SQ_VALU_MFMA_BUSY_CYCLES")
-                derived.append(("MFMA busy fraction (MFMA_BUSY / 1024 SIMDs / (profiled time x 2.4 GHz))",
-                                cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (tm * 1e-6 * 2.4e9)))
+                if cs.get("GRBM_GUI_ACTIVE", 0) > 0:
+                    ghz = cs["GRBM_GUI_ACTIVE"] / 8 / (pass_time("GRBM_GUI_ACTIVE") * 1e3)
+                    label = f"measured {ghz:.2f} GHz (GRBM_GUI_ACTIVE / 8 XCDs / time)"
+                else:
+                    ghz, label = 2.4, "ASSUMED 2.4 GHz"
+                derived.append((f"MFMA busy fraction (MFMA_BUSY / ASSUMED 1024 SIMDs / (profiled time x {label}))",
+                                cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (tm * 1e-6 * ghz * 1e9)))
             if "SQ_LDS_BANK_CONFLICT" in cs and cs.get("SQ_LDS_IDX_ACTIVE", 0) > 0:
                 derived.append(("LDS bank-conflict cycles / LDS active", cs["SQ_LDS_BANK_CONFLICT"] / cs["SQ_LDS_IDX_ACTIVE"]))
             for name, v in derived:
