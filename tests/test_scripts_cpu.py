@@ -51,13 +51,14 @@ def test_test_init_pytest_collectable():
 
 def test_mnist_onegpu_cpu_learns():
     p = _run(["mnist_onegpu.py", "--device", "cpu", "--image-size", "32", "--epochs", "1", "--max-steps", "60",
-              "--log-interval", "20", "--lr", "0.05", "--dataset-size", "600", "--json"])
+              "--log-interval", "20", "--lr", "0.05", "--dataset-size", "600", "--json", "--phase-times"])
     assert p.returncode == 0, p.stderr
     losses = [float(x) for x in re.findall(r"Epoch \[1/1\], Step \[\d+/60\], Loss: ([\d.]+)", p.stdout)]
     assert len(losses) == 3
     assert "Training complete in: " in p.stdout
     summ = json.loads(p.stdout.strip().splitlines()[-1])
     assert summ["steps"] == 60
+    assert set(summ["phases"]) == {"forward", "backward", "optimizer"}  # StepTimer (host wall time on CPU)
 
 
 def test_mnist_distributed_cpu(tmp_path):

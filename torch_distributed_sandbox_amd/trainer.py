@@ -26,7 +26,7 @@ from .ops import CrossEntropyLoss, SGD
 from .parallel import DistributedDataParallel, DistributedSampler
 from .parallel import distributed as tdist
 from .utils import checkpoint, fault
-from .utils.timing import nvtx_range
+from .utils.timing import StepTimer
 
 
 def add_common_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
@@ -42,8 +42,11 @@ def add_common_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--checkpoint", default="", help="save a checkpoint here at the end (rank 0)")
     p.add_argument("--resume", default="", help="resume from this checkpoint")
     p.add_argument("--json", action="store_true", help="print a JSON summary line at the end")
-    p.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations"],
+    p.add_argument("--grad-exchange", default="auto", choices=["auto", "allreduce", "activations", "sharded", "chunked"],
                    help="DDP gradient path of the big fc layer (parallel/factored.py)")
+    p.add_argument("--phase-times", action="store_true",
+                   help="time forward / backward / optimizer per step with HIP events (utils/timing.StepTimer; "
+                        "adds them to the summary; roctx ranges with TDS_ROCTX=1)")
     p.add_argument("--overlap-optimizer", action=argparse.BooleanOptionalAction, default=True,
                    help="finish the fc bucket (collective + SGD) on a side stream under the next forward")
     p.add_argument("--bucket-mb", default=None, type=float, help="DDP bucket cap (MB, default 25 like torch)")
@@ -102,19 +105,20 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
     steps_done = 0
     t_first = None
     loss = None
+    timer = StepTimer(enabled=getattr(args, "phase_times", False) and device.type == "cuda")
     for epoch in range(start_epoch, args.epochs):
         loader.set_epoch(epoch)
         for i, (images, labels) in enumerate(loader):
             if args.max_steps and i >= args.max_steps:
                 break
             fault.maybe_inject(rank, steps_done)
-            with nvtx_range("forward"):
+            with timer.phase("forward"):
                 outputs = model(images)
                 loss = criterion(outputs, labels)
             optimizer.zero_grad()
-            with nvtx_range("backward"):
+            with timer.phase("backward"):
                 loss.backward()
-            with nvtx_range("optimizer"):
+            with timer.phase("optimizer"):
                 optimizer.step()
             if distributed:
                 # the reference builds a group every step (mnist_distributed.py:99-100); cached here
@@ -149,6 +153,8 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
         summary["ms_per_step"] = 1e3 * dt / (steps_done - 1)
     if device.type == "cuda":
         summary["peak_mem_gb"] = torch.cuda.max_memory_allocated(device) / 1e9
+    if getattr(args, "phase_times", False):
+        summary["phases"] = timer.summary()
     if gpu == 0:
         print("Training complete in: " + str(datetime.now() - start), flush=True)
         if args.json:

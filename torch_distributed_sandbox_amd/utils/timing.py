@@ -48,7 +48,9 @@ def nvtx_range(name: str):
 
 
 class StepTimer:
-    """Per-phase GPU timing with events; call :meth:`summary` after a sync."""
+    """Per-phase GPU timing with events (``trainer.py --phase-times``); call :meth:`summary`
+    at the end.  Disabled, a phase only records host wall time (and still emits its roctx
+    range when ``TDS_ROCTX=1``)."""
 
     def __init__(self, enabled: bool = True):
         self.enabled = enabled and torch.cuda.is_available()
@@ -59,7 +61,8 @@ class StepTimer:
     def phase(self, name: str):
         if not self.enabled:
             t0 = time.perf_counter()
-            yield
+            with nvtx_range(name):
+                yield
             self._wall[name] += time.perf_counter() - t0
             return
         s = torch.cuda.Event(enable_timing=True)
