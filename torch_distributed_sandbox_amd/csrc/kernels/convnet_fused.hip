@@ -168,7 +168,11 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
               hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
               lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
             }
+#if defined(TDS_L1_EXP) && TDS_L1_EXP == 2
+            acc[a][c] = f32x4{(float)(bh[0] ^ bl[1]), (float)wah[0], (float)wal[1], 0.f};
+#else
             acc[a][c] = mfma_bf16x3(wah, wal, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
+#endif
           }
         // BN1 affine -> 2x2 max-pool (first max in scan order) -> ReLU -> bf16 hi|lo record +
         // argmax byte (bit 2 = ReLU passes the gradient) for channels 4g .. 4g+3
@@ -199,7 +203,11 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
         uint32_t h01, l01, h23, l23;
         split2_bf16(pv[0], pv[1], h01, l01);
         split2_bf16(pv[2], pv[3], h23, l23);
+#if defined(TDS_L1_EXP) && TDS_L1_EXP == 1
+        if (prow < P && pcol < PW && pv[0] == 1234.5f) {
+#else
         if (prow < P && pcol < PW) {
+#endif
           const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
           uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
           dst[g] = make_uint2(h01, h23);

@@ -23,9 +23,11 @@
 //   ya  : one float4 per image (the 4 waves together read one 4 KiB run per image),
 //   W   : one 4-float group per class from the fc's own (c, h, w) layout at the same row and
 //         columns -- a wave-instruction covers one 1 KiB row run.  A row starts at a 16-B boundary
-//         only when (c*Q*Q + y*Q) % 4 == 0 (for Q = 750 every odd row is 8 B off): the group is
-//         then moved as two float2 (or four floats), picked per wave, so no access straddles a
-//         16-B granule -- misaligned dwordx4 stores of the weight update cost 14% of the backward,
+//         only when (c*Q*Q + y*Q) % 4 == 0 (for Q = 750 every odd row is 8 B off).  Loads are
+//         dwordx4 at any dword alignment (split loads cost the forward ~50%: 0.27 vs 0.18 ms for
+//         the same bytes); stores of a misaligned group are moved as two float2 (or four floats),
+//         picked per wave, so no store straddles a 16-B granule -- misaligned dwordx4 stores of
+//         the weight update cost 14% of the backward,
 //   g2m : one float4 per image (same index as ya), dW / updated W: one 4-float group per class.
 // No LDS and no barriers in the stream: the next chunk's loads are issued before the current
 // one is reduced.  64-bit indexing throughout (no buffer descriptors).
@@ -38,6 +40,10 @@ namespace tds {
 constexpr int HP_THREADS = 256;
 constexpr int HP_BAND = 4;                  // block rows per workgroup
 constexpr int HP_MAXB = 8;                  // images per pass (larger batches run in passes)
+#ifndef TDS_HP_PF
+#define TDS_HP_PF 1
+#endif
+constexpr bool HP_PF = TDS_HP_PF != 0;      // register prefetch of the next chunk
 
 struct HPGrid {
   int nband;
@@ -95,26 +101,17 @@ struct HPRow {
   }
 };
 
-template <int AL>
-__device__ __forceinline__ float4 hp_ld4a(const float* p) {
-  if constexpr (AL == 0) return *reinterpret_cast<const float4*>(p);
-  if constexpr (AL == 2) {
-    const float2 u = *reinterpret_cast<const float2*>(p), v = *reinterpret_cast<const float2*>(p + 2);
-    return make_float4(u.x, u.y, v.x, v.y);
-  }
-  return make_float4(p[0], p[1], p[2], p[3]);
-}
+// 4 consecutive floats at any dword alignment (one global_load_dwordx4)
+__device__ __forceinline__ float4 hp_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
 // loads of one chunk: ya float4 per image, weight 4-groups per class (zeros outside the image)
 template <int NB>
 struct HPLoad {
   float4 y[NB], w[10];
-  template <int AL>
-  __device__ __forceinline__ void issue_w(const float* W, int64_t QQ, const HPRow& rw, int NC) {
-#pragma unroll
-    for (int j = 0; j < 10; ++j)
-      if (j < NC) w[j] = hp_ld4a<AL>(W + (int64_t)j * 32 * QQ + rw.ldoff);
-  }
+  int sh, nvalid;  // this lane's edge geometry for fix()
+  // the loads only: their consumers (fix(), the reduction) run one iteration later, so the wait
+  // for them is vmcnt(#loads of the NEXT chunk) -- an edge fix-up right after the loads made
+  // it a vmcnt(0) on the prefetch and serialised every chunk on its own latency
   __device__ __forceinline__ void issue(const float* __restrict__ ya, const float* W, const PBGeom& g, const HPThread& th,
                                         int c, int R, int b0, int NC) {
     const int64_t plane = g.plane(), QQ = (int64_t)g.Q * g.Q;
@@ -123,10 +120,18 @@ struct HPLoad {
 #pragma unroll
     for (int b = 0; b < NB; ++b) y[b] = *reinterpret_cast<const float4*>(ya + (int64_t)(b0 + b) * 32 * plane + yi);
     const HPRow rw(g, th, c, R);
-    if (rw.al == 0) issue_w<0>(W, QQ, rw, NC);
-    else if (rw.al == 2) issue_w<2>(W, QQ, rw, NC);
-    else issue_w<1>(W, QQ, rw, NC);
-    // re-align the shifted edge groups, zero what lies outside the image (and classes >= NC)
+    sh = rw.sh;
+    nvalid = rw.nvalid;
+    // one dwordx4 per group at any dword alignment (global loads need only 4-B alignment;
+    // tools/micro/head_stream_bw.hip streams this exact pattern with 8-B-misaligned odd rows at
+    // 6.1 TB/s).  Only the STORES split misaligned groups (hp_st4).  Classes >= NC read class 0.
+#pragma unroll
+    for (int j = 0; j < 10; ++j) w[j] = hp_ld4(W + (int64_t)(j < NC ? j : 0) * 32 * QQ + rw.ldoff);
+  }
+  // re-align the shifted edge groups, zero what lies outside the image and classes >= NC;
+  // wave-uniformly skipped for interior chunks with all classes present
+  __device__ __forceinline__ void fix(int NC) {
+    if (NC == 10 && __builtin_amdgcn_ballot_w64(sh != 0 || nvalid != 4) == 0) return;
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
       const float e[4] = {w[j].x, w[j].y, w[j].z, w[j].w};
@@ -134,8 +139,8 @@ struct HPLoad {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         float v = e[k];
-        if (rw.sh > 0) v = (k + rw.sh < 4) ? e[(k + rw.sh) & 3] : 0.f;
-        o[k] = (j < NC && k < rw.nvalid) ? v : 0.f;
+        if (sh > 0) v = (k + sh < 4) ? e[(k + sh) & 3] : 0.f;
+        o[k] = (j < NC && k < nvalid) ? v : 0.f;
       }
       w[j] = make_float4(o[0], o[1], o[2], o[3]);
     }
@@ -181,21 +186,27 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
   const int nch = (g.Q8 + 31) / 32;
   const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
   HPLoad<NB> cur, nxt;
-  if (nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
+  if (HP_PF && nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
 #pragma unroll 1
   for (int i = 0; i < nit; ++i) {
     const int R = R0 + i / nch;
     const HPThread th(i % nch);
-    if (i + 1 < nit)  // next chunk in flight
+    if (!HP_PF) cur.issue(ya, W, g, th, c, R, b0, NC);
+    if (HP_PF && i + 1 < nit)  // next chunk in flight
       nxt.issue(ya, W, g, HPThread((i + 1) % nch), c, R0 + (i + 1) / nch, b0, NC);
+    cur.fix(NC);
     const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
     const bool rok = th.blk < g.Q8 && py < Q;
+    const bool xfull = __builtin_amdgcn_ballot_w64(!(rok && px0 + 3 < Q)) == 0;  // wave-uniform
     float x[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
       const float yy[4] = {cur.y[b].x, cur.y[b].y, cur.y[b].z, cur.y[b].w};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) x[b][k] = (rok && px0 + k < Q) ? hp_relu(fmaf(a, yy[k], bb)) : 0.f;
+      for (int k = 0; k < 4; ++k) {
+        const float v = hp_relu(fmaf(a, yy[k], bb));
+        x[b][k] = (xfull || (rok && px0 + k < Q)) ? v : 0.f;
+      }
     }
     if (xout != nullptr && rok) {
 #pragma unroll
@@ -211,7 +222,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
       for (int b = 0; b < NB; ++b)
         acc[b][j] = fmaf(x[b][0], w4.x, fmaf(x[b][1], w4.y, fmaf(x[b][2], w4.z, fmaf(x[b][3], w4.w, acc[b][j]))));
     }
-    cur = nxt;
+    if (HP_PF) cur = nxt;
   }
   // deterministic workgroup reduction: waves (DPP), then 4 wave partials in fixed order
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -268,13 +279,15 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   const int nch = (g.Q8 + 31) / 32;
   const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
   HPLoad<NB> cur, nxt;
-  if (nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
+  if (HP_PF && nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
 #pragma unroll 1
   for (int i = 0; i < nit; ++i) {
     const int R = R0 + i / nch;
     const HPThread th(i % nch);
-    if (i + 1 < nit)  // next chunk in flight
+    if (!HP_PF) cur.issue(ya, W, g, th, c, R, b0, NC);
+    if (HP_PF && i + 1 < nit)  // next chunk in flight
       nxt.issue(ya, W, g, HPThread((i + 1) % nch), c, R0 + (i + 1) / nch, b0, NC);
+    cur.fix(NC);
     const bool bok = th.blk < g.Q8;
     const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
     const bool rok = bok && py < Q;
@@ -332,7 +345,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
         }
       }
     }
-    cur = nxt;
+    if (HP_PF) cur = nxt;
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   sdz = wave_sum(sdz);
