@@ -90,7 +90,7 @@ __device__ __forceinline__ void b2_xchg_put(f32x4* xs, const f32x4 (&acc)[8], in
 }
 
 // Wave D owns output rows 4D .. 4D+3: its partial + the partner's, then dp1.
-template <int D>
+template <int D, int DIAG = 0>
 __device__ __forceinline__ void b2_xchg_finish(const f32x4* xs, const f32x4 (&acc)[8], float* __restrict__ dp1,
                                                int lane, int b, int r0, int c0, int P) {
   const int li = lane & 15, g = lane >> 4;
@@ -98,7 +98,7 @@ __device__ __forceinline__ void b2_xchg_finish(const f32x4* xs, const f32x4 (&ac
   for (int i = 0; i < 4; ++i) {
     const f32x4 v = acc[4 * D + i] + xs[(D * 4 + i) * 64 + lane];
     const int row = r0 + 4 * D + i;
-    if (row < P) {
+    if (DIAG == 11 ? v[0] == 1234.5f : row < P) {  // DIAG 11 (timing only): no dp1 stores
       float* orow = dp1 + ((int64_t)b * P + row) * P * 16;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -119,7 +119,6 @@ struct B2Args {
   float* __restrict__ slab;
   const int* __restrict__ order;  // blocked tile order (tds_tile_order)
   int B, P, Q, tiles_r, tiles_c, per_img, total;
-  bool g2m_big;  // 32 g2m planes exceed a 4 GiB buffer-descriptor range: 64-bit loads
 };
 
 struct B2Tile {
@@ -149,7 +148,11 @@ __device__ __attribute__((aligned(16))) uint32_t g_b2_zero[4] = {0u, 0u, 0u, 0u}
 // The compiler cannot tell an LDS-DMA's destination from later LDS accesses, so every ds_read /
 // ds_write after one waits vmcnt(0) -- which drains the register loads issued for LATER
 // tiles too and defeats a multi-tile lookahead.
-template <int DIAG, int WV, bool REGP1 = false>  // WV: the wave (= role) this staging code runs in
+// BIG: 32 g2m planes of an image exceed a 4 GiB buffer-descriptor range (H >= 23170): 64-bit
+// g2m loads.  A template parameter, not a runtime flag: two alternative load paths under a
+// runtime branch make the compiler's wait-count analysis assume the fewer-loads path at the
+// merge and wait for vmcnt(0), draining the loads issued for later tiles.
+template <int DIAG, int WV, bool REGP1 = false, bool BIG = false>  // WV: the wave (= role) this staging code runs in
 struct B2Stager {
   float4 yv[B2_IPER][4], gv[B2_IPER];
   uint4 pr[REGP1 ? B2_DMA_PER_WAVE : 1];
@@ -181,7 +184,7 @@ struct B2Stager {
       int wy, wx;
       item_geom(tid, u, wy, wx);
       yoff[u] = (uint32_t)(((2 * wy) * a.P + 2 * wx) * 128 + c4 * 16);
-      goff[u] = a.g2m_big ? 0u : (uint32_t)(((int64_t)c4 * 4 * a.Q * a.Q + (int64_t)wy * a.Q + wx) * 4);
+      goff[u] = BIG ? 0u : (uint32_t)(((int64_t)c4 * 4 * a.Q * a.Q + (int64_t)wy * a.Q + wx) * 4);
       drec[u] = ((2 * wy) * B2_SC + 2 * wx) * 32 + (c4 & 3) * 8;
     }
 #pragma unroll
@@ -225,7 +228,7 @@ struct B2Stager {
       for (int q = 0; q < 4; ++q) oy[u][q] = yoff[u] + (uint32_t)(((q >> 1) * P + (q & 1)) * 128);
       og[u] = goff[u];
     }
-    if (!x.interior || a.g2m_big) {
+    if (!x.interior || BIG) {
       // edge tile: pooled windows outside the image read zeros (big: og only flags validity)
 #pragma unroll
       for (int u = 0; u < B2_IPER; ++u) {
@@ -291,7 +294,7 @@ struct B2Stager {
         yv[u][q] = DIAG == 7 ? make_float4(1.f, 0.f, 0.f, 0.f)  // timing only: no y2 loads
                              : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy[u][q], 0, 0));
       float g4[4];
-      if (!a.g2m_big) {
+      if constexpr (!BIG) {
         const uint32_t gstep = (uint32_t)(gplane * 4);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
@@ -578,7 +581,7 @@ __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict
     b3_barrier();  // tile t staged; the partner's exchange slot of tile t-1 is written
     if constexpr (ROLE < 2) {
       if (have_prev)
-        b2_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk + 1) & 1) * B2_XCHG), acc, a.dp1,
+        b2_xchg_finish<ROLE, DIAG>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk + 1) & 1) * B2_XCHG), acc, a.dp1,
                              lane, prev.b, prev.r0, prev.c0, a.P);
       b3_dgrad<ROLE, DIAG>(d_cur, R, acc, hp, lp, li);
       b2_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + B3_OFF_X + (kk & 1) * B2_XCHG), acc, lane);
@@ -594,7 +597,7 @@ __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict
   b3_barrier();
   if constexpr (ROLE < 2) {
     if (have_prev)
-      b2_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk_end - 1) & 1) * B2_XCHG), acc, a.dp1,
+      b2_xchg_finish<ROLE, DIAG>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk_end - 1) & 1) * B2_XCHG), acc, a.dp1,
                            lane, prev.b, prev.r0, prev.c0, a.P);
   } else {
     float* out = a.slab + (int64_t)blockIdx.x * 26 * 512;
@@ -609,7 +612,7 @@ __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict
   }
 }
 
-template <int WV, int DIAG>  // staging wave WV (0..3) = workgroup wave 4 + WV
+template <int WV, int DIAG, bool BIG>  // staging wave WV (0..3) = workgroup wave 4 + WV
 __device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_t) {
   if constexpr (DIAG == 5) {  // timing only: no staging at all (consumers read stale LDS)
     for (int t = first_t; t < a.total; t += gridDim.x) b3_barrier();
@@ -623,7 +626,7 @@ __device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_
   const float* kc = reinterpret_cast<const float*>(smem + B3_OFF_K);
   // two register sets: tile j's y2 / g2m registers are loaded two iterations before they are
   // staged (set j & 1), its p1 DMA lands in buffer j % 4
-  B2Stager<DIAG, WV, true> st0, st1;
+  B2Stager<DIAG, WV, true, BIG> st0, st1;
   st0.init(a, tid);
   st1.init(a, tid);
   const int G = gridDim.x;
@@ -635,8 +638,12 @@ __device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_
     st0.store(a, b2_decode(a, tile(0)), tid, dbuf(0), kc);
     st0.store_p1(pbuf(0), tid);
   }
-  if (tile(1) < a.total) st1.load(a, b2_decode(a, tile(1)), tid, nullptr);
-  if (tile(2) < a.total) st0.load(a, b2_decode(a, tile(2)), tid, nullptr);
+  // Loads are issued unconditionally (tiles past the end re-read the last tile, never staged):
+  // a load under a branch makes the compiler's wait-count analysis assume it was skipped, and
+  // the wait for the OLDER register set then drains the younger one too (vmcnt(0)).
+  auto ltile = [&](int j) { return b2_decode(a, min(tile(j), a.total - 1)); };
+  st1.load(a, ltile(1), tid, nullptr);
+  st0.load(a, ltile(2), tid, nullptr);
   // iteration kk stages tile kk+1 and loads tile kk+3 (both in set (kk+1) & 1)
   for (int kk = 0; tile(kk) < a.total; kk += 2) {
     b3_barrier();  // consumers start tile kk
@@ -644,19 +651,19 @@ __device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_
       st1.store(a, b2_decode(a, tile(kk + 1)), tid, dbuf(kk + 1), kc);
       st1.store_p1(pbuf(kk + 1), tid);
     }
-    if (tile(kk + 3) < a.total) st1.load(a, b2_decode(a, tile(kk + 3)), tid, nullptr);
+    st1.load(a, ltile(kk + 3), tid, nullptr);
     if (tile(kk + 1) >= a.total) break;
     b3_barrier();  // consumers start tile kk + 1
     if (tile(kk + 2) < a.total) {
       st0.store(a, b2_decode(a, tile(kk + 2)), tid, dbuf(kk + 2), kc);
       st0.store_p1(pbuf(kk + 2), tid);
     }
-    if (tile(kk + 4) < a.total) st0.load(a, b2_decode(a, tile(kk + 4)), tid, nullptr);
+    st0.load(a, ltile(kk + 4), tid, nullptr);
   }
   b3_barrier();
 }
 
-template <int DIAG>
+template <int DIAG, bool BIG>
 __global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
     const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
     const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
@@ -671,7 +678,6 @@ __global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
   a.tiles_r = (P + B2_TH - 1) / B2_TH;
   a.per_img = a.tiles_c * a.tiles_r;
   a.total = a.per_img * B;
-  a.g2m_big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;
   float* kc = reinterpret_cast<float*>(smem + B3_OFF_K);
   if (tid < 160) kc[tid] = (tid < 64) ? aff2[tid] : kbuf[tid - 64];
   __syncthreads();  // kc visible to the staging waves
@@ -681,10 +687,10 @@ __global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
     case 1: b3_mfma<1, DIAG>(a, wdpack, smem, t0); break;
     case 2: b3_mfma<2, DIAG>(a, wdpack, smem, t0); break;
     case 3: b3_mfma<3, DIAG>(a, wdpack, smem, t0); break;
-    case 4: b3_stage<0, DIAG>(a, smem, t0); break;
-    case 5: b3_stage<1, DIAG>(a, smem, t0); break;
-    case 6: b3_stage<2, DIAG>(a, smem, t0); break;
-    default: b3_stage<3, DIAG>(a, smem, t0); break;
+    case 4: b3_stage<0, DIAG, BIG>(a, smem, t0); break;
+    case 5: b3_stage<1, DIAG, BIG>(a, smem, t0); break;
+    case 6: b3_stage<2, DIAG, BIG>(a, smem, t0); break;
+    default: b3_stage<3, DIAG, BIG>(a, smem, t0); break;
   }
 }
 
@@ -701,7 +707,7 @@ void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c) {
 
 #ifdef TDS_DIAG
 // timing-only variants: 1 no MFMAs, 3 no global tile loads, 5 no staging, 7 no y2 loads, 9 no
-// BN2 / pool backward math in the staging.  Compiled only into a -DTDS_DIAG build
+// BN2 / pool backward math in the staging, 11 no dp1 stores.  Compiled only into a -DTDS_DIAG build
 // (python -m torch_distributed_sandbox_amd._build --variant diag -D TDS_DIAG; TDS_CONV2_DIAG=N).
 static int b3_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
@@ -716,19 +722,23 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
                     const short* wd, float* dp1, float* slab, const int* order, int nwg, int B, int P,
                     hipStream_t st) {
   const int Q = P / 2;
-#define TDS_B3_LAUNCH(D)                                                                                               \
+  const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
+#define TDS_B3_LAUNCH_B(D, BG)                                                                                         \
   {                                                                                                                    \
     static bool set = false;                                                                                           \
     if (!set) {                                                                                                        \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd3_kernel<D>),                                   \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd3_kernel<D, BG>),                               \
                                 hipFuncAttributeMaxDynamicSharedMemorySize, B3_LDS);                                   \
       set = true;                                                                                                      \
     }                                                                                                                  \
-    hipLaunchKernelGGL(conv2_bwd3_kernel<D>, dim3(nwg), dim3(B3_THREADS), B3_LDS, st,                                  \
+    hipLaunchKernelGGL((conv2_bwd3_kernel<D, BG>), dim3(nwg), dim3(B3_THREADS), B3_LDS, st,                            \
                        reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, reinterpret_cast<const uint4*>(p1),       \
                        reinterpret_cast<const uint4*>(wd), dp1, slab, order, B, P, Q);                                  \
     TDS_LAUNCH_CHECK();                                                                                                \
   }
+#define TDS_B3_LAUNCH(D)           \
+  if (big) TDS_B3_LAUNCH_B(D, true) \
+  else TDS_B3_LAUNCH_B(D, false)
   switch (b3_diag_env()) {
 #ifdef TDS_DIAG
     case 1: TDS_B3_LAUNCH(1) break;
@@ -736,8 +746,10 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
     case 5: TDS_B3_LAUNCH(5) break;
     case 7: TDS_B3_LAUNCH(7) break;
     case 9: TDS_B3_LAUNCH(9) break;
+    case 11: TDS_B3_LAUNCH(11) break;
 #endif
     default: TDS_B3_LAUNCH(0) break;
   }
 #undef TDS_B3_LAUNCH
+#undef TDS_B3_LAUNCH_B
 }

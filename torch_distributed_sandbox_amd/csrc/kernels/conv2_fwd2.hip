@@ -74,7 +74,10 @@ __device__ __forceinline__ void f2_dma(const uint4* __restrict__ p1, const F2Til
 // edges feed only 1-2 MFMA triples, too few to hide an LDS round trip one row ahead.
 template <int DIAG>
 __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13][2], f32x4 (&acc)[4], int RH, int lane) {
-  constexpr int DEPTH = 4;
+#ifndef TDS_F2_DEPTH
+#define TDS_F2_DEPTH 4
+#endif
+  constexpr int DEPTH = TDS_F2_DEPTH;
   const int li = lane & 15, g = lane >> 4;
   const int boff = (g & 1) * 16;  // ci half of the 32-B record
   const char* ph = buf;
