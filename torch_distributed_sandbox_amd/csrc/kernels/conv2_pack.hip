@@ -97,12 +97,14 @@ void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, fl
   TDS_LAUNCH_CHECK();
 }
 
-// Blocked tile order (blocked_tile<32, 16, 4>, conv2_common.h) into a host array of
-// B * tiles_r * tiles_c ints: b << 24 | tile_row << 12 | tile_col.  The binding layer copies it
-// to a device tensor from the torch caching allocator and caches it per shape.
-int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c) {
-  if (B < 1 || B > 255 || tiles_r < 1 || tiles_r > 4095 || tiles_c < 1 || tiles_c > 4095) return -1;
-  constexpr int BC = 32, GR = 16, GC = 4;
+// Blocked tile order (conv2_common.h) into a host array of B * tiles_r * tiles_c ints:
+// b << 24 | tile_row << 12 | tile_col.  Bands of 32 tile columns, row groups of GR tile rows,
+// column groups of 4 (one XCD round of the forward's 512 workgroups = one 16 x 4 block).  The
+// binding layer copies it to a device tensor from the torch caching allocator and caches it
+// per (shape, GR).
+int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c, int GR) {
+  if (B < 1 || B > 255 || tiles_r < 1 || tiles_r > 4095 || tiles_c < 1 || tiles_c > 4095 || GR < 1) return -1;
+  constexpr int BC = 32, GC = 4;
   const int per_img = tiles_r * tiles_c, total = per_img * B;
   for (int t = 0; t < total; ++t) {
     const int b = t / per_img;

@@ -70,7 +70,7 @@ int tds_device_cus();
 void tds_set_cu_reserve(int n);
 int tds_cu_reserve();
 hipStream_t tds_cu_masked_stream(int device, int reserve);
-int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c);  // host: blocked tile order table
+int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c, int group_rows);  // host: blocked tile order table
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st);
 int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
