@@ -76,6 +76,26 @@ const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int n
   return dev.data_ptr<int>();
 }
 
+// Device copy of the rolling conv2 backward's walk table (tds_conv2_bwd_walk) per (device,
+// shape, workgroups), from the torch caching allocator, built once.
+const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg) {
+  static std::mutex mu;
+  static auto* cache = new std::map<std::tuple<int, int, int, int, int>, Tensor>();
+  constexpr int kSeg = 24;  // tiles per vertical segment (a segment start re-stages 4 rows)
+  const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c, nwg);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache->find(key);
+  if (it != cache->end()) return it->second.data_ptr<int>();
+  const int64_t n = tds_conv2_bwd_walk(nullptr, B, tiles_r, tiles_c, nwg, kSeg);
+  TORCH_CHECK(n > 0, "tdsa fused: conv2 backward walk needs B <= 63 and <= 4095 tiles per side (B=", B, ", tiles ",
+              tiles_r, " x ", tiles_c, ")");
+  auto host = at::empty({n}, at::TensorOptions().dtype(at::kInt));
+  tds_conv2_bwd_walk(host.data_ptr<int>(), B, tiles_r, tiles_c, nwg, kSeg);
+  Tensor dev = host.to(like.device());
+  (*cache)[key] = dev;
+  return dev.data_ptr<int>();
+}
+
 int64_t pb_plane(int64_t P) { return tds_pb_plane((int)(P / 2)); }
 
 // ---------------------------------------------------------------- layer 1 forward
@@ -323,13 +343,13 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
   need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
-  TORCH_CHECK(B <= 255 && P >= 2, "fused_conv2_backward_y2: 1 <= batch <= 255 and P >= 2");
+  TORCH_CHECK(B <= 63 && P >= 2, "fused_conv2_backward_y2: 1 <= batch <= 63 and P >= 2");
   c10::DeviceGuard guard(p1.device());
   hipStream_t st = stream_of(p1);
   const int nwg = tds_conv2_bwd3_num_wg();
   int tr = 0, tc = 0;
   tds_conv2_bwd3_tiles((int)P, &tr, &tc);
-  const int* order = tile_order(p1, (int)B, tr, tc, nwg);
+  const int* order = bwd_walk(p1, (int)B, tr, tc, nwg);
   auto dp1 = at::empty({B, P, P, 16}, p1.options());
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options());
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");

@@ -1,29 +1,39 @@
-// conv2 backward v2: BN2 / ReLU / max-pool backward fused into conv2 dgrad + wgrad,
-// laid out for TWO 4-wave workgroups per CU.
+// conv2 backward: BN2 / ReLU / max-pool backward fused into conv2 dgrad + wgrad
+// (SURVEY.md §2.4 K16-K21), one persistent 8-wave workgroup per CU.
 //
-// Why a second design (conv2_bwd_fused_kernel in conv2_bf16x3.hip is the first): that
-// kernel runs one 8-wave workgroup per CU, so its staging phase (global loads -> BN2
-// backward VALU -> LDS stores, between two barriers) and its MFMA phase alternate on
-// every SIMD; rocprof showed the MFMA pipe busy 35% of the time and waves parked on
-// barriers/waits half of it.  Here each workgroup needs < 80 KiB of LDS and <= 256 VGPRs
-// per wave, so two co-reside on a CU and one workgroup's staging runs under the other's
-// MFMAs.  What makes it fit:
-//   * output tile 8 x 16 (staged 12 x 20 records incl. the 2-pixel halo);
-//   * the dgrad weight fragments live in REGISTERS, not LDS: the 25 flipped taps are
-//     split over the two dgrad waves (13 + 12 taps, 8 VGPRs each), each wave produces a
-//     partial dp1 for the whole tile, and the halves are exchanged through 8 KiB of LDS;
-//   * wgrad: two waves, 13 taps each (tap 25 = the bias "ones" column), K = 32 pixels =
-//     two output rows, operands by ds_read_b64_tr_b16 transposed reads.
+// Roles (one per SIMD each):
+//   waves 0/1 : dgrad, taps grouped by kx so an input row's A fragment serves up to 5 output
+//               rows:  wave 0 = kx {0,1} x ky 0-4  +  kx 4 x ky 0-2
+//                      wave 1 = kx {2,3} x ky 0-4  +  kx 4 x ky 3-4
+//               weights in registers; each wave makes a partial dp1 of the whole 8 x 16 tile,
+//               the halves are exchanged through LDS (double-buffered slots).
+//   waves 2/3 : wgrad, taps 0-12 / 13-25 (tap 25 = the bias "ones" column), both co halves, K =
+//               32 pixels = two output rows, operands by ds_read_b64_tr_b16; accumulated over the
+//               workgroup's tiles; slab[wg][26][32][16] reduced in fixed order afterwards.
+//   waves 4-7 : staging: y2 / pooled gradient g2m / p1 -> BN2 / ReLU / pool backward (dy2 =
+//               k1*dz + k2*y2 + k3 at the window's argmax) -> dy2 and p1 bf16 hi|lo rows in LDS.
 //
-// Per tile (4 waves, one per SIMD):
-//   wave 0/1 : dgrad, taps grouped by kx so an input row's A fragment serves up to 5
-//              output rows:  wave 0 = kx {0,1} x ky 0-4  +  kx 4 x ky 0-2
-//                            wave 1 = kx {2,3} x ky 0-4  +  kx 4 x ky 3-4
-//   wave 2/3 : wgrad, taps 0-12 / 13-25, both co halves, accumulated over the tiles of
-//              the persistent workgroup; slab[wg][26][32][16] reduced in fp64 afterwards.
-// LDS (72 448 B): dy2 planes (hi co0-15, hi co16-31, lo co0-15, lo co16-31) | 2 x p1 planes
-// (hi, lo; LDS-DMA, double-buffered) | dgrad exchange | BN2 backward constants.
+// ROLLING WINDOW.  A tile of 8 output rows needs dy2 and p1 on 12 rows (2-row halo above and
+// below).  Each workgroup walks vertical SEGMENTS of tiles (one tile column of one image, ~24
+// tiles top to bottom, host table tds_conv2_bwd_walk): consecutive tiles share 4 of those 12
+// rows, so the staging waves load, recompute and store only the 8 NEW rows of each tile; its
+// last 4 rows are stored twice, the second time as the TOP rows of the next tile's slot, so
+// every tile reads its 12 rows contiguously from one slot (one base address: the consumers'
+// LDS offsets are immediates, as with a slot that stages all 12 rows).  A segment's first tile
+// gets its 4 top rows from a prologue staged straight into its slot's top.  Against a tile that stages all 12 rows this
+// cuts the staging's global loads (y2 + g2m + p1) and BN2-backward work by a third; the loads
+// were the kernel's largest cost (timing build without them: 1.05 vs 1.56 ms).
+//
+// LDS, in ROW BLOCKS (one staged image row of 20 records per block):
+//   dy2 row block: 4 planes (hi co0-15, hi co16-31, lo co0-15, lo co16-31) x 20 x 32 B = 2560 B
+//   p1  row block: 2 planes (hi, lo) x 20 x 32 B = 1280 B
+//   3 ring slots of 12 row blocks (tile k in slot k % 3: 4 top + 8 new rows), 2 dgrad exchange
+//   slots, BN2 backward constants: 155 264 B.
+// One bare s_barrier per tile (after lgkmcnt(0)) separates producer and consumers: while the
+// consumers read slot k%3, the staging writes slot (k+1)%3's new rows and slot (k+2)%3's top
+// (the slot of tile k-1, finished); the register loads for tile k+3 are already in flight.
 #include <cstdlib>
+#include <vector>
 
 #include "conv2_common.h"
 #include "launchers.h"
@@ -31,31 +41,53 @@
 
 namespace tds {
 
-constexpr int B2_TH = 8, B2_TC = 16;
-constexpr int B2_SR = B2_TH + 4, B2_SC = B2_TC + 4;      // 12 x 20 staged records
-constexpr int B2_REC = B2_SR * B2_SC;                      // 240
-constexpr int B2_THREADS = 256;
-constexpr int B2_DPLANE = B2_REC * 32 + 32;                // 7712 B
-// p1 planes are filled by LDS-DMA (global_load_lds_dwordx4): one wave-instruction writes
-// 32 records x 32 B of one plane, so a plane holds 8 such groups (256 records, 240 used),
-// and they are double-buffered (tile t+1's DMA runs under tile t's MFMAs).
-constexpr int B2_PGROUPS = 8;
-constexpr int B2_PPLANE = B2_PGROUPS * 32 * 32;            // 8192 B
-constexpr int B2_PBUF = 2 * B2_PPLANE;                     // hi + lo planes
-constexpr int B2_OFF_P = 4 * B2_DPLANE;                    // 30848
-constexpr int B2_OFF_X = B2_OFF_P + 2 * B2_PBUF;           // 63616
-constexpr int B2_XCHG = 2 * 4 * 64 * 16;                   // 8192
-constexpr int B2_OFF_K = B2_OFF_X + B2_XCHG;               // 71808
-constexpr int B2_LDS = B2_OFF_K + 5 * 32 * 4;              // 72448
-constexpr int B2_NWIN = (B2_SR / 2) * (B2_SC / 2);         // 60 pooling windows
-constexpr int B2_ITEMS = B2_NWIN * 8;                      // (window, 4-channel chunk)
-constexpr int B2_IPER = (B2_ITEMS + B2_THREADS - 1) / B2_THREADS;   // 2
-constexpr int B2_DMA_PER_WAVE = 2 * B2_PGROUPS / (B2_THREADS / 64);  // 4 p1 DMA instructions per wave
-static_assert(B2_LDS % 16 == 0 && B2_OFF_P % 16 == 0 && B2_OFF_X % 16 == 0 && B2_OFF_K % 16 == 0, "LDS carve");
-static_assert(2 * B2_LDS <= 160 * 1024, "two workgroups per CU");
+constexpr int BR_TH = 8, BR_TC = 16;       // output tile
+constexpr int BR_SC = BR_TC + 4;           // 20 staged columns (2-pixel halo each side)
+constexpr int BR_DPL = BR_SC * 32;         // 640 B: one plane of a row block
+constexpr int BR_DROW = 4 * BR_DPL;        // 2560 B: dy2 row block
+constexpr int BR_PROW = 2 * BR_DPL;        // 1280 B: p1 row block
+constexpr int BR_THREADS = 512;
+constexpr int BR_SLOT = 12;                                  // row blocks per ring slot
+constexpr int BR_OFF_D = 0;                                  // 3 x 12 dy2 row blocks
+constexpr int BR_OFF_P = BR_OFF_D + 3 * BR_SLOT * BR_DROW;   // 3 x 12 p1 row blocks
+constexpr int BR_XCHG = 2 * 4 * 64 * 16;                     // 8 KiB exchange slot
+constexpr int BR_OFF_X = BR_OFF_P + 3 * BR_SLOT * BR_PROW;   // 2 exchange slots
+constexpr int BR_OFF_K = BR_OFF_X + 2 * BR_XCHG;             // 160 floats of constants
+constexpr int BR_LDS = BR_OFF_K + 5 * 32 * 4;
+static_assert(BR_LDS <= 160 * 1024 && BR_OFF_X % 16 == 0 && BR_OFF_K % 16 == 0, "LDS carve");
 
-// dgrad tap groups: group I of wave D covers kx = KX, ky = KY0 .. KY0 + NKY - 1; its
-// weights sit in register slots 5I .. 5I + NKY - 1.
+// walk table entries (tds_conv2_bwd_walk): bit 31 = first tile of a segment, bit 30 = past the
+// end of this workgroup's list (the low bits then repeat its last tile), b << 24 | tr << 12 | tc
+constexpr uint32_t kWalkStart = 0x80000000u, kWalkEnd = 0x40000000u;
+struct BRTile {
+  int b, r0, c0;
+  bool start, end;
+};
+__device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k, int nwg, int w) {
+  // 32-bit index (the table is far below 2^31 entries): with a 64-bit one the compiler keeps
+  // copies of the wgrad accumulators across the tile loop and spills them (256 VGPRs + scratch
+  // against 189)
+  const uint32_t v = (uint32_t)walk[k * nwg + w];
+  BRTile x;
+  x.start = (v & kWalkStart) != 0;
+  x.end = (v & kWalkEnd) != 0;
+  x.b = (int)((v >> 24) & 63);
+  x.r0 = (int)((v >> 12) & 4095) * BR_TH;
+  x.c0 = (int)(v & 4095) * BR_TC;
+  return x;
+}
+
+struct BRArgs {
+  const float4* __restrict__ y2;
+  const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
+  const uint4* __restrict__ p1;
+  float* __restrict__ dp1;
+  float* __restrict__ slab;
+  const int* __restrict__ walk;
+  int B, P, Q, nwg, w;
+};
+
+// ---------------------------------------------------------------------------- dgrad
 template <int D, int I>
 struct DgGroup {
   static constexpr int KX = D == 0 ? (I == 0 ? 0 : I == 1 ? 1 : 4) : (I == 0 ? 2 : I == 1 ? 3 : 4);
@@ -64,7 +96,7 @@ struct DgGroup {
 };
 
 template <int D, int I>
-__device__ __forceinline__ void b2_load_w_group(const uint4* __restrict__ wd, f32x4 (&R)[13][2], int lane) {
+__device__ __forceinline__ void br_load_w_group(const uint4* __restrict__ wd, f32x4 (&R)[13][2], int lane) {
   using G = DgGroup<D, I>;
 #pragma unroll
   for (int k = 0; k < G::NKY; ++k) {
@@ -76,29 +108,29 @@ __device__ __forceinline__ void b2_load_w_group(const uint4* __restrict__ wd, f3
 }
 
 template <int D>
-__device__ __forceinline__ void b2_load_w(const uint4* __restrict__ wd, f32x4 (&R)[13][2], int lane) {
-  b2_load_w_group<D, 0>(wd, R, lane);
-  b2_load_w_group<D, 1>(wd, R, lane);
-  b2_load_w_group<D, 2>(wd, R, lane);
+__device__ __forceinline__ void br_load_w(const uint4* __restrict__ wd, f32x4 (&R)[13][2], int lane) {
+  br_load_w_group<D, 0>(wd, R, lane);
+  br_load_w_group<D, 1>(wd, R, lane);
+  br_load_w_group<D, 2>(wd, R, lane);
 }
 
 // Wave D hands the partner's rows (4(1-D) .. +3) to the exchange slot 1-D.
 template <int D>
-__device__ __forceinline__ void b2_xchg_put(f32x4* xs, const f32x4 (&acc)[8], int lane) {
+__device__ __forceinline__ void br_xchg_put(f32x4* xs, const f32x4 (&acc)[8], int lane) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) xs[((1 - D) * 4 + i) * 64 + lane] = acc[4 * (1 - D) + i];
 }
 
 // Wave D owns output rows 4D .. 4D+3: its partial + the partner's, then dp1.
-template <int D, int DIAG = 0>
-__device__ __forceinline__ void b2_xchg_finish(const f32x4* xs, const f32x4 (&acc)[8], float* __restrict__ dp1,
+template <int D>
+__device__ __forceinline__ void br_xchg_finish(const f32x4* xs, const f32x4 (&acc)[8], float* __restrict__ dp1,
                                                int lane, int b, int r0, int c0, int P) {
   const int li = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const f32x4 v = acc[4 * D + i] + xs[(D * 4 + i) * 64 + lane];
     const int row = r0 + 4 * D + i;
-    if (DIAG == 11 ? v[0] == 1234.5f : row < P) {  // DIAG 11 (timing only): no dp1 stores
+    if (row < P) {
       float* orow = dp1 + ((int64_t)b * P + row) * P * 16;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -109,344 +141,15 @@ __device__ __forceinline__ void b2_xchg_finish(const f32x4* xs, const f32x4 (&ac
   }
 }
 
-// Per-thread staging state: the next tile's y2 windows, pooled gradients and p1 records
-// in registers (loaded under the current tile's MFMAs), then BN2 backward -> LDS.
-struct B2Args {
-  const float4* __restrict__ y2;
-  const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
-  const uint4* __restrict__ p1;
-  float* __restrict__ dp1;
-  float* __restrict__ slab;
-  const int* __restrict__ order;  // blocked tile order (tds_tile_order)
-  int B, P, Q, tiles_r, tiles_c, per_img, total;
+// The 12 staged rows of a tile, contiguous in its slot (r: a compile-time row in the unrolled
+// loops, so r * row-block size folds into the LDS instruction's offset)
+struct BRRows {
+  const char* dl;
+  const char* pl;
+  __device__ __forceinline__ const char* d(int r) const { return dl + r * BR_DROW; }
+  __device__ __forceinline__ const char* p(int r) const { return pl + r * BR_PROW; }
 };
 
-struct B2Tile {
-  int b, r0, c0;
-  bool interior;  // whole staged region inside the pooled image: no bounds / padding work
-};
-
-__device__ __forceinline__ B2Tile b2_decode(const B2Args& a, int t) {
-  B2Tile x;
-  int tr, tc;
-  tile_from_order(a.order, t, x.b, tr, tc);
-  x.r0 = tr * B2_TH;
-  x.c0 = tc * B2_TC;
-  x.interior = x.r0 >= 2 && x.c0 >= 2 && x.r0 + B2_SR - 2 <= 2 * a.Q && x.c0 + B2_SC - 2 <= 2 * a.Q;
-  return x;
-}
-
-// wave-uniform buffer descriptor over [base, base + 2 GiB): per-lane byte offsets in voffset,
-// an invalid lane gets kB2Oob and reads zeros (hardware range check, no exec masking)
-constexpr uint32_t kB2Oob = 0xFFFFFFF0u;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t b2_rsrc(const void* base) { return tds_buffer_rsrc(base, 0x7FFFFFF0u); }
-
-// 16 zero bytes: the LDS-DMA source of staged p1 records outside the image
-__device__ __attribute__((aligned(16))) uint32_t g_b2_zero[4] = {0u, 0u, 0u, 0u};
-
-// REGP1 (v3): p1 records go global -> registers -> ds_write in store() instead of LDS-DMA.
-// The compiler cannot tell an LDS-DMA's destination from later LDS accesses, so every ds_read /
-// ds_write after one waits vmcnt(0) -- which drains the register loads issued for LATER
-// tiles too and defeats a multi-tile lookahead.
-// BIG: 32 g2m planes of an image exceed a 4 GiB buffer-descriptor range (H >= 23170): 64-bit
-// g2m loads.  A template parameter, not a runtime flag: two alternative load paths under a
-// runtime branch make the compiler's wait-count analysis assume the fewer-loads path at the
-// merge and wait for vmcnt(0), draining the loads issued for later tiles.
-template <int DIAG, int WV, bool REGP1 = false, bool BIG = false>  // WV: the wave (= role) this staging code runs in
-struct B2Stager {
-  float4 yv[B2_IPER][4], gv[B2_IPER];
-  uint4 pr[REGP1 ? B2_DMA_PER_WAVE : 1];
-  // per-thread byte offsets (fixed for the kernel): global, relative to the tile's
-  // descriptor bases, and LDS, of each staging item (window x 4 channels); p1 DMA sources
-  uint32_t yoff[B2_IPER], goff[B2_IPER], doff[B2_DMA_PER_WAVE];
-  int drec[B2_IPER];
-
-  // staging item u of this thread: window (wy, wx)
-  __device__ __forceinline__ static void item_geom(int tid, int u, int& wy, int& wx) {
-    const int it = tid + u * B2_THREADS;
-    const int w = (it < B2_ITEMS ? it : 0) >> 3;
-    wy = w / (B2_SC / 2);
-    wx = w - wy * (B2_SC / 2);
-  }
-  // p1 DMA instruction j of wave wv: plane pl, record group rg; lane -> record, 16-B half
-  __device__ __forceinline__ static void dma_geom(int wv, int j, int lane, int& pl, int& rg, int& px, int& half) {
-    const int k = wv * B2_DMA_PER_WAVE + j;
-    pl = k / B2_PGROUPS;
-    rg = k - pl * B2_PGROUPS;
-    px = rg * 32 + (lane >> 1);
-    half = lane & 1;
-  }
-
-  __device__ __forceinline__ void init(const B2Args& a, int tid) {
-    const int c4 = tid & 7;
-#pragma unroll
-    for (int u = 0; u < B2_IPER; ++u) {
-      int wy, wx;
-      item_geom(tid, u, wy, wx);
-      yoff[u] = (uint32_t)(((2 * wy) * a.P + 2 * wx) * 128 + c4 * 16);
-      goff[u] = BIG ? 0u : (uint32_t)(((int64_t)c4 * 4 * a.Q * a.Q + (int64_t)wy * a.Q + wx) * 4);
-      drec[u] = ((2 * wy) * B2_SC + 2 * wx) * 32 + (c4 & 3) * 8;
-    }
-#pragma unroll
-    for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
-      int pl, rg, px, half;
-      dma_geom(WV, j, tid & 63, pl, rg, px, half);
-      const int pxc = px < B2_REC ? px : 0;
-      const int rr = pxc / B2_SC, cc = pxc - rr * B2_SC;
-      doff[j] = (uint32_t)((rr * a.P + cc) * 64 + pl * 32 + half * 16);
-    }
-  }
-
-  // tile x: y2 windows + pooled gradients -> registers; p1 -> LDS buffer pbuf by DMA
-  __device__ __forceinline__ void load(const B2Args& a, const B2Tile& x, int tid, char* pbuf) {
-    if constexpr (DIAG == 3) {
-#pragma unroll
-      for (int u = 0; u < B2_IPER; ++u) {
-        gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) yv[u][q] = gv[u];
-      }
-      return;
-    }
-    const int P = a.P, Q = a.Q;
-    const int64_t img = (int64_t)x.b * P;
-    const __amdgpu_buffer_rsrc_t ry =
-        b2_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 128);
-    const char* pbase = reinterpret_cast<const char*>(a.p1) + ((img + x.r0 - 2) * P + (x.c0 - 2)) * 64;
-    uint32_t oy[B2_IPER][4];
-    // pooled gradients: window (wy, wx) is pooled position (r0/2 - 1 + wy, c0/2 - 1 + wx), four
-    // channel planes of the planar g2m.  One buffer descriptor per tile (base: the tile's pooled
-    // origin in channel 0 of its image) while 32 planes fit a 4 GiB range (H < 23170); beyond
-    // that, 64-bit addresses.
-    const int64_t gplane = (int64_t)Q * Q;
-    const __amdgpu_buffer_rsrc_t rg =
-        tds_buffer_rsrc(a.g2m + (int64_t)x.b * 32 * gplane + (int64_t)(x.r0 / 2 - 1) * Q + (x.c0 / 2 - 1), 0xFFFFFFF0u);
-    uint32_t og[B2_IPER];
-#pragma unroll
-    for (int u = 0; u < B2_IPER; ++u) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) oy[u][q] = yoff[u] + (uint32_t)(((q >> 1) * P + (q & 1)) * 128);
-      og[u] = goff[u];
-    }
-    if (!x.interior || BIG) {
-      // edge tile: pooled windows outside the image read zeros (big: og only flags validity)
-#pragma unroll
-      for (int u = 0; u < B2_IPER; ++u) {
-        int wy, wx;
-        item_geom(tid, u, wy, wx);
-        const int py = x.r0 / 2 - 1 + wy, px = x.c0 / 2 - 1 + wx;
-        const bool ok = tid + u * B2_THREADS < B2_ITEMS && py >= 0 && py < Q && px >= 0 && px < Q;
-        if (!ok) og[u] = kB2Oob;
-      }
-    }
-    const char* psrc[B2_DMA_PER_WAVE];
-#pragma unroll
-    for (int j = 0; j < B2_DMA_PER_WAVE; ++j) psrc[j] = pbase + doff[j];
-    if (!x.interior) {
-      // edge tile: lanes outside the image (or past the item count) read zeros
-      const int lo_r = max(0, 2 - x.r0), hi_r = min(B2_SR, P - x.r0 + 2);
-      const int lo_c = max(0, 2 - x.c0), hi_c = min(B2_SC, P - x.c0 + 2);
-#pragma unroll
-      for (int u = 0; u < B2_IPER; ++u) {
-        int wy, wx;
-        item_geom(tid, u, wy, wx);
-        const bool item = tid + u * B2_THREADS < B2_ITEMS;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int lr = 2 * wy + (q >> 1), lc = 2 * wx + (q & 1);
-          if (!(item && lr >= lo_r && lr < hi_r && lc >= lo_c && lc < hi_c)) oy[u][q] = kB2Oob;
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
-        int pl, rgp, px, half;
-        dma_geom(WV, j, tid & 63, pl, rgp, px, half);
-        const int rr = px / B2_SC, cc = px - rr * B2_SC;
-        if (!(px < B2_REC && rr >= lo_r && rr < hi_r && cc >= lo_c && cc < hi_c))
-          psrc[j] = reinterpret_cast<const char*>(g_b2_zero);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
-        int pl, rgp, px, half;
-        dma_geom(WV, j, tid & 63, pl, rgp, px, half);
-        if (px >= B2_REC) psrc[j] = reinterpret_cast<const char*>(g_b2_zero);
-      }
-    }
-    const __amdgpu_buffer_rsrc_t rp = b2_rsrc(pbase);
-#pragma unroll
-    for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
-      if constexpr (REGP1) {
-        // buffer loads (not flat: a flat load makes every later wait a full vmcnt(0) drain)
-        const uint32_t po = psrc[j] == reinterpret_cast<const char*>(g_b2_zero) ? kB2Oob : doff[j];
-        pr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, po, 0, 0));
-      } else {
-        int pl, rgp, px, half;
-        dma_geom(WV, j, 0, pl, rgp, px, half);
-        __builtin_amdgcn_global_load_lds(psrc[j], (__attribute__((address_space(3))) void*)(pbuf + pl * B2_PPLANE + rgp * 1024),
-                                         16, 0, 0);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < B2_IPER; ++u) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        yv[u][q] = DIAG == 7 ? make_float4(1.f, 0.f, 0.f, 0.f)  // timing only: no y2 loads
-                             : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, oy[u][q], 0, 0));
-      float g4[4];
-      if constexpr (!BIG) {
-        const uint32_t gstep = (uint32_t)(gplane * 4);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          g4[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                                rg, og[u] == kB2Oob ? kB2Oob : og[u] + k * gstep, 0, 0));
-      } else {
-        int wy, wx;
-        item_geom(tid, u, wy, wx);
-        const float* gp = a.g2m + ((int64_t)x.b * 32 + 4 * (tid & 7)) * gplane +
-                          (int64_t)(x.r0 / 2 - 1 + wy) * Q + (x.c0 / 2 - 1 + wx);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) g4[k] = og[u] == kB2Oob ? 0.f : gp[k * gplane];
-      }
-      gv[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
-    }
-  }
-
-  // BN2 / ReLU / pool backward of the staged windows -> dy2 hi|lo planes.
-  // dy2 = k1*dz + k2*y2 + k3, dz = pooled gradient at the window's argmax of a*y2 + b.
-  // Interior tiles take a short path: every window pooled, every pixel inside the image,
-  // argmax by max3 + first-equal (torch's scan-order tie rule); a NaN anywhere in the
-  // thread's windows sends the wave to the general path (torch's NaN-wins rule).
-  // REGP1: the tile's p1 records -> plane buffer pbuf (same layout the DMA writes)
-  __device__ __forceinline__ void store_p1(char* pbuf, int tid) {
-    if constexpr (REGP1) {
-#pragma unroll
-      for (int j = 0; j < B2_DMA_PER_WAVE; ++j) {
-        int pl, rgp, px, half;
-        dma_geom(WV, j, tid & 63, pl, rgp, px, half);
-        *reinterpret_cast<uint4*>(pbuf + pl * B2_PPLANE + rgp * 1024 + (tid & 63) * 16) = pr[j];
-      }
-    }
-  }
-
-  __device__ __forceinline__ void store(const B2Args& a, const B2Tile& x, int tid, char* d_l, const float* kc) {
-    const int c4 = tid & 7;
-    const int P = a.P, Q = a.Q;
-    const float4 ka4 = *reinterpret_cast<const float4*>(&kc[0 * 32 + 4 * c4]);
-    const float4 kb4 = *reinterpret_cast<const float4*>(&kc[1 * 32 + 4 * c4]);
-    const float4 k14 = *reinterpret_cast<const float4*>(&kc[2 * 32 + 4 * c4]);
-    const float4 k24 = *reinterpret_cast<const float4*>(&kc[3 * 32 + 4 * c4]);
-    const float4 k34 = *reinterpret_cast<const float4*>(&kc[4 * 32 + 4 * c4]);
-    const float ka[4] = {ka4.x, ka4.y, ka4.z, ka4.w}, kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
-    const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, k2[4] = {k24.x, k24.y, k24.z, k24.w},
-                k3[4] = {k34.x, k34.y, k34.z, k34.w};
-    bool fast = x.interior;
-    if (fast) {
-      float nsum = 0.f;
-#pragma unroll
-      for (int u = 0; u < B2_IPER; ++u)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) nsum += (yv[u][q].x + yv[u][q].y) + (yv[u][q].z + yv[u][q].w);
-      fast = __builtin_amdgcn_ballot_w64(isnan(nsum)) == 0;  // wave-uniform
-    }
-#pragma unroll
-    for (int u = 0; u < B2_IPER; ++u) {
-      const int it = tid + u * B2_THREADS;
-      if (it >= B2_ITEMS) continue;
-      float y[4][4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        y[q][0] = yv[u][q].x; y[q][1] = yv[u][q].y; y[q][2] = yv[u][q].z; y[q][3] = yv[u][q].w;
-      }
-      const float gg[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
-      float d[4][4];
-      if constexpr (DIAG == 9) {  // timing only: no BN2 / pool backward math (dy2 := y2 + g)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int cc = 0; cc < 4; ++cc) d[q][cc] = y[q][cc] + gg[cc];
-      } else if (fast) {
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          float z[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) z[q] = fmaf(ka[cc], y[q][cc], kb[cc]);
-          const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
-          const bool e0 = z[0] == m, e1 = !e0 && z[1] == m, e2 = !e0 && !e1 && z[2] == m;
-          const bool e3 = !e0 && !e1 && !e2;
-          const float base[4] = {fmaf(k2[cc], y[0][cc], k3[cc]), fmaf(k2[cc], y[1][cc], k3[cc]),
-                                 fmaf(k2[cc], y[2][cc], k3[cc]), fmaf(k2[cc], y[3][cc], k3[cc])};
-          const float kg = k1[cc] * gg[cc];
-          d[0][cc] = e0 ? base[0] + kg : base[0];
-          d[1][cc] = e1 ? base[1] + kg : base[1];
-          d[2][cc] = e2 ? base[2] + kg : base[2];
-          d[3][cc] = e3 ? base[3] + kg : base[3];
-        }
-      } else {
-        int wy, wx;
-        item_geom(tid, u, wy, wx);
-        const int gy = x.r0 - 2 + 2 * wy, gx = x.c0 - 2 + 2 * wx;
-        const bool pooled = gy >= 0 && gx >= 0 && (gy >> 1) < Q && (gx >> 1) < Q;
-#pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
-          float m = ka[cc] * y[0][cc] + kb[cc];
-          int ai = 0;
-#pragma unroll
-          for (int q = 1; q < 4; ++q) {
-            const float z = ka[cc] * y[q][cc] + kb[cc];
-            if (z > m || isnan(z)) { m = z; ai = q; }  // first max in scan order, NaN wins (torch)
-          }
-          const int am = pooled ? ai : -1;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int r = gy + (q >> 1), c = gx + (q & 1);
-            const bool inb = r >= 0 && r < P && c >= 0 && c < P;  // zero padding outside the image
-            const float dz = am == q ? gg[cc] : 0.f;
-            d[q][cc] = inb ? fmaf(k1[cc], dz, fmaf(k2[cc], y[q][cc], k3[cc])) : 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        uint32_t h01, l01, h23, l23;
-        split2_bf16(d[q][0], d[q][1], h01, l01);
-        split2_bf16(d[q][2], d[q][3], h23, l23);
-        const int off = drec[u] + ((q >> 1) * B2_SC + (q & 1)) * 32;
-        *reinterpret_cast<uint2*>(d_l + (c4 >> 2) * B2_DPLANE + off) = make_uint2(h01, h23);
-        *reinterpret_cast<uint2*>(d_l + (2 + (c4 >> 2)) * B2_DPLANE + off) = make_uint2(l01, l23);
-      }
-    }
-  }
-};
-
-// ============================================================================ v3: producer/consumer waves
-// Counters on v2 (rocprofv3 --pmc, docs/KERNELS.md): MFMA busy ~41% of the kernel, ~725 VALU
-// instructions per wave per tile against ~312 MFMAs, and every wave alternating staging and
-// MFMA phases between two barriers, so with two waves per SIMD the MFMA pipe idles whenever
-// both sit in the same phase.  v3 splits the roles: one 8-wave workgroup per CU, waves 0-3 run
-// ONLY the dgrad/wgrad MFMA loops of v2 (one per SIMD), waves 4-7 ONLY stage (BN2/ReLU/pool
-// backward -> dy2 hi|lo planes; p1 by LDS-DMA).  Staging runs one tile ahead into double-
-// buffered dy2 / p1 planes; its y2 / g2m / p1 register loads run three tiles ahead (two
-// register sets: staging alone was memory-latency bound; no LDS-DMA, see B2Stager), the dgrad
-// exchange slots are double-buffered, so ONE barrier per tile separates producer and
-// consumer.  The barrier is a bare s_barrier after lgkmcnt(0): a producer's register loads
-// for later tiles stay in flight across it.
-constexpr int B3_THREADS = 512;
-constexpr int B3_DBUF = 4 * B2_DPLANE;                      // dy2 hi/lo planes of one tile
-constexpr int B3_OFF_P = 2 * B3_DBUF;                       // 61696: 3 x p1 buffers
-constexpr int B3_NP = 2;                                   // p1 buffers (staged with dy2, one tile ahead)
-constexpr int B3_OFF_X = B3_OFF_P + B3_NP * B2_PBUF;        // 127232: 2 x exchange slots
-constexpr int B3_OFF_K = B3_OFF_X + 2 * B2_XCHG;            // 143616
-constexpr int B3_LDS = B3_OFF_K + 5 * 32 * 4;               // 144256
-static_assert(B3_LDS <= 160 * 1024 && B3_OFF_P % 16 == 0 && B3_OFF_X % 16 == 0 && B3_OFF_K % 16 == 0, "v3 LDS carve");
-
-__device__ __forceinline__ void b3_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// v3 MFMA loops: the v2 loops (b2_dgrad, b2_wgrad) prefetch operands one step ahead and
-// restart the pipeline at every kx group / K-step; with ONE MFMA wave per SIMD nothing hides
-// those bubbles (v3 with staging disabled ran at ~67% MFMA utilisation).  Here each role's
-// tile is one flat, fully unrolled sequence with operands fetched two steps ahead across
-// group / K-step boundaries.
 template <int D>
 struct DgSeq {
   static constexpr int n(int i) { return 8 + (i < 2 ? 5 : (D == 0 ? 3 : 2)) - 1; }  // rows of group i
@@ -458,8 +161,10 @@ struct DgSeq {
   static constexpr int nky(int i) { return i < 2 ? 5 : (D == 0 ? 3 : 2); }
 };
 
+// one flat, fully unrolled sequence of A-fragment rows with operands fetched two steps ahead
+// across group boundaries (one MFMA wave per SIMD: nothing else hides a bubble)
 template <int D, int DIAG>
-__device__ __forceinline__ void b3_dgrad(const char* d_l, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int lp,
+__device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int lp,
                                          int li) {
   using Q = DgSeq<D>;
 #pragma unroll
@@ -467,9 +172,9 @@ __device__ __forceinline__ void b3_dgrad(const char* d_l, const f32x4 (&R)[13][2
   s16x8 ah[3], al[3];
   auto load_a = [&](int s, int buf) {
     const int i = Q::grp(s), r = Q::row(s);
-    const int rec = (Q::ky0(i) + r) * B2_SC + Q::kx(i) + li;
-    ah[buf] = lds8<DIAG>(d_l + hp + rec * 32);
-    al[buf] = lds8<DIAG>(d_l + lp + rec * 32);
+    const char* rb = rw.d(Q::ky0(i) + r) + (Q::kx(i) + li) * 32;
+    ah[buf] = lds8<DIAG>(rb + hp);
+    al[buf] = lds8<DIAG>(rb + lp);
   };
   load_a(0, 0);
   load_a(1, 1);
@@ -488,19 +193,21 @@ __device__ __forceinline__ void b3_dgrad(const char* d_l, const f32x4 (&R)[13][2
   }
 }
 
+// ---------------------------------------------------------------------------- wgrad
 template <int E, int DIAG>
-__device__ __forceinline__ void b3_wgrad(const char* d_l, const char* p_l, f32x4 (&wacc)[13][2], int lane,
-                                         const s16x8& ones_hi, const s16x8& zero8) {
+__device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2], int lane, const s16x8& ones_hi,
+                                         const s16x8& zero8) {
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
   s16x8 ahi[2][2], alo[2][2], bhi[3], blo[3];
+  auto drow = [&](int r) { return rw.d(r); };
+  auto prow = [&](int r) { return rw.p(r); };
   auto load_a = [&](int m, int slot) {
-    const int ra = (2 * m + 2) * B2_SC + 2 + 4 * g + q4;
+    const char* r0 = drow(2 * m + 2) + (2 + 4 * g + q4) * 32 + p4 * 8;
+    const char* r1 = drow(2 * m + 3) + (2 + 4 * g + q4) * 32 + p4 * 8;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const s16x4 x0 = ldtr<DIAG>(d_l + h * B2_DPLANE + ra * 32 + p4 * 8);
-      const s16x4 x1 = ldtr<DIAG>(d_l + h * B2_DPLANE + (ra + B2_SC) * 32 + p4 * 8);
-      const s16x4 y0 = ldtr<DIAG>(d_l + (2 + h) * B2_DPLANE + ra * 32 + p4 * 8);
-      const s16x4 y1 = ldtr<DIAG>(d_l + (2 + h) * B2_DPLANE + (ra + B2_SC) * 32 + p4 * 8);
+      const s16x4 x0 = ldtr<DIAG>(r0 + h * BR_DPL), x1 = ldtr<DIAG>(r1 + h * BR_DPL);
+      const s16x4 y0 = ldtr<DIAG>(r0 + (2 + h) * BR_DPL), y1 = ldtr<DIAG>(r1 + (2 + h) * BR_DPL);
       ahi[slot][h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
       alo[slot][h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
     }
@@ -509,11 +216,11 @@ __device__ __forceinline__ void b3_wgrad(const char* d_l, const char* p_l, f32x4
     const int m = s / 13, tap = 13 * E + s % 13;
     if (tap < 25) {
       const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-      const int rb = (2 * m + ky) * B2_SC + kx + 4 * g + q4;
-      const s16x4 x0 = ldtr<DIAG>(p_l + rb * 32 + p4 * 8);
-      const s16x4 x1 = ldtr<DIAG>(p_l + (rb + B2_SC) * 32 + p4 * 8);
-      const s16x4 y0 = ldtr<DIAG>(p_l + B2_PPLANE + rb * 32 + p4 * 8);
-      const s16x4 y1 = ldtr<DIAG>(p_l + B2_PPLANE + (rb + B2_SC) * 32 + p4 * 8);
+      const int col = (kx + 4 * g + q4) * 32 + p4 * 8;
+      const char* r0 = prow(2 * m + ky) + col;
+      const char* r1 = prow(2 * m + ky + 1) + col;
+      const s16x4 x0 = ldtr<DIAG>(r0), x1 = ldtr<DIAG>(r1);
+      const s16x4 y0 = ldtr<DIAG>(r0 + BR_DPL), y1 = ldtr<DIAG>(r1 + BR_DPL);
       bhi[buf] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
       blo[buf] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
     } else {
@@ -549,10 +256,17 @@ __device__ __forceinline__ void b3_wgrad(const char* d_l, const char* p_l, f32x4
   }
 }
 
+__device__ __forceinline__ void br_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ BRRows br_rows(char* smem, int k) {
+  const int s = __builtin_amdgcn_readfirstlane(k % 3);
+  return BRRows{smem + BR_OFF_D + s * BR_SLOT * BR_DROW, smem + BR_OFF_P + s * BR_SLOT * BR_PROW};
+}
+
 template <int ROLE, int DIAG>  // ROLE 0/1 = dgrad wave D, 2/3 = wgrad
-__device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict__ wdpack, char* smem, int first_t) {
-#ifdef TDS_B3_MFMA_PRIO
-  __builtin_amdgcn_s_setprio(TDS_B3_MFMA_PRIO);
+__device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict__ wdpack, char* smem) {
+#ifdef TDS_BR_MFMA_PRIO
+  __builtin_amdgcn_s_setprio(TDS_BR_MFMA_PRIO);
 #endif
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
@@ -562,42 +276,37 @@ __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict
   f32x4 acc[8];
 #pragma unroll
   for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  if constexpr (ROLE < 2) b2_load_w<ROLE>(wdpack, R, lane);
+  if constexpr (ROLE < 2) br_load_w<ROLE>(wdpack, R, lane);
   s16x8 ones_hi, zero8;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     ones_hi[j] = (short)(li == 0 ? 0x3f80 : 0);
     zero8[j] = 0;
   }
-  const int hp = (g >> 1) * B2_DPLANE + (g & 1) * 16;
-  const int lp = (2 + (g >> 1)) * B2_DPLANE + (g & 1) * 16;
-  B2Tile prev{0, 0, 0, false};
-  bool have_prev = false;
-  int t = first_t;
-  for (int kk = 0; t < a.total; t += gridDim.x, ++kk) {
-    const B2Tile cur = b2_decode(a, t);
-    char* d_cur = smem + (kk & 1) * B3_DBUF;
-    char* p_cur = smem + B3_OFF_P + (kk % B3_NP) * B2_PBUF;
-    b3_barrier();  // tile t staged; the partner's exchange slot of tile t-1 is written
+  const int hp = (g >> 1) * BR_DPL + (g & 1) * 16;
+  const int lp = (2 + (g >> 1)) * BR_DPL + (g & 1) * 16;
+  BRTile prev{0, 0, 0, false, true};
+  int kk = 0;
+  for (;; ++kk) {
+    const BRTile cur = br_decode(a.walk, kk, a.nwg, a.w);
+    if (cur.end) break;
+    br_barrier();  // tile kk staged; the partner's exchange slot of tile kk-1 is written
+    const BRRows rw = br_rows(smem, kk);
     if constexpr (ROLE < 2) {
-      if (have_prev)
-        b2_xchg_finish<ROLE, DIAG>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk + 1) & 1) * B2_XCHG), acc, a.dp1,
+      if (!prev.end)
+        br_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + BR_OFF_X + ((kk + 1) & 1) * BR_XCHG), acc, a.dp1,
                              lane, prev.b, prev.r0, prev.c0, a.P);
-      b3_dgrad<ROLE, DIAG>(d_cur, R, acc, hp, lp, li);
-      b2_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + B3_OFF_X + (kk & 1) * B2_XCHG), acc, lane);
+      br_dgrad<ROLE, DIAG>(rw, R, acc, hp, lp, li);
+      br_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + BR_OFF_X + (kk & 1) * BR_XCHG), acc, lane);
     } else {
-      b3_wgrad<ROLE - 2, DIAG>(d_cur, p_cur, R, lane, ones_hi, zero8);
+      br_wgrad<ROLE - 2, DIAG>(rw, R, lane, ones_hi, zero8);
     }
     prev = cur;
-    have_prev = true;
   }
-  // kk == number of tiles here; the last put went to slot (kk - 1) & 1
-  int kk_end = 0;
-  for (int tt = first_t; tt < a.total; tt += gridDim.x) ++kk_end;
-  b3_barrier();
+  br_barrier();  // the last exchange slot is written
   if constexpr (ROLE < 2) {
-    if (have_prev)
-      b2_xchg_finish<ROLE, DIAG>(reinterpret_cast<const f32x4*>(smem + B3_OFF_X + ((kk_end - 1) & 1) * B2_XCHG), acc, a.dp1,
+    if (!prev.end)
+      br_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + BR_OFF_X + ((kk - 1) & 1) * BR_XCHG), acc, a.dp1,
                            lane, prev.b, prev.r0, prev.c0, a.P);
   } else {
     float* out = a.slab + (int64_t)blockIdx.x * 26 * 512;
@@ -612,85 +321,320 @@ __device__ __forceinline__ void b3_mfma(const B2Args& a, const uint4* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------- staging
+// Out-of-range lanes get this byte offset: the buffer load's range check returns zeros.
+constexpr uint32_t kBROob = 0xFFFFFFF0u;
+
+// Staging of NR rows (8: a tile's new rows, 4: a segment prologue) of image rows R0 ..
+// R0+NR-1 (R0 even), columns c0-2 .. c0+17, into dy2 / p1 row blocks.  Item = (2x2 pooling
+// window, 4-channel chunk): NR/2 x 10 windows x 8 chunks.  BIG: the 32 g2m planes of an image
+// exceed a 4 GiB buffer-descriptor range (64-bit g2m loads); a template parameter, because two
+// load paths under a runtime branch make the compiler wait vmcnt(0) at their merge.
+template <int NR, int WV, bool BIG, int DIAG>
+struct BRStager {
+  static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
+  static constexpr int ITEMS = NWIN * 8;
+  static constexpr int IPER = (ITEMS + 255) / 256;
+  static constexpr int PIECES = NR * BR_SC * 4;  // 16-B p1 pieces
+  static constexpr int PPER = (PIECES + 255) / 256;
+  float4 yv[IPER][4], gv[IPER];
+  uint4 pr[PPER];
+
+  __device__ __forceinline__ static void item_geom(int it, int& wy, int& wx) {
+    const int w = (it < ITEMS ? it : 0) >> 3;
+    wy = w / (BR_SC / 2);
+    wx = w - wy * (BR_SC / 2);
+  }
+
+  // the block is wholly inside the image and every window is pooled (no bounds work)
+  __device__ __forceinline__ static bool interior(const BRArgs& a, int R0, int c0) {
+    return R0 >= 0 && R0 + NR <= 2 * a.Q && c0 - 2 >= 0 && c0 + BR_TC + 2 <= 2 * a.Q;
+  }
+
+  __device__ __forceinline__ void load(const BRArgs& a, int b, int R0, int c0, int tid) {
+    if constexpr (DIAG == 3) {
+#pragma unroll
+      for (int u = 0; u < IPER; ++u) {
+        gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) yv[u][q] = gv[u];
+      }
+#pragma unroll
+      for (int j = 0; j < PPER; ++j) pr[j] = make_uint4(0u, 0u, 0u, 0u);
+      return;
+    }
+    const int P = a.P, Q = a.Q;
+    const bool in = interior(a, R0, c0);
+    const int64_t img = (int64_t)b * P;
+    // y2 / p1: one descriptor per block, based at (R0, c0-2); lanes outside the image -> kBROob
+    const __amdgpu_buffer_rsrc_t ry =
+        tds_buffer_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + R0) * P + (c0 - 2)) * 128, 0xFFFFFFF0u);
+    const __amdgpu_buffer_rsrc_t rp =
+        tds_buffer_rsrc(reinterpret_cast<const char*>(a.p1) + ((img + R0) * P + (c0 - 2)) * 64, 0xFFFFFFF0u);
+    const int64_t gplane = (int64_t)Q * Q;
+    const int py0 = R0 / 2, px0 = c0 / 2 - 1;
+    const __amdgpu_buffer_rsrc_t rg =
+        tds_buffer_rsrc(a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0, 0xFFFFFFF0u);
+    const int c4 = tid & 7;
+#pragma unroll
+    for (int u = 0; u < IPER; ++u) {
+      const int it = tid + 256 * u;
+      int wy, wx;
+      item_geom(it, wy, wx);
+      const bool item = it < ITEMS;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int lr = 2 * wy + (q >> 1), lc = 2 * wx + (q & 1);
+        const int gr = R0 + lr, gc = c0 - 2 + lc;
+        const bool ok = item && (in || (gr >= 0 && gr < P && gc >= 0 && gc < P));
+        const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 128 + c4 * 16) : kBROob;
+        yv[u][q] = DIAG == 7 ? make_float4(1.f, 0.f, 0.f, 0.f)
+                             : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0));
+      }
+      const int py = py0 + wy, px = px0 + wx;
+      const bool pooled = item && (in || (py >= 0 && py < Q && px >= 0 && px < Q));
+      float g4[4];
+      if constexpr (!BIG) {
+        const uint32_t og = (uint32_t)(((int64_t)c4 * 4 * gplane + (int64_t)wy * Q + wx) * 4);
+        const uint32_t gstep = (uint32_t)(gplane * 4);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          g4[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
+                                                                                 0, 0));
+      } else {
+        const float* gp = a.g2m + ((int64_t)b * 32 + 4 * c4) * gplane + (int64_t)(pooled ? py : 0) * Q + (pooled ? px : 0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g4[k] = gp[k * gplane];  // masked at use (store: pooled)
+      }
+      gv[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
+    }
+#pragma unroll
+    for (int j = 0; j < PPER; ++j) {
+      const int e = tid + 256 * j;
+      const int rec = (e < PIECES ? e : 0) >> 2, q = e & 3;
+      const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
+      const int gr = R0 + lr, gc = c0 - 2 + lc;
+      const bool ok = e < PIECES && (in || (gr >= 0 && gr < P && gc >= 0 && gc < P));
+      const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 64 + q * 16) : kBROob;
+      pr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
+    }
+  }
+
+  // BN2 / ReLU / pool backward of the staged windows -> dy2 hi|lo rows at dbase; p1 -> pbase;
+  // MIRROR: rows 4-7 stored a second time at dmir / pmir (the next slot's top rows).
+  // dy2 = k1*dz + k2*y2 + k3, dz = pooled gradient at the window's argmax of a*y2 + b.  Interior
+  // blocks take a short path (argmax by max + first-equal, torch's scan-order tie rule); a NaN
+  // anywhere in the wave's windows sends it to the general path (torch's NaN-wins rule).
+  template <bool MIRROR>
+  __device__ __forceinline__ void store(const BRArgs& a, int R0, int c0, int tid, char* dbase, char* pbase,
+                                        const float* kc, char* dmir, char* pmir) {
+    if constexpr (DIAG == 3) {}
+    const int c4 = tid & 7;
+    const int P = a.P, Q = a.Q;
+    const float4 ka4 = *reinterpret_cast<const float4*>(&kc[0 * 32 + 4 * c4]);
+    const float4 kb4 = *reinterpret_cast<const float4*>(&kc[1 * 32 + 4 * c4]);
+    const float4 k14 = *reinterpret_cast<const float4*>(&kc[2 * 32 + 4 * c4]);
+    const float4 k24 = *reinterpret_cast<const float4*>(&kc[3 * 32 + 4 * c4]);
+    const float4 k34 = *reinterpret_cast<const float4*>(&kc[4 * 32 + 4 * c4]);
+    const float ka[4] = {ka4.x, ka4.y, ka4.z, ka4.w}, kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
+    const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, k2[4] = {k24.x, k24.y, k24.z, k24.w},
+                k3[4] = {k34.x, k34.y, k34.z, k34.w};
+    bool fast = interior(a, R0, c0);
+    if (fast) {
+      float nsum = 0.f;
+#pragma unroll
+      for (int u = 0; u < IPER; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nsum += (yv[u][q].x + yv[u][q].y) + (yv[u][q].z + yv[u][q].w);
+      fast = __builtin_amdgcn_ballot_w64(isnan(nsum)) == 0;  // wave-uniform
+    }
+#pragma unroll
+    for (int u = 0; u < IPER; ++u) {
+      const int it = tid + 256 * u;
+      if (it >= ITEMS) continue;
+      int wy, wx;
+      item_geom(it, wy, wx);
+      float y[4][4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        y[q][0] = yv[u][q].x; y[q][1] = yv[u][q].y; y[q][2] = yv[u][q].z; y[q][3] = yv[u][q].w;
+      }
+      const float gg[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+      float d[4][4];
+      if constexpr (DIAG == 9) {  // timing only: no BN2 / pool backward math
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int cc = 0; cc < 4; ++cc) d[q][cc] = y[q][cc] + gg[cc];
+      } else if (fast) {
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          float z[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) z[q] = fmaf(ka[cc], y[q][cc], kb[cc]);
+          const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+          const bool e0 = z[0] == m, e1 = !e0 && z[1] == m, e2 = !e0 && !e1 && z[2] == m;
+          const bool e3 = !e0 && !e1 && !e2;
+          const float base[4] = {fmaf(k2[cc], y[0][cc], k3[cc]), fmaf(k2[cc], y[1][cc], k3[cc]),
+                                 fmaf(k2[cc], y[2][cc], k3[cc]), fmaf(k2[cc], y[3][cc], k3[cc])};
+          const float kg = k1[cc] * gg[cc];
+          d[0][cc] = e0 ? base[0] + kg : base[0];
+          d[1][cc] = e1 ? base[1] + kg : base[1];
+          d[2][cc] = e2 ? base[2] + kg : base[2];
+          d[3][cc] = e3 ? base[3] + kg : base[3];
+        }
+      } else {
+        const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;
+        const bool pooled = gy >= 0 && gx >= 0 && (gy >> 1) < Q && (gx >> 1) < Q;
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+          float m = ka[cc] * y[0][cc] + kb[cc];
+          int ai = 0;
+#pragma unroll
+          for (int q = 1; q < 4; ++q) {
+            const float z = ka[cc] * y[q][cc] + kb[cc];
+            if (z > m || isnan(z)) { m = z; ai = q; }  // first max in scan order, NaN wins (torch)
+          }
+          const int am = pooled ? ai : -1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int r = gy + (q >> 1), c = gx + (q & 1);
+            const bool inb = r >= 0 && r < P && c >= 0 && c < P;  // zero padding outside the image
+            const float dz = am == q ? gg[cc] : 0.f;
+            d[q][cc] = inb ? fmaf(k1[cc], dz, fmaf(k2[cc], y[q][cc], k3[cc])) : 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        uint32_t h01, l01, h23, l23;
+        split2_bf16(d[q][0], d[q][1], h01, l01);
+        split2_bf16(d[q][2], d[q][3], h23, l23);
+        const int lr = 2 * wy + (q >> 1);
+        const int ro = (2 * wx + (q & 1)) * 32 + (c4 & 3) * 8;
+        char* rec = dbase + lr * BR_DROW + ro;
+        *reinterpret_cast<uint2*>(rec + (c4 >> 2) * BR_DPL) = make_uint2(h01, h23);
+        *reinterpret_cast<uint2*>(rec + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
+        if (MIRROR && lr >= 4) {
+          char* mr = dmir + (lr - 4) * BR_DROW + ro;
+          *reinterpret_cast<uint2*>(mr + (c4 >> 2) * BR_DPL) = make_uint2(h01, h23);
+          *reinterpret_cast<uint2*>(mr + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PPER; ++j) {
+      const int e = tid + 256 * j;
+      if (e < PIECES) {
+        const int rec = e >> 2, q = e & 3;
+        const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
+        const int po = (q >> 1) * BR_DPL + lc * 32 + (q & 1) * 16;
+        *reinterpret_cast<uint4*>(pbase + lr * BR_PROW + po) = pr[j];
+        if (MIRROR && lr >= 4) *reinterpret_cast<uint4*>(pmir + (lr - 4) * BR_PROW + po) = pr[j];
+      }
+    }
+  }
+};
+
 template <int WV, int DIAG, bool BIG>  // staging wave WV (0..3) = workgroup wave 4 + WV
-__device__ __forceinline__ void b3_stage(const B2Args& a, char* smem, int first_t) {
+__device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   if constexpr (DIAG == 5) {  // timing only: no staging at all (consumers read stale LDS)
-    for (int t = first_t; t < a.total; t += gridDim.x) b3_barrier();
-    b3_barrier();
+    for (int k = 0; !br_decode(a.walk, k, a.nwg, a.w).end; ++k) br_barrier();
+    br_barrier();
     return;
   }
-#ifdef TDS_B3_STAGE_PRIO
-  __builtin_amdgcn_s_setprio(TDS_B3_STAGE_PRIO);
+#ifdef TDS_BR_STAGE_PRIO
+  __builtin_amdgcn_s_setprio(TDS_BR_STAGE_PRIO);
 #endif
   const int tid = threadIdx.x - 256;
-  const float* kc = reinterpret_cast<const float*>(smem + B3_OFF_K);
-  // two register sets: tile j's y2 / g2m registers are loaded two iterations before they are
-  // staged (set j & 1), its p1 DMA lands in buffer j % 4
-  B2Stager<DIAG, WV, true, BIG> st0, st1;
-  st0.init(a, tid);
-  st1.init(a, tid);
-  const int G = gridDim.x;
-  auto tile = [&](int j) { return first_t + j * G; };
-  auto pbuf = [&](int j) { return smem + B3_OFF_P + (j % B3_NP) * B2_PBUF; };  // written in store(j)
-  auto dbuf = [&](int j) { return smem + (j & 1) * B3_DBUF; };
-  if (tile(0) < a.total) {
-    st0.load(a, b2_decode(a, tile(0)), tid, nullptr);
-    st0.store(a, b2_decode(a, tile(0)), tid, dbuf(0), kc);
-    st0.store_p1(pbuf(0), tid);
+  const float* kc = reinterpret_cast<const float*>(smem + BR_OFF_K);
+  // slot j % 3: rows 0-3 (top) at dtop / ptop, the tile's 8 new rows at +4
+  auto dtop = [&](int j) { return smem + BR_OFF_D + (j % 3) * BR_SLOT * BR_DROW; };
+  auto ptop = [&](int j) { return smem + BR_OFF_P + (j % 3) * BR_SLOT * BR_PROW; };
+  // tile j's new rows, its last 4 mirrored into tile j+1's top (overwritten by a prologue when
+  // tile j+1 starts a segment: a later iteration, past a barrier)
+  auto stage = [&](BRStager<8, WV, BIG, DIAG>& s, int j, const BRTile& x) {
+    s.template store<true>(a, x.r0 + 2, x.c0, tid, dtop(j) + 4 * BR_DROW, ptop(j) + 4 * BR_PROW, kc, dtop(j + 1),
+                           ptop(j + 1));
+  };
+  // a segment's first tile: its 4 top rows (image rows r0-2 .. r0+1) staged synchronously
+  // straight into its slot's top (once per ~24 tiles)
+  auto prologue = [&](int j, const BRTile& x) {
+    BRStager<4, WV, BIG, DIAG> pro;
+    pro.load(a, x.b, x.r0 - 2, x.c0, tid);
+    pro.template store<false>(a, x.r0 - 2, x.c0, tid, dtop(j), ptop(j), kc, nullptr, nullptr);
+  };
+  // two register sets: tile j's new-row loads are issued two tiles before they are staged.
+  // Loads are unconditional (past the end: the list's last tile again, never staged): a load
+  // under a branch makes the wait for the OLDER set drain the younger one too (vmcnt(0)).
+  BRStager<8, WV, BIG, DIAG> st0, st1;
+  auto tile = [&](int j) { return br_decode(a.walk, j, a.nwg, a.w); };
+  auto ld = [&](BRStager<8, WV, BIG, DIAG>& s, int j) {
+    const BRTile x = tile(j);
+    s.load(a, x.b, x.r0 + 2, x.c0, tid);
+  };
+  // (a prologue runs after the set that stages the same tile is stored and before that set is
+  // reloaded, so its registers are the set's)
+  {
+    const BRTile x0 = tile(0);
+    if (!x0.end) {
+      ld(st0, 0);
+      stage(st0, 0, x0);
+      prologue(0, x0);
+    }
   }
-  // Loads are issued unconditionally (tiles past the end re-read the last tile, never staged):
-  // a load under a branch makes the compiler's wait-count analysis assume it was skipped, and
-  // the wait for the OLDER register set then drains the younger one too (vmcnt(0)).
-  auto ltile = [&](int j) { return b2_decode(a, min(tile(j), a.total - 1)); };
-  st1.load(a, ltile(1), tid, nullptr);
-  st0.load(a, ltile(2), tid, nullptr);
+  ld(st1, 1);
+  ld(st0, 2);
   // iteration kk stages tile kk+1 and loads tile kk+3 (both in set (kk+1) & 1)
-  for (int kk = 0; tile(kk) < a.total; kk += 2) {
-    b3_barrier();  // consumers start tile kk
-    if (tile(kk + 1) < a.total) {
-      st1.store(a, b2_decode(a, tile(kk + 1)), tid, dbuf(kk + 1), kc);
-      st1.store_p1(pbuf(kk + 1), tid);
+  for (int kk = 0; !tile(kk).end; kk += 2) {
+    br_barrier();  // consumers start tile kk
+    {
+      const BRTile x = tile(kk + 1);
+      if (!x.end) {
+        stage(st1, kk + 1, x);
+        if (x.start) prologue(kk + 1, x);
+      }
     }
-    st1.load(a, ltile(kk + 3), tid, nullptr);
-    if (tile(kk + 1) >= a.total) break;
-    b3_barrier();  // consumers start tile kk + 1
-    if (tile(kk + 2) < a.total) {
-      st0.store(a, b2_decode(a, tile(kk + 2)), tid, dbuf(kk + 2), kc);
-      st0.store_p1(pbuf(kk + 2), tid);
+    ld(st1, kk + 3);
+    if (tile(kk + 1).end) break;
+    br_barrier();  // consumers start tile kk + 1
+    {
+      const BRTile x = tile(kk + 2);
+      if (!x.end) {
+        stage(st0, kk + 2, x);
+        if (x.start) prologue(kk + 2, x);
+      }
     }
-    st0.load(a, ltile(kk + 4), tid, nullptr);
+    ld(st0, kk + 4);
   }
-  b3_barrier();
+  br_barrier();
 }
 
 template <int DIAG, bool BIG>
-__global__ __launch_bounds__(B3_THREADS, 2) void conv2_bwd3_kernel(
+__global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
     const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
     const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
-    float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ order, int B, int P, int Q) {
+    float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ walk, int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  B2Args a;
-  a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.order = order;
-  a.B = B; a.P = P; a.Q = Q;
-  a.tiles_c = (P + B2_TC - 1) / B2_TC;
-  a.tiles_r = (P + B2_TH - 1) / B2_TH;
-  a.per_img = a.tiles_c * a.tiles_r;
-  a.total = a.per_img * B;
-  float* kc = reinterpret_cast<float*>(smem + B3_OFF_K);
+  BRArgs a;
+  a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.walk = walk;
+  a.B = B; a.P = P; a.Q = P / 2;
+  a.nwg = gridDim.x;
+  a.w = xcd_remap(blockIdx.x, gridDim.x);  // this workgroup's list (XCD-contiguous: neighbouring columns)
+  float* kc = reinterpret_cast<float*>(smem + BR_OFF_K);
   if (tid < 160) kc[tid] = (tid < 64) ? aff2[tid] : kbuf[tid - 64];
   __syncthreads();  // kc visible to the staging waves
-  const int t0 = xcd_remap(blockIdx.x, gridDim.x);
   switch (wv) {
-    case 0: b3_mfma<0, DIAG>(a, wdpack, smem, t0); break;
-    case 1: b3_mfma<1, DIAG>(a, wdpack, smem, t0); break;
-    case 2: b3_mfma<2, DIAG>(a, wdpack, smem, t0); break;
-    case 3: b3_mfma<3, DIAG>(a, wdpack, smem, t0); break;
-    case 4: b3_stage<0, DIAG, BIG>(a, smem, t0); break;
-    case 5: b3_stage<1, DIAG, BIG>(a, smem, t0); break;
-    case 6: b3_stage<2, DIAG, BIG>(a, smem, t0); break;
-    default: b3_stage<3, DIAG, BIG>(a, smem, t0); break;
+    case 0: br_mfma<0, DIAG>(a, wdpack, smem); break;
+    case 1: br_mfma<1, DIAG>(a, wdpack, smem); break;
+    case 2: br_mfma<2, DIAG>(a, wdpack, smem); break;
+    case 3: br_mfma<3, DIAG>(a, wdpack, smem); break;
+    case 4: br_stage<0, DIAG, BIG>(a, smem); break;
+    case 5: br_stage<1, DIAG, BIG>(a, smem); break;
+    case 6: br_stage<2, DIAG, BIG>(a, smem); break;
+    default: br_stage<3, DIAG, BIG>(a, smem); break;
   }
 }
 
@@ -701,55 +645,95 @@ using namespace tds;
 int tds_conv2_bwd3_num_wg() { return tds_conv2_num_wg(); }  // one 8-wave workgroup per CU
 
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c) {
-  *tiles_r = (P + B2_TH - 1) / B2_TH;
-  *tiles_c = (P + B2_TC - 1) / B2_TC;
+  *tiles_r = (P + BR_TH - 1) / BR_TH;
+  *tiles_c = (P + BR_TC - 1) / BR_TC;
+}
+
+// Walk table of the rolling conv2 backward: segments of ~seg tiles down one tile column of one
+// image; segment s (image-major, then row band, then column) goes to workgroup list s % nwg, so
+// the workgroups of one XCD (contiguous lists after xcd_remap) take neighbouring columns of the
+// same band.  out == nullptr: returns the table length (rows x nwg ints); else fills it (rows =
+// longest list + 3, the tail of each list marked kWalkEnd over a copy of its last tile, which
+// the staging's look-ahead loads re-read).  Returns -1 on unsupported sizes.
+int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, int seg) {
+  if (B < 1 || B > 63 || tiles_r < 1 || tiles_r > 4095 || tiles_c < 1 || tiles_c > 4095 || nwg < 1 || seg < 2)
+    return -1;
+  const int nband = (tiles_r + seg - 1) / seg;
+  // near-equal bands (lengths differ by at most 1, every band >= 2 tiles when tiles_r >= 2)
+  std::vector<int> bstart(nband + 1);
+  for (int j = 0; j <= nband; ++j) bstart[j] = (int)((int64_t)j * tiles_r / nband);
+  std::vector<int> len(nwg, 0);
+  const int64_t nseg = (int64_t)B * nband * tiles_c;
+  for (int64_t s = 0; s < nseg; ++s) {
+    const int j = (int)((s / tiles_c) % nband);
+    len[s % nwg] += bstart[j + 1] - bstart[j];
+  }
+  int maxlen = 0;
+  for (int v : len) maxlen = v > maxlen ? v : maxlen;
+  const int rows = maxlen + 3;
+  if ((int64_t)rows * nwg >= ((int64_t)1 << 31)) return -1;  // the kernel indexes it in 32 bits
+  if (out == nullptr) return (int64_t)rows * nwg;
+  std::vector<int> fill(nwg, 0);
+  std::vector<uint32_t> last(nwg, 0u);
+  for (int64_t s = 0; s < nseg; ++s) {
+    const int b = (int)(s / ((int64_t)nband * tiles_c));
+    const int j = (int)((s / tiles_c) % nband), tc = (int)(s % tiles_c);
+    const int w = (int)(s % nwg);
+    for (int tr = bstart[j]; tr < bstart[j + 1]; ++tr) {
+      const uint32_t code = ((uint32_t)b << 24) | ((uint32_t)tr << 12) | (uint32_t)tc;
+      out[(int64_t)fill[w]++ * nwg + w] = (int)(code | (tr == bstart[j] ? kWalkStart : 0u));
+      last[w] = code;
+    }
+  }
+  for (int w = 0; w < nwg; ++w)
+    for (int k = fill[w]; k < rows; ++k) out[(int64_t)k * nwg + w] = (int)(last[w] | kWalkEnd);
+  return (int64_t)rows * nwg;
 }
 
 #ifdef TDS_DIAG
 // timing-only variants: 1 no MFMAs, 3 no global tile loads, 5 no staging, 7 no y2 loads, 9 no
-// BN2 / pool backward math in the staging, 11 no dp1 stores.  Compiled only into a -DTDS_DIAG build
+// BN2 / pool backward math in the staging.  Compiled only into a -DTDS_DIAG build
 // (python -m torch_distributed_sandbox_amd._build --variant diag -D TDS_DIAG; TDS_CONV2_DIAG=N).
-static int b3_diag_env() {
+static int br_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
   return e ? std::atoi(e) : 0;
 }
 #else
-static int b3_diag_env() { return 0; }
+static int br_diag_env() { return 0; }
 #endif
 
-// g2m: planar [B][32][Q][Q]; order: the blocked tile order table (tds_tile_order_fill) from the caller
+// g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups
 void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, const int* order, int nwg, int B, int P,
+                    const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P,
                     hipStream_t st) {
   const int Q = P / 2;
   const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
-#define TDS_B3_LAUNCH_B(D, BG)                                                                                         \
+#define TDS_BR_LAUNCH_B(D, BG)                                                                                         \
   {                                                                                                                    \
     static bool set = false;                                                                                           \
     if (!set) {                                                                                                        \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd3_kernel<D, BG>),                               \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, B3_LDS);                                   \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(conv2_bwd_roll_kernel<D, BG>),                           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, BR_LDS);                                   \
       set = true;                                                                                                      \
     }                                                                                                                  \
-    hipLaunchKernelGGL((conv2_bwd3_kernel<D, BG>), dim3(nwg), dim3(B3_THREADS), B3_LDS, st,                            \
+    hipLaunchKernelGGL((conv2_bwd_roll_kernel<D, BG>), dim3(nwg), dim3(BR_THREADS), BR_LDS, st,                        \
                        reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, reinterpret_cast<const uint4*>(p1),       \
-                       reinterpret_cast<const uint4*>(wd), dp1, slab, order, B, P, Q);                                  \
+                       reinterpret_cast<const uint4*>(wd), dp1, slab, walk, B, P);                                      \
     TDS_LAUNCH_CHECK();                                                                                                \
   }
-#define TDS_B3_LAUNCH(D)           \
-  if (big) TDS_B3_LAUNCH_B(D, true) \
-  else TDS_B3_LAUNCH_B(D, false)
-  switch (b3_diag_env()) {
+#define TDS_BR_LAUNCH(D)           \
+  if (big) TDS_BR_LAUNCH_B(D, true) \
+  else TDS_BR_LAUNCH_B(D, false)
+  switch (br_diag_env()) {
 #ifdef TDS_DIAG
-    case 1: TDS_B3_LAUNCH(1) break;
-    case 3: TDS_B3_LAUNCH(3) break;
-    case 5: TDS_B3_LAUNCH(5) break;
-    case 7: TDS_B3_LAUNCH(7) break;
-    case 9: TDS_B3_LAUNCH(9) break;
-    case 11: TDS_B3_LAUNCH(11) break;
+    case 1: TDS_BR_LAUNCH(1) break;
+    case 3: TDS_BR_LAUNCH(3) break;
+    case 5: TDS_BR_LAUNCH(5) break;
+    case 7: TDS_BR_LAUNCH(7) break;
+    case 9: TDS_BR_LAUNCH(9) break;
 #endif
-    default: TDS_B3_LAUNCH(0) break;
+    default: TDS_BR_LAUNCH(0) break;
   }
-#undef TDS_B3_LAUNCH
-#undef TDS_B3_LAUNCH_B
+#undef TDS_BR_LAUNCH
+#undef TDS_BR_LAUNCH_B
 }

@@ -79,8 +79,11 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const fl
                     double* partial, const int* order, int nwg, int B, int P, hipStream_t st);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
+// rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups
 void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, const int* order, int nwg, int B, int P, hipStream_t st);
+                    const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P, hipStream_t st);
+// host: per-workgroup tile lists of vertical segments of ~seg tiles; out == nullptr -> length
+int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, int seg);
 
 // ---- convnet_fused.hip
 int tds_fused_num_wg(int per_cu);
