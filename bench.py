@@ -67,6 +67,9 @@ def _parser():
                     help="cpu: rehearsal of the launch/exchange path on the torch-ops plan (small --image-size)")
     ap.add_argument("--shared-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (needs --backend gloo); recorded in the JSON")
+    ap.add_argument("--allreduce-probe", action=argparse.BooleanOptionalAction, default=True,
+                    help="world > 1: after the timed steps, time a few all-reduces over the same communicator "
+                         "and report their bus bandwidth in config.allreduce_probe (outside the timed region)")
     ap.add_argument("--spawn-timeout", type=float, default=1800.0,
                     help="self-spawn: terminate all ranks if the job runs longer than this (s)")
     return ap
@@ -97,6 +100,35 @@ def _spawn_ranks(args, argv) -> int:
         print(f"bench.py: {e}", file=sys.stderr, flush=True)
         return 124
     return 0
+
+
+def _allreduce_probe(tdist, device, world, on_gpu):
+    """All-reduce (SUM) bus bandwidth over the bench's own communicator, after the timed steps:
+    the xGMI numbers behind the step time (busbw = 2 (W-1)/W x bytes / time, the ring volume per
+    link).  Sizes: a conv/BN-sized bucket, a mid bucket, and the 720 MB fc gradient on GPU."""
+    sizes = [4 << 20, 64 << 20, 720_000_040] if on_gpu else [1 << 20]
+    out = []
+    for nbytes in sizes:
+        t = torch.ones(nbytes // 4, device=device, dtype=torch.float32)
+        iters = 5 if on_gpu else 2
+        for _ in range(2):
+            tdist.all_reduce(t)
+        if on_gpu:
+            torch.cuda.synchronize(device)
+        tdist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            tdist.all_reduce(t)
+        if on_gpu:
+            torch.cuda.synchronize(device)
+        dt = (time.perf_counter() - t0) / iters
+        g = torch.tensor([dt], device=device, dtype=torch.float64)
+        tdist.all_reduce(g, tdist.ReduceOp.MAX)
+        dt = float(g.item())
+        out.append({"MB": round(nbytes / 1e6, 3), "ms": round(dt * 1e3, 3),
+                    "busbw_GBps": round(2 * (world - 1) / world * nbytes / dt / 1e9, 2)})
+        del t
+    return out
 
 
 def main(argv=None) -> int:
@@ -181,9 +213,28 @@ def run(argv) -> None:
     src_pool = src_pool.view(pool, B, 28, 28)
     lab_pool = lab_pool.view(pool, B)
 
+    # input pipeline: batch i+1 is upsampled on a side stream while step i computes (the role
+    # of the reference's DataLoader prefetch); the step waits on that stream, and the batch is
+    # recorded on the compute stream so the caching allocator cannot recycle it early
+    data_stream = torch.cuda.Stream(device) if on_gpu else None
+
+    def produce(i):
+        j = i % pool
+        if data_stream is None:
+            return TF.upsample_bilinear_u8(src_pool[j], H, W)
+        data_stream.wait_stream(torch.cuda.current_stream(device))  # the previous step's reads of src
+        with torch.cuda.stream(data_stream):
+            return TF.upsample_bilinear_u8(src_pool[j], H, W)
+
+    pending = {}
+
     def step(i):
         j = i % pool
-        images = TF.upsample_bilinear_u8(src_pool[j], H, W)
+        images = pending.pop(i) if i in pending else produce(i)
+        if data_stream is not None:
+            torch.cuda.current_stream(device).wait_stream(data_stream)
+            images.record_stream(torch.cuda.current_stream(device))
+        pending[i + 1] = produce(i + 1)
         out = ddp(images)
         loss = criterion(out, lab_pool[j])
         optimizer.zero_grad()
@@ -211,6 +262,7 @@ def run(argv) -> None:
         tdist.all_reduce(t, tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item()) if loss is not None else None
+    probe = _allreduce_probe(tdist, device, world, on_gpu) if world > 1 and args.allreduce_probe else None
     ms = 1e3 * elapsed / max(1, args.steps)
     imgs_per_sec = world * B * args.steps / elapsed
     if rank == 0:
@@ -235,6 +287,8 @@ def run(argv) -> None:
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3) if on_gpu else None,
             "final_loss": final_loss,
         }
+        if probe is not None:
+            config["allreduce_probe"] = probe
         if args.shared_device:
             config["shared_device"] = True  # rehearsal: all ranks on one GPU, not a multi-GPU number
         rec = {

@@ -55,6 +55,23 @@ Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shap
 
 int l1_wg() { return tds_fused_num_wg(4); }
 
+// Fork / join events of one device (timing disabled), created once and never destroyed.
+struct ForkJoin {
+  hipEvent_t fork, join;
+};
+const ForkJoin& fork_join(int dev) {
+  static std::mutex mu;
+  static auto* cache = new std::map<int, ForkJoin>();
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache->find(dev);
+  if (it != cache->end()) return it->second;
+  ForkJoin fj{};
+  TORCH_CHECK(hipEventCreateWithFlags(&fj.fork, hipEventDisableTiming) == hipSuccess &&
+                  hipEventCreateWithFlags(&fj.join, hipEventDisableTiming) == hipSuccess,
+              "tdsa fused: hipEventCreateWithFlags failed");
+  return (*cache)[dev] = fj;
+}
+
 // Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
 // torch caching allocator, built once.  The map is never destroyed (no frees at process exit).
 const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg) {
@@ -130,10 +147,19 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   TORCH_CHECK(nac > 0, "fused_l1_forward: W % 4 == 0 required (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo.dtype(at::kDouble));
   auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
-  tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
-                 st);
+  // border strips on a side stream beside the autocorrelation (fork / join by events; both
+  // buffers come from st's pool and st waits for the join before anything reads them)
+  const int dev = (int)x.get_device();
+  hipStream_t side = c10::hip::getStreamFromPool(false, dev).stream();
+  const ForkJoin& fj = fork_join(dev);
+  TORCH_CHECK(hipEventRecord(fj.fork, st) == hipSuccess && hipStreamWaitEvent(side, fj.fork, 0) == hipSuccess,
+              "fused_l1_forward: stream fork");
+  tds_x_border(x.data_ptr<float>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, side);
+  TORCH_CHECK(hipEventRecord(fj.join, side) == hipSuccess, "fused_l1_forward: stream join");
+  tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, (int)B, (int)H, (int)W, st);
   auto asum = at::empty({42}, fo.dtype(at::kDouble));
   tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
+  TORCH_CHECK(hipStreamWaitEvent(st, fj.join, 0) == hipSuccess, "fused_l1_forward: stream join");
   auto gram = at::empty({650}, fo.dtype(at::kDouble));
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
   tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W,
@@ -246,6 +272,15 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
 // update_lr > 0: the plain-SGD step of fc.weight runs in the same pass (W -= lr * dW).
 // returns (dW [into dw_out if given; empty when !compute_dw], db_fc, dgamma2, dbeta2, g2m, kbuf)
 // BN2 partial-sum workspace (doubles) of the head backward for B images at pooled size P/2
+// Host copy of the conv2 backward walk table (CPU int tensor [rows, nwg]) for tests/inspection.
+Tensor conv2_bwd_walk_table(int64_t B, int64_t tiles_r, int64_t tiles_c, int64_t nwg, int64_t seg) {
+  const int64_t n = tds_conv2_bwd_walk(nullptr, (int)B, (int)tiles_r, (int)tiles_c, (int)nwg, (int)seg);
+  TORCH_CHECK(n > 0, "conv2_bwd_walk_table: unsupported sizes");
+  auto t = at::empty({n / nwg, nwg}, at::TensorOptions().dtype(at::kInt));
+  tds_conv2_bwd_walk(t.data_ptr<int>(), (int)B, (int)tiles_r, (int)tiles_c, (int)nwg, (int)seg);
+  return t;
+}
+
 int64_t head_bwd_workspace(int64_t B, int64_t P) {
   const int Q = (int)(P / 2);
   return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_pb_nblk(Q) * 2;
@@ -446,6 +481,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
+  m.def("conv2_bwd_walk_table(int B, int tiles_r, int tiles_c, int nwg, int seg) -> Tensor", &conv2_bwd_walk_table);
   m.def(
       "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale, "
       "Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",

@@ -32,6 +32,7 @@
 // One bare s_barrier per tile (after lgkmcnt(0)) separates producer and consumers: while the
 // consumers read slot k%3, the staging writes slot (k+1)%3's new rows and slot (k+2)%3's top
 // (the slot of tile k-1, finished); the register loads for tile k+3 are already in flight.
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -650,9 +651,13 @@ void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c) {
 }
 
 // Walk table of the rolling conv2 backward: segments of ~seg tiles down one tile column of one
-// image; segment s (image-major, then row band, then column) goes to workgroup list s % nwg, so
-// the workgroups of one XCD (contiguous lists after xcd_remap) take neighbouring columns of the
-// same band.  out == nullptr: returns the table length (rows x nwg ints); else fills it (rows =
+// image (segment s: image-major, then row band, then column).  Whole rounds of nwg segments go
+// round-robin (segment s to list s % nwg: the workgroups of one XCD, contiguous lists after
+// xcd_remap, take neighbouring columns of the same band).  The last, partial round is cut into
+// nwg near-equal runs of consecutive tiles instead (a run may start mid-segment or cross into
+// the next column: each such start is flagged and re-stages its 4 top rows), so no workgroup
+// ends a whole segment after the others (the round-robin tail left a 4.7 % spread at the bench
+// shape).  out == nullptr: returns the table length (rows x nwg ints); else fills it (rows =
 // longest list + 3, the tail of each list marked kWalkEnd over a copy of its last tile, which
 // the staging's look-ahead loads re-read).  Returns -1 on unsupported sizes.
 int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, int seg) {
@@ -662,32 +667,59 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
   // near-equal bands (lengths differ by at most 1, every band >= 2 tiles when tiles_r >= 2)
   std::vector<int> bstart(nband + 1);
   for (int j = 0; j <= nband; ++j) bstart[j] = (int)((int64_t)j * tiles_r / nband);
-  std::vector<int> len(nwg, 0);
   const int64_t nseg = (int64_t)B * nband * tiles_c;
+  const int64_t nfull = nseg / nwg * nwg;  // segments dealt in whole rounds
+  auto seg_of = [&](int64_t s, int& b, int& j, int& tc) {
+    b = (int)(s / ((int64_t)nband * tiles_c));
+    j = (int)((s / tiles_c) % nband);
+    tc = (int)(s % tiles_c);
+  };
+  std::vector<int64_t> len(nwg, 0);
+  int64_t ntail = 0;
   for (int64_t s = 0; s < nseg; ++s) {
-    const int j = (int)((s / tiles_c) % nband);
-    len[s % nwg] += bstart[j + 1] - bstart[j];
+    int b, j, tc;
+    seg_of(s, b, j, tc);
+    if (s < nfull) len[s % nwg] += bstart[j + 1] - bstart[j];
+    else ntail += bstart[j + 1] - bstart[j];
   }
-  int maxlen = 0;
-  for (int v : len) maxlen = v > maxlen ? v : maxlen;
-  const int rows = maxlen + 3;
-  if ((int64_t)rows * nwg >= ((int64_t)1 << 31)) return -1;  // the kernel indexes it in 32 bits
-  if (out == nullptr) return (int64_t)rows * nwg;
-  std::vector<int> fill(nwg, 0);
+  const int64_t tbase = ntail / nwg, textra = ntail % nwg;
+  int64_t maxlen = 0;
+  for (int w = 0; w < nwg; ++w) maxlen = std::max(maxlen, len[w] + tbase + (w < textra ? 1 : 0));
+  const int64_t rows = maxlen + 3;
+  if (rows * nwg >= ((int64_t)1 << 31)) return -1;  // the kernel indexes it in 32 bits
+  if (out == nullptr) return rows * nwg;
+  std::vector<int64_t> fill(nwg, 0);
   std::vector<uint32_t> last(nwg, 0u);
+  auto put = [&](int w, uint32_t code, bool start) {
+    out[fill[w]++ * nwg + w] = (int)(code | (start ? kWalkStart : 0u));
+    last[w] = code;
+  };
+  int tw = 0;                                   // tail: current list
+  int64_t tgot = 0, twant = tbase + (0 < textra ? 1 : 0);
   for (int64_t s = 0; s < nseg; ++s) {
-    const int b = (int)(s / ((int64_t)nband * tiles_c));
-    const int j = (int)((s / tiles_c) % nband), tc = (int)(s % tiles_c);
-    const int w = (int)(s % nwg);
+    int b, j, tc;
+    seg_of(s, b, j, tc);
     for (int tr = bstart[j]; tr < bstart[j + 1]; ++tr) {
       const uint32_t code = ((uint32_t)b << 24) | ((uint32_t)tr << 12) | (uint32_t)tc;
-      out[(int64_t)fill[w]++ * nwg + w] = (int)(code | (tr == bstart[j] ? kWalkStart : 0u));
-      last[w] = code;
+      if (s < nfull) {
+        put((int)(s % nwg), code, tr == bstart[j]);
+        continue;
+      }
+      while (twant == 0) {  // lists that get no tail tiles (ntail < nwg)
+        ++tw;
+        twant = tbase + (tw < textra ? 1 : 0);
+      }
+      put(tw, code, tr == bstart[j] || tgot == 0);
+      if (++tgot == twant) {
+        ++tw;
+        tgot = 0;
+        twant = tw < nwg ? tbase + (tw < textra ? 1 : 0) : 0;
+      }
     }
   }
   for (int w = 0; w < nwg; ++w)
-    for (int k = fill[w]; k < rows; ++k) out[(int64_t)k * nwg + w] = (int)(last[w] | kWalkEnd);
-  return (int64_t)rows * nwg;
+    for (int64_t k = fill[w]; k < rows; ++k) out[k * nwg + w] = (int)(last[w] | kWalkEnd);
+  return rows * nwg;
 }
 
 #ifdef TDS_DIAG

@@ -251,37 +251,6 @@ __global__ void bn_finalize_shifted_kernel(const double* __restrict__ partial, i
   aff[C + c] = bt - (float)mean * gm * invstd;
 }
 
-// Border strips: for each image, line L in {row 0,1,H-2,H-1, col 0,1,W-2,W-1} and d in
-// [-4,4]^2: strip[L][d] = sum_{u on line L} x(u) x(u+d); also plain line sums (d = "none").
-// grid: (82 (81 d + 1 plain), 8 lines), block reduces over B images and the line.
-__global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__ x, double* __restrict__ strips,
-                                                       int B, int H, int W) {
-  __shared__ double sh[8];
-  const int di = blockIdx.x, L = blockIdx.y;
-  const int dy = di / 9 - 4, dx = di % 9 - 4;
-  const bool plain = di == 81;
-  const bool is_row = L < 4;
-  const int fixed = is_row ? (L < 2 ? L : H - 4 + L) : (L < 6 ? L - 4 : W - 8 + L);
-  const int len = is_row ? W : H;
-  double s = 0.0;
-  for (int b = 0; b < B; ++b) {
-    const float* xb = x + (int64_t)b * H * W;
-    for (int i = threadIdx.x; i < len; i += blockDim.x) {
-      const int r = is_row ? fixed : i, c = is_row ? i : fixed;
-      if (r < 0 || r >= H || c < 0 || c >= W) continue;
-      const float u = xb[(int64_t)r * W + c];
-      if (plain) {
-        s += u;
-      } else {
-        const int r2 = r + dy, c2 = c + dx;
-        if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) s += (double)u * xb[(int64_t)r2 * W + c2];
-      }
-    }
-  }
-  s = block_sum(s, sh);
-  if (threadIdx.x == 0) strips[L * 82 + di] = s;
-}
-
 // head kernels: see head_fused.hip
 
 // out[e] = sum_k in[(e / inner) * ostride + (e % inner) + k * kstride]  (one workgroup per output, fp64)
@@ -299,17 +268,24 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
 // BN backward finalize from (sum dz, sum dz*y) partials:
 //   dgamma = invstd*(sdzy - mean*sdz), dbeta = sdz,
 //   dy = k1*dz + k2*y + k3,  k1 = g*is, k2 = -g*is^3*(sdzy - mean*sdz)/n, k3 = -g*is*sdz/n - k2*mean
-__global__ void bn_bwd_finalize2_kernel(const double* __restrict__ partial, int C, int nchunk, int64_t n,
-                                        const float* __restrict__ gamma, const float* __restrict__ stats,
-                                        float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ kbuf,
-                                        double* __restrict__ sums_out) {
-  const int c = threadIdx.x;
-  if (c >= C) return;
+// One workgroup per channel (the head backward leaves ~10^3 partials per channel: a serial
+// loop per channel took 21 us).
+__global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __restrict__ partial, int C, int nchunk,
+                                                               int64_t n, const float* __restrict__ gamma,
+                                                               const float* __restrict__ stats,
+                                                               float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                               float* __restrict__ kbuf, double* __restrict__ sums_out) {
+  __shared__ double sh[8];
+  const int c = blockIdx.x;
   double sdz = 0.0, sdzy = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    sdz += partial[((int64_t)c * nchunk + k) * 2];
-    sdzy += partial[((int64_t)c * nchunk + k) * 2 + 1];
+  for (int k = threadIdx.x; k < nchunk; k += blockDim.x) {
+    const double2 v = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nchunk + k) * 2);
+    sdz += v.x;
+    sdzy += v.y;
   }
+  sdz = block_sum(sdz, sh);
+  sdzy = block_sum(sdzy, sh);
+  if (threadIdx.x != 0) return;
   const double mean = stats[c], is = stats[C + c];
   const double gm = gamma ? gamma[c] : 1.0;
   const double sdxh = sdzy - mean * sdz;  // sum dz*(y-mean)
@@ -351,7 +327,7 @@ constexpr int LB_PER = (LB_V + 255) / 256;
 // (the sparse kernel's tile); 4 waves, wave w = row pairs 2w, 2w+1 x 4 column segments.  The
 // dp1 / argmax tile and the x tile (packed bf16 hi|lo words, as l1_conv_bf3 stages it)
 // go through LDS; fp32 MFMA accumulation per tile (256 pixels), fp64 across tiles.
-// partial[wg*4 + wave][16][27] in the sparse kernel's layout ([0] sum dz, [1] 0, [2+j] taps).
+// partial[wg][16][27] in the sparse kernel's layout ([0] sum dz, [1] 0, [2+j] taps).
 constexpr int LM_XS = 80;  // x tile row stride (words): 20 rows x (72 staged + pad) columns
 __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restrict__ x, const float* __restrict__ dp1,
                                                           const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
@@ -510,20 +486,28 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
 #pragma unroll
       for (int r = 0; r < 4; ++r) dacc[blk][r] += (double)acc[blk][r];
   }
-  // D layout: lane holds column n = 16*blk + li, rows co = 4*g + r
-  double* out = partial + ((int64_t)blockIdx.x * 4 + wv) * 16 * LB_NACC;
+  // D layout: lane holds column n = 16*blk + li, rows co = 4*g + r.  The 4 waves' sums are
+  // added in LDS (fixed order) so the workgroup writes ONE partial row (the cross-workgroup
+  // reduction reads a quarter of the rows it did with one row per wave).
+  __syncthreads();  // the last tile's LDS reads are done
+  double* red = reinterpret_cast<double*>(lds);  // [4 waves][16 co][27]: 13.8 KB of the tile buffers
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int n = 16 * blk + li;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int co = 4 * g + r;
-      if (n < 25) out[co * LB_NACC + 2 + n] = dacc[blk][r];
-      else if (n == 25) out[co * LB_NACC + 0] = dacc[blk][r];
-      else if (n == 26) out[co * LB_NACC + 1] = 0.0;
+      double* o = red + (wv * 16 + 4 * g + r) * LB_NACC;
+      if (n < 25) o[2 + n] = dacc[blk][r];
+      else if (n == 25) o[0] = dacc[blk][r];
+      else if (n == 26) o[1] = 0.0;
     }
   }
+  __syncthreads();
+  double* out = partial + (int64_t)blockIdx.x * 16 * LB_NACC;
+  for (int e = tid; e < 16 * LB_NACC; e += 256)
+    out[e] = (red[e] + red[16 * LB_NACC + e]) + (red[2 * 16 * LB_NACC + e] + red[3 * 16 * LB_NACC + e]);
 }
+static_assert(4 * 16 * LB_NACC * 8 <= LB_NP * 64 + LB_NP * 16 + LB_XR * LM_XS * 4, "l1_bwd LDS reduction scratch");
 
 // Gram of the conv1 patches from the x autocorrelation (one workgroup):
 //   G[k][j] = Full(d) - sum_{excluded rows of k} R(d,row) - sum_{excluded cols} C(d,col)
@@ -620,13 +604,17 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
 
 // Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
 //   dw1[c][j] = a1 sdzx[c][j] + a2 (sum_k w1[c][k] G[k][j] + b1[c] S[j]) + a3 S[j]
-__global__ void l1_finalize_kernel(const double* __restrict__ bwd_sum, const double* __restrict__ gram,
-                                   int64_t n, const float* __restrict__ w1, const float* __restrict__ b1,
-                                   const float* __restrict__ gamma1, const float* __restrict__ stats1,
-                                   float* __restrict__ dw1, float* __restrict__ db1, float* __restrict__ dgamma1,
-                                   float* __restrict__ dbeta1, float scale) {
-  const int c = threadIdx.x;
-  if (c >= 16) return;
+// one thread per (c, j) (400 of 512); every thread of channel c forms its a1..a3 (25 FMAs).
+__global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restrict__ bwd_sum,
+                                                          const double* __restrict__ gram, int64_t n,
+                                                          const float* __restrict__ w1, const float* __restrict__ b1,
+                                                          const float* __restrict__ gamma1,
+                                                          const float* __restrict__ stats1, float* __restrict__ dw1,
+                                                          float* __restrict__ db1, float* __restrict__ dgamma1,
+                                                          float* __restrict__ dbeta1, float scale) {
+  const int e = threadIdx.x;
+  if (e >= 16 * 25) return;
+  const int c = e / 25, j = e - 25 * (e / 25);
   const double* acc = bwd_sum + c * LB_NACC;
   const double* G = gram;
   const double* S = gram + 625;
@@ -635,21 +623,20 @@ __global__ void l1_finalize_kernel(const double* __restrict__ bwd_sum, const dou
   const double sdz = acc[0];
   // sum dz1 * y1 = w1[c] . sum dz1 xpatch + b1[c] sum dz1  (y1 = w1 . xpatch + b1)
   double sdzy = (double)b1[c] * sdz;
-  for (int j = 0; j < 25; ++j) sdzy += (double)w1[c * 25 + j] * acc[2 + j];
+  for (int k = 0; k < 25; ++k) sdzy += (double)w1[c * 25 + k] * acc[2 + k];
   const double sdxh = sdzy - mean * sdz;
-  if (dgamma1) dgamma1[c] = (float)(is * sdxh);
-  if (dbeta1) dbeta1[c] = (float)sdz;
   const double a1 = gm * is;
   const double a2 = -gm * is * is * is * sdxh / (double)n;
   const double a3 = -gm * is * sdz / (double)n - a2 * mean;
-  // db1 = sum dy1 = a1 sdz + a2 sum y1 + a3 n  (sum y1 = n*mean)
-  if (db1) db1[c] = (float)(scale * (a1 * sdz + a2 * (double)n * mean + a3 * (double)n));
-  for (int j = 0; j < 25; ++j) {
-    double h = (double)b1[c] * S[j];
-    for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k * 25 + j];
-    const double v = a1 * acc[2 + j] + a2 * h + a3 * S[j];
-    dw1[c * 25 + j] = (float)(scale * v);
+  if (j == 0) {
+    if (dgamma1) dgamma1[c] = (float)(is * sdxh);
+    if (dbeta1) dbeta1[c] = (float)sdz;
+    // db1 = sum dy1 = a1 sdz + a2 sum y1 + a3 n  (sum y1 = n*mean)
+    if (db1) db1[c] = (float)(scale * (a1 * sdz + a2 * (double)n * mean + a3 * (double)n));
   }
+  double h = (double)b1[c] * S[j];
+  for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k * 25 + j];
+  dw1[c * 25 + j] = (float)(scale * (a1 * acc[2 + j] + a2 * h + a3 * S[j]));
 }
 
 }  // namespace tds
@@ -679,11 +666,6 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
   TDS_LAUNCH_CHECK();
 }
 
-void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(x_border_kernel, dim3(82, 8), dim3(256), 0, st, x, strips, B, H, W);
-  TDS_LAUNCH_CHECK();
-}
-
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
                          hipStream_t st) {
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(n), dim3(256), 0, st, in, out, nchunk, inner, ostride, kstride);
@@ -692,12 +674,12 @@ void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int i
 
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
                           float* dgamma, float* dbeta, float* kbuf, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(1), dim3(64), 0, st, partial, C, nchunk, n, gamma, stats, dgamma,
+  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(C), dim3(256), 0, st, partial, C, nchunk, n, gamma, stats, dgamma,
                      dbeta, kbuf, nullptr);
   TDS_LAUNCH_CHECK();
 }
 
-int tds_l1_bwd_rows(int nwg) { return 4 * nwg; }
+int tds_l1_bwd_rows(int nwg) { return nwg; }
 
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
                 double* partial, int nwg, int B, int H, int W, hipStream_t st) {
@@ -711,7 +693,7 @@ void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t*
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st) {
-  hipLaunchKernelGGL(l1_finalize_kernel, dim3(1), dim3(64), 0, st, bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1,
+  hipLaunchKernelGGL(l1_finalize_kernel, dim3(1), dim3(512), 0, st, bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1,
                      dgamma1, dbeta1, scale);
   TDS_LAUNCH_CHECK();
 }

@@ -27,12 +27,51 @@ static int x_autocorr_num_wg(int B, int H, int W) {
   return (int)((threads + 255) / 256);
 }
 
+// Border strips (the Gram's edge corrections, l1_build_gram): for line L in {row 0, 1, H-2,
+// H-1, col 0, 1, W-2, W-1} and d in [-4,4]^2, strip[L][d] = sum over the batch and the line of
+// x(u) x(u+d); d index 81 = the plain line sum.  One workgroup per (d, L), launched on a side
+// stream beside the autocorrelation (fused_l1_forward): its workgroups are latency-bound
+// loops, and as the first 656 workgroups of the autocorrelation's own launch they held its
+// slots (167 us for both against 99 + 35 us serial).
+__device__ void x_border_block(const float* __restrict__ x, double* __restrict__ strips, int B, int H, int W, int di,
+                               int L, double* sh) {
+  const int dy = di / 9 - 4, dx = di % 9 - 4;
+  const bool plain = di == 81;
+  const bool is_row = L < 4;
+  const int fixed = is_row ? (L < 2 ? L : H - 4 + L) : (L < 6 ? L - 4 : W - 8 + L);
+  const int len = is_row ? W : H;
+  double s = 0.0;
+  for (int b = 0; b < B; ++b) {
+    const float* xb = x + (int64_t)b * H * W;
+    for (int i = threadIdx.x; i < len; i += blockDim.x) {
+      const int r = is_row ? fixed : i, c = is_row ? i : fixed;
+      if (r < 0 || r >= H || c < 0 || c >= W) continue;
+      const float u = xb[(int64_t)r * W + c];
+      if (plain) {
+        s += u;
+      } else {
+        const int r2 = r + dy, c2 = c + dx;
+        if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) s += (double)u * xb[(int64_t)r2 * W + c2];
+      }
+    }
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) strips[L * 82 + di] = s;
+}
+
+__global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__ x, double* __restrict__ strips, int B,
+                                                       int H, int W) {
+  __shared__ double sh[8];
+  x_border_block(x, strips, B, H, W, blockIdx.x, blockIdx.y, sh);
+}
+
 __global__ __launch_bounds__(256, 3) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
                                                          int B, int H, int W) {
   __shared__ double red[4][42];
+  const int blk = blockIdx.x;
   const int tid = threadIdx.x;
   const int ncg = W / 4, nband = (H + AC_RB - 1) / AC_RB;
-  const int64_t gt = (int64_t)blockIdx.x * 256 + tid;
+  const int64_t gt = (int64_t)blk * 256 + tid;
   float acc[42];
 #pragma unroll
   for (int i = 0; i < 42; ++i) acc[i] = 0.f;
@@ -93,7 +132,7 @@ __global__ __launch_bounds__(256, 3) void x_autocorr_kernel(const float* __restr
     if (lane == 0) red[wv][i] = s;
   }
   __syncthreads();
-  if (tid < 42) partial[(int64_t)blockIdx.x * 42 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+  if (tid < 42) partial[(int64_t)blk * 42 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
 }  // namespace tds
@@ -102,12 +141,16 @@ using namespace tds;
 
 int tds_x_autocorr_num_wg(int B, int H, int W) { return x_autocorr_num_wg(B, H, W); }
 
-void tds_x_autocorr(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
+void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st) {
+  hipLaunchKernelGGL(x_border_kernel, dim3(82, 8), dim3(256), 0, st, x, strips, B, H, W);
+  TDS_LAUNCH_CHECK();
+}
+
+void tds_x_autocorr(const float* x, double* ac_partial, int nwg, int B, int H, int W, hipStream_t st) {
   if (nwg < 1 || nwg != x_autocorr_num_wg(B, H, W)) {  // the partial buffer is sized by tds_x_autocorr_num_wg
     tds_launch_fail("x_autocorr: workgroup count does not match the shape (needs W % 4 == 0)");
     return;
   }
   hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
   TDS_LAUNCH_CHECK();
-  tds_x_border(x, strips, B, H, W, st);
 }
