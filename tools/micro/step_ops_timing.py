@@ -95,6 +95,14 @@ def main():
                 continue
             res[name] = round(timeit(fn, a.iters), 4)
             print(f"{name:11s} {res[name]:.4f} ms", flush=True)
+        if os.environ.get("TDS_CONV2_DIAG") == "13":  # per-role barrier-wait fractions (diag build)
+            c2b()
+            torch.cuda.synchronize()
+            clk = ops.conv2_bwd_clock_dump(ops.device_cus()).to(torch.int64) & 0xFFFFFFFF
+            for name, sl in (("dgrad", slice(0, 2)), ("wgrad", slice(2, 4)), ("staging", slice(4, 8))):
+                w, t = clk[:, sl, 0].sum().item(), clk[:, sl, 1].sum().item()
+                print(f"clock {name:8s} waits {w / max(t, 1):.3f} of its run "
+                      f"(mean run {clk[:, sl, 1].float().mean().item():.0f} cycles)", flush=True)
         print(json.dumps({"variant": os.environ.get("TDS_SO_VARIANT", ""), "ms": res,
                           "sum_ms": round(sum(res.values()), 4)}), flush=True)
 

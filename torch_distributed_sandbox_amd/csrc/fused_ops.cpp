@@ -281,6 +281,15 @@ Tensor conv2_bwd_walk_table(int64_t B, int64_t tiles_r, int64_t tiles_c, int64_t
   return t;
 }
 
+// Per-wave barrier-wait clocks of the last conv2 backward launch of a TDS_CONV2_DIAG=13 diag
+// build ([nwg][8][wait, total] shader-clock cycles; zeros in production builds).
+Tensor conv2_bwd_clock_dump(int64_t nwg) {
+  auto t = at::zeros({nwg, 8, 2}, at::TensorOptions().dtype(at::kInt));
+  const int n = tds_conv2_bwd_clock_read(reinterpret_cast<uint32_t*>(t.data_ptr<int>()), (int)(nwg * 16));
+  TORCH_CHECK(n >= 0, "conv2_bwd_clock_dump: hipMemcpyFromSymbol failed");
+  return t;
+}
+
 int64_t head_bwd_workspace(int64_t B, int64_t P) {
   const int Q = (int)(P / 2);
   return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_pb_nblk(Q) * 2;
@@ -481,6 +490,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
+  m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);
   m.def("conv2_bwd_walk_table(int B, int tiles_r, int tiles_c, int nwg, int seg) -> Tensor", &conv2_bwd_walk_table);
   m.def(
       "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale, "

@@ -259,6 +259,39 @@ __device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2],
 
 __device__ __forceinline__ void br_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// DIAG 13 (timing-only build): shader-clock cycles each wave spends waiting at the per-tile
+// barriers vs its whole run, stored per wave in g_br_clk[wg][wave][wait, total] (read back by
+// tds_conv2_bwd_clock_read): which role waits for which.  (printf here made the kernel 10^4x
+// slower.)
+constexpr int kBRClkMaxWg = 1024;
+__device__ uint32_t g_br_clk[kBRClkMaxWg * 8 * 2];
+template <int DIAG>
+struct BRClock {
+  uint64_t wait = 0, t0 = 0;
+  __device__ __forceinline__ void start() {
+    if constexpr (DIAG == 13) t0 = __builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void barrier() {
+    if constexpr (DIAG == 13) {
+      const uint64_t a = __builtin_amdgcn_s_memtime();
+      br_barrier();
+      wait += __builtin_amdgcn_s_memtime() - a;
+    } else {
+      br_barrier();
+    }
+  }
+  __device__ __forceinline__ void report() {
+    if constexpr (DIAG == 13) {
+      const uint64_t tot = __builtin_amdgcn_s_memtime() - t0;
+      const int i = ((int)blockIdx.x * 8 + (int)(threadIdx.x >> 6)) * 2;
+      if ((threadIdx.x & 63) == 0 && blockIdx.x < kBRClkMaxWg) {
+        g_br_clk[i] = (uint32_t)wait;
+        g_br_clk[i + 1] = (uint32_t)tot;
+      }
+    }
+  }
+};
+
 __device__ __forceinline__ BRRows br_rows(char* smem, int k) {
   const int s = __builtin_amdgcn_readfirstlane(k % 3);
   return BRRows{smem + BR_OFF_D + s * BR_SLOT * BR_DROW, smem + BR_OFF_P + s * BR_SLOT * BR_PROW};
@@ -287,11 +320,13 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
   const int hp = (g >> 1) * BR_DPL + (g & 1) * 16;
   const int lp = (2 + (g >> 1)) * BR_DPL + (g & 1) * 16;
   BRTile prev{0, 0, 0, false, true};
+  BRClock<DIAG> clk;
+  clk.start();
   int kk = 0;
   for (;; ++kk) {
     const BRTile cur = br_decode(a.walk, kk, a.nwg, a.w);
     if (cur.end) break;
-    br_barrier();  // tile kk staged; the partner's exchange slot of tile kk-1 is written
+    clk.barrier();  // tile kk staged; the partner's exchange slot of tile kk-1 is written
     const BRRows rw = br_rows(smem, kk);
     if constexpr (ROLE < 2) {
       if (!prev.end)
@@ -304,7 +339,8 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
     }
     prev = cur;
   }
-  br_barrier();  // the last exchange slot is written
+  clk.barrier();  // the last exchange slot is written
+  clk.report();
   if constexpr (ROLE < 2) {
     if (!prev.end)
       br_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + BR_OFF_X + ((kk - 1) & 1) * BR_XCHG), acc, a.dp1,
@@ -569,6 +605,8 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   // Loads are unconditional (past the end: the list's last tile again, never staged): a load
   // under a branch makes the wait for the OLDER set drain the younger one too (vmcnt(0)).
   BRStager<8, WV, BIG, DIAG> st0, st1;
+  BRClock<DIAG> clk;
+  clk.start();
   auto tile = [&](int j) { return br_decode(a.walk, j, a.nwg, a.w); };
   auto ld = [&](BRStager<8, WV, BIG, DIAG>& s, int j) {
     const BRTile x = tile(j);
@@ -588,7 +626,7 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   ld(st0, 2);
   // iteration kk stages tile kk+1 and loads tile kk+3 (both in set (kk+1) & 1)
   for (int kk = 0; !tile(kk).end; kk += 2) {
-    br_barrier();  // consumers start tile kk
+    clk.barrier();  // consumers start tile kk
     {
       const BRTile x = tile(kk + 1);
       if (!x.end) {
@@ -598,7 +636,7 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
     }
     ld(st1, kk + 3);
     if (tile(kk + 1).end) break;
-    br_barrier();  // consumers start tile kk + 1
+    clk.barrier();  // consumers start tile kk + 1
     {
       const BRTile x = tile(kk + 2);
       if (!x.end) {
@@ -608,7 +646,8 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
     }
     ld(st0, kk + 4);
   }
-  br_barrier();
+  clk.barrier();
+  clk.report();
 }
 
 template <int DIAG, bool BIG>
@@ -644,6 +683,12 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
 using namespace tds;
 
 int tds_conv2_bwd3_num_wg() { return tds_conv2_num_wg(); }  // one 8-wave workgroup per CU
+
+// DIAG 13 clocks of the last launch: n uint32 (2 per wave, 8 waves per workgroup)
+int tds_conv2_bwd_clock_read(uint32_t* host, int n) {
+  if (n > kBRClkMaxWg * 16) n = kBRClkMaxWg * 16;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_br_clk), (size_t)n * 4, 0, hipMemcpyDeviceToHost) == hipSuccess ? n : -1;
+}
 
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c) {
   *tiles_r = (P + BR_TH - 1) / BR_TH;
@@ -724,7 +769,7 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
 
 #ifdef TDS_DIAG
 // timing-only variants: 1 no MFMAs, 3 no global tile loads, 5 no staging, 7 no y2 loads, 9 no
-// BN2 / pool backward math in the staging.  Compiled only into a -DTDS_DIAG build
+// BN2 / pool backward math in the staging, 13 the full kernel with per-wave barrier-wait clocks.  Compiled only into a -DTDS_DIAG build
 // (python -m torch_distributed_sandbox_amd._build --variant diag -D TDS_DIAG; TDS_CONV2_DIAG=N).
 static int br_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
@@ -763,6 +808,7 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
     case 5: TDS_BR_LAUNCH(5) break;
     case 7: TDS_BR_LAUNCH(7) break;
     case 9: TDS_BR_LAUNCH(9) break;
+    case 13: TDS_BR_LAUNCH(13) break;
 #endif
     default: TDS_BR_LAUNCH(0) break;
   }
