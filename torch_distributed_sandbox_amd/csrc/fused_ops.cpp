@@ -98,7 +98,10 @@ const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int n
 const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg) {
   static std::mutex mu;
   static auto* cache = new std::map<std::tuple<int, int, int, int, int>, Tensor>();
-  constexpr int kSeg = 24;  // tiles per vertical segment (a segment start re-stages 4 rows)
+#ifndef TDS_BWD_SEG
+#define TDS_BWD_SEG 48  // A/B (r2_seg.sh): 24 / 48 / 96 / 200 tiles = 1.551 / 1.534 / 1.546 / 1.584 ms
+#endif
+  constexpr int kSeg = TDS_BWD_SEG;  // tiles per vertical segment (a segment start re-stages 4 rows)
   const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c, nwg);
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache->find(key);

@@ -14,7 +14,7 @@
 //               k1*dz + k2*y2 + k3 at the window's argmax) -> dy2 and p1 bf16 hi|lo rows in LDS.
 //
 // ROLLING WINDOW.  A tile of 8 output rows needs dy2 and p1 on 12 rows (2-row halo above and
-// below).  Each workgroup walks vertical SEGMENTS of tiles (one tile column of one image, ~24
+// below).  Each workgroup walks vertical SEGMENTS of tiles (one tile column of one image, ~48
 // tiles top to bottom, host table tds_conv2_bwd_walk): consecutive tiles share 4 of those 12
 // rows, so the staging waves load, recompute and store only the 8 NEW rows of each tile; its
 // last 4 rows are stored twice, the second time as the TOP rows of the next tile's slot, so
@@ -595,7 +595,7 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
                            ptop(j + 1));
   };
   // a segment's first tile: its 4 top rows (image rows r0-2 .. r0+1) staged synchronously
-  // straight into its slot's top (once per ~24 tiles)
+  // straight into its slot's top (once per ~48 tiles)
   auto prologue = [&](int j, const BRTile& x) {
     BRStager<4, WV, BIG, DIAG> pro;
     pro.load(a, x.b, x.r0 - 2, x.c0, tid);
