@@ -90,8 +90,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tds_buffer_rsrc(const void* ba
   const uint64_t v = reinterpret_cast<uint64_t>(base);
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  // every field wave-uniform (readfirstlane): a descriptor the compiler cannot prove uniform
+  // gets a waterfall loop around each buffer instruction
   return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | (uint64_t)lo), (short)0,
-                                           (int)bytes, 0x00020000);
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
 // The head backward's pooled gradient g2m is PLANAR, [B][32][Q][Q] (the fc flatten order):
