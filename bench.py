@@ -67,6 +67,10 @@ def _parser():
                     help="cpu: rehearsal of the launch/exchange path on the torch-ops plan (small --image-size)")
     ap.add_argument("--shared-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (needs --backend gloo); recorded in the JSON")
+    ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
+                    help="upsample the next batch on a side stream during the current step (off by default: "
+                         "it runs beside the memory-bound layer-1 kernels and slowed them; A/B 1256/1284 img/s "
+                         "with vs 1257/1304 without, tools/gpu_sessions/r2_border.sh)")
     ap.add_argument("--allreduce-probe", action=argparse.BooleanOptionalAction, default=True,
                     help="world > 1: after the timed steps, time a few all-reduces over the same communicator "
                          "and report their bus bandwidth in config.allreduce_probe (outside the timed region)")
@@ -216,7 +220,7 @@ def run(argv) -> None:
     # input pipeline: batch i+1 is upsampled on a side stream while step i computes (the role
     # of the reference's DataLoader prefetch); the step waits on that stream, and the batch is
     # recorded on the compute stream so the caching allocator cannot recycle it early
-    data_stream = torch.cuda.Stream(device) if on_gpu else None
+    data_stream = torch.cuda.Stream(device) if on_gpu and args.prefetch else None
 
     def produce(i):
         j = i % pool
@@ -234,7 +238,8 @@ def run(argv) -> None:
         if data_stream is not None:
             torch.cuda.current_stream(device).wait_stream(data_stream)
             images.record_stream(torch.cuda.current_stream(device))
-        pending[i + 1] = produce(i + 1)
+        if data_stream is not None:
+            pending[i + 1] = produce(i + 1)
         out = ddp(images)
         loss = criterion(out, lab_pool[j])
         optimizer.zero_grad()

@@ -55,23 +55,6 @@ Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shap
 
 int l1_wg() { return tds_fused_num_wg(4); }
 
-// Fork / join events of one device (timing disabled), created once and never destroyed.
-struct ForkJoin {
-  hipEvent_t fork, join;
-};
-const ForkJoin& fork_join(int dev) {
-  static std::mutex mu;
-  static auto* cache = new std::map<int, ForkJoin>();
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = cache->find(dev);
-  if (it != cache->end()) return it->second;
-  ForkJoin fj{};
-  TORCH_CHECK(hipEventCreateWithFlags(&fj.fork, hipEventDisableTiming) == hipSuccess &&
-                  hipEventCreateWithFlags(&fj.join, hipEventDisableTiming) == hipSuccess,
-              "tdsa fused: hipEventCreateWithFlags failed");
-  return (*cache)[dev] = fj;
-}
-
 // Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
 // torch caching allocator, built once.  The map is never destroyed (no frees at process exit).
 const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg) {
@@ -150,19 +133,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   TORCH_CHECK(nac > 0, "fused_l1_forward: W % 4 == 0 required (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo.dtype(at::kDouble));
   auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
-  // border strips on a side stream beside the autocorrelation (fork / join by events; both
-  // buffers come from st's pool and st waits for the join before anything reads them)
-  const int dev = (int)x.get_device();
-  hipStream_t side = c10::hip::getStreamFromPool(false, dev).stream();
-  const ForkJoin& fj = fork_join(dev);
-  TORCH_CHECK(hipEventRecord(fj.fork, st) == hipSuccess && hipStreamWaitEvent(side, fj.fork, 0) == hipSuccess,
-              "fused_l1_forward: stream fork");
-  tds_x_border(x.data_ptr<float>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, side);
-  TORCH_CHECK(hipEventRecord(fj.join, side) == hipSuccess, "fused_l1_forward: stream join");
   tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, (int)B, (int)H, (int)W, st);
+  // (on a side stream beside the autocorrelation the two kernels slowed each other: 176 + 94
+  // us overlapped vs 99 + 35 us serial)
+  tds_x_border(x.data_ptr<float>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, st);
   auto asum = at::empty({42}, fo.dtype(at::kDouble));
   tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
-  TORCH_CHECK(hipStreamWaitEvent(st, fj.join, 0) == hipSuccess, "fused_l1_forward: stream join");
   auto gram = at::empty({650}, fo.dtype(at::kDouble));
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
   tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W,

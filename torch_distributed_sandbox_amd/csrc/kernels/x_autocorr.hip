@@ -29,10 +29,12 @@ static int x_autocorr_num_wg(int B, int H, int W) {
 
 // Border strips (the Gram's edge corrections, l1_build_gram): for line L in {row 0, 1, H-2,
 // H-1, col 0, 1, W-2, W-1} and d in [-4,4]^2, strip[L][d] = sum over the batch and the line of
-// x(u) x(u+d); d index 81 = the plain line sum.  One workgroup per (d, L), launched on a side
-// stream beside the autocorrelation (fused_l1_forward): its workgroups are latency-bound
-// loops, and as the first 656 workgroups of the autocorrelation's own launch they held its
-// slots (167 us for both against 99 + 35 us serial).
+// x(u) x(u+d); d index 81 = the plain line sum.  One workgroup per (d, L), launched after the
+// autocorrelation.  Measured alternatives, all slower: the border workgroups as the first 656
+// of the autocorrelation's own launch (they held its slots: 167 us for both vs 99 + 35 us),
+// the two kernels on separate streams (176 + 94 us overlapped), and workgroups per (line, dy,
+// line chunk) with the 9 dx products per pixel and chunk partials folded in l1_gram (45 us
+// here + 11 us more in l1_gram).
 __device__ void x_border_block(const float* __restrict__ x, double* __restrict__ strips, int B, int H, int W, int di,
                                int L, double* sh) {
   const int dy = di / 9 - 4, dx = di % 9 - 4;
