@@ -141,12 +141,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
   auto gram = at::empty({650}, fo.dtype(at::kDouble));
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
-  tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W,
-              w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), st);
   auto stats = at::empty({32}, fo);
   auto aff = at::empty({32}, fo);
-  tds_bn_finalize_shifted(sums.data_ptr<double>(), 16, 1, B * H * W, b1.data_ptr<float>(), (float)eps,
-                          (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+  tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W,
+              w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps,
+              (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1, argmax
   auto p1 = at::empty({B, P, P, 16}, fo);  // carrier of bf16 [B,P,P,32]
   auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
@@ -227,12 +226,10 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
   }
   c10::DeviceGuard guard(ya.device());
   hipStream_t st = stream_of(ya);
-  auto sums2 = at::empty({64}, ya.options().dtype(at::kDouble));
-  tds_reduce_partials(partial2.data_ptr<double>(), sums2.data_ptr<double>(), 64, nch, 2, (int64_t)nch * 2, 2, st);
   auto stats = at::empty({64}, ya.options());
   auto aff = at::empty({64}, ya.options());
-  tds_bn_finalize_shifted(sums2.data_ptr<double>(), 32, 1, B * P * P, b2.data_ptr<float>(), (float)eps,
-                          (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+  tds_bn_reduce_finalize(partial2.data_ptr<double>(), 32, nch, B * P * P, b2.data_ptr<float>(), (float)eps,
+                         (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   const int nblk = 32 * tds_head_pb_nblk((int)Q);
   auto part = at::empty({(int64_t)nblk * B * NC}, ya.options().dtype(at::kDouble));
   auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
@@ -344,11 +341,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
   auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");
   auto kbuf = at::empty({96}, ya.options());
-  tds_bn_bwd_finalize2(partial.data_ptr<double>(), 32, npass * nblk, B * P * P, g, stats2.data_ptr<float>(),
-                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), st);
   auto dbfc = sink_or_empty(dbfc_out, {NC}, ya, "dbfc_out");
-  at::sum_out(dbfc, dlogits, {0});
-  if (scale != 1.0) dbfc.mul_(scale);
+  tds_bn_bwd_finalize2(partial.data_ptr<double>(), 32, npass * nblk, B * P * P, g, stats2.data_ptr<float>(),
+                       dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), dlogits.data_ptr<float>(),
+                       (int)B, (int)NC, dbfc.data_ptr<float>(), (float)scale, st);
   check_launches("fused_head_backward");
   return {dW, dbfc, dgamma, dbeta, g2m, kbuf};
 }

@@ -219,21 +219,12 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
   }
 }
 
-// Shifted BN finalize: statistics were accumulated on (y - shift[c]).
-__global__ void bn_finalize_shifted_kernel(const double* __restrict__ partial, int C, int nchunk, int64_t n,
-                                           const float* __restrict__ shift, float eps, float momentum,
-                                           const float* __restrict__ gamma, const float* __restrict__ beta,
-                                           float* __restrict__ stats /* mean[C], invstd[C] */,
-                                           float* __restrict__ running_mean, float* __restrict__ running_var,
-                                           int64_t* __restrict__ num_batches, float* __restrict__ aff /* a[C], b[C] */) {
-  const int c = threadIdx.x;
-  if (c == 0 && num_batches) num_batches[0] += 1;
-  if (c >= C) return;
-  double s = 0.0, ss = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    s += partial[((int64_t)c * nchunk + k) * 2];
-    ss += partial[((int64_t)c * nchunk + k) * 2 + 1];
-  }
+// Shifted BN finalize of channel c from its sums of (y - shift[c]) and (y - shift[c])^2.
+__device__ void bn_finalize_channel(int c, int C, double s, double ss, int64_t n, const float* __restrict__ shift,
+                                    float eps, float momentum, const float* __restrict__ gamma,
+                                    const float* __restrict__ beta, float* __restrict__ stats,
+                                    float* __restrict__ running_mean, float* __restrict__ running_var,
+                                    float* __restrict__ aff) {
   const double m0 = s / (double)n;
   double var = ss / (double)n - m0 * m0;
   if (var < 0.0) var = 0.0;
@@ -249,6 +240,45 @@ __global__ void bn_finalize_shifted_kernel(const double* __restrict__ partial, i
   const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
   aff[c] = gm * invstd;
   aff[C + c] = bt - (float)mean * gm * invstd;
+}
+
+// BN2: reduce the per-workgroup partials of channel c (partial[c][nchunk][2], fixed order) and
+// finalize it -- one workgroup per channel, one launch instead of a reduction + a finalize.
+__global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(
+    const double* __restrict__ partial, int C, int nchunk, int64_t n, const float* __restrict__ shift, float eps,
+    float momentum, const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ stats,
+    float* __restrict__ running_mean, float* __restrict__ running_var, int64_t* __restrict__ num_batches,
+    float* __restrict__ aff) {
+  __shared__ double sh[8];
+  const int c = blockIdx.x;
+  double s = 0.0, ss = 0.0;
+  for (int k = threadIdx.x; k < nchunk; k += blockDim.x) {
+    s += partial[((int64_t)c * nchunk + k) * 2];
+    ss += partial[((int64_t)c * nchunk + k) * 2 + 1];
+  }
+  s = block_sum(s, sh);
+  ss = block_sum(ss, sh);
+  if (threadIdx.x != 0) return;
+  if (c == 0 && num_batches) num_batches[0] += 1;
+  bn_finalize_channel(c, C, s, ss, n, shift, eps, momentum, gamma, beta, stats, running_mean, running_var, aff);
+}
+
+// Shifted BN finalize: statistics were accumulated on (y - shift[c]).
+__global__ void bn_finalize_shifted_kernel(const double* __restrict__ partial, int C, int nchunk, int64_t n,
+                                           const float* __restrict__ shift, float eps, float momentum,
+                                           const float* __restrict__ gamma, const float* __restrict__ beta,
+                                           float* __restrict__ stats /* mean[C], invstd[C] */,
+                                           float* __restrict__ running_mean, float* __restrict__ running_var,
+                                           int64_t* __restrict__ num_batches, float* __restrict__ aff /* a[C], b[C] */) {
+  const int c = threadIdx.x;
+  if (c == 0 && num_batches) num_batches[0] += 1;
+  if (c >= C) return;
+  double s = 0.0, ss = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    s += partial[((int64_t)c * nchunk + k) * 2];
+    ss += partial[((int64_t)c * nchunk + k) * 2 + 1];
+  }
+  bn_finalize_channel(c, C, s, ss, n, shift, eps, momentum, gamma, beta, stats, running_mean, running_var, aff);
 }
 
 // head kernels: see head_fused.hip
@@ -270,13 +300,24 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
 //   dy = k1*dz + k2*y + k3,  k1 = g*is, k2 = -g*is^3*(sdzy - mean*sdz)/n, k3 = -g*is*sdz/n - k2*mean
 // One workgroup per channel (the head backward leaves ~10^3 partials per channel: a serial
 // loop per channel took 21 us).
+// Block C (the last) also forms the fc bias gradient dbfc[j] = scale * sum_b dl[b][j].
 __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __restrict__ partial, int C, int nchunk,
                                                                int64_t n, const float* __restrict__ gamma,
                                                                const float* __restrict__ stats,
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                               float* __restrict__ kbuf, double* __restrict__ sums_out) {
+                                                               float* __restrict__ kbuf, double* __restrict__ sums_out,
+                                                               const float* __restrict__ dl, int B, int NC,
+                                                               float* __restrict__ dbfc, float scale) {
   __shared__ double sh[8];
   const int c = blockIdx.x;
+  if (c == C) {
+    if (dbfc && (int)threadIdx.x < NC) {
+      float v = 0.f;
+      for (int b = 0; b < B; ++b) v += dl[b * NC + threadIdx.x];
+      dbfc[threadIdx.x] = v * scale;
+    }
+    return;
+  }
   double sdz = 0.0, sdzy = 0.0;
   for (int k = threadIdx.x; k < nchunk; k += blockDim.x) {
     const double2 v = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nchunk + k) * 2);
@@ -576,7 +617,12 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
 __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__ ac_sum,
                                                       const double* __restrict__ strips, const float* __restrict__ x,
                                                       int B, int H, int W, const float* __restrict__ w1,
-                                                      double* __restrict__ gram, double* __restrict__ sums) {
+                                                      double* __restrict__ gram, double* __restrict__ sums,
+                                                      const float* __restrict__ b1, float eps, float momentum,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      float* __restrict__ stats, float* __restrict__ running_mean,
+                                                      float* __restrict__ running_var, int64_t* __restrict__ num_batches,
+                                                      float* __restrict__ aff) {
   __shared__ double full[81];
   __shared__ double G[25][25];
   __shared__ double S[25];
@@ -599,6 +645,10 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
     }
     sums[tid * 2] = s;
     sums[tid * 2 + 1] = q;
+    // BN1 statistics of (y1 - b1) finalized here (no separate finalize launch)
+    if (tid == 0 && num_batches) num_batches[0] += 1;
+    bn_finalize_channel(tid, 16, s, q, (int64_t)B * H * W, b1, eps, momentum, gamma, beta, stats, running_mean,
+                        running_var, aff);
   }
 }
 
@@ -646,8 +696,11 @@ using namespace tds;
 int tds_fused_num_wg(int per_cu) { return tds_device_cus() * per_cu; }
 
 void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
-                 double* gram, double* sums, hipStream_t st) {
-  hipLaunchKernelGGL(l1_gram_kernel, dim3(1), dim3(256), 0, st, ac_sum, strips, x, B, H, W, w1, gram, sums);
+                 double* gram, double* sums, const float* b1, float eps, float momentum, const float* gamma,
+                 const float* beta, float* stats, float* running_mean, float* running_var, int64_t* num_batches,
+                 float* aff, hipStream_t st) {
+  hipLaunchKernelGGL(l1_gram_kernel, dim3(1), dim3(256), 0, st, ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps,
+                     momentum, gamma, beta, stats, running_mean, running_var, num_batches, aff);
   TDS_LAUNCH_CHECK();
 }
 
@@ -666,6 +719,14 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
   TDS_LAUNCH_CHECK();
 }
 
+void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
+                            float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
+                            float* running_var, int64_t* num_batches, float* aff, hipStream_t st) {
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(C), dim3(256), 0, st, partial, C, nchunk, n, shift, eps, momentum,
+                     gamma, beta, stats, running_mean, running_var, num_batches, aff);
+  TDS_LAUNCH_CHECK();
+}
+
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
                          hipStream_t st) {
   hipLaunchKernelGGL(reduce_partials_kernel, dim3(n), dim3(256), 0, st, in, out, nchunk, inner, ostride, kstride);
@@ -673,9 +734,14 @@ void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int i
 }
 
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
-                          float* dgamma, float* dbeta, float* kbuf, hipStream_t st) {
-  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(C), dim3(256), 0, st, partial, C, nchunk, n, gamma, stats, dgamma,
-                     dbeta, kbuf, nullptr);
+                          float* dgamma, float* dbeta, float* kbuf, const float* dl, int B, int NC, float* dbfc,
+                          float scale, hipStream_t st) {
+  if (dbfc && (NC < 1 || NC > 256)) {
+    tds_launch_fail("bn_bwd_finalize2: the fc bias gradient needs 1 <= classes <= 256");
+    return;
+  }
+  hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(C + 1), dim3(256), 0, st, partial, C, nchunk, n, gamma, stats, dgamma,
+                     dbeta, kbuf, nullptr, dl, B, NC, dbfc, scale);
   TDS_LAUNCH_CHECK();
 }
 

@@ -244,11 +244,20 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
   }
 }
 
-// logits[i] = sums[i] + bias[i % NC]
-__global__ void head_logits_kernel(const double* __restrict__ sums, const float* __restrict__ bias,
-                                   float* __restrict__ logits, int BN, int NC) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < BN) logits[i] = (float)sums[i] + (bias ? bias[i % NC] : 0.f);
+// sums[i] = sum_k partial[k][i] (fixed order), logits[i] = sums[i] + bias[i % NC]: one workgroup
+// per logit, the cross-workgroup reduction and the bias in one launch
+__global__ __launch_bounds__(256) void head_logits_kernel(const double* __restrict__ partial, int nwg,
+                                                          double* __restrict__ sums, const float* __restrict__ bias,
+                                                          float* __restrict__ logits, int BN, int NC) {
+  __shared__ double sh[8];
+  const int i = blockIdx.x;
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nwg; k += blockDim.x) s += partial[(int64_t)k * BN + i];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    sums[i] = s;
+    logits[i] = (float)s + (bias ? bias[i % NC] : 0.f);
+  }
 }
 
 // Backward for images b0 .. b0+NB-1.
@@ -391,8 +400,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 #undef TDS_HPF
   }
   const int BN = B * NC;
-  tds_reduce_partials(partial, sums, BN, nwg, BN, 0, BN, st);
-  hipLaunchKernelGGL(head_logits_kernel, dim3((BN + 63) / 64), dim3(64), 0, st, sums, bias, logits, BN, NC);
+  hipLaunchKernelGGL(head_logits_kernel, dim3(BN), dim3(256), 0, st, partial, nwg, sums, bias, logits, BN, NC);
   TDS_LAUNCH_CHECK();
   return 0;
 }

@@ -88,7 +88,9 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
 // ---- convnet_fused.hip
 int tds_fused_num_wg(int per_cu);
 void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
-                 double* gram, double* sums, hipStream_t st);
+                 double* gram, double* sums, const float* b1, float eps, float momentum, const float* gamma,
+                 const float* beta, float* stats, float* running_mean, float* running_var, int64_t* num_batches,
+                 float* aff, hipStream_t st);  // Gram + patch sums + the BN1 finalize
 void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
                   int B, int H, int W, hipStream_t st);
 void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
@@ -101,7 +103,12 @@ void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
                          hipStream_t st);
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
-                          float* dgamma, float* dbeta, float* kbuf, hipStream_t st);
+                          float* dgamma, float* dbeta, float* kbuf, const float* dl, int B, int NC, float* dbfc,
+                          float scale, hipStream_t st);  // + dbfc = scale * sum_b dl (when dbfc)
+// BN statistics from per-workgroup partials [C][nchunk][2] reduced and finalized in one launch
+void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
+                            float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
+                            float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
 void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
                 double* partial, int nwg, int B, int H, int W, hipStream_t st);
