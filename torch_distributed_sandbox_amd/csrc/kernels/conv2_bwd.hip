@@ -40,6 +40,13 @@
 #include "launchers.h"
 #include "pooled_layout.h"
 
+#ifndef TDS_BR_LOAD_PRIO
+#define TDS_BR_LOAD_PRIO 3  // wave priority while a staging wave issues its look-ahead loads
+#endif
+#ifndef TDS_BR_MFMA_PRIO
+#define TDS_BR_MFMA_PRIO 1  // wave priority of the dgrad / wgrad waves
+#endif
+
 namespace tds {
 
 constexpr int BR_TH = 8, BR_TC = 16;       // output tile
@@ -299,9 +306,7 @@ __device__ __forceinline__ BRRows br_rows(char* smem, int k) {
 
 template <int ROLE, int DIAG>  // ROLE 0/1 = dgrad wave D, 2/3 = wgrad
 __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict__ wdpack, char* smem) {
-#ifdef TDS_BR_MFMA_PRIO
-  __builtin_amdgcn_s_setprio(TDS_BR_MFMA_PRIO);
-#endif
+  __builtin_amdgcn_s_setprio(TDS_BR_MFMA_PRIO);  // above the staging waves' VALU work
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   f32x4 R[13][2];
@@ -580,9 +585,6 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
     br_barrier();
     return;
   }
-#ifdef TDS_BR_STAGE_PRIO
-  __builtin_amdgcn_s_setprio(TDS_BR_STAGE_PRIO);
-#endif
   const int tid = threadIdx.x - 256;
   const float* kc = reinterpret_cast<const float*>(smem + BR_OFF_K);
   // slot j % 3: rows 0-3 (top) at dtop / ptop, the tile's 8 new rows at +4
@@ -610,7 +612,12 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   auto tile = [&](int j) { return br_decode(a.walk, j, a.nwg, a.w); };
   auto ld = [&](BRStager<8, WV, BIG, DIAG>& s, int j) {
     const BRTile x = tile(j);
+    // the look-ahead loads issue at raised priority (the SIMD's MFMA wave otherwise delays
+    // them), the BN2-backward VALU work at the lowest (tools/gpu_sessions/r2_knobs.sh: 1.519 /
+    // 1.501 ms vs 1.522-1.567 ms in six runs of the same kernel without priorities)
+    __builtin_amdgcn_s_setprio(TDS_BR_LOAD_PRIO);
     s.load(a, x.b, x.r0 + 2, x.c0, tid);
+    __builtin_amdgcn_s_setprio(0);
   };
   // (a prologue runs after the set that stages the same tile is stored and before that set is
   // reloaded, so its registers are the set's)
