@@ -57,10 +57,13 @@ def _parser():
                     help="fc gradient path under DDP (parallel/factored.py); auto picks by the xGMI byte model")
     ap.add_argument("--allreduce-chunks", type=int, default=None,
                     help="K-chunks of the fc weight gradient in the all-reduce regime (default 4 on GPU)")
-    ap.add_argument("--reserve-cus", type=int, default=0,
-                    help="keep N CUs out of the compute (CU-masked stream) for RCCL's kernels (utils/streams.py)")
+    ap.add_argument("--reserve-cus", type=int, default=None,
+                    help="keep N CUs (a multiple of 32) out of the compute stream and confine the native "
+                         "communicator's stream to them (utils/streams.py); default 32 at world > 1 on "
+                         "rccl-native, else 0")
     ap.add_argument("--rccl-max-ctas", type=int, default=0,
-                    help="bound RCCL's workgroups per collective (ncclConfig maxCTAs; TDS_RCCL_MAX_CTAS)")
+                    help="bound RCCL's workgroups per collective (ncclConfig maxCTAs; TDS_RCCL_MAX_CTAS); "
+                         "default: the reserved CU count on rccl-native")
     ap.add_argument("--overlap-optimizer", action=argparse.BooleanOptionalAction, default=True,
                     help="finish the fc bucket (collective + SGD) on a side stream under the next forward's convs")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
@@ -68,12 +71,16 @@ def _parser():
     ap.add_argument("--shared-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (needs --backend gloo); recorded in the JSON")
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
-                    help="upsample the next batch on a side stream during the current step (off by default: "
-                         "it runs beside the memory-bound layer-1 kernels and slowed them; A/B 1256/1284 img/s "
-                         "with vs 1257/1304 without, tools/gpu_sessions/r2_border.sh)")
+                    help="produce the next batch (upsample + BN1 input moments) on a side stream beside the "
+                         "current step's conv2 backward")
     ap.add_argument("--allreduce-probe", action=argparse.BooleanOptionalAction, default=True,
                     help="world > 1: after the timed steps, time a few all-reduces over the same communicator "
                          "and report their bus bandwidth in config.allreduce_probe (outside the timed region)")
+    ap.add_argument("--sim-comm-us", type=int, default=0,
+                    help="1-GPU rehearsal of a collective's CU footprint: after each forward, hold "
+                         "--sim-comm-ctas workgroups of RCCL's size (256 threads, 19.7 KB LDS) for this many "
+                         "microseconds on a side stream (recorded in the JSON; not a training number)")
+    ap.add_argument("--sim-comm-ctas", type=int, default=16)
     ap.add_argument("--spawn-timeout", type=float, default=1800.0,
                     help="self-spawn: terminate all ranks if the job runs longer than this (s)")
     return ap
@@ -174,8 +181,21 @@ def run(argv) -> None:
         device = torch.device("cuda", local_rank)
     else:
         device = torch.device("cpu")
-    if args.rccl_max_ctas > 0:
-        os.environ["TDS_RCCL_MAX_CTAS"] = str(args.rccl_max_ctas)
+    # CU split for overlapped collectives (utils/streams.py, docs/DISTRIBUTED.md): by default at
+    # world > 1 on the native communicator, 32 CUs (4 per XCD, one per shader engine) are kept
+    # out of the compute and RCCL's kernels are confined to them with at most as many CTAs.
+    # Set before the process group, whose communicator stream takes the complement mask.
+    reserve = args.reserve_cus
+    if reserve is None:
+        reserve = 32 if on_gpu and world > 1 and backend == "rccl-native" else 0
+    rccl_max_ctas = args.rccl_max_ctas or (reserve if backend == "rccl-native" else 0)
+    if rccl_max_ctas > 0:
+        os.environ["TDS_RCCL_MAX_CTAS"] = str(rccl_max_ctas)
+    if on_gpu and reserve > 0:
+        # CU-masked compute stream, current for everything below (utils/streams.py)
+        from torch_distributed_sandbox_amd.utils.streams import reserve_cus_for_comm
+
+        torch.cuda.set_stream(reserve_cus_for_comm(reserve, device))
     if world > 1 or args.grad_exchange in ("activations", "sharded", "chunked"):
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -194,11 +214,6 @@ def run(argv) -> None:
             if float(t.item()) != want:
                 raise RuntimeError(f"rccl-native sanity all-reduce gave {float(t.item())}, expected {want}")
 
-    if on_gpu and args.reserve_cus > 0:
-        # CU-masked compute stream, current for everything below (utils/streams.py)
-        from torch_distributed_sandbox_amd.utils.streams import reserve_cus_for_comm
-
-        torch.cuda.set_stream(reserve_cus_for_comm(args.reserve_cus, device))
     H = W = args.image_size
     B = args.batch_size
     torch.manual_seed(0)
@@ -217,34 +232,62 @@ def run(argv) -> None:
     src_pool = src_pool.view(pool, B, 28, 28)
     lab_pool = lab_pool.view(pool, B)
 
-    # input pipeline: batch i+1 is upsampled on a side stream while step i computes (the role
-    # of the reference's DataLoader prefetch); the step waits on that stream, and the batch is
-    # recorded on the compute stream so the caching allocator cannot recycle it early
+    # input pipeline (the role of the reference's DataLoader prefetch): batch i+1 -- the 28x28 ->
+    # HxW upsample and, for the fused plan, the batch's x moments behind BN1's statistics
+    # (convnet_fused.input_stats: weight-independent) -- is produced on a side stream that starts
+    # when step i's conv2 backward is enqueued, so it runs beside that MFMA-bound kernel instead
+    # of on the step's critical path.  Step i+1's compute stream waits on it; the tensors are
+    # recorded on the compute stream so the caching allocator cannot recycle them early.  A step
+    # whose hook did not fire (no fused plan, first step) produces its batch inline.  The work per
+    # timed step is unchanged: each step produces exactly one batch.
+    from torch_distributed_sandbox_amd.models import convnet_fused
+
     data_stream = torch.cuda.Stream(device) if on_gpu and args.prefetch else None
+    with_stats = data_stream is not None and args.mode != "layers"
 
     def produce(i):
-        j = i % pool
-        if data_stream is None:
-            return TF.upsample_bilinear_u8(src_pool[j], H, W)
-        data_stream.wait_stream(torch.cuda.current_stream(device))  # the previous step's reads of src
-        with torch.cuda.stream(data_stream):
-            return TF.upsample_bilinear_u8(src_pool[j], H, W)
+        return TF.upsample_bilinear_u8(src_pool[i % pool], H, W)
 
     pending = {}
+    sim_stream = None
+    if on_gpu and args.sim_comm_us > 0:
+        # on the communication side of the CU split when there is one, as RCCL's kernels would be
+        h = tds._ext.ops().cu_comm_stream(device.index) if reserve > 0 else 0
+        sim_stream = torch.cuda.ExternalStream(h, device=device) if h else torch.cuda.Stream(device, priority=-1)
+
+    def prefetch(i):
+        cur = torch.cuda.current_stream(device)
+        data_stream.wait_stream(cur)
+        with torch.cuda.stream(data_stream):
+            x = produce(i)
+            stats = convnet_fused.input_stats(x) if with_stats else None
+        x.record_stream(cur)
+        if stats is not None:
+            for t in stats:
+                t.record_stream(cur)
+            convnet_fused.attach_input_stats(x, stats)
+        pending[i] = x
 
     def step(i):
         j = i % pool
-        images = pending.pop(i) if i in pending else produce(i)
-        if data_stream is not None:
+        if i in pending:
+            images = pending.pop(i)
             torch.cuda.current_stream(device).wait_stream(data_stream)
-            images.record_stream(torch.cuda.current_stream(device))
+        else:
+            images = produce(i)
         if data_stream is not None:
-            pending[i + 1] = produce(i + 1)
+            convnet_fused.before_conv2_backward(lambda: prefetch(i + 1))
         out = ddp(images)
+        if sim_stream is not None:
+            sim_stream.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(sim_stream):
+                tds._ext.ops().comm_spin(out, args.sim_comm_us, args.sim_comm_ctas, 19744)
         loss = criterion(out, lab_pool[j])
         optimizer.zero_grad()
         loss.backward()
         optimizer.step()
+        if data_stream is not None:
+            convnet_fused._before_conv2_backward.clear()  # (a plan without the hook)
         return loss
 
     def sync_all():
@@ -286,14 +329,18 @@ def run(argv) -> None:
             "overlap_optimizer": ddp.overlap_optimizer,
             "fc_grad": ddp.fc_grad_path(),
             "allreduce_chunks": ddp.allreduce_chunks,
-            "reserve_cus": args.reserve_cus,
-            "rccl_max_ctas": args.rccl_max_ctas or None,
+            "reserve_cus": reserve,
+            "prefetch": data_stream is not None,
+            "rccl_max_ctas": rccl_max_ctas or None,
             "optimizer": "SGD(lr=1e-4)",
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3) if on_gpu else None,
             "final_loss": final_loss,
         }
         if probe is not None:
             config["allreduce_probe"] = probe
+        if sim_stream is not None:
+            config["sim_comm"] = {"us": args.sim_comm_us, "ctas": args.sim_comm_ctas,
+                                  "cu_mask_layout": os.environ.get("TDS_CU_MASK_LAYOUT", "striped")}
         if args.shared_device:
             config["shared_device"] = True  # rehearsal: all ranks on one GPU, not a multi-GPU number
         rec = {

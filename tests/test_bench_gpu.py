@@ -21,9 +21,12 @@ def _bench(args, timeout=240):
     return recs[0]
 
 
-def test_bench_one_gpu_small(gpu):
-    r = _bench(["--image-size", "512", "--steps", "3", "--warmup", "1"])
+@pytest.mark.parametrize("prefetch", [False, True])
+def test_bench_one_gpu_small(gpu, prefetch):
+    r = _bench(["--image-size", "512", "--steps", "3", "--warmup", "1",
+                "--prefetch" if prefetch else "--no-prefetch"])
     assert r["n_gpus"] == 1 and r["config"]["fc_grad"] == "local" and r["value"] > 0
+    assert r["config"]["prefetch"] is prefetch
 
 
 @pytest.mark.parametrize("exchange", ["auto", "allreduce"])

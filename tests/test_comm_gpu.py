@@ -277,14 +277,15 @@ def test_rccl_native_count_and_sendrecv(pg, gpu):
 
 
 def test_cu_reserve_and_masked_stream(gpu):
-    """utils/streams.py: a CU-masked compute stream with 16 CUs left to communication kernels;
+    """utils/streams.py: a CU-masked compute stream with 32 CUs left to communication kernels;
     the persistent kernels size their grids to the remaining CUs and the step matches the
     full-chip one (summation order of the per-workgroup partials differs)."""
     import copy
 
     from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import CrossEntropyLoss
-    from torch_distributed_sandbox_amd.utils.streams import compute_cus, reserve_cus_for_comm
+    from torch_distributed_sandbox_amd import _ext
+    from torch_distributed_sandbox_amd.utils.streams import comm_stream, compute_cus, reserve_cus_for_comm
 
     torch.manual_seed(0)
     H = 128
@@ -295,8 +296,22 @@ def test_cu_reserve_and_masked_stream(gpu):
     full = compute_cus()
     CrossEntropyLoss()(m1(x), y).backward()
     try:
-        s = reserve_cus_for_comm(16, gpu)
-        assert compute_cus() == full - 16
+        with pytest.raises(ValueError):
+            reserve_cus_for_comm(16, gpu)
+        assert comm_stream(gpu) is None
+        s = reserve_cus_for_comm(32, gpu)
+        assert compute_cus() == full - 32
+        cs = comm_stream(gpu)
+        # the two sides of the split land on disjoint CUs: 4 per XCC on the comm side
+        with torch.cuda.stream(cs):
+            where_c = _ext.ops().cu_probe(x, 50, 512).cpu()
+        with torch.cuda.stream(s):
+            where_s = _ext.ops().cu_probe(x, 50, 2048).cpu()
+        torch.cuda.synchronize()
+        cu_c = {(a, (b >> 8) & 0xFF) for a, b in where_c.tolist()}
+        cu_s = {(a, (b >> 8) & 0xFF) for a, b in where_s.tolist()}
+        assert not cu_c & cu_s
+        assert len(cu_c) == 32 and len(cu_s) == full - 32
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             CrossEntropyLoss()(m2(x), y).backward()

@@ -104,6 +104,54 @@ def test_layer1_forward(gpu, H):
     _check(gram[625:], S, 2e-6, "S")
 
 
+def test_layer1_precomputed_input_stats(gpu):
+    """fused_l1_forward with the x moments computed beforehand on another stream (the input
+    pipeline hand-off) is bit-identical to computing them inline."""
+    torch.manual_seed(1)
+    B, H = 2, 132
+    x = torch.rand(B, 1, H, H, device=gpu)
+    w1 = torch.randn(16, 1, 5, 5, device=gpu) * 0.2
+    b1 = torch.randn(16, device=gpu) * 0.1
+    g1 = torch.rand(16, device=gpu) + 0.5
+    be1 = torch.randn(16, device=gpu) * 0.1
+
+    def run(asum=None, strips=None):
+        rm, rv = torch.zeros(16, device=gpu), torch.ones(16, device=gpu)
+        nbt = torch.zeros((), dtype=torch.long, device=gpu)
+        out = _ops().fused_l1_forward(x, w1, b1, g1, be1, rm, rv, nbt, 0.1, 1e-5, asum, strips)
+        return list(out) + [rm, rv]
+
+    side = torch.cuda.Stream(gpu)
+    side.wait_stream(torch.cuda.current_stream(gpu))
+    with torch.cuda.stream(side):
+        asum, strips = _ops().l1_input_stats(x)
+    torch.cuda.current_stream(gpu).wait_stream(side)
+    for a, b in zip(run(), run(asum, strips)):
+        assert torch.equal(a, b)
+    with pytest.raises(RuntimeError):
+        _ops().fused_l1_forward(x, w1, b1, g1, be1, None, None, None, 0.1, 1e-5, asum[:41].contiguous(), strips)
+
+
+def test_model_uses_attached_input_stats(gpu):
+    """ConvNet(fused) consumes stats attached by the input pipeline; an in-place change of the
+    batch invalidates them."""
+    from torch_distributed_sandbox_amd.models import ConvNet, convnet_fused
+
+    torch.manual_seed(0)
+    H = 64
+    x = torch.rand(2, 1, H, H, device=gpu)
+    m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    m2 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    m2.load_state_dict(m1.state_dict())
+    ref = m1(x)
+    x2 = x.clone()
+    convnet_fused.attach_input_stats(x2, convnet_fused.input_stats(x2))
+    assert convnet_fused._take_input_stats(x2)[0] is not None
+    assert torch.equal(m2(x2), ref)
+    x2.mul_(2.0)
+    assert convnet_fused._take_input_stats(x2) == (None, None)
+
+
 @pytest.mark.parametrize("P", [40, 38, 37])
 def test_conv2_forward(gpu, P):
     """y2, the BN2 partial sums, and ya = window max / min of y2 by the sign of gamma2

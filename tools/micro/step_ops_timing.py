@@ -35,8 +35,13 @@ def main():
     ap.add_argument("--image-size", type=int, default=3000)
     ap.add_argument("--batch-size", type=int, default=5)
     ap.add_argument("--only", default="")
+    ap.add_argument("--reserve-cus", type=int, default=0, help="run on a CU-masked stream (utils/streams.py)")
     a = ap.parse_args()
     ops = tds._ext.ops()
+    if a.reserve_cus:
+        from torch_distributed_sandbox_amd.utils.streams import reserve_cus_for_comm
+
+        torch.cuda.set_stream(reserve_cus_for_comm(a.reserve_cus, torch.device("cuda", 0)))
     from torch_distributed_sandbox_amd.data import synthetic_batch
     from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import functional as TF

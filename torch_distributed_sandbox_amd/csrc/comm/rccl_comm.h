@@ -50,6 +50,9 @@
 
 #include "comm/comm.h"
 
+// csrc/kernels/cu_budget.hip: stream confined to the CUs reserved for communication (or nullptr)
+hipStream_t tds_cu_comm_stream(int device);
+
 namespace tds_comm {
 
 #define TDS_RCCL(cmd)                                                                   \
@@ -209,9 +212,18 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     return t;
   }
 
+  // The communicator's stream: with CUs reserved for communication (utils/streams.py) the
+  // stream confined to those CUs (cu_budget.hip), so RCCL's kernels never sit on a CU a
+  // persistent compute workgroup waits for; otherwise a high-priority pool stream.
+  static c10::hip::HIPStream comm_stream_for(int64_t device) {
+    if (hipStream_t s = tds_cu_comm_stream((int)device))
+      return c10::hip::getStreamFromExternal(s, (c10::DeviceIndex)device);
+    return c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device);
+  }
+
   RcclComm(int64_t rank, int64_t world, int64_t device, at::Tensor id, int64_t timeout_ms)
       : st_(std::make_shared<RcclState>()),
-        stream_(c10::hip::getStreamFromPool(/*isHighPriority=*/true, (c10::DeviceIndex)device)) {
+        stream_(comm_stream_for(device)) {
     TORCH_CHECK(id.numel() == (int64_t)sizeof(ncclUniqueId) && id.scalar_type() == at::kByte,
                 "RcclComm: bad unique id");
     st_->rank = rank;

@@ -103,15 +103,46 @@ int64_t pb_plane(int64_t P) { return tds_pb_plane((int)(P / 2)); }
 
 // ---------------------------------------------------------------- layer 1 forward
 // returns (p1 carrier, idx1, stats1[mean16|invstd16], ac_partial, strips)
+void check_l1_input(const Tensor& x, const char* what) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), what, ": x");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, what, ": x must be [B,1,H,W]");
+  TORCH_CHECK(x.size(2) == x.size(3) && x.size(2) >= 8, what, ": square images with H >= 8");
+  TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= 32, what, ": 1 <= B <= 32 per rank");
+}
+
+// The weight-independent half of the BN1 statistics: the x autocorrelation sums (42 doubles)
+// and the border strips (9 x 82 doubles).  conv1 is linear in x, so BN1's batch mean and
+// variance are these moments contracted with w1 (tds_l1_gram); they depend on the batch only,
+// which lets an input pipeline produce them with the batch (on its own stream, beside the
+// previous step's backward) and hand them to fused_l1_forward.
+std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
+  check_l1_input(x, "l1_input_stats");
+  const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
+  c10::DeviceGuard guard(x.device());
+  hipStream_t st = stream_of(x);
+  auto fo = x.options().dtype(at::kDouble);
+  // one thread per 4 x 8 pixel block: each fp32 partial covers 32 products (fp64 beyond)
+  const int nac = tds_x_autocorr_num_wg((int)B, (int)H, (int)W);
+  TORCH_CHECK(nac > 0, "l1_input_stats: W % 4 == 0 required (autocorrelation kernel)");
+  auto ac = at::empty({(int64_t)nac * 42}, fo);
+  auto strips = at::empty({9 * 82}, fo);
+  tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, (int)B, (int)H, (int)W, st);
+  // (on a side stream beside the autocorrelation the two kernels slowed each other: 176 + 94
+  // us overlapped vs 99 + 35 us serial)
+  tds_x_border(x.data_ptr<float>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, st);
+  auto asum = at::empty({42}, fo);
+  tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
+  check_launches("l1_input_stats");
+  return {asum, strips};
+}
+
 std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     const Tensor& x, const Tensor& w1, const Tensor& b1, const c10::optional<Tensor>& gamma1,
     const c10::optional<Tensor>& beta1, const c10::optional<Tensor>& rm1, const c10::optional<Tensor>& rv1,
-    const c10::optional<Tensor>& nbt1, double momentum, double eps) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "fused_l1_forward: x");
-  TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, "fused_l1_forward: x must be [B,1,H,W]");
+    const c10::optional<Tensor>& nbt1, double momentum, double eps, const c10::optional<Tensor>& asum_in,
+    const c10::optional<Tensor>& strips_in) {
+  check_l1_input(x, "fused_l1_forward");
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
-  TORCH_CHECK(H == W && H >= 8, "fused_l1_forward: square images with H >= 8");
-  TORCH_CHECK(B >= 1 && B <= 32, "fused_l1_forward: 1 <= B <= 32 per rank");
   need(w1, at::kFloat, {16, 1, 5, 5}, "conv1.weight");
   need(b1, at::kFloat, {16}, "conv1.bias");
   const float* g = optf(gamma1, 16, "bn1.weight");
@@ -127,18 +158,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   hipStream_t st = stream_of(x);
   const int64_t P = H / 2;
   auto fo = x.options();
-  // x autocorrelation + border strips -> Gram G / patch sums S -> BN1 statistics in closed form
-  // one thread per 4 x 8 pixel block: each fp32 partial covers 32 products (fp64 beyond)
-  const int nac = tds_x_autocorr_num_wg((int)B, (int)H, (int)W);
-  TORCH_CHECK(nac > 0, "fused_l1_forward: W % 4 == 0 required (autocorrelation kernel)");
-  auto ac = at::empty({(int64_t)nac * 42}, fo.dtype(at::kDouble));
-  auto strips = at::empty({9 * 82}, fo.dtype(at::kDouble));
-  tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, (int)B, (int)H, (int)W, st);
-  // (on a side stream beside the autocorrelation the two kernels slowed each other: 176 + 94
-  // us overlapped vs 99 + 35 us serial)
-  tds_x_border(x.data_ptr<float>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, st);
-  auto asum = at::empty({42}, fo.dtype(at::kDouble));
-  tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
+  // x autocorrelation + border strips (precomputed by the input pipeline, or here) -> Gram G /
+  // patch sums S -> BN1 statistics in closed form
+  Tensor asum, strips;
+  if (asum_in.has_value() && asum_in->defined()) {
+    TORCH_CHECK(strips_in.has_value() && strips_in->defined(), "fused_l1_forward: asum without strips");
+    need(*asum_in, at::kDouble, {42}, "precomputed autocorrelation sums");
+    need(*strips_in, at::kDouble, {9 * 82}, "precomputed border strips");
+    asum = *asum_in;
+    strips = *strips_in;
+  } else {
+    std::tie(asum, strips) = l1_input_stats(x);
+  }
   auto gram = at::empty({650}, fo.dtype(at::kDouble));
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
   auto stats = at::empty({32}, fo);
@@ -387,11 +418,37 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
 void set_cu_reserve(int64_t n) { tds_set_cu_reserve((int)n); }
 int64_t cu_reserve() { return tds_cu_reserve(); }
 int64_t device_cus() { return tds_device_cus(); }
-int64_t cu_masked_stream(int64_t device, int64_t reserve) {
-  hipStream_t s = tds_cu_masked_stream((int)device, (int)reserve);
+int64_t cu_masked_stream(int64_t device, int64_t reserve, bool striped) {
+  hipStream_t s = tds_cu_masked_stream((int)device, (int)reserve, striped);
   TORCH_CHECK(s != nullptr, "cu_masked_stream: hipExtStreamCreateWithCUMask failed (device ", device, ", reserve ",
               reserve, ")");
   return (int64_t)reinterpret_cast<intptr_t>(s);
+}
+
+// the communication stream of the CU split (0 when no CUs are reserved)
+int64_t cu_comm_stream(int64_t device) { return (int64_t)reinterpret_cast<intptr_t>(tds_cu_comm_stream((int)device)); }
+
+// one-GPU rehearsal of a collective's CU footprint (cu_budget.hip): `nblocks` workgroups of 256
+// threads holding `lds_bytes` of LDS each for `us` microseconds, on the current stream
+void comm_spin(const Tensor& like, int64_t us, int64_t nblocks, int64_t lds_bytes) {
+  TORCH_CHECK(like.is_cuda(), "comm_spin: needs a GPU tensor");
+  TORCH_CHECK(us >= 0 && us <= 1000000 && nblocks >= 1 && nblocks <= 1024 && lds_bytes >= 1024 &&
+                  lds_bytes <= 64 * 1024,
+              "comm_spin: 0 <= us <= 1e6, 1 <= nblocks <= 1024, 1 KiB <= lds <= 64 KiB");
+  c10::DeviceGuard guard(like.device());
+  auto sink = at::empty({nblocks}, like.options().dtype(at::kInt));
+  tds_comm_spin(us, (int)nblocks, (int)lds_bytes, sink.data_ptr<int>(), stream_of(like));
+  check_launches("comm_spin");
+}
+
+// where the current stream's workgroups land: [nblocks, 2] int32 (XCC id, HW_ID register)
+Tensor cu_probe(const Tensor& like, int64_t us, int64_t nblocks) {
+  TORCH_CHECK(like.is_cuda() && us >= 0 && us <= 100000 && nblocks >= 1 && nblocks <= 65536, "cu_probe: arguments");
+  c10::DeviceGuard guard(like.device());
+  auto out = at::empty({nblocks, 2}, like.options().dtype(at::kInt));
+  tds_cu_probe(us, (int)nblocks, out.data_ptr<int>(), stream_of(like));
+  check_launches("cu_probe");
+  return out;
 }
 
 // test hook: one launch of a trivial kernel with the given dynamic LDS / block size (a request
@@ -447,8 +504,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
 TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
-      "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps) -> (Tensor, Tensor, Tensor, Tensor)",
+      "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps, Tensor? asum=None, Tensor? strips=None) -> "
+      "(Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_forward);
+  m.def("l1_input_stats(Tensor x) -> (Tensor, Tensor)", &l1_input_stats);
   m.def("conv2_pack(Tensor w2) -> (Tensor, Tensor)", &conv2_pack);
   m.def("fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2) -> (Tensor, Tensor, Tensor)",
         &fused_conv2_forward);
@@ -480,5 +539,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("set_cu_reserve(int n) -> ()", &set_cu_reserve);
   m.def("cu_reserve() -> int", &cu_reserve);
   m.def("device_cus() -> int", &device_cus);
-  m.def("cu_masked_stream(int device, int reserve) -> int", &cu_masked_stream);
+  m.def("cu_masked_stream(int device, int reserve, bool striped=True) -> int", &cu_masked_stream);
+  m.def("comm_spin(Tensor like, int us, int nblocks, int lds_bytes) -> ()", &comm_spin);
+  m.def("cu_probe(Tensor like, int us, int nblocks) -> Tensor", &cu_probe);
+  m.def("cu_comm_stream(int device) -> int", &cu_comm_stream);
 }

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <mutex>
+#include <utility>
 #include <cstdint>
 #include <vector>
 
@@ -39,12 +41,13 @@ void tds_set_cu_reserve(int n) { g_reserve.store(n > 0 ? n : 0, std::memory_orde
 int tds_cu_reserve() { return g_reserve.load(std::memory_order_relaxed); }
 
 // A stream of `device` whose kernels may use every CU but `reserve` of them, reserve/8 per XCD
-// (hipExtStreamCreateWithCUMask).  The mask is in the driver's logical CU numbering, which on
-// MI355X runs XCD by XCD (32 CUs each): masking the top CUs of the chip instead left one XCD
-// with half its CUs, and the workgroups dispatched round-robin to it (one persistent workgroup
-// per CU) ran in two rounds -- the whole step took +70 %.  Returns nullptr on failure (or a
-// reserve that is not a multiple of 8).  The stream lives for the process.
-hipStream_t tds_cu_masked_stream(int device, int reserve) {
+// (hipExtStreamCreateWithCUMask).  Two numberings of the mask bits are possible: `striped`
+// (bit c -> XCD c % 8, the order the dispatcher deals workgroups round-robin to the XCDs) and
+// `blocked` (XCD by XCD, 32 bits each).  A mask built for the wrong one leaves some XCDs with
+// fewer CUs than the persistent grid gives them workgroups, which then run in two rounds (the
+// whole step +60-70 %).  Returns nullptr on failure (or a reserve that is not a multiple of 8).
+// The stream lives for the process.
+hipStream_t tds_cu_masked_stream(int device, int reserve, bool striped) {
   if (reserve < 0 || reserve % 8 != 0) return nullptr;
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return nullptr;
@@ -55,11 +58,89 @@ hipStream_t tds_cu_masked_stream(int device, int reserve) {
     const int n = prop.multiProcessorCount, nxcd = 8, per = n / nxcd, rx = reserve / nxcd;
     if (n % nxcd == 0 && per - rx >= 1) {
       std::vector<uint32_t> mask((n + 31) / 32, 0u);
-      for (int cu = 0; cu < n; ++cu)
-        if (cu % per < per - rx) mask[cu / 32] |= 1u << (cu % 32);
+      for (int cu = 0; cu < n; ++cu) {
+        const int local = striped ? cu / nxcd : cu % per;  // the CU's index inside its XCD
+        if (local < per - rx) mask[cu / 32] |= 1u << (cu % 32);
+      }
       if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) s = nullptr;
     }
   }
   (void)hipSetDevice(prev);
   return s;
+}
+
+// The communication side of the split: a stream of `device` confined to the CUs the compute
+// stream leaves out (the complement of tds_cu_masked_stream's striped mask for the current
+// reserve), so RCCL's kernels -- launched on the communicator's stream -- land on CUs no
+// persistent compute workgroup waits for.  nullptr when no CUs are reserved.  Cached per
+// (device, reserve); the streams live for the process.
+hipStream_t tds_cu_comm_stream(int device) {
+  const int reserve = g_reserve.load(std::memory_order_relaxed);
+  if (reserve <= 0 || reserve % 8 != 0 || device < 0 || device >= kMaxDev) return nullptr;
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<int, int>, hipStream_t>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  for (auto& e : cache)
+    if (e.first.first == device && e.first.second == reserve) return e.second;
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  hipDeviceProp_t prop;
+  hipStream_t s = nullptr;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+    const int n = prop.multiProcessorCount, nxcd = 8, per = n / nxcd, rx = reserve / nxcd;
+    if (n % nxcd == 0 && per - rx >= 1) {
+      std::vector<uint32_t> mask((n + 31) / 32, 0u);
+      for (int cu = 0; cu < n; ++cu)
+        if (cu / nxcd >= per - rx) mask[cu / 32] |= 1u << (cu % 32);
+      if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) s = nullptr;
+    }
+  }
+  (void)hipSetDevice(prev);
+  if (s) cache.push_back({{device, reserve}, s});
+  return s;
+}
+
+// ---- one-GPU rehearsal of a collective's CU footprint -----------------------------------
+// RCCL's generic kernel on gfx950 takes 256 threads, 19.7 KB of LDS and 261-280 VGPRs per
+// workgroup (librccl code-object metadata), one workgroup per channel, resident for the whole
+// collective.  comm_spin_kernel holds the same LDS for `us` microseconds on each of its
+// workgroups (constant 100 MHz clock), so a single-GPU step can be timed with a "collective"
+// in flight: a persistent compute kernel cannot place a workgroup on a CU the spin occupies.
+__global__ __launch_bounds__(256) void comm_spin_kernel(int64_t ticks, int* sink) {
+  extern __shared__ int lds[];
+  const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+  lds[threadIdx.x] = (int)threadIdx.x;
+  int acc = 0;
+  while ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    __builtin_amdgcn_s_sleep(8);
+    acc += lds[(threadIdx.x + acc) & 255];
+  }
+  if (acc == 0x7fffffff) sink[blockIdx.x] = acc;  // never true: keeps the loop
+}
+
+void tds_comm_spin(int64_t us, int nblocks, int lds_bytes, int* sink, hipStream_t st) {
+  hipLaunchKernelGGL(comm_spin_kernel, dim3(nblocks), dim3(256), (size_t)lds_bytes, st, us * 100, sink);
+}
+
+// Where workgroups land: each workgroup holds 64 KiB of LDS for ~`us` microseconds (so the
+// dispatcher spreads them over the CUs it may use) and records its XCC and HW_ID (CU, SE).
+__global__ __launch_bounds__(64) void cu_probe_kernel(int64_t ticks, int* out) {
+  extern __shared__ int lds[];
+  const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
+  int hwid, xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  lds[threadIdx.x] = hwid;
+  while ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = xcc;
+    out[2 * blockIdx.x + 1] = lds[0];
+  }
+}
+
+void tds_cu_probe(int64_t us, int nblocks, int* out, hipStream_t st) {
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(cu_probe_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                            64 * 1024);
+  hipLaunchKernelGGL(cu_probe_kernel, dim3(nblocks), dim3(64), 64 * 1024, st, us * 100, out);
 }

@@ -69,7 +69,10 @@ int tds_conv2_num_wg();  // CUs (tds_device_cus)
 int tds_device_cus();
 void tds_set_cu_reserve(int n);
 int tds_cu_reserve();
-hipStream_t tds_cu_masked_stream(int device, int reserve);
+hipStream_t tds_cu_masked_stream(int device, int reserve, bool striped);
+hipStream_t tds_cu_comm_stream(int device);
+void tds_comm_spin(int64_t us, int nblocks, int lds_bytes, int* sink, hipStream_t st);
+void tds_cu_probe(int64_t us, int nblocks, int* out, hipStream_t st);
 int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c, int group_rows);  // host: blocked tile order table
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st);
 int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)

@@ -57,6 +57,48 @@ def supported(model, x) -> bool:
     return True
 
 
+# ---- input pipeline hand-off ---------------------------------------------------------
+# BN1's batch statistics are the batch's x moments (autocorrelation sums + border strips,
+# ops.l1_input_stats) contracted with conv1's weights.  The moments depend on the batch only, so
+# an input pipeline may compute them with the batch, on its own stream, and attach them to it;
+# _Layer1 then skips that part.  The pipeline is responsible for ordering (the consuming stream
+# waits on the producing stream before the forward, and the tensors are record_stream'ed).
+
+
+def input_stats(x):
+    """(asum[42], strips[738]) fp64 x moments of a [B,1,H,W] fp32 batch, on the current stream."""
+    return _ext.ops().l1_input_stats(x.contiguous())
+
+
+def attach_input_stats(x, stats):
+    """Hand precomputed ``input_stats(x)`` to the forward that consumes ``x`` (valid until x is
+    modified in place)."""
+    x._tds_l1_stats = (x._version, stats)
+    return x
+
+
+def _take_input_stats(x):
+    st = getattr(x, "_tds_l1_stats", None)
+    if st is None or st[0] != x._version:
+        return None, None
+    return st[1]
+
+
+# One-shot callbacks run (on the host, in the backward's thread) right before the conv2
+# backward -- the step's longest, MFMA-bound kernel -- is enqueued: work they put on another
+# stream after waiting on the current one runs beside it (bench.py / trainer input prefetch).
+_before_conv2_backward = []
+
+
+def before_conv2_backward(fn):
+    _before_conv2_backward.append(fn)
+
+
+def _run_before_conv2_backward():
+    while _before_conv2_backward:
+        _before_conv2_backward.pop(0)()
+
+
 def _sinks(ctx, params, first):
     """Gradient destinations for ``params`` (bucket views when DDP registered sinks,
     ops/grad_sink.py; None for parameters that need no gradient).  ``first`` is the
@@ -82,8 +124,10 @@ class _Layer1(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps):
         ops = _ext.ops()
+        asum, strips = _take_input_stats(x)
         x = x.contiguous()
-        p1, idx1, stats1, gram = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps)
+        p1, idx1, stats1, gram = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps, asum,
+                                                      strips)
         ctx.save_for_backward(x, p1, idx1, w1, b1, g1, stats1, gram)
         ctx.params = (w1, b1, g1, be1)
         ctx.mark_non_differentiable(idx1)
@@ -125,6 +169,7 @@ class _Conv2(torch.autograd.Function):
     def backward(ctx, _dy2_placeholder, _unused, _unused_ya):
         p1, wd, y2 = ctx.saved_tensors
         link = ctx.link
+        _run_before_conv2_backward()
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
         dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, p1, wd, 1.0,
                                                            *_sinks(ctx, ctx.params, 1))

@@ -12,6 +12,7 @@ The RCCL side is bounded with ``TDS_RCCL_MIN_CTAS`` / ``TDS_RCCL_MAX_CTAS`` (the
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -19,22 +20,44 @@ import torch
 from .. import _ext
 
 
+def mask_layout() -> str:
+    """CU-mask bit numbering (csrc/kernels/cu_budget.hip): ``TDS_CU_MASK_LAYOUT`` = striped
+    (default) | blocked."""
+    v = os.environ.get("TDS_CU_MASK_LAYOUT", "striped").strip().lower()
+    if v not in ("striped", "blocked"):
+        raise ValueError(f"TDS_CU_MASK_LAYOUT must be striped|blocked, got {v!r}")
+    return v
+
+
 def reserve_cus_for_comm(n: int, device: Optional[torch.device] = None) -> Optional[torch.cuda.Stream]:
-    """Reserve ``n`` CUs (a multiple of 8: n/8 per XCD) for communication kernels; returns the
+    """Reserve ``n`` CUs (a multiple of 32: n/8 per XCD) for communication kernels; returns the
     CU-masked compute stream (None and no change when ``n`` is 0).  Create it before the model
     and DDP, and make it current for the whole training loop (autograd's accumulation nodes
     remember the stream they were created on)."""
     ops = _ext.ops()
     n = int(n)
-    if n % 8:
-        raise ValueError(f"reserve_cus_for_comm: n must be a multiple of 8 (n/8 CUs per XCD), got {n}")
+    if n % 32:
+        # n/8 CUs per XCD, and per XCD a multiple of its 4 shader engines: with 2 of an XCD's 32
+        # CUs out, two engines keep 7 CUs, the dispatcher still deals the 30 persistent
+        # workgroups 8/8/7/7 over the engines from wherever its round-robin stands, and a
+        # workgroup waits a whole round (measured at reserve 16: conv2 backward 1.56 -> 3.07 ms,
+        # step +60 %; reserve 32: +5 %, tools/gpu_sessions/r2_cuprobe2.sh)
+        raise ValueError(f"reserve_cus_for_comm: n must be a multiple of 32 (4 CUs per XCD), got {n}")
     if n <= 0:
         ops.set_cu_reserve(0)
         return None
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    handle = ops.cu_masked_stream(dev.index, n)
+    handle = ops.cu_masked_stream(dev.index, n, mask_layout() == "striped")
     ops.set_cu_reserve(n)
     return torch.cuda.ExternalStream(handle, device=dev)
+
+
+def comm_stream(device: Optional[torch.device] = None) -> Optional[torch.cuda.Stream]:
+    """The stream confined to the reserved CUs (what the native RCCL communicator launches on),
+    or None when no CUs are reserved."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    h = int(_ext.ops().cu_comm_stream(dev.index))
+    return torch.cuda.ExternalStream(h, device=dev) if h else None
 
 
 def compute_cus() -> int:
