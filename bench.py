@@ -181,27 +181,27 @@ def run(argv) -> None:
         device = torch.device("cuda", local_rank)
     else:
         device = torch.device("cpu")
-    # CU split for overlapped collectives (utils/streams.py, docs/DISTRIBUTED.md): by default at
-    # world > 1 on the native communicator, 32 CUs (4 per XCD, one per shader engine) are kept
-    # out of the compute and RCCL's kernels are confined to them with at most as many CTAs.
-    # Set before the process group, whose communicator stream takes the complement mask.
+    # CU split for overlapped collectives (parallel/distributed.py init_process_group comm_cus,
+    # utils/streams.py, docs/DISTRIBUTED.md): on rccl-native the process group sets it up
+    # (default 32 CUs at world > 1); otherwise --reserve-cus masks the compute side only
+    if args.rccl_max_ctas > 0:
+        os.environ["TDS_RCCL_MAX_CTAS"] = str(args.rccl_max_ctas)
     reserve = args.reserve_cus
-    if reserve is None:
-        reserve = 32 if on_gpu and world > 1 and backend == "rccl-native" else 0
-    rccl_max_ctas = args.rccl_max_ctas or (reserve if backend == "rccl-native" else 0)
-    if rccl_max_ctas > 0:
-        os.environ["TDS_RCCL_MAX_CTAS"] = str(rccl_max_ctas)
-    if on_gpu and reserve > 0:
-        # CU-masked compute stream, current for everything below (utils/streams.py)
-        from torch_distributed_sandbox_amd.utils.streams import reserve_cus_for_comm
-
-        torch.cuda.set_stream(reserve_cus_for_comm(reserve, device))
     if world > 1 or args.grad_exchange in ("activations", "sharded", "chunked"):
         if world == 1:
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29533")
         tdist.init_process_group(backend, rank=rank, world_size=world,
-                                 device_id=local_rank if on_gpu and backend != "gloo" else None)
+                                 device_id=local_rank if on_gpu and backend != "gloo" else None,
+                                 comm_cus=reserve if backend == "rccl-native" else None)
+    if backend == "rccl-native" and tdist.is_initialized():
+        reserve = tdist.comm_cus()
+    elif on_gpu and reserve:
+        from torch_distributed_sandbox_amd.utils.streams import reserve_cus_for_comm
+
+        torch.cuda.set_stream(reserve_cus_for_comm(reserve, device))
+    reserve = reserve or 0
+    rccl_max_ctas = int(os.environ.get("TDS_RCCL_MAX_CTAS", "0") or 0) if backend == "rccl-native" else 0
     rccl_ranks = None
     if tdist.is_initialized():
         comm, kind = native_comm_of(None)

@@ -86,17 +86,24 @@ def is_initialized() -> bool:
 
 def init_process_group(backend: Optional[str] = None, init_method: Optional[str] = None, rank: Optional[int] = None,
                        world_size: Optional[int] = None, timeout: datetime.timedelta = DEFAULT_TIMEOUT,
-                       device_id: Optional[int] = None, store=None) -> None:
+                       device_id: Optional[int] = None, store=None, comm_cus: Optional[int] = None) -> None:
     """Initialise the default group.  ``rank``/``world_size`` default to the
     ``RANK``/``WORLD_SIZE`` environment (torchrun); ``init_method`` defaults to
     ``env://`` (``MASTER_ADDR``/``MASTER_PORT``).  ``store="native"`` (or
     ``TDS_STORE=native``) rendezvouses through this package's C++ TCP store
-    (parallel/store.py) instead of c10d's."""
+    (parallel/store.py) instead of c10d's.
+
+    ``comm_cus`` (``rccl-native`` only): CUs split off for communication
+    (utils/streams.py, docs/DISTRIBUTED.md) -- a CU-masked compute stream is made
+    current on this thread and the communicator's stream is confined to the other
+    CUs, with RCCL's CTAs bounded to the same count.  Default (None):
+    ``TDS_COMM_CUS`` or 32 at world size > 1, 0 at world size 1."""
     b = _normalise_backend(backend)
     if rank is None:
         rank = int(os.environ.get("RANK", "0"))
     if world_size is None:
         world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    _state["comm_cus"] = 0
     if store is None and init_method is None and os.environ.get("TDS_STORE", "") == "native":
         store = "native"
     if isinstance(store, str):
@@ -122,9 +129,24 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
             # eager communicator init (bound to this GPU) instead of lazy first-collective init
             kwargs["device_id"] = torch.device("cuda", device_id)
         # (rccl-native always creates its communicator eagerly in the backend constructor)
+    if b == "rccl-native":
+        if comm_cus is None:
+            comm_cus = int(os.environ.get("TDS_COMM_CUS", "32")) if world_size > 1 else 0
+        if comm_cus > 0:
+            from ..utils.streams import reserve_cus_for_comm
+
+            os.environ.setdefault("TDS_RCCL_MAX_CTAS", str(comm_cus))
+            # before the communicator exists: its stream takes the complement mask
+            torch.cuda.set_stream(reserve_cus_for_comm(comm_cus, torch.device("cuda", device_id)))
+            _state["comm_cus"] = comm_cus
     dist.init_process_group(**kwargs)
     _state["backend"] = b
     _state["groups"] = {}
+
+
+def comm_cus() -> int:
+    """CUs split off for communication by ``init_process_group`` (0: none)."""
+    return int(_state.get("comm_cus", 0))
 
 
 def destroy_process_group(group=None) -> None:
