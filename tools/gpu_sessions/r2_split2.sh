@@ -13,3 +13,9 @@ b() {
 b base
 b r32_sim3000 --reserve-cus 32 --sim-comm-us 3000 --sim-comm-ctas 32
 b native_ex_r32 --grad-exchange activations --reserve-cus 32
+for k in 1 2 3; do
+  b def_$k
+  TDS_SO_VARIANT=nt b nt_$k
+done
+timeout -k 10 150 python -u tools/micro/step_ops_timing.py --iters 10 > $O/ops_def.log 2>&1 && tail -1 $O/ops_def.log
+TDS_SO_VARIANT=nt timeout -k 10 150 python -u tools/micro/step_ops_timing.py --iters 10 > $O/ops_nt.log 2>&1 && tail -1 $O/ops_nt.log

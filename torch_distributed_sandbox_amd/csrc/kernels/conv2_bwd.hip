@@ -143,7 +143,7 @@ __device__ __forceinline__ void br_xchg_finish(const f32x4* xs, const f32x4 (&ac
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int col = c0 + 4 * g + r;
-        if (col < P) orow[(int64_t)col * 16 + li] = v[r];
+        if (col < P) orow[(int64_t)col * 16 + li] = v[r];  // plain: read next by the layer-1 backward
       }
     }
   }

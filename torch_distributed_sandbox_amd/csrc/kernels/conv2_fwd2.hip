@@ -187,7 +187,7 @@ __device__ __forceinline__ void f2_store_ya(const float* ystage, const F2Tile& x
   if (tr >= pg.Q4 || tc >= pg.Q8) return;          // (odd P: a last tile row beyond the pooled image)
   const int e = threadIdx.x, co = e >> 3, part = e & 7;
   const float4 v = *reinterpret_cast<const float4*>(ystage + f2_ystage_off(co, part * 4));
-  *reinterpret_cast<float4*>(ya + ((((int64_t)x.b * 32 + co) * pg.Q4 + tr) * pg.Q8 + tc) * 32 + part * 4) = v;
+  st_stream(reinterpret_cast<float4*>(ya + ((((int64_t)x.b * 32 + co) * pg.Q4 + tr) * pg.Q8 + tc) * 32 + part * 4), v);
 }
 
 // the whole workgroup stores a staged tile: thread e, i -> float4 q = e + 256 i of
@@ -202,7 +202,7 @@ __device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, flo
     const int row = q >> 7, px = (q >> 3) & 15, chunk = q & 7;
     const int gr = x.r0 + row, gc = x.c0 + px;
     const float4 v = *reinterpret_cast<const float4*>(stage + f2_stage_off(row, px, chunk));
-    if (gr < P && gc < P) *reinterpret_cast<float4*>(y2 + (((int64_t)x.b * P + gr) * P + gc) * 32 + chunk * 4) = v;
+    if (gr < P && gc < P) st_stream(reinterpret_cast<float4*>(y2 + (((int64_t)x.b * P + gr) * P + gc) * 32 + chunk * 4), v);
   }
 }
 

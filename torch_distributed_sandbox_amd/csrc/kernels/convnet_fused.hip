@@ -210,9 +210,9 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
 #endif
           const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
           uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
-          dst[g] = make_uint2(h01, h23);
-          dst[4 + g] = make_uint2(l01, l23);
-          reinterpret_cast<uint32_t*>(idx1 + rec * 16)[g] = ixw;
+          st_stream(dst + g, make_uint2(h01, h23));
+          st_stream(dst + 4 + g, make_uint2(l01, l23));
+          st_stream(reinterpret_cast<uint32_t*>(idx1 + rec * 16) + g, ixw);
         }
       }
     }

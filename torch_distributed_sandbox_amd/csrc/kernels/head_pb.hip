@@ -65,18 +65,27 @@ struct HPThread {
   }
 };
 
-// 4 consecutive floats of a weight row at p; al = (element index of p) % 4, wave-uniform
-__device__ __forceinline__ void hp_st4(float* p, int al, float4 v) {
+#ifndef TDS_G2M_NT
+#define TDS_G2M_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void hp_st(T* p, T v, bool nt) {
+  if (nt) st_stream(p, v); else *p = v;
+}
+
+// 4 consecutive floats of a weight row at p; al = (element index of p) % 4, wave-uniform;
+// nt: non-temporal (common.h st_stream)
+__device__ __forceinline__ void hp_st4(float* p, int al, float4 v, bool nt = true) {
   if (al == 0) {
-    *reinterpret_cast<float4*>(p) = v;
+    hp_st(reinterpret_cast<float4*>(p), v, nt);
   } else if (al == 2) {
-    *reinterpret_cast<float2*>(p) = make_float2(v.x, v.y);
-    *reinterpret_cast<float2*>(p + 2) = make_float2(v.z, v.w);
+    hp_st(reinterpret_cast<float2*>(p), make_float2(v.x, v.y), nt);
+    hp_st(reinterpret_cast<float2*>(p + 2), make_float2(v.z, v.w), nt);
   } else {
-    p[0] = v.x;
-    p[1] = v.y;
-    p[2] = v.z;
-    p[3] = v.w;
+    hp_st(p, v.x, nt);
+    hp_st(p + 1, v.y, nt);
+    hp_st(p + 2, v.z, nt);
+    hp_st(p + 3, v.w, nt);
   }
 }
 
@@ -148,16 +157,17 @@ struct HPLoad {
 };
 
 // store a 4-group of class j of the weight layout at this thread's (row, 4 columns), inside the image only
-__device__ __forceinline__ void hp_store4(float* out, const PBGeom& g, const HPRow& rw, int j, float4 v) {
+__device__ __forceinline__ void hp_store4(float* out, const PBGeom& g, const HPRow& rw, int j, float4 v,
+                                          bool nt = true) {
   if (rw.nvalid == 0) return;
   float* p = out + (int64_t)j * 32 * g.Q * (int64_t)g.Q + rw.off;
   if (rw.nvalid == 4) {
-    hp_st4(p, rw.al, v);
+    hp_st4(p, rw.al, v, nt);
   } else {
     const float e[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-      if (k < rw.nvalid) p[k] = e[k];
+      if (k < rw.nvalid) hp_st(p + k, e[k], nt);
   }
 }
 
@@ -321,7 +331,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
         sdz += gm[k];
         sdy = fmaf(gm[k], ok ? yy[k] : 0.f, sdy);
       }
-      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]));  // planar, like a weight plane
+      // planar, like a weight plane
+      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]), TDS_G2M_NT != 0);
     }
     if constexpr (WITH_DW) {
       const HPRow& rw = rwg;
