@@ -176,12 +176,13 @@ def test_activation_exchange_fused_convnet(pg, gpu, mode):
 
 @pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("sharded", False),
                                            ("chunked", False),
-                                           ("allreduce", True)])
+                                           ("allreduce", True), ("activations", True), ("sharded", True)])
 def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     """overlap_optimizer: the fc bucket's collective + SGD update run on a side stream
     and the next forward's head waits on a parameter fence; the trajectory must be
     identical to the sequential step.  fuse=True: at world size 1 the fc weight's SGD
-    step runs inside the head backward kernel (ops/fused_update.py)."""
+    step runs inside the head backward kernel, or with an exchange forced inside the
+    exchange's dW formation (update-only linear_dw; ops/fused_update.py)."""
     import copy
 
     from torch_distributed_sandbox_amd.models import ConvNet

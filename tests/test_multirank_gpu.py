@@ -56,7 +56,9 @@ def _worker(rank, world, port, mode, overlap, out):
         torch.cuda.synchronize()
         # read after the step: with overlap_optimizer the fc bucket's collective is only
         # waited for (on the side stream) inside optimizer.step(); the step leaves .grad as is
-        grads = {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
+        # (None: the step was applied while the gradient was formed -- the exchange's
+        # optimizer-in-backward under overlap_optimizer, ops/fused_update.py)
+        grads = {n: None if p.grad is None else p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
         params = {n: p.detach().cpu().clone() for n, p in m.named_parameters()}
         rec["steps"].append({"loss": float(loss.item()), "grads": grads, "bufs": bufs, "params": params})
     rec["fc_grad"] = ddp.fc_grad_path()
@@ -91,6 +93,8 @@ def test_fused_ddp_two_ranks_matches_fp64_average(gpu, tmp_path, mode, overlap):
     recs = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
     assert recs[0]["fc_grad"] == {"allreduce": "allreduce", "activations": "activation-exchange",
                                   "sharded": "sharded-exchange", "chunked": "chunked-allreduce"}[mode]
+    fused_expected = overlap and mode in ("activations", "sharded")
+    assert (recs[0]["steps"][0]["grads"]["fc.weight"] is None) == fused_expected
     xs, ys = _data(world)
     params, bufs0 = recs[0]["p0"], recs[0]["b0"]
     for s in range(STEPS):
@@ -108,8 +112,16 @@ def test_fused_ddp_two_ranks_matches_fp64_average(gpu, tmp_path, mode, overlap):
         avg = {n: v / world for n, v in avg.items()}
         for n in avg:
             g0 = recs[0]["steps"][s]["grads"][n]
+            p1 = recs[0]["steps"][s]["params"][n]
+            fused = g0 is None
+            if fused:  # update-only exchange: the applied step is the gradient
+                assert overlap and mode in ("activations", "sharded") and n == "fc.weight", (s, n)
+                g0 = ((params[n].double() - p1.double()) / LR).float()
             for r in range(1, world):  # every rank holds the same averaged gradient
-                assert torch.equal(recs[r]["steps"][s]["grads"][n], g0), (s, n, r)
+                gr = recs[r]["steps"][s]["grads"][n]
+                assert (gr is None) == fused, (s, n, r)
+                if not fused:
+                    assert torch.equal(gr, g0), (s, n, r)
             ref_g = avg[n]
             if n.endswith("0.bias"):  # conv bias before BN: analytically zero, both sides noise
                 wg = avg[n.replace("bias", "weight")].abs().max().item()
@@ -119,9 +131,9 @@ def test_fused_ddp_two_ranks_matches_fp64_average(gpu, tmp_path, mode, overlap):
             flip_reach = n.startswith("layer1.") or n.startswith("layer2.0.")
             assert rel <= (2e-2 if ties and flip_reach else 2e-3), (s, n, rel, ties)
             # post-step parameters: identical on every rank, = p - lr * averaged grad
-            p1 = recs[0]["steps"][s]["params"][n]
             for r in range(1, world):
                 assert torch.equal(recs[r]["steps"][s]["params"][n], p1), (s, n, r)
-            assert torch.allclose(p1, params[n] - LR * g0, rtol=1e-6, atol=1e-7), (s, n)
+            if not fused:
+                assert torch.allclose(p1, params[n] - LR * g0, rtol=1e-6, atol=1e-7), (s, n)
         params = recs[0]["steps"][s]["params"]
         bufs0 = recs[0]["steps"][s]["bufs"]

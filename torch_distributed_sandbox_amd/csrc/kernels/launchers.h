@@ -51,7 +51,7 @@ void tds_bn_bwd(const float* dy, const float* x, int B, int C, int64_t HW, const
 // ---- linear.hip (skinny M<=8, N<=16)
 int tds_linear_fwd_nblk(int64_t K);
 int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, int N, int64_t K, int64_t ldw,
-                  float scale, int acc, hipStream_t st);
+                  float scale, int acc, float upd_lr, hipStream_t st);
 int tds_linear_fwd_skinny(const float* x, const float* W, const float* bias, float* out, float* partial, int M, int N,
                           int64_t K, int nblk, hipStream_t st);
 int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float* dx, float* dW, float* db, int M,

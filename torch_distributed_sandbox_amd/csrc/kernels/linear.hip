@@ -183,7 +183,8 @@ __global__ __launch_bounds__(256) void linear_bwd_skinny_kernel(const float* __r
 // 16 columns of x per step; memory-bound on reading x and writing dW.
 __global__ __launch_bounds__(256) void linear_dw_mfma_kernel(const float* __restrict__ g, const float* __restrict__ x,
                                                              float* __restrict__ dW, float* __restrict__ db, int M,
-                                                             int N, int64_t K, int64_t ldw, float scale, int acc) {
+                                                             int N, int64_t K, int64_t ldw, float scale, int acc,
+                                                             float upd_lr) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int li = lane & 15, gq = lane >> 4;
   const int steps = (M + 3) / 4;
@@ -218,7 +219,11 @@ __global__ __launch_bounds__(256) void linear_dw_mfma_kernel(const float* __rest
         if (n < N) {
           float* ptr = dW + (int64_t)n * ldw + col;
           const float v = scale * d[r];
-          *ptr = acc ? *ptr + v : v;
+          if (upd_lr != 0.f) {
+            *ptr = *ptr - upd_lr * v;  // update-only: dW is the weight, torch SGD p -= lr * g
+          } else {
+            *ptr = acc ? *ptr + v : v;
+          }
         }
       }
     }
@@ -275,13 +280,13 @@ int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float
 }
 
 int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, int N, int64_t K, int64_t ldw,
-                  float scale, int acc, hipStream_t st) {
+                  float scale, int acc, float upd_lr, hipStream_t st) {
   if (M > 64 || N > 16 || M < 1 || ldw < K) return -1;
   int64_t ncb = (K + 15) / 16;
   int64_t grid = (ncb + 3) / 4;
   if (grid > 8192) grid = 8192;
   hipLaunchKernelGGL(linear_dw_mfma_kernel, dim3((unsigned)grid), dim3(256), 0, st, dy, x, dW, db, M, N, K, ldw,
-                     scale, acc);
+                     scale, acc, upd_lr);
   TDS_LAUNCH_CHECK();
   return 0;
 }

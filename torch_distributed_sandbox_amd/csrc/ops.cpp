@@ -373,8 +373,11 @@ Tensor linear_bwd_into(const Tensor& dy, const Tensor& x, const Tensor& w, const
 // dW may be a column slice of a wider row-major matrix (unit column stride, any row stride):
 // the sharded fc exchange writes its shard straight into the full gradient.  More than 64
 // rows run as 64-row passes that accumulate.
+// update_lr != 0: UPDATE-ONLY -- dw is the weight itself (or a column slice of it) and receives
+// the plain SGD step dw -= update_lr * (scale * dy^T x) with no gradient materialised (the fc
+// exchange's optimizer-in-backward, parallel/factored.py); db is still written as a gradient.
 void linear_dw(const Tensor& dy, const Tensor& x, const Tensor& dw, const c10::optional<Tensor>& db, double scale,
-               bool accumulate) {
+               bool accumulate, double update_lr) {
   check_f32_dev(dy, "grad_output");
   check_f32_dev(x, "input");
   TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat, "tdsa.linear_dw: dW must be a float32 GPU tensor");
@@ -390,7 +393,7 @@ void linear_dw(const Tensor& dy, const Tensor& x, const Tensor& dw, const c10::o
     const int64_t mc = std::min<int64_t>(64, M - m0);
     const int rc = tds_linear_dw(dy.data_ptr<float>() + m0 * N, x.data_ptr<float>() + m0 * K, dw.data_ptr<float>(),
                                  opt_mut_ptr(db), (int)mc, (int)N, K, dw.stride(0), (float)scale,
-                                 (accumulate || m0 > 0) ? 1 : 0, cur_stream(x));
+                                 (accumulate || m0 > 0) ? 1 : 0, (float)update_lr, cur_stream(x));
     TORCH_CHECK(rc == 0, "tdsa.linear_dw: bad launch shape");
   }
   check_launches("linear_dw");
@@ -429,6 +432,7 @@ TORCH_LIBRARY(tdsa, m) {
       "linear_bwd_into(Tensor dy, Tensor x, Tensor w, Tensor(a!)? dw_out, Tensor(b!)? db_out, float scale, "
       "bool accumulate, bool need_dx) -> Tensor",
       &linear_bwd_into);
-  m.def("linear_dw(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db, float scale, bool accumulate) -> ()",
+  m.def("linear_dw(Tensor dy, Tensor x, Tensor(a!) dw, Tensor(b!)? db, float scale, bool accumulate, "
+        "float update_lr=0.0) -> ()",
         &linear_dw);
 }

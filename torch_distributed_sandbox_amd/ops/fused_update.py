@@ -32,12 +32,19 @@ def unregister(param) -> None:
         delattr(param, _ATTR)
 
 
-def take(param):
-    """Learning rate for an in-backward update of ``param`` this step, or None."""
+def take(param, exchanged: bool = False):
+    """Learning rate for an in-backward update of ``param`` this step, or None.
+
+    ``exchanged=False``: asked by the kernel that produces the LOCAL gradient (world size 1
+    only).  ``exchanged=True``: asked by the fc gradient exchange (parallel/factored.py), whose
+    dW formation already sums every rank's rows, so the averaged step can be applied there at
+    any world size."""
     if param is None:
         return None
     fn = getattr(param, _ATTR, None)
-    return fn("query") if fn is not None else None
+    if fn is None:
+        return None
+    return fn("query_exchange" if exchanged else "query")
 
 
 def keep_grad(param) -> bool:

@@ -436,7 +436,7 @@ class DistributedDataParallel(nn.Module):
             if self._deferred and hasattr(optimizer, "set_deferred"):
                 optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred], self._run_deferred_update,
                                        lambda p: id(p) in self._fused_done)
-                if self.world_size == 1 and self.fuse_update_in_backward:
+                if self.fuse_update_in_backward and (self.world_size == 1 or self._exchanges):
                     self._register_fused_updates(optimizer)
         return optimizer
 
@@ -466,7 +466,13 @@ class DistributedDataParallel(nn.Module):
                         if what == "applied_no_grad":
                             self._mark_ready_without_grad(p)
                         return None
-                    # only a plain synchronised step whose gradient lands straight in the bucket
+                    # only a plain synchronised step whose gradient lands straight in the bucket;
+                    # a local gradient ("query") only at world size 1, the exchange's averaged one
+                    # ("query_exchange", parallel/factored.py) at any world size
+                    if what == "query" and self.world_size != 1:
+                        return None
+                    if what == "query_exchange" and self.keep_fused_grads:
+                        return None
                     if not self.require_backward_grad_sync or p.grad is not None or id(p) in self._fused_done:
                         return None
                     return plain_sgd_lr()

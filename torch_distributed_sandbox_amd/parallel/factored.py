@@ -331,6 +331,18 @@ class ActivationExchange:
         tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
         self._x_work.wait()
         scale = 1.0 / self.world
+        from ..ops import fused_update
+
+        # optimizer-in-backward (DDP overlap_optimizer, plain SGD, ops/fused_update.py): the
+        # averaged step is applied to the weight while its gradient is formed -- no dW in HBM and
+        # no separate SGD sweep over the 720 MB weight; .grad stays None
+        lr = fused_update.take(self.weight, exchanged=True) if dy.is_cuda else None
+        if lr:
+            with torch.no_grad():
+                self._finish_update(dy_all, rows, scale, float(lr))
+            fused_update.applied(self.weight)
+            self._done()
+            return
         with torch.no_grad():
             (dw, acc_w), (db, acc_b) = self._targets()
             if self.active == "activations":
@@ -351,10 +363,43 @@ class ActivationExchange:
         self.weight.grad = dw
         if self.bias is not None:
             self.bias.grad = db
+        self._done()
+
+    def _done(self):
         self.last_path = "activation-exchange" if self.active == "activations" else "sharded-exchange"
         self._x_buf = self._x_work = self._dy = self._x_local = None
         self.active = None
         self.steps_exchanged += 1
+
+    def _finish_update(self, dy_all, rows: int, scale: float, lr: float):
+        """Update-only finish: W -= lr * scale * dy_allᵀ X (activations: every column here;
+        sharded: this rank's column shard, then an all-gather of the UPDATED shards straight
+        into W); the bias keeps its gradient path (tiny, stepped by the optimizer)."""
+        from .. import _ext
+        from . import distributed as tdist
+
+        (_, _), (db, acc_b) = self._targets()
+        W = self.weight.data
+        ops = _ext.ops()
+        if self.active == "activations":
+            ops.linear_dw(dy_all, self._x_buf, W, db, scale, acc_b, lr)
+        else:
+            bounds = shard_bounds(W.shape[1], self.world)
+            me = tdist.get_rank(self.group)
+            k0, k1 = bounds[me]
+            if k1 > k0:
+                x_rows = self._x_buf.view(self.world * rows, k1 - k0)
+                ops.linear_dw(dy_all, x_rows, W[:, k0:k1], db, scale, acc_b, lr)
+            elif db is not None:
+                s_b = dy_all.sum(0).mul_(scale)
+                db.add_(s_b) if acc_b else db.copy_(s_b)
+            n_out = W.shape[0]
+            sends = [(W[c, k0:k1], s) for s in range(self.world) if s != me and k1 > k0 for c in range(n_out)]
+            recvs = [(W[c, a:e], s) for s, (a, e) in enumerate(bounds) if s != me and e > a for c in range(n_out)]
+            if sends or recvs:
+                tdist.sendrecv(sends, recvs, group=self.group, async_op=True).wait()
+        if self.bias is not None:
+            self.bias.grad = db
 
 
 def _dw_rows(dy_all, x_rows, dw, db, scale: float, acc_w: bool, acc_b: bool):
