@@ -104,7 +104,8 @@ def _worker(local, args):
     rank = int(os.environ.get("RANK", local))
     world = int(os.environ.get("WORLD_SIZE", args.gpus))
     on_gpu = args.device == "cuda"
-    dist.init_process_group(args.backend, rank=rank, world_size=world, device_id=local if on_gpu else None)
+    dist.init_process_group(args.backend, rank=rank, world_size=world, device_id=local if on_gpu else None,
+                            comm_cus=args.comm_cus)
     dev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
     rows = []
     sizes = _sizes(args.max_bytes) + ([] if args.no_ddp_sizes else sorted(DDP_SIZES.values()))
@@ -128,7 +129,8 @@ def _worker(local, args):
         for r in ex:
             bw = r["link_MB"] / r["us"] * 1e3 if r["us"] > 0 else 0.0
             print(f"{r['path']:<55} {r['us']:>10.1f} us  {r['link_MB']:>8.1f} MB/link  {bw:>7.2f} GB/s/link")
-        rec = {"backend": args.backend, "world": world, "device": args.device, "rows": rows, "exchanges": ex}
+        rec = {"backend": args.backend, "world": world, "device": args.device, "comm_cus": dist.comm_cus(),
+               "rows": rows, "exchanges": ex}
         print(json.dumps(rec))
         if args.out:
             with open(args.out, "w") as f:
@@ -140,6 +142,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--backend", default="rccl", help="rccl | rccl-native | gloo | host")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"])
+    ap.add_argument("--comm-cus", type=int, default=None,
+                    help="rccl-native: CUs the communicator's stream is confined to (default 32 at world > 1, "
+                         "as in training; 0 = unconfined)")
     ap.add_argument("--no-ddp-sizes", action="store_true", help="skip the 720 MB / 53 KB DDP bucket sizes")
     ap.add_argument("--exchanges", action="store_true", help="also time the fc-gradient paths (factored.py)")
     ap.add_argument("--rows", type=int, default=5, help="per-rank fc rows for --exchanges (bench: 5)")
