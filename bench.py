@@ -43,8 +43,8 @@ DTYPE = ("fp32 (conv1/conv2 fwd+dgrad+wgrad: bf16x3 split-precision MFMA with fp
 def _parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--image-size", type=int, default=3000)
     ap.add_argument("--batch-size", type=int, default=5, help="per-rank batch (reference: 5)")
     ap.add_argument("--mode", default="auto", choices=["auto", "fused", "layers"])
