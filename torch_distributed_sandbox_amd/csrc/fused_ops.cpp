@@ -53,7 +53,13 @@ Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shap
   return at::empty(shape, like.options().dtype(at::kFloat));
 }
 
-int l1_wg() { return tds_fused_num_wg(4); }
+// layer-1 conv workgroups per CU (grid-stride tile loop).  Sweep on MI355X (isolated layer-1
+// forward, ms): 2 -> 0.524, 4 -> 0.443, 6 -> 0.433, 8 -> 0.429; bench 3.62-3.63 vs 3.64-3.68 ms
+// per step at 4 (tools/gpu_sessions/r2_l1wg.sh)
+#ifndef TDS_L1_PER_CU
+#define TDS_L1_PER_CU 8
+#endif
+int l1_wg() { return tds_fused_num_wg(TDS_L1_PER_CU); }
 
 // Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
 // torch caching allocator, built once.  The map is never destroyed (no frees at process exit).
