@@ -19,7 +19,10 @@ namespace tds {
 // zeros by the descriptor's range check.  Each fp32
 // accumulator sums 4 * AC_RB = 32 products; waves reduce in fp32, the workgroup in fp64
 // (partial[wg][42], slot 41 = plain sum).  Requires W % 4 == 0.
-constexpr int AC_RB = 8;
+#ifndef TDS_AC_RB
+#define TDS_AC_RB 8
+#endif
+constexpr int AC_RB = TDS_AC_RB;
 
 static int x_autocorr_num_wg(int B, int H, int W) {
   if (W % 4 != 0 || B < 1 || H < 1) return 0;

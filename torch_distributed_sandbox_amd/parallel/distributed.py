@@ -28,6 +28,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import warnings
 from typing import Optional, Sequence
 
 import torch
@@ -135,10 +136,19 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
         if comm_cus > 0:
             from ..utils.streams import reserve_cus_for_comm
 
-            os.environ.setdefault("TDS_RCCL_MAX_CTAS", str(comm_cus))
+            if comm_cus % 32:
+                raise ValueError(f"comm_cus must be a multiple of 32 (one CU per shader engine), got {comm_cus}")
             # before the communicator exists: its stream takes the complement mask
-            torch.cuda.set_stream(reserve_cus_for_comm(comm_cus, torch.device("cuda", device_id)))
-            _state["comm_cus"] = comm_cus
+            try:
+                stream = reserve_cus_for_comm(comm_cus, torch.device("cuda", device_id))
+            except RuntimeError as e:  # no CU masking here: run unsplit
+                warnings.warn(f"init_process_group: CU split of {comm_cus} CUs unavailable ({e}); "
+                              "collectives share the CUs with the compute")
+                reserve_cus_for_comm(0)
+            else:
+                os.environ.setdefault("TDS_RCCL_MAX_CTAS", str(comm_cus))
+                torch.cuda.set_stream(stream)
+                _state["comm_cus"] = comm_cus
     dist.init_process_group(**kwargs)
     _state["backend"] = b
     _state["groups"] = {}
