@@ -127,7 +127,7 @@ std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
   auto fo = x.options().dtype(at::kDouble);
-  // one thread per 4 x 8 pixel block: each fp32 partial covers 32 products (fp64 beyond)
+  // one thread per 4 x 16 pixel block: each fp32 partial covers 64 products (fp64 beyond)
   const int nac = tds_x_autocorr_num_wg((int)B, (int)H, (int)W);
   TORCH_CHECK(nac > 0, "l1_input_stats: W % 4 == 0 required (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo);

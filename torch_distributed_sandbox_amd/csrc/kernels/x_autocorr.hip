@@ -17,10 +17,12 @@ namespace tds {
 // wave's lanes span at most two images of any size that matters, so lane offsets stay under
 // 4 GiB for images up to 2^29 pixels (23170^2) whatever the batch; lanes outside the image read
 // zeros by the descriptor's range check.  Each fp32
-// accumulator sums 4 * AC_RB = 32 products; waves reduce in fp32, the workgroup in fp64
+// accumulator sums 4 * AC_RB = 64 products; waves reduce in fp32, the workgroup in fp64
 // (partial[wg][42], slot 41 = plain sum).  Requires W % 4 == 0.
+// rows per thread: sweep on MI355X (isolated layer-1 forward, which includes this kernel):
+// 4 -> 0.488 ms, 8 -> 0.435, 16 -> 0.407 (tools/gpu_sessions/r2_acrb.sh)
 #ifndef TDS_AC_RB
-#define TDS_AC_RB 8
+#define TDS_AC_RB 16
 #endif
 constexpr int AC_RB = TDS_AC_RB;
 
