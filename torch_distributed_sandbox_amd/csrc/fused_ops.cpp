@@ -117,7 +117,7 @@ void check_l1_input(const Tensor& x, const char* what) {
 }
 
 // The weight-independent half of the BN1 statistics: the x autocorrelation sums (42 doubles)
-// and the border strips (9 x 82 doubles).  conv1 is linear in x, so BN1's batch mean and
+// and the per-image border strips (B x 8 x 82 doubles).  conv1 is linear in x, so BN1's batch mean and
 // variance are these moments contracted with w1 (tds_l1_gram); they depend on the batch only,
 // which lets an input pipeline produce them with the batch (on its own stream, beside the
 // previous step's backward) and hand them to fused_l1_forward.
@@ -131,7 +131,7 @@ std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
   const int nac = tds_x_autocorr_num_wg((int)B, (int)H, (int)W);
   TORCH_CHECK(nac > 0, "l1_input_stats: W % 4 == 0 required (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo);
-  auto strips = at::empty({9 * 82}, fo);
+  auto strips = at::empty({B * 8 * 82}, fo);
   tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, (int)B, (int)H, (int)W, st);
   // (on a side stream beside the autocorrelation the two kernels slowed each other: 176 + 94
   // us overlapped vs 99 + 35 us serial)
@@ -170,7 +170,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   if (asum_in.has_value() && asum_in->defined()) {
     TORCH_CHECK(strips_in.has_value() && strips_in->defined(), "fused_l1_forward: asum without strips");
     need(*asum_in, at::kDouble, {42}, "precomputed autocorrelation sums");
-    need(*strips_in, at::kDouble, {9 * 82}, "precomputed border strips");
+    need(*strips_in, at::kDouble, {B * 8 * 82}, "precomputed border strips");
     asum = *asum_in;
     strips = *strips_in;
   } else {

@@ -555,10 +555,16 @@ static_assert(4 * 16 * LB_NACC * 8 <= LB_NP * 64 + LB_NP * 16 + LB_XR * LM_XS * 
 //             + sum corners,  d = o_j - o_k  (see x_autocorr / x_border)
 //   S[j]    = sum of x over the pixels tap j sees (total - excluded lines + corners)
 // ac_sum: reduced autocorrelation [42] (slot 41 = plain sum).
-__device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips,
+__device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips_b,
                               const float* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
-                              double* full) {
+                              double* full, double* strips) {
   const int tid = threadIdx.x;
+  // per-image border strips [B][8][82] -> batch sums, images in order
+  for (int e = tid; e < 8 * 82; e += blockDim.x) {
+    double v = 0.0;
+    for (int b = 0; b < B; ++b) v += strips_b[(int64_t)b * 8 * 82 + e];
+    strips[e] = v;
+  }
   if (tid < 81) {
     const int dy = tid / 9 - 4, dx = tid % 9 - 4;
     int sy = dy, sx = dx;
@@ -627,7 +633,8 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
   __shared__ double G[25][25];
   __shared__ double S[25];
   __shared__ double Gw[16][25];
-  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full);
+  __shared__ double strips_sum[8 * 82];
+  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum);
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {

@@ -32,44 +32,43 @@ static int x_autocorr_num_wg(int B, int H, int W) {
   return (int)((threads + 255) / 256);
 }
 
-// Border strips (the Gram's edge corrections, l1_build_gram): for line L in {row 0, 1, H-2,
-// H-1, col 0, 1, W-2, W-1} and d in [-4,4]^2, strip[L][d] = sum over the batch and the line of
-// x(u) x(u+d); d index 81 = the plain line sum.  One workgroup per (d, L), launched after the
-// autocorrelation.  Measured alternatives, all slower: the border workgroups as the first 656
-// of the autocorrelation's own launch (they held its slots: 167 us for both vs 99 + 35 us),
-// the two kernels on separate streams (176 + 94 us overlapped), and workgroups per (line, dy,
-// line chunk) with the 9 dx products per pixel and chunk partials folded in l1_gram (45 us
-// here + 11 us more in l1_gram).
-__device__ void x_border_block(const float* __restrict__ x, double* __restrict__ strips, int B, int H, int W, int di,
-                               int L, double* sh) {
+// Border strips (the Gram's edge corrections, l1_build_gram): for image b, line L in {row 0, 1,
+// H-2, H-1, col 0, 1, W-2, W-1} and d in [-4,4]^2, strips[b][L][d] = sum over the line of
+// x(u) x(u+d); d index 81 = the plain line sum.  One workgroup per (d, L, b); l1_build_gram
+// sums the images in a fixed order.  (One workgroup per (d, L) looping over the batch ran 35 us,
+// latency-bound on its serial loop.)  Measured alternatives, all slower: the border workgroups
+// as the first 656 of the autocorrelation's own launch (they held its slots: 167 us for both
+// vs 99 + 35 us), the two kernels on separate streams (176 + 94 us overlapped), and workgroups
+// per (line, dy, line chunk) with the 9 dx products per pixel and chunk partials folded in
+// l1_gram (45 us here + 11 us more in l1_gram).
+__device__ void x_border_block(const float* __restrict__ x, double* __restrict__ strips, int H, int W, int di, int L,
+                               int b, double* sh) {
   const int dy = di / 9 - 4, dx = di % 9 - 4;
   const bool plain = di == 81;
   const bool is_row = L < 4;
   const int fixed = is_row ? (L < 2 ? L : H - 4 + L) : (L < 6 ? L - 4 : W - 8 + L);
   const int len = is_row ? W : H;
   double s = 0.0;
-  for (int b = 0; b < B; ++b) {
-    const float* xb = x + (int64_t)b * H * W;
-    for (int i = threadIdx.x; i < len; i += blockDim.x) {
-      const int r = is_row ? fixed : i, c = is_row ? i : fixed;
-      if (r < 0 || r >= H || c < 0 || c >= W) continue;
-      const float u = xb[(int64_t)r * W + c];
-      if (plain) {
-        s += u;
-      } else {
-        const int r2 = r + dy, c2 = c + dx;
-        if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) s += (double)u * xb[(int64_t)r2 * W + c2];
-      }
+  const float* xb = x + (int64_t)b * H * W;
+  for (int i = threadIdx.x; i < len; i += blockDim.x) {
+    const int r = is_row ? fixed : i, c = is_row ? i : fixed;
+    if (r < 0 || r >= H || c < 0 || c >= W) continue;
+    const float u = xb[(int64_t)r * W + c];
+    if (plain) {
+      s += u;
+    } else {
+      const int r2 = r + dy, c2 = c + dx;
+      if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) s += (double)u * xb[(int64_t)r2 * W + c2];
     }
   }
   s = block_sum(s, sh);
-  if (threadIdx.x == 0) strips[L * 82 + di] = s;
+  if (threadIdx.x == 0) strips[((int64_t)b * 8 + L) * 82 + di] = s;
 }
 
 __global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__ x, double* __restrict__ strips, int B,
                                                        int H, int W) {
   __shared__ double sh[8];
-  x_border_block(x, strips, B, H, W, blockIdx.x, blockIdx.y, sh);
+  x_border_block(x, strips, H, W, blockIdx.x, blockIdx.y, blockIdx.z, sh);
 }
 
 __global__ __launch_bounds__(256, 3) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
@@ -149,7 +148,7 @@ using namespace tds;
 int tds_x_autocorr_num_wg(int B, int H, int W) { return x_autocorr_num_wg(B, H, W); }
 
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(x_border_kernel, dim3(82, 8), dim3(256), 0, st, x, strips, B, H, W);
+  hipLaunchKernelGGL(x_border_kernel, dim3(82, 8, B), dim3(256), 0, st, x, strips, B, H, W);
   TDS_LAUNCH_CHECK();
 }
 

@@ -66,7 +66,7 @@ def supported(model, x) -> bool:
 
 
 def input_stats(x):
-    """(asum[42], strips[738]) fp64 x moments of a [B,1,H,W] fp32 batch, on the current stream."""
+    """(asum[42], strips[B*8*82]) fp64 x moments of a [B,1,H,W] fp32 batch, on the current stream."""
     return _ext.ops().l1_input_stats(x.contiguous())
 
 
