@@ -132,10 +132,8 @@ std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
   TORCH_CHECK(nac > 0, "l1_input_stats: W % 4 == 0 required (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo);
   auto strips = at::empty({B * 8 * 82}, fo);
-  tds_x_autocorr(x.data_ptr<float>(), ac.data_ptr<double>(), nac, (int)B, (int)H, (int)W, st);
-  // (on a side stream beside the autocorrelation the two kernels slowed each other: 176 + 94
-  // us overlapped vs 99 + 35 us serial)
-  tds_x_border(x.data_ptr<float>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, st);
+  tds_x_moments(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
+                st);
   auto asum = at::empty({42}, fo);
   tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
   check_launches("l1_input_stats");

@@ -100,7 +100,7 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
                              float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
                              float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_x_autocorr_num_wg(int B, int H, int W);  // partial rows tds_x_autocorr writes
-void tds_x_autocorr(const float* x, double* ac_partial, int nwg, int B, int H, int W, hipStream_t st);
+void tds_x_moments(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
 int tds_conv2_bwd_clock_read(uint32_t* host, int n);  // DIAG 13 per-wave barrier clocks (diag builds)
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st);  // border strips [B][8][82]
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,

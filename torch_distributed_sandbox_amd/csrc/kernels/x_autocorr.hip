@@ -71,9 +71,17 @@ __global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__
   x_border_block(x, strips, H, W, blockIdx.x, blockIdx.y, blockIdx.z, sh);
 }
 
+// Workgroups nac .. nac + 656 B - 1 of the launch (after every autocorrelation workgroup) are
+// border-strip workgroups (d, L, b): they fill the CUs the autocorrelation's tail frees.
 __global__ __launch_bounds__(256, 3) void x_autocorr_kernel(const float* __restrict__ x, double* __restrict__ partial,
-                                                         int B, int H, int W) {
+                                                         int B, int H, int W, double* __restrict__ strips, int nac) {
   __shared__ double red[4][42];
+  if ((int)blockIdx.x >= nac) {
+    __shared__ double sh[8];
+    const int j = (int)blockIdx.x - nac;
+    x_border_block(x, strips, H, W, j % 82, (j / 82) % 8, j / 656, sh);
+    return;
+  }
   const int blk = blockIdx.x;
   const int tid = threadIdx.x;
   const int ncg = W / 4, nband = (H + AC_RB - 1) / AC_RB;
@@ -152,11 +160,25 @@ void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream
   TDS_LAUNCH_CHECK();
 }
 
-void tds_x_autocorr(const float* x, double* ac_partial, int nwg, int B, int H, int W, hipStream_t st) {
+// one launch (measured: layer-1 forward 0.407 -> 0.402 ms, bench 3.73-3.75 vs 3.75-3.76 ms,
+// tools/gpu_sessions/r2_acmerge.sh); 0 = two launches
+#ifndef TDS_AC_MERGE_BORDER
+#define TDS_AC_MERGE_BORDER 1
+#endif
+
+// x moments for BN1: autocorrelation partials [nwg][42] and per-image border strips [B][8][82]
+// (TDS_AC_MERGE_BORDER: one launch, the border workgroups behind the autocorrelation's)
+void tds_x_moments(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
   if (nwg < 1 || nwg != x_autocorr_num_wg(B, H, W)) {  // the partial buffer is sized by tds_x_autocorr_num_wg
     tds_launch_fail("x_autocorr: workgroup count does not match the shape (needs W % 4 == 0)");
     return;
   }
-  hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W);
+  if (TDS_AC_MERGE_BORDER) {
+    hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg + 656 * B), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
+    TDS_LAUNCH_CHECK();
+    return;
+  }
+  hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
   TDS_LAUNCH_CHECK();
+  tds_x_border(x, strips, B, H, W, st);
 }
