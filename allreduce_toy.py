@@ -7,7 +7,8 @@ reference parses and ignores them); groups are cached, not re-created per step.
 
 Usage:
   python allreduce_toy.py -s 2 --backend gloo            # CPU, no GPU needed
-  python allreduce_toy.py -s 8 --backend rccl            # one rank per MI355X
+  python allreduce_toy.py -s 8 --backend rccl-native     # one rank per MI355X, native RCCL communicator
+  python allreduce_toy.py -s 8 --backend rccl            # torch's ProcessGroupNCCL (RCCL)
   python allreduce_toy.py -s 2 -r 0 -i tcp://HOST:PORT   # run one rank by hand (multi-node)
 """
 import argparse
@@ -23,7 +24,9 @@ find_free_port = launch.find_free_port
 
 
 def _device_for(backend, rank):
-    if dist._normalise_backend(backend) == "rccl":
+    # the device backends (torch's RCCL process group and this package's rccl-native
+    # communicator) all-reduce a tensor on cuda:{rank}, as the reference does (allreduce_toy.py:30)
+    if dist.is_device_backend(backend):
         return torch.device("cuda", rank % torch.cuda.device_count())
     return torch.device("cpu")
 
@@ -52,7 +55,9 @@ def setup(rank, world_size, backend="rccl", steps=20, init_method=None):
 
 def main(argv=None):
     parser = argparse.ArgumentParser()
-    parser.add_argument("--backend", type=str, default="auto", help="rccl|nccl|gloo|host|auto")
+    parser.add_argument("--backend", type=str, default="auto",
+                        help="rccl-native (this package's RCCL communicator; auto on GPU) | rccl/nccl (torch "
+                             "ProcessGroupNCCL) | gloo (auto on CPU) | host (this package's TCP ring)")
     parser.add_argument("-i", "--init-method", type=str, default=None,
                         help="URL specifying how to initialize the package (default: env:// with a free port)")
     parser.add_argument("-s", "--world_size", type=int, default=2, help="Number of processes participating in the job.")

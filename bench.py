@@ -24,6 +24,24 @@ MAX over ranks.  Rank 0 prints one JSON line.
 Default multi-GPU stack: this package's RCCL communicator (``rccl-native``:
 own comm stream, non-blocking init with a bounded wait, watchdog) and the C++
 gradient reducer; ``--backend rccl`` selects torch's ProcessGroupNCCL instead.
+
+Failure handling (a multi-GPU run must succeed or explain itself inside the
+driver's 600 s lease):
+
+* every wait is bounded below the lease: rendezvous / communicator init /
+  collectives by ``--pg-timeout`` (default 120 s), the whole rank by
+  ``--deadline`` (default 540 s from process start), the self-spawned job by
+  ``--spawn-timeout`` (default 570 s);
+* on any failure exactly one JSON line still comes out, with ``"value": null``,
+  ``"status": "failed"``, the failing rank, its error and the exit status;
+* fallback (``--fallback``, default on when no ``--backend`` was given): if the
+  ``rccl-native`` attempt fails on any rank, all ranks agree through the
+  rendezvous store, tear it down and run once more on torch's ProcessGroupNCCL
+  (RCCL) with the plain bucket all-reduce, no CU split -- inside the same
+  processes (nothing is re-exec'd), labelled ``"backend": "rccl (fallback:
+  <reason>)"``.  A self-spawned job whose rank crashed is re-spawned once the
+  same way, with fresh child processes, by the parent (which never touched the
+  GPU).
 """
 from __future__ import annotations
 
@@ -35,7 +53,11 @@ import time
 
 import torch
 
+_T_START = time.time()  # process start (the --deadline clock)
+
 METRIC = "images/sec (whole node), 3000x3000 MNIST ConvNet DDP at 1/2/4/8 MI355X"
+MODEL = "ConvNet(conv5x5 1->16+BN+ReLU+pool2, conv5x5 16->32+BN+ReLU+pool2, fc 32*(H/4)^2->10)"
+DATA = "synthetic (seeded 28x28 uint8 sources upsampled on device to HxW; random labels; random init)"
 DTYPE = ("fp32 (conv1/conv2 fwd+dgrad+wgrad: bf16x3 split-precision MFMA with fp32 accumulate; "
          "BN, fc, CE, SGD: fp32)")
 
@@ -81,36 +103,88 @@ def _parser():
                          "--sim-comm-ctas workgroups of RCCL's size (256 threads, 19.7 KB LDS) for this many "
                          "microseconds on a side stream (recorded in the JSON; not a training number)")
     ap.add_argument("--sim-comm-ctas", type=int, default=16)
-    ap.add_argument("--spawn-timeout", type=float, default=1800.0,
+    ap.add_argument("--spawn-timeout", type=float, default=570.0,
                     help="self-spawn: terminate all ranks if the job runs longer than this (s)")
+    ap.add_argument("--pg-timeout", type=float, default=120.0,
+                    help="rendezvous, communicator init and per-collective timeout (s)")
+    ap.add_argument("--deadline", type=float, default=540.0,
+                    help="a rank still running this long after its start prints the failure record and exits (s)")
+    ap.add_argument("--fallback", action=argparse.BooleanOptionalAction, default=None,
+                    help="after a failed rccl-native attempt, run once more on torch's RCCL process group with "
+                         "the plain bucket all-reduce (default: on unless --backend is given)")
     return ap
 
 
-def _rank_entry(i: int, argv, world: int, master_addr: str, master_port: str):
+def _rank_entry(i: int, argv, world: int, master_addr: str, master_port: str, fallback_reason):
     os.environ.update({"RANK": str(i), "LOCAL_RANK": str(i), "WORLD_SIZE": str(world),
-                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": master_addr, "MASTER_PORT": master_port})
-    run(argv)
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": master_addr, "MASTER_PORT": master_port,
+                       "TDS_BENCH_CHILD": "1"})  # the spawning parent prints any failure record
+    if fallback_reason:
+        os.environ["TDS_BENCH_FALLBACK_REASON"] = fallback_reason
+    rc = run_rank(argv)
+    if rc:
+        sys.exit(rc)
+
+
+def _short(err: str, n: int = 400) -> str:
+    """The last meaningful line(s) of an error / traceback, bounded."""
+    lines = [ln.strip() for ln in str(err).strip().splitlines() if ln.strip()]
+    tail = " | ".join(lines[-2:]) if lines else str(err)
+    return tail[-n:]
+
+
+def _fail_record(args, world: int, failed_rank, error: str, rc: int, extra=None) -> dict:
+    cfg = {"model": MODEL, "global_batch": world * args.batch_size, "per_rank_batch": args.batch_size,
+           "seq_len": None, "image_size": [args.image_size, args.image_size], "parallelism": f"dp{world}"}
+    cfg.update(extra or {})
+    return {"metric": METRIC, "value": None, "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": DTYPE, "data": DATA, "status": "failed", "failed_rank": failed_rank,
+            "error": error, "rc": rc, "elapsed_s": round(time.time() - _T_START, 1), "config": cfg}
 
 
 def _spawn_ranks(args, argv) -> int:
-    """One process per GPU, started here (no GPU call happens in this parent)."""
+    """One process per GPU, started here (no GPU call happens in this parent).  If the job
+    fails (a rank raised, crashed or timed out) and no --backend was forced, it is re-spawned
+    ONCE with fresh rank processes on torch's RCCL process group with the plain bucket
+    all-reduce; if that fails too (or there is no time left) one failure record is printed."""
+    import tempfile
+
     from torch_distributed_sandbox_amd.parallel import launch
 
     addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
-    port = os.environ.get("MASTER_PORT") or launch.find_free_port(addr)
-    try:
-        launch.spawn(_rank_entry, args=(list(argv), args.gpus, addr, str(port)), nprocs=args.gpus,
-                     timeout=args.spawn_timeout)
-    except launch.ProcessRaisedException as e:
-        print(f"bench.py: rank {e.error_index} failed:{e}", file=sys.stderr, flush=True)
-        return 1
-    except launch.ProcessExitedException as e:
-        print(f"bench.py: {e}", file=sys.stderr, flush=True)
-        return e.exit_code if e.exit_code and e.exit_code > 0 else 1
-    except TimeoutError as e:
-        print(f"bench.py: {e}", file=sys.stderr, flush=True)
-        return 124
-    return 0
+    fallback = args.fallback if args.fallback is not None else args.backend is None
+    plans = [(list(argv), None)]
+    if fallback and args.device == "cuda":
+        plans.append((list(argv) + ["--backend", "rccl", "--grad-exchange", "allreduce", "--no-fallback"], "retry"))
+    fail = None
+    for k, (av, label) in enumerate(plans):
+        remaining = args.spawn_timeout - (time.time() - _T_START)
+        if k > 0 and remaining < 90:
+            break
+        port = (os.environ.get("MASTER_PORT") if k == 0 else None) or launch.find_free_port(addr)
+        reason = None if label is None else f"rank {fail[0]} of the first spawn: {fail[1]}"
+        with tempfile.TemporaryDirectory(prefix="tds_bench_") as td:
+            os.environ["TDS_BENCH_RESULT_FILE"] = os.path.join(td, "result.json")
+            try:
+                launch.spawn(_rank_entry, args=(av, args.gpus, addr, str(port), reason), nprocs=args.gpus,
+                             timeout=max(30.0, remaining))
+                return 0
+            except launch.ProcessRaisedException as e:
+                fail = (e.error_index, _short(str(e)), 1)
+            except launch.ProcessExitedException as e:
+                fail = (e.error_index, str(e), e.exit_code if e.exit_code and e.exit_code > 0 else 1)
+            except TimeoutError as e:
+                fail = (None, str(e), 124)
+            finally:
+                printed = os.path.exists(os.environ.pop("TDS_BENCH_RESULT_FILE"))
+            print(f"bench.py: spawn attempt {k} failed: rank {fail[0]}: {fail[1]}", file=sys.stderr, flush=True)
+            if printed:  # rank 0 already printed the measurement; the failure came after it (teardown)
+                return 0
+    print(json.dumps(_fail_record(args, args.gpus, fail[0], fail[1], fail[2],
+                                  {"spawn_attempts": len(plans) if fallback and args.device == "cuda" else 1})),
+          flush=True)
+    return fail[2]
 
 
 def _allreduce_probe(tdist, device, world, on_gpu):
@@ -147,19 +221,158 @@ def main(argv=None) -> int:
     args = _parser().parse_args(argv)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return _spawn_ranks(args, argv)
-    run(argv)
-    return 0
+    return run_rank(argv)
 
 
-def run(argv) -> None:
+def run_rank(argv) -> int:
+    """One rank: the attempts (rccl-native, then the torch-RCCL fallback), bounded by the
+    --deadline watchdog.  Rank 0 prints exactly one JSON line -- the measurement or, unless a
+    spawning parent reports for it, the failure record."""
+    import threading
+
     args = _parser().parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}")
+    child = os.environ.get("TDS_BENCH_CHILD") == "1"
+    phase = ["start"]
+    done = threading.Event()
+
+    def watchdog():
+        left = args.deadline - (time.time() - _T_START)
+        if done.wait(max(0.0, left)):
+            return
+        msg = f"rank {rank} still running {args.deadline:.0f} s after its start (phase: {phase[0]})"
+        print(f"bench.py: {msg}; exiting", file=sys.stderr, flush=True)
+        if rank == 0 and not child:
+            print(json.dumps(_fail_record(args, world, rank, msg, 124)), flush=True)
+        os._exit(124)
+
+    threading.Thread(target=watchdog, daemon=True, name="bench-deadline").start()
+    try:
+        rec = _run_attempts(args, world, rank, phase)
+    except BaseException as e:  # noqa: BLE001 -- reported, then re-raised for the exit status
+        msg = f"{type(e).__name__}: {_short(str(e))}"
+        print(f"bench.py: rank {rank} failed in phase {phase[0]}: {msg}", file=sys.stderr, flush=True)
+        if rank == 0 and not child:
+            print(json.dumps(_fail_record(args, world, rank, msg, 1, {"phase": phase[0]})), flush=True)
+        done.set()
+        if child:
+            raise
+        return 1
+    done.set()
+    if rank == 0 and rec is not None:
+        line = json.dumps(rec)
+        path = os.environ.get("TDS_BENCH_RESULT_FILE")
+        if path:
+            with open(path, "w") as f:
+                f.write(line + "\n")
+        print(line, flush=True)
+    return 0
+
+
+def _make_store(args, rank: int, world: int):
+    """The rendezvous store every attempt shares (each attempt under its own prefix), so the
+    ranks can agree on a fallback even when a communicator could not be created."""
+    import datetime
+
+    import torch.distributed as dist
+
+    addr = os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.setdefault("MASTER_PORT", "29533"))
+    return dist.TCPStore(addr, port, world, is_master=(rank == 0),
+                         timeout=datetime.timedelta(seconds=args.pg_timeout), wait_for_workers=True)
+
+
+def _run_attempts(args, world: int, rank: int, phase):
+    import datetime
+    import gc
+
+    import torch.distributed as dist
+
     on_gpu = args.device == "cuda"
-    backend = args.backend or ("rccl-native" if on_gpu else "gloo")
+    from torch_distributed_sandbox_amd.parallel.distributed import default_backend
+
+    backend = args.backend or default_backend(on_gpu)
+    fallback = args.fallback if args.fallback is not None else (args.backend is None and on_gpu)
+    label = None
+    if os.environ.get("TDS_BENCH_FALLBACK_REASON"):
+        label = f"{backend} (fallback: {os.environ['TDS_BENCH_FALLBACK_REASON']})"
+    attempts = [(backend, args.grad_exchange, args.reserve_cus, label)]
+    # the conservative stack: torch's own process group (RCCL on the GPU, gloo on a CPU
+    # rehearsal), plain bucket all-reduce, no CU split
+    plain = "rccl" if on_gpu else "gloo"
+    if fallback and world > 1 and backend != plain:
+        attempts.append((plain, "allreduce", 0, None))
+    dist_needed = world > 1 or args.grad_exchange in ("activations", "sharded", "chunked")
+    store = _make_store(args, rank, world) if dist_needed else None
+    # a collective that stalls raises (after --pg-timeout) instead of killing the rank, so the
+    # ranks can still agree on the fallback and report
+    os.environ.setdefault("TDS_RCCL_ERROR_HANDLING", "raise")
+    os.environ.setdefault("TDS_RCCL_INIT_TIMEOUT_MS", str(int(args.pg_timeout * 1000)))
+    reason = None
+    for k, (be, gx, reserve, lab) in enumerate(attempts):
+        if reason is not None:
+            lab = f"{be} (fallback: {reason})"
+        last = k == len(attempts) - 1
+        ok, err, rec = True, None, None
+        try:
+            rec = _attempt(args, world, rank, be, gx, reserve, lab, store, k, phase)
+        except Exception as e:  # noqa: BLE001
+            ok, err = False, f"{type(e).__name__}: {_short(str(e))}"
+            if last:
+                raise
+            del e
+        if store is None or len(attempts) == 1:
+            return rec
+        # every rank reports its attempt; all take the same decision
+        phase[0] = f"vote after attempt {k}"
+        store.set_timeout(datetime.timedelta(seconds=2 * args.pg_timeout + 30))
+        store.set(f"bench/vote{k}/{rank}", "ok" if ok else ("fail " + err)[:600])
+        votes = [store.get(f"bench/vote{k}/{r}").decode(errors="replace") for r in range(world)]
+        bad = [(r, v[5:]) for r, v in enumerate(votes) if v != "ok"]
+        # name the root cause: a rank that failed by itself before one that timed out waiting for it
+        bad.sort(key=lambda rv: ("timed out" in rv[1] or "timeout" in rv[1].lower(), rv[0]))
+        if not bad:
+            _teardown(abort=False)
+            return rec
+        if last:
+            raise RuntimeError(f"rank {bad[0][0]} failed: {bad[0][1]}")
+        reason = f"rank {bad[0][0]}: {bad[0][1]}"[:300]
+        print(f"bench.py: rank {rank}: attempt {k} ({be}) failed ({reason}); falling back", file=sys.stderr,
+              flush=True)
+        rec = None
+        _teardown(abort=True)
+        gc.collect()
+        if on_gpu:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    return None
+
+
+def _teardown(abort: bool) -> None:
+    from torch_distributed_sandbox_amd.parallel import distributed as tdist
+    from torch_distributed_sandbox_amd.parallel.rccl_backend import native_comm_of
+
+    if not tdist.is_initialized():
+        return
+    if abort:
+        comm, kind = native_comm_of(None)
+        if kind == "rccl":
+            comm.abort("bench fallback")
+    else:
+        tdist.barrier()
+    tdist.destroy_process_group()
+
+
+def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, store, k, phase):
+    """One full benchmark run (init, model, warmup, timed steps) on ``backend``; returns rank 0's
+    record (None elsewhere).  The process group is left up for the caller's vote/teardown."""
+    import datetime
+
+    import torch.distributed as dist
+
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    on_gpu = args.device == "cuda"
     if args.shared_device:
         if backend != "gloo":
             raise SystemExit("bench.py: --shared-device is a rehearsal mode and needs --backend gloo")
@@ -173,7 +386,10 @@ def run(argv) -> None:
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
     from torch_distributed_sandbox_amd.parallel import distributed as tdist
     from torch_distributed_sandbox_amd.parallel.rccl_backend import native_comm_of
+    from torch_distributed_sandbox_amd.utils import fault
 
+    phase[0] = f"attempt {k} ({backend}): init"
+    fault.maybe_inject_bench(rank, "init")
     if on_gpu:
         assert torch.cuda.is_available(), "bench.py needs a GPU (use --device cpu for a CPU rehearsal)"
         torch.cuda.set_device(local_rank)
@@ -186,12 +402,9 @@ def run(argv) -> None:
     # (default 32 CUs at world > 1); otherwise --reserve-cus masks the compute side only
     if args.rccl_max_ctas > 0:
         os.environ["TDS_RCCL_MAX_CTAS"] = str(args.rccl_max_ctas)
-    reserve = args.reserve_cus
-    if world > 1 or args.grad_exchange in ("activations", "sharded", "chunked"):
-        if world == 1:
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29533")
-        tdist.init_process_group(backend, rank=rank, world_size=world,
+    if store is not None:
+        tdist.init_process_group(backend, rank=rank, world_size=world, store=dist.PrefixStore(f"attempt{k}", store),
+                                 timeout=datetime.timedelta(seconds=args.pg_timeout),
                                  device_id=local_rank if on_gpu and backend != "gloo" else None,
                                  comm_cus=reserve if backend == "rccl-native" else None)
     if backend == "rccl-native" and tdist.is_initialized():
@@ -207,21 +420,22 @@ def run(argv) -> None:
         comm, kind = native_comm_of(None)
         if kind == "rccl":
             rccl_ranks = int(comm.comm_count())
-            # sanity: one collective over the live communicator before anything is timed
-            t = torch.full((1,), float(rank + 1), device=device)
-            tdist.all_reduce(t)
-            want = world * (world + 1) / 2
-            if float(t.item()) != want:
-                raise RuntimeError(f"rccl-native sanity all-reduce gave {float(t.item())}, expected {want}")
+        # sanity: one collective over the live communicator before anything is timed
+        t = torch.full((1,), float(rank + 1), device=device)
+        tdist.all_reduce(t)
+        want = world * (world + 1) / 2
+        if float(t.item()) != want:
+            raise RuntimeError(f"{backend} sanity all-reduce gave {float(t.item())}, expected {want}")
 
     H = W = args.image_size
     B = args.batch_size
     torch.manual_seed(0)
+    phase[0] = f"attempt {k} ({backend}): model"
     model = ConvNet(image_shape=(H, W), device=device, mode=args.mode)
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), 1e-4)
     ddp = DistributedDataParallel(model, device_ids=[local_rank] if on_gpu else None, bucket_cap_mb=args.bucket_mb,
-                                  grad_exchange=args.grad_exchange, overlap_optimizer=args.overlap_optimizer,
+                                  grad_exchange=grad_exchange, overlap_optimizer=args.overlap_optimizer,
                                   allreduce_chunks=args.allreduce_chunks)
 
     ddp.attach_optimizer(optimizer)
@@ -297,9 +511,12 @@ def run(argv) -> None:
             torch.cuda.synchronize()
 
     loss = None
+    phase[0] = f"attempt {k} ({backend}): warmup"
     for i in range(args.warmup):
+        fault.maybe_inject_bench(rank, "step")
         loss = step(i)
     sync_all()
+    phase[0] = f"attempt {k} ({backend}): timed steps"
     t0 = time.perf_counter()
     for i in range(args.steps):
         loss = step(args.warmup + i)
@@ -310,12 +527,13 @@ def run(argv) -> None:
         tdist.all_reduce(t, tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item()) if loss is not None else None
+    phase[0] = f"attempt {k} ({backend}): report"
     probe = _allreduce_probe(tdist, device, world, on_gpu) if world > 1 and args.allreduce_probe else None
     ms = 1e3 * elapsed / max(1, args.steps)
     imgs_per_sec = world * B * args.steps / elapsed
     if rank == 0:
         config = {
-            "model": "ConvNet(conv5x5 1->16+BN+ReLU+pool2, conv5x5 16->32+BN+ReLU+pool2, fc 32*(H/4)^2->10)",
+            "model": MODEL,
             "global_batch": world * B,
             "per_rank_batch": B,
             "seq_len": None,
@@ -323,7 +541,8 @@ def run(argv) -> None:
             "parallelism": f"dp{world}",
             "mode": args.mode,
             "device": args.device,
-            "backend": backend if world > 1 else None,
+            "backend": (backend_label or backend) if world > 1 else None,
+            "attempt": k,
             "rccl_ranks": rccl_ranks,
             "reducer": ddp.reducer_kind,
             "overlap_optimizer": ddp.overlap_optimizer,
@@ -355,13 +574,11 @@ def run(argv) -> None:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": DTYPE,
-            "data": "synthetic (seeded 28x28 uint8 sources upsampled on device to HxW; random labels; random init)",
+            "data": DATA,
             "config": config,
         }
-        print(json.dumps(rec), flush=True)
-    if tdist.is_initialized():
-        tdist.barrier()
-        tdist.destroy_process_group()
+        return rec
+    return None
 
 
 if __name__ == "__main__":

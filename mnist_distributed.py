@@ -25,7 +25,9 @@ def main(argv=None):
     parser.add_argument("-n", "--nodes", default=1, type=int, metavar="N", help="number of nodes")
     parser.add_argument("-g", "--gpus", default=1, type=int, help="number of gpus (ranks) per node")
     parser.add_argument("-nr", "--nr", default=0, type=int, help="ranking within the nodes")
-    parser.add_argument("--backend", default="auto", help="rccl|nccl|gloo|host|auto")
+    parser.add_argument("--backend", default="auto",
+                        help="rccl-native (auto on GPU: this package's RCCL communicator + C++ reducer, the stack "
+                             "bench.py measures) | rccl/nccl (torch ProcessGroupNCCL) | gloo (auto on CPU) | host")
     parser.add_argument("--master-addr", default=None)
     parser.add_argument("--master-port", default=None)
     parser.add_argument("--avg-loss", action="store_true", help="log the global-average loss (all_reduce AVG)")

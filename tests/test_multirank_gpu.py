@@ -28,7 +28,7 @@ def _data(world):
     return xs, ys
 
 
-def _worker(rank, world, port, mode, overlap, out):
+def _worker(rank, world, port, mode, overlap, out, plan="fused"):
     os.environ.update({"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
@@ -39,7 +39,7 @@ def _worker(rank, world, port, mode, overlap, out):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
-    m = ConvNet(image_shape=(H, H), device=dev, mode="fused")
+    m = ConvNet(image_shape=(H, H), device=dev, mode=plan)
     ddp = DistributedDataParallel(m, grad_exchange=mode, overlap_optimizer=overlap)
     opt = ddp.attach_optimizer(SGD(m.parameters(), LR))
     crit = CrossEntropyLoss()
@@ -85,10 +85,23 @@ def _ref_step(params, bufs, x, y):
 @pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("mode", ["allreduce", "activations", "sharded", "chunked"])
 def test_fused_ddp_two_ranks_matches_fp64_average(gpu, tmp_path, mode, overlap):
+    _check_two_ranks(tmp_path, mode, overlap, "fused")
+
+
+@pytest.mark.parametrize("mode", ["activations", "sharded"])
+def test_layers_plan_exchange_overlap_matches_fp64_average(gpu, tmp_path, mode):
+    """The generic per-layer plan's exchanged Linear under the overlapped optimizer: its
+    backward computes dX from the fc weight and then hands dY to the exchange, whose side
+    stream updates that same weight in place -- dX (and through it every conv gradient) must
+    see the pre-update weight (dX was once queued after the exchange)."""
+    _check_two_ranks(tmp_path, mode, True, "layers")
+
+
+def _check_two_ranks(tmp_path, mode, overlap, plan):
     from torch_distributed_sandbox_amd.parallel import launch
 
     world = 2
-    launch.spawn(_worker, args=(world, launch.find_free_port(), mode, overlap, str(tmp_path)), nprocs=world,
+    launch.spawn(_worker, args=(world, launch.find_free_port(), mode, overlap, str(tmp_path), plan), nprocs=world,
                  timeout=240)
     recs = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
     assert recs[0]["fc_grad"] == {"allreduce": "allreduce", "activations": "activation-exchange",

@@ -120,7 +120,8 @@ def test_bench_spawn_failure_propagates_cpu():
     p = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "32", "--steps", "1", "--warmup", "0",
               "--backend", "host", "--shared-device"], timeout=200)
     assert p.returncode != 0
-    assert not _json_lines(p.stdout)
+    (r,) = _json_lines(p.stdout)  # one failure record, no measurement
+    assert r["status"] == "failed" and r["value"] is None and "shared-device" in r["error"]
 
 
 def test_bench_allreduce_cpu_rehearsal():
@@ -132,3 +133,84 @@ def test_bench_allreduce_cpu_rehearsal():
     rec = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
     assert rec["world"] == 2 and len(rec["rows"]) == 6
     assert [r["path"].split()[0] for r in rec["exchanges"]] == ["activations", "sharded", "chunked", "allreduce"]
+
+
+# ---- W=8 rehearsal and bounded failure handling (bench.py's first real multi-GPU run must
+# succeed or explain itself inside the driver's lease)
+
+@pytest.mark.parametrize("backend", ["gloo", "host"])
+def test_bench_w8_cpu(backend):
+    """The 8-rank path end to end: self-spawn, rendezvous, the W=8 fc-gradient choice (sharded
+    exchange by the byte model) and the one JSON line."""
+    # 256^2: the fc weight (10 x 131072) is big enough to be an exchange candidate
+    p = _run(["bench.py", "--gpus", "8", "--device", "cpu", "--image-size", "256", "--steps", "1", "--warmup", "1",
+              "--backend", backend, "--no-allreduce-probe"], timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (r,) = _json_lines(p.stdout)
+    assert r["n_gpus"] == 8 and r["config"]["global_batch"] == 40 and r["config"]["parallelism"] == "dp8"
+    assert r["config"]["fc_grad"] == "sharded-exchange"
+    assert r["config"]["reducer"] == ("native" if backend == "host" else "python")
+
+
+def test_bench_rank_that_never_joins_reports_json():
+    """A rank that never reaches the rendezvous: the job ends within the bounded waits and the
+    parent prints ONE failure record naming the failing rank."""
+    import time
+
+    t0 = time.time()
+    p = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "32", "--steps", "1", "--warmup", "1",
+              "--backend", "gloo", "--pg-timeout", "8", "--deadline", "60", "--spawn-timeout", "90"],
+             env={"TDS_BENCH_FAULT": "1:init:hang"}, timeout=200)
+    assert time.time() - t0 < 150
+    assert p.returncode != 0
+    (r,) = _json_lines(p.stdout)
+    assert r["status"] == "failed" and r["value"] is None and r["n_gpus"] == 2
+    assert r["failed_rank"] in (0, 1) and r["error"] and r["rc"] != 0
+
+
+def test_bench_rank_deadline_reports_json_under_torchrun_env():
+    """Run as one rank of an externally launched job (WORLD_SIZE set, the driver's torchrun
+    form) that cannot finish: rank 0 itself prints the failure record at its deadline."""
+    p = _run(["bench.py", "--gpus", "1", "--device", "cpu", "--image-size", "32", "--steps", "1", "--warmup", "2",
+              "--deadline", "20"],
+             env={"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0", "TDS_BENCH_FAULT": "0:step:hang"}, timeout=200)
+    assert p.returncode == 124
+    (r,) = _json_lines(p.stdout)
+    assert r["status"] == "failed" and "still running" in r["error"]
+
+
+def test_bench_falls_back_after_a_failed_attempt_cpu():
+    """Attempt 0 (the native host backend) fails on rank 1 mid-warmup; every rank votes through
+    the rendezvous store, tears the group down and the plain stack (gloo, bucket all-reduce)
+    produces the measurement, labelled with the reason."""
+    p = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "32", "--steps", "1", "--warmup", "1",
+              "--backend", "host", "--fallback", "--pg-timeout", "15", "--no-allreduce-probe"],
+             env={"TDS_BENCH_FAULT": "1:step:raise:1"}, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (r,) = _json_lines(p.stdout)
+    assert r["value"] > 0 and r["config"]["attempt"] == 1
+    assert r["config"]["backend"].startswith("gloo (fallback: rank 1")
+    assert "InjectedFault" in r["config"]["backend"]
+
+
+def test_trainer_and_bench_pick_the_same_stack(monkeypatch):
+    """mnist_distributed.py (trainer) and bench.py default to the same multi-GPU stack on a GPU:
+    rccl-native (this package's communicator, so the C++ reducer) with the CU split."""
+    import argparse
+
+    sys.path.insert(0, ROOT)
+    import bench
+    from torch_distributed_sandbox_amd.parallel import distributed as tdist
+    from torch_distributed_sandbox_amd.trainer import add_common_args, resolve_backend
+
+    monkeypatch.setattr(torch.cuda, "is_available", lambda: True)
+    targs = add_common_args(argparse.ArgumentParser()).parse_args([])
+    targs.backend = "auto"
+    bargs = bench._parser().parse_args([])
+    assert bargs.backend is None and bargs.device == "cuda"
+    assert resolve_backend(targs) == tdist.default_backend(bargs.device == "cuda") == "rccl-native"
+    assert tdist._normalise_backend("auto") == "rccl-native"
+    assert tdist.is_device_backend("rccl-native") and tdist.is_device_backend("nccl")
+    assert not tdist.is_device_backend("gloo")
+    targs.backend = "rccl"
+    assert resolve_backend(targs) == "rccl"  # torch's ProcessGroupNCCL stays selectable

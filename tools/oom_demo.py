@@ -12,10 +12,14 @@ fitting 288 GB is much larger.  This script:
    the out-of-memory error (expected),
 3. runs --steps steps at batch 5 on the same image size (fits) and reports
    peak memory and images/sec,
-4. under torchrun with N ranks: step 3 is the DDP run, effective batch 5N.
+4. with --gpus N (ranks started here, one per GPU, like bench.py and the reference's
+   mp.spawn) or under torchrun with N ranks: step 2 runs on rank 0 alone, step 3 is the
+   DDP run over all ranks, effective batch 5N.
 
-    python tools/oom_demo.py --image-size 18000
-    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 tools/oom_demo.py --image-size 18000
+    python tools/oom_demo.py --image-size 18000                  # 1 GPU
+    python tools/oom_demo.py --gpus 8 --image-size 18000         # the DDP half: 8 ranks
+    python tools/oom_demo.py --gpus 2 --shared-device --image-size 1024 --calib-size 512
+                                                                 # rehearsal: 2 gloo ranks on cuda:0
 """
 import argparse
 import gc
@@ -82,50 +86,85 @@ def run(H, B, steps, device, world, rank):
             "images_per_sec_node": round(world * B / dt, 2) if dt else None}
 
 
-def main():
+def _parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--image-size", type=int, default=18000)
     ap.add_argument("--bs-fail", type=int, default=10)
     ap.add_argument("--bs-fit", type=int, default=5)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--calib-size", type=int, default=3000)
-    args = ap.parse_args()
-    from torch_distributed_sandbox_amd.parallel import distributed as tdist
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU) started by this script")
+    ap.add_argument("--backend", default=None, help="process group for --gpus > 1 (default: rccl-native)")
+    ap.add_argument("--shared-device", action="store_true",
+                    help="rehearsal: every rank on cuda:0 over gloo (plumbing only, not an OOM result)")
+    ap.add_argument("--timeout", type=float, default=1800.0, help="--gpus > 1: terminate the ranks after this (s)")
+    return ap
 
+
+def _rank_entry(i, argv, world, addr, port):
+    os.environ.update({"RANK": str(i), "LOCAL_RANK": str(i), "WORLD_SIZE": str(world), "LOCAL_WORLD_SIZE": str(world),
+                       "MASTER_ADDR": addr, "MASTER_PORT": port})
+    main(argv)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = _parser().parse_args(argv)
+    from torch_distributed_sandbox_amd.parallel import distributed as tdist
+    from torch_distributed_sandbox_amd.parallel import launch
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the parent starts one rank per GPU and never touches the GPU itself
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        launch.spawn(_rank_entry, args=(argv, args.gpus, addr, launch.find_free_port(addr)), nprocs=args.gpus,
+                     timeout=args.timeout)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.shared_device else int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
-    if world > 1:
-        tdist.init_process_group("rccl", rank=rank, world_size=world, device_id=local)
     H = args.image_size
-    total = torch.cuda.get_device_properties(device).total_memory
-    act, fixed = calibrate(args.calib_size, device)
-    gc.collect()
-    torch.cuda.empty_cache()
-    rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1), "world_size": world,
-           "model": {"calibrated_at": args.calib_size, "act_bytes_per_px_per_image": round(act, 1),
-                     "fixed_bytes_per_px": round(fixed, 1),
-                     "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed) / 1e9, 1)
-                                      for b in (args.bs_fit, args.bs_fail)},
-                     "predicted_oom_edge_bs%d" % args.bs_fail:
-                         int((total / (args.bs_fail * act + fixed)) ** 0.5)}}
-    # 1) batch 10 on one GPU (every rank tries it alone: no collective inside)
-    try:
-        r = run(H, args.bs_fail, 1, device, 1, rank) if world == 1 else None
-        rec["bs_fail_result"] = {"oom": False, **(r or {})}
-    except torch.cuda.OutOfMemoryError as e:
-        msg = str(e).split("\n")[0]
-        rec["bs_fail_result"] = {"oom": True, "error": msg[:300]}
-    gc.collect()
-    torch.cuda.empty_cache()
-    # 2) batch 5 per rank (DDP over all ranks when launched with torchrun)
-    rec["bs_fit_result"] = run(H, args.bs_fit, args.steps, device, world, rank)
-    rec["effective_batch"] = args.bs_fit * world
+    rec = None
     if rank == 0:
+        # the single-GPU half runs on rank 0 BEFORE the process group exists (DDP at world size
+        # 1, no collective); the other ranks wait in the rendezvous meanwhile
+        total = torch.cuda.get_device_properties(device).total_memory
+        act, fixed = calibrate(args.calib_size, device)
+        gc.collect()
+        torch.cuda.empty_cache()
+        rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1), "world_size": world,
+               "model": {"calibrated_at": args.calib_size, "act_bytes_per_px_per_image": round(act, 1),
+                         "fixed_bytes_per_px": round(fixed, 1),
+                         "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed) / 1e9, 1)
+                                          for b in (args.bs_fit, args.bs_fail)},
+                         "predicted_oom_edge_bs%d" % args.bs_fail:
+                             int((total / (args.bs_fail * act + fixed)) ** 0.5)}}
+        if args.shared_device:
+            rec["shared_device"] = True  # rehearsal: all ranks on one GPU
+        # 1) batch 10 on ONE GPU
+        try:
+            r = run(H, args.bs_fail, 1, device, 1, rank)
+            rec["bs_fail_result"] = {"oom": False, **r}
+        except torch.cuda.OutOfMemoryError as e:
+            msg = str(e).split("\n")[0]
+            rec["bs_fail_result"] = {"oom": True, "error": msg[:300]}
+        gc.collect()
+        torch.cuda.empty_cache()
+    if world > 1:
+        import datetime
+
+        backend = "gloo" if args.shared_device else (args.backend or tdist.default_backend(True))
+        tdist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(hours=1),
+                                 device_id=None if backend == "gloo" else local)
+    # 2) batch 5 per rank: DDP over all ranks
+    fit = run(H, args.bs_fit, args.steps, device, world, rank)
+    if rank == 0:
+        rec["bs_fit_result"] = fit
+        rec["effective_batch"] = args.bs_fit * world
         print(json.dumps(rec), flush=True)
     if world > 1:
+        tdist.barrier()
         tdist.destroy_process_group()
 
 

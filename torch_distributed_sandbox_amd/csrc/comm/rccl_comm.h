@@ -128,12 +128,44 @@ struct RcclState {
   std::condition_variable cv;
   bool stop = false;  // guarded by mu
 
+  // Completion events are pooled: a collective's event is shared by its Work and the
+  // watchdog's pending entry and goes back to the pool when both have let go, so the hot
+  // path (2-40 collectives per step on the exchange paths) creates no events after warm-up.
+  std::mutex pool_mu;
+  std::vector<hipEvent_t> event_pool;  // guarded by pool_mu
+  ~RcclState() {
+    for (hipEvent_t e : event_pool) (void)hipEventDestroy(e);
+  }
+
   struct Pending {
-    hipEvent_t done;
+    std::shared_ptr<hipEvent_t> done;
     std::chrono::steady_clock::time_point start;
     std::string what;
   };
   std::deque<Pending> pending;  // guarded by mu
+
+  // A pooled event, returned to the pool (not destroyed) once the last holder drops it.
+  static std::shared_ptr<hipEvent_t> take_event(const std::shared_ptr<RcclState>& self) {
+    hipEvent_t e = nullptr;
+    {
+      std::lock_guard<std::mutex> g(self->pool_mu);
+      if (!self->event_pool.empty()) {
+        e = self->event_pool.back();
+        self->event_pool.pop_back();
+      }
+    }
+    if (e == nullptr) TDS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    std::weak_ptr<RcclState> weak = self;
+    return std::shared_ptr<hipEvent_t>(new hipEvent_t(e), [weak](hipEvent_t* p) {
+      if (auto st = weak.lock()) {
+        std::lock_guard<std::mutex> g(st->pool_mu);
+        st->event_pool.push_back(*p);
+      } else {
+        (void)hipEventDestroy(*p);
+      }
+      delete p;
+    });
+  }
 
   void check_ok() {
     if (aborted.load()) {
@@ -169,28 +201,26 @@ struct RcclState {
 
 struct RcclWork : CommWork {
   std::shared_ptr<RcclState> st;
-  hipEvent_t done = nullptr;
+  std::shared_ptr<hipEvent_t> done;  // pooled (RcclState::take_event)
   int device = 0;
 
-  RcclWork(std::shared_ptr<RcclState> s, hipEvent_t e) : st(std::move(s)), done(e), device(st->device) {}
-  ~RcclWork() override {
-    if (done) (void)hipEventDestroy(done);
-  }
+  RcclWork(std::shared_ptr<RcclState> s, std::shared_ptr<hipEvent_t> e)
+      : st(std::move(s)), done(std::move(e)), device(st->device) {}
 
   void wait() override {
     st->check_ok();
     c10::hip::HIPGuard g((c10::DeviceIndex)device);
-    TDS_HIP(hipStreamWaitEvent(c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream(), done, 0));
+    TDS_HIP(hipStreamWaitEvent(c10::hip::getCurrentHIPStream((c10::DeviceIndex)device).stream(), *done, 0));
   }
   bool is_completed() override {
     st->check_ok();
-    return hipEventQuery(done) == hipSuccess;
+    return hipEventQuery(*done) == hipSuccess;
   }
   void synchronize() override {
     const auto t0 = std::chrono::steady_clock::now();
     while (true) {
       st->check_ok();
-      hipError_t e = hipEventQuery(done);
+      hipError_t e = hipEventQuery(*done);
       if (e == hipSuccess) return;
       TORCH_CHECK(e == hipErrorNotReady, "rccl work: ", hipGetErrorString(e));
       if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(st->timeout_ms)) {
@@ -495,22 +525,32 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     // comm stream waits for the producer work already queued on the caller's stream
     TDS_HIP(hipEventRecord(ready_, cur));
     TDS_HIP(hipStreamWaitEvent(cs, ready_, 0));
+    // An RCCL error inside fn (including a non-blocking call that did not settle within the
+    // timeout) aborts the communicator -- after comm_mu is released, so the abort (and the
+    // watchdog, which polls under the same lock) can take it -- instead of leaving it in flight.
+    std::string err;
     {
       std::lock_guard<std::mutex> cl(st_->comm_mu);
       st_->check_ok();
-      fn(st_->comm, cs);
+      try {
+        fn(st_->comm, cs);
+      } catch (const std::exception& e) {
+        err = e.what();
+      }
+    }
+    if (!err.empty()) {
+      st_->fail(std::string(what) + ": " + err);
+      st_->check_ok();
+      TORCH_CHECK(false, what, ": ", err);
     }
     for (const auto& t : ts) c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), stream_);
-    hipEvent_t done;
-    TDS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
-    TDS_HIP(hipEventRecord(done, cs));
-    // the watchdog tracks its own event (the Work may be dropped before completion)
-    hipEvent_t wd;
-    TDS_HIP(hipEventCreateWithFlags(&wd, hipEventDisableTiming));
-    TDS_HIP(hipEventRecord(wd, cs));
+    // one pooled event serves the Work and the watchdog (which keeps it alive if the Work is
+    // dropped before completion)
+    auto done = RcclState::take_event(st_);
+    TDS_HIP(hipEventRecord(*done, cs));
     {
       std::lock_guard<std::mutex> gl(st_->mu);
-      st_->pending.push_back({wd, std::chrono::steady_clock::now(), what});
+      st_->pending.push_back({done, std::chrono::steady_clock::now(), what});
     }
     if (st_->debug_sync) debug_sync_check(cs, what);
     return c10::make_intrusive<RcclWork>(st_, done);
@@ -542,10 +582,9 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
       std::string why;
       while (!s->pending.empty()) {
         auto& p = s->pending.front();
-        hipError_t e = hipEventQuery(p.done);
+        hipError_t e = hipEventQuery(*p.done);
         if (e == hipSuccess) {
-          (void)hipEventDestroy(p.done);
-          s->pending.pop_front();
+          s->pending.pop_front();  // back to the pool once the Work is gone too
           continue;
         }
         if (e != hipErrorNotReady) {

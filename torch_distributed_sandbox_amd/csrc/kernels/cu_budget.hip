@@ -20,6 +20,10 @@ namespace {
 constexpr int kMaxDev = 64;
 std::atomic<int> g_cus[kMaxDev];
 std::atomic<int> g_reserve{0};
+std::atomic<bool> g_striped{true};  // mask-bit numbering of the last compute mask (tds_cu_masked_stream)
+
+// Index of CU bit `cu` inside its XCD under either numbering (see tds_cu_masked_stream).
+inline int cu_local(int cu, int nxcd, int per, bool striped) { return striped ? cu / nxcd : cu % per; }
 }  // namespace
 
 int tds_device_cus() {
@@ -59,29 +63,31 @@ hipStream_t tds_cu_masked_stream(int device, int reserve, bool striped) {
     if (n % nxcd == 0 && per - rx >= 1) {
       std::vector<uint32_t> mask((n + 31) / 32, 0u);
       for (int cu = 0; cu < n; ++cu) {
-        const int local = striped ? cu / nxcd : cu % per;  // the CU's index inside its XCD
-        if (local < per - rx) mask[cu / 32] |= 1u << (cu % 32);
+        if (cu_local(cu, nxcd, per, striped) < per - rx) mask[cu / 32] |= 1u << (cu % 32);
       }
       if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) s = nullptr;
     }
   }
   (void)hipSetDevice(prev);
+  if (s) g_striped.store(striped, std::memory_order_relaxed);
   return s;
 }
 
 // The communication side of the split: a stream of `device` confined to the CUs the compute
-// stream leaves out (the complement of tds_cu_masked_stream's striped mask for the current
-// reserve), so RCCL's kernels -- launched on the communicator's stream -- land on CUs no
-// persistent compute workgroup waits for.  nullptr when no CUs are reserved.  Cached per
-// (device, reserve); the streams live for the process.
+// stream leaves out (the exact complement of tds_cu_masked_stream's mask for the current reserve,
+// in the same bit numbering), so RCCL's kernels -- launched on the communicator's stream -- land
+// on CUs no persistent compute workgroup waits for.  nullptr when no CUs are reserved.  Cached
+// per (device, reserve, numbering); the streams live for the process.
 hipStream_t tds_cu_comm_stream(int device) {
   const int reserve = g_reserve.load(std::memory_order_relaxed);
+  const bool striped = g_striped.load(std::memory_order_relaxed);
   if (reserve <= 0 || reserve % 8 != 0 || device < 0 || device >= kMaxDev) return nullptr;
+  const int key = reserve * 2 + (striped ? 1 : 0);
   static std::mutex mu;
   static std::vector<std::pair<std::pair<int, int>, hipStream_t>> cache;
   std::lock_guard<std::mutex> g(mu);
   for (auto& e : cache)
-    if (e.first.first == device && e.first.second == reserve) return e.second;
+    if (e.first.first == device && e.first.second == key) return e.second;
   int prev = 0;
   if (hipGetDevice(&prev) != hipSuccess) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
@@ -92,12 +98,12 @@ hipStream_t tds_cu_comm_stream(int device) {
     if (n % nxcd == 0 && per - rx >= 1) {
       std::vector<uint32_t> mask((n + 31) / 32, 0u);
       for (int cu = 0; cu < n; ++cu)
-        if (cu / nxcd >= per - rx) mask[cu / 32] |= 1u << (cu % 32);
+        if (cu_local(cu, nxcd, per, striped) >= per - rx) mask[cu / 32] |= 1u << (cu % 32);
       if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) s = nullptr;
     }
   }
   (void)hipSetDevice(prev);
-  if (s) cache.push_back({{device, reserve}, s});
+  if (s) cache.push_back({{device, key}, s});
   return s;
 }
 

@@ -186,13 +186,18 @@ class _ExchangedLinear(torch.autograd.Function):
     def backward(ctx, gy):
         x2, w = ctx.saved_tensors
         gy = gy.contiguous()
-        ctx.ex.defer(gy, x2)
         dx = None
         if ctx.needs_input_grad[0]:
             if gy.is_cuda and x2.shape[0] <= 8 and w.shape[0] <= 16:
                 dx = _ext.ops().linear_bwd_into(gy, x2, w.contiguous(), None, None, 1.0, False, True)
             else:
                 dx = gy.mm(w)
+        # only now: on the GPU defer() issues the rest of the exchange on a side stream right
+        # away, and under the overlapped optimizer that includes the in-place SGD step of w
+        # (update-only linear_dw) -- the dX kernel above must be queued first, or the side
+        # stream could update w while dX still reads it (the stream wait in defer() orders the
+        # side stream after everything already on this one)
+        ctx.ex.defer(gy, x2)
         return dx, None, None, None
 
 

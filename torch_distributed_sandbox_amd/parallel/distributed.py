@@ -13,7 +13,7 @@ Backends
                          registered with torch.distributed as a custom backend.
 ``"rccl-native"``        this package's C++ RCCL communicator (own comm stream,
                          event works, watchdog/abort; ``parallel/rccl_backend.py``).
-``None``                 ``rccl`` when a GPU is visible, else ``gloo``
+``None`` / ``"auto"``     ``rccl-native`` when a GPU is visible, else ``gloo``
                          (the reference's auto-switch, test_init.py:84-88).
 
 Fixes vs the reference (documented deviations):
@@ -51,9 +51,22 @@ _state = {
 }
 
 
+def default_backend(on_gpu: Optional[bool] = None) -> str:
+    """The tuned stack every entry point uses unless told otherwise (bench.py, the trainers,
+    the toy): this package's RCCL communicator + C++ reducer on the GPU, gloo on the CPU."""
+    if on_gpu is None:
+        on_gpu = torch.cuda.is_available()
+    return "rccl-native" if on_gpu else "gloo"
+
+
+def is_device_backend(backend: Optional[str]) -> bool:
+    """Does ``backend`` move device (GPU) tensors (RCCL: torch's or this package's)?"""
+    return _normalise_backend(backend) in ("rccl", "rccl-native")
+
+
 def _normalise_backend(backend: Optional[str]) -> str:
     if backend is None or backend == "auto":
-        return "rccl" if torch.cuda.is_available() else "gloo"
+        return default_backend()
     b = backend.lower()
     if b in ("nccl", "rccl", "cuda", "hip"):
         return "rccl"
@@ -146,12 +159,34 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
                               "collectives share the CUs with the compute")
                 reserve_cus_for_comm(0)
             else:
-                os.environ.setdefault("TDS_RCCL_MAX_CTAS", str(comm_cus))
+                if "TDS_RCCL_MAX_CTAS" not in os.environ:
+                    os.environ["TDS_RCCL_MAX_CTAS"] = str(comm_cus)
+                    _state["set_max_ctas"] = True
+                _state["prev_stream"] = torch.cuda.current_stream(device_id)
                 torch.cuda.set_stream(stream)
                 _state["comm_cus"] = comm_cus
-    dist.init_process_group(**kwargs)
+    try:
+        dist.init_process_group(**kwargs)
+    except BaseException:
+        _undo_cu_split()
+        raise
     _state["backend"] = b
     _state["groups"] = {}
+
+
+def _undo_cu_split() -> None:
+    """Reverse what init_process_group's CU split changed in this process: the persistent
+    kernels' CU reserve, the current (CU-masked) stream and a TDS_RCCL_MAX_CTAS it exported."""
+    if _state.pop("set_max_ctas", False):
+        os.environ.pop("TDS_RCCL_MAX_CTAS", None)
+    prev = _state.pop("prev_stream", None)
+    if _state.get("comm_cus", 0):
+        from .. import _ext
+
+        _ext.ops().set_cu_reserve(0)
+        if prev is not None:
+            torch.cuda.set_stream(prev)
+    _state["comm_cus"] = 0
 
 
 def comm_cus() -> int:
@@ -166,6 +201,7 @@ def destroy_process_group(group=None) -> None:
         _state["groups"] = {}
         _state["backend"] = None
         dist.destroy_process_group()
+        _undo_cu_split()
     else:
         for k, g in list(_state["groups"].items()):
             if g is group:

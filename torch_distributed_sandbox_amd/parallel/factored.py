@@ -132,15 +132,14 @@ class ActivationExchange:
             return self.mode
         if self.mode == "chunked":
             return "chunked" if self.chunks > 1 else None
-        if self.world <= 1:
+        if self.world <= 1 or self.mode != "auto":
             return None
-        p = "allreduce"
-        if self.mode == "auto":
-            out_f, in_f = self.weight.shape
-            p = choose_path(rows, out_f, in_f, self.world)
-        if p == "allreduce":
-            return "chunked" if self.chunks > 1 else None
-        return p
+        out_f, in_f = self.weight.shape
+        p = choose_path(rows, out_f, in_f, self.world)
+        # auto's all-reduce regime is the plain bucket all-reduce: the chunked path costs more
+        # compute than it saves on the links (W=1 forced: +4.4 ms/step, docs/DISTRIBUTED.md), so
+        # it runs only when asked for
+        return None if p == "allreduce" else p
 
     def needs_rows(self) -> bool:
         """Does the running exchange need the layer's input rows (X) from its forward?"""

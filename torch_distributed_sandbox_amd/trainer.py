@@ -50,7 +50,19 @@ def add_common_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--overlap-optimizer", action=argparse.BooleanOptionalAction, default=True,
                    help="finish the fc bucket (collective + SGD) on a side stream under the next forward")
     p.add_argument("--bucket-mb", default=None, type=float, help="DDP bucket cap (MB, default 25 like torch)")
+    p.add_argument("--reserve-cus", default=None, type=int,
+                   help="rccl-native: CUs split off for the collectives (multiple of 32; default 32 at world > 1)")
     return p
+
+
+def resolve_backend(args) -> str:
+    """--backend, or the tuned default (parallel.distributed.default_backend): rccl-native on
+    the GPU -- the stack bench.py measures -- and gloo on the CPU."""
+    b = getattr(args, "backend", None)
+    if b in (None, "auto"):
+        on_gpu = args.device != "cpu" and torch.cuda.is_available()
+        return tdist.default_backend(on_gpu)
+    return tdist._normalise_backend(b)
 
 
 def _device(args, gpu: int) -> torch.device:
@@ -70,11 +82,12 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
     if distributed:
         rank = args.nr * args.gpus + gpu
         world = args.world_size
-        backend = args.backend
-        if backend in (None, "auto"):
-            backend = "rccl" if (args.device != "cpu" and torch.cuda.is_available()) else "gloo"
+        backend = resolve_backend(args)
+        dev_backend = tdist.is_device_backend(backend)
+        # the same stack bench.py measures: rccl-native + C++ reducer + the compute/comm CU split
         tdist.init_process_group(backend=backend, world_size=world, rank=rank,
-                                 device_id=gpu if tdist._normalise_backend(backend) == "rccl" else None)
+                                 device_id=gpu if dev_backend else None,
+                                 comm_cus=getattr(args, "reserve_cus", None) if backend == "rccl-native" else None)
     device = _device(args, gpu)
     torch.manual_seed(0)
     H = W = args.image_size
