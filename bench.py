@@ -58,8 +58,9 @@ _T_START = time.time()  # process start (the --deadline clock)
 METRIC = "images/sec (whole node), 3000x3000 MNIST ConvNet DDP at 1/2/4/8 MI355X"
 MODEL = "ConvNet(conv5x5 1->16+BN+ReLU+pool2, conv5x5 16->32+BN+ReLU+pool2, fc 32*(H/4)^2->10)"
 DATA = "synthetic (seeded 28x28 uint8 sources upsampled on device to HxW; random labels; random init)"
-DTYPE = ("fp32 (conv1/conv2 fwd+dgrad+wgrad: bf16x3 split-precision MFMA with fp32 accumulate; "
-         "BN, fc, CE, SGD: fp32)")
+DTYPE = ("fp32 (conv1 fwd+wgrad: bf16x3 split-precision MFMA; conv2 fwd+dgrad+wgrad: fp16x2 split MFMA -- one "
+         "operand exact as fp16 hi+lo, the other rounded once, <= 2^-11 per product = the TF32 unit roundoff of the "
+         "reference's cuDNN convs; fp32 accumulate; BN, fc, CE, SGD: fp32)")
 
 
 def _parser():
@@ -77,6 +78,8 @@ def _parser():
     ap.add_argument("--grad-exchange", default="auto",
                     choices=["auto", "allreduce", "activations", "sharded", "chunked"],
                     help="fc gradient path under DDP (parallel/factored.py); auto picks by the xGMI byte model")
+    ap.add_argument("--exchange-compress", action=argparse.BooleanOptionalAction, default=True,
+                    help="send the activation exchange's fc input rows zero-suppressed (lossless, parallel/zs.py)")
     ap.add_argument("--allreduce-chunks", type=int, default=None,
                     help="K-chunks of the fc weight gradient in the all-reduce regime (default 4 on GPU)")
     ap.add_argument("--reserve-cus", type=int, default=None,
@@ -436,7 +439,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     optimizer = SGD(model.parameters(), 1e-4)
     ddp = DistributedDataParallel(model, device_ids=[local_rank] if on_gpu else None, bucket_cap_mb=args.bucket_mb,
                                   grad_exchange=grad_exchange, overlap_optimizer=args.overlap_optimizer,
-                                  allreduce_chunks=args.allreduce_chunks)
+                                  allreduce_chunks=args.allreduce_chunks, exchange_compress=args.exchange_compress)
 
     ddp.attach_optimizer(optimizer)
 
@@ -548,6 +551,8 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             "overlap_optimizer": ddp.overlap_optimizer,
             "fc_grad": ddp.fc_grad_path(),
             "allreduce_chunks": ddp.allreduce_chunks,
+            "x_exchange": [{"ratio": round(ex.x_ratio, 4), **ex.zs_stats} for ex in ddp.exchanges if ex.compress
+                           and ex.zs_stats["steps"]] or None,
             "reserve_cus": reserve,
             "prefetch": data_stream is not None,
             "rccl_max_ctas": rccl_max_ctas or None,

@@ -156,3 +156,31 @@ def test_upsample(gpu):
     # bilinear weights in fp32 vs fp64 may round a half differently: <= 1 LSB
     assert (y.double().cpu() - ref).abs().max().item() <= 1.0 / 255 + 1e-6
     assert ((y.double().cpu() - ref).abs() > 1e-6).float().mean().item() < 1e-3
+
+
+@pytest.mark.parametrize("n", [1, 2047, 2048, 100_003, 3 * 2048 * 5])
+def test_zs_encode_decode_matches_reference(gpu, n):
+    """Zero-suppressed fc-row codec (csrc/kernels/zs_exchange.hip) vs the torch reference of
+    parallel/zs.py: identical meta and values, a bitwise round trip, -0.0 and NaN kept, values
+    past the capacity dropped (count still exact)."""
+    from torch_distributed_sandbox_amd.parallel import zs
+
+    torch.manual_seed(n % 97)
+    x = torch.relu(torch.randn(n, device=gpu))
+    x[::9] = -0.0
+    if n > 10:
+        x[3] = float("nan")
+    meta = torch.empty(zs.meta_numel(n), dtype=torch.int32, device=gpu)
+    vals = torch.empty(n, device=gpu)
+    nnz = zs.encode(x, meta, vals)
+    rmeta, rvals, rnnz = zs.encode_ref(x.cpu())
+    assert int(nnz) == rnnz
+    assert torch.equal(meta.cpu(), rmeta)
+    assert torch.equal(vals[:rnnz].cpu().view(torch.int32), rvals.view(torch.int32))
+    out = torch.full((n,), 3.0, device=gpu)
+    zs.decode(meta, vals[:max(1, rnnz)], out)
+    assert torch.equal(out.view(torch.int32), x.view(torch.int32))
+    if rnnz > 8:  # capacity below the count: the count stays exact, the extra values are dropped
+        small = torch.full((rnnz // 2,), -1.0, device=gpu)
+        assert int(zs.encode(x, meta, small)) == rnnz
+        assert torch.equal(small.cpu().view(torch.int32), rvals[:rnnz // 2].view(torch.int32))

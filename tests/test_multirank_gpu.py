@@ -104,7 +104,7 @@ def _check_two_ranks(tmp_path, mode, overlap, plan):
     launch.spawn(_worker, args=(world, launch.find_free_port(), mode, overlap, str(tmp_path), plan), nprocs=world,
                  timeout=240)
     recs = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
-    assert recs[0]["fc_grad"] == {"allreduce": "allreduce", "activations": "activation-exchange",
+    assert recs[0]["fc_grad"] == {"allreduce": "allreduce", "activations": "activation-exchange(zs)",
                                   "sharded": "sharded-exchange", "chunked": "chunked-allreduce"}[mode]
     fused_expected = overlap and mode in ("activations", "sharded")
     assert (recs[0]["steps"][0]["grads"]["fc.weight"] is None) == fused_expected

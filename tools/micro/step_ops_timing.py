@@ -62,10 +62,11 @@ def main():
                                             n1.running_var, n1.num_batches_tracked, 0.1, 1e-5)
 
         def pack():
-            st["pack"] = ops.conv2_pack(c2.weight)
+            st["mag"] = torch.zeros(33, dtype=torch.int32, device=x.device)
+            st["pack"] = ops.conv2_pack(c2.weight, st["mag"])
 
         def c2f():
-            st["c2"] = ops.fused_conv2_forward(st["l1"][0], st["pack"][0], c2.bias, n2.weight)
+            st["c2"] = ops.fused_conv2_forward(st["l1"][0], st["pack"][0], c2.bias, n2.weight, st["mag"])
 
         def hf():
             y2, partial2, ya = st["c2"]
@@ -78,12 +79,13 @@ def main():
 
         def hb():
             _, stats2, aff2 = st["hf"]
-            st["hb"] = ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, n2.weight, fc.weight, P, dw, 1.0, True)
+            st["hb"] = ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, n2.weight, fc.weight, P, dw, 1.0, True,
+                                               mag=st["mag"])
 
         def c2b():
             y2 = st["c2"][0]
             g2m, kbuf = st["hb"][4], st["hb"][5]
-            st["c2b"] = ops.fused_conv2_backward_y2(y2, g2m, st["hf"][2], kbuf, st["l1"][0], st["pack"][1], 1.0)
+            st["c2b"] = ops.fused_conv2_backward_y2(y2, g2m, st["hf"][2], kbuf, st["mag"], st["l1"][0], st["pack"][1], 1.0)
 
         def l1b():
             p1, idx1, stats1, gram = st["l1"]

@@ -1,12 +1,13 @@
 // Plan-level ops of the fused ConvNet execution (torch.ops.tdsa.fused_*).
 // Each op = a few kernel launches on the current stream, all shapes checked on
-// the host first.  Tensor "carriers": packed bf16 hi|lo activations are handed
-// to autograd as float32 tensors of the same byte size, so that gradients line
-// up shape-for-shape:
-//   p1 carrier  [B,P,P,16] f32  == bytes of bf16 [B,P,P,32] (hi16|lo16)   <-> dp1  [B,P,P,16] f32
+// the host first.  Activation formats:
+//   p1          [B,P,P,16] fp16 (conv2's single-rounded fp16x2 operand; its fp32 gradient dp1
+//               [B,P,P,16] travels to the layer-1 backward beside autograd, models/convnet_fused.py)
 //   y2          [B,P,P,32] f32
 //   ya          [B,32,PB] f32: pooled-blocked planes (kernels/pooled_layout.h)
 //   g2m         [B,32,Q,Q] f32: planar pooled gradient
+//   mag         [33] int32: the step's magnitude bounds (max |y2| per channel, max |g2m|, float
+//               bits) behind the conv2 backward's fp16 gradient scale; reset by conv2_pack
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -181,8 +182,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W,
               w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps,
               (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
-  // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1, argmax
-  auto p1 = at::empty({B, P, P, 16}, fo);  // carrier of bf16 [B,P,P,32]
+  // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1 (fp16), argmax
+  auto p1 = at::empty({B, P, P, 16}, fo.dtype(at::kHalf));
   auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
   tds_l1_apply(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(), p1.data_ptr(),
                idx1.data_ptr<uint8_t>(), l1_wg(), (int)B, (int)H, (int)W, st);
@@ -191,12 +192,20 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
 }
 
 // ---------------------------------------------------------------- conv2 forward
-std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2) {
+uint32_t* opt_mag(const c10::optional<Tensor>& mag) {
+  if (!mag.has_value() || !mag->defined()) return nullptr;
+  need(*mag, at::kInt, {33}, "mag (magnitude bounds)");
+  return reinterpret_cast<uint32_t*>(mag->data_ptr<int>());
+}
+
+// fp16 hi/lo weight packs of the conv2 forward and data gradient; resets mag when given
+std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tensor>& mag) {
   need(w2, at::kFloat, {32, 16, 5, 5}, "conv2.weight");
   c10::DeviceGuard guard(w2.device());
   auto wp = at::empty({2 * 13 * 2 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
   auto wd = at::empty({2 * 25 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
-  tds_conv2_pack_weights(w2.data_ptr<float>(), wp.data_ptr<int16_t>(), wd.data_ptr<int16_t>(), stream_of(w2));
+  tds_conv2_pack_weights(w2.data_ptr<float>(), wp.data_ptr<int16_t>(), wd.data_ptr<int16_t>(), opt_mag(mag),
+                         stream_of(w2));
   check_launches("conv2_pack");
   return {wp, wd};
 }
@@ -204,10 +213,11 @@ std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2) {
 // returns (y2 [B,P,P,32], BN2 partials, ya [B,32,PB]: y2 at each 2x2 window's argmax of the BN2
 // output, resolved by the sign of gamma2)
 std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& wp, const Tensor& b2,
-                                                       const c10::optional<Tensor>& gamma2) {
-  TORCH_CHECK(p1.dim() == 4 && p1.size(1) == p1.size(2) && p1.size(3) == 16, "fused_conv2_forward: p1 carrier");
+                                                       const c10::optional<Tensor>& gamma2,
+                                                       const c10::optional<Tensor>& mag) {
+  TORCH_CHECK(p1.dim() == 4 && p1.size(1) == p1.size(2) && p1.size(3) == 16, "fused_conv2_forward: p1 [B,P,P,16]");
   const int64_t B = p1.size(0), P = p1.size(1);
-  need(p1, at::kFloat, {B, P, P, 16}, "p1");
+  need(p1, at::kHalf, {B, P, P, 16}, "p1");
   need(wp, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
   need(b2, at::kFloat, {32}, "conv2.bias");
   const float* g = optf(gamma2, 32, "bn2.weight");
@@ -221,7 +231,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const T
   auto ya = at::empty({B, 32, pb_plane(P)}, p1.options());
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
   tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr<float>(),
-                 ya.data_ptr<float>(), partial.data_ptr<double>(), order, nwg, (int)B, (int)P, stream_of(p1));
+                 ya.data_ptr<float>(), partial.data_ptr<double>(), opt_mag(mag), order, nwg, (int)B, (int)P,
+                 stream_of(p1));
   check_launches("fused_conv2_forward");
   return {y2, partial, ya};
 }
@@ -314,7 +325,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     const c10::optional<Tensor>& gamma2, const Tensor& wfc, int64_t P, const c10::optional<Tensor>& dw_out,
     double scale, bool compute_dw, double update_lr, const c10::optional<Tensor>& dbfc_out,
     const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out, bool keep_dw, int64_t c_begin,
-    int64_t c_end, bool finalize, const c10::optional<Tensor>& g2m_out, const c10::optional<Tensor>& partial_out) {
+    int64_t c_end, bool finalize, const c10::optional<Tensor>& g2m_out, const c10::optional<Tensor>& partial_out,
+    const c10::optional<Tensor>& mag) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_backward: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_backward: needs P/2 >= 4 pooled columns and B >= 1");
@@ -366,7 +378,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
                                  dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
                                  compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                  upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
-                                 (float)scale, (float)update_lr, (int)c_begin, (int)c_end, st);
+                                 (float)scale, (float)update_lr, (int)c_begin, (int)c_end,
+                                 opt_mag(mag) ? opt_mag(mag) + 32 : nullptr, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
   if (!finalize) {
     check_launches("fused_head_backward");
@@ -387,11 +400,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
 // ---------------------------------------------------------------- conv2 backward
 // BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2, g2m, aff2, kbuf, p1) -> (dp1, dw2, db2)
 std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& g2m, const Tensor& aff2,
-                                                           const Tensor& kbuf, const Tensor& p1, const Tensor& wd,
-                                                           double scale, const c10::optional<Tensor>& dw_out,
+                                                           const Tensor& kbuf, const Tensor& mag, const Tensor& p1,
+                                                           const Tensor& wd, double scale,
+                                                           const c10::optional<Tensor>& dw_out,
                                                            const c10::optional<Tensor>& db_out) {
   const int64_t B = p1.size(0), P = p1.size(1);
-  need(p1, at::kFloat, {B, P, P, 16}, "p1");
+  need(p1, at::kHalf, {B, P, P, 16}, "p1");
+  need(mag, at::kInt, {33}, "mag (magnitude bounds of the forward and the head backward)");
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
   need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
   need(aff2, at::kFloat, {64}, "aff2");
@@ -409,8 +424,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
   tds_conv2_bwd3(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
-                 p1.data_ptr(), wd.data_ptr<int16_t>(), dp1.data_ptr<float>(), slab.data_ptr<float>(), order, nwg,
-                 (int)B, (int)P, st);
+                 reinterpret_cast<const uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(), wd.data_ptr<int16_t>(),
+                 dp1.data_ptr<float>(), slab.data_ptr<float>(), order, nwg, (int)B, (int)P, st);
   tds_conv2_wgrad_reduce(slab.data_ptr<float>(), nwg, dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, st);
   check_launches("fused_conv2_backward_y2");
   return {dp1, dw2, db2};
@@ -477,7 +492,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3), P = H / 2;
   need(x, at::kFloat, {B, 1, H, W}, "x");
   need(dp1, at::kFloat, {B, P, P, 16}, "dp1");
-  need(p1, at::kFloat, {B, P, P, 16}, "p1");
+  need(p1, at::kHalf, {B, P, P, 16}, "p1");
   need(idx1, at::kByte, {B, P, P, 16}, "idx1");
   need(w1, at::kFloat, {16, 1, 5, 5}, "conv1.weight");
   need(b1, at::kFloat, {16}, "conv1.bias");
@@ -503,18 +518,55 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   return {dw1, db1, dg, dbe};
 }
 
+// ---------------------------------------------------------------- zero-suppressed X exchange
+// (parallel/zs.py: format; kernels/zs_exchange.hip)
+Tensor zs_encode(const Tensor& x, const Tensor& meta_out, const Tensor& values_out) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "zs_encode: x fp32 contiguous GPU");
+  const int64_t n = x.numel(), P = tds_zs_npages(n);
+  TORCH_CHECK(n > 0, "zs_encode: empty x");
+  need(meta_out, at::kInt, {P * 65}, "zs meta_out");
+  TORCH_CHECK(values_out.is_cuda() && values_out.scalar_type() == at::kFloat && values_out.is_contiguous() &&
+                  values_out.dim() == 1,
+              "zs_encode: values_out fp32 1-d contiguous GPU");
+  TORCH_CHECK(x.device() == meta_out.device() && x.device() == values_out.device(), "zs_encode: one device");
+  c10::DeviceGuard guard(x.device());
+  auto counts = at::empty({P}, x.options().dtype(at::kInt));
+  auto nnz = at::empty({}, x.options().dtype(at::kLong));
+  tds_zs_encode(x.data_ptr<float>(), n, meta_out.data_ptr<int>(), counts.data_ptr<int>(), values_out.data_ptr<float>(),
+                values_out.numel(), nnz.data_ptr<int64_t>(), stream_of(x));
+  check_launches("zs_encode");
+  return nnz;
+}
+
+void zs_decode(const Tensor& meta, const Tensor& values, const Tensor& out) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous(), "zs_decode: out fp32 GPU");
+  const int64_t n = out.numel(), P = tds_zs_npages(n);
+  TORCH_CHECK(n > 0, "zs_decode: empty out");
+  need(meta, at::kInt, {P * 65}, "zs meta");
+  TORCH_CHECK(values.is_cuda() && values.scalar_type() == at::kFloat && values.is_contiguous(),
+              "zs_decode: values fp32 contiguous GPU");
+  c10::DeviceGuard guard(out.device());
+  tds_zs_decode(meta.data_ptr<int>(), values.data_ptr<float>(), values.numel(), out.data_ptr<float>(), n,
+                stream_of(out));
+  check_launches("zs_decode");
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(tdsa, m) {
+  m.def("zs_encode(Tensor x, Tensor(a!) meta_out, Tensor(b!) values_out) -> Tensor", &zs_encode);
+  m.def("zs_decode(Tensor meta, Tensor values, Tensor(a!) out) -> ()", &zs_decode);
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
       "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps, Tensor? asum=None, Tensor? strips=None) -> "
       "(Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_forward);
   m.def("l1_input_stats(Tensor x) -> (Tensor, Tensor)", &l1_input_stats);
-  m.def("conv2_pack(Tensor w2) -> (Tensor, Tensor)", &conv2_pack);
-  m.def("fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2) -> (Tensor, Tensor, Tensor)",
-        &fused_conv2_forward);
+  m.def("conv2_pack(Tensor w2, Tensor(a!)? mag=None) -> (Tensor, Tensor)", &conv2_pack);
+  m.def(
+      "fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2, Tensor(a!)? mag=None) -> "
+      "(Tensor, Tensor, Tensor)",
+      &fused_conv2_forward);
   m.def(
       "fused_head_forward(Tensor ya, Tensor partial2, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
       "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc, int P, "
@@ -524,15 +576,15 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "fused_head_backward(Tensor dlogits, Tensor ya, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor(e!) wfc, "
       "int P, Tensor(a!)? dw_out, float scale, bool compute_dw=True, float update_lr=0.0, "
       "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None, bool keep_dw=True, "
-      "int c_begin=0, int c_end=32, bool finalize=True, Tensor(f!)? g2m_out=None, Tensor(g!)? partial_out=None) -> "
-      "(Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
+      "int c_begin=0, int c_end=32, bool finalize=True, Tensor(f!)? g2m_out=None, Tensor(g!)? partial_out=None, "
+      "Tensor(h!)? mag=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
   m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);
   m.def("conv2_bwd_walk_table(int B, int tiles_r, int tiles_c, int nwg, int seg) -> Tensor", &conv2_bwd_walk_table);
   m.def(
-      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor p1, Tensor wd, float scale, "
-      "Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
+      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor mag, Tensor p1, Tensor wd, "
+      "float scale, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
       &fused_conv2_backward_y2);
   m.def(
       "fused_l1_backward(Tensor dp1, Tensor x, Tensor p1, Tensor idx1, Tensor w1, Tensor b1, Tensor? gamma1, "

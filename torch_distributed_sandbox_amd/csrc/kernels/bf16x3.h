@@ -57,6 +57,53 @@ __device__ __forceinline__ void split2_bf16(float a, float b, uint32_t& hi, uint
   lo = __builtin_bit_cast(uint32_t, l);
 }
 
+// ---------------------------------------------------------------------------- fp16x2
+// The conv2 kernels (conv2_fwd2.hip, conv2_bwd.hip) run on v_mfma_f32_16x16x32_f16 with ONE
+// operand carried exactly (fp16 hi + fp16 lo, 22 significant bits) and the other rounded once
+// to fp16 (11 significant bits): c += a*bhi + a*blo, 2 MFMAs per product instead of bf16x3's 3.
+// Per-product relative error <= 2^-11 (the single operand's rounding) -- the unit roundoff of
+// the TF32 convolutions cuDNN runs for the reference by default (10 explicit mantissa bits; TF32
+// rounds BOTH operands, so its product error is up to 2^-10).  fp16's exponent range is
+// narrower than fp32's: activations (p1, O(1)) fit as they are, the conv2 output gradient is
+// carried with a power-of-two scale chosen per step from a bound of its magnitude.
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x4 mfma_f16(const s16x8& a, const s16x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8_t, a), __builtin_bit_cast(f16x8_t, b), c, 0,
+                                                0, 0);
+}
+
+// c += a * (bhi + blo) (small term first)
+__device__ __forceinline__ f32x4 mfma_f16x2(const s16x8& a, const s16x8& bhi, const s16x8& blo, f32x4 c) {
+  c = mfma_f16(a, blo, c);
+  c = mfma_f16(a, bhi, c);
+  return c;
+}
+
+// two floats -> packed fp16 pair (v_cvt_pk_f16_f32, round to nearest even; element 0 low)
+__device__ __forceinline__ uint32_t cvt2_f16(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2_t){a, b}, f16x2_t));
+}
+
+// exact split of two floats: hi = f16(x), lo = f16(x - hi), each as a packed pair
+__device__ __forceinline__ void split2_f16(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const f16x2_t h = __builtin_convertvector((f32x2_t){a, b}, f16x2_t);
+  const f32x2_t hf = __builtin_convertvector(h, f32x2_t);
+  const f16x2_t l = __builtin_convertvector((f32x2_t){a - hf.x, b - hf.y}, f16x2_t);
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, l);
+}
+
+__device__ __forceinline__ void split_f16(float x, unsigned short& hi, unsigned short& lo) {
+  uint32_t h, l;
+  split2_f16(x, 0.f, h, l);
+  hi = (unsigned short)(h & 0xffffu);
+  lo = (unsigned short)(l & 0xffffu);
+}
+
+constexpr unsigned short kF16One = 0x3C00;
+
 // lane ^ 1 (within each quad) through DPP quad_perm [1,0,3,2]: no LDS crossbar traffic
 __device__ __forceinline__ float dpp_xor1(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));

@@ -1,5 +1,13 @@
 // conv2 backward: BN2 / ReLU / max-pool backward fused into conv2 dgrad + wgrad
-// (SURVEY.md §2.4 K16-K21), one persistent 8-wave workgroup per CU.
+// (SURVEY.md §2.4 K16-K21), one persistent 8-wave workgroup per CU, on v_mfma_f32_16x16x32_f16
+// with the fp16x2 split (bf16x3.h; 2 MFMAs per product):
+//   dgrad: dp1 = convT(dy2, w2)  -- dy2 the single-rounded fp16 operand, w2 exact (hi + lo)
+//   wgrad: dw2 = sum dy2 (x) p1  -- dy2 exact (hi + lo), p1 the forward's fp16 operand as is
+// dy2 is carried with a power-of-two scale 2^e: from the step's magnitude bounds (max |y2| per
+// channel from the forward, max |g2m| from the head backward) |dy2| <= |k1| max|g2m| + |k2|
+// max|y2| + |k3| per channel, and e puts the largest bound in [2^14, 2^15) -- no fp16
+// overflow by construction, ~28 binades of full fp16 precision below it.  The products are
+// unscaled exactly (power of two) in the dp1 / weight-slab epilogues.
 //
 // Roles (one per SIMD each):
 //   waves 0/1 : dgrad, taps grouped by kx so an input row's A fragment serves up to 5 output
@@ -11,7 +19,8 @@
 //               32 pixels = two output rows, operands by ds_read_b64_tr_b16; accumulated over the
 //               workgroup's tiles; slab[wg][26][32][16] reduced in fixed order afterwards.
 //   waves 4-7 : staging: y2 / pooled gradient g2m / p1 -> BN2 / ReLU / pool backward (dy2 =
-//               k1*dz + k2*y2 + k3 at the window's argmax) -> dy2 and p1 bf16 hi|lo rows in LDS.
+//               k1*dz + k2*y2 + k3 at the window's argmax) -> dy2 fp16 hi|lo rows (scaled) and
+//               p1 fp16 rows in LDS.
 //
 // ROLLING WINDOW.  A tile of 8 output rows needs dy2 and p1 on 12 rows (2-row halo above and
 // below).  Each workgroup walks vertical SEGMENTS of tiles (one tile column of one image, ~48
@@ -26,9 +35,9 @@
 //
 // LDS, in ROW BLOCKS (one staged image row of 20 records per block):
 //   dy2 row block: 4 planes (hi co0-15, hi co16-31, lo co0-15, lo co16-31) x 20 x 32 B = 2560 B
-//   p1  row block: 2 planes (hi, lo) x 20 x 32 B = 1280 B
+//   p1  row block: 1 plane x 20 x 32 B = 640 B
 //   3 ring slots of 12 row blocks (tile k in slot k % 3: 4 top + 8 new rows), 2 dgrad exchange
-//   slots, BN2 backward constants: 155 264 B.
+//   slots, BN2 backward constants + the dy2 scale: 132 240 B.
 // One bare s_barrier per tile (after lgkmcnt(0)) separates producer and consumers: while the
 // consumers read slot k%3, the staging writes slot (k+1)%3's new rows and slot (k+2)%3's top
 // (the slot of tile k-1, finished); the register loads for tile k+3 are already in flight.
@@ -53,15 +62,16 @@ constexpr int BR_TH = 8, BR_TC = 16;       // output tile
 constexpr int BR_SC = BR_TC + 4;           // 20 staged columns (2-pixel halo each side)
 constexpr int BR_DPL = BR_SC * 32;         // 640 B: one plane of a row block
 constexpr int BR_DROW = 4 * BR_DPL;        // 2560 B: dy2 row block
-constexpr int BR_PROW = 2 * BR_DPL;        // 1280 B: p1 row block
+constexpr int BR_PROW = BR_DPL;            // 640 B: p1 row block (one fp16 plane)
 constexpr int BR_THREADS = 512;
 constexpr int BR_SLOT = 12;                                  // row blocks per ring slot
 constexpr int BR_OFF_D = 0;                                  // 3 x 12 dy2 row blocks
 constexpr int BR_OFF_P = BR_OFF_D + 3 * BR_SLOT * BR_DROW;   // 3 x 12 p1 row blocks
 constexpr int BR_XCHG = 2 * 4 * 64 * 16;                     // 8 KiB exchange slot
 constexpr int BR_OFF_X = BR_OFF_P + 3 * BR_SLOT * BR_PROW;   // 2 exchange slots
-constexpr int BR_OFF_K = BR_OFF_X + 2 * BR_XCHG;             // 160 floats of constants
-constexpr int BR_LDS = BR_OFF_K + 5 * 32 * 4;
+constexpr int BR_OFF_K = BR_OFF_X + 2 * BR_XCHG;             // 160 floats of constants + 4
+constexpr int BR_KINV = 160;                                 // kc[160] = 2^-e (the dy2 scale's inverse)
+constexpr int BR_LDS = BR_OFF_K + (5 * 32 + 4) * 4;
 static_assert(BR_LDS <= 160 * 1024 && BR_OFF_X % 16 == 0 && BR_OFF_K % 16 == 0, "LDS carve");
 
 // walk table entries (tds_conv2_bwd_walk): bit 31 = first tile of a segment, bit 30 = past the
@@ -132,11 +142,11 @@ __device__ __forceinline__ void br_xchg_put(f32x4* xs, const f32x4 (&acc)[8], in
 // Wave D owns output rows 4D .. 4D+3: its partial + the partner's, then dp1.
 template <int D>
 __device__ __forceinline__ void br_xchg_finish(const f32x4* xs, const f32x4 (&acc)[8], float* __restrict__ dp1,
-                                               int lane, int b, int r0, int c0, int P) {
+                                               int lane, int b, int r0, int c0, int P, float inv) {
   const int li = lane & 15, g = lane >> 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const f32x4 v = acc[4 * D + i] + xs[(D * 4 + i) * 64 + lane];
+    const f32x4 v = (acc[4 * D + i] + xs[(D * 4 + i) * 64 + lane]) * inv;  // 2^-e: exact
     const int row = r0 + 4 * D + i;
     if (row < P) {
       float* orow = dp1 + ((int64_t)b * P + row) * P * 16;
@@ -172,17 +182,15 @@ struct DgSeq {
 // one flat, fully unrolled sequence of A-fragment rows with operands fetched two steps ahead
 // across group boundaries (one MFMA wave per SIMD: nothing else hides a bubble)
 template <int D, int DIAG>
-__device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int lp,
-                                         int li) {
+__device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int li) {
   using Q = DgSeq<D>;
 #pragma unroll
   for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 ah[3], al[3];
+  s16x8 ah[3];  // dy2 hi only: the single-rounded operand
   auto load_a = [&](int s, int buf) {
     const int i = Q::grp(s), r = Q::row(s);
     const char* rb = rw.d(Q::ky0(i) + r) + (Q::kx(i) + li) * 32;
     ah[buf] = lds8<DIAG>(rb + hp);
-    al[buf] = lds8<DIAG>(rb + lp);
   };
   load_a(0, 0);
   load_a(1, 1);
@@ -195,18 +203,29 @@ __device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][
     for (int k = 0; k < 5; ++k) {
       const int o = r - k;
       if (k < Q::nky(i) && o >= 0 && o < 8)
-        acc[o] = mma3<DIAG>(ah[s % 3], al[s % 3], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
+        acc[o] = mma2<DIAG>(ah[s % 3], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
                             __builtin_bit_cast(s16x8, R[5 * i + k][1]), acc[o]);
     }
   }
 }
 
 // ---------------------------------------------------------------------------- wgrad
+// c += (ahi + alo) * b: the wgrad's exact operand is dy2 (A), p1 (B) the single-rounded one
+template <int DIAG>
+__device__ __forceinline__ f32x4 mma2a(const s16x8& ahi, const s16x8& alo, const s16x8& b, f32x4 c) {
+  if constexpr (DIAG == 1) {
+    c[0] += (float)((int)(ahi[0] ^ alo[1] ^ b[2]) & 1);
+    return c;
+  } else {
+    c = mfma_f16(alo, b, c);
+    return mfma_f16(ahi, b, c);
+  }
+}
+
 template <int E, int DIAG>
-__device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2], int lane, const s16x8& ones_hi,
-                                         const s16x8& zero8) {
+__device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2], int lane, const s16x8& ones) {
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-  s16x8 ahi[2][2], alo[2][2], bhi[3], blo[3];
+  s16x8 ahi[2][2], alo[2][2], bv[3];
   auto drow = [&](int r) { return rw.d(r); };
   auto prow = [&](int r) { return rw.p(r); };
   auto load_a = [&](int m, int slot) {
@@ -228,12 +247,9 @@ __device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2],
       const char* r0 = prow(2 * m + ky) + col;
       const char* r1 = prow(2 * m + ky + 1) + col;
       const s16x4 x0 = ldtr<DIAG>(r0), x1 = ldtr<DIAG>(r1);
-      const s16x4 y0 = ldtr<DIAG>(r0 + BR_DPL), y1 = ldtr<DIAG>(r1 + BR_DPL);
-      bhi[buf] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      blo[buf] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+      bv[buf] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
     } else {
-      bhi[buf] = ones_hi;  // bias gradient column
-      blo[buf] = zero8;
+      bv[buf] = ones;  // bias gradient column
     }
   };
   // K-steps m in a rolled loop (static buffer indices inside), operands rotated at the end
@@ -249,7 +265,7 @@ __device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2],
       if (k == 10 && m + 1 < 4) load_a(m + 1, 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int h = 0; h < 2; ++h) wacc[k][h] = mma3<DIAG>(ahi[0][h], alo[0][h], bhi[k % 3], blo[k % 3], wacc[k][h]);
+      for (int h = 0; h < 2; ++h) wacc[k][h] = mma2a<DIAG>(ahi[0][h], alo[0][h], bv[k % 3], wacc[k][h]);
     }
     // taps 0, 1 of the next K-step sit in buffers 1, 2 (13 % 3 == 1), its A in slot 1
 #pragma unroll
@@ -257,10 +273,8 @@ __device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2],
       ahi[0][h] = ahi[1][h];
       alo[0][h] = alo[1][h];
     }
-    bhi[0] = bhi[1];
-    blo[0] = blo[1];
-    bhi[1] = bhi[2];
-    blo[1] = blo[2];
+    bv[0] = bv[1];
+    bv[1] = bv[2];
   }
 }
 
@@ -316,14 +330,11 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
 #pragma unroll
   for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (ROLE < 2) br_load_w<ROLE>(wdpack, R, lane);
-  s16x8 ones_hi, zero8;
+  s16x8 ones;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    ones_hi[j] = (short)(li == 0 ? 0x3f80 : 0);
-    zero8[j] = 0;
-  }
+  for (int j = 0; j < 8; ++j) ones[j] = (short)(li == 0 ? kF16One : 0);
   const int hp = (g >> 1) * BR_DPL + (g & 1) * 16;
-  const int lp = (2 + (g >> 1)) * BR_DPL + (g & 1) * 16;
+  const float inv = reinterpret_cast<const float*>(smem + BR_OFF_K)[BR_KINV];  // 2^-e
   BRTile prev{0, 0, 0, false, true};
   BRClock<DIAG> clk;
   clk.start();
@@ -336,11 +347,11 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
     if constexpr (ROLE < 2) {
       if (!prev.end)
         br_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + BR_OFF_X + ((kk + 1) & 1) * BR_XCHG), acc, a.dp1,
-                             lane, prev.b, prev.r0, prev.c0, a.P);
-      br_dgrad<ROLE, DIAG>(rw, R, acc, hp, lp, li);
+                             lane, prev.b, prev.r0, prev.c0, a.P, inv);
+      br_dgrad<ROLE, DIAG>(rw, R, acc, hp, li);
       br_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + BR_OFF_X + (kk & 1) * BR_XCHG), acc, lane);
     } else {
-      br_wgrad<ROLE - 2, DIAG>(rw, R, lane, ones_hi, zero8);
+      br_wgrad<ROLE - 2, DIAG>(rw, R, lane, ones);
     }
     prev = cur;
   }
@@ -349,7 +360,7 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
   if constexpr (ROLE < 2) {
     if (!prev.end)
       br_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + BR_OFF_X + ((kk - 1) & 1) * BR_XCHG), acc, a.dp1,
-                           lane, prev.b, prev.r0, prev.c0, a.P);
+                           lane, prev.b, prev.r0, prev.c0, a.P, inv);
   } else {
     float* out = a.slab + (int64_t)blockIdx.x * 26 * 512;
 #pragma unroll
@@ -358,7 +369,7 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[(tap * 32 + 16 * h + 4 * g + r) * 16 + li] = R[k][h][r];
+        for (int r = 0; r < 4; ++r) out[(tap * 32 + 16 * h + 4 * g + r) * 16 + li] = R[k][h][r] * inv;
     }
   }
 }
@@ -377,7 +388,7 @@ struct BRStager {
   static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
   static constexpr int ITEMS = NWIN * 8;
   static constexpr int IPER = (ITEMS + 255) / 256;
-  static constexpr int PIECES = NR * BR_SC * 4;  // 16-B p1 pieces
+  static constexpr int PIECES = NR * BR_SC * 2;  // 16-B p1 pieces (32-B fp16 records)
   static constexpr int PPER = (PIECES + 255) / 256;
   float4 yv[IPER][4], gv[IPER];
   uint4 pr[PPER];
@@ -412,7 +423,7 @@ struct BRStager {
     const __amdgpu_buffer_rsrc_t ry =
         tds_buffer_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + R0) * P + (c0 - 2)) * 128, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t rp =
-        tds_buffer_rsrc(reinterpret_cast<const char*>(a.p1) + ((img + R0) * P + (c0 - 2)) * 64, 0xFFFFFFF0u);
+        tds_buffer_rsrc(reinterpret_cast<const char*>(a.p1) + ((img + R0) * P + (c0 - 2)) * 32, 0xFFFFFFF0u);
     const int64_t gplane = (int64_t)Q * Q;
     const int py0 = R0 / 2, px0 = c0 / 2 - 1;
     const __amdgpu_buffer_rsrc_t rg =
@@ -453,11 +464,11 @@ struct BRStager {
 #pragma unroll
     for (int j = 0; j < PPER; ++j) {
       const int e = tid + 256 * j;
-      const int rec = (e < PIECES ? e : 0) >> 2, q = e & 3;
+      const int rec = (e < PIECES ? e : 0) >> 1, q = e & 1;
       const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
       const int gr = R0 + lr, gc = c0 - 2 + lc;
       const bool ok = e < PIECES && (in || (gr >= 0 && gr < P && gc >= 0 && gc < P));
-      const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 64 + q * 16) : kBROob;
+      const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 32 + q * 16) : kBROob;
       pr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
     }
   }
@@ -549,9 +560,9 @@ struct BRStager {
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        uint32_t h01, l01, h23, l23;
-        split2_bf16(d[q][0], d[q][1], h01, l01);
-        split2_bf16(d[q][2], d[q][3], h23, l23);
+        uint32_t h01, l01, h23, l23;  // (k1..k3 carry the scale 2^e: d is dy2 * 2^e)
+        split2_f16(d[q][0], d[q][1], h01, l01);
+        split2_f16(d[q][2], d[q][3], h23, l23);
         const int lr = 2 * wy + (q >> 1);
         const int ro = (2 * wx + (q & 1)) * 32 + (c4 & 3) * 8;
         char* rec = dbase + lr * BR_DROW + ro;
@@ -568,9 +579,9 @@ struct BRStager {
     for (int j = 0; j < PPER; ++j) {
       const int e = tid + 256 * j;
       if (e < PIECES) {
-        const int rec = e >> 2, q = e & 3;
+        const int rec = e >> 1, q = e & 1;
         const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
-        const int po = (q >> 1) * BR_DPL + lc * 32 + (q & 1) * 16;
+        const int po = lc * 32 + q * 16;
         *reinterpret_cast<uint4*>(pbase + lr * BR_PROW + po) = pr[j];
         if (MIRROR && lr >= 4) *reinterpret_cast<uint4*>(pmir + (lr - 4) * BR_PROW + po) = pr[j];
       }
@@ -660,8 +671,9 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
 template <int DIAG, bool BIG>
 __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
     const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
-    const float* __restrict__ kbuf, const uint4* __restrict__ p1, const uint4* __restrict__ wdpack,
-    float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ walk, int B, int P) {
+    const float* __restrict__ kbuf, const uint32_t* __restrict__ mag, const uint4* __restrict__ p1,
+    const uint4* __restrict__ wdpack, float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ walk,
+    int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -671,8 +683,30 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
   a.nwg = gridDim.x;
   a.w = xcd_remap(blockIdx.x, gridDim.x);  // this workgroup's list (XCD-contiguous: neighbouring columns)
   float* kc = reinterpret_cast<float*>(smem + BR_OFF_K);
-  if (tid < 160) kc[tid] = (tid < 64) ? aff2[tid] : kbuf[tid - 64];
-  __syncthreads();  // kc visible to the staging waves
+  if (tid < 64) {
+    // the dy2 scale 2^e (header): wave 0, lane c < 32 bounds channel c; k1..k3 are scaled in
+    // place, kc[BR_KINV] = 2^-e for the epilogues
+    const int c = tid & 31;
+    const float k1 = kbuf[c], k2 = kbuf[32 + c], k3 = kbuf[64 + c];
+    const float gmx = __uint_as_float(mag[32]), ymx = __uint_as_float(mag[c]);
+    float bound = fabsf(k1) * gmx + fabsf(k2) * ymx + fabsf(k3);
+    bound = wave_max(tid < 32 ? bound : 0.f);  // NaN/inf bound: no scaling (e = 0)
+    int e = 0;
+    if (bound > 0.f && __builtin_isfinite(bound)) {
+      int x;
+      (void)frexpf(bound, &x);  // bound < 2^x
+      e = min(60, max(-60, 15 - x));
+    }
+    const float sc = ldexpf(1.f, e);
+    kc[tid] = aff2[tid];
+    if (tid < 32) {
+      kc[64 + c] = k1 * sc;
+      kc[96 + c] = k2 * sc;
+      kc[128 + c] = k3 * sc;
+    }
+    if (tid == 0) kc[BR_KINV] = ldexpf(1.f, -e);
+  }
+  __syncthreads();  // kc visible to every role
   switch (wv) {
     case 0: br_mfma<0, DIAG>(a, wdpack, smem); break;
     case 1: br_mfma<1, DIAG>(a, wdpack, smem); break;
@@ -787,8 +821,8 @@ static int br_diag_env() { return 0; }
 #endif
 
 // g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups
-void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P,
+void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const uint32_t* mag,
+                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P,
                     hipStream_t st) {
   const int Q = P / 2;
   const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
@@ -801,7 +835,7 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
       set = true;                                                                                                      \
     }                                                                                                                  \
     hipLaunchKernelGGL((conv2_bwd_roll_kernel<D, BG>), dim3(nwg), dim3(BR_THREADS), BR_LDS, st,                        \
-                       reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, reinterpret_cast<const uint4*>(p1),       \
+                       reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, mag, reinterpret_cast<const uint4*>(p1),  \
                        reinterpret_cast<const uint4*>(wd), dp1, slab, walk, B, P);                                      \
     TDS_LAUNCH_CHECK();                                                                                                \
   }

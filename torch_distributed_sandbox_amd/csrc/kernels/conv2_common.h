@@ -20,6 +20,16 @@ __device__ __forceinline__ f32x4 mma3(const s16x8& ah, const s16x8& al, const s1
     return mfma_bf16x3(ah, al, bh, bl, c);
   }
 }
+// fp16x2 (bf16x3.h): c += a * (bh + bl)
+template <int DIAG>
+__device__ __forceinline__ f32x4 mma2(const s16x8& a, const s16x8& bh, const s16x8& bl, f32x4 c) {
+  if constexpr (DIAG == 1) {
+    c[0] += (float)((int)(a[0] ^ bh[2] ^ bl[3]) & 1);
+    return c;
+  } else {
+    return mfma_f16x2(a, bh, bl, c);
+  }
+}
 template <int DIAG>
 __device__ __forceinline__ s16x8 lds8(const void* p) {
   if constexpr (DIAG == 2) {

@@ -1,8 +1,10 @@
 // conv2 forward v2 (Conv2d(16, 32, 5, pad 2), mnist_onegpu.py:20):
 // y2 = conv(p1) + b2 in NHWC fp32, plus BN2 batch-statistic partials, on
-// v_mfma_f32_16x16x32_bf16 with the bf16x3 split, laid out for SEVERAL small workgroups
-// per CU (the design of conv2_bwd2.hip):
-//   * 4 waves per workgroup, output tile 8 rows x 16 columns (staged p1: 12 x 20 records);
+// v_mfma_f32_16x16x32_f16 with the fp16x2 split (bf16x3.h: p1 is the single-rounded fp16
+// operand, the weights are carried exactly as fp16 hi + lo; 2 MFMAs per product), laid out for
+// SEVERAL small workgroups per CU (the design of conv2_bwd2.hip):
+//   * 4 waves per workgroup, output tile 8 rows x 16 columns (staged p1: 12 x 20 records of
+//     32 B);
 //   * weights in REGISTERS: wave w owns co half nt = w & 1 and output rows 4(w>>1) .. +3,
 //     all 13 K-steps of its half (13 x (hi, lo) fragments = 104 VGPRs), loaded once;
 //   * p1 staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs, no VALU), double-buffered:
@@ -15,6 +17,8 @@
 //     statistics are.  Every lane holds whole windows of its channel, the 4 x 8 pooled block
 //     of the tile is staged in LDS and stored as ya (pooled_layout.h): one 128-B line per
 //     channel.  The head then streams ya (72 MB per image at 3000^2) instead of y2 (288 MB).
+//   * max |y2| per channel goes to an atomic max (mag): with the head backward's max |g2m| it
+//     bounds the conv2 output gradient, whose fp16 scale the backward picks from it.
 // K order and input-row sharing as conv2_fwd_bf16x3_kernel: K-step s < 10 pairs taps
 // (ky = s>>1, kx = 2(s&1) + (g>>1)) so one staged input row R serves output rows R - ky;
 // s = 10 + kp pairs (ky = 2kp + (g>>1), kx = 4) with lane groups 2-3 reading row R+1.
@@ -30,15 +34,15 @@ constexpr int F2_TH = 8, F2_TC = 16;
 constexpr int F2_SR = F2_TH + 4, F2_SC = F2_TC + 4;  // 12 x 20 staged records
 constexpr int F2_REC = F2_SR * F2_SC;                  // 240
 constexpr int F2_THREADS = 256;
-constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records per plane
-constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records, 240 used)
-constexpr int F2_PBUF = 2 * F2_PPLANE;                 // hi + lo
+constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records (1 KiB)
+constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records of 32 B, 240 used)
+constexpr int F2_PBUF = F2_PPLANE;                     // one fp16 plane
 constexpr int F2_STAGE = F2_TH * F2_TC * 32 * 4;        // finished tile: 8 x 16 px x 32 co fp32 = 16 KiB
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
 constexpr int F2_YSTAGE = 32 * 32 * 4;                 // pooled block: 32 co x 4 x 8 fp32 = 4 KiB
 constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
-constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging: 72 KiB
-constexpr int F2_DMA_PER_WAVE = 2 * F2_PGROUPS / (F2_THREADS / 64);  // 4
+constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging: 56 KiB
+constexpr int F2_DMA_PER_WAVE = F2_PGROUPS / (F2_THREADS / 64);  // 2
 static_assert(F2_LDS % 16 == 0, "LDS carve");
 static_assert(2 * F2_LDS <= 160 * 1024, "two workgroups per CU");
 
@@ -52,19 +56,16 @@ struct F2Tile {
 template <int DIAG, int WV>
 __device__ __forceinline__ void f2_dma(const uint4* __restrict__ p1, const F2Tile& x, int P, char* buf, int lane) {
   if constexpr (DIAG == 3) return;
-  const char* base = reinterpret_cast<const char*>(p1) + (((int64_t)x.b * P + x.r0 - 2) * P + (x.c0 - 2)) * 64;
+  const char* base = reinterpret_cast<const char*>(p1) + (((int64_t)x.b * P + x.r0 - 2) * P + (x.c0 - 2)) * 32;
 #pragma unroll
   for (int j = 0; j < F2_DMA_PER_WAVE; ++j) {
-    const int k = WV * F2_DMA_PER_WAVE + j;
-    const int pl = k / F2_PGROUPS, rg = k - pl * F2_PGROUPS;
+    const int rg = WV * F2_DMA_PER_WAVE + j;
     const int px = rg * 32 + (lane >> 1), half = lane & 1;
     const int rr = px / F2_SC, cc = px - rr * F2_SC;
     const int gr = x.r0 - 2 + rr, gc = x.c0 - 2 + cc;
     const bool ok = px < F2_REC && gr >= 0 && gr < P && gc >= 0 && gc < P;
-    const char* src = ok ? base + ((int64_t)rr * P + cc) * 64 + pl * 32 + half * 16
-                         : reinterpret_cast<const char*>(g_f2_zero);
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + pl * F2_PPLANE + rg * 1024),
-                                     16, 0, 0);
+    const char* src = ok ? base + ((int64_t)rr * P + cc) * 32 + half * 16 : reinterpret_cast<const char*>(g_f2_zero);
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(buf + rg * 1024), 16, 0, 0);
   }
 }
 
@@ -81,10 +82,9 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
   const int li = lane & 15, g = lane >> 4;
   const int boff = (g & 1) * 16;  // ci half of the 32-B record
   const char* ph = buf;
-  const char* pl = buf + F2_PPLANE;
 #pragma unroll
   for (int o = 0; o < 4; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 ah[DEPTH], al[DEPTH];
+  s16x8 ah[DEPTH];
   // load i: group i / 8 (0, 1: kx pairs 2a + (g>>1); 2: kx = 4 with lane groups 2-3 one row down)
   auto load_a = [&](int i) {
     const int grp = i >> 3, R = i & 7;
@@ -97,7 +97,6 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
       rec = row * F2_SC + li + 4;
     }
     ah[i % DEPTH] = lds8<DIAG>(ph + rec * 32 + boff);
-    al[i % DEPTH] = lds8<DIAG>(pl + rec * 32 + boff);
   };
 #pragma unroll
   for (int i = 0; i < DEPTH - 1; ++i) load_a(i);
@@ -111,7 +110,7 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
       for (int ky = 0; ky < 5; ++ky) {
         const int o = R - ky;
         if (o >= 0 && o < 4)
-          acc[o] = mma3<DIAG>(ah[cur], al[cur], __builtin_bit_cast(s16x8, W[2 * ky + grp][0]),
+          acc[o] = mma2<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[2 * ky + grp][0]),
                               __builtin_bit_cast(s16x8, W[2 * ky + grp][1]), acc[o]);
       }
     } else {
@@ -119,7 +118,7 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
       for (int kp = 0; kp < 3; ++kp) {
         const int o = R - 2 * kp;
         if (o >= 0 && o < 4)
-          acc[o] = mma3<DIAG>(ah[cur], al[cur], __builtin_bit_cast(s16x8, W[10 + kp][0]),
+          acc[o] = mma2<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[10 + kp][0]),
                               __builtin_bit_cast(s16x8, W[10 + kp][1]), acc[o]);
       }
     }
@@ -148,7 +147,8 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
 
 // stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li]
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
-                                         int RH, int NT, int lane, float bco, bool neg, float& s_acc, float& q_acc) {
+                                         int RH, int NT, int lane, float bco, bool neg, float& s_acc, float& q_acc,
+                                         uint32_t& ymx) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
 #pragma unroll
@@ -162,6 +162,7 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
       if (rok && x.c0 + px < P) {
         s_acc += v;
         q_acc += v * v;
+        ymx = max(ymx, __float_as_uint(v + bco) & 0x7fffffffu);  // |y2| bits (NaN: above every finite)
       }
       *reinterpret_cast<float*>(stage + f2_stage_off(row, px, co >> 2) + (co & 3) * 4) = v + bco;
     }
@@ -210,7 +211,8 @@ template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
                                        const float* __restrict__ bias, const float* __restrict__ gamma,
                                        float* __restrict__ y2, float* __restrict__ ya, double* __restrict__ partial,
-                                       const int* __restrict__ order, int B, int P, char* smem) {
+                                       uint32_t* __restrict__ mag, const int* __restrict__ order, int B, int P,
+                                       char* smem) {
   constexpr int NT = WV & 1, RH = WV >> 1;
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int tiles_c = (P + F2_TC - 1) / F2_TC, tiles_r = (P + F2_TH - 1) / F2_TH;
@@ -234,6 +236,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
   float s_acc = 0.f, q_acc = 0.f;
+  uint32_t ymx = 0u;
   f32x4 acc[4];
   F2Tile prev{0, 0, 0};
   bool have_prev = false;
@@ -252,7 +255,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     }
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
     f2_stage(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane, bco,
-             neg, s_acc, q_acc);
+             neg, s_acc, q_acc, ymx);
     prev = cur;
     have_prev = true;
   }
@@ -260,6 +263,11 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   if (have_prev) {
     f2_store<DIAG>(smem + F2_OFF_S + ((kk - 1) & 1) * F2_STAGE, prev, y2, P);
     f2_store_ya(ys + ((kk - 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
+  }
+  if (mag != nullptr) {  // max |y2| of channel 16NT + li: the 4 lane groups, then one atomic per wave
+    ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 16, 64));
+    ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 32, 64));
+    if (lane < 16) atomicMax(mag + 16 * NT + li, ymx);
   }
   // BN2 partials: reduce the 4 lane groups, then the two row-halves of this co half
   s_acc += __shfl_xor(s_acc, 16, 64);
@@ -288,13 +296,14 @@ __global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* 
                                                                    const float* __restrict__ gamma,
                                                                    float* __restrict__ y2, float* __restrict__ ya,
                                                                    double* __restrict__ partial,
+                                                                   uint32_t* __restrict__ mag,
                                                                    const int* __restrict__ order, int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
-  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
-  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
-  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
-  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, order, B, P, smem);
+  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
+  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
+  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
+  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
 }
 
 }  // namespace tds
@@ -322,7 +331,7 @@ static int f2_diag_env() { return 0; }
 
 // order: the blocked tile order table (tds_tile_order_fill), allocated by the caller
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, const int* order, int nwg, int B, int P, hipStream_t st) {
+                    double* partial, uint32_t* mag, const int* order, int nwg, int B, int P, hipStream_t st) {
   const dim3 grid(nwg), block(F2_THREADS);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wp);
@@ -340,12 +349,12 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const fl
   }
   switch (f2_diag_env()) {
 #ifdef TDS_DIAG
-    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
-    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
-    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
-    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
 #endif
-    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, order, B, P); break;
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
   }
   TDS_LAUNCH_CHECK();
 }

@@ -1,13 +1,14 @@
 // conv2 of the ConvNet (Conv2d(16, 32, 5, stride 1, pad 2), mnist_onegpu.py:20): shared host
-// pieces of the bf16x3 MFMA kernels (conv2_fwd2.hip, conv2_bwd.hip) -- the on-device weight
-// packing into MFMA fragment order, the deterministic fp64 reduction of the per-workgroup weight
+// pieces of the fp16x2 MFMA kernels (conv2_fwd2.hip, conv2_bwd.hip; bf16x3.h) -- the on-device
+// weight packing into MFMA fragment order (fp16 hi + lo: the exactly carried operand of the
+// forward and the data gradient), the deterministic fp64 reduction of the per-workgroup weight
 // gradient slabs, and the blocked tile order table.  SURVEY.md §2.4 K5 / K19 / K20.
 //
 // Activation formats (produced/consumed by convnet_fused.hip and the conv2 kernels):
-//   p1  [B][P][P][32] bf16 : ch 0-15 = hi(ci), 16-31 = lo(ci)      (pooled layer-1 output)
+//   p1  [B][P][P][16] fp16                                          (pooled layer-1 output)
 //   y2  [B][P][P][32] fp32                                          (conv2 output, incl. bias)
 //   dp1 [B][P][P][16] fp32                                          (grad wrt p1)
-// MFMA mapping (v_mfma_f32_16x16x32_bf16, lane l: i = l&15, g = l>>4):
+// MFMA mapping (v_mfma_f32_16x16x32_f16, lane l: i = l&15, g = l>>4):
 //   A[i][k = 8g+j] (8 consecutive k per lane), B[k = 8g+j][n = i], C row = 4g+r, col = i.
 #include <vector>
 
@@ -21,10 +22,13 @@ namespace tds {
 //       input-row A fragment serves every output row:  s < 10: (ky = s>>1, kx = 2(s&1) + (g>>1));
 //       s = 10 + kp: (ky = 2kp + (g>>1), kx = 4)  (ky = 5 -> zero)
 // dgrad: wd[hl][s<25][g<4][ci16][j8],      k = 32s+8g+j -> tap' = s, co = 8g+j; w = w2[co][ci][24-tap']
+// mag (optional, 33 words): the step's magnitude bounds (max |y2| per channel, max |g2m|) are
+// reset here, at the start of the conv2 forward they feed (conv2_fwd2.hip, head_pb.hip)
 __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* __restrict__ wp,
-                                          short* __restrict__ wd) {
+                                          short* __restrict__ wd, uint32_t* __restrict__ mag) {
   const int FW = 13 * 2 * 4 * 16 * 8;  // per hl plane (fwd)
   const int DW = 25 * 4 * 16 * 8;      // per hl plane (dgrad)
+  if (mag != nullptr && blockIdx.x == 0 && threadIdx.x < 33) mag[threadIdx.x] = 0u;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < FW + DW; e += gridDim.x * blockDim.x) {
     if (e < FW) {
       const int j = e & 7, co_in = (e >> 3) & 15, g = (e >> 7) & 3, nt = (e >> 9) & 1, s = e >> 10;
@@ -33,7 +37,7 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
       const int ci = 8 * (g & 1) + j, co = nt * 16 + co_in;
       const float v = ky < 5 ? w2[(co * 16 + ci) * 25 + ky * 5 + kx] : 0.f;
       unsigned short hi, lo;
-      split_bf16(v, hi, lo);
+      split_f16(v, hi, lo);
       wp[e] = (short)hi;
       wp[FW + e] = (short)lo;
     } else {
@@ -42,7 +46,7 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
       const int co = 8 * g + j;
       const float v = w2[(co * 16 + ci) * 25 + (24 - s)];
       unsigned short hi, lo;
-      split_bf16(v, hi, lo);
+      split_f16(v, hi, lo);
       wd[f] = (short)hi;
       wd[DW + f] = (short)lo;
     }
@@ -85,8 +89,8 @@ __global__ __launch_bounds__(256) void conv2_wgrad_reduce_kernel(const float* __
 
 using namespace tds;
 
-void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t st) {
-  hipLaunchKernelGGL(conv2_pack_weights_kernel, dim3(64), dim3(256), 0, st, w2, wp, wd);
+void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, hipStream_t st) {
+  hipLaunchKernelGGL(conv2_pack_weights_kernel, dim3(64), dim3(256), 0, st, w2, wp, wd, mag);
   TDS_LAUNCH_CHECK();
 }
 

@@ -6,9 +6,9 @@
 //                     and S = sum xpatch (l1_gram).  BN1 statistics follow in closed form
 //                     (sum y1 - b1 = w1.S, sum (y1 - b1)^2 = w1^T G w1), so conv1 runs ONCE;
 //                     G and S are reused by the closed-form conv1 weight gradient.
-//   l1_conv         : conv1 (exact fp32, v_mfma_f32_16x16x4_f32), BN1 affine, ReLU, 2x2 max-pool
-//                     -> p1 (bf16 hi|lo NHWC) and a 1-byte argmax per pooled value; y1 is never
-//                     written (2.88 GB saved).
+//   l1_conv         : conv1 (bf16x3 MFMA), BN1 affine, ReLU, 2x2 max-pool -> p1 (fp16 NHWC, 32-B
+//                     records: conv2's single-rounded operand) and a 1-byte argmax per pooled
+//                     value; y1 is never written (2.88 GB saved).
 //   [conv2 fwd + BN2 stats]
 //   head_fwd        : BN2 affine + ReLU + 2x2 pool + fc, one pass over y2 and W (p2 never stored).
 // Backward
@@ -200,18 +200,16 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
           pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
           ixw |= (am | (m > 0.f ? 4u : 0u)) << (8 * r);
         }
-        uint32_t h01, l01, h23, l23;
-        split2_bf16(pv[0], pv[1], h01, l01);
-        split2_bf16(pv[2], pv[3], h23, l23);
+        // p1 is conv2's single fp16 operand (bf16x3.h, fp16x2): one rounding, 32-B records
+        const uint32_t h01 = cvt2_f16(pv[0], pv[1]), h23 = cvt2_f16(pv[2], pv[3]);
 #if defined(TDS_L1_EXP) && TDS_L1_EXP == 1
         if (prow < P && pcol < PW && pv[0] == 1234.5f) {
 #else
         if (prow < P && pcol < PW) {
 #endif
           const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
-          uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 4);  // 64-B record: hi[16] | lo[16]
+          uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 2);  // 32-B record: fp16[16]
           st_stream(dst + g, make_uint2(h01, h23));
-          st_stream(dst + 4 + g, make_uint2(l01, l23));
           st_stream(reinterpret_cast<uint32_t*>(idx1 + rec * 16) + g, ixw);
         }
       }

@@ -61,8 +61,9 @@ int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float
 int tds_take_launch_error(char* buf, int n);  // 1 (and the message) if a launch failed since the last call
 void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  // test hook: a launch of any config
 
-// ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, bf16x3 split MFMA)
-void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, hipStream_t st);
+// ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, fp16x2 split MFMA)
+// mag (optional): 33 words of magnitude bounds [max|y2| per channel (32) | max|g2m|], reset here
+void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, hipStream_t st);
 int tds_conv2_num_wg();  // CUs (tds_device_cus)
 // ---- cu_budget.hip: CUs the persistent kernels may use (all minus a reserve for RCCL) and
 // CU-masked compute streams
@@ -78,13 +79,16 @@ void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, fl
 int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
 // y2 [B,P,P,32]; ya pooled-blocked (pooled_layout.h), max/min of each 2x2 window by sign(gamma2)
+// mag (optional): atomic max of |y2| per channel into mag[0..32)
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, const int* order, int nwg, int B, int P, hipStream_t st);
+                    double* partial, uint32_t* mag, const int* order, int nwg, int B, int P, hipStream_t st);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups
-void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const void* p1,
-                    const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P, hipStream_t st);
+// mag: the forward's / head backward's magnitude bounds (the fp16 scale of dy2)
+void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const uint32_t* mag,
+                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P,
+                    hipStream_t st);
 // host: per-workgroup tile lists of vertical segments of ~seg tiles; out == nullptr -> length
 int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, int seg);
 
@@ -127,6 +131,15 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 int tds_head_bwd_pb_npass(int B);
 // channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
 // soon as its launch lands; the BN2 partials of the other channels are left untouched)
+// gmax (optional): atomic max of |g2m| (float bits) -- the conv2 backward's fp16 scale bound
 int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
-                    int c1, hipStream_t st);
+                    int c1, uint32_t* gmax, hipStream_t st);
+
+// ---- zs_exchange.hip (zero-suppressed fc-input rows, parallel/zs.py)
+int64_t tds_zs_npages(int64_t n);
+// meta [npages * 65] (offsets + mask words), counts [npages] scratch, vals [cap] (dropped past
+// cap), nnz: int64 device scalar
+void tds_zs_encode(const float* x, int64_t n, int* meta, int* counts, float* vals, int64_t cap, int64_t* nnz,
+                   hipStream_t st);
+void tds_zs_decode(const int* meta, const float* vals, int64_t cap, float* out, int64_t n, hipStream_t st);

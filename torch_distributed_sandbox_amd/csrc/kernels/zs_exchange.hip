@@ -1,0 +1,177 @@
+// Zero-suppressed encoding of the fc input rows X for the fc-gradient exchanges
+// (parallel/zs.py has the format and the torch reference; parallel/factored.py the protocol).
+// X is a ReLU output; the exchange sends its non-zero values plus a bitmask and rebuilds X bit
+// for bit, so the exchanged gradient is bitwise the dense exchange's.
+//
+// Pages of 2048 flat elements, one 256-thread workgroup per page, thread t owns elements
+// 8t .. 8t+7 of its page (one byte of the mask).  meta[p*65] = the page's value offset,
+// meta[p*65 + 1 + j] = mask word j (bit i <-> element 32j + i, "non-zero" = any bit set).
+//   encode: zs_count (mask words + per-page counts) -> zs_scan (one workgroup: offsets + nnz)
+//           -> zs_compact (values in element order, dropped past the capacity)
+//   decode: zs_expand (values back to their places, zeros elsewhere)
+#include "common.h"
+#include "launchers.h"
+
+namespace tds {
+
+constexpr int ZS_PAGE = 2048;
+constexpr int ZS_META = 1 + ZS_PAGE / 32;
+
+// this thread's 8 elements as raw bits (zeros past n)
+__device__ __forceinline__ void zs_load8(const uint32_t* __restrict__ x, int64_t e0, int64_t n, uint32_t (&v)[8]) {
+  if (e0 + 8 <= n && (e0 & 3) == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0) {
+    const uint4 a = *reinterpret_cast<const uint4*>(x + e0), b = *reinterpret_cast<const uint4*>(x + e0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = e0 + i < n ? x[e0 + i] : 0u;
+  }
+}
+
+__device__ __forceinline__ uint32_t zs_byte(const uint32_t (&v)[8]) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m |= (v[i] != 0u ? 1u : 0u) << i;
+  return m;
+}
+
+// exclusive prefix of one value per thread over the 256-thread workgroup (+ the total)
+__device__ __forceinline__ int zs_block_scan(int v, int* sh, int& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  if (lane == 63) sh[wv] = incl;
+  __syncthreads();
+  int base = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int s = sh[w];
+    if (w < wv) base += s;
+    total += s;
+  }
+  __syncthreads();
+  return base + incl - v;
+}
+
+__global__ __launch_bounds__(256) void zs_count_kernel(const uint32_t* __restrict__ x, int64_t n,
+                                                       int* __restrict__ meta, int* __restrict__ counts) {
+  __shared__ uint32_t bytes[256];
+  __shared__ int sh[4];
+  const int64_t p = blockIdx.x;
+  uint32_t v[8];
+  zs_load8(x, p * ZS_PAGE + 8 * (int64_t)threadIdx.x, n, v);
+  const uint32_t m = zs_byte(v);
+  bytes[threadIdx.x] = m;
+  int total;
+  (void)zs_block_scan(__builtin_popcount(m), sh, total);  // (its barriers order the bytes too)
+  if (threadIdx.x < 64) {
+    const int j = threadIdx.x;
+    const uint32_t w = bytes[4 * j] | (bytes[4 * j + 1] << 8) | (bytes[4 * j + 2] << 16) | (bytes[4 * j + 3] << 24);
+    meta[p * ZS_META + 1 + j] = (int)w;
+  }
+  if (threadIdx.x == 0) counts[p] = total;
+}
+
+// one 1024-thread workgroup: meta[p*65] = sum_{q<p} counts[q]; nnz = the total
+__global__ __launch_bounds__(1024) void zs_scan_kernel(const int* __restrict__ counts, int64_t npages,
+                                                       int* __restrict__ meta, int64_t* __restrict__ nnz) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (npages + 1023) / 1024, q0 = t * per, q1 = min(npages, q0 + per);
+  int64_t s = 0;
+  for (int64_t q = q0; q < q1; ++q) s += counts[q];
+  part[t] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele over the 1024 chunk sums
+    const int64_t o = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += o;
+    __syncthreads();
+  }
+  int64_t run = part[t] - s;
+  for (int64_t q = q0; q < q1; ++q) {
+    meta[q * ZS_META] = (int)run;
+    run += counts[q];
+  }
+  if (t == 1023) *nnz = part[1023];
+}
+
+__global__ __launch_bounds__(256) void zs_compact_kernel(const uint32_t* __restrict__ x, int64_t n,
+                                                         const int* __restrict__ meta, uint32_t* __restrict__ vals,
+                                                         int64_t cap) {
+  __shared__ int sh[4];
+  const int64_t p = blockIdx.x;
+  uint32_t v[8];
+  zs_load8(x, p * ZS_PAGE + 8 * (int64_t)threadIdx.x, n, v);
+  const uint32_t m = zs_byte(v);
+  int total;
+  const int ex = zs_block_scan(__builtin_popcount(m), sh, total);
+  int64_t pos = (int64_t)meta[p * ZS_META] + ex;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (v[i] != 0u) {
+      if (pos < cap) vals[pos] = v[i];
+      ++pos;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void zs_expand_kernel(const int* __restrict__ meta, const uint32_t* __restrict__ vals,
+                                                        int64_t cap, uint32_t* __restrict__ out, int64_t n) {
+  __shared__ int sh[4];
+  const int64_t p = blockIdx.x;
+  const uint32_t w = (uint32_t)meta[p * ZS_META + 1 + (threadIdx.x >> 2)];
+  const uint32_t m = (w >> (8 * (threadIdx.x & 3))) & 0xffu;
+  int total;
+  const int ex = zs_block_scan(__builtin_popcount(m), sh, total);
+  int64_t pos = (int64_t)meta[p * ZS_META] + ex;
+  uint32_t v[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[i] = 0u;
+    if ((m >> i) & 1u) {
+      v[i] = pos < cap ? vals[pos] : 0u;
+      ++pos;
+    }
+  }
+  const int64_t e0 = p * ZS_PAGE + 8 * (int64_t)threadIdx.x;
+  if (e0 + 8 <= n && (reinterpret_cast<uintptr_t>(out) & 15) == 0) {
+    *reinterpret_cast<uint4*>(out + e0) = make_uint4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<uint4*>(out + e0 + 4) = make_uint4(v[4], v[5], v[6], v[7]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (e0 + i < n) out[e0 + i] = v[i];
+  }
+}
+
+}  // namespace tds
+
+using namespace tds;
+
+int64_t tds_zs_npages(int64_t n) { return (n + ZS_PAGE - 1) / ZS_PAGE; }
+
+void tds_zs_encode(const float* x, int64_t n, int* meta, int* counts, float* vals, int64_t cap, int64_t* nnz,
+                   hipStream_t st) {
+  const int64_t P = tds_zs_npages(n);
+  const uint32_t* xb = reinterpret_cast<const uint32_t*>(x);
+  hipLaunchKernelGGL(zs_count_kernel, dim3((unsigned)P), dim3(256), 0, st, xb, n, meta, counts);
+  TDS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(zs_scan_kernel, dim3(1), dim3(1024), 0, st, counts, P, meta, nnz);
+  TDS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(zs_compact_kernel, dim3((unsigned)P), dim3(256), 0, st, xb, n, meta,
+                     reinterpret_cast<uint32_t*>(vals), cap);
+  TDS_LAUNCH_CHECK();
+}
+
+void tds_zs_decode(const int* meta, const float* vals, int64_t cap, float* out, int64_t n, hipStream_t st) {
+  const int64_t P = tds_zs_npages(n);
+  hipLaunchKernelGGL(zs_expand_kernel, dim3((unsigned)P), dim3(256), 0, st, meta,
+                     reinterpret_cast<const uint32_t*>(vals), cap, reinterpret_cast<uint32_t*>(out), n);
+  TDS_LAUNCH_CHECK();
+}

@@ -5,8 +5,8 @@ fp32 NCHW tensors.  This plan runs the network as three
 autograd Functions over NHWC/bf16x3 activations (kernels in
 ``csrc/kernels/convnet_fused.hip``, ``conv2_fwd2.hip``, ``conv2_bwd.hip``, ``head_pb.hip``):
 
-``_Layer1``  x -> p1            conv1 + BN1(batch stats) + ReLU + pool, conv1 never stored
-``_Conv2``   p1 -> y2, ya       conv2 (bf16x3 MFMA) with BN2 batch-stat partials and the 2x2
+``_Layer1``  x -> p1            conv1 + BN1(batch stats) + ReLU + pool, conv1 never stored; p1 in fp16
+``_Conv2``   p1 -> y2, ya       conv2 (fp16x2 MFMA) with BN2 batch-stat partials and the 2x2
                                 max-pool (ya = y2 at each window's argmax, resolved by the sign
                                 of BN2's gamma) fused; its backward rebuilds dy2 from y2 in LDS
                                 (BN2/pool backward fused)
@@ -19,11 +19,18 @@ layer1, so the fc gradient (the 720 MB DDP bucket) is complete — and its
 collective launched — before the conv backward starts (SURVEY.md §3.4 overlap
 property).
 
-Numerics: BN, pooling, fc, the loss and SGD are exact fp32; conv1 and conv2
-(fwd/dgrad/wgrad) use the bf16x3 split (hi*hi + hi*lo + lo*hi, fp32
-accumulate): ~2^-16 relative error per product, tighter than the TF32
-convolutions cuDNN runs for the reference by default.  ``mode='layers'`` is
-the exact-fp32 generic path.
+Numerics: BN, pooling, fc, the loss and SGD are exact fp32.  conv1 (fwd + wgrad) uses the
+bf16x3 split (hi*hi + hi*lo + lo*hi, fp32 accumulate, ~2^-16 per product).  conv2 (fwd, dgrad,
+wgrad) uses the fp16x2 split (csrc/kernels/bf16x3.h): one operand exact as fp16 hi + lo, the
+other rounded once to fp16 -- p1 (stored in fp16) in the forward and the weight gradient, the
+conv2 output gradient (scaled by a power of two per step, from the magnitude bounds ``mag``) in
+the data gradient -- so the per-product error is <= 2^-11, the unit roundoff of the TF32
+convolutions cuDNN runs for the reference by default (TF32 rounds both operands).
+``mode='layers'`` is the exact-fp32 generic path.
+
+Gradient hand-off beside autograd: the fp16 p1 is an autograd output, but its gradient dp1 is
+fp32; the conv2 backward hands dp1 to the layer-1 backward through a link object and gives
+autograd a zero-stride fp16 placeholder (no kernel, no memory), as it does for y2.
 """
 from __future__ import annotations
 
@@ -120,9 +127,15 @@ def _zero_scalar(device, dtype):
     return z
 
 
+class _Layer1Link:
+    """Carries the conv2 backward's fp32 dp1 to the layer-1 backward (p1 itself is fp16)."""
+
+    __slots__ = ("dp1",)
+
+
 class _Layer1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps):
+    def forward(ctx, x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps, link1):
         ops = _ext.ops()
         asum, strips = _take_input_stats(x)
         x = x.contiguous()
@@ -130,16 +143,18 @@ class _Layer1(torch.autograd.Function):
                                                       strips)
         ctx.save_for_backward(x, p1, idx1, w1, b1, g1, stats1, gram)
         ctx.params = (w1, b1, g1, be1)
+        ctx.link1 = link1
         ctx.mark_non_differentiable(idx1)
         return p1
 
     @staticmethod
-    def backward(ctx, dp1):
+    def backward(ctx, _dp1_placeholder):
         x, p1, idx1, w1, b1, g1, stats1, gram = ctx.saved_tensors
+        dp1 = ctx.link1.dp1
+        ctx.link1.dp1 = None
         outs = _sinks(ctx, ctx.params, 1)
-        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1.contiguous(), x, p1, idx1, w1, b1, g1, stats1, gram, 1.0,
-                                                           *outs)
-        return None, dw1, db1, dg1, dbe1, None, None, None, None, None
+        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1, x, p1, idx1, w1, b1, g1, stats1, gram, 1.0, *outs)
+        return None, dw1, db1, dg1, dbe1, None, None, None, None, None, None
 
 
 class _Layer2Link:
@@ -148,18 +163,22 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag")
 
 
 class _Conv2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, p1, w2, b2, g2, link):
+    def forward(ctx, p1, w2, b2, g2, link, link1):
         ops = _ext.ops()
-        wp, wd = ops.conv2_pack(w2.contiguous())
-        y2, partial2, ya = ops.fused_conv2_forward(p1, wp, b2, g2)
+        # magnitude bounds of this step (max |y2| per channel here, max |g2m| in the head
+        # backward): the conv2 backward's fp16 scale of dy2; reset by conv2_pack
+        link.mag = torch.empty(33, device=p1.device, dtype=torch.int32)
+        wp, wd = ops.conv2_pack(w2.contiguous(), link.mag)
+        y2, partial2, ya = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
         ctx.save_for_backward(p1, wd, y2)
         ctx.params = (w2, b2)
         ctx.link = link
+        ctx.link1 = link1
         ctx.mark_non_differentiable(partial2, ya)
         # no zero-filled gradients for partial2 / ya (a 360 MB fill per step at the bench shape)
         ctx.set_materialize_grads(False)
@@ -171,10 +190,14 @@ class _Conv2(torch.autograd.Function):
         link = ctx.link
         _run_before_conv2_backward()
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
-        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, p1, wd, 1.0,
+        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, link.mag, p1, wd, 1.0,
                                                            *_sinks(ctx, ctx.params, 1))
-        link.g2m = link.kbuf = link.aff2 = None
-        return (dp1 if ctx.needs_input_grad[0] else None), dw2, db2, None, None
+        link.g2m = link.kbuf = link.aff2 = link.mag = None
+        dp1_ph = None
+        if ctx.needs_input_grad[0]:
+            ctx.link1.dp1 = dp1
+            dp1_ph = _zero_scalar(p1.device, p1.dtype).expand(p1.shape)
+        return dp1_ph, dw2, db2, None, None, None
 
 
 class _Head(torch.autograd.Function):
@@ -224,7 +247,7 @@ class _Head(torch.autograd.Function):
                 last = i == len(chunks) - 1
                 res = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, dst, 1.0, True, 0.0,
                                               None, dg_o if last else None, dbe_o if last else None, True,
-                                              k0 // (Q * Q), k1 // (Q * Q), last, g2m_buf, part)
+                                              k0 // (Q * Q), k1 // (Q * Q), last, g2m_buf, part, ctx.link.mag)
                 if acc_w:
                     dw[:, k0:k1].add_(dst[:, k0:k1])
                 ex.chunk_ready(dw, k0, k1)
@@ -236,7 +259,7 @@ class _Head(torch.autograd.Function):
         elif ex is not None:
             # fc gradients come from the activation exchange (parallel/factored.py)
             _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, None, 1.0,
-                                                                 False)
+                                                                 False, mag=ctx.link.mag)
             ex.defer(dlogits)
             dW = dbfc = None
         else:
@@ -250,7 +273,8 @@ class _Head(torch.autograd.Function):
             dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (12, 4, 5))
             dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P,
                                                                      dw_out if keep else None, 1.0, True,
-                                                                     float(lr or 0.0), dbfc_o, dg_o, dbe_o, keep)
+                                                                     float(lr or 0.0), dbfc_o, dg_o, dbe_o, keep,
+                                                                     mag=ctx.link.mag)
             if lr:
                 # update-only step: no gradient for the weight (dW is None), as in torch's
                 # optimizer-in-backward; the owner marks the parameter ready
@@ -266,10 +290,11 @@ def forward(model, x):
     conv1, bn1 = model.layer1[0], model.layer1[1]
     conv2, bn2 = model.layer2[0], model.layer2[1]
     fc = model.fc
+    link1 = _Layer1Link()
     p1 = _Layer1.apply(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
-                       bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps))
+                       bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps), link1)
     link = _Layer2Link()
-    y2, partial2, ya = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, link)
+    y2, partial2, ya = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, link, link1)
     # the fc update may still be running on DDP's side stream (overlap_optimizer): wait here,
     # after the convolutions were queued, not before
     param_fence.wait(fc.weight)

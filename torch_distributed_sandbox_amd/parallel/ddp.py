@@ -71,7 +71,7 @@ class DistributedDataParallel(nn.Module):
                  gradient_as_bucket_view: bool = True, flat_params: bool = True, static_graph: bool = False,
                  reducer: str = "auto", grad_exchange: str = "auto", overlap_optimizer: bool = False,
                  fuse_update_in_backward: bool = True, keep_fused_grads: bool = False,
-                 allreduce_chunks: Optional[int] = None):
+                 allreduce_chunks: Optional[int] = None, exchange_compress: bool = True):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -181,7 +181,8 @@ class DistributedDataParallel(nn.Module):
                 self._exchanges.append(factored.ActivationExchange(
                     lyr.weight, lyr.bias, process_group, self.world_size, grad_exchange,
                     self._make_skip_fn(b), self._make_view_fn(lyr.weight),
-                    self._make_view_fn(lyr.bias) if lyr.bias is not None else None, chunks=self.allreduce_chunks))
+                    self._make_view_fn(lyr.bias) if lyr.bias is not None else None, chunks=self.allreduce_chunks,
+                    compress=exchange_compress))
 
         # ---- overlapped optimizer: the big layers' buckets finish (collective + SGD
         # update) on a side stream while the next forward's convolutions run

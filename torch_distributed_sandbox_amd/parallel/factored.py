@@ -43,6 +43,16 @@ dense gradient is the smallest message, and a third mode shortens its critical p
 The result is the average DDP produces (floating-point summation order differs,
 as it does between all-reduce algorithms), bit-identical on every rank.
 
+Zero suppression (``compress``, default on): X is a ReLU output, so the activation exchange
+sends it zero-suppressed (parallel/zs.py: a bitmask plus the non-zero values, rebuilt bit for bit
+on the receiver -- the gradient and the parameters after the step are bitwise those of the dense
+exchange).  Two all-gathers: the fixed-size mask/offset record (3.2 % of the dense rows, with
+each rank's non-zero count in its tail) and the values at a capacity ``cap`` kept from earlier
+steps (the first step sends the dense size).  The host learns the counts from the first gather
+only when the step's gradient is formed (``defer``, after the head backward is queued); a count
+above the capacity sends the dense rows once more for that step.  The byte model takes the
+measured ratio: ``link_bytes("activations")`` = B·K·4·ratio.
+
 Protocol (driven by ``parallel/ddp.py``):
 
 * ``arm(sync)`` each DDP forward: the exchange may run this step.
@@ -73,23 +83,24 @@ def get(weight) -> Optional["ActivationExchange"]:
     return getattr(weight, _ATTR, None) if weight is not None else None
 
 
-def link_bytes(path: str, rows: int, out_f: int, in_f: int, world: int, elem: int = 4) -> float:
-    """Bytes one rank sends over each of its links per step for ``path`` (model above)."""
+def link_bytes(path: str, rows: int, out_f: int, in_f: int, world: int, elem: int = 4, x_ratio: float = 1.0) -> float:
+    """Bytes one rank sends over each of its links per step for ``path`` (model above);
+    ``x_ratio``: the zero-suppressed size of the activation rows relative to dense."""
     if world <= 1:
         return 0.0
     if path == "allreduce":
         return 2.0 * out_f * in_f * elem / world
     if path == "activations":
-        return float(rows * in_f * elem)
+        return float(rows * in_f * elem) * x_ratio
     if path == "sharded":
         return float((rows + out_f) * in_f * elem) / world
     raise ValueError(path)
 
 
-def choose_path(rows: int, out_f: int, in_f: int, world: int) -> str:
+def choose_path(rows: int, out_f: int, in_f: int, world: int, x_ratio: float = 1.0) -> str:
     """Cheapest of allreduce / activations / sharded by per-link bytes (ties: earlier start)."""
     order = ("activations", "sharded", "allreduce")
-    costs = {p: link_bytes(p, rows, out_f, in_f, world) for p in order}
+    costs = {p: link_bytes(p, rows, out_f, in_f, world, x_ratio=x_ratio) for p in order}
     return min(order, key=lambda p: (costs[p], order.index(p)))
 
 
@@ -102,8 +113,11 @@ def shard_bounds(in_f: int, world: int) -> List[Tuple[int, int]]:
 class ActivationExchange:
     """One exchange-capable Linear layer under DDP (see the module docstring)."""
 
+    CAP_MARGIN = 1.03     # value capacity over the largest recent non-zero count
+    CAP_ROUND = 1 << 16   # capacities rounded up to 64 Ki elements (stable allocations)
+
     def __init__(self, weight: torch.nn.Parameter, bias: Optional[torch.nn.Parameter], group, world: int,
-                 mode: str, set_skip, weight_view, bias_view, chunks: int = 1):
+                 mode: str, set_skip, weight_view, bias_view, chunks: int = 1, compress: bool = True):
         if mode not in ("auto", "activations", "sharded", "chunked", "allreduce"):
             raise ValueError(f"ActivationExchange mode must be auto|activations|sharded|chunked|allreduce, got {mode!r}")
         self.weight, self.bias = weight, bias
@@ -118,6 +132,12 @@ class ActivationExchange:
         self._x_buf = self._x_work = self._dy = self._x_local = None
         self.side_stream = None  # DDP(overlap_optimizer=True): its update stream, which also finishes the exchange
         self._own_stream = None  # otherwise (GPU): a private side stream
+        # zero-suppressed activation rows (parallel/zs.py)
+        self.compress = bool(compress)
+        self._zs = None  # this step's encoded exchange: dict
+        self._cap = None  # value capacity per rank (elements), from earlier steps' counts
+        self.x_ratio = 1.0  # measured zero-suppressed / dense bytes of the last compressed step
+        self.zs_stats = {"steps": 0, "overflows": 0, "last_nnz": None}
         setattr(weight, _ATTR, self)
 
     def detach(self):
@@ -135,7 +155,7 @@ class ActivationExchange:
         if self.world <= 1 or self.mode != "auto":
             return None
         out_f, in_f = self.weight.shape
-        p = choose_path(rows, out_f, in_f, self.world)
+        p = choose_path(rows, out_f, in_f, self.world, x_ratio=self.x_ratio if self.compress else 1.0)
         # auto's all-reduce regime is the plain bucket all-reduce: the chunked path costs more
         # compute than it saves on the links (W=1 forced: +4.4 ms/step, docs/DISTRIBUTED.md), so
         # it runs only when asked for
@@ -255,7 +275,9 @@ class ActivationExchange:
             return True
         x2d = x2d.detach().contiguous()
         rows, in_f = x2d.shape
-        if path == "activations":
+        if path == "activations" and self.compress and x2d.dtype == torch.float32:
+            self._begin_zs(x2d)
+        elif path == "activations":
             self._x_buf = torch.empty((self.world * rows, in_f), device=x2d.device, dtype=x2d.dtype)
             self._x_work = tdist.all_gather_into_tensor(self._x_buf, x2d, group=self.group, async_op=True)
         else:
@@ -272,6 +294,97 @@ class ActivationExchange:
         self._set_skip(True)
         return True
 
+    def _begin_zs(self, x2d: torch.Tensor):
+        """Zero-suppressed all-gather of the rows (module docstring): encode, gather the fixed-
+        size mask/offset records with each rank's count in their tail, then the values at this
+        step's capacity.  The counts are copied to the host asynchronously after the first
+        gather, so ``defer`` can check them without waiting for the values."""
+        from . import distributed as tdist
+        from . import zs
+
+        W, dev = self.world, x2d.device
+        n = x2d.numel()
+        M = zs.meta_numel(n)
+        cap = min(n, self._cap) if self._cap else n
+        meta = torch.empty(M + 2, device=dev, dtype=torch.int32)
+        vals = torch.empty(cap, device=dev, dtype=torch.float32)
+        nnz = zs.encode(x2d, meta[:M], vals)
+        meta[M:].view(torch.int64).copy_(nnz.view(1).to(dev))
+        meta_all = torch.empty(W * (M + 2), device=dev, dtype=torch.int32)
+        w_meta = tdist.all_gather_into_tensor(meta_all, meta, group=self.group, async_op=True)
+        counts_host = counts_ev = None
+        if dev.type == "cuda":
+            # the counts to the host behind the first gather only (not behind the values)
+            cstream = self._count_stream(dev)
+            with torch.cuda.stream(cstream):
+                w_meta.wait()
+                counts = meta_all.view(W, M + 2)[:, M:].contiguous().view(torch.int64).view(W)
+                counts_host = torch.empty(W, dtype=torch.int64, pin_memory=True)
+                counts_host.copy_(counts, non_blocking=True)
+                counts_ev = torch.cuda.Event()
+                counts_ev.record(cstream)
+                meta_all.record_stream(cstream)
+        vals_all = torch.empty(W * cap, device=dev, dtype=torch.float32)
+        w_vals = tdist.all_gather_into_tensor(vals_all, vals, group=self.group, async_op=True)
+        self._zs = {"n": n, "M": M, "cap": cap, "meta": meta, "vals": vals, "meta_all": meta_all, "vals_all": vals_all,
+                    "w_meta": w_meta, "w_vals": w_vals, "counts_host": counts_host, "counts_ev": counts_ev,
+                    "rows": x2d.shape[0], "in_f": x2d.shape[1]}
+        self._x_work = None  # set by _zs_resolve
+
+    def _count_stream(self, dev):
+        st = getattr(self, "_cstream", None)
+        if st is None:
+            st = self._cstream = torch.cuda.Stream(device=dev)
+        return st
+
+    def _zs_resolve(self):
+        """Host side of the zero-suppressed gather (called from ``defer`` on the host): check the
+        counts against the capacity, update the capacity for the next steps, and set up the
+        dense rows self._x_buf with a work that completes once they are rebuilt (or, on an
+        overflow, once the dense fallback gather has landed)."""
+        from . import distributed as tdist
+
+        z, self._zs = self._zs, None
+        W, n, cap = self.world, z["n"], z["cap"]
+        if z["counts_ev"] is not None:
+            z["counts_ev"].synchronize()
+            counts = [int(v) for v in z["counts_host"].tolist()]
+        else:  # CPU: the gathers are synchronous enough to read directly
+            z["w_meta"].wait()
+            M = z["M"]
+            counts = [int(v) for v in z["meta_all"].view(W, M + 2)[:, M:].contiguous().view(torch.int64).view(W)]
+        mx = max(counts)
+        self.zs_stats["steps"] += 1
+        self.zs_stats["last_nnz"] = counts
+        self._cap = min(n, -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND)
+        self.x_ratio = (mx + (z["M"] + 2) * 1.0) / n  # bytes relative to dense (4-byte words both)
+        rows, in_f = z["rows"], z["in_f"]
+        self._x_buf = torch.empty((W * rows, in_f), device=z["meta"].device, dtype=torch.float32)
+        if mx > cap:  # a count above this step's capacity: the dense rows, once
+            self.zs_stats["overflows"] += 1
+            z["w_vals"].wait()
+            self._x_work = tdist.all_gather_into_tensor(self._x_buf, self._x_local, group=self.group, async_op=True)
+            return
+        self._zs_decode_pending = z
+
+    def _zs_decode(self):
+        """Rebuild every rank's rows into self._x_buf (current stream = where the gradient is
+        formed), after the values gather."""
+        from . import zs
+
+        z = getattr(self, "_zs_decode_pending", None)
+        if z is None:
+            return
+        self._zs_decode_pending = None
+        z["w_meta"].wait()
+        z["w_vals"].wait()
+        W, n, M, cap = self.world, z["n"], z["M"], z["cap"]
+        meta_all = z["meta_all"].view(W, M + 2)
+        vals_all = z["vals_all"].view(W, cap)
+        out = self._x_buf.view(W, n)
+        for r in range(W):
+            zs.decode(meta_all[r, :M], vals_all[r], out[r])
+
     # ---------------------------------------------------------------- backward
     def defer(self, dy: torch.Tensor, x2: Optional[torch.Tensor] = None):
         """Called from the layer's backward with dY.  On the GPU the rest of the exchange
@@ -284,6 +397,8 @@ class ActivationExchange:
             self.chunked_linear_backward(dy.detach().contiguous(), x2.detach())
             return
         self._dy = dy.detach().contiguous()
+        if self._zs is not None:
+            self._zs_resolve()
         if not self._dy.is_cuda:
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
             return
@@ -297,6 +412,9 @@ class ActivationExchange:
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
         keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
+        z = getattr(self, "_zs_decode_pending", None)
+        if z is not None:
+            keep = keep + (z["meta_all"], z["vals_all"], z["meta"], z["vals"])
         with torch.cuda.stream(side):
             for t in keep:
                 t.record_stream(side)
@@ -328,7 +446,10 @@ class ActivationExchange:
         rows = dy.shape[0]
         dy_all = torch.empty((self.world * rows, dy.shape[1]), device=dy.device, dtype=dy.dtype)
         tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
-        self._x_work.wait()
+        if getattr(self, "_zs_decode_pending", None) is not None:
+            self._zs_decode()
+        else:
+            self._x_work.wait()
         scale = 1.0 / self.world
         from ..ops import fused_update
 
@@ -366,6 +487,8 @@ class ActivationExchange:
 
     def _done(self):
         self.last_path = "activation-exchange" if self.active == "activations" else "sharded-exchange"
+        if self.active == "activations" and self.compress and self.zs_stats["steps"]:
+            self.last_path = "activation-exchange(zs)"
         self._x_buf = self._x_work = self._dy = self._x_local = None
         self.active = None
         self.steps_exchanged += 1
