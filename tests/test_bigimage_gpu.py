@@ -1,6 +1,7 @@
 """One fused-plan training step on an image past every 32-bit / 2 GiB boundary: B=1, H=24000
 (x alone is 2.3 GB, the fc weight 11.5 G parameters = 46 GB), checked against a chunked fp64
-reference computed on the same GPU (the OOM story of the reference, README.md:9-15, scaled to
+reference computed on the same GPU -- the loss, BN running statistics, the fc weight gradient
+past flat index 2^31 and the conv2 weight / bias gradients (the OOM story of the reference, README.md:9-15, scaled to
 288 GB per MI355X).  The reference runs the reference model's ops (Conv2d -> BatchNorm2d(train) ->
 ReLU -> MaxPool2d, twice, then Linear and CrossEntropy, mnist_onegpu.py:14-24) in fp64, row chunk
 by row chunk, with the convolutions as unfold + GEMM."""
@@ -52,6 +53,15 @@ def _layer(x, w, b, g, be, nrows):
     return torch.cat(out, 1), mean, var, n
 
 
+@torch.no_grad()
+def _cols(x, r0, r1):
+    """im2col of conv output rows [r0, r1) of x [C, H, W] (5x5, zero padding 2): [C*25, rows*W]."""
+    C, Hh, Ww = x.shape
+    lo, hi = max(0, r0 - 2), min(Hh, r1 + 2)
+    xc = F.pad(x[:, lo:hi].double(), (2, 2, 2 - (r0 - lo), 2 - (hi - r1)))
+    return F.unfold(xc.unsqueeze(0), 5)[0]
+
+
 def test_one_step_beyond_2gib(gpu):
     from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import CrossEntropyLoss
@@ -66,6 +76,12 @@ def test_one_step_beyond_2gib(gpu):
     loss.backward()
     ours = float(loss.item())
     assert all(torch.isfinite(p.grad).all().item() for p in m.parameters())
+    # gradient slices to check against fp64 below: conv2's weight / bias (the fp16x2 backward over
+    # 144 M positions) and the fc weight's last two pooled rows of channel 31 of class 9 (flat
+    # index ~10.4 G, far past 2^31)
+    Qg = H // 4
+    fc_tail = m.fc.weight.grad.view(10, 32, Qg, Qg)[9, 31, -2:].clone()
+    dw2_ours, db2_ours = m.layer2[0].weight.grad.clone(), m.layer2[0].bias.grad.clone()
     for p in m.parameters():
         p.grad = None
     del loss
@@ -83,7 +99,6 @@ def test_one_step_beyond_2gib(gpu):
     torch.cuda.empty_cache()
     P = H // 2
     p2, mean2, var2, n2 = _layer(p1, c2.weight, c2.bias, bn2.weight, bn2.bias, P)
-    del p1
     torch.testing.assert_close(bn2.running_mean.double(), 0.1 * mean2, rtol=1e-4, atol=1e-6)
     Q = P // 2
     W = m.fc.weight.detach().view(10, 32, Q, Q)
@@ -91,6 +106,52 @@ def test_one_step_beyond_2gib(gpu):
     for r0 in range(0, Q, 256):
         r1 = min(Q, r0 + 256)
         logits += torch.einsum("jchw,chw->j", W[:, :, r0:r1].double(), p2[:, r0:r1])
-    del p2
     ref = float(F.cross_entropy(logits.unsqueeze(0), y))
     assert abs(ours - ref) <= 1e-4 * max(1.0, abs(ref)), (ours, ref)
+    # fc weight gradient past 2^31: dW[j] = dl[j] * X (batch 1, mean loss)
+    dl = torch.softmax(logits, 0)
+    dl[int(y)] -= 1.0
+    torch.testing.assert_close(fc_tail.double(), dl[9] * p2[31, -2:], rtol=1e-5, atol=1e-12)
+    # conv2 weight / bias gradient: dL/dp2 = sum_j dl[j] W[j], then the fp64 chain
+    dp2 = torch.zeros_like(p2)
+    for r0 in range(0, Q, 256):
+        r1 = min(Q, r0 + 256)
+        dp2[:, r0:r1] = torch.einsum("j,jchw->chw", dl, W[:, :, r0:r1].double())
+    del p2
+    # fp64 chain BN2(train) -> ReLU -> MaxPool backward, then conv2's weight gradient as
+    # dy @ im2col(p1)^T, chunk by chunk: pass 1 forms the BN2 backward sums, pass 2 the gradient
+    # (one im2col per chunk and pass, shared by the conv recompute and the gradient GEMM)
+    w2 = c2.weight.detach().double().view(32, 400)
+    b2 = c2.bias.detach().double().view(32, 1)
+    a2 = bn2.weight.detach().double() / torch.sqrt(var2 + 1e-5)
+    sh2 = bn2.bias.detach().double() - mean2 * a2
+    inv = 1.0 / torch.sqrt(var2 + 1e-5)
+
+    def chunk(r0, r1):
+        cols = _cols(p1, r0, r1)
+        yc = (w2 @ cols + b2).view(32, r1 - r0, P)
+        z = yc * a2.view(-1, 1, 1) + sh2.view(-1, 1, 1)
+        r = torch.relu(z)
+        _, idx = F.max_pool2d(r.unsqueeze(0), 2, 2, return_indices=True)
+        dr = F.max_unpool2d(dp2[:, r0 // 2:r1 // 2].unsqueeze(0), idx, 2, 2, output_size=r.shape[-2:])[0]
+        dz = dr * (z > 0)
+        xh = (yc - mean2.view(-1, 1, 1)) * inv.view(-1, 1, 1)
+        return cols, dz, xh
+
+    sdz = torch.zeros(32, dtype=torch.float64, device=gpu)
+    sdzx = torch.zeros_like(sdz)
+    for r0 in range(0, P, ROWS):
+        _, dz, xh = chunk(r0, min(P, r0 + ROWS))
+        sdz += dz.sum((1, 2))
+        sdzx += (dz * xh).sum((1, 2))
+    dw2 = torch.zeros(32, 400, dtype=torch.float64, device=gpu)
+    db2 = torch.zeros(32, dtype=torch.float64, device=gpu)
+    for r0 in range(0, P, ROWS):
+        cols, dz, xh = chunk(r0, min(P, r0 + ROWS))
+        dy = a2.view(-1, 1, 1) * (dz - (sdz / n2).view(-1, 1, 1) - xh * (sdzx / n2).view(-1, 1, 1))
+        dw2 += dy.reshape(32, -1) @ cols.t()
+        db2 += dy.sum((1, 2))
+    rel = ((dw2_ours.double().view(32, 400) - dw2).norm() / dw2.norm()).item()
+    assert rel <= 2e-3, f"layer2.0.weight grad rel L2 err {rel:.2e}"
+    # conv bias before BN: analytically zero, both sides rounding noise
+    assert (db2_ours.double() - db2).abs().max().item() <= 1e-3 * dw2.abs().max().item() + 1e-9

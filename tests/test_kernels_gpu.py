@@ -184,3 +184,27 @@ def test_zs_encode_decode_matches_reference(gpu, n):
         small = torch.full((rnnz // 2,), -1.0, device=gpu)
         assert int(zs.encode(x, meta, small)) == rnnz
         assert torch.equal(small.cpu().view(torch.int32), rvals[:rnnz // 2].view(torch.int32))
+
+
+def test_zs_segmented_codec_matches_reference(gpu):
+    """Segmented codec of the sharded exchange (zs_seg_* kernels) vs the torch reference:
+    (destination shard, row) segments of uneven length, an empty one, capacity slots."""
+    from torch_distributed_sandbox_amd.parallel import zs
+
+    torch.manual_seed(4)
+    B, K = 3, 9000
+    x = torch.relu(torch.randn(B, K, device=gpu))
+    bounds = [(0, 2560), (2560, 2560), (2560, 6400), (6400, 9000)]  # one empty shard
+    segs = [(b * K + a, e - a) for (a, e) in bounds for b in range(B)]
+    cap = 2100
+    lay_g, lay_c = zs.SegLayout(segs, gpu), zs.SegLayout(segs, "cpu")
+    meta = torch.empty(lay_g.meta_numel, dtype=torch.int32, device=gpu)
+    vals = torch.empty(lay_g.nseg * cap, device=gpu)
+    cnt = zs.seg_encode(x, lay_g, meta, vals, cap)
+    rmeta = torch.empty(lay_c.meta_numel, dtype=torch.int32)
+    rvals = torch.zeros(lay_c.nseg * cap)
+    rcnt = zs.seg_encode(x.cpu(), lay_c, rmeta, rvals, cap)
+    assert torch.equal(cnt.cpu(), rcnt) and torch.equal(meta.cpu(), rmeta)
+    out = torch.full((B, K), 9.0, device=gpu)
+    zs.seg_decode(meta, lay_g, vals, cap, out)
+    assert torch.equal(out, x)

@@ -447,6 +447,11 @@ int64_t cu_masked_stream(int64_t device, int64_t reserve, bool striped) {
 // the communication stream of the CU split (0 when no CUs are reserved)
 int64_t cu_comm_stream(int64_t device) { return (int64_t)reinterpret_cast<intptr_t>(tds_cu_comm_stream((int)device)); }
 
+// a further stream on one side of the CU split (0 when no CUs are reserved)
+int64_t cu_side_stream(int64_t device, bool comm) {
+  return (int64_t)reinterpret_cast<intptr_t>(tds_cu_side_stream((int)device, comm));
+}
+
 // one-GPU rehearsal of a collective's CU footprint (cu_budget.hip): `nblocks` workgroups of 256
 // threads holding `lds_bytes` of LDS each for `us` microseconds, on the current stream
 void comm_spin(const Tensor& like, int64_t us, int64_t nblocks, int64_t lds_bytes) {
@@ -551,10 +556,66 @@ void zs_decode(const Tensor& meta, const Tensor& values, const Tensor& out) {
   check_launches("zs_decode");
 }
 
+void check_pages(const Tensor& start, const Tensor& cnt, const Tensor& seg, const Tensor& like) {
+  TORCH_CHECK(start.is_cuda() && start.scalar_type() == at::kLong && start.dim() == 1 && start.is_contiguous(),
+              "zs pages: start int64 [npages]");
+  need(cnt, at::kInt, {start.numel()}, "zs pages: cnt");
+  need(seg, at::kInt, {start.numel()}, "zs pages: seg");
+  TORCH_CHECK(start.device() == like.device(), "zs pages: one device");
+}
+
+// segmented encode (parallel/zs.py SegLayout): returns seg_nnz [nseg] int64
+Tensor zs_seg_encode(const Tensor& x, const Tensor& pg_start, const Tensor& pg_cnt, const Tensor& pg_seg,
+                     const Tensor& seg_first, const Tensor& seg_npg, const Tensor& meta_out, const Tensor& values_out,
+                     int64_t cap) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), "zs_seg_encode: x fp32 GPU");
+  check_pages(pg_start, pg_cnt, pg_seg, x);
+  const int64_t P = pg_start.numel(), S = seg_first.numel();
+  need(seg_first, at::kInt, {S}, "zs seg_first");
+  need(seg_npg, at::kInt, {S}, "zs seg_npg");
+  need(meta_out, at::kInt, {P * 65}, "zs meta_out");
+  TORCH_CHECK(values_out.is_cuda() && values_out.scalar_type() == at::kFloat && values_out.numel() == S * cap &&
+                  values_out.is_contiguous(),
+              "zs_seg_encode: values_out fp32 [nseg * cap]");
+  c10::DeviceGuard guard(x.device());
+  auto counts = at::empty({P}, x.options().dtype(at::kInt));
+  auto nnz = at::empty({S}, x.options().dtype(at::kLong));
+  if (P > 0)
+    tds_zs_seg_encode(x.data_ptr<float>(), pg_start.data_ptr<int64_t>(), pg_cnt.data_ptr<int>(), pg_seg.data_ptr<int>(),
+                      P, seg_first.data_ptr<int>(), seg_npg.data_ptr<int>(), (int)S, meta_out.data_ptr<int>(),
+                      counts.data_ptr<int>(), values_out.data_ptr<float>(), cap, nnz.data_ptr<int64_t>(), stream_of(x));
+  else
+    nnz.zero_();
+  check_launches("zs_seg_encode");
+  return nnz;
+}
+
+void zs_seg_decode(const Tensor& meta, const Tensor& pg_start, const Tensor& pg_cnt, const Tensor& pg_seg,
+                   const Tensor& values, int64_t cap, const Tensor& out) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous(), "zs_seg_decode: out fp32 GPU");
+  check_pages(pg_start, pg_cnt, pg_seg, out);
+  const int64_t P = pg_start.numel();
+  need(meta, at::kInt, {P * 65}, "zs meta");
+  TORCH_CHECK(values.is_cuda() && values.scalar_type() == at::kFloat && values.is_contiguous(), "zs_seg_decode: values");
+  c10::DeviceGuard guard(out.device());
+  if (P > 0)
+    tds_zs_seg_decode(meta.data_ptr<int>(), pg_start.data_ptr<int64_t>(), pg_cnt.data_ptr<int>(), pg_seg.data_ptr<int>(),
+                      P, values.data_ptr<float>(), cap, out.data_ptr<float>(), stream_of(out));
+  check_launches("zs_seg_decode");
+}
+
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("zs_encode(Tensor x, Tensor(a!) meta_out, Tensor(b!) values_out) -> Tensor", &zs_encode);
+  m.def(
+      "zs_seg_encode(Tensor x, Tensor pg_start, Tensor pg_cnt, Tensor pg_seg, Tensor seg_first, Tensor seg_npg, "
+      "Tensor(a!) meta_out, Tensor(b!) values_out, int cap) -> Tensor",
+      &zs_seg_encode);
+  m.def(
+      "zs_seg_decode(Tensor meta, Tensor pg_start, Tensor pg_cnt, Tensor pg_seg, Tensor values, int cap, "
+      "Tensor(a!) out) -> ()",
+      &zs_seg_decode);
   m.def("zs_decode(Tensor meta, Tensor values, Tensor(a!) out) -> ()", &zs_decode);
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
@@ -599,4 +660,5 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("comm_spin(Tensor like, int us, int nblocks, int lds_bytes) -> ()", &comm_spin);
   m.def("cu_probe(Tensor like, int us, int nblocks) -> Tensor", &cu_probe);
   m.def("cu_comm_stream(int device) -> int", &cu_comm_stream);
+  m.def("cu_side_stream(int device, bool comm) -> int", &cu_side_stream);
 }

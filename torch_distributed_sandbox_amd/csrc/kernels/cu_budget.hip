@@ -107,6 +107,40 @@ hipStream_t tds_cu_comm_stream(int device) {
   return s;
 }
 
+// A further stream of `device` on one side of the current split (comm: the reserved CUs; else
+// the compute CUs), distinct from the communicator's and the compute stream: DDP's side work
+// (the exchange's dW formation, the deferred SGD step) runs there so it neither lands on CUs a
+// persistent compute workgroup waits for nor queues behind RCCL's kernels.  nullptr when no
+// CUs are reserved.  Cached per (device, reserve, numbering, side).
+hipStream_t tds_cu_side_stream(int device, bool comm) {
+  const int reserve = g_reserve.load(std::memory_order_relaxed);
+  const bool striped = g_striped.load(std::memory_order_relaxed);
+  if (reserve <= 0 || reserve % 8 != 0 || device < 0 || device >= kMaxDev) return nullptr;
+  const int key = (reserve * 2 + (striped ? 1 : 0)) * 2 + (comm ? 1 : 0);
+  static std::mutex mu;
+  static std::vector<std::pair<std::pair<int, int>, hipStream_t>> cache;
+  std::lock_guard<std::mutex> g(mu);
+  for (auto& e : cache)
+    if (e.first.first == device && e.first.second == key) return e.second;
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  hipDeviceProp_t prop;
+  hipStream_t s = nullptr;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) {
+    const int n = prop.multiProcessorCount, nxcd = 8, per = n / nxcd, rx = reserve / nxcd;
+    if (n % nxcd == 0 && per - rx >= 1) {
+      std::vector<uint32_t> mask((n + 31) / 32, 0u);
+      for (int cu = 0; cu < n; ++cu)
+        if ((cu_local(cu, nxcd, per, striped) >= per - rx) == comm) mask[cu / 32] |= 1u << (cu % 32);
+      if (hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()) != hipSuccess) s = nullptr;
+    }
+  }
+  (void)hipSetDevice(prev);
+  if (s) cache.push_back({{device, key}, s});
+  return s;
+}
+
 // ---- one-GPU rehearsal of a collective's CU footprint -----------------------------------
 // RCCL's generic kernel on gfx950 takes 256 threads, 19.7 KB of LDS and 261-280 VGPRs per
 // workgroup (librccl code-object metadata), one workgroup per channel, resident for the whole

@@ -72,6 +72,7 @@ void tds_set_cu_reserve(int n);
 int tds_cu_reserve();
 hipStream_t tds_cu_masked_stream(int device, int reserve, bool striped);
 hipStream_t tds_cu_comm_stream(int device);
+hipStream_t tds_cu_side_stream(int device, bool comm);  // a further stream on one side of the split
 void tds_comm_spin(int64_t us, int nblocks, int lds_bytes, int* sink, hipStream_t st);
 void tds_cu_probe(int64_t us, int nblocks, int* out, hipStream_t st);
 int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c, int group_rows);  // host: blocked tile order table
@@ -143,3 +144,10 @@ int64_t tds_zs_npages(int64_t n);
 void tds_zs_encode(const float* x, int64_t n, int* meta, int* counts, float* vals, int64_t cap, int64_t* nnz,
                    hipStream_t st);
 void tds_zs_decode(const int* meta, const float* vals, int64_t cap, float* out, int64_t n, hipStream_t st);
+// segmented form (the sharded exchange): page table (start, cnt, seg) + per-segment first page /
+// page count; values in fixed-capacity slots per segment; seg_nnz [nseg] int64
+void tds_zs_seg_encode(const float* x, const int64_t* pg_start, const int* pg_cnt, const int* pg_seg, int64_t npages,
+                       const int* seg_first, const int* seg_npg, int nseg, int* meta, int* counts, float* vals,
+                       int64_t cap, int64_t* seg_nnz, hipStream_t st);
+void tds_zs_seg_decode(const int* meta, const int64_t* pg_start, const int* pg_cnt, const int* pg_seg, int64_t npages,
+                       const float* vals, int64_t cap, float* out, hipStream_t st);

@@ -150,9 +150,148 @@ __global__ __launch_bounds__(256) void zs_expand_kernel(const int* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------------------- segmented
+// The sharded exchange encodes each (row, destination shard) slice of X as a SEGMENT of its own
+// (offsets restart per segment, values go to a fixed-capacity slot per segment), so every
+// destination's part is one contiguous meta range and one run of value slots.  A page table
+// (built once per layout on the host, parallel/zs.py) gives each page its element start in the
+// source (encode) or destination (decode) tensor, its element count (<= 2048) and its segment;
+// each segment's pages are consecutive.
+struct ZSPages {
+  const int64_t* start;  // element start of page g
+  const int* cnt;        // elements in page g
+  const int* seg;        // segment of page g
+};
+
+__device__ __forceinline__ void zs_load_n(const uint32_t* __restrict__ x, int64_t e0, int n, uint32_t (&v)[8]) {
+  const int t0 = 8 * (int)threadIdx.x;
+  if (t0 + 8 <= n && ((reinterpret_cast<uintptr_t>(x + e0 + t0)) & 15) == 0) {
+    const uint4 a = *reinterpret_cast<const uint4*>(x + e0 + t0), b = *reinterpret_cast<const uint4*>(x + e0 + t0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = t0 + i < n ? x[e0 + t0 + i] : 0u;
+  }
+}
+
+__global__ __launch_bounds__(256) void zs_seg_count_kernel(const uint32_t* __restrict__ x, ZSPages pg,
+                                                           int* __restrict__ meta, int* __restrict__ counts) {
+  __shared__ uint32_t bytes[256];
+  __shared__ int sh[4];
+  const int64_t g = blockIdx.x;
+  uint32_t v[8];
+  zs_load_n(x, pg.start[g], pg.cnt[g], v);
+  const uint32_t m = zs_byte(v);
+  bytes[threadIdx.x] = m;
+  int total;
+  (void)zs_block_scan(__builtin_popcount(m), sh, total);
+  if (threadIdx.x < 64) {
+    const int j = threadIdx.x;
+    meta[g * ZS_META + 1 + j] =
+        (int)(bytes[4 * j] | (bytes[4 * j + 1] << 8) | (bytes[4 * j + 2] << 16) | (bytes[4 * j + 3] << 24));
+  }
+  if (threadIdx.x == 0) counts[g] = total;
+}
+
+// one workgroup per segment: page offsets within the segment, the segment's count
+__global__ __launch_bounds__(1024) void zs_seg_scan_kernel(const int* __restrict__ counts, const int* __restrict__ first,
+                                                           const int* __restrict__ npg, int* __restrict__ meta,
+                                                           int64_t* __restrict__ nnz) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x, sg = blockIdx.x;
+  const int64_t f = first[sg], np = npg[sg];
+  const int64_t per = (np + 1023) / 1024, q0 = t * per, q1 = min(np, q0 + per);
+  int64_t s = 0;
+  for (int64_t q = q0; q < q1; ++q) s += counts[f + q];
+  part[t] = s;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const int64_t o = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += o;
+    __syncthreads();
+  }
+  int64_t run = part[t] - s;
+  for (int64_t q = q0; q < q1; ++q) {
+    meta[(f + q) * ZS_META] = (int)run;
+    run += counts[f + q];
+  }
+  if (t == 1023) nnz[sg] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void zs_seg_compact_kernel(const uint32_t* __restrict__ x, ZSPages pg,
+                                                             const int* __restrict__ meta, uint32_t* __restrict__ vals,
+                                                             int64_t cap) {
+  __shared__ int sh[4];
+  const int64_t g = blockIdx.x;
+  uint32_t v[8];
+  zs_load_n(x, pg.start[g], pg.cnt[g], v);
+  const uint32_t m = zs_byte(v);
+  int total;
+  const int ex = zs_block_scan(__builtin_popcount(m), sh, total);
+  int64_t pos = (int64_t)meta[g * ZS_META] + ex;
+  uint32_t* slot = vals + (int64_t)pg.seg[g] * cap;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (v[i] != 0u) {
+      if (pos < cap) slot[pos] = v[i];
+      ++pos;
+    }
+  }
+}
+
+// decode: page g's mask/offset at meta[g], its values in slot pg.seg[g] (capacity cap), its
+// elements to out[pg.start[g] ..]
+__global__ __launch_bounds__(256) void zs_seg_expand_kernel(const int* __restrict__ meta, ZSPages pg,
+                                                            const uint32_t* __restrict__ vals, int64_t cap,
+                                                            uint32_t* __restrict__ out) {
+  __shared__ int sh[4];
+  const int64_t g = blockIdx.x;
+  const uint32_t w = (uint32_t)meta[g * ZS_META + 1 + (threadIdx.x >> 2)];
+  const uint32_t m = (w >> (8 * (threadIdx.x & 3))) & 0xffu;
+  int total;
+  const int ex = zs_block_scan(__builtin_popcount(m), sh, total);
+  int64_t pos = (int64_t)meta[g * ZS_META] + ex;
+  const uint32_t* slot = vals + (int64_t)pg.seg[g] * cap;
+  const int n = pg.cnt[g], t0 = 8 * (int)threadIdx.x;
+  uint32_t* o = out + pg.start[g];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint32_t v = 0u;
+    if ((m >> i) & 1u) {
+      v = pos < cap ? slot[pos] : 0u;
+      ++pos;
+    }
+    if (t0 + i < n) o[t0 + i] = v;
+  }
+}
+
 }  // namespace tds
 
 using namespace tds;
+
+void tds_zs_seg_encode(const float* x, const int64_t* pg_start, const int* pg_cnt, const int* pg_seg, int64_t npages,
+                       const int* seg_first, const int* seg_npg, int nseg, int* meta, int* counts, float* vals,
+                       int64_t cap, int64_t* seg_nnz, hipStream_t st) {
+  const ZSPages pg{pg_start, pg_cnt, pg_seg};
+  const uint32_t* xb = reinterpret_cast<const uint32_t*>(x);
+  hipLaunchKernelGGL(zs_seg_count_kernel, dim3((unsigned)npages), dim3(256), 0, st, xb, pg, meta, counts);
+  TDS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(zs_seg_scan_kernel, dim3((unsigned)nseg), dim3(1024), 0, st, counts, seg_first, seg_npg, meta,
+                     seg_nnz);
+  TDS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(zs_seg_compact_kernel, dim3((unsigned)npages), dim3(256), 0, st, xb, pg, meta,
+                     reinterpret_cast<uint32_t*>(vals), cap);
+  TDS_LAUNCH_CHECK();
+}
+
+void tds_zs_seg_decode(const int* meta, const int64_t* pg_start, const int* pg_cnt, const int* pg_seg, int64_t npages,
+                       const float* vals, int64_t cap, float* out, hipStream_t st) {
+  const ZSPages pg{pg_start, pg_cnt, pg_seg};
+  hipLaunchKernelGGL(zs_seg_expand_kernel, dim3((unsigned)npages), dim3(256), 0, st, meta, pg,
+                     reinterpret_cast<const uint32_t*>(vals), cap, reinterpret_cast<uint32_t*>(out));
+  TDS_LAUNCH_CHECK();
+}
 
 int64_t tds_zs_npages(int64_t n) { return (n + ZS_PAGE - 1) / ZS_PAGE; }
 

@@ -53,6 +53,12 @@ from . import factored
 _ALIGN_ELEMS = 64  # 256-byte alignment of every parameter slot in the flat buffers
 
 
+def _ext_loaded() -> bool:
+    from .. import _ext
+
+    return bool(_ext.load())
+
+
 def _align(n: int) -> int:
     return (n + _ALIGN_ELEMS - 1) // _ALIGN_ELEMS * _ALIGN_ELEMS
 
@@ -197,7 +203,11 @@ class DistributedDataParallel(nn.Module):
         self._deferred_works = {}
         self._side = None
         if self.overlap_optimizer and big_layers:
-            self._side = torch.cuda.Stream(device=dev)
+            # with CUs split off for the collectives (utils/streams.py) the side work keeps to the
+            # reserved CUs, off the persistent compute kernels' CUs (TDS_SIDE_CUS=compute|any)
+            from ..utils.streams import side_stream
+
+            self._side = (side_stream(dev) if _ext_loaded() else None) or torch.cuda.Stream(device=dev)
             self._deferred = [self._layer_bucket[id(lyr)] for lyr in big_layers]
             for b in self._deferred:
                 if self._native is not None:

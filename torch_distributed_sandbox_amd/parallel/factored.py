@@ -93,7 +93,7 @@ def link_bytes(path: str, rows: int, out_f: int, in_f: int, world: int, elem: in
     if path == "activations":
         return float(rows * in_f * elem) * x_ratio
     if path == "sharded":
-        return float((rows + out_f) * in_f * elem) / world
+        return float((rows * x_ratio + out_f) * in_f * elem) / world
     raise ValueError(path)
 
 
@@ -280,6 +280,8 @@ class ActivationExchange:
         elif path == "activations":
             self._x_buf = torch.empty((self.world * rows, in_f), device=x2d.device, dtype=x2d.dtype)
             self._x_work = tdist.all_gather_into_tensor(self._x_buf, x2d, group=self.group, async_op=True)
+        elif self.compress and x2d.dtype == torch.float32:
+            self._begin_zs_sharded(x2d)
         else:
             # all-to-all of column shards: rank s receives every rank's rows of shard s
             bounds = shard_bounds(in_f, self.world)
@@ -331,6 +333,77 @@ class ActivationExchange:
                     "rows": x2d.shape[0], "in_f": x2d.shape[1]}
         self._x_work = None  # set by _zs_resolve
 
+    def _layouts(self, rows: int, in_f: int, dev):
+        """(send, receive) segment layouts of the sharded exchange (parallel/zs.py SegLayout),
+        cached per shape: send = (destination shard s, row b) slices of X, destination-major;
+        receive = (source rank r, row b) rows of this rank's shard in the dense buffer."""
+        from . import distributed as tdist
+        from . import zs
+
+        key = (rows, in_f, str(dev))
+        lays = getattr(self, "_lays", None)
+        if lays is None or lays[0] != key:
+            bounds = shard_bounds(in_f, self.world)
+            me = tdist.get_rank(self.group)
+            k0, k1 = bounds[me]
+            send = zs.SegLayout([(b * in_f + a, e - a) for (a, e) in bounds for b in range(rows)], dev)
+            n_me = k1 - k0
+            recv = zs.SegLayout([((r * rows + b) * n_me, n_me) for r in range(self.world) for b in range(rows)], dev)
+            self._lays = lays = (key, send, recv, bounds)
+        return lays[1], lays[2], lays[3]
+
+    def _begin_zs_sharded(self, x2d: torch.Tensor):
+        """Zero-suppressed column-shard all-to-all: each (destination, row) slice is a segment
+        of its own (fixed-size records + a value slot of this step's capacity per segment);
+        every rank's segment counts are all-gathered, so all ranks take the same capacity and
+        overflow decisions."""
+        from . import distributed as tdist
+        from . import zs
+
+        W, dev = self.world, x2d.device
+        rows, in_f = x2d.shape
+        send, recv, bounds = self._layouts(rows, in_f, dev)
+        me = tdist.get_rank(self.group)
+        n_me = bounds[me][1] - bounds[me][0]
+        longest = max(e - a for a, e in bounds)
+        cap = max(1, min(longest, self._cap) if self._cap else longest)
+        meta_send = torch.empty(send.meta_numel, device=dev, dtype=torch.int32)
+        vals_send = torch.empty(send.nseg * cap, device=dev, dtype=torch.float32)
+        nnz = zs.seg_encode(x2d, send, meta_send, vals_send, cap).to(dev)
+        nnz_all = torch.empty(W * send.nseg, device=dev, dtype=torch.int64)
+        w_cnt = tdist.all_gather_into_tensor(nnz_all, nnz, group=self.group, async_op=True)
+        counts_host = counts_ev = None
+        if dev.type == "cuda":
+            cstream = self._count_stream(dev)
+            with torch.cuda.stream(cstream):
+                w_cnt.wait()
+                counts_host = torch.empty(W * send.nseg, dtype=torch.int64, pin_memory=True)
+                counts_host.copy_(nnz_all, non_blocking=True)
+                counts_ev = torch.cuda.Event()
+                counts_ev.record(cstream)
+                nnz_all.record_stream(cstream)
+        mr = recv.meta_numel // W  # one source's records for this rank's shard
+        meta_recv = torch.empty(W * mr, device=dev, dtype=torch.int32)
+        sends, recvs = [], []
+        for s_ in range(W):
+            m0, m1 = send.meta_range(s_ * rows, (s_ + 1) * rows)
+            if m1 > m0:
+                sends.append((meta_send[m0:m1], s_))
+        if mr > 0:
+            recvs = [(meta_recv[r * mr:(r + 1) * mr], r) for r in range(W)]
+        w_meta = tdist.sendrecv(sends, recvs, group=self.group, async_op=True)
+        vals_recv = torch.empty(W * rows * cap, device=dev, dtype=torch.float32)
+        span = rows * cap
+        sends_v = [(vals_send[s_ * span:(s_ + 1) * span], s_) for s_ in range(W) if bounds[s_][1] > bounds[s_][0]]
+        recvs_v = [(vals_recv[r * span:(r + 1) * span], r) for r in range(W)] if n_me > 0 else []
+        w_vals = tdist.sendrecv(sends_v, recvs_v, group=self.group, async_op=True)
+        self._x_buf = torch.empty((W, rows, n_me), device=dev, dtype=x2d.dtype)
+        self._zs = {"kind": "sharded", "n": longest, "cap": cap, "w_cnt": w_cnt, "nnz_all": nnz_all,
+                    "counts_host": counts_host, "counts_ev": counts_ev, "w_meta": w_meta, "w_vals": w_vals,
+                    "meta_recv": meta_recv, "vals_recv": vals_recv, "recv": recv, "keep": (meta_send, vals_send),
+                    "meta_bytes": send.meta_numel, "dense": x2d.numel()}
+        self._x_work = None
+
     def _count_stream(self, dev):
         st = getattr(self, "_cstream", None)
         if st is None:
@@ -345,6 +418,9 @@ class ActivationExchange:
         from . import distributed as tdist
 
         z, self._zs = self._zs, None
+        if z.get("kind") == "sharded":
+            self._zs_resolve_sharded(z)
+            return
         W, n, cap = self.world, z["n"], z["cap"]
         if z["counts_ev"] is not None:
             z["counts_ev"].synchronize()
@@ -367,6 +443,36 @@ class ActivationExchange:
             return
         self._zs_decode_pending = z
 
+    def _zs_resolve_sharded(self, z):
+        from . import distributed as tdist
+
+        if z["counts_ev"] is not None:
+            z["counts_ev"].synchronize()
+            counts = z["counts_host"]
+        else:
+            z["w_cnt"].wait()
+            counts = z["nnz_all"]
+        counts = [int(v) for v in counts.tolist()]
+        mx, cap = max(counts) if counts else 0, z["cap"]
+        self.zs_stats["steps"] += 1
+        self.zs_stats["last_nnz"] = max(counts) if counts else 0
+        self._cap = max(1, min(z["n"], -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND))
+        self.x_ratio = (sum(counts) / self.world + z["meta_bytes"]) / z["dense"]  # per rank, vs dense rows
+        if mx > cap:  # some segment overflowed its slot: the dense all-to-all, once
+            self.zs_stats["overflows"] += 1
+            z["w_meta"].wait()
+            z["w_vals"].wait()
+            x2d = self._x_local
+            rows, in_f = x2d.shape
+            bounds = shard_bounds(in_f, self.world)
+            me = tdist.get_rank(self.group)
+            k0, k1 = bounds[me]
+            sends = [(x2d[b, a:e], s_) for s_, (a, e) in enumerate(bounds) if e > a for b in range(rows)]
+            recvs = [(self._x_buf[s_, b], s_) for s_ in range(self.world) if k1 > k0 for b in range(rows)]
+            self._x_work = tdist.sendrecv(sends, recvs, group=self.group, async_op=True)
+            return
+        self._zs_decode_pending = z
+
     def _zs_decode(self):
         """Rebuild every rank's rows into self._x_buf (current stream = where the gradient is
         formed), after the values gather."""
@@ -378,6 +484,9 @@ class ActivationExchange:
         self._zs_decode_pending = None
         z["w_meta"].wait()
         z["w_vals"].wait()
+        if z.get("kind") == "sharded":
+            zs.seg_decode(z["meta_recv"], z["recv"], z["vals_recv"], z["cap"], self._x_buf)
+            return
         W, n, M, cap = self.world, z["n"], z["M"], z["cap"]
         meta_all = z["meta_all"].view(W, M + 2)
         vals_all = z["vals_all"].view(W, cap)
@@ -407,14 +516,20 @@ class ActivationExchange:
         join = side is None
         if side is None:
             if self._own_stream is None:
-                self._own_stream = torch.cuda.Stream(device=dev)
+                from ..utils.streams import side_stream
+
+                # the reserved CUs when a CU split is active (utils/streams.py), else a plain stream
+                self._own_stream = side_stream(dev) or torch.cuda.Stream(device=dev)
             side = self._own_stream
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
         keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
         z = getattr(self, "_zs_decode_pending", None)
         if z is not None:
-            keep = keep + (z["meta_all"], z["vals_all"], z["meta"], z["vals"])
+            if z.get("kind") == "sharded":
+                keep = keep + (z["meta_recv"], z["vals_recv"]) + z["keep"]
+            else:
+                keep = keep + (z["meta_all"], z["vals_all"], z["meta"], z["vals"])
         with torch.cuda.stream(side):
             for t in keep:
                 t.record_stream(side)
@@ -487,8 +602,8 @@ class ActivationExchange:
 
     def _done(self):
         self.last_path = "activation-exchange" if self.active == "activations" else "sharded-exchange"
-        if self.active == "activations" and self.compress and self.zs_stats["steps"]:
-            self.last_path = "activation-exchange(zs)"
+        if self.compress and self.zs_stats["steps"]:
+            self.last_path += "(zs)"
         self._x_buf = self._x_work = self._dy = self._x_local = None
         self.active = None
         self.steps_exchanged += 1

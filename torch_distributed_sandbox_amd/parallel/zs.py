@@ -129,3 +129,89 @@ def decode(meta: torch.Tensor, values: torch.Tensor, out: torch.Tensor) -> torch
         _ext.ops().zs_decode(meta, values, out)
         return out
     return decode_ref(meta, values, out)
+
+
+# ---------------------------------------------------------------------------- segmented form
+class SegLayout:
+    """Segments = flat element ranges ``(start, length)`` of one tensor, in order; each is cut
+    into pages of ``PAGE`` (its last page partial), page g's record at ``meta[g * META]`` with
+    offsets restarting per segment and its values in slot ``seg`` (a fixed capacity each).  The
+    sharded exchange lays out (destination shard, row) segments of X this way, so one
+    destination's share is one contiguous meta range and one run of slots
+    (csrc/kernels/zs_exchange.hip, zs_seg_*)."""
+
+    def __init__(self, segments, device):
+        self.segments = [(int(a), int(n)) for a, n in segments]
+        starts, cnts, segs, first, npg = [], [], [], [], []
+        for s, (a, n) in enumerate(self.segments):
+            first.append(len(starts))
+            k = npages(n) if n > 0 else 0
+            npg.append(k)
+            for p in range(k):
+                starts.append(a + p * PAGE)
+                cnts.append(min(PAGE, n - p * PAGE))
+                segs.append(s)
+        self.first, self.npg = first, npg
+        self.npages = len(starts)
+        dev = torch.device(device)
+        self.pg_start = torch.tensor(starts, dtype=torch.int64, device=dev)
+        self.pg_cnt = torch.tensor(cnts, dtype=torch.int32, device=dev)
+        self.pg_seg = torch.tensor(segs, dtype=torch.int32, device=dev)
+        self.seg_first = torch.tensor(first, dtype=torch.int32, device=dev)
+        self.seg_npg = torch.tensor(npg, dtype=torch.int32, device=dev)
+
+    @property
+    def nseg(self) -> int:
+        return len(self.segments)
+
+    @property
+    def meta_numel(self) -> int:
+        return self.npages * META
+
+    def meta_range(self, s0: int, s1: int) -> Tuple[int, int]:
+        """[begin, end) of segments s0 .. s1-1 in the meta buffer (consecutive segments)."""
+        g0 = self.first[s0] if s0 < self.nseg else self.npages
+        g1 = self.first[s1] if s1 < self.nseg else self.npages
+        return g0 * META, g1 * META
+
+
+def seg_encode(x: torch.Tensor, lay: SegLayout, meta_out: torch.Tensor, vals_out: torch.Tensor,
+               cap: int) -> torch.Tensor:
+    """Encode the segments of x (flat) into meta_out [lay.meta_numel] and vals_out [nseg * cap];
+    returns the per-segment counts, int64 [nseg] on x's device (no host sync)."""
+    if x.is_cuda:
+        from .. import _ext
+
+        return _ext.ops().zs_seg_encode(x.contiguous(), lay.pg_start, lay.pg_cnt, lay.pg_seg, lay.seg_first,
+                                        lay.seg_npg, meta_out, vals_out, int(cap))
+    flat = x.reshape(-1)
+    slots = vals_out.view(lay.nseg, cap) if lay.nseg else vals_out
+    counts = torch.zeros(lay.nseg, dtype=torch.int64)
+    for s, (a, n) in enumerate(lay.segments):
+        if n == 0:
+            continue
+        m0, m1 = lay.meta_range(s, s + 1)
+        meta, vals, nnz = encode_ref(flat[a:a + n])
+        meta_out[m0:m1].copy_(meta)
+        k = min(nnz, cap)
+        slots[s, :k].copy_(vals[:k])
+        counts[s] = nnz
+    return counts
+
+
+def seg_decode(meta: torch.Tensor, lay: SegLayout, vals: torch.Tensor, cap: int, out: torch.Tensor) -> torch.Tensor:
+    """Rebuild the segments of ``out`` (flat ranges of ``lay``) from ``meta`` [lay.meta_numel] and
+    the value slots ``vals`` [nseg * cap]; the counts must not exceed ``cap``."""
+    if out.is_cuda:
+        from .. import _ext
+
+        _ext.ops().zs_seg_decode(meta, lay.pg_start, lay.pg_cnt, lay.pg_seg, vals, int(cap), out)
+        return out
+    flat = out.reshape(-1)
+    slots = vals.view(lay.nseg, cap) if lay.nseg else vals
+    for s, (a, n) in enumerate(lay.segments):
+        if n == 0:
+            continue
+        m0, m1 = lay.meta_range(s, s + 1)
+        decode_ref(meta[m0:m1], slots[s], flat[a:a + n])
+    return out

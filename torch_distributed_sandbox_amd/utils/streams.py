@@ -63,3 +63,18 @@ def comm_stream(device: Optional[torch.device] = None) -> Optional[torch.cuda.St
 def compute_cus() -> int:
     """CUs the persistent kernels launch on (all minus the reserve)."""
     return int(_ext.ops().device_cus())
+
+
+def side_stream(device: Optional[torch.device] = None, side: Optional[str] = None) -> Optional[torch.cuda.Stream]:
+    """A stream for DDP's side work (the fc exchange's dW formation, the deferred SGD step) that
+    keeps to one side of the CU split: ``side`` = "comm" (the reserved CUs, default) | "compute"
+    | "any" (a plain stream: None here).  ``TDS_SIDE_CUS`` overrides the default.  None when no
+    CUs are reserved (then a plain stream is as good as any)."""
+    side = (side or os.environ.get("TDS_SIDE_CUS", "comm")).strip().lower()
+    if side not in ("comm", "compute", "any"):
+        raise ValueError(f"side stream placement must be comm|compute|any, got {side!r}")
+    if side == "any":
+        return None
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    h = int(_ext.ops().cu_side_stream(dev.index, side == "comm"))
+    return torch.cuda.ExternalStream(h, device=dev) if h else None
