@@ -148,7 +148,7 @@ def test_bench_w8_cpu(backend):
     assert p.returncode == 0, p.stderr[-3000:]
     (r,) = _json_lines(p.stdout)
     assert r["n_gpus"] == 8 and r["config"]["global_batch"] == 40 and r["config"]["parallelism"] == "dp8"
-    assert r["config"]["fc_grad"] == "sharded-exchange"
+    assert r["config"]["fc_grad"] == "sharded-exchange(zs)"  # zero-suppressed X shards (parallel/zs.py)
     assert r["config"]["reducer"] == ("native" if backend == "host" else "python")
 
 
