@@ -214,3 +214,34 @@ def test_trainer_and_bench_pick_the_same_stack(monkeypatch):
     assert not tdist.is_device_backend("gloo")
     targs.backend = "rccl"
     assert resolve_backend(targs) == "rccl"  # torch's ProcessGroupNCCL stays selectable
+
+
+def _torchrun(n, args, env=None, timeout=300):
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return _run(["-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr", "127.0.0.1",
+                 "--master-port", str(port)] + args, env=env, timeout=timeout)
+
+
+def test_bench_under_torchrun_cpu():
+    """The driver's multi-GPU form: torchrun starts the ranks, bench.py runs as each of them
+    (WORLD_SIZE set), rank 0 prints the one JSON line."""
+    p = _torchrun(2, ["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "32", "--steps", "2",
+                      "--warmup", "1", "--no-allreduce-probe"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    (r,) = _json_lines(p.stdout)
+    assert r["n_gpus"] == 2 and r["steps"] == 2 and r["value"] > 0 and r["config"]["parallelism"] == "dp2"
+
+
+def test_bench_under_torchrun_falls_back_cpu():
+    """Under torchrun there is no spawning parent: the ranks themselves vote through the store
+    and re-run on the plain stack in the same processes."""
+    p = _torchrun(2, ["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "32", "--steps", "1",
+                      "--warmup", "1", "--backend", "host", "--fallback", "--pg-timeout", "15",
+                      "--no-allreduce-probe"], env={"TDS_BENCH_FAULT": "1:step:raise:1"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    (r,) = _json_lines(p.stdout)
+    assert r["value"] > 0 and r["config"]["backend"].startswith("gloo (fallback: rank 1")
