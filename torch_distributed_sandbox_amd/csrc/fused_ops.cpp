@@ -227,8 +227,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const T
   int tr = 0, tc = 0;
   tds_conv2_fwd2_tiles((int)P, &tr, &tc);
   const int* order = tile_order(p1, (int)B, tr, tc, nwg);
-  auto y2 = at::empty({B, P, P, 32}, p1.options());
-  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options());
+  auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kFloat));
+  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
   tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr<float>(),
                  ya.data_ptr<float>(), partial.data_ptr<double>(), opt_mag(mag), order, nwg, (int)B, (int)P,
@@ -419,8 +419,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   int tr = 0, tc = 0;
   tds_conv2_bwd3_tiles((int)P, &tr, &tc);
   const int* order = bwd_walk(p1, (int)B, tr, tc, nwg);
-  auto dp1 = at::empty({B, P, P, 16}, p1.options());
-  auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options());
+  auto dp1 = at::empty({B, P, P, 16}, p1.options().dtype(at::kFloat));
+  auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options().dtype(at::kFloat));
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
   tds_conv2_bwd3(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
