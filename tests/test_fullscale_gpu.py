@@ -15,6 +15,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from _tf32ref import rel as _rel
+from _tf32ref import unfold_conv as _unfold_conv
 from test_model_gpu import RefConvNet
 
 pytestmark = pytest.mark.gpu
@@ -54,56 +56,6 @@ def _step(model, x, y, tag):
     return logits.detach(), loss.detach(), {n: p.grad.detach() for n, p in model.named_parameters()}
 
 
-def _unfold_conv(conv, tf32=False):
-    """fp64 5x5 'same' convolution as unfold + GEMM (MIOpen has no fp64 convolutions).  tf32:
-    the convolution cuDNN runs for the reference by default on Ampere (allow_tf32): every
-    operand of the forward, data gradient and weight gradient rounded to TF32 (10 explicit
-    mantissa bits), products and sums exact -- the precision class the reference number is
-    quoted at (gfx950 has no TF32, so it is emulated here)."""
-
-    if not tf32:
-        def fwd(x):
-            Bx, _, Hx, Wx = x.shape
-            cols = F.unfold(x, 5, padding=2)  # [B, C*25, H*W]
-            y = conv.weight.reshape(conv.out_channels, -1) @ cols + conv.bias.view(1, -1, 1)
-            return y.view(Bx, conv.out_channels, Hx, Wx)
-
-        return fwd
-
-    class _TF32Conv(torch.autograd.Function):
-        @staticmethod
-        def forward(ctx, x, w, b):
-            xr, wr = _tf32(x), _tf32(w)
-            ctx.save_for_backward(xr, wr)
-            Bx, _, Hx, Wx = x.shape
-            y = wr.reshape(wr.shape[0], -1) @ F.unfold(xr, 5, padding=2) + b.view(1, -1, 1)
-            return y.view(Bx, wr.shape[0], Hx, Wx)
-
-        @staticmethod
-        def backward(ctx, dy):
-            xr, wr = ctx.saved_tensors
-            dyr = _tf32(dy)
-            Bx, C, Hx, Wx = xr.shape
-            dcols = wr.reshape(wr.shape[0], -1).t() @ dyr.reshape(Bx, wr.shape[0], -1)
-            dx = F.fold(dcols, (Hx, Wx), 5, padding=2)
-            dw = torch.einsum("bok,bck->oc", dyr.reshape(Bx, wr.shape[0], -1), F.unfold(xr, 5, padding=2))
-            return dx, dw.view_as(wr), dy.sum((0, 2, 3))
-
-    return lambda x: _TF32Conv.apply(x, conv.weight, conv.bias)
-
-
-def _tf32(t):
-    """Round to TF32 (round to nearest even on 10 explicit mantissa bits), kept in fp64."""
-    b = t.float().view(torch.int32)
-    b = (b + 0xFFF + ((b >> 13) & 1)) & ~0x1FFF
-    return b.view(torch.float32).double()
-
-
-def _rel(a, b):
-    a, b = a.double(), b.double()
-    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
-
-
 def test_one_step_vs_eager_reference(gpu):
     from torch_distributed_sandbox_amd.data import synthetic_batch
     from torch_distributed_sandbox_amd.models import ConvNet, fc_in_features
@@ -126,7 +78,7 @@ def test_one_step_vs_eager_reference(gpu):
     reftf = RefConvNet(fc_in_features((H, H))).to(gpu).double()
     reftf.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in state.items()})
     for layer in (reftf.layer1, reftf.layer2):
-        layer[0].forward = _unfold_conv(layer[0], tf32=True)
+        layer[0].forward = _unfold_conv(layer[0], tf32_operands=True)
     ltf, lstf, gtf = _step(reftf, x.double(), y, "TF32-emulated convs (fp64 otherwise)")
     del reftf
 

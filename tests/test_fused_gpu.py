@@ -4,6 +4,8 @@ import pytest
 import torch
 import torch.nn.functional as F
 
+from _tf32ref import rel, unfold_conv
+
 pytestmark = pytest.mark.gpu
 
 
@@ -304,6 +306,13 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
         ours.layer2[1].weight[::3].neg_()  # some negative BN2 gammas: min-pooled windows
     ref = Ref(fc_in_features((H, H))).double()
     ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in ours.state_dict().items()})
+    # the reference's precision class: its convolutions with TF32 operands (tests/_tf32ref.py)
+    # (its own trajectory, like ours: both are compared with the fp64 one step by step)
+    reft = Ref(fc_in_features((H, H))).double()
+    reft.load_state_dict(ref.state_dict())
+    for layer in (reft.layer1, reft.layer2):
+        layer[0].forward = unfold_conv(layer[0], tf32_operands=True)
+    topt = torch.optim.SGD(reft.parameters(), lr)
     ours = ours.to(gpu)
     opt = SGD(ours.parameters(), lr)
     ropt = torch.optim.SGD(ref.parameters(), lr)
@@ -314,27 +323,37 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
         loss = crit(ours(x), y)
         opt.zero_grad()
         loss.backward()
+        topt.zero_grad()
+        F.cross_entropy(reft(x.double().cpu()), y.cpu()).backward()
         rl = F.cross_entropy(ref(x.double().cpu()), y.cpu())
         ropt.zero_grad()
         rl.backward()
         assert abs(loss.item() - rl.item()) <= 2e-4 * max(1.0, abs(rl.item())), (loss.item(), rl.item())
         rp = dict(ref.named_parameters())
+        rt = dict(reft.named_parameters())
         for n, p in ours.named_parameters():
             g, rg = p.grad.double().cpu(), rp[n].grad
             if n.endswith("0.bias"):  # analytically zero (bias before BN): rounding noise both sides
                 wsc = rp[n.replace("bias", "weight")].grad.abs().max().item()
                 assert (g - rg).abs().max().item() <= 1e-3 * wsc + 1e-6, f"step {s} {n}"
                 continue
-            # relative L2 (robust to rare argmax flips on near-tied pool windows)
-            rel = ((g - rg).norm() / rg.norm().clamp_min(1e-30)).item()
-            assert rel <= 1e-3, f"step {s} {n}: rel L2 err {rel:.3e}"
+            # relative L2 (robust to rare argmax flips on near-tied pool windows), bounded by 1e-3
+            # or by what the TF32 convolutions themselves make: conv1's weight gradient comes out
+            # of BN over every position, and that cancellation amplifies the per-product rounding
+            # of the conv2 data gradient (<= 2^-11 here, up to 2^-10 with TF32)
+            e, et = rel(g, rg), rel(rt[n].grad, rg)
+            print(f"step {s} {n:18s} ours {e:.3e}  tf32 {et:.3e}")
+            assert e <= max(1e-3, 1.5 * et), f"step {s} {n}: rel L2 err {e:.3e} (TF32 convs: {et:.3e})"
         opt.step()
         ropt.step()
-    rb = dict(ref.named_buffers())
+        topt.step()
+    rb, tb = dict(ref.named_buffers()), dict(reft.named_buffers())
     for n, b in ours.named_buffers():
         if b.is_floating_point():
             e, sc = _err(b, rb[n])
-            assert e <= 1e-4 * max(sc, 1.0), n
+            et, _ = _err(tb[n], rb[n])
+            print(f"buffer {n:24s} ours {e:.3e}  tf32 {et:.3e}  (scale {sc:.3e})")
+            assert e <= max(1e-4 * max(sc, 1.0), 1.5 * et), n
         else:
             assert int(b.item()) == int(rb[n].item()), n
 

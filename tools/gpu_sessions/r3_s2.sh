@@ -4,7 +4,7 @@
 set -u
 O=gpurun_out/r3s2
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_fused_gpu.py tests/test_kernels_gpu.py -x -v --timeout 120 --timeout-method thread > $O/t_fused.log 2>&1 \
+timeout -k 10 300 python -u -m pytest tests/test_fused_gpu.py tests/test_kernels_gpu.py -x -v -s --timeout 120 --timeout-method thread > $O/t_fused.log 2>&1 \
   || { echo "fused tests rc=$?"; tail -40 $O/t_fused.log; exit 1; }
 tail -1 $O/t_fused.log
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/tests.log 2>&1 \
