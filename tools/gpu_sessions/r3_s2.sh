@@ -4,12 +4,11 @@
 set -u
 O=gpurun_out/r3s2
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_fused_gpu.py tests/test_kernels_gpu.py -x -v -s --timeout 120 --timeout-method thread > $O/t_fused.log 2>&1 \
-  || { echo "fused tests rc=$?"; tail -40 $O/t_fused.log; exit 1; }
-tail -1 $O/t_fused.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $O/tests.log 2>&1 \
-  || { echo "tests rc=$?"; tail -40 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
+# test failures (rc 1) do not stop the session; a crash, abort or time limit does
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 400 --timeout-method thread > $O/tests.log 2>&1
+rc=$?
+grep -E "FAILED|passed|failed" $O/tests.log | tail -12
+[ $rc -le 1 ] || { echo "tests rc=$rc"; tail -40 $O/tests.log; exit 1; }
 timeout -k 10 120 python -u -c 'import __graft_entry__ as g; g.smoke()' > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
 b() {
