@@ -54,3 +54,11 @@ def unfold_conv(conv, tf32_operands=False):
 def rel(a, b):
     a, b = a.double(), b.double()
     return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+def tf32_convs(model):
+    """Patch a reference ConvNet (layer1 / layer2 Sequentials, conv first) in place so its
+    convolutions run with TF32 operands; returns the model."""
+    for layer in (model.layer1, model.layer2):
+        layer[0].forward = unfold_conv(layer[0], tf32_operands=True)
+    return model

@@ -5,6 +5,9 @@ import pytest
 import torch
 import torch.nn as nn
 
+from _tf32ref import rel as _rel
+from _tf32ref import tf32_convs
+
 pytestmark = pytest.mark.gpu
 
 
@@ -41,6 +44,9 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
     ours = ConvNet(image_shape=(H, H), mode=mode)
     ref = RefConvNet(fc_in_features((H, H))).double()
     ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in ours.state_dict().items()})
+    # the reference's precision class (TF32 convolutions), re-synced with ref every step: the
+    # fused plan's fp16x2 conv2 is bounded by max(fixed tolerance, 1.5 x what TF32 makes)
+    reft = tf32_convs(copy.deepcopy(ref))
     ours = ours.to(gpu)
     opt = SGD(ours.parameters(), 0.05)
     ropt = torch.optim.SGD(ref.parameters(), 0.05)
@@ -55,8 +61,11 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
         # windows), which made a multi-step comparison measure chaos, not kernel error.  The
         # update itself is pinned below against p - lr * p.grad.
         with torch.no_grad():
-            for (n, p), q in zip(ours.named_parameters(), ref.parameters()):
+            for (n, p), q, qt in zip(ours.named_parameters(), ref.parameters(), reft.parameters()):
                 q.copy_(p.detach().double().cpu())
+                qt.copy_(q)
+            for b, bt in zip(ref.buffers(), reft.buffers()):
+                bt.copy_(b)
         x = torch.rand(B, 1, H, H, device=gpu)
         y = torch.randint(0, 10, (B,), device=gpu)
         loss = crit(ours(x), y)
@@ -67,8 +76,13 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
         ties = sum(near_tie_windows(a) for a in pool_in)
         ropt.zero_grad()
         rloss.backward()
-        assert abs(loss.item() - rloss.item()) < 1e-4 * max(1, abs(rloss.item())), (loss.item(), rloss.item())
-        rp = dict(ref.named_parameters())
+        reft.zero_grad()
+        tloss = nn.functional.cross_entropy(reft(x.double().cpu()), y.cpu())
+        tloss.backward()
+        tl_err = abs(tloss.item() - rloss.item())
+        assert abs(loss.item() - rloss.item()) < max(1e-4 * max(1, abs(rloss.item())), 1.5 * tl_err), \
+            (loss.item(), rloss.item(), tloss.item())
+        rp, rt = dict(ref.named_parameters()), dict(reft.named_parameters())
         for n, p in ours.named_parameters():
             g, rg = p.grad.double().cpu(), rp[n].grad
             if n.endswith("0.bias"):
@@ -86,18 +100,20 @@ def _compare(mode, gpu, H=64, B=3, steps=2):
             # weights, BN1); BN2 and fc see the same tied value either way and stay at 2e-3.
             rel = ((g - rg).norm() / rg.norm().clamp_min(1e-30)).item()
             flip_reach = n.startswith("layer1.") or n.startswith("layer2.0.")
-            tol = 2e-2 if ties and flip_reach else 2e-3
-            assert rel <= tol, f"step {s} {n}: rel L2 err {rel:.3e} (near-tied windows: {ties})"
+            tol = max(2e-2 if ties and flip_reach else 2e-3, 1.5 * _rel(rt[n].grad, rg))
+            assert rel <= tol, f"step {s} {n}: rel L2 err {rel:.3e} > {tol:.3e} (near-tied windows: {ties})"
         before = {n: (p.detach().clone(), p.grad.detach().clone()) for n, p in ours.named_parameters()}
         opt.step()
         ropt.step()
         for n, p in ours.named_parameters():
             w0, g0 = before[n]
             assert torch.allclose(p.detach(), w0 - 0.05 * g0, rtol=1e-6, atol=1e-7), f"step {s} {n}: SGD update"
-    rb = dict(ref.named_buffers())
+    rb, tb = dict(ref.named_buffers()), dict(reft.named_buffers())
     for n, b in ours.named_buffers():
         if b.is_floating_point():
-            assert (b.double().cpu() - rb[n]).abs().max().item() < 1e-4, n
+            # reft's buffers: re-synced from ref, then updated by the last step's TF32 batch stats
+            et = (tb[n] - rb[n]).abs().max().item()
+            assert (b.double().cpu() - rb[n]).abs().max().item() < max(1e-4, 1.5 * et), n
         else:
             assert int(b.item()) == int(rb[n].item()), n
 

@@ -82,6 +82,10 @@ def main():
             st["hb"] = ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, n2.weight, fc.weight, P, dw, 1.0, True,
                                                mag=st["mag"])
 
+        def hb_nomag():  # A/B: the same launch without the |g2m| bound (atomic max)
+            _, stats2, aff2 = st["hf"]
+            ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, n2.weight, fc.weight, P, dw, 1.0, True)
+
         def c2b():
             y2 = st["c2"][0]
             g2m, kbuf = st["hb"][4], st["hb"][5]
@@ -92,7 +96,7 @@ def main():
             ops.fused_l1_backward(st["c2b"][0], x, p1, idx1, c1.weight, c1.bias, n1.weight, stats1, gram, 1.0)
 
         seq = [("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
-               ("conv2_bwd", c2b), ("l1_bwd", l1b)]
+               ("head_bwd_nomag", hb_nomag), ("conv2_bwd", c2b), ("l1_bwd", l1b)]
         for _, fn in seq:
             fn()
         only = set(a.only.split(",")) if a.only else None
