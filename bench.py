@@ -508,6 +508,10 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
         return loss
 
     def sync_all():
+        # a deferred parameter update (ops/param_fence.py: the exchange's fc step, queued by the
+        # next forward) is queued here, so the timed region holds exactly K updates
+        if hasattr(ddp, "wait_pending_updates"):
+            ddp.wait_pending_updates()
         if world > 1:
             tdist.barrier()
         if on_gpu:

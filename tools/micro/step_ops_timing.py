@@ -62,7 +62,7 @@ def main():
                                             n1.running_var, n1.num_batches_tracked, 0.1, 1e-5)
 
         def pack():
-            st["mag"] = torch.zeros(33, dtype=torch.int32, device=x.device)
+            st["mag"] = torch.zeros(ops.mag_numel(B, P), dtype=torch.int32, device=x.device)
             st["pack"] = ops.conv2_pack(c2.weight, st["mag"])
 
         def c2f():

@@ -6,8 +6,11 @@
 //   y2          [B,P,P,32] f32
 //   ya          [B,32,PB] f32: pooled-blocked planes (kernels/pooled_layout.h)
 //   g2m         [B,32,Q,Q] f32: planar pooled gradient
-//   mag         [33] int32: the step's magnitude bounds (max |y2| per channel, max |g2m|, float
-//               bits) behind the conv2 backward's fp16 gradient scale; reset by conv2_pack
+//   mag         int32 workspace [mag_numel(B, P)]: the step's magnitude bounds (float bits) behind
+//               the conv2 backward's fp16 gradient scale -- [0,32) max |y2| per channel, [32]
+//               max |g2m|, then per-workgroup maxima from the conv2 forward (ypart [32][nwg])
+//               and the head backward (gpart [32][npass][nblk]), written with plain stores and
+//               reduced into [0,33) by the BN2-backward finalize
 #include <ATen/ATen.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -192,9 +195,18 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
 }
 
 // ---------------------------------------------------------------- conv2 forward
-uint32_t* opt_mag(const c10::optional<Tensor>& mag) {
+constexpr int64_t kMagParts = 64;  // ypart offset in the mag workspace
+int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
+int64_t mag_gpart_count(int64_t B, int64_t P) {
+  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_pb_nblk((int)(P / 2));
+}
+int64_t mag_numel(int64_t B, int64_t P) { return kMagParts + 32 * mag_ypart_count() + mag_gpart_count(B, P); }
+
+uint32_t* opt_mag(const c10::optional<Tensor>& mag, int64_t numel = 33) {
   if (!mag.has_value() || !mag->defined()) return nullptr;
-  need(*mag, at::kInt, {33}, "mag (magnitude bounds)");
+  TORCH_CHECK(mag->is_cuda() && mag->scalar_type() == at::kInt && mag->is_contiguous() && mag->numel() >= numel,
+              "mag (magnitude-bound workspace) must be a contiguous int32 GPU tensor of >= ", numel,
+              " elements (ops.mag_numel)");
   return reinterpret_cast<uint32_t*>(mag->data_ptr<int>());
 }
 
@@ -231,8 +243,9 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const T
   auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
   tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr<float>(),
-                 ya.data_ptr<float>(), partial.data_ptr<double>(), opt_mag(mag), order, nwg, (int)B, (int)P,
-                 stream_of(p1));
+                 ya.data_ptr<float>(), partial.data_ptr<double>(),
+                 opt_mag(mag, kMagParts + 32 * mag_ypart_count()) ? opt_mag(mag) + kMagParts : nullptr, order, nwg,
+                 (int)B, (int)P, stream_of(p1));
   check_launches("fused_conv2_forward");
   return {y2, partial, ya};
 }
@@ -379,7 +392,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
                                  compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                  upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
                                  (float)scale, (float)update_lr, (int)c_begin, (int)c_end,
-                                 opt_mag(mag) ? opt_mag(mag) + 32 : nullptr, st);
+                                 opt_mag(mag, mag_numel(B, P)) ? opt_mag(mag) + kMagParts + 32 * mag_ypart_count()
+                                                               : nullptr,
+                                 st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
   if (!finalize) {
     check_launches("fused_head_backward");
@@ -390,9 +405,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");
   auto kbuf = at::empty({96}, ya.options());
   auto dbfc = sink_or_empty(dbfc_out, {NC}, ya, "dbfc_out");
+  uint32_t* m = opt_mag(mag, mag_numel(B, P));
   tds_bn_bwd_finalize2(partial.data_ptr<double>(), 32, npass * nblk, B * P * P, g, stats2.data_ptr<float>(),
                        dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), dlogits.data_ptr<float>(),
-                       (int)B, (int)NC, dbfc.data_ptr<float>(), (float)scale, st);
+                       (int)B, (int)NC, dbfc.data_ptr<float>(), (float)scale, m ? m + kMagParts : nullptr,
+                       (int)mag_ypart_count(), m ? m + kMagParts + 32 * mag_ypart_count() : nullptr,
+                       (int)mag_gpart_count(B, P), m, st);
   check_launches("fused_head_backward");
   return {dW, dbfc, dgamma, dbeta, g2m, kbuf};
 }
@@ -406,7 +424,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
                                                            const c10::optional<Tensor>& db_out) {
   const int64_t B = p1.size(0), P = p1.size(1);
   need(p1, at::kHalf, {B, P, P, 16}, "p1");
-  need(mag, at::kInt, {33}, "mag (magnitude bounds of the forward and the head backward)");
+  opt_mag(mag);  // [0,33): the magnitude bounds of the forward and the head backward
   need(y2, at::kFloat, {B, P, P, 32}, "y2");
   need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
   need(aff2, at::kFloat, {64}, "aff2");
@@ -534,11 +552,11 @@ Tensor zs_encode(const Tensor& x, const Tensor& meta_out, const Tensor& values_o
                   values_out.dim() == 1,
               "zs_encode: values_out fp32 1-d contiguous GPU");
   TORCH_CHECK(x.device() == meta_out.device() && x.device() == values_out.device(), "zs_encode: one device");
+  TORCH_CHECK(n < ((int64_t)1 << 31), "zs_encode: the format's int32 offsets need < 2^31 elements");
   c10::DeviceGuard guard(x.device());
-  auto counts = at::empty({P}, x.options().dtype(at::kInt));
   auto nnz = at::empty({}, x.options().dtype(at::kLong));
-  tds_zs_encode(x.data_ptr<float>(), n, meta_out.data_ptr<int>(), counts.data_ptr<int>(), values_out.data_ptr<float>(),
-                values_out.numel(), nnz.data_ptr<int64_t>(), stream_of(x));
+  tds_zs_encode(x.data_ptr<float>(), n, meta_out.data_ptr<int>(), values_out.data_ptr<float>(), values_out.numel(),
+                nnz.data_ptr<int64_t>(), stream_of(x));
   check_launches("zs_encode");
   return nnz;
 }
@@ -641,6 +659,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor(h!)? mag=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
+  m.def("mag_numel(int B, int P) -> int", &mag_numel);
+  m.def("mag_ypart_count() -> int", &mag_ypart_count);
   m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);
   m.def("conv2_bwd_walk_table(int B, int tiles_r, int tiles_c, int nwg, int seg) -> Tensor", &conv2_bwd_walk_table);
   m.def(

@@ -88,6 +88,19 @@ __device__ __forceinline__ T block_sum(T v, T* scratch) {
   return r;
 }
 
+// Block-wide max (same contract as block_sum).
+template <typename T>
+__device__ __forceinline__ T block_max(T v, T* scratch) {
+  v = wave_max(v);
+  const int nw = blockDim.x / TDS_WAVE;
+  __syncthreads();
+  if (lane_id() == 0) scratch[wave_id()] = v;
+  __syncthreads();
+  T r = scratch[0];
+  for (int i = 1; i < nw; ++i) r = r > scratch[i] ? r : scratch[i];
+  return r;
+}
+
 // Round-to-nearest-even f32 -> bf16 bits (finite inputs; NaN stays NaN via cast path).
 __device__ __forceinline__ unsigned short f32_to_bf16_bits(float f) {
   unsigned int u = __float_as_uint(f);

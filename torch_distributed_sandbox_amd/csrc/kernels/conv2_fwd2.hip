@@ -17,8 +17,10 @@
 //     statistics are.  Every lane holds whole windows of its channel, the 4 x 8 pooled block
 //     of the tile is staged in LDS and stored as ya (pooled_layout.h): one 128-B line per
 //     channel.  The head then streams ya (72 MB per image at 3000^2) instead of y2 (288 MB).
-//   * max |y2| per channel goes to an atomic max (mag): with the head backward's max |g2m| it
-//     bounds the conv2 output gradient, whose fp16 scale the backward picks from it.
+//   * max |y2| per channel and workgroup goes to ypart (a region of the step's magnitude-bound
+//     workspace, fused_ops.cpp "mag"); reduced with the head backward's max |g2m| by the BN2
+//     backward finalize, it bounds the conv2 output gradient, whose fp16 scale the backward
+//     picks from it.
 // K order and input-row sharing as conv2_fwd_bf16x3_kernel: K-step s < 10 pairs taps
 // (ky = s>>1, kx = 2(s&1) + (g>>1)) so one staged input row R serves output rows R - ky;
 // s = 10 + kp pairs (ky = 2kp + (g>>1), kx = 4) with lane groups 2-3 reading row R+1.
@@ -211,7 +213,7 @@ template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
                                        const float* __restrict__ bias, const float* __restrict__ gamma,
                                        float* __restrict__ y2, float* __restrict__ ya, double* __restrict__ partial,
-                                       uint32_t* __restrict__ mag, const int* __restrict__ order, int B, int P,
+                                       uint32_t* __restrict__ ypart, const int* __restrict__ order, int B, int P,
                                        char* smem) {
   constexpr int NT = WV & 1, RH = WV >> 1;
   const int lane = threadIdx.x & 63, li = lane & 15;
@@ -264,21 +266,21 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     f2_store<DIAG>(smem + F2_OFF_S + ((kk - 1) & 1) * F2_STAGE, prev, y2, P);
     f2_store_ya(ys + ((kk - 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
   }
-  if (mag != nullptr) {  // max |y2| of channel 16NT + li: the 4 lane groups, then one atomic per wave
-    ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 16, 64));
-    ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 32, 64));
-    if (lane < 16) atomicMax(mag + 16 * NT + li, ymx);
-  }
+  // max |y2| of channel 16NT + li over the 4 lane groups (then the two waves of this co half)
+  ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 16, 64));
+  ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 32, 64));
   // BN2 partials: reduce the 4 lane groups, then the two row-halves of this co half
   s_acc += __shfl_xor(s_acc, 16, 64);
   s_acc += __shfl_xor(s_acc, 32, 64);
   q_acc += __shfl_xor(q_acc, 16, 64);
   q_acc += __shfl_xor(q_acc, 32, 64);
   __syncthreads();  // all operand reads done: reuse the LDS for the reduction
-  double* red = reinterpret_cast<double*>(smem);  // [4 waves][16 co][2]
+  double* red = reinterpret_cast<double*>(smem);                   // [4 waves][16 co][2]
+  uint32_t* yred = reinterpret_cast<uint32_t*>(smem + 4 * 16 * 2 * 8);  // [4 waves][16 co]
   if (lane < 16) {
     red[(WV * 16 + li) * 2 + 0] = (double)s_acc;
     red[(WV * 16 + li) * 2 + 1] = (double)q_acc;
+    yred[WV * 16 + li] = ymx;
   }
   __syncthreads();
   if (WV == 0 && lane < 64) {
@@ -286,6 +288,9 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     // waves with this co half: nt (rows 0-3) and nt + 2 (rows 4-7)
     const double v = red[(nt * 16 + c16) * 2 + k] + red[((nt + 2) * 16 + c16) * 2 + k];
     partial[((int64_t)co * gridDim.x + blockIdx.x) * 2 + k] = v;
+    // this workgroup's max |y2| per channel: a plain store per (channel, workgroup), reduced by
+    // the BN2-backward finalize (no same-address atomics: 16 K of them cost ~40 us in the head)
+    if (ypart != nullptr && k == 0) ypart[co * gridDim.x + blockIdx.x] = max(yred[nt * 16 + c16], yred[(nt + 2) * 16 + c16]);
   }
 }
 
@@ -296,14 +301,14 @@ __global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* 
                                                                    const float* __restrict__ gamma,
                                                                    float* __restrict__ y2, float* __restrict__ ya,
                                                                    double* __restrict__ partial,
-                                                                   uint32_t* __restrict__ mag,
+                                                                   uint32_t* __restrict__ ypart,
                                                                    const int* __restrict__ order, int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
-  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
-  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
-  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
-  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, mag, order, B, P, smem);
+  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
+  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
+  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
+  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
 }
 
 }  // namespace tds
@@ -331,7 +336,7 @@ static int f2_diag_env() { return 0; }
 
 // order: the blocked tile order table (tds_tile_order_fill), allocated by the caller
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, uint32_t* mag, const int* order, int nwg, int B, int P, hipStream_t st) {
+                    double* partial, uint32_t* ypart, const int* order, int nwg, int B, int P, hipStream_t st) {
   const dim3 grid(nwg), block(F2_THREADS);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wp);
@@ -349,12 +354,12 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const fl
   }
   switch (f2_diag_env()) {
 #ifdef TDS_DIAG
-    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
-    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
-    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
-    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
 #endif
-    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, mag, order, B, P); break;
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
   }
   TDS_LAUNCH_CHECK();
 }

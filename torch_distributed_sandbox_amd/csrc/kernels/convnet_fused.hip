@@ -305,9 +305,21 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __r
                                                                float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                                float* __restrict__ kbuf, double* __restrict__ sums_out,
                                                                const float* __restrict__ dl, int B, int NC,
-                                                               float* __restrict__ dbfc, float scale) {
+                                                               float* __restrict__ dbfc, float scale,
+                                                               const uint32_t* __restrict__ ypart, int nyp,
+                                                               const uint32_t* __restrict__ gpart, int ngp,
+                                                               uint32_t* __restrict__ mag) {
   __shared__ double sh[8];
+  __shared__ uint32_t shm[8];
   const int c = blockIdx.x;
+  if (mag != nullptr) {  // magnitude bounds of the conv2 backward's fp16 scale (conv2_bwd.hip)
+    const uint32_t* src = c == C ? gpart : ypart + (int64_t)c * nyp;
+    const int cnt = c == C ? ngp : nyp;
+    uint32_t m = 0u;
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) m = max(m, src[k]);
+    m = block_max(m, shm);
+    if (threadIdx.x == 0) mag[c] = m;
+  }
   if (c == C) {
     if (dbfc && (int)threadIdx.x < NC) {
       float v = 0.f;
@@ -740,13 +752,14 @@ void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int i
 
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
                           float* dgamma, float* dbeta, float* kbuf, const float* dl, int B, int NC, float* dbfc,
-                          float scale, hipStream_t st) {
+                          float scale, const uint32_t* ypart, int nyp, const uint32_t* gpart, int ngp, uint32_t* mag,
+                          hipStream_t st) {
   if (dbfc && (NC < 1 || NC > 256)) {
     tds_launch_fail("bn_bwd_finalize2: the fc bias gradient needs 1 <= classes <= 256");
     return;
   }
   hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(C + 1), dim3(256), 0, st, partial, C, nchunk, n, gamma, stats, dgamma,
-                     dbeta, kbuf, nullptr, dl, B, NC, dbfc, scale);
+                     dbeta, kbuf, nullptr, dl, B, NC, dbfc, scale, ypart, nyp, gpart, ngp, mag);
   TDS_LAUNCH_CHECK();
 }
 

@@ -275,16 +275,19 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const double* __restri
 //   partial[c][pass*nblk + blk][2] = { sum g2m, sum g2m * ya }       (BN2 backward sums)
 //   dW[j][c][pos] (= or +=) scale * sum_b dl[b][j] X[b][c][pos]      (WITH_DW; ACC adds)
 //   Wupd = W - lr * dW                                               (UPD: SGD step fused)
-//   gmax (optional): atomic max of |g2m| as float bits (NaN-propagating as an unsigned max) --
-//   the magnitude bound behind the conv2 backward's fp16 scale (conv2_bwd.hip)
+//   gpart (optional): this workgroup's max |g2m| as float bits (NaN-propagating as an unsigned
+//   max), at [(c*npass + pass)*nblk + band] -- reduced by the BN2-backward finalize into the
+//   magnitude bound behind the conv2 backward's fp16 scale (conv2_bwd.hip).  Plain stores: one
+//   same-address atomic per wave cost ~40 us per step (12.8 K of them at 3000^2).
 // KEEP: dW is also stored (UPD without KEEP: the update only -- optimizer-in-backward semantics,
 // the gradient itself is never materialised, 720 MB less written at 3000^2).
 template <int NB, bool WITH_DW, bool ACC, bool UPD, bool KEEP = true>
 __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     const float* __restrict__ ya, const float* W, const float* __restrict__ aff2, const float* __restrict__ dl,
     float* __restrict__ g2m, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass, int npass,
-    int NC, float scale, float lr, int c0, uint32_t* __restrict__ gmax) {
+    int NC, float scale, float lr, int c0, uint32_t* __restrict__ gpart) {
   __shared__ float red[2][HP_THREADS / 64];
+  __shared__ uint32_t gred[HP_THREADS / 64];
   const HPGrid hg = hp_grid(g);
   const int wg = blockIdx.x;
   const int c = c0 + wg / hg.per_channel(), band = wg - (c - c0) * hg.per_channel();
@@ -330,7 +333,9 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
           gs = fmaf(dls[b * 10 + j], wk, gs);
         }
         gm[k] = (ok && z > 0.f) ? gs : 0.f;
+#ifndef TDS_HP_NO_GMX  // (A/B timing variant only)
         gmx = max(gmx, __float_as_uint(gm[k]) & 0x7fffffffu);
+#endif
         x[b][k] = ok ? hp_relu(z) : 0.f;
         sdz += gm[k];
         sdy = fmaf(gm[k], ok ? yy[k] : 0.f, sdy);
@@ -372,17 +377,21 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     if (HP_PF) cur = nxt;
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (gmax != nullptr) {
-    gmx = wave_max(gmx);
-    if (lane == 0) atomicMax(gmax, gmx);
-  }
+  gmx = wave_max(gmx);
   sdz = wave_sum(sdz);
   sdy = wave_sum(sdy);
   if (lane == 0) {
     red[0][wv] = sdz;
     red[1][wv] = sdy;
+    gred[wv] = gmx;
   }
   __syncthreads();
+  if (gpart != nullptr && threadIdx.x == 0) {
+    uint32_t m = gred[0];
+#pragma unroll
+    for (int i = 1; i < HP_THREADS / 64; ++i) m = max(m, gred[i]);
+    gpart[((int64_t)c * npass + pass) * hg.per_channel() + band] = m;
+  }
   if (threadIdx.x < 2) {
     const int k = threadIdx.x;
     const double s = (((double)red[k][0] + (double)red[k][1]) + (double)red[k][2]) + (double)red[k][3];
@@ -429,7 +438,7 @@ int tds_head_bwd_pb_npass(int B) { return (B + HP_MAXB - 1) / HP_MAXB; }
 
 int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
-                    int c1, uint32_t* gmax, hipStream_t st) {
+                    int c1, uint32_t* gpart, hipStream_t st) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1 || c0 < 0 || c1 > 32 || c0 >= c1) return -1;
   const int npass = tds_head_bwd_pb_npass(B);
   if (Wupd && npass != 1) return -2;  // the fused SGD step needs the whole dW in one pass
@@ -441,7 +450,7 @@ int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const 
     const bool acc = pass > 0;
 #define TDS_HPB_E(NBV, WD, AC, UP, KP)                                                                             \
   hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, \
-                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gmax);
+                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gpart);
 #define TDS_HPB(NBV)                                   \
   case NBV:                                            \
     if (!dW && Wupd) {                                 \

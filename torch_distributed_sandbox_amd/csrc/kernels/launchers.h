@@ -62,7 +62,7 @@ int tds_take_launch_error(char* buf, int n);  // 1 (and the message) if a launch
 void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  // test hook: a launch of any config
 
 // ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, fp16x2 split MFMA)
-// mag (optional): 33 words of magnitude bounds [max|y2| per channel (32) | max|g2m|], reset here
+// mag (optional): 33 words of magnitude bounds [max|y2| per channel (32) | max|g2m|], zeroed here
 void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, hipStream_t st);
 int tds_conv2_num_wg();  // CUs (tds_device_cus)
 // ---- cu_budget.hip: CUs the persistent kernels may use (all minus a reserve for RCCL) and
@@ -80,9 +80,9 @@ void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, fl
 int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
 // y2 [B,P,P,32]; ya pooled-blocked (pooled_layout.h), max/min of each 2x2 window by sign(gamma2)
-// mag (optional): atomic max of |y2| per channel into mag[0..32)
+// ypart (optional): max |y2| per (channel, workgroup), [32][nwg] float bits
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, uint32_t* mag, const int* order, int nwg, int B, int P, hipStream_t st);
+                    double* partial, uint32_t* ypart, const int* order, int nwg, int B, int P, hipStream_t st);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups
@@ -110,9 +110,12 @@ int tds_conv2_bwd_clock_read(uint32_t* host, int n);  // DIAG 13 per-wave barrie
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st);  // border strips [B][8][82]
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
                          hipStream_t st);
+// + dbfc = scale * sum_b dl (when dbfc); + the magnitude bounds (when mag): mag[c] = max of
+// ypart[c][0..nyp), mag[C] = max of gpart[0..ngp) (float bits, unsigned max)
 void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, const float* gamma, const float* stats,
                           float* dgamma, float* dbeta, float* kbuf, const float* dl, int B, int NC, float* dbfc,
-                          float scale, hipStream_t st);  // + dbfc = scale * sum_b dl (when dbfc)
+                          float scale, const uint32_t* ypart, int nyp, const uint32_t* gpart, int ngp, uint32_t* mag,
+                          hipStream_t st);
 // BN statistics from per-workgroup partials [C][nchunk][2] reduced and finalized in one launch
 void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
                             float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
@@ -132,17 +135,16 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 int tds_head_bwd_pb_npass(int B);
 // channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
 // soon as its launch lands; the BN2 partials of the other channels are left untouched)
-// gmax (optional): atomic max of |g2m| (float bits) -- the conv2 backward's fp16 scale bound
+// gpart (optional): max |g2m| per workgroup (float bits), [32][npass][nblk]
 int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
-                    int c1, uint32_t* gmax, hipStream_t st);
+                    int c1, uint32_t* gpart, hipStream_t st);
 
 // ---- zs_exchange.hip (zero-suppressed fc-input rows, parallel/zs.py)
 int64_t tds_zs_npages(int64_t n);
 // meta [npages * 65] (offsets + mask words), counts [npages] scratch, vals [cap] (dropped past
 // cap), nnz: int64 device scalar
-void tds_zs_encode(const float* x, int64_t n, int* meta, int* counts, float* vals, int64_t cap, int64_t* nnz,
-                   hipStream_t st);
+void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t cap, int64_t* nnz, hipStream_t st);
 void tds_zs_decode(const int* meta, const float* vals, int64_t cap, float* out, int64_t n, hipStream_t st);
 // segmented form (the sharded exchange): page table (start, cnt, seg) + per-segment first page /
 // page count; values in fixed-capacity slots per segment; seg_nnz [nseg] int64

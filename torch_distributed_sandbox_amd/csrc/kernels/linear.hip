@@ -230,6 +230,72 @@ __global__ __launch_bounds__(256) void linear_dw_mfma_kernel(const float* __rest
   }
 }
 
+// Same contract as linear_dw_mfma_kernel, for the aligned case (K, ldw multiples of 4, 16-B
+// aligned rows): a streaming VALU kernel, 4 columns per thread.  The fc exchange's update is
+// one pass over the 720 MB weight (read + write) and every rank's rows of x: it is bound by
+// HBM, and the MFMA kernel above moves it in 64-B pieces (16 columns x one float per lane, one
+// column block in flight per wave): 754 us for 1.8 GB at the bench shape.  Here every access is
+// a 16-B-per-lane vector (1 KiB per wave instruction) and a thread has its NN weight rows and 8
+// x rows in flight at once.  g (dY, tiny and wave-uniform) comes through scalar loads.
+template <int NN>
+__global__ __launch_bounds__(256) void linear_dw_vec_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                                            float* __restrict__ dW, float* __restrict__ db, int M,
+                                                            int64_t K, int64_t ldw, float scale, int acc,
+                                                            float upd_lr) {
+  if (db && blockIdx.x == 0 && threadIdx.x < NN) {
+    float t = 0.f;
+    for (int m = 0; m < M; ++m) t += g[m * NN + threadIdx.x];
+    db[threadIdx.x] = acc ? db[threadIdx.x] + scale * t : scale * t;
+  }
+  const bool rmw = upd_lr != 0.f || acc;
+  const int64_t nq = K / 4;
+  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+    const int64_t col = 4 * q;
+    float4 w[NN];
+    if (rmw) {
+#pragma unroll
+      for (int n = 0; n < NN; ++n) w[n] = *reinterpret_cast<const float4*>(dW + (int64_t)n * ldw + col);
+    }
+    float4 s[NN];
+#pragma unroll
+    for (int n = 0; n < NN; ++n) s[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int m0 = 0; m0 < M; m0 += 8) {
+      float4 xv[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        xv[i] = m0 + i < M ? __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(
+                                                              x + (int64_t)(m0 + i) * K + col)))
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (m0 + i < M) {
+#pragma unroll
+          for (int n = 0; n < NN; ++n) {
+            const float gv = g[(m0 + i) * NN + n];
+            s[n].x = fmaf(gv, xv[i].x, s[n].x);
+            s[n].y = fmaf(gv, xv[i].y, s[n].y);
+            s[n].z = fmaf(gv, xv[i].z, s[n].z);
+            s[n].w = fmaf(gv, xv[i].w, s[n].w);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < NN; ++n) {
+      const float4 v = make_float4(scale * s[n].x, scale * s[n].y, scale * s[n].z, scale * s[n].w);
+      float4 o;
+      if (upd_lr != 0.f) {  // update-only: dW is the weight, torch SGD p -= lr * g
+        o = make_float4(w[n].x - upd_lr * v.x, w[n].y - upd_lr * v.y, w[n].z - upd_lr * v.z, w[n].w - upd_lr * v.w);
+      } else if (acc) {
+        o = make_float4(w[n].x + v.x, w[n].y + v.y, w[n].z + v.z, w[n].w + v.w);
+      } else {
+        o = v;
+      }
+      *reinterpret_cast<float4*>(dW + (int64_t)n * ldw + col) = o;
+    }
+  }
+}
+
 }  // namespace tds
 
 using namespace tds;
@@ -282,6 +348,20 @@ int tds_linear_bwd_skinny(const float* dy, const float* x, const float* W, float
 int tds_linear_dw(const float* dy, const float* x, float* dW, float* db, int M, int N, int64_t K, int64_t ldw,
                   float scale, int acc, float upd_lr, hipStream_t st) {
   if (M > 64 || N > 16 || M < 1 || ldw < K) return -1;
+  const bool aligned = K % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)dW & 15) == 0;
+  if (aligned && (N == 10 || N == 16)) {
+    int64_t grid = (K / 4 + 255) / 256;
+    if (grid > 4096) grid = 4096;
+    if (grid < 1) grid = 1;
+    if (N == 10)
+      hipLaunchKernelGGL(linear_dw_vec_kernel<10>, dim3((unsigned)grid), dim3(256), 0, st, dy, x, dW, db, M, K, ldw,
+                         scale, acc, upd_lr);
+    else
+      hipLaunchKernelGGL(linear_dw_vec_kernel<16>, dim3((unsigned)grid), dim3(256), 0, st, dy, x, dW, db, M, K, ldw,
+                         scale, acc, upd_lr);
+    TDS_LAUNCH_CHECK();
+    return 0;
+  }
   int64_t ncb = (K + 15) / 16;
   int64_t grid = (ncb + 3) / 4;
   if (grid > 8192) grid = 8192;

@@ -170,9 +170,9 @@ class _Conv2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, p1, w2, b2, g2, link, link1):
         ops = _ext.ops()
-        # magnitude bounds of this step (max |y2| per channel here, max |g2m| in the head
-        # backward): the conv2 backward's fp16 scale of dy2; reset by conv2_pack
-        link.mag = torch.empty(33, device=p1.device, dtype=torch.int32)
+        # magnitude bounds of this step (per-workgroup max |y2| here, max |g2m| in the head
+        # backward, reduced by its BN2 finalize): the conv2 backward's fp16 scale of dy2
+        link.mag = torch.empty(ops.mag_numel(p1.shape[0], p1.shape[1]), device=p1.device, dtype=torch.int32)
         wp, wd = ops.conv2_pack(w2.contiguous(), link.mag)
         y2, partial2, ya = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
         ctx.save_for_backward(p1, wd, y2)

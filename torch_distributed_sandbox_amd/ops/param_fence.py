@@ -1,12 +1,19 @@
-"""Parameter fences: let an update of a parameter run on a side stream and make
-only the first reader of that parameter wait for it.
+"""Parameter fences: let an update of a parameter run elsewhere and make only the first
+reader of that parameter wait for it.
 
-``DistributedDataParallel(overlap_optimizer=True)`` finishes the fc layer's
-gradient collective and its SGD update on a side stream while the next step's
-convolution forward runs on the compute stream; the fused head / Linear forward
-calls :func:`wait` on the fc weight before reading it, which orders the
-compute stream after the update (a device-side event wait; the host never
-blocks).
+``DistributedDataParallel(overlap_optimizer=True)`` finishes the fc layer's gradient
+collective and its SGD update off the critical path while the next step's convolution
+forward runs; the fused head / Linear forward calls :func:`wait` on the fc weight before
+reading it.  A fence is a list of
+
+* events (an update queued on a side stream: the current stream waits for it on the device,
+  the host never blocks), and
+* deferred updates (:func:`defer`: a callable that queues the update itself on the current
+  stream when the parameter is first needed -- the fc gradient exchange's weight update,
+  parallel/factored.py, which then runs on the whole GPU right before the head forward
+  instead of competing with the backward's persistent kernels),
+
+processed in the order they were added.
 """
 from __future__ import annotations
 
@@ -15,19 +22,41 @@ import torch
 _ATTR = "_tds_param_fence"
 
 
+def _fences(param):
+    f = getattr(param, _ATTR, None)
+    if f is None:
+        f = []
+        setattr(param, _ATTR, f)
+    return f
+
+
 def set(param: torch.Tensor, event) -> None:  # noqa: A001 - mirrors a setter
-    setattr(param, _ATTR, event)
+    """Readers of ``param`` wait for ``event`` (after anything fenced before it)."""
+    _fences(param).append(("event", event))
+
+
+def defer(param: torch.Tensor, fn) -> None:
+    """``fn()`` queues a pending update of ``param`` on the current stream; it runs once, at the
+    first :func:`wait` on ``param``."""
+    _fences(param).append(("fn", fn))
 
 
 def wait(param) -> None:
-    """Order the current stream after a pending update of ``param`` (if any)."""
+    """Order the current stream after every pending update of ``param`` (running the deferred
+    ones on it)."""
     if param is None:
         return
-    ev = getattr(param, _ATTR, None)
-    if ev is not None:
-        torch.cuda.current_stream(param.device).wait_event(ev)
-        delattr(param, _ATTR)
+    f = getattr(param, _ATTR, None)
+    if not f:
+        return
+    delattr(param, _ATTR)
+    cur = torch.cuda.current_stream(param.device) if param.is_cuda else None
+    for kind, v in f:
+        if kind == "fn":
+            v()
+        elif cur is not None:
+            cur.wait_event(v)
 
 
 def pending(param) -> bool:
-    return getattr(param, _ATTR, None) is not None
+    return bool(getattr(param, _ATTR, None))

@@ -476,21 +476,24 @@ class ActivationExchange:
     def _zs_decode(self):
         """Rebuild every rank's rows into self._x_buf (current stream = where the gradient is
         formed), after the values gather."""
-        from . import zs
-
         z = getattr(self, "_zs_decode_pending", None)
         if z is None:
             return
         self._zs_decode_pending = None
+        self._zs_decode_into(z, self._x_buf)
+
+    def _zs_decode_into(self, z, x_buf):
+        from . import zs
+
         z["w_meta"].wait()
         z["w_vals"].wait()
         if z.get("kind") == "sharded":
-            zs.seg_decode(z["meta_recv"], z["recv"], z["vals_recv"], z["cap"], self._x_buf)
+            zs.seg_decode(z["meta_recv"], z["recv"], z["vals_recv"], z["cap"], x_buf)
             return
         W, n, M, cap = self.world, z["n"], z["M"], z["cap"]
         meta_all = z["meta_all"].view(W, M + 2)
         vals_all = z["vals_all"].view(W, cap)
-        out = self._x_buf.view(W, n)
+        out = x_buf.view(W, n)
         for r in range(W):
             zs.decode(meta_all[r, :M], vals_all[r], out[r])
 
@@ -512,6 +515,8 @@ class ActivationExchange:
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
             return
         dev = self._dy.device
+        if self._defer_update_inline():
+            return
         side = self.side_stream
         join = side is None
         if side is None:
@@ -537,6 +542,69 @@ class ActivationExchange:
         if join:
             torch.autograd.Variable._execution_engine.queue_callback(
                 lambda: torch.cuda.current_stream(dev).wait_stream(side))
+
+    def _defer_update_inline(self) -> bool:
+        """Activations path under DDP's overlapped optimizer with the step fused in (plain SGD):
+        leave the weight update -- decode, dW formation and ``W -= lr·dW`` in one ``linear_dw``
+        sweep over the 720 MB weight -- to the first reader of the weight, the next forward's
+        head, where it runs on the compute stream across the whole GPU (ops/param_fence.py:
+        ``defer``).  Run beside the backward's persistent kernels on a side stream the same
+        sweep took 1.7-2.0 ms and slowed the conv2 / layer-1 backward by ~0.8 ms (world 1,
+        forced exchange, profiles/r3_exchange_side_vs_inline.md).  The bias keeps its side-stream
+        path (dY gather, bias gradient, the optimizer's step), which needs dY only.
+        ``TDS_EXCHANGE_UPDATE=side`` keeps the whole finish on the side stream."""
+        import os
+
+        from ..ops import fused_update, param_fence
+        from . import distributed as tdist
+
+        if self.active != "activations" or self.side_stream is None:
+            return False
+        if os.environ.get("TDS_EXCHANGE_UPDATE", "inline").strip().lower() != "inline":
+            return False
+        lr = fused_update.take(self.weight, exchanged=True)
+        if not lr:
+            return False
+        dy = self._dy
+        dev = dy.device
+        rows = dy.shape[0]
+        scale = 1.0 / self.world
+        cur = torch.cuda.current_stream(dev)
+        side = self.side_stream
+        side.wait_stream(cur)
+        dy_all = torch.empty((self.world * rows, dy.shape[1]), device=dev, dtype=dy.dtype)
+        with torch.cuda.stream(side), torch.no_grad():
+            dy.record_stream(side)
+            tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
+            (_, _), (db, acc_b) = self._targets()
+            if db is not None:
+                s_b = dy_all.sum(0).mul_(scale)
+                db.add_(s_b) if acc_b else db.copy_(s_b)
+                self.bias.grad = db
+            ev_dy = torch.cuda.Event()
+            ev_dy.record(side)
+        z = getattr(self, "_zs_decode_pending", None)
+        self._zs_decode_pending = None
+        x_buf, x_work = self._x_buf, self._x_work
+        keep = (self._x_local,)  # the local rows stay alive until the gathers reading them are done
+        weight, lr = self.weight, float(lr)
+
+        def update():
+            from .. import _ext
+
+            torch.cuda.current_stream(dev).wait_event(ev_dy)
+            if z is not None:
+                self._zs_decode_into(z, x_buf)
+            else:
+                x_work.wait()
+            with torch.no_grad():
+                _ext.ops().linear_dw(dy_all, x_buf, weight.data, None, scale, False, lr)
+            assert keep
+
+        param_fence.defer(weight, update)
+        fused_update.applied(weight)
+        self._done()
+        return True
 
     def _targets(self):
         """(dW, accumulate_w), (db, accumulate_b) — gradients accumulated under no_sync()

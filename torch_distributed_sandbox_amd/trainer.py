@@ -154,6 +154,8 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
                 else:
                     print("Epoch [{}/{}], Step [{}/{}], Loss: {:.4f}".format(
                         epoch + 1, args.epochs, i + 1, total_step, shown.item()), flush=True)
+    if hasattr(model, "wait_pending_updates"):
+        model.wait_pending_updates()  # the last step's deferred fc update (ops/param_fence.py)
     if device.type == "cuda":
         torch.cuda.synchronize()
     t_end = time.perf_counter()

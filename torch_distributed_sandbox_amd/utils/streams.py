@@ -67,10 +67,15 @@ def compute_cus() -> int:
 
 def side_stream(device: Optional[torch.device] = None, side: Optional[str] = None) -> Optional[torch.cuda.Stream]:
     """A stream for DDP's side work (the fc exchange's dW formation, the deferred SGD step) that
-    keeps to one side of the CU split: ``side`` = "comm" (the reserved CUs, default) | "compute"
-    | "any" (a plain stream: None here).  ``TDS_SIDE_CUS`` overrides the default.  None when no
-    CUs are reserved (then a plain stream is as good as any)."""
-    side = (side or os.environ.get("TDS_SIDE_CUS", "comm")).strip().lower()
+    keeps to one side of the CU split: ``side`` = "any" (a plain stream: None here; default) |
+    "comm" (the reserved CUs) | "compute".  ``TDS_SIDE_CUS`` overrides the default.  None when no
+    CUs are reserved (then a plain stream is as good as any).
+
+    Measured at world 1 with 32 CUs reserved and the exchange forced (tools/gpu_sessions/
+    r3_s3.sh, docs/DISTRIBUTED.md): the 32 reserved CUs are far too few for the exchange's dW
+    formation (activations 7.91 ms/step on "comm" vs 5.32 on "any" and 5.31 on "compute";
+    sharded 8.44 / 5.25 / 5.11), so the default is a plain stream."""
+    side = (side or os.environ.get("TDS_SIDE_CUS", "any")).strip().lower()
     if side not in ("comm", "compute", "any"):
         raise ValueError(f"side stream placement must be comm|compute|any, got {side!r}")
     if side == "any":
