@@ -158,7 +158,7 @@ def test_upsample(gpu):
     assert ((y.double().cpu() - ref).abs() > 1e-6).float().mean().item() < 1e-3
 
 
-@pytest.mark.parametrize("n", [1, 2047, 2048, 100_003, 3 * 2048 * 5])
+@pytest.mark.parametrize("n", [1, 2047, 2048, 100_003, 3 * 2048 * 5, 20_000_003])
 def test_zs_encode_decode_matches_reference(gpu, n):
     """Zero-suppressed fc-row codec (csrc/kernels/zs_exchange.hip) vs the torch reference of
     parallel/zs.py: identical meta and values, a bitwise round trip, -0.0 and NaN kept, values
@@ -184,6 +184,52 @@ def test_zs_encode_decode_matches_reference(gpu, n):
         small = torch.full((rnnz // 2,), -1.0, device=gpu)
         assert int(zs.encode(x, meta, small)) == rnnz
         assert torch.equal(small.cpu().view(torch.int32), rvals[:rnnz // 2].view(torch.int32))
+
+
+@pytest.mark.parametrize("K", [10_004, 4096])
+def test_linear_dw_zs_matches_dense(gpu, K):
+    """The exchange's dW formation straight from the all-gathered zero-suppressed rows
+    (linear_dw_zs: decoded in registers) is bitwise the dense linear_dw on the decoded rows --
+    gradient mode (with the bias) and the update-only step -- and matches fp64.  K = 10 004: a
+    partial last 1024-column block, rows crossing pages."""
+    from torch_distributed_sandbox_amd.parallel import zs
+
+    torch.manual_seed(K)
+    W, rows, N = 3, 2, 10
+    xs = torch.relu(torch.randn(W, rows, K, device=gpu))
+    xs[:, :, ::7] = -0.0
+    n = rows * K
+    M = zs.meta_numel(n)
+    enc = [zs.encode_ref(xs[r].cpu()) for r in range(W)]
+    cap = max(e[2] for e in enc)
+    meta_all = torch.zeros(W, M + 2, dtype=torch.int32, device=gpu)
+    vals_all = torch.zeros(W, cap, device=gpu)
+    for r, (mt, vl, nz) in enumerate(enc):
+        meta_all[r, :M] = mt.to(gpu)
+        vals_all[r, :nz] = vl.to(gpu)
+    dy = torch.randn(W * rows, N, device=gpu)
+    x_rows = xs.reshape(W * rows, K).contiguous()
+    ops = _ops()
+    dw, db = torch.empty(N, K, device=gpu), torch.empty(N, device=gpu)
+    ops.linear_dw_zs(dy, meta_all, vals_all, rows, dw, db, 0.5, False)
+    dw_ref, db_ref = torch.empty_like(dw), torch.empty_like(db)
+    ops.linear_dw(dy, x_rows, dw_ref, db_ref, 0.5, False)
+    assert torch.equal(dw, dw_ref) and torch.equal(db, db_ref)
+    ref = 0.5 * dy.double().t() @ x_rows.double()
+    _check_rel(dw, ref, 1e-6)
+    # update-only step (the exchange's optimizer-in-backward): W -= lr * scale * dyᵀX
+    w0 = torch.randn(N, K, device=gpu)
+    w1, w2 = w0.clone(), w0.clone()
+    ops.linear_dw_zs(dy, meta_all, vals_all, rows, w1, None, 0.5, False, 0.1)
+    ops.linear_dw(dy, x_rows, w2, None, 0.5, False, 0.1)
+    assert torch.equal(w1, w2)
+    _check_rel(w1, w0.double() - 0.1 * ref, 1e-6)
+
+
+def _check_rel(a, ref, tol):
+    a, ref = a.double().cpu(), ref.double().cpu()
+    e = (a - ref).abs().max().item()
+    assert e <= tol * max(ref.abs().max().item(), 1e-30), e
 
 
 def test_zs_segmented_codec_matches_reference(gpu):

@@ -1,0 +1,32 @@
+#!/bin/bash
+# round 3: fused zero-suppressed dW update (linear_dw_zs), wave-wide look-back encode
+# (decoupled look-back) -- full GPU suite, head-backward A/B (max tracking), bench, forced
+# exchange costs, trace of the forced activation exchange
+set -u
+O=gpurun_out/r3s6
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 400 --timeout-method thread > $O/tests.log 2>&1
+rc=$?
+grep -E "FAILED|passed|failed" $O/tests.log | tail -12
+[ $rc -le 1 ] || { echo "tests rc=$rc"; tail -40 $O/tests.log; exit 1; }
+
+
+
+
+b() {
+  local name=$1; shift
+  timeout -k 10 200 python -u bench.py "$@" > $O/$name.log 2>&1 || { echo "$name rc=$?"; tail -20 $O/$name.log; exit 1; }
+  echo "$name: $(tail -1 $O/$name.log | python3 -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["value"], r["ms_per_step"], r["config"]["fc_grad"], r["config"]["reserve_cus"], r["config"].get("x_exchange"))')"
+}
+b bench_1 --steps 30 --warmup 5
+b bench_2 --steps 100 --warmup 10
+b act --steps 30 --warmup 5 --grad-exchange activations
+b act_dense --steps 30 --warmup 5 --grad-exchange activations --no-exchange-compress
+b shd --steps 30 --warmup 5 --grad-exchange sharded
+b act_r32 --steps 30 --warmup 5 --grad-exchange activations --reserve-cus 32
+b shd_r32 --steps 30 --warmup 5 --grad-exchange sharded --reserve-cus 32
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/act_prof -o run -- \
+  python3 $GRAFT_REPO_ROOT/bench.py --steps 10 --warmup 3 --grad-exchange activations > $GRAFT_REPO_ROOT/$O/act_prof.log 2>&1 \
+  || { echo "act prof rc=$?"; tail -20 $GRAFT_REPO_ROOT/$O/act_prof.log; exit 1; }
+echo "act prof ok"

@@ -574,6 +574,39 @@ void zs_decode(const Tensor& meta, const Tensor& values, const Tensor& out) {
   check_launches("zs_decode");
 }
 
+// dW (=/+=) scale dyᵀX or W -= update_lr * scale dyᵀX with X as the all-gathered zero-suppressed
+// rows: meta [W, P*65 + 2] int32 (the records + each rank's count), values [W, cap] fp32, `rows`
+// rows of K columns per rank; dy [W*rows, N].  The counts must not exceed cap (the caller checks).
+void linear_dw_zs(const Tensor& dy, const Tensor& meta, const Tensor& values, int64_t rows, const Tensor& dw,
+                  const c10::optional<Tensor>& db, double scale, bool accumulate, double update_lr) {
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == at::kFloat && dy.is_contiguous() && dy.dim() == 2,
+              "linear_dw_zs: dy fp32 [M, N] contiguous GPU");
+  const int64_t M = dy.size(0), N = dy.size(1);
+  TORCH_CHECK(dw.is_cuda() && dw.scalar_type() == at::kFloat && dw.dim() == 2 && dw.size(0) == N && dw.stride(1) == 1,
+              "linear_dw_zs: dW [N, K] unit-stride rows");
+  const int64_t K = dw.size(1);
+  TORCH_CHECK(rows >= 1 && M % rows == 0, "linear_dw_zs: dy rows must be W x rows");
+  const int64_t W = M / rows, P = tds_zs_npages(rows * K);
+  TORCH_CHECK(meta.is_cuda() && meta.scalar_type() == at::kInt && meta.is_contiguous() && meta.dim() == 2 &&
+                  meta.size(0) == W && meta.size(1) >= P * 65,
+              "linear_dw_zs: meta int32 [W, >= npages*65]");
+  TORCH_CHECK(values.is_cuda() && values.scalar_type() == at::kFloat && values.is_contiguous() && values.dim() == 2 &&
+                  values.size(0) == W,
+              "linear_dw_zs: values fp32 [W, cap]");
+  TORCH_CHECK(rows * K < ((int64_t)1 << 31), "linear_dw_zs: int32 offsets");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    need(*db, at::kFloat, {N}, "db");
+    dbp = db->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(dy.device());
+  const int rc = tds_linear_dw_zs(dy.data_ptr<float>(), meta.data_ptr<int>(), meta.size(1), values.data_ptr<float>(),
+                                  values.size(1), (int)rows, (int)M, (int)N, K, dw.data_ptr<float>(), dw.stride(0), dbp,
+                                  (float)scale, accumulate ? 1 : 0, (float)update_lr, stream_of(dy));
+  TORCH_CHECK(rc == 0, "linear_dw_zs: unsupported shape (K % 4, 16-B aligned rows, N in {10, 16})");
+  check_launches("linear_dw_zs");
+}
+
 void check_pages(const Tensor& start, const Tensor& cnt, const Tensor& seg, const Tensor& like) {
   TORCH_CHECK(start.is_cuda() && start.scalar_type() == at::kLong && start.dim() == 1 && start.is_contiguous(),
               "zs pages: start int64 [npages]");
@@ -626,6 +659,10 @@ void zs_seg_decode(const Tensor& meta, const Tensor& pg_start, const Tensor& pg_
 
 TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("zs_encode(Tensor x, Tensor(a!) meta_out, Tensor(b!) values_out) -> Tensor", &zs_encode);
+  m.def(
+      "linear_dw_zs(Tensor dy, Tensor meta, Tensor values, int rows, Tensor(a!) dw, Tensor(b!)? db, float scale, "
+      "bool accumulate, float update_lr=0.0) -> ()",
+      &linear_dw_zs);
   m.def(
       "zs_seg_encode(Tensor x, Tensor pg_start, Tensor pg_cnt, Tensor pg_seg, Tensor seg_first, Tensor seg_npg, "
       "Tensor(a!) meta_out, Tensor(b!) values_out, int cap) -> Tensor",

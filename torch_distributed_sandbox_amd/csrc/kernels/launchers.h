@@ -146,6 +146,10 @@ int64_t tds_zs_npages(int64_t n);
 // cap), nnz: int64 device scalar
 void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t cap, int64_t* nnz, hipStream_t st);
 void tds_zs_decode(const int* meta, const float* vals, int64_t cap, float* out, int64_t n, hipStream_t st);
+// linear_dw with X given as W source ranks' zero-suppressed encodings (decoded in registers)
+int tds_linear_dw_zs(const float* dy, const int* meta, int64_t mstride, const float* vals, int64_t cap, int rows,
+                     int M, int N, int64_t K, float* dW, int64_t ldw, float* db, float scale, int acc, float upd_lr,
+                     hipStream_t st);
 // segmented form (the sharded exchange): page table (start, cnt, seg) + per-segment first page /
 // page count; values in fixed-capacity slots per segment; seg_nnz [nseg] int64
 void tds_zs_seg_encode(const float* x, const int64_t* pg_start, const int* pg_cnt, const int* pg_seg, int64_t npages,

@@ -6,9 +6,10 @@
 // Pages of 2048 flat elements, one 256-thread workgroup per page, thread t owns elements
 // 8t .. 8t+7 of its page (one byte of the mask).  meta[p*65] = the page's value offset,
 // meta[p*65 + 1 + j] = mask word j (bit i <-> element 32j + i, "non-zero" = any bit set).
-//   encode: zs_encode -- ONE pass over X: mask words, the page's count, its value offset by a
-//           decoupled look-back over the preceding pages' published counts, and the values
-//           compacted through LDS into coalesced stores (dropped past the capacity).  (Three
+//   encode: zs_encode -- ONE pass over X, 8 pages per workgroup: mask words, the counts, the
+//           tile's value offset by a decoupled look-back over the preceding tiles' published
+//           counts, and the values compacted through LDS into coalesced stores (dropped past
+//           the capacity).  (Three
 //           passes -- count, a one-workgroup scan, compaction -- took 71 + 80 + 143 us at the
 //           3000^2 bench shape, on the compute stream.)
 //   decode: zs_expand (values back to their places, zeros elsewhere)
@@ -67,15 +68,20 @@ __device__ __forceinline__ int zs_block_scan(int v, int* sh, int& total) {
   return base + incl - v;
 }
 
-// Single-pass encode.  Page order is the order workgroups START (a ticket from a counter; the
-// workgroup drawing the last ticket resets it for the next call), so every page a workgroup
-// looks back at belongs to a workgroup that is already running or done -- no reliance on the
-// dispatcher's order.  Each page
-// publishes a 64-bit status word: [63:40] the call's epoch (24 bits; words of earlier calls never
-// match), [39:38] 1 = its own count, 2 = its inclusive prefix, [37:0] the value.  Thread 0 walks
-// back from page p-1, adding counts until it meets an inclusive prefix.  Status words and the
-// counter belong to one (device, stream) (host side below).
+// Single-pass encode over TILES of ZS_TILE pages (one workgroup each, the tile's X in
+// registers: 8 elements x 8 pages per thread).  Tile order is the order workgroups START (a
+// ticket from a counter; the workgroup drawing the last ticket resets it for the next call), so
+// every tile a workgroup looks back at belongs to a workgroup already running or done -- nothing
+// depends on the dispatcher's order or placement (cdna_hip_programming.md, Guideline 16).  Each
+// tile publishes a 64-bit status word (the value travels inside the atomic word: no payload to
+// make visible): [63:40] the call's epoch (24 bits; words of earlier calls never match), [39:38]
+// 1 = the tile's own count, 2 = its inclusive prefix, [37:0] the value.  Wave 0 walks back from
+// tile t-1, 64 tiles per round (one status word per lane), adding counts up to the nearest
+// inclusive prefix.  Measured at the bench shape (44 K pages): one page per workgroup spent
+// 550-590 us in the single ticket counter's same-address atomics and the walk; 8 pages per
+// workgroup cut both by 8x.  Status words and the counter belong to one (device, stream).
 constexpr int ZS_ST_VAL = 38, ZS_ST_EPOCH = 40;
+constexpr int ZS_TILE = 8;
 
 __device__ __forceinline__ void zs_status_store(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -84,61 +90,89 @@ __device__ __forceinline__ unsigned long long zs_status_load(unsigned long long*
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(256) void zs_encode_kernel(const uint32_t* __restrict__ x, int64_t n,
+__global__ __launch_bounds__(256) void zs_encode_kernel(const uint32_t* __restrict__ x, int64_t n, int64_t npages,
                                                         int* __restrict__ meta, uint32_t* __restrict__ vals,
                                                         int64_t cap, int64_t* __restrict__ nnz,
                                                         unsigned long long* __restrict__ status,
                                                         unsigned long long* __restrict__ ticket,
                                                         unsigned long long epoch) {
-  __shared__ uint32_t bytes[256];
+  __shared__ uint32_t bytes[ZS_TILE][256];
   __shared__ uint32_t lv[ZS_PAGE];
   __shared__ int sh[4];
-  __shared__ long long s_page, s_prefix;
+  __shared__ int ptot[ZS_TILE];
+  __shared__ long long s_tile, s_prefix;
   const int tid = threadIdx.x;
   if (tid == 0) {
     const unsigned long long t = atomicAdd(ticket, 1ull);
     if (t == (unsigned long long)gridDim.x - 1) zs_status_store(ticket, 0ull);  // every ticket is out
-    s_page = (long long)t;
+    s_tile = (long long)t;
   }
   __syncthreads();
-  const int64_t p = s_page;
-  uint32_t v[8];
-  zs_load8(x, p * ZS_PAGE + 8 * (int64_t)tid, n, v);
-  const uint32_t m = zs_byte(v);
-  bytes[tid] = m;
-  int total;
-  const int ex = zs_block_scan(__builtin_popcount(m), sh, total);  // (its barriers order bytes)
-  if (tid == 0) {
+  const int64_t tile = s_tile, p0 = tile * ZS_TILE;
+  uint32_t v[ZS_TILE][8];
+  int ex[ZS_TILE];
+#pragma unroll
+  for (int k = 0; k < ZS_TILE; ++k) zs_load8(x, (p0 + k) * ZS_PAGE + 8 * (int64_t)tid, n, v[k]);
+  int tile_total = 0;
+#pragma unroll
+  for (int k = 0; k < ZS_TILE; ++k) {
+    const uint32_t m = zs_byte(v[k]);
+    bytes[k][tid] = m;
+    int total;
+    ex[k] = zs_block_scan(__builtin_popcount(m), sh, total);  // (its barriers order bytes)
+    if (tid == 0) ptot[k] = total;
+    tile_total += total;
+  }
+  if (tid < 64) {  // wave 0: the look-back, 64 predecessor tiles per round (lane i <-> tile q - i)
     const unsigned long long tag = epoch << ZS_ST_EPOCH, agg = 1ull << ZS_ST_VAL, inc = 2ull << ZS_ST_VAL;
     const unsigned long long vmask = (1ull << ZS_ST_VAL) - 1;
     long long prefix = 0;
-    if (p > 0) {
-      zs_status_store(status + p, tag | agg | (unsigned long long)total);
-      for (int64_t q = p - 1;; --q) {
-        unsigned long long w;
-        do {
-          w = zs_status_load(status + q);
-        } while ((w >> ZS_ST_EPOCH) != epoch || ((w >> ZS_ST_VAL) & 3ull) == 0);
-        prefix += (long long)(w & vmask);
-        if (((w >> ZS_ST_VAL) & 3ull) == 2ull) break;
+    if (tile > 0) {
+      if (tid == 0) zs_status_store(status + tile, tag | agg | (unsigned long long)tile_total);
+      for (int64_t q = tile - 1;; q -= 64) {
+        const int64_t qi = q - tid;
+        // tiles before the first count as an inclusive prefix of 0
+        unsigned long long w = qi >= 0 ? 0ull : (tag | inc);
+        bool ready = qi < 0;
+        while (__builtin_amdgcn_ballot_w64(!ready) != 0ull) {
+          if (!ready) {
+            w = zs_status_load(status + qi);
+            ready = (w >> ZS_ST_EPOCH) == epoch && ((w >> ZS_ST_VAL) & 3ull) != 0ull;
+          }
+        }
+        const unsigned long long incl = __builtin_amdgcn_ballot_w64(((w >> ZS_ST_VAL) & 3ull) == 2ull);
+        const int first = incl ? __builtin_ctzll(incl) : 64;  // the nearest inclusive prefix
+        prefix += wave_sum(tid <= first ? (long long)(w & vmask) : 0ll);
+        if (incl) break;
       }
     }
-    zs_status_store(status + p, tag | inc | (unsigned long long)(prefix + total));
-    s_prefix = prefix;
-    meta[p * ZS_META] = (int)prefix;
-    if (p == (int64_t)gridDim.x - 1) *nnz = prefix + total;
+    if (tid == 0) {
+      zs_status_store(status + tile, tag | inc | (unsigned long long)(prefix + tile_total));
+      s_prefix = prefix;
+      if (tile == (int64_t)gridDim.x - 1) *nnz = prefix + tile_total;
+    }
   }
-  if (tid < 64)
-    meta[p * ZS_META + 1 + tid] =
-        (int)(bytes[4 * tid] | (bytes[4 * tid + 1] << 8) | (bytes[4 * tid + 2] << 16) | (bytes[4 * tid + 3] << 24));
-  int pos = ex;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (v[i] != 0u) lv[pos++] = v[i];
   __syncthreads();
-  const int64_t o = s_prefix;
-  for (int i = tid; i < total; i += 256)
-    if (o + i < cap) vals[o + i] = lv[i];
+  long long o = s_prefix;
+#pragma unroll
+  for (int k = 0; k < ZS_TILE; ++k) {
+    const int64_t p = p0 + k;
+    if (p >= npages) break;  // (workgroup-uniform)
+    if (tid == 0) meta[p * ZS_META] = (int)o;
+    if (tid < 64)
+      meta[p * ZS_META + 1 + tid] = (int)(bytes[k][4 * tid] | (bytes[k][4 * tid + 1] << 8) |
+                                          (bytes[k][4 * tid + 2] << 16) | (bytes[k][4 * tid + 3] << 24));
+    int pos = ex[k];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (v[k][i] != 0u) lv[pos++] = v[k][i];
+    __syncthreads();
+    const int total = ptot[k];
+    for (int i = tid; i < total; i += 256)
+      if (o + i < cap) vals[o + i] = lv[i];
+    o += total;
+    __syncthreads();  // lv is rewritten by the next page
+  }
 }
 
 __global__ __launch_bounds__(256) void zs_expand_kernel(const int* __restrict__ meta, const uint32_t* __restrict__ vals,
@@ -286,9 +320,131 @@ __global__ __launch_bounds__(256) void zs_seg_expand_kernel(const int* __restric
   }
 }
 
+// ---------------------------------------------------------------------------- fused update
+// dW (=/+=) scale * dYᵀX, or the update-only W -= lr * scale * dYᵀX (linear_dw's contract), with
+// X given zero-suppressed: the all-gathered encodings of the W source ranks (rank r: meta at
+// meta + r*mstride, values at vals + r*cap; its `rows` rows of K columns encoded flat).  Row
+// m = r*rows + b of dY pairs with local row b of rank r.  The rows are decoded in registers:
+// no dense X is written and read back (zs_expand + linear_dw moved 2 x 360 MB per source rank
+// more at the bench shape).
+//
+// A workgroup takes 1024 columns (4 per thread, one 16-B piece of each output row).  For each X
+// row the span lies in at most 2 pages: their 2 x 64 mask words are loaded into LDS and turned
+// into exclusive popcount prefixes (one wave per page), so a thread finds its 4 values' offset
+// with one LDS read and a popcount.  Needs K % 4 == 0 (a thread's 4 columns share a mask word).
+constexpr int ZD_COLS = 1024;
+
+template <int NN>
+__global__ __launch_bounds__(256) void linear_dw_zs_kernel(const float* __restrict__ g, const int* __restrict__ meta,
+                                                           int64_t mstride, const uint32_t* __restrict__ vals,
+                                                           int64_t cap, int rows, int M, int64_t K,
+                                                           float* __restrict__ dW, int64_t ldw,
+                                                           float* __restrict__ db, float scale, int acc,
+                                                           float upd_lr) {
+  __shared__ int pre[2][2][64];   // [buffer][page of the span][word]: value offset of the word
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (db && blockIdx.x == 0 && tid < NN) {
+    float t = 0.f;
+    for (int m = 0; m < M; ++m) t += g[m * NN + tid];
+    db[tid] = acc ? db[tid] + scale * t : scale * t;
+  }
+  const int64_t nblk = (K + ZD_COLS - 1) / ZD_COLS;
+  for (int64_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    const int64_t c0 = blk * ZD_COLS, col = c0 + 4 * tid;
+    const bool cv = col < K;
+    float4 s[NN];
+#pragma unroll
+    for (int n = 0; n < NN; ++n) s[n] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int m = 0; m < M; ++m) {
+      const int r = m / rows, b = m - r * rows;
+      const int* mr = meta + r * mstride;
+      const int64_t e0 = (int64_t)b * K + c0, pg0 = e0 / ZS_PAGE;
+      const int buf = m & 1;
+      if (wv < 2) {  // wave w: page pg0 + w of the span (beyond the rank's pages: never read)
+        const int64_t pg = pg0 + wv;
+        const int64_t npg = ((int64_t)rows * K + ZS_PAGE - 1) / ZS_PAGE;
+        int cnt = 0, off = 0;
+        if (pg < npg) {
+          cnt = __builtin_popcount((uint32_t)mr[pg * ZS_META + 1 + lane]);
+          off = mr[pg * ZS_META];
+        }
+        int incl = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const int o = __shfl_up(incl, d, 64);
+          if (lane >= d) incl += o;
+        }
+        pre[buf][wv][lane] = off + incl - cnt;
+      }
+      __syncthreads();  // (double-buffered: the next row's prefixes go to the other buffer)
+      float4 xv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (cv) {
+        const int64_t e = (int64_t)b * K + col;
+        const int64_t pg = e / ZS_PAGE;
+        const int pos = (int)(e - pg * ZS_PAGE), wj = pos >> 5, bit = pos & 31;
+        const uint32_t w = (uint32_t)mr[pg * ZS_META + 1 + wj];
+        const uint32_t m4 = (w >> bit) & 0xFu;
+        if (m4) {
+          int64_t o = (int64_t)pre[buf][(int)(pg - pg0)][wj] + __builtin_popcount(w & ((1u << bit) - 1u));
+          const uint32_t* vr = vals + r * cap;
+          float x4[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            x4[k] = 0.f;
+            if ((m4 >> k) & 1u) x4[k] = __uint_as_float(vr[o++]);
+          }
+          xv = make_float4(x4[0], x4[1], x4[2], x4[3]);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < NN; ++n) {
+        const float gv = g[m * NN + n];
+        s[n].x = fmaf(gv, xv.x, s[n].x);
+        s[n].y = fmaf(gv, xv.y, s[n].y);
+        s[n].z = fmaf(gv, xv.z, s[n].z);
+        s[n].w = fmaf(gv, xv.w, s[n].w);
+      }
+    }
+    if (cv) {
+#pragma unroll
+      for (int n = 0; n < NN; ++n) {
+        float4* ptr = reinterpret_cast<float4*>(dW + (int64_t)n * ldw + col);
+        const float4 v = make_float4(scale * s[n].x, scale * s[n].y, scale * s[n].z, scale * s[n].w);
+        if (upd_lr != 0.f) {
+          const float4 w0 = *ptr;
+          *ptr = make_float4(w0.x - upd_lr * v.x, w0.y - upd_lr * v.y, w0.z - upd_lr * v.z, w0.w - upd_lr * v.w);
+        } else if (acc) {
+          const float4 w0 = *ptr;
+          *ptr = make_float4(w0.x + v.x, w0.y + v.y, w0.z + v.z, w0.w + v.w);
+        } else {
+          *ptr = v;
+        }
+      }
+    }
+    __syncthreads();  // the prefix buffers are rewritten by the next block's first rows
+  }
+}
+
 }  // namespace tds
 
 using namespace tds;
+
+int tds_linear_dw_zs(const float* dy, const int* meta, int64_t mstride, const float* vals, int64_t cap, int rows,
+                     int M, int N, int64_t K, float* dW, int64_t ldw, float* db, float scale, int acc, float upd_lr,
+                     hipStream_t st) {
+  if (M < 1 || rows < 1 || M % rows || K % 4 || ldw % 4 || ((uintptr_t)dW & 15) || (N != 10 && N != 16)) return -1;
+  int64_t grid = (K + ZD_COLS - 1) / ZD_COLS;
+  if (grid > 8192) grid = 8192;
+  const uint32_t* v = reinterpret_cast<const uint32_t*>(vals);
+  if (N == 10)
+    hipLaunchKernelGGL(linear_dw_zs_kernel<10>, dim3((unsigned)grid), dim3(256), 0, st, dy, meta, mstride, v, cap, rows,
+                       M, K, dW, ldw, db, scale, acc, upd_lr);
+  else
+    hipLaunchKernelGGL(linear_dw_zs_kernel<16>, dim3((unsigned)grid), dim3(256), 0, st, dy, meta, mstride, v, cap, rows,
+                       M, K, dW, ldw, db, scale, acc, upd_lr);
+  TDS_LAUNCH_CHECK();
+  return 0;
+}
 
 void tds_zs_seg_encode(const float* x, const int64_t* pg_start, const int* pg_cnt, const int* pg_seg, int64_t npages,
                        const int* seg_first, const int* seg_npg, int nseg, int* meta, int* counts, float* vals,
@@ -357,12 +513,13 @@ bool zs_lookback(int64_t P, hipStream_t st, unsigned long long*& status, unsigne
 void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t cap, int64_t* nnz, hipStream_t st) {
   const int64_t P = tds_zs_npages(n);
   unsigned long long *status = nullptr, *ticket = nullptr, epoch = 0;
-  if (!zs_lookback(P, st, status, ticket, epoch)) {
+  if (!zs_lookback((P + ZS_TILE - 1) / ZS_TILE, st, status, ticket, epoch)) {
     tds_launch_fail("zs_encode: look-back state allocation failed");
     return;
   }
-  hipLaunchKernelGGL(zs_encode_kernel, dim3((unsigned)P), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(x), n,
-                     meta, reinterpret_cast<uint32_t*>(vals), cap, nnz, status, ticket, epoch);
+  const int64_t tiles = (P + ZS_TILE - 1) / ZS_TILE;
+  hipLaunchKernelGGL(zs_encode_kernel, dim3((unsigned)tiles), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(x), n,
+                     P, meta, reinterpret_cast<uint32_t*>(vals), cap, nnz, status, ticket, epoch);
   TDS_LAUNCH_CHECK();
 }
 

@@ -435,8 +435,8 @@ class ActivationExchange:
         self._cap = min(n, -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND)
         self.x_ratio = (mx + (z["M"] + 2) * 1.0) / n  # bytes relative to dense (4-byte words both)
         rows, in_f = z["rows"], z["in_f"]
-        self._x_buf = torch.empty((W * rows, in_f), device=z["meta"].device, dtype=torch.float32)
         if mx > cap:  # a count above this step's capacity: the dense rows, once
+            self._x_buf = torch.empty((W * rows, in_f), device=z["meta"].device, dtype=torch.float32)
             self.zs_stats["overflows"] += 1
             z["w_vals"].wait()
             self._x_work = tdist.all_gather_into_tensor(self._x_buf, self._x_local, group=self.group, async_op=True)
@@ -480,7 +480,26 @@ class ActivationExchange:
         if z is None:
             return
         self._zs_decode_pending = None
+        if self._x_buf is None:
+            self._x_buf = torch.empty((self.world * z["rows"], z["in_f"]), device=z["meta"].device, dtype=torch.float32)
         self._zs_decode_into(z, self._x_buf)
+
+    @staticmethod
+    def _zs_fused(z) -> bool:
+        """The gathered activation rows can feed the dW formation encoded (``linear_dw_zs``:
+        decoded in registers, no dense rows written and read back)."""
+        return z is not None and z.get("kind") != "sharded" and z["meta"].is_cuda
+
+    def _dw_zs(self, z, dy_all, dw, db, scale: float, acc: bool, lr: float = 0.0):
+        """dW (=/+=) scale·dy_allᵀX (or the update-only W -= lr·scale·dy_allᵀX) straight from the
+        all-gathered encodings, on the current stream after both gathers."""
+        from .. import _ext
+
+        z["w_meta"].wait()
+        z["w_vals"].wait()
+        W, M, cap = self.world, z["M"], z["cap"]
+        _ext.ops().linear_dw_zs(dy_all, z["meta_all"].view(W, M + 2), z["vals_all"].view(W, cap), z["rows"], dw, db,
+                                scale, acc, lr)
 
     def _zs_decode_into(self, z, x_buf):
         from . import zs
@@ -537,7 +556,8 @@ class ActivationExchange:
                 keep = keep + (z["meta_all"], z["vals_all"], z["meta"], z["vals"])
         with torch.cuda.stream(side):
             for t in keep:
-                t.record_stream(side)
+                if t is not None:
+                    t.record_stream(side)
             self._finish()
         if join:
             torch.autograd.Variable._execution_engine.queue_callback(
@@ -585,6 +605,8 @@ class ActivationExchange:
             ev_dy.record(side)
         z = getattr(self, "_zs_decode_pending", None)
         self._zs_decode_pending = None
+        if z is not None and not self._zs_fused(z):
+            self._x_buf = torch.empty((self.world * rows, z["in_f"]), device=dev, dtype=torch.float32)
         x_buf, x_work = self._x_buf, self._x_work
         keep = (self._x_local,)  # the local rows stay alive until the gathers reading them are done
         weight, lr = self.weight, float(lr)
@@ -593,11 +615,14 @@ class ActivationExchange:
             from .. import _ext
 
             torch.cuda.current_stream(dev).wait_event(ev_dy)
-            if z is not None:
-                self._zs_decode_into(z, x_buf)
-            else:
-                x_work.wait()
             with torch.no_grad():
+                if self._zs_fused(z):
+                    self._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
+                    return
+                if z is not None:
+                    self._zs_decode_into(z, x_buf)
+                else:
+                    x_work.wait()
                 _ext.ops().linear_dw(dy_all, x_buf, weight.data, None, scale, False, lr)
             assert keep
 
@@ -629,10 +654,15 @@ class ActivationExchange:
         rows = dy.shape[0]
         dy_all = torch.empty((self.world * rows, dy.shape[1]), device=dy.device, dtype=dy.dtype)
         tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
-        if getattr(self, "_zs_decode_pending", None) is not None:
-            self._zs_decode()
+        zf = getattr(self, "_zs_decode_pending", None)
+        if self.active == "activations" and self._zs_fused(zf):
+            self._zs_decode_pending = None  # formed from the encodings below (_dw_zs)
         else:
-            self._x_work.wait()
+            zf = None
+            if getattr(self, "_zs_decode_pending", None) is not None:
+                self._zs_decode()
+            else:
+                self._x_work.wait()
         scale = 1.0 / self.world
         from ..ops import fused_update
 
@@ -642,13 +672,20 @@ class ActivationExchange:
         lr = fused_update.take(self.weight, exchanged=True) if dy.is_cuda else None
         if lr:
             with torch.no_grad():
-                self._finish_update(dy_all, rows, scale, float(lr))
+                self._finish_update(dy_all, rows, scale, float(lr), zf)
             fused_update.applied(self.weight)
             self._done()
             return
         with torch.no_grad():
             (dw, acc_w), (db, acc_b) = self._targets()
-            if self.active == "activations":
+            if zf is not None:
+                if db is not None and acc_b != acc_w:
+                    s_b = dy_all.sum(0).mul_(scale)
+                    db.add_(s_b) if acc_b else db.copy_(s_b)
+                    self._dw_zs(zf, dy_all, dw, None, scale, acc_w)
+                else:
+                    self._dw_zs(zf, dy_all, dw, db, scale, acc_w)
+            elif self.active == "activations":
                 _dw_rows(dy_all, self._x_buf, dw, db, scale, acc_w, acc_b)
             else:
                 bounds = shard_bounds(dw.shape[1], self.world)
@@ -676,7 +713,7 @@ class ActivationExchange:
         self.active = None
         self.steps_exchanged += 1
 
-    def _finish_update(self, dy_all, rows: int, scale: float, lr: float):
+    def _finish_update(self, dy_all, rows: int, scale: float, lr: float, zf=None):
         """Update-only finish: W -= lr * scale * dy_allᵀ X (activations: every column here;
         sharded: this rank's column shard, then an all-gather of the UPDATED shards straight
         into W); the bias keeps its gradient path (tiny, stepped by the optimizer)."""
@@ -686,7 +723,9 @@ class ActivationExchange:
         (_, _), (db, acc_b) = self._targets()
         W = self.weight.data
         ops = _ext.ops()
-        if self.active == "activations":
+        if self.active == "activations" and zf is not None:
+            self._dw_zs(zf, dy_all, W, db, scale, acc_b, lr)
+        elif self.active == "activations":
             ops.linear_dw(dy_all, self._x_buf, W, db, scale, acc_b, lr)
         else:
             bounds = shard_bounds(W.shape[1], self.world)
