@@ -501,7 +501,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
                 tds._ext.ops().comm_spin(out, args.sim_comm_us, args.sim_comm_ctas, 19744)
         loss = criterion(out, lab_pool[j])
         optimizer.zero_grad()
-        loss.backward()
+        TF.backward(loss)
         optimizer.step()
         if data_stream is not None:
             convnet_fused._before_conv2_backward.clear()  # (a plan without the hook)

@@ -129,6 +129,31 @@ def test_cross_entropy(gpu):
     _close(dz2, zr2.grad, 1e-6, 1e-6)
 
 
+def test_cross_entropy_backward_seeds(gpu):
+    """TF.backward(loss) (cached unit seed, no scale kernel) == loss.backward() == 2x for a 2 seed."""
+    from torch_distributed_sandbox_amd.ops import functional as TF
+
+    torch.manual_seed(0)
+    z0 = torch.randn(5, 10, device=gpu) * 3
+    lab = torch.tensor([1, 0, 9, 2, 4], device=gpu)
+    grads = []
+    for how in ("unit", "plain", "two"):
+        z = z0.clone().requires_grad_(True)
+        loss = TF.cross_entropy(z, lab)
+        if how == "unit":
+            TF.backward(loss)
+        elif how == "plain":
+            loss.backward()
+        else:
+            loss.backward(torch.full((), 2.0, device=gpu))
+        grads.append(z.grad)
+    assert torch.equal(grads[0], grads[1])
+    assert torch.equal(grads[2], 2 * grads[1])
+    zr = z0.double().cpu().requires_grad_(True)
+    F.cross_entropy(zr, lab.cpu()).backward()
+    _close(grads[0], zr.grad, 1e-6, 1e-6)
+
+
 def test_sgd(gpu):
     ps = [torch.randn(n, device=gpu) for n in (7, 1000, 33)]
     gs = [torch.randn_like(p) for p in ps]

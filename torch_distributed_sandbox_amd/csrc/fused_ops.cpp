@@ -67,28 +67,59 @@ int l1_wg() { return tds_fused_num_wg(TDS_L1_PER_CU); }
 
 // Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
 // torch caching allocator, built once.  The map is never destroyed (no frees at process exit).
-const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg) {
+// TDS_TILE_LISTS=0 keeps the work-index-major layout (A/B only): *sw / *sk are the strides of
+// (workgroup, k-th tile of that workgroup) in the device table either way.
+bool tile_lists() {
+  static const bool on = [] {
+    const char* e = std::getenv("TDS_TILE_LISTS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg, int* sw, int* sk) {
   static std::mutex mu;
   static auto* cache = new std::map<std::tuple<int, int, int, int, int>, Tensor>();
   // 16-row groups for both conv2 kernels: for the backward's 256 workgroups (32 per XCD
   // round) 4 / 8 / 16 / 32 rows measured 1.585 / 1.603 / 1.572 / 1.564 ms -- within noise
   const int gr = 16;
-  (void)nwg;  const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c, gr);
+  const bool lists = tile_lists();
+  const int64_t total = (int64_t)B * tiles_r * tiles_c;
+  const int64_t rows = (total + nwg - 1) / nwg;
+  *sw = lists ? (int)rows : 1;
+  *sk = lists ? 1 : nwg;
+  const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c, nwg);
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache->find(key);
   if (it != cache->end()) return it->second.data_ptr<int>();
-  auto host = at::empty({(int64_t)B * tiles_r * tiles_c}, at::TensorOptions().dtype(at::kInt));
+  auto host = at::empty({total}, at::TensorOptions().dtype(at::kInt));
   const int rc = tds_tile_order_fill(host.data_ptr<int>(), B, tiles_r, tiles_c, gr);
   TORCH_CHECK(rc == 0, "tdsa fused: tile order table needs B <= 255 and <= 4095 tiles per side (B=", B,
               ", tiles ", tiles_r, " x ", tiles_c, ")");
-  Tensor dev = host.to(like.device());
+  // on the device as per-workgroup lists: work index t = w + kk * nwg at [w][kk] (rows =
+  // ceil(total / nwg), the tail padded with the list's last entry), so one workgroup's
+  // consecutive tiles share a scalar-cache line (16 entries) instead of one line each
+  Tensor dev;
+  if (lists) {
+    auto l = at::empty({(int64_t)nwg, rows}, at::TensorOptions().dtype(at::kInt));
+    const int* src = host.data_ptr<int>();
+    int* dst = l.data_ptr<int>();
+    for (int64_t w = 0; w < nwg; ++w)
+      for (int64_t k = 0; k < rows; ++k) dst[w * rows + k] = src[std::min(w + k * nwg, total - 1)];
+    dev = l.to(like.device());
+  } else {
+    dev = host.to(like.device());
+  }
   (*cache)[key] = dev;
   return dev.data_ptr<int>();
 }
 
 // Device copy of the rolling conv2 backward's walk table (tds_conv2_bwd_walk) per (device,
 // shape, workgroups), from the torch caching allocator, built once.
-const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg) {
+// On the device the table is stored per workgroup ([nwg][rows], rows returned): one
+// workgroup's consecutive tiles then share a scalar-cache line (16 entries) -- the host layout
+// [rows][nwg] put each tile's entry on a line of its own, a scalar miss per tile in every wave.
+const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg, int* sw, int* sk) {
   static std::mutex mu;
   static auto* cache = new std::map<std::tuple<int, int, int, int, int>, Tensor>();
 #ifndef TDS_BWD_SEG
@@ -97,14 +128,21 @@ const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg
   constexpr int kSeg = TDS_BWD_SEG;  // tiles per vertical segment (a segment start re-stages 4 rows)
   const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c, nwg);
   std::lock_guard<std::mutex> lock(mu);
+  const bool lists = tile_lists();
   auto it = cache->find(key);
-  if (it != cache->end()) return it->second.data_ptr<int>();
+  if (it != cache->end()) {
+    *sw = lists ? (int)(it->second.numel() / nwg) : 1;
+    *sk = lists ? 1 : nwg;
+    return it->second.data_ptr<int>();
+  }
   const int64_t n = tds_conv2_bwd_walk(nullptr, B, tiles_r, tiles_c, nwg, kSeg);
   TORCH_CHECK(n > 0, "tdsa fused: conv2 backward walk needs B <= 63 and <= 4095 tiles per side (B=", B, ", tiles ",
               tiles_r, " x ", tiles_c, ")");
-  auto host = at::empty({n}, at::TensorOptions().dtype(at::kInt));
+  auto host = at::empty({n / nwg, (int64_t)nwg}, at::TensorOptions().dtype(at::kInt));
   tds_conv2_bwd_walk(host.data_ptr<int>(), B, tiles_r, tiles_c, nwg, kSeg);
-  Tensor dev = host.to(like.device());
+  *sw = lists ? (int)(n / nwg) : 1;
+  *sk = lists ? 1 : nwg;
+  Tensor dev = (lists ? host.t().contiguous() : host).to(like.device());
   (*cache)[key] = dev;
   return dev.data_ptr<int>();
 }
@@ -238,14 +276,15 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const T
   const int nwg = tds_conv2_fwd2_num_wg();
   int tr = 0, tc = 0;
   tds_conv2_fwd2_tiles((int)P, &tr, &tc);
-  const int* order = tile_order(p1, (int)B, tr, tc, nwg);
+  int sw = 0, sk = 0;
+  const int* order = tile_order(p1, (int)B, tr, tc, nwg, &sw, &sk);
   auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kFloat));
   auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
   tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr<float>(),
                  ya.data_ptr<float>(), partial.data_ptr<double>(),
                  opt_mag(mag, kMagParts + 32 * mag_ypart_count()) ? opt_mag(mag) + kMagParts : nullptr, order, nwg,
-                 (int)B, (int)P, stream_of(p1));
+                 sw, sk, (int)B, (int)P, stream_of(p1));
   check_launches("fused_conv2_forward");
   return {y2, partial, ya};
 }
@@ -436,14 +475,15 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   const int nwg = tds_conv2_bwd3_num_wg();
   int tr = 0, tc = 0;
   tds_conv2_bwd3_tiles((int)P, &tr, &tc);
-  const int* order = bwd_walk(p1, (int)B, tr, tc, nwg);
+  int sw = 0, sk = 0;
+  const int* order = bwd_walk(p1, (int)B, tr, tc, nwg, &sw, &sk);
   auto dp1 = at::empty({B, P, P, 16}, p1.options().dtype(at::kFloat));
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options().dtype(at::kFloat));
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
   tds_conv2_bwd3(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
                  reinterpret_cast<const uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(), wd.data_ptr<int16_t>(),
-                 dp1.data_ptr<float>(), slab.data_ptr<float>(), order, nwg, (int)B, (int)P, st);
+                 dp1.data_ptr<float>(), slab.data_ptr<float>(), order, nwg, sw, sk, (int)B, (int)P, st);
   tds_conv2_wgrad_reduce(slab.data_ptr<float>(), nwg, dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, st);
   check_launches("fused_conv2_backward_y2");
   return {dp1, dw2, db2};

@@ -81,11 +81,14 @@ struct BRTile {
   int b, r0, c0;
   bool start, end;
 };
-__device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k, int nwg, int w) {
+__device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k, int sk, int w) {
   // 32-bit index (the table is far below 2^31 entries): with a 64-bit one the compiler keeps
   // copies of the wgrad accumulators across the tile loop and spills them (256 VGPRs + scratch
-  // against 189)
-  const uint32_t v = (uint32_t)walk[k * nwg + w];
+  // against 189).  walk is already offset to this workgroup's list (w * sw); the device table is
+  // per workgroup ([nwg][rows], fused_ops.cpp bwd_walk, sk = 1): 16 consecutive tiles per
+  // scalar-cache line.
+  (void)w;
+  const uint32_t v = (uint32_t)walk[k * sk];
   BRTile x;
   x.start = (v & kWalkStart) != 0;
   x.end = (v & kWalkEnd) != 0;
@@ -102,7 +105,7 @@ struct BRArgs {
   float* __restrict__ dp1;
   float* __restrict__ slab;
   const int* __restrict__ walk;
-  int B, P, Q, nwg, w;
+  int B, P, Q, sk, w;
 };
 
 // ---------------------------------------------------------------------------- dgrad
@@ -340,7 +343,7 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
   clk.start();
   int kk = 0;
   for (;; ++kk) {
-    const BRTile cur = br_decode(a.walk, kk, a.nwg, a.w);
+    const BRTile cur = br_decode(a.walk, kk, a.sk, a.w);
     if (cur.end) break;
     clk.barrier();  // tile kk staged; the partner's exchange slot of tile kk-1 is written
     const BRRows rw = br_rows(smem, kk);
@@ -383,7 +386,7 @@ constexpr uint32_t kBROob = 0xFFFFFFF0u;
 // window, 4-channel chunk): NR/2 x 10 windows x 8 chunks.  BIG: the 32 g2m planes of an image
 // exceed a 4 GiB buffer-descriptor range (64-bit g2m loads); a template parameter, because two
 // load paths under a runtime branch make the compiler wait vmcnt(0) at their merge.
-template <int NR, int WV, bool BIG, int DIAG>
+template <int NR, bool BIG, int DIAG>
 struct BRStager {
   static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
   static constexpr int ITEMS = NWIN * 8;
@@ -589,10 +592,13 @@ struct BRStager {
   }
 };
 
-template <int WV, int DIAG, bool BIG>  // staging wave WV (0..3) = workgroup wave 4 + WV
+// One code copy for all four staging waves (workgroup waves 4-7; a wave's share of the work
+// comes from threadIdx).  Instantiated per wave, the four identical copies (~36 KB each) made the
+// kernel 168 KB of code, far beyond the instruction cache its CU shares.
+template <int DIAG, bool BIG>
 __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   if constexpr (DIAG == 5) {  // timing only: no staging at all (consumers read stale LDS)
-    for (int k = 0; !br_decode(a.walk, k, a.nwg, a.w).end; ++k) br_barrier();
+    for (int k = 0; !br_decode(a.walk, k, a.sk, a.w).end; ++k) br_barrier();
     br_barrier();
     return;
   }
@@ -603,25 +609,25 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   auto ptop = [&](int j) { return smem + BR_OFF_P + (j % 3) * BR_SLOT * BR_PROW; };
   // tile j's new rows, its last 4 mirrored into tile j+1's top (overwritten by a prologue when
   // tile j+1 starts a segment: a later iteration, past a barrier)
-  auto stage = [&](BRStager<8, WV, BIG, DIAG>& s, int j, const BRTile& x) {
+  auto stage = [&](BRStager<8, BIG, DIAG>& s, int j, const BRTile& x) {
     s.template store<true>(a, x.r0 + 2, x.c0, tid, dtop(j) + 4 * BR_DROW, ptop(j) + 4 * BR_PROW, kc, dtop(j + 1),
                            ptop(j + 1));
   };
   // a segment's first tile: its 4 top rows (image rows r0-2 .. r0+1) staged synchronously
   // straight into its slot's top (once per ~48 tiles)
   auto prologue = [&](int j, const BRTile& x) {
-    BRStager<4, WV, BIG, DIAG> pro;
+    BRStager<4, BIG, DIAG> pro;
     pro.load(a, x.b, x.r0 - 2, x.c0, tid);
     pro.template store<false>(a, x.r0 - 2, x.c0, tid, dtop(j), ptop(j), kc, nullptr, nullptr);
   };
   // two register sets: tile j's new-row loads are issued two tiles before they are staged.
   // Loads are unconditional (past the end: the list's last tile again, never staged): a load
   // under a branch makes the wait for the OLDER set drain the younger one too (vmcnt(0)).
-  BRStager<8, WV, BIG, DIAG> st0, st1;
+  BRStager<8, BIG, DIAG> st0, st1;
   BRClock<DIAG> clk;
   clk.start();
-  auto tile = [&](int j) { return br_decode(a.walk, j, a.nwg, a.w); };
-  auto ld = [&](BRStager<8, WV, BIG, DIAG>& s, int j) {
+  auto tile = [&](int j) { return br_decode(a.walk, j, a.sk, a.w); };
+  auto ld = [&](BRStager<8, BIG, DIAG>& s, int j) {
     const BRTile x = tile(j);
     // the look-ahead loads issue at raised priority (the SIMD's MFMA wave otherwise delays
     // them), the BN2-backward VALU work at the lowest (tools/gpu_sessions/r2_knobs.sh: 1.519 /
@@ -673,15 +679,16 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
     const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
     const float* __restrict__ kbuf, const uint32_t* __restrict__ mag, const uint4* __restrict__ p1,
     const uint4* __restrict__ wdpack, float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ walk,
-    int B, int P) {
+    int sw, int sk, int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   BRArgs a;
   a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.walk = walk;
   a.B = B; a.P = P; a.Q = P / 2;
-  a.nwg = gridDim.x;
+  a.sk = sk;
   a.w = xcd_remap(blockIdx.x, gridDim.x);  // this workgroup's list (XCD-contiguous: neighbouring columns)
+  a.walk = walk + a.w * sw;
   float* kc = reinterpret_cast<float*>(smem + BR_OFF_K);
   if (tid < 64) {
     // the dy2 scale 2^e (header): wave 0, lane c < 32 bounds channel c; k1..k3 are scaled in
@@ -712,10 +719,7 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
     case 1: br_mfma<1, DIAG>(a, wdpack, smem); break;
     case 2: br_mfma<2, DIAG>(a, wdpack, smem); break;
     case 3: br_mfma<3, DIAG>(a, wdpack, smem); break;
-    case 4: br_stage<0, DIAG, BIG>(a, smem); break;
-    case 5: br_stage<1, DIAG, BIG>(a, smem); break;
-    case 6: br_stage<2, DIAG, BIG>(a, smem); break;
-    default: br_stage<3, DIAG, BIG>(a, smem); break;
+    default: br_stage<DIAG, BIG>(a, smem); break;  // waves 4-7
   }
 }
 
@@ -820,10 +824,11 @@ static int br_diag_env() {
 static int br_diag_env() { return 0; }
 #endif
 
-// g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups
+// g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
+// [nwg][rows] (fused_ops.cpp bwd_walk)
 void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const uint32_t* mag,
-                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P,
-                    hipStream_t st) {
+                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int sw, int sk,
+                    int B, int P, hipStream_t st) {
   const int Q = P / 2;
   const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
 #define TDS_BR_LAUNCH_B(D, BG)                                                                                         \
@@ -836,7 +841,7 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
     }                                                                                                                  \
     hipLaunchKernelGGL((conv2_bwd_roll_kernel<D, BG>), dim3(nwg), dim3(BR_THREADS), BR_LDS, st,                        \
                        reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, mag, reinterpret_cast<const uint4*>(p1),  \
-                       reinterpret_cast<const uint4*>(wd), dp1, slab, walk, B, P);                                      \
+                       reinterpret_cast<const uint4*>(wd), dp1, slab, walk, sw, sk, B, P);                                      \
     TDS_LAUNCH_CHECK();                                                                                                \
   }
 #define TDS_BR_LAUNCH(D)           \

@@ -213,16 +213,20 @@ template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
                                        const float* __restrict__ bias, const float* __restrict__ gamma,
                                        float* __restrict__ y2, float* __restrict__ ya, double* __restrict__ partial,
-                                       uint32_t* __restrict__ ypart, const int* __restrict__ order, int B, int P,
-                                       char* smem) {
+                                       uint32_t* __restrict__ ypart, const int* __restrict__ order, int sw, int sk,
+                                       int B, int P, char* smem) {
   constexpr int NT = WV & 1, RH = WV >> 1;
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int tiles_c = (P + F2_TC - 1) / F2_TC, tiles_r = (P + F2_TH - 1) / F2_TH;
   const int per_img = tiles_c * tiles_r, total = per_img * B;
-  auto decode = [&](int t) {
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  // work index t = w + kk * grid at mine[kk * sk]: the table is per workgroup (fused_ops.cpp
+  // tile_order, sw = ceil(total / grid), sk = 1), so consecutive tiles share a scalar-cache line
+  const int* __restrict__ mine = order + w * sw;
+  auto decode = [&](int kk) {
     F2Tile x;
     int tr, tc;
-    tile_from_order(order, t, x.b, tr, tc);
+    tile_from_order(mine, kk * sk, x.b, tr, tc);
     x.r0 = tr * F2_TH;
     x.c0 = tc * F2_TC;
     return x;
@@ -242,15 +246,15 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   f32x4 acc[4];
   F2Tile prev{0, 0, 0};
   bool have_prev = false;
-  int t = xcd_remap(blockIdx.x, gridDim.x);
-  if (t < total) f2_dma<DIAG, WV>(p1, decode(t), P, smem, lane);
+  int t = w;
+  if (t < total) f2_dma<DIAG, WV>(p1, decode(0), P, smem, lane);
   int kk = 0;
   for (; t < total; t += gridDim.x, ++kk) {
-    const F2Tile cur = decode(t);
+    const F2Tile cur = decode(kk);
     // tile t's DMA landed (vmcnt(0) + barrier); p1 buffer (kk+1)&1 is free; the staged
     // tile t-1 (stage (kk+1)&1) is complete
     __syncthreads();
-    if (t + (int)gridDim.x < total) f2_dma<DIAG, WV>(p1, decode(t + gridDim.x), P, smem + ((kk + 1) & 1) * F2_PBUF, lane);
+    if (t + (int)gridDim.x < total) f2_dma<DIAG, WV>(p1, decode(kk + 1), P, smem + ((kk + 1) & 1) * F2_PBUF, lane);
     if (have_prev) {
       f2_store<DIAG>(smem + F2_OFF_S + ((kk + 1) & 1) * F2_STAGE, prev, y2, P);
       f2_store_ya(ys + ((kk + 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
@@ -302,13 +306,14 @@ __global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* 
                                                                    float* __restrict__ y2, float* __restrict__ ya,
                                                                    double* __restrict__ partial,
                                                                    uint32_t* __restrict__ ypart,
-                                                                   const int* __restrict__ order, int B, int P) {
+                                                                   const int* __restrict__ order, int sw, int sk,
+                                                                   int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
-  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
-  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
-  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
-  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, B, P, smem);
+  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
+  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
+  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
+  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
 }
 
 }  // namespace tds
@@ -334,9 +339,10 @@ static int f2_diag_env() {
 static int f2_diag_env() { return 0; }
 #endif
 
-// order: the blocked tile order table (tds_tile_order_fill), allocated by the caller
+// order: the blocked tile order table (tds_tile_order_fill) as per-workgroup lists [nwg][ceil(total / nwg)]
+// (fused_ops.cpp tile_order, sw / sk: the strides of workgroup / tile), allocated by the caller
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, uint32_t* ypart, const int* order, int nwg, int B, int P, hipStream_t st) {
+                    double* partial, uint32_t* ypart, const int* order, int nwg, int sw, int sk, int B, int P, hipStream_t st) {
   const dim3 grid(nwg), block(F2_THREADS);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wp);
@@ -354,12 +360,12 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const fl
   }
   switch (f2_diag_env()) {
 #ifdef TDS_DIAG
-    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
-    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
-    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
-    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
 #endif
-    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, B, P); break;
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
   }
   TDS_LAUNCH_CHECK();
 }

@@ -82,14 +82,14 @@ void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
 // y2 [B,P,P,32]; ya pooled-blocked (pooled_layout.h), max/min of each 2x2 window by sign(gamma2)
 // ypart (optional): max |y2| per (channel, workgroup), [32][nwg] float bits
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, uint32_t* ypart, const int* order, int nwg, int B, int P, hipStream_t st);
+                    double* partial, uint32_t* ypart, const int* order, int nwg, int sw, int sk, int B, int P, hipStream_t st);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups
 // mag: the forward's / head backward's magnitude bounds (the fp16 scale of dy2)
 void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const uint32_t* mag,
-                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int B, int P,
-                    hipStream_t st);
+                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int sw, int sk,
+                    int B, int P, hipStream_t st);
 // host: per-workgroup tile lists of vertical segments of ~seg tiles; out == nullptr -> length
 int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, int seg);
 

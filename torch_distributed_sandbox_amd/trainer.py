@@ -23,6 +23,7 @@ from . import _ext
 from .data import DeviceUpsampleLoader, SyntheticMNIST
 from .models import ConvNet
 from .ops import CrossEntropyLoss, SGD
+from .ops import functional as TF
 from .parallel import DistributedDataParallel, DistributedSampler
 from .parallel import distributed as tdist
 from .utils import checkpoint, fault
@@ -130,7 +131,7 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
                 loss = criterion(outputs, labels)
             optimizer.zero_grad()
             with timer.phase("backward"):
-                loss.backward()
+                TF.backward(loss)
             with timer.phase("optimizer"):
                 optimizer.step()
             if distributed:
