@@ -49,7 +49,19 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 # per-file device-compiler flags.  x_autocorr.hip: the SLP vectorizer pairs the 41 shift
 # accumulators into v_pk_fma_f32 whose misaligned operand pairs cost ~4 v_mov per FMA pair
 # (322 moves against 80 packed FMAs per row); scalar v_fmac needs none.
-HIP_FILE_FLAGS = {"x_autocorr.hip": ["-fno-slp-vectorize"]}
+# conv2_bwd.hip / conv2_fwd2.hip: packed f32 VALU (the vectorizer's v_pk_fma/add/mul_f32 in the
+# staging and epilogue math) costs more issue cycles than scalar ops beside the MFMAs of the
+# same SIMD; same-box A/B (tools/gpu_sessions/r3_s14.sh): conv2 backward 1.247 -> 1.109 ms,
+# forward 0.621 -> 0.588 ms, bench 3.327 -> 3.112 ms/step.  (convnet_fused.hip keeps it: its
+# layer-1 backward ran 0.31 -> 0.36 ms without.)
+HIP_FILE_FLAGS = {
+    "x_autocorr.hip": ["-fno-slp-vectorize"],
+    "conv2_bwd.hip": ["-fno-slp-vectorize"],
+    "conv2_fwd2.hip": ["-fno-slp-vectorize"],
+}
+# A/B builds: TDS_NOSLP_FILES=a.hip,b.hip adds -fno-slp-vectorize to those files as well
+for _f in filter(None, os.environ.get("TDS_NOSLP_FILES", "").split(",")):
+    HIP_FILE_FLAGS.setdefault(_f, []).append("-fno-slp-vectorize")
 
 
 def _torch_paths():

@@ -565,10 +565,28 @@ static_assert(4 * 16 * LB_NACC * 8 <= LB_NP * 64 + LB_NP * 16 + LB_XR * LM_XS * 
 //             + sum corners,  d = o_j - o_k  (see x_autocorr / x_border)
 //   S[j]    = sum of x over the pixels tap j sees (total - excluded lines + corners)
 // ac_sum: reduced autocorrelation [42] (slot 41 = plain sum).
+// The corner terms read x only inside the 6 x 6 pixel block at each image corner (excluded rows /
+// columns lie within 2 of the border, their partners within 4 more): those blocks are loaded into
+// LDS once, all loads in flight together (read one by one from global memory inside the loops
+// below, they made this one-workgroup kernel latency-bound: 19 us per step).  H, W >= 12.
+constexpr int L1G_MAXB = 32;
+struct L1Corners {
+  float v[L1G_MAXB][4][6][6];
+  __device__ float at(int b, int r, int c, int H, int W) const {
+    const int q = (r >= 6 ? 2 : 0) + (c >= 6 ? 1 : 0);
+    return v[b][q][r >= 6 ? r - (H - 6) : r][c >= 6 ? c - (W - 6) : c];
+  }
+};
+
 __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips_b,
                               const float* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
-                              double* full, double* strips) {
+                              double* full, double* strips, L1Corners& cx) {
   const int tid = threadIdx.x;
+  for (int e = tid; e < B * 144; e += blockDim.x) {
+    const int b = e / 144, q = (e / 36) % 4, i = (e / 6) % 6, j = e % 6;
+    const int r = q < 2 ? i : H - 6 + i, c = (q & 1) == 0 ? j : W - 6 + j;
+    cx.v[b][q][i][j] = x[(int64_t)b * H * W + (int64_t)r * W + c];
+  }
   // per-image border strips [B][8][82] -> batch sums, images in order
   for (int e = tid; e < 8 * 82; e += blockDim.x) {
     double v = 0.0;
@@ -606,10 +624,7 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
         for (int q = 0; q < nc; ++q) {
           const int r = er[i], cc = ec[q], r2 = r + dy, c2 = cc + dx;
           if (r2 < 0 || r2 >= H || c2 < 0 || c2 >= W) continue;
-          for (int b = 0; b < B; ++b) {
-            const float* xb = x + (int64_t)b * H * W;
-            v += (double)xb[(int64_t)r * W + cc] * xb[(int64_t)r2 * W + c2];
-          }
+          for (int b = 0; b < B; ++b) v += (double)cx.at(b, r, cc, H, W) * cx.at(b, r2, c2, H, W);
         }
       G[k][j] = v;
     } else {
@@ -618,7 +633,7 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
       for (int i = 0; i < nc; ++i) v -= strips[line_index_col(ec[i]) * 82 + 81];
       for (int i = 0; i < ne; ++i)
         for (int q = 0; q < nc; ++q)
-          for (int b = 0; b < B; ++b) v += x[(int64_t)b * H * W + (int64_t)er[i] * W + ec[q]];
+          for (int b = 0; b < B; ++b) v += cx.at(b, er[i], ec[q], H, W);
       S[j] = v;
     }
   }
@@ -644,7 +659,8 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
   __shared__ double S[25];
   __shared__ double Gw[16][25];
   __shared__ double strips_sum[8 * 82];
-  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum);
+  __shared__ L1Corners cx;
+  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, cx);
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {
@@ -716,6 +732,10 @@ void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int
                  double* gram, double* sums, const float* b1, float eps, float momentum, const float* gamma,
                  const float* beta, float* stats, float* running_mean, float* running_var, int64_t* num_batches,
                  float* aff, hipStream_t st) {
+  if (B > L1G_MAXB || H < 12 || W < 12) {
+    tds_launch_fail("l1_gram: needs batch <= 32 and H, W >= 12");
+    return;
+  }
   hipLaunchKernelGGL(l1_gram_kernel, dim3(1), dim3(256), 0, st, ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps,
                      momentum, gamma, beta, stats, running_mean, running_var, num_batches, aff);
   TDS_LAUNCH_CHECK();
