@@ -16,5 +16,6 @@ def _dump():
 
 atexit.register(_dump)
 here = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, here)
 sys.argv = [os.path.join(here, "bench.py")] + sys.argv[1:]
 runpy.run_path(sys.argv[0], run_name="__main__")

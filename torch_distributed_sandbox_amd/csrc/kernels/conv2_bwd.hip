@@ -564,8 +564,8 @@ struct BRStager {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         uint32_t h01, l01, h23, l23;  // (k1..k3 carry the scale 2^e: d is dy2 * 2^e)
-        split2_f16(d[q][0], d[q][1], h01, l01);
-        split2_f16(d[q][2], d[q][3], h23, l23);
+        split2_f16_mix(d[q][0], d[q][1], h01, l01);
+        split2_f16_mix(d[q][2], d[q][3], h23, l23);
         const int lr = 2 * wy + (q >> 1);
         const int ro = (2 * wx + (q & 1)) * 32 + (c4 & 3) * 8;
         char* rec = dbase + lr * BR_DROW + ro;
