@@ -412,10 +412,14 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
                                  comm_cus=reserve if backend == "rccl-native" else None)
     if backend == "rccl-native" and tdist.is_initialized():
         reserve = tdist.comm_cus()
+    own_split = False
+    if backend == "rccl-native" and tdist.is_initialized():
+        pass
     elif on_gpu and reserve:
         from torch_distributed_sandbox_amd.utils.streams import reserve_cus_for_comm
 
         torch.cuda.set_stream(reserve_cus_for_comm(reserve, device))
+        own_split = True
     reserve = reserve or 0
     rccl_max_ctas = int(os.environ.get("TDS_RCCL_MAX_CTAS", "0") or 0) if backend == "rccl-native" else 0
     rccl_ranks = None
@@ -534,6 +538,11 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
         tdist.all_reduce(t, tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss.item()) if loss is not None else None
+    if own_split:
+        # the masked streams end with the run, not at process exit (utils/streams.py)
+        from torch_distributed_sandbox_amd.utils.streams import release_streams
+
+        release_streams()
     phase[0] = f"attempt {k} ({backend}): report"
     probe = _allreduce_probe(tdist, device, world, on_gpu) if world > 1 and args.allreduce_probe else None
     ms = 1e3 * elapsed / max(1, args.steps)

@@ -325,3 +325,42 @@ def test_cu_reserve_and_masked_stream(gpu):
         if n.endswith("0.bias"):
             continue
         torch.testing.assert_close(q.grad, p.grad, rtol=1e-4, atol=1e-7, msg=n)
+
+
+_RELEASE_SCRIPT = r"""
+import torch
+from torch_distributed_sandbox_amd.models import ConvNet
+from torch_distributed_sandbox_amd.ops import CrossEntropyLoss
+from torch_distributed_sandbox_amd.utils.streams import (comm_stream, compute_cus, release_streams,
+                                                         reserve_cus_for_comm)
+dev = torch.device("cuda", 0)
+full = compute_cus()
+torch.manual_seed(0)
+m = ConvNet(image_shape=(64, 64), device=dev, mode="fused")
+x = torch.rand(2, 1, 64, 64, device=dev)
+y = torch.tensor([3, 5], device=dev)
+torch.cuda.set_stream(reserve_cus_for_comm(32, dev))
+assert comm_stream(dev) is not None and compute_cus() == full - 32
+CrossEntropyLoss()(m(x), y).backward()
+n = release_streams()
+assert n == 2, n  # the compute stream and the comm side
+assert compute_cus() == full and comm_stream(dev) is None
+assert torch.cuda.current_stream() == torch.cuda.default_stream()
+CrossEntropyLoss()(m(x), y).backward()  # the default stream works on
+torch.cuda.synchronize()
+print("release ok")
+"""
+
+
+def test_release_masked_streams(gpu):
+    """utils/streams.release_streams: the CU-masked streams are destroyed at the end of a run
+    (not left to process exit, where their teardown races rocprofv3's finalization); the
+    reserve returns to 0 and the default stream carries on.  In a child process: the streams
+    of this one stay untouched."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _RELEASE_SCRIPT], cwd=repo, capture_output=True, text=True,
+                       timeout=180)
+    assert r.returncode == 0 and "release ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]

@@ -505,6 +505,8 @@ int64_t cu_masked_stream(int64_t device, int64_t reserve, bool striped) {
 // the communication stream of the CU split (0 when no CUs are reserved)
 int64_t cu_comm_stream(int64_t device) { return (int64_t)reinterpret_cast<intptr_t>(tds_cu_comm_stream((int)device)); }
 
+int64_t cu_release_streams() { return tds_cu_release_streams(); }
+
 // a further stream on one side of the CU split (0 when no CUs are reserved)
 int64_t cu_side_stream(int64_t device, bool comm) {
   return (int64_t)reinterpret_cast<intptr_t>(tds_cu_side_stream((int)device, comm));
@@ -757,5 +759,6 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("comm_spin(Tensor like, int us, int nblocks, int lds_bytes) -> ()", &comm_spin);
   m.def("cu_probe(Tensor like, int us, int nblocks) -> Tensor", &cu_probe);
   m.def("cu_comm_stream(int device) -> int", &cu_comm_stream);
+  m.def("cu_release_streams() -> int", &cu_release_streams);
   m.def("cu_side_stream(int device, bool comm) -> int", &cu_side_stream);
 }

@@ -44,6 +44,16 @@ void tds_set_cu_reserve(int n) { g_reserve.store(n > 0 ? n : 0, std::memory_orde
 
 int tds_cu_reserve() { return g_reserve.load(std::memory_order_relaxed); }
 
+// Every CU-masked stream this file creates, for tds_cu_release_streams.
+static std::mutex g_masked_mu;
+static std::vector<hipStream_t> g_masked;
+static std::mutex g_comm_mu, g_side_mu;
+static std::vector<std::pair<std::pair<int, int>, hipStream_t>> g_comm_cache, g_side_cache;
+static void note_masked(hipStream_t s) {
+  std::lock_guard<std::mutex> g(g_masked_mu);
+  g_masked.push_back(s);
+}
+
 // A stream of `device` whose kernels may use every CU but `reserve` of them, reserve/8 per XCD
 // (hipExtStreamCreateWithCUMask).  Two numberings of the mask bits are possible: `striped`
 // (bit c -> XCD c % 8, the order the dispatcher deals workgroups round-robin to the XCDs) and
@@ -69,7 +79,10 @@ hipStream_t tds_cu_masked_stream(int device, int reserve, bool striped) {
     }
   }
   (void)hipSetDevice(prev);
-  if (s) g_striped.store(striped, std::memory_order_relaxed);
+  if (s) {
+    g_striped.store(striped, std::memory_order_relaxed);
+    note_masked(s);
+  }
   return s;
 }
 
@@ -83,9 +96,8 @@ hipStream_t tds_cu_comm_stream(int device) {
   const bool striped = g_striped.load(std::memory_order_relaxed);
   if (reserve <= 0 || reserve % 8 != 0 || device < 0 || device >= kMaxDev) return nullptr;
   const int key = reserve * 2 + (striped ? 1 : 0);
-  static std::mutex mu;
-  static std::vector<std::pair<std::pair<int, int>, hipStream_t>> cache;
-  std::lock_guard<std::mutex> g(mu);
+  auto& cache = g_comm_cache;
+  std::lock_guard<std::mutex> g(g_comm_mu);
   for (auto& e : cache)
     if (e.first.first == device && e.first.second == key) return e.second;
   int prev = 0;
@@ -103,7 +115,10 @@ hipStream_t tds_cu_comm_stream(int device) {
     }
   }
   (void)hipSetDevice(prev);
-  if (s) cache.push_back({{device, key}, s});
+  if (s) {
+    cache.push_back({{device, key}, s});
+    note_masked(s);
+  }
   return s;
 }
 
@@ -117,9 +132,8 @@ hipStream_t tds_cu_side_stream(int device, bool comm) {
   const bool striped = g_striped.load(std::memory_order_relaxed);
   if (reserve <= 0 || reserve % 8 != 0 || device < 0 || device >= kMaxDev) return nullptr;
   const int key = (reserve * 2 + (striped ? 1 : 0)) * 2 + (comm ? 1 : 0);
-  static std::mutex mu;
-  static std::vector<std::pair<std::pair<int, int>, hipStream_t>> cache;
-  std::lock_guard<std::mutex> g(mu);
+  auto& cache = g_side_cache;
+  std::lock_guard<std::mutex> g(g_side_mu);
   for (auto& e : cache)
     if (e.first.first == device && e.first.second == key) return e.second;
   int prev = 0;
@@ -137,8 +151,41 @@ hipStream_t tds_cu_side_stream(int device, bool comm) {
     }
   }
   (void)hipSetDevice(prev);
-  if (s) cache.push_back({{device, key}, s});
+  if (s) {
+    cache.push_back({{device, key}, s});
+    note_masked(s);
+  }
   return s;
+}
+
+// Synchronize and destroy every CU-masked stream created here; the caches forget them.  For the
+// end of a single-process run that used the split (bench.py --reserve-cus): left to process
+// exit, the HIP runtime's teardown of their HSA queues and rocprofiler-sdk's own finalization
+// race -- under rocprofv3 the tool's __cxa_finalize handler faults inside libhsa-runtime64 on a
+// queue page already unmapped (frames resolved with tools/micro/exit_maps.py,
+// tools/gpu_sessions/r3_s16.sh).  The caller must no longer use the streams (nor the torch
+// ExternalStream objects around them).  Returns how many were destroyed.
+int tds_cu_release_streams() {
+  std::vector<hipStream_t> all;
+  {
+    std::lock_guard<std::mutex> g(g_masked_mu);
+    all.swap(g_masked);
+  }
+  {
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    g_comm_cache.clear();
+  }
+  {
+    std::lock_guard<std::mutex> g(g_side_mu);
+    g_side_cache.clear();
+  }
+  int n = 0;
+  for (hipStream_t s : all) {
+    (void)hipStreamSynchronize(s);
+    if (hipStreamDestroy(s) == hipSuccess) ++n;
+  }
+  g_reserve.store(0, std::memory_order_relaxed);
+  return n;
 }
 
 // ---- one-GPU rehearsal of a collective's CU footprint -----------------------------------

@@ -73,6 +73,7 @@ int tds_cu_reserve();
 hipStream_t tds_cu_masked_stream(int device, int reserve, bool striped);
 hipStream_t tds_cu_comm_stream(int device);
 hipStream_t tds_cu_side_stream(int device, bool comm);  // a further stream on one side of the split
+int tds_cu_release_streams();  // destroy every CU-masked stream (end of a run); returns the count
 void tds_comm_spin(int64_t us, int nblocks, int lds_bytes, int* sink, hipStream_t st);
 void tds_cu_probe(int64_t us, int nblocks, int* out, hipStream_t st);
 int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c, int group_rows);  // host: blocked tile order table

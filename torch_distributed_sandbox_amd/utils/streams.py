@@ -83,3 +83,17 @@ def side_stream(device: Optional[torch.device] = None, side: Optional[str] = Non
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     h = int(_ext.ops().cu_side_stream(dev.index, side == "comm"))
     return torch.cuda.ExternalStream(h, device=dev) if h else None
+
+
+def release_streams() -> int:
+    """End of a single-process run that used the split: synchronize, make the default stream
+    current, and destroy every CU-masked stream (csrc/kernels/cu_budget.hip
+    ``tds_cu_release_streams``); the compute reserve returns to 0.  Nothing may use the masked
+    streams (or their ExternalStream wrappers) afterwards.  Left to process exit, the runtime's
+    teardown of their queues races rocprofiler-sdk's finalization (an exit-time fault under
+    rocprofv3 only).  Returns how many streams were destroyed."""
+    if not torch.cuda.is_available():
+        return 0
+    torch.cuda.synchronize()
+    torch.cuda.set_stream(torch.cuda.default_stream())
+    return int(_ext.ops().cu_release_streams())
