@@ -95,6 +95,10 @@ def _parser():
                     help="cpu: rehearsal of the launch/exchange path on the torch-ops plan (small --image-size)")
     ap.add_argument("--shared-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (needs --backend gloo); recorded in the JSON")
+    ap.add_argument("--input", default="fp32", choices=["levels", "fp32"],
+                    help="how each step's batch reaches the model: 'levels' = the resized images' uint8 levels "
+                         "(ToTensor's 1/255 folded into conv1 by the fused plan, models/convnet.py to_image), "
+                         "'fp32' = the ToTensor image materialised by the upsample kernel")
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
                     help="produce the next batch (upsample + BN1 input moments) on a side stream beside the "
                          "current step's conv2 backward")
@@ -467,7 +471,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     with_stats = data_stream is not None and args.mode != "layers"
 
     def produce(i):
-        return TF.upsample_bilinear_u8(src_pool[i % pool], H, W)
+        return TF.upsample_bilinear_u8(src_pool[i % pool], H, W, levels=args.input == "levels")
 
     pending = {}
     sim_stream = None
@@ -568,6 +572,8 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
                            and ex.zs_stats["steps"]] or None,
             "reserve_cus": reserve,
             "prefetch": data_stream is not None,
+            "input": ("uint8 levels (ToTensor's 1/255 folded into conv1)" if args.input == "levels"
+                      else "fp32 image"),
             "rccl_max_ctas": rccl_max_ctas or None,
             "optimizer": "SGD(lr=1e-4)",
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3) if on_gpu else None,

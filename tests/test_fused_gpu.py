@@ -296,10 +296,11 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     assert (db2.double().cpu() - br.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item()
 
 
-def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
+def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False):
     import torch.nn as nn
 
     from torch_distributed_sandbox_amd.models import ConvNet, fc_in_features
+    from torch_distributed_sandbox_amd.models.convnet import to_image
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
 
     class Ref(nn.Module):
@@ -331,9 +332,17 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
     ropt = torch.optim.SGD(ref.parameters(), lr)
     crit = CrossEntropyLoss()
     for s in range(steps):
-        x = torch.rand(B, 1, H, H, device=gpu)
+        if levels:  # uint8 levels of resized 28x28 sources (the input pipeline's), the references get
+            # the ToTensor image
+            from torch_distributed_sandbox_amd.ops import functional as TF
+
+            src = torch.randint(0, 256, (B, 28, 28), device=gpu, dtype=torch.uint8)
+            xin = TF.upsample_bilinear_u8(src, H, H, levels=True)
+            x = to_image(xin)
+        else:
+            x = xin = torch.rand(B, 1, H, H, device=gpu)
         y = torch.randint(0, 10, (B,), device=gpu)
-        loss = crit(ours(x), y)
+        loss = crit(ours(xin), y)
         opt.zero_grad()
         loss.backward()
         topt.zero_grad()
@@ -373,6 +382,83 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05):
 
 def test_fused_model_matches_reference(gpu):
     _fused_vs_ref(gpu, B=3, H=64)
+
+
+@pytest.mark.parametrize("H", [64, 76])
+def test_fused_model_levels_input_matches_reference(gpu, H):
+    """uint8 level batches (ToTensor's 1/255 folded into conv1, the x moments from exact integer
+    dot products) against the fp64 / TF32 references fed the fp32 image."""
+    _fused_vs_ref(gpu, B=3 if H == 64 else 2, H=H, steps=2 if H == 64 else 1, levels=True)
+
+
+@pytest.mark.parametrize("H", [68, 264])
+def test_layer1_levels_forward_backward(gpu, H):
+    """fused_l1_forward / fused_l1_backward on uint8 levels == the same ops on the fp32 image
+    (x = level * fp32(1/255)): the Gram exactly as fp64 (integer moments), p1 / argmax and the
+    layer-1 gradients to the bf16x3 class of the fp32-image path."""
+    from torch_distributed_sandbox_amd.models.convnet import to_image
+
+    torch.manual_seed(3)
+    B = 3
+    lv = torch.randint(0, 256, (B, 1, H, H), device=gpu, dtype=torch.uint8)
+    lv[0, 0, :7, :9] = 255  # saturated corner blocks: the Gram's corner terms
+    lv[1, 0, -6:, -6:] = 0
+    x = to_image(lv)
+    w1 = torch.randn(16, 1, 5, 5, device=gpu) * 0.2
+    b1 = torch.randn(16, device=gpu) * 0.1
+    g1 = torch.rand(16, device=gpu) + 0.5
+    be1 = torch.randn(16, device=gpu) * 0.1
+
+    def fwd(inp):
+        rm, rv = torch.zeros(16, device=gpu), torch.ones(16, device=gpu)
+        nbt = torch.zeros((), dtype=torch.long, device=gpu)
+        return _ops().fused_l1_forward(inp, w1, b1, g1, be1, rm, rv, nbt, 0.1, 1e-5), rm, rv
+
+    (p1l, idxl, statsl, graml), rml, rvl = fwd(lv)
+    (p1f, idxf, statsf, gramf), rmf, rvf = fwd(x)
+    # exact integer moments of the levels, scaled in fp64 by the fp32 constant
+    sc = float(torch.tensor(1.0 / 255.0, dtype=torch.float32))
+    pat = F.unfold(lv.double().cpu(), 5, padding=2)
+    G = torch.einsum("bkp,bjp->kj", pat, pat) * (sc * sc)
+    S = pat.sum((0, 2)) * sc
+    _check(graml[:625].view(25, 25), G, 1e-13, "G (levels)")
+    _check(graml[625:], S, 1e-13, "S (levels)")
+    # ... and of the fp32 image within its own per-pixel rounding (2^-24)
+    pat = F.unfold(x.double().cpu(), 5, padding=2)
+    _check(graml[:625].view(25, 25), torch.einsum("bkp,bjp->kj", pat, pat), 1e-7, "G (image)")
+    _check(statsl, statsf, 1e-5, "stats1")
+    _check(rml, rmf, 1e-5, "running_mean")
+    _check(rvl, rvf, 1e-5, "running_var")
+    _check(p1l.float(), p1f.float(), 2e-3, "p1")
+    assert (idxl == idxf).float().mean().item() > 0.999
+    P = H // 2
+    dp1 = torch.randn(B, P, P, 16, device=gpu)
+    outl = _ops().fused_l1_backward(dp1, lv, p1l, idxl, w1, b1, g1, statsl, graml, 1.0)
+    outf = _ops().fused_l1_backward(dp1, x, p1f, idxf, w1, b1, g1, statsf, gramf, 1.0)
+    # fp64 reference: the same layer in autograd, dp1 routed by max-pool's own argmax
+    prm = [t.detach().double().cpu().requires_grad_() for t in (w1, b1, g1, be1)]
+    y = F.conv2d(x.double().cpu(), prm[0], prm[1], padding=2)
+    z = F.batch_norm(y, None, None, prm[2], prm[3], True, 0.1, 1e-5)
+    F.max_pool2d(F.relu(z), 2, 2).backward(dp1.double().cpu().permute(0, 3, 1, 2))
+    for a, b, r, n in zip(outl, outf, prm, ("dw1", "db1", "dgamma1", "dbeta1")):
+        if n == "db1":  # analytically ~0 (bias before BN): rounding noise on both sides
+            assert (a - b).abs().max().item() <= 1e-3 * outf[0].abs().max().item() + 1e-6, n
+            continue
+        el, ef = rel(a.double().cpu(), r.grad.view(a.shape)), rel(b.double().cpu(), r.grad.view(b.shape))
+        print(f"{n}: levels {el:.3e}  fp32 image {ef:.3e}")
+        assert el <= max(1e-3, 1.5 * ef), n
+
+
+def test_upsample_levels(gpu):
+    """levels=True returns the rounded levels the fp32 output is made of (x = level * fp32(1/255))."""
+    from torch_distributed_sandbox_amd.models.convnet import to_image
+    from torch_distributed_sandbox_amd.ops import functional as TF
+
+    src = torch.randint(0, 256, (3, 28, 28), device=gpu, dtype=torch.uint8)
+    for H in (300, 302):  # 302: rows not 4-byte aligned -> the scalar tail path
+        lv = TF.upsample_bilinear_u8(src, H, H, levels=True)
+        assert lv.dtype == torch.uint8 and lv.shape == (3, 1, H, H)
+        assert torch.equal(to_image(lv), TF.upsample_bilinear_u8(src, H, H))
 
 
 def test_fused_model_matches_reference_odd_pool(gpu):

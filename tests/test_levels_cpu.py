@@ -1,0 +1,32 @@
+"""uint8 level batches (the resized images before ToTensor) as model input, on the CPU plans:
+ConvNet reads them as levels * fp32(1/255), exactly what the fp32 upsample produces."""
+import torch
+
+from torch_distributed_sandbox_amd.models import ConvNet
+from torch_distributed_sandbox_amd.models.convnet import LEVEL_SCALE, to_image
+from torch_distributed_sandbox_amd.ops import functional as TF
+
+
+def test_to_image_matches_totensor_scale():
+    lv = torch.arange(256, dtype=torch.uint8).view(1, 1, 16, 16)
+    x = to_image(lv)
+    assert x.dtype == torch.float32
+    assert torch.equal(x, lv.float() * torch.tensor(LEVEL_SCALE, dtype=torch.float32))
+    f = torch.rand(2, 1, 4, 4)
+    assert to_image(f) is f
+
+
+def test_upsample_levels_cpu():
+    src = torch.randint(0, 256, (2, 28, 28), dtype=torch.uint8)
+    lv = TF.upsample_bilinear_u8(src, 64, 64, levels=True)
+    assert lv.dtype == torch.uint8 and lv.shape == (2, 1, 64, 64)
+    assert torch.allclose(to_image(lv), TF.upsample_bilinear_u8(src, 64, 64), atol=1e-7)
+
+
+def test_convnet_levels_input_equals_image_input():
+    torch.manual_seed(0)
+    m = ConvNet(image_shape=(32, 32))
+    lv = torch.randint(0, 256, (2, 1, 32, 32), dtype=torch.uint8)
+    out_l = m(lv)
+    out_f = m(to_image(lv))
+    assert torch.equal(out_l, out_f)

@@ -16,6 +16,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -64,6 +65,17 @@ Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shap
 #define TDS_L1_PER_CU 8
 #endif
 int l1_wg() { return tds_fused_num_wg(TDS_L1_PER_CU); }
+
+// layer-1 backward workgroups per CU: 4 waves each, <= 128 VGPRs (__launch_bounds__(256, 3) keeps the
+// kernel at 124-126), so 3 or 4 fit a CU.  TDS_L1B_PER_CU overrides it (A/B sweeps only).
+int l1b_wg() {
+  static const int per_cu = [] {
+    const char* e = std::getenv("TDS_L1B_PER_CU");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 8 ? v : 3;
+  }();
+  return tds_fused_num_wg(per_cu);
+}
 
 // Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
 // torch caching allocator, built once.  The map is never destroyed (no frees at process exit).
@@ -151,8 +163,10 @@ int64_t pb_plane(int64_t P) { return tds_pb_plane((int)(P / 2)); }
 
 // ---------------------------------------------------------------- layer 1 forward
 // returns (p1 carrier, idx1, stats1[mean16|invstd16], ac_partial, strips)
+// x: fp32 images, or uint8 levels (ToTensor's input: x = level / 255, folded into the kernels)
 void check_l1_input(const Tensor& x, const char* what) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kFloat && x.is_contiguous(), what, ": x");
+  TORCH_CHECK(x.is_cuda() && (x.scalar_type() == at::kFloat || x.scalar_type() == at::kByte) && x.is_contiguous(),
+              what, ": x must be a contiguous fp32 or uint8 GPU tensor");
   TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, what, ": x must be [B,1,H,W]");
   TORCH_CHECK(x.size(2) == x.size(3) && x.size(2) >= 8, what, ": square images with H >= 8");
   TORCH_CHECK(x.size(0) >= 1 && x.size(0) <= 32, what, ": 1 <= B <= 32 per rank");
@@ -174,8 +188,12 @@ std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
   TORCH_CHECK(nac > 0, "l1_input_stats: W % 4 == 0 required (autocorrelation kernel)");
   auto ac = at::empty({(int64_t)nac * 42}, fo);
   auto strips = at::empty({B * 8 * 82}, fo);
-  tds_x_moments(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
-                st);
+  if (x.scalar_type() == at::kByte)
+    tds_x_moments_u8(x.data_ptr<uint8_t>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H,
+                     (int)W, st);
+  else
+    tds_x_moments(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
+                  st);
   auto asum = at::empty({42}, fo);
   tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
   check_launches("l1_input_stats");
@@ -203,7 +221,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
   const int64_t P = H / 2;
-  auto fo = x.options();
+  auto fo = x.options().dtype(at::kFloat);
+  const bool levels = x.scalar_type() == at::kByte;
   // x autocorrelation + border strips (precomputed by the input pipeline, or here) -> Gram G /
   // patch sums S -> BN1 statistics in closed form
   Tensor asum, strips;
@@ -220,14 +239,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
   auto stats = at::empty({32}, fo);
   auto aff = at::empty({32}, fo);
-  tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr<float>(), (int)B, (int)H, (int)W,
+  tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H, (int)W,
               w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps,
               (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1 (fp16), argmax
   auto p1 = at::empty({B, P, P, 16}, fo.dtype(at::kHalf));
   auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
-  tds_l1_apply(x.data_ptr<float>(), w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(), p1.data_ptr(),
-               idx1.data_ptr<uint8_t>(), l1_wg(), (int)B, (int)H, (int)W, st);
+  tds_l1_apply(x.data_ptr(), levels, w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(),
+               p1.data_ptr(), idx1.data_ptr<uint8_t>(), l1_wg(), (int)B, (int)H, (int)W, st);
   check_launches("fused_l1_forward");
   return {p1, idx1, stats, gram};
 }
@@ -555,7 +574,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
                                                              const c10::optional<Tensor>& dbe_out) {
   TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, "fused_l1_backward: x");
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3), P = H / 2;
-  need(x, at::kFloat, {B, 1, H, W}, "x");
+  const bool levels = x.scalar_type() == at::kByte;
+  need(x, levels ? at::kByte : at::kFloat, {B, 1, H, W}, "x");
   need(dp1, at::kFloat, {B, P, P, 16}, "dp1");
   need(p1, at::kHalf, {B, P, P, 16}, "p1");
   need(idx1, at::kByte, {B, P, P, 16}, "idx1");
@@ -566,10 +586,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   const float* g = optf(gamma1, 16, "bn1.weight");
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
-  const int nwg = tds_fused_num_wg(3), rows = tds_l1_bwd_rows(nwg);  // 3 workgroups fit a CU (156 VGPRs)
+  const int nwg = l1b_wg(), rows = tds_l1_bwd_rows(nwg);
   auto partial = at::empty({(int64_t)rows * 16 * 27}, x.options().dtype(at::kDouble));
-  tds_l1_bwd(x.data_ptr<float>(), dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(), w1.data_ptr<float>(),
-             b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
+  tds_l1_bwd(x.data_ptr(), levels, dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(),
+             w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);
   auto dw1 = sink_or_empty(dw_out, {16, 1, 5, 5}, x, "dw1_out");

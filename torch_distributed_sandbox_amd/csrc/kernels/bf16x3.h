@@ -32,6 +32,13 @@ __device__ __forceinline__ f32x4 mfma_bf16x3(const s16x8& ahi, const s16x8& alo,
   return c;
 }
 
+// c += (ahi + alo) * b for a b that is exact in bf16 (integer levels <= 256): two products
+__device__ __forceinline__ f32x4 mfma_bf16x2a(const s16x8& ahi, const s16x8& alo, const s16x8& b, f32x4 c) {
+  c = mfma_bf16(alo, b, c);
+  c = mfma_bf16(ahi, b, c);
+  return c;
+}
+
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
   unsigned int u = __float_as_uint(f);
   if ((u & 0x7f800000u) == 0x7f800000u) return (unsigned short)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));  // inf/nan

@@ -32,6 +32,9 @@ constexpr int L1_TR = 16;           // conv1 output rows per tile
 constexpr int L1_TC = 64;           // conv1 output cols per tile
 constexpr int L1_XR = L1_TR + 4;
 constexpr int L1_XS = 80;           // LDS row stride (floats): 16 mod 32 -> paired taps hit disjoint banks
+// uint8 level input: x = L1_LEVEL_SCALE * level, the fp32 constant upsample_bilinear_u8 (elementwise.hip)
+// and ToTensor scale by
+constexpr float L1_LEVEL_SCALE = 1.f / 255.f;
 
 __device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
@@ -56,7 +59,11 @@ __device__ __forceinline__ int l1b_tap(int g, int j) {
   return -1;
 }
 
-__global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restrict__ x, const float* __restrict__ w1,
+// LV: x holds uint8 levels (x = L1_LEVEL_SCALE * level).  A level is exact in bf16, so the LDS word
+// is the level's fp32 bit pattern (bf16 hi | lo = 0), conv1 takes two MFMAs (w hi, w lo) per
+// product instead of three and half the operand perms, and the scale folds into BN1's affine.
+template <bool LV>
+__global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict__ xv, const float* __restrict__ w1,
                                                       const float* __restrict__ b1, const float* __restrict__ aff,
                                                       uint4* __restrict__ p1, uint8_t* __restrict__ idx1, int B,
                                                       int H, int W) {
@@ -93,6 +100,12 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
 #pragma unroll
   for (int r = 0; r < 4; ++r) fin = fin && __builtin_isfinite(ea[r]) && __builtin_isfinite(ebb[r]) && ea[r] != 0.f;
   const bool fast_ok = __builtin_amdgcn_ballot_w64(!fin) == 0 && __syncthreads_and(fin) != 0;
+  if constexpr (LV) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ea[r] *= L1_LEVEL_SCALE;  // z = ea * (scale * acc + b1) + eb
+  }
+  const float* __restrict__ x = static_cast<const float*>(xv);
+  const uint8_t* __restrict__ xl = static_cast<const uint8_t*>(xv);
 
   // x tile staging: LDS column 0 <-> global column c0-4 (16-B aligned since W % 4 == 0),
   // 20 rows x 18 float4; the next tile's loads are issued before this tile's MFMAs.
@@ -102,7 +115,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
   auto load_tile = [&](int t) {
     const int b = t / per_img, rem = t - b * per_img;
     const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
-    const float* xb = x + (int64_t)b * H * W;
+    const float* xb = LV ? nullptr : x + (int64_t)b * H * W;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = tid + 256 * u;
@@ -110,7 +123,12 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
       if (e < NV) {
         const int rr = e / 18, cv = e - rr * 18;
         const int gr = r0 - 2 + rr, gc = c0 - 4 + 4 * cv;
-        if (gr >= 0 && gr < H && gc >= 0 && gc < W) v = *reinterpret_cast<const float4*>(xb + (int64_t)gr * W + gc);
+        if (gr >= 0 && gr < H && gc >= 0 && gc < W) {
+          if constexpr (LV)  // 4 levels in .x
+            v.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(xl + (int64_t)b * H * W + (int64_t)gr * W + gc));
+          else
+            v = *reinterpret_cast<const float4*>(xb + (int64_t)gr * W + gc);
+        }
       }
       pre[u] = v;
     }
@@ -127,6 +145,16 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
       const int e = tid + 256 * u;
       if (e < NV) {
         const int rr = e / 18, cv = e - rr * 18;
+        if constexpr (LV) {  // levels are finite; word = fp32 bits of the level = bf16 hi | lo 0
+          const uint32_t q = __float_as_uint(pre[u].x);
+          uint4 v;
+          v.x = __float_as_uint((float)(q & 0xFFu));
+          v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
+          v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
+          v.w = __float_as_uint((float)(q >> 24));
+          *reinterpret_cast<uint4*>(xs + rr * L1_XS + 4 * cv) = v;
+          continue;
+        }
         nonfinite |= !__builtin_isfinite((pre[u].x + pre[u].y) + (pre[u].z + pre[u].w));
         uint32_t h01, l01, h23, l23;
         split2_bf16(pre[u].x, pre[u].y, h01, l01);
@@ -166,12 +194,15 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const float* __restric
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
-              lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+              if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
             }
 #if defined(TDS_L1_EXP) && TDS_L1_EXP == 2
             acc[a][c] = f32x4{(float)(bh[0] ^ bl[1]), (float)wah[0], (float)wal[1], 0.f};
 #else
-            acc[a][c] = mfma_bf16x3(wah, wal, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
+            if constexpr (LV)
+              acc[a][c] = mfma_bf16x2a(wah, wal, bh, f32x4{0.f, 0.f, 0.f, 0.f});
+            else
+              acc[a][c] = mfma_bf16x3(wah, wal, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
 #endif
           }
         // BN1 affine -> 2x2 max-pool (first max in scan order) -> ReLU -> bf16 hi|lo record +
@@ -380,7 +411,10 @@ constexpr int LB_PER = (LB_V + 255) / 256;
 // go through LDS; fp32 MFMA accumulation per tile (256 pixels), fp64 across tiles.
 // partial[wg][16][27] in the sparse kernel's layout ([0] sum dz, [1] 0, [2+j] taps).
 constexpr int LM_XS = 80;  // x tile row stride (words): 20 rows x (72 staged + pad) columns
-__global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restrict__ x, const float* __restrict__ dp1,
+// LV: x holds uint8 levels (see l1_conv_bf3_kernel): the x operand is exact in bf16, two MFMAs per
+// product (dz hi, dz lo), half the B perms; the tap sums are scaled by L1_LEVEL_SCALE at the end.
+template <bool LV>
+__global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const float* __restrict__ dp1,
                                                           const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
                                                           double* __restrict__ partial, int B, int H, int W) {
   __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LB_XR * LM_XS * 4];
@@ -416,6 +450,8 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
     const int r = tid >> 2, c = tid & 3;
     xs[r * LM_XS + 72 + c] = r < 2 ? 0x3F800000u : 0u;
   }
+  const float* __restrict__ x = static_cast<const float*>(xv);
+  const uint8_t* __restrict__ xl = static_cast<const uint8_t*>(xv);
   uint4 pre[LB_PER];
   auto load_tile = [&](int t) {
     const int b = t / per_img, rem = t - b * per_img;
@@ -440,8 +476,12 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
         e -= LB_V_DP + LB_V_PH + LB_V_ID;
         const int rr = e / 18, cv = e - rr * 18;
         const int gr = 2 * pr0 - 2 + rr, gcol = 2 * pc0 - 4 + 4 * cv;
-        if (gr >= 0 && gr < H && gcol >= 0 && gcol < W)
-          v = *reinterpret_cast<const uint4*>(x + ((int64_t)b * H + gr) * W + gcol);
+        if (gr >= 0 && gr < H && gcol >= 0 && gcol < W) {
+          if constexpr (LV)  // 4 levels in .x
+            v.x = *reinterpret_cast<const uint32_t*>(xl + ((int64_t)b * H + gr) * W + gcol);
+          else
+            v = *reinterpret_cast<const uint4*>(x + ((int64_t)b * H + gr) * W + gcol);
+        }
       }
       pre[u] = v;
     }
@@ -456,6 +496,16 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
       else if (e < LB_V) {
         e -= LB_V_DP + LB_V_PH + LB_V_ID;
         const int rr = e / 18, cv = e - rr * 18;
+        if constexpr (LV) {  // word = fp32 bits of the level = bf16 hi | lo 0
+          const uint32_t q = pre[u].x;
+          uint4 v;
+          v.x = __float_as_uint((float)(q & 0xFFu));
+          v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
+          v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
+          v.w = __float_as_uint((float)(q >> 24));
+          *reinterpret_cast<uint4*>(xs + rr * LM_XS + 4 * cv) = v;
+          continue;
+        }
         const float4 f = __builtin_bit_cast(float4, pre[u]);
         uint32_t h01, l01, h23, l23;
         split2_bf16(f.x, f.y, h01, l01);
@@ -526,9 +576,12 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
-            lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+            if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
           }
-          acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
+          if constexpr (LV)
+            acc[blk] = mfma_bf16x2a(ah, al, bh, acc[blk]);
+          else
+            acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
         }
       }
     }
@@ -548,7 +601,7 @@ __global__ __launch_bounds__(256) void l1_bwd_mfma_kernel(const float* __restric
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       double* o = red + (wv * 16 + 4 * g + r) * LB_NACC;
-      if (n < 25) o[2 + n] = dacc[blk][r];
+      if (n < 25) o[2 + n] = LV ? dacc[blk][r] * (double)L1_LEVEL_SCALE : dacc[blk][r];
       else if (n == 25) o[0] = dacc[blk][r];
       else if (n == 26) o[1] = 0.0;
     }
@@ -578,14 +631,17 @@ struct L1Corners {
   }
 };
 
+// T = uint8_t: x holds levels (x = xs * level); the sums are of the levels and G, S are scaled by
+// xs^2, xs at the end (fp64), so the Gram is that of the fp32 image either way.
+template <typename T>
 __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips_b,
-                              const float* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
-                              double* full, double* strips, L1Corners& cx) {
+                              const T* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
+                              double* full, double* strips, L1Corners& cx, double xs) {
   const int tid = threadIdx.x;
   for (int e = tid; e < B * 144; e += blockDim.x) {
     const int b = e / 144, q = (e / 36) % 4, i = (e / 6) % 6, j = e % 6;
     const int r = q < 2 ? i : H - 6 + i, c = (q & 1) == 0 ? j : W - 6 + j;
-    cx.v[b][q][i][j] = x[(int64_t)b * H * W + (int64_t)r * W + c];
+    cx.v[b][q][i][j] = (float)x[(int64_t)b * H * W + (int64_t)r * W + c];
   }
   // per-image border strips [B][8][82] -> batch sums, images in order
   for (int e = tid; e < 8 * 82; e += blockDim.x) {
@@ -626,7 +682,7 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
           if (r2 < 0 || r2 >= H || c2 < 0 || c2 >= W) continue;
           for (int b = 0; b < B; ++b) v += (double)cx.at(b, r, cc, H, W) * cx.at(b, r2, c2, H, W);
         }
-      G[k][j] = v;
+      G[k][j] = v * (xs * xs);
     } else {
       v = ac_sum[41];
       for (int i = 0; i < ne; ++i) v -= strips[line_index_row(er[i]) * 82 + 81];
@@ -634,7 +690,7 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
       for (int i = 0; i < ne; ++i)
         for (int q = 0; q < nc; ++q)
           for (int b = 0; b < B; ++b) v += cx.at(b, er[i], ec[q], H, W);
-      S[j] = v;
+      S[j] = v * xs;
     }
   }
   __syncthreads();
@@ -645,22 +701,23 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
 //   sum_px (y1 - b1)[c]   = w1[c] . S
 //   sum_px (y1 - b1)^2[c] = w1[c]^T G w1[c]
 // gram = G[625] | S[25] (fp64); sums = [c][sum, sumsq] in the bn_finalize_shifted layout.
+template <typename T>
 __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__ ac_sum,
-                                                      const double* __restrict__ strips, const float* __restrict__ x,
+                                                      const double* __restrict__ strips, const T* __restrict__ x,
                                                       int B, int H, int W, const float* __restrict__ w1,
                                                       double* __restrict__ gram, double* __restrict__ sums,
                                                       const float* __restrict__ b1, float eps, float momentum,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
-                                                      float* __restrict__ aff) {
+                                                      float* __restrict__ aff, double xs) {
   __shared__ double full[81];
   __shared__ double G[25][25];
   __shared__ double S[25];
   __shared__ double Gw[16][25];
   __shared__ double strips_sum[8 * 82];
   __shared__ L1Corners cx;
-  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, cx);
+  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, cx, xs);
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {
@@ -728,7 +785,8 @@ using namespace tds;
 
 int tds_fused_num_wg(int per_cu) { return tds_device_cus() * per_cu; }
 
-void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
+void tds_l1_gram(const double* ac_sum, const double* strips, const void* x, bool levels, int B, int H, int W,
+                 const float* w1,
                  double* gram, double* sums, const float* b1, float eps, float momentum, const float* gamma,
                  const float* beta, float* stats, float* running_mean, float* running_var, int64_t* num_batches,
                  float* aff, hipStream_t st) {
@@ -736,15 +794,25 @@ void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int
     tds_launch_fail("l1_gram: needs batch <= 32 and H, W >= 12");
     return;
   }
-  hipLaunchKernelGGL(l1_gram_kernel, dim3(1), dim3(256), 0, st, ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps,
-                     momentum, gamma, beta, stats, running_mean, running_var, num_batches, aff);
+  if (levels)
+    hipLaunchKernelGGL(l1_gram_kernel<uint8_t>, dim3(1), dim3(256), 0, st, ac_sum, strips,
+                       static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats,
+                       running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
+  else
+    hipLaunchKernelGGL(l1_gram_kernel<float>, dim3(1), dim3(256), 0, st, ac_sum, strips, static_cast<const float*>(x),
+                       B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean, running_var,
+                       num_batches, aff, 1.0);
   TDS_LAUNCH_CHECK();
 }
 
-void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
-                  int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(l1_conv_bf3_kernel, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff, reinterpret_cast<uint4*>(p1),
-                     idx1, B, H, W);
+void tds_l1_apply(const void* x, bool levels, const float* w1, const float* b1, const float* aff, void* p1,
+                  uint8_t* idx1, int nwg, int B, int H, int W, hipStream_t st) {
+  if (levels)
+    hipLaunchKernelGGL(l1_conv_bf3_kernel<true>, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff,
+                       reinterpret_cast<uint4*>(p1), idx1, B, H, W);
+  else
+    hipLaunchKernelGGL(l1_conv_bf3_kernel<false>, dim3(nwg), dim3(256), 0, st, x, w1, b1, aff,
+                       reinterpret_cast<uint4*>(p1), idx1, B, H, W);
   TDS_LAUNCH_CHECK();
 }
 
@@ -785,12 +853,16 @@ void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, c
 
 int tds_l1_bwd_rows(int nwg) { return nwg; }
 
-void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
-                double* partial, int nwg, int B, int H, int W, hipStream_t st) {
+void tds_l1_bwd(const void* x, bool levels, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1,
+                const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st) {
   (void)w1;
   (void)b1;
-  hipLaunchKernelGGL(l1_bwd_mfma_kernel, dim3(nwg), dim3(256), 0, st, x, dp1, reinterpret_cast<const uint4*>(p1), idx1,
-                     partial, B, H, W);
+  if (levels)
+    hipLaunchKernelGGL(l1_bwd_mfma_kernel<true>, dim3(nwg), dim3(256), 0, st, x, dp1,
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
+  else
+    hipLaunchKernelGGL(l1_bwd_mfma_kernel<false>, dim3(nwg), dim3(256), 0, st, x, dp1,
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   TDS_LAUNCH_CHECK();
 }
 

@@ -111,8 +111,11 @@ __global__ void maxpool2_bwd_kernel(const float* __restrict__ gy, const uint8_t*
 // image is read again right away by the layer-1 kernels and can stay in the MALL).  The arithmetic order is exactly the
 // per-pixel formula above, so the result is bit-identical to the scalar form.
 constexpr int kUpsMaxW = 256;
+// U8OUT: the rounded level itself (uint8), i.e. ToTensor's input before its 1/255 -- the fused
+// ConvNet plan folds that scale into conv1 (convnet_fused.hip, x_autocorr.hip).
+template <bool U8OUT>
 __global__ void __launch_bounds__(256) upsample_bilinear_u8_kernel(const uint8_t* __restrict__ src,
-                                                                   float* __restrict__ dst, int B, int h, int w,
+                                                                   void* __restrict__ dstv, int B, int h, int w,
                                                                    int H, int W) {
   __shared__ float rows[2][kUpsMaxW];
   const int Y = blockIdx.x, b = blockIdx.y;
@@ -128,8 +131,7 @@ __global__ void __launch_bounds__(256) upsample_bilinear_u8_kernel(const uint8_t
     rows[1][x] = (float)s[y1 * w + x];
   }
   __syncthreads();
-  float* d = dst + ((int64_t)b * H + Y) * W;
-  auto pix = [&](int X) {
+  auto lvl = [&](int X) {
     float fx = ((float)X + 0.5f) * sx - 0.5f;
     fx = fminf(fmaxf(fx, 0.f), (float)(w - 1));
     const int x0 = (int)fx;
@@ -137,10 +139,23 @@ __global__ void __launch_bounds__(256) upsample_bilinear_u8_kernel(const uint8_t
     const float ax = fx - (float)x0;
     const float top = (1.f - ax) * rows[0][x0] + ax * rows[0][x1];
     const float bot = (1.f - ax) * rows[1][x0] + ax * rows[1][x1];
-    float v = (1.f - ay) * top + ay * bot;
-    v = fminf(fmaxf(rintf(v), 0.f), 255.f);
-    return v * (1.f / 255.f);
+    const float v = (1.f - ay) * top + ay * bot;
+    return fminf(fmaxf(rintf(v), 0.f), 255.f);
   };
+  if constexpr (U8OUT) {
+    uint8_t* d8 = reinterpret_cast<uint8_t*>(dstv) + ((int64_t)b * H + Y) * W;
+    const int W4 = ((((uintptr_t)d8) & 3) == 0) ? (W >> 2) : 0;
+    for (int q = threadIdx.x; q < W4; q += blockDim.x) {
+      const int X = q << 2;
+      const uint32_t v = (uint32_t)lvl(X) | ((uint32_t)lvl(X + 1) << 8) | ((uint32_t)lvl(X + 2) << 16) |
+                         ((uint32_t)lvl(X + 3) << 24);
+      reinterpret_cast<uint32_t*>(d8)[q] = v;
+    }
+    for (int X = (W4 << 2) + threadIdx.x; X < W; X += blockDim.x) d8[X] = (uint8_t)lvl(X);
+    return;
+  }
+  float* d = reinterpret_cast<float*>(dstv) + ((int64_t)b * H + Y) * W;
+  auto pix = [&](int X) { return lvl(X) * (1.f / 255.f); };
   const bool vec = ((((uintptr_t)d) & 15) == 0);
   const int W4 = vec ? (W >> 2) : 0;
   for (int q = threadIdx.x; q < W4; q += blockDim.x) {
@@ -330,13 +345,17 @@ void tds_maxpool2_bwd(const float* gy, const uint8_t* idx, float* gx, int64_t pl
   hipLaunchKernelGGL(maxpool2_bwd_kernel, dim3(grid_for(total, 256, 4)), dim3(256), 0, st, gy, idx, gx, planes, H, W);
   TDS_LAUNCH_CHECK();
 }
-void tds_upsample_bilinear_u8(const uint8_t* src, float* dst, int B, int h, int w, int H, int W, hipStream_t st) {
+void tds_upsample_bilinear_u8(const uint8_t* src, void* dst, bool u8_out, int B, int h, int w, int H, int W,
+                              hipStream_t st) {
   if ((int64_t)B * H * W == 0) return;
   if (w > kUpsMaxW || h < 1 || B > 65535) {  // the op wrapper rejects these shapes first (ops.cpp)
     tds_launch_fail("upsample_bilinear_u8: unsupported shape");
     return;
   }
-  hipLaunchKernelGGL(upsample_bilinear_u8_kernel, dim3(H, B), dim3(256), 0, st, src, dst, B, h, w, H, W);
+  if (u8_out)
+    hipLaunchKernelGGL(upsample_bilinear_u8_kernel<true>, dim3(H, B), dim3(256), 0, st, src, dst, B, h, w, H, W);
+  else
+    hipLaunchKernelGGL(upsample_bilinear_u8_kernel<false>, dim3(H, B), dim3(256), 0, st, src, dst, B, h, w, H, W);
   TDS_LAUNCH_CHECK();
 }
 void tds_sgd_multi(const SgdChunkTable& tab, float lr, float wd, float momentum, float dampening, int nesterov,

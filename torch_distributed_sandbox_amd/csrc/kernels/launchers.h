@@ -11,7 +11,8 @@ void tds_relu_fwd(const float* x, float* y, int64_t n, hipStream_t st);
 void tds_relu_bwd(const float* g, const float* out, float* dx, int64_t n, hipStream_t st);
 void tds_maxpool2_fwd(const float* x, float* y, uint8_t* idx, int64_t planes, int H, int W, hipStream_t st);
 void tds_maxpool2_bwd(const float* gy, const uint8_t* idx, float* gx, int64_t planes, int H, int W, hipStream_t st);
-void tds_upsample_bilinear_u8(const uint8_t* src, float* dst, int B, int h, int w, int H, int W, hipStream_t st);
+void tds_upsample_bilinear_u8(const uint8_t* src, void* dst, bool u8_out, int B, int h, int w, int H, int W,
+                              hipStream_t st);
 
 #define TDS_SGD_MAX_TENSORS 48
 struct SgdChunkTable {
@@ -96,17 +97,21 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
 
 // ---- convnet_fused.hip
 int tds_fused_num_wg(int per_cu);
-void tds_l1_gram(const double* ac_sum, const double* strips, const float* x, int B, int H, int W, const float* w1,
+void tds_l1_gram(const double* ac_sum, const double* strips, const void* x, bool levels, int B, int H, int W,
+                 const float* w1,
                  double* gram, double* sums, const float* b1, float eps, float momentum, const float* gamma,
                  const float* beta, float* stats, float* running_mean, float* running_var, int64_t* num_batches,
                  float* aff, hipStream_t st);  // Gram + patch sums + the BN1 finalize
-void tds_l1_apply(const float* x, const float* w1, const float* b1, const float* aff, void* p1, uint8_t* idx1, int nwg,
-                  int B, int H, int W, hipStream_t st);
+// levels: x is uint8 levels (x = level / 255, convnet_fused.hip L1_LEVEL_SCALE), else fp32
+void tds_l1_apply(const void* x, bool levels, const float* w1, const float* b1, const float* aff, void* p1,
+                  uint8_t* idx1, int nwg, int B, int H, int W, hipStream_t st);
 void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n, const float* shift, float eps,
                              float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
                              float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_x_autocorr_num_wg(int B, int H, int W);  // partial rows tds_x_autocorr writes
 void tds_x_moments(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
+void tds_x_moments_u8(const uint8_t* x, double* ac_partial, int nwg, double* strips, int B, int H, int W,
+                      hipStream_t st);  // the same moments of uint8 levels (exact)
 int tds_conv2_bwd_clock_read(uint32_t* host, int n);  // DIAG 13 per-wave barrier clocks (diag builds)
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st);  // border strips [B][8][82]
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
@@ -122,8 +127,8 @@ void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n,
                             float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
                             float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
-void tds_l1_bwd(const float* x, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1, const float* b1,
-                double* partial, int nwg, int B, int H, int W, hipStream_t st);
+void tds_l1_bwd(const void* x, bool levels, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1,
+                const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);

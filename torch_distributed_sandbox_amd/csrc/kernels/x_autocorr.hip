@@ -41,7 +41,8 @@ static int x_autocorr_num_wg(int B, int H, int W) {
 // vs 99 + 35 us), the two kernels on separate streams (176 + 94 us overlapped), and workgroups
 // per (line, dy, line chunk) with the 9 dx products per pixel and chunk partials folded in
 // l1_gram (45 us here + 11 us more in l1_gram).
-__device__ void x_border_block(const float* __restrict__ x, double* __restrict__ strips, int H, int W, int di, int L,
+template <typename T>
+__device__ void x_border_block(const T* __restrict__ x, double* __restrict__ strips, int H, int W, int di, int L,
                                int b, double* sh) {
   const int dy = di / 9 - 4, dx = di % 9 - 4;
   const bool plain = di == 81;
@@ -49,23 +50,24 @@ __device__ void x_border_block(const float* __restrict__ x, double* __restrict__
   const int fixed = is_row ? (L < 2 ? L : H - 4 + L) : (L < 6 ? L - 4 : W - 8 + L);
   const int len = is_row ? W : H;
   double s = 0.0;
-  const float* xb = x + (int64_t)b * H * W;
+  const T* xb = x + (int64_t)b * H * W;
   for (int i = threadIdx.x; i < len; i += blockDim.x) {
     const int r = is_row ? fixed : i, c = is_row ? i : fixed;
     if (r < 0 || r >= H || c < 0 || c >= W) continue;
-    const float u = xb[(int64_t)r * W + c];
+    const float u = (float)xb[(int64_t)r * W + c];
     if (plain) {
       s += u;
     } else {
       const int r2 = r + dy, c2 = c + dx;
-      if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) s += (double)u * xb[(int64_t)r2 * W + c2];
+      if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) s += (double)u * (double)xb[(int64_t)r2 * W + c2];
     }
   }
   s = block_sum(s, sh);
   if (threadIdx.x == 0) strips[((int64_t)b * 8 + L) * 82 + di] = s;
 }
 
-__global__ __launch_bounds__(256) void x_border_kernel(const float* __restrict__ x, double* __restrict__ strips, int B,
+template <typename T>
+__global__ __launch_bounds__(256) void x_border_kernel(const T* __restrict__ x, double* __restrict__ strips, int B,
                                                        int H, int W) {
   __shared__ double sh[8];
   x_border_block(x, strips, H, W, blockIdx.x, blockIdx.y, blockIdx.z, sh);
@@ -149,6 +151,88 @@ __global__ __launch_bounds__(256, 3) void x_autocorr_kernel(const float* __restr
   if (tid < 42) partial[(int64_t)blk * 42 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
 }
 
+
+// The same sums over uint8 levels (the fused plan's input when the batch is handed over as
+// ToTensor's levels, ops/functional.py upsample_bilinear_u8(levels=True)): every product is an
+// integer <= 255^2, so the sums are EXACT in u32 (a thread's accumulator <= 64 * 255^2, a wave's
+// <= 2^28) and one v_dot4_u32_u8 takes a pixel quad's 4 products of one offset: the partner
+// quad of offset dx is a byte window of the row's three dwords (v_alignbyte).  41 dot4 + <= 41
+// alignbyte per quad and row instead of 168 FMAs.  Rows are 12-byte runs (cols c-4 .. c+7), 3
+// dword loads per row; the level image is a quarter of the fp32 bytes.
+__global__ __launch_bounds__(256, 3) void x_autocorr_u8_kernel(const uint8_t* __restrict__ x,
+                                                            double* __restrict__ partial, int B, int H, int W,
+                                                            double* __restrict__ strips, int nac) {
+  __shared__ double red[4][42];
+  if ((int)blockIdx.x >= nac) {
+    __shared__ double sh[8];
+    const int j = (int)blockIdx.x - nac;
+    x_border_block(x, strips, H, W, j % 82, (j / 82) % 8, j / 656, sh);
+    return;
+  }
+  const int blk = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int ncg = W / 4, nband = (H + AC_RB - 1) / AC_RB;
+  const int64_t gt = (int64_t)blk * 256 + tid;
+  uint32_t acc[42];
+#pragma unroll
+  for (int i = 0; i < 42; ++i) acc[i] = 0u;
+  if (gt < (int64_t)B * nband * ncg) {
+    const int cg = (int)(gt % ncg);
+    const int64_t rest = gt / ncg;
+    const int band = (int)(rest % nband), b = (int)(rest / nband);
+    const int c = 4 * cg, r0 = band * AC_RB;
+    const int b0 = __builtin_amdgcn_readfirstlane(b);
+    const int64_t img = (int64_t)H * W;
+    const int64_t span = (int64_t)(B - b0) * img;
+    const __amdgpu_buffer_rsrc_t rx =
+        tds_buffer_rsrc(x + (int64_t)b0 * img, (uint32_t)(span < 0xFFFFFFF0LL ? span : 0xFFFFFFF0LL));
+    constexpr uint32_t kOob = 0xFFFFFFF0u;
+    const uint32_t base = (uint32_t)((int64_t)(b - b0) * img + c);
+    const bool has_l = c >= 4, has_r = c + 4 < W;
+    auto ld_row = [&](int r, uint32_t (&row)[3]) {
+      const uint32_t o = base + (uint32_t)r * (uint32_t)W;
+      const bool in = r < H;
+      row[0] = __builtin_amdgcn_raw_buffer_load_b32(rx, in && has_l ? o - 4 : kOob, 0, 0);
+      row[1] = __builtin_amdgcn_raw_buffer_load_b32(rx, in ? o : kOob, 0, 0);
+      row[2] = __builtin_amdgcn_raw_buffer_load_b32(rx, in && has_r ? o + 4 : kOob, 0, 0);
+    };
+    // bytes s .. s+3 of a row's 12 (s = 4 + dx in 0..8)
+    auto win = [](const uint32_t (&row)[3], int s) -> uint32_t {
+      return (s & 3) == 0 ? row[s >> 2] : __builtin_amdgcn_alignbyte(row[(s >> 2) + 1], row[s >> 2], s & 3);
+    };
+    uint32_t w[5][3], nx[3];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) ld_row(r0 + i, w[i]);
+#pragma unroll 1
+    for (int i = 0; i < AC_RB; ++i) {
+      if (i + 1 < AC_RB) ld_row(r0 + i + 5, nx);
+      const uint32_t u = w[0][1];  // this thread's 4 pixels (rows >= H loaded as zeros)
+      int k = 0;
+#pragma unroll
+      for (int dx = 0; dx <= 4; ++dx) acc[k] = __builtin_amdgcn_udot4(u, win(w[0], 4 + dx), acc[k], false), ++k;
+#pragma unroll
+      for (int dy = 1; dy <= 4; ++dy)
+#pragma unroll
+        for (int dx = -4; dx <= 4; ++dx) acc[k] = __builtin_amdgcn_udot4(u, win(w[dy], 4 + dx), acc[k], false), ++k;
+      acc[41] = __builtin_amdgcn_udot4(u, 0x01010101u, acc[41], false);
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) w[k2][q] = w[k2 + 1][q];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) w[4][q] = nx[q];
+    }
+  }
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < 42; ++i) {
+    const uint32_t s = wave_sum(acc[i]);
+    if (lane == 0) red[wv][i] = (double)s;
+  }
+  __syncthreads();
+  if (tid < 42) partial[(int64_t)blk * 42 + tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+}
+
 }  // namespace tds
 
 using namespace tds;
@@ -156,7 +240,7 @@ using namespace tds;
 int tds_x_autocorr_num_wg(int B, int H, int W) { return x_autocorr_num_wg(B, H, W); }
 
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(x_border_kernel, dim3(82, 8, B), dim3(256), 0, st, x, strips, B, H, W);
+  hipLaunchKernelGGL(x_border_kernel<float>, dim3(82, 8, B), dim3(256), 0, st, x, strips, B, H, W);
   TDS_LAUNCH_CHECK();
 }
 
@@ -181,4 +265,15 @@ void tds_x_moments(const float* x, double* ac_partial, int nwg, double* strips, 
   hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
   TDS_LAUNCH_CHECK();
   tds_x_border(x, strips, B, H, W, st);
+}
+
+// the same moments of uint8 levels (x = levels / 255 is scaled in l1_gram), one launch
+void tds_x_moments_u8(const uint8_t* x, double* ac_partial, int nwg, double* strips, int B, int H, int W,
+                      hipStream_t st) {
+  if (nwg < 1 || nwg != x_autocorr_num_wg(B, H, W)) {
+    tds_launch_fail("x_autocorr_u8: workgroup count does not match the shape (needs W % 4 == 0)");
+    return;
+  }
+  hipLaunchKernelGGL(x_autocorr_u8_kernel, dim3(nwg + 656 * B), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
+  TDS_LAUNCH_CHECK();
 }

@@ -90,15 +90,16 @@ Tensor maxpool2_bwd(const Tensor& gy, const Tensor& idx, int64_t H, int64_t W) {
   return gx;
 }
 
-Tensor upsample_bilinear_u8(const Tensor& src, int64_t H, int64_t W) {
+// levels=True: the rounded uint8 levels (ToTensor's input) instead of level / 255 in fp32
+Tensor upsample_bilinear_u8(const Tensor& src, int64_t H, int64_t W, bool levels) {
   TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.is_contiguous() && src.dim() == 3,
               "tdsa.upsample_bilinear_u8: expected contiguous uint8 [B,h,w] on GPU");
   TORCH_CHECK(src.size(1) >= 1 && src.size(2) >= 1 && src.size(2) <= 256 && src.size(0) <= 65535 && H >= 1 &&
                   W >= 1 && H <= INT32_MAX && W <= INT32_MAX,
               "tdsa.upsample_bilinear_u8: source width must be 1..256 and batch <= 65535");
   c10::DeviceGuard g(src.device());
-  auto dst = at::empty({src.size(0), 1, H, W}, src.options().dtype(at::kFloat));
-  tds_upsample_bilinear_u8(src.data_ptr<uint8_t>(), dst.data_ptr<float>(), (int)src.size(0), (int)src.size(1),
+  auto dst = at::empty({src.size(0), 1, H, W}, src.options().dtype(levels ? at::kByte : at::kFloat));
+  tds_upsample_bilinear_u8(src.data_ptr<uint8_t>(), dst.data_ptr(), levels, (int)src.size(0), (int)src.size(1),
                            (int)src.size(2), (int)H, (int)W, cur_stream(src));
   check_launches("upsample_bilinear_u8");
   return dst;
@@ -406,7 +407,7 @@ TORCH_LIBRARY(tdsa, m) {
   m.def("relu_bwd(Tensor grad, Tensor out) -> Tensor", &relu_bwd);
   m.def("maxpool2_fwd(Tensor x) -> (Tensor, Tensor)", &maxpool2_fwd);
   m.def("maxpool2_bwd(Tensor grad, Tensor idx, int H, int W) -> Tensor", &maxpool2_bwd);
-  m.def("upsample_bilinear_u8(Tensor src, int H, int W) -> Tensor", &upsample_bilinear_u8);
+  m.def("upsample_bilinear_u8(Tensor src, int H, int W, bool levels=False) -> Tensor", &upsample_bilinear_u8);
   m.def(
       "sgd_step_(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] moms, float lr, float weight_decay, float momentum, "
       "float dampening, bool nesterov, bool first_step) -> ()",

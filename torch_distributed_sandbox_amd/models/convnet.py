@@ -15,6 +15,11 @@ Differences from the reference, by design:
   gfx950 plan (``models/convnet_fused.py``) runs the whole network as five
   fused kernels per direction; otherwise the layer-by-layer native ops run
   (``mode='layers'``), and on CPU the PyTorch reference ops.
+* ``forward`` also takes a uint8 batch: the resized images' levels before the
+  reference's ``ToTensor`` (mnist_onegpu.py:50-52), read as ``levels / 255``
+  (``to_image``).  The fused plan folds that scale into conv1 and its batch
+  statistics, so the fp32 image (4x the bytes) is never written or read; the
+  other plans convert first.
 """
 from __future__ import annotations
 
@@ -24,6 +29,15 @@ import torch.nn as nn
 from ..ops import modules as M
 
 IMAGE_SHAPE = (3000, 3000)
+LEVEL_SCALE = 1.0 / 255.0  # fp32(1/255): the scale ToTensor and the upsample kernel apply to uint8 levels
+
+
+def to_image(x: torch.Tensor) -> torch.Tensor:
+    """fp32 image of a uint8 level batch (x * fp32(1/255), as the upsample kernel scales);
+    fp32 batches pass through."""
+    if x.dtype == torch.uint8:
+        return x.float().mul_(torch.tensor(LEVEL_SCALE, dtype=torch.float32).item())
+    return x
 
 
 def fc_in_features(image_shape, channels: int = 32) -> int:
@@ -83,4 +97,4 @@ class ConvNet(nn.Module):
             from . import convnet_fused
 
             return convnet_fused.forward(self, x)
-        return self._forward_layers(x)
+        return self._forward_layers(to_image(x))

@@ -44,7 +44,8 @@ from ..parallel import factored
 def supported(model, x) -> bool:
     if not (x.is_cuda and model.training and torch.is_grad_enabled()):
         return False
-    if x.dim() != 4 or x.shape[1] != 1 or x.dtype != torch.float32:
+    # uint8: ToTensor's levels, x = levels / 255 folded into conv1 (models/convnet.py to_image)
+    if x.dim() != 4 or x.shape[1] != 1 or x.dtype not in (torch.float32, torch.uint8):
         return False
     B, _, H, W = x.shape
     # H % 4: conv2 runs on the pooled P = H/2 grid and pools again; H >= 16: the head's 4-column
@@ -73,7 +74,8 @@ def supported(model, x) -> bool:
 
 
 def input_stats(x):
-    """(asum[42], strips[B*8*82]) fp64 x moments of a [B,1,H,W] fp32 batch, on the current stream."""
+    """(asum[42], strips[B*8*82]) fp64 x moments of a [B,1,H,W] fp32 batch, on the current stream
+    (of the levels for a uint8 batch: l1_gram scales them)."""
     return _ext.ops().l1_input_stats(x.contiguous())
 
 

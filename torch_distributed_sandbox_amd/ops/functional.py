@@ -275,10 +275,15 @@ def cross_entropy(logits, labels, ignore_index: int = -100, label_smoothing: flo
 
 
 # --------------------------------------------------------------------------- data: bilinear u8 upsample
-def upsample_bilinear_u8(src: torch.Tensor, H: int, W: int) -> torch.Tensor:
-    """[B,h,w] uint8 -> [B,1,H,W] float32 in [0,1] (PIL-style bilinear + ToTensor)."""
+def upsample_bilinear_u8(src: torch.Tensor, H: int, W: int, levels: bool = False) -> torch.Tensor:
+    """[B,h,w] uint8 -> [B,1,H,W] float32 in [0,1] (PIL-style bilinear + ToTensor).
+
+    ``levels=True`` returns the rounded uint8 levels instead (the resized PIL image before
+    ToTensor): ``ConvNet`` takes such a batch as ``levels / 255`` and its fused plan folds the
+    1/255 into conv1, so the 4x larger fp32 image is never written or read."""
     if not src.is_cuda:
         x = src.float().unsqueeze(1)
         y = F.interpolate(x, size=(H, W), mode="bilinear", align_corners=False)
-        return y.round_().clamp_(0, 255).div_(255.0)
-    return _ext.ops().upsample_bilinear_u8(src.contiguous(), int(H), int(W))
+        y = y.round_().clamp_(0, 255)
+        return y.to(torch.uint8) if levels else y.div_(255.0)
+    return _ext.ops().upsample_bilinear_u8(src.contiguous(), int(H), int(W), bool(levels))
