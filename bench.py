@@ -95,7 +95,7 @@ def _parser():
                     help="cpu: rehearsal of the launch/exchange path on the torch-ops plan (small --image-size)")
     ap.add_argument("--shared-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (needs --backend gloo); recorded in the JSON")
-    ap.add_argument("--input", default="fp32", choices=["levels", "fp32"],
+    ap.add_argument("--input", default="levels", choices=["levels", "fp32"],
                     help="how each step's batch reaches the model: 'levels' = the resized images' uint8 levels "
                          "(ToTensor's 1/255 folded into conv1 by the fused plan, models/convnet.py to_image), "
                          "'fp32' = the ToTensor image materialised by the upsample kernel")

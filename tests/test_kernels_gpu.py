@@ -173,10 +173,14 @@ def test_sgd(gpu):
         _close(a, b, 1e-6, 1e-6)
 
 
-def test_upsample(gpu):
-    src = torch.randint(0, 256, (3, 28, 28), dtype=torch.uint8, device=gpu)
-    y = _ops().upsample_bilinear_u8(src, 300, 301)
-    ref = F.interpolate(src.float().unsqueeze(1).cpu().double(), size=(300, 301), mode="bilinear",
+@pytest.mark.parametrize("hw,HW", [(28, (300, 301)), (28, (301, 300)), (70, (300, 300)), (70, (37, 301))])
+def test_upsample(gpu, hw, HW):
+    # 28^2: the whole-source kernel (8 rows per workgroup); 70^2 > 4096 px: one row per workgroup
+    src = torch.randint(0, 256, (3, hw, hw), dtype=torch.uint8, device=gpu)
+    y = _ops().upsample_bilinear_u8(src, *HW)
+    lv = _ops().upsample_bilinear_u8(src, *HW, True)
+    assert torch.equal(lv.float() * torch.tensor(1.0 / 255.0, dtype=torch.float32), y)
+    ref = F.interpolate(src.float().unsqueeze(1).cpu().double(), size=HW, mode="bilinear",
                         align_corners=False).round().clamp(0, 255) / 255.0
     # bilinear weights in fp32 vs fp64 may round a half differently: <= 1 LSB
     assert (y.double().cpu() - ref).abs().max().item() <= 1.0 / 255 + 1e-6

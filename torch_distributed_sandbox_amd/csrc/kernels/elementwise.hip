@@ -111,34 +111,21 @@ __global__ void maxpool2_bwd_kernel(const float* __restrict__ gy, const uint8_t*
 // image is read again right away by the layer-1 kernels and can stay in the MALL).  The arithmetic order is exactly the
 // per-pixel formula above, so the result is bit-identical to the scalar form.
 constexpr int kUpsMaxW = 256;
-// U8OUT: the rounded level itself (uint8), i.e. ToTensor's input before its 1/255 -- the fused
-// ConvNet plan folds that scale into conv1 (convnet_fused.hip, x_autocorr.hip).
+constexpr int kUpsImg = 4096;  // sources up to this many pixels are staged whole (28x28 = 784)
+constexpr int kUpsRows = 8;    // output rows per workgroup when the source is staged whole
+
+// one output row Y from the two source rows r0 (y0), r1 (y1) in LDS
 template <bool U8OUT>
-__global__ void __launch_bounds__(256) upsample_bilinear_u8_kernel(const uint8_t* __restrict__ src,
-                                                                   void* __restrict__ dstv, int B, int h, int w,
-                                                                   int H, int W) {
-  __shared__ float rows[2][kUpsMaxW];
-  const int Y = blockIdx.x, b = blockIdx.y;
-  const float sy = (float)h / (float)H, sx = (float)w / (float)W;
-  float fy = ((float)Y + 0.5f) * sy - 0.5f;
-  fy = fminf(fmaxf(fy, 0.f), (float)(h - 1));
-  const int y0 = (int)fy;
-  const int y1 = min(y0 + 1, h - 1);
-  const float ay = fy - (float)y0;
-  const uint8_t* s = src + (int64_t)b * h * w;
-  for (int x = threadIdx.x; x < w; x += blockDim.x) {
-    rows[0][x] = (float)s[y0 * w + x];
-    rows[1][x] = (float)s[y1 * w + x];
-  }
-  __syncthreads();
+__device__ __forceinline__ void ups_row(const float* r0, const float* r1, float ay, void* __restrict__ dstv, int b,
+                                        int Y, int w, int H, int W, float sx) {
   auto lvl = [&](int X) {
     float fx = ((float)X + 0.5f) * sx - 0.5f;
     fx = fminf(fmaxf(fx, 0.f), (float)(w - 1));
     const int x0 = (int)fx;
     const int x1 = min(x0 + 1, w - 1);
     const float ax = fx - (float)x0;
-    const float top = (1.f - ax) * rows[0][x0] + ax * rows[0][x1];
-    const float bot = (1.f - ax) * rows[1][x0] + ax * rows[1][x1];
+    const float top = (1.f - ax) * r0[x0] + ax * r0[x1];
+    const float bot = (1.f - ax) * r1[x0] + ax * r1[x1];
     const float v = (1.f - ay) * top + ay * bot;
     return fminf(fmaxf(rintf(v), 0.f), 255.f);
   };
@@ -152,19 +139,128 @@ __global__ void __launch_bounds__(256) upsample_bilinear_u8_kernel(const uint8_t
       reinterpret_cast<uint32_t*>(d8)[q] = v;
     }
     for (int X = (W4 << 2) + threadIdx.x; X < W; X += blockDim.x) d8[X] = (uint8_t)lvl(X);
-    return;
+  } else {
+    float* d = reinterpret_cast<float*>(dstv) + ((int64_t)b * H + Y) * W;
+    auto pix = [&](int X) { return lvl(X) * (1.f / 255.f); };
+    const bool vec = ((((uintptr_t)d) & 15) == 0);
+    const int W4 = vec ? (W >> 2) : 0;
+    for (int q = threadIdx.x; q < W4; q += blockDim.x) {
+      const int X = q << 2;
+      f32x4 v;
+      v[0] = pix(X); v[1] = pix(X + 1); v[2] = pix(X + 2); v[3] = pix(X + 3);
+      reinterpret_cast<f32x4*>(d)[q] = v;
+    }
+    for (int X = (W4 << 2) + threadIdx.x; X < W; X += blockDim.x) d[X] = pix(X);
   }
-  float* d = reinterpret_cast<float*>(dstv) + ((int64_t)b * H + Y) * W;
-  auto pix = [&](int X) { return lvl(X) * (1.f / 255.f); };
-  const bool vec = ((((uintptr_t)d) & 15) == 0);
+}
+
+__device__ __forceinline__ void ups_vtaps(int Y, int h, float sy, int& y0, int& y1, float& ay) {
+  float fy = ((float)Y + 0.5f) * sy - 0.5f;
+  fy = fminf(fmaxf(fy, 0.f), (float)(h - 1));
+  y0 = (int)fy;
+  y1 = min(y0 + 1, h - 1);
+  ay = fy - (float)y0;
+}
+
+// One workgroup per output row (grid = H x B): the row's two source rows staged in LDS.
+// U8OUT: the rounded level itself (uint8), i.e. ToTensor's input before its 1/255 -- the fused
+// ConvNet plan folds that scale into conv1 (convnet_fused.hip, x_autocorr.hip).
+template <bool U8OUT>
+__global__ void __launch_bounds__(256) upsample_bilinear_u8_kernel(const uint8_t* __restrict__ src,
+                                                                   void* __restrict__ dstv, int B, int h, int w,
+                                                                   int H, int W) {
+  __shared__ float rows[2][kUpsMaxW];
+  const int Y = blockIdx.x, b = blockIdx.y;
+  const float sy = (float)h / (float)H, sx = (float)w / (float)W;
+  int y0, y1;
+  float ay;
+  ups_vtaps(Y, h, sy, y0, y1, ay);
+  const uint8_t* s = src + (int64_t)b * h * w;
+  for (int x = threadIdx.x; x < w; x += blockDim.x) {
+    rows[0][x] = (float)s[y0 * w + x];
+    rows[1][x] = (float)s[y1 * w + x];
+  }
+  __syncthreads();
+  ups_row<U8OUT>(rows[0], rows[1], ay, dstv, b, Y, w, H, W, sx);
+}
+
+// Small sources (h*w <= kUpsImg, the 28x28 MNIST digits): the whole source image staged once per
+// workgroup and kUpsRows output rows per workgroup (grid = ceil(H / kUpsRows) x B); a thread keeps
+// the horizontal taps of its 4 columns in registers for all the rows (the kernel is VALU-bound: one
+// row per workgroup recomputed them per pixel and ran at 38 us for 5 x 3000^2).  Same arithmetic
+// per pixel as ups_row, so the output is bit-identical to the row kernel.
+template <bool U8OUT>
+__global__ void __launch_bounds__(256) upsample_bilinear_u8_img_kernel(const uint8_t* __restrict__ src,
+                                                                       void* __restrict__ dstv, int B, int h, int w,
+                                                                       int H, int W) {
+  __shared__ float img[kUpsImg];
+  const int b = blockIdx.y, Yb = blockIdx.x * kUpsRows;
+  const float sy = (float)h / (float)H, sx = (float)w / (float)W;
+  const uint8_t* s = src + (int64_t)b * h * w;
+  for (int i = threadIdx.x; i < h * w; i += blockDim.x) img[i] = (float)s[i];
+  __syncthreads();
+  const int nr = min(kUpsRows, H - Yb);
+  // rows of this workgroup start 4-byte (u8) / 16-byte (fp32) aligned only when W allows it
+  const bool vec = (W & 3) == 0;
   const int W4 = vec ? (W >> 2) : 0;
   for (int q = threadIdx.x; q < W4; q += blockDim.x) {
-    const int X = q << 2;
-    f32x4 v;
-    v[0] = pix(X); v[1] = pix(X + 1); v[2] = pix(X + 2); v[3] = pix(X + 3);
-    reinterpret_cast<f32x4*>(d)[q] = v;
+    int x0[4], x1[4];
+    float ax[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float fx = ((float)(4 * q + k) + 0.5f) * sx - 0.5f;
+      fx = fminf(fmaxf(fx, 0.f), (float)(w - 1));
+      x0[k] = (int)fx;
+      x1[k] = min(x0[k] + 1, w - 1);
+      ax[k] = fx - (float)x0[k];
+    }
+    for (int r = 0; r < nr; ++r) {
+      int y0, y1;
+      float ay;
+      ups_vtaps(Yb + r, h, sy, y0, y1, ay);
+      const float* r0 = img + y0 * w;
+      const float* r1 = img + y1 * w;
+      float lv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float top = (1.f - ax[k]) * r0[x0[k]] + ax[k] * r0[x1[k]];
+        const float bot = (1.f - ax[k]) * r1[x0[k]] + ax[k] * r1[x1[k]];
+        const float v = (1.f - ay) * top + ay * bot;
+        lv[k] = fminf(fmaxf(rintf(v), 0.f), 255.f);
+      }
+      const int64_t row = (int64_t)b * H + Yb + r;
+      if constexpr (U8OUT) {
+        reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(dstv) + row * W)[q] =
+            (uint32_t)lv[0] | ((uint32_t)lv[1] << 8) | ((uint32_t)lv[2] << 16) | ((uint32_t)lv[3] << 24);
+      } else {
+        f32x4 v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = lv[k] * (1.f / 255.f);
+        reinterpret_cast<f32x4*>(reinterpret_cast<float*>(dstv) + row * W)[q] = v;
+      }
+    }
   }
-  for (int X = (W4 << 2) + threadIdx.x; X < W; X += blockDim.x) d[X] = pix(X);
+  if (W4 * 4 < W) {  // the unvectorised remainder (every column when W % 4 != 0)
+    for (int r = 0; r < nr; ++r) {
+      int y0, y1;
+      float ay;
+      ups_vtaps(Yb + r, h, sy, y0, y1, ay);
+      const float* r0 = img + y0 * w;
+      const float* r1 = img + y1 * w;
+      for (int X = W4 * 4 + threadIdx.x; X < W; X += blockDim.x) {
+        float fx = ((float)X + 0.5f) * sx - 0.5f;
+        fx = fminf(fmaxf(fx, 0.f), (float)(w - 1));
+        const int a0 = (int)fx, a1 = min(a0 + 1, w - 1);
+        const float a = fx - (float)a0;
+        const float top = (1.f - a) * r0[a0] + a * r0[a1];
+        const float bot = (1.f - a) * r1[a0] + a * r1[a1];
+        const float v = fminf(fmaxf(rintf((1.f - ay) * top + ay * bot), 0.f), 255.f);
+        const int64_t o = ((int64_t)b * H + Yb + r) * W + X;
+        if constexpr (U8OUT) reinterpret_cast<uint8_t*>(dstv)[o] = (uint8_t)v;
+        else reinterpret_cast<float*>(dstv)[o] = v * (1.f / 255.f);
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------- SGD over a tensor list
@@ -352,10 +448,17 @@ void tds_upsample_bilinear_u8(const uint8_t* src, void* dst, bool u8_out, int B,
     tds_launch_fail("upsample_bilinear_u8: unsupported shape");
     return;
   }
-  if (u8_out)
+  if (h * w <= kUpsImg) {
+    const dim3 grid((H + kUpsRows - 1) / kUpsRows, B);
+    if (u8_out)
+      hipLaunchKernelGGL(upsample_bilinear_u8_img_kernel<true>, grid, dim3(256), 0, st, src, dst, B, h, w, H, W);
+    else
+      hipLaunchKernelGGL(upsample_bilinear_u8_img_kernel<false>, grid, dim3(256), 0, st, src, dst, B, h, w, H, W);
+  } else if (u8_out) {
     hipLaunchKernelGGL(upsample_bilinear_u8_kernel<true>, dim3(H, B), dim3(256), 0, st, src, dst, B, h, w, H, W);
-  else
+  } else {
     hipLaunchKernelGGL(upsample_bilinear_u8_kernel<false>, dim3(H, B), dim3(256), 0, st, src, dst, B, h, w, H, W);
+  }
   TDS_LAUNCH_CHECK();
 }
 void tds_sgd_multi(const SgdChunkTable& tab, float lr, float wd, float momentum, float dampening, int nesterov,
