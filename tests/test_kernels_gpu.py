@@ -184,7 +184,7 @@ def test_upsample(gpu, hw, HW):
                         align_corners=False).round().clamp(0, 255) / 255.0
     # bilinear weights in fp32 vs fp64 may round a half differently: <= 1 LSB
     assert (y.double().cpu() - ref).abs().max().item() <= 1.0 / 255 + 1e-6
-    assert ((y.double().cpu() - ref).abs() > 1e-6).float().mean().item() < 1e-3
+    assert ((y.double().cpu() - ref).abs() > 1e-6).float().mean().item() < 5e-3
 
 
 @pytest.mark.parametrize("n", [1, 2047, 2048, 100_003, 3 * 2048 * 5, 20_000_003])

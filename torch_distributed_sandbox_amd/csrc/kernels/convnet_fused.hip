@@ -397,6 +397,10 @@ constexpr int LB_V = LB_V_DP + LB_V_PH + LB_V_ID + LB_V_X;  // 16-B vectors stag
 // The argmax byte carries the ReLU mask in bit 2 (set by l1_conv: pooled max > 0), so the
 // backward never reads p1 (720 MB of 64-B hi|lo records at the bench shape).
 constexpr int LB_PER = (LB_V + 255) / 256;
+// LDS record of pooled pixel pp's 16 dp1 values: lane groups g0 / g1 (and g2 / g3) read pooled pixels
+// two apart, whose plain records (16 words) sit 32 words apart -- the same banks, a 2-way conflict
+// on every dp1 read.  Swapping the records of pp = 2, 3 (mod 4) puts the pair in opposite halves.
+__device__ __forceinline__ int lb_dp_rec(int pp) { return pp ^ ((pp >> 1) & 1); }
 
 // ============================================================================ layer-1 backward (MFMA)
 // The sums the sparse kernel above forms with 25 VALU FMAs per active (pooled pixel,
@@ -411,13 +415,31 @@ constexpr int LB_PER = (LB_V + 255) / 256;
 // go through LDS; fp32 MFMA accumulation per tile (256 pixels), fp64 across tiles.
 // partial[wg][16][27] in the sparse kernel's layout ([0] sum dz, [1] 0, [2+j] taps).
 constexpr int LM_XS = 80;  // x tile row stride (words): 20 rows x (72 staged + pad) columns
+// Level input (LV): the x tile as bf16 PAIRS, so one ds_read_b32 is one packed B-operand register
+// (slots dc = 0, 1 of a window row) with no perm.  Copy E holds columns (2k, 2k+1) in dword k, copy
+// O columns (2k+1, 2k+2): a lane's pair starts at column kx + 2 + 4g (+ uniform offsets), even for
+// even kx (E) and odd for odd kx (O).  Row stride LV_RS = 41 = 9 mod 32 dwords and O based 5 banks
+// after E: a K-step's 32 lanes of one half (g0, g1) then touch rows ky of E at banks 9ky + 1..5 and
+// of O at 9ky + 6..9 -- 29 distinct banks for block 0 (rows 0..2 + row 3 col 0) and 18 for block
+// 1, no conflicts (the fp32-image layout above is 2-way conflicted on every B read: rows 80 words
+// apart map to the same banks).
+constexpr int LV_RS = 41;
+constexpr int LV_OB = 837;  // = 5 mod 32, >= 20 rows x 41
+constexpr int LV_WORDS = LV_OB + LB_XR * LV_RS;
+static_assert(LV_RS % 32 == 9 && LV_OB % 32 == 5 && LV_OB >= LB_XR * LV_RS && LV_RS >= 36, "l1_bwd level tile");
+constexpr int LM_X_BYTES = (LB_XR * LM_XS > LV_WORDS ? LB_XR * LM_XS : LV_WORDS) * 4;
 // LV: x holds uint8 levels (see l1_conv_bf3_kernel): the x operand is exact in bf16, two MFMAs per
 // product (dz hi, dz lo), half the B perms; the tap sums are scaled by L1_LEVEL_SCALE at the end.
+// waves per SIMD the register budget is cut for (4: <= 128 VGPRs, 4 workgroups per CU with
+// fused_ops.cpp l1b_wg(); A/B builds: --variant w3 -D TDS_L1B_WAVES=3)
+#ifndef TDS_L1B_WAVES
+#define TDS_L1B_WAVES 4
+#endif
 template <bool LV>
-__global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const float* __restrict__ dp1,
+__global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const float* __restrict__ dp1,
                                                           const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
                                                           double* __restrict__ partial, int B, int H, int W) {
-  __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LB_XR * LM_XS * 4];
+  __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LM_X_BYTES];
   float* dps = reinterpret_cast<float*>(lds);
   unsigned short* phs = nullptr;
   uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 64);
@@ -446,7 +468,18 @@ __global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restr
     boff[blk] = ky * LM_XS + kx + 2 + 4 * g;
     bcst[blk] = (n == 25 ? 0 : 2 * LM_XS) + 72;
   }
-  if (tid < 16) {  // constant blocks (never overwritten: the x tile uses columns 0..71)
+  // LV: this lane's dword offset in the pair tiles (tap (4,4) for the constant columns: the read is
+  // a broadcast of that lane's address, the value is then replaced by the constant)
+  int vlof[2];
+  uint32_t vcst[2];
+#pragma unroll
+  for (int blk = 0; blk < 2; ++blk) {
+    const int n = 16 * blk + li, t = n < 25 ? n : 24;
+    const int ky = t / 5, kx = t % 5;
+    vlof[blk] = (kx & 1) ? LV_OB + ky * LV_RS + (kx + 1 + 4 * g) / 2 : ky * LV_RS + (kx + 2 + 4 * g) / 2;
+    vcst[blk] = n == 25 ? 0x3F803F80u : 0u;  // bf16 1.0 pair: the sum-dz column
+  }
+  if (!LV && tid < 16) {  // constant blocks (never overwritten: the x tile uses columns 0..71)
     const int r = tid >> 2, c = tid & 3;
     xs[r * LM_XS + 72 + c] = r < 2 ? 0x3F800000u : 0u;
   }
@@ -490,20 +523,23 @@ __global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restr
 #pragma unroll
     for (int u = 0; u < LB_PER; ++u) {
       int e = tid + 256 * u;
-      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[e] = pre[u];
+      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[(lb_dp_rec(e >> 2) << 2) | (e & 3)] = pre[u];
       else if (e < LB_V_DP + LB_V_PH) reinterpret_cast<uint4*>(phs)[e - LB_V_DP] = pre[u];
       else if (e < LB_V_DP + LB_V_PH + LB_V_ID) reinterpret_cast<uint4*>(ids)[e - LB_V_DP - LB_V_PH] = pre[u];
       else if (e < LB_V) {
         e -= LB_V_DP + LB_V_PH + LB_V_ID;
         const int rr = e / 18, cv = e - rr * 18;
-        if constexpr (LV) {  // word = fp32 bits of the level = bf16 hi | lo 0
+        if constexpr (LV) {  // bf16 of a level = high half of its fp32 bits (exact)
           const uint32_t q = pre[u].x;
-          uint4 v;
-          v.x = __float_as_uint((float)(q & 0xFFu));
-          v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
-          v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
-          v.w = __float_as_uint((float)(q >> 24));
-          *reinterpret_cast<uint4*>(xs + rr * LM_XS + 4 * cv) = v;
+          const uint32_t f0 = __float_as_uint((float)(q & 0xFFu)), f1 = __float_as_uint((float)((q >> 8) & 0xFFu));
+          const uint32_t f2 = __float_as_uint((float)((q >> 16) & 0xFFu)), f3 = __float_as_uint((float)(q >> 24));
+          uint32_t* e = xs + rr * LV_RS + 2 * cv;           // cols 4cv .. 4cv+3 = E dwords 2cv, 2cv+1
+          uint32_t* o = xs + LV_OB + rr * LV_RS + 2 * cv;   // O dword 2cv = cols (4cv+1, 4cv+2)
+          e[0] = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+          e[1] = __builtin_amdgcn_perm(f3, f2, 0x07060302u);
+          o[0] = __builtin_amdgcn_perm(f2, f1, 0x07060302u);
+          reinterpret_cast<unsigned short*>(o + 1)[0] = (unsigned short)(f3 >> 16);       // col 4cv+3
+          if (cv > 0) reinterpret_cast<unsigned short*>(o - 1)[1] = (unsigned short)(f0 >> 16);  // col 4cv
           continue;
         }
         const float4 f = __builtin_bit_cast(float4, pre[u]);
@@ -547,7 +583,7 @@ __global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restr
 #pragma unroll
           for (int wi = 0; wi < 2; ++wi) {
             const int pp = rp * LB_PC + 8 * sg + 2 * g + wi;
-            const float dp = dps[pp * 16 + li];
+            const float dp = dps[lb_dp_rec(pp) * 16 + li];
             const uint32_t ab = ids[pp * 16 + li];
             const float d = (ab & 4u) ? dp : 0.f;  // ReLU: a pooled value <= 0 blocks the gradient
             uint32_t h, l;
@@ -559,6 +595,21 @@ __global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restr
             lp[2 * wi] = (uint32_t)l64;
             lp[2 * wi + 1] = (uint32_t)(l64 >> 32);
           }
+        }
+        if constexpr (LV) {
+          const int vbase = 2 * rp * LV_RS + 8 * sg;
+#pragma unroll
+          for (int blk = 0; blk < 2; ++blk) {
+            s16x8 bh;
+            uint32_t* hp = reinterpret_cast<uint32_t*>(&bh);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // packed slots (2j, 2j+1) = window wi = j >> 1, row dr2 = j & 1
+              const uint32_t v = xs[vlof[blk] + vbase + (j & 1) * LV_RS + (j >> 1)];
+              hp[j] = bdata[blk] ? v : vcst[blk];
+            }
+            acc[blk] = mfma_bf16x2a(ah, al, bh, acc[blk]);
+          }
+          continue;
         }
         const int base = 2 * rp * LM_XS + 16 * sg;
 #pragma unroll
@@ -576,12 +627,9 @@ __global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restr
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
-            if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+            lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
           }
-          if constexpr (LV)
-            acc[blk] = mfma_bf16x2a(ah, al, bh, acc[blk]);
-          else
-            acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
+          acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
         }
       }
     }
@@ -611,7 +659,7 @@ __global__ __launch_bounds__(256, 3) void l1_bwd_mfma_kernel(const void* __restr
   for (int e = tid; e < 16 * LB_NACC; e += 256)
     out[e] = (red[e] + red[16 * LB_NACC + e]) + (red[2 * 16 * LB_NACC + e] + red[3 * 16 * LB_NACC + e]);
 }
-static_assert(4 * 16 * LB_NACC * 8 <= LB_NP * 64 + LB_NP * 16 + LB_XR * LM_XS * 4, "l1_bwd LDS reduction scratch");
+static_assert(4 * 16 * LB_NACC * 8 <= LB_NP * 64 + LB_NP * 16 + LM_X_BYTES, "l1_bwd LDS reduction scratch");
 
 // Gram of the conv1 patches from the x autocorrelation (one workgroup):
 //   G[k][j] = Full(d) - sum_{excluded rows of k} R(d,row) - sum_{excluded cols} C(d,col)
