@@ -82,10 +82,15 @@ class SyntheticMNIST:
 
 class DeviceUpsampleLoader:
     """``DataLoader(dataset, batch_size, sampler/shuffle)`` equivalent that yields
-    ``(images[B,1,H,W] f32 on device, labels[B] i64 on device)``."""
+    ``(images[B,1,H,W] f32 on device, labels[B] i64 on device)``.
+
+    ``levels=True`` yields the resized images' uint8 levels instead of the ToTensor image (the
+    ConvNet reads them as ``levels / 255``, models/convnet.py ``to_image``; its fused plan never
+    materialises the fp32 image)."""
 
     def __init__(self, dataset: SyntheticMNIST, batch_size: int, image_shape, device, sampler=None,
-                 shuffle: bool = False, seed: int = 0, drop_last: bool = False):
+                 shuffle: bool = False, seed: int = 0, drop_last: bool = False, levels: bool = False):
+        self.levels = levels
         self.dataset, self.batch_size = dataset, batch_size
         self.H, self.W = image_shape
         self.device = torch.device(device)
@@ -121,7 +126,7 @@ class DeviceUpsampleLoader:
             if self.device.type == "cuda":
                 src = src.pin_memory().to(self.device, non_blocking=True)
                 lab = lab.pin_memory().to(self.device, non_blocking=True)
-            yield TF.upsample_bilinear_u8(src, self.H, self.W), lab
+            yield TF.upsample_bilinear_u8(src, self.H, self.W, levels=self.levels), lab
 
 
 def synthetic_batch(batch_size: int, image_shape, device, seed: int = 0, num_classes: int = 10,

@@ -39,6 +39,9 @@ def add_common_args(p: argparse.ArgumentParser) -> argparse.ArgumentParser:
     p.add_argument("--dataset-size", default=60000, type=int, help="synthetic MNIST size (reference: 60000)")
     p.add_argument("--log-interval", default=100, type=int)
     p.add_argument("--mode", default="auto", choices=["auto", "fused", "layers"], help="ConvNet execution plan")
+    p.add_argument("--input", default="levels", choices=["levels", "fp32"],
+                   help="batches as the resized images' uint8 levels (ToTensor's 1/255 folded into conv1) or as "
+                        "the materialised fp32 ToTensor image")
     p.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"])
     p.add_argument("--checkpoint", default="", help="save a checkpoint here at the end (rank 0)")
     p.add_argument("--resume", default="", help="resume from this checkpoint")
@@ -106,11 +109,12 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
     if args.resume:
         _, start_epoch, _ = checkpoint.load(args.resume, model, optimizer, map_location=device)
     dataset = SyntheticMNIST(size=args.dataset_size)
+    levels = getattr(args, "input", "levels") == "levels"
     if distributed:
         sampler = DistributedSampler(len(dataset), num_replicas=world, rank=rank)
-        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, sampler=sampler)
+        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, sampler=sampler, levels=levels)
     else:
-        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, shuffle=True)
+        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, shuffle=True, levels=levels)
 
     start = datetime.now()
     total_step = len(loader)
