@@ -30,3 +30,16 @@ def test_convnet_levels_input_equals_image_input():
     out_l = m(lv)
     out_f = m(to_image(lv))
     assert torch.equal(out_l, out_f)
+
+
+def test_layer1_backward_level_lds_layout():
+    """The level layer-1 backward's LDS image (tools/micro/l1b_lds_check.py): every B-operand read
+    returns its packed pair and no lane half hits two addresses in one bank."""
+    import importlib.util
+    import os
+
+    path = os.path.join(os.path.dirname(__file__), "..", "tools", "micro", "l1b_lds_check.py")
+    spec = importlib.util.spec_from_file_location("l1b_lds_check", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.main()
