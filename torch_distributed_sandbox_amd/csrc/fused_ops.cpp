@@ -590,7 +590,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   hipStream_t st = stream_of(x);
   const int nwg = l1b_wg(), rows = tds_l1_bwd_rows(nwg);
   auto partial = at::empty({(int64_t)rows * 16 * 27}, x.options().dtype(at::kDouble));
-  tds_l1_bwd(x.data_ptr(), levels, dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(),
+  static const bool pairs = [] {  // the bf16-pair LDS layout (convnet_fused.hip PAIRS), opt-in
+    const char* e = std::getenv("TDS_L1B_PAIRS");
+    return e && e[0] == '1';
+  }();
+  tds_l1_bwd(x.data_ptr(), levels, pairs, dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(),
              w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);

@@ -400,7 +400,8 @@ constexpr int LB_PER = (LB_V + 255) / 256;
 // LDS record of pooled pixel pp's 16 dp1 values: lane groups g0 / g1 (and g2 / g3) read pooled pixels
 // two apart, whose plain records (16 words) sit 32 words apart -- the same banks, a 2-way conflict
 // on every dp1 read.  Swapping the records of pp = 2, 3 (mod 4) puts the pair in opposite halves.
-__device__ __forceinline__ int lb_dp_rec(int pp) { return pp ^ ((pp >> 1) & 1); }
+template <bool SW>
+__device__ __forceinline__ int lb_dp_rec(int pp) { return SW ? pp ^ ((pp >> 1) & 1) : pp; }
 
 // ============================================================================ layer-1 backward (MFMA)
 // The sums the sparse kernel above forms with 25 VALU FMAs per active (pooled pixel,
@@ -431,11 +432,16 @@ constexpr int LM_X_BYTES = (LB_XR * LM_XS > LV_WORDS ? LB_XR * LM_XS : LV_WORDS)
 // LV: x holds uint8 levels (see l1_conv_bf3_kernel): the x operand is exact in bf16, two MFMAs per
 // product (dz hi, dz lo), half the B perms; the tap sums are scaled by L1_LEVEL_SCALE at the end.
 // waves per SIMD the register budget is cut for (4: <= 128 VGPRs, 4 workgroups per CU with
-// fused_ops.cpp l1b_wg(); A/B builds: --variant w3 -D TDS_L1B_WAVES=3)
+// fused_ops.cpp l1b_wg(); 3: <= 168, the measured configuration -- the compiler then keeps the
+// default variants at 124-126 VGPRs, so 4 workgroups still fit a CU)
 #ifndef TDS_L1B_WAVES
-#define TDS_L1B_WAVES 4
+#define TDS_L1B_WAVES 3
 #endif
-template <bool LV>
+// PAIRS (level input only; TDS_L1B_PAIRS=1 at run time, fused_ops.cpp): the conflict-free bf16-pair
+// x tile and the swizzled dp1 records below.  Opt-in until timed on MI355X: it compiles to 144
+// VGPRs under the default budget (3 workgroups per CU: run it with TDS_L1B_PER_CU=3) and spills a
+// few dwords at 128.
+template <bool LV, bool PAIRS>
 __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const float* __restrict__ dp1,
                                                           const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
                                                           double* __restrict__ partial, int B, int H, int W) {
@@ -479,7 +485,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
     vlof[blk] = (kx & 1) ? LV_OB + ky * LV_RS + (kx + 1 + 4 * g) / 2 : ky * LV_RS + (kx + 2 + 4 * g) / 2;
     vcst[blk] = n == 25 ? 0x3F803F80u : 0u;  // bf16 1.0 pair: the sum-dz column
   }
-  if (!LV && tid < 16) {  // constant blocks (never overwritten: the x tile uses columns 0..71)
+  if (!(LV && PAIRS) && tid < 16) {  // constant blocks (never overwritten: the x tile uses columns 0..71)
     const int r = tid >> 2, c = tid & 3;
     xs[r * LM_XS + 72 + c] = r < 2 ? 0x3F800000u : 0u;
   }
@@ -523,12 +529,22 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
 #pragma unroll
     for (int u = 0; u < LB_PER; ++u) {
       int e = tid + 256 * u;
-      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[(lb_dp_rec(e >> 2) << 2) | (e & 3)] = pre[u];
+      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[(lb_dp_rec<PAIRS>(e >> 2) << 2) | (e & 3)] = pre[u];
       else if (e < LB_V_DP + LB_V_PH) reinterpret_cast<uint4*>(phs)[e - LB_V_DP] = pre[u];
       else if (e < LB_V_DP + LB_V_PH + LB_V_ID) reinterpret_cast<uint4*>(ids)[e - LB_V_DP - LB_V_PH] = pre[u];
       else if (e < LB_V) {
         e -= LB_V_DP + LB_V_PH + LB_V_ID;
         const int rr = e / 18, cv = e - rr * 18;
+        if constexpr (LV && !PAIRS) {  // word = fp32 bits of the level = bf16 hi | lo 0
+          const uint32_t q = pre[u].x;
+          uint4 v;
+          v.x = __float_as_uint((float)(q & 0xFFu));
+          v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
+          v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
+          v.w = __float_as_uint((float)(q >> 24));
+          *reinterpret_cast<uint4*>(xs + rr * LM_XS + 4 * cv) = v;
+          continue;
+        }
         if constexpr (LV) {  // bf16 of a level = high half of its fp32 bits (exact)
           const uint32_t q = pre[u].x;
           const uint32_t f0 = __float_as_uint((float)(q & 0xFFu)), f1 = __float_as_uint((float)((q >> 8) & 0xFFu));
@@ -583,7 +599,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
 #pragma unroll
           for (int wi = 0; wi < 2; ++wi) {
             const int pp = rp * LB_PC + 8 * sg + 2 * g + wi;
-            const float dp = dps[lb_dp_rec(pp) * 16 + li];
+            const float dp = dps[lb_dp_rec<PAIRS>(pp) * 16 + li];
             const uint32_t ab = ids[pp * 16 + li];
             const float d = (ab & 4u) ? dp : 0.f;  // ReLU: a pooled value <= 0 blocks the gradient
             uint32_t h, l;
@@ -596,7 +612,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
             lp[2 * wi + 1] = (uint32_t)(l64 >> 32);
           }
         }
-        if constexpr (LV) {
+        if constexpr (LV && PAIRS) {
           const int vbase = 2 * rp * LV_RS + 8 * sg;
 #pragma unroll
           for (int blk = 0; blk < 2; ++blk) {
@@ -627,9 +643,12 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
-            lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+            if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
           }
-          acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
+          if constexpr (LV)  // levels are exact in bf16: lo = 0
+            acc[blk] = mfma_bf16x2a(ah, al, bh, acc[blk]);
+          else
+            acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
         }
       }
     }
@@ -901,15 +920,18 @@ void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, c
 
 int tds_l1_bwd_rows(int nwg) { return nwg; }
 
-void tds_l1_bwd(const void* x, bool levels, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1,
-                const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st) {
+void tds_l1_bwd(const void* x, bool levels, bool pairs, const float* dp1, const void* p1, const uint8_t* idx1,
+                const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st) {
   (void)w1;
   (void)b1;
-  if (levels)
-    hipLaunchKernelGGL(l1_bwd_mfma_kernel<true>, dim3(nwg), dim3(256), 0, st, x, dp1,
+  if (levels && pairs)
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, true>), dim3(nwg), dim3(256), 0, st, x, dp1,
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
+  else if (levels)
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, false>), dim3(nwg), dim3(256), 0, st, x, dp1,
                        reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   else
-    hipLaunchKernelGGL(l1_bwd_mfma_kernel<false>, dim3(nwg), dim3(256), 0, st, x, dp1,
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<false, false>), dim3(nwg), dim3(256), 0, st, x, dp1,
                        reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   TDS_LAUNCH_CHECK();
 }

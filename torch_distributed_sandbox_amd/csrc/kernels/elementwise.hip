@@ -8,6 +8,8 @@
 //
 // All kernels are wave64, 16-byte vectorised where the layout allows, grid-capped
 // at ~2048 blocks with grid-stride loops (Guideline 11).
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -448,7 +450,13 @@ void tds_upsample_bilinear_u8(const uint8_t* src, void* dst, bool u8_out, int B,
     tds_launch_fail("upsample_bilinear_u8: unsupported shape");
     return;
   }
-  if (h * w <= kUpsImg) {
+  // whole-source kernel: opt-in (TDS_UPS_IMG=1) until timed on MI355X -- its first form (8 rows per
+  // workgroup without the hoisted taps) measured 44 us vs 38 us for the row kernel
+  static const bool img = [] {
+    const char* e = std::getenv("TDS_UPS_IMG");
+    return e && e[0] == '1';
+  }();
+  if (img && h * w <= kUpsImg) {
     const dim3 grid((H + kUpsRows - 1) / kUpsRows, B);
     if (u8_out)
       hipLaunchKernelGGL(upsample_bilinear_u8_img_kernel<true>, grid, dim3(256), 0, st, src, dst, B, h, w, H, W);

@@ -127,8 +127,8 @@ void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n,
                             float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
                             float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
-void tds_l1_bwd(const void* x, bool levels, const float* dp1, const void* p1, const uint8_t* idx1, const float* w1,
-                const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st);
+void tds_l1_bwd(const void* x, bool levels, bool pairs, const float* dp1, const void* p1, const uint8_t* idx1,
+                const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);
