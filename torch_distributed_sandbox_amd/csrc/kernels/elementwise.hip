@@ -450,11 +450,12 @@ void tds_upsample_bilinear_u8(const uint8_t* src, void* dst, bool u8_out, int B,
     tds_launch_fail("upsample_bilinear_u8: unsupported shape");
     return;
   }
-  // whole-source kernel: opt-in (TDS_UPS_IMG=1) until timed on MI355X -- its first form (8 rows per
-  // workgroup without the hoisted taps) measured 44 us vs 38 us for the row kernel
+  // whole-source kernel for small sources: 31.0 us vs 37.6 us for the row kernel at 5 x 3000^2, bench
+  // 2.891 / 2.899 vs 2.915 / 2.929 ms per step same box (tools/gpu_sessions/r3_s23.sh; its first form,
+  // without the hoisted taps, measured 44 us).  TDS_UPS_IMG=0 selects the row kernel (A/B only).
   static const bool img = [] {
     const char* e = std::getenv("TDS_UPS_IMG");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   if (img && h * w <= kUpsImg) {
     const dim3 grid((H + kUpsRows - 1) / kUpsRows, B);
