@@ -34,14 +34,20 @@ driver's 600 s lease):
   ``--spawn-timeout`` (default 570 s);
 * on any failure exactly one JSON line still comes out, with ``"value": null``,
   ``"status": "failed"``, the failing rank, its error and the exit status;
-* fallback (``--fallback``, default on when no ``--backend`` was given): if the
-  ``rccl-native`` attempt fails on any rank, all ranks agree through the
-  rendezvous store, tear it down and run once more on torch's ProcessGroupNCCL
-  (RCCL) with the plain bucket all-reduce, no CU split -- inside the same
-  processes (nothing is re-exec'd), labelled ``"backend": "rccl (fallback:
-  <reason>)"``.  A self-spawned job whose rank crashed is re-spawned once the
-  same way, with fresh child processes, by the parent (which never touched the
-  GPU).
+* preflight (world > 1): before the warmup, every collective the step will use
+  (buffer broadcast, bucket all-reduces, the fc path's all-gathers / grouped
+  point-to-point exchanges at their real sizes) runs once on the live
+  communicator with a bounded wait; times and bus bandwidths are reported in
+  ``config.preflight`` -- a broken link fails the attempt there, named;
+* fallback tiers (``--fallback``, default on when no ``--backend`` was given):
+  if an attempt fails on any rank, all ranks agree through the rendezvous store,
+  tear it down and run again inside the same processes (nothing is re-exec'd):
+  1. ``rccl-native`` + CU split + the fc exchange picked by ``auto``;
+  2. torch's ProcessGroupNCCL (RCCL), no CU split, the SAME fc exchange;
+  3. torch's ProcessGroupNCCL with the plain 720 MB bucket all-reduce;
+  labelled ``"backend": "rccl (fallback: <reason>)"`` and ``"tier": "k/n"``.  A
+  self-spawned job whose rank crashed is re-spawned once from tier 2, with fresh
+  child processes, by the parent (which never touched the GPU).
 """
 from __future__ import annotations
 
@@ -116,6 +122,14 @@ def _parser():
                     help="rendezvous, communicator init and per-collective timeout (s)")
     ap.add_argument("--deadline", type=float, default=540.0,
                     help="a rank still running this long after its start prints the failure record and exits (s)")
+    ap.add_argument("--preflight", action=argparse.BooleanOptionalAction, default=True,
+                    help="world > 1: before the warmup, run every collective the step uses once on the live "
+                         "communicator, each with a bounded wait (--preflight-timeout); the times and bus "
+                         "bandwidths go to config.preflight")
+    ap.add_argument("--preflight-timeout", type=float, default=60.0)
+    ap.add_argument("--step-times", action="store_true",
+                    help="record each timed step's GPU time with events (config.step_ms; diagnostics)")
+    ap.add_argument("--lr", type=float, default=1e-4, help="SGD learning rate (reference: 1e-4)")
     ap.add_argument("--fallback", action=argparse.BooleanOptionalAction, default=None,
                     help="after a failed rccl-native attempt, run once more on torch's RCCL process group with "
                          "the plain bucket all-reduce (default: on unless --backend is given)")
@@ -163,7 +177,9 @@ def _spawn_ranks(args, argv) -> int:
     fallback = args.fallback if args.fallback is not None else args.backend is None
     plans = [(list(argv), None)]
     if fallback and args.device == "cuda":
-        plans.append((list(argv) + ["--backend", "rccl", "--grad-exchange", "allreduce", "--no-fallback"], "retry"))
+        # torch's RCCL process group, no CU split, same fc path; its own in-process fallback is
+        # the plain bucket all-reduce
+        plans.append((list(argv) + ["--backend", "rccl", "--reserve-cus", "0", "--fallback"], "retry"))
     fail = None
     for k, (av, label) in enumerate(plans):
         remaining = args.spawn_timeout - (time.time() - _T_START)
@@ -221,6 +237,57 @@ def _allreduce_probe(tdist, device, world, on_gpu):
                     "busbw_GBps": round(2 * (world - 1) / world * nbytes / dt / 1e9, 2)})
         del t
     return out
+
+
+_BUS = {  # bytes on the busiest link per byte counted (nccl-tests "busbw" conventions)
+    "all_reduce": lambda w: 2.0 * (w - 1) / w,   # nbytes = the buffer
+    "all_gather": lambda w: (w - 1) / w,         # nbytes = the gathered output
+    "broadcast": lambda w: 1.0,
+    "sendrecv": lambda w: 1.0,                   # nbytes = what one peer link carries
+}
+
+
+def _preflight(ddp, tdist, device, world: int, rank: int, rows: int, timeout_s: float):
+    """Run every collective the step will use once (``DistributedDataParallel.preflight``: the
+    buffer broadcast, the reducer's bucket all-reduces, the fc path's gathers / point-to-point
+    exchanges at their real sizes) on the live communicator and its streams, before any model
+    work.  Each gets a bounded wait: its completion event is polled on the host and a collective
+    still running after ``timeout_s`` raises, so a broken link, a missing peer or a collective
+    the backend cannot run fails the attempt here -- named -- instead of mid-warmup.  Returns
+    [{"op", "MB", "ms", "busbw_GBps"}] (the second of two runs of each; the first pays RCCL's
+    lazy channel setup) and the fc path."""
+    from torch_distributed_sandbox_amd.utils import fault
+
+    on_gpu = device.type == "cuda"
+    out = []
+
+    def wait_bounded(name, work, t0):
+        if work is not None:
+            work.wait()  # RCCL: the current stream waits on the device; gloo/host: on the host
+        if not on_gpu:
+            return
+        ev = torch.cuda.Event()
+        ev.record()
+        while not ev.query():
+            if time.perf_counter() - t0 > timeout_s:
+                raise TimeoutError(f"preflight: {name} did not complete within {timeout_s:.0f} s on rank {rank}")
+            time.sleep(2e-4)
+
+    def timed(name, nbytes, kind, issue):
+        best = None
+        for _ in range(2):
+            fault.maybe_inject_bench(rank, "preflight")
+            t0 = time.perf_counter()
+            wait_bounded(name, issue(), t0)
+            best = time.perf_counter() - t0
+        out.append({"op": name, "MB": round(nbytes / 1e6, 3), "ms": round(best * 1e3, 3),
+                    "busbw_GBps": round(_BUS[kind](world) * nbytes / best / 1e9, 2)})
+
+    info = ddp.preflight(rows, timed)
+    t0 = time.perf_counter()
+    tdist.barrier()
+    out.append({"op": "barrier", "MB": 0.0, "ms": round((time.perf_counter() - t0) * 1e3, 3), "busbw_GBps": None})
+    return out, info["fc_path"]
 
 
 def main(argv=None) -> int:
@@ -305,11 +372,15 @@ def _run_attempts(args, world: int, rank: int, phase):
     if os.environ.get("TDS_BENCH_FALLBACK_REASON"):
         label = f"{backend} (fallback: {os.environ['TDS_BENCH_FALLBACK_REASON']})"
     attempts = [(backend, args.grad_exchange, args.reserve_cus, label)]
-    # the conservative stack: torch's own process group (RCCL on the GPU, gloo on a CPU
-    # rehearsal), plain bucket all-reduce, no CU split
+    # fallback tiers: torch's own process group (RCCL on the GPU, gloo on a CPU rehearsal)
+    # with no CU split, first keeping the fc gradient path (the zero-suppressed exchange runs on
+    # ProcessGroupNCCL's all_gather_into_tensor / batch_isend_irecv too), then -- last resort --
+    # the plain 720 MB bucket all-reduce
     plain = "rccl" if on_gpu else "gloo"
-    if fallback and world > 1 and backend != plain:
-        attempts.append((plain, "allreduce", 0, None))
+    if fallback and world > 1:
+        for tier in ((plain, args.grad_exchange, 0, None), (plain, "allreduce", 0, None)):
+            if all((a[0], a[1]) != tier[:2] for a in attempts):
+                attempts.append(tier)
     dist_needed = world > 1 or args.grad_exchange in ("activations", "sharded", "chunked")
     store = _make_store(args, rank, world) if dist_needed else None
     # a collective that stalls raises (after --pg-timeout) instead of killing the rank, so the
@@ -329,6 +400,8 @@ def _run_attempts(args, world: int, rank: int, phase):
             if last:
                 raise
             del e
+        if rec is not None:
+            rec["config"]["tier"] = f"{k + 1}/{len(attempts)}"
         if store is None or len(attempts) == 1:
             return rec
         # every rank reports its attempt; all take the same decision
@@ -362,6 +435,7 @@ def _teardown(abort: bool) -> None:
 
     if not tdist.is_initialized():
         return
+    split = tdist.comm_cus() > 0
     if abort:
         comm, kind = native_comm_of(None)
         if kind == "rccl":
@@ -369,6 +443,11 @@ def _teardown(abort: bool) -> None:
     else:
         tdist.barrier()
     tdist.destroy_process_group()
+    if split:
+        # the communicator's CU-masked streams end with it, not at process exit (utils/streams.py)
+        from torch_distributed_sandbox_amd.utils.streams import release_streams
+
+        release_streams()
 
 
 def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, store, k, phase):
@@ -444,12 +523,18 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     phase[0] = f"attempt {k} ({backend}): model"
     model = ConvNet(image_shape=(H, W), device=device, mode=args.mode)
     criterion = CrossEntropyLoss()
-    optimizer = SGD(model.parameters(), 1e-4)
+    optimizer = SGD(model.parameters(), args.lr)
     ddp = DistributedDataParallel(model, device_ids=[local_rank] if on_gpu else None, bucket_cap_mb=args.bucket_mb,
                                   grad_exchange=grad_exchange, overlap_optimizer=args.overlap_optimizer,
                                   allreduce_chunks=args.allreduce_chunks, exchange_compress=args.exchange_compress)
 
     ddp.attach_optimizer(optimizer)
+
+    preflight = None
+    if args.preflight and tdist.is_initialized():  # world > 1, or a forced exchange at world 1
+        phase[0] = f"attempt {k} ({backend}): preflight"
+        preflight, planned = _preflight(ddp, tdist, device, world, rank, B, args.preflight_timeout)
+        preflight = {"fc_path": planned, "collectives": preflight}
 
     # a pool of synthetic 28x28 sources; each step upsamples a different slice on device
     pool = 16
@@ -532,9 +617,14 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
         loss = step(i)
     sync_all()
     phase[0] = f"attempt {k} ({backend}): timed steps"
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if on_gpu and args.step_times else None
     t0 = time.perf_counter()
     for i in range(args.steps):
+        if evs is not None:
+            evs[i].record()
         loss = step(args.warmup + i)
+    if evs is not None:
+        evs[-1].record()
     sync_all()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -575,10 +665,14 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             "input": ("uint8 levels (ToTensor's 1/255 folded into conv1)" if args.input == "levels"
                       else "fp32 image"),
             "rccl_max_ctas": rccl_max_ctas or None,
-            "optimizer": "SGD(lr=1e-4)",
+            "optimizer": f"SGD(lr={args.lr:g})",
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3) if on_gpu else None,
             "final_loss": final_loss,
         }
+        if evs is not None:
+            config["step_ms"] = [round(evs[i].elapsed_time(evs[i + 1]), 4) for i in range(args.steps)]
+        if preflight is not None:
+            config["preflight"] = preflight
         if probe is not None:
             config["allreduce_probe"] = probe
         if sim_stream is not None:

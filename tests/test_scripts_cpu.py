@@ -245,3 +245,44 @@ def test_bench_under_torchrun_falls_back_cpu():
     assert p.returncode == 0, p.stderr[-3000:]
     (r,) = _json_lines(p.stdout)
     assert r["value"] > 0 and r["config"]["backend"].startswith("gloo (fallback: rank 1")
+
+
+@pytest.mark.parametrize("world,phase", [(2, "preflight"), (2, "step"), (8, "preflight"), (8, "step")])
+def test_bench_fallback_tiers_keep_the_exchange_cpu(world, phase):
+    """A fault on rank 1 in the collective preflight or mid-warmup of tier 1 (the native host
+    ring standing in for rccl-native): the ranks vote, tear down and run tier 2 -- torch's own
+    process group (gloo standing in for ProcessGroupNCCL) with the SAME zero-suppressed fc
+    exchange, not the dense all-reduce.  The JSON names the tier, the reason and the preflight
+    of the tier that ran."""
+    p = _run(["bench.py", "--gpus", str(world), "--device", "cpu", "--image-size", "232", "--steps", "1",
+              "--warmup", "1", "--backend", "host", "--fallback", "--pg-timeout", "30", "--no-allreduce-probe"],
+             env={"TDS_BENCH_FAULT": f"1:{phase}:raise:1"}, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (r,) = _json_lines(p.stdout)
+    c = r["config"]
+    assert r["value"] > 0 and c["attempt"] == 1 and c["tier"] == "2/3"
+    assert c["backend"].startswith("gloo (fallback: rank 1") and f"phase {phase}" in c["backend"]
+    want = "activation-exchange(zs)" if world == 2 else "sharded-exchange(zs)"
+    assert c["fc_grad"] == want
+    pf = c["preflight"]
+    assert pf["fc_path"] == ("activations" if world == 2 else "sharded")
+    ops = [x["op"] for x in pf["collectives"]]
+    assert "BN buffer broadcast (coalesced)" in ops and ops[-1] == "barrier"
+    if world == 2:
+        assert "zs values all-gather (first-step capacity)" in ops
+    else:
+        assert "X column-shard exchange (per peer)" in ops and "updated W shard exchange (per peer)" in ops
+    assert all(x["ms"] >= 0 for x in pf["collectives"])
+
+
+def test_bench_last_tier_is_the_bucket_allreduce_cpu():
+    """Tiers 1 and 2 both fail in the preflight: tier 3, the plain bucket all-reduce, runs."""
+    p = _run(["bench.py", "--gpus", "2", "--device", "cpu", "--image-size", "232", "--steps", "1",
+              "--warmup", "1", "--backend", "host", "--fallback", "--pg-timeout", "30", "--no-allreduce-probe"],
+             env={"TDS_BENCH_FAULT": "1:preflight:raise:2"}, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    (r,) = _json_lines(p.stdout)
+    c = r["config"]
+    assert r["value"] > 0 and c["attempt"] == 2 and c["tier"] == "3/3"
+    assert c["fc_grad"] == "allreduce" and c["preflight"]["fc_path"] == "allreduce"
+    assert any(x["op"].startswith("bucket 0 all-reduce") for x in c["preflight"]["collectives"])

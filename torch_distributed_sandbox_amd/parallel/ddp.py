@@ -346,6 +346,35 @@ class DistributedDataParallel(nn.Module):
                 b.copy_(flat[o:o + n].view_as(b))
                 o += n
 
+    # ------------------------------------------------------------------ preflight
+    def preflight(self, rows: int, timed) -> dict:
+        """Issue once, on the live process group and its streams, every collective a synchronised
+        training step with ``rows`` local rows will run -- the rank-0 buffer broadcast, the
+        all-reduce of every bucket the fc gradient path leaves to the reducer, and each exchange's
+        own collectives (parallel/factored.py ``preflight``) -- each through ``timed(name,
+        nbytes, kind, issue)`` (see bench.py ``_preflight``: a bounded wait and a time per
+        collective).  RCCL sets up its point-to-point channels and algorithms on first use, so
+        that cost (and any failure) lands here instead of in the first training step.  Returns
+        {"fc_path": ...}."""
+        if self.world_size == 1 and not self._exchanges:
+            return {"fc_path": "local"}
+        g = self.process_group
+        paths = {}
+        for ex in self._exchanges:
+            paths[id(self._bucket_of[id(ex.weight)])] = ex.preflight(rows, timed)
+        if self.broadcast_buffers and self.world_size > 1 and any(True for _ in self.module.buffers()):
+            nb = sum(b.numel() * b.element_size() for b in self.module.buffers())
+            timed("BN buffer broadcast (coalesced)", nb, "broadcast", lambda: self._broadcast_buffers_now())
+        for b in self._buckets:
+            if paths.get(id(b)) is not None or self.world_size == 1:
+                continue  # this bucket's gradient travels by its exchange (world 1: no all-reduce)
+            seg = torch.zeros(b.numel, device=self.device, dtype=self.flat_grad.dtype)
+            timed(f"bucket {b.index} all-reduce (AVG)", b.numel * seg.element_size(), "all_reduce",
+                  lambda seg=seg: tdist.all_reduce(seg, tdist.ReduceOp.AVG, group=g, async_op=True))
+            del seg
+        used = [p for p in paths.values() if p is not None]
+        return {"fc_path": "+".join(used) if used else "allreduce"}
+
     # ------------------------------------------------------------------ forward
     def forward(self, *args, **kwargs):
         if self.broadcast_buffers and self.world_size > 1:

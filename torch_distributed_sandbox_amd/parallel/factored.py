@@ -79,6 +79,17 @@ _ATTR = "_tds_activation_exchange"
 _SHARD_ALIGN = 64  # shard boundaries on 256-byte multiples
 
 
+def _meta_row(m: int) -> int:
+    """int32 words of one rank's record in the activation exchange: the m mask/offset words,
+    one pad word when m is odd, then the int64 non-zero count at an 8-byte aligned offset."""
+    return m + (m & 1) + 2
+
+
+def _counts_of(meta_all: torch.Tensor, world: int, row: int) -> torch.Tensor:
+    """The [world] int64 counts in the tails of the all-gathered records (row = _meta_row)."""
+    return meta_all.view(world, row)[:, row - 2:].contiguous().view(torch.int64).view(world)
+
+
 def get(weight) -> Optional["ActivationExchange"]:
     return getattr(weight, _ATTR, None) if weight is not None else None
 
@@ -135,8 +146,12 @@ class ActivationExchange:
         # zero-suppressed activation rows (parallel/zs.py)
         self.compress = bool(compress)
         self._zs = None  # this step's encoded exchange: dict
-        self._cap = None  # value capacity per rank (elements), from earlier steps' counts
-        self.x_ratio = 1.0  # measured zero-suppressed / dense bytes of the last compressed step
+        # value capacity (elements) per path, from that path's earlier counts: "activations" holds
+        # a per-rank total, "sharded" a per-segment slot, so neither may seed the other
+        self._cap = {}
+        # measured zero-suppressed / dense bytes of the busiest rank's rows in the last compressed
+        # step (one definition for both paths: the byte model prices the busiest link)
+        self.x_ratio = 1.0
         self.zs_stats = {"steps": 0, "overflows": 0, "last_nnz": None}
         setattr(weight, _ATTR, self)
 
@@ -238,6 +253,61 @@ class ActivationExchange:
                 db.add_(s_b) if acc_b else db.copy_(s_b)
         self.chunked_done(dw, db)
 
+    def preflight(self, rows: int, timed) -> Optional[str]:
+        """Issue once, at the sizes of a step with ``rows`` local rows, every collective the path
+        ``auto`` (or the forced mode) picks would run, each through ``timed(name, nbytes, kind,
+        issue)`` -- ``issue()`` starts it and returns its work (or None) -- so a launcher can bound
+        and time them before any model work (bench.py's preflight).  Returns the path (None: the
+        plain bucket all-reduce, which the caller preflights with the buckets)."""
+        from . import distributed as tdist
+        from . import zs
+
+        path = self.path(rows)
+        if path is None:
+            return None
+        W, g = self.world, self.group
+        out_f, in_f = self.weight.shape
+        dev = self.weight.device
+        me = tdist.get_rank(g)
+
+        def gather(name, numel, dtype):
+            src = torch.zeros(numel, device=dev, dtype=dtype)
+            dst = torch.empty(W * numel, device=dev, dtype=dtype)
+            nb = dst.numel() * dst.element_size()
+            timed(name, nb, "all_gather", lambda: tdist.all_gather_into_tensor(dst, src, group=g, async_op=True))
+
+        def peers(name, numel, nrows):
+            # one grouped exchange with every peer: nrows chunks of numel elements each way
+            bufs_s = [torch.zeros(numel, device=dev) for _ in range(nrows)]
+            bufs_r = [torch.empty(numel, device=dev) for _ in range(nrows * W)]
+            sends = [(t, p) for p in range(W) if p != me for t in bufs_s]
+            recvs = [(bufs_r[p * nrows + i], p) for p in range(W) if p != me for i in range(nrows)]
+            nb = numel * 4 * nrows  # per peer (link)
+            timed(name, nb, "sendrecv", lambda: tdist.sendrecv(sends, recvs, group=g, async_op=True))
+
+        n = rows * in_f
+        zs_ok = self.compress and n < (1 << 31)
+        if path == "activations":
+            if zs_ok:
+                gather("zs records all-gather (int32)", _meta_row(zs.meta_numel(n)), torch.int32)
+                cap = min(n, self._cap["activations"]) if self._cap.get("activations") else n
+                gather("zs values all-gather (first-step capacity)", cap, torch.float32)
+            else:
+                gather("activation rows all-gather", n, torch.float32)
+            gather("dY all-gather", rows * out_f, torch.float32)
+        elif path == "sharded":
+            longest = max(e - a for a, e in shard_bounds(in_f, W))
+            if zs_ok:
+                gather("zs segment counts all-gather (int64)", W * rows, torch.int64)
+            peers("X column-shard exchange (per peer)", longest, rows)
+            gather("dY all-gather", rows * out_f, torch.float32)
+            peers("updated W shard exchange (per peer)", longest, out_f)
+        elif path == "chunked":
+            seg = torch.zeros(-(-in_f // self.chunks), device=dev)
+            timed("chunk row-segment all-reduce (AVG)", seg.numel() * 4, "all_reduce",
+                  lambda: tdist.all_reduce(seg, tdist.ReduceOp.AVG, group=g, async_op=True))
+        return path
+
     def worthwhile(self, rows: int) -> bool:
         return self.path(rows) is not None
 
@@ -275,12 +345,15 @@ class ActivationExchange:
             return True
         x2d = x2d.detach().contiguous()
         rows, in_f = x2d.shape
-        if path == "activations" and self.compress and x2d.dtype == torch.float32:
+        # the zero-suppressed format's offsets are int32 (csrc/kernels/zs_exchange.hip): larger
+        # inputs take the dense exchange of the same path
+        zs_ok = self.compress and x2d.dtype == torch.float32 and x2d.numel() < (1 << 31)
+        if path == "activations" and zs_ok:
             self._begin_zs(x2d)
         elif path == "activations":
             self._x_buf = torch.empty((self.world * rows, in_f), device=x2d.device, dtype=x2d.dtype)
             self._x_work = tdist.all_gather_into_tensor(self._x_buf, x2d, group=self.group, async_op=True)
-        elif self.compress and x2d.dtype == torch.float32:
+        elif zs_ok:
             self._begin_zs_sharded(x2d)
         else:
             # all-to-all of column shards: rank s receives every rank's rows of shard s
@@ -307,12 +380,13 @@ class ActivationExchange:
         W, dev = self.world, x2d.device
         n = x2d.numel()
         M = zs.meta_numel(n)
-        cap = min(n, self._cap) if self._cap else n
-        meta = torch.empty(M + 2, device=dev, dtype=torch.int32)
+        R = _meta_row(M)
+        cap = min(n, self._cap["activations"]) if self._cap.get("activations") else n
+        meta = torch.empty(R, device=dev, dtype=torch.int32)
         vals = torch.empty(cap, device=dev, dtype=torch.float32)
         nnz = zs.encode(x2d, meta[:M], vals)
-        meta[M:].view(torch.int64).copy_(nnz.view(1).to(dev))
-        meta_all = torch.empty(W * (M + 2), device=dev, dtype=torch.int32)
+        meta[R - 2:].view(torch.int64).copy_(nnz.view(1).to(dev))
+        meta_all = torch.empty(W * R, device=dev, dtype=torch.int32)
         w_meta = tdist.all_gather_into_tensor(meta_all, meta, group=self.group, async_op=True)
         counts_host = counts_ev = None
         if dev.type == "cuda":
@@ -320,7 +394,7 @@ class ActivationExchange:
             cstream = self._count_stream(dev)
             with torch.cuda.stream(cstream):
                 w_meta.wait()
-                counts = meta_all.view(W, M + 2)[:, M:].contiguous().view(torch.int64).view(W)
+                counts = _counts_of(meta_all, W, R)
                 counts_host = torch.empty(W, dtype=torch.int64, pin_memory=True)
                 counts_host.copy_(counts, non_blocking=True)
                 counts_ev = torch.cuda.Event()
@@ -328,7 +402,7 @@ class ActivationExchange:
                 meta_all.record_stream(cstream)
         vals_all = torch.empty(W * cap, device=dev, dtype=torch.float32)
         w_vals = tdist.all_gather_into_tensor(vals_all, vals, group=self.group, async_op=True)
-        self._zs = {"n": n, "M": M, "cap": cap, "meta": meta, "vals": vals, "meta_all": meta_all, "vals_all": vals_all,
+        self._zs = {"n": n, "M": M, "R": R, "cap": cap, "meta": meta, "vals": vals, "meta_all": meta_all, "vals_all": vals_all,
                     "w_meta": w_meta, "w_vals": w_vals, "counts_host": counts_host, "counts_ev": counts_ev,
                     "rows": x2d.shape[0], "in_f": x2d.shape[1]}
         self._x_work = None  # set by _zs_resolve
@@ -366,7 +440,7 @@ class ActivationExchange:
         me = tdist.get_rank(self.group)
         n_me = bounds[me][1] - bounds[me][0]
         longest = max(e - a for a, e in bounds)
-        cap = max(1, min(longest, self._cap) if self._cap else longest)
+        cap = max(1, min(longest, self._cap["sharded"]) if self._cap.get("sharded") else longest)
         meta_send = torch.empty(send.meta_numel, device=dev, dtype=torch.int32)
         vals_send = torch.empty(send.nseg * cap, device=dev, dtype=torch.float32)
         nnz = zs.seg_encode(x2d, send, meta_send, vals_send, cap).to(dev)
@@ -401,7 +475,7 @@ class ActivationExchange:
         self._zs = {"kind": "sharded", "n": longest, "cap": cap, "w_cnt": w_cnt, "nnz_all": nnz_all,
                     "counts_host": counts_host, "counts_ev": counts_ev, "w_meta": w_meta, "w_vals": w_vals,
                     "meta_recv": meta_recv, "vals_recv": vals_recv, "recv": recv, "keep": (meta_send, vals_send),
-                    "meta_bytes": send.meta_numel, "dense": x2d.numel()}
+                    "meta_bytes": send.meta_numel, "dense": x2d.numel(), "nseg": send.nseg}
         self._x_work = None
 
     def _count_stream(self, dev):
@@ -410,66 +484,74 @@ class ActivationExchange:
             st = self._cstream = torch.cuda.Stream(device=dev)
         return st
 
+    def _zs_counts(self, z):
+        """The all-gathered non-zero counts of an encoded step, on the host (CUDA: from the pinned
+        copy queued behind the first, small gather; by the time a caller asks -- the end of the
+        backward, or the next forward's head -- it has landed, so the wait is a formality)."""
+        W = self.world
+        if z.get("kind") == "sharded":
+            if z["counts_ev"] is not None:
+                z["counts_ev"].synchronize()
+                return [int(v) for v in z["counts_host"].tolist()]
+            z["w_cnt"].wait()
+            return [int(v) for v in z["nnz_all"].tolist()]
+        if z["counts_ev"] is not None:
+            z["counts_ev"].synchronize()
+            return [int(v) for v in z["counts_host"].tolist()]
+        z["w_meta"].wait()  # CPU: the gathers are synchronous enough to read directly
+        return [int(v) for v in _counts_of(z["meta_all"], W, z["R"]).tolist()]
+
+    def _zs_check(self, z) -> bool:
+        """Account one encoded step: statistics, the path's capacity for the next steps and the
+        measured ratio; True when some count exceeded this step's capacity (its values did not
+        all travel: the step must use the dense rows)."""
+        counts = self._zs_counts(z)
+        self.zs_stats["steps"] += 1
+        if z.get("kind") == "sharded":
+            mx = max(counts) if counts else 0
+            self.zs_stats["last_nnz"] = mx
+            self._cap["sharded"] = max(1, min(z["n"], -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND))
+            per_rank = [sum(counts[r * z["nseg"]:(r + 1) * z["nseg"]]) for r in range(self.world)]
+            self.x_ratio = (max(per_rank) + z["meta_bytes"]) / z["dense"]  # busiest rank vs its dense rows
+        else:
+            mx = max(counts)
+            self.zs_stats["last_nnz"] = counts
+            self._cap["activations"] = min(z["n"], -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND)
+            self.x_ratio = (mx + z["R"] * 1.0) / z["n"]  # bytes relative to dense (4-byte words both)
+        if mx > z["cap"]:
+            self.zs_stats["overflows"] += 1
+            return True
+        return False
+
     def _zs_resolve(self):
-        """Host side of the zero-suppressed gather (called from ``defer`` on the host): check the
-        counts against the capacity, update the capacity for the next steps, and set up the
-        dense rows self._x_buf with a work that completes once they are rebuilt (or, on an
-        overflow, once the dense fallback gather has landed)."""
+        """Host side of the zero-suppressed exchange (CPU, and the GPU side-stream finish, which
+        runs from an end-of-backward callback): check the counts, then set up the dense rows
+        self._x_buf -- rebuilt from the encodings, or, after an overflow, a dense re-send of this
+        step's rows (every rank saw the same counts, so all take the same branch)."""
         from . import distributed as tdist
 
         z, self._zs = self._zs, None
+        overflow = self._zs_check(z)
         if z.get("kind") == "sharded":
-            self._zs_resolve_sharded(z)
+            if overflow:  # some segment overflowed its slot: the dense all-to-all, once
+                z["w_meta"].wait()
+                z["w_vals"].wait()
+                x2d = self._x_local
+                rows, in_f = x2d.shape
+                bounds = shard_bounds(in_f, self.world)
+                me = tdist.get_rank(self.group)
+                k0, k1 = bounds[me]
+                sends = [(x2d[b, a:e], s_) for s_, (a, e) in enumerate(bounds) if e > a for b in range(rows)]
+                recvs = [(self._x_buf[s_, b], s_) for s_ in range(self.world) if k1 > k0 for b in range(rows)]
+                self._x_work = tdist.sendrecv(sends, recvs, group=self.group, async_op=True)
+                return
+            self._zs_decode_pending = z
             return
-        W, n, cap = self.world, z["n"], z["cap"]
-        if z["counts_ev"] is not None:
-            z["counts_ev"].synchronize()
-            counts = [int(v) for v in z["counts_host"].tolist()]
-        else:  # CPU: the gathers are synchronous enough to read directly
-            z["w_meta"].wait()
-            M = z["M"]
-            counts = [int(v) for v in z["meta_all"].view(W, M + 2)[:, M:].contiguous().view(torch.int64).view(W)]
-        mx = max(counts)
-        self.zs_stats["steps"] += 1
-        self.zs_stats["last_nnz"] = counts
-        self._cap = min(n, -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND)
-        self.x_ratio = (mx + (z["M"] + 2) * 1.0) / n  # bytes relative to dense (4-byte words both)
-        rows, in_f = z["rows"], z["in_f"]
-        if mx > cap:  # a count above this step's capacity: the dense rows, once
-            self._x_buf = torch.empty((W * rows, in_f), device=z["meta"].device, dtype=torch.float32)
-            self.zs_stats["overflows"] += 1
+        if overflow:  # a count above this step's capacity: the dense rows, once
+            rows, in_f = z["rows"], z["in_f"]
+            self._x_buf = torch.empty((self.world * rows, in_f), device=z["meta"].device, dtype=torch.float32)
             z["w_vals"].wait()
             self._x_work = tdist.all_gather_into_tensor(self._x_buf, self._x_local, group=self.group, async_op=True)
-            return
-        self._zs_decode_pending = z
-
-    def _zs_resolve_sharded(self, z):
-        from . import distributed as tdist
-
-        if z["counts_ev"] is not None:
-            z["counts_ev"].synchronize()
-            counts = z["counts_host"]
-        else:
-            z["w_cnt"].wait()
-            counts = z["nnz_all"]
-        counts = [int(v) for v in counts.tolist()]
-        mx, cap = max(counts) if counts else 0, z["cap"]
-        self.zs_stats["steps"] += 1
-        self.zs_stats["last_nnz"] = max(counts) if counts else 0
-        self._cap = max(1, min(z["n"], -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND))
-        self.x_ratio = (sum(counts) / self.world + z["meta_bytes"]) / z["dense"]  # per rank, vs dense rows
-        if mx > cap:  # some segment overflowed its slot: the dense all-to-all, once
-            self.zs_stats["overflows"] += 1
-            z["w_meta"].wait()
-            z["w_vals"].wait()
-            x2d = self._x_local
-            rows, in_f = x2d.shape
-            bounds = shard_bounds(in_f, self.world)
-            me = tdist.get_rank(self.group)
-            k0, k1 = bounds[me]
-            sends = [(x2d[b, a:e], s_) for s_, (a, e) in enumerate(bounds) if e > a for b in range(rows)]
-            recvs = [(self._x_buf[s_, b], s_) for s_ in range(self.world) if k1 > k0 for b in range(rows)]
-            self._x_work = tdist.sendrecv(sends, recvs, group=self.group, async_op=True)
             return
         self._zs_decode_pending = z
 
@@ -484,11 +566,22 @@ class ActivationExchange:
             self._x_buf = torch.empty((self.world * z["rows"], z["in_f"]), device=z["meta"].device, dtype=torch.float32)
         self._zs_decode_into(z, self._x_buf)
 
-    @staticmethod
-    def _zs_fused(z) -> bool:
-        """The gathered activation rows can feed the dW formation encoded (``linear_dw_zs``:
-        decoded in registers, no dense rows written and read back)."""
-        return z is not None and z.get("kind") != "sharded" and z["meta"].is_cuda
+    def _zs_fused(self, z, targets=()) -> bool:
+        """Can the gathered activation rows feed the dW formation encoded (``linear_dw_zs``:
+        decoded in registers, no dense rows written and read back)?  That kernel takes N in
+        {10, 16} outputs, K % 4 == 0 and 16-byte aligned rows of every tensor it writes
+        (zs_exchange.hip tds_linear_dw_zs); anything else decodes and runs ``linear_dw``."""
+        if z is None or z.get("kind") == "sharded" or not z["meta"].is_cuda:
+            return False
+        n_out, k = self.weight.shape
+        if n_out not in (10, 16) or k % 4:
+            return False
+        for t in targets:
+            if t is None:
+                continue
+            if t.stride(1) != 1 or t.stride(0) % 4 or t.data_ptr() % 16:
+                return False
+        return True
 
     def _dw_zs(self, z, dy_all, dw, db, scale: float, acc: bool, lr: float = 0.0):
         """dW (=/+=) scale·dy_allᵀX (or the update-only W -= lr·scale·dy_allᵀX) straight from the
@@ -497,8 +590,8 @@ class ActivationExchange:
 
         z["w_meta"].wait()
         z["w_vals"].wait()
-        W, M, cap = self.world, z["M"], z["cap"]
-        _ext.ops().linear_dw_zs(dy_all, z["meta_all"].view(W, M + 2), z["vals_all"].view(W, cap), z["rows"], dw, db,
+        W, R, cap = self.world, z["R"], z["cap"]
+        _ext.ops().linear_dw_zs(dy_all, z["meta_all"].view(W, R), z["vals_all"].view(W, cap), z["rows"], dw, db,
                                 scale, acc, lr)
 
     def _zs_decode_into(self, z, x_buf):
@@ -509,8 +602,8 @@ class ActivationExchange:
         if z.get("kind") == "sharded":
             zs.seg_decode(z["meta_recv"], z["recv"], z["vals_recv"], z["cap"], x_buf)
             return
-        W, n, M, cap = self.world, z["n"], z["M"], z["cap"]
-        meta_all = z["meta_all"].view(W, M + 2)
+        W, n, M, R, cap = self.world, z["n"], z["M"], z["R"], z["cap"]
+        meta_all = z["meta_all"].view(W, R)
         vals_all = z["vals_all"].view(W, cap)
         out = x_buf.view(W, n)
         for r in range(W):
@@ -518,24 +611,34 @@ class ActivationExchange:
 
     # ---------------------------------------------------------------- backward
     def defer(self, dy: torch.Tensor, x2: Optional[torch.Tensor] = None):
-        """Called from the layer's backward with dY.  On the GPU the rest of the exchange
-        (dY gather, dW formation, shard all-gather) is issued right here on a side stream,
-        so it overlaps the rest of the backward; the compute stream only waits for it at
-        the end of backward (or, under DDP's overlapped optimizer, the optimizer's side
-        stream does).  On the CPU it runs from an end-of-backward callback.  ``chunked``: the
-        weight gradient is formed here from ``x2`` chunk by chunk, each chunk all-reduced."""
+        """Called from the layer's backward with dY.  The host never waits here: on the GPU the
+        rest of the exchange (dY gather, the zero-suppressed count check, dW formation, shard
+        all-gather) is either left to the weight's first reader in the next forward
+        (``_defer_update_inline``) or issued on a side stream from an end-of-backward callback,
+        i.e. after every backward kernel is queued, so a count check that has to wait for the
+        gathered counts cannot open a gap between the head backward and the conv2 backward.
+        The compute stream waits for the side stream at the end of backward (or, under DDP's
+        overlapped optimizer, the optimizer's side stream does).  On the CPU it all runs from
+        an end-of-backward callback.  ``chunked``: the weight gradient is formed here from ``x2``
+        chunk by chunk, each chunk all-reduced."""
         if self.active == "chunked":
             self.chunked_linear_backward(dy.detach().contiguous(), x2.detach())
             return
         self._dy = dy.detach().contiguous()
-        if self._zs is not None:
-            self._zs_resolve()
         if not self._dy.is_cuda:
+            if self._zs is not None:
+                self._zs_resolve()
             torch.autograd.Variable._execution_engine.queue_callback(self._finish)
             return
-        dev = self._dy.device
         if self._defer_update_inline():
             return
+        torch.autograd.Variable._execution_engine.queue_callback(self._finish_on_side)
+
+    def _finish_on_side(self):
+        """GPU finish of the exchange on a side stream (end-of-backward callback)."""
+        dev = self._dy.device
+        if self._zs is not None:
+            self._zs_resolve()
         side = self.side_stream
         join = side is None
         if side is None:
@@ -560,19 +663,21 @@ class ActivationExchange:
                     t.record_stream(side)
             self._finish()
         if join:
-            torch.autograd.Variable._execution_engine.queue_callback(
-                lambda: torch.cuda.current_stream(dev).wait_stream(side))
+            cur.wait_stream(side)
 
     def _defer_update_inline(self) -> bool:
         """Activations path under DDP's overlapped optimizer with the step fused in (plain SGD):
-        leave the weight update -- decode, dW formation and ``W -= lr·dW`` in one ``linear_dw``
-        sweep over the 720 MB weight -- to the first reader of the weight, the next forward's
-        head, where it runs on the compute stream across the whole GPU (ops/param_fence.py:
+        leave the weight update -- the count check, decode, dW formation and ``W -= lr·dW`` in one
+        ``linear_dw`` sweep over the 720 MB weight -- to the first reader of the weight, the next
+        forward's head, where it runs on the compute stream across the whole GPU (ops/param_fence.py:
         ``defer``).  Run beside the backward's persistent kernels on a side stream the same
         sweep took 1.7-2.0 ms and slowed the conv2 / layer-1 backward by ~0.8 ms (world 1,
-        forced exchange, profiles/r3_exchange_side_vs_inline.md).  The bias keeps its side-stream
-        path (dY gather, bias gradient, the optimizer's step), which needs dY only.
-        ``TDS_EXCHANGE_UPDATE=side`` keeps the whole finish on the side stream."""
+        forced exchange, profiles/r3_exchange_side_vs_inline.md).  The host reads the gathered
+        counts only there (they landed during this step's backward); after an overflow the
+        update re-sends this step's rows dense from that point (all ranks saw the same counts).
+        The bias keeps its side-stream path (dY gather, bias gradient, the optimizer's step),
+        which needs dY only.  ``TDS_EXCHANGE_UPDATE=side`` keeps the whole finish on the side
+        stream."""
         import os
 
         from ..ops import fused_update, param_fence
@@ -603,28 +708,32 @@ class ActivationExchange:
                 self.bias.grad = db
             ev_dy = torch.cuda.Event()
             ev_dy.record(side)
-        z = getattr(self, "_zs_decode_pending", None)
-        self._zs_decode_pending = None
-        if z is not None and not self._zs_fused(z):
-            self._x_buf = torch.empty((self.world * rows, z["in_f"]), device=dev, dtype=torch.float32)
-        x_buf, x_work = self._x_buf, self._x_work
-        keep = (self._x_local,)  # the local rows stay alive until the gathers reading them are done
-        weight, lr = self.weight, float(lr)
+        z, self._zs = self._zs, None
+        x_work, x_local, x_dense = self._x_work, self._x_local, self._x_buf
+        in_f = self.weight.shape[1]
+        weight, lr, group, world = self.weight, float(lr), self.group, self.world
 
         def update():
             from .. import _ext
 
             torch.cuda.current_stream(dev).wait_event(ev_dy)
             with torch.no_grad():
-                if self._zs_fused(z):
-                    self._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
-                    return
+                x_buf = None
                 if z is not None:
-                    self._zs_decode_into(z, x_buf)
+                    if not self._zs_check(z):
+                        if self._zs_fused(z, (weight.data,)):
+                            self._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
+                            return
+                        x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
+                        self._zs_decode_into(z, x_buf)
+                    else:  # overflow: this step's rows, dense, from every rank
+                        z["w_vals"].wait()
+                        x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
+                        tdist.all_gather_into_tensor(x_buf, x_local, group=group)
                 else:
                     x_work.wait()
+                    x_buf = x_dense
                 _ext.ops().linear_dw(dy_all, x_buf, weight.data, None, scale, False, lr)
-            assert keep
 
         param_fence.defer(weight, update)
         fused_update.applied(weight)
@@ -655,7 +764,8 @@ class ActivationExchange:
         dy_all = torch.empty((self.world * rows, dy.shape[1]), device=dy.device, dtype=dy.dtype)
         tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
         zf = getattr(self, "_zs_decode_pending", None)
-        if self.active == "activations" and self._zs_fused(zf):
+        targets = (self.weight.data, self._wview(), self.weight.grad)
+        if self.active == "activations" and self._zs_fused(zf, targets):
             self._zs_decode_pending = None  # formed from the encodings below (_dw_zs)
         else:
             zf = None
