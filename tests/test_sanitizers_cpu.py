@@ -66,3 +66,23 @@ def test_host_comm_under_sanitizers(sanitized, world):
     assert f"sanitize_host_comm ok: world={world}" in r.stdout
     for marker in ("runtime error", "AddressSanitizer", "ThreadSanitizer"):
         assert marker not in r.stderr, r.stderr[-4000:]
+
+
+@pytest.mark.parametrize("kind", ["plain", "tsan"])
+def test_rccl_settle_abort_protocol(kind):
+    """The native RCCL communicator's lock protocol (csrc/comm/settle.h): an abort requested
+    while a non-blocking call settles under the communicator lock is honoured within one poll
+    (not after the call's 20 s timeout), and the watchdog's poll never blocks behind the call.
+    Also built under ThreadSanitizer."""
+    if shutil.which("g++") is None and shutil.which("c++") is None:
+        pytest.skip("no host C++ compiler")
+    os.makedirs(OUT_DIR, exist_ok=True)
+    exe = os.path.join(OUT_DIR, f"settle_protocol_{kind}")
+    src = os.path.join(HERE, "native", "settle_protocol.cpp")
+    cxx = shutil.which("g++") or "c++"
+    flags = ["-fsanitize=thread"] if kind == "tsan" else []
+    subprocess.run([cxx, "-std=c++17", "-O1", "-g", f"-I{CSRC}"] + flags + [src, "-o", exe, "-lpthread"],
+                   check=True, timeout=300)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "settle protocol ok" in p.stdout

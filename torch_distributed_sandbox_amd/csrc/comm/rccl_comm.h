@@ -49,6 +49,7 @@
 #include <vector>
 
 #include "comm/comm.h"
+#include "comm/settle.h"
 
 // csrc/kernels/cu_budget.hip: stream confined to the CUs reserved for communication (or nullptr)
 hipStream_t tds_cu_comm_stream(int device);
@@ -62,22 +63,26 @@ namespace tds_comm {
   } while (0)
 // A communicator created non-blocking may return ncclInProgress from any call;
 // the call has then been accepted and finishes asynchronously.  Poll the async
-// state until it settles (bounded), then check it like a blocking result.
-inline ncclResult_t nccl_settle(ncclResult_t r, ncclComm_t c, int64_t timeout_ms) {
+// state until it settles (bounded, and cut short by an abort request: settle.h),
+// then check it like a blocking result.
+inline ncclResult_t nccl_settle(ncclResult_t r, ncclComm_t c, int64_t timeout_ms, const std::atomic<bool>* aborted) {
   if (r != ncclInProgress || c == nullptr) return r;
-  const auto t0 = std::chrono::steady_clock::now();
-  ncclResult_t st = ncclInProgress;
-  while (true) {
-    if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return ncclInternalError;
-    if (st != ncclInProgress) return st;
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) return ncclInProgress;
-    std::this_thread::yield();
-  }
+  const int st = settle_wait(
+      [c]() -> int {
+        ncclResult_t a = ncclInProgress;
+        if (ncclCommGetAsyncError(c, &a) != ncclSuccess) return (int)ncclInternalError;
+        return a == ncclInProgress ? kSettleInProgress : (int)a;
+      },
+      aborted, timeout_ms);
+  if (st == kSettleAborted) return ncclInvalidUsage;  // the watchdog is aborting the communicator
+  if (st == kSettleTimeout) return ncclInProgress;
+  return (ncclResult_t)st;
 }
 #define TDS_RCCL_C(c, cmd)                                                                   \
   do {                                                                                       \
-    ncclResult_t r_ = nccl_settle((cmd), (c), st_->timeout_ms);                              \
-    TORCH_CHECK(r_ == ncclSuccess, "RCCL error '", ncclGetErrorString(r_), "' in ", #cmd);  \
+    ncclResult_t r_ = nccl_settle((cmd), (c), st_->timeout_ms, &st_->aborted);               \
+    TORCH_CHECK(r_ == ncclSuccess, "RCCL error '", ncclGetErrorString(r_), "' in ", #cmd,    \
+                st_->aborted.load() ? " (communicator aborted while the call settled)" : ""); \
   } while (0)
 #define TDS_HIP(cmd)                                                                   \
   do {                                                                                 \
@@ -174,22 +179,22 @@ struct RcclState {
     }
   }
 
-  // Abort once; called from the watchdog (or a failing wait).
+  // Abort once; called from the watchdog (or a failing wait).  `aborted` is published before
+  // comm_mu is taken: a call settling under comm_mu sees it on its next poll and returns, so
+  // the abort waits one poll, not the call's timeout (settle.h).
   void fail(const std::string& why) {
-    bool expected = false;
-    if (!aborted.compare_exchange_strong(expected, true)) return;
+    if (!claim_abort(aborted)) return;
     {
       std::lock_guard<std::mutex> g(mu);
       error = why;
     }
     std::fprintf(stderr, "[tds rccl] rank %lld: %s -- aborting communicator\n", (long long)rank, why.c_str());
     std::fflush(stderr);
-    {
-      std::lock_guard<std::mutex> g(comm_mu);
+    abort_locked(comm_mu, [this] {
       ncclComm_t c = comm;
       comm = nullptr;
       if (c) ncclCommAbort(c);
-    }
+    });
     if (exit_on_error) {
       std::fprintf(stderr, "[tds rccl] rank %lld: terminating process (TDS_RCCL_ERROR_HANDLING=raise to disable)\n",
                    (long long)rank);
@@ -595,11 +600,14 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
         break;  // collectives complete in order on the comm stream
       }
       if (why.empty()) {
-        std::lock_guard<std::mutex> cl(s->comm_mu);
-        ncclResult_t ae = ncclSuccess;
-        if (s->comm && ncclCommGetAsyncError(s->comm, &ae) == ncclSuccess && ae != ncclSuccess &&
-            ae != ncclInProgress)
-          why = std::string("RCCL async error: ") + ncclGetErrorString(ae);
+        // try-lock only: while a call holds comm_mu its own settle loop polls this same async
+        // state (settle.h), so the watchdog never stalls behind a settling call
+        try_poll_locked(s->comm_mu, [&] {
+          ncclResult_t ae = ncclSuccess;
+          if (s->comm && ncclCommGetAsyncError(s->comm, &ae) == ncclSuccess && ae != ncclSuccess &&
+              ae != ncclInProgress)
+            why = std::string("RCCL async error: ") + ncclGetErrorString(ae);
+        });
       }
       if (!why.empty()) {
         lk.unlock();
