@@ -80,7 +80,7 @@ def test_layer1_forward(gpu, H):
     be1 = torch.randn(16, device=gpu) * 0.1
     rm, rv = torch.zeros(16, device=gpu), torch.ones(16, device=gpu)
     nbt = torch.zeros((), dtype=torch.long, device=gpu)
-    p1, idx1, stats, gram = _ops().fused_l1_forward(x, w1, b1, g1, be1, rm, rv, nbt, 0.1, 1e-5)
+    p1, idx1, stats, gram, _ = _ops().fused_l1_forward(x, w1, b1, g1, be1, rm, rv, nbt, 0.1, 1e-5)
     xd = x.double().cpu()
     y = F.conv2d(xd, w1.double().cpu(), b1.double().cpu(), padding=2)
     rmr, rvr = torch.zeros(16, dtype=torch.float64), torch.ones(16, dtype=torch.float64)
@@ -296,7 +296,7 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     assert (db2.double().cpu() - br.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item()
 
 
-def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False):
+def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_scale=None, p1_above=None):
     import torch.nn as nn
 
     from torch_distributed_sandbox_amd.models import ConvNet, fc_in_features
@@ -318,6 +318,10 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False):
     ours = ConvNet(image_shape=(H, H), mode="fused")
     with torch.no_grad():
         ours.layer2[1].weight[::3].neg_()  # some negative BN2 gammas: min-pooled windows
+        if gamma1 is not None:  # BN1 output (= p1, conv2's fp16 operand) scaled up
+            ours.layer1[1].weight.fill_(gamma1)
+        if w2_scale is not None:  # conv2 weights scaled down (the exactly carried fp16 operand)
+            ours.layer2[0].weight.mul_(w2_scale)
     ref = Ref(fc_in_features((H, H))).double()
     ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in ours.state_dict().items()})
     # the reference's precision class: its convolutions with TF32 operands (tests/_tf32ref.py)
@@ -342,6 +346,9 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False):
         else:
             x = xin = torch.rand(B, 1, H, H, device=gpu)
         y = torch.randint(0, 10, (B,), device=gpu)
+        if p1_above is not None and s == 0:  # the case is real: fp32 p1 leaves fp16's range
+            with torch.no_grad():
+                assert ref.layer1(x.double().cpu()).max().item() > p1_above
         loss = crit(ours(xin), y)
         opt.zero_grad()
         loss.backward()
@@ -384,6 +391,21 @@ def test_fused_model_matches_reference(gpu):
     _fused_vs_ref(gpu, B=3, H=64)
 
 
+def test_fused_model_p1_beyond_fp16_range(gpu):
+    """BN1's gamma at 3e4: the fp32 p1 passes fp16's 65504.  The layer-1 epilogue stores p1 at
+    the power-of-two scale its Samuelson bound (|xhat| <= sqrt(n-1)) asks for and the conv2
+    kernels take it out: forward, gradients and buffers still match the fp64 reference within
+    the TF32 class, never inf / NaN."""
+    _fused_vs_ref(gpu, B=3, H=64, gamma1=3e4, p1_above=65504.0)
+
+
+def test_fused_model_tiny_conv2_weights(gpu):
+    """conv2 weights ~5e-6 (below fp16's normal range 2^-14): packed at a power-of-two scale
+    (conv2_pack.hip) so hi + lo stay exact; the step matches the fp64 reference within the TF32
+    class."""
+    _fused_vs_ref(gpu, B=3, H=64, w2_scale=1e-4)
+
+
 @pytest.mark.parametrize("H", [64, 76])
 def test_fused_model_levels_input_matches_reference(gpu, H):
     """uint8 level batches (ToTensor's 1/255 folded into conv1, the x moments from exact integer
@@ -414,8 +436,8 @@ def test_layer1_levels_forward_backward(gpu, H):
         nbt = torch.zeros((), dtype=torch.long, device=gpu)
         return _ops().fused_l1_forward(inp, w1, b1, g1, be1, rm, rv, nbt, 0.1, 1e-5), rm, rv
 
-    (p1l, idxl, statsl, graml), rml, rvl = fwd(lv)
-    (p1f, idxf, statsf, gramf), rmf, rvf = fwd(x)
+    (p1l, idxl, statsl, graml, _), rml, rvl = fwd(lv)
+    (p1f, idxf, statsf, gramf, _), rmf, rvf = fwd(x)
     # exact integer moments of the levels, scaled in fp64 by the fp32 constant
     sc = float(torch.tensor(1.0 / 255.0, dtype=torch.float32))
     pat = F.unfold(lv.double().cpu(), 5, padding=2)

@@ -38,3 +38,19 @@ def test_oom_demo_ddp_half_shared_device_rehearsal(gpu):
     assert rec["world_size"] == 2 and rec["effective_batch"] == 10 and rec["shared_device"]
     assert rec["bs_fail_result"]["oom"] is False  # 512^2 fits: the rehearsal checks the path only
     assert rec["bs_fit_result"]["batch_per_rank"] == 5 and rec["bs_fit_result"]["ms_per_step"] > 0
+
+
+def test_mnist_onegpu_runs_the_tuned_plan(gpu):
+    """mnist_onegpu.py on the GPU runs the plan bench.py measures (DDP wrapper at world size 1:
+    flat buffers, the fc SGD step fused into the head backward, overlapped optimizer) with the
+    device-resident loader, and still prints the reference's log lines."""
+    import json
+
+    p = subprocess.run([sys.executable, "mnist_onegpu.py", "--image-size", "512", "--epochs", "1", "--max-steps", "6",
+                        "--log-interval", "3", "--dataset-size", "200", "--json"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "Epoch [1/1], Step [3/6], Loss:" in p.stdout and "Training complete in:" in p.stdout
+    r = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert r["steps"] == 6 and r["plan"].startswith("DDP wrapper (native reducer, fc grad local")
+    assert "overlap_optimizer=True" in r["plan"] and r["ms_per_step"] > 0

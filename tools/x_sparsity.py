@@ -31,7 +31,7 @@ def fc_input(model, x):
     conv2, bn2 = model.layer2[0], model.layer2[1]
     fc = model.fc
     with torch.no_grad():
-        p1, _, _, _ = ops.fused_l1_forward(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, None, None, None,
+        p1, _, _, _, p1s = ops.fused_l1_forward(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, None, None, None,
                                            float(bn1.momentum), float(bn1.eps), None, None)
         wp, _ = ops.conv2_pack(conv2.weight)
         y2, partial2, ya = ops.fused_conv2_forward(p1, wp, conv2.bias, bn2.weight)

@@ -202,7 +202,9 @@ std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
   return {asum, strips};
 }
 
-std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
+// returns (p1 [B,P,P,16] fp16, idx1, stats1 [mean16|invstd16], gram, p1_scale [1]: the power of two
+// p1 is stored at -- 1 unless BN1's affine could push p1 past fp16's range, convnet_fused.hip)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     const Tensor& x, const Tensor& w1, const Tensor& b1, const c10::optional<Tensor>& gamma1,
     const c10::optional<Tensor>& beta1, const c10::optional<Tensor>& rm1, const c10::optional<Tensor>& rv1,
     const c10::optional<Tensor>& nbt1, double momentum, double eps, const c10::optional<Tensor>& asum_in,
@@ -240,7 +242,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   auto gram = at::empty({650}, fo.dtype(at::kDouble));
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
   auto stats = at::empty({32}, fo);
-  auto aff = at::empty({32}, fo);
+  auto aff = at::empty({33}, fo);  // a16 | b16 | p1 scale
   tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H, (int)W,
               w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps,
               (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
@@ -250,11 +252,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   tds_l1_apply(x.data_ptr(), levels, w1.data_ptr<float>(), b1.data_ptr<float>(), aff.data_ptr<float>(),
                p1.data_ptr(), idx1.data_ptr<uint8_t>(), l1_wg(), (int)B, (int)H, (int)W, st);
   check_launches("fused_l1_forward");
-  return {p1, idx1, stats, gram};
+  return {p1, idx1, stats, gram, aff.narrow(0, 32, 1)};
 }
 
 // ---------------------------------------------------------------- conv2 forward
-constexpr int64_t kMagParts = 64;  // ypart offset in the mag workspace
+constexpr int64_t kMagParts = 64;   // ypart offset in the mag workspace
+constexpr int64_t kMagScales = 40;  // conv2 epilogue scales (csrc/kernels/conv2_common.h)
 int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
 int64_t mag_gpart_count(int64_t B, int64_t P) {
   return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_pb_nblk((int)(P / 2));
@@ -270,12 +273,16 @@ uint32_t* opt_mag(const c10::optional<Tensor>& mag, int64_t numel = 33) {
 }
 
 // fp16 hi/lo weight packs of the conv2 forward and data gradient; resets mag when given
-std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tensor>& mag) {
+// With mag: weights packed at a power-of-two scale that keeps them in fp16's normal range, the
+// scale and p1_scale's inverse recorded in mag for the conv2 epilogues (conv2_pack.hip).
+std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tensor>& mag,
+                                      const c10::optional<Tensor>& p1_scale) {
   need(w2, at::kFloat, {32, 16, 5, 5}, "conv2.weight");
+  const float* ps = optf(p1_scale, 1, "p1_scale");
   c10::DeviceGuard guard(w2.device());
   auto wp = at::empty({2 * 13 * 2 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
   auto wd = at::empty({2 * 25 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
-  tds_conv2_pack_weights(w2.data_ptr<float>(), wp.data_ptr<int16_t>(), wd.data_ptr<int16_t>(), opt_mag(mag),
+  tds_conv2_pack_weights(w2.data_ptr<float>(), wp.data_ptr<int16_t>(), wd.data_ptr<int16_t>(), opt_mag(mag), ps,
                          stream_of(w2));
   check_launches("conv2_pack");
   return {wp, wd};
@@ -304,8 +311,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const T
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
   tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr<float>(),
                  ya.data_ptr<float>(), partial.data_ptr<double>(),
-                 opt_mag(mag, kMagParts + 32 * mag_ypart_count()) ? opt_mag(mag) + kMagParts : nullptr, order, nwg,
-                 sw, sk, (int)B, (int)P, stream_of(p1));
+                 opt_mag(mag, kMagParts + 32 * mag_ypart_count()) ? opt_mag(mag) + kMagParts : nullptr,
+                 opt_mag(mag) ? opt_mag(mag) + kMagScales : nullptr, order, nwg, sw, sk, (int)B, (int)P, stream_of(p1));
   check_launches("fused_conv2_forward");
   return {y2, partial, ya};
 }
@@ -743,10 +750,10 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
       "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps, Tensor? asum=None, Tensor? strips=None) -> "
-      "(Tensor, Tensor, Tensor, Tensor)",
+      "(Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_forward);
   m.def("l1_input_stats(Tensor x) -> (Tensor, Tensor)", &l1_input_stats);
-  m.def("conv2_pack(Tensor w2, Tensor(a!)? mag=None) -> (Tensor, Tensor)", &conv2_pack);
+  m.def("conv2_pack(Tensor w2, Tensor(a!)? mag=None, Tensor? p1_scale=None) -> (Tensor, Tensor)", &conv2_pack);
   m.def(
       "fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2, Tensor(a!)? mag=None) -> "
       "(Tensor, Tensor, Tensor)",

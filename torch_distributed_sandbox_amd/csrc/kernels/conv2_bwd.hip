@@ -70,7 +70,7 @@ constexpr int BR_OFF_P = BR_OFF_D + 3 * BR_SLOT * BR_DROW;   // 3 x 12 p1 row bl
 constexpr int BR_XCHG = 2 * 4 * 64 * 16;                     // 8 KiB exchange slot
 constexpr int BR_OFF_X = BR_OFF_P + 3 * BR_SLOT * BR_PROW;   // 2 exchange slots
 constexpr int BR_OFF_K = BR_OFF_X + 2 * BR_XCHG;             // 160 floats of constants + 4
-constexpr int BR_KINV = 160;                                 // kc[160] = 2^-e (the dy2 scale's inverse)
+constexpr int BR_KINV = 160;  // kc[160] = 2^-e * 2^-ew (dp1), kc[161] = 2^-e / p1 scale (weight taps), kc[162] = 2^-e (bias)
 constexpr int BR_LDS = BR_OFF_K + (5 * 32 + 4) * 4;
 static_assert(BR_LDS <= 160 * 1024 && BR_OFF_X % 16 == 0 && BR_OFF_K % 16 == 0, "LDS carve");
 
@@ -337,7 +337,10 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)(li == 0 ? kF16One : 0);
   const int hp = (g >> 1) * BR_DPL + (g & 1) * 16;
-  const float inv = reinterpret_cast<const float*>(smem + BR_OFF_K)[BR_KINV];  // 2^-e
+  // epilogue scales (powers of two, exact): dp1 takes out the dy2 and packed-weight scales, the
+  // weight-gradient slab the dy2 and p1 scales, the bias tap (dy2 sums) the dy2 scale only
+  const float inv = reinterpret_cast<const float*>(smem + BR_OFF_K)[ROLE < 2 ? BR_KINV : BR_KINV + 1];
+  const float inv_b = reinterpret_cast<const float*>(smem + BR_OFF_K)[BR_KINV + 2];
   BRTile prev{0, 0, 0, false, true};
   BRClock<DIAG> clk;
   clk.start();
@@ -372,7 +375,7 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
 #pragma unroll
       for (int h = 0; h < 2; ++h)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) out[(tap * 32 + 16 * h + 4 * g + r) * 16 + li] = R[k][h][r] * inv;
+        for (int r = 0; r < 4; ++r) out[(tap * 32 + 16 * h + 4 * g + r) * 16 + li] = R[k][h][r] * (tap < 25 ? inv : inv_b);
     }
   }
 }
@@ -711,7 +714,12 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
       kc[96 + c] = k2 * sc;
       kc[128 + c] = k3 * sc;
     }
-    if (tid == 0) kc[BR_KINV] = ldexpf(1.f, -e);
+    if (tid == 0) {
+      const float ie = ldexpf(1.f, -e);
+      kc[BR_KINV] = ie * __uint_as_float(mag[kMagScales]);          // dy2 and packed-weight scales
+      kc[BR_KINV + 1] = ie * __uint_as_float(mag[kMagScales + 1]);  // dy2 and p1 scales
+      kc[BR_KINV + 2] = ie;
+    }
   }
   __syncthreads();  // kc visible to every role
   switch (wv) {

@@ -7,6 +7,10 @@
 
 namespace tds {
 
+// Words of the step's magnitude workspace ("mag", fused_ops.cpp) past the 33 bounds: written by
+// conv2_pack_weights_kernel, read by the conv2 forward / backward epilogues (powers of two).
+constexpr int kMagScales = 40;  // mag[40] = 2^-ew (packed weights' scale), mag[41] = 1 / p1 scale
+
 // ---------------------------------------------------------------------------- diagnostics
 // DIAG = 0: the real kernel.  Timing-only builds (tools/conv2_diag.py, TDS_CONV2_DIAG):
 //   1: no MFMAs (operand reads kept alive by one VALU op),  2: no LDS operand reads

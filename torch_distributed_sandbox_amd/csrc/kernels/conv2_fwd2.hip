@@ -149,8 +149,8 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
 
 // stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li]
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
-                                         int RH, int NT, int lane, float bco, bool neg, float& s_acc, float& q_acc,
-                                         uint32_t& ymx) {
+                                         int RH, int NT, int lane, float bco, float inv, bool neg, float& s_acc,
+                                         float& q_acc, uint32_t& ymx) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
 #pragma unroll
@@ -160,24 +160,27 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int px = 4 * g + r;
-      const float v = acc[o][r];  // y2 - b2: statistics shifted by the bias
+      const float v = acc[o][r];  // (y2 - b2) / inv: statistics shifted by the bias, scaled at the end
+      const float y = fmaf(v, inv, bco);
       if (rok && x.c0 + px < P) {
         s_acc += v;
         q_acc += v * v;
-        ymx = max(ymx, __float_as_uint(v + bco) & 0x7fffffffu);  // |y2| bits (NaN: above every finite)
+        ymx = max(ymx, __float_as_uint(y) & 0x7fffffffu);  // |y2| bits (NaN: above every finite)
       }
-      *reinterpret_cast<float*>(stage + f2_stage_off(row, px, co >> 2) + (co & 3) * 4) = v + bco;
+      *reinterpret_cast<float*>(stage + f2_stage_off(row, px, co >> 2) + (co & 3) * 4) = y;
     }
   }
   // pooled windows (rows 4RH + 2i + {0,1}, columns 4g + 2j + {0,1}) -> ya block entry
-  // (prow 2RH + i, pcol 2g + j); fp32 addition is monotone, so max(v) + b2 == max(v + b2)
+  // (prow 2RH + i, pcol 2g + j); v -> v * inv + b2 is monotone (inv > 0) and rounds monotonically,
+  // so ext(v) * inv + b2 == ext(v * inv + b2)
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     float e[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
-      e[j] = f2_ext4(acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], acc[2 * i + 1][2 * j + 1], neg) +
-             bco;
+      e[j] = fmaf(f2_ext4(acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], acc[2 * i + 1][2 * j + 1],
+                          neg),
+                  inv, bco);
     // pcols 2g, 2g+1 are adjacent floats of one swizzled chunk: one ds_write_b64
     *reinterpret_cast<float2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_float2(e[0], e[1]);
   }
@@ -213,8 +216,8 @@ template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
                                        const float* __restrict__ bias, const float* __restrict__ gamma,
                                        float* __restrict__ y2, float* __restrict__ ya, double* __restrict__ partial,
-                                       uint32_t* __restrict__ ypart, const int* __restrict__ order, int sw, int sk,
-                                       int B, int P, char* smem) {
+                                       uint32_t* __restrict__ ypart, const uint32_t* __restrict__ scales,
+                                       const int* __restrict__ order, int sw, int sk, int B, int P, char* smem) {
   constexpr int NT = WV & 1, RH = WV >> 1;
   const int lane = threadIdx.x & 63, li = lane & 15;
   const int tiles_c = (P + F2_TC - 1) / F2_TC, tiles_r = (P + F2_TH - 1) / F2_TH;
@@ -238,6 +241,8 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
 #pragma unroll
     for (int hl = 0; hl < 2; ++hl) W[s][hl] = __builtin_bit_cast(f32x4, wpack[((hl * 13 + s) * 2 + NT) * 64 + lane]);
   const float bco = bias[16 * NT + li];
+  // the packed weights' and p1's power-of-two scales (conv2_pack.hip): y2 = acc * inv + b2, exact
+  const float inv = scales != nullptr ? __uint_as_float(scales[0]) * __uint_as_float(scales[1]) : 1.f;
   const bool neg = gamma != nullptr && gamma[16 * NT + li] < 0.f;
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
@@ -261,7 +266,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     }
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
     f2_stage(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane, bco,
-             neg, s_acc, q_acc, ymx);
+             inv, neg, s_acc, q_acc, ymx);
     prev = cur;
     have_prev = true;
   }
@@ -290,7 +295,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   if (WV == 0 && lane < 64) {
     const int co = lane >> 1, k = lane & 1, nt = co >> 4, c16 = co & 15;
     // waves with this co half: nt (rows 0-3) and nt + 2 (rows 4-7)
-    const double v = red[(nt * 16 + c16) * 2 + k] + red[((nt + 2) * 16 + c16) * 2 + k];
+    const double v = (red[(nt * 16 + c16) * 2 + k] + red[((nt + 2) * 16 + c16) * 2 + k]) * (k ? (double)inv * inv : inv);
     partial[((int64_t)co * gridDim.x + blockIdx.x) * 2 + k] = v;
     // this workgroup's max |y2| per channel: a plain store per (channel, workgroup), reduced by
     // the BN2-backward finalize (no same-address atomics: 16 K of them cost ~40 us in the head)
@@ -306,14 +311,15 @@ __global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* 
                                                                    float* __restrict__ y2, float* __restrict__ ya,
                                                                    double* __restrict__ partial,
                                                                    uint32_t* __restrict__ ypart,
+                                                                   const uint32_t* __restrict__ scales,
                                                                    const int* __restrict__ order, int sw, int sk,
                                                                    int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
-  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
-  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
-  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
-  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P, smem);
+  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
+  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
+  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
+  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
 }
 
 }  // namespace tds
@@ -342,7 +348,8 @@ static int f2_diag_env() { return 0; }
 // order: the blocked tile order table (tds_tile_order_fill) as per-workgroup lists [nwg][ceil(total / nwg)]
 // (fused_ops.cpp tile_order, sw / sk: the strides of workgroup / tile), allocated by the caller
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, uint32_t* ypart, const int* order, int nwg, int sw, int sk, int B, int P, hipStream_t st) {
+                    double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
+                    int B, int P, hipStream_t st) {
   const dim3 grid(nwg), block(F2_THREADS);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wp);
@@ -360,12 +367,12 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const fl
   }
   switch (f2_diag_env()) {
 #ifdef TDS_DIAG
-    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
-    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
-    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
-    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
 #endif
-    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, order, sw, sk, B, P); break;
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
   }
   TDS_LAUNCH_CHECK();
 }

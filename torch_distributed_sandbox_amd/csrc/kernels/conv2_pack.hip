@@ -22,20 +22,53 @@ namespace tds {
 //       input-row A fragment serves every output row:  s < 10: (ky = s>>1, kx = 2(s&1) + (g>>1));
 //       s = 10 + kp: (ky = 2kp + (g>>1), kx = 4)  (ky = 5 -> zero)
 // dgrad: wd[hl][s<25][g<4][ci16][j8],      k = 32s+8g+j -> tap' = s, co = 8g+j; w = w2[co][ci][24-tap']
-// mag (optional, 33 words): the step's magnitude bounds (max |y2| per channel, max |g2m|) are
-// reset here, at the start of the conv2 forward they feed (conv2_fwd2.hip, head_pb.hip)
+// mag (optional, kMagScales + 2 words): the step's magnitude bounds (max |y2| per channel, max
+// |g2m|) are reset here, at the start of the conv2 forward they feed (conv2_fwd2.hip, head_pb.hip).
+//
+// fp16 range of the exactly carried weights: hi + lo represents w to ~2^-22 relative only while
+// lo stays a normal fp16 (|w| >= ~2^-3); below fp16's normal range (|w| < 2^-14) even the
+// per-product bound 2^-11 of fp16x2 breaks.  With mag given, the packed weights are w * 2^ew with
+// max |w| * 2^ew in [2^14, 2^15) (every block finds max |w| itself over the 12 800 weights: no
+// inter-block step), and mag[kMagScales] = 2^-ew, mag[kMagScales + 1] = 1 / p1_scale (the layer-1
+// range guard, convnet_fused.hip l1_gram; 1 when not given) are what the conv2 forward and
+// backward epilogues multiply their accumulators by (powers of two: exact).  Without mag the
+// weights are packed unscaled.
 __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* __restrict__ wp,
-                                          short* __restrict__ wd, uint32_t* __restrict__ mag) {
+                                          short* __restrict__ wd, uint32_t* __restrict__ mag,
+                                          const float* __restrict__ p1_scale) {
   const int FW = 13 * 2 * 4 * 16 * 8;  // per hl plane (fwd)
   const int DW = 25 * 4 * 16 * 8;      // per hl plane (dgrad)
-  if (mag != nullptr && blockIdx.x == 0 && threadIdx.x < 33) mag[threadIdx.x] = 0u;
+  __shared__ float red[4];
+  float wsc = 1.f;
+  if (mag != nullptr) {
+    float m = 0.f;
+    for (int e = threadIdx.x; e < 32 * 16 * 25; e += blockDim.x) m = fmaxf(m, fabsf(w2[e]));  // NaN: ignored
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    int ew = 0;
+    if (m > 0.f && __builtin_isfinite(m)) {
+      int x;
+      (void)frexpf(m, &x);  // m < 2^x
+      ew = min(100, max(-100, 15 - x));
+    }
+    wsc = ldexpf(1.f, ew);
+    if (blockIdx.x == 0) {
+      if (threadIdx.x < 33) mag[threadIdx.x] = 0u;
+      if (threadIdx.x == 0) {
+        mag[kMagScales] = __float_as_uint(ldexpf(1.f, -ew));
+        mag[kMagScales + 1] = __float_as_uint(p1_scale != nullptr ? 1.f / p1_scale[0] : 1.f);
+      }
+    }
+  }
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < FW + DW; e += gridDim.x * blockDim.x) {
     if (e < FW) {
       const int j = e & 7, co_in = (e >> 3) & 15, g = (e >> 7) & 3, nt = (e >> 9) & 1, s = e >> 10;
       const int ky = s < 10 ? (s >> 1) : 2 * (s - 10) + (g >> 1);
       const int kx = s < 10 ? 2 * (s & 1) + (g >> 1) : 4;
       const int ci = 8 * (g & 1) + j, co = nt * 16 + co_in;
-      const float v = ky < 5 ? w2[(co * 16 + ci) * 25 + ky * 5 + kx] : 0.f;
+      const float v = ky < 5 ? w2[(co * 16 + ci) * 25 + ky * 5 + kx] * wsc : 0.f;
       unsigned short hi, lo;
       split_f16(v, hi, lo);
       wp[e] = (short)hi;
@@ -44,7 +77,7 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
       const int f = e - FW;
       const int j = f & 7, ci = (f >> 3) & 15, g = (f >> 7) & 3, s = f >> 9;
       const int co = 8 * g + j;
-      const float v = w2[(co * 16 + ci) * 25 + (24 - s)];
+      const float v = w2[(co * 16 + ci) * 25 + (24 - s)] * wsc;
       unsigned short hi, lo;
       split_f16(v, hi, lo);
       wd[f] = (short)hi;
@@ -89,8 +122,9 @@ __global__ __launch_bounds__(256) void conv2_wgrad_reduce_kernel(const float* __
 
 using namespace tds;
 
-void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, hipStream_t st) {
-  hipLaunchKernelGGL(conv2_pack_weights_kernel, dim3(64), dim3(256), 0, st, w2, wp, wd, mag);
+void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, const float* p1_scale,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(conv2_pack_weights_kernel, dim3(64), dim3(256), 0, st, w2, wp, wd, mag, p1_scale);
   TDS_LAUNCH_CHECK();
 }
 

@@ -253,7 +253,7 @@ __device__ void bn_finalize_channel(int c, int C, double s, double ss, int64_t n
                                     float eps, float momentum, const float* __restrict__ gamma,
                                     const float* __restrict__ beta, float* __restrict__ stats,
                                     float* __restrict__ running_mean, float* __restrict__ running_var,
-                                    float* __restrict__ aff) {
+                                    float* __restrict__ aff, float aff_scale = 1.f) {
   const double m0 = s / (double)n;
   double var = ss / (double)n - m0 * m0;
   if (var < 0.0) var = 0.0;
@@ -267,8 +267,8 @@ __device__ void bn_finalize_channel(int c, int C, double s, double ss, int64_t n
     running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
   }
   const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  aff[c] = gm * invstd;
-  aff[C + c] = bt - (float)mean * gm * invstd;
+  aff[c] = gm * invstd * aff_scale;  // aff_scale: a power of two (the p1 range guard), exact
+  aff[C + c] = (bt - (float)mean * gm * invstd) * aff_scale;
 }
 
 // BN2: reduce the per-workgroup partials of channel c (partial[c][nchunk][2], fixed order) and
@@ -793,6 +793,29 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
     for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k][j];
     Gw[c][j] = h * (double)w1[c * 25 + j];
   }
+  // p1's fp16 range guard (conv2's single operand, fp16x2): p1 = relu(gamma * xhat + beta) and,
+  // for ANY batch, |xhat| <= sqrt(n - 1) (Samuelson's inequality, population variance; eps only
+  // shrinks it), so max p1 <= max_c |gamma_c| sqrt(n - 1) + |beta_c| before the data is seen.
+  // If that bound (with a 2^-10 margin for the conv's rounding) passes fp16's 65504, the BN1
+  // affine -- and with it p1 -- is scaled by the power of two 2^e1 that keeps it in range
+  // (ReLU and max-pool commute with it); aff[32] = 2^e1, taken out exactly by the conv2 kernels
+  // (conv2_pack.hip records its inverse).  |gamma| <= ~9.7 at beta = 0 leaves e1 = 0, p1 as is.
+  float p1_scale = 1.f;
+  if (tid < 64) {
+    const int c = tid & 15;
+    const double sq = sqrt((double)((int64_t)B * H * W - 1));
+    double bound = tid < 16 ? fabs(gamma ? (double)gamma[c] : 1.0) * sq + fabs(beta ? (double)beta[c] : 0.0) : 0.0;
+    for (int off = 32; off > 0; off >>= 1) bound = fmax(bound, __shfl_xor(bound, off, 64));
+    bound *= 1.0 + 1.0 / 1024.0;
+    int e1 = 0;
+    if (bound > 65504.0 && __builtin_isfinite(bound)) {
+      int x;
+      (void)frexp(bound / 65504.0, &x);  // bound / 65504 < 2^x
+      e1 = -min(x, 120);
+    }
+    p1_scale = ldexpf(1.f, e1);
+    if (tid == 0) aff[32] = p1_scale;
+  }
   __syncthreads();
   if (tid < 16) {
     double s = 0.0, q = 0.0;
@@ -805,7 +828,7 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
     // BN1 statistics of (y1 - b1) finalized here (no separate finalize launch)
     if (tid == 0 && num_batches) num_batches[0] += 1;
     bn_finalize_channel(tid, 16, s, q, (int64_t)B * H * W, b1, eps, momentum, gamma, beta, stats, running_mean,
-                        running_var, aff);
+                        running_var, aff, p1_scale);
   }
 }
 

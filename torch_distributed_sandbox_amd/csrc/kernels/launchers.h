@@ -64,7 +64,8 @@ void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  //
 
 // ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, fp16x2 split MFMA)
 // mag (optional): 33 words of magnitude bounds [max|y2| per channel (32) | max|g2m|], zeroed here
-void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, hipStream_t st);
+void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, const float* p1_scale,
+                            hipStream_t st);
 int tds_conv2_num_wg();  // CUs (tds_device_cus)
 // ---- cu_budget.hip: CUs the persistent kernels may use (all minus a reserve for RCCL) and
 // CU-masked compute streams
@@ -83,8 +84,10 @@ int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
 // y2 [B,P,P,32]; ya pooled-blocked (pooled_layout.h), max/min of each 2x2 window by sign(gamma2)
 // ypart (optional): max |y2| per (channel, workgroup), [32][nwg] float bits
+// scales (optional): mag + kMagScales (conv2_pack.hip), the packed weights' and p1's inverse scales
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
-                    double* partial, uint32_t* ypart, const int* order, int nwg, int sw, int sk, int B, int P, hipStream_t st);
+                    double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
+                    int B, int P, hipStream_t st);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups

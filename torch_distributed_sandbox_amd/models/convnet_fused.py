@@ -130,9 +130,10 @@ def _zero_scalar(device, dtype):
 
 
 class _Layer1Link:
-    """Carries the conv2 backward's fp32 dp1 to the layer-1 backward (p1 itself is fp16)."""
+    """Carries the conv2 backward's fp32 dp1 to the layer-1 backward (p1 itself is fp16), and the
+    power-of-two scale p1 is stored at to the conv2 kernels."""
 
-    __slots__ = ("dp1",)
+    __slots__ = ("dp1", "p1_scale")
 
 
 class _Layer1(torch.autograd.Function):
@@ -141,8 +142,9 @@ class _Layer1(torch.autograd.Function):
         ops = _ext.ops()
         asum, strips = _take_input_stats(x)
         x = x.contiguous()
-        p1, idx1, stats1, gram = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps, asum,
-                                                      strips)
+        p1, idx1, stats1, gram, p1_scale = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps,
+                                                                asum, strips)
+        link1.p1_scale = p1_scale  # p1's fp16 range guard (a power of two, 1 normally): conv2 takes it out
         ctx.save_for_backward(x, p1, idx1, w1, b1, g1, stats1, gram)
         ctx.params = (w1, b1, g1, be1)
         ctx.link1 = link1
@@ -175,7 +177,7 @@ class _Conv2(torch.autograd.Function):
         # magnitude bounds of this step (per-workgroup max |y2| here, max |g2m| in the head
         # backward, reduced by its BN2 finalize): the conv2 backward's fp16 scale of dy2
         link.mag = torch.empty(ops.mag_numel(p1.shape[0], p1.shape[1]), device=p1.device, dtype=torch.int32)
-        wp, wd = ops.conv2_pack(w2.contiguous(), link.mag)
+        wp, wd = ops.conv2_pack(w2.contiguous(), link.mag, getattr(link1, "p1_scale", None))
         y2, partial2, ya = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
         ctx.save_for_backward(p1, wd, y2)
         ctx.params = (w2, b2)

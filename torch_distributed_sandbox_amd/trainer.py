@@ -99,7 +99,13 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
     batch_size = args.batch_size
     criterion = CrossEntropyLoss()
     optimizer = SGD(model.parameters(), args.lr)
-    if distributed:
+    if distributed or device.type == "cuda":
+        # the tuned plan bench.py measures, also for the single-GPU script: at world size 1 the
+        # wrapper owns the flat parameter / gradient buffers (one SGD sweep over the small
+        # parameters), fuses the fc weight's SGD step into the head backward kernel
+        # (ops/fused_update.py) and finishes the rest under the next forward (overlap_optimizer)
+        # -- the reference's mnist_onegpu.py has no wrapper and steps all 180 M parameters in a
+        # separate pass
         model = DistributedDataParallel(model, device_ids=[gpu] if device.type == "cuda" else None,
                                         bucket_cap_mb=getattr(args, "bucket_mb", None),
                                         grad_exchange=getattr(args, "grad_exchange", "auto"),
@@ -165,7 +171,10 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
         torch.cuda.synchronize()
     t_end = time.perf_counter()
     summary = {"rank": rank, "world_size": world, "steps": steps_done, "batch_size": batch_size,
-               "image_size": H, "final_loss": float(loss.item()) if loss is not None else None}
+               "image_size": H, "final_loss": float(loss.item()) if loss is not None else None,
+               "plan": (f"DDP wrapper ({getattr(model, 'reducer_kind', '?')} reducer, fc grad "
+                        f"{model.fc_grad_path()}, overlap_optimizer={model.overlap_optimizer})"
+                        if isinstance(model, DistributedDataParallel) else "plain module")}
     if t_first is not None and steps_done > 1:
         dt = t_end - t_first
         summary["images_per_sec_per_rank"] = (steps_done - 1) * batch_size / dt
