@@ -1,10 +1,10 @@
-"""Numerics of the fused ConvNet plan (NHWC; conv1 bf16x3, conv2 fp16x2; pooled-blocked ya/g2m)
-vs fp64 PyTorch references of the same ops."""
+"""Numerics of the fused ConvNet plan (NHWC; conv1 bf16x3, conv2 TF32-class fp16 or fp16x2 by build;
+pooled-blocked ya/g2m) vs fp64 PyTorch references of the same ops."""
 import pytest
 import torch
 import torch.nn.functional as F
 
-from _tf32ref import rel, unfold_conv
+from _tf32ref import rel, tf32, unfold_conv
 
 pytestmark = pytest.mark.gpu
 
@@ -24,6 +24,25 @@ def _err(a, b):
 def _check(a, b, rel, name=""):
     e, s = _err(a, b)
     assert e <= rel * s + 1e-12, f"{name}: max err {e:.3e} vs scale {s:.3e} (rel {e / max(s, 1e-30):.2e})"
+
+
+def _split() -> bool:
+    """The build's conv2 operand precision (csrc/kernels/conv2_common.h TDS_CONV2_SPLIT): True =
+    fp16x2 (one operand hi + lo), False = one fp16 MFMA per product, both operands rounded to
+    TF32's 11 significant bits."""
+    return bool(_ops().conv2_split())
+
+
+def _check_conv(a, ref, ref_tf32, split_rel, name):
+    """A conv2 result vs fp64: split builds within ``split_rel`` (only one operand rounded); the
+    TF32-class build within 1.5x the error the same convolution with TF32-rounded operands makes
+    (tests/_tf32ref.py), or 1e-5 when that is smaller."""
+    if _split():
+        _check(a, ref, split_rel, name)
+        return
+    e, s = _err(a, ref)
+    et, _ = _err(ref_tf32, ref)
+    assert e <= max(1e-5 * s, 1.5 * et) + 1e-12, f"{name}: max err {e:.3e} vs TF32 convs {et:.3e} (scale {s:.3e})"
 
 
 def new_mag(gpu, B, P):
@@ -172,8 +191,10 @@ def test_conv2_forward(gpu, P):
     wp, wd = _ops().conv2_pack(w2, mag)
     y2, partial, ya = _ops().fused_conv2_forward(p, wp, b2, g2, mag)
     ref = F.conv2d(p.permute(0, 3, 1, 2).double().cpu(), w2.double().cpu(), b2.double().cpu(), padding=2)
-    # the weights are carried exactly (fp16 hi + lo): only fp32 accumulation error remains
-    _check(y2.permute(0, 3, 1, 2), ref, 5e-5, "y2")
+    reft = F.conv2d(p.permute(0, 3, 1, 2).double().cpu(), tf32(w2.cpu()), b2.double().cpu(), padding=2)
+    # split: the weights are carried exactly (fp16 hi + lo), only fp32 accumulation error remains;
+    # TF32 class: the weights rounded once, as TF32 rounds them
+    _check_conv(y2.permute(0, 3, 1, 2), ref, reft, 5e-5, "y2")
     # max |y2| per channel: the workgroups' maxima (plain stores) reduce to exactly the largest
     # stored value (the head backward's BN2 finalize does this reduction in the model)
     assert torch.equal(ypart(mag).amax(1).view(torch.float32), y2.abs().amax((0, 1, 2)))
@@ -288,10 +309,14 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     wr = w2.double().cpu().requires_grad_(True)
     br = torch.zeros(32, dtype=torch.float64, requires_grad=True)
     F.conv2d(pr, wr, br, padding=2).backward(dy2)
-    # dgrad: dy2 is the single-rounded fp16 operand (2^-11 per element)
-    _check(dp1.permute(0, 3, 1, 2), pr.grad, 5e-4, "dp1")
-    # wgrad: dy2 exact (fp16 hi + lo), p1 the stored fp16 operand itself
-    _check(dw2, wr.grad, 5e-5, "dw2")
+    # the same convolution backward with TF32 operands (dy2 and w2 rounded; p1 is fp16 already)
+    prt = p.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
+    wrt = tf32(w2.cpu()).requires_grad_(True)
+    F.conv2d(prt, wrt, None, padding=2).backward(tf32(dy2))
+    # dgrad: dy2 is the single-rounded fp16 operand (2^-11 per element), w2 split or rounded
+    _check_conv(dp1.permute(0, 3, 1, 2), pr.grad, prt.grad, 5e-4, "dp1")
+    # wgrad: dy2 exact (fp16 hi + lo) or rounded, p1 the stored fp16 operand itself
+    _check_conv(dw2, wr.grad, wrt.grad, 5e-5, "dw2")
     # conv bias before BN: sum(dy2) is analytically zero, both sides are rounding noise
     assert (db2.double().cpu() - br.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item()
 
@@ -348,16 +373,20 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_sca
         y = torch.randint(0, 10, (B,), device=gpu)
         if p1_above is not None and s == 0:  # the case is real: fp32 p1 leaves fp16's range
             with torch.no_grad():
-                assert ref.layer1(x.double().cpu()).max().item() > p1_above
+                import copy  # (a copy: the probe forward must not touch ref's BN running stats)
+
+                assert copy.deepcopy(ref.layer1)(x.double().cpu()).max().item() > p1_above
         loss = crit(ours(xin), y)
         opt.zero_grad()
         loss.backward()
         topt.zero_grad()
-        F.cross_entropy(reft(x.double().cpu()), y.cpu()).backward()
+        tl = F.cross_entropy(reft(x.double().cpu()), y.cpu())
+        tl.backward()
         rl = F.cross_entropy(ref(x.double().cpu()), y.cpu())
         ropt.zero_grad()
         rl.backward()
-        assert abs(loss.item() - rl.item()) <= 2e-4 * max(1.0, abs(rl.item())), (loss.item(), rl.item())
+        assert abs(loss.item() - rl.item()) <= max(2e-4 * max(1.0, abs(rl.item())), 1.5 * abs(tl.item() - rl.item())), (
+            loss.item(), rl.item(), tl.item())
         rp = dict(ref.named_parameters())
         rt = dict(reft.named_parameters())
         for n, p in ours.named_parameters():
@@ -396,7 +425,9 @@ def test_fused_model_p1_beyond_fp16_range(gpu):
     the power-of-two scale its Samuelson bound (|xhat| <= sqrt(n-1)) asks for and the conv2
     kernels take it out: forward, gradients and buffers still match the fp64 reference within
     the TF32 class, never inf / NaN."""
-    _fused_vs_ref(gpu, B=3, H=64, gamma1=3e4, p1_above=65504.0)
+    # one step: at this gamma the lr-0.05 step moves conv2's weights by O(1e3) and the next step
+    # is a different problem for each trajectory
+    _fused_vs_ref(gpu, B=3, H=64, steps=1, gamma1=3e4, p1_above=65504.0)
 
 
 def test_fused_model_tiny_conv2_weights(gpu):

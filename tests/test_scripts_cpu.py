@@ -102,7 +102,7 @@ def test_bench_self_spawns_ranks_cpu():
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
     assert r["config"]["global_batch"] == 10 and r["config"]["parallelism"] == "dp2"
     assert r["config"]["backend"] == "gloo" and r["value"] > 0
-    assert "bf16x3" in r["dtype"]
+    assert r["dtype"] == "fp32 (CPU rehearsal: torch ops)"
     (pr,) = r["config"]["allreduce_probe"]  # post-timing all-reduce bandwidth over the same communicator
     assert pr["MB"] > 0 and pr["ms"] > 0 and pr["busbw_GBps"] > 0
 

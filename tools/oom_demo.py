@@ -67,7 +67,7 @@ def run(H, B, steps, device, world, rank):
     src, lab = synthetic_batch(B, (H, H), device, seed=7 + rank)
     t0 = None
     for i in range(steps):
-        images = TF.upsample_bilinear_u8(src, H, H)
+        images = TF.upsample_bilinear_u8(src, H, H, levels=True)  # the bench / trainer default input
         loss = crit(ddp(images), lab)
         opt.zero_grad()
         loss.backward()

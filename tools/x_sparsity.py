@@ -9,7 +9,13 @@ head-forward kernel's x_out and reports, after 0 and after --train-steps SGD ste
 * the bytes of a lossless zero-suppressed encoding (1 mask bit per value + the non-zero
   values, per 32-value group), relative to the dense fp32 rows.
 
-    python tools/x_sparsity.py [--image-size 3000] [--batch-size 5] [--train-steps 20]
+    python tools/x_sparsity.py [--image-size 3000] [--batch-size 5] [--train-steps 20] [--data noise|mnist]
+
+``--data noise``: the bench's sources (uniform random 28x28 levels); ``--data mnist``: the
+trainer's SyntheticMNIST digits (dark background, bright strokes: data/synthetic.py).  Both go
+through the bench's input path (uint8 levels upsampled on device).  The JSON also carries the
+ratio of the exchange's real page format (parallel/zs.py: 2048-value pages, 64 mask words each
++ the non-zero values + the count slot) and the path ``choose_path`` picks with it at W = 2, 4, 8.
 """
 import argparse
 import json
@@ -43,6 +49,8 @@ def fc_input(model, x):
 
 
 def stats(X, group=32):
+    from torch_distributed_sandbox_amd.parallel import factored, zs
+
     zero = X == 0
     B, K = X.shape
     C = 32
@@ -52,9 +60,12 @@ def stats(X, group=32):
     mask_bytes = n / 8
     # per-group counts (one byte per group of 32 is enough to locate the compacted values)
     enc = mask_bytes + nz * 4 + n / group
+    # the exchange's own format (factored._meta_row: records + count slot), per rank = per batch
+    page_ratio = (nz + factored._meta_row(zs.meta_numel(n))) / n
     return {"zero_frac": round(1 - nz / n, 4), "zero_frac_per_channel": [round(v, 3) for v in per_ch],
             "dense_MB": round(n * 4 / 1e6, 1), "zero_suppressed_MB": round(enc / 1e6, 1),
-            "ratio": round(enc / (n * 4), 4)}
+            "ratio": round(enc / (n * 4), 4), "page_format_ratio": round(page_ratio, 4),
+            "choose_path": {w: factored.choose_path(B, 10, K, w, x_ratio=page_ratio) for w in (2, 4, 8)}}
 
 
 def main():
@@ -62,6 +73,7 @@ def main():
     ap.add_argument("--image-size", type=int, default=3000)
     ap.add_argument("--batch-size", type=int, default=5)
     ap.add_argument("--train-steps", type=int, default=20)
+    ap.add_argument("--data", default="noise", choices=["noise", "mnist"])
     args = ap.parse_args()
     from torch_distributed_sandbox_amd.data import synthetic_batch
     from torch_distributed_sandbox_amd.models import ConvNet
@@ -75,18 +87,25 @@ def main():
     opt = SGD(model.parameters(), 1e-4)
     crit = CrossEntropyLoss()
     pool = 16
-    src, lab = synthetic_batch(B * pool, (H, H), dev, seed=1234)
+    if args.data == "mnist":
+        from torch_distributed_sandbox_amd.data import SyntheticMNIST
+
+        ds = SyntheticMNIST(size=B * pool)
+        s_, l_ = ds.batch(list(range(B * pool)))
+        src, lab = s_.to(dev), l_.to(dev)
+    else:
+        src, lab = synthetic_batch(B * pool, (H, H), dev, seed=1234)
     src, lab = src.view(pool, B, 28, 28), lab.view(pool, B)
-    out = {"image_size": H, "batch": B}
-    x = TF.upsample_bilinear_u8(src[0], H, H)
+    out = {"image_size": H, "batch": B, "data": args.data}
+    x = TF.upsample_bilinear_u8(src[0], H, H, levels=True)
     out["step0"] = stats(fc_input(model, x))
     for i in range(args.train_steps):
-        x = TF.upsample_bilinear_u8(src[i % pool], H, H)
+        x = TF.upsample_bilinear_u8(src[i % pool], H, H, levels=True)
         loss = crit(model(x), lab[i % pool])
         opt.zero_grad()
         loss.backward()
         opt.step()
-    x = TF.upsample_bilinear_u8(src[args.train_steps % pool], H, H)
+    x = TF.upsample_bilinear_u8(src[args.train_steps % pool], H, H, levels=True)
     out[f"step{args.train_steps}"] = stats(fc_input(model, x))
     print(json.dumps(out), flush=True)
 

@@ -754,6 +754,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       &fused_l1_forward);
   m.def("l1_input_stats(Tensor x) -> (Tensor, Tensor)", &l1_input_stats);
   m.def("conv2_pack(Tensor w2, Tensor(a!)? mag=None, Tensor? p1_scale=None) -> (Tensor, Tensor)", &conv2_pack);
+  m.def("conv2_split() -> int", []() -> int64_t { return tds_conv2_split(); });
   m.def(
       "fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2, Tensor(a!)? mag=None) -> "
       "(Tensor, Tensor, Tensor)",

@@ -206,21 +206,24 @@ __device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][
     for (int k = 0; k < 5; ++k) {
       const int o = r - k;
       if (k < Q::nky(i) && o >= 0 && o < 8)
-        acc[o] = mma2<DIAG>(ah[s % 3], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
+        acc[o] = mmaw<DIAG>(ah[s % 3], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
                             __builtin_bit_cast(s16x8, R[5 * i + k][1]), acc[o]);
     }
   }
 }
 
 // ---------------------------------------------------------------------------- wgrad
-// c += (ahi + alo) * b: the wgrad's exact operand is dy2 (A), p1 (B) the single-rounded one
+// c += (ahi + alo) * b: split, the wgrad's exact operand is dy2 (A), p1 (B) the single-rounded
+// one; unsplit (TDS_CONV2_SPLIT 0, conv2_common.h) c += ahi * b, both rounded once
 template <int DIAG>
 __device__ __forceinline__ f32x4 mma2a(const s16x8& ahi, const s16x8& alo, const s16x8& b, f32x4 c) {
   if constexpr (DIAG == 1) {
     c[0] += (float)((int)(ahi[0] ^ alo[1] ^ b[2]) & 1);
     return c;
-  } else {
+  } else if constexpr (kConv2Split) {
     c = mfma_f16(alo, b, c);
+    return mfma_f16(ahi, b, c);
+  } else {
     return mfma_f16(ahi, b, c);
   }
 }
@@ -237,9 +240,13 @@ __device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2],
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const s16x4 x0 = ldtr<DIAG>(r0 + h * BR_DPL), x1 = ldtr<DIAG>(r1 + h * BR_DPL);
-      const s16x4 y0 = ldtr<DIAG>(r0 + (2 + h) * BR_DPL), y1 = ldtr<DIAG>(r1 + (2 + h) * BR_DPL);
       ahi[slot][h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      alo[slot][h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+      if constexpr (kConv2Split) {
+        const s16x4 y0 = ldtr<DIAG>(r0 + (2 + h) * BR_DPL), y1 = ldtr<DIAG>(r1 + (2 + h) * BR_DPL);
+        alo[slot][h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
+      } else {
+        alo[slot][h] = ahi[slot][h];  // (unused)
+      }
     }
   };
   auto load_b = [&](int s, int buf) {
@@ -566,18 +573,23 @@ struct BRStager {
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        uint32_t h01, l01, h23, l23;  // (k1..k3 carry the scale 2^e: d is dy2 * 2^e)
-        split2_f16_mix(d[q][0], d[q][1], h01, l01);
-        split2_f16_mix(d[q][2], d[q][3], h23, l23);
+        uint32_t h01, l01 = 0u, h23, l23 = 0u;  // (k1..k3 carry the scale 2^e: d is dy2 * 2^e)
+        if constexpr (kConv2Split) {
+          split2_f16_mix(d[q][0], d[q][1], h01, l01);
+          split2_f16_mix(d[q][2], d[q][3], h23, l23);
+        } else {  // dy2 rounded once (TF32-class, conv2_common.h): no lo planes
+          h01 = cvt2_f16(d[q][0], d[q][1]);
+          h23 = cvt2_f16(d[q][2], d[q][3]);
+        }
         const int lr = 2 * wy + (q >> 1);
         const int ro = (2 * wx + (q & 1)) * 32 + (c4 & 3) * 8;
         char* rec = dbase + lr * BR_DROW + ro;
         *reinterpret_cast<uint2*>(rec + (c4 >> 2) * BR_DPL) = make_uint2(h01, h23);
-        *reinterpret_cast<uint2*>(rec + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
+        if constexpr (kConv2Split) *reinterpret_cast<uint2*>(rec + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
         if (MIRROR && lr >= 4) {
           char* mr = dmir + (lr - 4) * BR_DROW + ro;
           *reinterpret_cast<uint2*>(mr + (c4 >> 2) * BR_DPL) = make_uint2(h01, h23);
-          *reinterpret_cast<uint2*>(mr + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
+          if constexpr (kConv2Split) *reinterpret_cast<uint2*>(mr + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
         }
       }
     }

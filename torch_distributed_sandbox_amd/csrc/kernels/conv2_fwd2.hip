@@ -112,7 +112,7 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
       for (int ky = 0; ky < 5; ++ky) {
         const int o = R - ky;
         if (o >= 0 && o < 4)
-          acc[o] = mma2<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[2 * ky + grp][0]),
+          acc[o] = mmaw<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[2 * ky + grp][0]),
                               __builtin_bit_cast(s16x8, W[2 * ky + grp][1]), acc[o]);
       }
     } else {
@@ -120,7 +120,7 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
       for (int kp = 0; kp < 3; ++kp) {
         const int o = R - 2 * kp;
         if (o >= 0 && o < 4)
-          acc[o] = mma2<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[10 + kp][0]),
+          acc[o] = mmaw<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[10 + kp][0]),
                               __builtin_bit_cast(s16x8, W[10 + kp][1]), acc[o]);
       }
     }

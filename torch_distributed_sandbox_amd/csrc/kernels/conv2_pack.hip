@@ -130,6 +130,8 @@ void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag
 
 int tds_conv2_num_wg() { return tds_device_cus(); }
 
+int tds_conv2_split() { return kConv2Split ? 1 : 0; }  // the build's conv2 operand precision (conv2_common.h)
+
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st) {
   hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db, scale);
   TDS_LAUNCH_CHECK();

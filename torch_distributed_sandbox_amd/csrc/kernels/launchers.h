@@ -64,6 +64,7 @@ void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  //
 
 // ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, fp16x2 split MFMA)
 // mag (optional): 33 words of magnitude bounds [max|y2| per channel (32) | max|g2m|], zeroed here
+int tds_conv2_split();  // 1: fp16x2 (one operand hi + lo), 0: one fp16 MFMA per product (TF32 class)
 void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, const float* p1_scale,
                             hipStream_t st);
 int tds_conv2_num_wg();  // CUs (tds_device_cus)

@@ -25,6 +25,10 @@ namespace tds {
 #define TDS_AC_RB 16
 #endif
 constexpr int AC_RB = TDS_AC_RB;
+// the uint8 path's moments are exact u32 sums: a thread adds 4 * AC_RB products of <= 255^2 and
+// a wave 64 threads' sums (x_autocorr_u8_kernel), which must stay below 2^32
+static_assert((unsigned long long)AC_RB * 4ull * 64ull * 65025ull < (1ull << 32),
+              "TDS_AC_RB too large: the u8 moments' u32 wave sums would overflow");
 
 static int x_autocorr_num_wg(int B, int H, int W) {
   if (W % 4 != 0 || B < 1 || H < 1) return 0;

@@ -228,8 +228,7 @@ class _CrossEntropy(torch.autograd.Function):
     def forward(ctx, logits, labels, ignore_index, label_smoothing):
         loss, dlogits = _ext.ops().cross_entropy(logits.contiguous(), labels.contiguous(), ignore_index,
                                                  label_smoothing)
-        ctx.save_for_backward(dlogits)
-        ctx.mark_non_differentiable()
+        ctx.save_for_backward(dlogits)  # (labels are integer: autograd already treats them as constants)
         return loss
 
     @staticmethod
