@@ -541,13 +541,12 @@ struct BRStager {
           const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
           const bool e0 = z[0] == m, e1 = !e0 && z[1] == m, e2 = !e0 && !e1 && z[2] == m;
           const bool e3 = !e0 && !e1 && !e2;
-          const float base[4] = {fmaf(k2[cc], y[0][cc], k3[cc]), fmaf(k2[cc], y[1][cc], k3[cc]),
-                                 fmaf(k2[cc], y[2][cc], k3[cc]), fmaf(k2[cc], y[3][cc], k3[cc])};
-          const float kg = k1[cc] * gg[cc];
-          d[0][cc] = e0 ? base[0] + kg : base[0];
-          d[1][cc] = e1 ? base[1] + kg : base[1];
-          d[2][cc] = e2 ? base[2] + kg : base[2];
-          d[3][cc] = e3 ? base[3] + kg : base[3];
+          // the pooled gradient folded into the constant: select + FMA per pixel
+          const float k3g = fmaf(k1[cc], gg[cc], k3[cc]);
+          d[0][cc] = fmaf(k2[cc], y[0][cc], e0 ? k3g : k3[cc]);
+          d[1][cc] = fmaf(k2[cc], y[1][cc], e1 ? k3g : k3[cc]);
+          d[2][cc] = fmaf(k2[cc], y[2][cc], e2 ? k3g : k3[cc]);
+          d[3][cc] = fmaf(k2[cc], y[3][cc], e3 ? k3g : k3[cc]);
         }
       } else {
         const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;
