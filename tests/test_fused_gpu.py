@@ -201,8 +201,9 @@ def test_conv2_forward(gpu, P):
     # BN2 partials: sum over workgroups of (sum, sumsq) of y2 - b2
     s = partial.view(32, -1, 2).sum(1).cpu()
     yc = ref - b2.double().cpu().view(1, 32, 1, 1)
-    _check(s[:, 0], yc.sum((0, 2, 3)), 1e-4, "sum")
-    _check(s[:, 1], (yc * yc).sum((0, 2, 3)), 1e-4, "sumsq")
+    yct = reft - b2.double().cpu().view(1, 32, 1, 1)
+    _check_conv(s[:, 0], yc.sum((0, 2, 3)), yct.sum((0, 2, 3)), 1e-4, "sum")
+    _check_conv(s[:, 1], (yc * yc).sum((0, 2, 3)), (yct * yct).sum((0, 2, 3)), 1e-4, "sumsq")
     # ya: extremes of the kernel's own y2 (exact selection, no rounding involved)
     Q = P // 2
     want = window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q].float(), (g2 < 0))
@@ -317,8 +318,14 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     _check_conv(dp1.permute(0, 3, 1, 2), pr.grad, prt.grad, 5e-4, "dp1")
     # wgrad: dy2 exact (fp16 hi + lo) or rounded, p1 the stored fp16 operand itself
     _check_conv(dw2, wr.grad, wrt.grad, 5e-5, "dw2")
-    # conv bias before BN: sum(dy2) is analytically zero, both sides are rounding noise
-    assert (db2.double().cpu() - br.grad).abs().max().item() <= 1e-4 * wr.grad.abs().max().item()
+    # conv bias before BN: sum(dy2) is analytically zero, both sides are rounding noise; with dy2
+    # rounded once to 11 significant bits (TF32 class) the noise is bounded by 2^-11 sum|dy2|
+    err = (db2.double().cpu() - br.grad).abs()
+    if _split():
+        assert err.max().item() <= 1e-4 * wr.grad.abs().max().item()
+    else:
+        bound = dy2.abs().sum((0, 2, 3)) * 2.0 ** -11 * 1.01 + 1e-4 * wr.grad.abs().max().item()
+        assert bool((err <= bound).all()), (err.max().item(), bound.min().item())
 
 
 def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_scale=None, p1_above=None):
