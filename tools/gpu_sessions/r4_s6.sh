@@ -7,6 +7,9 @@ set -u
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/r4s6
 mkdir -p $O
+cd $R
+timeout -k 10 200 python3 -u bench.py --gpus 1 --steps 20 --warmup 20 --step-times > $O/w20.log 2>&1 || { echo "w20 rc=$?"; exit 1; }
+python3 -c "import json,sys; r=json.loads(open('$O/w20.log').read().strip().splitlines()[-1]); s=r['config']['step_ms']; print('warmup20', r['ms_per_step'], s[:4], s[-3:])"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- \
   python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/trace.log 2>&1 || { echo "trace rc=$?"; tail -5 $O/trace.log; exit 1; }
