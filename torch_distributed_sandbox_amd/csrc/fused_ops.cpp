@@ -278,6 +278,7 @@ uint32_t* opt_mag(const c10::optional<Tensor>& mag, int64_t numel = 33) {
 std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tensor>& mag,
                                       const c10::optional<Tensor>& p1_scale) {
   need(w2, at::kFloat, {32, 16, 5, 5}, "conv2.weight");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w2.data_ptr()) % 16 == 0, "conv2_pack: conv2.weight must be 16-B aligned");
   const float* ps = optf(p1_scale, 1, "p1_scale");
   c10::DeviceGuard guard(w2.device());
   auto wp = at::empty({2 * 13 * 2 * 4 * 16 * 8}, w2.options().dtype(at::kShort));

@@ -39,7 +39,9 @@ constexpr int F2_THREADS = 256;
 constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records (1 KiB)
 constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records of 32 B, 240 used)
 constexpr int F2_PBUF = F2_PPLANE;                     // one fp16 plane
-constexpr int F2_STAGE = F2_TH * F2_TC * 32 * 4;        // finished tile: 8 x 16 px x 32 co fp32 = 16 KiB
+constexpr int F2_PXREC = 32 * 4 + 16;                 // staged pixel record: 32 co fp32 + 16 B pad (banks)
+constexpr int F2_STAGE_DATA = F2_TH * F2_TC * 32 * 4;   // finished tile: 8 x 16 px x 32 co fp32 = 16 KiB
+constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;       // its padded staging buffer (18 KiB)
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
 constexpr int F2_YSTAGE = 32 * 32 * 4;                 // pooled block: 32 co x 4 x 8 fp32 = 4 KiB
 constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
@@ -127,13 +129,15 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
   }
 }
 
-// A finished tile goes to LDS first ([row][px][32 co], 16-B chunks XOR-swizzled by px & 7 so
-// the MFMA-layout writes are conflict-free), then the workgroup stores it as full 128-B
-// pixel records, 1 KiB contiguous per wave-instruction.  (Stored straight from the MFMA
-// layout, each wave wrote 64-B halves of lines whose other half came from another wave:
-// the y2 writes then cost ~0.3 ms more, TDS_CONV2_DIAG=4.)
+// A finished tile goes to LDS first ([row][px][32 co] with 144-B pixel records: the 16-B pad
+// puts the 4 lane groups' pixels 4g + r on disjoint bank quarters, so the MFMA-layout writes
+// are conflict-free AND every lane's 16 writes are one base register plus immediate offsets --
+// the XOR swizzle it replaces cost 2-3 VALU per element), then the workgroup stores it as full
+// 128-B pixel records, 1 KiB contiguous per wave-instruction.  (Stored straight from the MFMA
+// layout, each wave wrote 64-B halves of lines whose other half came from another wave: the y2
+// writes then cost ~0.3 ms more, TDS_CONV2_DIAG=4.)
 __device__ __forceinline__ int f2_stage_off(int row, int px, int chunk) {
-  return ((row * F2_TC + px) * 8 + (chunk ^ (px & 7))) * 16;
+  return (row * F2_TC + px) * F2_PXREC + chunk * 16;
 }
 
 // pooled block staging: channel co's 32 floats [prow 4][pcol 8], float4 chunks XOR-swizzled by co
@@ -147,29 +151,42 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
   return neg ? mn : mx;
 }
 
-// stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li]
+// stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li].
+// EDGE: a tile reaching past the image (last tile row / column) masks its statistics; interior
+// tiles (all but ~1 %) accumulate unmasked and take max |y2| with the NaN-propagating
+// v_maximum_f32 (|y| as a source modifier): 4 VALU per output instead of ~8 (the kernel's VALU
+// issue competes with the MFMAs of the same SIMD).
+template <bool EDGE>
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
                                          int RH, int NT, int lane, float bco, float inv, bool neg, float& s_acc,
                                          float& q_acc, uint32_t& ymx) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
+  float ymf = 0.f;
 #pragma unroll
   for (int o = 0; o < 4; ++o) {
     const int row = 4 * RH + o;
-    const bool rok = x.r0 + row < P;
+    const bool rok = !EDGE || x.r0 + row < P;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int px = 4 * g + r;
       const float v = acc[o][r];  // (y2 - b2) / inv: statistics shifted by the bias, scaled at the end
       const float y = fmaf(v, inv, bco);
-      if (rok && x.c0 + px < P) {
+      if constexpr (EDGE) {
+        if (rok && x.c0 + px < P) {
+          s_acc += v;
+          q_acc += v * v;
+          ymx = max(ymx, __float_as_uint(y) & 0x7fffffffu);  // |y2| bits (NaN: above every finite)
+        }
+      } else {
         s_acc += v;
-        q_acc += v * v;
-        ymx = max(ymx, __float_as_uint(y) & 0x7fffffffu);  // |y2| bits (NaN: above every finite)
+        q_acc = fmaf(v, v, q_acc);
+        ymf = __builtin_elementwise_maximum(ymf, fabsf(y));  // NaN wins (as the bits' unsigned max)
       }
       *reinterpret_cast<float*>(stage + f2_stage_off(row, px, co >> 2) + (co & 3) * 4) = y;
     }
   }
+  if constexpr (!EDGE) ymx = max(ymx, __float_as_uint(ymf));
   // pooled windows (rows 4RH + 2i + {0,1}, columns 4g + 2j + {0,1}) -> ya block entry
   // (prow 2RH + i, pcol 2g + j); v -> v * inv + b2 is monotone (inv > 0) and rounds monotonically,
   // so ext(v) * inv + b2 == ext(v * inv + b2)
@@ -203,7 +220,7 @@ __device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, flo
   if constexpr (DIAG == 4) return;  // timing-only: no y2
   const int e = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < F2_STAGE / 16 / F2_THREADS; ++i) {
+  for (int i = 0; i < F2_STAGE_DATA / 16 / F2_THREADS; ++i) {
     const int q = e + F2_THREADS * i;
     const int row = q >> 7, px = (q >> 3) & 15, chunk = q & 7;
     const int gr = x.r0 + row, gc = x.c0 + px;
@@ -265,8 +282,12 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
       f2_store_ya(ys + ((kk + 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
     }
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
-    f2_stage(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane, bco,
-             inv, neg, s_acc, q_acc, ymx);
+    if (cur.r0 + F2_TH <= P && cur.c0 + F2_TC <= P)  // tile-uniform
+      f2_stage<false>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
+                      bco, inv, neg, s_acc, q_acc, ymx);
+    else
+      f2_stage<true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
+                     bco, inv, neg, s_acc, q_acc, ymx);
     prev = cur;
     have_prev = true;
   }
