@@ -28,8 +28,8 @@ namespace tds {
 // fp16 range of the exactly carried weights: hi + lo represents w to ~2^-22 relative only while
 // lo stays a normal fp16 (|w| >= ~2^-3); below fp16's normal range (|w| < 2^-14) even the
 // per-product bound 2^-11 of fp16x2 breaks.  With mag given, the packed weights are w * 2^ew with
-// max |w| * 2^ew in [2^14, 2^15) (one 1024-thread workgroup: max |w| over the 12 800 weights by
-// float4 loads, then the packing), and mag[kMagScales] = 2^-ew, mag[kMagScales + 1] = 1 / p1_scale (the layer-1
+// max |w| * 2^ew in [2^14, 2^15) (every block finds max |w| itself over the 12 800 weights, by
+// float4 loads from L2: no inter-block step), and mag[kMagScales] = 2^-ew, mag[kMagScales + 1] = 1 / p1_scale (the layer-1
 // range guard, convnet_fused.hip l1_gram; 1 when not given) are what the conv2 forward and
 // backward epilogues multiply their accumulators by (powers of two: exact).  Without mag the
 // weights are packed unscaled.
@@ -43,10 +43,15 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
   if (mag != nullptr) {
     float m = 0.f;
     const float4* w4 = reinterpret_cast<const float4*>(w2);  // (a contiguous fp32 tensor: 16-B aligned)
-    for (int e = threadIdx.x; e < 32 * 16 * 25 / 4; e += blockDim.x) {  // NaN: ignored
-      const float4 v = w4[e];
-      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    float4 v[13];  // all loads in flight first (3200 float4 over 256 threads)
+#pragma unroll
+    for (int k = 0; k < 13; ++k) {
+      const int e = threadIdx.x + k * 256;
+      v[k] = e < 32 * 16 * 25 / 4 ? w4[e] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+#pragma unroll
+    for (int k = 0; k < 13; ++k)  // NaN: ignored
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[k].x), fabsf(v[k].y)), fmaxf(fabsf(v[k].z), fabsf(v[k].w))));
     m = wave_max(m);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
@@ -129,7 +134,7 @@ using namespace tds;
 
 void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, const float* p1_scale,
                             hipStream_t st) {
-  hipLaunchKernelGGL(conv2_pack_weights_kernel, dim3(1), dim3(1024), 0, st, w2, wp, wd, mag, p1_scale);
+  hipLaunchKernelGGL(conv2_pack_weights_kernel, dim3(64), dim3(256), 0, st, w2, wp, wd, mag, p1_scale);
   TDS_LAUNCH_CHECK();
 }
 
