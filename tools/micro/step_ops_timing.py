@@ -92,7 +92,7 @@ def main():
             st["c2b"] = ops.fused_conv2_backward_y2(y2, g2m, st["hf"][2], kbuf, st["mag"], st["l1"][0], st["pack"][1], 1.0)
 
         def l1b():
-            p1, idx1, stats1, gram = st["l1"]
+            p1, idx1, stats1, gram = st["l1"][:4]
             ops.fused_l1_backward(st["c2b"][0], x, p1, idx1, c1.weight, c1.bias, n1.weight, stats1, gram, 1.0)
 
         seq = [("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
