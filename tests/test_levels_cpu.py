@@ -34,7 +34,8 @@ def test_convnet_levels_input_equals_image_input():
 
 def test_layer1_backward_level_lds_layout():
     """The level layer-1 backward's LDS image (tools/micro/l1b_lds_check.py): every B-operand read
-    returns its packed pair and no lane half hits two addresses in one bank."""
+    returns its packed pair and no lane half hits two addresses in one bank; the default word layout
+    (stride 137, ones block) likewise returns every tap word / the sum-dz 1.0 conflict-free."""
     import importlib.util
     import os
 
@@ -43,3 +44,4 @@ def test_layer1_backward_level_lds_layout():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.main()
+    assert mod.word_layout()

@@ -402,6 +402,12 @@ constexpr int LB_PER = (LB_V + 255) / 256;
 // on every dp1 read.  Swapping the records of pp = 2, 3 (mod 4) puts the pair in opposite halves.
 template <bool SW>
 __device__ __forceinline__ int lb_dp_rec(int pp) { return SW ? pp ^ ((pp >> 1) & 1) : pp; }
+__device__ __forceinline__ void lb_store4(uint32_t* p, const uint4& v) {
+  p[0] = v.x;
+  p[1] = v.y;
+  p[2] = v.z;
+  p[3] = v.w;
+}
 
 // ============================================================================ layer-1 backward (MFMA)
 // The sums the sparse kernel above forms with 25 VALU FMAs per active (pooled pixel,
@@ -415,15 +421,25 @@ __device__ __forceinline__ int lb_dp_rec(int pp) { return SW ? pp ^ ((pp >> 1) &
 // dp1 / argmax tile and the x tile (packed bf16 hi|lo words, as l1_conv_bf3 stages it)
 // go through LDS; fp32 MFMA accumulation per tile (256 pixels), fp64 across tiles.
 // partial[wg][16][27] in the sparse kernel's layout ([0] sum dz, [1] 0, [2+j] taps).
-constexpr int LM_XS = 80;  // x tile row stride (words): 20 rows x (72 staged + pad) columns
+// x tile row stride (words): 20 rows x (72 staged columns + 65 columns of bf16 1.0).  137 = 9 mod 32:
+// a K-step's B read (one ds_read_b32 lane half = taps of 3-4 rows x 9 columns) then hits distinct banks
+// (80 put rows ky and ky + 2 on the same banks: 2-way on every read).  The sum-dz lanes (n = 25) read
+// the ones block at LM_ONES past the K-step base, a bank no data lane of that read touches; the pad
+// lanes (n = 26..31, outputs discarded) read tap 24's address (a broadcast).  tools/micro/
+// l1b_lds_check.py emulates both layouts' reads.  (The dp1 record swap lb_dp_rec stays PAIRS-only:
+// in the word layout it raises the kernel from 124 to 148 VGPRs, 3 workgroups per CU instead of 4,
+// for ~10 % of the LDS cycles.)
+constexpr int LM_XS = 137;
+constexpr int LM_ONES = LM_XS + 80;
+static_assert(LM_XS % 32 == 9 && 80 + 3 * 16 + 3 < LM_XS && 1 + 2 * 7 + 1 < LB_XR, "l1_bwd ones block");
 // Level input (LV): the x tile as bf16 PAIRS, so one ds_read_b32 is one packed B-operand register
 // (slots dc = 0, 1 of a window row) with no perm.  Copy E holds columns (2k, 2k+1) in dword k, copy
 // O columns (2k+1, 2k+2): a lane's pair starts at column kx + 2 + 4g (+ uniform offsets), even for
 // even kx (E) and odd for odd kx (O).  Row stride LV_RS = 41 = 9 mod 32 dwords and O based 5 banks
 // after E: a K-step's 32 lanes of one half (g0, g1) then touch rows ky of E at banks 9ky + 1..5 and
 // of O at 9ky + 6..9 -- 29 distinct banks for block 0 (rows 0..2 + row 3 col 0) and 18 for block
-// 1, no conflicts (the fp32-image layout above is 2-way conflicted on every B read: rows 80 words
-// apart map to the same banks).
+// 1, no conflicts (the word layout above is conflict-free too since round 4, with twice the reads and
+// a perm per packed register).
 constexpr int LV_RS = 41;
 constexpr int LV_OB = 837;  // = 5 mod 32, >= 20 rows x 41
 constexpr int LV_WORDS = LV_OB + LB_XR * LV_RS;
@@ -460,19 +476,15 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   // lane group g holds windows 2g, 2g+1 whole -- dz1 of a window is one pooled value placed
   // at its argmax slot (a 64-bit shift), no per-pixel selects.
   // B-operand geometry: x tile word offset (tile origin row r0 - 2, column c0 - 4) of this
-  // lane's tap relative to the K-step base 2*rp*XS + 16*s; slot j adds koffB(j).  Taps >= 25
-  // read a constant block kept in the tile's padding columns 72..75 (rows 0-1: bf16 1.0 for
-  // the sum-dz column n = 25; rows 2-3: zeros).
+  // lane's tap relative to the K-step base 2*rp*XS + 16*s; slot j adds (row dr2, column 2wi + dc).
+  // n = 25 reads the ones block (bf16 1.0: the sum-dz column), n = 26..31 tap 24 (discarded).
   int boff[2];
   bool bdata[2];
-  int bcst[2];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
-    const int n = 16 * blk + li;
+    const int n = 16 * blk + li, t = n < 25 ? n : 24;
     bdata[blk] = n < 25;
-    const int ky = n < 25 ? n / 5 : 0, kx = n < 25 ? n % 5 : 0;
-    boff[blk] = ky * LM_XS + kx + 2 + 4 * g;
-    bcst[blk] = (n == 25 ? 0 : 2 * LM_XS) + 72;
+    boff[blk] = n == 25 ? LM_ONES : (t / 5) * LM_XS + t % 5 + 2 + 4 * g;
   }
   // LV: this lane's dword offset in the pair tiles (tap (4,4) for the constant columns: the read is
   // a broadcast of that lane's address, the value is then replaced by the constant)
@@ -485,10 +497,9 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
     vlof[blk] = (kx & 1) ? LV_OB + ky * LV_RS + (kx + 1 + 4 * g) / 2 : ky * LV_RS + (kx + 2 + 4 * g) / 2;
     vcst[blk] = n == 25 ? 0x3F803F80u : 0u;  // bf16 1.0 pair: the sum-dz column
   }
-  if (!(LV && PAIRS) && tid < 16) {  // constant blocks (never overwritten: the x tile uses columns 0..71)
-    const int r = tid >> 2, c = tid & 3;
-    xs[r * LM_XS + 72 + c] = r < 2 ? 0x3F800000u : 0u;
-  }
+  if (!(LV && PAIRS))  // the ones block (never overwritten: the x tile uses columns 0..71)
+    for (int e = tid; e < LB_XR * (LM_XS - 72); e += 256)
+      xs[(e / (LM_XS - 72)) * LM_XS + 72 + e % (LM_XS - 72)] = 0x3F800000u;  // bf16 1.0 | lo 0
   const float* __restrict__ x = static_cast<const float*>(xv);
   const uint8_t* __restrict__ xl = static_cast<const uint8_t*>(xv);
   uint4 pre[LB_PER];
@@ -542,7 +553,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
           v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
           v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
           v.w = __float_as_uint((float)(q >> 24));
-          *reinterpret_cast<uint4*>(xs + rr * LM_XS + 4 * cv) = v;
+          lb_store4(xs + rr * LM_XS + 4 * cv, v);  // odd row stride: dword stores
           continue;
         }
         if constexpr (LV) {  // bf16 of a level = high half of its fp32 bits (exact)
@@ -567,7 +578,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
         v.y = __builtin_amdgcn_perm(h01, l01, 0x07060302u);
         v.z = __builtin_amdgcn_perm(h23, l23, 0x05040100u);
         v.w = __builtin_amdgcn_perm(h23, l23, 0x07060302u);
-        *reinterpret_cast<uint4*>(xs + rr * LM_XS + 4 * cv) = v;
+        lb_store4(xs + rr * LM_XS + 4 * cv, v);  // odd row stride: dword stores
       }
     }
   };
@@ -630,7 +641,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
         const int base = 2 * rp * LM_XS + 16 * sg;
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
-          const int bo = bdata[blk] ? base + boff[blk] : bcst[blk];
+          const int bo = base + boff[blk];
           uint32_t u[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
