@@ -89,7 +89,8 @@ def main():
         def c2b():
             y2 = st["c2"][0]
             g2m, kbuf = st["hb"][4], st["hb"][5]
-            st["c2b"] = ops.fused_conv2_backward_y2(y2, g2m, st["hf"][2], kbuf, st["mag"], st["l1"][0], st["pack"][1], 1.0)
+            st["c2b"] = ops.fused_conv2_backward_y2(y2, g2m, st["hf"][2], kbuf, c2.bias, st["mag"], st["l1"][0],
+                                                        st["pack"][1], 1.0)
 
         def l1b():
             p1, idx1, stats1, gram = st["l1"][:4]

@@ -289,8 +289,9 @@ std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tens
   return {wp, wd};
 }
 
-// returns (y2 [B,P,P,32], BN2 partials, ya [B,32,PB]: y2 at each 2x2 window's argmax of the BN2
-// output, resolved by the sign of gamma2)
+// returns (y2h [B,P,P,32] fp16: the conv2 output bias-free at the y2h scale mag[kMagScales + 2]
+// (1 without mag; kernels/conv2_common.h), BN2 partials, ya [B,32,PB]: y2 at each 2x2 window's
+// argmax of the BN2 output, resolved by the sign of gamma2)
 std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& wp, const Tensor& b2,
                                                        const c10::optional<Tensor>& gamma2,
                                                        const c10::optional<Tensor>& mag) {
@@ -307,10 +308,10 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const T
   tds_conv2_fwd2_tiles((int)P, &tr, &tc);
   int sw = 0, sk = 0;
   const int* order = tile_order(p1, (int)B, tr, tc, nwg, &sw, &sk);
-  auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kFloat));
+  auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kHalf));  // y2h (kernels/conv2_common.h)
   auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
-  tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr<float>(),
+  tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr(),
                  ya.data_ptr<float>(), partial.data_ptr<double>(),
                  opt_mag(mag, kMagParts + 32 * mag_ypart_count()) ? opt_mag(mag) + kMagParts : nullptr,
                  opt_mag(mag) ? opt_mag(mag) + kMagScales : nullptr, order, nwg, sw, sk, (int)B, (int)P, stream_of(p1));
@@ -486,14 +487,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
 // ---------------------------------------------------------------- conv2 backward
 // BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2, g2m, aff2, kbuf, p1) -> (dp1, dw2, db2)
 std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& g2m, const Tensor& aff2,
-                                                           const Tensor& kbuf, const Tensor& mag, const Tensor& p1,
+                                                           const Tensor& kbuf, const Tensor& b2, const Tensor& mag,
+                                                           const Tensor& p1,
                                                            const Tensor& wd, double scale,
                                                            const c10::optional<Tensor>& dw_out,
                                                            const c10::optional<Tensor>& db_out) {
   const int64_t B = p1.size(0), P = p1.size(1);
   need(p1, at::kHalf, {B, P, P, 16}, "p1");
-  opt_mag(mag);  // [0,33): the magnitude bounds of the forward and the head backward
-  need(y2, at::kFloat, {B, P, P, 32}, "y2");
+  opt_mag(mag, kMagScales + 3);  // the magnitude bounds of the forward / head backward, the y2h decode
+  need(y2, at::kHalf, {B, P, P, 32}, "y2h (fused_conv2_forward's)");
+  need(b2, at::kFloat, {32}, "conv2.bias");
   need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
@@ -510,8 +513,9 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options().dtype(at::kFloat));
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
-  tds_conv2_bwd3(y2.data_ptr<float>(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
-                 reinterpret_cast<const uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(), wd.data_ptr<int16_t>(),
+  tds_conv2_bwd3(y2.data_ptr(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
+                 b2.data_ptr<float>(), reinterpret_cast<const uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(),
+                 wd.data_ptr<int16_t>(),
                  dp1.data_ptr<float>(), slab.data_ptr<float>(), order, nwg, sw, sk, (int)B, (int)P, st);
   tds_conv2_wgrad_reduce(slab.data_ptr<float>(), nwg, dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, st);
   check_launches("fused_conv2_backward_y2");
@@ -778,7 +782,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);
   m.def("conv2_bwd_walk_table(int B, int tiles_r, int tiles_c, int nwg, int seg) -> Tensor", &conv2_bwd_walk_table);
   m.def(
-      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor mag, Tensor p1, Tensor wd, "
+      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor b2, Tensor mag, Tensor p1, "
+      "Tensor wd, "
       "float scale, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
       &fused_conv2_backward_y2);
   m.def(

@@ -99,7 +99,7 @@ __device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k,
 }
 
 struct BRArgs {
-  const float4* __restrict__ y2;
+  const uint2* __restrict__ y2;  // y2h [B][P][P][32] fp16 (conv2_common.h)
   const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
   const uint4* __restrict__ p1;
   float* __restrict__ dp1;
@@ -403,7 +403,8 @@ struct BRStager {
   static constexpr int IPER = (ITEMS + 255) / 256;
   static constexpr int PIECES = NR * BR_SC * 2;  // 16-B p1 pieces (32-B fp16 records)
   static constexpr int PPER = (PIECES + 255) / 256;
-  float4 yv[IPER][4], gv[IPER];
+  uint2 yv[IPER][4];  // y2h: 4 channels of one pixel
+  float4 gv[IPER];
   uint4 pr[PPER];
 
   __device__ __forceinline__ static void item_geom(int it, int& wy, int& wx) {
@@ -423,7 +424,7 @@ struct BRStager {
       for (int u = 0; u < IPER; ++u) {
         gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) yv[u][q] = gv[u];
+        for (int q = 0; q < 4; ++q) yv[u][q] = make_uint2(0u, 0u);
       }
 #pragma unroll
       for (int j = 0; j < PPER; ++j) pr[j] = make_uint4(0u, 0u, 0u, 0u);
@@ -434,7 +435,7 @@ struct BRStager {
     const int64_t img = (int64_t)b * P;
     // y2 / p1: one descriptor per block, based at (R0, c0-2); lanes outside the image -> kBROob
     const __amdgpu_buffer_rsrc_t ry =
-        tds_buffer_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + R0) * P + (c0 - 2)) * 128, 0xFFFFFFF0u);
+        tds_buffer_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + R0) * P + (c0 - 2)) * 64, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t rp =
         tds_buffer_rsrc(reinterpret_cast<const char*>(a.p1) + ((img + R0) * P + (c0 - 2)) * 32, 0xFFFFFFF0u);
     const int64_t gplane = (int64_t)Q * Q;
@@ -453,9 +454,9 @@ struct BRStager {
         const int lr = 2 * wy + (q >> 1), lc = 2 * wx + (q & 1);
         const int gr = R0 + lr, gc = c0 - 2 + lc;
         const bool ok = item && (in || (gr >= 0 && gr < P && gc >= 0 && gc < P));
-        const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 128 + c4 * 16) : kBROob;
-        yv[u][q] = DIAG == 7 ? make_float4(1.f, 0.f, 0.f, 0.f)
-                             : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(ry, off, 0, 0));
+        const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 64 + c4 * 8) : kBROob;
+        yv[u][q] = DIAG == 7 ? make_uint2(0x3C00u, 0u)
+                             : __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, 0));
       }
       const int py = py0 + wy, px = px0 + wx;
       const bool pooled = item && (in || (py >= 0 && py < Q && px >= 0 && px < Q));
@@ -506,13 +507,13 @@ struct BRStager {
     const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, k2[4] = {k24.x, k24.y, k24.z, k24.w},
                 k3[4] = {k34.x, k34.y, k34.z, k34.w};
     bool fast = interior(a, R0, c0);
-    if (fast) {
-      float nsum = 0.f;
+    if (fast) {  // a NaN among the fp16 values: exponent all ones, mantissa non-zero
+      uint32_t nan = 0u;
 #pragma unroll
       for (int u = 0; u < IPER; ++u)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) nsum += (yv[u][q].x + yv[u][q].y) + (yv[u][q].z + yv[u][q].w);
-      fast = __builtin_amdgcn_ballot_w64(isnan(nsum)) == 0;  // wave-uniform
+        for (int q = 0; q < 4; ++q) nan |= f16x2_nan(yv[u][q].x) | f16x2_nan(yv[u][q].y);
+      fast = __builtin_amdgcn_ballot_w64(nan != 0u) == 0;  // wave-uniform
     }
 #pragma unroll
     for (int u = 0; u < IPER; ++u) {
@@ -520,10 +521,13 @@ struct BRStager {
       if (it >= ITEMS) continue;
       int wy, wx;
       item_geom(it, wy, wx);
-      float y[4][4];
+      float y[4][4];  // the stored values (ka, kb, k2, k3 carry the decode: kernel header)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        y[q][0] = yv[u][q].x; y[q][1] = yv[u][q].y; y[q][2] = yv[u][q].z; y[q][3] = yv[u][q].w;
+        y[q][0] = f16_val(yv[u][q].x);
+        y[q][1] = f16_val(yv[u][q].x >> 16);
+        y[q][2] = f16_val(yv[u][q].y);
+        y[q][3] = f16_val(yv[u][q].y >> 16);
       }
       const float gg[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
       float d[4][4];
@@ -690,8 +694,9 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
 
 template <int DIAG, bool BIG>
 __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
-    const float4* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
-    const float* __restrict__ kbuf, const uint32_t* __restrict__ mag, const uint4* __restrict__ p1,
+    const uint2* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
+    const float* __restrict__ kbuf, const float* __restrict__ b2, const uint32_t* __restrict__ mag,
+    const uint4* __restrict__ p1,
     const uint4* __restrict__ wdpack, float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ walk,
     int sw, int sk, int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -719,11 +724,17 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
       e = min(60, max(-60, 15 - x));
     }
     const float sc = ldexpf(1.f, e);
-    kc[tid] = aff2[tid];
+    // the staging reads y2h (conv2_common.h): y2 = h * d + b2, d = inv / 2^k (powers of two), so
+    // a*y2 + b = (a d) h + (a b2 + b) and k2*y2 + k3 = (k2 d) h + (k2 b2 + k3)
+    const float d = __uint_as_float(mag[kMagScales]) * __uint_as_float(mag[kMagScales + 1]) /
+                    __uint_as_float(mag[kMagScales + 2]);
     if (tid < 32) {
+      const float ka = aff2[c], kb = aff2[32 + c], bc = b2[c];
+      kc[c] = ka * d;
+      kc[32 + c] = fmaf(ka, bc, kb);
       kc[64 + c] = k1 * sc;
-      kc[96 + c] = k2 * sc;
-      kc[128 + c] = k3 * sc;
+      kc[96 + c] = k2 * d * sc;
+      kc[128 + c] = fmaf(k2, bc, k3) * sc;
     }
     if (tid == 0) {
       const float ie = ldexpf(1.f, -e);
@@ -845,9 +856,9 @@ static int br_diag_env() { return 0; }
 
 // g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
 // [nwg][rows] (fused_ops.cpp bwd_walk)
-void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const uint32_t* mag,
-                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int sw, int sk,
-                    int B, int P, hipStream_t st) {
+void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
+                    const uint32_t* mag, const void* p1, const short* wd, float* dp1, float* slab, const int* walk,
+                    int nwg, int sw, int sk, int B, int P, hipStream_t st) {
   const int Q = P / 2;
   const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
 #define TDS_BR_LAUNCH_B(D, BG)                                                                                         \
@@ -859,7 +870,8 @@ void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const 
       set = true;                                                                                                      \
     }                                                                                                                  \
     hipLaunchKernelGGL((conv2_bwd_roll_kernel<D, BG>), dim3(nwg), dim3(BR_THREADS), BR_LDS, st,                        \
-                       reinterpret_cast<const float4*>(y2), g2m, aff2, kbuf, mag, reinterpret_cast<const uint4*>(p1),  \
+                       reinterpret_cast<const uint2*>(y2h), g2m, aff2, kbuf, b2, mag,                                    \
+                       reinterpret_cast<const uint4*>(p1),                                                            \
                        reinterpret_cast<const uint4*>(wd), dp1, slab, walk, sw, sk, B, P);                                      \
     TDS_LAUNCH_CHECK();                                                                                                \
   }

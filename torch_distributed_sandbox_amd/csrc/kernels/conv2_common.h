@@ -9,7 +9,29 @@ namespace tds {
 
 // Words of the step's magnitude workspace ("mag", fused_ops.cpp) past the 33 bounds: written by
 // conv2_pack_weights_kernel, read by the conv2 forward / backward epilogues (powers of two).
-constexpr int kMagScales = 40;  // mag[40] = 2^-ew (packed weights' scale), mag[41] = 1 / p1 scale
+constexpr int kMagScales = 40;  // mag[40] = 2^-ew (packed weights' scale), mag[41] = 1 / p1 scale,
+                                // mag[42] = 2^k, the y2h store factor (conv2_fwd2.hip)
+
+// ---------------------------------------------------------------------------- y2h
+// The conv2 output travels from the forward to the backward as y2h [B][P][P][32] fp16 (64 B per
+// pixel, half of fp32): y2h = fp16(acc * 2^k), acc the bias-free MFMA accumulator (y2 = acc * inv
+// + b2), 2^k from conv2_pack: max_c sum |w_c| * 2^ew * 1.01 * 2^k <= 1, so with |p1 operand| <=
+// 65504 no value can overflow, and everything above 2^-14 of the fp16 grid keeps 11 significant
+// bits (TF32's).  Rounding is to nearest, except that each 2x2 pooling window's first extreme
+// (max for gamma2 >= 0, min for gamma2 < 0: the forward's argmax) is moved one fp16 step outward
+// when rounding made an earlier-scanned pixel of its window equal to it -- so the backward's
+// first-extreme scan over the stored values picks the forward's pixel (conv2_fwd2.hip
+// f2_keep_first).
+__device__ __forceinline__ uint32_t f16_bits(float x) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)x);
+}
+__device__ __forceinline__ float f16_val(uint32_t h) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(h & 0xFFFFu));
+}
+// non-zero when either fp16 of the pair is a NaN
+__device__ __forceinline__ uint32_t f16x2_nan(uint32_t x) {
+  return (uint32_t)((x & 0x7FFFu) > 0x7C00u) | (uint32_t)(((x >> 16) & 0x7FFFu) > 0x7C00u);
+}
 
 // ---------------------------------------------------------------------------- diagnostics
 // DIAG = 0: the real kernel.  Timing-only builds (tools/conv2_diag.py, TDS_CONV2_DIAG):

@@ -1,5 +1,6 @@
 // conv2 forward v2 (Conv2d(16, 32, 5, pad 2), mnist_onegpu.py:20):
-// y2 = conv(p1) + b2 in NHWC fp32, plus BN2 batch-statistic partials, on
+// y2 = conv(p1) + b2, stored as y2h (NHWC fp16, bias-free, scaled: conv2_common.h), plus BN2
+// batch-statistic partials, on
 // v_mfma_f32_16x16x32_f16 with the fp16x2 split (bf16x3.h: p1 is the single-rounded fp16
 // operand, the weights are carried exactly as fp16 hi + lo; 2 MFMAs per product), laid out for
 // SEVERAL small workgroups per CU (the design of conv2_bwd2.hip):
@@ -9,7 +10,7 @@
 //     all 13 K-steps of its half (13 x (hi, lo) fragments = 104 VGPRs), loaded once;
 //   * p1 staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs, no VALU), double-buffered:
 //     tile t+1 streams in while tile t is on the MFMAs;
-//   * the epilogue of tile t (y2 stores + statistics) runs after tile t+1's DMA is issued,
+//   * the epilogue of tile t (y2h stores + statistics) runs after tile t+1's DMA is issued,
 //     from a second accumulator set, so the stores drain under the next MFMAs;
 //   * the epilogue also resolves the 2x2 max-pool of the BN2 output: BN2's affine a*y + b is
 //     monotone per channel with the sign of gamma (a = gamma * invstd), so the window's
@@ -39,9 +40,8 @@ constexpr int F2_THREADS = 256;
 constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records (1 KiB)
 constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records of 32 B, 240 used)
 constexpr int F2_PBUF = F2_PPLANE;                     // one fp16 plane
-constexpr int F2_PXREC = 32 * 4 + 16;                 // staged pixel record: 32 co fp32 + 16 B pad (banks)
-constexpr int F2_STAGE_DATA = F2_TH * F2_TC * 32 * 4;   // finished tile: 8 x 16 px x 32 co fp32 = 16 KiB
-constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;       // its padded staging buffer (18 KiB)
+constexpr int F2_PXREC = 32 * 4 + 16;                 // staged pixel record: 32 co dwords (y2h bits) + 16 B pad (banks)
+constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;       // a finished tile's padded staging buffer (18 KiB)
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
 constexpr int F2_YSTAGE = 32 * 32 * 4;                 // pooled block: 32 co x 4 x 8 fp32 = 4 KiB
 constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
@@ -151,6 +151,27 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
   return neg ? mn : mx;
 }
 
+// y2h rounding of one pooling window (conv2_common.h): h0..h3 = fp16(v * 2^k) to nearest in scan
+// order, m = the window's extreme (f2_ext4).  The forward's argmax a is the first q with v_q == m;
+// to nearest, an earlier pixel can round to the same fp16 as a (a near-tie): then a moves one
+// step outward, strictly past it.  Rare and divergent: the branch costs ~nothing when no lane
+// ties.  (A NaN window takes the backward's NaN path, whatever is stored.)
+__device__ __forceinline__ void f2_keep_first(uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3, float v0,
+                                              float v1, float v2, float m, bool neg) {
+  const bool e0 = v0 == m, e1 = v1 == m, e2 = v2 == m;
+  const uint32_t ha = e0 ? h0 : e1 ? h1 : e2 ? h2 : h3;
+  const float ra = f16_val(ha);
+  const bool tie = !e0 && (f16_val(h0) == ra || (!e1 && (f16_val(h1) == ra || (!e2 && f16_val(h2) == ra))));
+  if (tie) {
+    // outward = up (max window) / down (min window): +1 on the bits when the sign bit differs
+    // from the direction's, -1 otherwise (ha is finite: |v * 2^k| < 65504 by construction)
+    const uint32_t out = ((ha >> 15) & 1u) ^ (neg ? 0u : 1u) ? ha + 1u : ha - 1u;
+    if (e1) h1 = out;
+    else if (e2) h2 = out;
+    else h3 = out;
+  }
+}
+
 // stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li].
 // EDGE: a tile reaching past the image (last tile row / column) masks its statistics; interior
 // tiles (all but ~1 %) accumulate unmasked and take max |y2| with the NaN-propagating
@@ -158,11 +179,16 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
 // issue competes with the MFMAs of the same SIMD).
 template <bool EDGE>
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
-                                         int RH, int NT, int lane, float bco, float inv, bool neg, float& s_acc,
-                                         float& q_acc, uint32_t& ymx) {
+                                         int RH, int NT, int lane, float bco, float inv, float ksc, bool neg,
+                                         float& s_acc, float& q_acc, uint32_t& ymx) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
   float ymf = 0.f;
+  uint32_t h[4][4];  // y2h bits (conv2_common.h)
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) h[o][r] = f16_bits(acc[o][r] * ksc);
 #pragma unroll
   for (int o = 0; o < 4; ++o) {
     const int row = 4 * RH + o;
@@ -183,7 +209,6 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
         q_acc = fmaf(v, v, q_acc);
         ymf = __builtin_elementwise_maximum(ymf, fabsf(y));  // NaN wins (as the bits' unsigned max)
       }
-      *reinterpret_cast<float*>(stage + f2_stage_off(row, px, co >> 2) + (co & 3) * 4) = y;
     }
   }
   if constexpr (!EDGE) ymx = max(ymx, __float_as_uint(ymf));
@@ -194,13 +219,22 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
   for (int i = 0; i < 2; ++i) {
     float e[2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      e[j] = fmaf(f2_ext4(acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], acc[2 * i + 1][2 * j + 1],
-                          neg),
-                  inv, bco);
+    for (int j = 0; j < 2; ++j) {
+      const float m = f2_ext4(acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], acc[2 * i + 1][2 * j + 1],
+                              neg);
+      e[j] = fmaf(m, inv, bco);
+      f2_keep_first(h[2 * i][2 * j], h[2 * i][2 * j + 1], h[2 * i + 1][2 * j], h[2 * i + 1][2 * j + 1],
+                    acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], m, neg);
+    }
     // pcols 2g, 2g+1 are adjacent floats of one swizzled chunk: one ds_write_b64
     *reinterpret_cast<float2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_float2(e[0], e[1]);
   }
+  // the y2h bits, one dword per value (f2_store packs channel pairs)
+#pragma unroll
+  for (int o = 0; o < 4; ++o)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<uint32_t*>(stage + f2_stage_off(4 * RH + o, 4 * g + r, co >> 2) + (co & 3) * 4) = h[o][r];
 }
 
 // the workgroup stores the staged pooled block: thread e -> channel e / 8, float4 e % 8
@@ -213,27 +247,37 @@ __device__ __forceinline__ void f2_store_ya(const float* ystage, const F2Tile& x
   st_stream(reinterpret_cast<float4*>(ya + ((((int64_t)x.b * 32 + co) * pg.Q4 + tr) * pg.Q8 + tc) * 32 + part * 4), v);
 }
 
-// the whole workgroup stores a staged tile: thread e, i -> float4 q = e + 256 i of
-// [row 8][px 16][chunk 8]: a wave-instruction writes 1 KiB of one y2 row
+// the whole workgroup stores a staged tile as y2h: thread e, i -> 8 channels q = e + 256 i of
+// [row 8][px 16][c8 4] (two staged 4-channel chunks packed to 16 B): a wave-instruction writes
+// 1 KiB, 16 pixels of one row
 template <int DIAG>
-__device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, float* __restrict__ y2, int P) {
-  if constexpr (DIAG == 4) return;  // timing-only: no y2
+__device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, unsigned short* __restrict__ y2h, int P) {
+  if constexpr (DIAG == 4) return;  // timing-only: no y2h
   const int e = threadIdx.x;
 #pragma unroll
-  for (int i = 0; i < F2_STAGE_DATA / 16 / F2_THREADS; ++i) {
+  for (int i = 0; i < F2_TH * F2_TC * 4 / F2_THREADS; ++i) {
     const int q = e + F2_THREADS * i;
-    const int row = q >> 7, px = (q >> 3) & 15, chunk = q & 7;
+    const int row = q >> 6, px = (q >> 2) & 15, c8 = q & 3;
     const int gr = x.r0 + row, gc = x.c0 + px;
-    const float4 v = *reinterpret_cast<const float4*>(stage + f2_stage_off(row, px, chunk));
-    if (gr < P && gc < P) st_stream(reinterpret_cast<float4*>(y2 + (((int64_t)x.b * P + gr) * P + gc) * 32 + chunk * 4), v);
+    const uint4 a = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8));
+    const uint4 b = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8 + 1));
+    uint4 v;
+    v.x = __builtin_amdgcn_perm(a.y, a.x, 0x05040100u);
+    v.y = __builtin_amdgcn_perm(a.w, a.z, 0x05040100u);
+    v.z = __builtin_amdgcn_perm(b.y, b.x, 0x05040100u);
+    v.w = __builtin_amdgcn_perm(b.w, b.z, 0x05040100u);
+    if (gr < P && gc < P)
+      st_stream(reinterpret_cast<float4*>(y2h + (((int64_t)x.b * P + gr) * P + gc) * 32 + c8 * 8),
+                __builtin_bit_cast(float4, v));
   }
 }
 
 template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
                                        const float* __restrict__ bias, const float* __restrict__ gamma,
-                                       float* __restrict__ y2, float* __restrict__ ya, double* __restrict__ partial,
-                                       uint32_t* __restrict__ ypart, const uint32_t* __restrict__ scales,
+                                       unsigned short* __restrict__ y2, float* __restrict__ ya,
+                                       double* __restrict__ partial, uint32_t* __restrict__ ypart,
+                                       const uint32_t* __restrict__ scales,
                                        const int* __restrict__ order, int sw, int sk, int B, int P, char* smem) {
   constexpr int NT = WV & 1, RH = WV >> 1;
   const int lane = threadIdx.x & 63, li = lane & 15;
@@ -260,6 +304,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   const float bco = bias[16 * NT + li];
   // the packed weights' and p1's power-of-two scales (conv2_pack.hip): y2 = acc * inv + b2, exact
   const float inv = scales != nullptr ? __uint_as_float(scales[0]) * __uint_as_float(scales[1]) : 1.f;
+  const float ksc = scales != nullptr ? __uint_as_float(scales[2]) : 1.f;  // y2h store factor
   const bool neg = gamma != nullptr && gamma[16 * NT + li] < 0.f;
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
@@ -284,10 +329,10 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
     if (cur.r0 + F2_TH <= P && cur.c0 + F2_TC <= P)  // tile-uniform
       f2_stage<false>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
-                      bco, inv, neg, s_acc, q_acc, ymx);
+                      bco, inv, ksc, neg, s_acc, q_acc, ymx);
     else
       f2_stage<true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
-                     bco, inv, neg, s_acc, q_acc, ymx);
+                     bco, inv, ksc, neg, s_acc, q_acc, ymx);
     prev = cur;
     have_prev = true;
   }
@@ -329,7 +374,7 @@ __global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* 
                                                                    const uint4* __restrict__ wpack,
                                                                    const float* __restrict__ bias,
                                                                    const float* __restrict__ gamma,
-                                                                   float* __restrict__ y2, float* __restrict__ ya,
+                                                                   unsigned short* __restrict__ y2, float* __restrict__ ya,
                                                                    double* __restrict__ partial,
                                                                    uint32_t* __restrict__ ypart,
                                                                    const uint32_t* __restrict__ scales,
@@ -357,7 +402,7 @@ void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c) {
 
 #ifdef TDS_DIAG
 // timing-only variants (tools/conv2_diag.py): 1 no MFMAs, 2 no LDS operand reads, 3 no global
-// tile loads, 4 no y2 stores.  Compiled only into a -DTDS_DIAG build.
+// tile loads, 4 no y2h stores.  Compiled only into a -DTDS_DIAG build.
 static int f2_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
   return e ? std::atoi(e) : 0;
@@ -368,10 +413,11 @@ static int f2_diag_env() { return 0; }
 
 // order: the blocked tile order table (tds_tile_order_fill) as per-workgroup lists [nwg][ceil(total / nwg)]
 // (fused_ops.cpp tile_order, sw / sk: the strides of workgroup / tile), allocated by the caller
-void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
                     double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
                     int B, int P, hipStream_t st) {
   const dim3 grid(nwg), block(F2_THREADS);
+  unsigned short* y2 = static_cast<unsigned short*>(y2h);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wp);
   static bool lds_set = false;

@@ -6,7 +6,7 @@
 //
 // Activation formats (produced/consumed by convnet_fused.hip and the conv2 kernels):
 //   p1  [B][P][P][16] fp16                                          (pooled layer-1 output)
-//   y2  [B][P][P][32] fp32                                          (conv2 output, incl. bias)
+//   y2h [B][P][P][32] fp16                        (conv2 output: bias-free, scaled; conv2_common.h)
 //   dp1 [B][P][P][16] fp32                                          (grad wrt p1)
 // MFMA mapping (v_mfma_f32_16x16x32_f16, lane l: i = l&15, g = l>>4):
 //   A[i][k = 8g+j] (8 consecutive k per lane), B[k = 8g+j][n = i], C row = 4g+r, col = i.
@@ -31,8 +31,9 @@ namespace tds {
 // max |w| * 2^ew in [2^14, 2^15) (every block finds max |w| itself over the 12 800 weights, by
 // float4 loads from L2: no inter-block step), and mag[kMagScales] = 2^-ew, mag[kMagScales + 1] = 1 / p1_scale (the layer-1
 // range guard, convnet_fused.hip l1_gram; 1 when not given) are what the conv2 forward and
-// backward epilogues multiply their accumulators by (powers of two: exact).  Without mag the
-// weights are packed unscaled.
+// backward epilogues multiply their accumulators by (powers of two: exact); mag[kMagScales + 2]
+// is the y2h store factor (conv2_common.h).  Without mag the weights are packed unscaled (and
+// the forward stores y2h unscaled).
 __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* __restrict__ wp,
                                           short* __restrict__ wd, uint32_t* __restrict__ mag,
                                           const float* __restrict__ p1_scale) {
@@ -65,10 +66,34 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
     }
     wsc = ldexpf(1.f, ew);
     if (blockIdx.x == 0) {
+      // the y2h store factor 2^k (conv2_common.h): L = max_c sum |w_c| (channel c = 100 float4,
+      // 8 lanes each, summed in a fixed order), 1.01 * L * 2^ew * 2^k <= 1
+      const int c = threadIdx.x >> 3, j = threadIdx.x & 7;
+      float l1 = 0.f;
+      for (int k = j; k < 100; k += 8) {
+        const float4 q = w4[c * 100 + k];
+        l1 += (fabsf(q.x) + fabsf(q.y)) + (fabsf(q.z) + fabsf(q.w));
+      }
+      l1 += __shfl_xor(l1, 1, 64);
+      l1 += __shfl_xor(l1, 2, 64);
+      l1 += __shfl_xor(l1, 4, 64);
+      l1 = wave_max(l1);
+      if ((threadIdx.x & 63) == 0) red[8 + (threadIdx.x >> 6)] = l1;
+      __syncthreads();
+      float L = red[8];
+      for (int i = 1; i < (int)(blockDim.x >> 6); ++i) L = fmaxf(L, red[8 + i]);
+      L *= 1.01f * wsc;
+      int ky = 0;
+      if (L > 0.f && __builtin_isfinite(L)) {
+        int x;
+        (void)frexpf(L, &x);  // L < 2^x
+        ky = min(100, max(-100, -x));
+      }
       if (threadIdx.x < 33) mag[threadIdx.x] = 0u;
       if (threadIdx.x == 0) {
         mag[kMagScales] = __float_as_uint(ldexpf(1.f, -ew));
         mag[kMagScales + 1] = __float_as_uint(p1_scale != nullptr ? 1.f / p1_scale[0] : 1.f);
+        mag[kMagScales + 2] = __float_as_uint(ldexpf(1.f, ky));
       }
     }
   }

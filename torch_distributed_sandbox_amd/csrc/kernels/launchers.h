@@ -83,19 +83,21 @@ int tds_tile_order_fill(int* out, int B, int tiles_r, int tiles_c, int group_row
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st);
 int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
-// y2 [B,P,P,32]; ya pooled-blocked (pooled_layout.h), max/min of each 2x2 window by sign(gamma2)
+// y2h [B,P,P,32] fp16 (conv2_common.h); ya pooled-blocked (pooled_layout.h), max/min of each 2x2
+// window of y2 by sign(gamma2)
 // ypart (optional): max |y2| per (channel, workgroup), [32][nwg] float bits
 // scales (optional): mag + kMagScales (conv2_pack.hip), the packed weights' and p1's inverse scales
-void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, float* y2, float* ya,
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
                     double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
                     int B, int P, hipStream_t st);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups
-// mag: the forward's / head backward's magnitude bounds (the fp16 scale of dy2)
-void tds_conv2_bwd3(const float* y2, const float* g2m, const float* aff2, const float* kbuf, const uint32_t* mag,
-                    const void* p1, const short* wd, float* dp1, float* slab, const int* walk, int nwg, int sw, int sk,
-                    int B, int P, hipStream_t st);
+// mag: the forward's / head backward's magnitude bounds (the fp16 scale of dy2) and the y2h
+// decode (conv2_common.h); b2: conv2.bias (y2h is bias-free)
+void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
+                    const uint32_t* mag, const void* p1, const short* wd, float* dp1, float* slab, const int* walk,
+                    int nwg, int sw, int sk, int B, int P, hipStream_t st);
 // host: per-workgroup tile lists of vertical segments of ~seg tiles; out == nullptr -> length
 int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, int seg);
 

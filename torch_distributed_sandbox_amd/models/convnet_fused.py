@@ -194,8 +194,8 @@ class _Conv2(torch.autograd.Function):
         link = ctx.link
         _run_before_conv2_backward()
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
-        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, link.mag, p1, wd, 1.0,
-                                                           *_sinks(ctx, ctx.params, 1))
+        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, ctx.params[1], link.mag,
+                                                           p1, wd, 1.0, *_sinks(ctx, ctx.params, 1))
         link.g2m = link.kbuf = link.aff2 = link.mag = None
         dp1_ph = None
         if ctx.needs_input_grad[0]:
