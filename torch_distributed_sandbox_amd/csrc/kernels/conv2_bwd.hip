@@ -490,8 +490,10 @@ struct BRStager {
   // BN2 / ReLU / pool backward of the staged windows -> dy2 hi|lo rows at dbase; p1 -> pbase;
   // MIRROR: rows 4-7 stored a second time at dmir / pmir (the next slot's top rows).
   // dy2 = k1*dz + k2*y2 + k3, dz = pooled gradient at the window's argmax of a*y2 + b.  Interior
-  // blocks take a short path (argmax by max + first-equal, torch's scan-order tie rule); a NaN
-  // anywhere in the wave's windows sends it to the general path (torch's NaN-wins rule).
+  // blocks take a short path (argmax by max + first-equal, torch's scan-order tie rule; no NaN
+  // rule: a NaN in y2 makes its channel's BN2 statistics NaN, hence a, b, k1..k3, hence every dy2
+  // of the channel, whichever pixel dz goes to -- as in torch).  Border blocks take the general
+  // path (zero padding, unpooled last row / column, torch's NaN-wins scan).
   template <bool MIRROR>
   __device__ __forceinline__ void store(const BRArgs& a, int R0, int c0, int tid, char* dbase, char* pbase,
                                         const float* kc, char* dmir, char* pmir) {
@@ -506,15 +508,7 @@ struct BRStager {
     const float ka[4] = {ka4.x, ka4.y, ka4.z, ka4.w}, kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
     const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, k2[4] = {k24.x, k24.y, k24.z, k24.w},
                 k3[4] = {k34.x, k34.y, k34.z, k34.w};
-    bool fast = interior(a, R0, c0);
-    if (fast) {  // a NaN among the fp16 values: exponent all ones, mantissa non-zero
-      uint32_t nan = 0u;
-#pragma unroll
-      for (int u = 0; u < IPER; ++u)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) nan |= f16x2_nan(yv[u][q].x) | f16x2_nan(yv[u][q].y);
-      fast = __builtin_amdgcn_ballot_w64(nan != 0u) == 0;  // wave-uniform
-    }
+    const bool fast = interior(a, R0, c0);
 #pragma unroll
     for (int u = 0; u < IPER; ++u) {
       const int it = tid + 256 * u;

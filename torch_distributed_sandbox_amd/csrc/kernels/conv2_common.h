@@ -28,10 +28,6 @@ __device__ __forceinline__ uint32_t f16_bits(float x) {
 __device__ __forceinline__ float f16_val(uint32_t h) {
   return (float)__builtin_bit_cast(_Float16, (unsigned short)(h & 0xFFFFu));
 }
-// non-zero when either fp16 of the pair is a NaN
-__device__ __forceinline__ uint32_t f16x2_nan(uint32_t x) {
-  return (uint32_t)((x & 0x7FFFu) > 0x7C00u) | (uint32_t)(((x >> 16) & 0x7FFFu) > 0x7C00u);
-}
 
 // ---------------------------------------------------------------------------- diagnostics
 // DIAG = 0: the real kernel.  Timing-only builds (tools/conv2_diag.py, TDS_CONV2_DIAG):
