@@ -16,13 +16,13 @@ fitting 288 GB is much larger.  This script:
    mp.spawn) or under torchrun with N ranks: step 2 runs on rank 0 alone, step 3 is the
    DDP run over all ranks, effective batch 5N.
 
-    python tools/oom_demo.py                                     # 1 GPU, 20400^2
+    python tools/oom_demo.py                                     # 1 GPU, 23000^2
     python tools/oom_demo.py --gpus 8                            # the DDP half: 8 ranks
 
 Round 4 re-measured the plan at HEAD (uint8 level input, fp16 p1): at 18000^2 a batch of 10
-now fits (275 GB peak, profiles/r4_oom_demo_18000.json), the calibrated model puts the batch-10
-edge at ~19 900 px, so the default image edge is 20400 (batch 10 predicted 325 GB > 309 GB,
-batch 5 200 GB).
+now fits (275 GB peak, profiles/r4_oom_demo_18000.json).  With the conv2 output stored as y2h
+(64 B per pixel instead of 128) the edge moved again: at 23000^2 batch 10 runs out of memory and
+batch 5 trains at 224.9 GB peak (profiles/r4_oom_demo_23000.json), so the default edge is 23000.
     python tools/oom_demo.py --gpus 2 --shared-device --image-size 1024 --calib-size 512
                                                                  # rehearsal: 2 gloo ranks on cuda:0
 """
@@ -93,7 +93,7 @@ def run(H, B, steps, device, world, rank):
 
 def _parser():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--image-size", type=int, default=20400)
+    ap.add_argument("--image-size", type=int, default=23000)
     ap.add_argument("--bs-fail", type=int, default=10)
     ap.add_argument("--bs-fit", type=int, default=5)
     ap.add_argument("--steps", type=int, default=3)
