@@ -418,6 +418,8 @@ struct BRStager {
     return R0 >= 0 && R0 + NR <= 2 * a.Q && c0 - 2 >= 0 && c0 + BR_TC + 2 <= 2 * a.Q;
   }
 
+  // (bounds as bitwise &, | of unsigned compares: short-circuit && / || compiled to exec-mask
+  // branches around every load's address, and the merges cost a vmcnt(0) per load set)
   __device__ __forceinline__ void load(const BRArgs& a, int b, int R0, int c0, int tid) {
     if constexpr (DIAG == 3) {
 #pragma unroll
@@ -453,13 +455,13 @@ struct BRStager {
       for (int q = 0; q < 4; ++q) {
         const int lr = 2 * wy + (q >> 1), lc = 2 * wx + (q & 1);
         const int gr = R0 + lr, gc = c0 - 2 + lc;
-        const bool ok = item && (in || (gr >= 0 && gr < P && gc >= 0 && gc < P));
+        const bool ok = item & (in | (((uint32_t)gr < (uint32_t)P) & ((uint32_t)gc < (uint32_t)P)));
         const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 64 + c4 * 8) : kBROob;
         yv[u][q] = DIAG == 7 ? make_uint2(0x3C00u, 0u)
                              : __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, 0));
       }
       const int py = py0 + wy, px = px0 + wx;
-      const bool pooled = item && (in || (py >= 0 && py < Q && px >= 0 && px < Q));
+      const bool pooled = item & (in | (((uint32_t)py < (uint32_t)Q) & ((uint32_t)px < (uint32_t)Q)));
       float g4[4];
       if constexpr (!BIG) {
         const uint32_t og = (uint32_t)(((int64_t)c4 * 4 * gplane + (int64_t)wy * Q + wx) * 4);
@@ -481,7 +483,7 @@ struct BRStager {
       const int rec = (e < PIECES ? e : 0) >> 1, q = e & 1;
       const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
       const int gr = R0 + lr, gc = c0 - 2 + lc;
-      const bool ok = e < PIECES && (in || (gr >= 0 && gr < P && gc >= 0 && gc < P));
+      const bool ok = (e < PIECES) & (in | (((uint32_t)gr < (uint32_t)P) & ((uint32_t)gc < (uint32_t)P)));
       const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 32 + q * 16) : kBROob;
       pr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
     }
@@ -498,6 +500,19 @@ struct BRStager {
   __device__ __forceinline__ void store(const BRArgs& a, int R0, int c0, int tid, char* dbase, char* pbase,
                                         const float* kc, char* dmir, char* pmir) {
     if constexpr (DIAG == 3) {}
+    // every register of the set is read here, on every path: the items / pieces past ITEMS /
+    // PIECES are skipped below under exec masks, and a load whose result was consumed only
+    // under a branch stays "pending" at the merge for the compiler's waitcnt pass -- the next
+    // write of that register (the look-ahead loads into this set) then got a vmcnt(0), draining
+    // the OTHER set's look-ahead loads too
+#pragma unroll
+    for (int u = 0; u < IPER; ++u) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(yv[u][q].x), "v"(yv[u][q].y));
+      asm volatile("" ::"v"(gv[u].x), "v"(gv[u].y), "v"(gv[u].z), "v"(gv[u].w));
+    }
+#pragma unroll
+    for (int j = 0; j < PPER; ++j) asm volatile("" ::"v"(pr[j].x), "v"(pr[j].y), "v"(pr[j].z), "v"(pr[j].w));
     const int c4 = tid & 7;
     const int P = a.P, Q = a.Q;
     const float4 ka4 = *reinterpret_cast<const float4*>(&kc[0 * 32 + 4 * c4]);
@@ -660,8 +675,13 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   }
   ld(st1, 1);
   ld(st0, 2);
-  // iteration kk stages tile kk+1 and loads tile kk+3 (both in set (kk+1) & 1)
-  for (int kk = 0; !tile(kk).end; kk += 2) {
+  // iteration kk stages tile kk+1 and loads tile kk+3 (set st1), then stages tile kk+2 and loads
+  // tile kk+4 (set st0).  One exit, and both load sets issued on every path through the body:
+  // with a break between them, the structurized loop had a path back to the header on which
+  // st1's loads were the youngest, and the waitcnt pass then drained BOTH sets (vmcnt(0)) at
+  // every staging of st1 -- the look-ahead was one tile, not two.
+  bool more = !tile(0).end;
+  for (int kk = 0; more; kk += 2) {
     clk.barrier();  // consumers start tile kk
     {
       const BRTile x = tile(kk + 1);
@@ -671,16 +691,17 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
       }
     }
     ld(st1, kk + 3);
-    if (tile(kk + 1).end) break;
-    clk.barrier();  // consumers start tile kk + 1
-    {
+    const bool second = !tile(kk + 1).end;
+    if (second) {
+      clk.barrier();  // consumers start tile kk + 1
       const BRTile x = tile(kk + 2);
       if (!x.end) {
         stage(st0, kk + 2, x);
         if (x.start) prologue(kk + 2, x);
       }
     }
-    ld(st0, kk + 4);
+    ld(st0, kk + 4);  // (past the end: the list's last tile again, never staged)
+    more = second && !tile(kk + 2).end;
   }
   clk.barrier();
   clk.report();
