@@ -386,6 +386,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __r
 }
 
 
+// zero source of the layer-1 backward's out-of-range prefetch lanes
+__device__ __attribute__((aligned(16))) uint4 g_l1b_zero = {0u, 0u, 0u, 0u};
+
 // layer-1 backward tile: 8 pooled rows x 32 pooled columns (x tile 20 rows incl. the halo)
 constexpr int LB_PR = 8, LB_PC = 32;
 constexpr int LB_XR = 2 * LB_PR + 4;
@@ -397,6 +400,7 @@ constexpr int LB_V = LB_V_DP + LB_V_PH + LB_V_ID + LB_V_X;  // 16-B vectors stag
 // The argmax byte carries the ReLU mask in bit 2 (set by l1_conv: pooled max > 0), so the
 // backward never reads p1 (720 MB of 64-B hi|lo records at the bench shape).
 constexpr int LB_PER = (LB_V + 255) / 256;
+static_assert(LB_V_PH == 0 && LB_V_DP % 256 == 0 && LB_V_ID % 256 == 0, "l1_bwd prefetch classes per vector");
 // LDS record of pooled pixel pp's 16 dp1 values: lane groups g0 / g1 (and g2 / g3) read pooled pixels
 // two apart, whose plain records (16 words) sit 32 words apart -- the same banks, a 2-way conflict
 // on every dp1 read.  Swapping the records of pp = 2, 3 (mod 4) puts the pair in opposite halves.
@@ -503,40 +507,51 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   const float* __restrict__ x = static_cast<const float*>(xv);
   const uint8_t* __restrict__ xl = static_cast<const uint8_t*>(xv);
   uint4 pre[LB_PER];
+  // One unconditional load per vector u: the class of vector u (dp1 records, argmax bytes, x
+  // words) is a compile-time property of u (LB_V_DP and LB_V_ID are multiples of 256, the block is
+  // 256 threads), and lanes out of range read a zero vector.  (Loads under per-lane branches had
+  // to land before the branches merged: the compiler waited for each one right after issuing it,
+  // which serialised the whole prefetch.)
   auto load_tile = [&](int t) {
     const int b = t / per_img, rem = t - b * per_img;
     const int pr0 = (rem / tiles_c) * LB_PR, pc0 = (rem % tiles_c) * LB_PC;
 #pragma unroll
     for (int u = 0; u < LB_PER; ++u) {
-      int e = tid + 256 * u;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (e < LB_V_DP + LB_V_PH + LB_V_ID) {
-        int q, nq;
-        if (e < LB_V_DP) { q = e & 3; nq = 4; e >>= 2; }
-        else if (e < LB_V_DP + LB_V_PH) { e -= LB_V_DP; q = e & 1; nq = 2; e >>= 1; }
-        else { e -= LB_V_DP + LB_V_PH; q = 0; nq = 1; }
-        const int gpr = pr0 + e / LB_PC, gpc = pc0 + e % LB_PC;
-        if (gpr < P && gpc < PW) {
-          const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
-          if (nq == 4) v = reinterpret_cast<const uint4*>(dp1)[rec * 4 + q];
-          else if (nq == 2) v = p1[rec * 4 + q];
-          else v = reinterpret_cast<const uint4*>(idx1)[rec];
-        }
-      } else if (e < LB_V) {
-        e -= LB_V_DP + LB_V_PH + LB_V_ID;
-        const int rr = e / 18, cv = e - rr * 18;
+      const int e = tid + 256 * u;
+      if (256 * u < LB_V_DP) {
+        const int pp = e >> 2, q = e & 3;
+        const int gpr = pr0 + pp / LB_PC, gpc = pc0 + pp % LB_PC;
+        const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
+        const uint4* src = (gpr < P) & (gpc < PW) ? reinterpret_cast<const uint4*>(dp1) + rec * 4 + q : &g_l1b_zero;
+        pre[u] = *src;
+      } else if (256 * u < LB_V_DP + LB_V_ID) {
+        const int pp = e - LB_V_DP;
+        const int gpr = pr0 + pp / LB_PC, gpc = pc0 + pp % LB_PC;
+        const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
+        const uint4* src = (gpr < P) & (gpc < PW) ? reinterpret_cast<const uint4*>(idx1) + rec : &g_l1b_zero;
+        pre[u] = *src;
+      } else {
+        const int ex = e - LB_V_DP - LB_V_ID;
+        const int rr = ex / 18, cv = ex - rr * 18;
         const int gr = 2 * pr0 - 2 + rr, gcol = 2 * pc0 - 4 + 4 * cv;
-        if (gr >= 0 && gr < H && gcol >= 0 && gcol < W) {
-          if constexpr (LV)  // 4 levels in .x
-            v.x = *reinterpret_cast<const uint32_t*>(xl + ((int64_t)b * H + gr) * W + gcol);
-          else
-            v = *reinterpret_cast<const uint4*>(x + ((int64_t)b * H + gr) * W + gcol);
+        const bool ok = (ex < LB_V_X) & ((uint32_t)gr < (uint32_t)H) & ((uint32_t)gcol < (uint32_t)W);
+        const int64_t o = ((int64_t)b * H + gr) * W + gcol;
+        if constexpr (LV) {  // 4 levels in .x
+          const uint32_t* src = ok ? reinterpret_cast<const uint32_t*>(xl + o) : &g_l1b_zero.x;
+          pre[u] = make_uint4(*src, 0u, 0u, 0u);
+        } else {
+          const uint4* src = ok ? reinterpret_cast<const uint4*>(x + o) : &g_l1b_zero;
+          pre[u] = *src;
         }
       }
-      pre[u] = v;
     }
   };
   auto store_tile = [&]() {
+    // every prefetch register read here on every path (the stores below are predicated): a
+    // result consumed only under a branch stays "pending" for the waitcnt pass, and the next
+    // prefetch into it then waits for every load in flight
+#pragma unroll
+    for (int u = 0; u < LB_PER; ++u) asm volatile("" ::"v"(pre[u].x), "v"(pre[u].y), "v"(pre[u].z), "v"(pre[u].w));
 #pragma unroll
     for (int u = 0; u < LB_PER; ++u) {
       int e = tid + 256 * u;
