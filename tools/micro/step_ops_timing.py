@@ -94,7 +94,8 @@ def main():
 
         def l1b():
             p1, idx1, stats1, gram = st["l1"][:4]
-            ops.fused_l1_backward(st["c2b"][0], x, p1, idx1, c1.weight, c1.bias, n1.weight, stats1, gram, 1.0)
+            ops.fused_l1_backward(st["c2b"][0], st["mag"][44:45], x, p1, idx1, c1.weight, c1.bias, n1.weight, stats1,
+                                  gram, 1.0)
 
         seq = [("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
                ("head_bwd_nomag", hb_nomag), ("conv2_bwd", c2b), ("l1_bwd", l1b)]

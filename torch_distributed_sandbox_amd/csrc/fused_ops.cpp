@@ -7,7 +7,7 @@
 //   ya          [B,32,PB] f32: pooled-blocked planes (kernels/pooled_layout.h)
 //   g2m         [B,32,Q,Q] f32: planar pooled gradient
 //   mag         int32 workspace [mag_numel(B, P)]: the step's magnitude bounds (float bits) behind
-//               the conv2 backward's fp16 gradient scale -- [0,32) max |y2| per channel, [32]
+//               the conv2 backward's fp16 gradient scale -- [0,32) max |y2 - b2| per channel, [32]
 //               max |g2m|, then per-workgroup maxima from the conv2 forward (ypart [32][nwg])
 //               and the head backward (gpart [32][npass][nblk]), written with plain stores and
 //               reduced into [0,33) by the BN2-backward finalize
@@ -485,7 +485,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
 }
 
 // ---------------------------------------------------------------- conv2 backward
-// BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2, g2m, aff2, kbuf, p1) -> (dp1, dw2, db2)
+// BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2h, g2m, aff2, kbuf, b2, p1) -> (dp1h, dw2, db2);
+// dp1h's decode factor lands in mag[kMagScales + 4] (fused_l1_backward's dp1_dec)
 std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& g2m, const Tensor& aff2,
                                                            const Tensor& kbuf, const Tensor& b2, const Tensor& mag,
                                                            const Tensor& p1,
@@ -494,7 +495,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
                                                            const c10::optional<Tensor>& db_out) {
   const int64_t B = p1.size(0), P = p1.size(1);
   need(p1, at::kHalf, {B, P, P, 16}, "p1");
-  opt_mag(mag, kMagScales + 3);  // the magnitude bounds of the forward / head backward, the y2h decode
+  opt_mag(mag, kMagScales + 5);  // the magnitude bounds of the forward / head backward, the y2h decode, the
+                                 // dp1h factors (kernels/conv2_common.h; mag[kMagScales + 4] is written)
   need(y2, at::kHalf, {B, P, P, 32}, "y2h (fused_conv2_forward's)");
   need(b2, at::kFloat, {32}, "conv2.bias");
   need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
@@ -509,14 +511,14 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   tds_conv2_bwd3_tiles((int)P, &tr, &tc);
   int sw = 0, sk = 0;
   const int* order = bwd_walk(p1, (int)B, tr, tc, nwg, &sw, &sk);
-  auto dp1 = at::empty({B, P, P, 16}, p1.options().dtype(at::kFloat));
+  auto dp1 = at::empty({B, P, (P + 3) / 4, 16, 4}, p1.options().dtype(at::kHalf));  // dp1h (kernels/conv2_common.h)
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options().dtype(at::kFloat));
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
   tds_conv2_bwd3(y2.data_ptr(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
-                 b2.data_ptr<float>(), reinterpret_cast<const uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(),
+                 b2.data_ptr<float>(), reinterpret_cast<uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(),
                  wd.data_ptr<int16_t>(),
-                 dp1.data_ptr<float>(), slab.data_ptr<float>(), order, nwg, sw, sk, (int)B, (int)P, st);
+                 dp1.data_ptr(), slab.data_ptr<float>(), order, nwg, sw, sk, (int)B, (int)P, st);
   tds_conv2_wgrad_reduce(slab.data_ptr<float>(), nwg, dw2.data_ptr<float>(), db2.data_ptr<float>(), (float)scale, st);
   check_launches("fused_conv2_backward_y2");
   return {dp1, dw2, db2};
@@ -578,7 +580,8 @@ void launch_probe(const Tensor& like, int64_t lds_bytes, int64_t threads) {
 }
 
 // ---------------------------------------------------------------- layer 1 backward
-std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, const Tensor& x, const Tensor& p1,
+std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, const Tensor& dp1_dec,
+                                                             const Tensor& x, const Tensor& p1,
                                                              const Tensor& idx1, const Tensor& w1, const Tensor& b1,
                                                              const c10::optional<Tensor>& gamma1, const Tensor& stats1,
                                                              const Tensor& gram, double scale,
@@ -590,7 +593,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3), P = H / 2;
   const bool levels = x.scalar_type() == at::kByte;
   need(x, levels ? at::kByte : at::kFloat, {B, 1, H, W}, "x");
-  need(dp1, at::kFloat, {B, P, P, 16}, "dp1");
+  need(dp1, at::kHalf, {B, P, (W / 2 + 3) / 4, 16, 4}, "dp1h (fused_conv2_backward_y2's)");
+  TORCH_CHECK(dp1_dec.is_cuda() && dp1_dec.scalar_type() == at::kInt && dp1_dec.numel() >= 1,
+              "dp1_dec: the dp1h decode factor (int32 GPU view of mag[kMagScales + 4])");
   need(p1, at::kHalf, {B, P, P, 16}, "p1");
   need(idx1, at::kByte, {B, P, P, 16}, "idx1");
   need(w1, at::kFloat, {16, 1, 5, 5}, "conv1.weight");
@@ -606,7 +611,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
     const char* e = std::getenv("TDS_L1B_PAIRS");
     return e && e[0] == '1';
   }();
-  tds_l1_bwd(x.data_ptr(), levels, pairs, dp1.data_ptr<float>(), p1.data_ptr(), idx1.data_ptr<uint8_t>(),
+  tds_l1_bwd(x.data_ptr(), levels, pairs, dp1.data_ptr(), reinterpret_cast<const uint32_t*>(dp1_dec.data_ptr<int>()),
+             p1.data_ptr(), idx1.data_ptr<uint8_t>(),
              w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);
@@ -782,12 +788,12 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);
   m.def("conv2_bwd_walk_table(int B, int tiles_r, int tiles_c, int nwg, int seg) -> Tensor", &conv2_bwd_walk_table);
   m.def(
-      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor b2, Tensor mag, Tensor p1, "
+      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor b2, Tensor(c!) mag, Tensor p1, "
       "Tensor wd, "
       "float scale, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
       &fused_conv2_backward_y2);
   m.def(
-      "fused_l1_backward(Tensor dp1, Tensor x, Tensor p1, Tensor idx1, Tensor w1, Tensor b1, Tensor? gamma1, "
+      "fused_l1_backward(Tensor dp1, Tensor dp1_dec, Tensor x, Tensor p1, Tensor idx1, Tensor w1, Tensor b1, Tensor? gamma1, "
       "Tensor stats1, Tensor gram, float scale, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None, "
       "Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None) -> (Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_backward);

@@ -3,9 +3,9 @@
 // with the fp16x2 split (bf16x3.h; 2 MFMAs per product):
 //   dgrad: dp1 = convT(dy2, w2)  -- dy2 the single-rounded fp16 operand, w2 exact (hi + lo)
 //   wgrad: dw2 = sum dy2 (x) p1  -- dy2 exact (hi + lo), p1 the forward's fp16 operand as is
-// dy2 is carried with a power-of-two scale 2^e: from the step's magnitude bounds (max |y2| per
-// channel from the forward, max |g2m| from the head backward) |dy2| <= |k1| max|g2m| + |k2|
-// max|y2| + |k3| per channel, and e puts the largest bound in [2^14, 2^15) -- no fp16
+// dy2 is carried with a power-of-two scale 2^e: from the step's magnitude bounds (max |y2 - b2|
+// per channel from the forward, max |g2m| from the head backward) |dy2| <= |k1| max|g2m| + |k2|
+// (max|y2 - b2| + |b2|) + |k3| per channel, and e puts the largest bound in [2^14, 2^15) -- no fp16
 // overflow by construction, ~28 binades of full fp16 precision below it.  The products are
 // unscaled exactly (power of two) in the dp1 / weight-slab epilogues.
 //
@@ -70,7 +70,8 @@ constexpr int BR_OFF_P = BR_OFF_D + 3 * BR_SLOT * BR_DROW;   // 3 x 12 p1 row bl
 constexpr int BR_XCHG = 2 * 4 * 64 * 16;                     // 8 KiB exchange slot
 constexpr int BR_OFF_X = BR_OFF_P + 3 * BR_SLOT * BR_PROW;   // 2 exchange slots
 constexpr int BR_OFF_K = BR_OFF_X + 2 * BR_XCHG;             // 160 floats of constants + 4
-constexpr int BR_KINV = 160;  // kc[160] = 2^-e * 2^-ew (dp1), kc[161] = 2^-e / p1 scale (weight taps), kc[162] = 2^-e (bias)
+constexpr int BR_KINV = 160;  // kc[160] = 2^-e * 2^-ew (dp1), kc[161] = 2^-e / p1 scale (weight taps), kc[162] = 2^-e (bias),
+                              // kc[163] = 2^kd (the dp1h store factor)
 constexpr int BR_LDS = BR_OFF_K + (5 * 32 + 4) * 4;
 static_assert(BR_LDS <= 160 * 1024 && BR_OFF_X % 16 == 0 && BR_OFF_K % 16 == 0, "LDS carve");
 
@@ -102,7 +103,7 @@ struct BRArgs {
   const uint2* __restrict__ y2;  // y2h [B][P][P][32] fp16 (conv2_common.h)
   const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
   const uint4* __restrict__ p1;
-  float* __restrict__ dp1;
+  uint2* __restrict__ dp1;  // dp1h (conv2_common.h)
   float* __restrict__ slab;
   const int* __restrict__ walk;
   int B, P, Q, sk, w;
@@ -142,23 +143,22 @@ __device__ __forceinline__ void br_xchg_put(f32x4* xs, const f32x4 (&acc)[8], in
   for (int i = 0; i < 4; ++i) xs[((1 - D) * 4 + i) * 64 + lane] = acc[4 * (1 - D) + i];
 }
 
-// Wave D owns output rows 4D .. 4D+3: its partial + the partner's, then dp1.
+// Wave D owns output rows 4D .. 4D+3: its partial + the partner's, then dp1h (conv2_common.h): the
+// lane's 4 columns 4g + r of channel li are 8 contiguous bytes, a row's 64 lanes 512 (columns
+// past P land in the last column group's padding)
 template <int D>
-__device__ __forceinline__ void br_xchg_finish(const f32x4* xs, const f32x4 (&acc)[8], float* __restrict__ dp1,
-                                               int lane, int b, int r0, int c0, int P, float inv) {
+__device__ __forceinline__ void br_xchg_finish(const f32x4* xs, const f32x4 (&acc)[8], uint2* __restrict__ dp1h,
+                                               int lane, int b, int r0, int c0, int P, float sd) {
   const int li = lane & 15, g = lane >> 4;
+  const int PG = (P + 3) >> 2;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const f32x4 v = (acc[4 * D + i] + xs[(D * 4 + i) * 64 + lane]) * inv;  // 2^-e: exact
+    const f32x4 v = (acc[4 * D + i] + xs[(D * 4 + i) * 64 + lane]) * sd;  // 2^kd: exact
     const int row = r0 + 4 * D + i;
-    if (row < P) {
-      float* orow = dp1 + ((int64_t)b * P + row) * P * 16;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int col = c0 + 4 * g + r;
-        if (col < P) orow[(int64_t)col * 16 + li] = v[r];  // plain: read next by the layer-1 backward
-      }
-    }
+    // (a tile past the image's right edge: whole column groups beyond PG are not stored -- they
+    // would land in the next row)
+    if (row < P && (c0 >> 2) + g < PG)  // plain stores: read next by the layer-1 backward
+      dp1h[(((int64_t)b * P + row) * PG + (c0 >> 2) + g) * 16 + li] = make_uint2(cvt2_f16(v[0], v[1]), cvt2_f16(v[2], v[3]));
   }
 }
 
@@ -344,9 +344,10 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
 #pragma unroll
   for (int j = 0; j < 8; ++j) ones[j] = (short)(li == 0 ? kF16One : 0);
   const int hp = (g >> 1) * BR_DPL + (g & 1) * 16;
-  // epilogue scales (powers of two, exact): dp1 takes out the dy2 and packed-weight scales, the
-  // weight-gradient slab the dy2 and p1 scales, the bias tap (dy2 sums) the dy2 scale only
-  const float inv = reinterpret_cast<const float*>(smem + BR_OFF_K)[ROLE < 2 ? BR_KINV : BR_KINV + 1];
+  // epilogue scales (powers of two, exact): dp1h is stored at 2^kd (its decode, 2^-e 2^-ew 2^-kd,
+  // goes to mag[kMagScales + 4]), the weight-gradient slab takes out the dy2 and p1 scales, the
+  // bias tap (dy2 sums) the dy2 scale only
+  const float inv = reinterpret_cast<const float*>(smem + BR_OFF_K)[ROLE < 2 ? BR_KINV + 3 : BR_KINV + 1];
   const float inv_b = reinterpret_cast<const float*>(smem + BR_OFF_K)[BR_KINV + 2];
   BRTile prev{0, 0, 0, false, true};
   BRClock<DIAG> clk;
@@ -712,8 +713,8 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
     const uint2* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
     const float* __restrict__ kbuf, const float* __restrict__ b2, const uint32_t* __restrict__ mag,
     const uint4* __restrict__ p1,
-    const uint4* __restrict__ wdpack, float* __restrict__ dp1, float* __restrict__ slab, const int* __restrict__ walk,
-    int sw, int sk, int B, int P) {
+    const uint4* __restrict__ wdpack, uint2* __restrict__ dp1, uint32_t* __restrict__ dp1_dec, float* __restrict__ slab,
+    const int* __restrict__ walk, int sw, int sk, int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -729,7 +730,8 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
     // place, kc[BR_KINV] = 2^-e for the epilogues
     const int c = tid & 31;
     const float k1 = kbuf[c], k2 = kbuf[32 + c], k3 = kbuf[64 + c];
-    const float gmx = __uint_as_float(mag[32]), ymx = __uint_as_float(mag[c]);
+    // mag[c] = max |y2 - b2| (conv2_fwd2.hip): |y2| <= mag[c] + |b2|
+    const float gmx = __uint_as_float(mag[32]), ymx = __uint_as_float(mag[c]) + fabsf(b2[c]);
     float bound = fabsf(k1) * gmx + fabsf(k2) * ymx + fabsf(k3);
     bound = wave_max(tid < 32 ? bound : 0.f);  // NaN/inf bound: no scaling (e = 0)
     int e = 0;
@@ -752,10 +754,12 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
       kc[128 + c] = fmaf(k2, bc, k3) * sc;
     }
     if (tid == 0) {
-      const float ie = ldexpf(1.f, -e);
+      const float ie = ldexpf(1.f, -e), sd = __uint_as_float(mag[kMagScales + 3]);
       kc[BR_KINV] = ie * __uint_as_float(mag[kMagScales]);          // dy2 and packed-weight scales
       kc[BR_KINV + 1] = ie * __uint_as_float(mag[kMagScales + 1]);  // dy2 and p1 scales
       kc[BR_KINV + 2] = ie;
+      kc[BR_KINV + 3] = sd;                                         // the dp1h store factor
+      if (blockIdx.x == 0) dp1_dec[0] = __float_as_uint(kc[BR_KINV] / sd);  // exact: powers of two
     }
   }
   __syncthreads();  // kc visible to every role
@@ -872,7 +876,7 @@ static int br_diag_env() { return 0; }
 // g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
 // [nwg][rows] (fused_ops.cpp bwd_walk)
 void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
-                    const uint32_t* mag, const void* p1, const short* wd, float* dp1, float* slab, const int* walk,
+                    uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st) {
   const int Q = P / 2;
   const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
@@ -887,7 +891,8 @@ void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const 
     hipLaunchKernelGGL((conv2_bwd_roll_kernel<D, BG>), dim3(nwg), dim3(BR_THREADS), BR_LDS, st,                        \
                        reinterpret_cast<const uint2*>(y2h), g2m, aff2, kbuf, b2, mag,                                    \
                        reinterpret_cast<const uint4*>(p1),                                                            \
-                       reinterpret_cast<const uint4*>(wd), dp1, slab, walk, sw, sk, B, P);                                      \
+                       reinterpret_cast<const uint4*>(wd), static_cast<uint2*>(dp1h), mag + kMagScales + 4, slab, walk, \
+                       sw, sk, B, P);                                                                                 \
     TDS_LAUNCH_CHECK();                                                                                                \
   }
 #define TDS_BR_LAUNCH(D)           \

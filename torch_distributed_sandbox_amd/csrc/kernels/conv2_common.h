@@ -10,7 +10,18 @@ namespace tds {
 // Words of the step's magnitude workspace ("mag", fused_ops.cpp) past the 33 bounds: written by
 // conv2_pack_weights_kernel, read by the conv2 forward / backward epilogues (powers of two).
 constexpr int kMagScales = 40;  // mag[40] = 2^-ew (packed weights' scale), mag[41] = 1 / p1 scale,
-                                // mag[42] = 2^k, the y2h store factor (conv2_fwd2.hip)
+                                // mag[42] = 2^k, the y2h store factor (conv2_fwd2.hip),
+                                // mag[43] = 2^kd, the dp1h store factor (conv2_bwd.hip),
+                                // mag[44] = the dp1h decode (written by the conv2 backward)
+
+// ---------------------------------------------------------------------------- dp1h
+// The conv2 data gradient dp1 travels to the layer-1 backward as dp1h [B][P][PG = ceil(P/4)][16 ch]
+// [4 px] fp16: h = fp16(acc * 2^kd), acc the dgrad accumulator (dp1 = acc * 2^-e * 2^-ew).  The
+// dy2 operand is below 2^15 by its scale e, so |acc| <= 2^15 max_ci sum |w~_ci| and conv2_pack
+// picks 2^kd with 1.01 * 2^15 * max_ci sum_{co,tap} |w_co,ci,tap| * 2^ew * 2^kd <= 65504: no
+// overflow, 11 significant bits (the TF32 rounding the reference's conv1 weight gradient applies
+// to this operand).  The layout is the dgrad MFMA's: a lane's 4 columns of one channel are 8
+// contiguous bytes, a wave-instruction 512 contiguous bytes of one row.
 
 // ---------------------------------------------------------------------------- y2h
 // The conv2 output travels from the forward to the backward as y2h [B][P][P][32] fp16 (64 B per

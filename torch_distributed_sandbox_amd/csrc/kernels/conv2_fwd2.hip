@@ -18,7 +18,7 @@
 //     statistics are.  Every lane holds whole windows of its channel, the 4 x 8 pooled block
 //     of the tile is staged in LDS and stored as ya (pooled_layout.h): one 128-B line per
 //     channel.  The head then streams ya (72 MB per image at 3000^2) instead of y2 (288 MB).
-//   * max |y2| per channel and workgroup goes to ypart (a region of the step's magnitude-bound
+//   * max |y2 - b2| per channel and workgroup goes to ypart (a region of the step's magnitude-bound
 //     workspace, fused_ops.cpp "mag"); reduced with the head backward's max |g2m| by the BN2
 //     backward finalize, it bounds the conv2 output gradient, whose fp16 scale the backward
 //     picks from it.
@@ -40,15 +40,22 @@ constexpr int F2_THREADS = 256;
 constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records (1 KiB)
 constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records of 32 B, 240 used)
 constexpr int F2_PBUF = F2_PPLANE;                     // one fp16 plane
-constexpr int F2_PXREC = 32 * 4 + 16;                 // staged pixel record: 32 co dwords (y2h bits) + 16 B pad (banks)
-constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;       // a finished tile's padded staging buffer (18 KiB)
+// TDS_F2_WG: workgroups per CU.  2: the staged tile holds one dword per value (the y2h bits), 60 KiB
+// of LDS; 3 (A/B variant): the staged tile holds the y2h halves themselves (channel pairs joined by
+// one DPP move), 44 KiB, and the kernel is cut to 168 VGPRs
+#ifndef TDS_F2_WG
+#define TDS_F2_WG 2
+#endif
+constexpr bool F2_H16 = TDS_F2_WG == 3;
+constexpr int F2_PXREC = F2_H16 ? 32 * 2 + 16 : 32 * 4 + 16;  // staged pixel record: 32 co + 16 B pad (banks)
+constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;           // a finished tile's padded staging buffer
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
 constexpr int F2_YSTAGE = 32 * 32 * 4;                 // pooled block: 32 co x 4 x 8 fp32 = 4 KiB
 constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
-constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging: 56 KiB
+constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging
 constexpr int F2_DMA_PER_WAVE = F2_PGROUPS / (F2_THREADS / 64);  // 2
 static_assert(F2_LDS % 16 == 0, "LDS carve");
-static_assert(2 * F2_LDS <= 160 * 1024, "two workgroups per CU");
+static_assert(TDS_F2_WG * F2_LDS <= 160 * 1024, "workgroups per CU");
 
 // 16 zero bytes: the DMA source of staged records outside the image
 __device__ __attribute__((aligned(16))) uint32_t g_f2_zero[4] = {0u, 0u, 0u, 0u};
@@ -136,7 +143,7 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
 // 128-B pixel records, 1 KiB contiguous per wave-instruction.  (Stored straight from the MFMA
 // layout, each wave wrote 64-B halves of lines whose other half came from another wave: the y2
 // writes then cost ~0.3 ms more, TDS_CONV2_DIAG=4.)
-__device__ __forceinline__ int f2_stage_off(int row, int px, int chunk) {
+__device__ __forceinline__ int f2_stage_off(int row, int px, int chunk) {  // chunk: 16 B
   return (row * F2_TC + px) * F2_PXREC + chunk * 16;
 }
 
@@ -162,7 +169,7 @@ __device__ __forceinline__ void f2_keep_first(uint32_t& h0, uint32_t& h1, uint32
   const uint32_t ha = e0 ? h0 : e1 ? h1 : e2 ? h2 : h3;
   const float ra = f16_val(ha);
   const bool tie = !e0 && (f16_val(h0) == ra || (!e1 && (f16_val(h1) == ra || (!e2 && f16_val(h2) == ra))));
-  if (tie) {
+  if (tie) {  // (if-converted; a wave-ballot skip measured no faster: tools/gpu_sessions/r4_s18.sh)
     // outward = up (max window) / down (min window): +1 on the bits when the sign bit differs
     // from the direction's, -1 otherwise (ha is finite: |v * 2^k| < 65504 by construction)
     const uint32_t out = ((ha >> 15) & 1u) ^ (neg ? 0u : 1u) ? ha + 1u : ha - 1u;
@@ -174,13 +181,15 @@ __device__ __forceinline__ void f2_keep_first(uint32_t& h0, uint32_t& h1, uint32
 
 // stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li].
 // EDGE: a tile reaching past the image (last tile row / column) masks its statistics; interior
-// tiles (all but ~1 %) accumulate unmasked and take max |y2| with the NaN-propagating
-// v_maximum_f32 (|y| as a source modifier): 4 VALU per output instead of ~8 (the kernel's VALU
-// issue competes with the MFMAs of the same SIMD).
+// tiles (all but ~1 %) accumulate unmasked, in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: two
+// outputs per instruction), and take max |y2 - b2| as max |acc| with the NaN-propagating
+// v_maximum_f32 (|v| as a source modifier; scaled by inv once per workgroup).  A wave64 VALU
+// instruction holds its SIMD for 4 cycles, and that issue competes with the same SIMD's MFMAs.
+typedef float f2v __attribute__((ext_vector_type(2)));
 template <bool EDGE>
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
                                          int RH, int NT, int lane, float bco, float inv, float ksc, bool neg,
-                                         float& s_acc, float& q_acc, uint32_t& ymx) {
+                                         f2v& s_acc, f2v& q_acc, uint32_t& ymx) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
   float ymf = 0.f;
@@ -189,25 +198,28 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
   for (int o = 0; o < 4; ++o)
 #pragma unroll
     for (int r = 0; r < 4; ++r) h[o][r] = f16_bits(acc[o][r] * ksc);
+  // acc = (y2 - b2) / inv: statistics shifted by the bias, scaled at the end
 #pragma unroll
   for (int o = 0; o < 4; ++o) {
     const int row = 4 * RH + o;
     const bool rok = !EDGE || x.r0 + row < P;
+    if constexpr (EDGE) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int px = 4 * g + r;
-      const float v = acc[o][r];  // (y2 - b2) / inv: statistics shifted by the bias, scaled at the end
-      const float y = fmaf(v, inv, bco);
-      if constexpr (EDGE) {
-        if (rok && x.c0 + px < P) {
-          s_acc += v;
-          q_acc += v * v;
-          ymx = max(ymx, __float_as_uint(y) & 0x7fffffffu);  // |y2| bits (NaN: above every finite)
+      for (int r = 0; r < 4; ++r) {
+        const float v = acc[o][r];
+        if (rok && x.c0 + 4 * g + r < P) {
+          s_acc.x += v;
+          q_acc.x += v * v;
+          ymx = max(ymx, __float_as_uint(v) & 0x7fffffffu);  // |v| bits (NaN: above every finite)
         }
-      } else {
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; r += 2) {
+        const f2v v = {acc[o][r], acc[o][r + 1]};
         s_acc += v;
-        q_acc = fmaf(v, v, q_acc);
-        ymf = __builtin_elementwise_maximum(ymf, fabsf(y));  // NaN wins (as the bits' unsigned max)
+        q_acc = __builtin_elementwise_fma(v, v, q_acc);
+        ymf = __builtin_elementwise_maximum(ymf, __builtin_elementwise_maximum(fabsf(v.x), fabsf(v.y)));  // NaN wins
       }
     }
   }
@@ -229,12 +241,26 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
     // pcols 2g, 2g+1 are adjacent floats of one swizzled chunk: one ds_write_b64
     *reinterpret_cast<float2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_float2(e[0], e[1]);
   }
-  // the y2h bits, one dword per value (f2_store packs channel pairs)
+  if constexpr (F2_H16) {
+    // the y2h halves: even lanes join their odd neighbour's (channel co + 1) by a quad-permute DPP
+    // move and write the pair (row, px) of channels co, co + 1
 #pragma unroll
-  for (int o = 0; o < 4; ++o)
+    for (int o = 0; o < 4; ++o)
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      *reinterpret_cast<uint32_t*>(stage + f2_stage_off(4 * RH + o, 4 * g + r, co >> 2) + (co & 3) * 4) = h[o][r];
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)h[o][r], 0xF5, 0xF, 0xF, false);  // quad [1,1,3,3]
+        if ((li & 1) == 0)
+          *reinterpret_cast<uint32_t*>(stage + (((4 * RH + o) * F2_TC + 4 * g + r) * F2_PXREC) + co * 2) =
+              (h[o][r] & 0xFFFFu) | (nb << 16);
+      }
+  } else {
+    // the y2h bits, one dword per value (f2_store packs channel pairs)
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<uint32_t*>(stage + f2_stage_off(4 * RH + o, 4 * g + r, co >> 2) + (co & 3) * 4) = h[o][r];
+  }
 }
 
 // the workgroup stores the staged pooled block: thread e -> channel e / 8, float4 e % 8
@@ -259,13 +285,17 @@ __device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, uns
     const int q = e + F2_THREADS * i;
     const int row = q >> 6, px = (q >> 2) & 15, c8 = q & 3;
     const int gr = x.r0 + row, gc = x.c0 + px;
-    const uint4 a = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8));
-    const uint4 b = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8 + 1));
     uint4 v;
-    v.x = __builtin_amdgcn_perm(a.y, a.x, 0x05040100u);
-    v.y = __builtin_amdgcn_perm(a.w, a.z, 0x05040100u);
-    v.z = __builtin_amdgcn_perm(b.y, b.x, 0x05040100u);
-    v.w = __builtin_amdgcn_perm(b.w, b.z, 0x05040100u);
+    if constexpr (F2_H16) {
+      v = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, c8));
+    } else {
+      const uint4 a = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8));
+      const uint4 b = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8 + 1));
+      v.x = __builtin_amdgcn_perm(a.y, a.x, 0x05040100u);
+      v.y = __builtin_amdgcn_perm(a.w, a.z, 0x05040100u);
+      v.z = __builtin_amdgcn_perm(b.y, b.x, 0x05040100u);
+      v.w = __builtin_amdgcn_perm(b.w, b.z, 0x05040100u);
+    }
     if (gr < P && gc < P)
       st_stream(reinterpret_cast<float4*>(y2h + (((int64_t)x.b * P + gr) * P + gc) * 32 + c8 * 8),
                 __builtin_bit_cast(float4, v));
@@ -308,7 +338,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   const bool neg = gamma != nullptr && gamma[16 * NT + li] < 0.f;
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
-  float s_acc = 0.f, q_acc = 0.f;
+  f2v s_acc = {0.f, 0.f}, q_acc = {0.f, 0.f};
   uint32_t ymx = 0u;
   f32x4 acc[4];
   F2Tile prev{0, 0, 0};
@@ -341,20 +371,21 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     f2_store<DIAG>(smem + F2_OFF_S + ((kk - 1) & 1) * F2_STAGE, prev, y2, P);
     f2_store_ya(ys + ((kk - 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
   }
-  // max |y2| of channel 16NT + li over the 4 lane groups (then the two waves of this co half)
+  // max |acc| of channel 16NT + li over the 4 lane groups (then the two waves of this co half)
   ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 16, 64));
   ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 32, 64));
   // BN2 partials: reduce the 4 lane groups, then the two row-halves of this co half
-  s_acc += __shfl_xor(s_acc, 16, 64);
-  s_acc += __shfl_xor(s_acc, 32, 64);
-  q_acc += __shfl_xor(q_acc, 16, 64);
-  q_acc += __shfl_xor(q_acc, 32, 64);
+  float s_sum = s_acc.x + s_acc.y, q_sum = q_acc.x + q_acc.y;
+  s_sum += __shfl_xor(s_sum, 16, 64);
+  s_sum += __shfl_xor(s_sum, 32, 64);
+  q_sum += __shfl_xor(q_sum, 16, 64);
+  q_sum += __shfl_xor(q_sum, 32, 64);
   __syncthreads();  // all operand reads done: reuse the LDS for the reduction
   double* red = reinterpret_cast<double*>(smem);                   // [4 waves][16 co][2]
   uint32_t* yred = reinterpret_cast<uint32_t*>(smem + 4 * 16 * 2 * 8);  // [4 waves][16 co]
   if (lane < 16) {
-    red[(WV * 16 + li) * 2 + 0] = (double)s_acc;
-    red[(WV * 16 + li) * 2 + 1] = (double)q_acc;
+    red[(WV * 16 + li) * 2 + 0] = (double)s_sum;
+    red[(WV * 16 + li) * 2 + 1] = (double)q_sum;
     yred[WV * 16 + li] = ymx;
   }
   __syncthreads();
@@ -363,14 +394,17 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     // waves with this co half: nt (rows 0-3) and nt + 2 (rows 4-7)
     const double v = (red[(nt * 16 + c16) * 2 + k] + red[((nt + 2) * 16 + c16) * 2 + k]) * (k ? (double)inv * inv : inv);
     partial[((int64_t)co * gridDim.x + blockIdx.x) * 2 + k] = v;
-    // this workgroup's max |y2| per channel: a plain store per (channel, workgroup), reduced by
+    // this workgroup's max |y2 - b2| per channel: a plain store per (channel, workgroup), reduced by
     // the BN2-backward finalize (no same-address atomics: 16 K of them cost ~40 us in the head)
-    if (ypart != nullptr && k == 0) ypart[co * gridDim.x + blockIdx.x] = max(yred[nt * 16 + c16], yred[(nt + 2) * 16 + c16]);
+    // (max |acc| * inv = max |y2 - b2|: inv is a power of two, the order and the NaN survive)
+    if (ypart != nullptr && k == 0)
+      ypart[co * gridDim.x + blockIdx.x] =
+          __float_as_uint(__uint_as_float(max(yred[nt * 16 + c16], yred[(nt + 2) * 16 + c16])) * inv);
   }
 }
 
 template <int DIAG>
-__global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* __restrict__ p1,
+__global__ __launch_bounds__(F2_THREADS, TDS_F2_WG) void conv2_fwd2_kernel(const uint4* __restrict__ p1,
                                                                    const uint4* __restrict__ wpack,
                                                                    const float* __restrict__ bias,
                                                                    const float* __restrict__ gamma,
@@ -392,8 +426,8 @@ __global__ __launch_bounds__(F2_THREADS, 2) void conv2_fwd2_kernel(const uint4* 
 
 using namespace tds;
 
-// workgroups the forward launches (BN2 partial rows): 2 per CU
-int tds_conv2_fwd2_num_wg() { return 2 * tds_conv2_num_wg(); }
+// workgroups the forward launches (BN2 partial rows): TDS_F2_WG per CU
+int tds_conv2_fwd2_num_wg() { return TDS_F2_WG * tds_conv2_num_wg(); }
 
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c) {
   *tiles_r = (P + F2_TH - 1) / F2_TH;

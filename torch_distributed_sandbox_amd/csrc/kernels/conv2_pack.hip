@@ -7,7 +7,7 @@
 // Activation formats (produced/consumed by convnet_fused.hip and the conv2 kernels):
 //   p1  [B][P][P][16] fp16                                          (pooled layer-1 output)
 //   y2h [B][P][P][32] fp16                        (conv2 output: bias-free, scaled; conv2_common.h)
-//   dp1 [B][P][P][16] fp32                                          (grad wrt p1)
+//   dp1h [B][P][ceil(P/4)][16][4] fp16           (grad wrt p1: scaled, dgrad-MFMA layout; conv2_common.h)
 // MFMA mapping (v_mfma_f32_16x16x32_f16, lane l: i = l&15, g = l>>4):
 //   A[i][k = 8g+j] (8 consecutive k per lane), B[k = 8g+j][n = i], C row = 4g+r, col = i.
 #include <vector>
@@ -89,11 +89,37 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
         (void)frexpf(L, &x);  // L < 2^x
         ky = min(100, max(-100, -x));
       }
+      // the dp1h store factor 2^kd (conv2_common.h): Ld = max_ci sum_{co,tap} |w| (16 lanes per ci,
+      // co = lane and lane + 16, fixed order), 1.01 * 2^15 * Ld * 2^ew * 2^kd <= 65504
+      __syncthreads();  // red[8..] read above
+      {
+        const int ci = threadIdx.x >> 4, j = threadIdx.x & 15;
+        float ld = 0.f;
+        for (int co = j; co < 32; co += 16)
+          for (int tp = 0; tp < 25; ++tp) ld += fabsf(w2[(co * 16 + ci) * 25 + tp]);
+        ld += __shfl_xor(ld, 1, 64);
+        ld += __shfl_xor(ld, 2, 64);
+        ld += __shfl_xor(ld, 4, 64);
+        ld += __shfl_xor(ld, 8, 64);
+        ld = wave_max(ld);
+        if ((threadIdx.x & 63) == 0) red[8 + (threadIdx.x >> 6)] = ld;
+      }
+      __syncthreads();
+      float Ld = red[8];
+      for (int i = 1; i < (int)(blockDim.x >> 6); ++i) Ld = fmaxf(Ld, red[8 + i]);
+      Ld *= 1.01f * 32768.f / 65504.f * wsc;
+      int kd = 0;
+      if (Ld > 0.f && __builtin_isfinite(Ld)) {
+        int x;
+        (void)frexpf(Ld, &x);  // Ld < 2^x
+        kd = min(100, max(-100, -x));
+      }
       if (threadIdx.x < 33) mag[threadIdx.x] = 0u;
       if (threadIdx.x == 0) {
         mag[kMagScales] = __float_as_uint(ldexpf(1.f, -ew));
         mag[kMagScales + 1] = __float_as_uint(p1_scale != nullptr ? 1.f / p1_scale[0] : 1.f);
         mag[kMagScales + 2] = __float_as_uint(ldexpf(1.f, ky));
+        mag[kMagScales + 3] = __float_as_uint(ldexpf(1.f, kd));
       }
     }
   }

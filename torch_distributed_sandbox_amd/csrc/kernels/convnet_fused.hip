@@ -27,6 +27,9 @@
 
 namespace tds {
 
+// zero source of the layer-1 kernels' out-of-range prefetch lanes
+__device__ __attribute__((aligned(16))) uint4 g_l1b_zero = {0u, 0u, 0u, 0u};
+
 // ============================================================================ layer 1 conv
 constexpr int L1_TR = 16;           // conv1 output rows per tile
 constexpr int L1_TC = 64;           // conv1 output cols per tile
@@ -112,25 +115,25 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
   constexpr int NV = L1_XR * 18;
   constexpr int PER = (NV + 255) / 256;
   float4 pre[PER];
+  // unconditional loads (out-of-range lanes read a zero vector): a load under a per-lane branch
+  // is waited for before the branches merge (conv2_bwd.hip, l1_bwd_mfma_kernel)
   auto load_tile = [&](int t) {
     const int b = t / per_img, rem = t - b * per_img;
     const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
-    const float* xb = LV ? nullptr : x + (int64_t)b * H * W;
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = tid + 256 * u;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e < NV) {
-        const int rr = e / 18, cv = e - rr * 18;
-        const int gr = r0 - 2 + rr, gc = c0 - 4 + 4 * cv;
-        if (gr >= 0 && gr < H && gc >= 0 && gc < W) {
-          if constexpr (LV)  // 4 levels in .x
-            v.x = __uint_as_float(*reinterpret_cast<const uint32_t*>(xl + (int64_t)b * H * W + (int64_t)gr * W + gc));
-          else
-            v = *reinterpret_cast<const float4*>(xb + (int64_t)gr * W + gc);
-        }
+      const int rr = e / 18, cv = e - rr * 18;
+      const int gr = r0 - 2 + rr, gc = c0 - 4 + 4 * cv;
+      const bool ok = (e < NV) & ((uint32_t)gr < (uint32_t)H) & ((uint32_t)gc < (uint32_t)W);
+      const int64_t o = ((int64_t)b * H + gr) * W + gc;
+      if constexpr (LV) {  // 4 levels in .x
+        const uint32_t* src = ok ? reinterpret_cast<const uint32_t*>(xl + o) : &g_l1b_zero.x;
+        pre[u] = make_float4(__uint_as_float(*src), 0.f, 0.f, 0.f);
+      } else {
+        const float4* src = ok ? reinterpret_cast<const float4*>(x + o) : reinterpret_cast<const float4*>(&g_l1b_zero);
+        pre[u] = *src;
       }
-      pre[u] = v;
     }
   };
   int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -140,6 +143,8 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
     const int r0 = (rem / tiles_c) * L1_TR, c0 = (rem % tiles_c) * L1_TC;
     __syncthreads();
     bool nonfinite = false;
+#pragma unroll
+    for (int u = 0; u < PER; ++u) asm volatile("" ::"v"(pre[u].x), "v"(pre[u].y), "v"(pre[u].z), "v"(pre[u].w));
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = tid + 256 * u;
@@ -169,7 +174,9 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
     }
     // a non-finite x anywhere in the tile (or a degenerate BN1 affine) sends the whole tile to
     // the general epilogue (torch's NaN rules); otherwise no window can hold a NaN
-    const bool slow = __syncthreads_or(nonfinite) != 0 || !fast_ok;
+    // (wave-uniform in an SGPR: as a per-lane bool the compiler computed both epilogues below
+    // and selected, ~40 % more VALU per window)
+    const bool slow = __builtin_amdgcn_readfirstlane((__syncthreads_or(nonfinite) != 0 || !fast_ok) ? 1 : 0) != 0;
     if (t + (int)gridDim.x < total) load_tile(t + gridDim.x);
 #pragma unroll
     for (int rp = 0; rp < 2; ++rp) {
@@ -211,33 +218,34 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
         const int pcol = (c0 >> 1) + 16 * sp + li;
         float pv[4];
         uint32_t ixw = 0;
+        // scan order: (row 0, col 0), (row 0, col 1), (row 1, col 0), (row 1, col 1)
+        if (!slow) {  // every z finite (tile-uniform)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          // scan order: (row 0, col 0), (row 0, col 1), (row 1, col 0), (row 1, col 1)
-          const float z0 = fmaf(ea[r], acc[0][0][r], ebb[r]), z1 = fmaf(ea[r], acc[0][1][r], ebb[r]);
-          const float z2 = fmaf(ea[r], acc[1][0][r], ebb[r]), z3 = fmaf(ea[r], acc[1][1][r], ebb[r]);
-          float m;
-          uint32_t am;
-          if (!slow) {  // every z finite (tile-uniform)
-            m = fmaxf(fmaxf(z0, z1), fmaxf(z2, z3));
-            am = z0 == m ? 0u : z1 == m ? 1u : z2 == m ? 2u : 3u;  // first max
-          } else {      // torch's rule: update when (v > max || isnan(v)), relu(NaN) = NaN
-            m = z0;
-            am = 0;
+          for (int r = 0; r < 4; ++r) {
+            const float z0 = fmaf(ea[r], acc[0][0][r], ebb[r]), z1 = fmaf(ea[r], acc[0][1][r], ebb[r]);
+            const float z2 = fmaf(ea[r], acc[1][0][r], ebb[r]), z3 = fmaf(ea[r], acc[1][1][r], ebb[r]);
+            const float m = fmaxf(fmaxf(z0, z1), fmaxf(z2, z3));
+            const uint32_t am = z0 == m ? 0u : z1 == m ? 1u : z2 == m ? 2u : 3u;  // first max
+            pv[r] = fmaxf(m, 0.f);
+            ixw |= (am | (m > 0.f ? 4u : 0u)) << (8 * r);
+          }
+        } else {  // torch's rule: update when (v > max || isnan(v)), relu(NaN) = NaN
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float z0 = fmaf(ea[r], acc[0][0][r], ebb[r]), z1 = fmaf(ea[r], acc[0][1][r], ebb[r]);
+            const float z2 = fmaf(ea[r], acc[1][0][r], ebb[r]), z3 = fmaf(ea[r], acc[1][1][r], ebb[r]);
+            float m = z0;
+            uint32_t am = 0;
             if (z1 > m || isnan(z1)) { m = z1; am = 1; }
             if (z2 > m || isnan(z2)) { m = z2; am = 2; }
             if (z3 > m || isnan(z3)) { m = z3; am = 3; }
+            pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
+            ixw |= (am | (m > 0.f ? 4u : 0u)) << (8 * r);
           }
-          pv[r] = m > 0.f ? m : (isnan(m) ? m : 0.f);
-          ixw |= (am | (m > 0.f ? 4u : 0u)) << (8 * r);
         }
         // p1 is conv2's single fp16 operand (bf16x3.h, fp16x2): one rounding, 32-B records
         const uint32_t h01 = cvt2_f16(pv[0], pv[1]), h23 = cvt2_f16(pv[2], pv[3]);
-#if defined(TDS_L1_EXP) && TDS_L1_EXP == 1
-        if (prow < P && pcol < PW && pv[0] == 1234.5f) {
-#else
         if (prow < P && pcol < PW) {
-#endif
           const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
           uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 2);  // 32-B record: fp16[16]
           st_stream(dst + g, make_uint2(h01, h23));
@@ -386,26 +394,21 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __r
 }
 
 
-// zero source of the layer-1 backward's out-of-range prefetch lanes
-__device__ __attribute__((aligned(16))) uint4 g_l1b_zero = {0u, 0u, 0u, 0u};
-
 // layer-1 backward tile: 8 pooled rows x 32 pooled columns (x tile 20 rows incl. the halo)
 constexpr int LB_PR = 8, LB_PC = 32;
 constexpr int LB_XR = 2 * LB_PR + 4;
 constexpr int LB_XS = 76;  // LDS x row stride (floats); column 0 <-> global column 2*pc0 - 4
 constexpr int LB_NACC = 27;
 constexpr int LB_NP = LB_PR * LB_PC;                     // pooled pixels per tile
-constexpr int LB_V_DP = LB_NP * 4, LB_V_PH = 0, LB_V_ID = LB_NP, LB_V_X = LB_XR * 18;
+// dp1h (conv2_common.h: [B][P][ceil(P/4)][16][4] fp16): a tile row is 8 column groups x 128 B
+constexpr int LB_V_DP = LB_NP * 2, LB_V_PH = 0, LB_V_ID = LB_NP, LB_V_X = LB_XR * 18;
 constexpr int LB_V = LB_V_DP + LB_V_PH + LB_V_ID + LB_V_X;  // 16-B vectors staged per tile
 // The argmax byte carries the ReLU mask in bit 2 (set by l1_conv: pooled max > 0), so the
 // backward never reads p1 (720 MB of 64-B hi|lo records at the bench shape).
 constexpr int LB_PER = (LB_V + 255) / 256;
 static_assert(LB_V_PH == 0 && LB_V_DP % 256 == 0 && LB_V_ID % 256 == 0, "l1_bwd prefetch classes per vector");
-// LDS record of pooled pixel pp's 16 dp1 values: lane groups g0 / g1 (and g2 / g3) read pooled pixels
-// two apart, whose plain records (16 words) sit 32 words apart -- the same banks, a 2-way conflict
-// on every dp1 read.  Swapping the records of pp = 2, 3 (mod 4) puts the pair in opposite halves.
-template <bool SW>
-__device__ __forceinline__ int lb_dp_rec(int pp) { return SW ? pp ^ ((pp >> 1) & 1) : pp; }
+// fp16 bits (low half) -> float
+__device__ __forceinline__ float lb_f16(uint32_t h) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(h & 0xFFFFu)); }
 __device__ __forceinline__ void lb_store4(uint32_t* p, const uint4& v) {
   p[0] = v.x;
   p[1] = v.y;
@@ -430,9 +433,7 @@ __device__ __forceinline__ void lb_store4(uint32_t* p, const uint4& v) {
 // (80 put rows ky and ky + 2 on the same banks: 2-way on every read).  The sum-dz lanes (n = 25) read
 // the ones block at LM_ONES past the K-step base, a bank no data lane of that read touches; the pad
 // lanes (n = 26..31, outputs discarded) read tap 24's address (a broadcast).  tools/micro/
-// l1b_lds_check.py emulates both layouts' reads.  (The dp1 record swap lb_dp_rec stays PAIRS-only:
-// in the word layout it raises the kernel from 124 to 148 VGPRs, 3 workgroups per CU instead of 4,
-// for ~10 % of the LDS cycles.)
+// l1b_lds_check.py emulates both layouts' reads.
 constexpr int LM_XS = 137;
 constexpr int LM_ONES = LM_XS + 80;
 static_assert(LM_XS % 32 == 9 && 80 + 3 * 16 + 3 < LM_XS && 1 + 2 * 7 + 1 < LB_XR, "l1_bwd ones block");
@@ -458,23 +459,23 @@ constexpr int LM_X_BYTES = (LB_XR * LM_XS > LV_WORDS ? LB_XR * LM_XS : LV_WORDS)
 #define TDS_L1B_WAVES 3
 #endif
 // PAIRS (level input only; TDS_L1B_PAIRS=1 at run time, fused_ops.cpp): the conflict-free bf16-pair
-// x tile and the swizzled dp1 records below.  Opt-in until timed on MI355X: it compiles to 144
-// VGPRs under the default budget (3 workgroups per CU: run it with TDS_L1B_PER_CU=3) and spills a
-// few dwords at 128.
+// x tile above.  Opt-in: timed slower than the default word layout (docs/KERNELS.md).
 template <bool LV, bool PAIRS>
-__global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const float* __restrict__ dp1,
+__global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const uint4* __restrict__ dp1,
+                                                          const uint32_t* __restrict__ dp1_dec,
                                                           const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
                                                           double* __restrict__ partial, int B, int H, int W) {
   __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LM_X_BYTES];
-  float* dps = reinterpret_cast<float*>(lds);
+  const uint32_t* dps = reinterpret_cast<const uint32_t*>(lds);  // dp1h tile [row 8][group 8][ch 16][px 4] fp16
   unsigned short* phs = nullptr;
   uint8_t* ids = reinterpret_cast<uint8_t*>(lds + LB_NP * 64);
   uint32_t* xs = reinterpret_cast<uint32_t*>(lds + LB_NP * 80);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
-  const int P = H / 2, PW = W / 2;
+  const int P = H / 2, PW = W / 2, PG = (PW + 3) >> 2;
   const int tiles_c = (PW + LB_PC - 1) / LB_PC, tiles_r = (P + LB_PR - 1) / LB_PR;
   const int per_img = tiles_c * tiles_r, total = per_img * B;
+  const double dec = (double)__uint_as_float(dp1_dec[0]);
 
   // K ordering of a K-step (2 rows x 16 columns = 8 pooling windows): k = 4*w + 2*dr + dc, so
   // lane group g holds windows 2g, 2g+1 whole -- dz1 of a window is one pooled value placed
@@ -518,11 +519,10 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
 #pragma unroll
     for (int u = 0; u < LB_PER; ++u) {
       const int e = tid + 256 * u;
-      if (256 * u < LB_V_DP) {
-        const int pp = e >> 2, q = e & 3;
-        const int gpr = pr0 + pp / LB_PC, gpc = pc0 + pp % LB_PC;
-        const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
-        const uint4* src = (gpr < P) & (gpc < PW) ? reinterpret_cast<const uint4*>(dp1) + rec * 4 + q : &g_l1b_zero;
+      if (256 * u < LB_V_DP) {  // dp1h: 64 vectors per tile row (8 column groups x 8)
+        const int gpr = pr0 + (e >> 6), cg = (pc0 >> 2) + ((e >> 3) & 7);
+        const int64_t rec = ((int64_t)b * P + gpr) * PG + cg;
+        const uint4* src = (gpr < P) & (cg < PG) ? dp1 + rec * 8 + (e & 7) : &g_l1b_zero;
         pre[u] = *src;
       } else if (256 * u < LB_V_DP + LB_V_ID) {
         const int pp = e - LB_V_DP;
@@ -555,7 +555,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
 #pragma unroll
     for (int u = 0; u < LB_PER; ++u) {
       int e = tid + 256 * u;
-      if (e < LB_V_DP) reinterpret_cast<uint4*>(dps)[(lb_dp_rec<PAIRS>(e >> 2) << 2) | (e & 3)] = pre[u];
+      if (e < LB_V_DP) reinterpret_cast<uint4*>(lds)[e] = pre[u];
       else if (e < LB_V_DP + LB_V_PH) reinterpret_cast<uint4*>(phs)[e - LB_V_DP] = pre[u];
       else if (e < LB_V_DP + LB_V_PH + LB_V_ID) reinterpret_cast<uint4*>(ids)[e - LB_V_DP - LB_V_PH] = pre[u];
       else if (e < LB_V) {
@@ -622,10 +622,13 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
         {
           uint32_t* hp = reinterpret_cast<uint32_t*>(&ah);
           uint32_t* lp = reinterpret_cast<uint32_t*>(&al);
+          // pooled columns 8sg + 2g + {0, 1}: column group 2sg + (g >> 1), pixels 2(g & 1) + {0, 1} --
+          // one dword (a 32-lane half reads 32 consecutive words: conflict-free)
+          const uint32_t dpair = dps[((rp * 8 + 2 * sg + (g >> 1)) * 16 + li) * 2 + (g & 1)];
 #pragma unroll
           for (int wi = 0; wi < 2; ++wi) {
             const int pp = rp * LB_PC + 8 * sg + 2 * g + wi;
-            const float dp = dps[lb_dp_rec<PAIRS>(pp) * 16 + li];
+            const float dp = lb_f16(dpair >> (16 * wi));
             const uint32_t ab = ids[pp * 16 + li];
             const float d = (ab & 4u) ? dp : 0.f;  // ReLU: a pooled value <= 0 blocks the gradient
             uint32_t h, l;
@@ -694,8 +697,9 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       double* o = red + (wv * 16 + 4 * g + r) * LB_NACC;
-      if (n < 25) o[2 + n] = LV ? dacc[blk][r] * (double)L1_LEVEL_SCALE : dacc[blk][r];
-      else if (n == 25) o[0] = dacc[blk][r];
+      // (dec: dp1h's decode, a power of two)
+      if (n < 25) o[2 + n] = LV ? dacc[blk][r] * ((double)L1_LEVEL_SCALE * dec) : dacc[blk][r] * dec;
+      else if (n == 25) o[0] = dacc[blk][r] * dec;
       else if (n == 26) o[1] = 0.0;
     }
   }
@@ -969,18 +973,20 @@ void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, c
 
 int tds_l1_bwd_rows(int nwg) { return nwg; }
 
-void tds_l1_bwd(const void* x, bool levels, bool pairs, const float* dp1, const void* p1, const uint8_t* idx1,
-                const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st) {
+void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
+                const uint8_t* idx1, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
+                hipStream_t st) {
   (void)w1;
   (void)b1;
+  const uint4* d = static_cast<const uint4*>(dp1h);
   if (levels && pairs)
-    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, true>), dim3(nwg), dim3(256), 0, st, x, dp1,
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, true>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
                        reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   else if (levels)
-    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, false>), dim3(nwg), dim3(256), 0, st, x, dp1,
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, false>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
                        reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   else
-    hipLaunchKernelGGL((l1_bwd_mfma_kernel<false, false>), dim3(nwg), dim3(256), 0, st, x, dp1,
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<false, false>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
                        reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   TDS_LAUNCH_CHECK();
 }

@@ -40,10 +40,6 @@ namespace tds {
 constexpr int HP_THREADS = 256;
 constexpr int HP_BAND = 4;                  // block rows per workgroup
 constexpr int HP_MAXB = 8;                  // images per pass (larger batches run in passes)
-#ifndef TDS_HP_PF
-#define TDS_HP_PF 1
-#endif
-constexpr bool HP_PF = TDS_HP_PF != 0;      // register prefetch of the next chunk
 
 struct HPGrid {
   int nband;
@@ -195,15 +191,16 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
   // iteration i: block row R0 + i / nch, chunk (32 blocks) i % nch of the row
   const int nch = (g.Q8 + 31) / 32;
   const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
-  HPLoad<NB> cur, nxt;
-  if (HP_PF && nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
-#pragma unroll 1
-  for (int i = 0; i < nit; ++i) {
+  // two load sets in alternation (no register copy): chunk i+1's loads are issued, into the other
+  // set, before chunk i is consumed, on every path (past the end: the last chunk again, unused)
+  HPLoad<NB> ld0, ld1;
+  auto issue = [&](HPLoad<NB>& L, int i) {
+    const int ii = i < nit ? i : nit - 1;
+    L.issue(ya, W, g, HPThread(ii % nch), c, R0 + ii / nch, b0, NC);
+  };
+  auto body = [&](HPLoad<NB>& cur, int i) {
     const int R = R0 + i / nch;
     const HPThread th(i % nch);
-    if (!HP_PF) cur.issue(ya, W, g, th, c, R, b0, NC);
-    if (HP_PF && i + 1 < nit)  // next chunk in flight
-      nxt.issue(ya, W, g, HPThread((i + 1) % nch), c, R0 + (i + 1) / nch, b0, NC);
     cur.fix(NC);
     const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
     const bool rok = th.blk < g.Q8 && py < Q;
@@ -232,7 +229,14 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
       for (int b = 0; b < NB; ++b)
         acc[b][j] = fmaf(x[b][0], w4.x, fmaf(x[b][1], w4.y, fmaf(x[b][2], w4.z, fmaf(x[b][3], w4.w, acc[b][j]))));
     }
-    if (HP_PF) cur = nxt;
+  };
+  if (nit > 0) issue(ld0, 0);
+#pragma unroll 1
+  for (int i = 0; i < nit; i += 2) {
+    issue(ld1, i + 1);
+    body(ld0, i);
+    issue(ld0, i + 2);
+    if (i + 1 < nit) body(ld1, i + 1);
   }
   // deterministic workgroup reduction: waves (DPP), then 4 wave partials in fixed order
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -303,15 +307,15 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   uint32_t gmx = 0u;  // max |g2m| bits
   const int nch = (g.Q8 + 31) / 32;
   const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
-  HPLoad<NB> cur, nxt;
-  if (HP_PF && nit > 0) cur.issue(ya, W, g, HPThread(0), c, R0, b0, NC);
-#pragma unroll 1
-  for (int i = 0; i < nit; ++i) {
+  // two load sets in alternation, as in the forward
+  HPLoad<NB> ld0, ld1;
+  auto issue = [&](HPLoad<NB>& L, int i) {
+    const int ii = i < nit ? i : nit - 1;
+    L.issue(ya, W, g, HPThread(ii % nch), c, R0 + ii / nch, b0, NC);
+  };
+  auto body = [&](HPLoad<NB>& cur, int i) {
     const int R = R0 + i / nch;
     const HPThread th(i % nch);
-    if (!HP_PF) cur.issue(ya, W, g, th, c, R, b0, NC);
-    if (HP_PF && i + 1 < nit)  // next chunk in flight
-      nxt.issue(ya, W, g, HPThread((i + 1) % nch), c, R0 + (i + 1) / nch, b0, NC);
     cur.fix(NC);
     const bool bok = th.blk < g.Q8;
     const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
@@ -374,7 +378,14 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
         }
       }
     }
-    if (HP_PF) cur = nxt;
+  };
+  if (nit > 0) issue(ld0, 0);
+#pragma unroll 1
+  for (int i = 0; i < nit; i += 2) {
+    issue(ld1, i + 1);
+    body(ld0, i);
+    issue(ld0, i + 2);
+    if (i + 1 < nit) body(ld1, i + 1);
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   gmx = wave_max(gmx);

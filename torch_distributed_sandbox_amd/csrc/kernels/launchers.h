@@ -85,7 +85,7 @@ int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
 // y2h [B,P,P,32] fp16 (conv2_common.h); ya pooled-blocked (pooled_layout.h), max/min of each 2x2
 // window of y2 by sign(gamma2)
-// ypart (optional): max |y2| per (channel, workgroup), [32][nwg] float bits
+// ypart (optional): max |y2 - b2| per (channel, workgroup), [32][nwg] float bits
 // scales (optional): mag + kMagScales (conv2_pack.hip), the packed weights' and p1's inverse scales
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
                     double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
@@ -95,8 +95,9 @@ void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups
 // mag: the forward's / head backward's magnitude bounds (the fp16 scale of dy2) and the y2h
 // decode (conv2_common.h); b2: conv2.bias (y2h is bias-free)
+// dp1h [B][P][ceil(P/4)][16][4] fp16 (conv2_common.h); its decode factor goes to mag[kMagScales + 4]
 void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
-                    const uint32_t* mag, const void* p1, const short* wd, float* dp1, float* slab, const int* walk,
+                    uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st);
 // host: per-workgroup tile lists of vertical segments of ~seg tiles; out == nullptr -> length
 int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, int seg);
@@ -133,8 +134,10 @@ void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n,
                             float momentum, const float* gamma, const float* beta, float* stats, float* running_mean,
                             float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
-void tds_l1_bwd(const void* x, bool levels, bool pairs, const float* dp1, const void* p1, const uint8_t* idx1,
-                const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W, hipStream_t st);
+// dp1h: the conv2 backward's (conv2_common.h), dp1_dec: its decode factor (float bits, device)
+void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
+                const uint8_t* idx1, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
+                hipStream_t st);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);

@@ -130,10 +130,10 @@ def _zero_scalar(device, dtype):
 
 
 class _Layer1Link:
-    """Carries the conv2 backward's fp32 dp1 to the layer-1 backward (p1 itself is fp16), and the
-    power-of-two scale p1 is stored at to the conv2 kernels."""
+    """Carries the conv2 backward's dp1h (fp16, scaled: csrc/kernels/conv2_common.h) and its decode
+    factor to the layer-1 backward, and the power-of-two scale p1 is stored at to the conv2 kernels."""
 
-    __slots__ = ("dp1", "p1_scale")
+    __slots__ = ("dp1", "dp1_dec", "p1_scale")
 
 
 class _Layer1(torch.autograd.Function):
@@ -154,10 +154,11 @@ class _Layer1(torch.autograd.Function):
     @staticmethod
     def backward(ctx, _dp1_placeholder):
         x, p1, idx1, w1, b1, g1, stats1, gram = ctx.saved_tensors
-        dp1 = ctx.link1.dp1
-        ctx.link1.dp1 = None
+        dp1, dp1_dec = ctx.link1.dp1, ctx.link1.dp1_dec
+        ctx.link1.dp1 = ctx.link1.dp1_dec = None
         outs = _sinks(ctx, ctx.params, 1)
-        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1, x, p1, idx1, w1, b1, g1, stats1, gram, 1.0, *outs)
+        dw1, db1, dg1, dbe1 = _ext.ops().fused_l1_backward(dp1, dp1_dec, x, p1, idx1, w1, b1, g1, stats1, gram, 1.0,
+                                                           *outs)
         return None, dw1, db1, dg1, dbe1, None, None, None, None, None, None
 
 
@@ -174,7 +175,7 @@ class _Conv2(torch.autograd.Function):
     @staticmethod
     def forward(ctx, p1, w2, b2, g2, link, link1):
         ops = _ext.ops()
-        # magnitude bounds of this step (per-workgroup max |y2| here, max |g2m| in the head
+        # magnitude bounds of this step (per-workgroup max |y2 - b2| here, max |g2m| in the head
         # backward, reduced by its BN2 finalize): the conv2 backward's fp16 scale of dy2
         link.mag = torch.empty(ops.mag_numel(p1.shape[0], p1.shape[1]), device=p1.device, dtype=torch.int32)
         wp, wd = ops.conv2_pack(w2.contiguous(), link.mag, getattr(link1, "p1_scale", None))
@@ -196,10 +197,12 @@ class _Conv2(torch.autograd.Function):
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
         dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, ctx.params[1], link.mag,
                                                            p1, wd, 1.0, *_sinks(ctx, ctx.params, 1))
+        mag = link.mag
         link.g2m = link.kbuf = link.aff2 = link.mag = None
         dp1_ph = None
         if ctx.needs_input_grad[0]:
-            ctx.link1.dp1 = dp1
+            # dp1h (fp16, scaled) and its decode factor, which the conv2 backward wrote into mag
+            ctx.link1.dp1, ctx.link1.dp1_dec = dp1, mag[44:45]
             dp1_ph = _zero_scalar(p1.device, p1.dtype).expand(p1.shape)
         return dp1_ph, dw2, db2, None, None, None
 
