@@ -40,11 +40,11 @@ constexpr int F2_THREADS = 256;
 constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records (1 KiB)
 constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records of 32 B, 240 used)
 constexpr int F2_PBUF = F2_PPLANE;                     // one fp16 plane
-// TDS_F2_WG: workgroups per CU.  2: the staged tile holds one dword per value (the y2h bits), 60 KiB
-// of LDS; 3 (A/B variant): the staged tile holds the y2h halves themselves (channel pairs joined by
-// one DPP move), 44 KiB, and the kernel is cut to 168 VGPRs
+// TDS_F2_WG: workgroups per CU.  3 (default): the staged tile holds the y2h halves themselves
+// (channel pairs joined by one DPP move), 44 KiB of LDS, 168 VGPRs -- 0.427 -> 0.407 ms isolated,
+// bench 2.443 -> 2.406 ms (tools/gpu_sessions/r4_s22.sh); 2: one dword per value, 60 KiB
 #ifndef TDS_F2_WG
-#define TDS_F2_WG 2
+#define TDS_F2_WG 3
 #endif
 constexpr bool F2_H16 = TDS_F2_WG == 3;
 constexpr int F2_PXREC = F2_H16 ? 32 * 2 + 16 : 32 * 4 + 16;  // staged pixel record: 32 co + 16 B pad (banks)

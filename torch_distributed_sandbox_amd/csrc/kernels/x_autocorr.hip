@@ -193,17 +193,21 @@ __global__ __launch_bounds__(256, 3) void x_autocorr_u8_kernel(const uint8_t* __
     constexpr uint32_t kOob = 0xFFFFFFF0u;
     const uint32_t base = (uint32_t)((int64_t)(b - b0) * img + c);
     const bool has_l = c >= 4, has_r = c + 4 < W;
+    // (offsets made out of range by OR-ing the high bits: no short-circuit branch, whose merges
+    // made the compiler wait for each row's loads at once)
     auto ld_row = [&](int r, uint32_t (&row)[3]) {
       const uint32_t o = base + (uint32_t)r * (uint32_t)W;
-      const bool in = r < H;
-      row[0] = __builtin_amdgcn_raw_buffer_load_b32(rx, in && has_l ? o - 4 : kOob, 0, 0);
-      row[1] = __builtin_amdgcn_raw_buffer_load_b32(rx, in ? o : kOob, 0, 0);
-      row[2] = __builtin_amdgcn_raw_buffer_load_b32(rx, in && has_r ? o + 4 : kOob, 0, 0);
+      const uint32_t oob = r < H ? 0u : kOob;
+      row[0] = __builtin_amdgcn_raw_buffer_load_b32(rx, (o - 4) | oob | (has_l ? 0u : kOob), 0, 0);
+      row[1] = __builtin_amdgcn_raw_buffer_load_b32(rx, o | oob, 0, 0);
+      row[2] = __builtin_amdgcn_raw_buffer_load_b32(rx, (o + 4) | oob | (has_r ? 0u : kOob), 0, 0);
     };
     // bytes s .. s+3 of a row's 12 (s = 4 + dx in 0..8)
     auto win = [](const uint32_t (&row)[3], int s) -> uint32_t {
       return (s & 3) == 0 ? row[s >> 2] : __builtin_amdgcn_alignbyte(row[(s >> 2) + 1], row[s >> 2], s & 3);
     };
+    // (fully unrolled, every row's loads can issue early: measured no faster, 73 vs 70 us in the
+    // step, tools/gpu_sessions/r4_s23.sh -- kept rolled)
     uint32_t w[5][3], nx[3];
 #pragma unroll
     for (int i = 0; i < 5; ++i) ld_row(r0 + i, w[i]);
