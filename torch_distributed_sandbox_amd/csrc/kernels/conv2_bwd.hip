@@ -824,7 +824,10 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
   const int64_t tbase = ntail / nwg, textra = ntail % nwg;
   int64_t maxlen = 0;
   for (int w = 0; w < nwg; ++w) maxlen = std::max(maxlen, len[w] + tbase + (w < textra ? 1 : 0));
-  const int64_t rows = maxlen + 3;
+  // + 4 end-marked entries: the staging's look-ahead reads tile k + 4 at the last iteration of a
+  // list of length k + 1 (br_stage: both load sets are issued on every path) -- with + 3 the longest
+  // list's last read ran one past its row (the next list, or past the table for the last one)
+  const int64_t rows = maxlen + 4;
   if (rows * nwg >= ((int64_t)1 << 31)) return -1;  // the kernel indexes it in 32 bits
   if (out == nullptr) return rows * nwg;
   std::vector<int64_t> fill(nwg, 0);

@@ -222,8 +222,12 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
         if (!slow) {  // every z finite (tile-uniform)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float z0 = fmaf(ea[r], acc[0][0][r], ebb[r]), z1 = fmaf(ea[r], acc[0][1][r], ebb[r]);
-            const float z2 = fmaf(ea[r], acc[1][0][r], ebb[r]), z3 = fmaf(ea[r], acc[1][1][r], ebb[r]);
+            // the affine in packed fp32 (v_pk_fma_f32: two window pixels per instruction; this
+            // epilogue, not the MFMAs, bounds the kernel)
+            const f32x2 ea2 = {ea[r], ea[r]}, eb2 = {ebb[r], ebb[r]};
+            const f32x2 zt = __builtin_elementwise_fma(f32x2{acc[0][0][r], acc[0][1][r]}, ea2, eb2);
+            const f32x2 zb = __builtin_elementwise_fma(f32x2{acc[1][0][r], acc[1][1][r]}, ea2, eb2);
+            const float z0 = zt.x, z1 = zt.y, z2 = zb.x, z3 = zb.y;
             const float m = fmaxf(fmaxf(z0, z1), fmaxf(z2, z3));
             const uint32_t am = z0 == m ? 0u : z1 == m ? 1u : z2 == m ? 2u : 3u;  // first max
             pv[r] = fmaxf(m, 0.f);
