@@ -275,15 +275,22 @@ __device__ __forceinline__ void f2_store_ya(const float* ystage, const F2Tile& x
 
 // the whole workgroup stores a staged tile as y2h: thread e, i -> 8 channels q = e + 256 i of
 // [row 8][px 16][c8 4] (two staged 4-channel chunks packed to 16 B): a wave-instruction writes
-// 1 KiB, 16 pixels of one row
+// 1 KiB, 16 pixels of one row.  H16: lane quad -> pixel through F2_QPX, so each 16-lane bank
+// group of ds_read_b128 ({0-3,12-15,20-27}, ...) reads pixels p, p+4, p+8, p+12, whose 80-B
+// records start 0, 64, 128, 192 B apart mod 256 -- conflict-free (quad = pixel read 3-way).
+constexpr uint64_t F2_QPX = 0xfeab6732dc894510ull;  // nibble quad -> px
 template <int DIAG>
 __device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, unsigned short* __restrict__ y2h, int P) {
   if constexpr (DIAG == 4) return;  // timing-only: no y2h
   const int e = threadIdx.x;
+#ifndef TDS_F2_QPX
+#define TDS_F2_QPX 1
+#endif
+  const int qpx = F2_H16 && TDS_F2_QPX ? (int)((F2_QPX >> (4 * ((e >> 2) & 15))) & 15u) : (e >> 2) & 15;
 #pragma unroll
   for (int i = 0; i < F2_TH * F2_TC * 4 / F2_THREADS; ++i) {
     const int q = e + F2_THREADS * i;
-    const int row = q >> 6, px = (q >> 2) & 15, c8 = q & 3;
+    const int row = q >> 6, px = qpx, c8 = q & 3;
     const int gr = x.r0 + row, gc = x.c0 + px;
     uint4 v;
     if constexpr (F2_H16) {

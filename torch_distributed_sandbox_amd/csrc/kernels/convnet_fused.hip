@@ -34,20 +34,24 @@ __device__ __attribute__((aligned(16))) uint4 g_l1b_zero = {0u, 0u, 0u, 0u};
 constexpr int L1_TR = 16;           // conv1 output rows per tile
 constexpr int L1_TC = 64;           // conv1 output cols per tile
 constexpr int L1_XR = L1_TR + 4;
-constexpr int L1_XS = 80;           // LDS row stride (floats): 16 mod 32 -> paired taps hit disjoint banks
+// LDS row stride (words), odd: the two 16-lane groups of a 32-lane half read taps one row apart
+// (l1b_tap: g = 0 / 1 and 2 / 3 differ in ky), and 2*li spans the 16 banks of one parity, so
+// an odd stride puts the two groups on opposite parities (conflict-free; 80 = 16 mod 32 put
+// them on the same 16 banks -- 2-way on every read, 33 % of LDS cycles in the round-4 PMC)
+#ifndef TDS_L1_XS
+#define TDS_L1_XS 81
+#endif
+constexpr int L1_XS = TDS_L1_XS;
 // uint8 level input: x = L1_LEVEL_SCALE * level, the fp32 constant upsample_bilinear_u8 (elementwise.hip)
 // and ToTensor scale by
 constexpr float L1_LEVEL_SCALE = 1.f / 255.f;
 
-__device__ __forceinline__ f32x4 mfma16x4(float a, float b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-}
-
-// K index k -> tap (ky = k % 5, kx = k / 5): consecutive k step down a column so the
-// two 16-lane groups of a 32-lane half read rows 80 floats apart (disjoint banks).
-__device__ __forceinline__ int l1_koff(int k) {
-  if (k >= 25) k = 0;
-  return (k % 5) * L1_XS + (k / 5);
+// 4 words at an odd-stride LDS row (no 16-B alignment)
+__device__ __forceinline__ void l1_store4(uint32_t* d, uint4 v) {
+  d[0] = v.x;
+  d[1] = v.y;
+  d[2] = v.z;
+  d[3] = v.w;
 }
 
 // conv1 on v_mfma_f32_16x16x32_bf16 with the bf16x3 split (bf16x3.h): K = 32 slots per lane
@@ -89,7 +93,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
     split_bf16(wv, h, l);
     wah[j] = (short)h;
     wal[j] = (short)l;
-    koff[j] = tp >= 0 ? (tp / 5) * L1_XS + (tp % 5) : 0;
+    koff[j] = tp >= 0 ? (tp / 5) * L1_XS + (tp % 5) : 1;  // pad: tap (0, 1) (odd word: opposite bank parity to g = 0 j = 7)
   }
 
   // per-lane epilogue constants for co = 4g + r: z = ea * (acc + b1) + eb = ea * acc + ebb
@@ -157,7 +161,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
           v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
           v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
           v.w = __float_as_uint((float)(q >> 24));
-          *reinterpret_cast<uint4*>(xs + rr * L1_XS + 4 * cv) = v;
+          l1_store4(xs + rr * L1_XS + 4 * cv, v);
           continue;
         }
         nonfinite |= !__builtin_isfinite((pre[u].x + pre[u].y) + (pre[u].z + pre[u].w));
@@ -169,7 +173,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
         v.y = __builtin_amdgcn_perm(h01, l01, 0x07060302u);
         v.z = __builtin_amdgcn_perm(h23, l23, 0x05040100u);
         v.w = __builtin_amdgcn_perm(h23, l23, 0x07060302u);
-        *reinterpret_cast<uint4*>(xs + rr * L1_XS + 4 * cv) = v;
+        l1_store4(xs + rr * L1_XS + 4 * cv, v);
       }
     }
     // a non-finite x anywhere in the tile (or a degenerate BN1 affine) sends the whole tile to
