@@ -293,7 +293,12 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   __shared__ float red[2][HP_THREADS / 64];
   __shared__ uint32_t gred[HP_THREADS / 64];
   const HPGrid hg = hp_grid(g);
-  const int wg = blockIdx.x;
+  // workgroups in the reverse of the forward's order: the backward starts on the channels the
+  // forward streamed last, whose ya / weight lines are still in the 256 MB Infinity Cache
+#ifndef TDS_HPB_REV
+#define TDS_HPB_REV 1
+#endif
+  const int wg = TDS_HPB_REV ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
   const int c = c0 + wg / hg.per_channel(), band = wg - (c - c0) * hg.per_channel();
   float dls[NB * 10];  // dlogits of this pass: wave-uniform, scalar loads
 #pragma unroll
