@@ -49,6 +49,9 @@
 #include "launchers.h"
 #include "pooled_layout.h"
 
+#ifndef TDS_BR_MIX
+#define TDS_BR_MIX 1  // fast staging path on v_fma_mix_f32 (fp16 y2h operands, no conversions)
+#endif
 #ifndef TDS_BR_LOAD_PRIO
 #define TDS_BR_LOAD_PRIO 3  // wave priority while a staging wave issues its look-ahead loads
 #endif
@@ -397,6 +400,17 @@ constexpr uint32_t kBROob = 0xFFFFFFF0u;
 // window, 4-channel chunk): NR/2 x 10 windows x 8 chunks.  BIG: the 32 g2m planes of an image
 // exceed a 4 GiB buffer-descriptor range (64-bit g2m loads); a template parameter, because two
 // load paths under a runtime branch make the compiler wait vmcnt(0) at their merge.
+// fma(a, channel cc of the 4 fp16 channels in v, c) on v_fma_mix_f32 (op_sel picks the half)
+__device__ __forceinline__ float br_fma_y(float a, uint2 v, int cc, float c) {
+  float d;
+  const uint32_t w = cc < 2 ? v.x : v.y;
+  if (cc & 1)
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(w), "v"(c));
+  else
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(w), "v"(c));
+  return d;
+}
+
 template <int NR, bool BIG, int DIAG>
 struct BRStager {
   static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
@@ -549,18 +563,24 @@ struct BRStager {
       } else if (fast) {
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
+          // y2h values straight into v_fma_mix_f32 (TDS_BR_MIX; br_fma_y), else converted once
+          auto fy = [&](float k, int q, float c) {
+            return TDS_BR_MIX ? br_fma_y(k, yv[u][q], cc, c) : fmaf(k, y[q][cc], c);
+          };
           float z[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) z[q] = fmaf(ka[cc], y[q][cc], kb[cc]);
-          const float m = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+          for (int q = 0; q < 4; ++q) z[q] = fy(ka[cc], q, kb[cc]);
+          // (IEEE maximum: fmaxf on the asm results would first canonicalize each operand)
+          const float m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(z[0], z[1]),
+                                                        __builtin_elementwise_maximum(z[2], z[3]));
           const bool e0 = z[0] == m, e1 = !e0 && z[1] == m, e2 = !e0 && !e1 && z[2] == m;
           const bool e3 = !e0 && !e1 && !e2;
           // the pooled gradient folded into the constant: select + FMA per pixel
           const float k3g = fmaf(k1[cc], gg[cc], k3[cc]);
-          d[0][cc] = fmaf(k2[cc], y[0][cc], e0 ? k3g : k3[cc]);
-          d[1][cc] = fmaf(k2[cc], y[1][cc], e1 ? k3g : k3[cc]);
-          d[2][cc] = fmaf(k2[cc], y[2][cc], e2 ? k3g : k3[cc]);
-          d[3][cc] = fmaf(k2[cc], y[3][cc], e3 ? k3g : k3[cc]);
+          d[0][cc] = fy(k2[cc], 0, e0 ? k3g : k3[cc]);
+          d[1][cc] = fy(k2[cc], 1, e1 ? k3g : k3[cc]);
+          d[2][cc] = fy(k2[cc], 2, e2 ? k3g : k3[cc]);
+          d[3][cc] = fy(k2[cc], 3, e3 ? k3g : k3[cc]);
         }
       } else {
         const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;

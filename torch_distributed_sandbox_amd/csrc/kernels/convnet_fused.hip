@@ -66,6 +66,29 @@ __device__ __forceinline__ int l1b_tap(int g, int j) {
   return -1;
 }
 
+// LV K-slot pairs: lane group g's slots 2p, 2p+1 hold horizontally adjacent taps (ky, kx0) and
+// (ky, kx0 + 1) of one row, so ONE ds_read_b32 of a pair word (bf16 x[c] | bf16 x[c+1] << 16, the
+// LV staging layout) is the B operand's two slots -- 4 reads and no v_perm per 8 slots instead of
+// 8 reads + 4 perms.  Rows 0-3: pairs kx (0,1), (2,3), (4,pad) in group g = ky; row 4 spread over
+// p = 3 as (4: 0,1) g0, (4: 3,4) g1, (4: 2,pad) g2; g3's p = 3 is a zero-weight pair reading (3,0).
+// Pads read column kx0 + 1 = 5 or 3 of the row with weight 0 (levels are finite).  Bank parity:
+// the two groups of a 32-lane half read offsets of opposite parity (odd L1_XS, row-4 kx0 0/3 and
+// 2/(3,0)), so with 2*li spanning one parity the 32 lanes hit 32 banks.
+#ifndef TDS_L1_PAIR
+#define TDS_L1_PAIR 1
+#endif
+struct L1Pair {
+  int ky, kx0;
+  bool second;  // slot 2p+1 carries a real tap
+};
+__device__ __forceinline__ L1Pair l1_pair(int g, int p) {
+  if (p < 3) return L1Pair{g, 2 * p, p < 2};
+  if (g == 0) return L1Pair{4, 0, true};
+  if (g == 1) return L1Pair{4, 3, true};
+  if (g == 2) return L1Pair{4, 2, false};
+  return L1Pair{3, 0, false};  // zero weights
+}
+
 // LV: x holds uint8 levels (x = L1_LEVEL_SCALE * level).  A level is exact in bf16, so the LDS word
 // is the level's fp32 bit pattern (bf16 hi | lo = 0), conv1 takes two MFMAs (w hi, w lo) per
 // product instead of three and half the operand perms, and the scale folds into BN1's affine.
@@ -75,6 +98,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
                                                       uint4* __restrict__ p1, uint8_t* __restrict__ idx1, int B,
                                                       int H, int W) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[L1_XR * L1_XS];  // x as (bf16 hi << 16 | bf16 lo)
+  constexpr bool PAIR = LV && TDS_L1_PAIR;  // (TDS_L1_PAIR 0: A/B builds only)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int P = H / 2, PW = W / 2;
@@ -87,13 +111,21 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
   int koff[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int tp = l1b_tap(g, j);
+    int tp;
+    if constexpr (PAIR) {
+      const L1Pair pr = l1_pair(g, j >> 1);
+      const bool real = (g < 3 || j < 6) && ((j & 1) == 0 || pr.second);
+      tp = real ? pr.ky * 5 + pr.kx0 + (j & 1) : -1;
+      if ((j & 1) == 0) koff[j >> 1] = pr.ky * L1_XS + pr.kx0;
+    } else {
+      tp = l1b_tap(g, j);
+      koff[j] = tp >= 0 ? (tp / 5) * L1_XS + (tp % 5) : 1;  // pad: tap (0, 1) (odd word: opposite bank parity to g = 0 j = 7)
+    }
     const float wv = tp >= 0 ? w1[li * 25 + tp] : 0.f;
     unsigned short h, l;
     split_bf16(wv, h, l);
     wah[j] = (short)h;
     wal[j] = (short)l;
-    koff[j] = tp >= 0 ? (tp / 5) * L1_XS + (tp % 5) : 1;  // pad: tap (0, 1) (odd word: opposite bank parity to g = 0 j = 7)
   }
 
   // per-lane epilogue constants for co = 4g + r: z = ea * (acc + b1) + eb = ea * acc + ebb
@@ -118,7 +150,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
   // 20 rows x 18 float4; the next tile's loads are issued before this tile's MFMAs.
   constexpr int NV = L1_XR * 18;
   constexpr int PER = (NV + 255) / 256;
-  float4 pre[PER];
+  float4 pre[PER];  // LV: .x = 4 levels, .y = the next 4 (the pair words' right neighbours)
   // unconditional loads (out-of-range lanes read a zero vector): a load under a per-lane branch
   // is waited for before the branches merge (conv2_bwd.hip, l1_bwd_mfma_kernel)
   auto load_tile = [&](int t) {
@@ -131,9 +163,12 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
       const int gr = r0 - 2 + rr, gc = c0 - 4 + 4 * cv;
       const bool ok = (e < NV) & ((uint32_t)gr < (uint32_t)H) & ((uint32_t)gc < (uint32_t)W);
       const int64_t o = ((int64_t)b * H + gr) * W + gc;
-      if constexpr (LV) {  // 4 levels in .x
+      if constexpr (LV) {  // 4 levels in .x, the next 4 in .y (zero past the image / the tile)
+        // (its own range test: at the image's left edge the word at column -1 pairs with x[0])
+        const bool okn = (e < NV) & (cv < 17) & ((uint32_t)gr < (uint32_t)H) & ((uint32_t)(gc + 4) < (uint32_t)W);
         const uint32_t* src = ok ? reinterpret_cast<const uint32_t*>(xl + o) : &g_l1b_zero.x;
-        pre[u] = make_float4(__uint_as_float(*src), 0.f, 0.f, 0.f);
+        const uint32_t* srn = okn ? reinterpret_cast<const uint32_t*>(xl + o + 4) : &g_l1b_zero.x;
+        pre[u] = make_float4(__uint_as_float(*src), PAIR ? __uint_as_float(*srn) : 0.f, 0.f, 0.f);
       } else {
         const float4* src = ok ? reinterpret_cast<const float4*>(x + o) : reinterpret_cast<const float4*>(&g_l1b_zero);
         pre[u] = *src;
@@ -154,14 +189,23 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
       const int e = tid + 256 * u;
       if (e < NV) {
         const int rr = e / 18, cv = e - rr * 18;
-        if constexpr (LV) {  // levels are finite; word = fp32 bits of the level = bf16 hi | lo 0
+        if constexpr (PAIR) {  // levels are exact in bf16 (the fp32 bits' upper half): pair words
           const uint32_t q = __float_as_uint(pre[u].x);
-          uint4 v;
-          v.x = __float_as_uint((float)(q & 0xFFu));
-          v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
-          v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
-          v.w = __float_as_uint((float)(q >> 24));
+          const uint32_t f0 = __float_as_uint((float)(q & 0xFFu)), f1 = __float_as_uint((float)((q >> 8) & 0xFFu));
+          const uint32_t f2 = __float_as_uint((float)((q >> 16) & 0xFFu)), f3 = __float_as_uint((float)(q >> 24));
+          const uint32_t f4 = __float_as_uint((float)(__float_as_uint(pre[u].y) & 0xFFu));
+          uint4 v;  // word c = bf16 x[c] | bf16 x[c+1] << 16
+          v.x = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+          v.y = __builtin_amdgcn_perm(f2, f1, 0x07060302u);
+          v.z = __builtin_amdgcn_perm(f3, f2, 0x07060302u);
+          v.w = __builtin_amdgcn_perm(f4, f3, 0x07060302u);
           l1_store4(xs + rr * L1_XS + 4 * cv, v);
+          continue;
+        } else if constexpr (LV) {  // (A/B build) word = fp32 bits of the level = bf16 hi | lo 0
+          const uint32_t q = __float_as_uint(pre[u].x);
+          l1_store4(xs + rr * L1_XS + 4 * cv,
+                    make_uint4(__float_as_uint((float)(q & 0xFFu)), __float_as_uint((float)((q >> 8) & 0xFFu)),
+                               __float_as_uint((float)((q >> 16) & 0xFFu)), __float_as_uint((float)(q >> 24))));
           continue;
         }
         nonfinite |= !__builtin_isfinite((pre[u].x + pre[u].y) + (pre[u].z + pre[u].w));
@@ -196,16 +240,27 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
           for (int c = 0; c < 2; ++c) {
             const int row = 4 * wv + 2 * rp + a;
             const uint32_t* src = xs + row * L1_XS + 2 + 32 * sp + 2 * li + c;  // +2: tile origin is c0-4
-            uint32_t u[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) u[j] = src[koff[j]];
             s16x8 bh, bl;
             uint32_t* hp = reinterpret_cast<uint32_t*>(&bh);
             uint32_t* lp = reinterpret_cast<uint32_t*>(&bl);
+            if constexpr (PAIR) {  // pair words: the B operand as read (l1_pair)
+              // (the c = 1 base laundered: merged with c = 0's reads into ds_read2_b32, each
+              // result pair straddled two MFMA operands and cost 3 v_mov per operand)
+              // (the word index, not the pointer: a laundered pointer loses the LDS address space
+              // and becomes flat loads, whose vmcnt wait also drains the x prefetch)
+              int i0 = row * L1_XS + 2 + 32 * sp + 2 * li + c;
+              if (c == 1) asm volatile("" : "+v"(i0));
+              typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+              bh = __builtin_bit_cast(s16x8, u32x4{xs[i0 + koff[0]], xs[i0 + koff[1]], xs[i0 + koff[2]], xs[i0 + koff[3]]});
+            } else {
+              uint32_t u[8];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
-              if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+              for (int j = 0; j < 8; ++j) u[j] = src[koff[j]];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
+                if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
+              }
             }
 #if defined(TDS_L1_EXP) && TDS_L1_EXP == 2
             acc[a][c] = f32x4{(float)(bh[0] ^ bl[1]), (float)wah[0], (float)wal[1], 0.f};
