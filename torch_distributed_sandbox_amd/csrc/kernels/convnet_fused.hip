@@ -521,6 +521,13 @@ constexpr int LM_X_BYTES = (LB_XR * LM_XS > LV_WORDS ? LB_XR * LM_XS : LV_WORDS)
 #ifndef TDS_L1B_WAVES
 #define TDS_L1B_WAVES 3
 #endif
+// H16 (level input, word layout): dz1 * x on ONE v_mfma_f32_16x16x32_f16 per product instead of
+// the bf16 pair (dz hi, dz lo): dz1 is dp1h's fp16 value as stored and a level (0..255) is exact
+// in fp16, so every product is exact either way; the A operand is the fp16 bits themselves (no
+// conversion, no bf16 split) and the MFMA count halves.  x words: fp16(level) << 16.
+#ifndef TDS_L1B_H16
+#define TDS_L1B_H16 1
+#endif
 // PAIRS (level input only; TDS_L1B_PAIRS=1 at run time, fused_ops.cpp): the conflict-free bf16-pair
 // x tile above.  Opt-in: timed slower than the default word layout (docs/KERNELS.md).
 template <bool LV, bool PAIRS>
@@ -565,9 +572,10 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
     vlof[blk] = (kx & 1) ? LV_OB + ky * LV_RS + (kx + 1 + 4 * g) / 2 : ky * LV_RS + (kx + 2 + 4 * g) / 2;
     vcst[blk] = n == 25 ? 0x3F803F80u : 0u;  // bf16 1.0 pair: the sum-dz column
   }
+  constexpr bool H16 = LV && !PAIRS && TDS_L1B_H16;
   if (!(LV && PAIRS))  // the ones block (never overwritten: the x tile uses columns 0..71)
-    for (int e = tid; e < LB_XR * (LM_XS - 72); e += 256)
-      xs[(e / (LM_XS - 72)) * LM_XS + 72 + e % (LM_XS - 72)] = 0x3F800000u;  // bf16 1.0 | lo 0
+    for (int e = tid; e < LB_XR * (LM_XS - 72); e += 256)  // bf16 1.0 | lo 0, or fp16 1.0 << 16
+      xs[(e / (LM_XS - 72)) * LM_XS + 72 + e % (LM_XS - 72)] = H16 ? 0x3C000000u : 0x3F800000u;
   const float* __restrict__ x = static_cast<const float*>(xv);
   const uint8_t* __restrict__ xl = static_cast<const uint8_t*>(xv);
   uint4 pre[LB_PER];
@@ -624,6 +632,12 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
       else if (e < LB_V) {
         e -= LB_V_DP + LB_V_PH + LB_V_ID;
         const int rr = e / 18, cv = e - rr * 18;
+        if constexpr (H16) {  // word = fp16(level) << 16 (exact)
+          const uint32_t q = pre[u].x;
+          auto h = [](uint32_t l) { return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)(float)l) << 16; };
+          lb_store4(xs + rr * LM_XS + 4 * cv, make_uint4(h(q & 0xFFu), h((q >> 8) & 0xFFu), h((q >> 16) & 0xFFu), h(q >> 24)));
+          continue;
+        }
         if constexpr (LV && !PAIRS) {  // word = fp32 bits of the level = bf16 hi | lo 0
           const uint32_t q = pre[u].x;
           uint4 v;
@@ -688,6 +702,16 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
           // pooled columns 8sg + 2g + {0, 1}: column group 2sg + (g >> 1), pixels 2(g & 1) + {0, 1} --
           // one dword (a 32-lane half reads 32 consecutive words: conflict-free)
           const uint32_t dpair = dps[((rp * 8 + 2 * sg + (g >> 1)) * 16 + li) * 2 + (g & 1)];
+          if constexpr (H16) {  // fp16 bits at the argmax slot, zero where ReLU blocks the gradient
+#pragma unroll
+            for (int wi = 0; wi < 2; ++wi) {
+              const uint32_t ab = ids[(rp * LB_PC + 8 * sg + 2 * g + wi) * 16 + li];
+              const uint32_t hb = (ab & 4u) ? ((dpair >> (16 * wi)) & 0xFFFFu) : 0u;
+              const uint64_t h64 = (uint64_t)hb << (16u * (ab & 3u));
+              hp[2 * wi] = (uint32_t)h64;
+              hp[2 * wi + 1] = (uint32_t)(h64 >> 32);
+            }
+          } else
 #pragma unroll
           for (int wi = 0; wi < 2; ++wi) {
             const int pp = rp * LB_PC + 8 * sg + 2 * g + wi;
@@ -737,7 +761,9 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
             hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
             if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
           }
-          if constexpr (LV)  // levels are exact in bf16: lo = 0
+          if constexpr (H16)  // fp16 x fp16, exact products
+            acc[blk] = mfma_f16(ah, bh, acc[blk]);
+          else if constexpr (LV)  // levels are exact in bf16: lo = 0
             acc[blk] = mfma_bf16x2a(ah, al, bh, acc[blk]);
           else
             acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
