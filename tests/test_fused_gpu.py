@@ -92,25 +92,33 @@ def _bits_to_half(b):
 
 def y2h_encode(y2, b2, g2, mag):
     """The forward's y2h (kernels/conv2_common.h) of a synthetic fp32 y2 [B,P,P,32]: fp16(acc * 2^k)
-    to nearest, acc = (y2 - b2) / inv, each window's first extreme moved one fp16 step outward when
-    an earlier pixel rounded equal to it.  Returns (y2h, the decoded fp32 y2 the kernels see)."""
+    to nearest, acc = (y2 - b2) / inv, and an a2: each window's first extreme (max, or min where
+    gamma2 < 0) of the stored values -- the pixel max_pool2d picks on the decoded y2 the references
+    see.  Returns (y2h, a2, the decoded fp32 y2 the kernels see)."""
     m = mag_floats(mag)
     inv, ksc = (m[40] * m[41]).item(), m[42].item()
     acc = (y2 - b2) / inv
     h = (acc * ksc).half()
     Q = y2.shape[1] // 2
-    wa, wb = _windows(acc, Q), _windows(h, Q).view(torch.int16).int() & 0xFFFF
-    neg = g2 < 0
-    a = first_extreme(wa, neg).unsqueeze(-1)
-    ha = wb.gather(-1, a)
-    ra = _bits_to_half(ha).float()
-    earlier = torch.arange(4, device=y2.device).view(1, 1, 1, 1, 4) < a
-    tie = ((_bits_to_half(wb).float() == ra) & earlier).any(-1, keepdim=True)
-    up = ~neg.view(1, 1, 1, 32, 1)
-    step = torch.where(((ha >> 15) & 1).bool() ^ up, 1, -1)
-    wb = wb.scatter(-1, a, torch.where(tie, ha + step, ha).int())
-    h = _unwindows(_bits_to_half(wb), h.clone())
-    return h, h.float() * (inv / ksc) + b2
+    a2 = a2_encode(first_extreme(_windows(h.float(), Q), g2 < 0))
+    return h, a2, h.float() * (inv / ksc) + b2
+
+
+def a2_encode(codes):
+    """argmax codes [B,Q,Q,32] (0..3) -> a2 [B,Q,Q,2] int32 (kernels/conv2_common.h): word h, bit c =
+    code bit 0 and bit 16 + c = code bit 1 of channel 16h + c"""
+    c = codes.long().view(*codes.shape[:3], 2, 16)
+    sh = torch.arange(16, device=codes.device)
+    w = (((c & 1) << sh) | (((c >> 1) & 1) << (sh + 16))).sum(-1)
+    return (w - (w >= 2 ** 31).long() * 2 ** 32).int()
+
+
+def a2_decode(a2):
+    """a2 [B,Q,Q,2] int32 -> codes [B,Q,Q,32]"""
+    w = a2.long() & 0xFFFFFFFF
+    sh = torch.arange(16, device=a2.device)
+    c = ((w.unsqueeze(-1) >> sh) & 1) | (((w.unsqueeze(-1) >> (sh + 16)) & 1) << 1)
+    return c.reshape(*a2.shape[:3], 32)
 
 
 def dp1h_decode(dp1h, dec, P):
@@ -259,7 +267,7 @@ def test_conv2_forward(gpu, P):
     g2 = torch.randn(32, device=gpu)  # mixed signs: max and min windows
     mag = new_mag(gpu, B, P)
     wp, wd = _ops().conv2_pack(w2, mag)
-    y2h, partial, ya = _ops().fused_conv2_forward(p, wp, b2, g2, mag)
+    y2h, partial, ya, a2 = _ops().fused_conv2_forward(p, wp, b2, g2, mag)
     assert y2h.dtype == torch.float16 and y2h.shape == (B, P, P, 32)
     v = y2h.float() * y2h_decode_factor(mag)  # y2 - b2 as stored (fp16 grid: 2^-11 relative)
     y2 = v + b2
@@ -267,7 +275,7 @@ def test_conv2_forward(gpu, P):
     reft = F.conv2d(p.permute(0, 3, 1, 2).double().cpu(), tf32(w2.cpu()), b2.double().cpu(), padding=2)
     # split: the weights are carried exactly (fp16 hi + lo), only fp32 accumulation error remains;
     # TF32 class: the weights rounded once, as TF32 rounds them; either way plus the y2h storage
-    # rounding (<= 1.5 fp16 steps of |y2 - b2| with the argmax nudge)
+    # rounding (<= half an fp16 step of |y2 - b2|)
     vmax = v.abs().max().item()
     e, sc = _err(y2.permute(0, 3, 1, 2), reft if not _split() else ref)
     assert e <= 2.0 ** -10 * vmax + 1e-5 * sc, (e, vmax)
@@ -283,23 +291,25 @@ def test_conv2_forward(gpu, P):
     yct = reft - b2.double().cpu().view(1, 32, 1, 1)
     _check_conv(s[:, 0], yc.sum((0, 2, 3)), yct.sum((0, 2, 3)), 1e-4, "sum")
     _check_conv(s[:, 1], (yc * yc).sum((0, 2, 3)), (yct * yct).sum((0, 2, 3)), 1e-4, "sumsq")
-    # ya: the fp32 window extremes; y2h keeps each window's argmax pixel (first in scan order)
+    # ya: the fp32 window extremes; a2: each window's argmax pixel (first in scan order)
     Q = P // 2
     want = window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q].float(), (g2 < 0))
     got = pb_to_planar(ya, Q)
     assert ((got - want).abs() <= 2.0 ** -10 * vmax).all(), (got - want).abs().max()
-    _check_argmax_kept(y2h, ref if _split() else reft, g2, Q)
+    _check_argmax_kept(a2, ref if _split() else reft, g2, Q)
 
 
-def _check_argmax_kept(y2h, ref_nchw, g2, Q, gap=1e-5):
-    """The first extreme of every window of the stored y2h is the reference's, wherever the
-    reference's top two values of the window differ by more than fp32 accumulation noise."""
-    r = _windows(ref_nchw.permute(0, 2, 3, 1).to(y2h.device), Q)
+def _check_argmax_kept(a2, ref_nchw, g2, Q, gap=1e-5):
+    """The forward's stored argmax codes (a2) name the reference's first extreme of every window
+    wherever the reference's top two values of the window differ by more than fp32 accumulation
+    noise."""
+    assert a2.dtype == torch.int32 and a2.shape == (ref_nchw.shape[0], Q, Q, 2)
+    r = _windows(ref_nchw.permute(0, 2, 3, 1).to(a2.device), Q)
     neg = g2 < 0
     key = torch.where(neg.view(1, 1, 1, 32, 1), -r, r)
     top2 = key.topk(2, -1).values
     clear = (top2[..., 0] - top2[..., 1]) > gap * r.abs().max()
-    got = first_extreme(_windows(y2h.float(), Q), neg)
+    got = a2_decode(a2)
     want = first_extreme(r, neg)
     assert clear.float().mean().item() > 0.5
     bad = (got != want) & clear
@@ -307,11 +317,10 @@ def _check_argmax_kept(y2h, ref_nchw, g2, Q, gap=1e-5):
 
 
 @pytest.mark.parametrize("P", [40, 37])
-def test_conv2_forward_y2h_keeps_argmax_on_near_ties(gpu, P):
+def test_conv2_forward_argmax_codes_on_near_ties(gpu, P):
     """Inputs on a 2^-10 grid make neighbouring outputs differ by about one fp16 step of y2h:
-    rounding to nearest alone would merge many windows' top two values; the forward moves the
-    argmax one step outward there (kernels/conv2_common.h), so the stored windows still name the
-    reference's argmax."""
+    rounding to nearest merges many windows' top two values in y2h; the argmax codes (a2) come
+    from the fp32 accumulators (kernels/conv2_common.h), so they still name the reference's."""
     torch.manual_seed(100 + P)
     B = 2
     p = (1.0 + torch.randint(0, 4, (B, P, P, 16), device=gpu).float() * 2.0 ** -10).half()
@@ -320,7 +329,7 @@ def test_conv2_forward_y2h_keeps_argmax_on_near_ties(gpu, P):
     g2 = torch.randn(32, device=gpu)
     mag = new_mag(gpu, B, P)
     wp, _ = _ops().conv2_pack(w2, mag)
-    y2h, _, _ = _ops().fused_conv2_forward(p, wp, b2, g2, mag)
+    y2h, _, _, a2 = _ops().fused_conv2_forward(p, wp, b2, g2, mag)
     pin = p.permute(0, 3, 1, 2).double().cpu()
     ref = F.conv2d(pin, w2.double().cpu() if _split() else tf32(w2.cpu()), None, padding=2)
     Q = P // 2
@@ -330,7 +339,7 @@ def test_conv2_forward_y2h_keeps_argmax_on_near_ties(gpu, P):
     top2 = key.topk(2, -1).values * y2h_decode_factor(mag) ** -1
     merged = (top2[..., 0].float().half() == top2[..., 1].float().half()) & (top2[..., 0] > top2[..., 1])
     assert merged.float().mean().item() > 0.01
-    _check_argmax_kept(y2h, ref, g2, Q)
+    _check_argmax_kept(a2, ref, g2, Q)
 
 
 def _head_case(gpu, P, B, seed):
@@ -417,7 +426,7 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     mag = new_mag(gpu, B, P)
     _, wd = ops.conv2_pack(w2, mag)
     # the forward's y2h of the synthetic y2; everything below (head, references) sees its decode
-    y2h, y2 = y2h_encode(y2, b2, g2, mag)
+    y2h, a2, y2 = y2h_encode(y2, b2, g2, mag)
     Q = P // 2
     yc = (y2 - b2).double()
     partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()
@@ -427,7 +436,7 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     yp.zero_()
     yp[:, 0] = (y2 - b2).abs().amax((0, 1, 2)).view(torch.int32)  # max |y2 - b2| per channel
     _, _, _, _, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, True, mag=mag)
-    dp1h, dw2, db2 = ops.fused_conv2_backward_y2(y2h, g2m, aff2, kbuf, b2, mag, p, wd, 1.0)
+    dp1h, dw2, db2 = ops.fused_conv2_backward_y2(y2h, a2, g2m, aff2, kbuf, b2, mag, p, wd, 1.0)
     dp1 = dp1h_decode(dp1h, mag_floats(mag)[44].item(), P)
     # fp64 reference: dy2 from the head chain, then the conv2 backward with that dy2
     yr = y2.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)

@@ -69,7 +69,7 @@ def main():
             st["c2"] = ops.fused_conv2_forward(st["l1"][0], st["pack"][0], c2.bias, n2.weight, st["mag"])
 
         def hf():
-            y2, partial2, ya = st["c2"]
+            y2, partial2, ya = st["c2"][:3]
             st["hf"] = ops.fused_head_forward(ya, partial2, c2.bias, n2.weight, n2.bias, n2.running_mean,
                                               n2.running_var, n2.num_batches_tracked, 0.1, 1e-5, fc.weight,
                                               fc.bias, P, None)
@@ -89,7 +89,7 @@ def main():
         def c2b():
             y2 = st["c2"][0]
             g2m, kbuf = st["hb"][4], st["hb"][5]
-            st["c2b"] = ops.fused_conv2_backward_y2(y2, g2m, st["hf"][2], kbuf, c2.bias, st["mag"], st["l1"][0],
+            st["c2b"] = ops.fused_conv2_backward_y2(y2, st["c2"][3], g2m, st["hf"][2], kbuf, c2.bias, st["mag"], st["l1"][0],
                                                         st["pack"][1], 1.0)
 
         def l1b():

@@ -40,7 +40,7 @@ def fc_input(model, x):
         p1, _, _, _, p1s = ops.fused_l1_forward(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, None, None, None,
                                            float(bn1.momentum), float(bn1.eps), None, None)
         wp, _ = ops.conv2_pack(conv2.weight)
-        y2, partial2, ya = ops.fused_conv2_forward(p1, wp, conv2.bias, bn2.weight)
+        y2, partial2, ya, _ = ops.fused_conv2_forward(p1, wp, conv2.bias, bn2.weight)
         P = y2.shape[1]
         xo = torch.empty((x.shape[0], fc.weight.shape[1]), device=x.device, dtype=torch.float32)
         ops.fused_head_forward(ya, partial2, conv2.bias, bn2.weight, bn2.bias, None, None, None, float(bn2.momentum),

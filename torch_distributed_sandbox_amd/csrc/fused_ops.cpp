@@ -291,8 +291,9 @@ std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tens
 
 // returns (y2h [B,P,P,32] fp16: the conv2 output bias-free at the y2h scale mag[kMagScales + 2]
 // (1 without mag; kernels/conv2_common.h), BN2 partials, ya [B,32,PB]: y2 at each 2x2 window's
-// argmax of the BN2 output, resolved by the sign of gamma2)
-std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& wp, const Tensor& b2,
+// argmax of the BN2 output, resolved by the sign of gamma2, a2 [B,P/2,P/2,2] int32: those argmaxes
+// as 2-bit codes (kernels/conv2_common.h), for the backward)
+std::tuple<Tensor, Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& wp, const Tensor& b2,
                                                        const c10::optional<Tensor>& gamma2,
                                                        const c10::optional<Tensor>& mag) {
   TORCH_CHECK(p1.dim() == 4 && p1.size(1) == p1.size(2) && p1.size(3) == 16, "fused_conv2_forward: p1 [B,P,P,16]");
@@ -311,12 +312,13 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const T
   auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kHalf));  // y2h (kernels/conv2_common.h)
   auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
+  auto a2 = at::empty({B, P / 2, P / 2, 2}, p1.options().dtype(at::kInt));
   tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr(),
-                 ya.data_ptr<float>(), partial.data_ptr<double>(),
+                 ya.data_ptr<float>(), reinterpret_cast<uint32_t*>(a2.data_ptr<int>()), partial.data_ptr<double>(),
                  opt_mag(mag, kMagParts + 32 * mag_ypart_count()) ? opt_mag(mag) + kMagParts : nullptr,
                  opt_mag(mag) ? opt_mag(mag) + kMagScales : nullptr, order, nwg, sw, sk, (int)B, (int)P, stream_of(p1));
   check_launches("fused_conv2_forward");
-  return {y2, partial, ya};
+  return {y2, partial, ya, a2};
 }
 
 // ---------------------------------------------------------------- head forward (BN2 finalize + fc)
@@ -485,9 +487,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
 }
 
 // ---------------------------------------------------------------- conv2 backward
-// BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2h, g2m, aff2, kbuf, b2, p1) -> (dp1h, dw2, db2);
-// dp1h's decode factor lands in mag[kMagScales + 4] (fused_l1_backward's dp1_dec)
-std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& g2m, const Tensor& aff2,
+// BN2/ReLU/pool backward fused into conv2 dgrad + wgrad: (y2h, a2, g2m, aff2, kbuf, b2, p1) -> (dp1h, dw2,
+// db2); dp1h's decode factor lands in mag[kMagScales + 4] (fused_l1_backward's dp1_dec)
+std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, const Tensor& a2, const Tensor& g2m,
+                                                           const Tensor& aff2,
                                                            const Tensor& kbuf, const Tensor& b2, const Tensor& mag,
                                                            const Tensor& p1,
                                                            const Tensor& wd, double scale,
@@ -498,6 +501,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   opt_mag(mag, kMagScales + 5);  // the magnitude bounds of the forward / head backward, the y2h decode, the
                                  // dp1h factors (kernels/conv2_common.h; mag[kMagScales + 4] is written)
   need(y2, at::kHalf, {B, P, P, 32}, "y2h (fused_conv2_forward's)");
+  need(a2, at::kInt, {B, P / 2, P / 2, 2}, "a2 (fused_conv2_forward's pooling argmax codes)");
   need(b2, at::kFloat, {32}, "conv2.bias");
   need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
   need(aff2, at::kFloat, {64}, "aff2");
@@ -515,7 +519,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options().dtype(at::kFloat));
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
-  tds_conv2_bwd3(y2.data_ptr(), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
+  tds_conv2_bwd3(y2.data_ptr(), reinterpret_cast<const uint32_t*>(a2.data_ptr<int>()), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
                  b2.data_ptr<float>(), reinterpret_cast<uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(),
                  wd.data_ptr<int16_t>(),
                  dp1.data_ptr(), slab.data_ptr<float>(), order, nwg, sw, sk, (int)B, (int)P, st);
@@ -768,7 +772,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("conv2_split() -> int", []() -> int64_t { return tds_conv2_split(); });
   m.def(
       "fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2, Tensor(a!)? mag=None) -> "
-      "(Tensor, Tensor, Tensor)",
+      "(Tensor, Tensor, Tensor, Tensor)",
       &fused_conv2_forward);
   m.def(
       "fused_head_forward(Tensor ya, Tensor partial2, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
@@ -788,7 +792,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);
   m.def("conv2_bwd_walk_table(int B, int tiles_r, int tiles_c, int nwg, int seg) -> Tensor", &conv2_bwd_walk_table);
   m.def(
-      "fused_conv2_backward_y2(Tensor y2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor b2, Tensor(c!) mag, Tensor p1, "
+      "fused_conv2_backward_y2(Tensor y2, Tensor a2, Tensor g2m, Tensor aff2, Tensor kbuf, Tensor b2, Tensor(c!) mag, Tensor p1, "
       "Tensor wd, "
       "float scale, Tensor(a!)? dw_out=None, Tensor(b!)? db_out=None) -> (Tensor, Tensor, Tensor)",
       &fused_conv2_backward_y2);

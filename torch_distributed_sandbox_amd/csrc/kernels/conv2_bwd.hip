@@ -104,6 +104,7 @@ __device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k,
 
 struct BRArgs {
   const uint2* __restrict__ y2;  // y2h [B][P][P][32] fp16 (conv2_common.h)
+  const uint32_t* __restrict__ a2;  // the forward's pooling argmax codes [B][Q][Q][2] (conv2_common.h)
   const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
   const uint4* __restrict__ p1;
   uint2* __restrict__ dp1;  // dp1h (conv2_common.h)
@@ -420,6 +421,7 @@ struct BRStager {
   static constexpr int PPER = (PIECES + 255) / 256;
   uint2 yv[IPER][4];  // y2h: 4 channels of one pixel
   float4 gv[IPER];
+  uint32_t av[IPER];  // a2: the window's argmax codes, 16 channels
   uint4 pr[PPER];
 
   __device__ __forceinline__ static void item_geom(int it, int& wy, int& wx) {
@@ -440,6 +442,7 @@ struct BRStager {
 #pragma unroll
       for (int u = 0; u < IPER; ++u) {
         gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        av[u] = 0u;
 #pragma unroll
         for (int q = 0; q < 4; ++q) yv[u][q] = make_uint2(0u, 0u);
       }
@@ -459,6 +462,7 @@ struct BRStager {
     const int py0 = R0 / 2, px0 = c0 / 2 - 1;
     const __amdgpu_buffer_rsrc_t rg =
         tds_buffer_rsrc(a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0, 0xFFFFFFF0u);
+    const __amdgpu_buffer_rsrc_t ra = tds_buffer_rsrc(a.a2 + (((int64_t)b * Q + py0) * Q + px0) * 2, 0xFFFFFFF0u);
     const int c4 = tid & 7;
 #pragma unroll
     for (int u = 0; u < IPER; ++u) {
@@ -477,6 +481,7 @@ struct BRStager {
       }
       const int py = py0 + wy, px = px0 + wx;
       const bool pooled = item & (in | (((uint32_t)py < (uint32_t)Q) & ((uint32_t)px < (uint32_t)Q)));
+      av[u] = __builtin_amdgcn_raw_buffer_load_b32(ra, pooled ? (uint32_t)(((wy * Q + wx) * 2 + (c4 >> 2)) * 4) : kBROob, 0, 0);
       float g4[4];
       if constexpr (!BIG) {
         const uint32_t og = (uint32_t)(((int64_t)c4 * 4 * gplane + (int64_t)wy * Q + wx) * 4);
@@ -506,11 +511,11 @@ struct BRStager {
 
   // BN2 / ReLU / pool backward of the staged windows -> dy2 hi|lo rows at dbase; p1 -> pbase;
   // MIRROR: rows 4-7 stored a second time at dmir / pmir (the next slot's top rows).
-  // dy2 = k1*dz + k2*y2 + k3, dz = pooled gradient at the window's argmax of a*y2 + b.  Interior
-  // blocks take a short path (argmax by max + first-equal, torch's scan-order tie rule; no NaN
-  // rule: a NaN in y2 makes its channel's BN2 statistics NaN, hence a, b, k1..k3, hence every dy2
-  // of the channel, whichever pixel dz goes to -- as in torch).  Border blocks take the general
-  // path (zero padding, unpooled last row / column, torch's NaN-wins scan).
+  // dy2 = k1*dz + k2*y2 + k3, dz = pooled gradient at the window's argmax, which the forward
+  // stored (a2, conv2_common.h: as max_pool2d's backward scatters to the indices its forward saved;
+  // a NaN in y2 makes its channel's BN2 statistics NaN, hence k1..k3 and every dy2 of the channel,
+  // wherever dz goes -- as in torch).  Interior blocks take a short path; border blocks the general
+  // one (zero padding, unpooled last row / column).
   template <bool MIRROR>
   __device__ __forceinline__ void store(const BRArgs& a, int R0, int c0, int tid, char* dbase, char* pbase,
                                         const float* kc, char* dmir, char* pmir) {
@@ -524,18 +529,15 @@ struct BRStager {
     for (int u = 0; u < IPER; ++u) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(yv[u][q].x), "v"(yv[u][q].y));
-      asm volatile("" ::"v"(gv[u].x), "v"(gv[u].y), "v"(gv[u].z), "v"(gv[u].w));
+      asm volatile("" ::"v"(gv[u].x), "v"(gv[u].y), "v"(gv[u].z), "v"(gv[u].w), "v"(av[u]));
     }
 #pragma unroll
     for (int j = 0; j < PPER; ++j) asm volatile("" ::"v"(pr[j].x), "v"(pr[j].y), "v"(pr[j].z), "v"(pr[j].w));
     const int c4 = tid & 7;
     const int P = a.P, Q = a.Q;
-    const float4 ka4 = *reinterpret_cast<const float4*>(&kc[0 * 32 + 4 * c4]);
-    const float4 kb4 = *reinterpret_cast<const float4*>(&kc[1 * 32 + 4 * c4]);
     const float4 k14 = *reinterpret_cast<const float4*>(&kc[2 * 32 + 4 * c4]);
     const float4 k24 = *reinterpret_cast<const float4*>(&kc[3 * 32 + 4 * c4]);
     const float4 k34 = *reinterpret_cast<const float4*>(&kc[4 * 32 + 4 * c4]);
-    const float ka[4] = {ka4.x, ka4.y, ka4.z, ka4.w}, kb[4] = {kb4.x, kb4.y, kb4.z, kb4.w};
     const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, k2[4] = {k24.x, k24.y, k24.z, k24.w},
                 k3[4] = {k34.x, k34.y, k34.z, k34.w};
     const bool fast = interior(a, R0, c0);
@@ -561,40 +563,27 @@ struct BRStager {
 #pragma unroll
           for (int cc = 0; cc < 4; ++cc) d[q][cc] = y[q][cc] + gg[cc];
       } else if (fast) {
+        // this item's 4 channels' codes: bits 4 (c4 & 3) .. +3 and 16 + that of the window's word
+        const uint32_t cw = av[u] >> (4 * (c4 & 3));
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
           // y2h values straight into v_fma_mix_f32 (TDS_BR_MIX; br_fma_y), else converted once
           auto fy = [&](float k, int q, float c) {
             return TDS_BR_MIX ? br_fma_y(k, yv[u][q], cc, c) : fmaf(k, y[q][cc], c);
           };
-          float z[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) z[q] = fy(ka[cc], q, kb[cc]);
-          // (IEEE maximum: fmaxf on the asm results would first canonicalize each operand)
-          const float m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(z[0], z[1]),
-                                                        __builtin_elementwise_maximum(z[2], z[3]));
-          const bool e0 = z[0] == m, e1 = !e0 && z[1] == m, e2 = !e0 && !e1 && z[2] == m;
-          const bool e3 = !e0 && !e1 && !e2;
+          const uint32_t code = ((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u);  // the forward's argmax
           // the pooled gradient folded into the constant: select + FMA per pixel
           const float k3g = fmaf(k1[cc], gg[cc], k3[cc]);
-          d[0][cc] = fy(k2[cc], 0, e0 ? k3g : k3[cc]);
-          d[1][cc] = fy(k2[cc], 1, e1 ? k3g : k3[cc]);
-          d[2][cc] = fy(k2[cc], 2, e2 ? k3g : k3[cc]);
-          d[3][cc] = fy(k2[cc], 3, e3 ? k3g : k3[cc]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) d[q][cc] = fy(k2[cc], q, code == (uint32_t)q ? k3g : k3[cc]);
         }
       } else {
         const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;
         const bool pooled = gy >= 0 && gx >= 0 && (gy >> 1) < Q && (gx >> 1) < Q;
+        const uint32_t cw = av[u] >> (4 * (c4 & 3));
 #pragma unroll
         for (int cc = 0; cc < 4; ++cc) {
-          float m = ka[cc] * y[0][cc] + kb[cc];
-          int ai = 0;
-#pragma unroll
-          for (int q = 1; q < 4; ++q) {
-            const float z = ka[cc] * y[q][cc] + kb[cc];
-            if (z > m || isnan(z)) { m = z; ai = q; }  // first max in scan order, NaN wins (torch)
-          }
-          const int am = pooled ? ai : -1;
+          const int am = pooled ? (int)(((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u)) : -1;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int r = gy + (q >> 1), c = gx + (q & 1);
@@ -730,8 +719,9 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
 
 template <int DIAG, bool BIG>
 __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
-    const uint2* __restrict__ y2, const float* __restrict__ g2m, const float* __restrict__ aff2,
-    const float* __restrict__ kbuf, const float* __restrict__ b2, const uint32_t* __restrict__ mag,
+    const uint2* __restrict__ y2, const uint32_t* __restrict__ a2, const float* __restrict__ g2m,
+    const float* __restrict__ aff2, const float* __restrict__ kbuf, const float* __restrict__ b2,
+    const uint32_t* __restrict__ mag,
     const uint4* __restrict__ p1,
     const uint4* __restrict__ wdpack, uint2* __restrict__ dp1, uint32_t* __restrict__ dp1_dec, float* __restrict__ slab,
     const int* __restrict__ walk, int sw, int sk, int B, int P) {
@@ -739,7 +729,7 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
   const int tid = threadIdx.x;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   BRArgs a;
-  a.y2 = y2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.walk = walk;
+  a.y2 = y2; a.a2 = a2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.walk = walk;
   a.B = B; a.P = P; a.Q = P / 2;
   a.sk = sk;
   a.w = xcd_remap(blockIdx.x, gridDim.x);  // this workgroup's list (XCD-contiguous: neighbouring columns)
@@ -898,7 +888,8 @@ static int br_diag_env() { return 0; }
 
 // g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
 // [nwg][rows] (fused_ops.cpp bwd_walk)
-void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
+void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const float* aff2, const float* kbuf,
+                    const float* b2,
                     uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st) {
   const int Q = P / 2;
@@ -912,7 +903,7 @@ void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const 
       set = true;                                                                                                      \
     }                                                                                                                  \
     hipLaunchKernelGGL((conv2_bwd_roll_kernel<D, BG>), dim3(nwg), dim3(BR_THREADS), BR_LDS, st,                        \
-                       reinterpret_cast<const uint2*>(y2h), g2m, aff2, kbuf, b2, mag,                                    \
+                       reinterpret_cast<const uint2*>(y2h), a2, g2m, aff2, kbuf, b2, mag,                                \
                        reinterpret_cast<const uint4*>(p1),                                                            \
                        reinterpret_cast<const uint4*>(wd), static_cast<uint2*>(dp1h), mag + kMagScales + 4, slab, walk, \
                        sw, sk, B, P);                                                                                 \

@@ -28,11 +28,16 @@ constexpr int kMagScales = 40;  // mag[40] = 2^-ew (packed weights' scale), mag[
 // pixel, half of fp32): y2h = fp16(acc * 2^k), acc the bias-free MFMA accumulator (y2 = acc * inv
 // + b2), 2^k from conv2_pack: max_c sum |w_c| * 2^ew * 1.01 * 2^k <= 1, so with |p1 operand| <=
 // 65504 no value can overflow, and everything above 2^-14 of the fp16 grid keeps 11 significant
-// bits (TF32's).  Rounding is to nearest, except that each 2x2 pooling window's first extreme
-// (max for gamma2 >= 0, min for gamma2 < 0: the forward's argmax) is moved one fp16 step outward
-// when rounding made an earlier-scanned pixel of its window equal to it -- so the backward's
-// first-extreme scan over the stored values picks the forward's pixel (conv2_fwd2.hip
-// f2_keep_first).
+// bits (TF32's).  Rounding is to nearest.  The pooling argmax does not come from these values:
+// the forward stores it (a2 below), as max_pool2d_with_indices saves its indices for its backward.
+//
+// a2 [B][Q][Q][2] uint32 (Q = P / 2, the pooled windows): each 2x2 window's argmax in scan order
+// (0 = (0,0), 1 = (0,1), 2 = (1,0), 3 = (1,1)) of the forward's fp32 conv2 output -- the first
+// extreme, max for gamma2 >= 0 and min for gamma2 < 0 (BN2's affine is monotone in the sign of
+// gamma2, so this is the first max of the BN2 output) -- as 2-bit codes of 16 channels per word:
+// word h holds channels 16h .. 16h+15, bit c = code bit 0, bit 16 + c = code bit 1 of channel
+// 16h + c.  8 B per window (22.5 MB at the bench shape); written by conv2_fwd2, read by the
+// conv2 backward's staging.
 __device__ __forceinline__ uint32_t f16_bits(float x) {
   return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)x);
 }

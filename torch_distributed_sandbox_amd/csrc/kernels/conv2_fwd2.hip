@@ -50,7 +50,7 @@ constexpr bool F2_H16 = TDS_F2_WG == 3;
 constexpr int F2_PXREC = F2_H16 ? 32 * 2 + 16 : 32 * 4 + 16;  // staged pixel record: 32 co + 16 B pad (banks)
 constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;           // a finished tile's padded staging buffer
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
-constexpr int F2_YSTAGE = 32 * 32 * 4;                 // pooled block: 32 co x 4 x 8 fp32 = 4 KiB
+constexpr int F2_YSTAGE = 32 * 32 * 4 + 32 * 2 * 4;     // pooled block: 32 co x 4 x 8 fp32 = 4 KiB, + a2 words
 constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
 constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging
 constexpr int F2_DMA_PER_WAVE = F2_PGROUPS / (F2_THREADS / 64);  // 2
@@ -158,27 +158,6 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
   return neg ? mn : mx;
 }
 
-// y2h rounding of one pooling window (conv2_common.h): h0..h3 = fp16(v * 2^k) to nearest in scan
-// order, m = the window's extreme (f2_ext4).  The forward's argmax a is the first q with v_q == m;
-// to nearest, an earlier pixel can round to the same fp16 as a (a near-tie): then a moves one
-// step outward, strictly past it.  Rare and divergent: the branch costs ~nothing when no lane
-// ties.  (A NaN window takes the backward's NaN path, whatever is stored.)
-__device__ __forceinline__ void f2_keep_first(uint32_t& h0, uint32_t& h1, uint32_t& h2, uint32_t& h3, float v0,
-                                              float v1, float v2, float m, bool neg) {
-  const bool e0 = v0 == m, e1 = v1 == m, e2 = v2 == m;
-  const uint32_t ha = e0 ? h0 : e1 ? h1 : e2 ? h2 : h3;
-  const float ra = f16_val(ha);
-  const bool tie = !e0 && (f16_val(h0) == ra || (!e1 && (f16_val(h1) == ra || (!e2 && f16_val(h2) == ra))));
-  if (tie) {  // (if-converted; a wave-ballot skip measured no faster: tools/gpu_sessions/r4_s18.sh)
-    // outward = up (max window) / down (min window): +1 on the bits when the sign bit differs
-    // from the direction's, -1 otherwise (ha is finite: |v * 2^k| < 65504 by construction)
-    const uint32_t out = ((ha >> 15) & 1u) ^ (neg ? 0u : 1u) ? ha + 1u : ha - 1u;
-    if (e1) h1 = out;
-    else if (e2) h2 = out;
-    else h3 = out;
-  }
-}
-
 // stage + shifted statistics of one finished tile: lane holds C[px = 4g + r][co = 16NT + li].
 // EDGE: a tile reaching past the image (last tile row / column) masks its statistics; interior
 // tiles (all but ~1 %) accumulate unmasked, in packed fp32 (v_pk_add_f32 / v_pk_fma_f32: two
@@ -189,7 +168,7 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 template <bool EDGE>
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
                                          int RH, int NT, int lane, float bco, float inv, float ksc, bool neg,
-                                         f2v& s_acc, f2v& q_acc, uint32_t& ymx) {
+                                         f2v& s_acc, f2v& q_acc, uint32_t& ymx, uint32_t* __restrict__ a2) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
   float ymf = 0.f;
@@ -227,19 +206,36 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
   // pooled windows (rows 4RH + 2i + {0,1}, columns 4g + 2j + {0,1}) -> ya block entry
   // (prow 2RH + i, pcol 2g + j); v -> v * inv + b2 is monotone (inv > 0) and rounds monotonically,
   // so ext(v) * inv + b2 == ext(v * inv + b2)
+  // and the argmax codes (a2, conv2_common.h): the first extreme in scan order, two code bits per
+  // channel gathered by ballots (lane = 16 g + li: channel 16NT + li of window column 2g + j)
+  uint64_t cb0[4], cb1[4];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     float e[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const float m = f2_ext4(acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], acc[2 * i + 1][2 * j + 1],
-                              neg);
+      const float v0 = acc[2 * i][2 * j], v1 = acc[2 * i][2 * j + 1], v2 = acc[2 * i + 1][2 * j];
+      const float m = f2_ext4(v0, v1, v2, acc[2 * i + 1][2 * j + 1], neg);
       e[j] = fmaf(m, inv, bco);
-      f2_keep_first(h[2 * i][2 * j], h[2 * i][2 * j + 1], h[2 * i + 1][2 * j], h[2 * i + 1][2 * j + 1],
-                    acc[2 * i][2 * j], acc[2 * i][2 * j + 1], acc[2 * i + 1][2 * j], m, neg);
+      const bool e0 = v0 == m, e1 = v1 == m, e2 = v2 == m;  // (a NaN window: code 3, unused)
+      cb0[2 * i + j] = __builtin_amdgcn_ballot_w64(!e0 & (e1 | !e2));  // code 1 or 3
+      cb1[2 * i + j] = __builtin_amdgcn_ballot_w64(!e0 & !e1);         // code 2 or 3
     }
     // pcols 2g, 2g+1 are adjacent floats of one swizzled chunk: one ds_write_b64
     *reinterpret_cast<float2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_float2(e[0], e[1]);
+  }
+  // lane li = 0 of group g stages the 4 windows (2RH + i, 2g + j) in LDS after the pooled block
+  // (word = bits 16g .. 16g+15 of each code-bit ballot: channels 16NT + 0..15); f2_store_a2 writes
+  // the tile's 32 windows as 4 rows of 64 B
+  {
+    const uint32_t sh = 16u * (uint32_t)g;
+    uint32_t* ab = reinterpret_cast<uint32_t*>(ystage + 32 * 32);
+    if (li == 0) {
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl)
+        ab[((2 * RH + (sl >> 1)) * 8 + 2 * g + (sl & 1)) * 2 + NT] =
+            ((uint32_t)(cb0[sl] >> sh) & 0xFFFFu) | ((uint32_t)(cb1[sl] >> sh) << 16);
+    }
   }
   if constexpr (F2_H16) {
     // the y2h halves: even lanes join their odd neighbour's (channel co + 1) by a quad-permute DPP
@@ -271,6 +267,15 @@ __device__ __forceinline__ void f2_store_ya(const float* ystage, const F2Tile& x
   const int e = threadIdx.x, co = e >> 3, part = e & 7;
   const float4 v = *reinterpret_cast<const float4*>(ystage + f2_ystage_off(co, part * 4));
   st_stream(reinterpret_cast<float4*>(ya + ((((int64_t)x.b * 32 + co) * pg.Q4 + tr) * pg.Q8 + tc) * 32 + part * 4), v);
+}
+
+// the tile's 32 pooling windows' argmax words (a2, conv2_common.h): thread e < 32 -> window e
+__device__ __forceinline__ void f2_store_a2(const float* ystage, const F2Tile& x, uint32_t* __restrict__ a2, int P) {
+  const int e = threadIdx.x, Q = P >> 1;
+  const int py = (x.r0 >> 1) + (e >> 3), px = (x.c0 >> 1) + (e & 7);
+  if (e < 32 && py < Q && px < Q)  // (non-temporal, as y2h: dirty lines left to the head forward cost it ~5 us)
+    st_stream(reinterpret_cast<uint2*>(a2 + (((int64_t)x.b * Q + py) * Q + px) * 2),
+              reinterpret_cast<const uint2*>(ystage + 32 * 32)[e]);
 }
 
 // the whole workgroup stores a staged tile as y2h: thread e, i -> 8 channels q = e + 256 i of
@@ -313,6 +318,7 @@ template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
                                        const float* __restrict__ bias, const float* __restrict__ gamma,
                                        unsigned short* __restrict__ y2, float* __restrict__ ya,
+                                       uint32_t* __restrict__ a2,
                                        double* __restrict__ partial, uint32_t* __restrict__ ypart,
                                        const uint32_t* __restrict__ scales,
                                        const int* __restrict__ order, int sw, int sk, int B, int P, char* smem) {
@@ -362,14 +368,15 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     if (have_prev) {
       f2_store<DIAG>(smem + F2_OFF_S + ((kk + 1) & 1) * F2_STAGE, prev, y2, P);
       f2_store_ya(ys + ((kk + 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
+      f2_store_a2(ys + ((kk + 1) & 1) * (F2_YSTAGE / 4), prev, a2, P);
     }
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
     if (cur.r0 + F2_TH <= P && cur.c0 + F2_TC <= P)  // tile-uniform
       f2_stage<false>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
-                      bco, inv, ksc, neg, s_acc, q_acc, ymx);
+                      bco, inv, ksc, neg, s_acc, q_acc, ymx, a2);
     else
       f2_stage<true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
-                     bco, inv, ksc, neg, s_acc, q_acc, ymx);
+                     bco, inv, ksc, neg, s_acc, q_acc, ymx, a2);
     prev = cur;
     have_prev = true;
   }
@@ -377,6 +384,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   if (have_prev) {
     f2_store<DIAG>(smem + F2_OFF_S + ((kk - 1) & 1) * F2_STAGE, prev, y2, P);
     f2_store_ya(ys + ((kk - 1) & 1) * (F2_YSTAGE / 4), prev, ya, pg);
+    f2_store_a2(ys + ((kk - 1) & 1) * (F2_YSTAGE / 4), prev, a2, P);
   }
   // max |acc| of channel 16NT + li over the 4 lane groups (then the two waves of this co half)
   ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 16, 64));
@@ -416,6 +424,7 @@ __global__ __launch_bounds__(F2_THREADS, TDS_F2_WG) void conv2_fwd2_kernel(const
                                                                    const float* __restrict__ bias,
                                                                    const float* __restrict__ gamma,
                                                                    unsigned short* __restrict__ y2, float* __restrict__ ya,
+                                                                   uint32_t* __restrict__ a2,
                                                                    double* __restrict__ partial,
                                                                    uint32_t* __restrict__ ypart,
                                                                    const uint32_t* __restrict__ scales,
@@ -423,10 +432,10 @@ __global__ __launch_bounds__(F2_THREADS, TDS_F2_WG) void conv2_fwd2_kernel(const
                                                                    int B, int P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
-  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
-  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
-  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
-  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P, smem);
+  if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
+  else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
+  else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
+  else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
 }
 
 }  // namespace tds
@@ -455,7 +464,7 @@ static int f2_diag_env() { return 0; }
 // order: the blocked tile order table (tds_tile_order_fill) as per-workgroup lists [nwg][ceil(total / nwg)]
 // (fused_ops.cpp tile_order, sw / sk: the strides of workgroup / tile), allocated by the caller
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
-                    double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
+                    uint32_t* a2, double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
                     int B, int P, hipStream_t st) {
   const dim3 grid(nwg), block(F2_THREADS);
   unsigned short* y2 = static_cast<unsigned short*>(y2h);
@@ -475,12 +484,12 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const fl
   }
   switch (f2_diag_env()) {
 #ifdef TDS_DIAG
-    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
-    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
-    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
-    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
 #endif
-    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, partial, ypart, scales, order, sw, sk, B, P); break;
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
   }
   TDS_LAUNCH_CHECK();
 }

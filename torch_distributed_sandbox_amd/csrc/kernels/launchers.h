@@ -84,11 +84,11 @@ void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, fl
 int tds_conv2_fwd2_num_wg();  // BN2 partial rows the forward writes (workgroups it launches)
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
 // y2h [B,P,P,32] fp16 (conv2_common.h); ya pooled-blocked (pooled_layout.h), max/min of each 2x2
-// window of y2 by sign(gamma2)
+// window of y2 by sign(gamma2); a2 [B][P/2][P/2][2]: the windows' argmax codes (conv2_common.h)
 // ypart (optional): max |y2 - b2| per (channel, workgroup), [32][nwg] float bits
 // scales (optional): mag + kMagScales (conv2_pack.hip), the packed weights' and p1's inverse scales
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
-                    double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
+                    uint32_t* a2, double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
                     int B, int P, hipStream_t st);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
@@ -96,7 +96,8 @@ void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // mag: the forward's / head backward's magnitude bounds (the fp16 scale of dy2) and the y2h
 // decode (conv2_common.h); b2: conv2.bias (y2h is bias-free)
 // dp1h [B][P][ceil(P/4)][16][4] fp16 (conv2_common.h); its decode factor goes to mag[kMagScales + 4]
-void tds_conv2_bwd3(const void* y2h, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
+// a2: the forward's pooling argmax codes (conv2_common.h)
+void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
                     uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st);
 // host: per-workgroup tile lists of vertical segments of ~seg tiles; out == nullptr -> length

@@ -179,8 +179,9 @@ class _Conv2(torch.autograd.Function):
         # backward, reduced by its BN2 finalize): the conv2 backward's fp16 scale of dy2
         link.mag = torch.empty(ops.mag_numel(p1.shape[0], p1.shape[1]), device=p1.device, dtype=torch.int32)
         wp, wd = ops.conv2_pack(w2.contiguous(), link.mag, getattr(link1, "p1_scale", None))
-        y2, partial2, ya = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
-        ctx.save_for_backward(p1, wd, y2)
+        # a2: each pooling window's argmax, saved for the backward (max_pool2d_with_indices' indices)
+        y2, partial2, ya, a2 = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
+        ctx.save_for_backward(p1, wd, y2, a2)
         ctx.params = (w2, b2)
         ctx.link = link
         ctx.link1 = link1
@@ -191,11 +192,11 @@ class _Conv2(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, _dy2_placeholder, _unused, _unused_ya):
-        p1, wd, y2 = ctx.saved_tensors
+        p1, wd, y2, a2 = ctx.saved_tensors
         link = ctx.link
         _run_before_conv2_backward()
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
-        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, link.g2m, link.aff2, link.kbuf, ctx.params[1], link.mag,
+        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, a2, link.g2m, link.aff2, link.kbuf, ctx.params[1], link.mag,
                                                            p1, wd, 1.0, *_sinks(ctx, ctx.params, 1))
         mag = link.mag
         link.g2m = link.kbuf = link.aff2 = link.mag = None
