@@ -55,6 +55,9 @@ ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 # forward 0.621 -> 0.588 ms, bench 3.327 -> 3.112 ms/step.  (convnet_fused.hip keeps it: its
 # layer-1 backward ran 0.31 -> 0.36 ms without.)
 HIP_FILE_FLAGS = {
+    # MFMA results straight into VGPRs: the layer-1 epilogues read every accumulator back
+    # (v_accvgpr_read_b32 x 64 per tile and wave with the default AGPR form)
+    "convnet_fused.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"],
     "x_autocorr.hip": ["-fno-slp-vectorize"],
     "conv2_bwd.hip": ["-fno-slp-vectorize"],
     "conv2_fwd2.hip": ["-fno-slp-vectorize"],

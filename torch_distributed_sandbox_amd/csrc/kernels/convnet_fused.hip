@@ -279,16 +279,30 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
         uint32_t ixw = 0;
         // scan order: (row 0, col 0), (row 0, col 1), (row 1, col 0), (row 1, col 1)
         if (!slow) {  // every z finite (tile-uniform)
+          // the affine in packed fp32 (v_pk_fma_f32 on channel pairs r, r+1 of one accumulator:
+          // adjacent registers as the MFMA left them, no moves; this epilogue, not the MFMAs,
+          // bounds the kernel)
+          float z[2][2][4];
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+#pragma unroll
+              for (int r = 0; r < 4; r += 2) {
+                const f32x2 zz = __builtin_elementwise_fma(f32x2{acc[a][c][r], acc[a][c][r + 1]},
+                                                           f32x2{ea[r], ea[r + 1]}, f32x2{ebb[r], ebb[r + 1]});
+                z[a][c][r] = zz.x;
+                z[a][c][r + 1] = zz.y;
+              }
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            // the affine in packed fp32 (v_pk_fma_f32: two window pixels per instruction; this
-            // epilogue, not the MFMAs, bounds the kernel)
-            const f32x2 ea2 = {ea[r], ea[r]}, eb2 = {ebb[r], ebb[r]};
-            const f32x2 zt = __builtin_elementwise_fma(f32x2{acc[0][0][r], acc[0][1][r]}, ea2, eb2);
-            const f32x2 zb = __builtin_elementwise_fma(f32x2{acc[1][0][r], acc[1][1][r]}, ea2, eb2);
-            const float z0 = zt.x, z1 = zt.y, z2 = zb.x, z3 = zb.y;
-            const float m = fmaxf(fmaxf(z0, z1), fmaxf(z2, z3));
-            const uint32_t am = z0 == m ? 0u : z1 == m ? 1u : z2 == m ? 2u : 3u;  // first max
+            const float z0 = z[0][0][r], z1 = z[0][1][r], z2 = z[1][0][r], z3 = z[1][1][r];
+            const float m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(z0, z1),
+                                                          __builtin_elementwise_maximum(z2, z3));
+            // first max, branch-free (the ?: chain compiled to exec-mask branches)
+            uint32_t am = z2 == m ? 2u : 3u;
+            am = z1 == m ? 1u : am;
+            am = z0 == m ? 0u : am;
             pv[r] = fmaxf(m, 0.f);
             ixw |= (am | (m > 0.f ? 4u : 0u)) << (8 * r);
           }
