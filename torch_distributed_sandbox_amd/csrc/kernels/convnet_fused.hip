@@ -538,7 +538,10 @@ constexpr int LM_X_BYTES = (LB_XR * LM_XS > LV_WORDS ? LB_XR * LM_XS : LV_WORDS)
 // H16 (level input, word layout): dz1 * x on ONE v_mfma_f32_16x16x32_f16 per product instead of
 // the bf16 pair (dz hi, dz lo): dz1 is dp1h's fp16 value as stored and a level (0..255) is exact
 // in fp16, so every product is exact either way; the A operand is the fp16 bits themselves (no
-// conversion, no bf16 split) and the MFMA count halves.  x words: fp16(level) << 16.
+// conversion, no bf16 split) and the MFMA count halves.  x words are PAIRS: word c = fp16 x[c] |
+// fp16 x[c+1] << 16 (the l1_conv layout), so a window row's two B slots (dc = 0, 1) are one
+// ds_read_b32 at the dc = 0 address -- 4 reads and no v_perm per operand; the ones block holds
+// the pair (1.0, 1.0).
 #ifndef TDS_L1B_H16
 #define TDS_L1B_H16 1
 #endif
@@ -589,7 +592,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   constexpr bool H16 = LV && !PAIRS && TDS_L1B_H16;
   if (!(LV && PAIRS))  // the ones block (never overwritten: the x tile uses columns 0..71)
     for (int e = tid; e < LB_XR * (LM_XS - 72); e += 256)  // bf16 1.0 | lo 0, or fp16 1.0 << 16
-      xs[(e / (LM_XS - 72)) * LM_XS + 72 + e % (LM_XS - 72)] = H16 ? 0x3C000000u : 0x3F800000u;
+      xs[(e / (LM_XS - 72)) * LM_XS + 72 + e % (LM_XS - 72)] = H16 ? 0x3C003C00u : 0x3F800000u;
   const float* __restrict__ x = static_cast<const float*>(xv);
   const uint8_t* __restrict__ xl = static_cast<const uint8_t*>(xv);
   uint4 pre[LB_PER];
@@ -621,9 +624,11 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
         const int gr = 2 * pr0 - 2 + rr, gcol = 2 * pc0 - 4 + 4 * cv;
         const bool ok = (ex < LB_V_X) & ((uint32_t)gr < (uint32_t)H) & ((uint32_t)gcol < (uint32_t)W);
         const int64_t o = ((int64_t)b * H + gr) * W + gcol;
-        if constexpr (LV) {  // 4 levels in .x
+        if constexpr (LV) {  // 4 levels in .x; H16: the next 4 in .y (the pair words' right neighbours)
           const uint32_t* src = ok ? reinterpret_cast<const uint32_t*>(xl + o) : &g_l1b_zero.x;
-          pre[u] = make_uint4(*src, 0u, 0u, 0u);
+          const bool okn = (ex < LB_V_X) & (cv < 17) & ((uint32_t)gr < (uint32_t)H) & ((uint32_t)(gcol + 4) < (uint32_t)W);
+          const uint32_t* srn = okn ? reinterpret_cast<const uint32_t*>(xl + o + 4) : &g_l1b_zero.x;
+          pre[u] = make_uint4(*src, H16 ? *srn : 0u, 0u, 0u);
         } else {
           const uint4* src = ok ? reinterpret_cast<const uint4*>(x + o) : &g_l1b_zero;
           pre[u] = *src;
@@ -646,10 +651,12 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
       else if (e < LB_V) {
         e -= LB_V_DP + LB_V_PH + LB_V_ID;
         const int rr = e / 18, cv = e - rr * 18;
-        if constexpr (H16) {  // word = fp16(level) << 16 (exact)
+        if constexpr (H16) {  // pair words: fp16 x[c] | fp16 x[c+1] << 16 (levels are exact)
           const uint32_t q = pre[u].x;
-          auto h = [](uint32_t l) { return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)(float)l) << 16; };
-          lb_store4(xs + rr * LM_XS + 4 * cv, make_uint4(h(q & 0xFFu), h((q >> 8) & 0xFFu), h((q >> 16) & 0xFFu), h(q >> 24)));
+          auto h = [](uint32_t l) { return (uint32_t)__builtin_bit_cast(unsigned short, (_Float16)(float)l); };
+          const uint32_t h0 = h(q & 0xFFu), h1 = h((q >> 8) & 0xFFu), h2 = h((q >> 16) & 0xFFu), h3 = h(q >> 24);
+          const uint32_t h4 = h(pre[u].y & 0xFFu);
+          lb_store4(xs + rr * LM_XS + 4 * cv, make_uint4(h0 | h1 << 16, h1 | h2 << 16, h2 | h3 << 16, h3 | h4 << 16));
           continue;
         }
         if constexpr (LV && !PAIRS) {  // word = fp32 bits of the level = bf16 hi | lo 0
@@ -716,14 +723,16 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
           // pooled columns 8sg + 2g + {0, 1}: column group 2sg + (g >> 1), pixels 2(g & 1) + {0, 1} --
           // one dword (a 32-lane half reads 32 consecutive words: conflict-free)
           const uint32_t dpair = dps[((rp * 8 + 2 * sg + (g >> 1)) * 16 + li) * 2 + (g & 1)];
-          if constexpr (H16) {  // fp16 bits at the argmax slot, zero where ReLU blocks the gradient
+          if constexpr (H16) {  // fp16 bits at the argmax slot, zero where ReLU blocks the gradient;
+            // K order here: dword 2 dr + wi = (window wi, row dr), halves dc = 0, 1 (the B reads'
+            // order: ds_read2_b32 pairs (wi 0, 1) of one row land in consecutive registers)
 #pragma unroll
             for (int wi = 0; wi < 2; ++wi) {
               const uint32_t ab = ids[(rp * LB_PC + 8 * sg + 2 * g + wi) * 16 + li];
               const uint32_t hb = (ab & 4u) ? ((dpair >> (16 * wi)) & 0xFFFFu) : 0u;
-              const uint64_t h64 = (uint64_t)hb << (16u * (ab & 3u));
-              hp[2 * wi] = (uint32_t)h64;
-              hp[2 * wi + 1] = (uint32_t)(h64 >> 32);
+              const uint32_t hs = hb << (16u * (ab & 1u));
+              hp[wi] = (ab & 2u) ? 0u : hs;
+              hp[2 + wi] = (ab & 2u) ? hs : 0u;
             }
           } else
 #pragma unroll
@@ -761,6 +770,13 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
           const int bo = base + boff[blk];
+          if constexpr (H16) {  // dword 2 dr + wi = (window wi, row dr), cols dc = 0, 1: one pair word
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const s16x8 bp = __builtin_bit_cast(
+                s16x8, u32x4{xs[bo], xs[bo + 2], xs[bo + LM_XS], xs[bo + LM_XS + 2]});
+            acc[blk] = mfma_f16(ah, bp, acc[blk]);
+            continue;
+          }
           uint32_t u[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
