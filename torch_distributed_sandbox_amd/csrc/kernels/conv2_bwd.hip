@@ -572,10 +572,19 @@ struct BRStager {
             return TDS_BR_MIX ? br_fma_y(k, yv[u][q], cc, c) : fmaf(k, y[q][cc], c);
           };
           const uint32_t code = ((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u);  // the forward's argmax
-          // the pooled gradient folded into the constant: select + FMA per pixel
+          // the pooled gradient folded into the constant: select + FMA per pixel.  The 4 compares
+          // go first (4 SGPR-pair masks): one VCC reused compare -> select -> compare cost an
+          // s_nop per pixel for the VALU-mask hazard
           const float k3g = fmaf(k1[cc], gg[cc], k3[cc]);
+          bool eq[4];
 #pragma unroll
-          for (int q = 0; q < 4; ++q) d[q][cc] = fy(k2[cc], q, code == (uint32_t)q ? k3g : k3[cc]);
+          for (int q = 0; q < 4; ++q) eq[q] = code == (uint32_t)q;
+#ifndef TDS_BR_BATCH_CMP
+#define TDS_BR_BATCH_CMP 1
+#endif
+          if constexpr (TDS_BR_BATCH_CMP != 0) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) d[q][cc] = fy(k2[cc], q, eq[q] ? k3g : k3[cc]);
         }
       } else {
         const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;
