@@ -260,7 +260,7 @@ constexpr int64_t kMagParts = 64;   // ypart offset in the mag workspace
 constexpr int64_t kMagScales = 40;  // conv2 epilogue scales (csrc/kernels/conv2_common.h)
 int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
 int64_t mag_gpart_count(int64_t B, int64_t P) {
-  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_pb_nblk((int)(P / 2));
+  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_bwd_pb_nblk((int)(P / 2));
 }
 int64_t mag_numel(int64_t B, int64_t P) { return kMagParts + 32 * mag_ypart_count() + mag_gpart_count(B, P); }
 
@@ -398,7 +398,7 @@ Tensor conv2_bwd_clock_dump(int64_t nwg) {
 
 int64_t head_bwd_workspace(int64_t B, int64_t P) {
   const int Q = (int)(P / 2);
-  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_pb_nblk(Q) * 2;
+  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_bwd_pb_nblk(Q) * 2;
 }
 
 // Channels [c_begin, c_end) of the head backward (K-chunked fc gradient): the caller passes the
@@ -449,7 +449,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into g2m_out");
     g2m = at::empty({B, 32, Q, Q}, ya.options());  // planar (the fc flatten order)
   }
-  const int nblk = tds_head_pb_nblk((int)Q), npass = tds_head_bwd_pb_npass((int)B);
+  const int nblk = tds_head_bwd_pb_nblk((int)Q), npass = tds_head_bwd_pb_npass((int)B);
   Tensor partial;
   if (partial_out.has_value() && partial_out->defined()) {
     need(*partial_out, at::kDouble, {head_bwd_workspace(B, P)}, "partial_out");

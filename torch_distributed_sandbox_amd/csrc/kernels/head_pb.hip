@@ -38,7 +38,16 @@
 namespace tds {
 
 constexpr int HP_THREADS = 256;
-constexpr int HP_BAND = 4;                  // block rows per workgroup
+#ifndef TDS_HP_BAND
+#define TDS_HP_BAND 4
+#endif
+constexpr int HP_BAND = TDS_HP_BAND;        // block rows per workgroup (forward)
+// the backward's band: 2 block rows (r4_s43: 2 / 4 / 8 -> backward 0.448 / 0.457 / 0.505 ms,
+// forward 0.227 / 0.212 / 0.232 -- each direction takes its best)
+#ifndef TDS_HP_BAND_B
+#define TDS_HP_BAND_B 2
+#endif
+constexpr int HP_BAND_B = TDS_HP_BAND_B;
 constexpr int HP_MAXB = 8;                  // images per pass (larger batches run in passes)
 
 struct HPGrid {
@@ -47,6 +56,7 @@ struct HPGrid {
 };
 
 __host__ __device__ inline HPGrid hp_grid(const PBGeom& g) { return HPGrid{(g.Q4 + HP_BAND - 1) / HP_BAND}; }
+__host__ __device__ inline HPGrid hp_grid_b(const PBGeom& g) { return HPGrid{(g.Q4 + HP_BAND_B - 1) / HP_BAND_B}; }
 
 __device__ __forceinline__ float hp_relu(float z) { return z > 0.f ? z : (isnan(z) ? z : 0.f); }
 
@@ -292,7 +302,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     int NC, float scale, float lr, int c0, uint32_t* __restrict__ gpart) {
   __shared__ float red[2][HP_THREADS / 64];
   __shared__ uint32_t gred[HP_THREADS / 64];
-  const HPGrid hg = hp_grid(g);
+  const HPGrid hg = hp_grid_b(g);
   // workgroups in the reverse of the forward's order: the backward starts on the channels the
   // forward streamed last, whose ya / weight lines are still in the 256 MB Infinity Cache
 #ifndef TDS_HPB_REV
@@ -311,7 +321,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   float sdz = 0.f, sdy = 0.f;
   uint32_t gmx = 0u;  // max |g2m| bits
   const int nch = (g.Q8 + 31) / 32;
-  const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
+  const int R0 = band * HP_BAND_B, nit = (min(g.Q4, R0 + HP_BAND_B) - R0) * nch;
   // two load sets in alternation, as in the forward
   HPLoad<NB> ld0, ld1;
   auto issue = [&](HPLoad<NB>& L, int i) {
@@ -420,7 +430,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
 
 using namespace tds;
 
-int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // workgroups per channel
+int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // forward workgroups per channel
+int tds_head_bwd_pb_nblk(int Q) { return hp_grid_b(pb_geom(Q)).per_channel(); }  // backward workgroups per channel
 int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
 
 // partial: double [32 * nblk][B*NC]; sums: double [B*NC]
@@ -459,7 +470,7 @@ int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const 
   const int npass = tds_head_bwd_pb_npass(B);
   if (Wupd && npass != 1) return -2;  // the fused SGD step needs the whole dW in one pass
   const PBGeom g = pb_geom(Q);
-  const int nwg = (c1 - c0) * hp_grid(g).per_channel();
+  const int nwg = (c1 - c0) * hp_grid_b(g).per_channel();
   for (int pass = 0; pass < npass; ++pass) {
     const int b0 = pass * HP_MAXB;
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;

@@ -146,6 +146,7 @@ void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const
 // ---- head_pb.hip (fc head on the pooled-blocked ya / g2m, pooled_layout.h)
 int64_t tds_pb_plane(int Q);  // floats per (image, channel) plane
 int tds_head_pb_nblk(int Q);  // workgroups per channel
+int tds_head_bwd_pb_nblk(int Q);  // the backward's workgroups per channel (its partial / gpart rows)
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st);
 int tds_head_bwd_pb_npass(int B);
