@@ -66,15 +66,15 @@ Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shap
 #endif
 int l1_wg() { return tds_fused_num_wg(TDS_L1_PER_CU); }
 
-// layer-1 backward workgroups per CU: 4 waves each, <= 128 VGPRs (__launch_bounds__(256, 3) keeps the
-// kernel at 124-126), so 4 fit a CU.  Same-box A/B (tools/gpu_sessions/r3_s21.sh): 4 -> 0.318 ms,
-// 3 -> 0.351 ms (level input); bench 2.889 / 2.911 vs 2.933 / 2.937 ms per step.  TDS_L1B_PER_CU
+// layer-1 backward workgroups per CU: 4 waves each.  Round 3 (124-126 VGPRs, 4 fit a CU): 4 -> 0.318
+// ms, 3 -> 0.351 ms (tools/gpu_sessions/r3_s21.sh).  Round 4's fp16 weight gradient runs at 87
+// VGPRs, so 5 fit (<= 102): 4 / 5 / 6 -> 0.143 / 0.138 / 0.145 ms (r4_s47.sh).  TDS_L1B_PER_CU
 // overrides it (A/B sweeps only).
 int l1b_wg() {
   static const int per_cu = [] {
     const char* e = std::getenv("TDS_L1B_PER_CU");
     const int v = e ? std::atoi(e) : 0;
-    return v >= 1 && v <= 8 ? v : 4;
+    return v >= 1 && v <= 8 ? v : 5;
   }();
   return tds_fused_num_wg(per_cu);
 }
