@@ -420,6 +420,10 @@ def _run_attempts(args, world: int, rank: int, phase):
         if rec is not None:
             rec["config"]["tier"] = f"{k + 1}/{len(attempts)}"
         if store is None or len(attempts) == 1:
+            if store is not None:
+                # the communicator goes down here, not in the static destructors at exit (under
+                # rocprofv3 those ran after the runtime's own teardown and crashed the process)
+                _teardown(abort=False)
             return rec
         # every rank reports its attempt; all take the same decision
         phase[0] = f"vote after attempt {k}"

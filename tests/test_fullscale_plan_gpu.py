@@ -1,0 +1,138 @@
+"""Full-scale numerics of the exact plan bench.py times (3000x3000, batch 5, one MI355X): two
+training steps of ``DistributedDataParallel(ConvNet, overlap_optimizer=True)`` at world size 1 on
+uint8 LEVEL input, ``SGD(lr=1e-4)`` attached to the wrapper -- the reference's step
+(mnist_onegpu.py:68-74: forward, loss, zero_grad, backward, step) through the kernels the bench
+runs: the level variants of the layer-1 kernels (``l1_conv_bf3<true>``, ``l1_bwd_mfma<true,..>``),
+the TF32-class conv2 kernels and the fc SGD step fused into ``head_bwd_pb<..,UPD>`` (the fc weight's
+gradient is never materialised: ``fc.weight.grad`` stays None), with the deferred parameter fence
+between the steps.
+
+After each step the loss, the logits, every parameter and the BN running buffers are compared
+with two references run in fp64 on the same weights and batches (unfold + GEMM convolutions, SGD
+in fp64): exact operands, and the reference's own precision class (TF32-rounded convolution
+operands, cuDNN's default ``allow_tf32``).  A parameter's error is measured against the size of
+its update (the test bounds ``|p_ours - p_64|`` by the gradient tolerance of
+tests/test_fullscale_gpu.py times ``|p_64 - p_0|``, plus the fp32 storage floor of the parameter,
+or by 1.5x the TF32 reference's error).  The errors are printed (``-s``) and quoted in
+docs/KERNELS.md ("Full-scale numerics of the benchmarked plan")."""
+import pytest
+import torch
+
+from _tf32ref import unfold_conv as _unfold_conv
+from test_fullscale_gpu import GRAD_TOL
+from test_model_gpu import RefConvNet
+
+pytestmark = pytest.mark.gpu
+
+H, B, LR, STEPS = 3000, 5, 1e-4, 2
+
+
+def _ref_run(state, xs, ys, tf32):
+    """Two fp64 SGD steps of the reference model (train mode, BN batch statistics)."""
+    import torch.nn.functional as F
+
+    from torch_distributed_sandbox_amd.models import fc_in_features
+    from torch_distributed_sandbox_amd.models.convnet import to_image
+
+    dev = xs[0].device
+    ref = RefConvNet(fc_in_features((H, H))).to(dev).double()
+    ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in state.items()})
+    for layer in (ref.layer1, ref.layer2):
+        layer[0].forward = _unfold_conv(layer[0], tf32_operands=tf32)
+    out = []
+    for x, y in zip(xs, ys):
+        logits = ref(to_image(x).double())
+        loss = F.cross_entropy(logits, y)
+        ref.zero_grad(set_to_none=True)
+        loss.backward()
+        with torch.no_grad():
+            for p in ref.parameters():
+                p -= LR * p.grad
+        torch.cuda.synchronize()
+        out.append({"logits": logits.detach(), "loss": loss.detach(),
+                    "params": {n: p.detach().clone() for n, p in ref.named_parameters()},
+                    "buffers": {n: b.detach().clone() for n, b in ref.named_buffers()}})
+    del ref
+    torch.cuda.empty_cache()
+    return out
+
+
+def _norm(t):
+    return t.double().norm().item()
+
+
+@pytest.mark.timeout(900)
+def test_two_steps_of_the_benchmarked_plan_vs_fp64(gpu):
+    from torch_distributed_sandbox_amd.data import synthetic_batch
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
+    from torch_distributed_sandbox_amd.ops import functional as TF
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    model = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    state0 = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    opt = SGD(model.parameters(), LR)
+    crit = CrossEntropyLoss()
+    ddp = DistributedDataParallel(model, device_ids=[0], overlap_optimizer=True)
+    ddp.attach_optimizer(opt)
+    src, lab = synthetic_batch(B * STEPS, (H, H), gpu, seed=1234)
+    xs = [TF.upsample_bilinear_u8(src[i * B:(i + 1) * B], H, H, levels=True) for i in range(STEPS)]
+    ys = [lab[i * B:(i + 1) * B] for i in range(STEPS)]
+    assert all(x.dtype == torch.uint8 for x in xs)
+
+    ours = []
+    for x, y in zip(xs, ys):
+        out = ddp(x)
+        loss = crit(out, y)
+        opt.zero_grad()
+        TF.backward(loss)
+        opt.step()
+        ddp.wait_pending_updates()
+        torch.cuda.synchronize()
+        # optimizer-in-backward at world 1: the fc step ran inside the head backward kernel
+        assert model.fc.weight.grad is None
+        ours.append({"logits": out.detach().clone(), "loss": loss.detach().clone(),
+                     "params": {n: p.detach().clone() for n, p in model.named_parameters()},
+                     "buffers": {n: b.detach().clone() for n, b in model.named_buffers()}})
+    assert ddp.fc_grad_path() == "local"
+    del ddp, model, opt
+    torch.cuda.empty_cache()
+
+    r64 = _ref_run(state0, xs, ys, tf32=False)
+    rtf = _ref_run(state0, xs, ys, tf32=True)
+
+    print(f"\nbenchmarked plan, {STEPS} steps at {H}x{H}, B={B}, SGD(lr={LR:g}), level input")
+    for s in range(STEPS):
+        o, a, t = ours[s], r64[s], rtf[s]
+        scale = a["logits"].abs().max().item()
+        e_log = (o["logits"].double() - a["logits"]).abs().max().item() / scale
+        e_log_tf = (t["logits"] - a["logits"]).abs().max().item() / scale
+        e_loss = abs(o["loss"].item() - a["loss"].item()) / abs(a["loss"].item())
+        e_loss_tf = abs(t["loss"].item() - a["loss"].item()) / abs(a["loss"].item())
+        print(f" step {s}: loss {o['loss'].item():.6f} (fp64 {a['loss'].item():.6f}); logits err {e_log:.3e} "
+              f"(TF32 ref {e_log_tf:.3e}); loss err {e_loss:.3e} (TF32 ref {e_loss_tf:.3e})")
+        assert e_log <= max(1e-4, 1.5 * e_log_tf), (s, e_log)
+        assert e_loss <= max(1e-4, 1.5 * e_loss_tf), (s, e_loss)
+        print(f"   {'parameter':18s} {'|ours-64|/|upd|':>16s} {'|tf32-64|/|upd|':>16s} {'fp32 floor/|upd|':>17s}")
+        for n, p64 in a["params"].items():
+            upd = max(_norm(p64 - state0[n].double()), 1e-300)  # this step's and the earlier steps' updates
+            e = _norm(o["params"][n].double() - p64)
+            e_tf = _norm(t["params"][n] - p64)
+            floor = 3.0 * (s + 1) * _norm(p64.float().double() - p64)
+            print(f"   {n:18s} {e / upd:16.3e} {e_tf / upd:16.3e} {floor / upd:17.3e}")
+            if n in ("layer1.0.bias", "layer2.0.bias"):
+                # conv bias before train-mode BN: analytically zero gradient, the update is
+                # rounding noise on every side; bounded by the matching weight's update
+                wupd = _norm(a["params"][n.replace("bias", "weight")] - state0[n.replace("bias", "weight")].double())
+                assert e <= 1e-3 * wupd + floor, (s, n, e)
+                continue
+            assert e <= max(GRAD_TOL[n] * upd + floor, 1.5 * e_tf + floor), (s, n, e / upd)
+        for n, b64 in a["buffers"].items():
+            if n.endswith("num_batches_tracked"):
+                assert int(o["buffers"][n].item()) == int(b64.item()) == s + 1, n
+                continue
+            e = _norm(o["buffers"][n].double() - b64)
+            e_tf = _norm(t["buffers"][n] - b64)
+            print(f"   {n:26s} |ours-64| {e:.3e}  |tf32-64| {e_tf:.3e}  |64| {_norm(b64):.3e}")
+            assert e <= max(1.5 * e_tf, 2e-6 * _norm(b64)), (s, n, e, e_tf)

@@ -108,7 +108,7 @@ def main():
                 continue
             res[name] = round(timeit(fn, a.iters), 4)
             print(f"{name:11s} {res[name]:.4f} ms", flush=True)
-        if os.environ.get("TDS_CONV2_DIAG") == "13":  # per-role barrier-wait fractions (diag build)
+        if os.environ.get("TDS_CONV2_DIAG", "0") == "13" or int(os.environ.get("TDS_CONV2_DIAG", "0") or 0) >= 16:  # per-role barrier-wait fractions (diag build)
             c2b()
             torch.cuda.synchronize()
             clk = ops.conv2_bwd_clock_dump(ops.device_cus()).to(torch.int64) & 0xFFFFFFFF

@@ -1,8 +1,11 @@
 // conv2 backward: BN2 / ReLU / max-pool backward fused into conv2 dgrad + wgrad
 // (SURVEY.md §2.4 K16-K21), one persistent 8-wave workgroup per CU, on v_mfma_f32_16x16x32_f16
-// with the fp16x2 split (bf16x3.h; 2 MFMAs per product):
-//   dgrad: dp1 = convT(dy2, w2)  -- dy2 the single-rounded fp16 operand, w2 exact (hi + lo)
-//   wgrad: dw2 = sum dy2 (x) p1  -- dy2 exact (hi + lo), p1 the forward's fp16 operand as is
+// in the TF32 class (round-4 default, conv2_common.h kConv2Split = 0): ONE MFMA per product, both
+// operands rounded once to fp16 (11 significant bits, TF32's significand):
+//   dgrad: dp1 = convT(dy2, w2)  -- dy2 rounded once (scaled), w2 as packed by conv2_pack (scaled)
+//   wgrad: dw2 = sum dy2 (x) p1  -- dy2 rounded once, p1 the forward's fp16 operand as is
+// (the -DTDS_CONV2_SPLIT=1 variant build keeps the round-3 fp16x2 split: the exact operand as fp16
+// hi + lo, 2 MFMAs per product; the "lo" planes and operands below exist only in that build)
 // dy2 is carried with a power-of-two scale 2^e: from the step's magnitude bounds (max |y2 - b2|
 // per channel from the forward, max |g2m| from the head backward) |dy2| <= |k1| max|g2m| + |k2|
 // (max|y2 - b2| + |b2|) + |k3| per channel, and e puts the largest bound in [2^14, 2^15) -- no fp16
@@ -300,14 +303,17 @@ __device__ __forceinline__ void br_barrier() { asm volatile("s_waitcnt lgkmcnt(0
 // slower.)
 constexpr int kBRClkMaxWg = 1024;
 __device__ uint32_t g_br_clk[kBRClkMaxWg * 8 * 2];
+constexpr bool br_clocked(int D) { return D == 13 || D >= 16; }
+constexpr bool br_no_stage(int D) { return D == 5 || (D >= 16 && (D & 1)); }
+constexpr bool br_idle(int D, int role) { return D >= 16 && (role < 2 ? (D & 4) : (D & 8)); }
 template <int DIAG>
 struct BRClock {
   uint64_t wait = 0, t0 = 0;
   __device__ __forceinline__ void start() {
-    if constexpr (DIAG == 13) t0 = __builtin_amdgcn_s_memtime();
+    if constexpr (br_clocked(DIAG)) t0 = __builtin_amdgcn_s_memtime();
   }
   __device__ __forceinline__ void barrier() {
-    if constexpr (DIAG == 13) {
+    if constexpr (br_clocked(DIAG)) {
       const uint64_t a = __builtin_amdgcn_s_memtime();
       br_barrier();
       wait += __builtin_amdgcn_s_memtime() - a;
@@ -316,7 +322,7 @@ struct BRClock {
     }
   }
   __device__ __forceinline__ void report() {
-    if constexpr (DIAG == 13) {
+    if constexpr (br_clocked(DIAG)) {
       const uint64_t tot = __builtin_amdgcn_s_memtime() - t0;
       const int i = ((int)blockIdx.x * 8 + (int)(threadIdx.x >> 6)) * 2;
       if ((threadIdx.x & 63) == 0 && blockIdx.x < kBRClkMaxWg) {
@@ -362,7 +368,9 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
     if (cur.end) break;
     clk.barrier();  // tile kk staged; the partner's exchange slot of tile kk-1 is written
     const BRRows rw = br_rows(smem, kk);
-    if constexpr (ROLE < 2) {
+    if constexpr (br_idle(DIAG, ROLE)) {
+      // timing-only: this role does nothing but the barriers
+    } else if constexpr (ROLE < 2) {
       if (!prev.end)
         br_xchg_finish<ROLE>(reinterpret_cast<const f32x4*>(smem + BR_OFF_X + ((kk + 1) & 1) * BR_XCHG), acc, a.dp1,
                              lane, prev.b, prev.r0, prev.c0, a.P, inv);
@@ -643,7 +651,7 @@ struct BRStager {
 // kernel 168 KB of code, far beyond the instruction cache its CU shares.
 template <int DIAG, bool BIG>
 __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
-  if constexpr (DIAG == 5) {  // timing only: no staging at all (consumers read stale LDS)
+  if constexpr (br_no_stage(DIAG)) {  // timing only: no staging at all (consumers read stale LDS)
     for (int k = 0; !br_decode(a.walk, k, a.sk, a.w).end; ++k) br_barrier();
     br_barrier();
     return;
@@ -885,7 +893,8 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
 
 #ifdef TDS_DIAG
 // timing-only variants: 1 no MFMAs, 3 no global tile loads, 5 no staging, 7 no y2 loads, 9 no
-// BN2 / pool backward math in the staging, 13 the full kernel with per-wave barrier-wait clocks.  Compiled only into a -DTDS_DIAG build
+// BN2 / pool backward math in the staging, 13 the full kernel with per-wave barrier-wait clocks,
+// 16..27 the flag sets of conv2_common.h (with clocks).  Compiled only into a -DTDS_DIAG build
 // (python -m torch_distributed_sandbox_amd._build --variant diag -D TDS_DIAG; TDS_CONV2_DIAG=N).
 static int br_diag_env() {
   const char* e = std::getenv("TDS_CONV2_DIAG");
@@ -929,6 +938,17 @@ void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const
     case 7: TDS_BR_LAUNCH(7) break;
     case 9: TDS_BR_LAUNCH(9) break;
     case 13: TDS_BR_LAUNCH(13) break;
+    // flag sets (conv2_common.h): 16 = full + clocks; +1 no staging, +2 no LDS operand reads,
+    // +4 dgrad idle, +8 wgrad idle
+    case 16: TDS_BR_LAUNCH(16) break;
+    case 17: TDS_BR_LAUNCH(17) break;
+    case 19: TDS_BR_LAUNCH(19) break;
+    case 20: TDS_BR_LAUNCH(20) break;
+    case 21: TDS_BR_LAUNCH(21) break;
+    case 23: TDS_BR_LAUNCH(23) break;
+    case 24: TDS_BR_LAUNCH(24) break;
+    case 25: TDS_BR_LAUNCH(25) break;
+    case 27: TDS_BR_LAUNCH(27) break;
 #endif
     default: TDS_BR_LAUNCH(0) break;
   }

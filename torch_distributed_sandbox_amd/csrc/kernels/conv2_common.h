@@ -49,6 +49,10 @@ __device__ __forceinline__ float f16_val(uint32_t h) {
 // DIAG = 0: the real kernel.  Timing-only builds (tools/conv2_diag.py, TDS_CONV2_DIAG):
 //   1: no MFMAs (operand reads kept alive by one VALU op),  2: no LDS operand reads
 //   (register constants), 3: no global tile loads (LDS holds whatever it held).
+// conv2 backward, DIAG >= 16: flag sets, per-role barrier clocks always on (conv2_bwd.hip):
+//   +1 no staging, +2 no LDS operand reads in the MFMA waves, +4 dgrad waves idle, +8 wgrad
+//   waves idle (an idle role only takes part in the per-tile barriers)
+constexpr bool diag_no_lds(int D) { return D == 2 || (D >= 16 && (D & 2)); }
 template <int DIAG>
 __device__ __forceinline__ f32x4 mma3(const s16x8& ah, const s16x8& al, const s16x8& bh, const s16x8& bl, f32x4 c) {
   if constexpr (DIAG == 1) {
@@ -98,7 +102,7 @@ __device__ __forceinline__ f32x4 mmaw(const s16x8& a, const s16x8& bh, const s16
 }
 template <int DIAG>
 __device__ __forceinline__ s16x8 lds8(const void* p) {
-  if constexpr (DIAG == 2) {
+  if constexpr (diag_no_lds(DIAG)) {
     const short v = (short)(threadIdx.x & 7);
     return s16x8{v, v, v, v, v, v, v, v};
   } else {
@@ -107,7 +111,7 @@ __device__ __forceinline__ s16x8 lds8(const void* p) {
 }
 template <int DIAG>
 __device__ __forceinline__ s16x4 ldtr(const void* p) {
-  if constexpr (DIAG == 2) {
+  if constexpr (diag_no_lds(DIAG)) {
     const short v = (short)(threadIdx.x & 7);
     return s16x4{v, v, v, v};
   } else {

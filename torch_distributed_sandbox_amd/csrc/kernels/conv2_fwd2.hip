@@ -1,13 +1,15 @@
 // conv2 forward v2 (Conv2d(16, 32, 5, pad 2), mnist_onegpu.py:20):
 // y2 = conv(p1) + b2, stored as y2h (NHWC fp16, bias-free, scaled: conv2_common.h), plus BN2
 // batch-statistic partials, on
-// v_mfma_f32_16x16x32_f16 with the fp16x2 split (bf16x3.h: p1 is the single-rounded fp16
-// operand, the weights are carried exactly as fp16 hi + lo; 2 MFMAs per product), laid out for
-// SEVERAL small workgroups per CU (the design of conv2_bwd2.hip):
+// v_mfma_f32_16x16x32_f16 in the TF32 class (round-4 default, conv2_common.h kConv2Split = 0):
+// ONE MFMA per product, p1 and the weights each rounded once to fp16 (11 significant bits, TF32's
+// significand) at exact power-of-two range scales; the round-3 fp16x2 form (weights as fp16 hi +
+// lo, 2 MFMAs per product) is the -DTDS_CONV2_SPLIT=1 variant build.  Laid out for SEVERAL small
+// workgroups per CU (3 at 168 VGPRs, 44 KiB LDS):
 //   * 4 waves per workgroup, output tile 8 rows x 16 columns (staged p1: 12 x 20 records of
 //     32 B);
 //   * weights in REGISTERS: wave w owns co half nt = w & 1 and output rows 4(w>>1) .. +3,
-//     all 13 K-steps of its half (13 x (hi, lo) fragments = 104 VGPRs), loaded once;
+//     all 13 K-steps of its half (13 fp16 fragments; 13 x (hi, lo) in the split build), loaded once;
 //   * p1 staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs, no VALU), double-buffered:
 //     tile t+1 streams in while tile t is on the MFMAs;
 //   * the epilogue of tile t (y2h stores + statistics) runs after tile t+1's DMA is issued,
@@ -351,7 +353,14 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   const bool neg = gamma != nullptr && gamma[16 * NT + li] < 0.f;
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
+  // BN2 partials: each tile's sums in fp32 (<= 16 values per lane), accumulated across the
+  // workgroup's tiles in fp64 (TDS_F2_STAT64; 0: one fp32 running sum per lane over ~1.8 K values,
+  // whose rounding grows with n (1 + mean^2 / var) in var = E[q] - E[s]^2)
+#ifndef TDS_F2_STAT64
+#define TDS_F2_STAT64 1
+#endif
   f2v s_acc = {0.f, 0.f}, q_acc = {0.f, 0.f};
+  double s_d = 0.0, q_d = 0.0;
   uint32_t ymx = 0u;
   f32x4 acc[4];
   F2Tile prev{0, 0, 0};
@@ -377,6 +386,12 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     else
       f2_stage<true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
                      bco, inv, ksc, neg, s_acc, q_acc, ymx, a2);
+    if constexpr (TDS_F2_STAT64 != 0) {
+      s_d += (double)(s_acc.x + s_acc.y);
+      q_d += (double)(q_acc.x + q_acc.y);
+      s_acc = f2v{0.f, 0.f};
+      q_acc = f2v{0.f, 0.f};
+    }
     prev = cur;
     have_prev = true;
   }
@@ -390,7 +405,8 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 16, 64));
   ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 32, 64));
   // BN2 partials: reduce the 4 lane groups, then the two row-halves of this co half
-  float s_sum = s_acc.x + s_acc.y, q_sum = q_acc.x + q_acc.y;
+  double s_sum = TDS_F2_STAT64 != 0 ? s_d : (double)(s_acc.x + s_acc.y);
+  double q_sum = TDS_F2_STAT64 != 0 ? q_d : (double)(q_acc.x + q_acc.y);
   s_sum += __shfl_xor(s_sum, 16, 64);
   s_sum += __shfl_xor(s_sum, 32, 64);
   q_sum += __shfl_xor(q_sum, 16, 64);
@@ -399,8 +415,8 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   double* red = reinterpret_cast<double*>(smem);                   // [4 waves][16 co][2]
   uint32_t* yred = reinterpret_cast<uint32_t*>(smem + 4 * 16 * 2 * 8);  // [4 waves][16 co]
   if (lane < 16) {
-    red[(WV * 16 + li) * 2 + 0] = (double)s_sum;
-    red[(WV * 16 + li) * 2 + 1] = (double)q_sum;
+    red[(WV * 16 + li) * 2 + 0] = s_sum;
+    red[(WV * 16 + li) * 2 + 1] = q_sum;
     yred[WV * 16 + li] = ymx;
   }
   __syncthreads();

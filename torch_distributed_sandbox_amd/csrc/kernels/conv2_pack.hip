@@ -1,7 +1,7 @@
 // conv2 of the ConvNet (Conv2d(16, 32, 5, stride 1, pad 2), mnist_onegpu.py:20): shared host
-// pieces of the fp16x2 MFMA kernels (conv2_fwd2.hip, conv2_bwd.hip; bf16x3.h) -- the on-device
-// weight packing into MFMA fragment order (fp16 hi + lo: the exactly carried operand of the
-// forward and the data gradient), the deterministic fp64 reduction of the per-workgroup weight
+// pieces of the fp16 MFMA kernels (conv2_fwd2.hip, conv2_bwd.hip) -- the on-device weight
+// packing into MFMA fragment order (w * 2^ew rounded once to fp16 in the TF32-class default; fp16
+// hi + lo in the -DTDS_CONV2_SPLIT=1 build), the deterministic fp64 reduction of the per-workgroup weight
 // gradient slabs, and the blocked tile order table.  SURVEY.md §2.4 K5 / K19 / K20.
 //
 // Activation formats (produced/consumed by convnet_fused.hip and the conv2 kernels):

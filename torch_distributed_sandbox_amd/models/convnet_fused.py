@@ -2,11 +2,11 @@
 
 The reference runs 13 ATen kernels forward and ~20 backward per step on
 fp32 NCHW tensors.  This plan runs the network as three
-autograd Functions over NHWC/bf16x3 activations (kernels in
+autograd Functions over NHWC fp16 / uint8-level activations (kernels in
 ``csrc/kernels/convnet_fused.hip``, ``conv2_fwd2.hip``, ``conv2_bwd.hip``, ``head_pb.hip``):
 
 ``_Layer1``  x -> p1            conv1 + BN1(batch stats) + ReLU + pool, conv1 never stored; p1 in fp16
-``_Conv2``   p1 -> y2, ya       conv2 (fp16x2 MFMA) with BN2 batch-stat partials and the 2x2
+``_Conv2``   p1 -> y2, ya       conv2 (TF32-class fp16 MFMA) with BN2 batch-stat partials and the 2x2
                                 max-pool (ya = y2 at each window's argmax, resolved by the sign
                                 of BN2's gamma) fused; its backward rebuilds dy2 from y2 in LDS
                                 (BN2/pool backward fused)
@@ -20,12 +20,15 @@ collective launched — before the conv backward starts (SURVEY.md §3.4 overlap
 property).
 
 Numerics: BN, pooling, fc, the loss and SGD are exact fp32.  conv1 (fwd + wgrad) uses the
-bf16x3 split (hi*hi + hi*lo + lo*hi, fp32 accumulate, ~2^-16 per product).  conv2 (fwd, dgrad,
-wgrad) uses the fp16x2 split (csrc/kernels/bf16x3.h): one operand exact as fp16 hi + lo, the
-other rounded once to fp16 -- p1 (stored in fp16) in the forward and the weight gradient, the
-conv2 output gradient (scaled by a power of two per step, from the magnitude bounds ``mag``) in
-the data gradient -- so the per-product error is <= 2^-11, the unit roundoff of the TF32
-convolutions cuDNN runs for the reference by default (TF32 rounds both operands).
+bf16x3 split (hi*hi + hi*lo + lo*hi, fp32 accumulate, ~2^-16 per product; on uint8 level input
+bf16x2, the level exact; the level-input weight gradient one fp16 MFMA, dp1h and the level both
+exact in fp16).  conv2 (fwd, dgrad, wgrad) runs in the TF32 class (round-4 default): ONE fp16 MFMA
+per product with both operands rounded once to 11 significant bits -- TF32's significand, the
+arithmetic of the cuDNN convolutions the reference runs under PyTorch's default ``allow_tf32`` --
+at exact power-of-two range scales (p1 by BN1's Samuelson bound, the weights by their max, the
+conv2 output gradient by the step's magnitude bounds ``mag``); docs/KERNELS.md "conv2 in the TF32
+class".  The round-3 fp16x2 split (one operand exact as fp16 hi + lo) is the
+``-DTDS_CONV2_SPLIT=1`` variant build (``ops.conv2_split()``).
 ``mode='layers'`` is the exact-fp32 generic path.
 
 Gradient hand-off beside autograd: the fp16 p1 is an autograd output, but its gradient dp1 is
