@@ -465,9 +465,15 @@ def _teardown(abort: bool) -> None:
         tdist.barrier()
     tdist.destroy_process_group()
     if split:
-        # the communicator's CU-masked streams end with it, not at process exit (utils/streams.py)
+        # the communicator's CU-masked streams end with it, not at process exit (utils/streams.py).
+        # The DDP wrapper's reference cycles still hold the native communicator (through its C++
+        # reducer) until a collection: free it first -- its tensors were used on the comm stream,
+        # and freeing them after that stream is destroyed fails (hipErrorInvalidHandle at exit)
+        import gc
+
         from torch_distributed_sandbox_amd.utils.streams import release_streams
 
+        gc.collect()
         release_streams()
 
 

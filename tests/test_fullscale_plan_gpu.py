@@ -106,27 +106,33 @@ def test_two_steps_of_the_benchmarked_plan_vs_fp64(gpu):
     for s in range(STEPS):
         o, a, t = ours[s], r64[s], rtf[s]
         scale = a["logits"].abs().max().item()
-        e_log = (o["logits"].double() - a["logits"]).abs().max().item() / scale
+        d_log = (o["logits"].double() - a["logits"]).abs().max().item()
+        e_log = d_log / scale
         e_log_tf = (t["logits"] - a["logits"]).abs().max().item() / scale
-        e_loss = abs(o["loss"].item() - a["loss"].item()) / abs(a["loss"].item())
+        d_loss = abs(o["loss"].item() - a["loss"].item())
+        e_loss = d_loss / abs(a["loss"].item())
         e_loss_tf = abs(t["loss"].item() - a["loss"].item()) / abs(a["loss"].item())
         print(f" step {s}: loss {o['loss'].item():.6f} (fp64 {a['loss'].item():.6f}); logits err {e_log:.3e} "
               f"(TF32 ref {e_log_tf:.3e}); loss err {e_loss:.3e} (TF32 ref {e_loss_tf:.3e})")
         assert e_log <= max(1e-4, 1.5 * e_log_tf), (s, e_log)
-        assert e_loss <= max(1e-4, 1.5 * e_loss_tf), (s, e_loss)
+        # the mean cross-entropy moves by at most 2 max|d logit| (|d logsumexp| <= max|d l|, and the
+        # label's logit): after a step the logits grow (loss ~65 here) and the TF32 reference's loss
+        # error can be smaller than its logits' by cancellation, so the loss is bounded through the logits
+        assert d_loss <= max(1e-4 * abs(a["loss"].item()), 2.0 * d_log * (1 + 1e-6)), (s, e_loss)
         print(f"   {'parameter':18s} {'|ours-64|/|upd|':>16s} {'|tf32-64|/|upd|':>16s} {'fp32 floor/|upd|':>17s}")
         for n, p64 in a["params"].items():
             upd = max(_norm(p64 - state0[n].double()), 1e-300)  # this step's and the earlier steps' updates
             e = _norm(o["params"][n].double() - p64)
             e_tf = _norm(t["params"][n] - p64)
             floor = 3.0 * (s + 1) * _norm(p64.float().double() - p64)
-            print(f"   {n:18s} {e / upd:16.3e} {e_tf / upd:16.3e} {floor / upd:17.3e}")
             if n in ("layer1.0.bias", "layer2.0.bias"):
                 # conv bias before train-mode BN: analytically zero gradient, the update is
                 # rounding noise on every side; bounded by the matching weight's update
                 wupd = _norm(a["params"][n.replace("bias", "weight")] - state0[n.replace("bias", "weight")].double())
+                print(f"   {n:18s} {'|ours-64| / |weight upd|':>34s} {e / wupd:.3e} (fp32 floor {floor / wupd:.3e})")
                 assert e <= 1e-3 * wupd + floor, (s, n, e)
                 continue
+            print(f"   {n:18s} {e / upd:16.3e} {e_tf / upd:16.3e} {floor / upd:17.3e}")
             assert e <= max(GRAD_TOL[n] * upd + floor, 1.5 * e_tf + floor), (s, n, e / upd)
         for n, b64 in a["buffers"].items():
             if n.endswith("num_batches_tracked"):

@@ -69,14 +69,18 @@ int l1_wg() { return tds_fused_num_wg(TDS_L1_PER_CU); }
 // layer-1 backward workgroups per CU: 4 waves each.  Round 3 (124-126 VGPRs, 4 fit a CU): 4 -> 0.318
 // ms, 3 -> 0.351 ms (tools/gpu_sessions/r3_s21.sh).  Round 4's fp16 weight gradient runs at 87
 // VGPRs, so 5 fit (<= 102): 4 / 5 / 6 -> 0.143 / 0.138 / 0.145 ms (r4_s47.sh).  TDS_L1B_PER_CU
-// overrides it (A/B sweeps only).
-int l1b_wg() {
-  static const int per_cu = [] {
+// overrides it (A/B sweeps only).  Capped by what the launched variant's registers allow
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor): the fp32-image and pair-layout variants need more
+// VGPRs than the level-input word layout, and a 5th workgroup that cannot be resident only adds a
+// second, partial wave of workgroups.
+int l1b_wg(bool levels, bool pairs) {
+  static const int req = [] {
     const char* e = std::getenv("TDS_L1B_PER_CU");
     const int v = e ? std::atoi(e) : 0;
     return v >= 1 && v <= 8 ? v : 5;
   }();
-  return tds_fused_num_wg(per_cu);
+  const int fit = tds_l1_bwd_max_per_cu(levels, pairs);
+  return tds_fused_num_wg(std::getenv("TDS_L1B_PER_CU") ? req : std::min(req, fit));
 }
 
 // Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
@@ -321,6 +325,92 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1,
   return {y2, partial, ya, a2};
 }
 
+// The conv2 forward with BN2 finalized inside its launch (conv2_fwd2.hip f2_finalize): returns (y2h,
+// ya, a2 as fused_conv2_forward, stats2 [mean32|invstd32], aff2 [a32|b32]); the running statistics
+// and num_batches_tracked are updated, and mag[0..32) gets max |y2 - b2| per channel (the conv2
+// backward's magnitude bound; fused_head_backward(ypart_done=True) then leaves it).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_conv2_forward_bn(
+    const Tensor& p1, const Tensor& wp, const Tensor& b2, const c10::optional<Tensor>& gamma2,
+    const c10::optional<Tensor>& beta2, const c10::optional<Tensor>& rm2, const c10::optional<Tensor>& rv2,
+    const c10::optional<Tensor>& nbt2, double momentum, double eps, const c10::optional<Tensor>& mag) {
+  TORCH_CHECK(p1.dim() == 4 && p1.size(1) == p1.size(2) && p1.size(3) == 16, "fused_conv2_forward_bn: p1 [B,P,P,16]");
+  const int64_t B = p1.size(0), P = p1.size(1);
+  need(p1, at::kHalf, {B, P, P, 16}, "p1");
+  need(wp, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
+  need(b2, at::kFloat, {32}, "conv2.bias");
+  const float* g = optf(gamma2, 32, "bn2.weight");
+  TORCH_CHECK(B <= 255 && P >= 2, "fused_conv2_forward_bn: 1 <= batch <= 255 and P >= 2");
+  int64_t* nb = nullptr;
+  if (nbt2.has_value() && nbt2->defined()) {
+    TORCH_CHECK(nbt2->is_cuda() && nbt2->scalar_type() == at::kLong && nbt2->numel() == 1, "bn2.num_batches_tracked");
+    nb = nbt2->data_ptr<int64_t>();
+  }
+  c10::DeviceGuard guard(p1.device());
+  const int nwg = tds_conv2_fwd2_num_wg();
+  int tr = 0, tc = 0;
+  tds_conv2_fwd2_tiles((int)P, &tr, &tc);
+  int sw = 0, sk = 0;
+  const int* order = tile_order(p1, (int)B, tr, tc, nwg, &sw, &sk);
+  auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kHalf));
+  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
+  auto a2 = at::empty({B, P / 2, P / 2, 2}, p1.options().dtype(at::kInt));
+  const int ndw = tds_conv2_fwd2_fin_doubles(nwg), nuw = tds_conv2_fwd2_fin_words(nwg);
+  auto partial = at::empty({32 * nwg * 2 + ndw}, p1.options().dtype(at::kDouble));
+  auto uwork = at::empty({nuw}, p1.options().dtype(at::kInt));
+  auto stats = at::empty({64}, p1.options().dtype(at::kFloat));
+  auto aff = at::empty({64}, p1.options().dtype(at::kFloat));
+  uint32_t* m = opt_mag(mag, kMagParts + 32 * mag_ypart_count());
+  TdsBnFin fin{};
+  fin.beta = optf(beta2, 32, "bn2.bias");
+  fin.eps = (float)eps;
+  fin.momentum = (float)momentum;
+  fin.stats = stats.data_ptr<float>();
+  fin.running_mean = const_cast<float*>(optf(rm2, 32, "bn2.running_mean"));
+  fin.running_var = const_cast<float*>(optf(rv2, 32, "bn2.running_var"));
+  fin.num_batches = nb;
+  fin.aff = aff.data_ptr<float>();
+  fin.mag = m;
+  fin.dwork = partial.data_ptr<double>() + 32 * nwg * 2;
+  fin.uwork = reinterpret_cast<uint32_t*>(uwork.data_ptr<int>());
+  tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr(), ya.data_ptr<float>(),
+                 reinterpret_cast<uint32_t*>(a2.data_ptr<int>()), partial.data_ptr<double>(), m ? m + kMagParts : nullptr,
+                 m ? m + kMagScales : nullptr, order, nwg, sw, sk, (int)B, (int)P, stream_of(p1), &fin);
+  check_launches("fused_conv2_forward_bn");
+  return {y2, ya, a2, stats, aff};
+}
+
+// The head forward on a finished BN2 affine (fused_conv2_forward_bn's aff2): logits only, finished
+// inside the head's launch (head_pb.hip HPFin) for B <= 8
+Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor& wfc, const c10::optional<Tensor>& bfc,
+                              int64_t P, const c10::optional<Tensor>& x_out) {
+  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_aff: ya must be [B,32,PB]");
+  const int64_t B = ya.size(0), Q = P / 2;
+  TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_forward_aff: needs P/2 >= 4 pooled columns and B >= 1");
+  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(aff2, at::kFloat, {64}, "aff2");
+  TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
+              "fc.weight must be [<=10, 32*Q*Q]");
+  const int64_t NC = wfc.size(0);
+  need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
+  const float* bf = optf(bfc, NC, "fc.bias");
+  float* xo = nullptr;
+  if (x_out.has_value() && x_out->defined()) {
+    need(*x_out, at::kFloat, {B, 32 * Q * Q}, "x_out (fc input rows)");
+    xo = x_out->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(ya.device());
+  const int nblk = 32 * tds_head_pb_nblk((int)Q);
+  auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
+  auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
+  auto logits = at::empty({B, NC}, ya.options());
+  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
+                                 part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
+                                 (int)Q, (int)NC, stream_of(ya));
+  TORCH_CHECK(rc == 0, "fused_head_forward_aff: unsupported shape");
+  check_launches("fused_head_forward_aff");
+  return logits;
+}
+
 // ---------------------------------------------------------------- head forward (BN2 finalize + fc)
 // returns (logits, stats2 [mean32|invstd32], aff2 [a32|b32])
 std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
@@ -361,7 +451,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
   tds_bn_reduce_finalize(partial2.data_ptr<double>(), 32, nch, B * P * P, b2.data_ptr<float>(), (float)eps,
                          (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   const int nblk = 32 * tds_head_pb_nblk((int)Q);
-  auto part = at::empty({(int64_t)nblk * B * NC}, ya.options().dtype(at::kDouble));
+  auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
   auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
   auto logits = at::empty({B, NC}, ya.options());
   const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
@@ -410,7 +500,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     double scale, bool compute_dw, double update_lr, const c10::optional<Tensor>& dbfc_out,
     const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out, bool keep_dw, int64_t c_begin,
     int64_t c_end, bool finalize, const c10::optional<Tensor>& g2m_out, const c10::optional<Tensor>& partial_out,
-    const c10::optional<Tensor>& mag) {
+    const c10::optional<Tensor>& mag, bool ypart_done) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_backward: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_backward: needs P/2 >= 4 pooled columns and B >= 1");
@@ -458,14 +548,33 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into partial_out");
     partial = at::empty({(int64_t)32 * npass * nblk * 2}, ya.options().dtype(at::kDouble));
   }
+  uint32_t* gp = opt_mag(mag, mag_numel(B, P)) ? opt_mag(mag) + kMagParts + 32 * mag_ypart_count() : nullptr;
+  // the BN2 backward finalize inside the head backward's launch (head_pb.hip HBFin): one pass over
+  // all channels, with the conv2 forward having reduced its magnitude parts (ypart_done)
+  const bool fin_in = finalize && whole && npass == 1 && ypart_done && tds_fused_fin_enabled();
+  if (fin_in) {
+    auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
+    auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");
+    auto kbuf = at::empty({96}, ya.options());
+    auto dbfc = sink_or_empty(dbfc_out, {NC}, ya, "dbfc_out");
+    auto cmax = at::empty({32}, ya.options().dtype(at::kInt));
+    TdsHeadBwdFin hf{reinterpret_cast<uint32_t*>(cmax.data_ptr<int>()), stats2.data_ptr<float>(), g,
+                     dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), dbfc.data_ptr<float>(),
+                     opt_mag(mag, mag_numel(B, P))};
+    const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
+                                   dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
+                                   compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
+                                   upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
+                                   (float)scale, (float)update_lr, 0, 32, gp, st, &hf);
+    TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
+    check_launches("fused_head_backward");
+    return {dW, dbfc, dgamma, dbeta, g2m, kbuf};
+  }
   const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
                                  dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
                                  compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                  upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
-                                 (float)scale, (float)update_lr, (int)c_begin, (int)c_end,
-                                 opt_mag(mag, mag_numel(B, P)) ? opt_mag(mag) + kMagParts + 32 * mag_ypart_count()
-                                                               : nullptr,
-                                 st);
+                                 (float)scale, (float)update_lr, (int)c_begin, (int)c_end, gp, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
   if (!finalize) {
     check_launches("fused_head_backward");
@@ -479,7 +588,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   uint32_t* m = opt_mag(mag, mag_numel(B, P));
   tds_bn_bwd_finalize2(partial.data_ptr<double>(), 32, npass * nblk, B * P * P, g, stats2.data_ptr<float>(),
                        dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), dlogits.data_ptr<float>(),
-                       (int)B, (int)NC, dbfc.data_ptr<float>(), (float)scale, m ? m + kMagParts : nullptr,
+                       (int)B, (int)NC, dbfc.data_ptr<float>(), (float)scale, m && !ypart_done ? m + kMagParts : nullptr,
                        (int)mag_ypart_count(), m ? m + kMagParts + 32 * mag_ypart_count() : nullptr,
                        (int)mag_gpart_count(B, P), m, st);
   check_launches("fused_head_backward");
@@ -609,21 +718,39 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   const float* g = optf(gamma1, 16, "bn1.weight");
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
-  const int nwg = l1b_wg(), rows = tds_l1_bwd_rows(nwg);
-  auto partial = at::empty({(int64_t)rows * 16 * 27}, x.options().dtype(at::kDouble));
   static const bool pairs = [] {  // the bf16-pair LDS layout (convnet_fused.hip PAIRS), opt-in
     const char* e = std::getenv("TDS_L1B_PAIRS");
     return e && e[0] == '1';
   }();
+  const int nwg = l1b_wg(levels, levels && pairs), rows = tds_l1_bwd_rows(nwg);
+  auto partial = at::empty({(int64_t)rows * 16 * 27}, x.options().dtype(at::kDouble));
+  auto dw1 = sink_or_empty(dw_out, {16, 1, 5, 5}, x, "dw1_out");
+  auto db1 = sink_or_empty(db_out, {16}, x, "db1_out");
+  auto dg = sink_or_empty(dg_out, {16}, x, "dgamma1_out");
+  auto dbe = sink_or_empty(dbe_out, {16}, x, "dbeta1_out");
+  // the reduction and the closed-form gradients inside the launch: opt-in (TDS_FUSED_FIN_L1=1) --
+  // its 1280 partial rows of 432 doubles need several dependent rounds of loads in one workgroup,
+  // measured slower than the two small launches it replaces (l1 backward 0.172 ms vs 0.131 + 2 x
+  // 0.007, r5_s3)
+  static const bool fin_l1 = [] {
+    const char* e = std::getenv("TDS_FUSED_FIN_L1");
+    return e && e[0] == '1';
+  }();
+  if (fin_l1 && tds_fused_fin_enabled()) {
+    auto work = at::empty({tds_l1_bwd_fin_doubles(nwg)}, x.options().dtype(at::kDouble));
+    TdsL1Fin lf{work.data_ptr<double>(), gram.data_ptr<double>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(),
+                db1.data_ptr<float>(), dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale};
+    tds_l1_bwd(x.data_ptr(), levels, pairs, dp1.data_ptr(), reinterpret_cast<const uint32_t*>(dp1_dec.data_ptr<int>()),
+               p1.data_ptr(), idx1.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
+               partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st, &lf);
+    check_launches("fused_l1_backward");
+    return {dw1, db1, dg, dbe};
+  }
   tds_l1_bwd(x.data_ptr(), levels, pairs, dp1.data_ptr(), reinterpret_cast<const uint32_t*>(dp1_dec.data_ptr<int>()),
              p1.data_ptr(), idx1.data_ptr<uint8_t>(),
              w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
   tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);
-  auto dw1 = sink_or_empty(dw_out, {16, 1, 5, 5}, x, "dw1_out");
-  auto db1 = sink_or_empty(db_out, {16}, x, "db1_out");
-  auto dg = sink_or_empty(dg_out, {16}, x, "dgamma1_out");
-  auto dbe = sink_or_empty(dbe_out, {16}, x, "dbeta1_out");
   tds_l1_finalize(bsum.data_ptr<double>(), gram.data_ptr<double>(), B * H * W, w1.data_ptr<float>(),
                   b1.data_ptr<float>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(), db1.data_ptr<float>(),
                   dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale, st);
@@ -784,8 +911,15 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "int P, Tensor(a!)? dw_out, float scale, bool compute_dw=True, float update_lr=0.0, "
       "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None, bool keep_dw=True, "
       "int c_begin=0, int c_end=32, bool finalize=True, Tensor(f!)? g2m_out=None, Tensor(g!)? partial_out=None, "
-      "Tensor(h!)? mag=None) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
+      "Tensor(h!)? mag=None, bool ypart_done=False) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_head_backward);
+  m.def(
+      "fused_conv2_forward_bn(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
+      "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor(d!)? mag=None) -> "
+      "(Tensor, Tensor, Tensor, Tensor, Tensor)",
+      &fused_conv2_forward_bn);
+  m.def("fused_head_forward_aff(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor(a!)? x_out=None) -> Tensor",
+        &fused_head_forward_aff);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
   m.def("mag_numel(int B, int P) -> int", &mag_numel);
   m.def("mag_ypart_count() -> int", &mag_ypart_count);

@@ -138,6 +138,113 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t tds_buffer_rsrc(const void* ba
                                            (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
+// ---------------------------------------------------------------------------- in-launch finalizers
+// A producer kernel whose per-workgroup partials used to go to a separate reduce / finalize launch
+// (6-8 us each at the bench shape, almost all of it the kernel boundary) reduces them itself: the
+// LAST workgroup of a group to arrive reduces the group's rows, the last group-reducer finalizes.
+// Hand-off per cdna_hip_programming.md Guideline 16, counter form with WRITE-THROUGH payload:
+//   producer: every handed-off value stored sc1 (st_agent: an agent-scope relaxed atomic store,
+//             global_store ... sc1) -> every wave s_waitcnt vmcnt(0) -> barrier -> lane 0 relaxed
+//             agent fetch_add on the counter.  No release fence: an agent release is a
+//             buffer_wbl2 of the XCD's whole L2, and in the streaming kernels (the conv2 forward's
+//             y2h / ya, the head backward's g2m / weight update, all non-temporal stores that sit
+//             dirty in L2) one per workgroup cost +0.34 ms per step (r5_s2);
+//   the workgroup that draws n - 1 is the reducer: agent acquire fence (this CU's L1) -> vmcnt(0)
+//   -> barrier, then every wave reads the rows with lane-indexed vector loads (never through the
+//   scalar cache: Pitfall 6).
+// Counters live in a per-(device, stream) word buffer zeroed when it is allocated
+// (tds_sync_words); the reducer resets its counter to 0 for the next launch on that stream.
+// `flag` is one int of the kernel's own LDS (the broadcast of "I am last").
+__device__ __forceinline__ bool tds_arrive(uint32_t* counter, uint32_t n, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = t == n - 1;
+    if (last) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last ? 1 : 0;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+// stores of handed-off data: write-through (sc1)
+__device__ __forceinline__ void st_agent(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sum of nrows rows of ncols doubles (row r at base + r * rstride), in a fixed order, by one
+// 256-thread workgroup in ONE round of loads: thread t takes column t % ncols of row group t / ncols
+// (G = 256 / ncols groups, rows g, g + G, ...; at most WRS_MAXL loads each, all issued before the
+// first add), the G group sums meet in LDS (part: G * ncols doubles) and threads t < ncols add them
+// in group order.  A reducer that walked its rows as a dependent chain paid one global round trip
+// (~1-2 us) per step, which made the in-launch finalizers slower than the launches they replaced
+// (r5_s3).  Returns the column sum in threads t < ncols (0 elsewhere).  Needs ncols <= 256 and
+// nrows <= WRS_MAXL * (256 / ncols).  Every thread of the workgroup must call it.
+constexpr int WRS_MAXL = 16;
+// (column c of row r at base + r * rstride + (c >> 1) * cstride2 + (c & 1): cstride2 = 2 for
+// contiguous rows; the conv2 forward's [channel][workgroup][2] partials use cstride2 = 2 * nwg)
+__device__ __forceinline__ double wide_row_sum(const double* base, int nrows, int ncols, int64_t rstride,
+                                               double* part, int64_t cstride2 = 2) {
+  const int t = (int)threadIdx.x, G = 256 / ncols;
+  const int col = t % ncols, grp = t / ncols;
+  const int64_t coff = (int64_t)(col >> 1) * cstride2 + (col & 1);
+  double s = 0.0;
+  if (grp < G) {
+    double v[WRS_MAXL];
+#pragma unroll
+    for (int k = 0; k < WRS_MAXL; ++k) {
+      const int r = grp + k * G;
+      v[k] = r < nrows ? base[(int64_t)r * rstride + coff] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < WRS_MAXL; ++k) s += v[k];
+    part[grp * ncols + col] = s;
+  }
+  __syncthreads();
+  double tot = 0.0;
+  if (t < ncols)
+    for (int q = 0; q < G; ++q) tot += part[q * ncols + t];
+  __syncthreads();  // part may be reused
+  return tot;
+}
+
+// max of nrows rows of ncols (<= 256) uint32 (row r at base + r * rstride), one round of loads,
+// threads t < ncols get the column max (same contract as wide_row_sum; part: 256 words)
+__device__ __forceinline__ uint32_t wide_row_max(const uint32_t* base, int nrows, int ncols, int64_t rstride,
+                                                 uint32_t* part) {
+  const int t = (int)threadIdx.x, G = 256 / ncols;
+  const int col = t % ncols, grp = t / ncols;
+  uint32_t m = 0u;
+  if (grp < G) {
+    uint32_t v[WRS_MAXL];
+#pragma unroll
+    for (int k = 0; k < WRS_MAXL; ++k) {
+      const int r = grp + k * G;
+      v[k] = r < nrows ? base[(int64_t)r * rstride + col] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < WRS_MAXL; ++k) m = max(m, v[k]);
+    part[grp * ncols + col] = m;
+  }
+  __syncthreads();
+  uint32_t tot = 0u;
+  if (t < ncols)
+    for (int q = 0; q < G; ++q) tot = max(tot, part[q * ncols + t]);
+  __syncthreads();
+  return tot;
+}
+
+// call sites of the in-launch finalizers (tds_sync_words: kSyncWordsPerSite counters each)
+enum TdsSyncSite { kSyncHeadFwd = 0, kSyncConv2Fwd = 1, kSyncHeadBwd = 2, kSyncL1Bwd = 3, kSyncXMoments = 4 };
+constexpr int kSyncSites = 8, kSyncWordsPerSite = 256;
+
 // The head backward's pooled gradient g2m is PLANAR, [B][32][Q][Q] (the fc flatten order):
 // its producer streams the fc weight planes and writes g2m in the same long per-channel runs
 // (head_bwd_stream_kernel).  Channels 4*c4 .. 4*c4+3 of pooled position (py, px) of image b:

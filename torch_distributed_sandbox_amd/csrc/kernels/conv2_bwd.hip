@@ -191,29 +191,34 @@ struct DgSeq {
 
 // one flat, fully unrolled sequence of A-fragment rows with operands fetched two steps ahead
 // across group boundaries (one MFMA wave per SIMD: nothing else hides a bubble)
+// A rows read TDS_BR_DG_DEPTH rows ahead (ring of DEPTH + 1; round 4: 2)
+#ifndef TDS_BR_DG_DEPTH
+#define TDS_BR_DG_DEPTH 2
+#endif
 template <int D, int DIAG>
 __device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int li) {
   using Q = DgSeq<D>;
+  constexpr int DP = TDS_BR_DG_DEPTH;
 #pragma unroll
   for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 ah[3];  // dy2 hi only: the single-rounded operand
+  s16x8 ah[DP + 1];  // dy2 hi only: the single-rounded operand
   auto load_a = [&](int s, int buf) {
     const int i = Q::grp(s), r = Q::row(s);
     const char* rb = rw.d(Q::ky0(i) + r) + (Q::kx(i) + li) * 32;
     ah[buf] = lds8<DIAG>(rb + hp);
   };
-  load_a(0, 0);
-  load_a(1, 1);
+#pragma unroll
+  for (int s = 0; s < DP; ++s) load_a(s, s);
 #pragma unroll
   for (int s = 0; s < Q::S; ++s) {
-    if (s + 2 < Q::S) load_a(s + 2, (s + 2) % 3);
+    if (s + DP < Q::S) load_a(s + DP, (s + DP) % (DP + 1));
     __builtin_amdgcn_sched_barrier(0);
     const int i = Q::grp(s), r = Q::row(s);
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int o = r - k;
       if (k < Q::nky(i) && o >= 0 && o < 8)
-        acc[o] = mmaw<DIAG>(ah[s % 3], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
+        acc[o] = mmaw<DIAG>(ah[s % (DP + 1)], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
                             __builtin_bit_cast(s16x8, R[5 * i + k][1]), acc[o]);
     }
   }
@@ -292,6 +297,58 @@ __device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2],
     }
     bv[0] = bv[1];
     bv[1] = bv[2];
+  }
+}
+
+// The same sums as one flat, fully unrolled sequence of the 52 (K-step, tap) steps with the B
+// operands read DEPTH steps ahead through a ring of DEPTH + 1 register sets, and the next K-step's A
+// operands ADEPTH steps before it starts (TDS_BR_WG_DEPTH > 0 selects it; 0 = the rolled loop
+// above, B two steps ahead).  Timing-only variants (r5_s2, conv2 backward with the wgrad waves
+// alone, no staging) put the rolled loop at ~36 cycles per MFMA with its LDS operand reads and ~21
+// without them: the reads' latency is what the MFMA stream waits on.
+#ifndef TDS_BR_WG_DEPTH
+#define TDS_BR_WG_DEPTH 0
+#endif
+#ifndef TDS_BR_WG_ADEPTH
+#define TDS_BR_WG_ADEPTH 6
+#endif
+template <int E, int DIAG, int DEPTH>
+__device__ __forceinline__ void br_wgrad_ring(const BRRows& rw, f32x4 (&wacc)[13][2], int lane, const s16x8& ones) {
+  static_assert(DEPTH >= 1 && TDS_BR_WG_ADEPTH >= 1 && TDS_BR_WG_ADEPTH < 13, "wgrad ring depths");
+  constexpr int NS = 4 * 13, AD = TDS_BR_WG_ADEPTH;
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  s16x8 a[2][2], bv[DEPTH + 1];
+  auto load_a = [&](int m, int slot) {
+    const char* r0 = rw.d(2 * m + 2) + (2 + 4 * g + q4) * 32 + p4 * 8;
+    const char* r1 = rw.d(2 * m + 3) + (2 + 4 * g + q4) * 32 + p4 * 8;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const s16x4 x0 = ldtr<DIAG>(r0 + h * BR_DPL), x1 = ldtr<DIAG>(r1 + h * BR_DPL);
+      a[slot][h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    }
+  };
+  auto load_b = [&](int s, int buf) {
+    const int m = s / 13, tap = 13 * E + s % 13;
+    if (tap < 25) {
+      const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+      const int col = (kx + 4 * g + q4) * 32 + p4 * 8;
+      const s16x4 x0 = ldtr<DIAG>(rw.p(2 * m + ky) + col), x1 = ldtr<DIAG>(rw.p(2 * m + ky + 1) + col);
+      bv[buf] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+    } else {
+      bv[buf] = ones;  // bias gradient column
+    }
+  };
+  load_a(0, 0);
+#pragma unroll
+  for (int s = 0; s < DEPTH; ++s) load_b(s, s % (DEPTH + 1));
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int m = s / 13, k = s % 13;
+    if (s + DEPTH < NS) load_b(s + DEPTH, (s + DEPTH) % (DEPTH + 1));
+    if (k == 13 - AD && m + 1 < 4) load_a(m + 1, (m + 1) & 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) wacc[k][h] = mma2a<DIAG>(a[m & 1][h], a[m & 1][h], bv[s % (DEPTH + 1)], wacc[k][h]);
   }
 }
 
@@ -376,6 +433,8 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
                              lane, prev.b, prev.r0, prev.c0, a.P, inv);
       br_dgrad<ROLE, DIAG>(rw, R, acc, hp, li);
       br_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + BR_OFF_X + (kk & 1) * BR_XCHG), acc, lane);
+    } else if constexpr (TDS_BR_WG_DEPTH > 0 && !kConv2Split) {
+      br_wgrad_ring<ROLE - 2, DIAG, TDS_BR_WG_DEPTH>(rw, R, lane, ones);
     } else {
       br_wgrad<ROLE - 2, DIAG>(rw, R, lane, ones);
     }

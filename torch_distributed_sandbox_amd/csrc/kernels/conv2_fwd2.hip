@@ -29,6 +29,7 @@
 // s = 10 + kp pairs (ky = 2kp + (g>>1), kx = 4) with lane groups 2-3 reading row R+1.
 #include <cstdlib>
 
+#include "bn_finalize.h"
 #include "conv2_common.h"
 #include "launchers.h"
 #include "pooled_layout.h"
@@ -424,13 +425,69 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     const int co = lane >> 1, k = lane & 1, nt = co >> 4, c16 = co & 15;
     // waves with this co half: nt (rows 0-3) and nt + 2 (rows 4-7)
     const double v = (red[(nt * 16 + c16) * 2 + k] + red[((nt + 2) * 16 + c16) * 2 + k]) * (k ? (double)inv * inv : inv);
-    partial[((int64_t)co * gridDim.x + blockIdx.x) * 2 + k] = v;
+    st_agent(partial + ((int64_t)co * gridDim.x + blockIdx.x) * 2 + k, v);  // (write-through: f2_finalize)
     // this workgroup's max |y2 - b2| per channel: a plain store per (channel, workgroup), reduced by
     // the BN2-backward finalize (no same-address atomics: 16 K of them cost ~40 us in the head)
     // (max |acc| * inv = max |y2 - b2|: inv is a power of two, the order and the NaN survive)
     if (ypart != nullptr && k == 0)
-      ypart[co * gridDim.x + blockIdx.x] =
-          __float_as_uint(__uint_as_float(max(yred[nt * 16 + c16], yred[(nt + 2) * 16 + c16])) * inv);
+      st_agent(ypart + co * gridDim.x + blockIdx.x,
+               __float_as_uint(__uint_as_float(max(yred[nt * 16 + c16], yred[(nt + 2) * 16 + c16])) * inv));
+  }
+}
+
+// In-launch BN2 finalize (common.h tds_arrive; replaces bn_reduce_finalize_kernel and the ypart
+// max of bn_bwd_finalize2): groups of F2_GROUP workgroups; the last of a group to arrive reduces
+// the group's partial rows (fixed order) into gsum[g][co][2] and its max |y2 - b2| into gmax[g][co];
+// the last group-reducer sums the groups in order, finalizes BN2 (batch statistics, running
+// statistics, the affine aff = [a|b]) and writes mag[co] = max |y2 - b2| for the conv2 backward.
+constexpr int F2_GROUP = 32;
+struct F2Fin {
+  uint32_t* sync;  // [0, ngroups): group counters, [kSyncWordsPerSite - 1]: groups
+  double* gsum;    // [ngroups][32][2]
+  uint32_t* gmax;  // [ngroups][32]
+  int64_t n;       // B * P * P
+  const float* beta;
+  float eps, momentum;
+  float* stats;    // [64]: mean | invstd
+  float* running_mean;
+  float* running_var;
+  int64_t* num_batches;
+  float* aff;      // [64]: a | b
+  uint32_t* mag;   // [32]: max |y2 - b2| per channel (float bits)
+};
+
+__device__ __forceinline__ void f2_finalize(const F2Fin& fin, const double* __restrict__ partial,
+                                            const uint32_t* __restrict__ ypart, const float* __restrict__ bias,
+                                            const float* __restrict__ gamma, int* flag) {
+  const int nwg = (int)gridDim.x, wg = (int)blockIdx.x, tid = (int)threadIdx.x;
+  const int ng = (nwg + F2_GROUP - 1) / F2_GROUP, g = wg / F2_GROUP;
+  const int w0 = g * F2_GROUP, w1 = min(nwg, w0 + F2_GROUP);
+  double* part = reinterpret_cast<double*>(flag + 4);  // (16 B past the flag, inside the kernel's LDS)
+  if (!tds_arrive(fin.sync + g, (uint32_t)(w1 - w0), flag)) return;
+  // this group's rows (workgroups w0 .. w1-1) of partial[co][w][k], one round of loads each
+  const double s = wide_row_sum(partial + (int64_t)w0 * 2, w1 - w0, 64, 2, part, 2 * (int64_t)nwg);
+  if (tid < 64) st_agent(fin.gsum + (int64_t)g * 64 + tid, s);
+  if (ypart != nullptr && tid < 32) {  // [co][nwg]: channel co's w0 .. w1-1 are contiguous
+    uint32_t v[F2_GROUP];
+#pragma unroll
+    for (int u = 0; u < F2_GROUP; ++u) v[u] = w0 + u < w1 ? ypart[(int64_t)tid * nwg + w0 + u] : 0u;
+    uint32_t m = 0u;
+#pragma unroll
+    for (int u = 0; u < F2_GROUP; ++u) m = max(m, v[u]);
+    st_agent(fin.gmax + g * 32 + tid, m);
+  }
+  if (!tds_arrive(fin.sync + kSyncWordsPerSite - 1, (uint32_t)ng, flag)) return;
+  // the groups' (co, k) sums and max |y2 - b2|: one round of loads each
+  const double sk = wide_row_sum(fin.gsum, ng, 64, 64, part);
+  const uint32_t mx = wide_row_max(fin.gmax, ng, 32, 32, reinterpret_cast<uint32_t*>(part + 128));
+  if (tid < 64) part[tid] = sk;  // (co, k) -> co * 2 + k
+  __syncthreads();
+  if (tid < 32) {
+    const int co = tid;
+    if (co == 0 && fin.num_batches) fin.num_batches[0] += 1;
+    bn_finalize_channel(co, 32, part[co * 2], part[co * 2 + 1], fin.n, bias, fin.eps, fin.momentum, gamma, fin.beta,
+                        fin.stats, fin.running_mean, fin.running_var, fin.aff);
+    if (fin.mag != nullptr && ypart != nullptr) fin.mag[co] = mx;
   }
 }
 
@@ -445,13 +502,17 @@ __global__ __launch_bounds__(F2_THREADS, TDS_F2_WG) void conv2_fwd2_kernel(const
                                                                    uint32_t* __restrict__ ypart,
                                                                    const uint32_t* __restrict__ scales,
                                                                    const int* __restrict__ order, int sw, int sk,
-                                                                   int B, int P) {
+                                                                   int B, int P, F2Fin fin) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform role
   if (wv == 0) f2_run<DIAG, 0>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
   else if (wv == 1) f2_run<DIAG, 1>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
   else if (wv == 2) f2_run<DIAG, 2>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
   else f2_run<DIAG, 3>(p1, wpack, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, smem);
+  if (fin.sync != nullptr) {
+    __syncthreads();  // (f2_run's last LDS reads done: smem is reused for the flag)
+    f2_finalize(fin, partial, ypart, bias, gamma, reinterpret_cast<int*>(smem));
+  }
 }
 
 }  // namespace tds
@@ -479,10 +540,33 @@ static int f2_diag_env() { return 0; }
 
 // order: the blocked tile order table (tds_tile_order_fill) as per-workgroup lists [nwg][ceil(total / nwg)]
 // (fused_ops.cpp tile_order, sw / sk: the strides of workgroup / tile), allocated by the caller
+int tds_conv2_fwd2_fin_doubles(int nwg) { return ((nwg + F2_GROUP - 1) / F2_GROUP) * 32 * 2; }
+int tds_conv2_fwd2_fin_words(int nwg) { return ((nwg + F2_GROUP - 1) / F2_GROUP) * 32; }
+
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
                     uint32_t* a2, double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
-                    int B, int P, hipStream_t st) {
+                    int B, int P, hipStream_t st, const TdsBnFin* bn) {
   const dim3 grid(nwg), block(F2_THREADS);
+  F2Fin fin{};
+  if (bn != nullptr) {
+    fin.sync = tds_sync_words(kSyncConv2Fwd, st);
+    if (fin.sync == nullptr || (nwg + F2_GROUP - 1) / F2_GROUP > WRS_MAXL * 4) {
+      tds_launch_fail("conv2_fwd2: in-launch BN2 finalize unavailable (sync words / group count)");
+      return;
+    }
+    fin.gsum = bn->dwork;
+    fin.gmax = bn->uwork;
+    fin.n = (int64_t)B * P * P;
+    fin.beta = bn->beta;
+    fin.eps = bn->eps;
+    fin.momentum = bn->momentum;
+    fin.stats = bn->stats;
+    fin.running_mean = bn->running_mean;
+    fin.running_var = bn->running_var;
+    fin.num_batches = bn->num_batches;
+    fin.aff = bn->aff;
+    fin.mag = bn->mag;
+  }
   unsigned short* y2 = static_cast<unsigned short*>(y2h);
   const uint4* pp = reinterpret_cast<const uint4*>(p1);
   const uint4* w = reinterpret_cast<const uint4*>(wp);
@@ -500,12 +584,12 @@ void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const fl
   }
   switch (f2_diag_env()) {
 #ifdef TDS_DIAG
-    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
-    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
-    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
-    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
+    case 1: hipLaunchKernelGGL(conv2_fwd2_kernel<1>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, fin); break;
+    case 2: hipLaunchKernelGGL(conv2_fwd2_kernel<2>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, fin); break;
+    case 3: hipLaunchKernelGGL(conv2_fwd2_kernel<3>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, fin); break;
+    case 4: hipLaunchKernelGGL(conv2_fwd2_kernel<4>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, fin); break;
 #endif
-    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P); break;
+    default: hipLaunchKernelGGL(conv2_fwd2_kernel<0>, grid, block, F2_LDS, st, pp, w, bias, gamma, y2, ya, a2, partial, ypart, scales, order, sw, sk, B, P, fin); break;
   }
   TDS_LAUNCH_CHECK();
 }

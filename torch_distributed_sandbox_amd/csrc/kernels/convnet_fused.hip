@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "bf16x3.h"
+#include "bn_finalize.h"
 #include "launchers.h"
 
 namespace tds {
@@ -333,29 +334,6 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
   }
 }
 
-// Shifted BN finalize of channel c from its sums of (y - shift[c]) and (y - shift[c])^2.
-__device__ void bn_finalize_channel(int c, int C, double s, double ss, int64_t n, const float* __restrict__ shift,
-                                    float eps, float momentum, const float* __restrict__ gamma,
-                                    const float* __restrict__ beta, float* __restrict__ stats,
-                                    float* __restrict__ running_mean, float* __restrict__ running_var,
-                                    float* __restrict__ aff, float aff_scale = 1.f) {
-  const double m0 = s / (double)n;
-  double var = ss / (double)n - m0 * m0;
-  if (var < 0.0) var = 0.0;
-  const double mean = m0 + (shift ? (double)shift[c] : 0.0);
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  stats[c] = (float)mean;
-  stats[C + c] = invstd;
-  if (running_mean) {
-    const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
-    running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
-    running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
-  }
-  const float gm = gamma ? gamma[c] : 1.f, bt = beta ? beta[c] : 0.f;
-  aff[c] = gm * invstd * aff_scale;  // aff_scale: a power of two (the p1 range guard), exact
-  aff[C + c] = (bt - (float)mean * gm * invstd) * aff_scale;
-}
-
 // BN2: reduce the per-workgroup partials of channel c (partial[c][nchunk][2], fixed order) and
 // finalize it -- one workgroup per channel, one launch instead of a reduction + a finalize.
 __global__ __launch_bounds__(256) void bn_reduce_finalize_kernel(
@@ -428,7 +406,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __r
   __shared__ double sh[8];
   __shared__ uint32_t shm[8];
   const int c = blockIdx.x;
-  if (mag != nullptr) {  // magnitude bounds of the conv2 backward's fp16 scale (conv2_bwd.hip)
+  // magnitude bounds of the conv2 backward's fp16 scale (conv2_bwd.hip); ypart == nullptr: the
+  // conv2 forward reduced its part (mag[0..C)) in its own launch (conv2_fwd2.hip f2_finalize)
+  if (mag != nullptr && (c == C || ypart != nullptr)) {
     const uint32_t* src = c == C ? gpart : ypart + (int64_t)c * nyp;
     const int cnt = c == C ? ngp : nyp;
     uint32_t m = 0u;
@@ -547,11 +527,66 @@ constexpr int LM_X_BYTES = (LB_XR * LM_XS > LV_WORDS ? LB_XR * LM_XS : LV_WORDS)
 #endif
 // PAIRS (level input only; TDS_L1B_PAIRS=1 at run time, fused_ops.cpp): the conflict-free bf16-pair
 // x tile above.  Opt-in: timed slower than the default word layout (docs/KERNELS.md).
+// In-launch finalize of the layer-1 backward (common.h tds_arrive; replaces reduce_partials_kernel
+// and l1_finalize_kernel): groups of LB_GROUP workgroups, the last of a group sums the group's
+// partial rows into gsum[g], the last group-reducer sums the groups (fixed order) into bsum and
+// forms the closed-form layer-1 gradients (l1_finalize_one).
+constexpr int LB_GROUP = 32;
+struct LBFin {
+  uint32_t* sync;  // [0, ngroups): groups, [kSyncWordsPerSite - 1]: the group-reducers
+  double* gsum;    // [ngroups][16 * 27]
+  double* bsum;    // [16 * 27]
+  const double* gram;
+  int64_t n;
+  const float *w1, *b1, *gamma1, *stats1;
+  float *dw1, *db1, *dgamma1, *dbeta1;
+  float scale;
+};
+__device__ __forceinline__ void l1_finalize_one(int e, const double* __restrict__ bwd_sum,
+                                                const double* __restrict__ gram, int64_t n,
+                                                const float* __restrict__ w1, const float* __restrict__ b1,
+                                                const float* __restrict__ gamma1, const float* __restrict__ stats1,
+                                                float* __restrict__ dw1, float* __restrict__ db1,
+                                                float* __restrict__ dgamma1, float* __restrict__ dbeta1, float scale);
+
+__device__ __forceinline__ void l1_bwd_fin(const LBFin& fin, const double* __restrict__ partial, int* flag,
+                                           double* bs_lds) {
+  constexpr int R = 16 * LB_NACC;
+  const int nwg = (int)gridDim.x, wg = (int)blockIdx.x, tid = (int)threadIdx.x;
+  const int ng = (nwg + LB_GROUP - 1) / LB_GROUP, g = wg / LB_GROUP;
+  const int w0 = g * LB_GROUP, w1 = min(nwg, w0 + LB_GROUP);
+  if (!tds_arrive(fin.sync + g, (uint32_t)(w1 - w0), flag)) return;
+  for (int e = tid; e < R; e += 256) {
+    double s = 0.0;
+    // 8 loads in flight at a time: the kernel's 5-per-CU occupancy leaves <= 96 VGPRs
+#pragma unroll 1
+    for (int u0 = 0; u0 < LB_GROUP; u0 += 8) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = w0 + u0 + u < w1 ? partial[(int64_t)(w0 + u0 + u) * R + e] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    st_agent(fin.gsum + (int64_t)g * R + e, s);
+  }
+  if (!tds_arrive(fin.sync + kSyncWordsPerSite - 1, (uint32_t)ng, flag)) return;
+  for (int e = tid; e < R; e += 256) {
+    double s = 0.0;
+    for (int q = 0; q < ng; ++q) s += fin.gsum[(int64_t)q * R + e];
+    bs_lds[e] = s;
+    fin.bsum[e] = s;  // (kept for inspection)
+  }
+  __syncthreads();
+  for (int e = tid; e < 16 * 25; e += 256)
+    l1_finalize_one(e, bs_lds, fin.gram, fin.n, fin.w1, fin.b1, fin.gamma1, fin.stats1, fin.dw1, fin.db1,
+                    fin.dgamma1, fin.dbeta1, fin.scale);
+}
+
 template <bool LV, bool PAIRS>
 __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const uint4* __restrict__ dp1,
                                                           const uint32_t* __restrict__ dp1_dec,
                                                           const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
-                                                          double* __restrict__ partial, int B, int H, int W) {
+                                                          double* __restrict__ partial, int B, int H, int W, LBFin fin) {
   __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LM_X_BYTES];
   const uint32_t* dps = reinterpret_cast<const uint32_t*>(lds);  // dp1h tile [row 8][group 8][ch 16][px 4] fp16
   unsigned short* phs = nullptr;
@@ -825,9 +860,12 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   __syncthreads();
   double* out = partial + (int64_t)blockIdx.x * 16 * LB_NACC;
   for (int e = tid; e < 16 * LB_NACC; e += 256)
-    out[e] = (red[e] + red[16 * LB_NACC + e]) + (red[2 * 16 * LB_NACC + e] + red[3 * 16 * LB_NACC + e]);
+    st_agent(out + e, (red[e] + red[16 * LB_NACC + e]) + (red[2 * 16 * LB_NACC + e] + red[3 * 16 * LB_NACC + e]));
+  if (fin.sync != nullptr)
+    l1_bwd_fin(fin, partial, reinterpret_cast<int*>(lds + 4 * 16 * LB_NACC * 8 + 16 * LB_NACC * 8),
+               reinterpret_cast<double*>(lds + 4 * 16 * LB_NACC * 8));
 }
-static_assert(4 * 16 * LB_NACC * 8 <= LB_NP * 64 + LB_NP * 16 + LM_X_BYTES, "l1_bwd LDS reduction scratch");
+static_assert(5 * 16 * LB_NACC * 8 + 16 <= LB_NP * 64 + LB_NP * 16 + LM_X_BYTES, "l1_bwd LDS reduction scratch");
 
 // Gram of the conv1 patches from the x autocorrelation (one workgroup):
 //   G[k][j] = Full(d) - sum_{excluded rows of k} R(d,row) - sum_{excluded cols} C(d,col)
@@ -984,15 +1022,12 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
 // Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
 //   dw1[c][j] = a1 sdzx[c][j] + a2 (sum_k w1[c][k] G[k][j] + b1[c] S[j]) + a3 S[j]
 // one thread per (c, j) (400 of 512); every thread of channel c forms its a1..a3 (25 FMAs).
-__global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restrict__ bwd_sum,
-                                                          const double* __restrict__ gram, int64_t n,
-                                                          const float* __restrict__ w1, const float* __restrict__ b1,
-                                                          const float* __restrict__ gamma1,
-                                                          const float* __restrict__ stats1, float* __restrict__ dw1,
-                                                          float* __restrict__ db1, float* __restrict__ dgamma1,
-                                                          float* __restrict__ dbeta1, float scale) {
-  const int e = threadIdx.x;
-  if (e >= 16 * 25) return;
+__device__ __forceinline__ void l1_finalize_one(int e, const double* __restrict__ bwd_sum,
+                                                const double* __restrict__ gram, int64_t n,
+                                                const float* __restrict__ w1, const float* __restrict__ b1,
+                                                const float* __restrict__ gamma1, const float* __restrict__ stats1,
+                                                float* __restrict__ dw1, float* __restrict__ db1,
+                                                float* __restrict__ dgamma1, float* __restrict__ dbeta1, float scale) {
   const int c = e / 25, j = e - 25 * (e / 25);
   const double* acc = bwd_sum + c * LB_NACC;
   const double* G = gram;
@@ -1016,6 +1051,18 @@ __global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restri
   double h = (double)b1[c] * S[j];
   for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k * 25 + j];
   dw1[c * 25 + j] = (float)(scale * (a1 * acc[2 + j] + a2 * h + a3 * S[j]));
+}
+
+__global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restrict__ bwd_sum,
+                                                          const double* __restrict__ gram, int64_t n,
+                                                          const float* __restrict__ w1, const float* __restrict__ b1,
+                                                          const float* __restrict__ gamma1,
+                                                          const float* __restrict__ stats1, float* __restrict__ dw1,
+                                                          float* __restrict__ db1, float* __restrict__ dgamma1,
+                                                          float* __restrict__ dbeta1, float scale) {
+  const int e = threadIdx.x;
+  if (e >= 16 * 25) return;
+  l1_finalize_one(e, bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
 }
 
 }  // namespace tds
@@ -1092,21 +1139,54 @@ void tds_bn_bwd_finalize2(const double* partial, int C, int nchunk, int64_t n, c
 
 int tds_l1_bwd_rows(int nwg) { return nwg; }
 
+// workgroups of the chosen layer-1 backward variant that fit one CU (its VGPRs decide: 87-99 for
+// the level-input word layout -> 5, the fp32-image path -> 4)
+int tds_l1_bwd_max_per_cu(bool levels, bool pairs) {
+  int n = 0;
+  hipError_t e;
+  if (levels && pairs) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<true, true>, 256, 0);
+  else if (levels) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<true, false>, 256, 0);
+  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<false, false>, 256, 0);
+  return e == hipSuccess && n > 0 ? n : 4;
+}
+
+int tds_l1_bwd_fin_doubles(int nwg) { return ((nwg + LB_GROUP - 1) / LB_GROUP) * 16 * LB_NACC + 16 * LB_NACC; }
+
 void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
                 const uint8_t* idx1, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
-                hipStream_t st) {
-  (void)w1;
-  (void)b1;
+                hipStream_t st, const TdsL1Fin* lf) {
   const uint4* d = static_cast<const uint4*>(dp1h);
+  LBFin fin{};
+  if (lf != nullptr) {
+    fin.sync = tds_sync_words(kSyncL1Bwd, st);
+    if (fin.sync == nullptr || (nwg + LB_GROUP - 1) / LB_GROUP >= kSyncWordsPerSite) {
+      tds_launch_fail("l1_bwd: in-launch finalize unavailable (sync words / group count)");
+      return;
+    }
+    const int ng = (nwg + LB_GROUP - 1) / LB_GROUP;
+    fin.gsum = lf->work;
+    fin.bsum = lf->work + (int64_t)ng * 16 * LB_NACC;
+    fin.gram = lf->gram;
+    fin.n = (int64_t)B * H * W;
+    fin.w1 = w1;
+    fin.b1 = b1;
+    fin.gamma1 = lf->gamma1;
+    fin.stats1 = lf->stats1;
+    fin.dw1 = lf->dw1;
+    fin.db1 = lf->db1;
+    fin.dgamma1 = lf->dgamma1;
+    fin.dbeta1 = lf->dbeta1;
+    fin.scale = lf->scale;
+  }
   if (levels && pairs)
     hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, true>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
-                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W, fin);
   else if (levels)
     hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, false>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
-                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W, fin);
   else
     hipLaunchKernelGGL((l1_bwd_mfma_kernel<false, false>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
-                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W, fin);
   TDS_LAUNCH_CHECK();
 }
 

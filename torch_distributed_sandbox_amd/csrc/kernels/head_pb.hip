@@ -179,14 +179,27 @@ __device__ __forceinline__ void hp_store4(float* out, const PBGeom& g, const HPR
 
 // Forward.  partial[blk][B*NC] (fp64): this workgroup's share of logits[b][j] for images
 // b0 .. b0+NB-1; xout (optional): X in the fc's flatten order, [B][32*Q*Q].
+// fin (optional, one pass: B <= HP_MAXB): the logits are finished in this launch -- the last
+// workgroup of channel c to arrive sums the channel's rows into fin.cpart[c] (fixed order), the last
+// channel to finish sums the 32 channel rows and adds the bias (common.h tds_arrive; replaces
+// head_logits_kernel and its launch).
+struct HPFin {
+  uint32_t* sync;        // 33 counters: [c] per channel, [32] channels
+  double* cpart;         // [32][B*NC]
+  double* sums;          // [B*NC]
+  const float* bias;     // [NC] or nullptr
+  float* logits;         // [B*NC]
+};
 template <int NB>
 __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __restrict__ ya,
                                                                  const float* __restrict__ W,
                                                                  const float* __restrict__ aff2,
                                                                  double* __restrict__ partial,
                                                                  float* __restrict__ xout, PBGeom g, int Btot, int b0,
-                                                                 int NC) {
+                                                                 int NC, HPFin fin) {
   __shared__ float red[HP_THREADS / 64][HP_MAXB * 10];
+  __shared__ int last_flag;
+  __shared__ double wpart[256];
   const HPGrid hg = hp_grid(g);
   const int wg = blockIdx.x;
   const int c = wg / hg.per_channel(), band = wg - c * hg.per_channel();
@@ -264,7 +277,21 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
     const int b = i / NC, j = i - b * NC;
     const double s = (((double)red[0][b * 10 + j] + (double)red[1][b * 10 + j]) + (double)red[2][b * 10 + j]) +
                      (double)red[3][b * 10 + j];
-    partial[(int64_t)wg * Btot * NC + (b0 + b) * NC + j] = s;
+    st_agent(partial + (int64_t)wg * Btot * NC + (b0 + b) * NC + j, s);  // (write-through: tds_arrive)
+  }
+  if (fin.sync == nullptr) return;
+  const int BN = Btot * NC, nb = hg.per_channel();
+  if (!tds_arrive(fin.sync + c, (uint32_t)nb, &last_flag)) return;
+  // this channel's rows (one round of loads behind tds_arrive's acquire; host: BN <= 80, nb <= 48)
+  {
+    const double s = wide_row_sum(partial + (int64_t)c * nb * BN, nb, BN, BN, wpart);
+    if ((int)threadIdx.x < BN) st_agent(fin.cpart + (int64_t)c * BN + threadIdx.x, s);
+  }
+  if (!tds_arrive(fin.sync + 32, 32u, &last_flag)) return;
+  const double s = wide_row_sum(fin.cpart, 32, BN, BN, wpart);
+  if ((int)threadIdx.x < BN) {
+    fin.sums[threadIdx.x] = s;
+    fin.logits[threadIdx.x] = (float)s + (fin.bias ? fin.bias[threadIdx.x % NC] : 0.f);
   }
 }
 
@@ -295,13 +322,34 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const double* __restri
 //   same-address atomic per wave cost ~40 us per step (12.8 K of them at 3000^2).
 // KEEP: dW is also stored (UPD without KEEP: the update only -- optimizer-in-backward semantics,
 // the gradient itself is never materialised, 720 MB less written at 3000^2).
+// fin (optional; one pass over all 32 channels): the BN2 backward finalize in this launch (replaces
+// bn_bwd_finalize2_kernel): the last workgroup of channel c to arrive sums the channel's BN2 partials
+// (band order) into dgamma / dbeta / the dy2 constants k1..k3 and its max |g2m|; the last channel
+// to finish writes mag[32] (the max over channels) and the fc bias gradient.
+struct HBFin {
+  uint32_t* sync;          // 33 counters
+  uint32_t* cmax;          // [32] per-channel max |g2m| bits
+  const float* stats;      // [64] mean | invstd of BN2
+  const float* gamma;      // [32] or nullptr
+  float* dgamma;           // [32] or nullptr
+  float* dbeta;            // [32] or nullptr
+  float* kbuf;             // [96] k1 | k2 | k3
+  int64_t n;               // B * P * P
+  int B;
+  float* dbfc;             // [NC] or nullptr
+  float scale;
+  uint32_t* mag;           // mag[32] <- max |g2m| (nullptr: no magnitude bound)
+};
+
 template <int NB, bool WITH_DW, bool ACC, bool UPD, bool KEEP = true>
 __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     const float* __restrict__ ya, const float* W, const float* __restrict__ aff2, const float* __restrict__ dl,
     float* __restrict__ g2m, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass, int npass,
-    int NC, float scale, float lr, int c0, uint32_t* __restrict__ gpart) {
+    int NC, float scale, float lr, int c0, uint32_t* __restrict__ gpart, HBFin fin) {
   __shared__ float red[2][HP_THREADS / 64];
   __shared__ uint32_t gred[HP_THREADS / 64];
+  __shared__ double dred[2][HP_THREADS / 64];
+  __shared__ int last_flag;
   const HPGrid hg = hp_grid_b(g);
   // workgroups in the reverse of the forward's order: the backward starts on the channels the
   // forward streamed last, whose ya / weight lines are still in the 256 MB Infinity Cache
@@ -416,13 +464,62 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     uint32_t m = gred[0];
 #pragma unroll
     for (int i = 1; i < HP_THREADS / 64; ++i) m = max(m, gred[i]);
-    gpart[((int64_t)c * npass + pass) * hg.per_channel() + band] = m;
+    st_agent(gpart + ((int64_t)c * npass + pass) * hg.per_channel() + band, m);  // (write-through: tds_arrive)
   }
   if (threadIdx.x < 2) {
     const int k = threadIdx.x;
     const double s = (((double)red[k][0] + (double)red[k][1]) + (double)red[k][2]) + (double)red[k][3];
     const int64_t nblk = (int64_t)hg.per_channel();
-    partial[(((int64_t)c * npass + pass) * nblk + band) * 2 + k] = s;
+    st_agent(partial + (((int64_t)c * npass + pass) * nblk + band) * 2 + k, s);
+  }
+  if (fin.sync == nullptr) return;
+  const int nb = hg.per_channel();
+  if (!tds_arrive(fin.sync + c, (uint32_t)nb, &last_flag)) return;
+  {  // channel c: its bands in order (one pass: partial row = c * nb + band)
+    double sdz = 0.0, sdzy = 0.0;
+    uint32_t m = 0u;
+    for (int k = lane + 64 * wv; k < nb; k += HP_THREADS) {  // (nb <= 256 at Q <= 2044: one load each)
+      const double2 v = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nb + k) * 2);
+      sdz += v.x;
+      sdzy += v.y;
+      if (gpart != nullptr) m = max(m, gpart[(int64_t)c * nb + k]);
+    }
+    sdz = wave_sum(sdz);
+    sdzy = wave_sum(sdzy);
+    m = wave_max(m);
+    if (lane == 0) {
+      dred[0][wv] = sdz;
+      dred[1][wv] = sdzy;
+      gred[wv] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      sdz = ((dred[0][0] + dred[0][1]) + dred[0][2]) + dred[0][3];
+      sdzy = ((dred[1][0] + dred[1][1]) + dred[1][2]) + dred[1][3];
+      m = max(max(gred[0], gred[1]), max(gred[2], gred[3]));
+      st_agent(fin.cmax + c, m);
+      const double mean = fin.stats[c], is = fin.stats[32 + c];
+      const double gm = fin.gamma ? fin.gamma[c] : 1.0;
+      const double sdxh = sdzy - mean * sdz;  // sum dz*(y-mean)
+      if (fin.dgamma) fin.dgamma[c] = (float)(is * sdxh);
+      if (fin.dbeta) fin.dbeta[c] = (float)sdz;
+      const double k1 = gm * is;
+      const double k2 = -gm * is * is * is * sdxh / (double)fin.n;
+      const double k3 = -gm * is * sdz / (double)fin.n - k2 * mean;
+      fin.kbuf[c] = (float)k1;
+      fin.kbuf[32 + c] = (float)k2;
+      fin.kbuf[64 + c] = (float)k3;
+    }
+  }
+  if (!tds_arrive(fin.sync + 32, 32u, &last_flag)) return;
+  if (threadIdx.x < 64) {
+    const uint32_t m = wave_max(threadIdx.x < 32 ? fin.cmax[threadIdx.x] : 0u);
+    if (threadIdx.x == 0 && fin.mag != nullptr) fin.mag[32] = m;
+  } else if (fin.dbfc != nullptr && (int)threadIdx.x - 64 < NC) {
+    const int j = (int)threadIdx.x - 64;
+    float v = 0.f;
+    for (int b = 0; b < fin.B; ++b) v += dl[b * NC + j];
+    fin.dbfc[j] = v * fin.scale;
   }
 }
 
@@ -434,18 +531,30 @@ int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // fo
 int tds_head_bwd_pb_nblk(int Q) { return hp_grid_b(pb_geom(Q)).per_channel(); }  // backward workgroups per channel
 int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
 
-// partial: double [32 * nblk][B*NC]; sums: double [B*NC]
+// partial: double [32 * nblk + 32][B*NC] (the last 32 rows: the in-launch finalizer's channel sums);
+// sums: double [B*NC].  fused_fin = false: the separate head_logits launch (the A/B reference)
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
-                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st) {
+                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st, bool fused_fin) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1) return -1;
   const PBGeom g = pb_geom(Q);
   const int nwg = 32 * hp_grid(g).per_channel();
+  // one pass: the logits are finished inside the launch (HPFin; partial then holds nwg + 32 rows)
+  HPFin fin{nullptr, nullptr, nullptr, nullptr, nullptr};
+  const int BN = B * NC, nbc = hp_grid(g).per_channel();
+  const bool wide_ok = BN <= 256 && nbc <= WRS_MAXL * (256 / BN) && 32 <= WRS_MAXL * (256 / BN);
+  if (B <= HP_MAXB && fused_fin && wide_ok && tds_fused_fin_enabled()) {
+    fin.sync = tds_sync_words(kSyncHeadFwd, st);
+    fin.cpart = partial + (int64_t)nwg * B * NC;
+    fin.sums = sums;
+    fin.bias = bias;
+    fin.logits = logits;
+  }
   for (int b0 = 0; b0 < B; b0 += HP_MAXB) {
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
 #define TDS_HPF(NBV)                                                                                                   \
   case NBV:                                                                                                            \
     hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
-                       B, b0, NC);                                                                                     \
+                       B, b0, NC, fin);                                                                                \
     TDS_LAUNCH_CHECK();                                                                                                \
     break;
     switch (nb) {
@@ -454,7 +563,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
     }
 #undef TDS_HPF
   }
-  const int BN = B * NC;
+  if (fin.sync != nullptr) return 0;
   hipLaunchKernelGGL(head_logits_kernel, dim3(BN), dim3(256), 0, st, partial, nwg, sums, bias, logits, BN, NC);
   TDS_LAUNCH_CHECK();
   return 0;
@@ -465,11 +574,28 @@ int tds_head_bwd_pb_npass(int B) { return (B + HP_MAXB - 1) / HP_MAXB; }
 
 int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
-                    int c1, uint32_t* gpart, hipStream_t st) {
+                    int c1, uint32_t* gpart, hipStream_t st, const TdsHeadBwdFin* hf) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1 || c0 < 0 || c1 > 32 || c0 >= c1) return -1;
   const int npass = tds_head_bwd_pb_npass(B);
   if (Wupd && npass != 1) return -2;  // the fused SGD step needs the whole dW in one pass
   const PBGeom g = pb_geom(Q);
+  HBFin fin{};
+  if (hf != nullptr) {
+    if (npass != 1 || c0 != 0 || c1 != 32 || hp_grid_b(g).per_channel() > HP_THREADS) return -3;
+    fin.sync = tds_sync_words(kSyncHeadBwd, st);
+    if (fin.sync == nullptr) return -4;
+    fin.cmax = hf->cmax;
+    fin.stats = hf->stats;
+    fin.gamma = hf->gamma;
+    fin.dgamma = hf->dgamma;
+    fin.dbeta = hf->dbeta;
+    fin.kbuf = hf->kbuf;
+    fin.n = (int64_t)B * (2 * Q) * (2 * Q);
+    fin.B = B;
+    fin.dbfc = hf->dbfc;
+    fin.scale = scale;
+    fin.mag = hf->mag;
+  }
   const int nwg = (c1 - c0) * hp_grid_b(g).per_channel();
   for (int pass = 0; pass < npass; ++pass) {
     const int b0 = pass * HP_MAXB;
@@ -477,7 +603,7 @@ int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const 
     const bool acc = pass > 0;
 #define TDS_HPB_E(NBV, WD, AC, UP, KP)                                                                             \
   hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, \
-                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gpart);
+                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gpart, fin);
 #define TDS_HPB(NBV)                                   \
   case NBV:                                            \
     if (!dW && Wupd) {                                 \

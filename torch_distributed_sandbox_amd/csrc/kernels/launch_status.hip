@@ -1,6 +1,10 @@
 // First failed kernel launch of the calling host thread (see TDS_LAUNCH_CHECK in common.h).
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "common.h"
 #include "launchers.h"
@@ -44,4 +48,35 @@ __global__ void tds_probe_kernel(int* out) {
 void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st) {
   hipLaunchKernelGGL(tds_probe_kernel, dim3(1), dim3(threads), lds_bytes, st, out);
   TDS_LAUNCH_CHECK();
+}
+
+// Counter words of the in-launch finalizers (common.h tds_arrive): one zeroed block per (device,
+// stream), kSyncWordsPerSite words per call site.  Zeroed once, on the stream, when allocated;
+// every reducer resets the counter it used, so each launch on that stream finds it at 0.
+uint32_t* tds_sync_words(int site, hipStream_t st) {
+  if (site < 0 || site >= tds::kSyncSites) return nullptr;
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, uint32_t*> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  uint32_t*& w = cache[{dev, st}];
+  if (w == nullptr) {
+    const size_t bytes = (size_t)tds::kSyncSites * tds::kSyncWordsPerSite * sizeof(uint32_t);
+    if (hipMalloc(&w, bytes) != hipSuccess) {
+      w = nullptr;
+      return nullptr;
+    }
+    if (hipMemsetAsync(w, 0, bytes, st) != hipSuccess) return nullptr;
+  }
+  return w + (size_t)site * tds::kSyncWordsPerSite;
+}
+
+// TDS_FUSED_FIN=0 restores the separate finalize launches (A/B timing and a fallback)
+bool tds_fused_fin_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("TDS_FUSED_FIN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }

@@ -87,9 +87,24 @@ void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c);
 // window of y2 by sign(gamma2); a2 [B][P/2][P/2][2]: the windows' argmax codes (conv2_common.h)
 // ypart (optional): max |y2 - b2| per (channel, workgroup), [32][nwg] float bits
 // scales (optional): mag + kMagScales (conv2_pack.hip), the packed weights' and p1's inverse scales
+// BN finalize inside a producer launch (conv2_fwd2: BN2): parameters and the outputs it writes
+struct TdsBnFin {
+  const float* beta;
+  float eps, momentum;
+  float* stats;          // [2C] mean | invstd
+  float* running_mean;   // nullable
+  float* running_var;
+  int64_t* num_batches;  // nullable
+  float* aff;            // [2C] a | b
+  uint32_t* mag;         // conv2_fwd2: [32] max |y2 - b2| (float bits), nullable
+  double* dwork;         // tds_conv2_fwd2_fin_doubles(nwg)
+  uint32_t* uwork;       // tds_conv2_fwd2_fin_words(nwg)
+};
+int tds_conv2_fwd2_fin_doubles(int nwg);
+int tds_conv2_fwd2_fin_words(int nwg);
 void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
                     uint32_t* a2, double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
-                    int B, int P, hipStream_t st);
+                    int B, int P, hipStream_t st, const TdsBnFin* bn = nullptr);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
 void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // rolling-window backward (conv2_bwd.hip): walk = tds_conv2_bwd_walk table for nwg workgroups
@@ -136,9 +151,20 @@ void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n,
                             float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
 // dp1h: the conv2 backward's (conv2_common.h), dp1_dec: its decode factor (float bits, device)
+// the layer-1 backward's finalize inside its launch (replaces tds_reduce_partials + tds_l1_finalize)
+struct TdsL1Fin {
+  double* work;  // tds_l1_bwd_fin_doubles(nwg)
+  const double* gram;
+  const float* gamma1;
+  const float* stats1;
+  float *dw1, *db1, *dgamma1, *dbeta1;
+  float scale;
+};
+int tds_l1_bwd_fin_doubles(int nwg);
+int tds_l1_bwd_max_per_cu(bool levels, bool pairs);  // occupancy of the variant (hipOccupancy...)
 void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
                 const uint8_t* idx1, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
-                hipStream_t st);
+                hipStream_t st, const TdsL1Fin* lf = nullptr);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);
@@ -147,15 +173,33 @@ void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const
 int64_t tds_pb_plane(int Q);  // floats per (image, channel) plane
 int tds_head_pb_nblk(int Q);  // workgroups per channel
 int tds_head_bwd_pb_nblk(int Q);  // the backward's workgroups per channel (its partial / gpart rows)
+// in-launch finalizer counters (launch_status.hip; common.h tds_arrive); nullptr: no fused finalize
+uint32_t* tds_sync_words(int site, hipStream_t st);
+bool tds_fused_fin_enabled();  // TDS_FUSED_FIN=0: the separate finalize launches
+
+// partial: [32 * nblk + 32][B*NC] doubles; fused_fin: logits finished in the launch (B <= 8)
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
-                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st);
+                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st,
+                    bool fused_fin = true);
 int tds_head_bwd_pb_npass(int B);
 // channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
 // soon as its launch lands; the BN2 partials of the other channels are left untouched)
 // gpart (optional): max |g2m| per workgroup (float bits), [32][npass][nblk]
+// hf (optional): the BN2 backward finalize inside the launch (one pass, all channels; replaces
+// tds_bn_bwd_finalize2 when the conv2 forward reduced mag[0..32) itself)
+struct TdsHeadBwdFin {
+  uint32_t* cmax;  // [32] scratch
+  const float* stats;
+  const float* gamma;
+  float* dgamma;
+  float* dbeta;
+  float* kbuf;     // [96]
+  float* dbfc;     // [NC] or nullptr
+  uint32_t* mag;   // mag[32] <- max |g2m|, or nullptr
+};
 int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
-                    int c1, uint32_t* gpart, hipStream_t st);
+                    int c1, uint32_t* gpart, hipStream_t st, const TdsHeadBwdFin* hf = nullptr);
 
 // ---- zs_exchange.hip (zero-suppressed fc-input rows, parallel/zs.py)
 int64_t tds_zs_npages(int64_t n);

@@ -37,6 +37,8 @@ autograd a zero-stride fp16 placeholder (no kernel, no memory), as it does for y
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import _ext
@@ -171,30 +173,43 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2", "mag")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done")
+
+
+# The small reductions behind BN2 (forward statistics, backward constants) and the logits run
+# inside the producing kernels' launches (the last workgroup to arrive finalizes: common.h
+# tds_arrive) instead of as separate launches; TDS_FUSED_FIN=0 restores the separate launches.
+_FUSED_FIN = os.environ.get("TDS_FUSED_FIN", "1").strip() != "0"
 
 
 class _Conv2(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, p1, w2, b2, g2, link, link1):
+    def forward(ctx, p1, w2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, link, link1):
         ops = _ext.ops()
         # magnitude bounds of this step (per-workgroup max |y2 - b2| here, max |g2m| in the head
-        # backward, reduced by its BN2 finalize): the conv2 backward's fp16 scale of dy2
+        # backward): the conv2 backward's fp16 scale of dy2
         link.mag = torch.empty(ops.mag_numel(p1.shape[0], p1.shape[1]), device=p1.device, dtype=torch.int32)
         wp, wd = ops.conv2_pack(w2.contiguous(), link.mag, getattr(link1, "p1_scale", None))
         # a2: each pooling window's argmax, saved for the backward (max_pool2d_with_indices' indices)
-        y2, partial2, ya, a2 = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
+        link.bn_done = _FUSED_FIN
+        if _FUSED_FIN:
+            # BN2 finalized in the conv2 forward's launch: (stats2, aff2) instead of the partials
+            y2, ya, a2, bn_a, bn_b = ops.fused_conv2_forward_bn(p1, wp, b2, g2, be2, rm2, rv2, nbt2, momentum, eps,
+                                                                link.mag)
+        else:
+            y2, bn_a, ya, a2 = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
+            bn_b = bn_a.new_empty(0)
         ctx.save_for_backward(p1, wd, y2, a2)
         ctx.params = (w2, b2)
         ctx.link = link
         ctx.link1 = link1
-        ctx.mark_non_differentiable(partial2, ya)
-        # no zero-filled gradients for partial2 / ya (a 360 MB fill per step at the bench shape)
+        ctx.mark_non_differentiable(ya, bn_a, bn_b)
+        # no zero-filled gradients for ya / the BN2 tensors (a 360 MB fill per step at the bench shape)
         ctx.set_materialize_grads(False)
-        return y2, partial2, ya
+        return y2, ya, bn_a, bn_b
 
     @staticmethod
-    def backward(ctx, _dy2_placeholder, _unused, _unused_ya):
+    def backward(ctx, _dy2_placeholder, _unused_ya, _unused_a, _unused_b):
         p1, wd, y2, a2 = ctx.saved_tensors
         link = ctx.link
         _run_before_conv2_backward()
@@ -208,7 +223,7 @@ class _Conv2(torch.autograd.Function):
             # dp1h (fp16, scaled) and its decode factor, which the conv2 backward wrote into mag
             ctx.link1.dp1, ctx.link1.dp1_dec = dp1, mag[44:45]
             dp1_ph = _zero_scalar(p1.device, p1.dtype).expand(p1.shape)
-        return dp1_ph, dw2, db2, None, None, None
+        return dp1_ph, dw2, db2, None, None, None, None, None, None, None, None, None
 
 
 class _Head(torch.autograd.Function):
@@ -217,14 +232,18 @@ class _Head(torch.autograd.Function):
     constants), autograd gets a zero-stride placeholder."""
 
     @staticmethod
-    def forward(ctx, y2, ya, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex, link):
+    def forward(ctx, y2, ya, bn_a, bn_b, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex, link):
         ops = _ext.ops()
         P = y2.shape[1]
         x_out = None
         if ex is not None and ex.planned(ya.shape[0]) in ("activations", "sharded"):
             x_out = torch.empty((ya.shape[0], wfc.shape[1]), device=ya.device, dtype=torch.float32)
-        logits, stats2, aff2 = ops.fused_head_forward(ya, partial2, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
-                                                      bfc, P, x_out)
+        if link.bn_done:  # (bn_a, bn_b) = BN2's (stats, affine), finalized by the conv2 forward
+            stats2, aff2 = bn_a, bn_b
+            logits = ops.fused_head_forward_aff(ya, aff2, wfc, bfc, P, x_out)
+        else:  # bn_a = the conv2 forward's BN2 partials
+            logits, stats2, aff2 = ops.fused_head_forward(ya, bn_a, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
+                                                          bfc, P, x_out)
         if ex is not None and not ex.begin(x_out, rows=ya.shape[0]):
             raise RuntimeError("fc gradient exchange refused to start after ready() agreed")
         ctx.save_for_backward(ya, stats2, aff2, g2, wfc)
@@ -250,7 +269,7 @@ class _Head(torch.autograd.Function):
             B, Q = ya.shape[0], P // 2
             g2m_buf = torch.empty((B, 32, Q, Q), device=ya.device, dtype=torch.float32)
             part = torch.empty(ops.head_bwd_workspace(B, P), device=ya.device, dtype=torch.float64)
-            _, dg_o, dbe_o = _sinks(ctx, ctx.small, (12, 4, 5))
+            _, dg_o, dbe_o = _sinks(ctx, ctx.small, (13, 5, 6))
             # accumulating under no_sync(): this step's chunk goes to a scratch dW, then is added
             dst = torch.empty_like(dw) if acc_w else dw
             chunks = ex.column_chunks(wfc.shape[1], planes=32)
@@ -270,22 +289,22 @@ class _Head(torch.autograd.Function):
         elif ex is not None:
             # fc gradients come from the activation exchange (parallel/factored.py)
             _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, None, 1.0,
-                                                                 False, mag=ctx.link.mag)
+                                                                 False, mag=ctx.link.mag, ypart_done=ctx.link.bn_done)
             ex.defer(dlogits)
             dW = dbfc = None
         else:
-            dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[11] else None, wfc.shape, wfc)
+            dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[12] else None, wfc.shape, wfc)
             # world size 1 under DDP(overlap_optimizer): the SGD step of the fc weight runs in
             # this same kernel (ops/fused_update.py)
             lr = None
-            if ctx.needs_input_grad[11] and ya.shape[0] <= 8:  # one pass of head_bwd_pb_kernel
+            if ctx.needs_input_grad[12] and ya.shape[0] <= 8:  # one pass of head_bwd_pb_kernel
                 lr = fused_update.take(ctx.wfc_param)
             keep = not lr or fused_update.keep_grad(ctx.wfc_param)
-            dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (12, 4, 5))
+            dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (13, 5, 6))
             dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P,
                                                                      dw_out if keep else None, 1.0, True,
                                                                      float(lr or 0.0), dbfc_o, dg_o, dbe_o, keep,
-                                                                     mag=ctx.link.mag)
+                                                                     mag=ctx.link.mag, ypart_done=ctx.link.bn_done)
             if lr:
                 # update-only step: no gradient for the weight (dW is None), as in torch's
                 # optimizer-in-backward; the owner marks the parameter ready
@@ -294,7 +313,7 @@ class _Head(torch.autograd.Function):
         link.g2m, link.kbuf, link.aff2 = g2m, kbuf, aff2
         shape, dtype, device = ctx.y2_meta
         dy2 = _zero_scalar(device, dtype).expand(shape)
-        return (dy2, None, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None, None)
+        return (dy2, None, None, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None, None)
 
 
 def forward(model, x):
@@ -305,7 +324,9 @@ def forward(model, x):
     p1 = _Layer1.apply(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
                        bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps), link1)
     link = _Layer2Link()
-    y2, partial2, ya = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, link, link1)
+    y2, ya, bn_a, bn_b = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
+                                      bn2.running_var, bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps),
+                                      link, link1)
     # the fc update may still be running on DDP's side stream (overlap_optimizer): wait here,
     # after the convolutions were queued, not before
     param_fence.wait(fc.weight)
@@ -313,5 +334,5 @@ def forward(model, x):
     ex = factored.get(fc.weight)
     if ex is not None and not ex.ready(x.shape[0]):
         ex = None
-    return _Head.apply(y2, ya, partial2, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
+    return _Head.apply(y2, ya, bn_a, bn_b, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
                        bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias, ex, link)
