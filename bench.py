@@ -133,6 +133,11 @@ def _parser():
                          "--sim-comm-ctas workgroups of RCCL's size (256 threads, 19.7 KB LDS) for this many "
                          "microseconds on a side stream (recorded in the JSON; not a training number)")
     ap.add_argument("--sim-comm-ctas", type=int, default=16)
+    ap.add_argument("--sim-sdma-mb", type=float, default=0.0,
+                    help="rehearsal on one GPU: after each forward, copy this many MB device-to-device on a side "
+                         "stream beside the backward (the fc exchange's bulk payload), joined at the step's end")
+    ap.add_argument("--sim-sdma-engine", default="nocu", choices=["nocu", "blit"],
+                    help="--sim-sdma-mb copy by the copy engines (hipMemcpyDeviceToDeviceNoCU) or the blit kernel")
     ap.add_argument("--spawn-timeout", type=float, default=570.0,
                     help="self-spawn: terminate all ranks if the job runs longer than this (s)")
     ap.add_argument("--pg-timeout", type=float, default=120.0,
@@ -609,6 +614,11 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             convnet_fused.attach_input_stats(x, stats)
         pending[i] = x
 
+    sdma = None
+    if on_gpu and args.sim_sdma_mb > 0:
+        n = int(args.sim_sdma_mb * 1e6) // 4
+        sdma = (torch.cuda.Stream(device), torch.empty(n, device=device), torch.zeros(n, device=device))
+
     def step(i):
         j = i % pool
         if i in pending:
@@ -623,10 +633,16 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             sim_stream.wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(sim_stream):
                 tds._ext.ops().comm_spin(out, args.sim_comm_us, args.sim_comm_ctas, 19744)
+        if sdma is not None:  # the copy starts when the forward is done and runs beside the backward
+            sdma[0].wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(sdma[0]):
+                tds._ext.ops().copy_engine(sdma[1], sdma[2], args.sim_sdma_engine == "nocu")
         loss = criterion(out, lab_pool[j])
         optimizer.zero_grad()
         TF.backward(loss)
         optimizer.step()
+        if sdma is not None:
+            torch.cuda.current_stream(device).wait_stream(sdma[0])
         if data_stream is not None:
             convnet_fused._before_conv2_backward.clear()  # (a plan without the hook)
         return loss
@@ -706,6 +722,8 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             config["preflight"] = preflight
         if probe is not None:
             config["allreduce_probe"] = probe
+        if sdma is not None:
+            config["sim_sdma"] = {"MB": args.sim_sdma_mb, "engine": args.sim_sdma_engine}
         if sim_stream is not None:
             config["sim_comm"] = {"us": args.sim_comm_us, "ctas": args.sim_comm_ctas,
                                   "cu_mask_layout": os.environ.get("TDS_CU_MASK_LAYOUT", "striped")}

@@ -174,6 +174,43 @@ def test_activation_exchange_fused_convnet(pg, gpu, mode):
     assert ddp.exchanges[0].steps_exchanged == 2
 
 
+def test_zs_encode_from_ya_bitwise(gpu):
+    """The activation exchange encodes the fc input rows straight from the fused head's ya and BN2
+    affine (ops.zs_encode_ya, kernels/zs_exchange.hip): its records, values and count must be bitwise
+    those of encoding the X the head forward writes (x_out), -0.0 / NaN included, and the
+    overflow path's materialised rows (factored._YaRows.dense) must be that X."""
+    import torch_distributed_sandbox_amd as tds
+    from torch_distributed_sandbox_amd.parallel import factored, zs
+
+    ops = tds._ext.ops()
+    torch.manual_seed(3)
+    for B, P in ((3, 64), (5, 100)):
+        Q = P // 2
+        Q4, Q8 = (Q + 3) // 4, (Q + 7) // 8  # pooled-blocked plane (kernels/pooled_layout.h)
+        ya = torch.randn(B, 32, Q4 * Q8 * 32, device=gpu)
+        ya.view(-1)[::997] = float("nan")
+        aff2 = torch.cat([torch.randn(32, device=gpu), torch.randn(32, device=gpu) * 0.5])
+        aff2[3] = 0.0  # a whole channel of +0.0 / -0.0 candidates
+        K = 32 * Q * Q
+        wfc = torch.randn(10, K, device=gpu) * 1e-3
+        x = torch.empty(B, K, device=gpu)
+        ops.fused_head_forward_aff(ya, aff2, wfc, None, P, x)
+        n = B * K
+        m1 = torch.empty(zs.meta_numel(n), device=gpu, dtype=torch.int32)
+        m2 = torch.empty_like(m1)
+        v1 = torch.full((n,), 7.0, device=gpu)
+        v2 = torch.full((n,), 7.0, device=gpu)
+        c1 = zs.encode(x, m1, v1)
+        c2 = ops.zs_encode_ya(ya, aff2, P, m2, v2)
+        torch.cuda.synchronize()
+        assert int(c1) == int(c2) and 0 < int(c1) < n
+        assert torch.equal(m1, m2)
+        k = int(c1)
+        assert torch.equal(v1[:k].view(torch.int32), v2[:k].view(torch.int32))
+        dense = factored._YaRows(ya, aff2, P, B, K).dense()
+        assert torch.equal(dense.view(torch.int32), x.view(torch.int32))
+
+
 @pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("sharded", False),
                                            ("chunked", False),
                                            ("allreduce", True), ("activations", True), ("sharded", True)])
@@ -203,6 +240,8 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     for step in range(4):
         x = torch.rand(3, 1, H, H, device=gpu, generator=g)
         y = torch.randint(0, 10, (3,), device=gpu, generator=g)
+        if step == 2 and d1.exchanges:  # a capacity below this step's counts: the dense re-send path
+            d1.exchanges[0].force_capacity_once(1)
         for d, o in ((d1, o1), (d2, o2)):
             loss = crit(d(x), y)
             o.zero_grad()
@@ -213,6 +252,8 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
             assert not d1._fused_done  # consumed by the step: the bias was updated, the weight skipped
     d1.wait_pending_updates()
     torch.cuda.synchronize()
+    if exchange in ("activations", "sharded") and d1.exchanges[0].compress:
+        assert d1.exchanges[0].zs_stats["overflows"] >= 1  # step 2 went through the dense re-send
     for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
         if fuse:  # same arithmetic (p - lr*g) in another kernel: equal up to fma contraction
             assert torch.allclose(p, q, rtol=1e-6, atol=1e-9), n

@@ -411,6 +411,47 @@ Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor
   return logits;
 }
 
+// The head forward applying the activation exchange's deferred weight update on the way through
+// (head_pb.hip HPUpd): wfc <- wfc - lr * scale * dy_all^T X with X decoded from the gathered zero-
+// suppressed encodings (meta_all [W, R] int32, vals_all [W, cap]), then the logits with the updated
+// weight.  rows: rows per rank (dy_all [W * rows, NC]).
+Tensor fused_head_forward_upd(const Tensor& ya, const Tensor& aff2, const Tensor& wfc, const c10::optional<Tensor>& bfc,
+                              int64_t P, const Tensor& dy_all, const Tensor& meta_all, const Tensor& vals_all,
+                              int64_t rows, double scale, double lr) {
+  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_upd: ya must be [B,32,PB]");
+  const int64_t B = ya.size(0), Q = P / 2;
+  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(aff2, at::kFloat, {64}, "aff2");
+  const int64_t NC = wfc.size(0), K = 32 * Q * Q;
+  need(wfc, at::kFloat, {NC, K}, "fc.weight");
+  const float* bf = optf(bfc, NC, "fc.bias");
+  TORCH_CHECK(meta_all.dim() == 2 && vals_all.dim() == 2 && meta_all.size(0) == vals_all.size(0),
+              "fused_head_forward_upd: meta_all [W, R], vals_all [W, cap]");
+  const int64_t W = meta_all.size(0), M = dy_all.size(0);
+  TORCH_CHECK(rows >= 1 && M == W * rows, "fused_head_forward_upd: dy_all must hold W * rows rows");
+  need(dy_all, at::kFloat, {M, NC}, "dy_all");
+  TORCH_CHECK(meta_all.scalar_type() == at::kInt && meta_all.is_contiguous() && vals_all.scalar_type() == at::kFloat &&
+                  vals_all.is_contiguous(), "fused_head_forward_upd: meta_all int32, vals_all fp32, contiguous");
+  const int64_t NP = tds_zs_npages(rows * K);
+  TORCH_CHECK(meta_all.size(1) >= NP * 65, "fused_head_forward_upd: meta_all rows shorter than the page records");
+  c10::DeviceGuard guard(ya.device());
+  hipStream_t st = stream_of(ya);
+  auto wo = at::empty({W, NP * 64}, ya.options().dtype(at::kInt));
+  tds_zs_word_offsets(meta_all.data_ptr<int>(), meta_all.size(1), NP, (int)W, wo.data_ptr<int>(), st);
+  const int nblk = 32 * tds_head_pb_nblk((int)Q);
+  auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
+  auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
+  auto logits = at::empty({B, NC}, ya.options());
+  const int rc = tds_head_fwd_pb_upd(ya.data_ptr<float>(), const_cast<float*>(wfc.data_ptr<float>()), bf,
+                                     aff2.data_ptr<float>(), part.data_ptr<double>(), lsum.data_ptr<double>(),
+                                     logits.data_ptr<float>(), (int)B, (int)Q, (int)NC, dy_all.data_ptr<float>(), (int)M,
+                                     (int)rows, meta_all.data_ptr<int>(), meta_all.size(1), wo.data_ptr<int>(), NP * 64,
+                                     vals_all.data_ptr<float>(), vals_all.size(1), (float)scale, (float)lr, st);
+  TORCH_CHECK(rc == 0, "fused_head_forward_upd: unsupported shape (B <= 8, W * rows <= 40, P/2 >= 8)");
+  check_launches("fused_head_forward_upd");
+  return logits;
+}
+
 // ---------------------------------------------------------------- head forward (BN2 finalize + fc)
 // returns (logits, stats2 [mean32|invstd32], aff2 [a32|b32])
 std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
@@ -662,6 +703,18 @@ int64_t cu_side_stream(int64_t device, bool comm) {
 
 // one-GPU rehearsal of a collective's CU footprint (cu_budget.hip): `nblocks` workgroups of 256
 // threads holding `lds_bytes` of LDS each for `us` microseconds, on the current stream
+// Device-to-device copy on the current stream of dst's device by the copy engines (SDMA, no compute
+// units: hipMemcpyDeviceToDeviceNoCU) or, nocu = false, the runtime's blit kernel -- the bulk
+// payload of the fc exchange rehearsed on one GPU (bench.py --sim-sdma-mb)
+void copy_engine(const Tensor& dst, const Tensor& src, bool nocu) {
+  TORCH_CHECK(dst.is_cuda() && src.is_cuda() && dst.is_contiguous() && src.is_contiguous() &&
+                  dst.nbytes() == src.nbytes(), "copy_engine: contiguous GPU tensors of equal size");
+  c10::DeviceGuard guard(dst.device());
+  const hipError_t e = hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), dst.nbytes(),
+                                      nocu ? hipMemcpyDeviceToDeviceNoCU : hipMemcpyDeviceToDevice, stream_of(dst));
+  TORCH_CHECK(e == hipSuccess, "copy_engine: hipMemcpyAsync failed: ", hipGetErrorString(e));
+}
+
 void comm_spin(const Tensor& like, int64_t us, int64_t nblocks, int64_t lds_bytes) {
   TORCH_CHECK(like.is_cuda(), "comm_spin: needs a GPU tensor");
   TORCH_CHECK(us >= 0 && us <= 1000000 && nblocks >= 1 && nblocks <= 1024 && lds_bytes >= 1024 &&
@@ -778,6 +831,27 @@ Tensor zs_encode(const Tensor& x, const Tensor& meta_out, const Tensor& values_o
   return nnz;
 }
 
+// The zs encoding of X = relu(a * ya + b) (the fused head's fc input, [B, 32*Q*Q] flat in the fc
+// order) read from ya [B,32,PB] and aff2 [64]: the dense X is never written (kernels/zs_exchange.hip)
+Tensor zs_encode_ya(const Tensor& ya, const Tensor& aff2, int64_t P, const Tensor& meta_out, const Tensor& values_out) {
+  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "zs_encode_ya: ya must be [B,32,PB]");
+  const int64_t B = ya.size(0), Q = P / 2, n = B * 32 * Q * Q, NP = tds_zs_npages(n);
+  TORCH_CHECK(Q >= 8, "zs_encode_ya: needs P/2 >= 8");
+  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(aff2, at::kFloat, {64}, "aff2");
+  need(meta_out, at::kInt, {NP * 65}, "zs meta_out");
+  TORCH_CHECK(values_out.is_cuda() && values_out.scalar_type() == at::kFloat && values_out.is_contiguous() &&
+                  values_out.dim() == 1 && values_out.device() == ya.device(),
+              "zs_encode_ya: values_out fp32 1-d contiguous GPU (ya's device)");
+  TORCH_CHECK(n < ((int64_t)1 << 31), "zs_encode_ya: the format's int32 offsets need < 2^31 elements");
+  c10::DeviceGuard guard(ya.device());
+  auto nnz = at::empty({}, ya.options().dtype(at::kLong));
+  tds_zs_encode_ya(ya.data_ptr<float>(), aff2.data_ptr<float>(), (int)B, (int)Q, meta_out.data_ptr<int>(),
+                   values_out.data_ptr<float>(), values_out.numel(), nnz.data_ptr<int64_t>(), stream_of(ya));
+  check_launches("zs_encode_ya");
+  return nnz;
+}
+
 void zs_decode(const Tensor& meta, const Tensor& values, const Tensor& out) {
   TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kFloat && out.is_contiguous(), "zs_decode: out fp32 GPU");
   const int64_t n = out.numel(), P = tds_zs_npages(n);
@@ -889,6 +963,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor(a!) out) -> ()",
       &zs_seg_decode);
   m.def("zs_decode(Tensor meta, Tensor values, Tensor(a!) out) -> ()", &zs_decode);
+  m.def("zs_encode_ya(Tensor ya, Tensor aff2, int P, Tensor(a!) meta_out, Tensor(b!) values_out) -> Tensor",
+        &zs_encode_ya);
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
       "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps, Tensor? asum=None, Tensor? strips=None) -> "
@@ -920,6 +996,10 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       &fused_conv2_forward_bn);
   m.def("fused_head_forward_aff(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor(a!)? x_out=None) -> Tensor",
         &fused_head_forward_aff);
+  m.def(
+      "fused_head_forward_upd(Tensor ya, Tensor aff2, Tensor(a!) wfc, Tensor? bfc, int P, Tensor dy_all, Tensor meta_all, "
+      "Tensor vals_all, int rows, float scale, float lr) -> Tensor",
+      &fused_head_forward_upd);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
   m.def("mag_numel(int B, int P) -> int", &mag_numel);
   m.def("mag_ypart_count() -> int", &mag_ypart_count);
@@ -941,6 +1021,7 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("device_cus() -> int", &device_cus);
   m.def("cu_masked_stream(int device, int reserve, bool striped=True) -> int", &cu_masked_stream);
   m.def("comm_spin(Tensor like, int us, int nblocks, int lds_bytes) -> ()", &comm_spin);
+  m.def("copy_engine(Tensor(a!) dst, Tensor src, bool nocu=True) -> ()", &copy_engine);
   m.def("cu_probe(Tensor like, int us, int nblocks) -> Tensor", &cu_probe);
   m.def("cu_comm_stream(int device) -> int", &cu_comm_stream);
   m.def("cu_release_streams() -> int", &cu_release_streams);

@@ -306,8 +306,11 @@ __device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2],
 // above, B two steps ahead).  Timing-only variants (r5_s2, conv2 backward with the wgrad waves
 // alone, no staging) put the rolled loop at ~36 cycles per MFMA with its LDS operand reads and ~21
 // without them: the reads' latency is what the MFMA stream waits on.
+// r5_s4: the wgrad waves alone 0.550 -> 0.347 ms at depth 6 (21.5 cycles per MFMA: their LDS read
+// latency hidden), the whole kernel 0.740 -> 0.728 (now bound by the staging); driver command
+// 2.282 / 2.284 -> 2.273 / 2.279 ms on the same box
 #ifndef TDS_BR_WG_DEPTH
-#define TDS_BR_WG_DEPTH 0
+#define TDS_BR_WG_DEPTH 6
 #endif
 #ifndef TDS_BR_WG_ADEPTH
 #define TDS_BR_WG_ADEPTH 6
@@ -363,6 +366,8 @@ __device__ uint32_t g_br_clk[kBRClkMaxWg * 8 * 2];
 constexpr bool br_clocked(int D) { return D == 13 || D >= 16; }
 constexpr bool br_no_stage(int D) { return D == 5 || (D >= 16 && (D & 1)); }
 constexpr bool br_idle(int D, int role) { return D >= 16 && (role < 2 ? (D & 4) : (D & 8)); }
+constexpr bool br_no_gload(int D) { return D == 3 || (D >= 16 && (D & 32)); }  // staging: no global loads
+constexpr bool br_no_math(int D) { return D == 9 || (D >= 16 && (D & 64)); }   // staging: no BN2 / pool math
 template <int DIAG>
 struct BRClock {
   uint64_t wait = 0, t0 = 0;
@@ -505,7 +510,7 @@ struct BRStager {
   // (bounds as bitwise &, | of unsigned compares: short-circuit && / || compiled to exec-mask
   // branches around every load's address, and the merges cost a vmcnt(0) per load set)
   __device__ __forceinline__ void load(const BRArgs& a, int b, int R0, int c0, int tid) {
-    if constexpr (DIAG == 3) {
+    if constexpr (br_no_gload(DIAG)) {
 #pragma unroll
       for (int u = 0; u < IPER; ++u) {
         gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -624,7 +629,7 @@ struct BRStager {
       }
       const float gg[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
       float d[4][4];
-      if constexpr (DIAG == 9) {  // timing only: no BN2 / pool backward math
+      if constexpr (br_no_math(DIAG)) {  // timing only: no BN2 / pool backward math
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
@@ -1008,6 +1013,12 @@ void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const
     case 24: TDS_BR_LAUNCH(24) break;
     case 25: TDS_BR_LAUNCH(25) break;
     case 27: TDS_BR_LAUNCH(27) break;
+    // +32 staging without global loads, +64 staging without the BN2 / pool math
+    case 28: TDS_BR_LAUNCH(28) break;
+    case 60: TDS_BR_LAUNCH(60) break;
+    case 92: TDS_BR_LAUNCH(92) break;
+    case 48: TDS_BR_LAUNCH(48) break;
+    case 80: TDS_BR_LAUNCH(80) break;
 #endif
     default: TDS_BR_LAUNCH(0) break;
   }

@@ -51,7 +51,8 @@ __device__ __forceinline__ float f16_val(uint32_t h) {
 //   (register constants), 3: no global tile loads (LDS holds whatever it held).
 // conv2 backward, DIAG >= 16: flag sets, per-role barrier clocks always on (conv2_bwd.hip):
 //   +1 no staging, +2 no LDS operand reads in the MFMA waves, +4 dgrad waves idle, +8 wgrad
-//   waves idle (an idle role only takes part in the per-tile barriers)
+//   waves idle (an idle role only takes part in the per-tile barriers), +32 staging without its
+//   global loads, +64 staging without the BN2 / pool backward math
 constexpr bool diag_no_lds(int D) { return D == 2 || (D >= 16 && (D & 2)); }
 template <int DIAG>
 __device__ __forceinline__ f32x4 mma3(const s16x8& ah, const s16x8& al, const s16x8& bh, const s16x8& bl, f32x4 c) {

@@ -190,16 +190,63 @@ struct HPFin {
   const float* bias;     // [NC] or nullptr
   float* logits;         // [B*NC]
 };
-template <int NB>
+// UPD: the fc-gradient exchange's deferred weight update applied on the way through (the activation
+// exchange, parallel/factored.py): W <- W - lr * scale * sum_m dY[m]^T X_m, X_m = row m of the M =
+// W_world * rows gathered rows, decoded from the zero-suppressed encodings (zs_exchange.hip format;
+// wo: per-word value offsets, tds_zs_word_offsets) -- the logits are then formed with the UPDATED
+// weight and the updated weight is stored, so the 720 MB weight is streamed once for both (the
+// separate update sweep linear_dw_zs read and wrote it, and the head forward read it again).  The
+// arithmetic per element is linear_dw_zs's: s = fma chain over m in order, W - lr * (scale * s).
+constexpr int HP_MAXM = 40;  // gathered rows the fused update takes (W_world * rows)
+struct HPUpd {
+  const float* dy;      // [M][NC]
+  const int* meta;      // rank r's page records at meta + r * mstride
+  int64_t mstride;
+  const int* wo;        // rank r's word offsets at wo + r * wostride
+  int64_t wostride;
+  const uint32_t* vals; // rank r's values at vals + r * cap
+  int64_t cap;
+  int M, rows;
+  float scale, lr;
+  float* Wout;          // the weight, updated in place
+};
+
+// X_m at elements e .. e+3 of rank r's flat rows (e % 4 in {0, 2}: the 4 lie in one word or the
+// last 2 bits of a word and the first 2 of the next)
+__device__ __forceinline__ float4 hp_zs_x4(const HPUpd& u, int r, int64_t e) {
+  const int* mr = u.meta + (int64_t)r * u.mstride;
+  const int64_t gw = e >> 5;
+  const int bit = (int)(e & 31);
+  const uint32_t w0 = (uint32_t)mr[(gw >> 6) * 65 + 1 + (gw & 63)];
+  const int64_t gw1 = gw + 1;
+  const uint32_t w1 = bit > 28 ? (uint32_t)mr[(gw1 >> 6) * 65 + 1 + (gw1 & 63)] : 0u;
+  const uint32_t m4 = ((w0 >> bit) | (bit > 28 ? w1 << (32 - bit) : 0u)) & 0xFu;
+  float x[4] = {0.f, 0.f, 0.f, 0.f};
+  if (m4 != 0u) {
+    const int64_t off = (int64_t)u.wo[(int64_t)r * u.wostride + gw] + __builtin_popcount(w0 & ((1u << bit) - 1u));
+    const uint32_t* vr = u.vals + (int64_t)r * u.cap + off;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if ((m4 >> k) & 1u) x[k] = __uint_as_float(vr[__builtin_popcount(m4 & ((1u << k) - 1u))]);
+  }
+  return make_float4(x[0], x[1], x[2], x[3]);
+}
+
+template <int NB, bool UPD = false>
 __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __restrict__ ya,
                                                                  const float* __restrict__ W,
                                                                  const float* __restrict__ aff2,
                                                                  double* __restrict__ partial,
                                                                  float* __restrict__ xout, PBGeom g, int Btot, int b0,
-                                                                 int NC, HPFin fin) {
+                                                                 int NC, HPFin fin, HPUpd upd) {
   __shared__ float red[HP_THREADS / 64][HP_MAXB * 10];
   __shared__ int last_flag;
   __shared__ double wpart[256];
+  __shared__ float s_dy[UPD ? HP_MAXM * 10 : 1];
+  if constexpr (UPD) {
+    for (int e = threadIdx.x; e < upd.M * NC; e += HP_THREADS) s_dy[(e / NC) * 10 + e % NC] = upd.dy[e];
+    __syncthreads();
+  }
   const HPGrid hg = hp_grid(g);
   const int wg = blockIdx.x;
   const int c = wg / hg.per_channel(), band = wg - c * hg.per_channel();
@@ -244,6 +291,47 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           if (px0 + k < Q) xout[(int64_t)(b0 + b) * K + c * QQ + (int64_t)py * Q + px0 + k] = x[b][k];
+    }
+    if constexpr (UPD) {
+      // the weight's update at this lane's 4 columns, then the logits with the updated weight
+      const HPRow rw(g, th, c, R);
+      if (rw.nvalid > 0) {
+        float sj[10][4];
+#pragma unroll
+        for (int j = 0; j < 10; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) sj[j][k] = 0.f;
+        const int64_t pos = (int64_t)c * QQ + (int64_t)py * Q + px0;
+#pragma unroll 1
+        for (int m = 0; m < upd.M; ++m) {
+          const int r = m / upd.rows, bl = m - r * upd.rows;
+          const float4 xm = hp_zs_x4(upd, r, (int64_t)bl * K + pos);
+#pragma unroll
+          for (int j = 0; j < 10; ++j) {
+            const float gv = s_dy[m * 10 + j];
+            sj[j][0] = fmaf(gv, xm.x, sj[j][0]);
+            sj[j][1] = fmaf(gv, xm.y, sj[j][1]);
+            sj[j][2] = fmaf(gv, xm.z, sj[j][2]);
+            sj[j][3] = fmaf(gv, xm.w, sj[j][3]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          if (j < NC) {
+            float4 w4 = cur.w[j];
+            w4 = make_float4(w4.x - upd.lr * (upd.scale * sj[j][0]), w4.y - upd.lr * (upd.scale * sj[j][1]),
+                             w4.z - upd.lr * (upd.scale * sj[j][2]), w4.w - upd.lr * (upd.scale * sj[j][3]));
+            hp_store4(upd.Wout, g, rw, j, w4);
+            // lanes' columns past the image stay 0 for the logits (fix() zeroed them)
+            const float e4[4] = {w4.x, w4.y, w4.z, w4.w};
+            const float o4[4] = {cur.w[j].x, cur.w[j].y, cur.w[j].z, cur.w[j].w};
+            float n4[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) n4[k] = k < rw.nvalid ? e4[k] : o4[k];
+            cur.w[j] = make_float4(n4[0], n4[1], n4[2], n4[3]);
+          }
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
@@ -554,7 +642,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 #define TDS_HPF(NBV)                                                                                                   \
   case NBV:                                                                                                            \
     hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
-                       B, b0, NC, fin);                                                                                \
+                       B, b0, NC, fin, HPUpd{});                                                                       \
     TDS_LAUNCH_CHECK();                                                                                                \
     break;
     switch (nb) {
@@ -566,6 +654,35 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
   if (fin.sync != nullptr) return 0;
   hipLaunchKernelGGL(head_logits_kernel, dim3(BN), dim3(256), 0, st, partial, nwg, sums, bias, logits, BN, NC);
   TDS_LAUNCH_CHECK();
+  return 0;
+}
+
+// The head forward with the activation exchange's deferred weight update fused (HPUpd): one pass
+// (B <= 8), M = W_world * rows <= HP_MAXM gathered rows, logits finished in the launch.  Returns -1 on
+// unsupported shapes (the caller then runs the separate update).
+int tds_head_fwd_pb_upd(const float* ya, float* Wfc, const float* bias, const float* aff2, double* partial,
+                        double* sums, float* logits, int B, int Q, int NC, const float* dy, int M, int rows,
+                        const int* meta, int64_t mstride, const int* wo, int64_t wostride, const float* vals,
+                        int64_t cap, float scale, float lr, hipStream_t st) {
+  if (B < 1 || B > HP_MAXB || NC < 1 || NC > 10 || Q < 8 || M < 1 || M > HP_MAXM || rows < 1 || M % rows) return -1;
+  const PBGeom g = pb_geom(Q);
+  const int nwg = 32 * hp_grid(g).per_channel();
+  const int BN = B * NC, nbc = hp_grid(g).per_channel();
+  if (!(BN <= 256 && nbc <= WRS_MAXL * (256 / BN) && 32 <= WRS_MAXL * (256 / BN))) return -1;
+  HPFin fin{tds_sync_words(kSyncHeadFwd, st), partial + (int64_t)nwg * B * NC, sums, bias, logits};
+  if (fin.sync == nullptr) return -1;
+  HPUpd upd{dy, meta, mstride, wo, wostride, reinterpret_cast<const uint32_t*>(vals), cap, M, rows, scale, lr, Wfc};
+#define TDS_HPU(NBV)                                                                                                \
+  case NBV:                                                                                                         \
+    hipLaunchKernelGGL((head_fwd_pb_kernel<NBV, true>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, \
+                       nullptr, g, B, 0, NC, fin, upd);                                                             \
+    TDS_LAUNCH_CHECK();                                                                                             \
+    break;
+  switch (B) {
+    TDS_HPU(1) TDS_HPU(2) TDS_HPU(3) TDS_HPU(4) TDS_HPU(5) TDS_HPU(6) TDS_HPU(7) TDS_HPU(8)
+    default: return -1;
+  }
+#undef TDS_HPU
   return 0;
 }
 

@@ -181,6 +181,11 @@ bool tds_fused_fin_enabled();  // TDS_FUSED_FIN=0: the separate finalize launche
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st,
                     bool fused_fin = true);
+// the head forward with the activation exchange's deferred weight update fused (head_pb.hip HPUpd)
+int tds_head_fwd_pb_upd(const float* ya, float* Wfc, const float* bias, const float* aff2, double* partial,
+                        double* sums, float* logits, int B, int Q, int NC, const float* dy, int M, int rows,
+                        const int* meta, int64_t mstride, const int* wo, int64_t wostride, const float* vals,
+                        int64_t cap, float scale, float lr, hipStream_t st);
 int tds_head_bwd_pb_npass(int B);
 // channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
 // soon as its launch lands; the BN2 partials of the other channels are left untouched)
@@ -206,6 +211,13 @@ int64_t tds_zs_npages(int64_t n);
 // meta [npages * 65] (offsets + mask words), counts [npages] scratch, vals [cap] (dropped past
 // cap), nnz: int64 device scalar
 void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t cap, int64_t* nnz, hipStream_t st);
+// the same encoding of X = relu(a * ya + b) read from the head's pooled-blocked ya and BN2 affine
+// (B images at pooled size Q): the dense X is never written
+void tds_zs_encode_ya(const float* ya, const float* aff2, int B, int Q, int* meta, float* vals, int64_t cap,
+                      int64_t* nnz, hipStream_t st);
+// per-word value offsets of W zs encodings (meta of rank r at meta + r * mstride, npages pages each):
+// wo [W][npages * 64]
+void tds_zs_word_offsets(const int* meta, int64_t mstride, int64_t npages, int W, int* wo, hipStream_t st);
 void tds_zs_decode(const int* meta, const float* vals, int64_t cap, float* out, int64_t n, hipStream_t st);
 // linear_dw with X given as W source ranks' zero-suppressed encodings (decoded in registers)
 int tds_linear_dw_zs(const float* dy, const int* meta, int64_t mstride, const float* vals, int64_t cap, int rows,

@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include "launchers.h"
+#include "pooled_layout.h"
 
 namespace tds {
 
@@ -68,6 +69,45 @@ __device__ __forceinline__ int zs_block_scan(int v, int* sh, int& total) {
   return base + incl - v;
 }
 
+// X straight from the head's inputs (the zs_encode_ya variant below): X[b][c][py][px] = relu(a[c] *
+// ya[b][c][py][px] + b[c]) with ya in the pooled-blocked layout (pooled_layout.h) -- the head
+// forward no longer writes the dense X (360 MB at the bench shape) for the encoder to read back.
+// The value is formed exactly as the head kernels form it (head_pb.hip: fmaf, then ReLU keeping a
+// NaN), so the encodings are bitwise those of the written X.
+struct ZSYa {
+  const float* ya;
+  const float* aff;  // [64]: a | b of BN2
+  PBGeom g;
+  int64_t K;         // 32 * Q * Q
+};
+// this thread's 8 elements e0 .. e0+7 of the flat X (zeros past n; n < 2^31 and Q >= 8: the
+// position is split once in 32 bits, then stepped along the row, at most one row change)
+__device__ __forceinline__ void zs_load8(const ZSYa& s, int64_t e0, int64_t n, uint32_t (&v)[8]) {
+  const uint32_t Q = (uint32_t)s.g.Q, QQ = Q * Q, K = (uint32_t)s.K;
+  const uint32_t e = (uint32_t)min(e0, n - 1);
+  uint32_t b = e / K, r = e - b * K;
+  uint32_t c = r / QQ, q = r - c * QQ;
+  uint32_t py = q / Q, px = q - py * Q;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const bool ok = e0 + i < n;  // (past n: b may be B -- read element 0 instead)
+    const int cc = ok ? (int)c : 0;
+    const float a = s.aff[cc], bb = s.aff[32 + cc];
+    const float z = fmaf(a, s.ya[ok ? s.g.index((int)b, cc, (int)py, (int)px) : 0], bb);
+    v[i] = ok ? __float_as_uint(z > 0.f ? z : (isnan(z) ? z : 0.f)) : 0u;
+    if (++px == Q) {
+      px = 0;
+      if (++py == Q) {
+        py = 0;
+        if (++c == 32) {
+          c = 0;
+          ++b;
+        }
+      }
+    }
+  }
+}
+
 // Single-pass encode over TILES of ZS_TILE pages (one workgroup each, the tile's X in
 // registers: 8 elements x 8 pages per thread).  Tile order is the order workgroups START (a
 // ticket from a counter; the workgroup drawing the last ticket resets it for the next call), so
@@ -90,7 +130,8 @@ __device__ __forceinline__ unsigned long long zs_status_load(unsigned long long*
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(256) void zs_encode_kernel(const uint32_t* __restrict__ x, int64_t n, int64_t npages,
+template <class SRC>
+__global__ __launch_bounds__(256) void zs_encode_kernel(SRC x, int64_t n, int64_t npages,
                                                         int* __restrict__ meta, uint32_t* __restrict__ vals,
                                                         int64_t cap, int64_t* __restrict__ nnz,
                                                         unsigned long long* __restrict__ status,
@@ -320,6 +361,27 @@ __global__ __launch_bounds__(256) void zs_seg_expand_kernel(const int* __restric
   }
 }
 
+// Value offset of every mask word of W encodings (the head forward's fused update reads a lane's 4
+// values from one word pair without walking its page): wo[r][p * 64 + j] = page offset + popcount of
+// words 0 .. j-1 of page p.  One wave per page.
+__global__ __launch_bounds__(256) void zs_word_offsets_kernel(const int* __restrict__ meta, int64_t mstride,
+                                                              int64_t npages, int W, int* __restrict__ wo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t gp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (rank, page)
+  if (gp >= npages * W) return;
+  const int r = (int)(gp / npages);
+  const int64_t p = gp - (int64_t)r * npages;
+  const int* mr = meta + (int64_t)r * mstride + p * ZS_META;
+  const int cnt = __builtin_popcount((uint32_t)mr[1 + lane]);
+  int incl = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int o = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += o;
+  }
+  wo[(int64_t)r * npages * 64 + p * 64 + lane] = mr[0] + incl - cnt;
+}
+
 // ---------------------------------------------------------------------------- fused update
 // dW (=/+=) scale * dYᵀX, or the update-only W -= lr * scale * dYᵀX (linear_dw's contract), with
 // X given zero-suppressed: the all-gathered encodings of the W source ranks (rank r: meta at
@@ -471,6 +533,13 @@ void tds_zs_seg_decode(const int* meta, const int64_t* pg_start, const int* pg_c
 
 int64_t tds_zs_npages(int64_t n) { return (n + ZS_PAGE - 1) / ZS_PAGE; }
 
+void tds_zs_word_offsets(const int* meta, int64_t mstride, int64_t npages, int W, int* wo, hipStream_t st) {
+  const int64_t waves = npages * W;
+  hipLaunchKernelGGL(zs_word_offsets_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, meta, mstride, npages,
+                     W, wo);
+  TDS_LAUNCH_CHECK();
+}
+
 namespace {
 // Look-back state of one (device, stream): status words (zeroed once when allocated; grown by a
 // fresh allocation, the old one is kept -- a kernel may still be using it), the ticket counter
@@ -518,8 +587,27 @@ void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t ca
     return;
   }
   const int64_t tiles = (P + ZS_TILE - 1) / ZS_TILE;
-  hipLaunchKernelGGL(zs_encode_kernel, dim3((unsigned)tiles), dim3(256), 0, st, reinterpret_cast<const uint32_t*>(x), n,
-                     P, meta, reinterpret_cast<uint32_t*>(vals), cap, nnz, status, ticket, epoch);
+  hipLaunchKernelGGL(zs_encode_kernel<const uint32_t*>, dim3((unsigned)tiles), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t*>(x), n, P, meta, reinterpret_cast<uint32_t*>(vals), cap, nnz,
+                     status, ticket, epoch);
+  TDS_LAUNCH_CHECK();
+}
+
+// The same encoding of X = relu(aff2 affine of ya) for B images at pooled size Q, read from ya
+void tds_zs_encode_ya(const float* ya, const float* aff2, int B, int Q, int* meta, float* vals, int64_t cap,
+                      int64_t* nnz, hipStream_t st) {
+  const PBGeom g = pb_geom(Q);
+  const int64_t K = (int64_t)32 * Q * Q, n = (int64_t)B * K;
+  const int64_t P = tds_zs_npages(n);
+  unsigned long long *status = nullptr, *ticket = nullptr, epoch = 0;
+  if (!zs_lookback((P + ZS_TILE - 1) / ZS_TILE, st, status, ticket, epoch)) {
+    tds_launch_fail("zs_encode_ya: look-back state allocation failed");
+    return;
+  }
+  const int64_t tiles = (P + ZS_TILE - 1) / ZS_TILE;
+  const ZSYa src{ya, aff2, g, K};
+  hipLaunchKernelGGL(zs_encode_kernel<ZSYa>, dim3((unsigned)tiles), dim3(256), 0, st, src, n, P, meta,
+                     reinterpret_cast<uint32_t*>(vals), cap, nnz, status, ticket, epoch);
   TDS_LAUNCH_CHECK();
 }
 

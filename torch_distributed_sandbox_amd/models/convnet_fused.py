@@ -173,7 +173,10 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update")
+
+    def __init__(self):
+        self.fc_update = None
 
 
 # The small reductions behind BN2 (forward statistics, backward constants) and the logits run
@@ -235,17 +238,36 @@ class _Head(torch.autograd.Function):
     def forward(ctx, y2, ya, bn_a, bn_b, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex, link):
         ops = _ext.ops()
         P = y2.shape[1]
+        B, K = ya.shape[0], wfc.shape[1]
         x_out = None
-        if ex is not None and ex.planned(ya.shape[0]) in ("activations", "sharded"):
-            x_out = torch.empty((ya.shape[0], wfc.shape[1]), device=ya.device, dtype=torch.float32)
+        # the zero-suppressed activation exchange encodes X from ya and the BN2 affine itself
+        # (ops.zs_encode_ya): the head then writes no dense X; the other paths need the rows
+        from_ya = ex is not None and link.bn_done and ex.wants_ya(B, K, ya)
+        if ex is not None and not from_ya and ex.planned(B) in ("activations", "sharded"):
+            x_out = torch.empty((B, K), device=ya.device, dtype=torch.float32)
+        upd_obj, link.fc_update = link.fc_update, None
+        fused_upd = None
+        if upd_obj is not None:
+            if link.bn_done and x_out is None:
+                fused_upd = upd_obj.fused_args()  # (None: it ran the update itself -- an overflow step)
+            else:
+                upd_obj()  # the separate update, before the weight is read
         if link.bn_done:  # (bn_a, bn_b) = BN2's (stats, affine), finalized by the conv2 forward
             stats2, aff2 = bn_a, bn_b
-            logits = ops.fused_head_forward_aff(ya, aff2, wfc, bfc, P, x_out)
+            if fused_upd is not None:
+                # the previous step's exchanged weight update, applied while the weight is
+                # streamed for these logits (ops.fused_head_forward_upd)
+                dy_all, meta_all, vals_all, rows, scale, lr = fused_upd
+                logits = ops.fused_head_forward_upd(ya, aff2, wfc, bfc, P, dy_all, meta_all, vals_all, rows, scale, lr)
+            else:
+                logits = ops.fused_head_forward_aff(ya, aff2, wfc, bfc, P, x_out)
         else:  # bn_a = the conv2 forward's BN2 partials
             logits, stats2, aff2 = ops.fused_head_forward(ya, bn_a, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
                                                           bfc, P, x_out)
-        if ex is not None and not ex.begin(x_out, rows=ya.shape[0]):
-            raise RuntimeError("fc gradient exchange refused to start after ready() agreed")
+        if ex is not None:
+            started = ex.begin_ya(ya, aff2, P, B, K) if from_ya else ex.begin(x_out, rows=B)
+            if not started:
+                raise RuntimeError("fc gradient exchange refused to start after ready() agreed")
         ctx.save_for_backward(ya, stats2, aff2, g2, wfc)
         ctx.P = P
         ctx.y2_meta = (y2.shape, y2.dtype, y2.device)
@@ -328,7 +350,10 @@ def forward(model, x):
                                       bn2.running_var, bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps),
                                       link, link1)
     # the fc update may still be running on DDP's side stream (overlap_optimizer): wait here,
-    # after the convolutions were queued, not before
+    # after the convolutions were queued, not before.  An exchanged update the head forward can
+    # apply itself (the activation exchange's, factored.py _Update) is handed to it instead
+    if _FUSED_FIN and x.shape[0] <= 8:
+        link.fc_update = param_fence.take(fc.weight, "zs_head")
     param_fence.wait(fc.weight)
     param_fence.wait(fc.bias)
     ex = factored.get(fc.weight)

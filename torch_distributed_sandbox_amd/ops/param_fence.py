@@ -58,5 +58,16 @@ def wait(param) -> None:
             cur.wait_event(v)
 
 
+def take(param, kind: str):
+    """The pending deferred update of ``param`` if it is its ONLY pending item and offers the fused
+    form ``kind`` (its ``fused_kind`` attribute), removed from the fence -- the caller applies it
+    (the fused head forward: ops.fused_head_forward_upd); else None and the fence is unchanged."""
+    f = getattr(param, _ATTR, None) if param is not None else None
+    if not f or len(f) != 1 or f[0][0] != "fn" or getattr(f[0][1], "fused_kind", None) != kind:
+        return None
+    delattr(param, _ATTR)
+    return f[0][1]
+
+
 def pending(param) -> bool:
     return bool(getattr(param, _ATTR, None))

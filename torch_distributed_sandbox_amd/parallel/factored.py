@@ -90,6 +90,32 @@ def _counts_of(meta_all: torch.Tensor, world: int, row: int) -> torch.Tensor:
     return meta_all.view(world, row)[:, row - 2:].contiguous().view(torch.int64).view(world)
 
 
+class _YaRows:
+    """This rank's fc input rows X = relu(a * ya + b) held as the fused head's pooled-blocked ``ya``
+    and BN2 affine ``aff2`` (the zero-suppressed encoder reads them, ops.zs_encode_ya: the dense X is
+    never written); materialised only for an overflow step's dense re-send."""
+
+    __slots__ = ("ya", "aff2", "P", "rows", "in_f")
+
+    def __init__(self, ya, aff2, P: int, rows: int, in_f: int):
+        self.ya, self.aff2, self.P, self.rows, self.in_f = ya, aff2, int(P), int(rows), int(in_f)
+
+    def tensors(self):
+        return (self.ya, self.aff2)
+
+    def dense(self) -> torch.Tensor:
+        from .. import _ext
+        from . import zs
+
+        n = self.rows * self.in_f
+        meta = torch.empty(zs.meta_numel(n), device=self.ya.device, dtype=torch.int32)
+        vals = torch.empty(n, device=self.ya.device, dtype=torch.float32)
+        _ext.ops().zs_encode_ya(self.ya, self.aff2, self.P, meta, vals)
+        out = torch.empty((self.rows, self.in_f), device=self.ya.device, dtype=torch.float32)
+        zs.decode(meta, vals, out)
+        return out
+
+
 def get(weight) -> Optional["ActivationExchange"]:
     return getattr(weight, _ATTR, None) if weight is not None else None
 
@@ -153,6 +179,7 @@ class ActivationExchange:
         # step (one definition for both paths: the byte model prices the busiest link)
         self.x_ratio = 1.0
         self.zs_stats = {"steps": 0, "overflows": 0, "last_nnz": None}
+        self._cap_once = None  # force_capacity_once
         setattr(weight, _ATTR, self)
 
     def detach(self):
@@ -369,22 +396,69 @@ class ActivationExchange:
         self._set_skip(True)
         return True
 
-    def _begin_zs(self, x2d: torch.Tensor):
+    def force_capacity_once(self, cap: int) -> None:
+        """Fault injection (tests): the next encoded step sends its values at capacity ``cap``
+        (elements; the sharded path: per segment), whatever the earlier counts gave -- a cap below
+        the step's counts drives the overflow path (the dense re-send)."""
+        self._cap_once = max(1, int(cap))
+
+    def _take_cap(self, path: str, n: int) -> int:
+        if self._cap_once is not None:
+            cap, self._cap_once = min(n, self._cap_once), None
+            return cap
+        return min(n, self._cap[path]) if self._cap.get(path) else n
+
+    def wants_ya(self, rows: int, in_f: int, ya: torch.Tensor) -> bool:
+        """Would a forward with ``rows`` rows encode its X straight from the fused head's ``ya``
+        (begin_ya: the zero-suppressed activation path on the GPU)?"""
+        return (ya.is_cuda and self.compress and self._eligible(rows) == "activations"
+                and rows * in_f < (1 << 31))
+
+    def begin_ya(self, ya: torch.Tensor, aff2: torch.Tensor, P: int, rows: int, in_f: int) -> bool:
+        """``begin`` for the fused head's activation exchange: the rows are encoded from ya and the
+        BN2 affine (ops.zs_encode_ya) instead of from a dense X the head would have written."""
+        if not self.wants_ya(rows, in_f, ya):
+            return False
+        src = _YaRows(ya.detach(), aff2.detach(), P, rows, in_f)
+        self._begin_zs(None, src)
+        self._x_local = src  # keep alive until the exchange completes (and the overflow re-send)
+        self.active = "activations"
+        self._set_skip(True)
+        return True
+
+    def _local_dense(self) -> torch.Tensor:
+        x = self._x_local
+        return x.dense() if isinstance(x, _YaRows) else x
+
+    def _local_tensors(self):
+        x = self._x_local
+        return x.tensors() if isinstance(x, _YaRows) else (x,)
+
+    def _begin_zs(self, x2d: Optional[torch.Tensor], ya_src: Optional[_YaRows] = None):
         """Zero-suppressed all-gather of the rows (module docstring): encode, gather the fixed-
         size mask/offset records with each rank's count in their tail, then the values at this
         step's capacity.  The counts are copied to the host asynchronously after the first
-        gather, so ``defer`` can check them without waiting for the values."""
+        gather, so ``defer`` can check them without waiting for the values.  ``ya_src``: encode
+        from the fused head's ya and BN2 affine instead of the dense rows."""
         from . import distributed as tdist
         from . import zs
 
-        W, dev = self.world, x2d.device
-        n = x2d.numel()
+        if ya_src is not None:
+            dev, n, shape = ya_src.ya.device, ya_src.rows * ya_src.in_f, (ya_src.rows, ya_src.in_f)
+        else:
+            dev, n, shape = x2d.device, x2d.numel(), tuple(x2d.shape)
+        W = self.world
         M = zs.meta_numel(n)
         R = _meta_row(M)
-        cap = min(n, self._cap["activations"]) if self._cap.get("activations") else n
+        cap = self._take_cap("activations", n)
         meta = torch.empty(R, device=dev, dtype=torch.int32)
         vals = torch.empty(cap, device=dev, dtype=torch.float32)
-        nnz = zs.encode(x2d, meta[:M], vals)
+        if ya_src is not None:
+            from .. import _ext
+
+            nnz = _ext.ops().zs_encode_ya(ya_src.ya, ya_src.aff2, ya_src.P, meta[:M], vals)
+        else:
+            nnz = zs.encode(x2d, meta[:M], vals)
         meta[R - 2:].view(torch.int64).copy_(nnz.view(1).to(dev))
         meta_all = torch.empty(W * R, device=dev, dtype=torch.int32)
         w_meta = tdist.all_gather_into_tensor(meta_all, meta, group=self.group, async_op=True)
@@ -404,7 +478,7 @@ class ActivationExchange:
         w_vals = tdist.all_gather_into_tensor(vals_all, vals, group=self.group, async_op=True)
         self._zs = {"n": n, "M": M, "R": R, "cap": cap, "meta": meta, "vals": vals, "meta_all": meta_all, "vals_all": vals_all,
                     "w_meta": w_meta, "w_vals": w_vals, "counts_host": counts_host, "counts_ev": counts_ev,
-                    "rows": x2d.shape[0], "in_f": x2d.shape[1]}
+                    "rows": shape[0], "in_f": shape[1]}
         self._x_work = None  # set by _zs_resolve
 
     def _layouts(self, rows: int, in_f: int, dev):
@@ -440,7 +514,7 @@ class ActivationExchange:
         me = tdist.get_rank(self.group)
         n_me = bounds[me][1] - bounds[me][0]
         longest = max(e - a for a, e in bounds)
-        cap = max(1, min(longest, self._cap["sharded"]) if self._cap.get("sharded") else longest)
+        cap = max(1, self._take_cap("sharded", longest))
         meta_send = torch.empty(send.meta_numel, device=dev, dtype=torch.int32)
         vals_send = torch.empty(send.nseg * cap, device=dev, dtype=torch.float32)
         nnz = zs.seg_encode(x2d, send, meta_send, vals_send, cap).to(dev)
@@ -551,7 +625,8 @@ class ActivationExchange:
             rows, in_f = z["rows"], z["in_f"]
             self._x_buf = torch.empty((self.world * rows, in_f), device=z["meta"].device, dtype=torch.float32)
             z["w_vals"].wait()
-            self._x_work = tdist.all_gather_into_tensor(self._x_buf, self._x_local, group=self.group, async_op=True)
+            self._x_work = tdist.all_gather_into_tensor(self._x_buf, self._local_dense(), group=self.group,
+                                                        async_op=True)
             return
         self._zs_decode_pending = z
 
@@ -650,7 +725,7 @@ class ActivationExchange:
             side = self._own_stream
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
-        keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
+        keep = (self._dy, self._x_buf) + (self._local_tensors() if self._x_local is not None else ())  # side stream
         z = getattr(self, "_zs_decode_pending", None)
         if z is not None:
             if z.get("kind") == "sharded":
@@ -709,33 +784,67 @@ class ActivationExchange:
             ev_dy = torch.cuda.Event()
             ev_dy.record(side)
         z, self._zs = self._zs, None
-        x_work, x_local, x_dense = self._x_work, self._x_local, self._x_buf
+        x_work, x_dense = self._x_work, self._x_buf
+        xl = self._x_local  # (captured: _done() below clears the attribute before update() runs)
+
+        def local_dense():
+            return xl.dense() if isinstance(xl, _YaRows) else xl
         in_f = self.weight.shape[1]
         weight, lr, group, world = self.weight, float(lr), self.group, self.world
 
-        def update():
-            from .. import _ext
+        ex = self
 
-            torch.cuda.current_stream(dev).wait_event(ev_dy)
-            with torch.no_grad():
-                x_buf = None
-                if z is not None:
-                    if not self._zs_check(z):
-                        if self._zs_fused(z, (weight.data,)):
-                            self._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
-                            return
-                        x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
-                        self._zs_decode_into(z, x_buf)
-                    else:  # overflow: this step's rows, dense, from every rank
-                        z["w_vals"].wait()
-                        x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
-                        tdist.all_gather_into_tensor(x_buf, x_local, group=group)
-                else:
-                    x_work.wait()
-                    x_buf = x_dense
-                _ext.ops().linear_dw(dy_all, x_buf, weight.data, None, scale, False, lr)
+        class _Update:
+            """The deferred update (param_fence.defer).  Called: queue it on the current stream.
+            The fused head forward may instead take it (param_fence.take(weight, "zs_head")) and call
+            ``fused_args()``: the count check, then -- no overflow -- the gathered encodings and dY
+            for the head forward to apply the update itself while it streams the weight for the
+            logits (ops.fused_head_forward_upd: one pass over the 720 MB weight instead of the
+            update sweep's read + write and the forward's read); otherwise the update runs here."""
 
-        param_fence.defer(weight, update)
+            fused_kind = ("zs_head" if z is not None and ex._zs_fused(z, (weight.data,)) and world * rows <= 40
+                          and weight.shape[0] <= 10 else None)
+
+            def __init__(self):
+                self.checked = None  # the count check's result (overflow?), once made
+
+            def _check(self):
+                if self.checked is None:
+                    self.checked = ex._zs_check(z)
+                return self.checked
+
+            def fused_args(self):
+                torch.cuda.current_stream(dev).wait_event(ev_dy)
+                if self._check():
+                    self()  # overflow: the dense re-send and the separate update
+                    return None
+                z["w_meta"].wait()
+                z["w_vals"].wait()
+                return (dy_all, z["meta_all"].view(world, z["R"]), z["vals_all"].view(world, z["cap"]), rows, scale, lr)
+
+            def __call__(self):
+                from .. import _ext
+
+                torch.cuda.current_stream(dev).wait_event(ev_dy)
+                with torch.no_grad():
+                    x_buf = None
+                    if z is not None:
+                        if not self._check():
+                            if ex._zs_fused(z, (weight.data,)):
+                                ex._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
+                                return
+                            x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
+                            ex._zs_decode_into(z, x_buf)
+                        else:  # overflow: this step's rows, dense, from every rank
+                            z["w_vals"].wait()
+                            x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
+                            tdist.all_gather_into_tensor(x_buf, local_dense(), group=group)
+                    else:
+                        x_work.wait()
+                        x_buf = x_dense
+                    _ext.ops().linear_dw(dy_all, x_buf, weight.data, None, scale, False, lr)
+
+        param_fence.defer(weight, _Update())
         fused_update.applied(weight)
         self._done()
         return True
