@@ -470,7 +470,7 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
         assert bool((err <= bound).all()), (err.max().item(), bound.min().item())
 
 
-def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_scale=None, p1_above=None):
+def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_scale=None, p1_above=None, g2_zero=()):
     import torch.nn as nn
 
     from torch_distributed_sandbox_amd.models import ConvNet, fc_in_features
@@ -496,6 +496,9 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_sca
             ours.layer1[1].weight.fill_(gamma1)
         if w2_scale is not None:  # conv2 weights scaled down (the exactly carried fp16 operand)
             ours.layer2[0].weight.mul_(w2_scale)
+        for c in g2_zero:  # BN2 gamma 0 with beta > 0: every window ties, torch pools its first position
+            ours.layer2[1].weight[c] = 0.0
+            ours.layer2[1].bias[c] = 0.25 + 0.1 * c
     ref = Ref(fc_in_features((H, H))).double()
     ref.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in ours.state_dict().items()})
     # the reference's precision class: its convolutions with TF32 operands (tests/_tf32ref.py)
@@ -551,6 +554,9 @@ def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_sca
             e, et = rel(g, rg), rel(rt[n].grad, rg)
             print(f"step {s} {n:18s} ours {e:.3e}  tf32 {et:.3e}")
             assert e <= max(1e-3, 1.5 * et), f"step {s} {n}: rel L2 err {e:.3e} (TF32 convs: {et:.3e})"
+            if n == "layer2.1.weight" and s == 0:
+                for c in g2_zero:  # dgamma2 = sum g * xhat at the pooled (first) position
+                    assert abs(g[c] - rg[c]).item() <= 1e-3 * rg.abs().max().item(), (c, g[c].item(), rg[c].item())
         opt.step()
         ropt.step()
         topt.step()
@@ -577,6 +583,27 @@ def test_fused_model_p1_beyond_fp16_range(gpu):
     # one step: at this gamma the lr-0.05 step moves conv2's weights by O(1e3) and the next step
     # is a different problem for each trajectory
     _fused_vs_ref(gpu, B=3, H=64, steps=1, gamma1=3e4, p1_above=65504.0)
+
+
+def test_fused_model_zero_bn2_gamma(gpu):
+    """BN2 gamma exactly 0 on two channels (beta > 0): every pooling window of those channels ties
+    at beta and torch's max-pool routes to the window's first position; the conv2 forward stores
+    argmax code 0 and that position's value (conv2_fwd2.hip f2_stage), so dgamma2 / dbeta2 and the
+    conv2 gradients match the fp64 reference."""
+    _fused_vs_ref(gpu, B=3, H=64, steps=1, g2_zero=(5, 6))
+
+
+def test_fused_conv2_bias_inplace_change_raises(gpu):
+    """The conv2 output is stored without its bias (y2h) and the backward rebuilds it with b2: b2 is
+    saved for backward, so an in-place change between forward and backward raises."""
+    from torch_distributed_sandbox_amd.models import ConvNet
+
+    m = ConvNet(image_shape=(64, 64), device=gpu, mode="fused")
+    out = m(torch.rand(2, 1, 64, 64, device=gpu))
+    with torch.no_grad():
+        m.layer2[0].bias.add_(1.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        out.sum().backward()
 
 
 def test_fused_model_tiny_conv2_weights(gpu):

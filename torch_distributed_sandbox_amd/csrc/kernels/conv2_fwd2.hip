@@ -170,7 +170,7 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
 typedef float f2v __attribute__((ext_vector_type(2)));
 template <bool EDGE>
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
-                                         int RH, int NT, int lane, float bco, float inv, float ksc, bool neg,
+                                         int RH, int NT, int lane, float bco, float inv, float ksc, bool neg, bool zg,
                                          f2v& s_acc, f2v& q_acc, uint32_t& ymx, uint32_t* __restrict__ a2) {
   const int li = lane & 15, g = lane >> 4;
   const int co = 16 * NT + li;
@@ -218,7 +218,10 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const float v0 = acc[2 * i][2 * j], v1 = acc[2 * i][2 * j + 1], v2 = acc[2 * i + 1][2 * j];
-      const float m = f2_ext4(v0, v1, v2, acc[2 * i + 1][2 * j + 1], neg);
+      // gamma2 == 0 (zg): every BN2 output of the window is beta2 and torch's max-pool keeps the
+      // first position: code 0, and ya holds that position's value (the head backward's dgamma2
+      // reads xhat there)
+      const float m = zg ? v0 : f2_ext4(v0, v1, v2, acc[2 * i + 1][2 * j + 1], neg);
       e[j] = fmaf(m, inv, bco);
       const bool e0 = v0 == m, e1 = v1 == m, e2 = v2 == m;  // (a NaN window: code 3, unused)
       cb0[2 * i + j] = __builtin_amdgcn_ballot_w64(!e0 & (e1 | !e2));  // code 1 or 3
@@ -352,6 +355,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   const float inv = scales != nullptr ? __uint_as_float(scales[0]) * __uint_as_float(scales[1]) : 1.f;
   const float ksc = scales != nullptr ? __uint_as_float(scales[2]) : 1.f;  // y2h store factor
   const bool neg = gamma != nullptr && gamma[16 * NT + li] < 0.f;
+  const bool zg = gamma != nullptr && gamma[16 * NT + li] == 0.f;
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
   // BN2 partials: each tile's sums in fp32 (<= 16 values per lane), accumulated across the
@@ -383,10 +387,10 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
     if (cur.r0 + F2_TH <= P && cur.c0 + F2_TC <= P)  // tile-uniform
       f2_stage<false>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
-                      bco, inv, ksc, neg, s_acc, q_acc, ymx, a2);
+                      bco, inv, ksc, neg, zg, s_acc, q_acc, ymx, a2);
     else
       f2_stage<true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
-                     bco, inv, ksc, neg, s_acc, q_acc, ymx, a2);
+                     bco, inv, ksc, neg, zg, s_acc, q_acc, ymx, a2);
     if constexpr (TDS_F2_STAT64 != 0) {
       s_d += (double)(s_acc.x + s_acc.y);
       q_d += (double)(q_acc.x + q_acc.y);

@@ -202,7 +202,9 @@ class _Conv2(torch.autograd.Function):
         else:
             y2, bn_a, ya, a2 = ops.fused_conv2_forward(p1, wp, b2, g2, link.mag)
             bn_b = bn_a.new_empty(0)
-        ctx.save_for_backward(p1, wd, y2, a2)
+        # b2 saved (autograd's version check): y2h is stored without the conv bias and the backward
+        # rebuilds y2 with it, so an in-place change to b2 before the backward must raise
+        ctx.save_for_backward(p1, wd, y2, a2, b2)
         ctx.params = (w2, b2)
         ctx.link = link
         ctx.link1 = link1
@@ -213,11 +215,11 @@ class _Conv2(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, _dy2_placeholder, _unused_ya, _unused_a, _unused_b):
-        p1, wd, y2, a2 = ctx.saved_tensors
+        p1, wd, y2, a2, b2 = ctx.saved_tensors
         link = ctx.link
         _run_before_conv2_backward()
         # BN2 / ReLU / pool backward fused into the conv2 data + weight gradients
-        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, a2, link.g2m, link.aff2, link.kbuf, ctx.params[1], link.mag,
+        dp1, dw2, db2 = _ext.ops().fused_conv2_backward_y2(y2, a2, link.g2m, link.aff2, link.kbuf, b2, link.mag,
                                                            p1, wd, 1.0, *_sinks(ctx, ctx.params, 1))
         mag = link.mag
         link.g2m = link.kbuf = link.aff2 = link.mag = None

@@ -172,6 +172,7 @@ class ActivationExchange:
         # zero-suppressed activation rows (parallel/zs.py)
         self.compress = bool(compress)
         self._zs = None  # this step's encoded exchange: dict
+        self._step_zs = False  # this step's rows travelled encoded (last_path's "(zs)" tag)
         # value capacity (elements) per path, from that path's earlier counts: "activations" holds
         # a per-rank total, "sharded" a per-segment slot, so neither may seed the other
         self._cap = {}
@@ -479,6 +480,7 @@ class ActivationExchange:
         self._zs = {"n": n, "M": M, "R": R, "cap": cap, "meta": meta, "vals": vals, "meta_all": meta_all, "vals_all": vals_all,
                     "w_meta": w_meta, "w_vals": w_vals, "counts_host": counts_host, "counts_ev": counts_ev,
                     "rows": shape[0], "in_f": shape[1]}
+        self._step_zs = True
         self._x_work = None  # set by _zs_resolve
 
     def _layouts(self, rows: int, in_f: int, dev):
@@ -550,6 +552,7 @@ class ActivationExchange:
                     "counts_host": counts_host, "counts_ev": counts_ev, "w_meta": w_meta, "w_vals": w_vals,
                     "meta_recv": meta_recv, "vals_recv": vals_recv, "recv": recv, "keep": (meta_send, vals_send),
                     "meta_bytes": send.meta_numel, "dense": x2d.numel(), "nseg": send.nseg}
+        self._step_zs = True
         self._x_work = None
 
     def _count_stream(self, dev):
@@ -926,8 +929,9 @@ class ActivationExchange:
 
     def _done(self):
         self.last_path = "activation-exchange" if self.active == "activations" else "sharded-exchange"
-        if self.compress and self.zs_stats["steps"]:
+        if self._step_zs:  # (under the deferred update the count check runs in the next forward)
             self.last_path += "(zs)"
+        self._step_zs = False
         self._x_buf = self._x_work = self._dy = self._x_local = None
         self.active = None
         self.steps_exchanged += 1
