@@ -302,6 +302,13 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
       (void)hipEventDestroy(ready_);
       ready_ = nullptr;
     }
+    // its storage was recorded on the comm stream: freed here, before a CU split's masked streams
+    // are destroyed (utils/streams.py release_streams), not by the destructor at process exit,
+    // where the allocator's event on the destroyed stream fails (hipErrorInvalidHandle)
+    if (barrier_buf_.defined()) {
+      (void)hipStreamSynchronize(stream_.stream());
+      barrier_buf_ = at::Tensor();
+    }
   }
 
   void abort(const std::string& why) {

@@ -253,10 +253,10 @@ class DistributedDataParallel(nn.Module):
 
     def fc_grad_path(self) -> str:
         """How the big fc layer's gradient was averaged in the steps run so far."""
-        if self.world_size == 1:
-            return "local"
         used = sorted({ex.last_path for ex in self._exchanges if ex.last_path})
-        return "+".join(used) if used else "allreduce"
+        if used:  # (at world 1 only when an exchange was forced)
+            return "+".join(used)
+        return "local" if self.world_size == 1 else "allreduce"
 
     # ------------------------------------------------------------------ setup helpers
     @staticmethod

@@ -198,6 +198,14 @@ def destroy_process_group(group=None) -> None:
     if not is_initialized():
         return
     if group is None:
+        # the native communicator ends here (torch's teardown shuts down only its own NCCL
+        # backends): its comm stream, watchdog and buffers go before the CU split is undone,
+        # whatever Python references to it outlive the group
+        from .rccl_backend import native_comm_of
+
+        comm, kind = native_comm_of(None)
+        if kind == "rccl" and hasattr(comm, "shutdown"):
+            comm.shutdown()
         _state["groups"] = {}
         _state["backend"] = None
         dist.destroy_process_group()
