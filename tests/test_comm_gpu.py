@@ -184,7 +184,7 @@ def test_zs_encode_from_ya_bitwise(gpu):
 
     ops = tds._ext.ops()
     torch.manual_seed(3)
-    for B, P in ((3, 64), (5, 100)):
+    for B, P in ((3, 64), (5, 100), (2, 150)):  # Q = 32, 50, 75: runs aligned, shifted, odd rows
         Q = P // 2
         Q4, Q8 = (Q + 3) // 4, (Q + 7) // 8  # pooled-blocked plane (kernels/pooled_layout.h)
         ya = torch.randn(B, 32, Q4 * Q8 * 32, device=gpu)
@@ -222,12 +222,13 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     exchange's dW formation (update-only linear_dw; ops/fused_update.py)."""
     import copy
 
-    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.models import ConvNet, convnet_fused
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss, param_fence
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
 
     torch.manual_seed(0)
     H = 256
+    fused0 = convnet_fused.STATS["head_fused_updates"]
     m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
     m2 = copy.deepcopy(m1)
     d1 = DistributedDataParallel(m1, grad_exchange=exchange, overlap_optimizer=True, fuse_update_in_backward=fuse)
@@ -254,6 +255,10 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
             assert not d1._fused_done  # consumed by the step: the bias was updated, the weight skipped
     d1.wait_pending_updates()
     torch.cuda.synchronize()
+    if exchange == "activations" and fuse and d1.exchanges[0].compress:
+        # steps 1 and 3 applied the previous step's update inside the head forward (step 2's
+        # count check saw the forced overflow and ran the separate update)
+        assert convnet_fused.STATS["head_fused_updates"] - fused0 >= 2
     if exchange in ("activations", "sharded") and d1.exchanges[0].compress:
         assert d1.exchanges[0].zs_stats["overflows"] >= 1  # step 2 went through the dense re-send
     for (n, p), q in zip(m1.named_parameters(), m2.parameters()):

@@ -58,6 +58,12 @@
 #ifndef TDS_BR_LOAD_PRIO
 #define TDS_BR_LOAD_PRIO 3  // wave priority while a staging wave issues its look-ahead loads
 #endif
+#ifndef TDS_BR_STAGE_SETS
+#define TDS_BR_STAGE_SETS 3  // staging look-ahead register sets (2 or 3)
+#endif
+#ifndef TDS_BR_PIECE_ROT
+#define TDS_BR_PIECE_ROT 1  // a tile's 64 extra p1 pieces to wave 5 (wave 4 takes the 64 extra items)
+#endif
 #ifndef TDS_BR_MFMA_PRIO
 #define TDS_BR_MFMA_PRIO 1  // wave priority of the dgrad / wgrad waves
 #endif
@@ -84,6 +90,8 @@ static_assert(BR_LDS <= 160 * 1024 && BR_OFF_X % 16 == 0 && BR_OFF_K % 16 == 0, 
 // walk table entries (tds_conv2_bwd_walk): bit 31 = first tile of a segment, bit 30 = past the
 // end of this workgroup's list (the low bits then repeat its last tile), b << 24 | tr << 12 | tc
 constexpr uint32_t kWalkStart = 0x80000000u, kWalkEnd = 0x40000000u;
+constexpr int BR_WALK_PAD = 8;  // end entries after each list (>= 2 x TDS_BR_STAGE_SETS)
+static_assert(BR_WALK_PAD >= 2 * TDS_BR_STAGE_SETS, "walk padding below the staging look-ahead");
 struct BRTile {
   int b, r0, c0;
   bool start, end;
@@ -496,6 +504,12 @@ struct BRStager {
   uint32_t av[IPER];  // a2: the window's argmax codes, 16 channels
   uint4 pr[PPER];
 
+  // the j-th p1 piece of staging lane tid: the set past 256 goes to wave 5 (lanes 64..127), the
+  // items past 256 to wave 4, so no staging wave takes both extras (TDS_BR_PIECE_ROT)
+  __device__ __forceinline__ static int piece(int tid, int j) {
+    return (TDS_BR_PIECE_ROT != 0 && j == 1 ? ((tid + 192) & 255) : tid) + 256 * j;
+  }
+
   __device__ __forceinline__ static void item_geom(int it, int& wy, int& wx) {
     const int w = (it < ITEMS ? it : 0) >> 3;
     wy = w / (BR_SC / 2);
@@ -571,7 +585,7 @@ struct BRStager {
     }
 #pragma unroll
     for (int j = 0; j < PPER; ++j) {
-      const int e = tid + 256 * j;
+      const int e = piece(tid, j);
       const int rec = (e < PIECES ? e : 0) >> 1, q = e & 1;
       const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
       const int gr = R0 + lr, gc = c0 - 2 + lc;
@@ -698,7 +712,7 @@ struct BRStager {
     }
 #pragma unroll
     for (int j = 0; j < PPER; ++j) {
-      const int e = tid + 256 * j;
+      const int e = piece(tid, j);
       if (e < PIECES) {
         const int rec = e >> 1, q = e & 1;
         const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
@@ -738,10 +752,12 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
     pro.load(a, x.b, x.r0 - 2, x.c0, tid);
     pro.template store<false>(a, x.r0 - 2, x.c0, tid, dtop(j), ptop(j), kc, nullptr, nullptr);
   };
-  // two register sets: tile j's new-row loads are issued two tiles before they are staged.
-  // Loads are unconditional (past the end: the list's last tile again, never staged): a load
-  // under a branch makes the wait for the OLDER set drain the younger one too (vmcnt(0)).
-  BRStager<8, BIG, DIAG> st0, st1;
+  // TDS_BR_STAGE_SETS register sets (2 or 3): tile j's new-row loads are issued that many tiles
+  // before they are staged (r5_s6: the staging's global loads, ~20 KB a tile, are latency-bound --
+  // the staging alone ran 0.53 ms, 0.26 without its loads; the sets live in VGPRs the MFMA
+  // roles' 180 leave free).  Loads are unconditional (past the end: the list's last tile again,
+  // never staged): a load under a branch makes the wait for the OLDER set drain the younger one
+  // too (vmcnt(0)).
   BRClock<DIAG> clk;
   clk.start();
   auto tile = [&](int j) { return br_decode(a.walk, j, a.sk, a.w); };
@@ -754,8 +770,53 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
     s.load(a, x.b, x.r0 + 2, x.c0, tid);
     __builtin_amdgcn_s_setprio(0);
   };
-  // (a prologue runs after the set that stages the same tile is stored and before that set is
-  // reloaded, so its registers are the set's)
+  // stage tile j from set s if it exists (a segment start also gets its prologue: after the set is
+  // stored and before it is reloaded, so its registers are the set's); false past the list's end
+  auto stage_if = [&](BRStager<8, BIG, DIAG>& s, int j) {
+    const BRTile x = tile(j);
+    if (!x.end) {
+      stage(s, j, x);
+      if (x.start) prologue(j, x);
+    }
+    return !x.end;
+  };
+#if TDS_BR_STAGE_SETS == 3
+  BRStager<8, BIG, DIAG> st0, st1, st2;
+  {
+    const BRTile x0 = tile(0);
+    if (!x0.end) {
+      ld(st0, 0);
+      stage(st0, 0, x0);
+      prologue(0, x0);
+    }
+  }
+  ld(st1, 1);
+  ld(st2, 2);
+  ld(st0, 3);
+  // iteration kk: tile kk+1 from st1 (reload: kk+4), kk+2 from st2 (kk+5), kk+3 from st0 (kk+6);
+  // one exit and every set reloaded on every path (the two-set loop's rule, below).  The walk
+  // table carries BR_WALK_PAD end entries: the last iteration (kk <= n-1) reads tile kk + 6.
+  bool more = !tile(0).end;
+  for (int kk = 0; more; kk += 3) {
+    clk.barrier();  // consumers start tile kk
+    const bool has1 = stage_if(st1, kk + 1);
+    ld(st1, kk + 4);
+    bool has2 = false;
+    if (has1) {
+      clk.barrier();  // tile kk + 1
+      has2 = stage_if(st2, kk + 2);
+    }
+    ld(st2, kk + 5);
+    bool has3 = false;
+    if (has2) {
+      clk.barrier();  // tile kk + 2
+      has3 = stage_if(st0, kk + 3);
+    }
+    ld(st0, kk + 6);
+    more = has3;
+  }
+#else
+  BRStager<8, BIG, DIAG> st0, st1;
   {
     const BRTile x0 = tile(0);
     if (!x0.end) {
@@ -774,26 +835,17 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   bool more = !tile(0).end;
   for (int kk = 0; more; kk += 2) {
     clk.barrier();  // consumers start tile kk
-    {
-      const BRTile x = tile(kk + 1);
-      if (!x.end) {
-        stage(st1, kk + 1, x);
-        if (x.start) prologue(kk + 1, x);
-      }
-    }
+    const bool second = stage_if(st1, kk + 1);
     ld(st1, kk + 3);
-    const bool second = !tile(kk + 1).end;
+    bool has2 = false;
     if (second) {
       clk.barrier();  // consumers start tile kk + 1
-      const BRTile x = tile(kk + 2);
-      if (!x.end) {
-        stage(st0, kk + 2, x);
-        if (x.start) prologue(kk + 2, x);
-      }
+      has2 = stage_if(st0, kk + 2);
     }
     ld(st0, kk + 4);  // (past the end: the list's last tile again, never staged)
-    more = second && !tile(kk + 2).end;
+    more = has2;
   }
+#endif
   clk.barrier();
   clk.report();
 }
@@ -915,10 +967,11 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
   const int64_t tbase = ntail / nwg, textra = ntail % nwg;
   int64_t maxlen = 0;
   for (int w = 0; w < nwg; ++w) maxlen = std::max(maxlen, len[w] + tbase + (w < textra ? 1 : 0));
-  // + 4 end-marked entries: the staging's look-ahead reads tile k + 4 at the last iteration of a
-  // list of length k + 1 (br_stage: both load sets are issued on every path) -- with + 3 the longest
-  // list's last read ran one past its row (the next list, or past the table for the last one)
-  const int64_t rows = maxlen + 4;
+  // + BR_WALK_PAD end-marked entries: the staging's look-ahead reads tile k + 2 * sets at the last
+  // iteration of a list of length k + 1 (br_stage: every load set is issued on every path; 4 with
+  // two sets, 6 with three) -- with too few the longest list's last read ran past its row (the
+  // next list, or past the table for the last one)
+  const int64_t rows = maxlen + BR_WALK_PAD;
   if (rows * nwg >= ((int64_t)1 << 31)) return -1;  // the kernel indexes it in 32 bits
   if (out == nullptr) return rows * nwg;
   std::vector<int64_t> fill(nwg, 0);

@@ -81,20 +81,50 @@ struct ZSYa {
   int64_t K;         // 32 * Q * Q
 };
 // this thread's 8 elements e0 .. e0+7 of the flat X (zeros past n; n < 2^31 and Q >= 8: the
-// position is split once in 32 bits, then stepped along the row, at most one row change)
+// position is split once in 32 bits).  Fast path (the run lies in one pooled row): the run is
+// columns px .. px+7 of row py, i.e. the row's 8-float pieces of blocks px/8 and px/8 + 1 (32-B
+// aligned, consecutive blocks 128 B apart) -- four 16-B loads, the 8 values picked by a funnel
+// shift of px % 8 (per-element 4-B gathers plus per-element affine loads ran the encode at
+// 0.44 ms, r5_s7).  Runs that cross a row end or pass n take the element-wise path.
+__device__ __forceinline__ float zs_x_of(float a, float b, float y) {
+  const float z = fmaf(a, y, b);
+  return z > 0.f ? z : (isnan(z) ? z : 0.f);
+}
 __device__ __forceinline__ void zs_load8(const ZSYa& s, int64_t e0, int64_t n, uint32_t (&v)[8]) {
   const uint32_t Q = (uint32_t)s.g.Q, QQ = Q * Q, K = (uint32_t)s.K;
   const uint32_t e = (uint32_t)min(e0, n - 1);
   uint32_t b = e / K, r = e - b * K;
   uint32_t c = r / QQ, q = r - c * QQ;
   uint32_t py = q / Q, px = q - py * Q;
+  if (e0 + 8 <= n && px + 8 <= Q) {
+    // blocks px/8 and px/8 + 1 of this row (px + 8 <= Q: the second block is inside the row)
+    const float* p = s.ya + s.g.index((int)b, (int)c, (int)py, (int)(px & ~7u));
+    const float4 q0 = *reinterpret_cast<const float4*>(p), q1 = *reinterpret_cast<const float4*>(p + 4);
+    const float4 q2 = *reinterpret_cast<const float4*>(p + 32), q3 = *reinterpret_cast<const float4*>(p + 36);
+    const uint32_t w[16] = {__float_as_uint(q0.x), __float_as_uint(q0.y), __float_as_uint(q0.z), __float_as_uint(q0.w),
+                            __float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z), __float_as_uint(q1.w),
+                            __float_as_uint(q2.x), __float_as_uint(q2.y), __float_as_uint(q2.z), __float_as_uint(q2.w),
+                            __float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z), __float_as_uint(q3.w)};
+    const uint32_t off = px & 7u;
+    // the shift as bit masks, not selects between array elements: LLVM folds c ? w[i + 4] : w[i]
+    // into w[i + (c ? 4 : 0)], a dynamic index that keeps the array in scratch memory
+    const uint32_t m4 = 0u - ((off >> 2) & 1u), m2 = 0u - ((off >> 1) & 1u), m1 = 0u - (off & 1u);
+    uint32_t t4[11], t2[9];
+#pragma unroll
+    for (int i = 0; i < 11; ++i) t4[i] = (w[i] & ~m4) | (w[i + 4] & m4);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) t2[i] = (t4[i] & ~m2) | (t4[i + 2] & m2);
+    const float a = s.aff[c], bb = s.aff[32 + c];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = __float_as_uint(zs_x_of(a, bb, __uint_as_float((t2[i] & ~m1) | (t2[i + 1] & m1))));
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const bool ok = e0 + i < n;  // (past n: b may be B -- read element 0 instead)
     const int cc = ok ? (int)c : 0;
-    const float a = s.aff[cc], bb = s.aff[32 + cc];
-    const float z = fmaf(a, s.ya[ok ? s.g.index((int)b, cc, (int)py, (int)px) : 0], bb);
-    v[i] = ok ? __float_as_uint(z > 0.f ? z : (isnan(z) ? z : 0.f)) : 0u;
+    const float y = s.ya[ok ? s.g.index((int)b, cc, (int)py, (int)px) : 0];
+    v[i] = ok ? __float_as_uint(zs_x_of(s.aff[cc], s.aff[32 + cc], y)) : 0u;
     if (++px == Q) {
       px = 0;
       if (++py == Q) {

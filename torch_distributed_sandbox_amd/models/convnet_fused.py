@@ -123,6 +123,8 @@ def _sinks(ctx, params, first):
 
 
 _ZERO = {}
+# counters the tests read: forward passes that applied the exchange's weight update in the head kernel
+STATS = {"head_fused_updates": 0}
 
 
 def _zero_scalar(device, dtype):
@@ -260,6 +262,7 @@ class _Head(torch.autograd.Function):
                 # the previous step's exchanged weight update, applied while the weight is
                 # streamed for these logits (ops.fused_head_forward_upd)
                 dy_all, meta_all, vals_all, rows, scale, lr = fused_upd
+                STATS["head_fused_updates"] += 1
                 logits = ops.fused_head_forward_upd(ya, aff2, wfc, bfc, P, dy_all, meta_all, vals_all, rows, scale, lr)
             else:
                 logits = ops.fused_head_forward_aff(ya, aff2, wfc, bfc, P, x_out)

@@ -59,14 +59,21 @@ def wait(param) -> None:
 
 
 def take(param, kind: str):
-    """The pending deferred update of ``param`` if it is its ONLY pending item and offers the fused
-    form ``kind`` (its ``fused_kind`` attribute), removed from the fence -- the caller applies it
-    (the fused head forward: ops.fused_head_forward_upd); else None and the fence is unchanged."""
+    """The pending deferred update of ``param`` if it is its ONLY deferred item and offers the
+    fused form ``kind`` (its ``fused_kind`` attribute), removed from the fence -- the caller applies
+    it (the fused head forward: ops.fused_head_forward_upd); else None and the fence is unchanged.
+    Events stay in the fence for the caller's :func:`wait` (under DDP's overlapped optimizer the
+    end-of-backward side-stream step fences every parameter of its bucket, this one included)."""
     f = getattr(param, _ATTR, None) if param is not None else None
-    if not f or len(f) != 1 or f[0][0] != "fn" or getattr(f[0][1], "fused_kind", None) != kind:
+    if not f:
         return None
-    delattr(param, _ATTR)
-    return f[0][1]
+    fns = [i for i, (k, _) in enumerate(f) if k == "fn"]
+    if len(fns) != 1 or getattr(f[fns[0]][1], "fused_kind", None) != kind:
+        return None
+    fn = f.pop(fns[0])[1]
+    if not f:
+        delattr(param, _ATTR)
+    return fn
 
 
 def pending(param) -> bool:
