@@ -213,8 +213,9 @@ def test_zs_encode_from_ya_bitwise(gpu):
 
 @pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("sharded", False),
                                            ("chunked", False),
-                                           ("allreduce", True), ("activations", True), ("sharded", True)])
-def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
+                                           ("allreduce", True), ("activations", True), ("sharded", True),
+                                           ("activations", "head")])
+def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse, monkeypatch):
     """overlap_optimizer: the fc bucket's collective + SGD update run on a side stream
     and the next forward's head waits on a parameter fence; the trajectory must be
     identical to the sequential step.  fuse=True: at world size 1 the fc weight's SGD
@@ -226,6 +227,12 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss, param_fence
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
 
+    from torch_distributed_sandbox_amd.parallel import factored
+
+    head = fuse == "head"  # the round-5 paths: X encoded from ya, the update applied in the head forward
+    monkeypatch.setattr(factored, "_ZS_FROM_YA", head)
+    monkeypatch.setattr(factored, "_HEAD_FUSED_UPDATE", head)
+    fuse = bool(fuse)
     torch.manual_seed(0)
     H = 256
     fused0 = convnet_fused.STATS["head_fused_updates"]
@@ -255,7 +262,7 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
             assert not d1._fused_done  # consumed by the step: the bias was updated, the weight skipped
     d1.wait_pending_updates()
     torch.cuda.synchronize()
-    if exchange == "activations" and fuse and d1.exchanges[0].compress:
+    if head and d1.exchanges[0].compress:
         # steps 1 and 3 applied the previous step's update inside the head forward (step 2's
         # count check saw the forced overflow and ran the separate update)
         assert convnet_fused.STATS["head_fused_updates"] - fused0 >= 2

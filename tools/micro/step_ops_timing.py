@@ -97,9 +97,41 @@ def main():
             ops.fused_l1_backward(st["c2b"][0], st["mag"][44:45], x, p1, idx1, c1.weight, c1.bias, n1.weight, stats1,
                                   gram, 1.0)
 
+        # the activation exchange's pieces (parallel/factored.py, world 1): the head forward writing X,
+        # the zero-suppressed encode from that X or straight from ya, the separate update sweep over the
+        # encodings, and the head forward applying that update itself
+        from torch_distributed_sandbox_amd.parallel import zs
+
+        K = fc.weight.shape[1]
+        xo = torch.empty(B, K, device=dev)
+        w2c = fc.weight.detach().clone()
+        meta = torch.empty(zs.meta_numel(B * K), device=dev, dtype=torch.int32)
+        vals = torch.empty(B * K, device=dev)
+
+        def hf_x():
+            ops.fused_head_forward_aff(st["c2"][2], st["hf"][2], w2c, fc.bias, P, xo)
+
+        def enc_x():
+            st["nnz"] = zs.encode(xo, meta, vals)
+
+        def enc_ya():
+            st["nnz"] = ops.zs_encode_ya(st["c2"][2], st["hf"][2], P, meta, vals)
+
+        def dw_zs():
+            ops.linear_dw_zs(dl, meta.view(1, -1), vals.view(1, -1), B, w2c, None, 1.0, False, 1e-12)
+
+        def hf_upd():
+            ops.fused_head_forward_upd(st["c2"][2], st["hf"][2], w2c, fc.bias, P, dl, meta.view(1, -1),
+                                       vals.view(1, -1), B, 1.0, 1e-12)
+
         seq = [("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
-               ("head_bwd_nomag", hb_nomag), ("conv2_bwd", c2b), ("l1_bwd", l1b)]
-        for _, fn in seq:
+               ("head_bwd_nomag", hb_nomag), ("conv2_bwd", c2b), ("l1_bwd", l1b),
+               ("head_fwd_x", hf_x), ("zs_enc_x", enc_x), ("zs_enc_ya", enc_ya), ("dw_zs", dw_zs), ("head_fwd_upd", hf_upd)]
+        only = set(a.only.split(",")) if a.only else None
+        for name, fn in seq:
+            if name in ("head_fwd_x", "zs_enc_x", "zs_enc_ya", "dw_zs", "head_fwd_upd") and only and not (
+                    only & {"head_fwd_x", "zs_enc_x", "zs_enc_ya", "dw_zs", "head_fwd_upd"}):
+                continue
             fn()
         only = set(a.only.split(",")) if a.only else None
         res = {}

@@ -71,6 +71,8 @@ Protocol (driven by ``parallel/ddp.py``):
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Tuple
 
 import torch
@@ -88,6 +90,14 @@ def _meta_row(m: int) -> int:
 def _counts_of(meta_all: torch.Tensor, world: int, row: int) -> torch.Tensor:
     """The [world] int64 counts in the tails of the all-gathered records (row = _meta_row)."""
     return meta_all.view(world, row)[:, row - 2:].contiguous().view(torch.int64).view(world)
+
+
+# A/B switches of the activation exchange's round-5 GPU paths (measured in docs/DISTRIBUTED.md):
+# TDS_ZS_FROM_YA: encode X straight from the fused head's ya + BN2 affine instead of from the dense X
+# the head forward writes; TDS_HEAD_FUSED_UPDATE: apply the previous step's exchanged weight update
+# inside the next head forward instead of a separate linear_dw_zs sweep.
+_ZS_FROM_YA = os.environ.get("TDS_ZS_FROM_YA", "0").strip() != "0"
+_HEAD_FUSED_UPDATE = os.environ.get("TDS_HEAD_FUSED_UPDATE", "0").strip() != "0"
 
 
 class _YaRows:
@@ -412,7 +422,7 @@ class ActivationExchange:
     def wants_ya(self, rows: int, in_f: int, ya: torch.Tensor) -> bool:
         """Would a forward with ``rows`` rows encode its X straight from the fused head's ``ya``
         (begin_ya: the zero-suppressed activation path on the GPU)?"""
-        return (ya.is_cuda and self.compress and self._eligible(rows) == "activations"
+        return (_ZS_FROM_YA and ya.is_cuda and self.compress and self._eligible(rows) == "activations"
                 and rows * in_f < (1 << 31))
 
     def begin_ya(self, ya: torch.Tensor, aff2: torch.Tensor, P: int, rows: int, in_f: int) -> bool:
@@ -805,8 +815,8 @@ class ActivationExchange:
             logits (ops.fused_head_forward_upd: one pass over the 720 MB weight instead of the
             update sweep's read + write and the forward's read); otherwise the update runs here."""
 
-            fused_kind = ("zs_head" if z is not None and ex._zs_fused(z, (weight.data,)) and world * rows <= 40
-                          and weight.shape[0] <= 10 else None)
+            fused_kind = ("zs_head" if _HEAD_FUSED_UPDATE and z is not None and ex._zs_fused(z, (weight.data,))
+                          and world * rows <= 40 and weight.shape[0] <= 10 else None)
 
             def __init__(self):
                 self.checked = None  # the count check's result (overflow?), once made
