@@ -198,6 +198,7 @@ struct HPFin {
 // separate update sweep linear_dw_zs read and wrote it, and the head forward read it again).  The
 // arithmetic per element is linear_dw_zs's: s = fma chain over m in order, W - lr * (scale * s).
 constexpr int HP_MAXM = 40;  // gathered rows the fused update takes (W_world * rows)
+constexpr int HP_MG = 5;     // rows decoded together (the bench's W_world * rows at world 1)
 struct HPUpd {
   const float* dy;      // [M][NC]
   const int* meta;      // rank r's page records at meta + r * mstride
@@ -212,22 +213,28 @@ struct HPUpd {
 };
 
 // X_m at elements e .. e+3 of rank r's flat rows (e % 4 in {0, 2}: the 4 lie in one word or the
-// last 2 bits of a word and the first 2 of the next)
+// last 2 bits of a word and the first 2 of the next).  Branch-free: every lane issues the same
+// loads (the second word re-reads the first when not needed; value indices clamped to the slot),
+// so a group of rows' loads can all be in flight at once -- a load under a per-lane branch makes
+// the compiler wait for everything older at the merge.
 __device__ __forceinline__ float4 hp_zs_x4(const HPUpd& u, int r, int64_t e) {
   const int* mr = u.meta + (int64_t)r * u.mstride;
   const int64_t gw = e >> 5;
   const int bit = (int)(e & 31);
+  const bool two = bit > 28;
+  const int64_t gw1 = two ? gw + 1 : gw;
   const uint32_t w0 = (uint32_t)mr[(gw >> 6) * 65 + 1 + (gw & 63)];
-  const int64_t gw1 = gw + 1;
-  const uint32_t w1 = bit > 28 ? (uint32_t)mr[(gw1 >> 6) * 65 + 1 + (gw1 & 63)] : 0u;
-  const uint32_t m4 = ((w0 >> bit) | (bit > 28 ? w1 << (32 - bit) : 0u)) & 0xFu;
-  float x[4] = {0.f, 0.f, 0.f, 0.f};
-  if (m4 != 0u) {
-    const int64_t off = (int64_t)u.wo[(int64_t)r * u.wostride + gw] + __builtin_popcount(w0 & ((1u << bit) - 1u));
-    const uint32_t* vr = u.vals + (int64_t)r * u.cap + off;
+  const uint32_t w1 = (uint32_t)mr[(gw1 >> 6) * 65 + 1 + (gw1 & 63)];
+  const int64_t base = (int64_t)u.wo[(int64_t)r * u.wostride + gw];
+  const uint32_t m4 = ((w0 >> bit) | (two ? w1 << (32 - bit) : 0u)) & 0xFu;
+  const int64_t off = base + __builtin_popcount(w0 & ((1u << bit) - 1u));
+  const uint32_t* vr = u.vals + (int64_t)r * u.cap;
+  float x[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if ((m4 >> k) & 1u) x[k] = __uint_as_float(vr[__builtin_popcount(m4 & ((1u << k) - 1u))]);
+  for (int k = 0; k < 4; ++k) {
+    const int64_t idx = min(off + __builtin_popcount(m4 & ((1u << k) - 1u)), u.cap - 1);
+    const float v = __uint_as_float(vr[idx]);
+    x[k] = ((m4 >> k) & 1u) ? v : 0.f;
   }
   return make_float4(x[0], x[1], x[2], x[3]);
 }
@@ -242,9 +249,12 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
   __shared__ float red[HP_THREADS / 64][HP_MAXB * 10];
   __shared__ int last_flag;
   __shared__ double wpart[256];
-  __shared__ float s_dy[UPD ? HP_MAXM * 10 : 1];
+  __shared__ float s_dy[UPD ? (HP_MAXM + HP_MG) * 10 : 1];
   if constexpr (UPD) {
-    for (int e = threadIdx.x; e < upd.M * NC; e += HP_THREADS) s_dy[(e / NC) * 10 + e % NC] = upd.dy[e];
+    for (int e = threadIdx.x; e < (HP_MAXM + HP_MG) * 10; e += HP_THREADS) {
+      const int m = e / 10, j = e - m * 10;
+      s_dy[e] = (m < upd.M && j < NC) ? upd.dy[m * NC + j] : 0.f;
+    }
     __syncthreads();
   }
   const HPGrid hg = hp_grid(g);
@@ -285,12 +295,14 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
         x[b][k] = (xfull || (rok && px0 + k < Q)) ? v : 0.f;
       }
     }
-    if (xout != nullptr && rok) {
+    if (xout != nullptr) {
+      // X rows in the fc's flatten order, an image's row offset (b K + c Q^2 + py Q) has the weight
+      // row's alignment (K = 32 Q^2): 16-B stores or float2 pairs as for the weight (hp_store4; 4-B
+      // stores per element cost the forward 0.14 ms at the bench shape, r5_s9)
+      const HPRow rwx(g, th, c, R);
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (px0 + k < Q) xout[(int64_t)(b0 + b) * K + c * QQ + (int64_t)py * Q + px0 + k] = x[b][k];
+        hp_store4(xout + (int64_t)(b0 + b) * K, g, rwx, 0, make_float4(x[b][0], x[b][1], x[b][2], x[b][3]), false);
     }
     if constexpr (UPD) {
       // the weight's update at this lane's 4 columns, then the logits with the updated weight
@@ -302,17 +314,29 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
 #pragma unroll
           for (int k = 0; k < 4; ++k) sj[j][k] = 0.f;
         const int64_t pos = (int64_t)c * QQ + (int64_t)py * Q + px0;
+        // rows in groups of HP_MG, each group's loads in flight together (one row at a time made
+        // 2 dependent round trips per row and chunk: the fused forward ran 0.80 ms, r5_s8); rows past
+        // M read row M-1 and add dy = 0 (s_dy is zero-padded), keeping the fma order m = 0, 1, ...
 #pragma unroll 1
-        for (int m = 0; m < upd.M; ++m) {
-          const int r = m / upd.rows, bl = m - r * upd.rows;
-          const float4 xm = hp_zs_x4(upd, r, (int64_t)bl * K + pos);
+        for (int m0 = 0; m0 < upd.M; m0 += HP_MG) {
+          float4 xm[HP_MG];
 #pragma unroll
-          for (int j = 0; j < 10; ++j) {
-            const float gv = s_dy[m * 10 + j];
-            sj[j][0] = fmaf(gv, xm.x, sj[j][0]);
-            sj[j][1] = fmaf(gv, xm.y, sj[j][1]);
-            sj[j][2] = fmaf(gv, xm.z, sj[j][2]);
-            sj[j][3] = fmaf(gv, xm.w, sj[j][3]);
+          for (int t = 0; t < HP_MG; ++t) {
+            const int m = min(m0 + t, upd.M - 1);
+            const int r = m / upd.rows, bl = m - r * upd.rows;
+            xm[t] = hp_zs_x4(upd, r, (int64_t)bl * K + pos);
+          }
+#pragma unroll
+          for (int t = 0; t < HP_MG; ++t) {
+            if (m0 + t >= upd.M) break;  // (uniform; no 0 * x terms: x may be inf)
+#pragma unroll
+            for (int j = 0; j < 10; ++j) {
+              const float gv = s_dy[(m0 + t) * 10 + j];
+              sj[j][0] = fmaf(gv, xm[t].x, sj[j][0]);
+              sj[j][1] = fmaf(gv, xm[t].y, sj[j][1]);
+              sj[j][2] = fmaf(gv, xm[t].z, sj[j][2]);
+              sj[j][3] = fmaf(gv, xm[t].w, sj[j][3]);
+            }
           }
         }
 #pragma unroll
