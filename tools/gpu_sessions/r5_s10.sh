@@ -11,3 +11,5 @@ b xa32_off 240 python3 -u bench.py --backend rccl-native --reserve-cus 32 --grad
 b xa32_upd 240 env TDS_HEAD_FUSED_UPDATE=1 python3 -u bench.py --backend rccl-native --reserve-cus 32 --grad-exchange activations --steps 20 --warmup 5
 b xa0_off 240 python3 -u bench.py --backend rccl-native --reserve-cus 0 --grad-exchange activations --steps 20 --warmup 5
 b drv 200 python3 -u bench.py --gpus 1 --steps 20 --warmup 5
+b xa32_ya 240 env TDS_ZS_FROM_YA=1 python3 -u bench.py --backend rccl-native --reserve-cus 32 --grad-exchange activations --steps 20 --warmup 5
+b xa32_both 240 env TDS_ZS_FROM_YA=1 TDS_HEAD_FUSED_UPDATE=1 python3 -u bench.py --backend rccl-native --reserve-cus 32 --grad-exchange activations --steps 20 --warmup 5

@@ -18,6 +18,7 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <type_traits>
 
 #include "common.h"
 #include "launchers.h"
@@ -138,6 +139,77 @@ __device__ __forceinline__ void zs_load8(const ZSYa& s, int64_t e0, int64_t n, u
   }
 }
 
+// The tile's X from ya through LDS (ZSYa, Q >= 16): a page of 2048 flat elements covers a few
+// pooled rows; its (row, 8-column block) PIECES are each one 32-B run of ya (2 x 16-B loads,
+// consecutive lanes on consecutive blocks of a row), written into the page's flat order in LDS
+// with the BN2 affine and ReLU applied, then read back as each thread's 8 elements.  Pages are
+// double-buffered: page k+1's pieces are loaded into registers while page k is written and read.
+// A page has at most 256 + (rows it touches) <= 385 pieces for Q >= 16 (2 slots per thread).
+// (Each thread gathering its own 8 elements -- 4-B loads, or 16-B loads of the two blocks they
+// straddle -- read ya at 0.35-0.44 ms against 0.17 ms for the dense X, r5_s7 / r5_s9.)
+struct ZSPiece {
+  int64_t pb;    // ya index of the run (0 when the piece does not exist)
+  int64_t f0;    // flat index of its first column
+  int c, ncol;   // channel; columns of the run inside the image (0: no piece)
+};
+__device__ __forceinline__ ZSPiece zs_piece(const ZSYa& s, int64_t E, int64_t n, int p) {
+  ZSPiece r{0, 0, 0, 0};
+  const int64_t Q = s.g.Q, Q8 = s.g.Q8;
+  if (E >= n) return r;
+  const int64_t gr0 = E / Q, cs0 = E - gr0 * Q;
+  const int64_t end = min(E + (int64_t)ZS_PAGE, n);
+  const int64_t nb0 = Q8 - (cs0 >> 3);  // blocks of the first row from the page's start column on
+  int64_t gr, blk;
+  if (p < nb0) {
+    gr = gr0;
+    blk = (cs0 >> 3) + p;
+  } else {
+    const int64_t q = p - nb0;
+    gr = gr0 + 1 + q / Q8;
+    blk = q - (q / Q8) * Q8;
+  }
+  const int64_t f0 = gr * Q + blk * 8;
+  if (f0 >= end) return r;  // past the page (or n)
+  const int64_t bc = gr / Q, py = gr - bc * Q;
+  r.pb = ((bc * s.g.Q4 + (py >> 2)) * Q8 + blk) * 32 + (py & 3) * 8;
+  r.f0 = f0;
+  r.c = (int)(bc & 31);
+  r.ncol = (int)min((int64_t)8, Q - blk * 8);
+  return r;
+}
+
+template <int SLOTS>
+struct ZSPageRegs {
+  float4 lo[SLOTS], hi[SLOTS];
+};
+
+template <int SLOTS>
+__device__ __forceinline__ void zs_page_load(const ZSYa& s, int64_t E, int64_t n, ZSPageRegs<SLOTS>& r, int tid) {
+#pragma unroll
+  for (int u = 0; u < SLOTS; ++u) {
+    const ZSPiece pc = zs_piece(s, E, n, tid + 256 * u);  // (no piece: reads ya[0 .. 7], unused)
+    r.lo[u] = *reinterpret_cast<const float4*>(s.ya + pc.pb);
+    r.hi[u] = *reinterpret_cast<const float4*>(s.ya + pc.pb + 4);
+  }
+}
+
+template <int SLOTS>
+__device__ __forceinline__ void zs_page_put(const ZSYa& s, int64_t E, int64_t n, const ZSPageRegs<SLOTS>& r,
+                                            uint32_t* xs, int tid) {
+  const int64_t end = min(E + (int64_t)ZS_PAGE, n);
+#pragma unroll
+  for (int u = 0; u < SLOTS; ++u) {
+    const ZSPiece pc = zs_piece(s, E, n, tid + 256 * u);
+    const float a = s.aff[pc.c], bb = s.aff[32 + pc.c];
+    const float y[8] = {r.lo[u].x, r.lo[u].y, r.lo[u].z, r.lo[u].w, r.hi[u].x, r.hi[u].y, r.hi[u].z, r.hi[u].w};
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int64_t f = pc.f0 + t;
+      if (t < pc.ncol && f >= E && f < end) xs[f - E] = __float_as_uint(zs_x_of(a, bb, y[t]));
+    }
+  }
+}
+
 // Single-pass encode over TILES of ZS_TILE pages (one workgroup each, the tile's X in
 // registers: 8 elements x 8 pages per thread).  Tile order is the order workgroups START (a
 // ticket from a counter; the workgroup drawing the last ticket resets it for the next call), so
@@ -172,6 +244,7 @@ __global__ __launch_bounds__(256) void zs_encode_kernel(SRC x, int64_t n, int64_
   __shared__ int sh[4];
   __shared__ int ptot[ZS_TILE];
   __shared__ long long s_tile, s_prefix;
+  __shared__ uint32_t xs[std::is_same<SRC, ZSYa>::value ? 2 * ZS_PAGE : 1];
   const int tid = threadIdx.x;
   if (tid == 0) {
     const unsigned long long t = atomicAdd(ticket, 1ull);
@@ -182,8 +255,26 @@ __global__ __launch_bounds__(256) void zs_encode_kernel(SRC x, int64_t n, int64_
   const int64_t tile = s_tile, p0 = tile * ZS_TILE;
   uint32_t v[ZS_TILE][8];
   int ex[ZS_TILE];
+  if constexpr (std::is_same<SRC, ZSYa>::value) {
+    // pages through LDS (zs_page_load / zs_page_put), page k+1's loads in flight under page k
+    ZSPageRegs<2> r0, r1;
+    zs_page_load<2>(x, p0 * ZS_PAGE, n, r0, tid);
 #pragma unroll
-  for (int k = 0; k < ZS_TILE; ++k) zs_load8(x, (p0 + k) * ZS_PAGE + 8 * (int64_t)tid, n, v[k]);
+    for (int k = 0; k < ZS_TILE; ++k) {
+      const int64_t E = (p0 + k) * ZS_PAGE;
+      if (k + 1 < ZS_TILE) zs_page_load<2>(x, E + ZS_PAGE, n, (k & 1) ? r0 : r1, tid);
+      uint32_t* buf = xs + (k & 1) * ZS_PAGE;
+      zs_page_put<2>(x, E, n, (k & 1) ? r1 : r0, buf, tid);
+      __syncthreads();  // (page k-1's reads of the other buffer are behind the previous barrier)
+      const uint4 q0 = *reinterpret_cast<const uint4*>(buf + 8 * tid), q1 = *reinterpret_cast<const uint4*>(buf + 8 * tid + 4);
+      const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[k][i] = E + 8 * tid + i < n ? w[i] : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < ZS_TILE; ++k) zs_load8(x, (p0 + k) * ZS_PAGE + 8 * (int64_t)tid, n, v[k]);
+  }
   int tile_total = 0;
 #pragma unroll
   for (int k = 0; k < ZS_TILE; ++k) {
@@ -626,6 +717,10 @@ void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t ca
 // The same encoding of X = relu(aff2 affine of ya) for B images at pooled size Q, read from ya
 void tds_zs_encode_ya(const float* ya, const float* aff2, int B, int Q, int* meta, float* vals, int64_t cap,
                       int64_t* nnz, hipStream_t st) {
+  if (Q < 16) {  // (a page's pieces fit the loader's two slots per thread from Q = 16 on)
+    tds_launch_fail("zs_encode_ya: needs Q >= 16");
+    return;
+  }
   const PBGeom g = pb_geom(Q);
   const int64_t K = (int64_t)32 * Q * Q, n = (int64_t)B * K;
   const int64_t P = tds_zs_npages(n);

@@ -423,7 +423,7 @@ class ActivationExchange:
         """Would a forward with ``rows`` rows encode its X straight from the fused head's ``ya``
         (begin_ya: the zero-suppressed activation path on the GPU)?"""
         return (_ZS_FROM_YA and ya.is_cuda and self.compress and self._eligible(rows) == "activations"
-                and rows * in_f < (1 << 31))
+                and rows * in_f < (1 << 31) and in_f >= 32 * 16 * 16)  # (the ya encoder needs Q >= 16)
 
     def begin_ya(self, ya: torch.Tensor, aff2: torch.Tensor, P: int, rows: int, in_f: int) -> bool:
         """``begin`` for the fused head's activation exchange: the rows are encoded from ya and the
