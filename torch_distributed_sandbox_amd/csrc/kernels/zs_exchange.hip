@@ -147,65 +147,93 @@ __device__ __forceinline__ void zs_load8(const ZSYa& s, int64_t e0, int64_t n, u
 // A page has at most 256 + (rows it touches) <= 385 pieces for Q >= 16 (2 slots per thread).
 // (Each thread gathering its own 8 elements -- 4-B loads, or 16-B loads of the two blocks they
 // straddle -- read ya at 0.35-0.44 ms against 0.17 ms for the dense X, r5_s7 / r5_s9.)
-struct ZSPiece {
-  int64_t pb;    // ya index of the run (0 when the piece does not exist)
-  int64_t f0;    // flat index of its first column
-  int c, ncol;   // channel; columns of the run inside the image (0: no piece)
+// A page's geometry, wave-uniform (computed once per page; 32-bit: n < 2^31).
+struct ZSPageGeo {
+  int E, end;        // flat range [E, end)
+  int gr0, cs0;      // its first row (global row b*32*Q + c*Q + py) and column
+  int bc0, py0;      // that row's plane (b*32 + c) and pooled row
+  int nb0;           // blocks of the first row from column cs0 on
+  bool none;         // the page lies past n
 };
-__device__ __forceinline__ ZSPiece zs_piece(const ZSYa& s, int64_t E, int64_t n, int p) {
-  ZSPiece r{0, 0, 0, 0};
-  const int64_t Q = s.g.Q, Q8 = s.g.Q8;
-  if (E >= n) return r;
-  const int64_t gr0 = E / Q, cs0 = E - gr0 * Q;
-  const int64_t end = min(E + (int64_t)ZS_PAGE, n);
-  const int64_t nb0 = Q8 - (cs0 >> 3);  // blocks of the first row from the page's start column on
-  int64_t gr, blk;
-  if (p < nb0) {
-    gr = gr0;
-    blk = (cs0 >> 3) + p;
-  } else {
-    const int64_t q = p - nb0;
-    gr = gr0 + 1 + q / Q8;
-    blk = q - (q / Q8) * Q8;
-  }
-  const int64_t f0 = gr * Q + blk * 8;
-  if (f0 >= end) return r;  // past the page (or n)
-  const int64_t bc = gr / Q, py = gr - bc * Q;
-  r.pb = ((bc * s.g.Q4 + (py >> 2)) * Q8 + blk) * 32 + (py & 3) * 8;
-  r.f0 = f0;
-  r.c = (int)(bc & 31);
-  r.ncol = (int)min((int64_t)8, Q - blk * 8);
-  return r;
+__device__ __forceinline__ ZSPageGeo zs_page_geo(const ZSYa& s, int64_t E64, int64_t n) {
+  ZSPageGeo g;
+  const int Q = s.g.Q;
+  g.none = E64 >= n;
+  g.E = g.none ? 0 : (int)E64;
+  g.end = (int)min(E64 + (int64_t)ZS_PAGE, n);
+  g.gr0 = g.E / Q;
+  g.cs0 = g.E - g.gr0 * Q;
+  g.bc0 = g.gr0 / Q;
+  g.py0 = g.gr0 - g.bc0 * Q;
+  g.nb0 = s.g.Q8 - (g.cs0 >> 3);
+  return g;
+}
+// floor(a / d) for 0 <= a < 2^20, d >= 1, from a float reciprocal with a one-step correction (a
+// 64-bit integer division per piece made the page staging VALU-bound)
+__device__ __forceinline__ int zs_div(int a, int d, float rd) {
+  int q = (int)((float)a * rd);
+  q -= (q * d > a) ? 1 : 0;
+  q += ((q + 1) * d <= a) ? 1 : 0;
+  return q;
 }
 
 template <int SLOTS>
 struct ZSPageRegs {
   float4 lo[SLOTS], hi[SLOTS];
+  int f0[SLOTS];     // flat index of the piece's first column
+  int8_t c[SLOTS];   // its channel
+  int8_t ncol[SLOTS];  // columns inside the image (0: no piece)
 };
 
 template <int SLOTS>
-__device__ __forceinline__ void zs_page_load(const ZSYa& s, int64_t E, int64_t n, ZSPageRegs<SLOTS>& r, int tid) {
+__device__ __forceinline__ void zs_page_load(const ZSYa& s, int64_t E64, int64_t n, ZSPageRegs<SLOTS>& r, int tid) {
+  const ZSPageGeo pg = zs_page_geo(s, E64, n);
+  const int Q = s.g.Q, Q8 = s.g.Q8;
+  const float rQ8 = 1.f / (float)Q8, rQ = 1.f / (float)Q;
 #pragma unroll
   for (int u = 0; u < SLOTS; ++u) {
-    const ZSPiece pc = zs_piece(s, E, n, tid + 256 * u);  // (no piece: reads ya[0 .. 7], unused)
-    r.lo[u] = *reinterpret_cast<const float4*>(s.ya + pc.pb);
-    r.hi[u] = *reinterpret_cast<const float4*>(s.ya + pc.pb + 4);
+    const int p = tid + 256 * u;
+    int i, blk;
+    if (p < pg.nb0) {
+      i = 0;
+      blk = (pg.cs0 >> 3) + p;
+    } else {
+      const int q = p - pg.nb0, t = zs_div(q, Q8, rQ8);
+      i = 1 + t;
+      blk = q - t * Q8;
+    }
+    const int64_t f0 = (int64_t)(pg.gr0 + i) * Q + blk * 8;
+    const bool ok = !pg.none && f0 < pg.end;
+    const int w = zs_div(pg.py0 + i, Q, rQ);  // rows past the plane's last
+    const int bc = pg.bc0 + w, py = pg.py0 + i - w * Q;
+    const int64_t pb = ok ? (((int64_t)bc * s.g.Q4 + (py >> 2)) * Q8 + blk) * 32 + (py & 3) * 8 : 0;
+    r.lo[u] = *reinterpret_cast<const float4*>(s.ya + pb);  // (no piece: ya[0 .. 7], unused)
+    r.hi[u] = *reinterpret_cast<const float4*>(s.ya + pb + 4);
+    r.f0[u] = ok ? (int)f0 : 0;
+    r.c[u] = (int8_t)(bc & 31);
+    r.ncol[u] = (int8_t)(ok ? min(8, Q - blk * 8) : 0);
   }
 }
 
 template <int SLOTS>
-__device__ __forceinline__ void zs_page_put(const ZSYa& s, int64_t E, int64_t n, const ZSPageRegs<SLOTS>& r,
+__device__ __forceinline__ void zs_page_put(const ZSYa& s, int64_t E64, int64_t n, const ZSPageRegs<SLOTS>& r,
                                             uint32_t* xs, int tid) {
-  const int64_t end = min(E + (int64_t)ZS_PAGE, n);
+  const int E = E64 < n ? (int)E64 : 0, end = (int)min(E64 + (int64_t)ZS_PAGE, n);
 #pragma unroll
   for (int u = 0; u < SLOTS; ++u) {
-    const ZSPiece pc = zs_piece(s, E, n, tid + 256 * u);
-    const float a = s.aff[pc.c], bb = s.aff[32 + pc.c];
+    const int c = r.c[u];
+    const float a = s.aff[c], bb = s.aff[32 + c];
     const float y[8] = {r.lo[u].x, r.lo[u].y, r.lo[u].z, r.lo[u].w, r.hi[u].x, r.hi[u].y, r.hi[u].z, r.hi[u].w};
+    const int f0 = r.f0[u];
+    if (r.ncol[u] == 8 && f0 >= E && f0 + 8 <= end) {  // the whole run is in the page (most pieces)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      const int64_t f = pc.f0 + t;
-      if (t < pc.ncol && f >= E && f < end) xs[f - E] = __float_as_uint(zs_x_of(a, bb, y[t]));
+      for (int t = 0; t < 8; ++t) xs[f0 - E + t] = __float_as_uint(zs_x_of(a, bb, y[t]));
+    } else {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int f = f0 + t;
+        if (t < r.ncol[u] && f >= E && f < end) xs[f - E] = __float_as_uint(zs_x_of(a, bb, y[t]));
+      }
     }
   }
 }
