@@ -382,6 +382,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
   const int e = blockIdx.x;
   const int64_t base = (int64_t)(e / inner) * ostride + (e % inner);
   double s = 0.0;
+#pragma unroll 8  // (the loads in flight together; the adds keep their order)
   for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += in[base + (int64_t)k * kstride];
   s = block_sum(s, sh);
   if (threadIdx.x == 0) out[e] = s;
@@ -892,14 +893,17 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
                               const T* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
                               double* full, double* strips, L1Corners& cx, double xs) {
   const int tid = threadIdx.x;
+#pragma unroll 4
   for (int e = tid; e < B * 144; e += blockDim.x) {
     const int b = e / 144, q = (e / 36) % 4, i = (e / 6) % 6, j = e % 6;
     const int r = q < 2 ? i : H - 6 + i, c = (q & 1) == 0 ? j : W - 6 + j;
     cx.v[b][q][i][j] = (float)x[(int64_t)b * H * W + (int64_t)r * W + c];
   }
   // per-image border strips [B][8][82] -> batch sums, images in order
+#pragma unroll 3
   for (int e = tid; e < 8 * 82; e += blockDim.x) {
     double v = 0.0;
+#pragma unroll 8
     for (int b = 0; b < B; ++b) v += strips_b[(int64_t)b * 8 * 82 + e];
     strips[e] = v;
   }
@@ -971,14 +975,18 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
   __shared__ double Gw[16][25];
   __shared__ double strips_sum[8 * 82];
   __shared__ L1Corners cx;
+  __shared__ float w1s[16 * 25];
+  // w1 staged once (its loads issued with the Gram's): the contractions below read it 50 times
+  // per thread, which as global loads ran one latency each (r5: l1_gram 20 us)
+  for (int e = threadIdx.x; e < 16 * 25; e += blockDim.x) w1s[e] = w1[e];
   l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, cx, xs);
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {
     const int c = e / 25, j = e % 25;
     double h = 0.0;
-    for (int k = 0; k < 25; ++k) h += (double)w1[c * 25 + k] * G[k][j];
-    Gw[c][j] = h * (double)w1[c * 25 + j];
+    for (int k = 0; k < 25; ++k) h += (double)w1s[c * 25 + k] * G[k][j];
+    Gw[c][j] = h * (double)w1s[c * 25 + j];
   }
   // p1's fp16 range guard (conv2's single operand, fp16x2): p1 = relu(gamma * xhat + beta) and,
   // for ANY batch, |xhat| <= sqrt(n - 1) (Samuelson's inequality, population variance; eps only
@@ -1007,7 +1015,7 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
   if (tid < 16) {
     double s = 0.0, q = 0.0;
     for (int j = 0; j < 25; ++j) {
-      s += (double)w1[tid * 25 + j] * S[j];
+      s += (double)w1s[tid * 25 + j] * S[j];
       q += Gw[tid][j];
     }
     sums[tid * 2] = s;
@@ -1060,9 +1068,18 @@ __global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restri
                                                           const float* __restrict__ stats1, float* __restrict__ dw1,
                                                           float* __restrict__ db1, float* __restrict__ dgamma1,
                                                           float* __restrict__ dbeta1, float scale) {
+  // the inputs staged in LDS with one round of loads (read through global memory, each thread's
+  // 75 dependent-free loads ran as a chain of latencies: 7 us for 400 outputs)
+  __shared__ double sg[650];
+  __shared__ double sb[16 * LB_NACC];
+  __shared__ float sw[16 * 25];
   const int e = threadIdx.x;
+  for (int i = e; i < 650; i += blockDim.x) sg[i] = gram[i];
+  for (int i = e; i < 16 * LB_NACC; i += blockDim.x) sb[i] = bwd_sum[i];
+  if (e < 16 * 25) sw[e] = w1[e];
+  __syncthreads();
   if (e >= 16 * 25) return;
-  l1_finalize_one(e, bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+  l1_finalize_one(e, sb, sg, n, sw, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
 }
 
 }  // namespace tds
