@@ -74,6 +74,9 @@ struct HPThread {
 #ifndef TDS_G2M_NT
 #define TDS_G2M_NT 1
 #endif
+#ifndef TDS_HP_WUPD_NT  // the backward's updated-weight stores non-temporal (A/B: 0 = plain stores)
+#define TDS_HP_WUPD_NT 1
+#endif
 template <class T>
 __device__ __forceinline__ void hp_st(T* p, T v, bool nt) {
   if (nt) st_stream(p, v); else *p = v;
@@ -547,7 +550,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
             if constexpr (KEEP) hp_store4(dW, g, rw, j, d);
             if constexpr (UPD) {  // torch SGD: p -= lr * g
               const float4 w = cur.w[j];
-              hp_store4(Wupd, g, rw, j, make_float4(w.x - lr * d.x, w.y - lr * d.y, w.z - lr * d.z, w.w - lr * d.w));
+              hp_store4(Wupd, g, rw, j, make_float4(w.x - lr * d.x, w.y - lr * d.y, w.z - lr * d.z, w.w - lr * d.w),
+                        TDS_HP_WUPD_NT != 0);
             }
           }
         }
