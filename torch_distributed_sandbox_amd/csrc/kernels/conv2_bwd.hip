@@ -56,7 +56,10 @@
 #define TDS_BR_MIX 1  // fast staging path on v_fma_mix_f32 (fp16 y2h operands, no conversions)
 #endif
 #ifndef TDS_BR_LOAD_PRIO
-#define TDS_BR_LOAD_PRIO 3  // wave priority while a staging wave issues its look-ahead loads
+// wave priority while a staging wave issues its look-ahead loads: 3 helped the two-set staging of
+// round 2; with three sets, 0 (r5_s13: isolated 0.668 -> 0.659 ms, driver's command 2.197 ->
+// 2.191 ms, two alternating runs each)
+#define TDS_BR_LOAD_PRIO 0
 #endif
 #ifndef TDS_BR_STAGE_SETS
 #define TDS_BR_STAGE_SETS 3  // staging look-ahead register sets (2 or 3)
