@@ -5,6 +5,10 @@
 set -u
 O=$GRAFT_REPO_ROOT/gpurun_out/r5s14
 mkdir -p $O
+source $GRAFT_REPO_ROOT/tools/gpu_sessions/lib.sh
+# the whole GPU suite and smoke() first, as the driver runs them at round end
+t gpu_all 900 tests -m gpu
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; echo "smoke rc=$?: $(tail -1 $O/smoke.log)"
 R=$GRAFT_REPO_ROOT
 cd /tmp && export TMPDIR=/tmp
 run() {
