@@ -124,7 +124,10 @@ def _parser():
                          "'fp32' = the ToTensor image materialised by the upsample kernel")
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
                     help="produce the next batch (upsample + BN1 input moments) on a side stream beside the "
-                         "current step's conv2 backward")
+                         "current step's head kernels (--prefetch-at)")
+    ap.add_argument("--prefetch-at", choices=["head", "conv2_bwd"], default="head",
+                    help="where --prefetch queues the next batch: beside the head forward / backward (memory-"
+                         "bound, room for the pipeline's workgroups) or beside the conv2 backward (round 2: no room)")
     ap.add_argument("--allreduce-probe", action=argparse.BooleanOptionalAction, default=True,
                     help="world > 1: after the timed steps, time a few all-reduces over the same communicator "
                          "and report their bus bandwidth in config.allreduce_probe (outside the timed region)")
@@ -581,8 +584,10 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     # input pipeline (the role of the reference's DataLoader prefetch): batch i+1 -- the 28x28 ->
     # HxW upsample and, for the fused plan, the batch's x moments behind BN1's statistics
     # (convnet_fused.input_stats: weight-independent) -- is produced on a side stream that starts
-    # when step i's conv2 backward is enqueued, so it runs beside that MFMA-bound kernel instead
-    # of on the step's critical path.  Step i+1's compute stream waits on it; the tensors are
+    # when step i's head forward is enqueued (--prefetch-at head), so its kernels run beside the
+    # memory-bound head forward / backward, whose workgroups leave registers and LDS free, instead
+    # of on the step's critical path (beside the conv2 backward, round 2, they got no CU until it
+    # ended).  Step i+1's compute stream waits on it; the tensors are
     # recorded on the compute stream so the caching allocator cannot recycle them early.  A step
     # whose hook did not fire (no fused plan, first step) produces its batch inline.  The work per
     # timed step is unchanged: each step produces exactly one batch.
@@ -627,7 +632,9 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
         else:
             images = produce(i)
         if data_stream is not None:
-            convnet_fused.before_conv2_backward(lambda: prefetch(i + 1))
+            hook = (convnet_fused.before_head_forward if args.prefetch_at == "head"
+                    else convnet_fused.before_conv2_backward)
+            hook(lambda: prefetch(i + 1))
         out = ddp(images)
         if sim_stream is not None:
             sim_stream.wait_stream(torch.cuda.current_stream(device))
@@ -645,6 +652,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             torch.cuda.current_stream(device).wait_stream(sdma[0])
         if data_stream is not None:
             convnet_fused._before_conv2_backward.clear()  # (a plan without the hook)
+            convnet_fused._before_head_forward.clear()
         return loss
 
     def sync_all():
@@ -708,7 +716,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             "x_exchange": [{"ratio": round(ex.x_ratio, 4), **ex.zs_stats} for ex in ddp.exchanges if ex.compress
                            and ex.zs_stats["steps"]] or None,
             "reserve_cus": reserve,
-            "prefetch": data_stream is not None,
+            "prefetch": args.prefetch_at if data_stream is not None else False,
             "input": ("uint8 levels (ToTensor's 1/255 folded into conv1)" if args.input == "levels"
                       else "fp32 image"),
             "rccl_max_ctas": rccl_max_ctas or None,

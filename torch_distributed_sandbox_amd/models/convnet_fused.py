@@ -102,15 +102,29 @@ def _take_input_stats(x):
 # backward -- the step's longest, MFMA-bound kernel -- is enqueued: work they put on another
 # stream after waiting on the current one runs beside it (bench.py / trainer input prefetch).
 _before_conv2_backward = []
+_before_head_forward = []
 
 
 def before_conv2_backward(fn):
     _before_conv2_backward.append(fn)
 
 
+def before_head_forward(fn):
+    """``fn()`` runs once, when the next fused head forward is about to be queued (the input
+    pipeline's prefetch point: work queued on another stream there runs beside the memory-bound
+    head kernels, whose register and LDS use leave room for it -- the persistent conv kernels
+    before and after them leave none)."""
+    _before_head_forward.append(fn)
+
+
 def _run_before_conv2_backward():
     while _before_conv2_backward:
         _before_conv2_backward.pop(0)()
+
+
+def _run_before_head_forward():
+    while _before_head_forward:
+        _before_head_forward.pop(0)()
 
 
 def _sinks(ctx, params, first):
@@ -241,6 +255,7 @@ class _Head(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y2, ya, bn_a, bn_b, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc, bfc, ex, link):
         ops = _ext.ops()
+        _run_before_head_forward()
         P = y2.shape[1]
         B, K = ya.shape[0], wfc.shape[1]
         x_out = None
