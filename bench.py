@@ -716,7 +716,8 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             "x_exchange": [{"ratio": round(ex.x_ratio, 4), **ex.zs_stats} for ex in ddp.exchanges if ex.compress
                            and ex.zs_stats["steps"]] or None,
             "reserve_cus": reserve,
-            "prefetch": args.prefetch_at if data_stream is not None else False,
+            "prefetch": data_stream is not None,
+            "prefetch_at": args.prefetch_at if data_stream is not None else None,
             "input": ("uint8 levels (ToTensor's 1/255 folded into conv1)" if args.input == "levels"
                       else "fp32 image"),
             "rccl_max_ctas": rccl_max_ctas or None,

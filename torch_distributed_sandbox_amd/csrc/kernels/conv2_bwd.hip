@@ -481,13 +481,33 @@ constexpr uint32_t kBROob = 0xFFFFFFF0u;
 
 // Staging of NR rows (8: a tile's new rows, 4: a segment prologue) of image rows R0 ..
 // R0+NR-1 (R0 even), columns c0-2 .. c0+17, into dy2 / p1 row blocks.  Item = (2x2 pooling
-// window, 4-channel chunk): NR/2 x 10 windows x 8 chunks.  BIG: the 32 g2m planes of an image
-// exceed a 4 GiB buffer-descriptor range (64-bit g2m loads); a template parameter, because two
-// load paths under a runtime branch make the compiler wait vmcnt(0) at their merge.
-// fma(a, channel cc of the 4 fp16 channels in v, c) on v_fma_mix_f32 (op_sel picks the half)
-__device__ __forceinline__ float br_fma_y(float a, uint2 v, int cc, float c) {
+// window, BR_CW-channel chunk): NR/2 x 10 windows x 32/BR_CW chunks.  BIG: the 32 g2m planes of an
+// image exceed a 4 GiB buffer-descriptor range (64-bit g2m loads); a template parameter, because
+// two load paths under a runtime branch make the compiler wait vmcnt(0) at their merge.
+// BR_CW = 8 (TDS_BR_CW): a pixel's 8 channels of y2h are one 16-B load and one 16-B dy2 store; a
+// tile's 160 items leave one per lane for waves 4-6 (r5_s14 PMC: the texture data path was busy
+// 81 % of the kernel, ~64 cycles per staging load instruction -- fewer, wider loads).
+#ifndef TDS_BR_CW
+#define TDS_BR_CW 4
+#endif
+constexpr int BR_CW = TDS_BR_CW;
+static_assert(BR_CW == 4 || BR_CW == 8, "staging chunk: 4 or 8 channels");
+constexpr int BR_NCH = 32 / BR_CW;  // chunks per window
+template <int CW> struct BRYv;
+template <> struct BRYv<4> { typedef uint2 T; };
+template <> struct BRYv<8> { typedef uint4 T; };
+typedef BRYv<BR_CW>::T BRY;  // one pixel's BR_CW fp16 y2h values
+
+__device__ __forceinline__ uint32_t br_word(const uint2& v, int i) { return i == 0 ? v.x : v.y; }
+__device__ __forceinline__ uint32_t br_word(const uint4& v, int i) {
+  return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
+}
+
+// fma(a, channel cc of the fp16 channels in v, c) on v_fma_mix_f32 (op_sel picks the half)
+template <class V>
+__device__ __forceinline__ float br_fma_y(float a, const V& v, int cc, float c) {
   float d;
-  const uint32_t w = cc < 2 ? v.x : v.y;
+  const uint32_t w = br_word(v, cc >> 1);
   if (cc & 1)
     asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(w), "v"(c));
   else
@@ -495,26 +515,46 @@ __device__ __forceinline__ float br_fma_y(float a, uint2 v, int cc, float c) {
   return d;
 }
 
+__device__ __forceinline__ void br_load_y_impl(__amdgpu_buffer_rsrc_t r, uint32_t off, uint2& v) {
+  v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ void br_load_y_impl(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4& v) {
+  v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ void br_put_words(char* r, const uint32_t (&h)[2]) {
+  *reinterpret_cast<uint2*>(r) = make_uint2(h[0], h[1]);
+}
+__device__ __forceinline__ void br_put_words(char* r, const uint32_t (&h)[4]) {
+  *reinterpret_cast<uint4*>(r) = make_uint4(h[0], h[1], h[2], h[3]);
+}
+__device__ __forceinline__ BRY br_load_y(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  BRY v;
+  br_load_y_impl(r, off, v);
+  return v;
+}
+
 template <int NR, bool BIG, int DIAG>
 struct BRStager {
   static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
-  static constexpr int ITEMS = NWIN * 8;
+  static constexpr int ITEMS = NWIN * BR_NCH;
   static constexpr int IPER = (ITEMS + 255) / 256;
   static constexpr int PIECES = NR * BR_SC * 2;  // 16-B p1 pieces (32-B fp16 records)
   static constexpr int PPER = (PIECES + 255) / 256;
-  uint2 yv[IPER][4];  // y2h: 4 channels of one pixel
-  float4 gv[IPER];
-  uint32_t av[IPER];  // a2: the window's argmax codes, 16 channels
+  BRY yv[IPER][4];      // y2h: BR_CW channels of each pixel of the window
+  float gv[IPER][BR_CW];
+  uint32_t av[IPER];    // a2: the window's argmax codes, 16 channels
   uint4 pr[PPER];
 
-  // the j-th p1 piece of staging lane tid: the set past 256 goes to wave 5 (lanes 64..127), the
-  // items past 256 to wave 4, so no staging wave takes both extras (TDS_BR_PIECE_ROT)
+  // the j-th p1 piece of staging lane tid: the set past 256 goes to a wave without an extra item
+  // (4-channel items: the 64 past 256 are wave 4's, pieces go to wave 5; 8-channel items: waves 4-6
+  // hold the 160, pieces go to wave 7) (TDS_BR_PIECE_ROT)
   __device__ __forceinline__ static int piece(int tid, int j) {
-    return (TDS_BR_PIECE_ROT != 0 && j == 1 ? ((tid + 192) & 255) : tid) + 256 * j;
+    constexpr int rot = BR_CW == 8 ? 64 : 192;
+    return (TDS_BR_PIECE_ROT != 0 && j == 1 ? ((tid + rot) & 255) : tid) + 256 * j;
   }
 
   __device__ __forceinline__ static void item_geom(int it, int& wy, int& wx) {
-    const int w = (it < ITEMS ? it : 0) >> 3;
+    const int w = (it < ITEMS ? it : 0) / BR_NCH;
     wy = w / (BR_SC / 2);
     wx = w - wy * (BR_SC / 2);
   }
@@ -530,10 +570,11 @@ struct BRStager {
     if constexpr (br_no_gload(DIAG)) {
 #pragma unroll
       for (int u = 0; u < IPER; ++u) {
-        gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int k = 0; k < BR_CW; ++k) gv[u][k] = 0.f;
         av[u] = 0u;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) yv[u][q] = make_uint2(0u, 0u);
+        for (int q = 0; q < 4; ++q) yv[u][q] = BRY{};
       }
 #pragma unroll
       for (int j = 0; j < PPER; ++j) pr[j] = make_uint4(0u, 0u, 0u, 0u);
@@ -552,7 +593,7 @@ struct BRStager {
     const __amdgpu_buffer_rsrc_t rg =
         tds_buffer_rsrc(a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t ra = tds_buffer_rsrc(a.a2 + (((int64_t)b * Q + py0) * Q + px0) * 2, 0xFFFFFFF0u);
-    const int c4 = tid & 7;
+    const int cb = (tid % BR_NCH) * BR_CW;  // the chunk's first channel (256 % BR_NCH == 0: every u)
 #pragma unroll
     for (int u = 0; u < IPER; ++u) {
       const int it = tid + 256 * u;
@@ -564,27 +605,24 @@ struct BRStager {
         const int lr = 2 * wy + (q >> 1), lc = 2 * wx + (q & 1);
         const int gr = R0 + lr, gc = c0 - 2 + lc;
         const bool ok = item & (in | (((uint32_t)gr < (uint32_t)P) & ((uint32_t)gc < (uint32_t)P)));
-        const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 64 + c4 * 8) : kBROob;
-        yv[u][q] = DIAG == 7 ? make_uint2(0x3C00u, 0u)
-                             : __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(ry, off, 0, 0));
+        const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 64 + cb * 2) : kBROob;
+        yv[u][q] = br_load_y(ry, off);
       }
       const int py = py0 + wy, px = px0 + wx;
       const bool pooled = item & (in | (((uint32_t)py < (uint32_t)Q) & ((uint32_t)px < (uint32_t)Q)));
-      av[u] = __builtin_amdgcn_raw_buffer_load_b32(ra, pooled ? (uint32_t)(((wy * Q + wx) * 2 + (c4 >> 2)) * 4) : kBROob, 0, 0);
-      float g4[4];
+      av[u] = __builtin_amdgcn_raw_buffer_load_b32(ra, pooled ? (uint32_t)(((wy * Q + wx) * 2 + (cb >> 4)) * 4) : kBROob, 0, 0);
       if constexpr (!BIG) {
-        const uint32_t og = (uint32_t)(((int64_t)c4 * 4 * gplane + (int64_t)wy * Q + wx) * 4);
+        const uint32_t og = (uint32_t)(((int64_t)cb * gplane + (int64_t)wy * Q + wx) * 4);
         const uint32_t gstep = (uint32_t)(gplane * 4);
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          g4[k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
-                                                                                 0, 0));
+        for (int k = 0; k < BR_CW; ++k)
+          gv[u][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
+                                                                                    0, 0));
       } else {
-        const float* gp = a.g2m + ((int64_t)b * 32 + 4 * c4) * gplane + (int64_t)(pooled ? py : 0) * Q + (pooled ? px : 0);
+        const float* gp = a.g2m + ((int64_t)b * 32 + cb) * gplane + (int64_t)(pooled ? py : 0) * Q + (pooled ? px : 0);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) g4[k] = gp[k * gplane];  // masked at use (store: pooled)
+        for (int k = 0; k < BR_CW; ++k) gv[u][k] = gp[k * gplane];  // masked at use (store: pooled)
       }
-      gv[u] = make_float4(g4[0], g4[1], g4[2], g4[3]);
     }
 #pragma unroll
     for (int j = 0; j < PPER; ++j) {
@@ -617,18 +655,27 @@ struct BRStager {
 #pragma unroll
     for (int u = 0; u < IPER; ++u) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) asm volatile("" ::"v"(yv[u][q].x), "v"(yv[u][q].y));
-      asm volatile("" ::"v"(gv[u].x), "v"(gv[u].y), "v"(gv[u].z), "v"(gv[u].w), "v"(av[u]));
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < BR_CW / 2; ++i) asm volatile("" ::"v"(br_word(yv[u][q], i)));
+#pragma unroll
+      for (int k = 0; k < BR_CW; ++k) asm volatile("" ::"v"(gv[u][k]));
+      asm volatile("" ::"v"(av[u]));
     }
 #pragma unroll
     for (int j = 0; j < PPER; ++j) asm volatile("" ::"v"(pr[j].x), "v"(pr[j].y), "v"(pr[j].z), "v"(pr[j].w));
-    const int c4 = tid & 7;
+    const int cb = (tid % BR_NCH) * BR_CW;
     const int P = a.P, Q = a.Q;
-    const float4 k14 = *reinterpret_cast<const float4*>(&kc[2 * 32 + 4 * c4]);
-    const float4 k24 = *reinterpret_cast<const float4*>(&kc[3 * 32 + 4 * c4]);
-    const float4 k34 = *reinterpret_cast<const float4*>(&kc[4 * 32 + 4 * c4]);
-    const float k1[4] = {k14.x, k14.y, k14.z, k14.w}, k2[4] = {k24.x, k24.y, k24.z, k24.w},
-                k3[4] = {k34.x, k34.y, k34.z, k34.w};
+    float k1[BR_CW], k2[BR_CW], k3[BR_CW];
+#pragma unroll
+    for (int h = 0; h < BR_CW / 4; ++h) {
+      const float4 a1 = *reinterpret_cast<const float4*>(&kc[2 * 32 + cb + 4 * h]);
+      const float4 a2v = *reinterpret_cast<const float4*>(&kc[3 * 32 + cb + 4 * h]);
+      const float4 a3 = *reinterpret_cast<const float4*>(&kc[4 * 32 + cb + 4 * h]);
+      k1[4 * h] = a1.x; k1[4 * h + 1] = a1.y; k1[4 * h + 2] = a1.z; k1[4 * h + 3] = a1.w;
+      k2[4 * h] = a2v.x; k2[4 * h + 1] = a2v.y; k2[4 * h + 2] = a2v.z; k2[4 * h + 3] = a2v.w;
+      k3[4 * h] = a3.x; k3[4 * h + 1] = a3.y; k3[4 * h + 2] = a3.z; k3[4 * h + 3] = a3.w;
+    }
     const bool fast = interior(a, R0, c0);
 #pragma unroll
     for (int u = 0; u < IPER; ++u) {
@@ -636,26 +683,26 @@ struct BRStager {
       if (it >= ITEMS) continue;
       int wy, wx;
       item_geom(it, wy, wx);
-      float y[4][4];  // the stored values (ka, kb, k2, k3 carry the decode: kernel header)
+      float y[4][BR_CW];  // the stored values (ka, kb, k2, k3 carry the decode: kernel header)
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        y[q][0] = f16_val(yv[u][q].x);
-        y[q][1] = f16_val(yv[u][q].x >> 16);
-        y[q][2] = f16_val(yv[u][q].y);
-        y[q][3] = f16_val(yv[u][q].y >> 16);
-      }
-      const float gg[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
-      float d[4][4];
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < BR_CW / 2; ++i) {
+          const uint32_t w = br_word(yv[u][q], i);
+          y[q][2 * i] = f16_val(w);
+          y[q][2 * i + 1] = f16_val(w >> 16);
+        }
+      float d[4][BR_CW];
+      // this item's channels' codes: bits (cb & 15) .. +BR_CW-1 and 16 + that of the window's word
+      const uint32_t cw = av[u] >> (cb & 15);
       if constexpr (br_no_math(DIAG)) {  // timing only: no BN2 / pool backward math
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int cc = 0; cc < 4; ++cc) d[q][cc] = y[q][cc] + gg[cc];
+          for (int cc = 0; cc < BR_CW; ++cc) d[q][cc] = y[q][cc] + gv[u][cc];
       } else if (fast) {
-        // this item's 4 channels' codes: bits 4 (c4 & 3) .. +3 and 16 + that of the window's word
-        const uint32_t cw = av[u] >> (4 * (c4 & 3));
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
+        for (int cc = 0; cc < BR_CW; ++cc) {
           // y2h values straight into v_fma_mix_f32 (TDS_BR_MIX; br_fma_y), else converted once
           auto fy = [&](float k, int q, float c) {
             return TDS_BR_MIX ? br_fma_y(k, yv[u][q], cc, c) : fmaf(k, y[q][cc], c);
@@ -664,7 +711,7 @@ struct BRStager {
           // the pooled gradient folded into the constant: select + FMA per pixel.  The 4 compares
           // go first (4 SGPR-pair masks): one VCC reused compare -> select -> compare cost an
           // s_nop per pixel for the VALU-mask hazard
-          const float k3g = fmaf(k1[cc], gg[cc], k3[cc]);
+          const float k3g = fmaf(k1[cc], gv[u][cc], k3[cc]);
           bool eq[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) eq[q] = code == (uint32_t)q;
@@ -678,39 +725,38 @@ struct BRStager {
       } else {
         const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;
         const bool pooled = gy >= 0 && gx >= 0 && (gy >> 1) < Q && (gx >> 1) < Q;
-        const uint32_t cw = av[u] >> (4 * (c4 & 3));
 #pragma unroll
-        for (int cc = 0; cc < 4; ++cc) {
+        for (int cc = 0; cc < BR_CW; ++cc) {
           const int am = pooled ? (int)(((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u)) : -1;
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int r = gy + (q >> 1), c = gx + (q & 1);
             const bool inb = r >= 0 && r < P && c >= 0 && c < P;  // zero padding outside the image
-            const float dz = am == q ? gg[cc] : 0.f;
+            const float dz = am == q ? gv[u][cc] : 0.f;
             d[q][cc] = inb ? fmaf(k1[cc], dz, fmaf(k2[cc], y[q][cc], k3[cc])) : 0.f;
           }
         }
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        uint32_t h01, l01 = 0u, h23, l23 = 0u;  // (k1..k3 carry the scale 2^e: d is dy2 * 2^e)
-        if constexpr (kConv2Split) {
-          split2_f16_mix(d[q][0], d[q][1], h01, l01);
-          split2_f16_mix(d[q][2], d[q][3], h23, l23);
-        } else {  // dy2 rounded once (TF32-class, conv2_common.h): no lo planes
-          h01 = cvt2_f16(d[q][0], d[q][1]);
-          h23 = cvt2_f16(d[q][2], d[q][3]);
+        uint32_t h[BR_CW / 2], l[BR_CW / 2];  // (k1..k3 carry the scale 2^e: d is dy2 * 2^e)
+#pragma unroll
+        for (int i = 0; i < BR_CW / 2; ++i) {
+          l[i] = 0u;
+          if constexpr (kConv2Split)
+            split2_f16_mix(d[q][2 * i], d[q][2 * i + 1], h[i], l[i]);
+          else  // dy2 rounded once (TF32-class, conv2_common.h): no lo planes
+            h[i] = cvt2_f16(d[q][2 * i], d[q][2 * i + 1]);
         }
         const int lr = 2 * wy + (q >> 1);
-        const int ro = (2 * wx + (q & 1)) * 32 + (c4 & 3) * 8;
+        const int ro = (2 * wx + (q & 1)) * 32 + (cb & 15) * 2;
         char* rec = dbase + lr * BR_DROW + ro;
-        *reinterpret_cast<uint2*>(rec + (c4 >> 2) * BR_DPL) = make_uint2(h01, h23);
-        if constexpr (kConv2Split) *reinterpret_cast<uint2*>(rec + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
-        if (MIRROR && lr >= 4) {
-          char* mr = dmir + (lr - 4) * BR_DROW + ro;
-          *reinterpret_cast<uint2*>(mr + (c4 >> 2) * BR_DPL) = make_uint2(h01, h23);
-          if constexpr (kConv2Split) *reinterpret_cast<uint2*>(mr + (2 + (c4 >> 2)) * BR_DPL) = make_uint2(l01, l23);
-        }
+        auto put = [&](char* r) {
+          br_put_words(r + (cb >> 4) * BR_DPL, h);
+          if constexpr (kConv2Split) br_put_words(r + (2 + (cb >> 4)) * BR_DPL, l);
+        };
+        put(rec);
+        if (MIRROR && lr >= 4) put(dmir + (lr - 4) * BR_DROW + ro);
       }
     }
 #pragma unroll
