@@ -592,7 +592,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   uint32_t* gp = opt_mag(mag, mag_numel(B, P)) ? opt_mag(mag) + kMagParts + 32 * mag_ypart_count() : nullptr;
   // the BN2 backward finalize inside the head backward's launch (head_pb.hip HBFin): one pass over
   // all channels, with the conv2 forward having reduced its magnitude parts (ypart_done)
-  const bool fin_in = finalize && whole && npass == 1 && ypart_done && tds_fused_fin_enabled();
+  // (its one-round reducer takes at most 256 workgroups per channel: past that -- images beyond
+  // ~2048^2 pooled -- the separate finalize below)
+  const bool fin_in = finalize && whole && npass == 1 && ypart_done && nblk <= 256 && tds_fused_fin_enabled();
   if (fin_in) {
     auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
     auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");

@@ -487,8 +487,8 @@ constexpr uint32_t kBROob = 0xFFFFFFF0u;
 // BR_CW = 8 (TDS_BR_CW): a pixel's 8 channels of y2h are one 16-B load and one 16-B dy2 store; a
 // tile's 160 items leave one per lane for waves 4-6 (r5_s14 PMC: the texture data path was busy
 // 81 % of the kernel, ~64 cycles per staging load instruction -- fewer, wider loads).
-#ifndef TDS_BR_CW
-#define TDS_BR_CW 4
+#ifndef TDS_BR_CW  // (r5_s16: 8 vs 4 -- isolated 0.696 -> 0.688 ms, driver's command 2.213 -> 2.199, 3 + 3 alternating)
+#define TDS_BR_CW 8
 #endif
 constexpr int BR_CW = TDS_BR_CW;
 static_assert(BR_CW == 4 || BR_CW == 8, "staging chunk: 4 or 8 channels");
