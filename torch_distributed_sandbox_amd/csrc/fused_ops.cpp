@@ -183,10 +183,9 @@ void check_l1_input(const Tensor& x, const char* what) {
 // variance are these moments contracted with w1 (tds_l1_gram); they depend on the batch only,
 // which lets an input pipeline produce them with the batch (on its own stream, beside the
 // previous step's backward) and hand them to fused_l1_forward.
-std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
-  check_l1_input(x, "l1_input_stats");
+// the x moments' per-workgroup partials [nac][42] and the border strips (no reduction yet)
+static std::tuple<Tensor, Tensor, int> x_moment_parts(const Tensor& x) {
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
-  c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
   auto fo = x.options().dtype(at::kDouble);
   // one thread per 4 x 16 pixel block: each fp32 partial covers 64 products (fp64 beyond)
@@ -200,7 +199,17 @@ std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
   else
     tds_x_moments(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
                   st);
-  auto asum = at::empty({42}, fo);
+  return {ac, strips, nac};
+}
+
+std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
+  check_l1_input(x, "l1_input_stats");
+  c10::DeviceGuard guard(x.device());
+  hipStream_t st = stream_of(x);
+  Tensor ac, strips;
+  int nac = 0;
+  std::tie(ac, strips, nac) = x_moment_parts(x);
+  auto asum = at::empty({42}, x.options().dtype(at::kDouble));
   tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
   check_launches("l1_input_stats");
   return {asum, strips};
@@ -233,23 +242,33 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   const bool levels = x.scalar_type() == at::kByte;
   // x autocorrelation + border strips (precomputed by the input pipeline, or here) -> Gram G /
   // patch sums S -> BN1 statistics in closed form
-  Tensor asum, strips;
-  if (asum_in.has_value() && asum_in->defined()) {
-    TORCH_CHECK(strips_in.has_value() && strips_in->defined(), "fused_l1_forward: asum without strips");
-    need(*asum_in, at::kDouble, {42}, "precomputed autocorrelation sums");
-    need(*strips_in, at::kDouble, {B * 8 * 82}, "precomputed border strips");
-    asum = *asum_in;
-    strips = *strips_in;
-  } else {
-    std::tie(asum, strips) = l1_input_stats(x);
-  }
   auto gram = at::empty({650}, fo.dtype(at::kDouble));
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
   auto stats = at::empty({32}, fo);
   auto aff = at::empty({33}, fo);  // a16 | b16 | p1 scale
-  tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H, (int)W,
-              w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps,
-              (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+  if (asum_in.has_value() && asum_in->defined()) {
+    TORCH_CHECK(strips_in.has_value() && strips_in->defined(), "fused_l1_forward: asum without strips");
+    need(*asum_in, at::kDouble, {42}, "precomputed autocorrelation sums");
+    need(*strips_in, at::kDouble, {B * 8 * 82}, "precomputed border strips");
+    tds_l1_gram(asum_in->data_ptr<double>(), strips_in->data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H,
+                (int)W, w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(),
+                (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+  } else {
+    // the moments' partials, then their reduction and the Gram in one launch (tds_l1_reduce_gram)
+    Tensor ac, strips;
+    int nac = 0;
+    std::tie(ac, strips, nac) = x_moment_parts(x);
+    auto asum = at::empty({42}, fo.dtype(at::kDouble));
+    if (!tds_l1_reduce_gram(ac.data_ptr<double>(), nac, asum.data_ptr<double>(), strips.data_ptr<double>(),
+                            x.data_ptr(), levels, (int)B, (int)H, (int)W, w1.data_ptr<float>(),
+                            gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps,
+                            (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st)) {
+      tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
+      tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H, (int)W,
+                  w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(),
+                  (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+    }
+  }
   // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1 (fp16), argmax
   auto p1 = at::empty({B, P, P, 16}, fo.dtype(at::kHalf));
   auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
@@ -805,10 +824,16 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
              p1.data_ptr(), idx1.data_ptr<uint8_t>(),
              w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
-  tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);
-  tds_l1_finalize(bsum.data_ptr<double>(), gram.data_ptr<double>(), B * H * W, w1.data_ptr<float>(),
-                  b1.data_ptr<float>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(), db1.data_ptr<float>(),
-                  dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale, st);
+  // the partials' reduction and the closed-form gradients in one launch (tds_l1_reduce_finalize)
+  if (!tds_l1_reduce_finalize(partial.data_ptr<double>(), rows, bsum.data_ptr<double>(), gram.data_ptr<double>(),
+                              B * H * W, w1.data_ptr<float>(), b1.data_ptr<float>(), g, stats1.data_ptr<float>(),
+                              dw1.data_ptr<float>(), db1.data_ptr<float>(), dg.data_ptr<float>(), dbe.data_ptr<float>(),
+                              (float)scale, st)) {
+    tds_reduce_partials(partial.data_ptr<double>(), bsum.data_ptr<double>(), 16 * 27, rows, 16 * 27, 0, 16 * 27, st);
+    tds_l1_finalize(bsum.data_ptr<double>(), gram.data_ptr<double>(), B * H * W, w1.data_ptr<float>(),
+                    b1.data_ptr<float>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(), db1.data_ptr<float>(),
+                    dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale, st);
+  }
   check_launches("fused_l1_backward");
   return {dw1, db1, dg, dbe};
 }

@@ -242,7 +242,10 @@ __device__ __forceinline__ uint32_t wide_row_max(const uint32_t* base, int nrows
 }
 
 // call sites of the in-launch finalizers (tds_sync_words: kSyncWordsPerSite counters each)
-enum TdsSyncSite { kSyncHeadFwd = 0, kSyncConv2Fwd = 1, kSyncHeadBwd = 2, kSyncL1Bwd = 3, kSyncXMoments = 4 };
+enum TdsSyncSite {
+  kSyncHeadFwd = 0, kSyncConv2Fwd = 1, kSyncHeadBwd = 2, kSyncL1Bwd = 3, kSyncXMoments = 4, kSyncL1Gram = 5,
+  kSyncL1Fin = 6
+};
 constexpr int kSyncSites = 8, kSyncWordsPerSite = 256;
 
 // The head backward's pooled gradient g2m is PLANAR, [B][32][Q][Q] (the fc flatten order):

@@ -960,7 +960,7 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
 //   sum_px (y1 - b1)^2[c] = w1[c]^T G w1[c]
 // gram = G[625] | S[25] (fp64); sums = [c][sum, sumsq] in the bn_finalize_shifted layout.
 template <typename T>
-__global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__ ac_sum,
+__device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
                                                       const double* __restrict__ strips, const T* __restrict__ x,
                                                       int B, int H, int W, const float* __restrict__ w1,
                                                       double* __restrict__ gram, double* __restrict__ sums,
@@ -1027,6 +1027,51 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
   }
 }
 
+
+template <typename T>
+__global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__ ac_sum,
+                                                      const double* __restrict__ strips, const T* __restrict__ x,
+                                                      int B, int H, int W, const float* __restrict__ w1,
+                                                      double* __restrict__ gram, double* __restrict__ sums,
+                                                      const float* __restrict__ b1, float eps, float momentum,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      float* __restrict__ stats, float* __restrict__ running_mean,
+                                                      float* __restrict__ running_var, int64_t* __restrict__ num_batches,
+                                                      float* __restrict__ aff, double xs) {
+  l1_gram_body<T>(ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean,
+                  running_var, num_batches, aff, xs);
+}
+
+// The x autocorrelation partials' reduction and the Gram in ONE launch: workgroup e sums column
+// e of the [nchunk][42] partials in reduce_partials_kernel's order (write-through), and the last
+// to arrive (common.h tds_arrive) runs l1_gram_body on the sums -- one launch boundary and one
+// launch floor fewer on the step's critical path than reduce_partials + l1_gram.
+template <typename T>
+__global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __restrict__ ac_part, int nchunk,
+                                                             double* __restrict__ ac_sum, uint32_t* __restrict__ sync,
+                                                             const double* __restrict__ strips, const T* __restrict__ x,
+                                                             int B, int H, int W, const float* __restrict__ w1,
+                                                             double* __restrict__ gram, double* __restrict__ sums,
+                                                             const float* __restrict__ b1, float eps, float momentum,
+                                                             const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float* __restrict__ stats,
+                                                             float* __restrict__ running_mean,
+                                                             float* __restrict__ running_var,
+                                                             int64_t* __restrict__ num_batches, float* __restrict__ aff,
+                                                             double xs) {
+  __shared__ double sh[8];
+  __shared__ int last;
+  const int e = blockIdx.x;
+  double s = 0.0;
+#pragma unroll 8
+  for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += ac_part[e + (int64_t)k * 42];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) st_agent(ac_sum + e, s);
+  if (!tds_arrive(sync, gridDim.x, &last)) return;
+  l1_gram_body<T>(ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean,
+                  running_var, num_batches, aff, xs);
+}
+
 // Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
 //   dw1[c][j] = a1 sdzx[c][j] + a2 (sum_k w1[c][k] G[k][j] + b1[c] S[j]) + a3 S[j]
 // one thread per (c, j) (400 of 512); every thread of channel c forms its a1..a3 (25 FMAs).
@@ -1061,6 +1106,25 @@ __device__ __forceinline__ void l1_finalize_one(int e, const double* __restrict_
   dw1[c * 25 + j] = (float)(scale * (a1 * acc[2 + j] + a2 * h + a3 * S[j]));
 }
 
+// l1_finalize_one over the 400 (c, j) with its inputs staged in LDS by one round of loads (read
+// through global memory, each thread's 75 dependent-free loads ran as a chain of latencies)
+__device__ __forceinline__ void l1_finalize_body(const double* __restrict__ bwd_sum, const double* __restrict__ gram,
+                                                 int64_t n, const float* __restrict__ w1, const float* __restrict__ b1,
+                                                 const float* __restrict__ gamma1, const float* __restrict__ stats1,
+                                                 float* __restrict__ dw1, float* __restrict__ db1,
+                                                 float* __restrict__ dgamma1, float* __restrict__ dbeta1, float scale) {
+  __shared__ double sg[650];
+  __shared__ double sb[16 * LB_NACC];
+  __shared__ float sw[16 * 25];
+  const int t = threadIdx.x;
+  for (int i = t; i < 650; i += blockDim.x) sg[i] = gram[i];
+  for (int i = t; i < 16 * LB_NACC; i += blockDim.x) sb[i] = bwd_sum[i];
+  for (int i = t; i < 16 * 25; i += blockDim.x) sw[i] = w1[i];
+  __syncthreads();
+  for (int e = t; e < 16 * 25; e += blockDim.x)
+    l1_finalize_one(e, sb, sg, n, sw, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+}
+
 __global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restrict__ bwd_sum,
                                                           const double* __restrict__ gram, int64_t n,
                                                           const float* __restrict__ w1, const float* __restrict__ b1,
@@ -1068,18 +1132,32 @@ __global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restri
                                                           const float* __restrict__ stats1, float* __restrict__ dw1,
                                                           float* __restrict__ db1, float* __restrict__ dgamma1,
                                                           float* __restrict__ dbeta1, float scale) {
-  // the inputs staged in LDS with one round of loads (read through global memory, each thread's
-  // 75 dependent-free loads ran as a chain of latencies: 7 us for 400 outputs)
-  __shared__ double sg[650];
-  __shared__ double sb[16 * LB_NACC];
-  __shared__ float sw[16 * 25];
-  const int e = threadIdx.x;
-  for (int i = e; i < 650; i += blockDim.x) sg[i] = gram[i];
-  for (int i = e; i < 16 * LB_NACC; i += blockDim.x) sb[i] = bwd_sum[i];
-  if (e < 16 * 25) sw[e] = w1[e];
-  __syncthreads();
-  if (e >= 16 * 25) return;
-  l1_finalize_one(e, sb, sg, n, sw, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+  l1_finalize_body(bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+}
+
+// The layer-1 backward partials' reduction and the closed-form gradients in ONE launch: workgroup
+// e sums column e of the [rows][432] partials in reduce_partials_kernel's order (write-through),
+// the last to arrive runs l1_finalize_body.
+__global__ __launch_bounds__(256) void l1_reduce_finalize_kernel(const double* __restrict__ part, int nchunk,
+                                                                 double* __restrict__ bwd_sum, uint32_t* __restrict__ sync,
+                                                                 const double* __restrict__ gram, int64_t n,
+                                                                 const float* __restrict__ w1,
+                                                                 const float* __restrict__ b1,
+                                                                 const float* __restrict__ gamma1,
+                                                                 const float* __restrict__ stats1,
+                                                                 float* __restrict__ dw1, float* __restrict__ db1,
+                                                                 float* __restrict__ dgamma1,
+                                                                 float* __restrict__ dbeta1, float scale) {
+  __shared__ double sh[8];
+  __shared__ int last;
+  const int e = blockIdx.x;
+  double s = 0.0;
+#pragma unroll 8
+  for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += part[e + (int64_t)k * (16 * LB_NACC)];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) st_agent(bwd_sum + e, s);
+  if (!tds_arrive(sync, gridDim.x, &last)) return;
+  l1_finalize_body(bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
 }
 
 }  // namespace tds
@@ -1213,4 +1291,39 @@ void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const
   hipLaunchKernelGGL(l1_finalize_kernel, dim3(1), dim3(512), 0, st, bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1,
                      dgamma1, dbeta1, scale);
   TDS_LAUNCH_CHECK();
+}
+
+// the [rows][432] partials' reduction + tds_l1_finalize in one launch (bwd_sum: the 432 sums, written)
+bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const double* gram, int64_t n,
+                            const float* w1, const float* b1, const float* gamma1, const float* stats1, float* dw1,
+                            float* db1, float* dgamma1, float* dbeta1, float scale, hipStream_t st) {
+  uint32_t* sync = tds_sync_words(kSyncL1Fin, st);
+  if (sync == nullptr) return false;
+  hipLaunchKernelGGL(l1_reduce_finalize_kernel, dim3(16 * LB_NACC), dim3(256), 0, st, part, rows, bwd_sum, sync, gram,
+                     n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+  TDS_LAUNCH_CHECK();
+  return true;
+}
+
+// the x autocorrelation partials' reduction [nchunk][42] -> ac_sum + tds_l1_gram in one launch
+bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, const double* strips, const void* x,
+                        bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,
+                        float eps, float momentum, const float* gamma, const float* beta, float* stats,
+                        float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st) {
+  if (B > L1G_MAXB || H < 12 || W < 12) {
+    tds_launch_fail("l1_gram: needs batch <= 32 and H, W >= 12");
+    return true;
+  }
+  uint32_t* sync = tds_sync_words(kSyncL1Gram, st);
+  if (sync == nullptr) return false;
+  if (levels)
+    hipLaunchKernelGGL(l1_reduce_gram_kernel<uint8_t>, dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync,
+                       strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta,
+                       stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
+  else
+    hipLaunchKernelGGL(l1_reduce_gram_kernel<float>, dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync, strips,
+                       static_cast<const float*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats,
+                       running_mean, running_var, num_batches, aff, 1.0);
+  TDS_LAUNCH_CHECK();
+  return true;
 }

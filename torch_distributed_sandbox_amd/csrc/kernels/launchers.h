@@ -165,6 +165,14 @@ int tds_l1_bwd_max_per_cu(bool levels, bool pairs);  // occupancy of the variant
 void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
                 const uint8_t* idx1, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
                 hipStream_t st, const TdsL1Fin* lf = nullptr);
+// the partial reductions fused with the single-workgroup finalizers (false: no sync words)
+bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const double* gram, int64_t n,
+                            const float* w1, const float* b1, const float* gamma1, const float* stats1, float* dw1,
+                            float* db1, float* dgamma1, float* dbeta1, float scale, hipStream_t st);
+bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, const double* strips, const void* x,
+                        bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,
+                        float eps, float momentum, const float* gamma, const float* beta, float* stats,
+                        float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);
