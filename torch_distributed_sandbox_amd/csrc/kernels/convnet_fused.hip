@@ -1148,14 +1148,21 @@ __global__ __launch_bounds__(256) void l1_reduce_finalize_kernel(const double* _
                                                                  float* __restrict__ dw1, float* __restrict__ db1,
                                                                  float* __restrict__ dgamma1,
                                                                  float* __restrict__ dbeta1, float scale) {
-  __shared__ double sh[8];
+  // 8 columns per workgroup (54 workgroups: one arrival each on the counter instead of 432 --
+  // same-address atomics serialize), 32 row lanes per column, row order fixed
+  __shared__ double sh[32][9];
   __shared__ int last;
-  const int e = blockIdx.x;
+  const int col = blockIdx.x * 8 + (threadIdx.x & 7), rl = threadIdx.x >> 3;
   double s = 0.0;
 #pragma unroll 8
-  for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += part[e + (int64_t)k * (16 * LB_NACC)];
-  s = block_sum(s, sh);
-  if (threadIdx.x == 0) st_agent(bwd_sum + e, s);
+  for (int k = rl; k < nchunk; k += 32) s += part[col + (int64_t)k * (16 * LB_NACC)];
+  sh[rl][threadIdx.x & 7] = s;
+  __syncthreads();
+  if (threadIdx.x < 8) {
+    double t = 0.0;
+    for (int i = 0; i < 32; ++i) t += sh[i][threadIdx.x];
+    st_agent(bwd_sum + col, t);
+  }
   if (!tds_arrive(sync, gridDim.x, &last)) return;
   l1_finalize_body(bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
 }
@@ -1299,7 +1306,8 @@ bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const
                             float* db1, float* dgamma1, float* dbeta1, float scale, hipStream_t st) {
   uint32_t* sync = tds_sync_words(kSyncL1Fin, st);
   if (sync == nullptr) return false;
-  hipLaunchKernelGGL(l1_reduce_finalize_kernel, dim3(16 * LB_NACC), dim3(256), 0, st, part, rows, bwd_sum, sync, gram,
+  static_assert((16 * LB_NACC) % 8 == 0, "8 columns per workgroup");
+  hipLaunchKernelGGL(l1_reduce_finalize_kernel, dim3(16 * LB_NACC / 8), dim3(256), 0, st, part, rows, bwd_sum, sync, gram,
                      n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
   TDS_LAUNCH_CHECK();
   return true;
