@@ -279,6 +279,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
 }
 
 // ---------------------------------------------------------------- conv2 forward
+constexpr int64_t kG2mSlack = 16;   // floats past g2m's end its allocations carry (conv2_bwd.hip GB runs)
 constexpr int64_t kMagParts = 64;   // ypart offset in the mag workspace
 constexpr int64_t kMagScales = 40;  // conv2 epilogue scales (csrc/kernels/conv2_common.h)
 int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
@@ -597,7 +598,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     g2m = *g2m_out;
   } else {
     TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into g2m_out");
-    g2m = at::empty({B, 32, Q, Q}, ya.options());  // planar (the fc flatten order)
+    // planar (the fc flatten order), with the 64 B of slack the conv2 backward's row loads may
+    // touch past the last row (conv2_bwd.hip BRStager GB)
+    g2m = at::empty({B * 32 * Q * Q + kG2mSlack}, ya.options()).narrow(0, 0, B * 32 * Q * Q).view({B, 32, Q, Q});
   }
   const int nblk = tds_head_bwd_pb_nblk((int)Q), npass = tds_head_bwd_pb_npass((int)B);
   Tensor partial;
@@ -675,6 +678,9 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   need(a2, at::kInt, {B, P / 2, P / 2, 2}, "a2 (fused_conv2_forward's pooling argmax codes)");
   need(b2, at::kFloat, {32}, "conv2.bias");
   need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
+  TORCH_CHECK((int64_t)g2m.storage().nbytes() >= (g2m.storage_offset() + g2m.numel() + kG2mSlack) * 4,
+              "fused_conv2_backward_y2: g2m needs ", kG2mSlack, " floats of slack after it (as fused_head_backward "
+              "allocates it): the staging's row loads may read past the last row");
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
   need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");

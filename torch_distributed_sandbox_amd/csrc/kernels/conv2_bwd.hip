@@ -87,7 +87,10 @@ constexpr int BR_OFF_X = BR_OFF_P + 3 * BR_SLOT * BR_PROW;   // 2 exchange slots
 constexpr int BR_OFF_K = BR_OFF_X + 2 * BR_XCHG;             // 160 floats of constants + 4
 constexpr int BR_KINV = 160;  // kc[160] = 2^-e * 2^-ew (dp1), kc[161] = 2^-e / p1 scale (weight taps), kc[162] = 2^-e (bias),
                               // kc[163] = 2^kd (the dp1h store factor)
-constexpr int BR_LDS = BR_OFF_K + (5 * 32 + 4) * 4;
+// the pipelined staging's pooled-gradient tiles (TDS_BR_GB): 2 x [4 pooled rows][10 cols][32 ch] fp32
+constexpr int BR_GTILE = 4 * 10 * 32;
+constexpr int BR_OFF_G = (BR_OFF_K + (5 * 32 + 4) * 4 + 15) / 16 * 16;
+constexpr int BR_LDS = BR_OFF_G + 2 * BR_GTILE * 4;
 static_assert(BR_LDS <= 160 * 1024 && BR_OFF_X % 16 == 0 && BR_OFF_K % 16 == 0, "LDS carve");
 
 // walk table entries (tds_conv2_bwd_walk): bit 31 = first tile of a segment, bit 30 = past the
@@ -533,7 +536,16 @@ __device__ __forceinline__ BRY br_load_y(__amdgpu_buffer_rsrc_t r, uint32_t off)
   return v;
 }
 
-template <int NR, bool BIG, int DIAG>
+// GB (the pipelined 8-row sets): the tile's pooled gradient g2m is not gathered per item (BR_CW
+// 4-B loads from as many channel planes) but per RUN -- one (channel, pooled row) of the tile's 10
+// pooled columns, on staging lanes 128-255: a 4-B load of the left halo column, two 16-B loads of
+// the 8 columns of the tile, a 4-B load of the right halo -- and passed to the items through an LDS
+// tile ([pooled row][col][channel]: two 16-B reads per item) written one tile ahead (put_runs).
+// Per tile 8 load instructions instead of 20 (r5_s14: the texture path, ~64 cycles per staging
+// load instruction, is the staging's limiter).  Mid loads past a row's end read the next row or,
+// for the tensor's last row, the 64 B of slack every g2m allocation carries (fused_ops.cpp): those
+// columns are never pooled.
+template <int NR, bool BIG, int DIAG, bool GB = false>
 struct BRStager {
   static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
   static constexpr int ITEMS = NWIN * BR_NCH;
@@ -544,6 +556,8 @@ struct BRStager {
   float gv[IPER][BR_CW];
   uint32_t av[IPER];    // a2: the window's argmax codes, 16 channels
   uint4 pr[PPER];
+  float4 rm0, rm1;      // GB: this lane's run, columns 1-4 and 5-8
+  float rl, rr;         // GB: its columns 0 and 9 (the halo)
 
   // the j-th p1 piece of staging lane tid: the set past 256 goes to a wave without an extra item
   // (4-channel items: the 64 past 256 are wave 4's, pieces go to wave 5; 8-channel items: waves 4-6
@@ -593,6 +607,27 @@ struct BRStager {
     const __amdgpu_buffer_rsrc_t rg =
         tds_buffer_rsrc(a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t ra = tds_buffer_rsrc(a.a2 + (((int64_t)b * Q + py0) * Q + px0) * 2, 0xFFFFFFF0u);
+    if constexpr (GB) {
+      // the runs first: put_runs waits for them one tile before the rest of this set is needed
+      const int rt = tid - 128;  // lanes 128-255: channel rt & 31, pooled row rt >> 5
+      const int c = rt & 31, wy = (rt >> 5) & 3;
+      const bool row = (rt >= 0) & ((uint32_t)(py0 + wy) < (uint32_t)Q);
+      const bool lok = row & (px0 >= 0), rok = row & (px0 + 9 < Q);
+      const int64_t e0 = (int64_t)c * gplane + (int64_t)wy * Q;  // element of column 0, from rg's base
+      if constexpr (!BIG) {
+        const uint32_t o = (uint32_t)(e0 * 4);
+        rl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lok ? o : kBROob, 0, 0));
+        rm0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 4 : kBROob, 0, 0));
+        rm1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 20 : kBROob, 0, 0));
+        rr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, rok ? o + 36 : kBROob, 0, 0));
+      } else {
+        const float* gp = a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0 + (row ? e0 : 0);
+        rl = lok ? gp[0] : 0.f;  // (BIG: 64-bit loads; the rare >4 GiB-per-image shapes)
+        rm0 = *reinterpret_cast<const float4*>(gp + 1);
+        rm1 = *reinterpret_cast<const float4*>(gp + 5);
+        rr = rok ? gp[9] : 0.f;
+      }
+    }
     const int cb = (tid % BR_NCH) * BR_CW;  // the chunk's first channel (256 % BR_NCH == 0: every u)
 #pragma unroll
     for (int u = 0; u < IPER; ++u) {
@@ -611,7 +646,9 @@ struct BRStager {
       const int py = py0 + wy, px = px0 + wx;
       const bool pooled = item & (in | (((uint32_t)py < (uint32_t)Q) & ((uint32_t)px < (uint32_t)Q)));
       av[u] = __builtin_amdgcn_raw_buffer_load_b32(ra, pooled ? (uint32_t)(((wy * Q + wx) * 2 + (cb >> 4)) * 4) : kBROob, 0, 0);
-      if constexpr (!BIG) {
+      if constexpr (GB) {
+        // (from the LDS tile in store())
+      } else if constexpr (!BIG) {
         const uint32_t og = (uint32_t)(((int64_t)cb * gplane + (int64_t)wy * Q + wx) * 4);
         const uint32_t gstep = (uint32_t)(gplane * 4);
 #pragma unroll
@@ -636,6 +673,19 @@ struct BRStager {
     }
   }
 
+  // GB: this set's runs into the LDS tile gb ([pooled row][col][channel])
+  __device__ __forceinline__ void put_runs(float* gb, int tid) const {
+    static_assert(GB, "runs only in the pipelined sets");
+    const int rt = tid - 128;
+    if (rt < 0) return;
+    const int c = rt & 31, wy = rt >> 5;
+    float* d = gb + wy * 10 * 32 + c;
+    d[0] = rl;
+    d[32] = rm0.x; d[64] = rm0.y; d[96] = rm0.z; d[128] = rm0.w;
+    d[160] = rm1.x; d[192] = rm1.y; d[224] = rm1.z; d[256] = rm1.w;
+    d[288] = rr;
+  }
+
   // BN2 / ReLU / pool backward of the staged windows -> dy2 hi|lo rows at dbase; p1 -> pbase;
   // MIRROR: rows 4-7 stored a second time at dmir / pmir (the next slot's top rows).
   // dy2 = k1*dz + k2*y2 + k3, dz = pooled gradient at the window's argmax, which the forward
@@ -645,7 +695,7 @@ struct BRStager {
   // one (zero padding, unpooled last row / column).
   template <bool MIRROR>
   __device__ __forceinline__ void store(const BRArgs& a, int R0, int c0, int tid, char* dbase, char* pbase,
-                                        const float* kc, char* dmir, char* pmir) {
+                                        const float* kc, char* dmir, char* pmir, const float* gb = nullptr) {
     if constexpr (DIAG == 3) {}
     // every register of the set is read here, on every path: the items / pieces past ITEMS /
     // PIECES are skipped below under exec masks, and a load whose result was consumed only
@@ -658,14 +708,29 @@ struct BRStager {
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int i = 0; i < BR_CW / 2; ++i) asm volatile("" ::"v"(br_word(yv[u][q], i)));
+      if constexpr (!GB) {
 #pragma unroll
-      for (int k = 0; k < BR_CW; ++k) asm volatile("" ::"v"(gv[u][k]));
+        for (int k = 0; k < BR_CW; ++k) asm volatile("" ::"v"(gv[u][k]));
+      }
       asm volatile("" ::"v"(av[u]));
     }
 #pragma unroll
     for (int j = 0; j < PPER; ++j) asm volatile("" ::"v"(pr[j].x), "v"(pr[j].y), "v"(pr[j].z), "v"(pr[j].w));
     const int cb = (tid % BR_NCH) * BR_CW;
     const int P = a.P, Q = a.Q;
+    if constexpr (GB) {  // the items' pooled gradients from the LDS tile (put_runs, a tile earlier)
+#pragma unroll
+      for (int u = 0; u < IPER; ++u) {
+        int wy, wx;
+        item_geom(tid + 256 * u, wy, wx);
+        const float4* gp = reinterpret_cast<const float4*>(gb + (wy * 10 + wx) * 32 + cb);
+#pragma unroll
+        for (int h = 0; h < BR_CW / 4; ++h) {
+          const float4 v = gp[h];
+          gv[u][4 * h] = v.x; gv[u][4 * h + 1] = v.y; gv[u][4 * h + 2] = v.z; gv[u][4 * h + 3] = v.w;
+        }
+      }
+    }
     float k1[BR_CW], k2[BR_CW], k3[BR_CW];
 #pragma unroll
     for (int h = 0; h < BR_CW / 4; ++h) {
@@ -790,9 +855,16 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   auto ptop = [&](int j) { return smem + BR_OFF_P + (j % 3) * BR_SLOT * BR_PROW; };
   // tile j's new rows, its last 4 mirrored into tile j+1's top (overwritten by a prologue when
   // tile j+1 starts a segment: a later iteration, past a barrier)
-  auto stage = [&](BRStager<8, BIG, DIAG>& s, int j, const BRTile& x) {
+#ifndef TDS_BR_GB
+#define TDS_BR_GB 1  // the pipelined sets take g2m by runs through an LDS tile (BRStager GB)
+#endif
+  constexpr bool GBS = TDS_BR_GB != 0 && TDS_BR_STAGE_SETS == 3;
+  typedef BRStager<8, BIG, DIAG, GBS> Set;
+  float* gtile = reinterpret_cast<float*>(smem + BR_OFF_G);
+  auto gbuf = [&](int j) { return gtile + (j & 1) * BR_GTILE; };
+  auto stage = [&](Set& s, int j, const BRTile& x) {
     s.template store<true>(a, x.r0 + 2, x.c0, tid, dtop(j) + 4 * BR_DROW, ptop(j) + 4 * BR_PROW, kc, dtop(j + 1),
-                           ptop(j + 1));
+                           ptop(j + 1), gbuf(j));
   };
   // a segment's first tile: its 4 top rows (image rows r0-2 .. r0+1) staged synchronously
   // straight into its slot's top (once per ~48 tiles)
@@ -810,7 +882,7 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   BRClock<DIAG> clk;
   clk.start();
   auto tile = [&](int j) { return br_decode(a.walk, j, a.sk, a.w); };
-  auto ld = [&](BRStager<8, BIG, DIAG>& s, int j) {
+  auto ld = [&](Set& s, int j) {
     const BRTile x = tile(j);
     // the look-ahead loads issue at raised priority (the SIMD's MFMA wave otherwise delays
     // them), the BN2-backward VALU work at the lowest (tools/gpu_sessions/r2_knobs.sh: 1.519 /
@@ -821,51 +893,59 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   };
   // stage tile j from set s if it exists (a segment start also gets its prologue: after the set is
   // stored and before it is reloaded, so its registers are the set's); false past the list's end
-  auto stage_if = [&](BRStager<8, BIG, DIAG>& s, int j) {
+  // GBS: nxt (the set holding tile j+1) puts its g2m runs into tile j+1's LDS tile; they are read
+  // after the next barrier, and that tile's previous contents (tile j-1) were read before this one
+  auto stage_if = [&](Set& s, Set& nxt, int j) {
     const BRTile x = tile(j);
     if (!x.end) {
       stage(s, j, x);
+      if constexpr (GBS) nxt.put_runs(gbuf(j + 1), tid);
       if (x.start) prologue(j, x);
     }
     return !x.end;
   };
 #if TDS_BR_STAGE_SETS == 3
-  BRStager<8, BIG, DIAG> st0, st1, st2;
+  Set st0, st1, st2;
   {
     const BRTile x0 = tile(0);
-    if (!x0.end) {
-      ld(st0, 0);
-      stage(st0, 0, x0);
+    if (!x0.end) {  // tile 0: its own synchronous set, g2m per item (no LDS tile precedes it)
+      BRStager<8, BIG, DIAG, false> s0;
+      __builtin_amdgcn_s_setprio(TDS_BR_LOAD_PRIO);
+      s0.load(a, x0.b, x0.r0 + 2, x0.c0, tid);
+      __builtin_amdgcn_s_setprio(0);
+      s0.template store<true>(a, x0.r0 + 2, x0.c0, tid, dtop(0) + 4 * BR_DROW, ptop(0) + 4 * BR_PROW, kc, dtop(1),
+                              ptop(1));
       prologue(0, x0);
     }
   }
   ld(st1, 1);
   ld(st2, 2);
   ld(st0, 3);
+  if constexpr (GBS) st1.put_runs(gbuf(1), tid);  // tile 1's, read after the loop's first barrier
   // iteration kk: tile kk+1 from st1 (reload: kk+4), kk+2 from st2 (kk+5), kk+3 from st0 (kk+6);
   // one exit and every set reloaded on every path (the two-set loop's rule, below).  The walk
   // table carries BR_WALK_PAD end entries: the last iteration (kk <= n-1) reads tile kk + 6.
   bool more = !tile(0).end;
   for (int kk = 0; more; kk += 3) {
     clk.barrier();  // consumers start tile kk
-    const bool has1 = stage_if(st1, kk + 1);
+    const bool has1 = stage_if(st1, st2, kk + 1);
     ld(st1, kk + 4);
     bool has2 = false;
     if (has1) {
       clk.barrier();  // tile kk + 1
-      has2 = stage_if(st2, kk + 2);
+      has2 = stage_if(st2, st0, kk + 2);
     }
     ld(st2, kk + 5);
     bool has3 = false;
     if (has2) {
       clk.barrier();  // tile kk + 2
-      has3 = stage_if(st0, kk + 3);
+      has3 = stage_if(st0, st1, kk + 3);
     }
     ld(st0, kk + 6);
     more = has3;
   }
 #else
-  BRStager<8, BIG, DIAG> st0, st1;
+  Set st0, st1;
   {
     const BRTile x0 = tile(0);
     if (!x0.end) {
@@ -884,12 +964,12 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   bool more = !tile(0).end;
   for (int kk = 0; more; kk += 2) {
     clk.barrier();  // consumers start tile kk
-    const bool second = stage_if(st1, kk + 1);
+    const bool second = stage_if(st1, st0, kk + 1);
     ld(st1, kk + 3);
     bool has2 = false;
     if (second) {
       clk.barrier();  // consumers start tile kk + 1
-      has2 = stage_if(st0, kk + 2);
+      has2 = stage_if(st0, st1, kk + 2);
     }
     ld(st0, kk + 4);  // (past the end: the list's last tile again, never staged)
     more = has2;
