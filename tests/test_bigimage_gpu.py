@@ -5,6 +5,8 @@ past flat index 2^31 and the conv2 weight / bias gradients (the OOM story of the
 288 GB per MI355X).  The reference runs the reference model's ops (Conv2d -> BatchNorm2d(train) ->
 ReLU -> MaxPool2d, twice, then Linear and CrossEntropy, mnist_onegpu.py:14-24) in fp64, row chunk
 by row chunk, with the convolutions as unfold + GEMM."""
+import gc
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -66,6 +68,9 @@ def test_one_step_beyond_2gib(gpu):
     from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import CrossEntropyLoss
 
+    # what earlier tests of the same process still hold (module-scoped fixtures, caches) is not this step's
+    gc.collect()
+    base = torch.cuda.memory_allocated(gpu)
     torch.manual_seed(0)
     m = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
     g = torch.Generator(device=gpu).manual_seed(3)
@@ -86,8 +91,8 @@ def test_one_step_beyond_2gib(gpu):
         p.grad = None
     del loss
     # nothing of the step outlives its backward: the fc weight and x remain
-    held = torch.cuda.memory_allocated(gpu)
-    assert held < m.fc.weight.numel() * 4 + x.numel() * 4 + 2**30, held
+    held = torch.cuda.memory_allocated(gpu) - base
+    assert held < m.fc.weight.numel() * 4 + x.numel() * 4 + 2**30, (held, base)
     torch.cuda.empty_cache()
     bn1, bn2 = m.layer1[1], m.layer2[1]
     c1, c2 = m.layer1[0], m.layer2[0]
