@@ -122,6 +122,10 @@ def _parser():
                     help="how each step's batch reaches the model: 'levels' = the resized images' uint8 levels "
                          "(ToTensor's 1/255 folded into conv1 by the fused plan, models/convnet.py to_image), "
                          "'fp32' = the ToTensor image materialised by the upsample kernel")
+    ap.add_argument("--fused-input-moments", action=argparse.BooleanOptionalAction, default=True,
+                    help="levels input, fused plan: the upsample kernel also forms the batch's x autocorrelation "
+                         "partials behind BN1's statistics (ops.functional.upsample_levels_moments); off: the "
+                         "layer-1 forward forms them from the written image")
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
                     help="produce the next batch (upsample + BN1 input moments) on a side stream beside the "
                          "current step's head kernels (--prefetch-at)")
@@ -596,7 +600,17 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     data_stream = torch.cuda.Stream(device) if on_gpu and args.prefetch else None
     with_stats = data_stream is not None and args.mode != "layers"
 
+    fused_moments = on_gpu and args.fused_input_moments and args.input == "levels" and args.mode != "layers"
+
     def produce(i):
+        if fused_moments:
+            # the step's input op with the x moments formed from its levels in the same pass: the layer-1
+            # forward then reduces them (no second read of the image); the batch's 45 M pixels and 41
+            # products per pixel are computed every step exactly as before
+            x, part = TF.upsample_levels_moments(src_pool[i % pool], H, W)
+            if part is not None:
+                convnet_fused.attach_input_stats(x, (part, None))
+            return x
         return TF.upsample_bilinear_u8(src_pool[i % pool], H, W, levels=args.input == "levels")
 
     pending = {}
@@ -611,12 +625,13 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
         data_stream.wait_stream(cur)
         with torch.cuda.stream(data_stream):
             x = produce(i)
-            stats = convnet_fused.input_stats(x) if with_stats else None
+            stats = convnet_fused.input_stats(x) if with_stats and not fused_moments else None
         x.record_stream(cur)
         if stats is not None:
-            for t in stats:
-                t.record_stream(cur)
             convnet_fused.attach_input_stats(x, stats)
+        for t in convnet_fused._take_input_stats(x):
+            if t is not None:
+                t.record_stream(cur)
         pending[i] = x
 
     sdma = None
@@ -717,6 +732,9 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
                            and ex.zs_stats["steps"]] or None,
             "reserve_cus": reserve,
             "prefetch": data_stream is not None,
+            # where the batch's x moments (BN1's weight-independent half) are formed: in the upsample's pass
+            # over the levels, by the prefetch stream's own kernel, or in the layer-1 forward
+            "input_moments": ("upsample" if fused_moments else "prefetch" if with_stats else "layer1_forward"),
             "prefetch_at": args.prefetch_at if data_stream is not None else None,
             "input": ("uint8 levels (ToTensor's 1/255 folded into conv1)" if args.input == "levels"
                       else "fp32 image"),

@@ -27,6 +27,7 @@ def test_bench_one_gpu_small(gpu, prefetch):
                 "--prefetch" if prefetch else "--no-prefetch"])
     assert r["n_gpus"] == 1 and r["config"]["fc_grad"] == "local" and r["value"] > 0
     assert r["config"]["prefetch"] is prefetch
+    assert r["config"]["input_moments"] == "upsample"
 
 
 @pytest.mark.parametrize("exchange", ["auto", "allreduce"])

@@ -45,3 +45,10 @@ def test_layer1_backward_level_lds_layout():
     spec.loader.exec_module(mod)
     assert mod.main()
     assert mod.word_layout()
+
+
+def test_upsample_levels_moments_cpu_is_plain_upsample():
+    """On CPU the fused input op is the plain level upsample without partials."""
+    src = torch.randint(0, 256, (2, 28, 28), dtype=torch.uint8)
+    x, part = TF.upsample_levels_moments(src, 64, 64)
+    assert part is None and torch.equal(x, TF.upsample_bilinear_u8(src, 64, 64, levels=True))

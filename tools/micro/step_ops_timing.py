@@ -124,7 +124,27 @@ def main():
             ops.fused_head_forward_upd(st["c2"][2], st["hf"][2], w2c, fc.bias, P, dl, meta.view(1, -1),
                                        vals.view(1, -1), B, 1.0, 1e-12)
 
-        seq = [("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
+        xl = TF.upsample_bilinear_u8(src, H, H, levels=True)
+
+        def ups():  # the bench's input op: uint8 levels
+            TF.upsample_bilinear_u8(src, H, H, levels=True)
+
+        def moments():  # the x moments' partials + border strips + reduction (levels input)
+            ops.l1_input_stats(xl)
+
+        def ups_mom():  # the input op fused with the moments' partials
+            st["um"] = ops.upsample_levels_moments(src, H, H)
+
+        def l1f_u8():  # the layer-1 forward on levels, reducing the fused op's partials (border strips in-launch)
+            ops.fused_l1_forward(st["um"][0], c1.weight, c1.bias, n1.weight, n1.bias, n1.running_mean,
+                                 n1.running_var, n1.num_batches_tracked, 0.1, 1e-5, st["um"][1], None)
+
+        def l1f_u8_self():  # ... forming the moments itself (autocorrelation + in-launch border)
+            ops.fused_l1_forward(xl, c1.weight, c1.bias, n1.weight, n1.bias, n1.running_mean,
+                                 n1.running_var, n1.num_batches_tracked, 0.1, 1e-5, None, None)
+
+        seq = [("ups", ups), ("moments", moments), ("ups_mom", ups_mom), ("l1_fwd_u8", l1f_u8),
+               ("l1_fwd_u8_self", l1f_u8_self), ("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
                ("head_bwd_nomag", hb_nomag), ("conv2_bwd", c2b), ("l1_bwd", l1b),
                ("head_fwd_x", hf_x), ("zs_enc_x", enc_x), ("zs_enc_ya", enc_ya), ("dw_zs", dw_zs), ("head_fwd_upd", hf_upd)]
         only = set(a.only.split(",")) if a.only else None

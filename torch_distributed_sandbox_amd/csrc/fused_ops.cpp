@@ -183,8 +183,9 @@ void check_l1_input(const Tensor& x, const char* what) {
 // variance are these moments contracted with w1 (tds_l1_gram); they depend on the batch only,
 // which lets an input pipeline produce them with the batch (on its own stream, beside the
 // previous step's backward) and hand them to fused_l1_forward.
-// the x moments' per-workgroup partials [nac][42] and the border strips (no reduction yet)
-static std::tuple<Tensor, Tensor, int> x_moment_parts(const Tensor& x) {
+// the x moments' per-workgroup partials [nac][42] and the border strips (no reduction yet); uint8
+// levels without border_wgs: the partials only (tds_l1_reduce_gram's border workgroups form the strips)
+static std::tuple<Tensor, Tensor, int> x_moment_parts(const Tensor& x, bool border_wgs) {
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
   hipStream_t st = stream_of(x);
   auto fo = x.options().dtype(at::kDouble);
@@ -195,7 +196,7 @@ static std::tuple<Tensor, Tensor, int> x_moment_parts(const Tensor& x) {
   auto strips = at::empty({B * 8 * 82}, fo);
   if (x.scalar_type() == at::kByte)
     tds_x_moments_u8(x.data_ptr<uint8_t>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H,
-                     (int)W, st);
+                     (int)W, st, border_wgs);
   else
     tds_x_moments(x.data_ptr<float>(), ac.data_ptr<double>(), nac, strips.data_ptr<double>(), (int)B, (int)H, (int)W,
                   st);
@@ -208,7 +209,7 @@ std::tuple<Tensor, Tensor> l1_input_stats(const Tensor& x) {
   hipStream_t st = stream_of(x);
   Tensor ac, strips;
   int nac = 0;
-  std::tie(ac, strips, nac) = x_moment_parts(x);
+  std::tie(ac, strips, nac) = x_moment_parts(x, true);
   auto asum = at::empty({42}, x.options().dtype(at::kDouble));
   tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
   check_launches("l1_input_stats");
@@ -246,7 +247,32 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
   auto sums = at::empty({32}, fo.dtype(at::kDouble));
   auto stats = at::empty({32}, fo);
   auto aff = at::empty({33}, fo);  // a16 | b16 | p1 scale
-  if (asum_in.has_value() && asum_in->defined()) {
+  // the moments' partials (from the fused upsample, ops.upsample_levels_moments, or here) -> their
+  // reduction and the Gram in one launch (tds_l1_reduce_gram), uint8 levels' border strips formed
+  // by workgroups of that launch
+  auto reduce_gram = [&](const Tensor& ac, int nac, Tensor& strips, bool border) {
+    auto asum = at::empty({42}, fo.dtype(at::kDouble));
+    if (tds_l1_reduce_gram(ac.data_ptr<double>(), nac, asum.data_ptr<double>(), strips.data_ptr<double>(),
+                           x.data_ptr(), levels, (int)B, (int)H, (int)W, w1.data_ptr<float>(), gram.data_ptr<double>(),
+                           sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps, (float)momentum, g, be,
+                           stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st, border))
+      return;
+    if (border) tds_x_border_u8(x.data_ptr<uint8_t>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, st);
+    tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
+    tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H, (int)W,
+                w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(),
+                (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+  };
+  const bool pre = asum_in.has_value() && asum_in->defined();
+  if (pre && asum_in->numel() != 42) {
+    // autocorrelation partials [rows][42] of this batch (ops.upsample_levels_moments), strips not yet formed
+    TORCH_CHECK(levels, "fused_l1_forward: precomputed moment partials need a uint8 level batch");
+    TORCH_CHECK(!(strips_in.has_value() && strips_in->defined()), "fused_l1_forward: partials come without strips");
+    TORCH_CHECK(asum_in->numel() % 42 == 0 && asum_in->numel() / 42 <= INT32_MAX, "fused_l1_forward: partials [rows][42]");
+    need(*asum_in, at::kDouble, {asum_in->numel()}, "precomputed autocorrelation partials");
+    auto strips = at::empty({B * 8 * 82}, fo.dtype(at::kDouble));
+    reduce_gram(*asum_in, (int)(asum_in->numel() / 42), strips, true);
+  } else if (pre) {
     TORCH_CHECK(strips_in.has_value() && strips_in->defined(), "fused_l1_forward: asum without strips");
     need(*asum_in, at::kDouble, {42}, "precomputed autocorrelation sums");
     need(*strips_in, at::kDouble, {B * 8 * 82}, "precomputed border strips");
@@ -254,20 +280,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
                 (int)W, w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(),
                 (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   } else {
-    // the moments' partials, then their reduction and the Gram in one launch (tds_l1_reduce_gram)
     Tensor ac, strips;
     int nac = 0;
-    std::tie(ac, strips, nac) = x_moment_parts(x);
-    auto asum = at::empty({42}, fo.dtype(at::kDouble));
-    if (!tds_l1_reduce_gram(ac.data_ptr<double>(), nac, asum.data_ptr<double>(), strips.data_ptr<double>(),
-                            x.data_ptr(), levels, (int)B, (int)H, (int)W, w1.data_ptr<float>(),
-                            gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps,
-                            (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st)) {
-      tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
-      tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H, (int)W,
-                  w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(),
-                  (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
-    }
+    std::tie(ac, strips, nac) = x_moment_parts(x, !levels);
+    reduce_gram(ac, nac, strips, levels);
   }
   // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1 (fp16), argmax
   auto p1 = at::empty({B, P, P, 16}, fo.dtype(at::kHalf));

@@ -25,6 +25,7 @@
 #include "bf16x3.h"
 #include "bn_finalize.h"
 #include "launchers.h"
+#include "xmom_u8.h"
 
 namespace tds {
 
@@ -1046,10 +1047,12 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
 // e of the [nchunk][42] partials in reduce_partials_kernel's order (write-through), and the last
 // to arrive (common.h tds_arrive) runs l1_gram_body on the sums -- one launch boundary and one
 // launch floor fewer on the step's critical path than reduce_partials + l1_gram.
-template <typename T>
+// BORDER (uint8 levels): workgroups 42 .. 42 + 4B - 1 form the border strips from x themselves
+// (xmom_u8.h, one per image side) and arrive with the column sums.
+template <typename T, bool BORDER>
 __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __restrict__ ac_part, int nchunk,
                                                              double* __restrict__ ac_sum, uint32_t* __restrict__ sync,
-                                                             const double* __restrict__ strips, const T* __restrict__ x,
+                                                             double* __restrict__ strips, const T* __restrict__ x,
                                                              int B, int H, int W, const float* __restrict__ w1,
                                                              double* __restrict__ gram, double* __restrict__ sums,
                                                              const float* __restrict__ b1, float eps, float momentum,
@@ -1062,11 +1065,17 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
   __shared__ double sh[8];
   __shared__ int last;
   const int e = blockIdx.x;
-  double s = 0.0;
+  if constexpr (BORDER) {
+    __shared__ uint32_t lines[BSIDE_LDS_WORDS];
+    if (e >= 42) x_border_side_u8(x, strips, (e - 42) >> 2, (e - 42) & 3, H, W, lines);
+  }
+  if (e < 42) {
+    double s = 0.0;
 #pragma unroll 8
-  for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += ac_part[e + (int64_t)k * 42];
-  s = block_sum(s, sh);
-  if (threadIdx.x == 0) st_agent(ac_sum + e, s);
+    for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += ac_part[e + (int64_t)k * 42];
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) st_agent(ac_sum + e, s);
+  }
   if (!tds_arrive(sync, gridDim.x, &last)) return;
   l1_gram_body<T>(ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean,
                   running_var, num_batches, aff, xs);
@@ -1314,24 +1323,34 @@ bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const
 }
 
 // the x autocorrelation partials' reduction [nchunk][42] -> ac_sum + tds_l1_gram in one launch
-bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, const double* strips, const void* x,
+// border: the strips are formed in this launch (uint8 levels only, lines <= XMOM_MAX_LINE long)
+bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, double* strips, const void* x,
                         bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,
                         float eps, float momentum, const float* gamma, const float* beta, float* stats,
-                        float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st) {
+                        float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st,
+                        bool border) {
   if (B > L1G_MAXB || H < 12 || W < 12) {
     tds_launch_fail("l1_gram: needs batch <= 32 and H, W >= 12");
     return true;
   }
+  if (border && (!levels || W % 4 != 0 || H > XMOM_MAX_LINE || W > XMOM_MAX_LINE || (int64_t)H * W > 0xFFFFFFF0LL)) {
+    tds_launch_fail("l1_reduce_gram: in-launch border strips need uint8 levels, W % 4 == 0 and lines <= 66051");
+    return true;
+  }
   uint32_t* sync = tds_sync_words(kSyncL1Gram, st);
   if (sync == nullptr) return false;
-  if (levels)
-    hipLaunchKernelGGL(l1_reduce_gram_kernel<uint8_t>, dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync,
-                       strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta,
-                       stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
+  if (levels && border)
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + 4 * B), dim3(256), 0, st, ac_part, nchunk,
+                       ac_sum, sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum,
+                       gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
+  else if (levels)
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, false>), dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum,
+                       sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma,
+                       beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
   else
-    hipLaunchKernelGGL(l1_reduce_gram_kernel<float>, dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync, strips,
-                       static_cast<const float*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats,
-                       running_mean, running_var, num_batches, aff, 1.0);
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<float, false>), dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync,
+                       strips, static_cast<const float*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta,
+                       stats, running_mean, running_var, num_batches, aff, 1.0);
   TDS_LAUNCH_CHECK();
   return true;
 }

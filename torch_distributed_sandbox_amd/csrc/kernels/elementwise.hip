@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "launchers.h"
+#include "ups_common.h"
 
 namespace tds {
 
@@ -112,24 +113,17 @@ __global__ void maxpool2_bwd_kernel(const float* __restrict__ gy, const uint8_t*
 // consecutive pixels with one 16-byte store (plain, not non-temporal: the 180 MB
 // image is read again right away by the layer-1 kernels and can stay in the MALL).  The arithmetic order is exactly the
 // per-pixel formula above, so the result is bit-identical to the scalar form.
-constexpr int kUpsMaxW = 256;
-constexpr int kUpsImg = 4096;  // sources up to this many pixels are staged whole (28x28 = 784)
-constexpr int kUpsRows = 8;    // output rows per workgroup when the source is staged whole
+// (kUpsMaxW / kUpsImg / kUpsRows and the per-pixel arithmetic: ups_common.h)
 
 // one output row Y from the two source rows r0 (y0), r1 (y1) in LDS
 template <bool U8OUT>
 __device__ __forceinline__ void ups_row(const float* r0, const float* r1, float ay, void* __restrict__ dstv, int b,
                                         int Y, int w, int H, int W, float sx) {
   auto lvl = [&](int X) {
-    float fx = ((float)X + 0.5f) * sx - 0.5f;
-    fx = fminf(fmaxf(fx, 0.f), (float)(w - 1));
-    const int x0 = (int)fx;
-    const int x1 = min(x0 + 1, w - 1);
-    const float ax = fx - (float)x0;
-    const float top = (1.f - ax) * r0[x0] + ax * r0[x1];
-    const float bot = (1.f - ax) * r1[x0] + ax * r1[x1];
-    const float v = (1.f - ay) * top + ay * bot;
-    return fminf(fmaxf(rintf(v), 0.f), 255.f);
+    int x0, x1;
+    float ax;
+    ups_taps(X, sx, w, x0, x1, ax);
+    return ups_level(ups_lerp(ups_lerp(r0[x0], r0[x1], ax), ups_lerp(r1[x0], r1[x1], ax), ay));
   };
   if constexpr (U8OUT) {
     uint8_t* d8 = reinterpret_cast<uint8_t*>(dstv) + ((int64_t)b * H + Y) * W;
@@ -157,11 +151,7 @@ __device__ __forceinline__ void ups_row(const float* r0, const float* r1, float 
 }
 
 __device__ __forceinline__ void ups_vtaps(int Y, int h, float sy, int& y0, int& y1, float& ay) {
-  float fy = ((float)Y + 0.5f) * sy - 0.5f;
-  fy = fminf(fmaxf(fy, 0.f), (float)(h - 1));
-  y0 = (int)fy;
-  y1 = min(y0 + 1, h - 1);
-  ay = fy - (float)y0;
+  ups_taps(Y, sy, h, y0, y1, ay);
 }
 
 // One workgroup per output row (grid = H x B): the row's two source rows staged in LDS.
@@ -209,13 +199,7 @@ __global__ void __launch_bounds__(256) upsample_bilinear_u8_img_kernel(const uin
     int x0[4], x1[4];
     float ax[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float fx = ((float)(4 * q + k) + 0.5f) * sx - 0.5f;
-      fx = fminf(fmaxf(fx, 0.f), (float)(w - 1));
-      x0[k] = (int)fx;
-      x1[k] = min(x0[k] + 1, w - 1);
-      ax[k] = fx - (float)x0[k];
-    }
+    for (int k = 0; k < 4; ++k) ups_taps(4 * q + k, sx, w, x0[k], x1[k], ax[k]);
     for (int r = 0; r < nr; ++r) {
       int y0, y1;
       float ay;
@@ -224,12 +208,8 @@ __global__ void __launch_bounds__(256) upsample_bilinear_u8_img_kernel(const uin
       const float* r1 = img + y1 * w;
       float lv[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float top = (1.f - ax[k]) * r0[x0[k]] + ax[k] * r0[x1[k]];
-        const float bot = (1.f - ax[k]) * r1[x0[k]] + ax[k] * r1[x1[k]];
-        const float v = (1.f - ay) * top + ay * bot;
-        lv[k] = fminf(fmaxf(rintf(v), 0.f), 255.f);
-      }
+      for (int k = 0; k < 4; ++k)
+        lv[k] = ups_level(ups_lerp(ups_lerp(r0[x0[k]], r0[x1[k]], ax[k]), ups_lerp(r1[x0[k]], r1[x1[k]], ax[k]), ay));
       const int64_t row = (int64_t)b * H + Yb + r;
       if constexpr (U8OUT) {
         reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(dstv) + row * W)[q] =
@@ -250,13 +230,10 @@ __global__ void __launch_bounds__(256) upsample_bilinear_u8_img_kernel(const uin
       const float* r0 = img + y0 * w;
       const float* r1 = img + y1 * w;
       for (int X = W4 * 4 + threadIdx.x; X < W; X += blockDim.x) {
-        float fx = ((float)X + 0.5f) * sx - 0.5f;
-        fx = fminf(fmaxf(fx, 0.f), (float)(w - 1));
-        const int a0 = (int)fx, a1 = min(a0 + 1, w - 1);
-        const float a = fx - (float)a0;
-        const float top = (1.f - a) * r0[a0] + a * r0[a1];
-        const float bot = (1.f - a) * r1[a0] + a * r1[a1];
-        const float v = fminf(fmaxf(rintf((1.f - ay) * top + ay * bot), 0.f), 255.f);
+        int a0, a1;
+        float a;
+        ups_taps(X, sx, w, a0, a1, a);
+        const float v = ups_level(ups_lerp(ups_lerp(r0[a0], r0[a1], a), ups_lerp(r1[a0], r1[a1], a), ay));
         const int64_t o = ((int64_t)b * H + Yb + r) * W + X;
         if constexpr (U8OUT) reinterpret_cast<uint8_t*>(dstv)[o] = (uint8_t)v;
         else reinterpret_cast<float*>(dstv)[o] = v * (1.f / 255.f);

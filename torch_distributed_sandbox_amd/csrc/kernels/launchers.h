@@ -133,8 +133,15 @@ void tds_bn_finalize_shifted(const double* partial, int C, int nchunk, int64_t n
                              float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
 int tds_x_autocorr_num_wg(int B, int H, int W);  // partial rows tds_x_autocorr writes
 void tds_x_moments(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st);
+// border = false: the autocorrelation partials only (the strips then come from tds_l1_reduce_gram's border)
 void tds_x_moments_u8(const uint8_t* x, double* ac_partial, int nwg, double* strips, int B, int H, int W,
-                      hipStream_t st);  // the same moments of uint8 levels (exact)
+                      hipStream_t st, bool border = true);
+// the uint8 levels' border strips alone [B][8][82] (fallback of the in-launch border)
+void tds_x_border_u8(const uint8_t* x, double* strips, int B, int H, int W, hipStream_t st);
+// fused upsample to uint8 levels + autocorrelation partials (ups_moments.hip): partial rows, 0 = unsupported shape
+int tds_ups_moments_rows(int B, int h, int w, int H, int W);
+void tds_ups_moments_u8(const uint8_t* src, uint8_t* x, double* partial, int nrows, int B, int h, int w, int H, int W,
+                        hipStream_t st);  // the same moments of uint8 levels (exact)
 int tds_conv2_bwd_clock_read(uint32_t* host, int n);  // DIAG 13 per-wave barrier clocks (diag builds)
 void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream_t st);  // border strips [B][8][82]
 void tds_reduce_partials(const double* in, double* out, int n, int nchunk, int inner, int64_t ostride, int64_t kstride,
@@ -169,10 +176,12 @@ void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const 
 bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const double* gram, int64_t n,
                             const float* w1, const float* b1, const float* gamma1, const float* stats1, float* dw1,
                             float* db1, float* dgamma1, float* dbeta1, float scale, hipStream_t st);
-bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, const double* strips, const void* x,
+// border: workgroups of the same launch form the uint8 levels' border strips (xmom_u8.h) first
+bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, double* strips, const void* x,
                         bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,
                         float eps, float momentum, const float* gamma, const float* beta, float* stats,
-                        float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st);
+                        float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st,
+                        bool border = false);
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);

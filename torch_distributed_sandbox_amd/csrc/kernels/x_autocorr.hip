@@ -277,11 +277,18 @@ void tds_x_moments(const float* x, double* ac_partial, int nwg, double* strips, 
 
 // the same moments of uint8 levels (x = levels / 255 is scaled in l1_gram), one launch
 void tds_x_moments_u8(const uint8_t* x, double* ac_partial, int nwg, double* strips, int B, int H, int W,
-                      hipStream_t st) {
+                      hipStream_t st, bool border_wgs) {
   if (nwg < 1 || nwg != x_autocorr_num_wg(B, H, W)) {
     tds_launch_fail("x_autocorr_u8: workgroup count does not match the shape (needs W % 4 == 0)");
     return;
   }
-  hipLaunchKernelGGL(x_autocorr_u8_kernel, dim3(nwg + 656 * B), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
+  // (without the border workgroups: 60 vs 76 us for the moments op at the bench shape, r5_s22)
+  hipLaunchKernelGGL(x_autocorr_u8_kernel, dim3(nwg + (border_wgs ? 656 * B : 0)), dim3(256), 0, st, x, ac_partial, B,
+                     H, W, strips, nwg);
+  TDS_LAUNCH_CHECK();
+}
+
+void tds_x_border_u8(const uint8_t* x, double* strips, int B, int H, int W, hipStream_t st) {
+  hipLaunchKernelGGL(x_border_kernel<uint8_t>, dim3(82, 8, B), dim3(256), 0, st, x, strips, B, H, W);
   TDS_LAUNCH_CHECK();
 }

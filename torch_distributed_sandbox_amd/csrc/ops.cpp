@@ -105,6 +105,28 @@ Tensor upsample_bilinear_u8(const Tensor& src, int64_t H, int64_t W, bool levels
   return dst;
 }
 
+// The uint8 level upsample fused with the x autocorrelation partials behind BN1's statistics
+// (ups_moments.hip): returns (levels [B,1,H,W] uint8, partials [rows * 42] fp64) for
+// fused_l1_forward's precomputed-moments argument.  Shapes the fused kernel does not take (W % 4,
+// sources past 4096 pixels) get the plain upsample and an empty partials tensor.
+std::tuple<Tensor, Tensor> upsample_levels_moments(const Tensor& src, int64_t H, int64_t W) {
+  TORCH_CHECK(src.is_cuda() && src.scalar_type() == at::kByte && src.is_contiguous() && src.dim() == 3,
+              "tdsa.upsample_levels_moments: expected contiguous uint8 [B,h,w] on GPU");
+  TORCH_CHECK(H >= 1 && W >= 1 && H <= INT32_MAX && W <= INT32_MAX && src.size(0) <= 65535,
+              "tdsa.upsample_levels_moments: bad output shape");
+  c10::DeviceGuard g(src.device());
+  const int B = (int)src.size(0), h = (int)src.size(1), w = (int)src.size(2);
+  const int rows = tds_ups_moments_rows(B, h, w, (int)H, (int)W);
+  if (rows == 0 || (int64_t)H * W > 0xFFFFFFF0LL)
+    return {upsample_bilinear_u8(src, H, W, true), at::empty({0}, src.options().dtype(at::kDouble))};
+  auto dst = at::empty({B, 1, H, W}, src.options());
+  auto part = at::empty({(int64_t)rows * 42}, src.options().dtype(at::kDouble));
+  tds_ups_moments_u8(src.data_ptr<uint8_t>(), dst.data_ptr<uint8_t>(), part.data_ptr<double>(), rows, B, h, w, (int)H,
+                     (int)W, cur_stream(src));
+  check_launches("upsample_levels_moments");
+  return {dst, part};
+}
+
 void sgd_step_(at::TensorList params, at::TensorList grads, at::TensorList moms, double lr, double wd,
                double momentum, double dampening, bool nesterov, bool first_step) {
   TORCH_CHECK(params.size() == grads.size(), "tdsa.sgd_step_: params/grads length mismatch");
@@ -408,6 +430,7 @@ TORCH_LIBRARY(tdsa, m) {
   m.def("maxpool2_fwd(Tensor x) -> (Tensor, Tensor)", &maxpool2_fwd);
   m.def("maxpool2_bwd(Tensor grad, Tensor idx, int H, int W) -> Tensor", &maxpool2_bwd);
   m.def("upsample_bilinear_u8(Tensor src, int H, int W, bool levels=False) -> Tensor", &upsample_bilinear_u8);
+  m.def("upsample_levels_moments(Tensor src, int H, int W) -> (Tensor, Tensor)", &upsample_levels_moments);
   m.def(
       "sgd_step_(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] moms, float lr, float weight_decay, float momentum, "
       "float dampening, bool nesterov, bool first_step) -> ()",

@@ -85,8 +85,9 @@ def input_stats(x):
 
 
 def attach_input_stats(x, stats):
-    """Hand precomputed ``input_stats(x)`` to the forward that consumes ``x`` (valid until x is
-    modified in place)."""
+    """Hand precomputed ``input_stats(x)`` -- or ``(partials, None)`` from
+    ``ops.functional.upsample_levels_moments`` -- to the forward that consumes ``x`` (valid until x
+    is modified in place)."""
     x._tds_l1_stats = (x._version, stats)
     return x
 
@@ -137,8 +138,9 @@ def _sinks(ctx, params, first):
 
 
 _ZERO = {}
-# counters the tests read: forward passes that applied the exchange's weight update in the head kernel
-STATS = {"head_fused_updates": 0}
+# counters the tests read: forward passes that applied the exchange's weight update in the head kernel,
+# and layer-1 forwards that took x moments precomputed by the input pipeline
+STATS = {"head_fused_updates": 0, "precomputed_input_moments": 0}
 
 
 def _zero_scalar(device, dtype):
@@ -162,6 +164,8 @@ class _Layer1(torch.autograd.Function):
     def forward(ctx, x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps, link1):
         ops = _ext.ops()
         asum, strips = _take_input_stats(x)
+        if asum is not None:
+            STATS["precomputed_input_moments"] += 1
         x = x.contiguous()
         p1, idx1, stats1, gram, p1_scale = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps,
                                                                 asum, strips)

@@ -286,3 +286,15 @@ def upsample_bilinear_u8(src: torch.Tensor, H: int, W: int, levels: bool = False
         y = y.round_().clamp_(0, 255)
         return y.to(torch.uint8) if levels else y.div_(255.0)
     return _ext.ops().upsample_bilinear_u8(src.contiguous(), int(H), int(W), bool(levels))
+
+
+def upsample_levels_moments(src: torch.Tensor, H: int, W: int):
+    """``upsample_bilinear_u8(src, H, W, levels=True)`` that also forms the batch's x
+    autocorrelation partials -- the weight-independent half of BN1's batch statistics in the fused
+    ConvNet plan -- in the same pass over the levels (csrc/kernels/ups_moments.hip).  Returns
+    ``(levels, partials)``; hand both to the model with ``convnet_fused.attach_input_stats(levels,
+    (partials, None))``.  ``partials`` is None on CPU and for shapes the fused kernel does not take."""
+    if not src.is_cuda:
+        return upsample_bilinear_u8(src, H, W, levels=True), None
+    x, part = _ext.ops().upsample_levels_moments(src.contiguous(), int(H), int(W))
+    return x, (part if part.numel() > 0 else None)
