@@ -104,3 +104,19 @@ def test_model_consumes_fused_partials(gpu):
     l2.backward()
     for p1, p2 in zip(m1.parameters(), m2.parameters()):
         assert torch.equal(p1.grad, p2.grad)
+
+
+def test_device_loader_attaches_partials(gpu):
+    """The trainer's loader (levels, moments=True) yields the plain levels with the partials attached."""
+    from torch_distributed_sandbox_amd.data.synthetic import DeviceUpsampleLoader, SyntheticMNIST
+    from torch_distributed_sandbox_amd.models import convnet_fused
+
+    ds = SyntheticMNIST(size=8)
+    plain = DeviceUpsampleLoader(ds, 4, (64, 64), gpu, levels=True)
+    fused = DeviceUpsampleLoader(ds, 4, (64, 64), gpu, levels=True, moments=True)
+    for (xa, ya), (xb, yb) in zip(plain, fused):
+        assert torch.equal(xa, xb) and torch.equal(ya, yb)
+        part, strips = convnet_fused._take_input_stats(xb)
+        assert strips is None and part is not None
+        assert part.numel() % 42 == 0
+        assert torch.equal(part.view(-1, 42).sum(0), _ops().l1_input_stats(xb)[0])

@@ -21,7 +21,7 @@ def main():
                         f"{float(r['AverageNs']) / 1e3:.3f}", f"{float(r['Percentage']):.2f}"])
     trace = list(csv.DictReader(open(base + "kernel_trace.csv")))
     trace.sort(key=lambda r: int(r["Start_Timestamp"]))
-    anchors = [i for i, r in enumerate(trace) if "upsample" in r["Kernel_Name"]]
+    anchors = [i for i, r in enumerate(trace) if "upsample" in r["Kernel_Name"] or "ups_moments" in r["Kernel_Name"]]
     with open(out + ".md", "w") as f:
         f.write(f"# {title}\n\nTotal GPU kernel time: {total / 1e6:.3f} ms over {steps} timed + warmup steps "
                 f"(per-kernel calls include warmup)\n\n")

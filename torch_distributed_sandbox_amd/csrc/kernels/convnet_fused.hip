@@ -892,7 +892,7 @@ struct L1Corners {
 template <typename T>
 __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips_b,
                               const T* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
-                              double* full, double* strips, L1Corners& cx, double xs) {
+                              double* full, double* strips, L1Corners& cx, double xs, int nch) {
   const int tid = threadIdx.x;
 #pragma unroll 4
   for (int e = tid; e < B * 144; e += blockDim.x) {
@@ -900,12 +900,25 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
     const int r = q < 2 ? i : H - 6 + i, c = (q & 1) == 0 ? j : W - 6 + j;
     cx.v[b][q][i][j] = (float)x[(int64_t)b * H * W + (int64_t)r * W + c];
   }
-  // per-image border strips [B][8][82] -> batch sums, images in order
+  // per-image border strips [B][8][nch][82] (nch line chunks, xmom_u8.h; 1 otherwise) -> batch
+  // sums, images then chunks in order
+  // (up to 16 values per sum in flight at once: written by other workgroups of the launch, they
+  // sit behind a cross-XCD round trip each -- as a dependent chain 15 of them cost ~20 us)
+  const int nv = B * nch;
 #pragma unroll 3
   for (int e = tid; e < 8 * 82; e += blockDim.x) {
+    const int L = e / 82, d = e - L * 82;
     double v = 0.0;
-#pragma unroll 8
-    for (int b = 0; b < B; ++b) v += strips_b[(int64_t)b * 8 * 82 + e];
+    for (int j0 = 0; j0 < nv; j0 += 16) {
+      double t[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int j = j0 + k, b = j / nch, ch = j - b * nch;
+        t[k] = j < nv ? strips_b[(((int64_t)b * 8 + L) * nch + ch) * 82 + d] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v += t[k];
+    }
     strips[e] = v;
   }
   if (tid < 81) {
@@ -969,7 +982,7 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
-                                                      float* __restrict__ aff, double xs) {
+                                                      float* __restrict__ aff, double xs, int nch = 1) {
   __shared__ double full[81];
   __shared__ double G[25][25];
   __shared__ double S[25];
@@ -980,7 +993,7 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
   // w1 staged once (its loads issued with the Gram's): the contractions below read it 50 times
   // per thread, which as global loads ran one latency each (r5: l1_gram 20 us)
   for (int e = threadIdx.x; e < 16 * 25; e += blockDim.x) w1s[e] = w1[e];
-  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, cx, xs);
+  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, cx, xs, nch);
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {
@@ -1065,9 +1078,13 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
   __shared__ double sh[8];
   __shared__ int last;
   const int e = blockIdx.x;
+  const int nch = BORDER ? xmom_border_chunks(H, W) : 1;
   if constexpr (BORDER) {
     __shared__ uint32_t lines[BSIDE_LDS_WORDS];
-    if (e >= 42) x_border_side_u8(x, strips, (e - 42) >> 2, (e - 42) & 3, H, W, lines);
+    if (e >= 42) {
+      const int j = e - 42;
+      x_border_side_u8(x, strips, j / (4 * nch), (j / nch) & 3, j % nch, nch, H, W, lines);
+    }
   }
   if (e < 42) {
     double s = 0.0;
@@ -1078,7 +1095,7 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
   }
   if (!tds_arrive(sync, gridDim.x, &last)) return;
   l1_gram_body<T>(ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean,
-                  running_var, num_batches, aff, xs);
+                  running_var, num_batches, aff, xs, nch);
 }
 
 // Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
@@ -1323,7 +1340,10 @@ bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const
 }
 
 // the x autocorrelation partials' reduction [nchunk][42] -> ac_sum + tds_l1_gram in one launch
-// border: the strips are formed in this launch (uint8 levels only, lines <= XMOM_MAX_LINE long)
+int tds_xmom_border_chunks(int H, int W) { return xmom_border_chunks(H, W); }
+
+// border: the strips are formed in this launch (uint8 levels only, lines <= XMOM_MAX_LINE long) into
+// strips [B][8][tds_xmom_border_chunks][82]
 bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, double* strips, const void* x,
                         bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,
                         float eps, float momentum, const float* gamma, const float* beta, float* stats,
@@ -1340,7 +1360,8 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
   uint32_t* sync = tds_sync_words(kSyncL1Gram, st);
   if (sync == nullptr) return false;
   if (levels && border)
-    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + 4 * B), dim3(256), 0, st, ac_part, nchunk,
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + 4 * B * xmom_border_chunks(H, W)), dim3(256),
+                       0, st, ac_part, nchunk,
                        ac_sum, sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum,
                        gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
   else if (levels)

@@ -176,6 +176,8 @@ void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const 
 bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const double* gram, int64_t n,
                             const float* w1, const float* b1, const float* gamma1, const float* stats1, float* dw1,
                             float* db1, float* dgamma1, float* dbeta1, float scale, hipStream_t st);
+// line chunks of the in-launch border strips: tds_l1_reduce_gram(border) writes strips [B][8][chunks][82]
+int tds_xmom_border_chunks(int H, int W);
 // border: workgroups of the same launch form the uint8 levels' border strips (xmom_u8.h) first
 bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, double* strips, const void* x,
                         bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,

@@ -54,6 +54,19 @@ __device__ __forceinline__ uint32_t um_shl1(uint32_t v) {  // lane l <- lane l +
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
 }
 
+// wave sum of a u32: quad / half-row / row steps as DPP adds, the two cross-row steps as swizzles
+__device__ __forceinline__ uint32_t um_wave_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+typedef float um_f2 __attribute__((ext_vector_type(2)));
+
 __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __restrict__ src,
                                                             uint8_t* __restrict__ x, double* __restrict__ partial,
                                                             int h, int w, int H, int W, int nqg, int qpw) {
@@ -61,7 +74,27 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
   const int b = blockIdx.y, unit = blockIdx.x, units = gridDim.x;
   const int lane = threadIdx.x;
   const uint8_t* s = src + (int64_t)b * h * w;
-  for (int i = lane; i < h * w; i += 64) img[i] = (float)s[i];
+  if (((h * w) & 3) == 0) {  // the source in words, every load issued before the first conversion
+    const uint32_t* s4 = reinterpret_cast<const uint32_t*>(s);
+    const int n4 = (h * w) >> 2;
+    for (int i0 = 0; i0 < n4; i0 += 4 * 64) {
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = i0 + k * 64 + lane < n4 ? s4[i0 + k * 64 + lane] : 0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = i0 + k * 64 + lane;
+        if (i < n4) {
+          img[4 * i] = (float)(v[k] & 0xFF);
+          img[4 * i + 1] = (float)((v[k] >> 8) & 0xFF);
+          img[4 * i + 2] = (float)((v[k] >> 16) & 0xFF);
+          img[4 * i + 3] = (float)(v[k] >> 24);
+        }
+      }
+    }
+  } else {
+    for (int i = lane; i < h * w; i += 64) img[i] = (float)s[i];
+  }
   __syncthreads();
   const int qg = unit % nqg, band = unit / nqg;
   const int q = qg * qpw + lane - 1;
@@ -72,7 +105,7 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
   float ax[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) ups_taps(vq ? 4 * q + k : 0, sx, w, x0[k], x1[k], ax[k]);
-  float top[4], bot[4];
+  um_f2 top[2], bot[2];  // pixels 0,1 | 2,3
   int ycur = -1;
   uint32_t acc[42];
 #pragma unroll
@@ -95,14 +128,22 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
             ycur = y0;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-              top[k] = ups_lerp(img[y0 * w + x0[k]], img[y0 * w + x1[k]], ax[k]);
-              bot[k] = ups_lerp(img[y1 * w + x0[k]], img[y1 * w + x1[k]], ax[k]);
+              top[k >> 1][k & 1] = ups_lerp(img[y0 * w + x0[k]], img[y0 * w + x1[k]], ax[k]);
+              bot[k >> 1][k & 1] = ups_lerp(img[y1 * w + x0[k]], img[y1 * w + x1[k]], ax[k]);
             }
           }
-          uint32_t lv[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) lv[k] = (uint32_t)ups_level(ups_lerp(top[k], bot[k], ay));
-          cur = vq ? (lv[0] | (lv[1] << 8) | (lv[2] << 16) | (lv[3] << 24)) : 0u;
+          // ups_level(ups_lerp(top, bot, ay)) two pixels per packed op: the lerp is ups_lerp's
+          // fmaf(ay, bot, (1 - ay) * top) elementwise, and a convex combination of levels lies in
+          // [0, 255 + 2^-15], so adding 1.5 * 2^23 rounds it to the nearest integer (ties to even, as
+          // rintf) into the low mantissa byte and the clamp never binds: the same level
+          const um_f2 ay2 = {ay, ay}, na2 = {1.f - ay, 1.f - ay}, mag = {12582912.f, 12582912.f};
+          const um_f2 m01 = __builtin_elementwise_fma(ay2, bot[0], na2 * top[0]) + mag;
+          const um_f2 m23 = __builtin_elementwise_fma(ay2, bot[1], na2 * top[1]) + mag;
+          // (__float_as_uint of the element VALUE: clang's __builtin_bit_cast of an ext-vector element
+          // lvalue read element 0 for every index)
+          const uint32_t l0 = __float_as_uint(m01.x) & 0xFFu, l1 = __float_as_uint(m01.y) & 0xFFu;
+          const uint32_t l2 = __float_as_uint(m23.x) & 0xFFu, l3 = __float_as_uint(m23.y) & 0xFFu;
+          cur = vq ? (l0 | (l1 << 8) | (l2 << 16) | (l3 << 24)) : 0u;
           if (own && i < UM_RB) xrow[(int64_t)i * (W >> 2)] = cur;
         }
         const uint32_t left = um_shr1(cur), right = um_shl1(cur);
@@ -127,7 +168,7 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
   double out = 0.0;
 #pragma unroll
   for (int k = 0; k < 42; ++k) {
-    const uint32_t v = wave_sum(acc[k]);
+    const uint32_t v = um_wave_sum(acc[k]);
     if (lane == k) out = (double)v;
   }
   if (lane < 42) partial[((int64_t)b * units + unit) * 42 + lane] = out;

@@ -18,16 +18,22 @@ constexpr int BSIDE_LD = BSIDE_CH / 4 + 2;    // words per stored line: one pad 
 constexpr int BSIDE_LDS_WORDS = 6 * BSIDE_LD;
 constexpr int XMOM_MAX_LINE = 66051;          // longest line whose u32 sums cannot wrap
 
+// line chunks per side: one workgroup each (all in flight together), partial sums per chunk
+__host__ __device__ inline int xmom_border_chunks(int H, int W) {
+  return ((H > W ? H : W) + BSIDE_CH - 1) / BSIDE_CH;
+}
+
 // bytes s .. s+3 of the 12 bytes (w0 | w1 | w2), s in 0..8
 __device__ __forceinline__ uint32_t xm_win(uint32_t w0, uint32_t w1, uint32_t w2, int s) {
   return s == 0 ? w0 : s < 4 ? __builtin_amdgcn_alignbyte(w1, w0, s) : s == 4 ? w1
        : s < 8 ? __builtin_amdgcn_alignbyte(w2, w1, s - 4) : w2;
 }
 
-// side 0 top, 1 bottom, 2 left, 3 right of image b; lines: BSIDE_LDS_WORDS words of LDS.  Every
+// Chunk ch (of nch) of side 0 top, 1 bottom, 2 left, 3 right of image b -> strips[b][L][ch][82]
+// (its partial sums; chunks past the line write zeros); lines: BSIDE_LDS_WORDS words of LDS.  Every
 // thread of the workgroup must call it.  Results stored write-through (st_agent) for the reducer.
 __device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, double* __restrict__ strips, int b,
-                                                 int side, int H, int W, uint32_t* lines) {
+                                                 int side, int ch, int nch, int H, int W, uint32_t* lines) {
   const bool rows = side < 2;
   const int N = rows ? W : H;                                  // positions along a line
   const int first = (side & 1) ? (rows ? H - 6 : W - 6) : 0;   // image row / col of stored line 0
@@ -42,7 +48,8 @@ __device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, 
 #pragma unroll
     for (int s = 0; s < 9; ++s) acc[m][s] = 0u;
   uint32_t plain = 0u;
-  for (int c0 = 0; c0 < N; c0 += BSIDE_CH) {
+  {
+    const int c0 = ch * BSIDE_CH;
     if (rows) {
       // word k of stored line t = image row first + t, positions c0 - 4 + 4k .. +3 (W % 4 == 0:
       // a word lies inside the row or outside it whole); all loads issued before the LDS writes
@@ -107,13 +114,13 @@ __device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, 
     }
     __syncthreads();
   }
-  // (positions past N are zeros in LDS: the last chunk's tail adds nothing)
+  // (positions past N are zeros in LDS: a chunk's tail past the line adds nothing)
 #pragma unroll
   for (int m = 0; m < 5; ++m) {
     const int pr = 4 * m + wv;
     if (pr < 18) {
       const int tl = pr / 9, dd = pr % 9 - 4;
-      double* out = strips + ((int64_t)b * 8 + 2 * side + tl) * 82;
+      double* out = strips + (((int64_t)b * 8 + 2 * side + tl) * nch + ch) * 82;
 #pragma unroll
       for (int s = 0; s < 9; ++s) {
         const uint32_t v = wave_sum(acc[m][s]);
@@ -123,7 +130,7 @@ __device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, 
   }
   if (wv < 2) {
     const uint32_t v = wave_sum(plain);
-    if (lane == 0) st_agent(strips + ((int64_t)b * 8 + 2 * side + wv) * 82 + 81, (double)v);
+    if (lane == 0) st_agent(strips + (((int64_t)b * 8 + 2 * side + wv) * nch + ch) * 82 + 81, (double)v);
   }
 }
 

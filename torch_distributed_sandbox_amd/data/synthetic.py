@@ -95,8 +95,12 @@ class DeviceUpsampleLoader:
     CPU batches are gathered per step as the reference's DataLoader does."""
 
     def __init__(self, dataset: SyntheticMNIST, batch_size: int, image_shape, device, sampler=None,
-                 shuffle: bool = False, seed: int = 0, drop_last: bool = False, levels: bool = False):
+                 shuffle: bool = False, seed: int = 0, drop_last: bool = False, levels: bool = False,
+                 moments: bool = False):
         self.levels = levels
+        # levels on the GPU: the upsample also forms the batch's x autocorrelation partials and
+        # attaches them for the fused ConvNet plan's BN1 statistics (ops.functional.upsample_levels_moments)
+        self.moments = moments and levels
         self.dataset, self.batch_size = dataset, batch_size
         self.H, self.W = image_shape
         self.device = torch.device(device)
@@ -142,6 +146,14 @@ class DeviceUpsampleLoader:
                 e = min(len(idx), s + self.batch_size)
                 if self.drop_last and e - s < self.batch_size:
                     break
+                if self.moments:
+                    from ..models import convnet_fused
+
+                    x, part = TF.upsample_levels_moments(ep_src[s:e], self.H, self.W)
+                    if part is not None:
+                        convnet_fused.attach_input_stats(x, (part, None))
+                    yield x, ep_lab[s:e]
+                    continue
                 yield TF.upsample_bilinear_u8(ep_src[s:e], self.H, self.W, levels=self.levels), ep_lab[s:e]
             return
         for s in range(0, len(idx), self.batch_size):

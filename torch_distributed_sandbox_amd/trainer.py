@@ -116,11 +116,14 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
         _, start_epoch, _ = checkpoint.load(args.resume, model, optimizer, map_location=device)
     dataset = SyntheticMNIST(size=args.dataset_size)
     levels = getattr(args, "input", "levels") == "levels"
+    moments = levels and getattr(args, "mode", "auto") != "layers"  # the fused plan reads them
     if distributed:
         sampler = DistributedSampler(len(dataset), num_replicas=world, rank=rank)
-        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, sampler=sampler, levels=levels)
+        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, sampler=sampler, levels=levels,
+                                      moments=moments)
     else:
-        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, shuffle=True, levels=levels)
+        loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, shuffle=True, levels=levels,
+                                      moments=moments)
 
     start = datetime.now()
     total_step = len(loader)
