@@ -892,14 +892,8 @@ struct L1Corners {
 template <typename T>
 __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips_b,
                               const T* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
-                              double* full, double* strips, L1Corners& cx, double xs, int nch) {
+                              double* full, double* strips, const L1Corners& cx, double xs, int nch) {
   const int tid = threadIdx.x;
-#pragma unroll 4
-  for (int e = tid; e < B * 144; e += blockDim.x) {
-    const int b = e / 144, q = (e / 36) % 4, i = (e / 6) % 6, j = e % 6;
-    const int r = q < 2 ? i : H - 6 + i, c = (q & 1) == 0 ? j : W - 6 + j;
-    cx.v[b][q][i][j] = (float)x[(int64_t)b * H * W + (int64_t)r * W + c];
-  }
   // per-image border strips [B][8][nch][82] (nch line chunks, xmom_u8.h; 1 otherwise) -> batch
   // sums, images then chunks in order
   // (up to 16 values per sum in flight at once: written by other workgroups of the launch, they
@@ -968,18 +962,50 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
   __syncthreads();
 }
 
+// What the Gram body reads besides the sums, staged in LDS by EVERY workgroup of its launch at the
+// start (l1_gram_stage): the reducing workgroup only learns it is last after the column sums, and
+// these loads issued then were rounds of global latency on the step's critical path (w1, the BN1
+// parameters and running statistics, the image corners).
+struct L1GramPre {
+  float w1s[16 * 25];
+  float prm[5][16];  // b1, gamma (1 if absent), beta (0), running mean, running var (0 if absent)
+  L1Corners cx;
+};
+
+template <typename T>
+__device__ __forceinline__ void l1_gram_stage(L1GramPre& pre, const T* __restrict__ x, int B, int H, int W,
+                                              const float* __restrict__ w1, const float* __restrict__ b1,
+                                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                                              const float* __restrict__ running_mean,
+                                              const float* __restrict__ running_var) {
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 16 * 25; e += blockDim.x) pre.w1s[e] = w1[e];
+  if (tid < 80) {
+    const int k = tid >> 4, c = tid & 15;
+    const float* p = k == 0 ? b1 : k == 1 ? gamma : k == 2 ? beta : k == 3 ? running_mean : running_var;
+    pre.prm[k][c] = p ? p[c] : (k == 1 ? 1.f : 0.f);
+  }
+  // corner blocks: x only inside the 6 x 6 pixel block at each image corner
+#pragma unroll 4
+  for (int e = tid; e < B * 144; e += blockDim.x) {
+    const int b = e / 144, q = (e / 36) % 4, i = (e / 6) % 6, j = e % 6;
+    const int r = q < 2 ? i : H - 6 + i, c = (q & 1) == 0 ? j : W - 6 + j;
+    pre.cx.v[b][q][i][j] = (float)x[(int64_t)b * H * W + (int64_t)r * W + c];
+  }
+}
+
 // Forward: Gram + patch sums (kept for the backward) and the BN1 statistics they
 // imply, so conv1 never runs a separate statistics pass:
 //   sum_px (y1 - b1)[c]   = w1[c] . S
 //   sum_px (y1 - b1)^2[c] = w1[c]^T G w1[c]
 // gram = G[625] | S[25] (fp64); sums = [c][sum, sumsq] in the bn_finalize_shifted layout.
+// pre: l1_gram_stage's LDS (staged and synchronized by the caller).
 template <typename T>
 __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
                                                       const double* __restrict__ strips, const T* __restrict__ x,
-                                                      int B, int H, int W, const float* __restrict__ w1,
+                                                      int B, int H, int W, const L1GramPre& pre,
                                                       double* __restrict__ gram, double* __restrict__ sums,
-                                                      const float* __restrict__ b1, float eps, float momentum,
-                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      float eps, float momentum,
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
                                                       float* __restrict__ aff, double xs, int nch = 1) {
@@ -988,12 +1014,8 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
   __shared__ double S[25];
   __shared__ double Gw[16][25];
   __shared__ double strips_sum[8 * 82];
-  __shared__ L1Corners cx;
-  __shared__ float w1s[16 * 25];
-  // w1 staged once (its loads issued with the Gram's): the contractions below read it 50 times
-  // per thread, which as global loads ran one latency each (r5: l1_gram 20 us)
-  for (int e = threadIdx.x; e < 16 * 25; e += blockDim.x) w1s[e] = w1[e];
-  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, cx, xs, nch);
+  const float* w1s = pre.w1s;
+  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, pre.cx, xs, nch);
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {
@@ -1013,7 +1035,7 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
   if (tid < 64) {
     const int c = tid & 15;
     const double sq = sqrt((double)((int64_t)B * H * W - 1));
-    double bound = tid < 16 ? fabs(gamma ? (double)gamma[c] : 1.0) * sq + fabs(beta ? (double)beta[c] : 0.0) : 0.0;
+    double bound = tid < 16 ? fabs((double)pre.prm[1][c]) * sq + fabs((double)pre.prm[2][c]) : 0.0;
     for (int off = 32; off > 0; off >>= 1) bound = fmax(bound, __shfl_xor(bound, off, 64));
     bound *= 1.0 + 1.0 / 1024.0;
     int e1 = 0;
@@ -1036,8 +1058,23 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
     sums[tid * 2 + 1] = q;
     // BN1 statistics of (y1 - b1) finalized here (no separate finalize launch)
     if (tid == 0 && num_batches) num_batches[0] += 1;
-    bn_finalize_channel(tid, 16, s, q, (int64_t)B * H * W, b1, eps, momentum, gamma, beta, stats, running_mean,
-                        running_var, aff, p1_scale);
+    // bn_finalize_channel (bn_finalize.h) on the staged parameters
+    const int64_t n = (int64_t)B * H * W;
+    const double m0 = s / (double)n;
+    double var = q / (double)n - m0 * m0;
+    if (var < 0.0) var = 0.0;
+    const double mean = m0 + (double)pre.prm[0][tid];
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    stats[tid] = (float)mean;
+    stats[16 + tid] = invstd;
+    if (running_mean) {
+      const double unb = n > 1 ? var * (double)n / (double)(n - 1) : var;
+      running_mean[tid] = (float)((1.0 - momentum) * pre.prm[3][tid] + momentum * mean);
+      running_var[tid] = (float)((1.0 - momentum) * pre.prm[4][tid] + momentum * unb);
+    }
+    const float gm = pre.prm[1][tid], bt = pre.prm[2][tid];
+    aff[tid] = gm * invstd * p1_scale;
+    aff[16 + tid] = (bt - (float)mean * gm * invstd) * p1_scale;
   }
 }
 
@@ -1052,8 +1089,11 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
                                                       float* __restrict__ aff, double xs) {
-  l1_gram_body<T>(ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean,
-                  running_var, num_batches, aff, xs);
+  __shared__ L1GramPre pre;
+  l1_gram_stage(pre, x, B, H, W, w1, b1, gamma, beta, running_mean, running_var);
+  __syncthreads();
+  l1_gram_body<T>(ac_sum, strips, x, B, H, W, pre, gram, sums, eps, momentum, stats, running_mean, running_var,
+                  num_batches, aff, xs);
 }
 
 // The x autocorrelation partials' reduction and the Gram in ONE launch: workgroup e sums column
@@ -1077,8 +1117,10 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
                                                              double xs) {
   __shared__ double sh[8];
   __shared__ int last;
+  __shared__ L1GramPre pre;
   const int e = blockIdx.x;
   const int nch = BORDER ? xmom_border_chunks(H, W) : 1;
+  l1_gram_stage(pre, x, B, H, W, w1, b1, gamma, beta, running_mean, running_var);  // (synchronized by tds_arrive)
   if constexpr (BORDER) {
     __shared__ uint32_t lines[BSIDE_LDS_WORDS];
     if (e >= 42) {
@@ -1088,14 +1130,14 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
   }
   if (e < 42) {
     double s = 0.0;
-#pragma unroll 8
+#pragma unroll 16
     for (int k = threadIdx.x; k < nchunk; k += blockDim.x) s += ac_part[e + (int64_t)k * 42];
     s = block_sum(s, sh);
     if (threadIdx.x == 0) st_agent(ac_sum + e, s);
   }
   if (!tds_arrive(sync, gridDim.x, &last)) return;
-  l1_gram_body<T>(ac_sum, strips, x, B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean,
-                  running_var, num_batches, aff, xs, nch);
+  l1_gram_body<T>(ac_sum, strips, x, B, H, W, pre, gram, sums, eps, momentum, stats, running_mean, running_var,
+                  num_batches, aff, xs, nch);
 }
 
 // Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
