@@ -894,34 +894,77 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
                               const T* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
                               double* full, double* strips, const L1Corners& cx, double xs, int nch) {
   const int tid = threadIdx.x;
+  // the autocorrelation sum this thread places in full[] (load issued with the strips' below)
+  double fa = 0.0;
+  if (tid < 81) {
+    const int dy = tid / 9 - 4, dx = tid % 9 - 4;
+    int sy = dy, sx = dx;
+    if (dy < 0 || (dy == 0 && dx < 0)) { sy = -dy; sx = -dx; }
+    fa = ac_sum[sy == 0 ? sx : 5 + (sy - 1) * 9 + (sx + 4)];
+  } else if (tid == 81) {
+    fa = ac_sum[41];  // the plain sum (full[81])
+  }
   // per-image border strips [B][8][nch][82] (nch line chunks, xmom_u8.h; 1 otherwise) -> batch
   // sums, images then chunks in order
   // (up to 16 values per sum in flight at once: written by other workgroups of the launch, they
   // sit behind a cross-XCD round trip each -- as a dependent chain 15 of them cost ~20 us)
   const int nv = B * nch;
-#pragma unroll 3
-  for (int e = tid; e < 8 * 82; e += blockDim.x) {
-    const int L = e / 82, d = e - L * 82;
-    double v = 0.0;
-    for (int j0 = 0; j0 < nv; j0 += 16) {
-      double t[16];
+  static_assert(8 * 82 <= 3 * 256, "three strip sums per thread");
+  {
+    // every thread's (up to) 3 x 16 loads issued before the first add (r5_s29b: 5.4 us for this
+    // phase with the loads issued per sum)
+    double t[3][16];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + 256 * u, L = e / 82, d = e - L * 82;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int j = j0 + k, b = j / nch, ch = j - b * nch;
-        t[k] = j < nv ? strips_b[(((int64_t)b * 8 + L) * nch + ch) * 82 + d] : 0.0;
+        const int b = k / nch, ch = k - b * nch;
+        t[u][k] = (e < 8 * 82 && k < nv) ? strips_b[(((int64_t)b * 8 + L) * nch + ch) * 82 + d] : 0.0;
       }
-#pragma unroll
-      for (int k = 0; k < 16; ++k) v += t[k];
     }
-    strips[e] = v;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      const int e = tid + 256 * u, L = e / 82, d = e - L * 82;
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v += t[u][k];
+      for (int j = 16; j < nv; ++j) {  // (more than 16 image-chunks: the rest one by one)
+        const int b = j / nch, ch = j - b * nch;
+        v += strips_b[(((int64_t)b * 8 + L) * nch + ch) * 82 + d];
+      }
+      if (e < 8 * 82) strips[e] = v;
+    }
   }
-  if (tid < 81) {
-    const int dy = tid / 9 - 4, dx = tid % 9 - 4;
-    int sy = dy, sx = dx;
-    if (dy < 0 || (dy == 0 && dx < 0)) { sy = -dy; sx = -dx; }
-    full[tid] = ac_sum[sy == 0 ? sx : 5 + (sy - 1) * 9 + (sx + 4)];
+  if (tid < 82) full[tid] = fa;
+  // corner products, all (corner row, corner col, offset) at once: cp[ri][ci][d] = sum_b x(b, r, c)
+  // x(b, r + dy, c + dx) for r in rows 0, 1, H-2, H-1 (ri 0..3), c likewise, the partner inside
+  // the image; cs[ri][ci] = sum_b x(b, r, c).  (Summed per Gram entry inside its loops, the
+  // B-long LDS chains cost 8 us of the one-workgroup body, r5_s29b.)
+  __shared__ double cp[16][81];
+  __shared__ double cs[16];
+  for (int e = tid; e < 16 * 81 + 16; e += blockDim.x) {
+    const bool sum = e >= 16 * 81;
+    const int rc = sum ? e - 16 * 81 : e / 81, d = sum ? 40 : e - rc * 81;
+    const int ri = rc >> 2, ci = rc & 3;
+    const int r = ri < 2 ? ri : H - 4 + ri, c = ci < 2 ? ci : W - 4 + ci;
+    const int r2 = r + d / 9 - 4, c2 = c + d % 9 - 4;
+    double v = 0.0;
+    if (sum) {
+#pragma unroll 8
+      for (int b = 0; b < B; ++b) v += cx.at(b, r, c, H, W);
+      cs[rc] = v;
+    } else {
+      if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W)
+#pragma unroll 8
+        for (int b = 0; b < B; ++b) v += (double)cx.at(b, r, c, H, W) * cx.at(b, r2, c2, H, W);
+      cp[rc][d] = v;
+    }
   }
   __syncthreads();
+#if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 4  // (A/B timing: the loads phase only)
+  return;
+#endif
   for (int e = tid; e < 625 + 25; e += blockDim.x) {
     const bool isS = e >= 625;
     const int k = isS ? e - 625 : e / 25, j = isS ? e - 625 : e % 25;
@@ -943,19 +986,14 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
       for (int i = 0; i < ne; ++i) v -= strips[line_index_row(er[i]) * 82 + di];
       for (int i = 0; i < nc; ++i) v -= strips[line_index_col(ec[i]) * 82 + di];
       for (int i = 0; i < ne; ++i)
-        for (int q = 0; q < nc; ++q) {
-          const int r = er[i], cc = ec[q], r2 = r + dy, c2 = cc + dx;
-          if (r2 < 0 || r2 >= H || c2 < 0 || c2 >= W) continue;
-          for (int b = 0; b < B; ++b) v += (double)cx.at(b, r, cc, H, W) * cx.at(b, r2, c2, H, W);
-        }
+        for (int q = 0; q < nc; ++q) v += cp[line_index_row(er[i]) * 4 + (line_index_col(ec[q]) - 4)][di];
       G[k][j] = v * (xs * xs);
     } else {
-      v = ac_sum[41];
+      v = full[81];
       for (int i = 0; i < ne; ++i) v -= strips[line_index_row(er[i]) * 82 + 81];
       for (int i = 0; i < nc; ++i) v -= strips[line_index_col(ec[i]) * 82 + 81];
       for (int i = 0; i < ne; ++i)
-        for (int q = 0; q < nc; ++q)
-          for (int b = 0; b < B; ++b) v += cx.at(b, er[i], ec[q], H, W);
+        for (int q = 0; q < nc; ++q) v += cs[line_index_row(er[i]) * 4 + (line_index_col(ec[q]) - 4)];
       S[j] = v * xs;
     }
   }
@@ -1009,13 +1047,16 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
                                                       float* __restrict__ aff, double xs, int nch = 1) {
-  __shared__ double full[81];
+  __shared__ double full[82];  // autocorrelation at the 81 offsets | the plain sum
   __shared__ double G[25][25];
   __shared__ double S[25];
   __shared__ double Gw[16][25];
   __shared__ double strips_sum[8 * 82];
   const float* w1s = pre.w1s;
   l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, pre.cx, xs, nch);
+#if defined(TDS_L1G_DIAG) && (TDS_L1G_DIAG == 3 || TDS_L1G_DIAG == 4)  // (A/B timing: the Gram build only)
+  return;
+#endif
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {
@@ -1120,7 +1161,6 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
   __shared__ L1GramPre pre;
   const int e = blockIdx.x;
   const int nch = BORDER ? xmom_border_chunks(H, W) : 1;
-  l1_gram_stage(pre, x, B, H, W, w1, b1, gamma, beta, running_mean, running_var);  // (synchronized by tds_arrive)
   if constexpr (BORDER) {
     __shared__ uint32_t lines[BSIDE_LDS_WORDS];
     if (e >= 42) {
@@ -1135,7 +1175,12 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
     s = block_sum(s, sh);
     if (threadIdx.x == 0) st_agent(ac_sum + e, s);
   }
+  // (after the workgroup's own loads: issued first, the stage's loads put a round trip before them)
+  l1_gram_stage(pre, x, B, H, W, w1, b1, gamma, beta, running_mean, running_var);  // (synchronized by tds_arrive)
   if (!tds_arrive(sync, gridDim.x, &last)) return;
+#if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 1  // (A/B timing builds only: the reducer without its Gram body)
+  return;
+#endif
   l1_gram_body<T>(ac_sum, strips, x, B, H, W, pre, gram, sums, eps, momentum, stats, running_mean, running_var,
                   num_batches, aff, xs, nch);
 }
@@ -1402,7 +1447,11 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
   uint32_t* sync = tds_sync_words(kSyncL1Gram, st);
   if (sync == nullptr) return false;
   if (levels && border)
+#if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 2  // (A/B timing builds only: no border workgroups)
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42), dim3(256),
+#else
     hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + 4 * B * xmom_border_chunks(H, W)), dim3(256),
+#endif
                        0, st, ac_part, nchunk,
                        ac_sum, sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum,
                        gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);

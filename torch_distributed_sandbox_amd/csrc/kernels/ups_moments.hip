@@ -54,17 +54,6 @@ __device__ __forceinline__ uint32_t um_shl1(uint32_t v) {  // lane l <- lane l +
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
 }
 
-// wave sum of a u32: quad / half-row / row steps as DPP adds, the two cross-row steps as swizzles
-__device__ __forceinline__ uint32_t um_wave_sum(uint32_t v) {
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
-}
-
 typedef float um_f2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __restrict__ src,
@@ -168,7 +157,7 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
   double out = 0.0;
 #pragma unroll
   for (int k = 0; k < 42; ++k) {
-    const uint32_t v = um_wave_sum(acc[k]);
+    const uint32_t v = xm_wave_sum(acc[k]);
     if (lane == k) out = (double)v;
   }
   if (lane < 42) partial[((int64_t)b * units + unit) * 42 + lane] = out;

@@ -23,6 +23,17 @@ __host__ __device__ inline int xmom_border_chunks(int H, int W) {
   return ((H > W ? H : W) + BSIDE_CH - 1) / BSIDE_CH;
 }
 
+// wave sum of a u32: quad / half-row / row steps as DPP adds, the two cross-row steps as swizzles
+__device__ __forceinline__ uint32_t xm_wave_sum(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
 // bytes s .. s+3 of the 12 bytes (w0 | w1 | w2), s in 0..8
 __device__ __forceinline__ uint32_t xm_win(uint32_t w0, uint32_t w1, uint32_t w2, int s) {
   return s == 0 ? w0 : s < 4 ? __builtin_amdgcn_alignbyte(w1, w0, s) : s == 4 ? w1
@@ -123,13 +134,13 @@ __device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, 
       double* out = strips + (((int64_t)b * 8 + 2 * side + tl) * nch + ch) * 82;
 #pragma unroll
       for (int s = 0; s < 9; ++s) {
-        const uint32_t v = wave_sum(acc[m][s]);
+        const uint32_t v = xm_wave_sum(acc[m][s]);
         if (lane == 0) st_agent(out + (rows ? (dd + 4) * 9 + s : s * 9 + (dd + 4)), (double)v);
       }
     }
   }
   if (wv < 2) {
-    const uint32_t v = wave_sum(plain);
+    const uint32_t v = xm_wave_sum(plain);
     if (lane == 0) st_agent(strips + (((int64_t)b * 8 + 2 * side + wv) * nch + ch) * 82 + 81, (double)v);
   }
 }
