@@ -126,6 +126,9 @@ def _parser():
                     help="levels input, fused plan: the upsample kernel also forms the batch's x autocorrelation "
                          "partials behind BN1's statistics (ops.functional.upsample_levels_moments); off: the "
                          "layer-1 forward forms them from the written image")
+    ap.add_argument("--fused-ce", action=argparse.BooleanOptionalAction, default=True,
+                    help="fused plan: the batch's labels go with it, and the head forward's finalizing workgroup "
+                         "forms the cross-entropy loss and dlogits with the logits (no separate CE launch)")
     ap.add_argument("--prefetch", action=argparse.BooleanOptionalAction, default=False,
                     help="produce the next batch (upsample + BN1 input moments) on a side stream beside the "
                          "current step's head kernels (--prefetch-at)")
@@ -601,6 +604,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     with_stats = data_stream is not None and args.mode != "layers"
 
     fused_moments = on_gpu and args.fused_input_moments and args.input == "levels" and args.mode != "layers"
+    fused_ce = on_gpu and args.fused_ce and args.mode != "layers"
 
     def produce(i):
         if fused_moments:
@@ -650,6 +654,10 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             hook = (convnet_fused.before_head_forward if args.prefetch_at == "head"
                     else convnet_fused.before_conv2_backward)
             hook(lambda: prefetch(i + 1))
+        labels = lab_pool[j]
+        if fused_ce:
+            # the loss and dlogits formed by the head forward's finalizing workgroup with the logits
+            convnet_fused.attach_labels(images, labels)
         out = ddp(images)
         if sim_stream is not None:
             sim_stream.wait_stream(torch.cuda.current_stream(device))
@@ -659,7 +667,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             sdma[0].wait_stream(torch.cuda.current_stream(device))
             with torch.cuda.stream(sdma[0]):
                 tds._ext.ops().copy_engine(sdma[1], sdma[2], args.sim_sdma_engine == "nocu")
-        loss = criterion(out, lab_pool[j])
+        loss = criterion(out, labels)
         optimizer.zero_grad()
         TF.backward(loss)
         optimizer.step()
@@ -735,6 +743,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             # where the batch's x moments (BN1's weight-independent half) are formed: in the upsample's pass
             # over the levels, by the prefetch stream's own kernel, or in the layer-1 forward
             "input_moments": ("upsample" if fused_moments else "prefetch" if with_stats else "layer1_forward"),
+            "loss_in_head": fused_ce,
             "prefetch_at": args.prefetch_at if data_stream is not None else None,
             "input": ("uint8 levels (ToTensor's 1/255 folded into conv1)" if args.input == "levels"
                       else "fp32 image"),

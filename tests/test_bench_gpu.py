@@ -27,7 +27,7 @@ def test_bench_one_gpu_small(gpu, prefetch):
                 "--prefetch" if prefetch else "--no-prefetch"])
     assert r["n_gpus"] == 1 and r["config"]["fc_grad"] == "local" and r["value"] > 0
     assert r["config"]["prefetch"] is prefetch
-    assert r["config"]["input_moments"] == "upsample"
+    assert r["config"]["input_moments"] == "upsample" and r["config"]["loss_in_head"] is True
 
 
 @pytest.mark.parametrize("exchange", ["auto", "allreduce"])

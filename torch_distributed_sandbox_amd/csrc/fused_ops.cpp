@@ -448,6 +448,48 @@ Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor
   return logits;
 }
 
+// fused_head_forward_aff with the batch's labels: the mean cross-entropy loss (torch's
+// CrossEntropyLoss defaults: ignore_index -100, no label smoothing) and dlogits formed by the
+// head forward's finalizing workgroup right after the logits (ce_small.h) -- one launch fewer than
+// logits then ops.cross_entropy, with the same arithmetic.  Returns (logits, loss, dlogits).
+std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, const Tensor& aff2, const Tensor& wfc,
+                                                             const c10::optional<Tensor>& bfc, int64_t P,
+                                                             const Tensor& labels) {
+  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_aff_ce: ya must be [B,32,PB]");
+  const int64_t B = ya.size(0), Q = P / 2;
+  TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_forward_aff_ce: needs P/2 >= 4 pooled columns and B >= 1");
+  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(aff2, at::kFloat, {64}, "aff2");
+  TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
+              "fc.weight must be [<=10, 32*Q*Q]");
+  const int64_t NC = wfc.size(0);
+  need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
+  need(labels, at::kLong, {B}, "labels");
+  const float* bf = optf(bfc, NC, "fc.bias");
+  c10::DeviceGuard guard(ya.device());
+  hipStream_t st = stream_of(ya);
+  const int nblk = 32 * tds_head_pb_nblk((int)Q);
+  auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
+  auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
+  auto logits = at::empty({B, NC}, ya.options());
+  auto dlogits = at::empty({B, NC}, ya.options());
+  auto loss = at::empty({}, ya.options());
+  auto inv = at::empty({1}, ya.options());
+  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
+                                 part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), nullptr,
+                                 (int)B, (int)Q, (int)NC, st, true, labels.data_ptr<int64_t>(),
+                                 dlogits.data_ptr<float>(), loss.data_ptr<float>(), inv.data_ptr<float>());
+  TORCH_CHECK(rc >= 0, "fused_head_forward_aff_ce: unsupported shape");
+  if (rc == 0) {  // (the finalizer was not in the launch: the separate CE)
+    auto row_loss = at::empty({B}, ya.options());
+    tds_cross_entropy(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), row_loss.data_ptr<float>(),
+                      dlogits.data_ptr<float>(), loss.data_ptr<float>(), inv.data_ptr<float>(), (int)B, (int)NC, -100,
+                      0.f, st);
+  }
+  check_launches("fused_head_forward_aff_ce");
+  return {logits, loss, dlogits};
+}
+
 // The head forward applying the activation exchange's deferred weight update on the way through
 // (head_pb.hip HPUpd): wfc <- wfc - lr * scale * dy_all^T X with X decoded from the gathered zero-
 // suppressed encodings (meta_all [W, R] int32, vals_all [W, cap]), then the logits with the updated
@@ -1046,6 +1088,9 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       &fused_conv2_forward_bn);
   m.def("fused_head_forward_aff(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor(a!)? x_out=None) -> Tensor",
         &fused_head_forward_aff);
+  m.def("fused_head_forward_aff_ce(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor labels) -> "
+        "(Tensor, Tensor, Tensor)",
+        &fused_head_forward_aff_ce);
   m.def(
       "fused_head_forward_upd(Tensor ya, Tensor aff2, Tensor(a!) wfc, Tensor? bfc, int P, Tensor dy_all, Tensor meta_all, "
       "Tensor vals_all, int rows, float scale, float lr) -> Tensor",

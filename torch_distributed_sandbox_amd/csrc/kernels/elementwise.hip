@@ -12,6 +12,7 @@
 
 #include "common.h"
 #include "launchers.h"
+#include "ce_small.h"
 #include "ups_common.h"
 
 namespace tds {
@@ -349,43 +350,7 @@ __global__ __launch_bounds__(256) void ce_small_kernel(const float* __restrict__
                                                        float* __restrict__ dlogits, float* __restrict__ loss_out,
                                                        float* __restrict__ inv_count_out, int M, int N,
                                                        int64_t ignore_index, float label_smoothing) {
-  __shared__ float rl[1024];
-  __shared__ float sh[16];
-  const int lane = lane_id(), nw = blockDim.x / TDS_WAVE;
-  const float eps = label_smoothing;
-  for (int row = wave_id(); row < M; row += nw) {
-    const float* z = logits + (int64_t)row * N;
-    float mx = -INFINITY;
-    for (int j = lane; j < N; j += TDS_WAVE) mx = fmaxf(mx, z[j]);
-    mx = wave_max(mx);
-    float sm = 0.f, zsum = 0.f;
-    for (int j = lane; j < N; j += TDS_WAVE) { sm += __expf(z[j] - mx); zsum += z[j]; }
-    sm = wave_sum(sm);
-    zsum = wave_sum(zsum);
-    const float lse = mx + __logf(sm);
-    const int64_t lab = labels[row];
-    const bool valid = lab != ignore_index;
-    if (lane == 0) rl[row] = valid ? (1.f - eps) * (lse - z[lab]) + eps * (lse - zsum / (float)N) : 0.f;
-    for (int j = lane; j < N; j += TDS_WAVE) {
-      float d = 0.f;
-      if (valid) d = __expf(z[j] - lse) - ((j == lab ? (1.f - eps) : 0.f) + eps / (float)N);
-      dlogits[(int64_t)row * N + j] = d;
-    }
-  }
-  __syncthreads();  // rl complete; this block's dlogits writes visible to the block
-  float l = 0.f, c = 0.f;
-  for (int r = threadIdx.x; r < M; r += blockDim.x) {
-    l += rl[r];
-    c += labels[r] != ignore_index ? 1.f : 0.f;
-  }
-  l = block_sum(l, sh);
-  c = block_sum(c, sh);
-  const float inv = c > 0.f ? 1.f / c : 0.f;
-  for (int64_t i = threadIdx.x; i < (int64_t)M * N; i += blockDim.x) dlogits[i] *= inv;
-  if (threadIdx.x == 0) {
-    loss_out[0] = c > 0.f ? l * inv : NAN;
-    inv_count_out[0] = inv;
-  }
+  ce_small_block(logits, labels, dlogits, loss_out, inv_count_out, M, N, ignore_index, label_smoothing);  // (ce_small.h)
 }
 
 // dlogits *= grad_out (scalar tensor on device) — keeps the backward sync-free.

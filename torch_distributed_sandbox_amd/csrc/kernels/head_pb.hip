@@ -32,6 +32,7 @@
 // No LDS and no barriers in the stream: the next chunk's loads are issued before the current
 // one is reduced.  64-bit indexing throughout (no buffer descriptors).
 #include "common.h"
+#include "ce_small.h"
 #include "launchers.h"
 #include "pooled_layout.h"
 
@@ -192,6 +193,12 @@ struct HPFin {
   double* sums;          // [B*NC]
   const float* bias;     // [NC] or nullptr
   float* logits;         // [B*NC]
+  // optional: the batch's labels [B] -> the cross-entropy loss (mean, torch's defaults) and dlogits
+  // [B*NC] formed by the same workgroup right after the logits (ce_small.h; no separate CE launch)
+  const int64_t* labels = nullptr;
+  float* dlogits = nullptr;
+  float* loss = nullptr;
+  float* inv_count = nullptr;
 };
 // UPD: the fc-gradient exchange's deferred weight update applied on the way through (the activation
 // exchange, parallel/factored.py): W <- W - lr * scale * sum_m dY[m]^T X_m, X_m = row m of the M =
@@ -404,10 +411,16 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
   }
   if (!tds_arrive(fin.sync + 32, 32u, &last_flag)) return;
   const double s = wide_row_sum(fin.cpart, 32, BN, BN, wpart);
+  __shared__ float lg[HP_MAXB * 10];
   if ((int)threadIdx.x < BN) {
+    const float z = (float)s + (fin.bias ? fin.bias[threadIdx.x % NC] : 0.f);
     fin.sums[threadIdx.x] = s;
-    fin.logits[threadIdx.x] = (float)s + (fin.bias ? fin.bias[threadIdx.x % NC] : 0.f);
+    fin.logits[threadIdx.x] = z;
+    lg[threadIdx.x] = z;
   }
+  if (fin.labels == nullptr) return;
+  __syncthreads();
+  ce_small_block(lg, fin.labels, fin.dlogits, fin.loss, fin.inv_count, Btot, NC, -100, 0.f);
 }
 
 // sums[i] = sum_k partial[k][i] (fixed order), logits[i] = sums[i] + bias[i % NC]: one workgroup
@@ -650,7 +663,8 @@ int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
 // partial: double [32 * nblk + 32][B*NC] (the last 32 rows: the in-launch finalizer's channel sums);
 // sums: double [B*NC].  fused_fin = false: the separate head_logits launch (the A/B reference)
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
-                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st, bool fused_fin) {
+                    double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st, bool fused_fin,
+                    const int64_t* labels, float* dlogits, float* loss, float* inv_count) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1) return -1;
   const PBGeom g = pb_geom(Q);
   const int nwg = 32 * hp_grid(g).per_channel();
@@ -664,6 +678,10 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
     fin.sums = sums;
     fin.bias = bias;
     fin.logits = logits;
+    fin.labels = labels;
+    fin.dlogits = dlogits;
+    fin.loss = loss;
+    fin.inv_count = inv_count;
   }
   for (int b0 = 0; b0 < B; b0 += HP_MAXB) {
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
@@ -679,7 +697,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
     }
 #undef TDS_HPF
   }
-  if (fin.sync != nullptr) return 0;
+  if (fin.sync != nullptr) return labels != nullptr ? 1 : 0;
   hipLaunchKernelGGL(head_logits_kernel, dim3(BN), dim3(256), 0, st, partial, nwg, sums, bias, logits, BN, NC);
   TDS_LAUNCH_CHECK();
   return 0;

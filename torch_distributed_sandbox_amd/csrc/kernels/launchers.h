@@ -196,10 +196,14 @@ int tds_head_bwd_pb_nblk(int Q);  // the backward's workgroups per channel (its 
 uint32_t* tds_sync_words(int site, hipStream_t st);
 bool tds_fused_fin_enabled();  // TDS_FUSED_FIN=0: the separate finalize launches
 
-// partial: [32 * nblk + 32][B*NC] doubles; fused_fin: logits finished in the launch (B <= 8)
+// partial: [32 * nblk + 32][B*NC] doubles; fused_fin: logits finished in the launch (B <= 8).
+// labels (optional, int64 [B]): the cross-entropy loss / dlogits / 1/count formed in the same launch
+// (head_pb.hip HPFin) -- returns 1 when it did, 0 when the caller must run tds_cross_entropy, < 0 on
+// an unsupported shape
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st,
-                    bool fused_fin = true);
+                    bool fused_fin = true, const int64_t* labels = nullptr, float* dlogits = nullptr,
+                    float* loss = nullptr, float* inv_count = nullptr);
 // the head forward with the activation exchange's deferred weight update fused (head_pb.hip HPUpd)
 int tds_head_fwd_pb_upd(const float* ya, float* Wfc, const float* bias, const float* aff2, double* partial,
                         double* sums, float* logits, int B, int Q, int NC, const float* dy, int M, int rows,

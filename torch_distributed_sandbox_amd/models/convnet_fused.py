@@ -99,6 +99,28 @@ def _take_input_stats(x):
     return st[1]
 
 
+# The batch's labels, attached by the training loop before the forward: the head forward's
+# finalizing workgroup then forms the cross-entropy loss and dlogits right after the logits
+# (ops.fused_head_forward_aff_ce), and ops.functional.cross_entropy takes them from the logits
+# instead of launching its own kernel.  Only torch's CrossEntropyLoss defaults (mean, ignore_index
+# -100, no label smoothing) are formed in the head; any other use of the logits is unaffected.
+def attach_labels(x, labels):
+    """Hand the batch's labels to the forward that consumes ``x`` (valid until x is modified in place)."""
+    x._tds_labels = (x._version, labels)
+    return x
+
+
+def _take_labels(x):
+    lb = getattr(x, "_tds_labels", None)
+    if lb is None or lb[0] != x._version:
+        return None
+    labels = lb[1]
+    if not (torch.is_tensor(labels) and labels.dtype == torch.int64 and labels.dim() == 1 and labels.is_cuda
+            and labels.shape[0] == x.shape[0] and labels.is_contiguous()):
+        return None
+    return labels
+
+
 # One-shot callbacks run (on the host, in the backward's thread) right before the conv2
 # backward -- the step's longest, MFMA-bound kernel -- is enqueued: work they put on another
 # stream after waiting on the current one runs beside it (bench.py / trainer input prefetch).
@@ -140,7 +162,7 @@ def _sinks(ctx, params, first):
 _ZERO = {}
 # counters the tests read: forward passes that applied the exchange's weight update in the head kernel,
 # and layer-1 forwards that took x moments precomputed by the input pipeline
-STATS = {"head_fused_updates": 0, "precomputed_input_moments": 0}
+STATS = {"head_fused_updates": 0, "precomputed_input_moments": 0, "head_fused_ce": 0}
 
 
 def _zero_scalar(device, dtype):
@@ -193,10 +215,12 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update", "labels", "ce")
 
     def __init__(self):
         self.fc_update = None
+        self.labels = None  # the batch's labels (attach_labels) -> ce = (labels, loss, dlogits) from the head
+        self.ce = None
 
 
 # The small reductions behind BN2 (forward statistics, backward constants) and the logits run
@@ -283,6 +307,11 @@ class _Head(torch.autograd.Function):
                 dy_all, meta_all, vals_all, rows, scale, lr = fused_upd
                 STATS["head_fused_updates"] += 1
                 logits = ops.fused_head_forward_upd(ya, aff2, wfc, bfc, P, dy_all, meta_all, vals_all, rows, scale, lr)
+            elif link.labels is not None and x_out is None:
+                # the loss and dlogits formed by the head forward's finalizing workgroup
+                logits, loss, dlogits = ops.fused_head_forward_aff_ce(ya, aff2, wfc, bfc, P, link.labels)
+                link.ce = (link.labels, loss, dlogits)
+                STATS["head_fused_ce"] += 1
             else:
                 logits = ops.fused_head_forward_aff(ya, aff2, wfc, bfc, P, x_out)
         else:  # bn_a = the conv2 forward's BN2 partials
@@ -385,5 +414,13 @@ def forward(model, x):
     ex = factored.get(fc.weight)
     if ex is not None and not ex.ready(x.shape[0]):
         ex = None
-    return _Head.apply(y2, ya, bn_a, bn_b, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
-                       bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias, ex, link)
+    link.labels = _take_labels(x)
+    logits = _Head.apply(y2, ya, bn_a, bn_b, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
+                         bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps), fc.weight, fc.bias, ex, link)
+    if link.ce is not None:
+        lab = link.ce[0]
+        # (ops.functional.cross_entropy takes it for these very labels: same memory, unchanged since)
+        logits._tds_ce = (logits._version, (lab.data_ptr(), tuple(lab.shape), lab.stride(), lab._version)) + link.ce[1:]
+        link.ce = None
+    link.labels = None
+    return logits

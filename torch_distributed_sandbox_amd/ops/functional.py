@@ -266,10 +266,36 @@ def backward(loss):
     loss.backward(_unit_seed(loss))
 
 
+class _CrossEntropyFromHead(torch.autograd.Function):
+    """The loss and dlogits the fused ConvNet head formed with the logits (models/convnet_fused.py
+    attach_labels, csrc/kernels/ce_small.h): the same arithmetic as _CrossEntropy, no launch."""
+
+    @staticmethod
+    def forward(ctx, logits, pre):
+        loss, dlogits = pre
+        ctx.save_for_backward(dlogits)
+        return loss
+
+    @staticmethod
+    def backward(ctx, gloss):
+        (dlogits,) = ctx.saved_tensors
+        if _is_unit_seed(gloss):
+            return dlogits, None
+        return _ext.ops().scale_by_scalar(dlogits, gloss.reshape(1).contiguous().float()), None
+
+
 def cross_entropy(logits, labels, ignore_index: int = -100, label_smoothing: float = 0.0):
     """Mean-reduced CE (``nn.CrossEntropyLoss()`` defaults) with a fused fwd+bwd kernel."""
     if not logits.is_cuda or logits.dim() != 2:
         return F.cross_entropy(logits, labels, ignore_index=ignore_index, label_smoothing=label_smoothing)
+    pre = getattr(logits, "_tds_ce", None)
+    if pre is not None:
+        logits._tds_ce = None
+        version, lab, loss, dlogits = pre
+        same = (torch.is_tensor(labels) and labels.dtype == torch.int64 and labels.is_cuda
+                and lab == (labels.data_ptr(), tuple(labels.shape), labels.stride(), labels._version))
+        if version == logits._version and same and int(ignore_index) == -100 and float(label_smoothing) == 0.0:
+            return _CrossEntropyFromHead.apply(logits, (loss, dlogits))
     return _CrossEntropy.apply(logits, labels.long(), int(ignore_index), float(label_smoothing))
 
 

@@ -21,7 +21,7 @@ import torch
 
 from . import _ext
 from .data import DeviceUpsampleLoader, SyntheticMNIST
-from .models import ConvNet
+from .models import ConvNet, convnet_fused
 from .ops import CrossEntropyLoss, SGD
 from .ops import functional as TF
 from .parallel import DistributedDataParallel, DistributedSampler
@@ -116,7 +116,8 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
         _, start_epoch, _ = checkpoint.load(args.resume, model, optimizer, map_location=device)
     dataset = SyntheticMNIST(size=args.dataset_size)
     levels = getattr(args, "input", "levels") == "levels"
-    moments = levels and getattr(args, "mode", "auto") != "layers"  # the fused plan reads them
+    fused_plan = getattr(args, "mode", "auto") != "layers"
+    moments = levels and fused_plan  # the fused plan reads them
     if distributed:
         sampler = DistributedSampler(len(dataset), num_replicas=world, rank=rank)
         loader = DeviceUpsampleLoader(dataset, batch_size, (H, W), device, sampler=sampler, levels=levels,
@@ -140,6 +141,9 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
                 break
             fault.maybe_inject(rank, steps_done)
             with timer.phase("forward"):
+                if fused_plan and images.is_cuda:
+                    # (fused plan: the loss and dlogits formed by the head forward with the logits)
+                    convnet_fused.attach_labels(images, labels)
                 outputs = model(images)
                 loss = criterion(outputs, labels)
             optimizer.zero_grad()
