@@ -167,6 +167,24 @@ const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg
 
 int64_t pb_plane(int64_t P) { return tds_pb_plane((int)(P / 2)); }
 
+// ---------------------------------------------------------------- the step's magnitude-bound workspace
+constexpr int64_t kG2mSlack = 16;   // floats past g2m's end its allocations carry (conv2_bwd.hip GB runs)
+constexpr int64_t kMagParts = 64;   // ypart offset in the mag workspace
+constexpr int64_t kMagScales = 40;  // conv2 epilogue scales (csrc/kernels/conv2_common.h)
+int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
+int64_t mag_gpart_count(int64_t B, int64_t P) {
+  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_bwd_pb_nblk((int)(P / 2));
+}
+int64_t mag_numel(int64_t B, int64_t P) { return kMagParts + 32 * mag_ypart_count() + mag_gpart_count(B, P); }
+
+uint32_t* opt_mag(const c10::optional<Tensor>& mag, int64_t numel = 33) {
+  if (!mag.has_value() || !mag->defined()) return nullptr;
+  TORCH_CHECK(mag->is_cuda() && mag->scalar_type() == at::kInt && mag->is_contiguous() && mag->numel() >= numel,
+              "mag (magnitude-bound workspace) must be a contiguous int32 GPU tensor of >= ", numel,
+              " elements (ops.mag_numel)");
+  return reinterpret_cast<uint32_t*>(mag->data_ptr<int>());
+}
+
 // ---------------------------------------------------------------- layer 1 forward
 // returns (p1 carrier, idx1, stats1[mean16|invstd16], ac_partial, strips)
 // x: fp32 images, or uint8 levels (ToTensor's input: x = level / 255, folded into the kernels)
@@ -222,8 +240,30 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     const Tensor& x, const Tensor& w1, const Tensor& b1, const c10::optional<Tensor>& gamma1,
     const c10::optional<Tensor>& beta1, const c10::optional<Tensor>& rm1, const c10::optional<Tensor>& rv1,
     const c10::optional<Tensor>& nbt1, double momentum, double eps, const c10::optional<Tensor>& asum_in,
-    const c10::optional<Tensor>& strips_in) {
+    const c10::optional<Tensor>& strips_in, const c10::optional<Tensor>& mag, const c10::optional<Tensor>& w2,
+    const c10::optional<Tensor>& wp_out, const c10::optional<Tensor>& wd_out) {
   check_l1_input(x, "fused_l1_forward");
+  // mag (optional): the Gram launch stores 1 / p1_scale at mag[kMagScales + 1] for the conv2
+  // kernels (the weight packing, conv2_pack(write_p1=False), then runs ahead on a side stream)
+  uint32_t* p1inv = opt_mag(mag, kMagScales + 2) ? opt_mag(mag) + kMagScales + 1 : nullptr;
+  // w2 + wp_out + wd_out (with mag): conv2's weights packed by workgroups of the Gram launch (or,
+  // on the paths without that launch, by the packing kernel right after the Gram) -- conv2_pack's
+  // outputs without its launch between layer 1 and conv2
+  const bool pack = w2.has_value() && w2->defined();
+  const float* pw2 = nullptr;
+  short *pwp = nullptr, *pwd = nullptr;
+  if (pack) {
+    TORCH_CHECK(p1inv != nullptr && wp_out.has_value() && wd_out.has_value(),
+                "fused_l1_forward: packing conv2's weights needs mag, wp_out and wd_out");
+    need(*w2, at::kFloat, {32, 16, 5, 5}, "conv2.weight");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(w2->data_ptr()) % 16 == 0, "fused_l1_forward: conv2.weight must be 16-B aligned");
+    need(*wp_out, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
+    need(*wd_out, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
+    pw2 = w2->data_ptr<float>();
+    pwp = wp_out->data_ptr<int16_t>();
+    pwd = wd_out->data_ptr<int16_t>();
+  }
+  bool packed = false;
   const int64_t B = x.size(0), H = x.size(2), W = x.size(3);
   need(w1, at::kFloat, {16, 1, 5, 5}, "conv1.weight");
   need(b1, at::kFloat, {16}, "conv1.bias");
@@ -255,13 +295,17 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     if (tds_l1_reduce_gram(ac.data_ptr<double>(), nac, asum.data_ptr<double>(), strips.data_ptr<double>(),
                            x.data_ptr(), levels, (int)B, (int)H, (int)W, w1.data_ptr<float>(), gram.data_ptr<double>(),
                            sums.data_ptr<double>(), b1.data_ptr<float>(), (float)eps, (float)momentum, g, be,
-                           stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st, border))
+                           stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st, border, p1inv, pw2, pwp, pwd,
+                           pack ? opt_mag(mag) : nullptr)) {
+      packed = pack;
       return;
+    }
     if (border) tds_x_border_u8(x.data_ptr<uint8_t>(), strips.data_ptr<double>(), (int)B, (int)H, (int)W, st);
     tds_reduce_partials(ac.data_ptr<double>(), asum.data_ptr<double>(), 42, nac, 42, 0, 42, st);
     tds_l1_gram(asum.data_ptr<double>(), strips.data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H, (int)W,
                 w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(),
-                (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+                (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st,
+                p1inv);
   };
   const bool pre = asum_in.has_value() && asum_in->defined();
   if (pre && asum_in->numel() != 42) {
@@ -278,7 +322,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     need(*strips_in, at::kDouble, {B * 8 * 82}, "precomputed border strips");
     tds_l1_gram(asum_in->data_ptr<double>(), strips_in->data_ptr<double>(), x.data_ptr(), levels, (int)B, (int)H,
                 (int)W, w1.data_ptr<float>(), gram.data_ptr<double>(), sums.data_ptr<double>(), b1.data_ptr<float>(),
-                (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
+                (float)eps, (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st,
+                p1inv);
   } else {
     Tensor ac, strips;
     int nac = 0;
@@ -286,6 +331,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     if (levels) strips = at::empty({B * 8 * 82 * tds_xmom_border_chunks((int)H, (int)W)}, fo.dtype(at::kDouble));
     reduce_gram(ac, nac, strips, levels);
   }
+  if (pack && !packed)
+    tds_conv2_pack_weights(pw2, pwp, pwd, opt_mag(mag), nullptr, st, /*write_p1=*/false);
   // the single conv1 pass: conv + BN1 affine + ReLU + pool -> p1 (fp16), argmax
   auto p1 = at::empty({B, P, P, 16}, fo.dtype(at::kHalf));
   auto idx1 = at::empty({B, P, P, 16}, fo.dtype(at::kByte));
@@ -296,28 +343,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
 }
 
 // ---------------------------------------------------------------- conv2 forward
-constexpr int64_t kG2mSlack = 16;   // floats past g2m's end its allocations carry (conv2_bwd.hip GB runs)
-constexpr int64_t kMagParts = 64;   // ypart offset in the mag workspace
-constexpr int64_t kMagScales = 40;  // conv2 epilogue scales (csrc/kernels/conv2_common.h)
-int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
-int64_t mag_gpart_count(int64_t B, int64_t P) {
-  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_bwd_pb_nblk((int)(P / 2));
-}
-int64_t mag_numel(int64_t B, int64_t P) { return kMagParts + 32 * mag_ypart_count() + mag_gpart_count(B, P); }
-
-uint32_t* opt_mag(const c10::optional<Tensor>& mag, int64_t numel = 33) {
-  if (!mag.has_value() || !mag->defined()) return nullptr;
-  TORCH_CHECK(mag->is_cuda() && mag->scalar_type() == at::kInt && mag->is_contiguous() && mag->numel() >= numel,
-              "mag (magnitude-bound workspace) must be a contiguous int32 GPU tensor of >= ", numel,
-              " elements (ops.mag_numel)");
-  return reinterpret_cast<uint32_t*>(mag->data_ptr<int>());
-}
-
 // fp16 hi/lo weight packs of the conv2 forward and data gradient; resets mag when given
 // With mag: weights packed at a power-of-two scale that keeps them in fp16's normal range, the
 // scale and p1_scale's inverse recorded in mag for the conv2 epilogues (conv2_pack.hip).
 std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tensor>& mag,
-                                      const c10::optional<Tensor>& p1_scale) {
+                                      const c10::optional<Tensor>& p1_scale, bool write_p1) {
   need(w2, at::kFloat, {32, 16, 5, 5}, "conv2.weight");
   TORCH_CHECK(reinterpret_cast<uintptr_t>(w2.data_ptr()) % 16 == 0, "conv2_pack: conv2.weight must be 16-B aligned");
   const float* ps = optf(p1_scale, 1, "p1_scale");
@@ -325,7 +355,7 @@ std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tens
   auto wp = at::empty({2 * 13 * 2 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
   auto wd = at::empty({2 * 25 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
   tds_conv2_pack_weights(w2.data_ptr<float>(), wp.data_ptr<int16_t>(), wd.data_ptr<int16_t>(), opt_mag(mag), ps,
-                         stream_of(w2));
+                         stream_of(w2), write_p1);
   check_launches("conv2_pack");
   return {wp, wd};
 }
@@ -1059,11 +1089,13 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
         &zs_encode_ya);
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
-      "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps, Tensor? asum=None, Tensor? strips=None) -> "
+      "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps, Tensor? asum=None, Tensor? strips=None, "
+      "Tensor(d!)? mag=None, Tensor? w2=None, Tensor(e!)? wp_out=None, Tensor(f!)? wd_out=None) -> "
       "(Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_l1_forward);
   m.def("l1_input_stats(Tensor x) -> (Tensor, Tensor)", &l1_input_stats);
-  m.def("conv2_pack(Tensor w2, Tensor(a!)? mag=None, Tensor? p1_scale=None) -> (Tensor, Tensor)", &conv2_pack);
+  m.def("conv2_pack(Tensor w2, Tensor(a!)? mag=None, Tensor? p1_scale=None, bool write_p1=True) -> (Tensor, Tensor)",
+        &conv2_pack);
   m.def("conv2_split() -> int", []() -> int64_t { return tds_conv2_split(); });
   m.def(
       "fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2, Tensor(a!)? mag=None) -> "

@@ -26,6 +26,7 @@
 #include "bn_finalize.h"
 #include "launchers.h"
 #include "xmom_u8.h"
+#include "conv2_pack.h"
 
 namespace tds {
 
@@ -1046,7 +1047,8 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
                                                       float eps, float momentum,
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
-                                                      float* __restrict__ aff, double xs, int nch = 1) {
+                                                      float* __restrict__ aff, double xs, int nch = 1,
+                                                      uint32_t* __restrict__ p1inv = nullptr) {
   __shared__ double full[82];  // autocorrelation at the 81 offsets | the plain sum
   __shared__ double G[25][25];
   __shared__ double S[25];
@@ -1087,6 +1089,9 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
     }
     p1_scale = ldexpf(1.f, e1);
     if (tid == 0) aff[32] = p1_scale;
+    // the conv2 kernels' copy of its inverse (mag[kMagScales + 1]), when the weight packing ran
+    // ahead of this launch (models/convnet_fused.py: conv2_pack on a side stream)
+    if (tid == 0 && p1inv != nullptr) *p1inv = __float_as_uint(1.f / p1_scale);
   }
   __syncthreads();
   if (tid < 16) {
@@ -1129,20 +1134,30 @@ __global__ __launch_bounds__(256) void l1_gram_kernel(const double* __restrict__
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
-                                                      float* __restrict__ aff, double xs) {
+                                                      float* __restrict__ aff, double xs, uint32_t* __restrict__ p1inv) {
   __shared__ L1GramPre pre;
   l1_gram_stage(pre, x, B, H, W, w1, b1, gamma, beta, running_mean, running_var);
   __syncthreads();
   l1_gram_body<T>(ac_sum, strips, x, B, H, W, pre, gram, sums, eps, momentum, stats, running_mean, running_var,
-                  num_batches, aff, xs);
+                  num_batches, aff, xs, 1, p1inv);
 }
 
 // The x autocorrelation partials' reduction and the Gram in ONE launch: workgroup e sums column
 // e of the [nchunk][42] partials in reduce_partials_kernel's order (write-through), and the last
 // to arrive (common.h tds_arrive) runs l1_gram_body on the sums -- one launch boundary and one
 // launch floor fewer on the step's critical path than reduce_partials + l1_gram.
-// BORDER (uint8 levels): workgroups 42 .. 42 + 4B - 1 form the border strips from x themselves
-// (xmom_u8.h, one per image side) and arrive with the column sums.
+// BORDER (uint8 levels): workgroups 42 .. 42 + 4B*chunks - 1 form the border strips from x
+// themselves (xmom_u8.h, one per image side and line chunk) and arrive with the column sums.
+// pack.n > 0: the last pack.n workgroups pack conv2's weights (conv2_pack.h; they do not arrive:
+// nothing of this launch reads their output, the conv2 kernels after it do), the Gram body storing
+// 1 / p1_scale where the packing would have (p1inv).
+struct L1Pack {
+  const float* w2;
+  short* wp;
+  short* wd;
+  uint32_t* mag;
+  int n;
+};
 template <typename T, bool BORDER>
 __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __restrict__ ac_part, int nchunk,
                                                              double* __restrict__ ac_sum, uint32_t* __restrict__ sync,
@@ -1155,15 +1170,20 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
                                                              float* __restrict__ running_mean,
                                                              float* __restrict__ running_var,
                                                              int64_t* __restrict__ num_batches, float* __restrict__ aff,
-                                                             double xs) {
+                                                             double xs, uint32_t* __restrict__ p1inv, L1Pack pack) {
   __shared__ double sh[8];
   __shared__ int last;
   __shared__ L1GramPre pre;
   const int e = blockIdx.x;
+  const int npart = (int)gridDim.x - pack.n;  // the workgroups that arrive
+  if (e >= npart) {
+    conv2_pack_block(pack.w2, pack.wp, pack.wd, pack.mag, nullptr, 0, e - npart, pack.n);
+    return;
+  }
   const int nch = BORDER ? xmom_border_chunks(H, W) : 1;
   if constexpr (BORDER) {
     __shared__ uint32_t lines[BSIDE_LDS_WORDS];
-    if (e >= 42) {
+    if (e >= 42) {  // (e < npart)
       const int j = e - 42;
       x_border_side_u8(x, strips, j / (4 * nch), (j / nch) & 3, j % nch, nch, H, W, lines);
     }
@@ -1177,12 +1197,12 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
   }
   // (after the workgroup's own loads: issued first, the stage's loads put a round trip before them)
   l1_gram_stage(pre, x, B, H, W, w1, b1, gamma, beta, running_mean, running_var);  // (synchronized by tds_arrive)
-  if (!tds_arrive(sync, gridDim.x, &last)) return;
+  if (!tds_arrive(sync, (uint32_t)npart, &last)) return;
 #if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 1  // (A/B timing builds only: the reducer without its Gram body)
   return;
 #endif
   l1_gram_body<T>(ac_sum, strips, x, B, H, W, pre, gram, sums, eps, momentum, stats, running_mean, running_var,
-                  num_batches, aff, xs, nch);
+                  num_batches, aff, xs, nch, p1inv);
 }
 
 // Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
@@ -1290,7 +1310,7 @@ void tds_l1_gram(const double* ac_sum, const double* strips, const void* x, bool
                  const float* w1,
                  double* gram, double* sums, const float* b1, float eps, float momentum, const float* gamma,
                  const float* beta, float* stats, float* running_mean, float* running_var, int64_t* num_batches,
-                 float* aff, hipStream_t st) {
+                 float* aff, hipStream_t st, uint32_t* p1inv) {
   if (B > L1G_MAXB || H < 12 || W < 12) {
     tds_launch_fail("l1_gram: needs batch <= 32 and H, W >= 12");
     return;
@@ -1298,11 +1318,11 @@ void tds_l1_gram(const double* ac_sum, const double* strips, const void* x, bool
   if (levels)
     hipLaunchKernelGGL(l1_gram_kernel<uint8_t>, dim3(1), dim3(256), 0, st, ac_sum, strips,
                        static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats,
-                       running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
+                       running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv);
   else
     hipLaunchKernelGGL(l1_gram_kernel<float>, dim3(1), dim3(256), 0, st, ac_sum, strips, static_cast<const float*>(x),
                        B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta, stats, running_mean, running_var,
-                       num_batches, aff, 1.0);
+                       num_batches, aff, 1.0, p1inv);
   TDS_LAUNCH_CHECK();
 }
 
@@ -1435,7 +1455,14 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
                         bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,
                         float eps, float momentum, const float* gamma, const float* beta, float* stats,
                         float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st,
-                        bool border) {
+                        bool border, uint32_t* p1inv, const float* pack_w2, short* pack_wp, short* pack_wd,
+                        uint32_t* pack_mag) {
+  // conv2's weight packing on extra workgroups of this launch (64, as conv2_pack_weights_kernel)
+  const L1Pack pack{pack_w2, pack_wp, pack_wd, pack_mag, pack_w2 != nullptr ? 64 : 0};
+  if (pack.n > 0 && p1inv == nullptr) {
+    tds_launch_fail("l1_reduce_gram: packing conv2's weights in the launch needs the p1 inverse slot");
+    return true;
+  }
   if (B > L1G_MAXB || H < 12 || W < 12) {
     tds_launch_fail("l1_gram: needs batch <= 32 and H, W >= 12");
     return true;
@@ -1448,21 +1475,22 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
   if (sync == nullptr) return false;
   if (levels && border)
 #if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 2  // (A/B timing builds only: no border workgroups)
-    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42), dim3(256),
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + pack.n), dim3(256),
 #else
-    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + 4 * B * xmom_border_chunks(H, W)), dim3(256),
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + 4 * B * xmom_border_chunks(H, W) + pack.n),
+                       dim3(256),
 #endif
                        0, st, ac_part, nchunk,
                        ac_sum, sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum,
-                       gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
+                       gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv, pack);
   else if (levels)
-    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, false>), dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum,
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, false>), dim3(42 + pack.n), dim3(256), 0, st, ac_part, nchunk, ac_sum,
                        sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma,
-                       beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE);
+                       beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv, pack);
   else
-    hipLaunchKernelGGL((l1_reduce_gram_kernel<float, false>), dim3(42), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync,
+    hipLaunchKernelGGL((l1_reduce_gram_kernel<float, false>), dim3(42 + pack.n), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync,
                        strips, static_cast<const float*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta,
-                       stats, running_mean, running_var, num_batches, aff, 1.0);
+                       stats, running_mean, running_var, num_batches, aff, 1.0, p1inv, pack);
   TDS_LAUNCH_CHECK();
   return true;
 }

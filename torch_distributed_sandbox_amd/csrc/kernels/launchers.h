@@ -65,8 +65,10 @@ void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  //
 // ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, fp16x2 split MFMA)
 // mag (optional): 33 words of magnitude bounds [max|y2| per channel (32) | max|g2m|], zeroed here
 int tds_conv2_split();  // 1: fp16x2 (one operand hi + lo), 0: one fp16 MFMA per product (TF32 class)
+// write_p1: store mag[kMagScales + 1] = 1 / p1_scale (1 without p1_scale); false: the layer-1 Gram
+// launch stores it (the packing then runs ahead of layer 1 on a side stream)
 void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, const float* p1_scale,
-                            hipStream_t st);
+                            hipStream_t st, bool write_p1 = true);
 int tds_conv2_num_wg();  // CUs (tds_device_cus)
 // ---- cu_budget.hip: CUs the persistent kernels may use (all minus a reserve for RCCL) and
 // CU-masked compute streams
@@ -124,7 +126,8 @@ void tds_l1_gram(const double* ac_sum, const double* strips, const void* x, bool
                  const float* w1,
                  double* gram, double* sums, const float* b1, float eps, float momentum, const float* gamma,
                  const float* beta, float* stats, float* running_mean, float* running_var, int64_t* num_batches,
-                 float* aff, hipStream_t st);  // Gram + patch sums + the BN1 finalize
+                 float* aff, hipStream_t st, uint32_t* p1inv = nullptr);  // Gram + patch sums + the BN1 finalize
+// (p1inv: where to store 1 / p1_scale as the conv2 kernels read it, mag + kMagScales + 1, or nullptr)
 // levels: x is uint8 levels (x = level / 255, convnet_fused.hip L1_LEVEL_SCALE), else fp32
 void tds_l1_apply(const void* x, bool levels, const float* w1, const float* b1, const float* aff, void* p1,
                   uint8_t* idx1, int nwg, int B, int H, int W, hipStream_t st);
@@ -183,7 +186,10 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
                         bool levels, int B, int H, int W, const float* w1, double* gram, double* sums, const float* b1,
                         float eps, float momentum, const float* gamma, const float* beta, float* stats,
                         float* running_mean, float* running_var, int64_t* num_batches, float* aff, hipStream_t st,
-                        bool border = false);
+                        bool border = false, uint32_t* p1inv = nullptr, const float* pack_w2 = nullptr,
+                        short* pack_wp = nullptr, short* pack_wd = nullptr, uint32_t* pack_mag = nullptr);
+// (pack_w2 given: 64 extra workgroups pack conv2's weights into pack_wp / pack_wd / pack_mag, as
+// tds_conv2_pack_weights(write_p1 = false); p1inv must then be given)
 void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const float* w1, const float* b1,
                      const float* gamma1, const float* stats1, float* dw1, float* db1, float* dgamma1, float* dbeta1,
                      float scale, hipStream_t st);

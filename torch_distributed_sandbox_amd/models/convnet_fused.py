@@ -178,7 +178,11 @@ class _Layer1Link:
     """Carries the conv2 backward's dp1h (fp16, scaled: csrc/kernels/conv2_common.h) and its decode
     factor to the layer-1 backward, and the power-of-two scale p1 is stored at to the conv2 kernels."""
 
-    __slots__ = ("dp1", "dp1_dec", "p1_scale")
+    __slots__ = ("dp1", "dp1_dec", "p1_scale", "mag", "pack")
+
+    def __init__(self):
+        self.mag = None  # the step's magnitude workspace when layer 1 packs conv2's weights
+        self.pack = (None, None, None)  # (w2, wp, wd) for that packing
 
 
 class _Layer1(torch.autograd.Function):
@@ -190,7 +194,8 @@ class _Layer1(torch.autograd.Function):
             STATS["precomputed_input_moments"] += 1
         x = x.contiguous()
         p1, idx1, stats1, gram, p1_scale = ops.fused_l1_forward(x, w1, b1, g1, be1, rm1, rv1, nbt1, momentum, eps,
-                                                                asum, strips)
+                                                                asum, strips, link1.mag, *link1.pack)
+        link1.pack = (None, None, None)
         link1.p1_scale = p1_scale  # p1's fp16 range guard (a power of two, 1 normally): conv2 takes it out
         ctx.save_for_backward(x, p1, idx1, w1, b1, g1, stats1, gram)
         ctx.params = (w1, b1, g1, be1)
@@ -215,10 +220,12 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update", "labels", "ce")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update", "labels", "ce", "pack")
 
     def __init__(self):
         self.fc_update = None
+        self.pack = None  # (wp, wd): conv2's weights packed by the layer-1 forward (_pack_in_layer1)
+        self.mag = None
         self.labels = None  # the batch's labels (attach_labels) -> ce = (labels, loss, dlogits) from the head
         self.ce = None
 
@@ -235,8 +242,12 @@ class _Conv2(torch.autograd.Function):
         ops = _ext.ops()
         # magnitude bounds of this step (per-workgroup max |y2 - b2| here, max |g2m| in the head
         # backward): the conv2 backward's fp16 scale of dy2
-        link.mag = torch.empty(ops.mag_numel(p1.shape[0], p1.shape[1]), device=p1.device, dtype=torch.int32)
-        wp, wd = ops.conv2_pack(w2.contiguous(), link.mag, getattr(link1, "p1_scale", None))
+        if link.pack is not None:  # packed by the layer-1 reducer's launch (its Gram stored 1 / p1_scale)
+            wp, wd = link.pack
+            link.pack = None
+        else:
+            link.mag = torch.empty(ops.mag_numel(p1.shape[0], p1.shape[1]), device=p1.device, dtype=torch.int32)
+            wp, wd = ops.conv2_pack(w2.contiguous(), link.mag, getattr(link1, "p1_scale", None))
         # a2: each pooling window's argmax, saved for the backward (max_pool2d_with_indices' indices)
         link.bn_done = _FUSED_FIN
         if _FUSED_FIN:
@@ -393,14 +404,38 @@ class _Head(torch.autograd.Function):
         return (dy2, None, None, None, None, dg2, dbe2, None, None, None, None, None, dW, dbfc, None, None)
 
 
+# conv2's weight packing (conv2_pack: fp16 fragments of the forward / data gradient and their range
+# scales; 64 workgroups, ~9 us as its own launch) depends on the weights only, except for the
+# inverse of p1's range scale, which the layer-1 Gram then stores itself: it runs as extra
+# workgroups of the layer-1 reducer's launch (fused_l1_forward's w2 / wp_out / wd_out), one launch
+# fewer between layer 1 and conv2.  (Queued on a side stream instead it cost a cross-stream wait
+# before the conv2 forward and host time before layer 1: not faster, r5_s32.)
+_PACK_IN_L1 = os.environ.get("TDS_PACK_IN_L1", "1").strip() != "0"
+
+
+def _pack_in_layer1(w2, x, link, link1):
+    if not (_PACK_IN_L1 and x.is_cuda and x.dim() == 4):
+        return
+    ops = _ext.ops()
+    dev = x.device
+    param_fence.wait(w2)  # a deferred update of the weights (overlap_optimizer) lands first
+    mag = torch.empty(ops.mag_numel(x.shape[0], x.shape[2] // 2), device=dev, dtype=torch.int32)
+    wp = torch.empty(2 * 13 * 2 * 4 * 16 * 8, device=dev, dtype=torch.int16)
+    wd = torch.empty(2 * 25 * 4 * 16 * 8, device=dev, dtype=torch.int16)
+    link.mag = link1.mag = mag
+    link1.pack = (w2.detach(), wp, wd)
+    link.pack = (wp, wd)
+
+
 def forward(model, x):
     conv1, bn1 = model.layer1[0], model.layer1[1]
     conv2, bn2 = model.layer2[0], model.layer2[1]
     fc = model.fc
     link1 = _Layer1Link()
+    link = _Layer2Link()
+    _pack_in_layer1(conv2.weight, x, link, link1)
     p1 = _Layer1.apply(x, conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
                        bn1.num_batches_tracked, float(bn1.momentum), float(bn1.eps), link1)
-    link = _Layer2Link()
     y2, ya, bn_a, bn_b = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
                                       bn2.running_var, bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps),
                                       link, link1)
