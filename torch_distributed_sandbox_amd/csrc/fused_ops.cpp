@@ -314,7 +314,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     TORCH_CHECK(!(strips_in.has_value() && strips_in->defined()), "fused_l1_forward: partials come without strips");
     TORCH_CHECK(asum_in->numel() % 42 == 0 && asum_in->numel() / 42 <= INT32_MAX, "fused_l1_forward: partials [rows][42]");
     need(*asum_in, at::kDouble, {asum_in->numel()}, "precomputed autocorrelation partials");
-    auto strips = at::empty({B * 8 * 82 * tds_xmom_border_chunks((int)H, (int)W)}, fo.dtype(at::kDouble));
+    // (the in-launch border: the strips accumulate elsewhere and this buffer carries the Gram body's
+    // corner table, 16 * 81 + 16 doubles; [B][8][82] strips on the fallback path)
+    auto strips = at::empty({std::max<int64_t>(B * 8 * 82, 16 * 81 + 16)}, fo.dtype(at::kDouble));
     reduce_gram(*asum_in, (int)(asum_in->numel() / 42), strips, true);
   } else if (pre) {
     TORCH_CHECK(strips_in.has_value() && strips_in->defined(), "fused_l1_forward: asum without strips");
@@ -328,7 +330,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
     Tensor ac, strips;
     int nac = 0;
     std::tie(ac, strips, nac) = x_moment_parts(x, !levels);
-    if (levels) strips = at::empty({B * 8 * 82 * tds_xmom_border_chunks((int)H, (int)W)}, fo.dtype(at::kDouble));
+    if (levels) strips = at::empty({std::max<int64_t>(B * 8 * 82, 16 * 81 + 16)}, fo.dtype(at::kDouble));
     reduce_gram(ac, nac, strips, levels);
   }
   if (pack && !packed)

@@ -888,12 +888,34 @@ struct L1Corners {
   }
 };
 
+// corner products, every (corner row, corner col, offset) triple: e < 16 * 81 -> cp[ri][ci][d] =
+// sum_b x(b, r, c) x(b, r + dy, c + dx) for r in rows 0, 1, H-2, H-1 (ri 0..3), c likewise, the
+// partner inside the image; e - 16 * 81 < 16 -> cs[ri][ci] = sum_b x(b, r, c).  (Summed per Gram
+// entry inside its loops, the B-long LDS chains cost 8 us of the one-workgroup body, r5_s29b.)
+__device__ __forceinline__ double l1_corner_term(const L1Corners& cx, int B, int H, int W, int e) {
+  const bool sum = e >= 16 * 81;
+  const int rc = sum ? e - 16 * 81 : e / 81, d = sum ? 40 : e - rc * 81;
+  const int ri = rc >> 2, ci = rc & 3;
+  const int r = ri < 2 ? ri : H - 4 + ri, c = ci < 2 ? ci : W - 4 + ci;
+  const int r2 = r + d / 9 - 4, c2 = c + d % 9 - 4;
+  double v = 0.0;
+  if (sum) {
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) v += cx.at(b, r, c, H, W);
+  } else if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W) {
+#pragma unroll 8
+    for (int b = 0; b < B; ++b) v += (double)cx.at(b, r, c, H, W) * cx.at(b, r2, c2, H, W);
+  }
+  return v;
+}
+
 // T = uint8_t: x holds levels (x = xs * level); the sums are of the levels and G, S are scaled by
 // xs^2, xs at the end (fp64), so the Gram is that of the fp32 image either way.
 template <typename T>
 __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* __restrict__ strips_b,
                               const T* __restrict__ x, int B, int H, int W, double (*G)[25], double* S,
-                              double* full, double* strips, const L1Corners& cx, double xs, int nch) {
+                              double* full, double* strips, const L1Corners& cx, double xs, int nch,
+                              unsigned long long* __restrict__ sacc, const double* __restrict__ cpg) {
   const int tid = threadIdx.x;
   // the autocorrelation sum this thread places in full[] (load issued with the strips' below)
   double fa = 0.0;
@@ -911,7 +933,31 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
   // sit behind a cross-XCD round trip each -- as a dependent chain 15 of them cost ~20 us)
   const int nv = B * nch;
   static_assert(8 * 82 <= 3 * 256, "three strip sums per thread");
-  {
+  __shared__ double cp[16][81];
+  __shared__ double cs[16];
+  if (sacc != nullptr) {
+    // the batch's strips as exact u64 sums (xmom_u8.h) and the corner table formed before the
+    // hand-off by the column workgroups (cpg): one round of loads; the accumulator is zeroed for
+    // the stream's next launch
+    unsigned long long a[3];
+    double c[6];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) a[u] = tid + 256 * u < 8 * 82 ? sacc[tid + 256 * u] : 0ull;
+#pragma unroll
+    for (int u = 0; u < 6; ++u) c[u] = tid + 256 * u < 16 * 81 + 16 ? cpg[tid + 256 * u] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (tid + 256 * u < 8 * 82) {
+        strips[tid + 256 * u] = (double)a[u];
+        sacc[tid + 256 * u] = 0ull;
+      }
+#pragma unroll
+    for (int u = 0; u < 6; ++u) {
+      const int e = tid + 256 * u;
+      if (e < 16 * 81) cp[e / 81][e % 81] = c[u];
+      else if (e < 16 * 81 + 16) cs[e - 16 * 81] = c[u];
+    }
+  } else {
     // every thread's (up to) 3 x 16 loads issued before the first add (r5_s29b: 5.4 us for this
     // phase with the loads issued per sum)
     double t[3][16];
@@ -938,30 +984,12 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
     }
   }
   if (tid < 82) full[tid] = fa;
-  // corner products, all (corner row, corner col, offset) at once: cp[ri][ci][d] = sum_b x(b, r, c)
-  // x(b, r + dy, c + dx) for r in rows 0, 1, H-2, H-1 (ri 0..3), c likewise, the partner inside
-  // the image; cs[ri][ci] = sum_b x(b, r, c).  (Summed per Gram entry inside its loops, the
-  // B-long LDS chains cost 8 us of the one-workgroup body, r5_s29b.)
-  __shared__ double cp[16][81];
-  __shared__ double cs[16];
-  for (int e = tid; e < 16 * 81 + 16; e += blockDim.x) {
-    const bool sum = e >= 16 * 81;
-    const int rc = sum ? e - 16 * 81 : e / 81, d = sum ? 40 : e - rc * 81;
-    const int ri = rc >> 2, ci = rc & 3;
-    const int r = ri < 2 ? ri : H - 4 + ri, c = ci < 2 ? ci : W - 4 + ci;
-    const int r2 = r + d / 9 - 4, c2 = c + d % 9 - 4;
-    double v = 0.0;
-    if (sum) {
-#pragma unroll 8
-      for (int b = 0; b < B; ++b) v += cx.at(b, r, c, H, W);
-      cs[rc] = v;
-    } else {
-      if (r2 >= 0 && r2 < H && c2 >= 0 && c2 < W)
-#pragma unroll 8
-        for (int b = 0; b < B; ++b) v += (double)cx.at(b, r, c, H, W) * cx.at(b, r2, c2, H, W);
-      cp[rc][d] = v;
+  if (sacc == nullptr)
+    for (int e = tid; e < 16 * 81 + 16; e += blockDim.x) {
+      const double v = l1_corner_term(cx, B, H, W, e);
+      if (e < 16 * 81) cp[e / 81][e % 81] = v;
+      else cs[e - 16 * 81] = v;
     }
-  }
   __syncthreads();
 #if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 4  // (A/B timing: the loads phase only)
   return;
@@ -1048,14 +1076,16 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
                                                       float* __restrict__ stats, float* __restrict__ running_mean,
                                                       float* __restrict__ running_var, int64_t* __restrict__ num_batches,
                                                       float* __restrict__ aff, double xs, int nch = 1,
-                                                      uint32_t* __restrict__ p1inv = nullptr) {
+                                                      uint32_t* __restrict__ p1inv = nullptr,
+                                                      unsigned long long* __restrict__ sacc = nullptr,
+                                                      const double* __restrict__ cpg = nullptr) {
   __shared__ double full[82];  // autocorrelation at the 81 offsets | the plain sum
   __shared__ double G[25][25];
   __shared__ double S[25];
   __shared__ double Gw[16][25];
   __shared__ double strips_sum[8 * 82];
   const float* w1s = pre.w1s;
-  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, pre.cx, xs, nch);
+  l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, pre.cx, xs, nch, sacc, cpg);
 #if defined(TDS_L1G_DIAG) && (TDS_L1G_DIAG == 3 || TDS_L1G_DIAG == 4)  // (A/B timing: the Gram build only)
   return;
 #endif
@@ -1170,7 +1200,9 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
                                                              float* __restrict__ running_mean,
                                                              float* __restrict__ running_var,
                                                              int64_t* __restrict__ num_batches, float* __restrict__ aff,
-                                                             double xs, uint32_t* __restrict__ p1inv, L1Pack pack) {
+                                                             double xs, uint32_t* __restrict__ p1inv, L1Pack pack,
+                                                             unsigned long long* __restrict__ sacc,
+                                                             double* __restrict__ cpg) {
   __shared__ double sh[8];
   __shared__ int last;
   __shared__ L1GramPre pre;
@@ -1185,7 +1217,7 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
     __shared__ uint32_t lines[BSIDE_LDS_WORDS];
     if (e >= 42) {  // (e < npart)
       const int j = e - 42;
-      x_border_side_u8(x, strips, j / (4 * nch), (j / nch) & 3, j % nch, nch, H, W, lines);
+      x_border_side_u8(x, sacc, j / (4 * nch), (j / nch) & 3, j % nch, nch, H, W, lines);
     }
   }
   if (e < 42) {
@@ -1197,12 +1229,21 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
   }
   // (after the workgroup's own loads: issued first, the stage's loads put a round trip before them)
   l1_gram_stage(pre, x, B, H, W, w1, b1, gamma, beta, running_mean, running_var);  // (synchronized by tds_arrive)
+  if constexpr (BORDER) {
+    // the column workgroups form the Gram body's corner table meanwhile (32 entries each), handed
+    // over with the sums
+    if (e < 42) {
+      __syncthreads();  // pre.cx staged
+      const int i = e * 32 + (int)threadIdx.x;
+      if (threadIdx.x < 32 && i < 16 * 81 + 16) st_agent(cpg + i, l1_corner_term(pre.cx, B, H, W, i));
+    }
+  }
   if (!tds_arrive(sync, (uint32_t)npart, &last)) return;
 #if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 1  // (A/B timing builds only: the reducer without its Gram body)
   return;
 #endif
   l1_gram_body<T>(ac_sum, strips, x, B, H, W, pre, gram, sums, eps, momentum, stats, running_mean, running_var,
-                  num_batches, aff, xs, nch, p1inv);
+                  num_batches, aff, xs, nch, p1inv, BORDER ? sacc : nullptr, BORDER ? cpg : nullptr);
 }
 
 // Closed-form layer-1 gradients (one workgroup) from the l1_bwd sums and the Gram:
@@ -1473,6 +1514,13 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
   }
   uint32_t* sync = tds_sync_words(kSyncL1Gram, st);
   if (sync == nullptr) return false;
+  // border: the strips accumulate in a zeroed u64 block (8 x 82 words) and the strips buffer (>= 1312
+  // doubles: B * 8 * chunks * 82) carries the corner table
+  unsigned long long* sacc = nullptr;
+  if (border) {
+    sacc = tds_zeroed_u64(0, 8 * 82, st);
+    if (sacc == nullptr) return false;
+  }
   if (levels && border)
 #if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 2  // (A/B timing builds only: no border workgroups)
     hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + pack.n), dim3(256),
@@ -1482,15 +1530,17 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
 #endif
                        0, st, ac_part, nchunk,
                        ac_sum, sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum,
-                       gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv, pack);
+                       gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv, pack,
+                       sacc, strips);
   else if (levels)
     hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, false>), dim3(42 + pack.n), dim3(256), 0, st, ac_part, nchunk, ac_sum,
                        sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma,
-                       beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv, pack);
+                       beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv, pack,
+                       nullptr, nullptr);
   else
     hipLaunchKernelGGL((l1_reduce_gram_kernel<float, false>), dim3(42 + pack.n), dim3(256), 0, st, ac_part, nchunk, ac_sum, sync,
                        strips, static_cast<const float*>(x), B, H, W, w1, gram, sums, b1, eps, momentum, gamma, beta,
-                       stats, running_mean, running_var, num_batches, aff, 1.0, p1inv, pack);
+                       stats, running_mean, running_var, num_batches, aff, 1.0, p1inv, pack, nullptr, nullptr);
   TDS_LAUNCH_CHECK();
   return true;
 }

@@ -4,6 +4,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <tuple>
 #include <utility>
 
 #include "common.h"
@@ -70,6 +71,33 @@ uint32_t* tds_sync_words(int site, hipStream_t st) {
     if (hipMemsetAsync(w, 0, bytes, st) != hipSuccess) return nullptr;
   }
   return w + (size_t)site * tds::kSyncWordsPerSite;
+}
+
+// A zeroed 64-bit accumulator block per (device, stream, key) of at least n words (grown by
+// reallocation when a larger n is asked for; zeroed on the stream when allocated).  Its users
+// atomically add exact integer sums into it and the consumer zeroes what it read, so each launch on
+// that stream finds it at 0 (like tds_sync_words' counters).
+unsigned long long* tds_zeroed_u64(int key, size_t n, hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::tuple<int, hipStream_t, int>, std::pair<unsigned long long*, size_t>> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& e = cache[{dev, st, key}];
+  if (e.first == nullptr || e.second < n) {
+    if (e.first != nullptr) {  // (the stream's earlier launches may still use the old block)
+      if (hipStreamSynchronize(st) != hipSuccess) return nullptr;
+      (void)hipFree(e.first);
+      e.first = nullptr;
+    }
+    if (hipMalloc(&e.first, n * sizeof(unsigned long long)) != hipSuccess) {
+      e.first = nullptr;
+      return nullptr;
+    }
+    e.second = n;
+    if (hipMemsetAsync(e.first, 0, n * sizeof(unsigned long long), st) != hipSuccess) return nullptr;
+  }
+  return e.first;
 }
 
 // TDS_FUSED_FIN=0 restores the separate finalize launches (A/B timing and a fallback)

@@ -200,6 +200,8 @@ int tds_head_pb_nblk(int Q);  // workgroups per channel
 int tds_head_bwd_pb_nblk(int Q);  // the backward's workgroups per channel (its partial / gpart rows)
 // in-launch finalizer counters (launch_status.hip; common.h tds_arrive); nullptr: no fused finalize
 uint32_t* tds_sync_words(int site, hipStream_t st);
+// a zeroed u64 accumulator block per (device, stream, key) of >= n words (launch_status.hip)
+unsigned long long* tds_zeroed_u64(int key, size_t n, hipStream_t st);
 bool tds_fused_fin_enabled();  // TDS_FUSED_FIN=0: the separate finalize launches
 
 // partial: [32 * nblk + 32][B*NC] doubles; fused_fin: logits finished in the launch (B <= 8).

@@ -1,7 +1,8 @@
 // Border strips of the uint8 x moments, computed by one 256-thread workgroup per (image, side) inside
 // the launch that reduces the autocorrelation partials (convnet_fused.hip l1_reduce_gram_kernel):
 // strips[b][L][d] = sum over line L of x(u) x(u + d), d in [-4,4]^2, d index 81 = the plain line sum;
-// L 0,1 = rows 0,1, 2,3 = rows H-2,H-1, 4,5 = cols 0,1, 6,7 = cols W-2,W-1 (l1_build_gram's layout).
+// L 0,1 = rows 0,1, 2,3 = rows H-2,H-1, 4,5 = cols 0,1, 6,7 = cols W-2,W-1 (l1_build_gram's layout),
+// summed over the batch.
 // A side's six outermost lines (the two strip lines and every partner line a |d| <= 4 reaches
 // inside the image) go through LDS in chunks of BSIDE_CH positions, loaded once -- the
 // per-(d, line) workgroups of x_autocorr.hip's merged launch re-read every line 82 times, column
@@ -18,7 +19,7 @@ constexpr int BSIDE_LD = BSIDE_CH / 4 + 2;    // words per stored line: one pad 
 constexpr int BSIDE_LDS_WORDS = 6 * BSIDE_LD;
 constexpr int XMOM_MAX_LINE = 66051;          // longest line whose u32 sums cannot wrap
 
-// line chunks per side: one workgroup each (all in flight together), partial sums per chunk
+// line chunks per side: one workgroup each (all in flight together)
 __host__ __device__ inline int xmom_border_chunks(int H, int W) {
   return ((H > W ? H : W) + BSIDE_CH - 1) / BSIDE_CH;
 }
@@ -40,11 +41,12 @@ __device__ __forceinline__ uint32_t xm_win(uint32_t w0, uint32_t w1, uint32_t w2
        : s < 8 ? __builtin_amdgcn_alignbyte(w2, w1, s - 4) : w2;
 }
 
-// Chunk ch (of nch) of side 0 top, 1 bottom, 2 left, 3 right of image b -> strips[b][L][ch][82]
-// (its partial sums; chunks past the line write zeros); lines: BSIDE_LDS_WORDS words of LDS.  Every
-// thread of the workgroup must call it.  Results stored write-through (st_agent) for the reducer.
-__device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, double* __restrict__ strips, int b,
-                                                 int side, int ch, int nch, int H, int W, uint32_t* lines) {
+// Chunk ch (of nch) of side 0 top, 1 bottom, 2 left, 3 right of image b: its partial sums added
+// into sacc[L][82] (the batch's strips, exact u64 integer sums: any order gives the same value;
+// agent-scope atomics, which the reducer sees after tds_arrive's acquire); lines: BSIDE_LDS_WORDS
+// words of LDS.  Every thread of the workgroup must call it.
+__device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, unsigned long long* __restrict__ sacc,
+                                                 int b, int side, int ch, int nch, int H, int W, uint32_t* lines) {
   const bool rows = side < 2;
   const int N = rows ? W : H;                                  // positions along a line
   const int first = (side & 1) ? (rows ? H - 6 : W - 6) : 0;   // image row / col of stored line 0
@@ -131,17 +133,21 @@ __device__ __forceinline__ void x_border_side_u8(const uint8_t* __restrict__ x, 
     const int pr = 4 * m + wv;
     if (pr < 18) {
       const int tl = pr / 9, dd = pr % 9 - 4;
-      double* out = strips + (((int64_t)b * 8 + 2 * side + tl) * nch + ch) * 82;
+      unsigned long long* out = sacc + (2 * side + tl) * 82;
 #pragma unroll
       for (int s = 0; s < 9; ++s) {
         const uint32_t v = xm_wave_sum(acc[m][s]);
-        if (lane == 0) st_agent(out + (rows ? (dd + 4) * 9 + s : s * 9 + (dd + 4)), (double)v);
+        if (lane == 0 && v != 0u)
+          __hip_atomic_fetch_add(out + (rows ? (dd + 4) * 9 + s : s * 9 + (dd + 4)), (unsigned long long)v,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   }
   if (wv < 2) {
     const uint32_t v = xm_wave_sum(plain);
-    if (lane == 0) st_agent(strips + (((int64_t)b * 8 + 2 * side + wv) * nch + ch) * 82 + 81, (double)v);
+    if (lane == 0 && v != 0u)
+      __hip_atomic_fetch_add(sacc + (2 * side + wv) * 82 + 81, (unsigned long long)v, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
