@@ -1337,8 +1337,22 @@ __global__ __launch_bounds__(256) void l1_reduce_finalize_kernel(const double* _
     for (int i = 0; i < 32; ++i) t += sh[i][threadIdx.x];
     st_agent(bwd_sum + col, t);
   }
+  // the body's other inputs staged by every workgroup before the hand-off (the reducer learns it is
+  // last only after its sums; loaded then they were a round of latency on the critical path)
+  __shared__ double sg[650];
+  __shared__ float sw[16 * 25], sp[64];  // w1 | b1[16], gamma1[16] (1 if absent), stats1[32]
+  for (int i = threadIdx.x; i < 650; i += blockDim.x) sg[i] = gram[i];
+  for (int i = threadIdx.x; i < 16 * 25; i += blockDim.x) sw[i] = w1[i];
+  if (threadIdx.x < 64) {
+    const int i = threadIdx.x;
+    sp[i] = i < 16 ? b1[i] : i < 32 ? (gamma1 ? gamma1[i - 16] : 1.f) : stats1[i - 32];
+  }
   if (!tds_arrive(sync, gridDim.x, &last)) return;
-  l1_finalize_body(bwd_sum, gram, n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
+  __shared__ double sb[16 * LB_NACC];
+  for (int i = threadIdx.x; i < 16 * LB_NACC; i += blockDim.x) sb[i] = bwd_sum[i];
+  __syncthreads();
+  for (int e = threadIdx.x; e < 16 * 25; e += blockDim.x)
+    l1_finalize_one(e, sb, sg, n, sw, sp, sp + 16, sp + 32, dw1, db1, dgamma1, dbeta1, scale);
 }
 
 }  // namespace tds

@@ -27,6 +27,7 @@
 
 namespace tds {
 
+// (isolated op, r5_s35: 32 rows 48.1 - 48.6 us, 40: 47.0 - 48.6, 48: 45.8 - 46.2, 64: 45.3 - 46.7)
 #ifndef TDS_UM_RB
 #define TDS_UM_RB 48
 #endif
