@@ -75,6 +75,11 @@ class SGD(torch.optim.Optimizer):
                         ps.append(fp[pos:off])
                         gs.append(fg[pos:off])
                     pos = off + n
+                # small leftovers of the deferred ranges the owner wants stepped here, in this sweep
+                owner = getattr(runner, "__self__", None)
+                for off, n in (owner.take_inline_deferred() if hasattr(owner, "take_inline_deferred") else []):
+                    ps.append(fp[off:off + n])
+                    gs.append(fg[off:off + n])
                 if ps:
                     _ext.ops().sgd_step_(ps, gs, [], lr, 0.0, 0.0, 0.0, False, False)
                 runner(lambda off, n, _lr=lr: _ext.ops().sgd_step_([fp[off:off + n]], [fg[off:off + n]], [], _lr,

@@ -201,6 +201,7 @@ class DistributedDataParallel(nn.Module):
         self._fused_done = set()  # ids of params whose step ran inside their backward kernel
         self._deferred: List[_Bucket] = []
         self._deferred_works = {}
+        self.last_deferred_inline = False  # the last step's deferred leftovers went into the optimizer's sweep
         self._side = None
         if self.overlap_optimizer and big_layers:
             # with CUs split off for the collectives (utils/streams.py) the side work keeps to the
@@ -535,6 +536,25 @@ class DistributedDataParallel(nn.Module):
         if b.pending == 0:
             self._launch(b)
 
+    # (leftovers of the deferred buckets at most this many elements, with no collective behind them,
+    # are updated inline by the optimizer's own sweep: at world size 1 the fc weight's step runs in
+    # its backward kernel and only the fc bias is left -- on the side stream it cost the next head
+    # forward a cross-stream wait, an ~11 us gap in the step's timeline, r5_s36)
+    _INLINE_DEFERRED_MAX = 1 << 16
+
+    def take_inline_deferred(self):
+        """Flat (offset, numel) ranges of the deferred buckets the optimizer should update in its
+        own sweep on the current stream this step (see _INLINE_DEFERRED_MAX); they are skipped by
+        _run_deferred_update, which then fences only what it updates itself."""
+        self._inline_done = set()
+        if self.world_size != 1 or not self._deferred:
+            return []
+        left = [p for b in self._deferred for p in b.params if id(p) not in self._fused_done]
+        if not left or sum(p.numel() for p in left) > self._INLINE_DEFERRED_MAX:
+            return []
+        self._inline_done = {id(p) for p in left}
+        return [self._slots[id(p)] for p in left]
+
     def _run_deferred_update(self, update_fn):
         """Finish the deferred buckets on the side stream: wait for this step's
         backward (compute stream) and the bucket collective, apply ``update_fn(offset,
@@ -544,13 +564,23 @@ class DistributedDataParallel(nn.Module):
 
         cur = torch.cuda.current_stream(self.device)
         side = self._side
-        side.wait_stream(cur)
         done, self._fused_done = self._fused_done, set()
+        inline, self._inline_done = getattr(self, "_inline_done", set()), set()
+        works = {}
+        for b in self._deferred:
+            w = self._deferred_works.pop(b.index, None)
+            if w is None and self._native is not None:
+                w = self._native.take_work(b.index)
+            works[b.index] = w
+        self.last_deferred_inline = bool(inline) and all(w is None for w in works.values()) and all(
+            id(p) in done or id(p) in inline for b in self._deferred for p in b.params)
+        if self.last_deferred_inline:
+            return  # everything was stepped in its backward or inline by the optimizer: no side work, no fence
+        done = done | inline
+        side.wait_stream(cur)
         with torch.cuda.stream(side):
             for b in self._deferred:
-                w = self._deferred_works.pop(b.index, None)
-                if w is None and self._native is not None:
-                    w = self._native.take_work(b.index)
+                w = works[b.index]
                 if w is not None:
                     w.wait()  # side stream waits for the bucket all-reduce
                 if not done:
