@@ -424,3 +424,44 @@ def test_release_masked_streams(gpu):
     r = subprocess.run([sys.executable, "-c", _RELEASE_SCRIPT], cwd=repo, capture_output=True, text=True,
                        timeout=180)
     assert r.returncode == 0 and "release ok" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+def test_loss_in_head_with_activation_exchange(pg, gpu):
+    """The activation exchange's head forward (writing X rows) also forms the loss when the labels
+    come with the batch: same losses and parameters over two steps as without them."""
+    import copy
+
+    from torch_distributed_sandbox_amd.models import ConvNet, convnet_fused
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    torch.manual_seed(0)
+    H = 128
+    m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
+    m2 = copy.deepcopy(m1)
+    d1 = DistributedDataParallel(m1, grad_exchange="activations")
+    d2 = DistributedDataParallel(m2, grad_exchange="activations")
+    o1 = d1.attach_optimizer(SGD(m1.parameters(), 1e-3))
+    o2 = d2.attach_optimizer(SGD(m2.parameters(), 1e-3))
+    crit = CrossEntropyLoss()
+    g = torch.Generator(device=gpu).manual_seed(7)
+    before = convnet_fused.STATS["head_fused_ce"]
+    for _ in range(2):
+        x = torch.rand(3, 1, H, H, device=gpu, generator=g)
+        y = torch.randint(0, 10, (3,), device=gpu, generator=g)
+        x2 = x.clone()
+        convnet_fused.attach_labels(x2, y)
+        losses = []
+        for d, o, xi in ((d1, o1, x), (d2, o2, x2)):
+            loss = crit(d(xi), y)
+            o.zero_grad()
+            loss.backward()
+            o.step()
+            losses.append(loss)
+        assert torch.equal(losses[0], losses[1])
+    d1.wait_pending_updates()
+    d2.wait_pending_updates()
+    torch.cuda.synchronize()
+    assert convnet_fused.STATS["head_fused_ce"] >= before + 2
+    for p1, p2 in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(p1, p2)

@@ -486,7 +486,7 @@ Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor
 // logits then ops.cross_entropy, with the same arithmetic.  Returns (logits, loss, dlogits).
 std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, const Tensor& aff2, const Tensor& wfc,
                                                              const c10::optional<Tensor>& bfc, int64_t P,
-                                                             const Tensor& labels) {
+                                                             const Tensor& labels, const c10::optional<Tensor>& x_out) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_aff_ce: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_forward_aff_ce: needs P/2 >= 4 pooled columns and B >= 1");
@@ -498,6 +498,11 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, c
   need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
   need(labels, at::kLong, {B}, "labels");
   const float* bf = optf(bfc, NC, "fc.bias");
+  float* xo = nullptr;
+  if (x_out.has_value() && x_out->defined()) {  // (the activation exchange's fc input rows)
+    need(*x_out, at::kFloat, {B, 32 * Q * Q}, "x_out (fc input rows)");
+    xo = x_out->data_ptr<float>();
+  }
   c10::DeviceGuard guard(ya.device());
   hipStream_t st = stream_of(ya);
   const int nblk = 32 * tds_head_pb_nblk((int)Q);
@@ -508,7 +513,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, c
   auto loss = at::empty({}, ya.options());
   auto inv = at::empty({1}, ya.options());
   const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
-                                 part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), nullptr,
+                                 part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo,
                                  (int)B, (int)Q, (int)NC, st, true, labels.data_ptr<int64_t>(),
                                  dlogits.data_ptr<float>(), loss.data_ptr<float>(), inv.data_ptr<float>());
   TORCH_CHECK(rc >= 0, "fused_head_forward_aff_ce: unsupported shape");
@@ -1122,8 +1127,8 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       &fused_conv2_forward_bn);
   m.def("fused_head_forward_aff(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor(a!)? x_out=None) -> Tensor",
         &fused_head_forward_aff);
-  m.def("fused_head_forward_aff_ce(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor labels) -> "
-        "(Tensor, Tensor, Tensor)",
+  m.def("fused_head_forward_aff_ce(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor labels, "
+        "Tensor(a!)? x_out=None) -> (Tensor, Tensor, Tensor)",
         &fused_head_forward_aff_ce);
   m.def(
       "fused_head_forward_upd(Tensor ya, Tensor aff2, Tensor(a!) wfc, Tensor? bfc, int P, Tensor dy_all, Tensor meta_all, "

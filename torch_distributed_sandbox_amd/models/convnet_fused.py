@@ -318,9 +318,9 @@ class _Head(torch.autograd.Function):
                 dy_all, meta_all, vals_all, rows, scale, lr = fused_upd
                 STATS["head_fused_updates"] += 1
                 logits = ops.fused_head_forward_upd(ya, aff2, wfc, bfc, P, dy_all, meta_all, vals_all, rows, scale, lr)
-            elif link.labels is not None and x_out is None:
+            elif link.labels is not None:
                 # the loss and dlogits formed by the head forward's finalizing workgroup
-                logits, loss, dlogits = ops.fused_head_forward_aff_ce(ya, aff2, wfc, bfc, P, link.labels)
+                logits, loss, dlogits = ops.fused_head_forward_aff_ce(ya, aff2, wfc, bfc, P, link.labels, x_out)
                 link.ce = (link.labels, loss, dlogits)
                 STATS["head_fused_ce"] += 1
             else:
