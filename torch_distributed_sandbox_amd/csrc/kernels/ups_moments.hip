@@ -102,6 +102,12 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
   for (int i = 0; i < 42; ++i) acc[i] = 0u;
   uint32_t ring[5][9];
   const int r0 = band * UM_RB;
+  // the vertical taps of the wave's rows r0 .. r0 + UM_RB + 3, lane i holding row r0 + i's (read
+  // back per row with v_readlane: one instruction each instead of the tap arithmetic per row)
+  static_assert(UM_RB + 4 <= 64, "one lane per row of the band");
+  int ty0 = 0, ty1 = 0;
+  float tay = 0.f;
+  ups_taps(min(r0 + lane, H - 1), sy, h, ty0, ty1, tay);
   uint32_t* xrow = reinterpret_cast<uint32_t*>(x + ((int64_t)b * H + r0) * W) + q;
 #pragma unroll 1
   for (int i0 = 0; i0 < UM_RB + 4; i0 += 5) {
@@ -111,9 +117,8 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
       if (i < UM_RB + 4) {
         uint32_t cur = 0u;
         if (r < H) {
-          int y0, y1;
-          float ay;
-          ups_taps(r, sy, h, y0, y1, ay);
+          const int y0 = __builtin_amdgcn_readlane(ty0, i), y1 = __builtin_amdgcn_readlane(ty1, i);
+          const float ay = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, tay), i));
           if (y0 != ycur) {  // wave-uniform: a new vertical tap pair
             ycur = y0;
 #pragma unroll
