@@ -116,7 +116,7 @@ def _take_labels(x):
         return None
     labels = lb[1]
     if not (torch.is_tensor(labels) and labels.dtype == torch.int64 and labels.dim() == 1 and labels.is_cuda
-            and labels.shape[0] == x.shape[0] and labels.is_contiguous()):
+            and labels.device == x.device and labels.shape[0] == x.shape[0] and labels.is_contiguous()):
         return None
     return labels
 
