@@ -497,6 +497,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, c
   const int64_t NC = wfc.size(0);
   need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
   need(labels, at::kLong, {B}, "labels");
+  TORCH_CHECK(labels.device() == ya.device(), "fused_head_forward_aff_ce: labels must be on ya's device");
   const float* bf = optf(bfc, NC, "fc.bias");
   float* xo = nullptr;
   if (x_out.has_value() && x_out->defined()) {  // (the activation exchange's fc input rows)
