@@ -16,6 +16,7 @@
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -114,6 +115,11 @@ const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int n
   const int rc = tds_tile_order_fill(host.data_ptr<int>(), B, tiles_r, tiles_c, gr);
   TORCH_CHECK(rc == 0, "tdsa fused: tile order table needs B <= 255 and <= 4095 tiles per side (B=", B,
               ", tiles ", tiles_r, " x ", tiles_c, ")");
+#ifndef TDS_F2_REV
+#define TDS_F2_REV 0
+#endif
+  // TDS_F2_REV: the conv2 forward walks p1 last-to-first, the reverse of the layer-1 conv's writes
+  if (TDS_F2_REV != 0) std::reverse(host.data_ptr<int>(), host.data_ptr<int>() + total);
   // on the device as per-workgroup lists: work index t = w + kk * nwg at [w][kk] (rows =
   // ceil(total / nwg), the tail padded with the list's last entry), so one workgroup's
   // consecutive tiles share a scalar-cache line (16 entries) instead of one line each

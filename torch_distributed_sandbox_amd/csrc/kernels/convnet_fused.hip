@@ -328,7 +328,11 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
         if (prow < P && pcol < PW) {
           const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
           uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 2);  // 32-B record: fp16[16]
-          st_stream(dst + g, make_uint2(h01, h23));
+#ifndef TDS_L1_P1_NT
+#define TDS_L1_P1_NT 1
+#endif
+          if constexpr (TDS_L1_P1_NT != 0) st_stream(dst + g, make_uint2(h01, h23));
+          else dst[g] = make_uint2(h01, h23);
           st_stream(reinterpret_cast<uint32_t*>(idx1 + rec * 16) + g, ixw);
         }
       }
@@ -639,7 +643,12 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   // 256 threads), and lanes out of range read a zero vector.  (Loads under per-lane branches had
   // to land before the branches merged: the compiler waited for each one right after issuing it,
   // which serialised the whole prefetch.)
+#ifndef TDS_L1B_REV
+#define TDS_L1B_REV 0
+#endif
   auto load_tile = [&](int t) {
+    // TDS_L1B_REV: walk the tiles last-to-first, the reverse of the conv2 backward's dp1 writes
+    if constexpr (TDS_L1B_REV != 0) t = total - 1 - t;
     const int b = t / per_img, rem = t - b * per_img;
     const int pr0 = (rem / tiles_c) * LB_PR, pc0 = (rem % tiles_c) * LB_PC;
 #pragma unroll
