@@ -42,31 +42,38 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
 }
 
 // dw2[co][ci][tap] = sum_wg slab (fixed order, fp64), db2[co] = sum_wg slab[tap 25][co][0].
-// A block owns 64 consecutive slab elements; its 4 waves sum interleaved quarters of the
-// workgroup rows (w = 4j + wave, 8 loads in flight per lane), then wave 0 adds the four
-// partials in a fixed order: deterministic, and 4x the parallelism of one lane per element.
-__global__ __launch_bounds__(256) void conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nwg,
-                                                                 float* __restrict__ dw, float* __restrict__ db,
-                                                                 float scale) {
-  __shared__ double part[4][64];
+// A block owns 64 consecutive slab elements; its WGR_WAVES waves sum interleaved shares of the
+// workgroup rows (w = WGR_WAVES * j + wave, 16 loads in flight per lane, rows past the end clamped
+// and added as 0.0, which keeps the sum), then wave 0 adds the partials in a fixed order: deterministic.  At 4 waves the
+// 256 rows take 4 rounds of loads, at 16 one.
+#ifndef TDS_WGR_WAVES
+#define TDS_WGR_WAVES 16  // (r5_s47: 4.9 us at 4 waves with clamped loads, 4.8 at 16; guarded loads 20 us at 4)
+#endif
+constexpr int WGR_WAVES = TDS_WGR_WAVES;
+__global__ __launch_bounds__(64 * WGR_WAVES) void conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nwg,
+                                                                            float* __restrict__ dw,
+                                                                            float* __restrict__ db, float scale) {
+  constexpr int NW = WGR_WAVES;
+  __shared__ double part[NW][64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + lane;  // over 26*32*16
   double s = 0.0;
   if (e < 26 * 512) {
-    int w = wv;
-    for (; w + 28 < nwg; w += 32) {
-      float v[8];
+    for (int w = wv; w < nwg; w += 16 * NW) {
+      float v[16];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = slab[(int64_t)(w + 4 * k) * 26 * 512 + e];
+      for (int k = 0; k < 16; ++k) v[k] = slab[(int64_t)min(w + NW * k, nwg - 1) * 26 * 512 + e];  // (clamped:
+      // a load under a branch is waited for inside it, which serialises the batch)
 #pragma unroll
-      for (int k = 0; k < 8; ++k) s += (double)v[k];
+      for (int k = 0; k < 16; ++k) s += w + NW * k < nwg ? (double)v[k] : 0.0;
     }
-    for (; w < nwg; w += 4) s += (double)slab[(int64_t)w * 26 * 512 + e];
   }
   part[wv][lane] = s;
   __syncthreads();
   if (wv != 0 || e >= 26 * 512) return;
-  const double tot = ((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane];
+  double tot = part[0][lane];
+#pragma unroll
+  for (int i = 1; i < NW; ++i) tot += part[i][lane];
   const int tap = e / 512, co = (e / 16) & 31, ci = e & 15;
   const float v = (float)tot * scale;
   if (tap < 25) dw[(co * 16 + ci) * 25 + tap] = v;
@@ -89,7 +96,7 @@ int tds_conv2_num_wg() { return tds_device_cus(); }
 int tds_conv2_split() { return kConv2Split ? 1 : 0; }  // the build's conv2 operand precision (conv2_common.h)
 
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(256), 0, st, slab, nwg, dw, db, scale);
+  hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(64 * WGR_WAVES), 0, st, slab, nwg, dw, db, scale);
   TDS_LAUNCH_CHECK();
 }
 

@@ -1319,9 +1319,14 @@ __global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restri
 }
 
 // The layer-1 backward partials' reduction and the closed-form gradients in ONE launch: workgroup
-// e sums column e of the [rows][432] partials in reduce_partials_kernel's order (write-through),
-// the last to arrive runs l1_finalize_body.
-__global__ __launch_bounds__(256) void l1_reduce_finalize_kernel(const double* __restrict__ part, int nchunk,
+// e sums columns 8e .. 8e+7 of the [rows][432] partials in a fixed order (write-through), the last
+// to arrive runs l1_finalize_body.
+#ifndef TDS_L1RF_LANES
+#define TDS_L1RF_LANES 128  // row lanes per column (workgroup = 8 x lanes threads; 32: 11.8 us, 128: 10.3, r5_s47)
+#endif
+constexpr int L1RF_LANES = TDS_L1RF_LANES;
+static_assert(L1RF_LANES % 8 == 0 && L1RF_LANES >= 8 && L1RF_LANES <= 128, "l1_reduce_finalize lanes");
+__global__ __launch_bounds__(8 * L1RF_LANES) void l1_reduce_finalize_kernel(const double* __restrict__ part, int nchunk,
                                                                  double* __restrict__ bwd_sum, uint32_t* __restrict__ sync,
                                                                  const double* __restrict__ gram, int64_t n,
                                                                  const float* __restrict__ w1,
@@ -1332,18 +1337,41 @@ __global__ __launch_bounds__(256) void l1_reduce_finalize_kernel(const double* _
                                                                  float* __restrict__ dgamma1,
                                                                  float* __restrict__ dbeta1, float scale) {
   // 8 columns per workgroup (54 workgroups: one arrival each on the counter instead of 432 --
-  // same-address atomics serialize), 32 row lanes per column, row order fixed
-  __shared__ double sh[32][9];
+  // same-address atomics serialize), L1RF_LANES row lanes per column; each lane issues 16 loads
+  // together (rows past the end clamped and added as 0.0, which keeps the sum), so 1280 rows take one round of loads at
+  // 128 lanes and three at 32
+  constexpr int RL = L1RF_LANES;
+  __shared__ double sh[RL][9];
   __shared__ int last;
   const int col = blockIdx.x * 8 + (threadIdx.x & 7), rl = threadIdx.x >> 3;
   double s = 0.0;
-#pragma unroll 8
-  for (int k = rl; k < nchunk; k += 32) s += part[col + (int64_t)k * (16 * LB_NACC)];
+  for (int k = rl; k < nchunk; k += 16 * RL) {
+    double v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = part[col + (int64_t)min(k + j * RL, nchunk - 1) * (16 * LB_NACC)];  // (clamped:
+    // a load under a branch is waited for inside it, which serialises the batch)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) s += k + j * RL < nchunk ? v[j] : 0.0;
+  }
   sh[rl][threadIdx.x & 7] = s;
   __syncthreads();
+  // fold to at most 32 row sums per column (fixed order), then 8 threads sum those in order
+  __shared__ double sf[32][9];
+  double(*rows)[9] = sh;
+  if constexpr (RL > 32) {
+    if (threadIdx.x < 256) {
+      const int c = threadIdx.x & 7, p = threadIdx.x >> 3;
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < RL / 32; ++i) t += sh[p * (RL / 32) + i][c];
+      sf[p][c] = t;
+    }
+    __syncthreads();
+    rows = sf;
+  }
   if (threadIdx.x < 8) {
     double t = 0.0;
-    for (int i = 0; i < 32; ++i) t += sh[i][threadIdx.x];
+    for (int i = 0; i < (RL < 32 ? RL : 32); ++i) t += rows[i][threadIdx.x];
     st_agent(bwd_sum + col, t);
   }
   // the body's other inputs staged by every workgroup before the hand-off (the reducer learns it is
@@ -1504,7 +1532,7 @@ bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const
   uint32_t* sync = tds_sync_words(kSyncL1Fin, st);
   if (sync == nullptr) return false;
   static_assert((16 * LB_NACC) % 8 == 0, "8 columns per workgroup");
-  hipLaunchKernelGGL(l1_reduce_finalize_kernel, dim3(16 * LB_NACC / 8), dim3(256), 0, st, part, rows, bwd_sum, sync, gram,
+  hipLaunchKernelGGL(l1_reduce_finalize_kernel, dim3(16 * LB_NACC / 8), dim3(8 * L1RF_LANES), 0, st, part, rows, bwd_sum, sync, gram,
                      n, w1, b1, gamma1, stats1, dw1, db1, dgamma1, dbeta1, scale);
   TDS_LAUNCH_CHECK();
   return true;
