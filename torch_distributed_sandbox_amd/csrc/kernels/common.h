@@ -186,7 +186,10 @@ __device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
 // in group order.  A reducer that walked its rows as a dependent chain paid one global round trip
 // (~1-2 us) per step, which made the in-launch finalizers slower than the launches they replaced
 // (r5_s3).  Returns the column sum in threads t < ncols (0 elsewhere).  Needs ncols <= 256 and
-// nrows <= WRS_MAXL * (256 / ncols).  Every thread of the workgroup must call it.
+// 1 <= nrows <= WRS_MAXL * (256 / ncols).  Every thread of the workgroup must call it.
+// Rows past nrows are loaded CLAMPED to the last row and dropped at the add: with the load under
+// `r < nrows ? load : 0` the compiler put each load in its own branch and waited for it there, so
+// the "one round" was 16 dependent round trips (r5_s47, found in the ISA).
 constexpr int WRS_MAXL = 16;
 // (column c of row r at base + r * rstride + (c >> 1) * cstride2 + (c & 1): cstride2 = 2 for
 // contiguous rows; the conv2 forward's [channel][workgroup][2] partials use cstride2 = 2 * nwg)
@@ -200,11 +203,10 @@ __device__ __forceinline__ double wide_row_sum(const double* base, int nrows, in
     double v[WRS_MAXL];
 #pragma unroll
     for (int k = 0; k < WRS_MAXL; ++k) {
-      const int r = grp + k * G;
-      v[k] = r < nrows ? base[(int64_t)r * rstride + coff] : 0.0;
+      v[k] = base[(int64_t)min(grp + k * G, nrows - 1) * rstride + coff];  // (clamped, see above)
     }
 #pragma unroll
-    for (int k = 0; k < WRS_MAXL; ++k) s += v[k];
+    for (int k = 0; k < WRS_MAXL; ++k) s += grp + k * G < nrows ? v[k] : 0.0;
     part[grp * ncols + col] = s;
   }
   __syncthreads();
@@ -226,8 +228,7 @@ __device__ __forceinline__ uint32_t wide_row_max(const uint32_t* base, int nrows
     uint32_t v[WRS_MAXL];
 #pragma unroll
     for (int k = 0; k < WRS_MAXL; ++k) {
-      const int r = grp + k * G;
-      v[k] = r < nrows ? base[(int64_t)r * rstride + col] : 0u;
+      v[k] = base[(int64_t)min(grp + k * G, nrows - 1) * rstride + col];  // (clamped: a repeat leaves the max)
     }
 #pragma unroll
     for (int k = 0; k < WRS_MAXL; ++k) m = max(m, v[k]);

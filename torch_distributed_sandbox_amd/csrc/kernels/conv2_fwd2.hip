@@ -474,7 +474,8 @@ __device__ __forceinline__ void f2_finalize(const F2Fin& fin, const double* __re
   if (ypart != nullptr && tid < 32) {  // [co][nwg]: channel co's w0 .. w1-1 are contiguous
     uint32_t v[F2_GROUP];
 #pragma unroll
-    for (int u = 0; u < F2_GROUP; ++u) v[u] = w0 + u < w1 ? ypart[(int64_t)tid * nwg + w0 + u] : 0u;
+    for (int u = 0; u < F2_GROUP; ++u) v[u] = ypart[(int64_t)tid * nwg + min(w0 + u, w1 - 1)];  // (clamped: a repeat
+    // leaves the max; a guarded load is waited for inside its branch, common.h wide_row_sum)
     uint32_t m = 0u;
 #pragma unroll
     for (int u = 0; u < F2_GROUP; ++u) m = max(m, v[u]);

@@ -951,9 +951,9 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
     unsigned long long a[3];
     double c[6];
 #pragma unroll
-    for (int u = 0; u < 3; ++u) a[u] = tid + 256 * u < 8 * 82 ? sacc[tid + 256 * u] : 0ull;
+    for (int u = 0; u < 3; ++u) a[u] = sacc[min(tid + 256 * u, 8 * 82 - 1)];  // (clamped: used only in range below)
 #pragma unroll
-    for (int u = 0; u < 6; ++u) c[u] = tid + 256 * u < 16 * 81 + 16 ? cpg[tid + 256 * u] : 0.0;
+    for (int u = 0; u < 6; ++u) c[u] = cpg[min(tid + 256 * u, 16 * 81 + 15)];  // (clamped, as a[])
 #pragma unroll
     for (int u = 0; u < 3; ++u)
       if (tid + 256 * u < 8 * 82) {
@@ -971,12 +971,13 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
     // phase with the loads issued per sum)
     double t[3][16];
 #pragma unroll
+    // (loads clamped into range and dropped at the add: guarded ones were waited for one by one)
     for (int u = 0; u < 3; ++u) {
-      const int e = tid + 256 * u, L = e / 82, d = e - L * 82;
+      const int e = min(tid + 256 * u, 8 * 82 - 1), L = e / 82, d = e - L * 82;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
-        const int b = k / nch, ch = k - b * nch;
-        t[u][k] = (e < 8 * 82 && k < nv) ? strips_b[(((int64_t)b * 8 + L) * nch + ch) * 82 + d] : 0.0;
+        const int kc = min(k, nv - 1), b = kc / nch, ch = kc - b * nch;
+        t[u][k] = strips_b[(((int64_t)b * 8 + L) * nch + ch) * 82 + d];
       }
     }
 #pragma unroll
@@ -984,7 +985,7 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
       const int e = tid + 256 * u, L = e / 82, d = e - L * 82;
       double v = 0.0;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) v += t[u][k];
+      for (int k = 0; k < 16; ++k) v += (e < 8 * 82 && k < nv) ? t[u][k] : 0.0;
       for (int j = 16; j < nv; ++j) {  // (more than 16 image-chunks: the rest one by one)
         const int b = j / nch, ch = j - b * nch;
         v += strips_b[(((int64_t)b * 8 + L) * nch + ch) * 82 + d];

@@ -70,7 +70,7 @@ __global__ __launch_bounds__(64) void ups_moments_u8_kernel(const uint8_t* __res
     for (int i0 = 0; i0 < n4; i0 += 4 * 64) {
       uint32_t v[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = i0 + k * 64 + lane < n4 ? s4[i0 + k * 64 + lane] : 0u;
+      for (int k = 0; k < 4; ++k) v[k] = s4[min(i0 + k * 64 + lane, n4 - 1)];  // (clamped: used only in range)
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int i = i0 + k * 64 + lane;
