@@ -41,6 +41,20 @@ def test_store_single_process_ops():
         c.wait(["never"], datetime.timedelta(milliseconds=300))
 
 
+def test_store_timed_out_wait_does_not_desync():
+    """A WAIT that timed out stays registered on the server until its key appears; the late reply
+    must not be read as the answer to the client's next request (the client reconnects)."""
+    s = _store(0)
+    c = _store(s.port, server=False)
+    with pytest.raises(RuntimeError):
+        c.wait(["late_key"], datetime.timedelta(milliseconds=200))
+    s.set("late_key", b"")  # the server answers the stale WAIT now
+    s.set("other", b"value")
+    time.sleep(0.1)
+    assert c.get("other") == b"value"
+    assert c.add("n", 2) == 2 and c.get("late_key") == b""
+
+
 def _w_store_rdzv(rank, world, port, backend):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

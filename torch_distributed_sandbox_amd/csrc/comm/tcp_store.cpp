@@ -251,7 +251,7 @@ class TCPStore : public torch::CustomClassHolder {
       request(WAIT, key, "", nullptr);
       response(nullptr);
     } catch (...) {
-      set_rcv_timeout(fd_, timeout_ms_);
+      reconnect();
       throw;
     }
     set_rcv_timeout(fd_, timeout_ms_);
@@ -308,10 +308,26 @@ class TCPStore : public torch::CustomClassHolder {
     }
     send_all(fd_, msg.data(), msg.size());
   }
+  // A request whose reply did not arrive in time leaves the server holding it (a blocked GET / WAIT
+  // is answered when its key appears): on this connection that late reply would be read as the
+  // answer to the NEXT request. The failed caller's connection is replaced instead (the server drops
+  // the old one's waiters when it closes).
+  void reconnect() {
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = -1;
+    try {
+      fd_ = connect_to(host_, port_, timeout_ms_);
+      set_rcv_timeout(fd_, timeout_ms_);
+    } catch (...) {
+      fd_ = -1;  // the next call fails on the closed connection
+    }
+  }
   uint8_t response(std::string* out) {
     uint8_t st = 0;
-    if (!recv_all_nothrow(fd_, &st, 1))
+    if (!recv_all_nothrow(fd_, &st, 1)) {
+      reconnect();
       throw std::runtime_error("tds TCPStore: timed out / connection lost waiting for the store");
+    }
     std::string v = recv_str(fd_);
     if (st == 2) throw std::runtime_error("tds TCPStore: server error: " + v);
     if (out) *out = std::move(v);
