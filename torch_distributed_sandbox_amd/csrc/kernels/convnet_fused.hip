@@ -644,7 +644,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   // to land before the branches merged: the compiler waited for each one right after issuing it,
   // which serialised the whole prefetch.)
 #ifndef TDS_L1B_REV
-#define TDS_L1B_REV 0
+#define TDS_L1B_REV 1  // (layer-1 backward 129.8 -> 128.0 us r5_s44, 132.8 -> 129.8 r5_s50)
 #endif
   auto load_tile = [&](int t) {
     // TDS_L1B_REV: walk the tiles last-to-first, the reverse of the conv2 backward's dp1 writes
