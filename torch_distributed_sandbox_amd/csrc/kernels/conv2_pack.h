@@ -21,8 +21,9 @@ __device__ __forceinline__ void conv2_pack_block(const float* __restrict__ w2, s
     float4 v[13];  // all loads in flight first (3200 float4 over 256 threads)
 #pragma unroll
     for (int k = 0; k < 13; ++k) {
-      const int e = threadIdx.x + k * 256;
-      v[k] = e < 32 * 16 * 25 / 4 ? w4[e] : make_float4(0.f, 0.f, 0.f, 0.f);
+      // (clamped, not guarded: a guarded load is waited for inside its branch; a repeated element
+      // leaves the max unchanged)
+      v[k] = w4[min((int)threadIdx.x + k * 256, 32 * 16 * 25 / 4 - 1)];
     }
 #pragma unroll
     for (int k = 0; k < 13; ++k)  // NaN: ignored
