@@ -71,7 +71,9 @@ DTYPE_SPLIT = ("fp32 (conv1 fwd+wgrad: bf16x3 split-precision MFMA; conv2 fwd+dg
 DTYPE_TF32 = ("fp32 (conv2 fwd+dgrad+wgrad: TF32-class -- one fp16 MFMA per product, both operands rounded to 11 "
               "significant bits = TF32's significand, exact power-of-two range scaling, fp32 accumulate: the arithmetic "
               "of the reference's default cuDNN TF32 convolutions; conv1 fwd+wgrad: bf16x3 split MFMA (~2^-16); BN, fc, "
-              "CE, SGD: fp32)")
+              "CE, SGD: fp32; stored in fp16 at exact power-of-two scales (11 significant bits): the conv2 output the "
+              "backward re-reads (y2h; BN2 statistics, pooled values and argmax from fp32) and the conv2 data gradient "
+              "(dp1h) -- docs/KERNELS.md 'y2h', 'dp1h')")
 
 
 def _dtype(on_gpu: bool = True) -> str:
@@ -162,6 +164,15 @@ def _parser():
     ap.add_argument("--step-times", action="store_true",
                     help="record each timed step's GPU time with events (config.step_ms; diagnostics)")
     ap.add_argument("--lr", type=float, default=1e-4, help="SGD learning rate (reference: 1e-4)")
+    ap.add_argument("--transport-tune", action=argparse.BooleanOptionalAction, default=None,
+                    help="before the model is built, time the fc exchange's collectives at each candidate "
+                         "(reserve-cus, rccl-max-ctas) on the live node and take the one with the lowest predicted "
+                         "step time (parallel/transport_tune.py; config.preflight.transport).  Default: on at "
+                         "world > 1 on rccl-native unless --reserve-cus / --rccl-max-ctas is given")
+    ap.add_argument("--store", default="native", choices=["native", "c10d"],
+                    help="rendezvous store (world > 1 or a forced exchange): this package's C++ TCP store, located "
+                         "through c10d's at MASTER_ADDR:MASTER_PORT (the agreed fallback), or c10d's only; "
+                         "TDS_STORE overrides.  The torch-RCCL fallback tiers always use c10d's")
     ap.add_argument("--fallback", action=argparse.BooleanOptionalAction, default=None,
                     help="after a failed rccl-native attempt, run once more on torch's RCCL process group with "
                          "the plain bucket all-reduce (default: on unless --backend is given)")
@@ -378,15 +389,20 @@ def run_rank(argv) -> int:
 
 def _make_store(args, rank: int, world: int):
     """The rendezvous store every attempt shares (each attempt under its own prefix), so the
-    ranks can agree on a fallback even when a communicator could not be created."""
+    ranks can agree on a fallback even when a communicator could not be created: this package's
+    C++ store (parallel/store.py ``rendezvous``; c10d's TCPStore at MASTER_ADDR:MASTER_PORT only
+    locates it, and replaces it on every rank if some rank cannot use it).  Returns (store, kind,
+    c10d store): the last one carries the rendezvous of the torch-RCCL fallback tiers, which run
+    torch's stack top to bottom."""
     import datetime
 
-    import torch.distributed as dist
+    from torch_distributed_sandbox_amd.parallel.store import rendezvous
 
-    addr = os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    port = int(os.environ.setdefault("MASTER_PORT", "29533"))
-    return dist.TCPStore(addr, port, world, is_master=(rank == 0),
-                         timeout=datetime.timedelta(seconds=args.pg_timeout), wait_for_workers=True)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    store, kind = rendezvous(rank, world, timeout=datetime.timedelta(seconds=args.pg_timeout),
+                             prefer=os.environ.get("TDS_STORE") or args.store)
+    return store, kind, getattr(store, "_locator", store)
 
 
 def _run_attempts(args, world: int, rank: int, phase):
@@ -414,11 +430,26 @@ def _run_attempts(args, world: int, rank: int, phase):
             if all((a[0], a[1]) != tier[:2] for a in attempts):
                 attempts.append(tier)
     dist_needed = world > 1 or args.grad_exchange in ("activations", "sharded", "chunked")
-    store = _make_store(args, rank, world) if dist_needed else None
+    store, store_kind, c10d_store = _make_store(args, rank, world) if dist_needed else (None, None, None)
     # a collective that stalls raises (after --pg-timeout) instead of killing the rank, so the
     # ranks can still agree on the fallback and report
     os.environ.setdefault("TDS_RCCL_ERROR_HANDLING", "raise")
     os.environ.setdefault("TDS_RCCL_INIT_TIMEOUT_MS", str(int(args.pg_timeout * 1000)))
+    tune = args.transport_tune
+    if tune is None:
+        tune = (world > 1 and on_gpu and backend == "rccl-native" and args.reserve_cus is None
+                and not args.rccl_max_ctas)
+    transport = None
+    if tune and backend == "rccl-native" and on_gpu and store is not None:
+        phase[0] = "transport tune"
+        transport = _tune_transport(args, store, rank, world)
+        ch = transport.get("chosen")
+        if ch is not None:
+            attempts[0] = (attempts[0][0], attempts[0][1], ch["reserve_cus"], attempts[0][3])
+            if ch["max_ctas"] > 0:
+                os.environ["TDS_RCCL_MAX_CTAS"] = str(ch["max_ctas"])
+            else:
+                os.environ.pop("TDS_RCCL_MAX_CTAS", None)
     reason = None
     for k, (be, gx, reserve, lab) in enumerate(attempts):
         if reason is not None:
@@ -426,7 +457,13 @@ def _run_attempts(args, world: int, rank: int, phase):
         last = k == len(attempts) - 1
         ok, err, rec = True, None, None
         try:
-            rec = _attempt(args, world, rank, be, gx, reserve, lab, store, k, phase)
+            # torch's own process group (the fallback tiers) rendezvouses on c10d's store
+            st, st_kind = (c10d_store, "c10d") if be == "rccl" and store is not None else (store, store_kind)
+            rec = _attempt(args, world, rank, be, gx, reserve, lab, st, k, phase)
+            if rec is not None:
+                rec["config"]["store"] = st_kind
+                if transport is not None:
+                    rec["config"].setdefault("preflight", {})["transport"] = transport
         except Exception as e:  # noqa: BLE001
             ok, err = False, f"{type(e).__name__}: {_short(str(e))}"
             if last:
@@ -463,6 +500,87 @@ def _run_attempts(args, world: int, rank: int, phase):
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
     return None
+
+
+def _tune_transport(args, store, rank: int, world: int) -> dict:
+    """parallel/transport_tune.py on the live node: for each candidate (reserve_cus, max_ctas), a
+    process group on this package's communicator with that split, the collectives the step's fc
+    exchange will issue at their real sizes (the path ``auto`` picks, zero-suppressed at the
+    expected ratio) timed -- max over ranks -- then torn down.  Rank 0's choice is everyone's."""
+    import datetime
+
+    import torch.distributed as dist
+
+    from torch_distributed_sandbox_amd.parallel import distributed as tdist
+    from torch_distributed_sandbox_amd.parallel import transport_tune as TT
+
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = torch.device("cuda", local_rank)
+    K = 32 * (args.image_size // 4) ** 2
+    path, colls = TT.step_collectives(max(2, world), args.batch_size, 10, K)
+    n_probe = [0]
+
+    def measure(cfg):
+        i = n_probe[0]
+        n_probe[0] += 1
+        saved = os.environ.get("TDS_RCCL_MAX_CTAS")
+        if cfg.max_ctas > 0:
+            os.environ["TDS_RCCL_MAX_CTAS"] = str(cfg.max_ctas)
+        else:
+            os.environ.pop("TDS_RCCL_MAX_CTAS", None)
+        try:
+            tdist.init_process_group("rccl-native", rank=rank, world_size=world,
+                                     store=dist.PrefixStore(f"tune{i}", store),
+                                     timeout=datetime.timedelta(seconds=args.pg_timeout), device_id=local_rank,
+                                     comm_cus=cfg.reserve_cus)
+            try:
+                issue = []
+                for kind, nbytes in colls:
+                    n = max(1, nbytes // 4)
+                    if kind == "all_gather":
+                        inp = torch.ones(n, device=dev)
+                        out = torch.empty(world * n, device=dev)
+                        issue.append(lambda out=out, inp=inp: tdist.all_gather_into_tensor(out, inp))
+                    elif kind == "sendrecv":
+                        sb = [torch.ones(n, device=dev) for _ in range(world)]
+                        rb = [torch.empty(n, device=dev) for _ in range(world)]
+                        peers = [r for r in range(world) if r != rank]
+                        issue.append(lambda sb=sb, rb=rb, peers=peers: tdist.sendrecv(
+                            [(sb[r], r) for r in peers], [(rb[r], r) for r in peers]).wait())
+                    else:
+                        t = torch.ones(n, device=dev)
+                        issue.append(lambda t=t: tdist.all_reduce(t, tdist.ReduceOp.AVG))
+                best = None
+                for _ in range(3):  # the first pays RCCL's lazy channel setup
+                    tdist.barrier()
+                    torch.cuda.synchronize(dev)
+                    t0 = time.perf_counter()
+                    for f in issue:
+                        f()
+                    torch.cuda.synchronize(dev)
+                    dt = time.perf_counter() - t0
+                    best = dt if best is None else min(best, dt)
+                g = torch.tensor([best], device=dev, dtype=torch.float64)
+                tdist.all_reduce(g, tdist.ReduceOp.MAX)
+                return float(g.item()) * 1e3
+            finally:
+                _teardown(abort=False)
+        finally:
+            if saved is None:
+                os.environ.pop("TDS_RCCL_MAX_CTAS", None)
+            else:
+                os.environ["TDS_RCCL_MAX_CTAS"] = saved
+            torch.cuda.empty_cache()
+
+    res = TT.choose(measure)
+    res["path"] = path
+    res["bytes_per_rank"] = [b for _, b in colls]
+    # one decision for all ranks (a candidate may fail on one rank only)
+    if rank == 0:
+        store.set("bench/transport", json.dumps(res))
+    else:
+        res = json.loads(store.get("bench/transport").decode())
+    return res
 
 
 def _teardown(abort: bool) -> None:

@@ -55,6 +55,96 @@ def test_store_timed_out_wait_does_not_desync():
     assert c.add("n", 2) == 2 and c.get("late_key") == b""
 
 
+def test_store_client_fails_fast_when_server_is_gone():
+    """A client whose server exited (rank 0 at teardown or after a crash) must fail at once --
+    not retry a connect for its whole timeout (here 60 s) -- on a plain request, on a WAIT that
+    was blocked when the server went away, and on every later call."""
+    s = _store(0, timeout_s=60)
+    c = _store(s.port, server=False, timeout_s=60)
+    s.set("k", b"v")
+    assert c.get("k") == b"v"
+    err = []
+
+    def blocked_wait():
+        try:
+            c.wait(["never"], datetime.timedelta(seconds=60))
+        except RuntimeError as e:
+            err.append((time.monotonic(), str(e)))
+
+    t = threading.Thread(target=blocked_wait)
+    t.start()
+    time.sleep(0.3)
+    t_stop = time.monotonic()
+    del s  # rank 0's store object: its server thread stops and closes every connection
+    t.join(timeout=10)
+    assert not t.is_alive() and err, "the blocked WAIT did not fail when the server went away"
+    assert err[0][0] - t_stop < 5 and "lost" in err[0][1], err
+    for op in (lambda: c.get("k"), lambda: c.set("a", b"b"), lambda: c.add("n", 1)):
+        t0 = time.monotonic()
+        with pytest.raises(RuntimeError, match="lost"):
+            op()
+        assert time.monotonic() - t0 < 5
+
+
+def _w_store_8rank_traffic(rank, world, port, out_dir):
+    """The rendezvous traffic of a real job through the default (native) store: the process
+    group's init, the RCCL communicator's ncclUniqueId exchange (the real ncclGetUniqueId bytes,
+    rccl_backend.exchange_unique_id), and the reference's per-step new_group -- 1000 calls
+    (mnist_distributed.py:99-100) -- plus real subgroup creations and collectives on them."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.pop("TDS_STORE", None)
+    from torch_distributed_sandbox_amd.parallel import distributed as dist
+    from torch_distributed_sandbox_amd.parallel.rccl_backend import exchange_unique_id
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    assert dist.store_kind() == "native", dist.store_kind()
+    store = dist._state["store"]
+    uids = [bytes(exchange_unique_id(store, rank, key=f"uid/{i}").numpy().tobytes()) for i in range(8)]
+    assert all(len(u) == 128 for u in uids) and len(set(uids)) == 8
+    with open(os.path.join(out_dir, f"uid{rank}"), "wb") as f:
+        f.write(b"".join(uids))
+    g0 = None
+    for step in range(1000):
+        g = dist.new_group(list(range(world)))
+        g0 = g if g0 is None else g0
+        assert g is g0
+    subs = [list(range(k)) for k in range(2, world + 1)] + [[r, (r + 1) % world] for r in range(world)]
+    for ranks in subs:
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            t = torch.tensor([float(rank)])
+            dist.all_reduce(t, group=g)
+            assert t.item() == float(sum(ranks))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_native_store_carries_8_rank_rendezvous(tmp_path):
+    launch.spawn(_w_store_8rank_traffic, args=(8, launch.find_free_port(), str(tmp_path)), nprocs=8, timeout=240)
+    blobs = {open(tmp_path / f"uid{r}", "rb").read() for r in range(8)}
+    assert len(blobs) == 1  # every rank got rank 0's ids
+
+
+def test_rendezvous_falls_back_to_c10d_on_every_rank():
+    """A native store rank 0 cannot create: every rank ends up on c10d's store and says why."""
+    from torch_distributed_sandbox_amd.parallel import store as S
+
+    class _Broken:
+        def __init__(self, *a, **k):
+            raise RuntimeError("no native store here")
+
+    real = S.NativeStore
+    S.NativeStore = _Broken
+    try:
+        st, kind = S.rendezvous(0, 1, port=launch.find_free_port(), timeout=datetime.timedelta(seconds=10))
+    finally:
+        S.NativeStore = real
+    assert kind.startswith("c10d (fallback: rank 0: RuntimeError: no native store here")
+    st.set("k", "v")
+    assert st.get("k") == b"v"
+
+
 def _w_store_rdzv(rank, world, port, backend):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

@@ -56,6 +56,59 @@ def test_collectives(world, backend):
     launch.spawn(_w_collectives, args=(world, launch.find_free_port(), backend), nprocs=world, timeout=180)
 
 
+# ---------------------------------------------------------------- lazy gradient slots
+@pytest.mark.parametrize("reducer", ["native", "python"])
+def test_big_layer_grad_slot_allocated_on_first_use(reducer):
+    """The big fc layer's weight slot is the flat gradient layout's tail and gets storage only
+    when a gradient is written there (parallel/ddp.py ``_lazy_from``; at world size 1 on the GPU
+    the fused update never writes one, tests/test_fullscale_plan_gpu.py).  A plain backward grows
+    the buffer once: every .grad is a view of the grown buffer, gradients and the flat SGD sweep
+    match torch."""
+    from torch_distributed_sandbox_amd.models import ConvNet
+    from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss
+    from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
+
+    H = 256  # fc 10 x 131072: an exchange candidate (>= 2^20 elements)
+    torch.manual_seed(0)
+    m = ConvNet(image_shape=(H, H))
+    ref = copy.deepcopy(m)
+    ddp = DistributedDataParallel(m, reducer=reducer)
+    assert ddp.reducer_kind == reducer
+    w = m.fc.weight
+    o, n = ddp._slots[id(w)]
+    assert o == ddp._lazy_from and o + n == ddp._total
+    assert ddp.flat_grad.numel() == ddp._lazy_from
+    assert ddp.grad_storage_bytes() < w.numel() * 4 // 10
+    assert ddp.bucket_layout()[0][2] == [(10,), (10, 32 * (H // 4) ** 2)]  # ready order kept
+    for p, q in zip(m.parameters(), ref.parameters()):
+        assert torch.equal(p, q)
+        assert p.data.untyped_storage().data_ptr() == ddp.flat_param.untyped_storage().data_ptr()
+    opt = ddp.attach_optimizer(SGD(m.parameters(), 0.05))
+    ropt = torch.optim.SGD(ref.parameters(), 0.05)
+    crit = CrossEntropyLoss()
+    g = torch.Generator().manual_seed(3)
+    ptr = None
+    for step in range(2):
+        x = torch.rand(2, 1, H, H, generator=g)
+        y = torch.randint(0, 10, (2,), generator=g)
+        opt.zero_grad()
+        crit(ddp(x), y).backward()
+        fg = ddp.flat_grad
+        assert fg.numel() == ddp._total
+        ptr = fg.data_ptr() if ptr is None else ptr
+        assert fg.data_ptr() == ptr  # grown once, in the first backward
+        for p in m.parameters():
+            assert p.grad.untyped_storage().data_ptr() == fg.untyped_storage().data_ptr()
+        ropt.zero_grad()
+        crit(ref(x), y).backward()
+        for (nm, p), q in zip(m.named_parameters(), ref.parameters()):
+            assert torch.allclose(p.grad, q.grad, rtol=1e-4, atol=1e-7), nm
+        opt.step()
+        ropt.step()
+        for (nm, p), q in zip(m.named_parameters(), ref.parameters()):
+            assert torch.allclose(p, q, rtol=1e-5, atol=1e-7), nm
+
+
 # ---------------------------------------------------------------- DDP equivalence
 def _w_ddp(rank, world, port, H, B, backend="gloo"):
     dist = _init(rank, world, port, backend)

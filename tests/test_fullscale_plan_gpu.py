@@ -92,6 +92,11 @@ def test_two_steps_of_the_benchmarked_plan_vs_fp64(gpu):
         torch.cuda.synchronize()
         # optimizer-in-backward at world 1: the fc step ran inside the head backward kernel
         assert model.fc.weight.grad is None
+        # ... so the fc weight's gradient slot was never allocated (parallel/ddp.py _lazy_from):
+        # the flat gradient buffer holds the conv/BN slots and the fc bias only
+        fc_slot = ddp._slots[id(model.fc.weight)]
+        assert ddp.flat_grad.numel() == ddp._lazy_from == fc_slot[0] < ddp._total
+        assert ddp.grad_storage_bytes() < 1 << 20
         ours.append({"logits": out.detach().clone(), "loss": loss.detach().clone(),
                      "params": {n: p.detach().clone() for n, p in model.named_parameters()},
                      "buffers": {n: b.detach().clone() for n, b in model.named_buffers()}})

@@ -129,6 +129,21 @@ def test_cross_entropy(gpu):
     _close(dz2, zr2.grad, 1e-6, 1e-6)
 
 
+def test_cross_entropy_out_of_range_label_gives_nan(gpu):
+    """torch raises 'Target out of bounds'; the kernel cannot raise, so a label outside [0, N)
+    (not ignore_index) makes the loss and that row's dlogits NaN -- never a read past the row.
+    The other rows' dlogits are unchanged."""
+    torch.manual_seed(0)
+    z = torch.randn(4, 10, device=gpu)
+    for bad in (10, -1, 1 << 40):
+        lab = torch.tensor([1, bad, 3, -100], device=gpu)
+        loss, dz = _ops().cross_entropy(z, lab, -100, 0.0)
+        torch.cuda.synchronize()
+        assert torch.isnan(loss).all()
+        assert torch.isnan(dz[1]).all()
+        assert torch.isfinite(dz[[0, 2, 3]]).all()
+
+
 def test_cross_entropy_backward_seeds(gpu):
     """TF.backward(loss) (cached unit seed, no scale kernel) == loss.backward() == 2x for a 2 seed."""
     from torch_distributed_sandbox_amd.ops import functional as TF

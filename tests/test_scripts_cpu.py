@@ -102,6 +102,7 @@ def test_bench_self_spawns_ranks_cpu():
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["warmup"] == 1
     assert r["config"]["global_batch"] == 10 and r["config"]["parallelism"] == "dp2"
     assert r["config"]["backend"] == "gloo" and r["value"] > 0
+    assert r["config"]["store"] == "native"  # the C++ rendezvous store (parallel/store.py rendezvous)
     assert r["dtype"] == "fp32 (CPU rehearsal: torch ops)"
     (pr,) = r["config"]["allreduce_probe"]  # post-timing all-reduce bandwidth over the same communicator
     assert pr["MB"] > 0 and pr["ms"] > 0 and pr["busbw_GBps"] > 0
@@ -150,6 +151,7 @@ def test_bench_w8_cpu(backend):
     assert r["n_gpus"] == 8 and r["config"]["global_batch"] == 40 and r["config"]["parallelism"] == "dp8"
     assert r["config"]["fc_grad"] == "sharded-exchange(zs)"  # zero-suppressed X shards (parallel/zs.py)
     assert r["config"]["reducer"] == ("native" if backend == "host" else "python")
+    assert r["config"]["store"] == "native"
 
 
 def test_bench_rank_that_never_joins_reports_json():
@@ -191,6 +193,7 @@ def test_bench_falls_back_after_a_failed_attempt_cpu():
     assert r["value"] > 0 and r["config"]["attempt"] == 1
     assert r["config"]["backend"].startswith("gloo (fallback: rank 1")
     assert "InjectedFault" in r["config"]["backend"]
+    assert r["config"]["store"] == "native"  # the vote and both attempts' rendezvous went through it
 
 
 def test_trainer_and_bench_pick_the_same_stack(monkeypatch):
@@ -234,6 +237,7 @@ def test_bench_under_torchrun_cpu():
     assert p.returncode == 0, p.stderr[-3000:]
     (r,) = _json_lines(p.stdout)
     assert r["n_gpus"] == 2 and r["steps"] == 2 and r["value"] > 0 and r["config"]["parallelism"] == "dp2"
+    assert r["config"]["store"] == "native"  # located through torchrun's agent store
 
 
 def test_bench_under_torchrun_falls_back_cpu():
@@ -262,6 +266,7 @@ def test_bench_fallback_tiers_keep_the_exchange_cpu(world, phase):
     c = r["config"]
     assert r["value"] > 0 and c["attempt"] == 1 and c["tier"] == "2/3"
     assert c["backend"].startswith("gloo (fallback: rank 1") and f"phase {phase}" in c["backend"]
+    assert c["store"] == "native"
     want = "activation-exchange(zs)" if world == 2 else "sharded-exchange(zs)"
     assert c["fc_grad"] == want
     pf = c["preflight"]

@@ -16,7 +16,7 @@ fitting 288 GB is much larger.  This script:
    mp.spawn) or under torchrun with N ranks: step 2 runs on rank 0 alone, step 3 is the
    DDP run over all ranks, effective batch 5N.
 
-    python tools/oom_demo.py                                     # 1 GPU, 23000^2
+    python tools/oom_demo.py                                     # 1 GPU, just past the batch-10 edge
     python tools/oom_demo.py --gpus 8                            # the DDP half: 8 ranks
 
 Round 4 re-measured the plan at HEAD (uint8 level input, fp16 p1): at 18000^2 a batch of 10
@@ -39,16 +39,22 @@ import torch  # noqa: E402
 
 # Memory model of the fused plan at HEAD, peak(H, B) = (act * B + fixed) * H^2 bytes, calibrated on
 # this GPU by two short runs at --calib-size (batch 1 and 2): act = bytes per input pixel per image
-# (x, p1 hi|lo, argmax, y2, ya, g2m, dp1, ...), fixed = per-pixel bytes that do not scale with the
-# batch (fc weight + gradient = 2 * 10 * 32 * (H/4)^2 * 4 B = 80 B/px, DDP flat buffers, ...).
+# (x levels, p1, argmax codes, y2h, ya, g2m, dp1h, ...), fixed = per-pixel bytes that do not scale
+# with the batch: the fc weight, 10 * 32 * (H/4)^2 * 4 B = 80 B/px, held once in DDP's flat parameter
+# buffer.  Its GRADIENT is not a fixed cost of this plan: the runs below train as bench.py and the
+# trainer do (DistributedDataParallel(overlap_optimizer=True), plain SGD), so at world size 1 the fc
+# weight steps inside the head backward kernel and its 80 B/px gradient slot is never allocated
+# (parallel/ddp.py _lazy_from; round 4's record still carried it: 39.4 GiB at 23000^2).  The DDP
+# constructor holds the flat buffer and one original parameter at a time (2 x 80 B/px, before any
+# activation exists).
 
 
 def calibrate(H, device):
-    a = run(H, 1, 1, device, 1, 0)["peak_gb"] * 1e9
-    b = run(H, 2, 1, device, 1, 0)["peak_gb"] * 1e9
+    ra, rb = run(H, 1, 1, device, 1, 0), run(H, 2, 1, device, 1, 0)
+    a, b = ra["peak_gb"] * 1e9, rb["peak_gb"] * 1e9
     act = (b - a) / (H * H)
     fixed = a / (H * H) - act
-    return act, fixed
+    return act, fixed, [ra, rb]
 
 
 def predicted_bytes(H, B, act, fixed):
@@ -62,11 +68,14 @@ def run(H, B, steps, device, world, rank):
     from torch_distributed_sandbox_amd.ops import functional as TF
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
 
+    gc.collect()
+    torch.cuda.empty_cache()
     torch.cuda.reset_peak_memory_stats(device)
+    base = torch.cuda.memory_allocated(device)  # anything a previous run left (should be ~0)
     torch.manual_seed(0)
     model = ConvNet(image_shape=(H, H), device=device)
     opt = SGD(model.parameters(), 1e-4)
-    ddp = DistributedDataParallel(model, device_ids=[device.index])
+    ddp = DistributedDataParallel(model, device_ids=[device.index], overlap_optimizer=True)
     ddp.attach_optimizer(opt)
     crit = CrossEntropyLoss()
     src, lab = synthetic_batch(B, (H, H), device, seed=7 + rank)
@@ -75,25 +84,30 @@ def run(H, B, steps, device, world, rank):
         images = TF.upsample_bilinear_u8(src, H, H, levels=True)  # the bench / trainer default input
         loss = crit(ddp(images), lab)
         opt.zero_grad()
-        loss.backward()
+        TF.backward(loss)
         opt.step()
+        ddp.wait_pending_updates()
         if i == 0:
             torch.cuda.synchronize()
             t0 = time.perf_counter()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / max(1, steps - 1) if steps > 1 else None
     peak = torch.cuda.max_memory_allocated(device)
+    grad_gb = ddp.grad_storage_bytes() / 1e9
     del ddp, model, opt, images, loss
     gc.collect()
     torch.cuda.empty_cache()
-    return {"batch_per_rank": B, "peak_gb": round(peak / 1e9, 2),
+    return {"batch_per_rank": B, "peak_gb": round((peak - base) / 1e9, 3), "base_gb": round(base / 1e9, 3),
+            "flat_grad_gb": round(grad_gb, 4),
             "ms_per_step": round(dt * 1e3, 2) if dt else None,
             "images_per_sec_node": round(world * B / dt, 2) if dt else None}
 
 
 def _parser():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--image-size", type=int, default=23000)
+    ap.add_argument("--image-size", type=int, default=0,
+                    help="0 (default): just past the calibrated model's batch-10 edge (batch 10 predicted at "
+                         ">= 106 %% of the GPU's memory), rounded up to a multiple of 500")
     ap.add_argument("--bs-fail", type=int, default=10)
     ap.add_argument("--bs-fit", type=int, default=5)
     ap.add_argument("--steps", type=int, default=3)
@@ -131,15 +145,21 @@ def main(argv=None):
     device = torch.device("cuda", local)
     H = args.image_size
     rec = None
+    if H <= 0 and world > 1:
+        raise SystemExit("oom_demo: --image-size 0 (auto) is for one process; give the size for --gpus > 1")
     if rank == 0:
         # the single-GPU half runs on rank 0 BEFORE the process group exists (DDP at world size
         # 1, no collective); the other ranks wait in the rendezvous meanwhile
         total = torch.cuda.get_device_properties(device).total_memory
-        act, fixed = calibrate(args.calib_size, device)
+        act, fixed, calib_runs = calibrate(args.calib_size, device)
         gc.collect()
         torch.cuda.empty_cache()
+        if H <= 0:
+            edge = (1.06 * total / (args.bs_fail * act + fixed)) ** 0.5
+            H = int(-(-edge // 500) * 500)
         rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1), "world_size": world,
-               "model": {"calibrated_at": args.calib_size, "act_bytes_per_px_per_image": round(act, 1),
+               "model": {"calibrated_at": args.calib_size, "calibration_runs": calib_runs,
+                         "act_bytes_per_px_per_image": round(act, 1),
                          "fixed_bytes_per_px": round(fixed, 1),
                          "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed) / 1e9, 1)
                                           for b in (args.bs_fit, args.bs_fail)},

@@ -78,17 +78,17 @@ def main():
                 derived.append(("HBM write GB/s (WRITE_SIZE KB / profiled time)",
                                 cs["WRITE_SIZE"] * 1024 / (pass_time("WRITE_SIZE") * 1e3)))
             if "SQ_VALU_MFMA_BUSY_CYCLES" in cs:
-                # summed over the SIMDs (ASSUMED 1024 = 256 CUs x 4).  Clock: measured from
-                # GRBM_GUI_ACTIVE (summed over the 8 XCDs) when that counter was collected,
-                # otherwise an ASSUMED 2.4 GHz -- the label says which
+                # summed over the SIMDs (ASSUMED 1024 = 256 CUs x 4), priced at a FIXED 2.4 GHz (the
+                # MI355X peak engine clock: an upper bound on the cycles available, so the fraction
+                # is a lower bound).  GRBM_GUI_ACTIVE / 8 / time is shown beside it only as a
+                # diagnostic: for kernels of a few hundred us it reads 3.0-3.5 GHz (counter skew
+                # across the 8 XCDs around short dispatches), which is not a physical clock
                 tm = pass_time("SQ_VALU_MFMA_BUSY_CYCLES")
+                derived.append(("MFMA busy fraction (MFMA_BUSY / 1024 SIMDs / (profiled time x 2.4 GHz))",
+                                cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (tm * 1e-6 * 2.4e9)))
                 if cs.get("GRBM_GUI_ACTIVE", 0) > 0:
                     ghz = cs["GRBM_GUI_ACTIVE"] / 8 / (pass_time("GRBM_GUI_ACTIVE") * 1e3)
-                    label = f"measured {ghz:.2f} GHz (GRBM_GUI_ACTIVE / 8 XCDs / time)"
-                else:
-                    ghz, label = 2.4, "ASSUMED 2.4 GHz"
-                derived.append((f"MFMA busy fraction (MFMA_BUSY / ASSUMED 1024 SIMDs / (profiled time x {label}))",
-                                cs["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (tm * 1e-6 * ghz * 1e9)))
+                    derived.append(("diagnostic only: GRBM_GUI_ACTIVE / 8 XCDs / profiled time, GHz", ghz))
             if "SQ_LDS_BANK_CONFLICT" in cs and cs.get("SQ_LDS_IDX_ACTIVE", 0) > 0:
                 derived.append(("LDS bank-conflict cycles / LDS active", cs["SQ_LDS_BANK_CONFLICT"] / cs["SQ_LDS_IDX_ACTIVE"]))
             for name, v in derived:

@@ -34,21 +34,27 @@ inline void send_all(int fd, const void* buf, size_t n) {
   }
 }
 
-// false on EOF / timeout / error
-inline bool recv_all_nothrow(int fd, void* buf, size_t n) {
+enum class RecvStatus { kOk, kTimeout, kClosed };
+
+// kTimeout: the socket's receive timeout (SO_RCVTIMEO) expired with the peer still connected;
+// kClosed: EOF, reset or any other error -- the connection is gone.
+inline RecvStatus recv_all_status(int fd, void* buf, size_t n) {
   char* p = static_cast<char*>(buf);
   while (n > 0) {
     ssize_t r = ::recv(fd, p, n, 0);
-    if (r == 0) return false;
+    if (r == 0) return RecvStatus::kClosed;
     if (r < 0) {
       if (errno == EINTR) continue;
-      return false;
+      return (errno == EAGAIN || errno == EWOULDBLOCK) ? RecvStatus::kTimeout : RecvStatus::kClosed;
     }
     p += r;
     n -= (size_t)r;
   }
-  return true;
+  return RecvStatus::kOk;
 }
+
+// false on EOF / timeout / error
+inline bool recv_all_nothrow(int fd, void* buf, size_t n) { return recv_all_status(fd, buf, n) == RecvStatus::kOk; }
 
 inline void recv_all(int fd, void* buf, size_t n) {
   if (!recv_all_nothrow(fd, buf, n)) throw std::runtime_error("tds net: connection closed or timed out");

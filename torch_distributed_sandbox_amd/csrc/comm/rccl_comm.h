@@ -305,9 +305,16 @@ class RcclComm : public torch::CustomClassHolder, public CollectiveComm {
     // its storage was recorded on the comm stream: freed here, before a CU split's masked streams
     // are destroyed (utils/streams.py release_streams), not by the destructor at process exit,
     // where the allocator's event on the destroyed stream fails (hipErrorInvalidHandle)
+    // After an abort a collective that was running may never finish, so the stream is not
+    // waited on (as for the communicator above): the buffer is leaked on purpose instead -- its
+    // block must not go back to the allocator while an aborted kernel may still write it.
     if (barrier_buf_.defined()) {
-      (void)hipStreamSynchronize(stream_.stream());
-      barrier_buf_ = at::Tensor();
+      if (!st_->aborted.load()) {
+        (void)hipStreamSynchronize(stream_.stream());
+        barrier_buf_ = at::Tensor();
+      } else {
+        new at::Tensor(std::move(barrier_buf_));  // NOLINT: intentional leak (a few bytes)
+      }
     }
   }
 

@@ -4,7 +4,10 @@
 //
 // Layout (owned by parallel/ddp.py): one flat gradient buffer; every parameter
 // has a fixed 256-byte aligned slot; slots are grouped into buckets in
-// gradient-ready order.  The reducer:
+// gradient-ready order.  The buffer may start SHORTER than the layout: the big
+// layers' weight slots sit at its end and get storage on first use (grow(); at
+// world size 1 the fc weight steps inside its backward kernel and never has a
+// gradient, so those 720 MB -- 39 GiB at 23000^2 -- are never allocated).  The reducer:
 //   * registers a post-hook on each parameter's AccumulateGrad node (C++ autograd,
 //     no Python on the backward path),
 //   * makes sure param.grad IS the bucket slot (kernels with a gradient sink
@@ -23,6 +26,7 @@
 #include <torch/custom_class.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <atomic>
 #include <memory>
 #include <string>
@@ -70,6 +74,9 @@ class Reducer : public torch::CustomClassHolder {
       ++b_count_[bk];
     }
     pending_ = b_count_;
+    for (size_t i = 0; i < p_off_.size(); ++i) total_ = std::max(total_, p_off_[i] + p_num_[i]);
+    for (size_t b = 0; b < b_off_.size(); ++b) total_ = std::max(total_, b_off_[b] + b_num_[b]);
+    TORCH_CHECK(flat_grad.numel() <= total_, "Reducer: flat_grad longer than the slot layout");
     b_ready_.assign(b_off_.size(), false);
     b_skip_.assign(b_off_.size(), false);
     b_defer_.assign(b_off_.size(), false);
@@ -145,11 +152,40 @@ class Reducer : public torch::CustomClassHolder {
     return w;
   }
 
+  // The buffer as it is now (parallel/ddp.py reads it back after a grow()).
+  at::Tensor flat_grad() const { return flat_grad_; }
+  int64_t layout_numel() const { return total_; }
+
+  // Give the whole layout storage: a new buffer, the resident prefix copied over, every
+  // .grad that was a view of the old buffer re-pointed.  Collectives in flight on the old
+  // buffer (in place) are ordered before the copy first.  The old buffer is kept alive:
+  // a collective queued on the comm stream may still read it.
+  void grow() {
+    if (flat_grad_.numel() >= total_) return;
+    for (auto& w : works_)
+      if (w) w->wait();
+    at::NoGradGuard ng;
+    at::Tensor g = at::zeros({total_}, flat_grad_.options());
+    if (flat_grad_.numel() > 0) g.narrow(0, 0, flat_grad_.numel()).copy_(flat_grad_);
+    for (size_t i = 0; i < params_.size(); ++i) {
+      at::Tensor& pg = params_[i].mutable_grad();
+      if (pg.defined() && pg.storage().is_alias_of(flat_grad_.storage()))
+        pg = g.narrow(0, p_off_[i], p_num_[i]).view(params_[i].sizes());
+    }
+    retired_.push_back(flat_grad_);
+    flat_grad_ = g;
+  }
+
+  at::Tensor slot(int64_t i) {
+    if (p_off_[i] + p_num_[i] > flat_grad_.numel()) grow();
+    return flat_grad_.narrow(0, p_off_[i], p_num_[i]);
+  }
+
   void on_ready(int64_t i) {
     auto& p = params_[i];
     at::Tensor& g = p.mutable_grad();
     if (!g.defined()) return;
-    at::Tensor view = flat_grad_.narrow(0, p_off_[i], p_num_[i]);
+    at::Tensor view = slot(i);
     if (g.data_ptr() != view.data_ptr() || !g.is_contiguous()) {
       // producer without a gradient sink: one copy into the slot, then .grad IS the slot
       at::NoGradGuard ng;
@@ -192,7 +228,7 @@ class Reducer : public torch::CustomClassHolder {
       }
       at::NoGradGuard ng;
       for (int64_t i : missing) {
-        at::Tensor v = flat_grad_.narrow(0, p_off_[i], p_num_[i]);
+        at::Tensor v = slot(i);
         v.zero_();
         params_[i].mutable_grad() = v.view(params_[i].sizes());
       }
@@ -215,6 +251,8 @@ class Reducer : public torch::CustomClassHolder {
 
  private:
   at::Tensor flat_grad_;
+  std::vector<at::Tensor> retired_;  // buffers replaced by grow()
+  int64_t total_ = 0;                // elements of the whole slot layout
   bool find_unused_;
   std::shared_ptr<std::atomic<Reducer*>> self_;
   std::vector<int64_t> p_off_, p_num_, p_bucket_, b_off_, b_num_, b_count_, pending_, ready_order_;
@@ -233,6 +271,7 @@ class Reducer : public torch::CustomClassHolder {
     b_ready_[b] = true;
     ready_order_.push_back(b);
     if (!sync_ || comm_ == nullptr || comm_->comm_world() == 1) return;
+    if (b_off_[b] + b_num_[b] > flat_grad_.numel()) grow();
     works_[b] = comm_->allreduce_async(flat_grad_.narrow(0, b_off_[b], b_num_[b]), R_AVG);
   }
 };
@@ -260,5 +299,9 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       .def("take_work", &tds_comm::Reducer::take_work)
       .def("mark_ready", &tds_comm::Reducer::mark_ready)
       .def("ready_order", &tds_comm::Reducer::ready_order)
-      .def("num_buckets", &tds_comm::Reducer::num_buckets);
+      .def("num_buckets", &tds_comm::Reducer::num_buckets)
+      .def("flat_grad", &tds_comm::Reducer::flat_grad)
+      .def("layout_numel", &tds_comm::Reducer::layout_numel)
+      .def("grow", &tds_comm::Reducer::grow)
+      .def("slot", &tds_comm::Reducer::slot);
 }

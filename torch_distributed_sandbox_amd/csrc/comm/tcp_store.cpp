@@ -246,15 +246,8 @@ class TCPStore : public torch::CustomClassHolder {
   bool check(const std::string& key) { return call_status(CHECK, key, "") == 0; }
   void wait(const std::string& key, int64_t timeout_ms) {
     std::lock_guard<std::mutex> g(mu_);
-    set_rcv_timeout(fd_, timeout_ms > 0 ? timeout_ms : timeout_ms_);
-    try {
-      request(WAIT, key, "", nullptr);
-      response(nullptr);
-    } catch (...) {
-      reconnect();
-      throw;
-    }
-    set_rcv_timeout(fd_, timeout_ms_);
+    request(WAIT, key, "", nullptr, timeout_ms > 0 ? timeout_ms : timeout_ms_);
+    response(nullptr);  // (a timed-out WAIT replaces the connection there, once)
   }
   bool delete_key(const std::string& key) { return call_status(DEL, key, "") == 0; }
   int64_t num_keys() {
@@ -295,7 +288,18 @@ class TCPStore : public torch::CustomClassHolder {
     if (!s.empty()) std::memcpy(t.data_ptr(), s.data(), s.size());
     return t;
   }
-  void request(uint8_t op, const std::string& key, const std::string& val, const std::string* val2) {
+  // One request on the connection.  ``rcv_ms`` bounds the wait for its reply (a WAIT passes its
+  // own timeout); every other request uses the store timeout.
+  void request(uint8_t op, const std::string& key, const std::string& val, const std::string* val2,
+               int64_t rcv_ms = -1) {
+    if (fd_ < 0) {
+      // the connection was dropped after a desync or a lost peer: one immediate attempt, so a
+      // store whose server is gone fails at once instead of retrying for the whole timeout
+      fd_ = try_connect_once();
+      if (fd_ < 0) throw std::runtime_error("tds TCPStore: connection to the store at " + host_ + ":" +
+                                            std::to_string(port_) + " lost (server gone?)");
+    }
+    set_rcv_timeout(fd_, rcv_ms > 0 ? rcv_ms : timeout_ms_);
     std::string msg;
     msg.push_back((char)op);
     put_u32(msg, (uint32_t)key.size());
@@ -306,32 +310,54 @@ class TCPStore : public torch::CustomClassHolder {
       put_u32(msg, (uint32_t)val2->size());
       msg += *val2;
     }
-    send_all(fd_, msg.data(), msg.size());
+    try {
+      send_all(fd_, msg.data(), msg.size());
+    } catch (...) {
+      drop_connection();
+      throw;
+    }
   }
-  // A request whose reply did not arrive in time leaves the server holding it (a blocked GET / WAIT
-  // is answered when its key appears): on this connection that late reply would be read as the
-  // answer to the NEXT request. The failed caller's connection is replaced instead (the server drops
-  // the old one's waiters when it closes).
-  void reconnect() {
+  int try_connect_once() {
+    try {
+      int fd = connect_to(host_, port_, 0);  // a single attempt (no retry loop)
+      set_rcv_timeout(fd, timeout_ms_);
+      return fd;
+    } catch (...) {
+      return -1;
+    }
+  }
+  void drop_connection() {
     if (fd_ >= 0) ::close(fd_);
     fd_ = -1;
-    try {
-      fd_ = connect_to(host_, port_, timeout_ms_);
-      set_rcv_timeout(fd_, timeout_ms_);
-    } catch (...) {
-      fd_ = -1;  // the next call fails on the closed connection
-    }
   }
+  // The reply to the request just sent.  Two ways to fail, handled differently:
+  //  * the receive timeout expired with the server still there: a blocked GET / WAIT stays
+  //    registered and is answered when its key appears -- on this connection that late reply
+  //    would be read as the answer to the NEXT request.  So the connection is replaced (one
+  //    immediate connect attempt; the server drops the old one's waiters when it closes);
+  //  * the server closed or reset the connection (it exited): no retry, the call fails now and
+  //    the next one makes a single connect attempt, which fails fast too.
+  // A reply cut off after its status byte leaves the stream desynced: the connection goes too.
   uint8_t response(std::string* out) {
     uint8_t st = 0;
-    if (!recv_all_nothrow(fd_, &st, 1)) {
-      reconnect();
-      throw std::runtime_error("tds TCPStore: timed out / connection lost waiting for the store");
+    RecvStatus rs = recv_all_status(fd_, &st, 1);
+    if (rs == RecvStatus::kOk) {
+      uint32_t n = 0;
+      rs = recv_all_status(fd_, &n, 4);
+      std::string v(rs == RecvStatus::kOk ? n : 0, '\0');
+      if (rs == RecvStatus::kOk && n) rs = recv_all_status(fd_, &v[0], n);
+      if (rs == RecvStatus::kOk) {
+        if (st == 2) throw std::runtime_error("tds TCPStore: server error: " + v);
+        if (out) *out = std::move(v);
+        return st;
+      }
     }
-    std::string v = recv_str(fd_);
-    if (st == 2) throw std::runtime_error("tds TCPStore: server error: " + v);
-    if (out) *out = std::move(v);
-    return st;
+    drop_connection();
+    if (rs == RecvStatus::kTimeout) {
+      fd_ = try_connect_once();
+      throw std::runtime_error("tds TCPStore: timed out waiting for the store");
+    }
+    throw std::runtime_error("tds TCPStore: connection to the store lost (server closed it)");
   }
   std::string call(uint8_t op, const std::string& key, const std::string& val) {
     std::lock_guard<std::mutex> g(mu_);

@@ -2,7 +2,8 @@
 // ignore_index, torch's CrossEntropyLoss defaults otherwise): the body of elementwise.hip's
 // ce_small_kernel, shared with the head forward's in-launch finalizer (head_pb.hip HPFin), which
 // forms the loss and dlogits right after the logits when the batch's labels came with it.  logits
-// may point to LDS.  Every thread of the workgroup must call it.
+// may point to LDS.  Every thread of the workgroup must call it.  Labels outside [0, N) other than
+// ignore_index give a NaN loss (and NaN dlogits rows) instead of reading past the row.
 #pragma once
 #include "common.h"
 
@@ -28,10 +29,14 @@ __device__ __forceinline__ void ce_small_block(const float* logits, const int64_
     const float lse = mx + __logf(sm);
     const int64_t lab = labels[row];
     const bool valid = lab != ignore_index;
-    if (lane == 0) rl[row] = valid ? (1.f - eps) * (lse - z[lab]) + eps * (lse - zsum / (float)N) : 0.f;
+    // a label outside [0, N) that is not ignore_index (torch raises 'Target out of bounds'): z is
+    // read at a clamped index, and the row's loss and dlogits are NaN, so the step's loss is NaN
+    const bool bad = valid && (lab < 0 || lab >= N);
+    const int64_t lz = bad ? 0 : lab;
+    if (lane == 0) rl[row] = bad ? NAN : valid ? (1.f - eps) * (lse - z[lz]) + eps * (lse - zsum / (float)N) : 0.f;
     for (int j = lane; j < N; j += TDS_WAVE) {
       float d = 0.f;
-      if (valid) d = __expf(z[j] - lse) - ((j == lab ? (1.f - eps) : 0.f) + eps / (float)N);
+      if (valid) d = bad ? NAN : __expf(z[j] - lse) - ((j == lz ? (1.f - eps) : 0.f) + eps / (float)N);
       dlogits[(int64_t)row * N + j] = d;
     }
   }

@@ -381,13 +381,15 @@ class _Head(torch.autograd.Function):
             ex.defer(dlogits)
             dW = dbfc = None
         else:
-            dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[12] else None, wfc.shape, wfc)
             # world size 1 under DDP(overlap_optimizer): the SGD step of the fc weight runs in
             # this same kernel (ops/fused_update.py)
             lr = None
             if ctx.needs_input_grad[12] and ya.shape[0] <= 8:  # one pass of head_bwd_pb_kernel
                 lr = fused_update.take(ctx.wfc_param)
             keep = not lr or fused_update.keep_grad(ctx.wfc_param)
+            # the gradient's destination (DDP's bucket slot) only when a gradient is written: an
+            # update-only step never requests the slot, so DDP never allocates it (ddp.py _lazy_from)
+            dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[12] and keep else None, wfc.shape, wfc)
             dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (13, 5, 6))
             dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P,
                                                                      dw_out if keep else None, 1.0, True,

@@ -24,8 +24,10 @@ class SGD(torch.optim.Optimizer):
         self._deferred = None  # ([(offset, numel)], runner) when DDP overlaps part of the update
         self._stepped = None  # predicate: parameter already stepped inside its backward (no .grad)
 
-    def set_flat_buffers(self, flat_param: torch.Tensor, flat_grad: torch.Tensor, params):
-        """Declare that ``params`` are views of ``flat_param`` with grads in ``flat_grad``."""
+    def set_flat_buffers(self, flat_param: torch.Tensor, flat_grad, params):
+        """Declare that ``params`` are views of ``flat_param`` with grads in ``flat_grad`` (a tensor,
+        or a callable returning the buffer as it is at step time: DDP allocates the big layers'
+        gradient slots at the buffer's end on first use, parallel/ddp.py ``_lazy_from``)."""
         ids = {id(p) for g in self.param_groups for p in g["params"]}
         if ids == {id(p) for p in params} and len(self.param_groups) == 1:
             self._flat = (flat_param, flat_grad, list(params))
@@ -40,10 +42,17 @@ class SGD(torch.optim.Optimizer):
         self._deferred = (sorted(ranges), runner) if ranges else None
         self._stepped = stepped
 
+    def _flat_grad(self):
+        fg = self._flat[1]
+        return fg() if callable(fg) else fg
+
     def _flat_ok(self):
         if self._flat is None:
             return False
-        fp, fg, params = self._flat
+        fp, _, params = self._flat
+        fg = self._flat_grad()
+        if self._deferred is None and fg.numel() != fp.numel():
+            return False  # (a gradient slot never allocated: no single sweep)
         for p in params:
             if p.grad is None:
                 if self._deferred is not None and self._stepped is not None and self._stepped(p):
@@ -64,7 +73,7 @@ class SGD(torch.optim.Optimizer):
             lr, mom, damp = group["lr"], group["momentum"], group["dampening"]
             wd, nest = group["weight_decay"], group["nesterov"]
             if (self._flat is not None and mom == 0.0 and wd == 0.0 and self._flat_ok() and self._flat[0].is_cuda):
-                fp, fg, _ = self._flat
+                fp, fg = self._flat[0], self._flat_grad()
                 if self._deferred is None:
                     _ext.ops().sgd_step_([fp], [fg], [], lr, 0.0, 0.0, 0.0, False, False)
                     continue
@@ -82,8 +91,8 @@ class SGD(torch.optim.Optimizer):
                     gs.append(fg[off:off + n])
                 if ps:
                     _ext.ops().sgd_step_(ps, gs, [], lr, 0.0, 0.0, 0.0, False, False)
-                runner(lambda off, n, _lr=lr: _ext.ops().sgd_step_([fp[off:off + n]], [fg[off:off + n]], [], _lr,
-                                                                   0.0, 0.0, 0.0, False, False))
+                runner(lambda off, n, _lr=lr: _ext.ops().sgd_step_([fp[off:off + n]], [self._flat_grad()[off:off + n]],
+                                                                   [], _lr, 0.0, 0.0, 0.0, False, False))
                 continue
             params, grads, bufs, first = [], [], [], False
             for p in group["params"]:

@@ -115,11 +115,10 @@ class DistributedDataParallel(nn.Module):
         order = list(reversed(self._params))
         cap_mb = 25.0 if bucket_cap_mb is None else float(bucket_cap_mb)
         limit = max(1, int(cap_mb * 1024 * 1024 // self._params[0].element_size()))
-        self._slots = {}  # id(param) -> (offset, numel)
+        # bucket membership, in gradient-ready order (torch's _compute_bucket_assignment_by_size)
         self._buckets: List[_Bucket] = []
         self._layer_bucket = {}  # id(exchange-candidate layer) -> bucket
-        off = 0
-        cur = _Bucket(0, 0)
+        cur, size = _Bucket(0, 0), 0
         for p in order:
             n = p.numel()
             lyr = layer_of.get(id(p))
@@ -129,35 +128,55 @@ class DistributedDataParallel(nn.Module):
                 if lb is None:
                     if cur.params:
                         self._buckets.append(cur)
-                        cur = _Bucket(len(self._buckets), off)
+                        cur, size = _Bucket(len(self._buckets), 0), 0
                     lb = cur
                     self._layer_bucket[id(lyr)] = lb
-                self._slots[id(p)] = (off, n)
                 lb.params.append(p)
-                off += _align(n)
-                lb.numel = off - lb.offset
                 if len(lb.params) == sum(q is not None for q in (lyr.weight, lyr.bias)):
                     self._buckets.append(lb)
-                    cur = _Bucket(len(self._buckets), off)
+                    cur, size = _Bucket(len(self._buckets), 0), 0
                 continue
-            # torch's _compute_bucket_assignment_by_size: add, then close once >= cap
-            self._slots[id(p)] = (off, n)
             cur.params.append(p)
-            off += _align(n)
-            cur.numel = off - cur.offset
-            if cur.numel >= limit:
+            size += _align(n)
+            if size >= limit:
                 self._buckets.append(cur)
-                cur = _Bucket(len(self._buckets), off)
+                cur, size = _Bucket(len(self._buckets), 0), 0
         if cur.params:
             self._buckets.append(cur)
+        # offsets: the big layers' buckets go last, each with its weight after its bias, so their
+        # weight slots form the tail of the flat layout.  The gradient buffer starts without that
+        # tail (``_lazy_from``): at world size 1 the fc weight steps inside its backward kernel and
+        # on the exchange paths its update is formed in the exchange, so its 720 MB slot (39 GiB at
+        # 23000^2) is only allocated when some path writes a gradient there (_slot / the
+        # native reducer's grow()).  Bucket indices keep the ready order above.
+        big = {id(b) for b in self._layer_bucket.values()}
+        self._slots = {}  # id(param) -> (offset, numel)
+        off = 0
+        lazy_from = None
+        for b in [b for b in self._buckets if id(b) not in big] + [b for b in self._buckets if id(b) in big]:
+            b.offset = off
+            if id(b) in big:
+                b.params.sort(key=lambda q: q.dim() >= 2)  # bias (if any) first, then the weight
+            for p in b.params:
+                if id(b) in big and p.dim() >= 2 and lazy_from is None:
+                    lazy_from = off
+                self._slots[id(p)] = (off, p.numel())
+                off += _align(p.numel())
+            b.numel = off - b.offset
         self._total = off
+        self._lazy_from = off if lazy_from is None else lazy_from
         self._bucket_of = {id(p): b for b in self._buckets for p in b.params}
 
+        self._native = None
+        self._retired_grads = []
         with torch.no_grad():
-            self.flat_grad = torch.zeros(self._total, device=dev, dtype=dtype)
+            self._flat_grad = torch.zeros(self._lazy_from, device=dev, dtype=dtype)
             if flat_params:
+                # one parameter at a time, the big weights first: copy, re-point, and the original's
+                # block goes back to the caching allocator -- the flat buffer and at most one
+                # original are held together (the gradient tail above is not allocated yet)
                 self.flat_param = torch.zeros(self._total, device=dev, dtype=dtype)
-                for p in order:
+                for p in sorted(order, key=lambda q: -q.numel()):
                     o, n = self._slots[id(p)]
                     self.flat_param[o:o + n].copy_(p.detach().reshape(-1))
                     p.data = self.flat_param[o:o + n].view_as(p)
@@ -240,7 +259,7 @@ class DistributedDataParallel(nn.Module):
                 o, n = self._slots[id(p)]
                 ps[idx[id(p)]] = torch.tensor([o, n, b.index])
         bs = torch.tensor([[b.offset, b.numel] for b in self._buckets], dtype=torch.int64)
-        r = _ext.classes().Reducer(self.flat_grad, ps, bs, bool(self.find_unused_parameters))
+        r = _ext.classes().Reducer(self._flat_grad, ps, bs, bool(self.find_unused_parameters))
         if kind == "rccl":
             r.set_rccl_comm(comm)
             self._rccl_comm = comm
@@ -288,19 +307,59 @@ class DistributedDataParallel(nn.Module):
     def exchanges(self):
         return list(self._exchanges)
 
+    @property
+    def flat_grad(self) -> torch.Tensor:
+        """The flat gradient buffer as it is now: without the big layers' weight slots until a
+        path writes a gradient there (see ``_lazy_from``); ``grad_view`` / the gradient sinks
+        grow it on demand."""
+        if self._native is not None:
+            return self._native.flat_grad()
+        return self._flat_grad
+
+    def _grow_flat_grad(self):
+        """Storage for the whole layout: a new buffer, the resident prefix copied, every .grad
+        that viewed the old buffer re-pointed (in-place collectives on it are ordered first)."""
+        if self._native is not None:
+            self._native.grow()
+            return
+        old = self._flat_grad
+        if old.numel() >= self._total:
+            return
+        for b in self._buckets:
+            if b.work is not None:
+                b.work.wait()
+        with torch.no_grad():
+            new = torch.zeros(self._total, device=old.device, dtype=old.dtype)
+            new[:old.numel()].copy_(old)
+            ptr = old.untyped_storage().data_ptr()
+            for p in self._params:
+                if p.grad is not None and p.grad.untyped_storage().data_ptr() == ptr:
+                    o, n = self._slots[id(p)]
+                    p.grad = new.narrow(0, o, n).view(p.shape)
+        self._retired_grads.append(old)  # a queued collective may still read it
+        self._flat_grad = new
+
+    def grad_storage_bytes(self) -> int:
+        """Bytes of gradient storage allocated so far (the layout may be larger, ``_total``)."""
+        return self.flat_grad.numel() * self.flat_grad.element_size()
+
+    def _slot(self, o: int, n: int) -> torch.Tensor:
+        if o + n > self.flat_grad.numel():
+            self._grow_flat_grad()
+        return self.flat_grad.narrow(0, o, n)
+
     def _make_view_fn(self, p):
         o, n = self._slots[id(p)]
         shape = p.shape
-        flat = self.flat_grad
 
         def view():
-            return flat.narrow(0, o, n).view(shape)
+            return self._slot(o, n).view(shape)
 
         return view
 
     def grad_view(self, p):
         o, n = self._slots[id(p)]
-        return self.flat_grad.narrow(0, o, n).view(p.shape)
+        return self._slot(o, n).view(p.shape)
 
     def _verify_param_shapes(self):
         """Same check as torch's _verify_param_shape_across_processes (C4): a hash
@@ -409,7 +468,7 @@ class DistributedDataParallel(nn.Module):
 
     def _on_grad_ready(self, p):
         o, n = self._slots[id(p)]
-        view = self.flat_grad.narrow(0, o, n)
+        view = self._slot(o, n)
         g = p.grad
         if g is None:
             return
@@ -432,7 +491,7 @@ class DistributedDataParallel(nn.Module):
         b.ready = True
         if self.world_size == 1 or not self.require_backward_grad_sync:
             return
-        seg = self.flat_grad.narrow(0, b.offset, b.numel)
+        seg = self._slot(b.offset, b.numel)
         b.work = tdist.all_reduce(seg, tdist.ReduceOp.AVG, group=self.process_group, async_op=True)
 
     def _finalize_backward(self):
@@ -473,7 +532,7 @@ class DistributedDataParallel(nn.Module):
         backward kernel instead (ops/fused_update.py): nothing to average, and the
         kernel already holds the weight and its gradient."""
         if self.flat_param is not None and hasattr(optimizer, "set_flat_buffers"):
-            optimizer.set_flat_buffers(self.flat_param, self.flat_grad, self._params)
+            optimizer.set_flat_buffers(self.flat_param, lambda: self.flat_grad, self._params)
             if self._deferred and hasattr(optimizer, "set_deferred"):
                 optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred], self._run_deferred_update,
                                        lambda p: id(p) in self._fused_done)
@@ -559,7 +618,17 @@ class DistributedDataParallel(nn.Module):
         """Finish the deferred buckets on the side stream: wait for this step's
         backward (compute stream) and the bucket collective, apply ``update_fn(offset,
         numel)`` (the optimizer's flat-slice update), then fence the parameters so
-        their first reader in the next forward waits (ops/param_fence.py)."""
+        their first reader in the next forward waits (ops/param_fence.py).
+
+        Contract with the optimizer (``ops.optim.SGD.step``, which finds this runner's owner
+        through ``runner.__self__``): per step, the optimizer MAY call ``take_inline_deferred()``
+        first and step the returned ranges in its own sweep on the current stream; it then MUST
+        call this runner in the same step.  Both consume the step's state (``_fused_done``,
+        ``_inline_done``).  A runner call without a preceding ``take_inline_deferred()`` (any other
+        optimizer) updates everything not stepped in its backward here, on the side stream.  Fast
+        path: when every deferred parameter was stepped in its backward or inline, no side work is
+        queued and no fence is set (``last_deferred_inline``).  Tests:
+        tests/test_param_fence_cpu.py."""
         from ..ops import param_fence
 
         cur = torch.cuda.current_stream(self.device)
@@ -584,6 +653,7 @@ class DistributedDataParallel(nn.Module):
                 if w is not None:
                     w.wait()  # side stream waits for the bucket all-reduce
                 if not done:
+                    self._slot(b.offset, b.numel)  # (storage for the whole bucket)
                     update_fn(b.offset, b.numel)
                     continue
                 for p in b.params:  # the backward already stepped some of them

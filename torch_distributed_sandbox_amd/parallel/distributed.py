@@ -103,9 +103,13 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
                        device_id: Optional[int] = None, store=None, comm_cus: Optional[int] = None) -> None:
     """Initialise the default group.  ``rank``/``world_size`` default to the
     ``RANK``/``WORLD_SIZE`` environment (torchrun); ``init_method`` defaults to
-    ``env://`` (``MASTER_ADDR``/``MASTER_PORT``).  ``store="native"`` (or
-    ``TDS_STORE=native``) rendezvouses through this package's C++ TCP store
-    (parallel/store.py) instead of c10d's.
+    ``env://`` (``MASTER_ADDR``/``MASTER_PORT``), which rendezvouses through this package's
+    C++ TCP store (parallel/store.py ``rendezvous``: c10d's store at ``MASTER_ADDR:MASTER_PORT``
+    only locates it, and is the agreed fallback if it cannot be used on some rank).
+    ``store="c10d"`` / ``TDS_STORE=c10d``, an explicit ``init_method`` or a
+    ``torch.distributed.Store`` object use that instead; so does ``backend="rccl"`` (torch's
+    ProcessGroupNCCL: torch's stack top to bottom, bench.py's fallback tiers).  ``store_kind()``
+    reports which store the group rendezvoused on.
 
     ``comm_cus`` (``rccl-native`` only): CUs split off for communication
     (utils/streams.py, docs/DISTRIBUTED.md) -- a CU-masked compute stream is made
@@ -118,15 +122,16 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
     if world_size is None:
         world_size = int(os.environ.get("WORLD_SIZE", "1"))
     _state["comm_cus"] = 0
-    if store is None and init_method is None and os.environ.get("TDS_STORE", "") == "native":
-        store = "native"
+    kind = "c10d" if init_method is not None else "given"
+    if store is None and init_method is None:
+        store = "c10d" if b == "rccl" else os.environ.get("TDS_STORE", "native") or "native"
     if isinstance(store, str):
-        if store != "native":
-            raise ValueError(f"unknown store {store!r} (expected 'native' or a torch.distributed.Store)")
-        from .store import create_store
+        if store not in ("native", "c10d"):
+            raise ValueError(f"unknown store {store!r} (expected 'native', 'c10d' or a torch.distributed.Store)")
+        from .store import rendezvous
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        store = create_store(rank, world_size, timeout=timeout)
+        store, kind = rendezvous(rank, world_size, timeout=timeout, prefer=store)
     kwargs = dict(backend=_torch_backend(b), rank=rank, world_size=world_size, timeout=timeout)
     if store is not None:
         kwargs["store"] = store
@@ -172,6 +177,14 @@ def init_process_group(backend: Optional[str] = None, init_method: Optional[str]
         raise
     _state["backend"] = b
     _state["groups"] = {}
+    _state["store_kind"] = kind
+    _state["store"] = store  # (rank 0 serves it: alive as long as the group)
+
+
+def store_kind() -> Optional[str]:
+    """The store the default group rendezvoused on: "native" (parallel/store.py), "c10d",
+    "c10d (fallback: ...)", or "given" (a store object passed in)."""
+    return _state.get("store_kind") if is_initialized() else None
 
 
 def _undo_cu_split() -> None:

@@ -862,13 +862,15 @@ class ActivationExchange:
         self._done()
         return True
 
-    def _targets(self):
+    def _targets(self, weight: bool = True):
         """(dW, accumulate_w), (db, accumulate_b) — gradients accumulated under no_sync()
-        are averaged first (one all-reduce), this step's exchanged average is added."""
+        are averaged first (one all-reduce), this step's exchanged average is added.
+        ``weight=False``: the bias only (dW is (None, False)); the weight's bucket slot is not
+        requested, so DDP never allocates it (parallel/ddp.py ``_lazy_from``)."""
         from . import distributed as tdist
 
         out = []
-        for p, view_fn in ((self.weight, self._wview), (self.bias, self._bview)):
+        for p, view_fn in ((self.weight if weight else None, self._wview), (self.bias, self._bview)):
             if p is None:
                 out.append((None, False))
             elif p.grad is not None:
@@ -886,7 +888,9 @@ class ActivationExchange:
         dy_all = torch.empty((self.world * rows, dy.shape[1]), device=dy.device, dtype=dy.dtype)
         tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
         zf = getattr(self, "_zs_decode_pending", None)
-        targets = (self.weight.data, self._wview(), self.weight.grad)
+        # (the bucket slot dW may be written to is 256-byte aligned with rows of K % 4 == 0 floats,
+        # which _zs_fused checks; it is not requested here, so the update-only path never allocates it)
+        targets = (self.weight.data, self.weight.grad)
         if self.active == "activations" and self._zs_fused(zf, targets):
             self._zs_decode_pending = None  # formed from the encodings below (_dw_zs)
         else:
@@ -953,7 +957,7 @@ class ActivationExchange:
         from .. import _ext
         from . import distributed as tdist
 
-        (_, _), (db, acc_b) = self._targets()
+        (_, _), (db, acc_b) = self._targets(weight=False)
         W = self.weight.data
         ops = _ext.ops()
         if self.active == "activations" and zf is not None:

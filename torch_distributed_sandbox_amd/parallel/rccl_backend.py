@@ -51,6 +51,20 @@ class _Work(dist.Work):
         return self._result
 
 
+def exchange_unique_id(store, rank: int, key: str = "rccl_uid") -> torch.Tensor:
+    """The communicator's ncclUniqueId (128 bytes): made by rank 0 (ncclGetUniqueId, no GPU
+    needed) and published through the rendezvous store -- this package's C++ store by default
+    (parallel/store.py) -- every other rank blocks in ``get`` until it is there."""
+    from .._ext import classes
+
+    if rank == 0:
+        uid = classes().RcclComm.unique_id()
+        store.set(key, bytes(uid.numpy().tobytes()))
+        return uid
+    raw = store.get(key)
+    return torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+
+
 class RcclProcessGroup(dist.ProcessGroup):
     def __init__(self, store, rank: int, world_size: int, timeout: datetime.timedelta):
         super().__init__(rank, world_size)
@@ -58,12 +72,7 @@ class RcclProcessGroup(dist.ProcessGroup):
 
         self._rank, self._world = rank, world_size
         dev = torch.cuda.current_device()
-        if rank == 0:
-            uid = classes().RcclComm.unique_id()
-            store.set("rccl_uid", bytes(uid.numpy().tobytes()))
-        else:
-            raw = store.get("rccl_uid")
-            uid = torch.frombuffer(bytearray(raw), dtype=torch.uint8)
+        uid = exchange_unique_id(store, rank)
         ms = int(timeout.total_seconds() * 1000) if timeout is not None else 600_000
         self._comm = classes().RcclComm(rank, world_size, dev, uid, ms)
         self.device_index = dev

@@ -181,7 +181,8 @@ def train(gpu: int, args, distributed: bool = False) -> dict:
                "image_size": H, "final_loss": float(loss.item()) if loss is not None else None,
                "plan": (f"DDP wrapper ({getattr(model, 'reducer_kind', '?')} reducer, fc grad "
                         f"{model.fc_grad_path()}, overlap_optimizer={model.overlap_optimizer})"
-                        if isinstance(model, DistributedDataParallel) else "plain module")}
+                        if isinstance(model, DistributedDataParallel) else "plain module"),
+               "store": tdist.store_kind() if distributed else None}
     if t_first is not None and steps_done > 1:
         dt = t_end - t_first
         summary["images_per_sec_per_rank"] = (steps_done - 1) * batch_size / dt
