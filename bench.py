@@ -65,9 +65,6 @@ METRIC = "images/sec (whole node), 3000x3000 MNIST ConvNet DDP at 1/2/4/8 MI355X
 MODEL = "ConvNet(conv5x5 1->16+BN+ReLU+pool2, conv5x5 16->32+BN+ReLU+pool2, fc 32*(H/4)^2->10)"
 DATA = ("synthetic (seeded 28x28 uint8 sources upsampled on device to HxW, a fresh batch every step -- no batch "
         "repeats within the run; random labels; random init)")
-DTYPE_SPLIT = ("fp32 (conv1 fwd+wgrad: bf16x3 split-precision MFMA; conv2 fwd+dgrad+wgrad: fp16x2 split MFMA -- one "
-               "operand exact as fp16 hi+lo, the other rounded once, <= 2^-11 per product; fp32 accumulate; BN, fc, CE, "
-               "SGD: fp32)")
 DTYPE_TF32 = ("fp32 (conv2 fwd+dgrad+wgrad: TF32-class -- one fp16 MFMA per product, both operands rounded to 11 "
               "significant bits = TF32's significand, exact power-of-two range scaling, fp32 accumulate: the arithmetic "
               "of the reference's default cuDNN TF32 convolutions; conv1 fwd+wgrad: bf16x3 split MFMA (~2^-16); BN, fc, "
@@ -77,13 +74,14 @@ DTYPE_TF32 = ("fp32 (conv2 fwd+dgrad+wgrad: TF32-class -- one fp16 MFMA per prod
 
 
 def _dtype(on_gpu: bool = True) -> str:
-    """The compute precision of this build (csrc/kernels/conv2_common.h TDS_CONV2_SPLIT)."""
+    """The compute precision of the GPU plan (csrc/kernels/conv2_common.h)."""
     if not on_gpu:
         return "fp32 (CPU rehearsal: torch ops)"
     try:
         import torch_distributed_sandbox_amd as tds
 
-        return DTYPE_SPLIT if int(tds._ext.ops().conv2_split()) else DTYPE_TF32
+        tds._ext.ops()
+        return DTYPE_TF32
     except Exception:  # noqa: BLE001 -- CPU rehearsal without the extension: the torch-ops plan
         return "fp32 (CPU rehearsal: torch ops)"
 

@@ -174,48 +174,10 @@ def test_activation_exchange_fused_convnet(pg, gpu, mode):
     assert ddp.exchanges[0].steps_exchanged == 2
 
 
-def test_zs_encode_from_ya_bitwise(gpu):
-    """The activation exchange encodes the fc input rows straight from the fused head's ya and BN2
-    affine (ops.zs_encode_ya, kernels/zs_exchange.hip): its records, values and count must be bitwise
-    those of encoding the X the head forward writes (x_out), -0.0 / NaN included, and the
-    overflow path's materialised rows (factored._YaRows.dense) must be that X."""
-    import torch_distributed_sandbox_amd as tds
-    from torch_distributed_sandbox_amd.parallel import factored, zs
-
-    ops = tds._ext.ops()
-    torch.manual_seed(3)
-    for B, P in ((3, 64), (5, 100), (2, 150)):  # Q = 32, 50, 75: runs aligned, shifted, odd rows
-        Q = P // 2
-        Q4, Q8 = (Q + 3) // 4, (Q + 7) // 8  # pooled-blocked plane (kernels/pooled_layout.h)
-        ya = torch.randn(B, 32, Q4 * Q8 * 32, device=gpu)
-        ya.view(-1)[::997] = float("nan")
-        aff2 = torch.cat([torch.randn(32, device=gpu), torch.randn(32, device=gpu) * 0.5])
-        aff2[3] = 0.0  # a whole channel of +0.0 / -0.0 candidates
-        K = 32 * Q * Q
-        wfc = torch.randn(10, K, device=gpu) * 1e-3
-        x = torch.empty(B, K, device=gpu)
-        ops.fused_head_forward_aff(ya, aff2, wfc, None, P, x)
-        n = B * K
-        m1 = torch.empty(zs.meta_numel(n), device=gpu, dtype=torch.int32)
-        m2 = torch.empty_like(m1)
-        v1 = torch.full((n,), 7.0, device=gpu)
-        v2 = torch.full((n,), 7.0, device=gpu)
-        c1 = zs.encode(x, m1, v1)
-        c2 = ops.zs_encode_ya(ya, aff2, P, m2, v2)
-        torch.cuda.synchronize()
-        assert int(c1) == int(c2) and 0 < int(c1) < n
-        assert torch.equal(m1, m2)
-        k = int(c1)
-        assert torch.equal(v1[:k].view(torch.int32), v2[:k].view(torch.int32))
-        dense = factored._YaRows(ya, aff2, P, B, K).dense()
-        assert torch.equal(dense.view(torch.int32), x.view(torch.int32))
-
-
 @pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("sharded", False),
                                            ("chunked", False),
-                                           ("allreduce", True), ("activations", True), ("sharded", True),
-                                           ("activations", "head")])
-def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse, monkeypatch):
+                                           ("allreduce", True), ("activations", True), ("sharded", True)])
+def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     """overlap_optimizer: the fc bucket's collective + SGD update run on a side stream
     and the next forward's head waits on a parameter fence; the trajectory must be
     identical to the sequential step.  fuse=True: at world size 1 the fc weight's SGD
@@ -223,19 +185,12 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse, monkeypat
     exchange's dW formation (update-only linear_dw; ops/fused_update.py)."""
     import copy
 
-    from torch_distributed_sandbox_amd.models import ConvNet, convnet_fused
+    from torch_distributed_sandbox_amd.models import ConvNet
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss, param_fence
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
 
-    from torch_distributed_sandbox_amd.parallel import factored
-
-    head = fuse == "head"  # the round-5 paths: X encoded from ya, the update applied in the head forward
-    monkeypatch.setattr(factored, "_ZS_FROM_YA", head)
-    monkeypatch.setattr(factored, "_HEAD_FUSED_UPDATE", head)
-    fuse = bool(fuse)
     torch.manual_seed(0)
     H = 256
-    fused0 = convnet_fused.STATS["head_fused_updates"]
     m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
     m2 = copy.deepcopy(m1)
     d1 = DistributedDataParallel(m1, grad_exchange=exchange, overlap_optimizer=True, fuse_update_in_backward=fuse)
@@ -267,10 +222,6 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse, monkeypat
             assert not d1._fused_done  # consumed by the step: the bias was updated, the weight skipped
     d1.wait_pending_updates()
     torch.cuda.synchronize()
-    if head and d1.exchanges[0].compress:
-        # steps 1 and 3 applied the previous step's update inside the head forward (step 2's
-        # count check saw the forced overflow and ran the separate update)
-        assert convnet_fused.STATS["head_fused_updates"] - fused0 >= 2
     if exchange in ("activations", "sharded") and d1.exchanges[0].compress:
         assert d1.exchanges[0].zs_stats["overflows"] >= 1  # step 2 went through the dense re-send
     for (n, p), q in zip(m1.named_parameters(), m2.parameters()):

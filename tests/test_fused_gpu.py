@@ -26,20 +26,10 @@ def _check(a, b, rel, name=""):
     assert e <= rel * s + 1e-12, f"{name}: max err {e:.3e} vs scale {s:.3e} (rel {e / max(s, 1e-30):.2e})"
 
 
-def _split() -> bool:
-    """The build's conv2 operand precision (csrc/kernels/conv2_common.h TDS_CONV2_SPLIT): True =
-    fp16x2 (one operand hi + lo), False = one fp16 MFMA per product, both operands rounded to
-    TF32's 11 significant bits."""
-    return bool(_ops().conv2_split())
-
-
-def _check_conv(a, ref, ref_tf32, split_rel, name):
-    """A conv2 result vs fp64: split builds within ``split_rel`` (only one operand rounded); the
-    TF32-class build within 1.5x the error the same convolution with TF32-rounded operands makes
-    (tests/_tf32ref.py), or 1e-5 when that is smaller."""
-    if _split():
-        _check(a, ref, split_rel, name)
-        return
+def _check_conv(a, ref, ref_tf32, name):
+    """A conv2 result vs fp64 (csrc/kernels/conv2_common.h: one fp16 MFMA per product, both
+    operands rounded to TF32's 11 significant bits): within 1.5x the error the same convolution
+    with TF32-rounded operands makes (tests/_tf32ref.py), or 1e-5 when that is smaller."""
     e, s = _err(a, ref)
     et, _ = _err(ref_tf32, ref)
     assert e <= max(1e-5 * s, 1.5 * et) + 1e-12, f"{name}: max err {e:.3e} vs TF32 convs {et:.3e} (scale {s:.3e})"
@@ -273,11 +263,10 @@ def test_conv2_forward(gpu, P):
     y2 = v + b2
     ref = F.conv2d(p.permute(0, 3, 1, 2).double().cpu(), w2.double().cpu(), b2.double().cpu(), padding=2)
     reft = F.conv2d(p.permute(0, 3, 1, 2).double().cpu(), tf32(w2.cpu()), b2.double().cpu(), padding=2)
-    # split: the weights are carried exactly (fp16 hi + lo), only fp32 accumulation error remains;
-    # TF32 class: the weights rounded once, as TF32 rounds them; either way plus the y2h storage
-    # rounding (<= half an fp16 step of |y2 - b2|)
+    # TF32 class: the weights rounded once, as TF32 rounds them, plus the y2h storage rounding
+    # (<= half an fp16 step of |y2 - b2|)
     vmax = v.abs().max().item()
-    e, sc = _err(y2.permute(0, 3, 1, 2), reft if not _split() else ref)
+    e, sc = _err(y2.permute(0, 3, 1, 2), reft)
     assert e <= 2.0 ** -10 * vmax + 1e-5 * sc, (e, vmax)
     # the stored values come from the same products as the statistics: check those against the
     # references as before (TF32-rounded operands or exact)
@@ -289,14 +278,14 @@ def test_conv2_forward(gpu, P):
     s = partial.view(32, -1, 2).sum(1).cpu()
     yc = ref - b2.double().cpu().view(1, 32, 1, 1)
     yct = reft - b2.double().cpu().view(1, 32, 1, 1)
-    _check_conv(s[:, 0], yc.sum((0, 2, 3)), yct.sum((0, 2, 3)), 1e-4, "sum")
-    _check_conv(s[:, 1], (yc * yc).sum((0, 2, 3)), (yct * yct).sum((0, 2, 3)), 1e-4, "sumsq")
+    _check_conv(s[:, 0], yc.sum((0, 2, 3)), yct.sum((0, 2, 3)), "sum")
+    _check_conv(s[:, 1], (yc * yc).sum((0, 2, 3)), (yct * yct).sum((0, 2, 3)), "sumsq")
     # ya: the fp32 window extremes; a2: each window's argmax pixel (first in scan order)
     Q = P // 2
     want = window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q].float(), (g2 < 0))
     got = pb_to_planar(ya, Q)
     assert ((got - want).abs() <= 2.0 ** -10 * vmax).all(), (got - want).abs().max()
-    _check_argmax_kept(a2, ref if _split() else reft, g2, Q)
+    _check_argmax_kept(a2, reft, g2, Q)
 
 
 def _check_argmax_kept(a2, ref_nchw, g2, Q, gap=1e-5):
@@ -331,7 +320,7 @@ def test_conv2_forward_argmax_codes_on_near_ties(gpu, P):
     wp, _ = _ops().conv2_pack(w2, mag)
     y2h, _, _, a2 = _ops().fused_conv2_forward(p, wp, b2, g2, mag)
     pin = p.permute(0, 3, 1, 2).double().cpu()
-    ref = F.conv2d(pin, w2.double().cpu() if _split() else tf32(w2.cpu()), None, padding=2)
+    ref = F.conv2d(pin, tf32(w2.cpu()), None, padding=2)
     Q = P // 2
     # the case is real: to nearest, many windows' top two values share one fp16
     r = _windows(ref.permute(0, 2, 3, 1), Q)
@@ -452,22 +441,19 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     prt = p.permute(0, 3, 1, 2).double().cpu().requires_grad_(True)
     wrt = tf32(w2.cpu()).requires_grad_(True)
     F.conv2d(prt, wrt, None, padding=2).backward(tf32(dy2))
-    # dgrad: dy2 is the single-rounded fp16 operand (2^-11 per element), w2 split or rounded, and
+    # dgrad: dy2 is the single-rounded fp16 operand (2^-11 per element), w2 rounded, and
     # the result is stored once as dp1h (fp16: <= 2^-11 of its value more)
     e, sc = _err(dp1.permute(0, 3, 1, 2), pr.grad)
-    et, _ = _err(prt.grad if not _split() else pr.grad, pr.grad)
-    bound = (5e-4 * sc if _split() else max(1e-5 * sc, 1.5 * et)) + 2.0 ** -11 * sc
+    et, _ = _err(prt.grad, pr.grad)
+    bound = max(1e-5 * sc, 1.5 * et) + 2.0 ** -11 * sc
     assert e <= bound, f"dp1: max err {e:.3e} vs bound {bound:.3e} (scale {sc:.3e})"
-    # wgrad: dy2 exact (fp16 hi + lo) or rounded, p1 the stored fp16 operand itself
-    _check_conv(dw2, wr.grad, wrt.grad, 5e-5, "dw2")
+    # wgrad: dy2 rounded, p1 the stored fp16 operand itself
+    _check_conv(dw2, wr.grad, wrt.grad, "dw2")
     # conv bias before BN: sum(dy2) is analytically zero, both sides are rounding noise; with dy2
     # rounded once to 11 significant bits (TF32 class) the noise is bounded by 2^-11 sum|dy2|
     err = (db2.double().cpu() - br.grad).abs()
-    if _split():
-        assert err.max().item() <= 1e-4 * wr.grad.abs().max().item()
-    else:
-        bound = dy2.abs().sum((0, 2, 3)) * 2.0 ** -11 * 1.01 + 1e-4 * wr.grad.abs().max().item()
-        assert bool((err <= bound).all()), (err.max().item(), bound.min().item())
+    bound = dy2.abs().sum((0, 2, 3)) * 2.0 ** -11 * 1.01 + 1e-4 * wr.grad.abs().max().item()
+    assert bool((err <= bound).all()), (err.max().item(), bound.min().item())
 
 
 def _fused_vs_ref(gpu, B, H, steps=2, lr=0.05, levels=False, gamma1=None, w2_scale=None, p1_above=None, g2_zero=()):

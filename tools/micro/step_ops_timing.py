@@ -98,8 +98,7 @@ def main():
                                   gram, 1.0)
 
         # the activation exchange's pieces (parallel/factored.py, world 1): the head forward writing X,
-        # the zero-suppressed encode from that X or straight from ya, the separate update sweep over the
-        # encodings, and the head forward applying that update itself
+        # the zero-suppressed encode of that X and the update sweep over the encodings
         from torch_distributed_sandbox_amd.parallel import zs
 
         K = fc.weight.shape[1]
@@ -114,15 +113,8 @@ def main():
         def enc_x():
             st["nnz"] = zs.encode(xo, meta, vals)
 
-        def enc_ya():
-            st["nnz"] = ops.zs_encode_ya(st["c2"][2], st["hf"][2], P, meta, vals)
-
         def dw_zs():
             ops.linear_dw_zs(dl, meta.view(1, -1), vals.view(1, -1), B, w2c, None, 1.0, False, 1e-12)
-
-        def hf_upd():
-            ops.fused_head_forward_upd(st["c2"][2], st["hf"][2], w2c, fc.bias, P, dl, meta.view(1, -1),
-                                       vals.view(1, -1), B, 1.0, 1e-12)
 
         xl = TF.upsample_bilinear_u8(src, H, H, levels=True)
 
@@ -146,11 +138,11 @@ def main():
         seq = [("ups", ups), ("moments", moments), ("ups_mom", ups_mom), ("l1_fwd_u8", l1f_u8),
                ("l1_fwd_u8_self", l1f_u8_self), ("l1_fwd", l1f), ("conv2_pack", pack), ("conv2_fwd", c2f), ("head_fwd", hf), ("head_bwd", hb),
                ("head_bwd_nomag", hb_nomag), ("conv2_bwd", c2b), ("l1_bwd", l1b),
-               ("head_fwd_x", hf_x), ("zs_enc_x", enc_x), ("zs_enc_ya", enc_ya), ("dw_zs", dw_zs), ("head_fwd_upd", hf_upd)]
+               ("head_fwd_x", hf_x), ("zs_enc_x", enc_x), ("dw_zs", dw_zs)]
         only = set(a.only.split(",")) if a.only else None
         for name, fn in seq:
-            if name in ("head_fwd_x", "zs_enc_x", "zs_enc_ya", "dw_zs", "head_fwd_upd") and only and not (
-                    only & {"head_fwd_x", "zs_enc_x", "zs_enc_ya", "dw_zs", "head_fwd_upd"}):
+            if name in ("head_fwd_x", "zs_enc_x", "dw_zs") and only and not (
+                    only & {"head_fwd_x", "zs_enc_x", "dw_zs"}):
                 continue
             fn()
         only = set(a.only.split(",")) if a.only else None

@@ -62,39 +62,20 @@ Tensor sink_or_empty(const c10::optional<Tensor>& out, std::vector<int64_t> shap
 // layer-1 conv workgroups per CU (grid-stride tile loop).  Sweep on MI355X (isolated layer-1
 // forward, ms): 2 -> 0.524, 4 -> 0.443, 6 -> 0.433, 8 -> 0.429; bench 3.62-3.63 vs 3.64-3.68 ms
 // per step at 4 (tools/gpu_sessions/r2_l1wg.sh)
-#ifndef TDS_L1_PER_CU
-#define TDS_L1_PER_CU 8
-#endif
-int l1_wg() { return tds_fused_num_wg(TDS_L1_PER_CU); }
+int l1_wg() { return tds_fused_num_wg(8); }
 
 // layer-1 backward workgroups per CU: 4 waves each.  Round 3 (124-126 VGPRs, 4 fit a CU): 4 -> 0.318
 // ms, 3 -> 0.351 ms (tools/gpu_sessions/r3_s21.sh).  Round 4's fp16 weight gradient runs at 87
-// VGPRs, so 5 fit (<= 102): 4 / 5 / 6 -> 0.143 / 0.138 / 0.145 ms (r4_s47.sh).  TDS_L1B_PER_CU
-// overrides it (A/B sweeps only).  Capped by what the launched variant's registers allow
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor): the fp32-image and pair-layout variants need more
-// VGPRs than the level-input word layout, and a 5th workgroup that cannot be resident only adds a
-// second, partial wave of workgroups.
-int l1b_wg(bool levels, bool pairs) {
-  static const int req = [] {
-    const char* e = std::getenv("TDS_L1B_PER_CU");
-    const int v = e ? std::atoi(e) : 0;
-    return v >= 1 && v <= 8 ? v : 5;
-  }();
-  const int fit = tds_l1_bwd_max_per_cu(levels, pairs);
-  return tds_fused_num_wg(std::getenv("TDS_L1B_PER_CU") ? req : std::min(req, fit));
-}
+// VGPRs, so 5 fit (<= 102): 4 / 5 / 6 -> 0.143 / 0.138 / 0.145 ms (r4_s47.sh).  Capped by what the
+// launched variant's registers allow (hipOccupancyMaxActiveBlocksPerMultiprocessor): the fp32-image
+// variant needs more VGPRs than the level-input one, and a 5th workgroup that cannot be resident
+// only adds a second, partial wave of workgroups.
+int l1b_wg(bool levels) { return tds_fused_num_wg(std::min(5, tds_l1_bwd_max_per_cu(levels))); }
 
 // Device copy of the blocked tile order (tds_tile_order_fill) per (device, shape), from the
 // torch caching allocator, built once.  The map is never destroyed (no frees at process exit).
-// TDS_TILE_LISTS=0 keeps the work-index-major layout (A/B only): *sw / *sk are the strides of
-// (workgroup, k-th tile of that workgroup) in the device table either way.
-bool tile_lists() {
-  static const bool on = [] {
-    const char* e = std::getenv("TDS_TILE_LISTS");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// On the device as per-workgroup lists: *sw / *sk are the strides of (workgroup, k-th tile of that
+// workgroup) in the device table.
 
 const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg, int* sw, int* sk) {
   static std::mutex mu;
@@ -102,11 +83,10 @@ const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int n
   // 16-row groups for both conv2 kernels: for the backward's 256 workgroups (32 per XCD
   // round) 4 / 8 / 16 / 32 rows measured 1.585 / 1.603 / 1.572 / 1.564 ms -- within noise
   const int gr = 16;
-  const bool lists = tile_lists();
   const int64_t total = (int64_t)B * tiles_r * tiles_c;
   const int64_t rows = (total + nwg - 1) / nwg;
-  *sw = lists ? (int)rows : 1;
-  *sk = lists ? 1 : nwg;
+  *sw = (int)rows;
+  *sk = 1;
   const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c, nwg);
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache->find(key);
@@ -115,25 +95,17 @@ const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int n
   const int rc = tds_tile_order_fill(host.data_ptr<int>(), B, tiles_r, tiles_c, gr);
   TORCH_CHECK(rc == 0, "tdsa fused: tile order table needs B <= 255 and <= 4095 tiles per side (B=", B,
               ", tiles ", tiles_r, " x ", tiles_c, ")");
-#ifndef TDS_F2_REV
-#define TDS_F2_REV 0
-#endif
-  // TDS_F2_REV: the conv2 forward walks p1 last-to-first, the reverse of the layer-1 conv's writes
-  if (TDS_F2_REV != 0) std::reverse(host.data_ptr<int>(), host.data_ptr<int>() + total);
+  // (the conv2 forward walking p1 last-to-first, the reverse of the layer-1 conv's writes, measured
+  // 385.2 -> 389.0 us, r5_s50: the forward keeps its order)
   // on the device as per-workgroup lists: work index t = w + kk * nwg at [w][kk] (rows =
   // ceil(total / nwg), the tail padded with the list's last entry), so one workgroup's
   // consecutive tiles share a scalar-cache line (16 entries) instead of one line each
-  Tensor dev;
-  if (lists) {
-    auto l = at::empty({(int64_t)nwg, rows}, at::TensorOptions().dtype(at::kInt));
-    const int* src = host.data_ptr<int>();
-    int* dst = l.data_ptr<int>();
-    for (int64_t w = 0; w < nwg; ++w)
-      for (int64_t k = 0; k < rows; ++k) dst[w * rows + k] = src[std::min(w + k * nwg, total - 1)];
-    dev = l.to(like.device());
-  } else {
-    dev = host.to(like.device());
-  }
+  auto l = at::empty({(int64_t)nwg, rows}, at::TensorOptions().dtype(at::kInt));
+  const int* src = host.data_ptr<int>();
+  int* dst = l.data_ptr<int>();
+  for (int64_t w = 0; w < nwg; ++w)
+    for (int64_t k = 0; k < rows; ++k) dst[w * rows + k] = src[std::min(w + k * nwg, total - 1)];
+  Tensor dev = l.to(like.device());
   (*cache)[key] = dev;
   return dev.data_ptr<int>();
 }
@@ -146,17 +118,15 @@ const int* tile_order(const Tensor& like, int B, int tiles_r, int tiles_c, int n
 const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg, int* sw, int* sk) {
   static std::mutex mu;
   static auto* cache = new std::map<std::tuple<int, int, int, int, int>, Tensor>();
-#ifndef TDS_BWD_SEG
-#define TDS_BWD_SEG 48  // A/B (r2_seg.sh): 24 / 48 / 96 / 200 tiles = 1.551 / 1.534 / 1.546 / 1.584 ms
-#endif
-  constexpr int kSeg = TDS_BWD_SEG;  // tiles per vertical segment (a segment start re-stages 4 rows)
+  // tiles per vertical segment (a segment start re-stages 4 rows); r2_seg.sh: 24 / 48 / 96 / 200
+  // tiles = 1.551 / 1.534 / 1.546 / 1.584 ms
+  constexpr int kSeg = 48;
   const auto key = std::make_tuple((int)like.get_device(), B, tiles_r, tiles_c, nwg);
   std::lock_guard<std::mutex> lock(mu);
-  const bool lists = tile_lists();
   auto it = cache->find(key);
   if (it != cache->end()) {
-    *sw = lists ? (int)(it->second.numel() / nwg) : 1;
-    *sk = lists ? 1 : nwg;
+    *sw = (int)(it->second.numel() / nwg);
+    *sk = 1;
     return it->second.data_ptr<int>();
   }
   const int64_t n = tds_conv2_bwd_walk(nullptr, B, tiles_r, tiles_c, nwg, kSeg);
@@ -164,9 +134,9 @@ const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg
               tiles_r, " x ", tiles_c, ")");
   auto host = at::empty({n / nwg, (int64_t)nwg}, at::TensorOptions().dtype(at::kInt));
   tds_conv2_bwd_walk(host.data_ptr<int>(), B, tiles_r, tiles_c, nwg, kSeg);
-  *sw = lists ? (int)(n / nwg) : 1;
-  *sk = lists ? 1 : nwg;
-  Tensor dev = (lists ? host.t().contiguous() : host).to(like.device());
+  *sw = (int)(n / nwg);
+  *sk = 1;
+  Tensor dev = host.t().contiguous().to(like.device());
   (*cache)[key] = dev;
   return dev.data_ptr<int>();
 }
@@ -263,8 +233,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_l1_forward(
                 "fused_l1_forward: packing conv2's weights needs mag, wp_out and wd_out");
     need(*w2, at::kFloat, {32, 16, 5, 5}, "conv2.weight");
     TORCH_CHECK(reinterpret_cast<uintptr_t>(w2->data_ptr()) % 16 == 0, "fused_l1_forward: conv2.weight must be 16-B aligned");
-    need(*wp_out, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
-    need(*wd_out, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
+    need(*wp_out, at::kShort, {13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
+    need(*wd_out, at::kShort, {25 * 4 * 16 * 8}, "conv2 dgrad pack");
     pw2 = w2->data_ptr<float>();
     pwp = wp_out->data_ptr<int16_t>();
     pwd = wd_out->data_ptr<int16_t>();
@@ -360,8 +330,8 @@ std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tens
   TORCH_CHECK(reinterpret_cast<uintptr_t>(w2.data_ptr()) % 16 == 0, "conv2_pack: conv2.weight must be 16-B aligned");
   const float* ps = optf(p1_scale, 1, "p1_scale");
   c10::DeviceGuard guard(w2.device());
-  auto wp = at::empty({2 * 13 * 2 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
-  auto wd = at::empty({2 * 25 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
+  auto wp = at::empty({13 * 2 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
+  auto wd = at::empty({25 * 4 * 16 * 8}, w2.options().dtype(at::kShort));
   tds_conv2_pack_weights(w2.data_ptr<float>(), wp.data_ptr<int16_t>(), wd.data_ptr<int16_t>(), opt_mag(mag), ps,
                          stream_of(w2), write_p1);
   check_launches("conv2_pack");
@@ -378,7 +348,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1,
   TORCH_CHECK(p1.dim() == 4 && p1.size(1) == p1.size(2) && p1.size(3) == 16, "fused_conv2_forward: p1 [B,P,P,16]");
   const int64_t B = p1.size(0), P = p1.size(1);
   need(p1, at::kHalf, {B, P, P, 16}, "p1");
-  need(wp, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
+  need(wp, at::kShort, {13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
   need(b2, at::kFloat, {32}, "conv2.bias");
   const float* g = optf(gamma2, 32, "bn2.weight");
   TORCH_CHECK(B <= 255 && P >= 2, "fused_conv2_forward: 1 <= batch <= 255 and P >= 2");
@@ -411,7 +381,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_conv2_forward_bn(
   TORCH_CHECK(p1.dim() == 4 && p1.size(1) == p1.size(2) && p1.size(3) == 16, "fused_conv2_forward_bn: p1 [B,P,P,16]");
   const int64_t B = p1.size(0), P = p1.size(1);
   need(p1, at::kHalf, {B, P, P, 16}, "p1");
-  need(wp, at::kShort, {2 * 13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
+  need(wp, at::kShort, {13 * 2 * 4 * 16 * 8}, "conv2 fwd pack");
   need(b2, at::kFloat, {32}, "conv2.bias");
   const float* g = optf(gamma2, 32, "bn2.weight");
   TORCH_CHECK(B <= 255 && P >= 2, "fused_conv2_forward_bn: 1 <= batch <= 255 and P >= 2");
@@ -532,47 +502,6 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, c
   }
   check_launches("fused_head_forward_aff_ce");
   return {logits, loss, dlogits};
-}
-
-// The head forward applying the activation exchange's deferred weight update on the way through
-// (head_pb.hip HPUpd): wfc <- wfc - lr * scale * dy_all^T X with X decoded from the gathered zero-
-// suppressed encodings (meta_all [W, R] int32, vals_all [W, cap]), then the logits with the updated
-// weight.  rows: rows per rank (dy_all [W * rows, NC]).
-Tensor fused_head_forward_upd(const Tensor& ya, const Tensor& aff2, const Tensor& wfc, const c10::optional<Tensor>& bfc,
-                              int64_t P, const Tensor& dy_all, const Tensor& meta_all, const Tensor& vals_all,
-                              int64_t rows, double scale, double lr) {
-  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_upd: ya must be [B,32,PB]");
-  const int64_t B = ya.size(0), Q = P / 2;
-  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
-  need(aff2, at::kFloat, {64}, "aff2");
-  const int64_t NC = wfc.size(0), K = 32 * Q * Q;
-  need(wfc, at::kFloat, {NC, K}, "fc.weight");
-  const float* bf = optf(bfc, NC, "fc.bias");
-  TORCH_CHECK(meta_all.dim() == 2 && vals_all.dim() == 2 && meta_all.size(0) == vals_all.size(0),
-              "fused_head_forward_upd: meta_all [W, R], vals_all [W, cap]");
-  const int64_t W = meta_all.size(0), M = dy_all.size(0);
-  TORCH_CHECK(rows >= 1 && M == W * rows, "fused_head_forward_upd: dy_all must hold W * rows rows");
-  need(dy_all, at::kFloat, {M, NC}, "dy_all");
-  TORCH_CHECK(meta_all.scalar_type() == at::kInt && meta_all.is_contiguous() && vals_all.scalar_type() == at::kFloat &&
-                  vals_all.is_contiguous(), "fused_head_forward_upd: meta_all int32, vals_all fp32, contiguous");
-  const int64_t NP = tds_zs_npages(rows * K);
-  TORCH_CHECK(meta_all.size(1) >= NP * 65, "fused_head_forward_upd: meta_all rows shorter than the page records");
-  c10::DeviceGuard guard(ya.device());
-  hipStream_t st = stream_of(ya);
-  auto wo = at::empty({W, NP * 64}, ya.options().dtype(at::kInt));
-  tds_zs_word_offsets(meta_all.data_ptr<int>(), meta_all.size(1), NP, (int)W, wo.data_ptr<int>(), st);
-  const int nblk = 32 * tds_head_pb_nblk((int)Q);
-  auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
-  auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
-  auto logits = at::empty({B, NC}, ya.options());
-  const int rc = tds_head_fwd_pb_upd(ya.data_ptr<float>(), const_cast<float*>(wfc.data_ptr<float>()), bf,
-                                     aff2.data_ptr<float>(), part.data_ptr<double>(), lsum.data_ptr<double>(),
-                                     logits.data_ptr<float>(), (int)B, (int)Q, (int)NC, dy_all.data_ptr<float>(), (int)M,
-                                     (int)rows, meta_all.data_ptr<int>(), meta_all.size(1), wo.data_ptr<int>(), NP * 64,
-                                     vals_all.data_ptr<float>(), vals_all.size(1), (float)scale, (float)lr, st);
-  TORCH_CHECK(rc == 0, "fused_head_forward_upd: unsupported shape (B <= 8, W * rows <= 40, P/2 >= 8)");
-  check_launches("fused_head_forward_upd");
-  return logits;
 }
 
 // ---------------------------------------------------------------- head forward (BN2 finalize + fc)
@@ -786,7 +715,7 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
               "allocates it): the staging's row loads may read past the last row");
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
-  need(wd, at::kShort, {2 * 25 * 4 * 16 * 8}, "conv2 dgrad pack");
+  need(wd, at::kShort, {25 * 4 * 16 * 8}, "conv2 dgrad pack");
   TORCH_CHECK(B <= 63 && P >= 2, "fused_conv2_backward_y2: 1 <= batch <= 63 and P >= 2");
   c10::DeviceGuard guard(p1.device());
   hipStream_t st = stream_of(p1);
@@ -901,37 +830,17 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_l1_backward(const Tensor& dp1, 
   const float* g = optf(gamma1, 16, "bn1.weight");
   c10::DeviceGuard guard(x.device());
   hipStream_t st = stream_of(x);
-  static const bool pairs = [] {  // the bf16-pair LDS layout (convnet_fused.hip PAIRS), opt-in
-    const char* e = std::getenv("TDS_L1B_PAIRS");
-    return e && e[0] == '1';
-  }();
-  const int nwg = l1b_wg(levels, levels && pairs), rows = tds_l1_bwd_rows(nwg);
+  const int nwg = l1b_wg(levels), rows = tds_l1_bwd_rows(nwg);
   auto partial = at::empty({(int64_t)rows * 16 * 27}, x.options().dtype(at::kDouble));
   auto dw1 = sink_or_empty(dw_out, {16, 1, 5, 5}, x, "dw1_out");
   auto db1 = sink_or_empty(db_out, {16}, x, "db1_out");
   auto dg = sink_or_empty(dg_out, {16}, x, "dgamma1_out");
   auto dbe = sink_or_empty(dbe_out, {16}, x, "dbeta1_out");
-  // the reduction and the closed-form gradients inside the launch: opt-in (TDS_FUSED_FIN_L1=1) --
-  // its 1280 partial rows of 432 doubles need several dependent rounds of loads in one workgroup,
-  // measured slower than the two small launches it replaces (l1 backward 0.172 ms vs 0.131 + 2 x
-  // 0.007, r5_s3)
-  static const bool fin_l1 = [] {
-    const char* e = std::getenv("TDS_FUSED_FIN_L1");
-    return e && e[0] == '1';
-  }();
-  if (fin_l1 && tds_fused_fin_enabled()) {
-    auto work = at::empty({tds_l1_bwd_fin_doubles(nwg)}, x.options().dtype(at::kDouble));
-    TdsL1Fin lf{work.data_ptr<double>(), gram.data_ptr<double>(), g, stats1.data_ptr<float>(), dw1.data_ptr<float>(),
-                db1.data_ptr<float>(), dg.data_ptr<float>(), dbe.data_ptr<float>(), (float)scale};
-    tds_l1_bwd(x.data_ptr(), levels, pairs, dp1.data_ptr(), reinterpret_cast<const uint32_t*>(dp1_dec.data_ptr<int>()),
-               p1.data_ptr(), idx1.data_ptr<uint8_t>(), w1.data_ptr<float>(), b1.data_ptr<float>(),
-               partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st, &lf);
-    check_launches("fused_l1_backward");
-    return {dw1, db1, dg, dbe};
-  }
-  tds_l1_bwd(x.data_ptr(), levels, pairs, dp1.data_ptr(), reinterpret_cast<const uint32_t*>(dp1_dec.data_ptr<int>()),
-             p1.data_ptr(), idx1.data_ptr<uint8_t>(),
-             w1.data_ptr<float>(), b1.data_ptr<float>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
+  // (the reduction and the closed-form gradients inside this launch measured slower than the one
+  // small launch below: its 1280 partial rows of 432 doubles need several dependent rounds of loads
+  // in one workgroup, l1 backward 0.172 ms vs 0.131 + 2 x 0.007, r5_s3)
+  tds_l1_bwd(x.data_ptr(), levels, dp1.data_ptr(), reinterpret_cast<const uint32_t*>(dp1_dec.data_ptr<int>()),
+             p1.data_ptr(), idx1.data_ptr<uint8_t>(), partial.data_ptr<double>(), nwg, (int)B, (int)H, (int)W, st);
   auto bsum = at::empty({16 * 27}, x.options().dtype(at::kDouble));
   // the partials' reduction and the closed-form gradients in one launch (tds_l1_reduce_finalize)
   if (!tds_l1_reduce_finalize(partial.data_ptr<double>(), rows, bsum.data_ptr<double>(), gram.data_ptr<double>(),
@@ -964,27 +873,6 @@ Tensor zs_encode(const Tensor& x, const Tensor& meta_out, const Tensor& values_o
   tds_zs_encode(x.data_ptr<float>(), n, meta_out.data_ptr<int>(), values_out.data_ptr<float>(), values_out.numel(),
                 nnz.data_ptr<int64_t>(), stream_of(x));
   check_launches("zs_encode");
-  return nnz;
-}
-
-// The zs encoding of X = relu(a * ya + b) (the fused head's fc input, [B, 32*Q*Q] flat in the fc
-// order) read from ya [B,32,PB] and aff2 [64]: the dense X is never written (kernels/zs_exchange.hip)
-Tensor zs_encode_ya(const Tensor& ya, const Tensor& aff2, int64_t P, const Tensor& meta_out, const Tensor& values_out) {
-  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "zs_encode_ya: ya must be [B,32,PB]");
-  const int64_t B = ya.size(0), Q = P / 2, n = B * 32 * Q * Q, NP = tds_zs_npages(n);
-  TORCH_CHECK(Q >= 8, "zs_encode_ya: needs P/2 >= 8");
-  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
-  need(aff2, at::kFloat, {64}, "aff2");
-  need(meta_out, at::kInt, {NP * 65}, "zs meta_out");
-  TORCH_CHECK(values_out.is_cuda() && values_out.scalar_type() == at::kFloat && values_out.is_contiguous() &&
-                  values_out.dim() == 1 && values_out.device() == ya.device(),
-              "zs_encode_ya: values_out fp32 1-d contiguous GPU (ya's device)");
-  TORCH_CHECK(n < ((int64_t)1 << 31), "zs_encode_ya: the format's int32 offsets need < 2^31 elements");
-  c10::DeviceGuard guard(ya.device());
-  auto nnz = at::empty({}, ya.options().dtype(at::kLong));
-  tds_zs_encode_ya(ya.data_ptr<float>(), aff2.data_ptr<float>(), (int)B, (int)Q, meta_out.data_ptr<int>(),
-                   values_out.data_ptr<float>(), values_out.numel(), nnz.data_ptr<int64_t>(), stream_of(ya));
-  check_launches("zs_encode_ya");
   return nnz;
 }
 
@@ -1099,8 +987,6 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor(a!) out) -> ()",
       &zs_seg_decode);
   m.def("zs_decode(Tensor meta, Tensor values, Tensor(a!) out) -> ()", &zs_decode);
-  m.def("zs_encode_ya(Tensor ya, Tensor aff2, int P, Tensor(a!) meta_out, Tensor(b!) values_out) -> Tensor",
-        &zs_encode_ya);
   m.def(
       "fused_l1_forward(Tensor x, Tensor w1, Tensor b1, Tensor? gamma1, Tensor? beta1, Tensor(a!)? rm1, "
       "Tensor(b!)? rv1, Tensor(c!)? nbt1, float momentum, float eps, Tensor? asum=None, Tensor? strips=None, "
@@ -1110,7 +996,6 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("l1_input_stats(Tensor x) -> (Tensor, Tensor)", &l1_input_stats);
   m.def("conv2_pack(Tensor w2, Tensor(a!)? mag=None, Tensor? p1_scale=None, bool write_p1=True) -> (Tensor, Tensor)",
         &conv2_pack);
-  m.def("conv2_split() -> int", []() -> int64_t { return tds_conv2_split(); });
   m.def(
       "fused_conv2_forward(Tensor p1, Tensor wp, Tensor b2, Tensor? gamma2, Tensor(a!)? mag=None) -> "
       "(Tensor, Tensor, Tensor, Tensor)",
@@ -1137,10 +1022,6 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def("fused_head_forward_aff_ce(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor labels, "
         "Tensor(a!)? x_out=None) -> (Tensor, Tensor, Tensor)",
         &fused_head_forward_aff_ce);
-  m.def(
-      "fused_head_forward_upd(Tensor ya, Tensor aff2, Tensor(a!) wfc, Tensor? bfc, int P, Tensor dy_all, Tensor meta_all, "
-      "Tensor vals_all, int rows, float scale, float lr) -> Tensor",
-      &fused_head_forward_upd);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
   m.def("mag_numel(int B, int P) -> int", &mag_numel);
   m.def("mag_ypart_count() -> int", &mag_ypart_count);

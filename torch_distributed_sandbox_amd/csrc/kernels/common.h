@@ -26,32 +26,26 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 typedef short bf16x4 __attribute__((ext_vector_type(4)));
 
 // Streaming stores of the step's large tensors (y2, ya, p1, idx1, g2m, the fc weight update):
-// non-temporal (TDS_NT=1, default).  A/B on MI355X, bench 3 x alternating: 3.64 vs 3.80 ms per
+// non-temporal.  A/B on MI355X against plain stores, bench 3 x alternating: 3.64 vs 3.80 ms per
 // step (layer-1 forward -68 us, conv2 forward -12 us, head backward -18 us;
 // tools/gpu_sessions/r2_split2.sh).  dp1 keeps plain stores: the layer-1 backward reads it
 // right after the conv2 backward (nt there measured +15 us).
-#ifndef TDS_NT
-#define TDS_NT 1
-#endif
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st_stream(float* p, float v) {
-  if constexpr (TDS_NT) __builtin_nontemporal_store(v, p); else *p = v;
+  __builtin_nontemporal_store(v, p);
 }
 __device__ __forceinline__ void st_stream(uint32_t* p, uint32_t v) {
-  if constexpr (TDS_NT) __builtin_nontemporal_store(v, p); else *p = v;
+  __builtin_nontemporal_store(v, p);
 }
 __device__ __forceinline__ void st_stream(float4* p, float4 v) {
-  if constexpr (TDS_NT) __builtin_nontemporal_store(__builtin_bit_cast(f32x4, v), reinterpret_cast<f32x4*>(p));
-  else *p = v;
+  __builtin_nontemporal_store(__builtin_bit_cast(f32x4, v), reinterpret_cast<f32x4*>(p));
 }
 __device__ __forceinline__ void st_stream(float2* p, float2 v) {
-  if constexpr (TDS_NT) __builtin_nontemporal_store(__builtin_bit_cast(f32x2, v), reinterpret_cast<f32x2*>(p));
-  else *p = v;
+  __builtin_nontemporal_store(__builtin_bit_cast(f32x2, v), reinterpret_cast<f32x2*>(p));
 }
 __device__ __forceinline__ void st_stream(uint2* p, uint2 v) {
-  if constexpr (TDS_NT) __builtin_nontemporal_store(__builtin_bit_cast(u32x2, v), reinterpret_cast<u32x2*>(p));
-  else *p = v;
+  __builtin_nontemporal_store(__builtin_bit_cast(u32x2, v), reinterpret_cast<u32x2*>(p));
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (TDS_WAVE - 1); }

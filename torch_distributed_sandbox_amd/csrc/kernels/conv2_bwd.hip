@@ -1,11 +1,9 @@
 // conv2 backward: BN2 / ReLU / max-pool backward fused into conv2 dgrad + wgrad
 // (SURVEY.md §2.4 K16-K21), one persistent 8-wave workgroup per CU, on v_mfma_f32_16x16x32_f16
-// in the TF32 class (round-4 default, conv2_common.h kConv2Split = 0): ONE MFMA per product, both
-// operands rounded once to fp16 (11 significant bits, TF32's significand):
+// in the TF32 class (conv2_common.h): ONE MFMA per product, both operands rounded once to fp16 (11
+// significant bits, TF32's significand):
 //   dgrad: dp1 = convT(dy2, w2)  -- dy2 rounded once (scaled), w2 as packed by conv2_pack (scaled)
 //   wgrad: dw2 = sum dy2 (x) p1  -- dy2 rounded once, p1 the forward's fp16 operand as is
-// (the -DTDS_CONV2_SPLIT=1 variant build keeps the round-3 fp16x2 split: the exact operand as fp16
-// hi + lo, 2 MFMAs per product; the "lo" planes and operands below exist only in that build)
 // dy2 is carried with a power-of-two scale 2^e: from the step's magnitude bounds (max |y2 - b2|
 // per channel from the forward, max |g2m| from the head backward) |dy2| <= |k1| max|g2m| + |k2|
 // (max|y2 - b2| + |b2|) + |k3| per channel, and e puts the largest bound in [2^14, 2^15) -- no fp16
@@ -21,9 +19,9 @@
 //   waves 2/3 : wgrad, taps 0-12 / 13-25 (tap 25 = the bias "ones" column), both co halves, K =
 //               32 pixels = two output rows, operands by ds_read_b64_tr_b16; accumulated over the
 //               workgroup's tiles; slab[wg][26][32][16] reduced in fixed order afterwards.
-//   waves 4-7 : staging: y2 / pooled gradient g2m / p1 -> BN2 / ReLU / pool backward (dy2 =
-//               k1*dz + k2*y2 + k3 at the window's argmax) -> dy2 fp16 hi|lo rows (scaled) and
-//               p1 fp16 rows in LDS.
+//   waves 4-7 : staging: y2h / argmax codes a2 / pooled gradient g2m / p1 -> BN2 / ReLU / pool
+//               backward (dy2 = k1*dz + k2*y2 + k3, dz at the window's argmax) -> dy2 fp16 rows
+//               (scaled) and p1 fp16 rows in LDS.
 //
 // ROLLING WINDOW.  A tile of 8 output rows needs dy2 and p1 on 12 rows (2-row halo above and
 // below).  Each workgroup walks vertical SEGMENTS of tiles (one tile column of one image, ~48
@@ -37,10 +35,10 @@
 // were the kernel's largest cost (timing build without them: 1.05 vs 1.56 ms).
 //
 // LDS, in ROW BLOCKS (one staged image row of 20 records per block):
-//   dy2 row block: 4 planes (hi co0-15, hi co16-31, lo co0-15, lo co16-31) x 20 x 32 B = 2560 B
+//   dy2 row block: 2 planes (co 0-15, co 16-31) x 20 x 32 B = 1280 B
 //   p1  row block: 1 plane x 20 x 32 B = 640 B
 //   3 ring slots of 12 row blocks (tile k in slot k % 3: 4 top + 8 new rows), 2 dgrad exchange
-//   slots, BN2 backward constants + the dy2 scale: 132 240 B.
+//   slots, BN2 backward constants + the dy2 scale, 2 pooled-gradient tiles: 96 400 B.
 // One bare s_barrier per tile (after lgkmcnt(0)) separates producer and consumers: while the
 // consumers read slot k%3, the staging writes slot (k+1)%3's new rows and slot (k+2)%3's top
 // (the slot of tile k-1, finished); the register loads for tile k+3 are already in flight.
@@ -52,31 +50,12 @@
 #include "launchers.h"
 #include "pooled_layout.h"
 
-#ifndef TDS_BR_MIX
-#define TDS_BR_MIX 1  // fast staging path on v_fma_mix_f32 (fp16 y2h operands, no conversions)
-#endif
-#ifndef TDS_BR_LOAD_PRIO
-// wave priority while a staging wave issues its look-ahead loads: 3 helped the two-set staging of
-// round 2; with three sets, 0 (r5_s13: isolated 0.668 -> 0.659 ms, driver's command 2.197 ->
-// 2.191 ms, two alternating runs each)
-#define TDS_BR_LOAD_PRIO 0
-#endif
-#ifndef TDS_BR_STAGE_SETS
-#define TDS_BR_STAGE_SETS 3  // staging look-ahead register sets (2 or 3)
-#endif
-#ifndef TDS_BR_PIECE_ROT
-#define TDS_BR_PIECE_ROT 1  // a tile's 64 extra p1 pieces to wave 5 (wave 4 takes the 64 extra items)
-#endif
-#ifndef TDS_BR_MFMA_PRIO
-#define TDS_BR_MFMA_PRIO 1  // wave priority of the dgrad / wgrad waves
-#endif
-
 namespace tds {
 
 constexpr int BR_TH = 8, BR_TC = 16;       // output tile
 constexpr int BR_SC = BR_TC + 4;           // 20 staged columns (2-pixel halo each side)
 constexpr int BR_DPL = BR_SC * 32;         // 640 B: one plane of a row block
-constexpr int BR_DROW = 4 * BR_DPL;        // 2560 B: dy2 row block
+constexpr int BR_DROW = 2 * BR_DPL;        // 1280 B: dy2 row block
 constexpr int BR_PROW = BR_DPL;            // 640 B: p1 row block (one fp16 plane)
 constexpr int BR_THREADS = 512;
 constexpr int BR_SLOT = 12;                                  // row blocks per ring slot
@@ -87,7 +66,7 @@ constexpr int BR_OFF_X = BR_OFF_P + 3 * BR_SLOT * BR_PROW;   // 2 exchange slots
 constexpr int BR_OFF_K = BR_OFF_X + 2 * BR_XCHG;             // 160 floats of constants + 4
 constexpr int BR_KINV = 160;  // kc[160] = 2^-e * 2^-ew (dp1), kc[161] = 2^-e / p1 scale (weight taps), kc[162] = 2^-e (bias),
                               // kc[163] = 2^kd (the dp1h store factor)
-// the pipelined staging's pooled-gradient tiles (TDS_BR_GB): 2 x [4 pooled rows][10 cols][32 ch] fp32
+// the pipelined staging's pooled-gradient tiles (BRStager GB): 2 x [4 pooled rows][10 cols][32 ch] fp32
 constexpr int BR_GTILE = 4 * 10 * 32;
 constexpr int BR_OFF_G = (BR_OFF_K + (5 * 32 + 4) * 4 + 15) / 16 * 16;
 constexpr int BR_LDS = BR_OFF_G + 2 * BR_GTILE * 4;
@@ -96,8 +75,10 @@ static_assert(BR_LDS <= 160 * 1024 && BR_OFF_X % 16 == 0 && BR_OFF_K % 16 == 0, 
 // walk table entries (tds_conv2_bwd_walk): bit 31 = first tile of a segment, bit 30 = past the
 // end of this workgroup's list (the low bits then repeat its last tile), b << 24 | tr << 12 | tc
 constexpr uint32_t kWalkStart = 0x80000000u, kWalkEnd = 0x40000000u;
-constexpr int BR_WALK_PAD = 8;  // end entries after each list (>= 2 x TDS_BR_STAGE_SETS)
-static_assert(BR_WALK_PAD >= 2 * TDS_BR_STAGE_SETS, "walk padding below the staging look-ahead");
+constexpr int BR_STAGE_SETS = 3;  // staging look-ahead register sets (br_stage)
+constexpr int BR_WALK_PAD = 8;    // end entries after each list (>= 2 x BR_STAGE_SETS)
+static_assert(BR_WALK_PAD >= 2 * BR_STAGE_SETS, "walk padding below the staging look-ahead");
+constexpr int BR_MFMA_PRIO = 1;   // wave priority of the dgrad / wgrad waves (above the staging's VALU)
 struct BRTile {
   int b, r0, c0;
   bool start, end;
@@ -144,9 +125,7 @@ __device__ __forceinline__ void br_load_w_group(const uint4* __restrict__ wd, f3
 #pragma unroll
   for (int k = 0; k < G::NKY; ++k) {
     const int s = (G::KY0 + k) * 5 + G::KX;  // flipped-tap index of the dgrad pack
-    const uint4 h = wd[s * 64 + lane], l = wd[(25 + s) * 64 + lane];
-    R[5 * I + k][0] = __builtin_bit_cast(f32x4, h);
-    R[5 * I + k][1] = __builtin_bit_cast(f32x4, l);
+    R[5 * I + k][0] = __builtin_bit_cast(f32x4, wd[s * 64 + lane]);
   }
 }
 
@@ -204,18 +183,15 @@ struct DgSeq {
 };
 
 // one flat, fully unrolled sequence of A-fragment rows with operands fetched two steps ahead
-// across group boundaries (one MFMA wave per SIMD: nothing else hides a bubble)
-// A rows read TDS_BR_DG_DEPTH rows ahead (ring of DEPTH + 1; round 4: 2)
-#ifndef TDS_BR_DG_DEPTH
-#define TDS_BR_DG_DEPTH 2
-#endif
+// across group boundaries (one MFMA wave per SIMD: nothing else hides a bubble), through a ring
+// of DP + 1 registers
 template <int D, int DIAG>
 __device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][2], f32x4 (&acc)[8], int hp, int li) {
   using Q = DgSeq<D>;
-  constexpr int DP = TDS_BR_DG_DEPTH;
+  constexpr int DP = 2;
 #pragma unroll
   for (int o = 0; o < 8; ++o) acc[o] = f32x4{0.f, 0.f, 0.f, 0.f};
-  s16x8 ah[DP + 1];  // dy2 hi only: the single-rounded operand
+  s16x8 ah[DP + 1];
   auto load_a = [&](int s, int buf) {
     const int i = Q::grp(s), r = Q::row(s);
     const char* rb = rw.d(Q::ky0(i) + r) + (Q::kx(i) + li) * 32;
@@ -232,107 +208,24 @@ __device__ __forceinline__ void br_dgrad(const BRRows& rw, const f32x4 (&R)[13][
     for (int k = 0; k < 5; ++k) {
       const int o = r - k;
       if (k < Q::nky(i) && o >= 0 && o < 8)
-        acc[o] = mmaw<DIAG>(ah[s % (DP + 1)], __builtin_bit_cast(s16x8, R[5 * i + k][0]),
-                            __builtin_bit_cast(s16x8, R[5 * i + k][1]), acc[o]);
+        acc[o] = mmaw<DIAG>(ah[s % (DP + 1)], __builtin_bit_cast(s16x8, R[5 * i + k][0]), acc[o]);
     }
   }
 }
 
 // ---------------------------------------------------------------------------- wgrad
-// c += (ahi + alo) * b: split, the wgrad's exact operand is dy2 (A), p1 (B) the single-rounded
-// one; unsplit (TDS_CONV2_SPLIT 0, conv2_common.h) c += ahi * b, both rounded once
-template <int DIAG>
-__device__ __forceinline__ f32x4 mma2a(const s16x8& ahi, const s16x8& alo, const s16x8& b, f32x4 c) {
-  if constexpr (DIAG == 1) {
-    c[0] += (float)((int)(ahi[0] ^ alo[1] ^ b[2]) & 1);
-    return c;
-  } else if constexpr (kConv2Split) {
-    c = mfma_f16(alo, b, c);
-    return mfma_f16(ahi, b, c);
-  } else {
-    return mfma_f16(ahi, b, c);
-  }
-}
-
-template <int E, int DIAG>
-__device__ __forceinline__ void br_wgrad(const BRRows& rw, f32x4 (&wacc)[13][2], int lane, const s16x8& ones) {
-  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-  s16x8 ahi[2][2], alo[2][2], bv[3];
-  auto drow = [&](int r) { return rw.d(r); };
-  auto prow = [&](int r) { return rw.p(r); };
-  auto load_a = [&](int m, int slot) {
-    const char* r0 = drow(2 * m + 2) + (2 + 4 * g + q4) * 32 + p4 * 8;
-    const char* r1 = drow(2 * m + 3) + (2 + 4 * g + q4) * 32 + p4 * 8;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const s16x4 x0 = ldtr<DIAG>(r0 + h * BR_DPL), x1 = ldtr<DIAG>(r1 + h * BR_DPL);
-      ahi[slot][h] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-      if constexpr (kConv2Split) {
-        const s16x4 y0 = ldtr<DIAG>(r0 + (2 + h) * BR_DPL), y1 = ldtr<DIAG>(r1 + (2 + h) * BR_DPL);
-        alo[slot][h] = s16x8{y0[0], y0[1], y0[2], y0[3], y1[0], y1[1], y1[2], y1[3]};
-      } else {
-        alo[slot][h] = ahi[slot][h];  // (unused)
-      }
-    }
-  };
-  auto load_b = [&](int s, int buf) {
-    const int m = s / 13, tap = 13 * E + s % 13;
-    if (tap < 25) {
-      const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-      const int col = (kx + 4 * g + q4) * 32 + p4 * 8;
-      const char* r0 = prow(2 * m + ky) + col;
-      const char* r1 = prow(2 * m + ky + 1) + col;
-      const s16x4 x0 = ldtr<DIAG>(r0), x1 = ldtr<DIAG>(r1);
-      bv[buf] = s16x8{x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
-    } else {
-      bv[buf] = ones;  // bias gradient column
-    }
-  };
-  // K-steps m in a rolled loop (static buffer indices inside), operands rotated at the end
-  load_a(0, 0);
-  load_b(0, 0);
-  load_b(1, 1);
-#pragma unroll 1
-  for (int m = 0; m < 4; ++m) {
-#pragma unroll
-    for (int k = 0; k < 13; ++k) {
-      if (k + 2 < 13) load_b(13 * m + k + 2, (k + 2) % 3);
-      else if (m + 1 < 4) load_b(13 * (m + 1) + k + 2 - 13, (k + 2) % 3);  // next K-step's first taps
-      if (k == 10 && m + 1 < 4) load_a(m + 1, 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) wacc[k][h] = mma2a<DIAG>(ahi[0][h], alo[0][h], bv[k % 3], wacc[k][h]);
-    }
-    // taps 0, 1 of the next K-step sit in buffers 1, 2 (13 % 3 == 1), its A in slot 1
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      ahi[0][h] = ahi[1][h];
-      alo[0][h] = alo[1][h];
-    }
-    bv[0] = bv[1];
-    bv[1] = bv[2];
-  }
-}
-
-// The same sums as one flat, fully unrolled sequence of the 52 (K-step, tap) steps with the B
-// operands read DEPTH steps ahead through a ring of DEPTH + 1 register sets, and the next K-step's A
-// operands ADEPTH steps before it starts (TDS_BR_WG_DEPTH > 0 selects it; 0 = the rolled loop
-// above, B two steps ahead).  Timing-only variants (r5_s2, conv2 backward with the wgrad waves
+// wgrad waves E = 0 / 1: taps 13E .. 13E+12 of both co halves, K = 32 pixels (two output rows) per
+// K-step, summed over the workgroup's tiles: one flat, fully unrolled sequence of the 52 (K-step,
+// tap) steps with the B operands read DEPTH steps ahead through a ring of DEPTH + 1 register sets,
+// and the next K-step's A operands AD steps before it starts.  Timing-only variants (r5_s2, conv2 backward with the wgrad waves
 // alone, no staging) put the rolled loop at ~36 cycles per MFMA with its LDS operand reads and ~21
 // without them: the reads' latency is what the MFMA stream waits on.
 // r5_s4: the wgrad waves alone 0.550 -> 0.347 ms at depth 6 (21.5 cycles per MFMA: their LDS read
 // latency hidden), the whole kernel 0.740 -> 0.728 (now bound by the staging); driver command
 // 2.282 / 2.284 -> 2.273 / 2.279 ms on the same box
-#ifndef TDS_BR_WG_DEPTH
-#define TDS_BR_WG_DEPTH 6
-#endif
-#ifndef TDS_BR_WG_ADEPTH
-#define TDS_BR_WG_ADEPTH 6
-#endif
-template <int E, int DIAG, int DEPTH>
+template <int E, int DIAG>
 __device__ __forceinline__ void br_wgrad_ring(const BRRows& rw, f32x4 (&wacc)[13][2], int lane, const s16x8& ones) {
-  static_assert(DEPTH >= 1 && TDS_BR_WG_ADEPTH >= 1 && TDS_BR_WG_ADEPTH < 13, "wgrad ring depths");
-  constexpr int NS = 4 * 13, AD = TDS_BR_WG_ADEPTH;
+  constexpr int NS = 4 * 13, DEPTH = 6, AD = 6;
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
   s16x8 a[2][2], bv[DEPTH + 1];
   auto load_a = [&](int m, int slot) {
@@ -365,7 +258,7 @@ __device__ __forceinline__ void br_wgrad_ring(const BRRows& rw, f32x4 (&wacc)[13
     if (k == 13 - AD && m + 1 < 4) load_a(m + 1, (m + 1) & 1);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int h = 0; h < 2; ++h) wacc[k][h] = mma2a<DIAG>(a[m & 1][h], a[m & 1][h], bv[s % (DEPTH + 1)], wacc[k][h]);
+    for (int h = 0; h < 2; ++h) wacc[k][h] = mmaw<DIAG>(a[m & 1][h], bv[s % (DEPTH + 1)], wacc[k][h]);
   }
 }
 
@@ -416,7 +309,7 @@ __device__ __forceinline__ BRRows br_rows(char* smem, int k) {
 
 template <int ROLE, int DIAG>  // ROLE 0/1 = dgrad wave D, 2/3 = wgrad
 __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict__ wdpack, char* smem) {
-  __builtin_amdgcn_s_setprio(TDS_BR_MFMA_PRIO);  // above the staging waves' VALU work
+  __builtin_amdgcn_s_setprio(BR_MFMA_PRIO);
   const int lane = threadIdx.x & 63;
   const int li = lane & 15, g = lane >> 4;
   f32x4 R[13][2];
@@ -452,10 +345,8 @@ __device__ __forceinline__ void br_mfma(const BRArgs& a, const uint4* __restrict
                              lane, prev.b, prev.r0, prev.c0, a.P, inv);
       br_dgrad<ROLE, DIAG>(rw, R, acc, hp, li);
       br_xchg_put<ROLE>(reinterpret_cast<f32x4*>(smem + BR_OFF_X + (kk & 1) * BR_XCHG), acc, lane);
-    } else if constexpr (TDS_BR_WG_DEPTH > 0 && !kConv2Split) {
-      br_wgrad_ring<ROLE - 2, DIAG, TDS_BR_WG_DEPTH>(rw, R, lane, ones);
     } else {
-      br_wgrad<ROLE - 2, DIAG>(rw, R, lane, ones);
+      br_wgrad_ring<ROLE - 2, DIAG>(rw, R, lane, ones);
     }
     prev = cur;
   }
@@ -487,21 +378,14 @@ constexpr uint32_t kBROob = 0xFFFFFFF0u;
 // window, BR_CW-channel chunk): NR/2 x 10 windows x 32/BR_CW chunks.  BIG: the 32 g2m planes of an
 // image exceed a 4 GiB buffer-descriptor range (64-bit g2m loads); a template parameter, because
 // two load paths under a runtime branch make the compiler wait vmcnt(0) at their merge.
-// BR_CW = 8 (TDS_BR_CW): a pixel's 8 channels of y2h are one 16-B load and one 16-B dy2 store; a
-// tile's 160 items leave one per lane for waves 4-6 (r5_s14 PMC: the texture data path was busy
-// 81 % of the kernel, ~64 cycles per staging load instruction -- fewer, wider loads).
-#ifndef TDS_BR_CW  // (r5_s16: 8 vs 4 -- isolated 0.696 -> 0.688 ms, driver's command 2.213 -> 2.199, 3 + 3 alternating)
-#define TDS_BR_CW 8
-#endif
-constexpr int BR_CW = TDS_BR_CW;
-static_assert(BR_CW == 4 || BR_CW == 8, "staging chunk: 4 or 8 channels");
+// BR_CW = 8: a pixel's 8 channels of y2h are one 16-B load and one 16-B dy2 store; a tile's 160
+// items leave one per lane for waves 4-6 (r5_s14 PMC: the texture data path was busy 81 % of the
+// kernel, ~64 cycles per staging load instruction -- fewer, wider loads; r5_s16: 8 vs 4 channels
+// isolated 0.696 -> 0.688 ms).
+constexpr int BR_CW = 8;
 constexpr int BR_NCH = 32 / BR_CW;  // chunks per window
-template <int CW> struct BRYv;
-template <> struct BRYv<4> { typedef uint2 T; };
-template <> struct BRYv<8> { typedef uint4 T; };
-typedef BRYv<BR_CW>::T BRY;  // one pixel's BR_CW fp16 y2h values
+typedef uint4 BRY;                  // one pixel's BR_CW fp16 y2h values
 
-__device__ __forceinline__ uint32_t br_word(const uint2& v, int i) { return i == 0 ? v.x : v.y; }
 __device__ __forceinline__ uint32_t br_word(const uint4& v, int i) {
   return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w;
 }
@@ -518,22 +402,8 @@ __device__ __forceinline__ float br_fma_y(float a, const V& v, int cc, float c) 
   return d;
 }
 
-__device__ __forceinline__ void br_load_y_impl(__amdgpu_buffer_rsrc_t r, uint32_t off, uint2& v) {
-  v = __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
-__device__ __forceinline__ void br_load_y_impl(__amdgpu_buffer_rsrc_t r, uint32_t off, uint4& v) {
-  v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
-}
-__device__ __forceinline__ void br_put_words(char* r, const uint32_t (&h)[2]) {
-  *reinterpret_cast<uint2*>(r) = make_uint2(h[0], h[1]);
-}
-__device__ __forceinline__ void br_put_words(char* r, const uint32_t (&h)[4]) {
-  *reinterpret_cast<uint4*>(r) = make_uint4(h[0], h[1], h[2], h[3]);
-}
 __device__ __forceinline__ BRY br_load_y(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  BRY v;
-  br_load_y_impl(r, off, v);
-  return v;
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
 // GB (the pipelined 8-row sets): the tile's pooled gradient g2m is not gathered per item (BR_CW
@@ -559,13 +429,9 @@ struct BRStager {
   float4 rm0, rm1;      // GB: this lane's run, columns 1-4 and 5-8
   float rl, rr;         // GB: its columns 0 and 9 (the halo)
 
-  // the j-th p1 piece of staging lane tid: the set past 256 goes to a wave without an extra item
-  // (4-channel items: the 64 past 256 are wave 4's, pieces go to wave 5; 8-channel items: waves 4-6
-  // hold the 160, pieces go to wave 7) (TDS_BR_PIECE_ROT)
-  __device__ __forceinline__ static int piece(int tid, int j) {
-    constexpr int rot = BR_CW == 8 ? 64 : 192;
-    return (TDS_BR_PIECE_ROT != 0 && j == 1 ? ((tid + rot) & 255) : tid) + 256 * j;
-  }
+  // the j-th p1 piece of staging lane tid: the set past 256 goes to a wave without an item (waves
+  // 4-6 hold the 160 items, the extra pieces go to wave 7)
+  __device__ __forceinline__ static int piece(int tid, int j) { return (j == 1 ? ((tid + 64) & 255) : tid) + 256 * j; }
 
   __device__ __forceinline__ static void item_geom(int it, int& wy, int& wx) {
     const int w = (it < ITEMS ? it : 0) / BR_NCH;
@@ -686,7 +552,7 @@ struct BRStager {
     d[288] = rr;
   }
 
-  // BN2 / ReLU / pool backward of the staged windows -> dy2 hi|lo rows at dbase; p1 -> pbase;
+  // BN2 / ReLU / pool backward of the staged windows -> dy2 rows at dbase; p1 -> pbase;
   // MIRROR: rows 4-7 stored a second time at dmir / pmir (the next slot's top rows).
   // dy2 = k1*dz + k2*y2 + k3, dz = pooled gradient at the window's argmax, which the forward
   // stored (a2, conv2_common.h: as max_pool2d's backward scatters to the indices its forward saved;
@@ -768,10 +634,8 @@ struct BRStager {
       } else if (fast) {
 #pragma unroll
         for (int cc = 0; cc < BR_CW; ++cc) {
-          // y2h values straight into v_fma_mix_f32 (TDS_BR_MIX; br_fma_y), else converted once
-          auto fy = [&](float k, int q, float c) {
-            return TDS_BR_MIX ? br_fma_y(k, yv[u][q], cc, c) : fmaf(k, y[q][cc], c);
-          };
+          // y2h values straight into v_fma_mix_f32 (br_fma_y)
+          auto fy = [&](float k, int q, float c) { return br_fma_y(k, yv[u][q], cc, c); };
           const uint32_t code = ((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u);  // the forward's argmax
           // the pooled gradient folded into the constant: select + FMA per pixel.  The 4 compares
           // go first (4 SGPR-pair masks): one VCC reused compare -> select -> compare cost an
@@ -780,10 +644,7 @@ struct BRStager {
           bool eq[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) eq[q] = code == (uint32_t)q;
-#ifndef TDS_BR_BATCH_CMP
-#define TDS_BR_BATCH_CMP 1
-#endif
-          if constexpr (TDS_BR_BATCH_CMP != 0) __builtin_amdgcn_sched_barrier(0);
+          __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int q = 0; q < 4; ++q) d[q][cc] = fy(k2[cc], q, eq[q] ? k3g : k3[cc]);
         }
@@ -804,21 +665,14 @@ struct BRStager {
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        uint32_t h[BR_CW / 2], l[BR_CW / 2];  // (k1..k3 carry the scale 2^e: d is dy2 * 2^e)
+        uint32_t h[BR_CW / 2];  // dy2 rounded once (TF32 class; k1..k3 carry the scale 2^e: d is dy2 * 2^e)
 #pragma unroll
-        for (int i = 0; i < BR_CW / 2; ++i) {
-          l[i] = 0u;
-          if constexpr (kConv2Split)
-            split2_f16_mix(d[q][2 * i], d[q][2 * i + 1], h[i], l[i]);
-          else  // dy2 rounded once (TF32-class, conv2_common.h): no lo planes
-            h[i] = cvt2_f16(d[q][2 * i], d[q][2 * i + 1]);
-        }
+        for (int i = 0; i < BR_CW / 2; ++i) h[i] = cvt2_f16(d[q][2 * i], d[q][2 * i + 1]);
         const int lr = 2 * wy + (q >> 1);
         const int ro = (2 * wx + (q & 1)) * 32 + (cb & 15) * 2;
         char* rec = dbase + lr * BR_DROW + ro;
         auto put = [&](char* r) {
-          br_put_words(r + (cb >> 4) * BR_DPL, h);
-          if constexpr (kConv2Split) br_put_words(r + (2 + (cb >> 4)) * BR_DPL, l);
+          *reinterpret_cast<uint4*>(r + (cb >> 4) * BR_DPL) = make_uint4(h[0], h[1], h[2], h[3]);
         };
         put(rec);
         if (MIRROR && lr >= 4) put(dmir + (lr - 4) * BR_DROW + ro);
@@ -855,11 +709,8 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   auto ptop = [&](int j) { return smem + BR_OFF_P + (j % 3) * BR_SLOT * BR_PROW; };
   // tile j's new rows, its last 4 mirrored into tile j+1's top (overwritten by a prologue when
   // tile j+1 starts a segment: a later iteration, past a barrier)
-#ifndef TDS_BR_GB
-#define TDS_BR_GB 1  // the pipelined sets take g2m by runs through an LDS tile (BRStager GB)
-#endif
-  constexpr bool GBS = TDS_BR_GB != 0 && TDS_BR_STAGE_SETS == 3;
-  typedef BRStager<8, BIG, DIAG, GBS> Set;
+  // the pipelined sets take g2m by runs through an LDS tile (BRStager GB)
+  typedef BRStager<8, BIG, DIAG, true> Set;
   float* gtile = reinterpret_cast<float*>(smem + BR_OFF_G);
   auto gbuf = [&](int j) { return gtile + (j & 1) * BR_GTILE; };
   auto stage = [&](Set& s, int j, const BRTile& x) {
@@ -873,7 +724,7 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
     pro.load(a, x.b, x.r0 - 2, x.c0, tid);
     pro.template store<false>(a, x.r0 - 2, x.c0, tid, dtop(j), ptop(j), kc, nullptr, nullptr);
   };
-  // TDS_BR_STAGE_SETS register sets (2 or 3): tile j's new-row loads are issued that many tiles
+  // BR_STAGE_SETS register sets: tile j's new-row loads are issued that many tiles
   // before they are staged (r5_s6: the staging's global loads, ~20 KB a tile, are latency-bound --
   // the staging alone ran 0.53 ms, 0.26 without its loads; the sets live in VGPRs the MFMA
   // roles' 180 leave free).  Loads are unconditional (past the end: the list's last tile again,
@@ -882,37 +733,31 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   BRClock<DIAG> clk;
   clk.start();
   auto tile = [&](int j) { return br_decode(a.walk, j, a.sk, a.w); };
+  // (the staging waves run at priority 0: with three sets in flight the look-ahead loads no longer
+  // need a raised priority, r5_s13: isolated 0.668 -> 0.659 ms without it)
   auto ld = [&](Set& s, int j) {
     const BRTile x = tile(j);
-    // the look-ahead loads issue at raised priority (the SIMD's MFMA wave otherwise delays
-    // them), the BN2-backward VALU work at the lowest (tools/gpu_sessions/r2_knobs.sh: 1.519 /
-    // 1.501 ms vs 1.522-1.567 ms in six runs of the same kernel without priorities)
-    __builtin_amdgcn_s_setprio(TDS_BR_LOAD_PRIO);
     s.load(a, x.b, x.r0 + 2, x.c0, tid);
-    __builtin_amdgcn_s_setprio(0);
   };
   // stage tile j from set s if it exists (a segment start also gets its prologue: after the set is
   // stored and before it is reloaded, so its registers are the set's); false past the list's end
-  // GBS: nxt (the set holding tile j+1) puts its g2m runs into tile j+1's LDS tile; they are read
+  // nxt (the set holding tile j+1) puts its g2m runs into tile j+1's LDS tile; they are read
   // after the next barrier, and that tile's previous contents (tile j-1) were read before this one
   auto stage_if = [&](Set& s, Set& nxt, int j) {
     const BRTile x = tile(j);
     if (!x.end) {
       stage(s, j, x);
-      if constexpr (GBS) nxt.put_runs(gbuf(j + 1), tid);
+      nxt.put_runs(gbuf(j + 1), tid);
       if (x.start) prologue(j, x);
     }
     return !x.end;
   };
-#if TDS_BR_STAGE_SETS == 3
   Set st0, st1, st2;
   {
     const BRTile x0 = tile(0);
     if (!x0.end) {  // tile 0: its own synchronous set, g2m per item (no LDS tile precedes it)
       BRStager<8, BIG, DIAG, false> s0;
-      __builtin_amdgcn_s_setprio(TDS_BR_LOAD_PRIO);
       s0.load(a, x0.b, x0.r0 + 2, x0.c0, tid);
-      __builtin_amdgcn_s_setprio(0);
       s0.template store<true>(a, x0.r0 + 2, x0.c0, tid, dtop(0) + 4 * BR_DROW, ptop(0) + 4 * BR_PROW, kc, dtop(1),
                               ptop(1));
       prologue(0, x0);
@@ -921,7 +766,7 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
   ld(st1, 1);
   ld(st2, 2);
   ld(st0, 3);
-  if constexpr (GBS) st1.put_runs(gbuf(1), tid);  // tile 1's, read after the loop's first barrier
+  st1.put_runs(gbuf(1), tid);  // tile 1's, read after the loop's first barrier
   // iteration kk: tile kk+1 from st1 (reload: kk+4), kk+2 from st2 (kk+5), kk+3 from st0 (kk+6);
   // one exit and every set reloaded on every path (the two-set loop's rule, below).  The walk
   // table carries BR_WALK_PAD end entries: the last iteration (kk <= n-1) reads tile kk + 6.
@@ -944,37 +789,6 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
     ld(st0, kk + 6);
     more = has3;
   }
-#else
-  Set st0, st1;
-  {
-    const BRTile x0 = tile(0);
-    if (!x0.end) {
-      ld(st0, 0);
-      stage(st0, 0, x0);
-      prologue(0, x0);
-    }
-  }
-  ld(st1, 1);
-  ld(st0, 2);
-  // iteration kk stages tile kk+1 and loads tile kk+3 (set st1), then stages tile kk+2 and loads
-  // tile kk+4 (set st0).  One exit, and both load sets issued on every path through the body:
-  // with a break between them, the structurized loop had a path back to the header on which
-  // st1's loads were the youngest, and the waitcnt pass then drained BOTH sets (vmcnt(0)) at
-  // every staging of st1 -- the look-ahead was one tile, not two.
-  bool more = !tile(0).end;
-  for (int kk = 0; more; kk += 2) {
-    clk.barrier();  // consumers start tile kk
-    const bool second = stage_if(st1, st0, kk + 1);
-    ld(st1, kk + 3);
-    bool has2 = false;
-    if (second) {
-      clk.barrier();  // consumers start tile kk + 1
-      has2 = stage_if(st0, st1, kk + 2);
-    }
-    ld(st0, kk + 4);  // (past the end: the list's last tile again, never staged)
-    more = has2;
-  }
-#endif
   clk.barrier();
   clk.report();
 }

@@ -54,51 +54,22 @@ __device__ __forceinline__ float f16_val(uint32_t h) {
 //   waves idle (an idle role only takes part in the per-tile barriers), +32 staging without its
 //   global loads, +64 staging without the BN2 / pool backward math
 constexpr bool diag_no_lds(int D) { return D == 2 || (D >= 16 && (D & 2)); }
+// Operand precision of the three conv2 products (forward, data gradient, weight gradient): ONE
+// v_mfma_f32_16x16x32_f16 per product, both operands rounded once to fp16 -- 11 significant bits,
+// exactly TF32's significand (10 explicit bits + the implicit one), products exact, fp32
+// accumulation: the arithmetic of the reference's cuDNN convolutions under PyTorch's default
+// allow_tf32 (Ampere).  fp16's narrower exponent range is covered by exact power-of-two scales:
+// the packed weights' (conv2_pack.hip), p1's range guard (convnet_fused.hip) and dy2's
+// magnitude-bound scale (conv2_bwd.hip) keep each operand's largest value in [2^14, 2^16), so
+// values down to 2^-28 of it are normal fp16.  (Rounds 2-3 carried one operand as fp16 hi + lo,
+// two MFMAs per product; that build is in git history.)
 template <int DIAG>
-__device__ __forceinline__ f32x4 mma3(const s16x8& ah, const s16x8& al, const s16x8& bh, const s16x8& bl, f32x4 c) {
+__device__ __forceinline__ f32x4 mmaw(const s16x8& a, const s16x8& b, f32x4 c) {
   if constexpr (DIAG == 1) {
-    c[0] += (float)((int)(ah[0] ^ al[1] ^ bh[2] ^ bl[3]) & 1);
+    c[0] += (float)((int)(a[0] ^ b[2]) & 1);
     return c;
   } else {
-    return mfma_bf16x3(ah, al, bh, bl, c);
-  }
-}
-// fp16x2 (bf16x3.h): c += a * (bh + bl)
-template <int DIAG>
-__device__ __forceinline__ f32x4 mma2(const s16x8& a, const s16x8& bh, const s16x8& bl, f32x4 c) {
-  if constexpr (DIAG == 1) {
-    c[0] += (float)((int)(a[0] ^ bh[2] ^ bl[3]) & 1);
-    return c;
-  } else {
-    return mfma_f16x2(a, bh, bl, c);
-  }
-}
-
-// Operand precision of the three conv2 products (forward, data gradient, weight gradient):
-//   TDS_CONV2_SPLIT 0 (default): ONE v_mfma_f32_16x16x32_f16 per product, both operands rounded
-//     once to fp16 -- 11 significant bits, exactly TF32's significand (10 explicit bits + the
-//     implicit one), products exact, fp32 accumulation: the arithmetic of the reference's cuDNN
-//     convolutions under PyTorch's default allow_tf32 (Ampere).  fp16's narrower exponent range
-//     is covered by exact power-of-two scales: the packed weights' (conv2_pack.hip), p1's range
-//     guard (convnet_fused.hip) and dy2's magnitude-bound scale (conv2_bwd.hip) keep each
-//     operand's largest value in [2^14, 2^16), so values down to 2^-28 of it are normal fp16.
-//   TDS_CONV2_SPLIT 1: fp16x2 -- one operand carried as fp16 hi + lo (22 bits), two MFMAs per
-//     product, <= 2^-11 per product (rounds 2-3).
-#ifndef TDS_CONV2_SPLIT
-#define TDS_CONV2_SPLIT 0
-#endif
-constexpr bool kConv2Split = TDS_CONV2_SPLIT != 0;
-
-// c += a * b, b given as fp16 hi (+ lo when split)
-template <int DIAG>
-__device__ __forceinline__ f32x4 mmaw(const s16x8& a, const s16x8& bh, const s16x8& bl, f32x4 c) {
-  if constexpr (kConv2Split) {
-    return mma2<DIAG>(a, bh, bl, c);
-  } else if constexpr (DIAG == 1) {
-    c[0] += (float)((int)(a[0] ^ bh[2]) & 1);
-    return c;
-  } else {
-    return mfma_f16(a, bh, c);
+    return mfma_f16(a, b, c);
   }
 }
 template <int DIAG>

@@ -1,15 +1,14 @@
 // conv2 forward v2 (Conv2d(16, 32, 5, pad 2), mnist_onegpu.py:20):
 // y2 = conv(p1) + b2, stored as y2h (NHWC fp16, bias-free, scaled: conv2_common.h), plus BN2
 // batch-statistic partials, on
-// v_mfma_f32_16x16x32_f16 in the TF32 class (round-4 default, conv2_common.h kConv2Split = 0):
-// ONE MFMA per product, p1 and the weights each rounded once to fp16 (11 significant bits, TF32's
-// significand) at exact power-of-two range scales; the round-3 fp16x2 form (weights as fp16 hi +
-// lo, 2 MFMAs per product) is the -DTDS_CONV2_SPLIT=1 variant build.  Laid out for SEVERAL small
+// v_mfma_f32_16x16x32_f16 in the TF32 class (conv2_common.h): ONE MFMA per product, p1 and the
+// weights each rounded once to fp16 (11 significant bits, TF32's significand) at exact
+// power-of-two range scales.  Laid out for SEVERAL small
 // workgroups per CU (3 at 168 VGPRs, 44 KiB LDS):
 //   * 4 waves per workgroup, output tile 8 rows x 16 columns (staged p1: 12 x 20 records of
 //     32 B);
 //   * weights in REGISTERS: wave w owns co half nt = w & 1 and output rows 4(w>>1) .. +3,
-//     all 13 K-steps of its half (13 fp16 fragments; 13 x (hi, lo) in the split build), loaded once;
+//     all 13 K-steps of its half (13 fp16 fragments), loaded once;
 //   * p1 staged by LDS-DMA (global_load_lds_dwordx4, no VGPRs, no VALU), double-buffered:
 //     tile t+1 streams in while tile t is on the MFMAs;
 //   * the epilogue of tile t (y2h stores + statistics) runs after tile t+1's DMA is issued,
@@ -43,14 +42,11 @@ constexpr int F2_THREADS = 256;
 constexpr int F2_PGROUPS = 8;                          // DMA groups of 32 records (1 KiB)
 constexpr int F2_PPLANE = F2_PGROUPS * 32 * 32;        // 8192 B (256 records of 32 B, 240 used)
 constexpr int F2_PBUF = F2_PPLANE;                     // one fp16 plane
-// TDS_F2_WG: workgroups per CU.  3 (default): the staged tile holds the y2h halves themselves
-// (channel pairs joined by one DPP move), 44 KiB of LDS, 168 VGPRs -- 0.427 -> 0.407 ms isolated,
-// bench 2.443 -> 2.406 ms (tools/gpu_sessions/r4_s22.sh); 2: one dword per value, 60 KiB
-#ifndef TDS_F2_WG
-#define TDS_F2_WG 3
-#endif
-constexpr bool F2_H16 = TDS_F2_WG == 3;
-constexpr int F2_PXREC = F2_H16 ? 32 * 2 + 16 : 32 * 4 + 16;  // staged pixel record: 32 co + 16 B pad (banks)
+// 3 workgroups per CU: the staged tile holds the y2h halves themselves (channel pairs joined by one
+// DPP move), 44 KiB of LDS, 168 VGPRs -- 0.427 -> 0.407 ms isolated against 2 workgroups with one
+// dword per value (tools/gpu_sessions/r4_s22.sh)
+constexpr int F2_WG = 3;
+constexpr int F2_PXREC = 32 * 2 + 16;  // staged pixel record: 32 co fp16 + 16 B pad (banks)
 constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;           // a finished tile's padded staging buffer
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
 constexpr int F2_YSTAGE = 32 * 32 * 4 + 32 * 2 * 4;     // pooled block: 32 co x 4 x 8 fp32 = 4 KiB, + a2 words
@@ -58,7 +54,7 @@ constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
 constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging
 constexpr int F2_DMA_PER_WAVE = F2_PGROUPS / (F2_THREADS / 64);  // 2
 static_assert(F2_LDS % 16 == 0, "LDS carve");
-static_assert(TDS_F2_WG * F2_LDS <= 160 * 1024, "workgroups per CU");
+static_assert(F2_WG * F2_LDS <= 160 * 1024, "workgroups per CU");
 
 // 16 zero bytes: the DMA source of staged records outside the image
 __device__ __attribute__((aligned(16))) uint32_t g_f2_zero[4] = {0u, 0u, 0u, 0u};
@@ -88,11 +84,8 @@ __device__ __forceinline__ void f2_dma(const uint4* __restrict__ p1, const F2Til
 // a 4-deep register ring, 3 rows ahead of the MFMAs that use them: the rows at a group's
 // edges feed only 1-2 MFMA triples, too few to hide an LDS round trip one row ahead.
 template <int DIAG>
-__device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13][2], f32x4 (&acc)[4], int RH, int lane) {
-#ifndef TDS_F2_DEPTH
-#define TDS_F2_DEPTH 4
-#endif
-  constexpr int DEPTH = TDS_F2_DEPTH;
+__device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13], f32x4 (&acc)[4], int RH, int lane) {
+  constexpr int DEPTH = 4;
   const int li = lane & 15, g = lane >> 4;
   const int boff = (g & 1) * 16;  // ci half of the 32-B record
   const char* ph = buf;
@@ -124,16 +117,14 @@ __device__ __forceinline__ void f2_compute(const char* buf, const f32x4 (&W)[13]
       for (int ky = 0; ky < 5; ++ky) {
         const int o = R - ky;
         if (o >= 0 && o < 4)
-          acc[o] = mmaw<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[2 * ky + grp][0]),
-                              __builtin_bit_cast(s16x8, W[2 * ky + grp][1]), acc[o]);
+          acc[o] = mmaw<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[2 * ky + grp]), acc[o]);
       }
     } else {
 #pragma unroll
       for (int kp = 0; kp < 3; ++kp) {
         const int o = R - 2 * kp;
         if (o >= 0 && o < 4)
-          acc[o] = mmaw<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[10 + kp][0]),
-                              __builtin_bit_cast(s16x8, W[10 + kp][1]), acc[o]);
+          acc[o] = mmaw<DIAG>(ah[cur], __builtin_bit_cast(s16x8, W[10 + kp]), acc[o]);
       }
     }
   }
@@ -243,26 +234,17 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
             ((uint32_t)(cb0[sl] >> sh) & 0xFFFFu) | ((uint32_t)(cb1[sl] >> sh) << 16);
     }
   }
-  if constexpr (F2_H16) {
-    // the y2h halves: even lanes join their odd neighbour's (channel co + 1) by a quad-permute DPP
-    // move and write the pair (row, px) of channels co, co + 1
+  // the y2h halves: even lanes join their odd neighbour's (channel co + 1) by a quad-permute DPP
+  // move and write the pair (row, px) of channels co, co + 1
 #pragma unroll
-    for (int o = 0; o < 4; ++o)
+  for (int o = 0; o < 4; ++o)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)h[o][r], 0xF5, 0xF, 0xF, false);  // quad [1,1,3,3]
-        if ((li & 1) == 0)
-          *reinterpret_cast<uint32_t*>(stage + (((4 * RH + o) * F2_TC + 4 * g + r) * F2_PXREC) + co * 2) =
-              (h[o][r] & 0xFFFFu) | (nb << 16);
-      }
-  } else {
-    // the y2h bits, one dword per value (f2_store packs channel pairs)
-#pragma unroll
-    for (int o = 0; o < 4; ++o)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        *reinterpret_cast<uint32_t*>(stage + f2_stage_off(4 * RH + o, 4 * g + r, co >> 2) + (co & 3) * 4) = h[o][r];
-  }
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)h[o][r], 0xF5, 0xF, 0xF, false);  // quad [1,1,3,3]
+      if ((li & 1) == 0)
+        *reinterpret_cast<uint32_t*>(stage + (((4 * RH + o) * F2_TC + 4 * g + r) * F2_PXREC) + co * 2) =
+            (h[o][r] & 0xFFFFu) | (nb << 16);
+    }
 }
 
 // the workgroup stores the staged pooled block: thread e -> channel e / 8, float4 e % 8
@@ -294,26 +276,13 @@ template <int DIAG>
 __device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, unsigned short* __restrict__ y2h, int P) {
   if constexpr (DIAG == 4) return;  // timing-only: no y2h
   const int e = threadIdx.x;
-#ifndef TDS_F2_QPX
-#define TDS_F2_QPX 1
-#endif
-  const int qpx = F2_H16 && TDS_F2_QPX ? (int)((F2_QPX >> (4 * ((e >> 2) & 15))) & 15u) : (e >> 2) & 15;
+  const int qpx = (int)((F2_QPX >> (4 * ((e >> 2) & 15))) & 15u);
 #pragma unroll
   for (int i = 0; i < F2_TH * F2_TC * 4 / F2_THREADS; ++i) {
     const int q = e + F2_THREADS * i;
     const int row = q >> 6, px = qpx, c8 = q & 3;
     const int gr = x.r0 + row, gc = x.c0 + px;
-    uint4 v;
-    if constexpr (F2_H16) {
-      v = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, c8));
-    } else {
-      const uint4 a = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8));
-      const uint4 b = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, 2 * c8 + 1));
-      v.x = __builtin_amdgcn_perm(a.y, a.x, 0x05040100u);
-      v.y = __builtin_amdgcn_perm(a.w, a.z, 0x05040100u);
-      v.z = __builtin_amdgcn_perm(b.y, b.x, 0x05040100u);
-      v.w = __builtin_amdgcn_perm(b.w, b.z, 0x05040100u);
-    }
+    const uint4 v = *reinterpret_cast<const uint4*>(stage + f2_stage_off(row, px, c8));
     if (gr < P && gc < P)
       st_stream(reinterpret_cast<float4*>(y2h + (((int64_t)x.b * P + gr) * P + gc) * 32 + c8 * 8),
                 __builtin_bit_cast(float4, v));
@@ -344,12 +313,10 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     x.c0 = tc * F2_TC;
     return x;
   };
-  // weights: fwd pack wp[hl][s][nt][g][co16][j8] -> uint4 index ((hl*13 + s)*2 + nt)*64 + lane
-  f32x4 W[13][2];
+  // weights: fwd pack wp[s][nt][g][co16][j8] -> uint4 index (s * 2 + nt) * 64 + lane (conv2_pack.hip)
+  f32x4 W[13];
 #pragma unroll
-  for (int s = 0; s < 13; ++s)
-#pragma unroll
-    for (int hl = 0; hl < 2; ++hl) W[s][hl] = __builtin_bit_cast(f32x4, wpack[((hl * 13 + s) * 2 + NT) * 64 + lane]);
+  for (int s = 0; s < 13; ++s) W[s] = __builtin_bit_cast(f32x4, wpack[(s * 2 + NT) * 64 + lane]);
   const float bco = bias[16 * NT + li];
   // the packed weights' and p1's power-of-two scales (conv2_pack.hip): y2 = acc * inv + b2, exact
   const float inv = scales != nullptr ? __uint_as_float(scales[0]) * __uint_as_float(scales[1]) : 1.f;
@@ -359,11 +326,8 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
   // BN2 partials: each tile's sums in fp32 (<= 16 values per lane), accumulated across the
-  // workgroup's tiles in fp64 (TDS_F2_STAT64; 0: one fp32 running sum per lane over ~1.8 K values,
-  // whose rounding grows with n (1 + mean^2 / var) in var = E[q] - E[s]^2)
-#ifndef TDS_F2_STAT64
-#define TDS_F2_STAT64 1
-#endif
+  // workgroup's tiles in fp64 (one fp32 running sum per lane over ~1.8 K values had rounding that
+  // grows with n (1 + mean^2 / var) in var = E[q] - E[s]^2)
   f2v s_acc = {0.f, 0.f}, q_acc = {0.f, 0.f};
   double s_d = 0.0, q_d = 0.0;
   uint32_t ymx = 0u;
@@ -391,12 +355,10 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
     else
       f2_stage<true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
                      bco, inv, ksc, neg, zg, s_acc, q_acc, ymx, a2);
-    if constexpr (TDS_F2_STAT64 != 0) {
-      s_d += (double)(s_acc.x + s_acc.y);
-      q_d += (double)(q_acc.x + q_acc.y);
-      s_acc = f2v{0.f, 0.f};
-      q_acc = f2v{0.f, 0.f};
-    }
+    s_d += (double)(s_acc.x + s_acc.y);
+    q_d += (double)(q_acc.x + q_acc.y);
+    s_acc = f2v{0.f, 0.f};
+    q_acc = f2v{0.f, 0.f};
     prev = cur;
     have_prev = true;
   }
@@ -410,8 +372,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 16, 64));
   ymx = max(ymx, (uint32_t)__shfl_xor((int)ymx, 32, 64));
   // BN2 partials: reduce the 4 lane groups, then the two row-halves of this co half
-  double s_sum = TDS_F2_STAT64 != 0 ? s_d : (double)(s_acc.x + s_acc.y);
-  double q_sum = TDS_F2_STAT64 != 0 ? q_d : (double)(q_acc.x + q_acc.y);
+  double s_sum = s_d, q_sum = q_d;
   s_sum += __shfl_xor(s_sum, 16, 64);
   s_sum += __shfl_xor(s_sum, 32, 64);
   q_sum += __shfl_xor(q_sum, 16, 64);
@@ -497,7 +458,7 @@ __device__ __forceinline__ void f2_finalize(const F2Fin& fin, const double* __re
 }
 
 template <int DIAG>
-__global__ __launch_bounds__(F2_THREADS, TDS_F2_WG) void conv2_fwd2_kernel(const uint4* __restrict__ p1,
+__global__ __launch_bounds__(F2_THREADS, F2_WG) void conv2_fwd2_kernel(const uint4* __restrict__ p1,
                                                                    const uint4* __restrict__ wpack,
                                                                    const float* __restrict__ bias,
                                                                    const float* __restrict__ gamma,
@@ -524,8 +485,8 @@ __global__ __launch_bounds__(F2_THREADS, TDS_F2_WG) void conv2_fwd2_kernel(const
 
 using namespace tds;
 
-// workgroups the forward launches (BN2 partial rows): TDS_F2_WG per CU
-int tds_conv2_fwd2_num_wg() { return TDS_F2_WG * tds_conv2_num_wg(); }
+// workgroups the forward launches (BN2 partial rows): F2_WG per CU
+int tds_conv2_fwd2_num_wg() { return F2_WG * tds_conv2_num_wg(); }
 
 void tds_conv2_fwd2_tiles(int P, int* tiles_r, int* tiles_c) {
   *tiles_r = (P + F2_TH - 1) / F2_TH;

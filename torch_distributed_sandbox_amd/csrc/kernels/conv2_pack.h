@@ -11,8 +11,8 @@ __device__ __forceinline__ void conv2_pack_block(const float* __restrict__ w2, s
                                                  short* __restrict__ wd, uint32_t* __restrict__ mag,
                                                  const float* __restrict__ p1_scale, int write_p1, int blk,
                                                  int nblk) {
-  const int FW = 13 * 2 * 4 * 16 * 8;  // per hl plane (fwd)
-  const int DW = 25 * 4 * 16 * 8;      // per hl plane (dgrad)
+  const int FW = 13 * 2 * 4 * 16 * 8;  // fwd fragments
+  const int DW = 25 * 4 * 16 * 8;      // dgrad fragments
   __shared__ float red[16];
   float wsc = 1.f;
   if (mag != nullptr) {
@@ -105,19 +105,13 @@ __device__ __forceinline__ void conv2_pack_block(const float* __restrict__ w2, s
       const int kx = s < 10 ? 2 * (s & 1) + (g >> 1) : 4;
       const int ci = 8 * (g & 1) + j, co = nt * 16 + co_in;
       const float v = ky < 5 ? w2[(co * 16 + ci) * 25 + ky * 5 + kx] * wsc : 0.f;
-      unsigned short hi, lo;
-      split_f16(v, hi, lo);
-      wp[e] = (short)hi;
-      wp[FW + e] = (short)lo;
+      wp[e] = (short)f16_bits(v);  // rounded once (TF32 class, conv2_common.h)
     } else {
       const int f = e - FW;
       const int j = f & 7, ci = (f >> 3) & 15, g = (f >> 7) & 3, s = f >> 9;
       const int co = 8 * g + j;
       const float v = w2[(co * 16 + ci) * 25 + (24 - s)] * wsc;
-      unsigned short hi, lo;
-      split_f16(v, hi, lo);
-      wd[f] = (short)hi;
-      wd[DW + f] = (short)lo;
+      wd[f] = (short)f16_bits(v);
     }
   }
 }

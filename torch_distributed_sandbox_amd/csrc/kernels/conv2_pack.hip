@@ -1,7 +1,7 @@
 // conv2 of the ConvNet (Conv2d(16, 32, 5, stride 1, pad 2), mnist_onegpu.py:20): shared host
 // pieces of the fp16 MFMA kernels (conv2_fwd2.hip, conv2_bwd.hip) -- the on-device weight
-// packing into MFMA fragment order (w * 2^ew rounded once to fp16 in the TF32-class default; fp16
-// hi + lo in the -DTDS_CONV2_SPLIT=1 build), the deterministic fp64 reduction of the per-workgroup weight
+// packing into MFMA fragment order (w * 2^ew rounded once to fp16: the TF32 class), the
+// deterministic fp64 reduction of the per-workgroup weight
 // gradient slabs, and the blocked tile order table.  SURVEY.md §2.4 K5 / K19 / K20.
 //
 // Activation formats (produced/consumed by convnet_fused.hip and the conv2 kernels):
@@ -19,16 +19,15 @@
 namespace tds {
 
 // ---------------------------------------------------------------------------- weight packing
-// fwd : wp[hl][s<13][nt<2][g<4][co16][j8], k = 32s+8g+j, ci = 8(g&1)+j, taps paired so that one
+// fwd : wp[s<13][nt<2][g<4][co16][j8], k = 32s+8g+j, ci = 8(g&1)+j, taps paired so that one
 //       input-row A fragment serves every output row:  s < 10: (ky = s>>1, kx = 2(s&1) + (g>>1));
 //       s = 10 + kp: (ky = 2kp + (g>>1), kx = 4)  (ky = 5 -> zero)
-// dgrad: wd[hl][s<25][g<4][ci16][j8],      k = 32s+8g+j -> tap' = s, co = 8g+j; w = w2[co][ci][24-tap']
+// dgrad: wd[s<25][g<4][ci16][j8],      k = 32s+8g+j -> tap' = s, co = 8g+j; w = w2[co][ci][24-tap']
 // mag (optional, kMagScales + 2 words): the step's magnitude bounds (max |y2| per channel, max
 // |g2m|) are reset here, at the start of the conv2 forward they feed (conv2_fwd2.hip, head_pb.hip).
 //
-// fp16 range of the exactly carried weights: hi + lo represents w to ~2^-22 relative only while
-// lo stays a normal fp16 (|w| >= ~2^-3); below fp16's normal range (|w| < 2^-14) even the
-// per-product bound 2^-11 of fp16x2 breaks.  With mag given, the packed weights are w * 2^ew with
+// fp16 range of the weights: below fp16's normal range (|w| < 2^-14) the 11-bit rounding breaks,
+// so with mag given the packed weights are w * 2^ew with
 // max |w| * 2^ew in [2^14, 2^15) (every block finds max |w| itself over the 12 800 weights, by
 // float4 loads from L2: no inter-block step), and mag[kMagScales] = 2^-ew, mag[kMagScales + 1] = 1 / p1_scale (the layer-1
 // range guard, convnet_fused.hip l1_gram; 1 when not given) are what the conv2 forward and
@@ -46,10 +45,7 @@ __global__ void conv2_pack_weights_kernel(const float* __restrict__ w2, short* _
 // workgroup rows (w = WGR_WAVES * j + wave, 16 loads in flight per lane, rows past the end clamped
 // and added as 0.0, which keeps the sum), then wave 0 adds the partials in a fixed order: deterministic.  At 4 waves the
 // 256 rows take 4 rounds of loads, at 16 one.
-#ifndef TDS_WGR_WAVES
-#define TDS_WGR_WAVES 16  // (r5_s47: 4.9 us at 4 waves with clamped loads, 4.8 at 16; guarded loads 20 us at 4)
-#endif
-constexpr int WGR_WAVES = TDS_WGR_WAVES;
+constexpr int WGR_WAVES = 16;  // (r5_s47: 4.9 us at 4 waves with clamped loads, 4.8 at 16; guarded loads 20 us at 4)
 __global__ __launch_bounds__(64 * WGR_WAVES) void conv2_wgrad_reduce_kernel(const float* __restrict__ slab, int nwg,
                                                                             float* __restrict__ dw,
                                                                             float* __restrict__ db, float scale) {
@@ -92,8 +88,6 @@ void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag
 }
 
 int tds_conv2_num_wg() { return tds_device_cus(); }
-
-int tds_conv2_split() { return kConv2Split ? 1 : 0; }  // the build's conv2 operand precision (conv2_common.h)
 
 void tds_conv2_wgrad_reduce(const float* slab, int nwg, float* dw, float* db, float scale, hipStream_t st) {
   hipLaunchKernelGGL(conv2_wgrad_reduce_kernel, dim3(26 * 512 / 64), dim3(64 * WGR_WAVES), 0, st, slab, nwg, dw, db, scale);

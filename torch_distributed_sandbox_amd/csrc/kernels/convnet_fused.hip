@@ -41,10 +41,7 @@ constexpr int L1_XR = L1_TR + 4;
 // (l1b_tap: g = 0 / 1 and 2 / 3 differ in ky), and 2*li spans the 16 banks of one parity, so
 // an odd stride puts the two groups on opposite parities (conflict-free; 80 = 16 mod 32 put
 // them on the same 16 banks -- 2-way on every read, 33 % of LDS cycles in the round-4 PMC)
-#ifndef TDS_L1_XS
-#define TDS_L1_XS 81
-#endif
-constexpr int L1_XS = TDS_L1_XS;
+constexpr int L1_XS = 81;
 // uint8 level input: x = L1_LEVEL_SCALE * level, the fp32 constant upsample_bilinear_u8 (elementwise.hip)
 // and ToTensor scale by
 constexpr float L1_LEVEL_SCALE = 1.f / 255.f;
@@ -77,9 +74,6 @@ __device__ __forceinline__ int l1b_tap(int g, int j) {
 // Pads read column kx0 + 1 = 5 or 3 of the row with weight 0 (levels are finite).  Bank parity:
 // the two groups of a 32-lane half read offsets of opposite parity (odd L1_XS, row-4 kx0 0/3 and
 // 2/(3,0)), so with 2*li spanning one parity the 32 lanes hit 32 banks.
-#ifndef TDS_L1_PAIR
-#define TDS_L1_PAIR 1
-#endif
 struct L1Pair {
   int ky, kx0;
   bool second;  // slot 2p+1 carries a real tap
@@ -101,7 +95,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
                                                       uint4* __restrict__ p1, uint8_t* __restrict__ idx1, int B,
                                                       int H, int W) {
   __shared__ __attribute__((aligned(16))) uint32_t xs[L1_XR * L1_XS];  // x as (bf16 hi << 16 | bf16 lo)
-  constexpr bool PAIR = LV && TDS_L1_PAIR;  // (TDS_L1_PAIR 0: A/B builds only)
+  constexpr bool PAIR = LV;  // level input: pair words (l1_pair)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
   const int P = H / 2, PW = W / 2;
@@ -204,12 +198,6 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
           v.w = __builtin_amdgcn_perm(f4, f3, 0x07060302u);
           l1_store4(xs + rr * L1_XS + 4 * cv, v);
           continue;
-        } else if constexpr (LV) {  // (A/B build) word = fp32 bits of the level = bf16 hi | lo 0
-          const uint32_t q = __float_as_uint(pre[u].x);
-          l1_store4(xs + rr * L1_XS + 4 * cv,
-                    make_uint4(__float_as_uint((float)(q & 0xFFu)), __float_as_uint((float)((q >> 8) & 0xFFu)),
-                               __float_as_uint((float)((q >> 16) & 0xFFu)), __float_as_uint((float)(q >> 24))));
-          continue;
         }
         nonfinite |= !__builtin_isfinite((pre[u].x + pre[u].y) + (pre[u].z + pre[u].w));
         uint32_t h01, l01, h23, l23;
@@ -265,14 +253,10 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
                 if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
               }
             }
-#if defined(TDS_L1_EXP) && TDS_L1_EXP == 2
-            acc[a][c] = f32x4{(float)(bh[0] ^ bl[1]), (float)wah[0], (float)wal[1], 0.f};
-#else
             if constexpr (LV)
               acc[a][c] = mfma_bf16x2a(wah, wal, bh, f32x4{0.f, 0.f, 0.f, 0.f});
             else
               acc[a][c] = mfma_bf16x3(wah, wal, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
-#endif
           }
         // BN1 affine -> 2x2 max-pool (first max in scan order) -> ReLU -> bf16 hi|lo record +
         // argmax byte (bit 2 = ReLU passes the gradient) for channels 4g .. 4g+3
@@ -328,11 +312,9 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
         if (prow < P && pcol < PW) {
           const int64_t rec = ((int64_t)b * P + prow) * PW + pcol;
           uint2* dst = reinterpret_cast<uint2*>(p1 + rec * 2);  // 32-B record: fp16[16]
-#ifndef TDS_L1_P1_NT
-#define TDS_L1_P1_NT 1
-#endif
-          if constexpr (TDS_L1_P1_NT != 0) st_stream(dst + g, make_uint2(h01, h23));
-          else dst[g] = make_uint2(h01, h23);
+          // (non-temporal: plain, allocating p1 stores cost the layer-1 conv +14 us and the conv2
+          // forward +23 us, r5_s44)
+          st_stream(dst + g, make_uint2(h01, h23));
           st_stream(reinterpret_cast<uint32_t*>(idx1 + rec * 16) + g, ixw);
         }
       }
@@ -501,99 +483,26 @@ __device__ __forceinline__ void lb_store4(uint32_t* p, const uint4& v) {
 constexpr int LM_XS = 137;
 constexpr int LM_ONES = LM_XS + 80;
 static_assert(LM_XS % 32 == 9 && 80 + 3 * 16 + 3 < LM_XS && 1 + 2 * 7 + 1 < LB_XR, "l1_bwd ones block");
-// Level input (LV): the x tile as bf16 PAIRS, so one ds_read_b32 is one packed B-operand register
-// (slots dc = 0, 1 of a window row) with no perm.  Copy E holds columns (2k, 2k+1) in dword k, copy
-// O columns (2k+1, 2k+2): a lane's pair starts at column kx + 2 + 4g (+ uniform offsets), even for
-// even kx (E) and odd for odd kx (O).  Row stride LV_RS = 41 = 9 mod 32 dwords and O based 5 banks
-// after E: a K-step's 32 lanes of one half (g0, g1) then touch rows ky of E at banks 9ky + 1..5 and
-// of O at 9ky + 6..9 -- 29 distinct banks for block 0 (rows 0..2 + row 3 col 0) and 18 for block
-// 1, no conflicts (the word layout above is conflict-free too since round 4, with twice the reads and
-// a perm per packed register).
-constexpr int LV_RS = 41;
-constexpr int LV_OB = 837;  // = 5 mod 32, >= 20 rows x 41
-constexpr int LV_WORDS = LV_OB + LB_XR * LV_RS;
-static_assert(LV_RS % 32 == 9 && LV_OB % 32 == 5 && LV_OB >= LB_XR * LV_RS && LV_RS >= 36, "l1_bwd level tile");
-constexpr int LM_X_BYTES = (LB_XR * LM_XS > LV_WORDS ? LB_XR * LM_XS : LV_WORDS) * 4;
-// LV: x holds uint8 levels (see l1_conv_bf3_kernel): the x operand is exact in bf16, two MFMAs per
-// product (dz hi, dz lo), half the B perms; the tap sums are scaled by L1_LEVEL_SCALE at the end.
+constexpr int LM_X_BYTES = LB_XR * LM_XS * 4;
+// LV: x holds uint8 levels (see l1_conv_bf3_kernel); the tap sums are scaled by L1_LEVEL_SCALE at
+// the end.
 // waves per SIMD the register budget is cut for (4: <= 128 VGPRs, 4 workgroups per CU with
 // fused_ops.cpp l1b_wg(); 3: <= 168, the measured configuration -- the compiler then keeps the
 // default variants at 124-126 VGPRs, so 4 workgroups still fit a CU)
-#ifndef TDS_L1B_WAVES
-#define TDS_L1B_WAVES 3
-#endif
-// H16 (level input, word layout): dz1 * x on ONE v_mfma_f32_16x16x32_f16 per product instead of
+constexpr int L1B_WAVES = 3;
+// Level input: dz1 * x on ONE v_mfma_f32_16x16x32_f16 per product instead of
 // the bf16 pair (dz hi, dz lo): dz1 is dp1h's fp16 value as stored and a level (0..255) is exact
 // in fp16, so every product is exact either way; the A operand is the fp16 bits themselves (no
 // conversion, no bf16 split) and the MFMA count halves.  x words are PAIRS: word c = fp16 x[c] |
 // fp16 x[c+1] << 16 (the l1_conv layout), so a window row's two B slots (dc = 0, 1) are one
 // ds_read_b32 at the dc = 0 address -- 4 reads and no v_perm per operand; the ones block holds
-// the pair (1.0, 1.0).
-#ifndef TDS_L1B_H16
-#define TDS_L1B_H16 1
-#endif
-// PAIRS (level input only; TDS_L1B_PAIRS=1 at run time, fused_ops.cpp): the conflict-free bf16-pair
-// x tile above.  Opt-in: timed slower than the default word layout (docs/KERNELS.md).
-// In-launch finalize of the layer-1 backward (common.h tds_arrive; replaces reduce_partials_kernel
-// and l1_finalize_kernel): groups of LB_GROUP workgroups, the last of a group sums the group's
-// partial rows into gsum[g], the last group-reducer sums the groups (fixed order) into bsum and
-// forms the closed-form layer-1 gradients (l1_finalize_one).
-constexpr int LB_GROUP = 32;
-struct LBFin {
-  uint32_t* sync;  // [0, ngroups): groups, [kSyncWordsPerSite - 1]: the group-reducers
-  double* gsum;    // [ngroups][16 * 27]
-  double* bsum;    // [16 * 27]
-  const double* gram;
-  int64_t n;
-  const float *w1, *b1, *gamma1, *stats1;
-  float *dw1, *db1, *dgamma1, *dbeta1;
-  float scale;
-};
-__device__ __forceinline__ void l1_finalize_one(int e, const double* __restrict__ bwd_sum,
-                                                const double* __restrict__ gram, int64_t n,
-                                                const float* __restrict__ w1, const float* __restrict__ b1,
-                                                const float* __restrict__ gamma1, const float* __restrict__ stats1,
-                                                float* __restrict__ dw1, float* __restrict__ db1,
-                                                float* __restrict__ dgamma1, float* __restrict__ dbeta1, float scale);
-
-__device__ __forceinline__ void l1_bwd_fin(const LBFin& fin, const double* __restrict__ partial, int* flag,
-                                           double* bs_lds) {
-  constexpr int R = 16 * LB_NACC;
-  const int nwg = (int)gridDim.x, wg = (int)blockIdx.x, tid = (int)threadIdx.x;
-  const int ng = (nwg + LB_GROUP - 1) / LB_GROUP, g = wg / LB_GROUP;
-  const int w0 = g * LB_GROUP, w1 = min(nwg, w0 + LB_GROUP);
-  if (!tds_arrive(fin.sync + g, (uint32_t)(w1 - w0), flag)) return;
-  for (int e = tid; e < R; e += 256) {
-    double s = 0.0;
-    // 8 loads in flight at a time: the kernel's 5-per-CU occupancy leaves <= 96 VGPRs
-#pragma unroll 1
-    for (int u0 = 0; u0 < LB_GROUP; u0 += 8) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = w0 + u0 + u < w1 ? partial[(int64_t)(w0 + u0 + u) * R + e] : 0.0;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    st_agent(fin.gsum + (int64_t)g * R + e, s);
-  }
-  if (!tds_arrive(fin.sync + kSyncWordsPerSite - 1, (uint32_t)ng, flag)) return;
-  for (int e = tid; e < R; e += 256) {
-    double s = 0.0;
-    for (int q = 0; q < ng; ++q) s += fin.gsum[(int64_t)q * R + e];
-    bs_lds[e] = s;
-    fin.bsum[e] = s;  // (kept for inspection)
-  }
-  __syncthreads();
-  for (int e = tid; e < 16 * 25; e += 256)
-    l1_finalize_one(e, bs_lds, fin.gram, fin.n, fin.w1, fin.b1, fin.gamma1, fin.stats1, fin.dw1, fin.db1,
-                    fin.dgamma1, fin.dbeta1, fin.scale);
-}
-
-template <bool LV, bool PAIRS>
-__global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const uint4* __restrict__ dp1,
+// the pair (1.0, 1.0).  (A conflict-free bf16-pair x tile, two MFMAs per product, timed slower and
+// is in git history.)  fp32 images (!LV): bf16x3, the x operand split hi + lo.
+template <bool LV>
+__global__ __launch_bounds__(256, L1B_WAVES) void l1_bwd_mfma_kernel(const void* __restrict__ xv, const uint4* __restrict__ dp1,
                                                           const uint32_t* __restrict__ dp1_dec,
                                                           const uint4* __restrict__ p1, const uint8_t* __restrict__ idx1,
-                                                          double* __restrict__ partial, int B, int H, int W, LBFin fin) {
+                                                          double* __restrict__ partial, int B, int H, int W) {
   __shared__ __attribute__((aligned(16))) char lds[LB_NP * 64 + LB_NP * 16 + LM_X_BYTES];
   const uint32_t* dps = reinterpret_cast<const uint32_t*>(lds);  // dp1h tile [row 8][group 8][ch 16][px 4] fp16
   unsigned short* phs = nullptr;
@@ -613,28 +522,15 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   // lane's tap relative to the K-step base 2*rp*XS + 16*s; slot j adds (row dr2, column 2wi + dc).
   // n = 25 reads the ones block (bf16 1.0: the sum-dz column), n = 26..31 tap 24 (discarded).
   int boff[2];
-  bool bdata[2];
 #pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     const int n = 16 * blk + li, t = n < 25 ? n : 24;
-    bdata[blk] = n < 25;
     boff[blk] = n == 25 ? LM_ONES : (t / 5) * LM_XS + t % 5 + 2 + 4 * g;
   }
-  // LV: this lane's dword offset in the pair tiles (tap (4,4) for the constant columns: the read is
-  // a broadcast of that lane's address, the value is then replaced by the constant)
-  int vlof[2];
-  uint32_t vcst[2];
-#pragma unroll
-  for (int blk = 0; blk < 2; ++blk) {
-    const int n = 16 * blk + li, t = n < 25 ? n : 24;
-    const int ky = t / 5, kx = t % 5;
-    vlof[blk] = (kx & 1) ? LV_OB + ky * LV_RS + (kx + 1 + 4 * g) / 2 : ky * LV_RS + (kx + 2 + 4 * g) / 2;
-    vcst[blk] = n == 25 ? 0x3F803F80u : 0u;  // bf16 1.0 pair: the sum-dz column
-  }
-  constexpr bool H16 = LV && !PAIRS && TDS_L1B_H16;
-  if (!(LV && PAIRS))  // the ones block (never overwritten: the x tile uses columns 0..71)
-    for (int e = tid; e < LB_XR * (LM_XS - 72); e += 256)  // bf16 1.0 | lo 0, or fp16 1.0 << 16
-      xs[(e / (LM_XS - 72)) * LM_XS + 72 + e % (LM_XS - 72)] = H16 ? 0x3C003C00u : 0x3F800000u;
+  constexpr bool H16 = LV;  // level input: fp16 pair words, one MFMA per product
+  // the ones block (never overwritten: the x tile uses columns 0..71)
+  for (int e = tid; e < LB_XR * (LM_XS - 72); e += 256)  // bf16 1.0 | lo 0, or fp16 1.0 << 16
+    xs[(e / (LM_XS - 72)) * LM_XS + 72 + e % (LM_XS - 72)] = H16 ? 0x3C003C00u : 0x3F800000u;
   const float* __restrict__ x = static_cast<const float*>(xv);
   const uint8_t* __restrict__ xl = static_cast<const uint8_t*>(xv);
   uint4 pre[LB_PER];
@@ -643,12 +539,11 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   // 256 threads), and lanes out of range read a zero vector.  (Loads under per-lane branches had
   // to land before the branches merged: the compiler waited for each one right after issuing it,
   // which serialised the whole prefetch.)
-#ifndef TDS_L1B_REV
-#define TDS_L1B_REV 1  // (layer-1 backward 129.8 -> 128.0 us r5_s44, 132.8 -> 129.8 r5_s50)
-#endif
   auto load_tile = [&](int t) {
-    // TDS_L1B_REV: walk the tiles last-to-first, the reverse of the conv2 backward's dp1 writes
-    if constexpr (TDS_L1B_REV != 0) t = total - 1 - t;
+    // tiles last-to-first, the reverse of the conv2 backward's dp1 writes: the first tiles read are
+    // the most recent writes, still in the Infinity Cache (129.8 -> 128.0 us r5_s44, 132.8 -> 129.8
+    // r5_s50)
+    t = total - 1 - t;
     const int b = t / per_img, rem = t - b * per_img;
     const int pr0 = (rem / tiles_c) * LB_PR, pc0 = (rem % tiles_c) * LB_PC;
 #pragma unroll
@@ -657,13 +552,13 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
       if (256 * u < LB_V_DP) {  // dp1h: 64 vectors per tile row (8 column groups x 8)
         const int gpr = pr0 + (e >> 6), cg = (pc0 >> 2) + ((e >> 3) & 7);
         const int64_t rec = ((int64_t)b * P + gpr) * PG + cg;
-        const uint4* src = (gpr < P) & (cg < PG) ? dp1 + rec * 8 + (e & 7) : &g_l1b_zero;
+        const uint4* src = ((gpr < P) & (cg < PG)) ? dp1 + rec * 8 + (e & 7) : &g_l1b_zero;
         pre[u] = *src;
       } else if (256 * u < LB_V_DP + LB_V_ID) {
         const int pp = e - LB_V_DP;
         const int gpr = pr0 + pp / LB_PC, gpc = pc0 + pp % LB_PC;
         const int64_t rec = ((int64_t)b * P + gpr) * PW + gpc;
-        const uint4* src = (gpr < P) & (gpc < PW) ? reinterpret_cast<const uint4*>(idx1) + rec : &g_l1b_zero;
+        const uint4* src = ((gpr < P) & (gpc < PW)) ? reinterpret_cast<const uint4*>(idx1) + rec : &g_l1b_zero;
         pre[u] = *src;
       } else {
         const int ex = e - LB_V_DP - LB_V_ID;
@@ -704,29 +599,6 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
           const uint32_t h0 = h(q & 0xFFu), h1 = h((q >> 8) & 0xFFu), h2 = h((q >> 16) & 0xFFu), h3 = h(q >> 24);
           const uint32_t h4 = h(pre[u].y & 0xFFu);
           lb_store4(xs + rr * LM_XS + 4 * cv, make_uint4(h0 | h1 << 16, h1 | h2 << 16, h2 | h3 << 16, h3 | h4 << 16));
-          continue;
-        }
-        if constexpr (LV && !PAIRS) {  // word = fp32 bits of the level = bf16 hi | lo 0
-          const uint32_t q = pre[u].x;
-          uint4 v;
-          v.x = __float_as_uint((float)(q & 0xFFu));
-          v.y = __float_as_uint((float)((q >> 8) & 0xFFu));
-          v.z = __float_as_uint((float)((q >> 16) & 0xFFu));
-          v.w = __float_as_uint((float)(q >> 24));
-          lb_store4(xs + rr * LM_XS + 4 * cv, v);  // odd row stride: dword stores
-          continue;
-        }
-        if constexpr (LV) {  // bf16 of a level = high half of its fp32 bits (exact)
-          const uint32_t q = pre[u].x;
-          const uint32_t f0 = __float_as_uint((float)(q & 0xFFu)), f1 = __float_as_uint((float)((q >> 8) & 0xFFu));
-          const uint32_t f2 = __float_as_uint((float)((q >> 16) & 0xFFu)), f3 = __float_as_uint((float)(q >> 24));
-          uint32_t* e = xs + rr * LV_RS + 2 * cv;           // cols 4cv .. 4cv+3 = E dwords 2cv, 2cv+1
-          uint32_t* o = xs + LV_OB + rr * LV_RS + 2 * cv;   // O dword 2cv = cols (4cv+1, 4cv+2)
-          e[0] = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
-          e[1] = __builtin_amdgcn_perm(f3, f2, 0x07060302u);
-          o[0] = __builtin_amdgcn_perm(f2, f1, 0x07060302u);
-          reinterpret_cast<unsigned short*>(o + 1)[0] = (unsigned short)(f3 >> 16);       // col 4cv+3
-          if (cv > 0) reinterpret_cast<unsigned short*>(o - 1)[1] = (unsigned short)(f0 >> 16);  // col 4cv
           continue;
         }
         const float4 f = __builtin_bit_cast(float4, pre[u]);
@@ -798,21 +670,6 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
             lp[2 * wi + 1] = (uint32_t)(l64 >> 32);
           }
         }
-        if constexpr (LV && PAIRS) {
-          const int vbase = 2 * rp * LV_RS + 8 * sg;
-#pragma unroll
-          for (int blk = 0; blk < 2; ++blk) {
-            s16x8 bh;
-            uint32_t* hp = reinterpret_cast<uint32_t*>(&bh);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {  // packed slots (2j, 2j+1) = window wi = j >> 1, row dr2 = j & 1
-              const uint32_t v = xs[vlof[blk] + vbase + (j & 1) * LV_RS + (j >> 1)];
-              hp[j] = bdata[blk] ? v : vcst[blk];
-            }
-            acc[blk] = mfma_bf16x2a(ah, al, bh, acc[blk]);
-          }
-          continue;
-        }
         const int base = 2 * rp * LM_XS + 16 * sg;
 #pragma unroll
         for (int blk = 0; blk < 2; ++blk) {
@@ -838,12 +695,7 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
             hp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x07060302u);
             if constexpr (!LV) lp[j] = __builtin_amdgcn_perm(u[2 * j + 1], u[2 * j], 0x05040100u);
           }
-          if constexpr (H16)  // fp16 x fp16, exact products
-            acc[blk] = mfma_f16(ah, bh, acc[blk]);
-          else if constexpr (LV)  // levels are exact in bf16: lo = 0
-            acc[blk] = mfma_bf16x2a(ah, al, bh, acc[blk]);
-          else
-            acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
+          acc[blk] = mfma_bf16x3(ah, al, bh, bl, acc[blk]);
         }
       }
     }
@@ -873,11 +725,8 @@ __global__ __launch_bounds__(256, TDS_L1B_WAVES) void l1_bwd_mfma_kernel(const v
   double* out = partial + (int64_t)blockIdx.x * 16 * LB_NACC;
   for (int e = tid; e < 16 * LB_NACC; e += 256)
     st_agent(out + e, (red[e] + red[16 * LB_NACC + e]) + (red[2 * 16 * LB_NACC + e] + red[3 * 16 * LB_NACC + e]));
-  if (fin.sync != nullptr)
-    l1_bwd_fin(fin, partial, reinterpret_cast<int*>(lds + 4 * 16 * LB_NACC * 8 + 16 * LB_NACC * 8),
-               reinterpret_cast<double*>(lds + 4 * 16 * LB_NACC * 8));
 }
-static_assert(5 * 16 * LB_NACC * 8 + 16 <= LB_NP * 64 + LB_NP * 16 + LM_X_BYTES, "l1_bwd LDS reduction scratch");
+static_assert(4 * 16 * LB_NACC * 8 <= LB_NP * 64 + LB_NP * 16 + LM_X_BYTES, "l1_bwd LDS reduction scratch");
 
 // Gram of the conv1 patches from the x autocorrelation (one workgroup):
 //   G[k][j] = Full(d) - sum_{excluded rows of k} R(d,row) - sum_{excluded cols} C(d,col)
@@ -1001,9 +850,6 @@ __device__ void l1_build_gram(const double* __restrict__ ac_sum, const double* _
       else cs[e - 16 * 81] = v;
     }
   __syncthreads();
-#if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 4  // (A/B timing: the loads phase only)
-  return;
-#endif
   for (int e = tid; e < 625 + 25; e += blockDim.x) {
     const bool isS = e >= 625;
     const int k = isS ? e - 625 : e / 25, j = isS ? e - 625 : e % 25;
@@ -1096,9 +942,6 @@ __device__ __forceinline__ void l1_gram_body(const double* __restrict__ ac_sum,
   __shared__ double strips_sum[8 * 82];
   const float* w1s = pre.w1s;
   l1_build_gram(ac_sum, strips, x, B, H, W, G, S, full, strips_sum, pre.cx, xs, nch, sacc, cpg);
-#if defined(TDS_L1G_DIAG) && (TDS_L1G_DIAG == 3 || TDS_L1G_DIAG == 4)  // (A/B timing: the Gram build only)
-  return;
-#endif
   const int tid = threadIdx.x;
   for (int e = tid; e < 650; e += blockDim.x) gram[e] = e < 625 ? G[e / 25][e % 25] : S[e - 625];
   for (int e = tid; e < 16 * 25; e += blockDim.x) {
@@ -1249,9 +1092,6 @@ __global__ __launch_bounds__(256) void l1_reduce_gram_kernel(const double* __res
     }
   }
   if (!tds_arrive(sync, (uint32_t)npart, &last)) return;
-#if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 1  // (A/B timing builds only: the reducer without its Gram body)
-  return;
-#endif
   l1_gram_body<T>(ac_sum, strips, x, B, H, W, pre, gram, sums, eps, momentum, stats, running_mean, running_var,
                   num_batches, aff, xs, nch, p1inv, BORDER ? sacc : nullptr, BORDER ? cpg : nullptr);
 }
@@ -1322,10 +1162,7 @@ __global__ __launch_bounds__(512) void l1_finalize_kernel(const double* __restri
 // The layer-1 backward partials' reduction and the closed-form gradients in ONE launch: workgroup
 // e sums columns 8e .. 8e+7 of the [rows][432] partials in a fixed order (write-through), the last
 // to arrive runs l1_finalize_body.
-#ifndef TDS_L1RF_LANES
-#define TDS_L1RF_LANES 128  // row lanes per column (workgroup = 8 x lanes threads; 32: 11.8 us, 128: 10.3, r5_s47)
-#endif
-constexpr int L1RF_LANES = TDS_L1RF_LANES;
+constexpr int L1RF_LANES = 128;  // row lanes per column (workgroup = 8 x lanes threads; 32: 11.8 us, 128: 10.3, r5_s47)
 static_assert(L1RF_LANES % 8 == 0 && L1RF_LANES >= 8 && L1RF_LANES <= 128, "l1_reduce_finalize lanes");
 __global__ __launch_bounds__(8 * L1RF_LANES) void l1_reduce_finalize_kernel(const double* __restrict__ part, int nchunk,
                                                                  double* __restrict__ bwd_sum, uint32_t* __restrict__ sync,
@@ -1469,52 +1306,22 @@ int tds_l1_bwd_rows(int nwg) { return nwg; }
 
 // workgroups of the chosen layer-1 backward variant that fit one CU (its VGPRs decide: 87-99 for
 // the level-input word layout -> 5, the fp32-image path -> 4)
-int tds_l1_bwd_max_per_cu(bool levels, bool pairs) {
+int tds_l1_bwd_max_per_cu(bool levels) {
   int n = 0;
-  hipError_t e;
-  if (levels && pairs) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<true, true>, 256, 0);
-  else if (levels) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<true, false>, 256, 0);
-  else e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<false, false>, 256, 0);
+  const hipError_t e = levels ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<true>, 256, 0)
+                              : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, l1_bwd_mfma_kernel<false>, 256, 0);
   return e == hipSuccess && n > 0 ? n : 4;
 }
 
-int tds_l1_bwd_fin_doubles(int nwg) { return ((nwg + LB_GROUP - 1) / LB_GROUP) * 16 * LB_NACC + 16 * LB_NACC; }
-
-void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
-                const uint8_t* idx1, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
-                hipStream_t st, const TdsL1Fin* lf) {
+void tds_l1_bwd(const void* x, bool levels, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
+                const uint8_t* idx1, double* partial, int nwg, int B, int H, int W, hipStream_t st) {
   const uint4* d = static_cast<const uint4*>(dp1h);
-  LBFin fin{};
-  if (lf != nullptr) {
-    fin.sync = tds_sync_words(kSyncL1Bwd, st);
-    if (fin.sync == nullptr || (nwg + LB_GROUP - 1) / LB_GROUP >= kSyncWordsPerSite) {
-      tds_launch_fail("l1_bwd: in-launch finalize unavailable (sync words / group count)");
-      return;
-    }
-    const int ng = (nwg + LB_GROUP - 1) / LB_GROUP;
-    fin.gsum = lf->work;
-    fin.bsum = lf->work + (int64_t)ng * 16 * LB_NACC;
-    fin.gram = lf->gram;
-    fin.n = (int64_t)B * H * W;
-    fin.w1 = w1;
-    fin.b1 = b1;
-    fin.gamma1 = lf->gamma1;
-    fin.stats1 = lf->stats1;
-    fin.dw1 = lf->dw1;
-    fin.db1 = lf->db1;
-    fin.dgamma1 = lf->dgamma1;
-    fin.dbeta1 = lf->dbeta1;
-    fin.scale = lf->scale;
-  }
-  if (levels && pairs)
-    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, true>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
-                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W, fin);
-  else if (levels)
-    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true, false>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
-                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W, fin);
+  if (levels)
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<true>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   else
-    hipLaunchKernelGGL((l1_bwd_mfma_kernel<false, false>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
-                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W, fin);
+    hipLaunchKernelGGL((l1_bwd_mfma_kernel<false>), dim3(nwg), dim3(256), 0, st, x, d, dp1_dec,
+                       reinterpret_cast<const uint4*>(p1), idx1, partial, B, H, W);
   TDS_LAUNCH_CHECK();
 }
 
@@ -1574,12 +1381,8 @@ bool tds_l1_reduce_gram(const double* ac_part, int nchunk, double* ac_sum, doubl
     if (sacc == nullptr) return false;
   }
   if (levels && border)
-#if defined(TDS_L1G_DIAG) && TDS_L1G_DIAG == 2  // (A/B timing builds only: no border workgroups)
-    hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + pack.n), dim3(256),
-#else
     hipLaunchKernelGGL((l1_reduce_gram_kernel<uint8_t, true>), dim3(42 + 4 * B * xmom_border_chunks(H, W) + pack.n),
                        dim3(256),
-#endif
                        0, st, ac_part, nchunk,
                        ac_sum, sync, strips, static_cast<const uint8_t*>(x), B, H, W, w1, gram, sums, b1, eps, momentum,
                        gamma, beta, stats, running_mean, running_var, num_batches, aff, (double)L1_LEVEL_SCALE, p1inv, pack,

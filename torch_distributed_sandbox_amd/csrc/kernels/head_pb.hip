@@ -39,16 +39,10 @@
 namespace tds {
 
 constexpr int HP_THREADS = 256;
-#ifndef TDS_HP_BAND
-#define TDS_HP_BAND 4
-#endif
-constexpr int HP_BAND = TDS_HP_BAND;        // block rows per workgroup (forward)
+constexpr int HP_BAND = 4;                  // block rows per workgroup (forward)
 // the backward's band: 2 block rows (r4_s43: 2 / 4 / 8 -> backward 0.448 / 0.457 / 0.505 ms,
 // forward 0.227 / 0.212 / 0.232 -- each direction takes its best)
-#ifndef TDS_HP_BAND_B
-#define TDS_HP_BAND_B 2
-#endif
-constexpr int HP_BAND_B = TDS_HP_BAND_B;
+constexpr int HP_BAND_B = 2;
 constexpr int HP_MAXB = 8;                  // images per pass (larger batches run in passes)
 
 struct HPGrid {
@@ -72,12 +66,6 @@ struct HPThread {
   }
 };
 
-#ifndef TDS_G2M_NT
-#define TDS_G2M_NT 1
-#endif
-#ifndef TDS_HP_WUPD_NT  // the backward's updated-weight stores non-temporal (A/B: 0 = plain stores)
-#define TDS_HP_WUPD_NT 1
-#endif
 template <class T>
 __device__ __forceinline__ void hp_st(T* p, T v, bool nt) {
   if (nt) st_stream(p, v); else *p = v;
@@ -200,73 +188,16 @@ struct HPFin {
   float* loss = nullptr;
   float* inv_count = nullptr;
 };
-// UPD: the fc-gradient exchange's deferred weight update applied on the way through (the activation
-// exchange, parallel/factored.py): W <- W - lr * scale * sum_m dY[m]^T X_m, X_m = row m of the M =
-// W_world * rows gathered rows, decoded from the zero-suppressed encodings (zs_exchange.hip format;
-// wo: per-word value offsets, tds_zs_word_offsets) -- the logits are then formed with the UPDATED
-// weight and the updated weight is stored, so the 720 MB weight is streamed once for both (the
-// separate update sweep linear_dw_zs read and wrote it, and the head forward read it again).  The
-// arithmetic per element is linear_dw_zs's: s = fma chain over m in order, W - lr * (scale * s).
-constexpr int HP_MAXM = 40;  // gathered rows the fused update takes (W_world * rows)
-constexpr int HP_MG = 5;     // rows decoded together (the bench's W_world * rows at world 1)
-struct HPUpd {
-  const float* dy;      // [M][NC]
-  const int* meta;      // rank r's page records at meta + r * mstride
-  int64_t mstride;
-  const int* wo;        // rank r's word offsets at wo + r * wostride
-  int64_t wostride;
-  const uint32_t* vals; // rank r's values at vals + r * cap
-  int64_t cap;
-  int M, rows;
-  float scale, lr;
-  float* Wout;          // the weight, updated in place
-};
-
-// X_m at elements e .. e+3 of rank r's flat rows (e % 4 in {0, 2}: the 4 lie in one word or the
-// last 2 bits of a word and the first 2 of the next).  Branch-free: every lane issues the same
-// loads (the second word re-reads the first when not needed; value indices clamped to the slot),
-// so a group of rows' loads can all be in flight at once -- a load under a per-lane branch makes
-// the compiler wait for everything older at the merge.
-__device__ __forceinline__ float4 hp_zs_x4(const HPUpd& u, int r, int64_t e) {
-  const int* mr = u.meta + (int64_t)r * u.mstride;
-  const int64_t gw = e >> 5;
-  const int bit = (int)(e & 31);
-  const bool two = bit > 28;
-  const int64_t gw1 = two ? gw + 1 : gw;
-  const uint32_t w0 = (uint32_t)mr[(gw >> 6) * 65 + 1 + (gw & 63)];
-  const uint32_t w1 = (uint32_t)mr[(gw1 >> 6) * 65 + 1 + (gw1 & 63)];
-  const int64_t base = (int64_t)u.wo[(int64_t)r * u.wostride + gw];
-  const uint32_t m4 = ((w0 >> bit) | (two ? w1 << (32 - bit) : 0u)) & 0xFu;
-  const int64_t off = base + __builtin_popcount(w0 & ((1u << bit) - 1u));
-  const uint32_t* vr = u.vals + (int64_t)r * u.cap;
-  float x[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t idx = min(off + __builtin_popcount(m4 & ((1u << k) - 1u)), u.cap - 1);
-    const float v = __uint_as_float(vr[idx]);
-    x[k] = ((m4 >> k) & 1u) ? v : 0.f;
-  }
-  return make_float4(x[0], x[1], x[2], x[3]);
-}
-
-template <int NB, bool UPD = false>
+template <int NB>
 __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __restrict__ ya,
                                                                  const float* __restrict__ W,
                                                                  const float* __restrict__ aff2,
                                                                  double* __restrict__ partial,
                                                                  float* __restrict__ xout, PBGeom g, int Btot, int b0,
-                                                                 int NC, HPFin fin, HPUpd upd) {
+                                                                 int NC, HPFin fin) {
   __shared__ float red[HP_THREADS / 64][HP_MAXB * 10];
   __shared__ int last_flag;
   __shared__ double wpart[256];
-  __shared__ float s_dy[UPD ? (HP_MAXM + HP_MG) * 10 : 1];
-  if constexpr (UPD) {
-    for (int e = threadIdx.x; e < (HP_MAXM + HP_MG) * 10; e += HP_THREADS) {
-      const int m = e / 10, j = e - m * 10;
-      s_dy[e] = (m < upd.M && j < NC) ? upd.dy[m * NC + j] : 0.f;
-    }
-    __syncthreads();
-  }
   const HPGrid hg = hp_grid(g);
   const int wg = blockIdx.x;
   const int c = wg / hg.per_channel(), band = wg - c * hg.per_channel();
@@ -313,59 +244,6 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
 #pragma unroll
       for (int b = 0; b < NB; ++b)
         hp_store4(xout + (int64_t)(b0 + b) * K, g, rwx, 0, make_float4(x[b][0], x[b][1], x[b][2], x[b][3]), false);
-    }
-    if constexpr (UPD) {
-      // the weight's update at this lane's 4 columns, then the logits with the updated weight
-      const HPRow rw(g, th, c, R);
-      if (rw.nvalid > 0) {
-        float sj[10][4];
-#pragma unroll
-        for (int j = 0; j < 10; ++j)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) sj[j][k] = 0.f;
-        const int64_t pos = (int64_t)c * QQ + (int64_t)py * Q + px0;
-        // rows in groups of HP_MG, each group's loads in flight together (one row at a time made
-        // 2 dependent round trips per row and chunk: the fused forward ran 0.80 ms, r5_s8); rows past
-        // M read row M-1 and add dy = 0 (s_dy is zero-padded), keeping the fma order m = 0, 1, ...
-#pragma unroll 1
-        for (int m0 = 0; m0 < upd.M; m0 += HP_MG) {
-          float4 xm[HP_MG];
-#pragma unroll
-          for (int t = 0; t < HP_MG; ++t) {
-            const int m = min(m0 + t, upd.M - 1);
-            const int r = m / upd.rows, bl = m - r * upd.rows;
-            xm[t] = hp_zs_x4(upd, r, (int64_t)bl * K + pos);
-          }
-#pragma unroll
-          for (int t = 0; t < HP_MG; ++t) {
-            if (m0 + t >= upd.M) break;  // (uniform; no 0 * x terms: x may be inf)
-#pragma unroll
-            for (int j = 0; j < 10; ++j) {
-              const float gv = s_dy[(m0 + t) * 10 + j];
-              sj[j][0] = fmaf(gv, xm[t].x, sj[j][0]);
-              sj[j][1] = fmaf(gv, xm[t].y, sj[j][1]);
-              sj[j][2] = fmaf(gv, xm[t].z, sj[j][2]);
-              sj[j][3] = fmaf(gv, xm[t].w, sj[j][3]);
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 10; ++j) {
-          if (j < NC) {
-            float4 w4 = cur.w[j];
-            w4 = make_float4(w4.x - upd.lr * (upd.scale * sj[j][0]), w4.y - upd.lr * (upd.scale * sj[j][1]),
-                             w4.z - upd.lr * (upd.scale * sj[j][2]), w4.w - upd.lr * (upd.scale * sj[j][3]));
-            hp_store4(upd.Wout, g, rw, j, w4);
-            // lanes' columns past the image stay 0 for the logits (fix() zeroed them)
-            const float e4[4] = {w4.x, w4.y, w4.z, w4.w};
-            const float o4[4] = {cur.w[j].x, cur.w[j].y, cur.w[j].z, cur.w[j].w};
-            float n4[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) n4[k] = k < rw.nvalid ? e4[k] : o4[k];
-            cur.w[j] = make_float4(n4[0], n4[1], n4[2], n4[3]);
-          }
-        }
-      }
     }
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
@@ -481,10 +359,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   const HPGrid hg = hp_grid_b(g);
   // workgroups in the reverse of the forward's order: the backward starts on the channels the
   // forward streamed last, whose ya / weight lines are still in the 256 MB Infinity Cache
-#ifndef TDS_HPB_REV
-#define TDS_HPB_REV 1
-#endif
-  const int wg = TDS_HPB_REV ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int wg = (int)gridDim.x - 1 - (int)blockIdx.x;
   const int c = c0 + wg / hg.per_channel(), band = wg - (c - c0) * hg.per_channel();
   float dls[NB * 10];  // dlogits of this pass: wave-uniform, scalar loads
 #pragma unroll
@@ -528,15 +403,13 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
           gs = fmaf(dls[b * 10 + j], wk, gs);
         }
         gm[k] = (ok && z > 0.f) ? gs : 0.f;
-#ifndef TDS_HP_NO_GMX  // (A/B timing variant only)
         gmx = max(gmx, __float_as_uint(gm[k]) & 0x7fffffffu);
-#endif
         x[b][k] = ok ? hp_relu(z) : 0.f;
         sdz += gm[k];
         sdy = fmaf(gm[k], ok ? yy[k] : 0.f, sdy);
       }
       // planar, like a weight plane
-      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]), TDS_G2M_NT != 0);
+      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]), true);
     }
     if constexpr (WITH_DW) {
       const HPRow& rw = rwg;
@@ -563,8 +436,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
             if constexpr (KEEP) hp_store4(dW, g, rw, j, d);
             if constexpr (UPD) {  // torch SGD: p -= lr * g
               const float4 w = cur.w[j];
-              hp_store4(Wupd, g, rw, j, make_float4(w.x - lr * d.x, w.y - lr * d.y, w.z - lr * d.z, w.w - lr * d.w),
-                        TDS_HP_WUPD_NT != 0);
+              hp_store4(Wupd, g, rw, j, make_float4(w.x - lr * d.x, w.y - lr * d.y, w.z - lr * d.z, w.w - lr * d.w));
             }
           }
         }
@@ -688,7 +560,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 #define TDS_HPF(NBV)                                                                                                   \
   case NBV:                                                                                                            \
     hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
-                       B, b0, NC, fin, HPUpd{});                                                                       \
+                       B, b0, NC, fin);                                                                                \
     TDS_LAUNCH_CHECK();                                                                                                \
     break;
     switch (nb) {
@@ -700,35 +572,6 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
   if (fin.sync != nullptr) return labels != nullptr ? 1 : 0;
   hipLaunchKernelGGL(head_logits_kernel, dim3(BN), dim3(256), 0, st, partial, nwg, sums, bias, logits, BN, NC);
   TDS_LAUNCH_CHECK();
-  return 0;
-}
-
-// The head forward with the activation exchange's deferred weight update fused (HPUpd): one pass
-// (B <= 8), M = W_world * rows <= HP_MAXM gathered rows, logits finished in the launch.  Returns -1 on
-// unsupported shapes (the caller then runs the separate update).
-int tds_head_fwd_pb_upd(const float* ya, float* Wfc, const float* bias, const float* aff2, double* partial,
-                        double* sums, float* logits, int B, int Q, int NC, const float* dy, int M, int rows,
-                        const int* meta, int64_t mstride, const int* wo, int64_t wostride, const float* vals,
-                        int64_t cap, float scale, float lr, hipStream_t st) {
-  if (B < 1 || B > HP_MAXB || NC < 1 || NC > 10 || Q < 8 || M < 1 || M > HP_MAXM || rows < 1 || M % rows) return -1;
-  const PBGeom g = pb_geom(Q);
-  const int nwg = 32 * hp_grid(g).per_channel();
-  const int BN = B * NC, nbc = hp_grid(g).per_channel();
-  if (!(BN <= 256 && nbc <= WRS_MAXL * (256 / BN) && 32 <= WRS_MAXL * (256 / BN))) return -1;
-  HPFin fin{tds_sync_words(kSyncHeadFwd, st), partial + (int64_t)nwg * B * NC, sums, bias, logits};
-  if (fin.sync == nullptr) return -1;
-  HPUpd upd{dy, meta, mstride, wo, wostride, reinterpret_cast<const uint32_t*>(vals), cap, M, rows, scale, lr, Wfc};
-#define TDS_HPU(NBV)                                                                                                \
-  case NBV:                                                                                                         \
-    hipLaunchKernelGGL((head_fwd_pb_kernel<NBV, true>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, \
-                       nullptr, g, B, 0, NC, fin, upd);                                                             \
-    TDS_LAUNCH_CHECK();                                                                                             \
-    break;
-  switch (B) {
-    TDS_HPU(1) TDS_HPU(2) TDS_HPU(3) TDS_HPU(4) TDS_HPU(5) TDS_HPU(6) TDS_HPU(7) TDS_HPU(8)
-    default: return -1;
-  }
-#undef TDS_HPU
   return 0;
 }
 

@@ -64,7 +64,6 @@ void tds_launch_probe(int* out, int lds_bytes, int threads, hipStream_t st);  //
 
 // ---- conv2_pack.hip / conv2_fwd2.hip / conv2_bwd.hip (NHWC, fp16x2 split MFMA)
 // mag (optional): 33 words of magnitude bounds [max|y2| per channel (32) | max|g2m|], zeroed here
-int tds_conv2_split();  // 1: fp16x2 (one operand hi + lo), 0: one fp16 MFMA per product (TF32 class)
 // write_p1: store mag[kMagScales + 1] = 1 / p1_scale (1 without p1_scale); false: the layer-1 Gram
 // launch stores it (the packing then runs ahead of layer 1 on a side stream)
 void tds_conv2_pack_weights(const float* w2, short* wp, short* wd, uint32_t* mag, const float* p1_scale,
@@ -162,19 +161,9 @@ void tds_bn_reduce_finalize(const double* partial, int C, int nchunk, int64_t n,
 int tds_l1_bwd_rows(int nwg);  // partial rows [rows][16][27] tds_l1_bwd writes
 // dp1h: the conv2 backward's (conv2_common.h), dp1_dec: its decode factor (float bits, device)
 // the layer-1 backward's finalize inside its launch (replaces tds_reduce_partials + tds_l1_finalize)
-struct TdsL1Fin {
-  double* work;  // tds_l1_bwd_fin_doubles(nwg)
-  const double* gram;
-  const float* gamma1;
-  const float* stats1;
-  float *dw1, *db1, *dgamma1, *dbeta1;
-  float scale;
-};
-int tds_l1_bwd_fin_doubles(int nwg);
-int tds_l1_bwd_max_per_cu(bool levels, bool pairs);  // occupancy of the variant (hipOccupancy...)
-void tds_l1_bwd(const void* x, bool levels, bool pairs, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
-                const uint8_t* idx1, const float* w1, const float* b1, double* partial, int nwg, int B, int H, int W,
-                hipStream_t st, const TdsL1Fin* lf = nullptr);
+int tds_l1_bwd_max_per_cu(bool levels);  // occupancy of the variant (hipOccupancy...)
+void tds_l1_bwd(const void* x, bool levels, const void* dp1h, const uint32_t* dp1_dec, const void* p1,
+                const uint8_t* idx1, double* partial, int nwg, int B, int H, int W, hipStream_t st);
 // the partial reductions fused with the single-workgroup finalizers (false: no sync words)
 bool tds_l1_reduce_finalize(const double* part, int rows, double* bwd_sum, const double* gram, int64_t n,
                             const float* w1, const float* b1, const float* gamma1, const float* stats1, float* dw1,
@@ -212,11 +201,6 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st,
                     bool fused_fin = true, const int64_t* labels = nullptr, float* dlogits = nullptr,
                     float* loss = nullptr, float* inv_count = nullptr);
-// the head forward with the activation exchange's deferred weight update fused (head_pb.hip HPUpd)
-int tds_head_fwd_pb_upd(const float* ya, float* Wfc, const float* bias, const float* aff2, double* partial,
-                        double* sums, float* logits, int B, int Q, int NC, const float* dy, int M, int rows,
-                        const int* meta, int64_t mstride, const int* wo, int64_t wostride, const float* vals,
-                        int64_t cap, float scale, float lr, hipStream_t st);
 int tds_head_bwd_pb_npass(int B);
 // channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
 // soon as its launch lands; the BN2 partials of the other channels are left untouched)
@@ -242,13 +226,7 @@ int64_t tds_zs_npages(int64_t n);
 // meta [npages * 65] (offsets + mask words), counts [npages] scratch, vals [cap] (dropped past
 // cap), nnz: int64 device scalar
 void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t cap, int64_t* nnz, hipStream_t st);
-// the same encoding of X = relu(a * ya + b) read from the head's pooled-blocked ya and BN2 affine
-// (B images at pooled size Q): the dense X is never written
-void tds_zs_encode_ya(const float* ya, const float* aff2, int B, int Q, int* meta, float* vals, int64_t cap,
-                      int64_t* nnz, hipStream_t st);
-// per-word value offsets of W zs encodings (meta of rank r at meta + r * mstride, npages pages each):
-// wo [W][npages * 64]
-void tds_zs_word_offsets(const int* meta, int64_t mstride, int64_t npages, int W, int* wo, hipStream_t st);
+
 void tds_zs_decode(const int* meta, const float* vals, int64_t cap, float* out, int64_t n, hipStream_t st);
 // linear_dw with X given as W source ranks' zero-suppressed encodings (decoded in registers)
 int tds_linear_dw_zs(const float* dy, const int* meta, int64_t mstride, const float* vals, int64_t cap, int rows,

@@ -28,10 +28,7 @@
 namespace tds {
 
 // (isolated op, r5_s35: 32 rows 48.1 - 48.6 us, 40: 47.0 - 48.6, 48: 45.8 - 46.2, 64: 45.3 - 46.7)
-#ifndef TDS_UM_RB
-#define TDS_UM_RB 48
-#endif
-constexpr int UM_RB = TDS_UM_RB;  // output rows per wave
+constexpr int UM_RB = 48;         // output rows per wave
 constexpr int UM_QPW = 62;        // quads per wave at most (lanes 1..62 own them)
 // a lane's sums: UM_RB rows x 4 products <= 255^2 each; the wave's: 62 lanes
 static_assert((unsigned long long)UM_RB * 4ull * 62ull * 65025ull < (1ull << 32), "u32 wave sums would wrap");

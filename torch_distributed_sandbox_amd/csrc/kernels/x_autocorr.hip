@@ -21,14 +21,11 @@ namespace tds {
 // (partial[wg][42], slot 41 = plain sum).  Requires W % 4 == 0.
 // rows per thread: sweep on MI355X (isolated layer-1 forward, which includes this kernel):
 // 4 -> 0.488 ms, 8 -> 0.435, 16 -> 0.407 (tools/gpu_sessions/r2_acrb.sh)
-#ifndef TDS_AC_RB
-#define TDS_AC_RB 16
-#endif
-constexpr int AC_RB = TDS_AC_RB;
+constexpr int AC_RB = 16;
 // the uint8 path's moments are exact u32 sums: a thread adds 4 * AC_RB products of <= 255^2 and
 // a wave 64 threads' sums (x_autocorr_u8_kernel), which must stay below 2^32
 static_assert((unsigned long long)AC_RB * 4ull * 64ull * 65025ull < (1ull << 32),
-              "TDS_AC_RB too large: the u8 moments' u32 wave sums would overflow");
+              "AC_RB too large: the u8 moments' u32 wave sums would overflow");
 
 static int x_autocorr_num_wg(int B, int H, int W) {
   if (W % 4 != 0 || B < 1 || H < 1) return 0;
@@ -252,27 +249,16 @@ void tds_x_border(const float* x, double* strips, int B, int H, int W, hipStream
   TDS_LAUNCH_CHECK();
 }
 
-// one launch (measured: layer-1 forward 0.407 -> 0.402 ms, bench 3.73-3.75 vs 3.75-3.76 ms,
-// tools/gpu_sessions/r2_acmerge.sh); 0 = two launches
-#ifndef TDS_AC_MERGE_BORDER
-#define TDS_AC_MERGE_BORDER 1
-#endif
-
-// x moments for BN1: autocorrelation partials [nwg][42] and per-image border strips [B][8][82]
-// (TDS_AC_MERGE_BORDER: one launch, the border workgroups behind the autocorrelation's)
+// x moments for BN1: autocorrelation partials [nwg][42] and per-image border strips [B][8][82] in
+// one launch, the border workgroups behind the autocorrelation's (measured: layer-1 forward 0.407 ->
+// 0.402 ms against two launches, tools/gpu_sessions/r2_acmerge.sh)
 void tds_x_moments(const float* x, double* ac_partial, int nwg, double* strips, int B, int H, int W, hipStream_t st) {
   if (nwg < 1 || nwg != x_autocorr_num_wg(B, H, W)) {  // the partial buffer is sized by tds_x_autocorr_num_wg
     tds_launch_fail("x_autocorr: workgroup count does not match the shape (needs W % 4 == 0)");
     return;
   }
-  if (TDS_AC_MERGE_BORDER) {
-    hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg + 656 * B), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
-    TDS_LAUNCH_CHECK();
-    return;
-  }
-  hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
+  hipLaunchKernelGGL(x_autocorr_kernel, dim3(nwg + 656 * B), dim3(256), 0, st, x, ac_partial, B, H, W, strips, nwg);
   TDS_LAUNCH_CHECK();
-  tds_x_border(x, strips, B, H, W, st);
 }
 
 // the same moments of uint8 levels (x = levels / 255 is scaled in l1_gram), one launch

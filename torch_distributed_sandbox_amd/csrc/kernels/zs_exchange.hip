@@ -70,174 +70,6 @@ __device__ __forceinline__ int zs_block_scan(int v, int* sh, int& total) {
   return base + incl - v;
 }
 
-// X straight from the head's inputs (the zs_encode_ya variant below): X[b][c][py][px] = relu(a[c] *
-// ya[b][c][py][px] + b[c]) with ya in the pooled-blocked layout (pooled_layout.h) -- the head
-// forward no longer writes the dense X (360 MB at the bench shape) for the encoder to read back.
-// The value is formed exactly as the head kernels form it (head_pb.hip: fmaf, then ReLU keeping a
-// NaN), so the encodings are bitwise those of the written X.
-struct ZSYa {
-  const float* ya;
-  const float* aff;  // [64]: a | b of BN2
-  PBGeom g;
-  int64_t K;         // 32 * Q * Q
-};
-// this thread's 8 elements e0 .. e0+7 of the flat X (zeros past n; n < 2^31 and Q >= 8: the
-// position is split once in 32 bits).  Fast path (the run lies in one pooled row): the run is
-// columns px .. px+7 of row py, i.e. the row's 8-float pieces of blocks px/8 and px/8 + 1 (32-B
-// aligned, consecutive blocks 128 B apart) -- four 16-B loads, the 8 values picked by a funnel
-// shift of px % 8 (per-element 4-B gathers plus per-element affine loads ran the encode at
-// 0.44 ms, r5_s7).  Runs that cross a row end or pass n take the element-wise path.
-__device__ __forceinline__ float zs_x_of(float a, float b, float y) {
-  const float z = fmaf(a, y, b);
-  return z > 0.f ? z : (isnan(z) ? z : 0.f);
-}
-__device__ __forceinline__ void zs_load8(const ZSYa& s, int64_t e0, int64_t n, uint32_t (&v)[8]) {
-  const uint32_t Q = (uint32_t)s.g.Q, QQ = Q * Q, K = (uint32_t)s.K;
-  const uint32_t e = (uint32_t)min(e0, n - 1);
-  uint32_t b = e / K, r = e - b * K;
-  uint32_t c = r / QQ, q = r - c * QQ;
-  uint32_t py = q / Q, px = q - py * Q;
-  if (e0 + 8 <= n && px + 8 <= Q) {
-    // blocks px/8 and px/8 + 1 of this row (px + 8 <= Q: the second block is inside the row)
-    const float* p = s.ya + s.g.index((int)b, (int)c, (int)py, (int)(px & ~7u));
-    const float4 q0 = *reinterpret_cast<const float4*>(p), q1 = *reinterpret_cast<const float4*>(p + 4);
-    const float4 q2 = *reinterpret_cast<const float4*>(p + 32), q3 = *reinterpret_cast<const float4*>(p + 36);
-    const uint32_t w[16] = {__float_as_uint(q0.x), __float_as_uint(q0.y), __float_as_uint(q0.z), __float_as_uint(q0.w),
-                            __float_as_uint(q1.x), __float_as_uint(q1.y), __float_as_uint(q1.z), __float_as_uint(q1.w),
-                            __float_as_uint(q2.x), __float_as_uint(q2.y), __float_as_uint(q2.z), __float_as_uint(q2.w),
-                            __float_as_uint(q3.x), __float_as_uint(q3.y), __float_as_uint(q3.z), __float_as_uint(q3.w)};
-    const uint32_t off = px & 7u;
-    // the shift as bit masks, not selects between array elements: LLVM folds c ? w[i + 4] : w[i]
-    // into w[i + (c ? 4 : 0)], a dynamic index that keeps the array in scratch memory
-    const uint32_t m4 = 0u - ((off >> 2) & 1u), m2 = 0u - ((off >> 1) & 1u), m1 = 0u - (off & 1u);
-    uint32_t t4[11], t2[9];
-#pragma unroll
-    for (int i = 0; i < 11; ++i) t4[i] = (w[i] & ~m4) | (w[i + 4] & m4);
-#pragma unroll
-    for (int i = 0; i < 9; ++i) t2[i] = (t4[i] & ~m2) | (t4[i + 2] & m2);
-    const float a = s.aff[c], bb = s.aff[32 + c];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = __float_as_uint(zs_x_of(a, bb, __uint_as_float((t2[i] & ~m1) | (t2[i + 1] & m1))));
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const bool ok = e0 + i < n;  // (past n: b may be B -- read element 0 instead)
-    const int cc = ok ? (int)c : 0;
-    const float y = s.ya[ok ? s.g.index((int)b, cc, (int)py, (int)px) : 0];
-    v[i] = ok ? __float_as_uint(zs_x_of(s.aff[cc], s.aff[32 + cc], y)) : 0u;
-    if (++px == Q) {
-      px = 0;
-      if (++py == Q) {
-        py = 0;
-        if (++c == 32) {
-          c = 0;
-          ++b;
-        }
-      }
-    }
-  }
-}
-
-// The tile's X from ya through LDS (ZSYa, Q >= 16): a page of 2048 flat elements covers a few
-// pooled rows; its (row, 8-column block) PIECES are each one 32-B run of ya (2 x 16-B loads,
-// consecutive lanes on consecutive blocks of a row), written into the page's flat order in LDS
-// with the BN2 affine and ReLU applied, then read back as each thread's 8 elements.  Pages are
-// double-buffered: page k+1's pieces are loaded into registers while page k is written and read.
-// A page has at most 256 + (rows it touches) <= 385 pieces for Q >= 16 (2 slots per thread).
-// (Each thread gathering its own 8 elements -- 4-B loads, or 16-B loads of the two blocks they
-// straddle -- read ya at 0.35-0.44 ms against 0.17 ms for the dense X, r5_s7 / r5_s9.)
-// A page's geometry, wave-uniform (computed once per page; 32-bit: n < 2^31).
-struct ZSPageGeo {
-  int E, end;        // flat range [E, end)
-  int gr0, cs0;      // its first row (global row b*32*Q + c*Q + py) and column
-  int bc0, py0;      // that row's plane (b*32 + c) and pooled row
-  int nb0;           // blocks of the first row from column cs0 on
-  bool none;         // the page lies past n
-};
-__device__ __forceinline__ ZSPageGeo zs_page_geo(const ZSYa& s, int64_t E64, int64_t n) {
-  ZSPageGeo g;
-  const int Q = s.g.Q;
-  g.none = E64 >= n;
-  g.E = g.none ? 0 : (int)E64;
-  g.end = (int)min(E64 + (int64_t)ZS_PAGE, n);
-  g.gr0 = g.E / Q;
-  g.cs0 = g.E - g.gr0 * Q;
-  g.bc0 = g.gr0 / Q;
-  g.py0 = g.gr0 - g.bc0 * Q;
-  g.nb0 = s.g.Q8 - (g.cs0 >> 3);
-  return g;
-}
-// floor(a / d) for 0 <= a < 2^20, d >= 1, from a float reciprocal with a one-step correction (a
-// 64-bit integer division per piece made the page staging VALU-bound)
-__device__ __forceinline__ int zs_div(int a, int d, float rd) {
-  int q = (int)((float)a * rd);
-  q -= (q * d > a) ? 1 : 0;
-  q += ((q + 1) * d <= a) ? 1 : 0;
-  return q;
-}
-
-template <int SLOTS>
-struct ZSPageRegs {
-  float4 lo[SLOTS], hi[SLOTS];
-  int f0[SLOTS];     // flat index of the piece's first column
-  int8_t c[SLOTS];   // its channel
-  int8_t ncol[SLOTS];  // columns inside the image (0: no piece)
-};
-
-template <int SLOTS>
-__device__ __forceinline__ void zs_page_load(const ZSYa& s, int64_t E64, int64_t n, ZSPageRegs<SLOTS>& r, int tid) {
-  const ZSPageGeo pg = zs_page_geo(s, E64, n);
-  const int Q = s.g.Q, Q8 = s.g.Q8;
-  const float rQ8 = 1.f / (float)Q8, rQ = 1.f / (float)Q;
-#pragma unroll
-  for (int u = 0; u < SLOTS; ++u) {
-    const int p = tid + 256 * u;
-    int i, blk;
-    if (p < pg.nb0) {
-      i = 0;
-      blk = (pg.cs0 >> 3) + p;
-    } else {
-      const int q = p - pg.nb0, t = zs_div(q, Q8, rQ8);
-      i = 1 + t;
-      blk = q - t * Q8;
-    }
-    const int64_t f0 = (int64_t)(pg.gr0 + i) * Q + blk * 8;
-    const bool ok = !pg.none && f0 < pg.end;
-    const int w = zs_div(pg.py0 + i, Q, rQ);  // rows past the plane's last
-    const int bc = pg.bc0 + w, py = pg.py0 + i - w * Q;
-    const int64_t pb = ok ? (((int64_t)bc * s.g.Q4 + (py >> 2)) * Q8 + blk) * 32 + (py & 3) * 8 : 0;
-    r.lo[u] = *reinterpret_cast<const float4*>(s.ya + pb);  // (no piece: ya[0 .. 7], unused)
-    r.hi[u] = *reinterpret_cast<const float4*>(s.ya + pb + 4);
-    r.f0[u] = ok ? (int)f0 : 0;
-    r.c[u] = (int8_t)(bc & 31);
-    r.ncol[u] = (int8_t)(ok ? min(8, Q - blk * 8) : 0);
-  }
-}
-
-template <int SLOTS>
-__device__ __forceinline__ void zs_page_put(const ZSYa& s, int64_t E64, int64_t n, const ZSPageRegs<SLOTS>& r,
-                                            uint32_t* xs, int tid) {
-  const int E = E64 < n ? (int)E64 : 0, end = (int)min(E64 + (int64_t)ZS_PAGE, n);
-#pragma unroll
-  for (int u = 0; u < SLOTS; ++u) {
-    const int c = r.c[u];
-    const float a = s.aff[c], bb = s.aff[32 + c];
-    const float y[8] = {r.lo[u].x, r.lo[u].y, r.lo[u].z, r.lo[u].w, r.hi[u].x, r.hi[u].y, r.hi[u].z, r.hi[u].w};
-    const int f0 = r.f0[u];
-    if (r.ncol[u] == 8 && f0 >= E && f0 + 8 <= end) {  // the whole run is in the page (most pieces)
-#pragma unroll
-      for (int t = 0; t < 8; ++t) xs[f0 - E + t] = __float_as_uint(zs_x_of(a, bb, y[t]));
-    } else {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) {
-        const int f = f0 + t;
-        if (t < r.ncol[u] && f >= E && f < end) xs[f - E] = __float_as_uint(zs_x_of(a, bb, y[t]));
-      }
-    }
-  }
-}
-
 // Single-pass encode over TILES of ZS_TILE pages (one workgroup each, the tile's X in
 // registers: 8 elements x 8 pages per thread).  Tile order is the order workgroups START (a
 // ticket from a counter; the workgroup drawing the last ticket resets it for the next call), so
@@ -272,7 +104,6 @@ __global__ __launch_bounds__(256) void zs_encode_kernel(SRC x, int64_t n, int64_
   __shared__ int sh[4];
   __shared__ int ptot[ZS_TILE];
   __shared__ long long s_tile, s_prefix;
-  __shared__ uint32_t xs[std::is_same<SRC, ZSYa>::value ? 2 * ZS_PAGE : 1];
   const int tid = threadIdx.x;
   if (tid == 0) {
     const unsigned long long t = atomicAdd(ticket, 1ull);
@@ -283,26 +114,8 @@ __global__ __launch_bounds__(256) void zs_encode_kernel(SRC x, int64_t n, int64_
   const int64_t tile = s_tile, p0 = tile * ZS_TILE;
   uint32_t v[ZS_TILE][8];
   int ex[ZS_TILE];
-  if constexpr (std::is_same<SRC, ZSYa>::value) {
-    // pages through LDS (zs_page_load / zs_page_put), page k+1's loads in flight under page k
-    ZSPageRegs<2> r0, r1;
-    zs_page_load<2>(x, p0 * ZS_PAGE, n, r0, tid);
 #pragma unroll
-    for (int k = 0; k < ZS_TILE; ++k) {
-      const int64_t E = (p0 + k) * ZS_PAGE;
-      if (k + 1 < ZS_TILE) zs_page_load<2>(x, E + ZS_PAGE, n, (k & 1) ? r0 : r1, tid);
-      uint32_t* buf = xs + (k & 1) * ZS_PAGE;
-      zs_page_put<2>(x, E, n, (k & 1) ? r1 : r0, buf, tid);
-      __syncthreads();  // (page k-1's reads of the other buffer are behind the previous barrier)
-      const uint4 q0 = *reinterpret_cast<const uint4*>(buf + 8 * tid), q1 = *reinterpret_cast<const uint4*>(buf + 8 * tid + 4);
-      const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[k][i] = E + 8 * tid + i < n ? w[i] : 0u;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < ZS_TILE; ++k) zs_load8(x, (p0 + k) * ZS_PAGE + 8 * (int64_t)tid, n, v[k]);
-  }
+  for (int k = 0; k < ZS_TILE; ++k) zs_load8(x, (p0 + k) * ZS_PAGE + 8 * (int64_t)tid, n, v[k]);
   int tile_total = 0;
 #pragma unroll
   for (int k = 0; k < ZS_TILE; ++k) {
@@ -510,27 +323,6 @@ __global__ __launch_bounds__(256) void zs_seg_expand_kernel(const int* __restric
   }
 }
 
-// Value offset of every mask word of W encodings (the head forward's fused update reads a lane's 4
-// values from one word pair without walking its page): wo[r][p * 64 + j] = page offset + popcount of
-// words 0 .. j-1 of page p.  One wave per page.
-__global__ __launch_bounds__(256) void zs_word_offsets_kernel(const int* __restrict__ meta, int64_t mstride,
-                                                              int64_t npages, int W, int* __restrict__ wo) {
-  const int lane = threadIdx.x & 63;
-  const int64_t gp = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (rank, page)
-  if (gp >= npages * W) return;
-  const int r = (int)(gp / npages);
-  const int64_t p = gp - (int64_t)r * npages;
-  const int* mr = meta + (int64_t)r * mstride + p * ZS_META;
-  const int cnt = __builtin_popcount((uint32_t)mr[1 + lane]);
-  int incl = cnt;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int o = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += o;
-  }
-  wo[(int64_t)r * npages * 64 + p * 64 + lane] = mr[0] + incl - cnt;
-}
-
 // ---------------------------------------------------------------------------- fused update
 // dW (=/+=) scale * dYᵀX, or the update-only W -= lr * scale * dYᵀX (linear_dw's contract), with
 // X given zero-suppressed: the all-gathered encodings of the W source ranks (rank r: meta at
@@ -682,13 +474,6 @@ void tds_zs_seg_decode(const int* meta, const int64_t* pg_start, const int* pg_c
 
 int64_t tds_zs_npages(int64_t n) { return (n + ZS_PAGE - 1) / ZS_PAGE; }
 
-void tds_zs_word_offsets(const int* meta, int64_t mstride, int64_t npages, int W, int* wo, hipStream_t st) {
-  const int64_t waves = npages * W;
-  hipLaunchKernelGGL(zs_word_offsets_kernel, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, st, meta, mstride, npages,
-                     W, wo);
-  TDS_LAUNCH_CHECK();
-}
-
 namespace {
 // Look-back state of one (device, stream): status words (zeroed once when allocated; grown by a
 // fresh allocation, the old one is kept -- a kernel may still be using it), the ticket counter
@@ -739,28 +524,6 @@ void tds_zs_encode(const float* x, int64_t n, int* meta, float* vals, int64_t ca
   hipLaunchKernelGGL(zs_encode_kernel<const uint32_t*>, dim3((unsigned)tiles), dim3(256), 0, st,
                      reinterpret_cast<const uint32_t*>(x), n, P, meta, reinterpret_cast<uint32_t*>(vals), cap, nnz,
                      status, ticket, epoch);
-  TDS_LAUNCH_CHECK();
-}
-
-// The same encoding of X = relu(aff2 affine of ya) for B images at pooled size Q, read from ya
-void tds_zs_encode_ya(const float* ya, const float* aff2, int B, int Q, int* meta, float* vals, int64_t cap,
-                      int64_t* nnz, hipStream_t st) {
-  if (Q < 16) {  // (a page's pieces fit the loader's two slots per thread from Q = 16 on)
-    tds_launch_fail("zs_encode_ya: needs Q >= 16");
-    return;
-  }
-  const PBGeom g = pb_geom(Q);
-  const int64_t K = (int64_t)32 * Q * Q, n = (int64_t)B * K;
-  const int64_t P = tds_zs_npages(n);
-  unsigned long long *status = nullptr, *ticket = nullptr, epoch = 0;
-  if (!zs_lookback((P + ZS_TILE - 1) / ZS_TILE, st, status, ticket, epoch)) {
-    tds_launch_fail("zs_encode_ya: look-back state allocation failed");
-    return;
-  }
-  const int64_t tiles = (P + ZS_TILE - 1) / ZS_TILE;
-  const ZSYa src{ya, aff2, g, K};
-  hipLaunchKernelGGL(zs_encode_kernel<ZSYa>, dim3((unsigned)tiles), dim3(256), 0, st, src, n, P, meta,
-                     reinterpret_cast<uint32_t*>(vals), cap, nnz, status, ticket, epoch);
   TDS_LAUNCH_CHECK();
 }
 

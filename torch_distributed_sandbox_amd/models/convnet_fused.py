@@ -27,8 +27,7 @@ per product with both operands rounded once to 11 significant bits -- TF32's sig
 arithmetic of the cuDNN convolutions the reference runs under PyTorch's default ``allow_tf32`` --
 at exact power-of-two range scales (p1 by BN1's Samuelson bound, the weights by their max, the
 conv2 output gradient by the step's magnitude bounds ``mag``); docs/KERNELS.md "conv2 in the TF32
-class".  The round-3 fp16x2 split (one operand exact as fp16 hi + lo) is the
-``-DTDS_CONV2_SPLIT=1`` variant build (``ops.conv2_split()``).
+class".
 ``mode='layers'`` is the exact-fp32 generic path.
 
 Gradient hand-off beside autograd: the fp16 p1 is an autograd output, but its gradient dp1 is
@@ -162,7 +161,7 @@ def _sinks(ctx, params, first):
 _ZERO = {}
 # counters the tests read: forward passes that applied the exchange's weight update in the head kernel,
 # and layer-1 forwards that took x moments precomputed by the input pipeline
-STATS = {"head_fused_updates": 0, "precomputed_input_moments": 0, "head_fused_ce": 0}
+STATS = {"precomputed_input_moments": 0, "head_fused_ce": 0}
 
 
 def _zero_scalar(device, dtype):
@@ -220,10 +219,9 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update", "labels", "ce", "pack")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "labels", "ce", "pack")
 
     def __init__(self):
-        self.fc_update = None
         self.pack = None  # (wp, wd): conv2's weights packed by the layer-1 forward (_pack_in_layer1)
         self.mag = None
         self.labels = None  # the batch's labels (attach_labels) -> ce = (labels, loss, dlogits) from the head
@@ -298,27 +296,12 @@ class _Head(torch.autograd.Function):
         P = y2.shape[1]
         B, K = ya.shape[0], wfc.shape[1]
         x_out = None
-        # the zero-suppressed activation exchange encodes X from ya and the BN2 affine itself
-        # (ops.zs_encode_ya): the head then writes no dense X; the other paths need the rows
-        from_ya = ex is not None and link.bn_done and ex.wants_ya(B, K, ya)
-        if ex is not None and not from_ya and ex.planned(B) in ("activations", "sharded"):
+        # the activation / sharded exchanges send the fc input rows X, which the head writes
+        if ex is not None and ex.planned(B) in ("activations", "sharded"):
             x_out = torch.empty((B, K), device=ya.device, dtype=torch.float32)
-        upd_obj, link.fc_update = link.fc_update, None
-        fused_upd = None
-        if upd_obj is not None:
-            if link.bn_done and x_out is None:
-                fused_upd = upd_obj.fused_args()  # (None: it ran the update itself -- an overflow step)
-            else:
-                upd_obj()  # the separate update, before the weight is read
         if link.bn_done:  # (bn_a, bn_b) = BN2's (stats, affine), finalized by the conv2 forward
             stats2, aff2 = bn_a, bn_b
-            if fused_upd is not None:
-                # the previous step's exchanged weight update, applied while the weight is
-                # streamed for these logits (ops.fused_head_forward_upd)
-                dy_all, meta_all, vals_all, rows, scale, lr = fused_upd
-                STATS["head_fused_updates"] += 1
-                logits = ops.fused_head_forward_upd(ya, aff2, wfc, bfc, P, dy_all, meta_all, vals_all, rows, scale, lr)
-            elif link.labels is not None:
+            if link.labels is not None:
                 # the loss and dlogits formed by the head forward's finalizing workgroup
                 logits, loss, dlogits = ops.fused_head_forward_aff_ce(ya, aff2, wfc, bfc, P, link.labels, x_out)
                 link.ce = (link.labels, loss, dlogits)
@@ -329,7 +312,7 @@ class _Head(torch.autograd.Function):
             logits, stats2, aff2 = ops.fused_head_forward(ya, bn_a, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
                                                           bfc, P, x_out)
         if ex is not None:
-            started = ex.begin_ya(ya, aff2, P, B, K) if from_ya else ex.begin(x_out, rows=B)
+            started = ex.begin(x_out, rows=B)
             if not started:
                 raise RuntimeError("fc gradient exchange refused to start after ready() agreed")
         ctx.save_for_backward(ya, stats2, aff2, g2, wfc)
@@ -422,8 +405,8 @@ def _pack_in_layer1(w2, x, link, link1):
     dev = x.device
     param_fence.wait(w2)  # a deferred update of the weights (overlap_optimizer) lands first
     mag = torch.empty(ops.mag_numel(x.shape[0], x.shape[2] // 2), device=dev, dtype=torch.int32)
-    wp = torch.empty(2 * 13 * 2 * 4 * 16 * 8, device=dev, dtype=torch.int16)
-    wd = torch.empty(2 * 25 * 4 * 16 * 8, device=dev, dtype=torch.int16)
+    wp = torch.empty(13 * 2 * 4 * 16 * 8, device=dev, dtype=torch.int16)
+    wd = torch.empty(25 * 4 * 16 * 8, device=dev, dtype=torch.int16)
     link.mag = link1.mag = mag
     link1.pack = (w2.detach(), wp, wd)
     link.pack = (wp, wd)
@@ -441,11 +424,9 @@ def forward(model, x):
     y2, ya, bn_a, bn_b = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
                                       bn2.running_var, bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps),
                                       link, link1)
-    # the fc update may still be running on DDP's side stream (overlap_optimizer): wait here,
-    # after the convolutions were queued, not before.  An exchanged update the head forward can
-    # apply itself (the activation exchange's, factored.py _Update) is handed to it instead
-    if _FUSED_FIN and x.shape[0] <= 8:
-        link.fc_update = param_fence.take(fc.weight, "zs_head")
+    # the fc update may still be running on DDP's side stream (overlap_optimizer), or deferred to
+    # here (the activation exchange's update sweep, factored.py _Update): wait / queue it now, after
+    # the convolutions were queued, not before
     param_fence.wait(fc.weight)
     param_fence.wait(fc.bias)
     ex = factored.get(fc.weight)

@@ -92,40 +92,6 @@ def _counts_of(meta_all: torch.Tensor, world: int, row: int) -> torch.Tensor:
     return meta_all.view(world, row)[:, row - 2:].contiguous().view(torch.int64).view(world)
 
 
-# A/B switches of the activation exchange's round-5 GPU paths (measured in docs/DISTRIBUTED.md):
-# TDS_ZS_FROM_YA: encode X straight from the fused head's ya + BN2 affine instead of from the dense X
-# the head forward writes; TDS_HEAD_FUSED_UPDATE: apply the previous step's exchanged weight update
-# inside the next head forward instead of a separate linear_dw_zs sweep.
-_ZS_FROM_YA = os.environ.get("TDS_ZS_FROM_YA", "0").strip() != "0"
-_HEAD_FUSED_UPDATE = os.environ.get("TDS_HEAD_FUSED_UPDATE", "0").strip() != "0"
-
-
-class _YaRows:
-    """This rank's fc input rows X = relu(a * ya + b) held as the fused head's pooled-blocked ``ya``
-    and BN2 affine ``aff2`` (the zero-suppressed encoder reads them, ops.zs_encode_ya: the dense X is
-    never written); materialised only for an overflow step's dense re-send."""
-
-    __slots__ = ("ya", "aff2", "P", "rows", "in_f")
-
-    def __init__(self, ya, aff2, P: int, rows: int, in_f: int):
-        self.ya, self.aff2, self.P, self.rows, self.in_f = ya, aff2, int(P), int(rows), int(in_f)
-
-    def tensors(self):
-        return (self.ya, self.aff2)
-
-    def dense(self) -> torch.Tensor:
-        from .. import _ext
-        from . import zs
-
-        n = self.rows * self.in_f
-        meta = torch.empty(zs.meta_numel(n), device=self.ya.device, dtype=torch.int32)
-        vals = torch.empty(n, device=self.ya.device, dtype=torch.float32)
-        _ext.ops().zs_encode_ya(self.ya, self.aff2, self.P, meta, vals)
-        out = torch.empty((self.rows, self.in_f), device=self.ya.device, dtype=torch.float32)
-        zs.decode(meta, vals, out)
-        return out
-
-
 def get(weight) -> Optional["ActivationExchange"]:
     return getattr(weight, _ATTR, None) if weight is not None else None
 
@@ -419,57 +385,22 @@ class ActivationExchange:
             return cap
         return min(n, self._cap[path]) if self._cap.get(path) else n
 
-    def wants_ya(self, rows: int, in_f: int, ya: torch.Tensor) -> bool:
-        """Would a forward with ``rows`` rows encode its X straight from the fused head's ``ya``
-        (begin_ya: the zero-suppressed activation path on the GPU)?"""
-        return (_ZS_FROM_YA and ya.is_cuda and self.compress and self._eligible(rows) == "activations"
-                and rows * in_f < (1 << 31) and in_f >= 32 * 16 * 16)  # (the ya encoder needs Q >= 16)
-
-    def begin_ya(self, ya: torch.Tensor, aff2: torch.Tensor, P: int, rows: int, in_f: int) -> bool:
-        """``begin`` for the fused head's activation exchange: the rows are encoded from ya and the
-        BN2 affine (ops.zs_encode_ya) instead of from a dense X the head would have written."""
-        if not self.wants_ya(rows, in_f, ya):
-            return False
-        src = _YaRows(ya.detach(), aff2.detach(), P, rows, in_f)
-        self._begin_zs(None, src)
-        self._x_local = src  # keep alive until the exchange completes (and the overflow re-send)
-        self.active = "activations"
-        self._set_skip(True)
-        return True
-
-    def _local_dense(self) -> torch.Tensor:
-        x = self._x_local
-        return x.dense() if isinstance(x, _YaRows) else x
-
-    def _local_tensors(self):
-        x = self._x_local
-        return x.tensors() if isinstance(x, _YaRows) else (x,)
-
-    def _begin_zs(self, x2d: Optional[torch.Tensor], ya_src: Optional[_YaRows] = None):
+    def _begin_zs(self, x2d: torch.Tensor):
         """Zero-suppressed all-gather of the rows (module docstring): encode, gather the fixed-
         size mask/offset records with each rank's count in their tail, then the values at this
         step's capacity.  The counts are copied to the host asynchronously after the first
-        gather, so ``defer`` can check them without waiting for the values.  ``ya_src``: encode
-        from the fused head's ya and BN2 affine instead of the dense rows."""
+        gather, so ``defer`` can check them without waiting for the values."""
         from . import distributed as tdist
         from . import zs
 
-        if ya_src is not None:
-            dev, n, shape = ya_src.ya.device, ya_src.rows * ya_src.in_f, (ya_src.rows, ya_src.in_f)
-        else:
-            dev, n, shape = x2d.device, x2d.numel(), tuple(x2d.shape)
+        dev, n, shape = x2d.device, x2d.numel(), tuple(x2d.shape)
         W = self.world
         M = zs.meta_numel(n)
         R = _meta_row(M)
         cap = self._take_cap("activations", n)
         meta = torch.empty(R, device=dev, dtype=torch.int32)
         vals = torch.empty(cap, device=dev, dtype=torch.float32)
-        if ya_src is not None:
-            from .. import _ext
-
-            nnz = _ext.ops().zs_encode_ya(ya_src.ya, ya_src.aff2, ya_src.P, meta[:M], vals)
-        else:
-            nnz = zs.encode(x2d, meta[:M], vals)
+        nnz = zs.encode(x2d, meta[:M], vals)
         meta[R - 2:].view(torch.int64).copy_(nnz.view(1).to(dev))
         meta_all = torch.empty(W * R, device=dev, dtype=torch.int32)
         w_meta = tdist.all_gather_into_tensor(meta_all, meta, group=self.group, async_op=True)
@@ -638,7 +569,7 @@ class ActivationExchange:
             rows, in_f = z["rows"], z["in_f"]
             self._x_buf = torch.empty((self.world * rows, in_f), device=z["meta"].device, dtype=torch.float32)
             z["w_vals"].wait()
-            self._x_work = tdist.all_gather_into_tensor(self._x_buf, self._local_dense(), group=self.group,
+            self._x_work = tdist.all_gather_into_tensor(self._x_buf, self._x_local, group=self.group,
                                                         async_op=True)
             return
         self._zs_decode_pending = z
@@ -738,7 +669,7 @@ class ActivationExchange:
             side = self._own_stream
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
-        keep = (self._dy, self._x_buf) + (self._local_tensors() if self._x_local is not None else ())  # side stream
+        keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
         z = getattr(self, "_zs_decode_pending", None)
         if z is not None:
             if z.get("kind") == "sharded":
@@ -799,41 +730,16 @@ class ActivationExchange:
         z, self._zs = self._zs, None
         x_work, x_dense = self._x_work, self._x_buf
         xl = self._x_local  # (captured: _done() below clears the attribute before update() runs)
-
-        def local_dense():
-            return xl.dense() if isinstance(xl, _YaRows) else xl
         in_f = self.weight.shape[1]
         weight, lr, group, world = self.weight, float(lr), self.group, self.world
 
         ex = self
 
         class _Update:
-            """The deferred update (param_fence.defer).  Called: queue it on the current stream.
-            The fused head forward may instead take it (param_fence.take(weight, "zs_head")) and call
-            ``fused_args()``: the count check, then -- no overflow -- the gathered encodings and dY
-            for the head forward to apply the update itself while it streams the weight for the
-            logits (ops.fused_head_forward_upd: one pass over the 720 MB weight instead of the
-            update sweep's read + write and the forward's read); otherwise the update runs here."""
-
-            fused_kind = ("zs_head" if _HEAD_FUSED_UPDATE and z is not None and ex._zs_fused(z, (weight.data,))
-                          and world * rows <= 40 and weight.shape[0] <= 10 else None)
-
-            def __init__(self):
-                self.checked = None  # the count check's result (overflow?), once made
-
-            def _check(self):
-                if self.checked is None:
-                    self.checked = ex._zs_check(z)
-                return self.checked
-
-            def fused_args(self):
-                torch.cuda.current_stream(dev).wait_event(ev_dy)
-                if self._check():
-                    self()  # overflow: the dense re-send and the separate update
-                    return None
-                z["w_meta"].wait()
-                z["w_vals"].wait()
-                return (dy_all, z["meta_all"].view(world, z["R"]), z["vals_all"].view(world, z["cap"]), rows, scale, lr)
+            """The deferred update (param_fence.defer), queued on the current stream when called: the
+            count check, then the update from the gathered encodings (or, after an overflow, from
+            this step's rows re-sent dense).  (Applying it inside the next head forward while it
+            streams the weight measured even with this separate sweep, 0.585 vs 0.570 ms, r5_s8.)"""
 
             def __call__(self):
                 from .. import _ext
@@ -842,7 +748,7 @@ class ActivationExchange:
                 with torch.no_grad():
                     x_buf = None
                     if z is not None:
-                        if not self._check():
+                        if not ex._zs_check(z):
                             if ex._zs_fused(z, (weight.data,)):
                                 ex._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
                                 return
@@ -851,7 +757,7 @@ class ActivationExchange:
                         else:  # overflow: this step's rows, dense, from every rank
                             z["w_vals"].wait()
                             x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
-                            tdist.all_gather_into_tensor(x_buf, local_dense(), group=group)
+                            tdist.all_gather_into_tensor(x_buf, xl, group=group)
                     else:
                         x_work.wait()
                         x_buf = x_dense
