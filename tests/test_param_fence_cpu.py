@@ -1,10 +1,13 @@
-"""ops/param_fence.py on the CPU: deferred updates run once at the first wait."""
+"""ops/param_fence.py on the CPU: deferred updates run once at the first wait, and the fused head
+forward's take() hands over the single deferred update while leaving any events for wait()."""
 import torch
 
 from torch_distributed_sandbox_amd.ops import param_fence
 
 
 class _Upd:
+    fused_kind = "groups"
+
     def __init__(self, log):
         self.log = log
 
@@ -20,6 +23,33 @@ def test_wait_runs_deferred_once():
     param_fence.wait(p)
     param_fence.wait(p)
     assert log == ["ran"] and not param_fence.pending(p)
+
+
+def test_take_leaves_events_for_wait():
+    # DDP's overlapped optimizer fences every parameter of the deferred bucket with the side
+    # stream's event after the exchange deferred the weight's update: take() must still hand the
+    # update over
+    p = torch.zeros(3)
+    log = []
+    upd = _Upd(log)
+    param_fence.defer(p, upd)
+    param_fence.set(p, "side-stream event")
+    assert param_fence.take(p, "groups") is upd
+    assert param_fence.pending(p)  # the event is still there for wait()
+    param_fence.wait(p)
+    assert not param_fence.pending(p) and log == []
+
+
+def test_take_refuses_other_kinds_and_two_updates():
+    p = torch.zeros(3)
+    log = []
+    param_fence.defer(p, _Upd(log))
+    assert param_fence.take(p, "other") is None
+    param_fence.defer(p, _Upd(log))
+    assert param_fence.take(p, "groups") is None  # two deferred updates: run in order by wait()
+    param_fence.wait(p)
+    assert log == ["ran", "ran"]
+    assert param_fence.take(None, "groups") is None
 
 
 def _deferred_ddp(monkeypatch):

@@ -17,4 +17,9 @@ echo "peak: $(tail -1 $O/drv_1.log | python3 -c 'import json,sys; c=json.loads(s
 cd /tmp && export TMPDIR=/tmp && cd $R
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 -u bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof.log 2>&1 || { echo "prof failed"; tail -5 $O/prof.log; exit 1; }
 echo "prof: $(grep '^{' $O/prof.log | cut -c1-100)"
+# memory-system probes: HBM read / copy / read-modify-write ceilings (the head backward's mix) and the
+# texture path's cost per load instruction by address pattern (the conv2 backward's staging)
+timeout -k 10 120 tools/micro/rw_bw > $O/rw_bw.log 2>&1 || { echo "rw_bw failed"; tail -5 $O/rw_bw.log; exit 1; }
+timeout -k 10 120 tools/micro/ta_pattern > $O/ta_pattern.log 2>&1 || { echo "ta_pattern failed"; tail -5 $O/ta_pattern.log; exit 1; }
+cat $O/rw_bw.log $O/ta_pattern.log
 echo done

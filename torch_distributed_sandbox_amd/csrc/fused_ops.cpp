@@ -504,6 +504,62 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, c
   return {logits, loss, dlogits};
 }
 
+// The head forward in channel-range launches (the activation exchange's column groups, parallel/
+// factored.py: each group's fc input rows can be encoded and start travelling while the next range
+// runs).  head_forward_range_ws allocates the step's shared workspace -- (partials, sums, logits,
+// dlogits, loss, 1/count) -- and fused_head_forward_range runs channels [c0, c1) over it, writing
+// that range's X rows into x_out [B, (c1-c0)*Q*Q]; the launch that completes the 32nd channel
+// finishes the logits (and, with labels, the cross-entropy) inside itself (head_pb.hip HPFin).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> head_forward_range_ws(const Tensor& ya, const Tensor& wfc,
+                                                                                 int64_t P) {
+  const int64_t B = ya.size(0), Q = P / 2, NC = wfc.size(0);
+  const int nblk = 32 * tds_head_pb_nblk((int)Q);
+  auto o = ya.options();
+  return {at::empty({(int64_t)(nblk + 32) * B * NC}, o.dtype(at::kDouble)), at::empty({B * NC}, o.dtype(at::kDouble)),
+          at::empty({B, NC}, o), at::empty({B, NC}, o), at::empty({}, o), at::empty({1}, o)};
+}
+
+void fused_head_forward_range(const Tensor& ya, const Tensor& aff2, const Tensor& wfc, const c10::optional<Tensor>& bfc,
+                              int64_t P, int64_t c0, int64_t c1, const Tensor& part, const Tensor& lsum,
+                              const Tensor& logits, const Tensor& dlogits, const Tensor& loss, const Tensor& inv,
+                              const c10::optional<Tensor>& labels, const c10::optional<Tensor>& x_out) {
+  TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_range: ya must be [B,32,PB]");
+  const int64_t B = ya.size(0), Q = P / 2;
+  TORCH_CHECK(Q >= 4 && B >= 1 && B <= 8, "fused_head_forward_range: needs P/2 >= 4 and 1 <= B <= 8 (one pass)");
+  TORCH_CHECK(0 <= c0 && c0 < c1 && c1 <= 32, "fused_head_forward_range: channels 0 <= c0 < c1 <= 32");
+  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(aff2, at::kFloat, {64}, "aff2");
+  TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
+              "fc.weight must be [<=10, 32*Q*Q]");
+  const int64_t NC = wfc.size(0);
+  need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
+  const float* bf = optf(bfc, NC, "fc.bias");
+  const int nblk = 32 * tds_head_pb_nblk((int)Q);
+  need(part, at::kDouble, {(int64_t)(nblk + 32) * B * NC}, "head partials");
+  need(lsum, at::kDouble, {B * NC}, "logit sums");
+  need(logits, at::kFloat, {B, NC}, "logits");
+  need(dlogits, at::kFloat, {B, NC}, "dlogits");
+  need(loss, at::kFloat, {}, "loss");
+  need(inv, at::kFloat, {1}, "1/count");
+  const int64_t* lab = nullptr;
+  if (labels.has_value() && labels->defined()) {
+    need(*labels, at::kLong, {B}, "labels");
+    lab = labels->data_ptr<int64_t>();
+  }
+  float* xo = nullptr;
+  if (x_out.has_value() && x_out->defined()) {
+    need(*x_out, at::kFloat, {B, (c1 - c0) * Q * Q}, "x_out (the range's fc input rows)");
+    xo = x_out->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(ya.device());
+  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
+                                 part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
+                                 (int)Q, (int)NC, stream_of(ya), true, lab, dlogits.data_ptr<float>(),
+                                 loss.data_ptr<float>(), inv.data_ptr<float>(), (int)c0, (int)c1);
+  TORCH_CHECK(rc >= 0, "fused_head_forward_range: unsupported shape or no in-launch finalize (TDS_FUSED_FIN=0)");
+  check_launches("fused_head_forward_range");
+}
+
 // ---------------------------------------------------------------- head forward (BN2 finalize + fc)
 // returns (logits, stats2 [mean32|invstd32], aff2 [a32|b32])
 std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
@@ -1023,6 +1079,13 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
         "Tensor(a!)? x_out=None) -> (Tensor, Tensor, Tensor)",
         &fused_head_forward_aff_ce);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
+  m.def("head_forward_range_ws(Tensor ya, Tensor wfc, int P) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
+        &head_forward_range_ws);
+  m.def(
+      "fused_head_forward_range(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, int c0, int c1, Tensor(a!) part, "
+      "Tensor(b!) lsum, Tensor(c!) logits, Tensor(d!) dlogits, Tensor(e!) loss, Tensor(f!) inv, Tensor? labels=None, "
+      "Tensor(g!)? x_out=None) -> ()",
+      &fused_head_forward_range);
   m.def("mag_numel(int B, int P) -> int", &mag_numel);
   m.def("mag_ypart_count() -> int", &mag_ypart_count);
   m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);

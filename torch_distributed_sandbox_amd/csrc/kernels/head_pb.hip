@@ -170,7 +170,9 @@ __device__ __forceinline__ void hp_store4(float* out, const PBGeom& g, const HPR
 }
 
 // Forward.  partial[blk][B*NC] (fp64): this workgroup's share of logits[b][j] for images
-// b0 .. b0+NB-1; xout (optional): X in the fc's flatten order, [B][32*Q*Q].
+// b0 .. b0+NB-1; xout (optional): X in the fc's flatten order, [B][32*Q*Q] -- or, for a launch over
+// channels [c0, c1) (the activation exchange's column groups, parallel/factored.py), that range's
+// columns as their own [B][(c1-c0)*Q*Q] rows (x_rs = (c1-c0)*Q*Q).
 // fin (optional, one pass: B <= HP_MAXB): the logits are finished in this launch -- the last
 // workgroup of channel c to arrive sums the channel's rows into fin.cpart[c] (fixed order), the last
 // channel to finish sums the 32 channel rows and adds the bias (common.h tds_arrive; replaces
@@ -194,16 +196,16 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
                                                                  const float* __restrict__ aff2,
                                                                  double* __restrict__ partial,
                                                                  float* __restrict__ xout, PBGeom g, int Btot, int b0,
-                                                                 int NC, HPFin fin) {
+                                                                 int NC, HPFin fin, int c0, int64_t x_rs) {
   __shared__ float red[HP_THREADS / 64][HP_MAXB * 10];
   __shared__ int last_flag;
   __shared__ double wpart[256];
   const HPGrid hg = hp_grid(g);
-  const int wg = blockIdx.x;
-  const int c = wg / hg.per_channel(), band = wg - c * hg.per_channel();
+  const int c = c0 + (int)blockIdx.x / hg.per_channel(), band = (int)blockIdx.x - (c - c0) * hg.per_channel();
+  const int wg = c * hg.per_channel() + band;  // this workgroup's partial row (all 32 channels' numbering)
   const float a = aff2[c], bb = aff2[32 + c];
   const int Q = g.Q;
-  const int64_t QQ = (int64_t)Q * Q, K = 32 * QQ;
+  const int64_t QQ = (int64_t)Q * Q;
   float acc[NB][10];
 #pragma unroll
   for (int b = 0; b < NB; ++b)
@@ -240,10 +242,13 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
       // X rows in the fc's flatten order, an image's row offset (b K + c Q^2 + py Q) has the weight
       // row's alignment (K = 32 Q^2): 16-B stores or float2 pairs as for the weight (hp_store4; 4-B
       // stores per element cost the forward 0.14 ms at the bench shape, r5_s9)
-      const HPRow rwx(g, th, c, R);
+      // (a channel range's own rows start at its first channel: offsets shift by c0 Q^2, a multiple
+      // of 4 floats whenever x_rs is -- the host checks -- so the alignment classes are unchanged)
+      HPRow rwx(g, th, c, R);
+      rwx.off -= (int64_t)c0 * QQ;
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-        hp_store4(xout + (int64_t)(b0 + b) * K, g, rwx, 0, make_float4(x[b][0], x[b][1], x[b][2], x[b][3]), false);
+        hp_store4(xout + (int64_t)(b0 + b) * x_rs, g, rwx, 0, make_float4(x[b][0], x[b][1], x[b][2], x[b][3]), false);
     }
 #pragma unroll
     for (int j = 0; j < 10; ++j) {
@@ -533,20 +538,26 @@ int tds_head_bwd_pb_nblk(int Q) { return hp_grid_b(pb_geom(Q)).per_channel(); } 
 int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
 
 // partial: double [32 * nblk + 32][B*NC] (the last 32 rows: the in-launch finalizer's channel sums);
-// sums: double [B*NC].  fused_fin = false: the separate head_logits launch (the A/B reference)
+// sums: double [B*NC].  fused_fin = false: the separate head_logits launch (the A/B reference).
+// [c0, c1) != [0, 32): this launch covers those channels only (in-launch finalize required: the
+// logits are finished by the launch that completes the 32nd channel, so a step's range launches
+// share partial / sums / logits and run on one stream); xout then holds the range's own rows.
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st, bool fused_fin,
-                    const int64_t* labels, float* dlogits, float* loss, float* inv_count) {
-  if (B < 1 || NC < 1 || NC > 10 || Q < 1) return -1;
+                    const int64_t* labels, float* dlogits, float* loss, float* inv_count, int c0, int c1) {
+  if (B < 1 || NC < 1 || NC > 10 || Q < 1 || c0 < 0 || c1 > 32 || c0 >= c1) return -1;
   const PBGeom g = pb_geom(Q);
-  const int nwg = 32 * hp_grid(g).per_channel();
+  const bool range = c0 != 0 || c1 != 32;
+  const int64_t QQ = (int64_t)Q * Q, x_rs = (int64_t)(c1 - c0) * QQ;
+  if (range && (x_rs % 4 != 0 || ((int64_t)c0 * QQ) % 4 != 0)) return -1;  // (X alignment classes, above)
+  const int nwg = (c1 - c0) * hp_grid(g).per_channel();
   // one pass: the logits are finished inside the launch (HPFin; partial then holds nwg + 32 rows)
   HPFin fin{nullptr, nullptr, nullptr, nullptr, nullptr};
   const int BN = B * NC, nbc = hp_grid(g).per_channel();
   const bool wide_ok = BN <= 256 && nbc <= WRS_MAXL * (256 / BN) && 32 <= WRS_MAXL * (256 / BN);
   if (B <= HP_MAXB && fused_fin && wide_ok && tds_fused_fin_enabled()) {
     fin.sync = tds_sync_words(kSyncHeadFwd, st);
-    fin.cpart = partial + (int64_t)nwg * B * NC;
+    fin.cpart = partial + (int64_t)32 * nbc * B * NC;
     fin.sums = sums;
     fin.bias = bias;
     fin.logits = logits;
@@ -555,12 +566,13 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
     fin.loss = loss;
     fin.inv_count = inv_count;
   }
+  if (range && fin.sync == nullptr) return -1;
   for (int b0 = 0; b0 < B; b0 += HP_MAXB) {
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
 #define TDS_HPF(NBV)                                                                                                   \
   case NBV:                                                                                                            \
     hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
-                       B, b0, NC, fin);                                                                                \
+                       B, b0, NC, fin, c0, x_rs);                                                                      \
     TDS_LAUNCH_CHECK();                                                                                                \
     break;
     switch (nb) {

@@ -200,7 +200,7 @@ bool tds_fused_fin_enabled();  // TDS_FUSED_FIN=0: the separate finalize launche
 int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st,
                     bool fused_fin = true, const int64_t* labels = nullptr, float* dlogits = nullptr,
-                    float* loss = nullptr, float* inv_count = nullptr);
+                    float* loss = nullptr, float* inv_count = nullptr, int c0 = 0, int c1 = 32);
 int tds_head_bwd_pb_npass(int B);
 // channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
 // soon as its launch lands; the BN2 partials of the other channels are left untouched)

@@ -161,7 +161,7 @@ def _sinks(ctx, params, first):
 _ZERO = {}
 # counters the tests read: forward passes that applied the exchange's weight update in the head kernel,
 # and layer-1 forwards that took x moments precomputed by the input pipeline
-STATS = {"precomputed_input_moments": 0, "head_fused_ce": 0}
+STATS = {"precomputed_input_moments": 0, "head_fused_ce": 0, "head_range_launches": 0}
 
 
 def _zero_scalar(device, dtype):
@@ -219,9 +219,10 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "labels", "ce", "pack")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update", "labels", "ce", "pack")
 
     def __init__(self):
+        self.fc_update = None  # the activation exchange's grouped deferred update, run range by range
         self.pack = None  # (wp, wd): conv2's weights packed by the layer-1 forward (_pack_in_layer1)
         self.mag = None
         self.labels = None  # the batch's labels (attach_labels) -> ce = (labels, loss, dlogits) from the head
@@ -284,6 +285,32 @@ class _Conv2(torch.autograd.Function):
         return dp1_ph, dw2, db2, None, None, None, None, None, None, None, None, None
 
 
+def _head_forward_grouped(ops, ya, aff2, wfc, bfc, P, ex, upd, link):
+    """The head forward with the grouped zero-suppressed activation exchange (parallel/factored.py):
+    one launch per column group (whole channel planes), each group's fc input rows handed to the
+    exchange right after its launch is queued -- its encode and gathers start there, while the next
+    ranges run -- and the previous step's exchanged update (``upd``) queued group by group right
+    before the launch that reads those columns.  The launch completing the 32nd channel finishes
+    the logits (and, with the batch's labels, the cross-entropy) in itself."""
+    B, K = ya.shape[0], wfc.shape[1]
+    QQ = K // 32
+    groups = ex.begin_groups(B, K, ya.device, planes=32)
+    ws = ops.head_forward_range_ws(ya, wfc, P)
+    for gi, (k0, k1) in enumerate(groups):
+        if upd is not None:
+            upd.run_until(k1)
+        xg = torch.empty((B, k1 - k0), device=ya.device, dtype=torch.float32)
+        ops.fused_head_forward_range(ya, aff2, wfc, bfc, P, k0 // QQ, k1 // QQ, *ws, link.labels, xg)
+        ex.group_ready(gi, xg)
+    if upd is not None:
+        upd()  # (groups past the last range, had the geometry changed)
+    STATS["head_range_launches"] += len(groups)
+    if link.labels is not None:
+        link.ce = (link.labels, ws[4], ws[3])
+        STATS["head_fused_ce"] += 1
+    return ws[2]
+
+
 class _Head(torch.autograd.Function):
     """BN2 finalize + affine + ReLU + fc over ya.  y2 is an input only so that autograd routes
     the conv2 backward through this node: its gradient travels in the link (g2m, BN2 backward
@@ -295,6 +322,19 @@ class _Head(torch.autograd.Function):
         _run_before_head_forward()
         P = y2.shape[1]
         B, K = ya.shape[0], wfc.shape[1]
+        upd, link.fc_update = link.fc_update, None
+        if link.bn_done and ex is not None and _FUSED_FIN and B <= 8 and ex.grouped(B, K):
+            logits = _head_forward_grouped(ops, ya, bn_b, wfc, bfc, P, ex, upd, link)
+            ctx.save_for_backward(ya, bn_a, bn_b, g2, wfc)
+            ctx.P = P
+            ctx.y2_meta = (y2.shape, y2.dtype, y2.device)
+            ctx.wfc_param = wfc
+            ctx.small = (bfc, g2, be2)
+            ctx.ex = ex
+            ctx.link = link
+            return logits
+        if upd is not None:
+            upd()  # the whole deferred update, before the weight is read
         x_out = None
         # the activation / sharded exchanges send the fc input rows X, which the head writes
         if ex is not None and ex.planned(B) in ("activations", "sharded"):
@@ -426,7 +466,9 @@ def forward(model, x):
                                       link, link1)
     # the fc update may still be running on DDP's side stream (overlap_optimizer), or deferred to
     # here (the activation exchange's update sweep, factored.py _Update): wait / queue it now, after
-    # the convolutions were queued, not before
+    # the convolutions were queued, not before.  A grouped update goes to the head forward, which
+    # queues it range by range
+    link.fc_update = param_fence.take(fc.weight, "groups")
     param_fence.wait(fc.weight)
     param_fence.wait(fc.bias)
     ex = factored.get(fc.weight)

@@ -58,5 +58,24 @@ def wait(param) -> None:
             cur.wait_event(v)
 
 
+def take(param, kind: str):
+    """The pending deferred update of ``param`` if it is its ONLY deferred item and offers the form
+    ``kind`` (its ``fused_kind`` attribute), removed from the fence -- the caller runs it (the fused
+    head forward runs the activation exchange's grouped update range by range,
+    parallel/factored.py ``_Update.run_until``); else None and the fence is unchanged.  Events stay
+    in the fence for the caller's :func:`wait` (under DDP's overlapped optimizer the end-of-backward
+    side-stream step fences every parameter of its bucket, this one included)."""
+    f = getattr(param, _ATTR, None) if param is not None else None
+    if not f:
+        return None
+    fns = [i for i, (k, _) in enumerate(f) if k == "fn"]
+    if len(fns) != 1 or getattr(f[fns[0]][1], "fused_kind", None) != kind:
+        return None
+    fn = f.pop(fns[0])[1]
+    if not f:
+        delattr(param, _ATTR)
+    return fn
+
+
 def pending(param) -> bool:
     return bool(getattr(param, _ATTR, None))

@@ -53,6 +53,14 @@ only when the step's gradient is formed (``defer``, after the head backward is q
 above the capacity sends the dense rows once more for that step.  The byte model takes the
 measured ratio: ``link_bytes("activations")`` = B·K·4·ratio.
 
+Column groups (activation path, zero-suppressed): the rows travel as ``groups`` column ranges
+(whole channel planes on the fused head), each encoded and gathered on its own.  The fused head
+forward runs one launch per group and hands each group's rows over as soon as its launch is
+queued (``begin_groups`` / ``group_ready``), so the first gather starts a quarter of the way
+through the head forward instead of after the whole forward and one encode of all rows; the
+deferred update (next forward) runs group by group right before the head launch that reads those
+columns (``_Update.run_until``), so a group's gathers only have to land before that launch.
+
 Protocol (driven by ``parallel/ddp.py``):
 
 * ``arm(sync)`` each DDP forward: the exchange may run this step.
@@ -130,12 +138,14 @@ class ActivationExchange:
     CAP_ROUND = 1 << 16   # capacities rounded up to 64 Ki elements (stable allocations)
 
     def __init__(self, weight: torch.nn.Parameter, bias: Optional[torch.nn.Parameter], group, world: int,
-                 mode: str, set_skip, weight_view, bias_view, chunks: int = 1, compress: bool = True):
+                 mode: str, set_skip, weight_view, bias_view, chunks: int = 1, compress: bool = True,
+                 groups: int = 4):
         if mode not in ("auto", "activations", "sharded", "chunked", "allreduce"):
             raise ValueError(f"ActivationExchange mode must be auto|activations|sharded|chunked|allreduce, got {mode!r}")
         self.weight, self.bias = weight, bias
         self.group, self.world, self.mode = group, world, mode
         self.chunks = max(1, int(chunks))
+        self.groups = max(1, int(groups))  # column groups of the zero-suppressed activation path
         self._works = []  # chunked: the per-chunk all-reduce works of this step
         self._set_skip, self._wview, self._bview = set_skip, weight_view, bias_view
         self.armed = False
@@ -147,7 +157,7 @@ class ActivationExchange:
         self._own_stream = None  # otherwise (GPU): a private side stream
         # zero-suppressed activation rows (parallel/zs.py)
         self.compress = bool(compress)
-        self._zs = None  # this step's encoded exchange: dict
+        self._zs = None  # this step's encoded exchange: dict (sharded) or list of per-group dicts (activations)
         self._step_zs = False  # this step's rows travelled encoded (last_path's "(zs)" tag)
         # value capacity (elements) per path, from that path's earlier counts: "activations" holds
         # a per-rank total, "sharded" a per-segment slot, so neither may seed the other
@@ -157,6 +167,7 @@ class ActivationExchange:
         self.x_ratio = 1.0
         self.zs_stats = {"steps": 0, "overflows": 0, "last_nnz": None}
         self._cap_once = None  # force_capacity_once
+        self._planes_hint = 0  # the fused head's channel planes (its groups are whole planes), once seen
         setattr(weight, _ATTR, self)
 
     def detach(self):
@@ -194,6 +205,16 @@ class ActivationExchange:
             cuts = [round(i * planes / n) for i in range(n + 1)]
             return [(cuts[i] * per, cuts[i + 1] * per) for i in range(n) if cuts[i + 1] > cuts[i]]
         return [(a, e) for a, e in shard_bounds(in_f, self.chunks) if e > a]
+
+    def column_groups(self, in_f: int, planes: int = 0):
+        """The [k0, k1) column ranges of the grouped activation exchange: ``groups`` ranges of whole
+        planes (the fused head: channels) or 64-aligned."""
+        if planes:
+            per = in_f // planes
+            n = min(self.groups, planes)
+            cuts = [round(i * planes / n) for i in range(n + 1)]
+            return [(cuts[i] * per, cuts[i + 1] * per) for i in range(n) if cuts[i + 1] > cuts[i]]
+        return [(a, e) for a, e in shard_bounds(in_f, self.groups) if e > a]
 
     def chunk_ready(self, dw: torch.Tensor, k0: int, k1: int):
         """Columns [k0, k1) of ``dw`` are final on the current stream: all-reduce their N row
@@ -293,9 +314,12 @@ class ActivationExchange:
         zs_ok = self.compress and n < (1 << 31)
         if path == "activations":
             if zs_ok:
-                gather("zs records all-gather (int32)", _meta_row(zs.meta_numel(n)), torch.int32)
-                cap = min(n, self._cap["activations"]) if self._cap.get("activations") else n
-                gather("zs values all-gather (first-step capacity)", cap, torch.float32)
+                for gi, (k0, k1) in enumerate(self.column_groups(in_f, self._planes_hint)):
+                    ng = rows * (k1 - k0)
+                    gather(f"zs records all-gather, group {gi} (int32)", _meta_row(zs.meta_numel(ng)), torch.int32)
+                    cap = self._cap.get(("activations", gi))
+                    gather(f"zs values all-gather, group {gi} (first-step capacity)", min(ng, cap) if cap else ng,
+                           torch.float32)
             else:
                 gather("activation rows all-gather", n, torch.float32)
             gather("dY all-gather", rows * out_f, torch.float32)
@@ -353,7 +377,10 @@ class ActivationExchange:
         # inputs take the dense exchange of the same path
         zs_ok = self.compress and x2d.dtype == torch.float32 and x2d.numel() < (1 << 31)
         if path == "activations" and zs_ok:
-            self._begin_zs(x2d)
+            groups = self.begin_groups(rows, in_f, x2d.device)
+            for gi, (k0, k1) in enumerate(groups):
+                self.group_ready(gi, x2d[:, k0:k1].contiguous())
+            return True
         elif path == "activations":
             self._x_buf = torch.empty((self.world * rows, in_f), device=x2d.device, dtype=x2d.dtype)
             self._x_work = tdist.all_gather_into_tensor(self._x_buf, x2d, group=self.group, async_op=True)
@@ -373,23 +400,60 @@ class ActivationExchange:
         self._set_skip(True)
         return True
 
+    def grouped(self, rows: int, in_f: int) -> bool:
+        """Would a forward with ``rows`` rows of ``in_f`` run the grouped zero-suppressed activation
+        exchange (begin_groups / group_ready)?"""
+        return self.compress and self._eligible(rows) == "activations" and rows * in_f < (1 << 31)
+
+    def begin_groups(self, rows: int, in_f: int, dev, planes: int = 0):
+        """Start a grouped zero-suppressed activation exchange: returns the column groups; the caller
+        hands each group's [rows, k1 - k0] rows to ``group_ready`` in order (the fused head: right
+        after that group's launch).  Every rank uses the same groups."""
+        if planes:
+            self._planes_hint = int(planes)
+        groups = self.column_groups(in_f, planes)
+        self._zs = []
+        self._zs_groups = groups
+        self._x_local = []
+        self._step_zs = True
+        self._x_work = None
+        self.active = "activations"
+        self._set_skip(True)
+        return groups
+
+    def group_ready(self, gi: int, xg: torch.Tensor):
+        """Group ``gi``'s rows are final on the current stream: encode them and start their two
+        gathers (records with the count in their tail, then the values at this group's capacity)."""
+        k0, k1 = self._zs_groups[gi]
+        if len(self._zs) != gi or tuple(xg.shape) != (xg.shape[0], k1 - k0):
+            raise RuntimeError(f"activation exchange: group {gi} out of order or of the wrong width")
+        xg = xg.detach().contiguous()
+        z = self._begin_zs(xg, gi)
+        z["k0"], z["k1"], z["x_local"] = k0, k1, xg
+        self._zs.append(z)
+        self._x_local.append(xg)  # keep alive until the exchange completes
+
     def force_capacity_once(self, cap: int) -> None:
         """Fault injection (tests): the next encoded step sends its values at capacity ``cap``
         (elements; the sharded path: per segment), whatever the earlier counts gave -- a cap below
         the step's counts drives the overflow path (the dense re-send)."""
         self._cap_once = max(1, int(cap))
 
-    def _take_cap(self, path: str, n: int) -> int:
+    def _take_cap(self, path: str, n: int, gi: Optional[int] = None) -> int:
         if self._cap_once is not None:
             cap, self._cap_once = min(n, self._cap_once), None
             return cap
-        return min(n, self._cap[path]) if self._cap.get(path) else n
+        cap = self._cap.get((path, gi)) if gi is not None else None
+        if cap is None:  # (a path-level capacity: the first step, or set by a test)
+            cap = self._cap.get(path)
+        return min(n, cap) if cap else n
 
-    def _begin_zs(self, x2d: torch.Tensor):
-        """Zero-suppressed all-gather of the rows (module docstring): encode, gather the fixed-
-        size mask/offset records with each rank's count in their tail, then the values at this
-        step's capacity.  The counts are copied to the host asynchronously after the first
-        gather, so ``defer`` can check them without waiting for the values."""
+    def _begin_zs(self, x2d: torch.Tensor, gi: int = 0):
+        """Zero-suppressed all-gather of one column group's rows (module docstring): encode, gather
+        the fixed-size mask/offset records with each rank's count in their tail, then the values at
+        the group's capacity.  The counts are copied to the host asynchronously after the first
+        gather, so the consumer can check them without waiting for the values.  Returns the group's
+        state."""
         from . import distributed as tdist
         from . import zs
 
@@ -397,7 +461,7 @@ class ActivationExchange:
         W = self.world
         M = zs.meta_numel(n)
         R = _meta_row(M)
-        cap = self._take_cap("activations", n)
+        cap = self._take_cap("activations", n, gi)
         meta = torch.empty(R, device=dev, dtype=torch.int32)
         vals = torch.empty(cap, device=dev, dtype=torch.float32)
         nnz = zs.encode(x2d, meta[:M], vals)
@@ -418,11 +482,9 @@ class ActivationExchange:
                 meta_all.record_stream(cstream)
         vals_all = torch.empty(W * cap, device=dev, dtype=torch.float32)
         w_vals = tdist.all_gather_into_tensor(vals_all, vals, group=self.group, async_op=True)
-        self._zs = {"n": n, "M": M, "R": R, "cap": cap, "meta": meta, "vals": vals, "meta_all": meta_all, "vals_all": vals_all,
-                    "w_meta": w_meta, "w_vals": w_vals, "counts_host": counts_host, "counts_ev": counts_ev,
-                    "rows": shape[0], "in_f": shape[1]}
-        self._step_zs = True
-        self._x_work = None  # set by _zs_resolve
+        return {"n": n, "M": M, "R": R, "cap": cap, "meta": meta, "vals": vals, "meta_all": meta_all,
+                "vals_all": vals_all, "w_meta": w_meta, "w_vals": w_vals, "counts_host": counts_host,
+                "counts_ev": counts_ev, "rows": shape[0], "in_f": shape[1], "gi": gi}
 
     def _layouts(self, rows: int, in_f: int, dev):
         """(send, receive) segment layouts of the sharded exchange (parallel/zs.py SegLayout),
@@ -541,6 +603,49 @@ class ActivationExchange:
             return True
         return False
 
+    def _zs_check_groups(self, zl) -> List[bool]:
+        """The count check of a grouped activation step (every group's counts are in by then): per
+        group, did some rank's count exceed the group's capacity?  Sets each group's capacity for the
+        next steps, the statistics (one step) and the measured ratio over all groups."""
+        W = self.world
+        over, tot, dense, per_rank = [], 0.0, 0, [0] * W
+        for z in zl:
+            counts = self._zs_counts(z)
+            mx = max(counts)
+            gi = z["gi"]
+            self._cap[("activations", gi)] = min(z["n"], -(-int(mx * self.CAP_MARGIN) // self.CAP_ROUND) * self.CAP_ROUND)
+            over.append(mx > z["cap"])
+            tot += mx + z["R"]
+            dense += z["n"]
+            for r in range(W):
+                per_rank[r] += counts[r]
+        self.zs_stats["steps"] += 1
+        self.zs_stats["last_nnz"] = per_rank
+        if any(over):
+            self.zs_stats["overflows"] += 1
+        self.x_ratio = tot / max(1, dense)  # bytes relative to dense (4-byte words both)
+        return over
+
+    def _zs_materialize_groups(self, zl, over):
+        """The paths that form the gradient from dense rows (CPU; the GPU side-stream finish, on
+        the side stream): the full [W * rows, in_f] rows in self._x_buf, each group decoded into its
+        columns -- or, after its overflow, that group's rows gathered dense."""
+        from . import distributed as tdist
+
+        rows, in_f = zl[0]["rows"], self.weight.shape[1]
+        dev = zl[0]["meta"].device
+        W = self.world
+        self._x_buf = torch.empty((W * rows, in_f), device=dev, dtype=torch.float32)
+        for z, o in zip(zl, over):
+            tmp = torch.empty((W * rows, z["k1"] - z["k0"]), device=dev, dtype=torch.float32)
+            if o:
+                z["w_vals"].wait()
+                tdist.all_gather_into_tensor(tmp, z["x_local"], group=self.group)
+            else:
+                self._zs_decode_into(z, tmp)
+            self._x_buf[:, z["k0"]:z["k1"]].copy_(tmp)
+        self._x_work = _DoneWork()
+
     def _zs_resolve(self):
         """Host side of the zero-suppressed exchange (CPU, and the GPU side-stream finish, which
         runs from an end-of-backward callback): check the counts, then set up the dense rows
@@ -549,6 +654,9 @@ class ActivationExchange:
         from . import distributed as tdist
 
         z, self._zs = self._zs, None
+        if isinstance(z, list):  # grouped activation step: check now, rebuild where the gradient is formed
+            self._zs_decode_pending = ("groups", z, self._zs_check_groups(z))
+            return
         overflow = self._zs_check(z)
         if z.get("kind") == "sharded":
             if overflow:  # some segment overflowed its slot: the dense all-to-all, once
@@ -581,6 +689,9 @@ class ActivationExchange:
         if z is None:
             return
         self._zs_decode_pending = None
+        if isinstance(z, tuple):
+            self._zs_materialize_groups(z[1], z[2])
+            return
         if self._x_buf is None:
             self._x_buf = torch.empty((self.world * z["rows"], z["in_f"]), device=z["meta"].device, dtype=torch.float32)
         self._zs_decode_into(z, self._x_buf)
@@ -590,7 +701,7 @@ class ActivationExchange:
         decoded in registers, no dense rows written and read back)?  That kernel takes N in
         {10, 16} outputs, K % 4 == 0 and 16-byte aligned rows of every tensor it writes
         (zs_exchange.hip tds_linear_dw_zs); anything else decodes and runs ``linear_dw``."""
-        if z is None or z.get("kind") == "sharded" or not z["meta"].is_cuda:
+        if not isinstance(z, dict) or z.get("kind") == "sharded" or not z["meta"].is_cuda:
             return False
         n_out, k = self.weight.shape
         if n_out not in (10, 16) or k % 4:
@@ -614,6 +725,8 @@ class ActivationExchange:
                                 scale, acc, lr)
 
     def _zs_decode_into(self, z, x_buf):
+        """Every rank's rows of one encoded tensor (a sharded step, or one activation group) into
+        x_buf [W * rows, width] (contiguous)."""
         from . import zs
 
         z["w_meta"].wait()
@@ -670,8 +783,13 @@ class ActivationExchange:
         cur = torch.cuda.current_stream(dev)
         side.wait_stream(cur)
         keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
+        keep = tuple(t for t in keep if not isinstance(t, list)) + tuple(self._x_local or ()) \
+            if isinstance(self._x_local, list) else keep
         z = getattr(self, "_zs_decode_pending", None)
-        if z is not None:
+        if isinstance(z, tuple):  # grouped activation step: every group's buffers
+            for zg in z[1]:
+                keep = keep + (zg["meta_all"], zg["vals_all"], zg["meta"], zg["vals"])
+        elif z is not None:
             if z.get("kind") == "sharded":
                 keep = keep + (z["meta_recv"], z["vals_recv"]) + z["keep"]
             else:
@@ -738,30 +856,68 @@ class ActivationExchange:
         class _Update:
             """The deferred update (param_fence.defer), queued on the current stream when called: the
             count check, then the update from the gathered encodings (or, after an overflow, from
-            this step's rows re-sent dense).  (Applying it inside the next head forward while it
-            streams the weight measured even with this separate sweep, 0.585 vs 0.570 ms, r5_s8.)"""
+            this step's rows re-sent dense).  A grouped step (a list of column groups) also runs
+            group by group: ``run_until(k)`` queues the groups that start below column k -- the fused
+            head forward calls it right before each of its range launches (``fused_kind``), so a
+            group's gathers only have to land before the launch that reads its columns.  (Applying
+            the update inside the head forward while it streams the weight measured even with this
+            separate sweep, 0.585 vs 0.570 ms, r5_s8.)"""
 
-            def __call__(self):
+            fused_kind = "groups" if isinstance(z, list) else None
+
+            def __init__(self):
+                self.over = None  # per group: did its counts overflow the capacity?
+                self.next = 0     # the next group to queue
+
+            def run_until(self, k_end):
                 from .. import _ext
 
                 torch.cuda.current_stream(dev).wait_event(ev_dy)
                 with torch.no_grad():
-                    x_buf = None
-                    if z is not None:
-                        if not ex._zs_check(z):
-                            if ex._zs_fused(z, (weight.data,)):
-                                ex._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
-                                return
-                            x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
-                            ex._zs_decode_into(z, x_buf)
-                        else:  # overflow: this step's rows, dense, from every rank
-                            z["w_vals"].wait()
-                            x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
-                            tdist.all_gather_into_tensor(x_buf, xl, group=group)
-                    else:
-                        x_work.wait()
-                        x_buf = x_dense
-                    _ext.ops().linear_dw(dy_all, x_buf, weight.data, None, scale, False, lr)
+                    if not isinstance(z, list):
+                        if self.next == 0:
+                            self.next = 1
+                            self._whole()
+                        return
+                    if self.over is None:
+                        self.over = ex._zs_check_groups(z)
+                    while self.next < len(z) and z[self.next]["k0"] < k_end:
+                        zg, o = z[self.next], self.over[self.next]
+                        self.next += 1
+                        wcols = weight.data[:, zg["k0"]:zg["k1"]]
+                        if not o and ex._zs_fused(zg, (wcols,)):
+                            ex._dw_zs(zg, dy_all, wcols, None, scale, False, lr)
+                            continue
+                        x_buf = torch.empty((world * rows, zg["k1"] - zg["k0"]), device=dev, dtype=torch.float32)
+                        if o:  # overflow: this group's rows, dense, from every rank
+                            zg["w_vals"].wait()
+                            tdist.all_gather_into_tensor(x_buf, zg["x_local"], group=group)
+                        else:
+                            ex._zs_decode_into(zg, x_buf)
+                        _ext.ops().linear_dw(dy_all, x_buf, wcols, None, scale, False, lr)
+
+            def _whole(self):
+                from .. import _ext
+
+                x_buf = None
+                if z is not None:
+                    if not ex._zs_check(z):
+                        if ex._zs_fused(z, (weight.data,)):
+                            ex._dw_zs(z, dy_all, weight.data, None, scale, False, lr)
+                            return
+                        x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
+                        ex._zs_decode_into(z, x_buf)
+                    else:  # overflow: this step's rows, dense, from every rank
+                        z["w_vals"].wait()
+                        x_buf = torch.empty((world * rows, in_f), device=dev, dtype=torch.float32)
+                        tdist.all_gather_into_tensor(x_buf, xl, group=group)
+                else:
+                    x_work.wait()
+                    x_buf = x_dense
+                _ext.ops().linear_dw(dy_all, x_buf, weight.data, None, scale, False, lr)
+
+            def __call__(self):
+                self.run_until(float("inf"))
 
         param_fence.defer(weight, _Update())
         fused_update.applied(weight)
@@ -901,3 +1057,10 @@ def _dw_rows(dy_all, x_rows, dw, db, scale: float, acc_w: bool, acc_b: bool):
     if db is not None:
         s_b = dy_all.sum(0).mul_(scale)
         db.add_(s_b) if acc_b else db.copy_(s_b)
+
+
+class _DoneWork:
+    """A finished work (the rows are already in place)."""
+
+    def wait(self):
+        return None
