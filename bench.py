@@ -103,6 +103,9 @@ def _parser():
                     help="fc gradient path under DDP (parallel/factored.py); auto picks by the xGMI byte model")
     ap.add_argument("--exchange-compress", action=argparse.BooleanOptionalAction, default=True,
                     help="send the activation exchange's fc input rows zero-suppressed (lossless, parallel/zs.py)")
+    ap.add_argument("--exchange-groups", type=int, default=None,
+                    help="column groups of the zero-suppressed activation exchange (one head launch, encode and "
+                         "gather pair each; default 4 at world > 1, 1 at world 1)
     ap.add_argument("--allreduce-chunks", type=int, default=None,
                     help="K-chunks of the fc weight gradient in the all-reduce regime (default 4 on GPU)")
     ap.add_argument("--reserve-cus", type=int, default=None,
@@ -165,8 +168,8 @@ def _parser():
     ap.add_argument("--transport-tune", action=argparse.BooleanOptionalAction, default=None,
                     help="before the model is built, time the fc exchange's collectives at each candidate "
                          "(reserve-cus, rccl-max-ctas) on the live node and take the one with the lowest predicted "
-                         "step time (parallel/transport_tune.py; config.preflight.transport).  Default: on at "
-                         "world > 1 on rccl-native unless --reserve-cus / --rccl-max-ctas is given")
+                         "step time (parallel/transport_tune.py; config.preflight.transport).  Off by default: "
+                         "its communicator re-creation crashed a one-GPU run (r6_s4), see docs/DISTRIBUTED.md")
     ap.add_argument("--store", default="native", choices=["native", "c10d"],
                     help="rendezvous store (world > 1 or a forced exchange): this package's C++ TCP store, located "
                          "through c10d's at MASTER_ADDR:MASTER_PORT (the agreed fallback), or c10d's only; "
@@ -222,6 +225,7 @@ def _spawn_ranks(args, argv) -> int:
         # the plain bucket all-reduce
         plans.append((list(argv) + ["--backend", "rccl", "--reserve-cus", "0", "--fallback"], "retry"))
     fail = None
+    port_retried = False
     for k, (av, label) in enumerate(plans):
         remaining = args.spawn_timeout - (time.time() - _T_START)
         if k > 0 and remaining < 90:
@@ -245,6 +249,12 @@ def _spawn_ranks(args, argv) -> int:
             print(f"bench.py: spawn attempt {k} failed: rank {fail[0]}: {fail[1]}", file=sys.stderr, flush=True)
             if printed:  # rank 0 already printed the measurement; the failure came after it (teardown)
                 return 0
+            if "address already in use" in str(fail[1]).lower() and not port_retried:
+                # the rendezvous port was taken between its probe and the store's bind: the same
+                # plan once more on a fresh port
+                port_retried = True
+                plans.insert(k + 1, (av, label))
+                os.environ.pop("MASTER_PORT", None)
     print(json.dumps(_fail_record(args, args.gpus, fail[0], fail[1], fail[2],
                                   {"spawn_attempts": len(plans) if fallback and args.device == "cuda" else 1})),
           flush=True)
@@ -433,10 +443,7 @@ def _run_attempts(args, world: int, rank: int, phase):
     # ranks can still agree on the fallback and report
     os.environ.setdefault("TDS_RCCL_ERROR_HANDLING", "raise")
     os.environ.setdefault("TDS_RCCL_INIT_TIMEOUT_MS", str(int(args.pg_timeout * 1000)))
-    tune = args.transport_tune
-    if tune is None:
-        tune = (world > 1 and on_gpu and backend == "rccl-native" and args.reserve_cus is None
-                and not args.rccl_max_ctas)
+    tune = bool(args.transport_tune)
     transport = None
     if tune and backend == "rccl-native" and on_gpu and store is not None:
         phase[0] = "transport tune"
@@ -684,7 +691,8 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     optimizer = SGD(model.parameters(), args.lr)
     ddp = DistributedDataParallel(model, device_ids=[local_rank] if on_gpu else None, bucket_cap_mb=args.bucket_mb,
                                   grad_exchange=grad_exchange, overlap_optimizer=args.overlap_optimizer,
-                                  allreduce_chunks=args.allreduce_chunks, exchange_compress=args.exchange_compress)
+                                  allreduce_chunks=args.allreduce_chunks, exchange_compress=args.exchange_compress,
+                                  exchange_groups=args.exchange_groups)
 
     ddp.attach_optimizer(optimizer)
 

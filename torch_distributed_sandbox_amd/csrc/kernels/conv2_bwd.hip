@@ -103,12 +103,14 @@ __device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k,
 struct BRArgs {
   const uint2* __restrict__ y2;  // y2h [B][P][P][32] fp16 (conv2_common.h)
   const uint32_t* __restrict__ a2;  // the forward's pooling argmax codes [B][Q][Q][2] (conv2_common.h)
-  const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
+  const float* __restrict__ g2m;  // [B][32][G] row-shifted pooled-blocked (pooled_layout.h G2MGeom)
   const uint4* __restrict__ p1;
   uint2* __restrict__ dp1;  // dp1h (conv2_common.h)
   float* __restrict__ slab;
   const int* __restrict__ walk;
   int B, P, Q, sk, w;
+  int gNR, gQ8;  // g2m's block rows / columns per plane (G2MGeom)
+  int64_t gG;    // g2m floats per (image, channel) plane
 };
 
 // ---------------------------------------------------------------------------- dgrad
@@ -407,14 +409,15 @@ __device__ __forceinline__ BRY br_load_y(__amdgpu_buffer_rsrc_t r, uint32_t off)
 }
 
 // GB (the pipelined 8-row sets): the tile's pooled gradient g2m is not gathered per item (BR_CW
-// 4-B loads from as many channel planes) but per RUN -- one (channel, pooled row) of the tile's 10
-// pooled columns, on staging lanes 128-255: a 4-B load of the left halo column, two 16-B loads of
-// the 8 columns of the tile, a 4-B load of the right halo -- and passed to the items through an LDS
-// tile ([pooled row][col][channel]: two 16-B reads per item) written one tile ahead (put_runs).
-// Per tile 8 load instructions instead of 20 (r5_s14: the texture path, ~64 cycles per staging
-// load instruction, is the staging's limiter).  Mid loads past a row's end read the next row or,
-// for the tensor's last row, the 64 B of slack every g2m allocation carries (fused_ops.cpp): those
-// columns are never pooled.
+// 4-B loads from as many channel planes) but per channel BLOCK: g2m is row-shifted pooled-blocked
+// (pooled_layout.h G2MGeom), so the tile's 4 pooled rows x 8 pooled columns of a channel are one
+// 128-B block -- every staging lane loads one 16-B piece of it (8 lanes per channel, a wave-
+// instruction 8 full lines) and one halo value (the column left / right of the block, from the
+// blocks beside it) -- and passed to the items through an LDS tile ([pooled row][col][channel]:
+// two 16-B reads per item) written one tile ahead (put_runs).  (Round 5 took (channel, pooled row)
+// runs of the planar g2m: 4 loads on each of 128 lanes, every lane on lines of its own -- at ~2
+// texture-path cycles per distinct line a wave-instruction touches, profiles/micro/
+// r6_s3_ta_pattern.txt, ~460 ns a tile against ~90 now.)
 template <int NR, bool BIG, int DIAG, bool GB = false>
 struct BRStager {
   static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
@@ -426,8 +429,8 @@ struct BRStager {
   float gv[IPER][BR_CW];
   uint32_t av[IPER];    // a2: the window's argmax codes, 16 channels
   uint4 pr[PPER];
-  float4 rm0, rm1;      // GB: this lane's run, columns 1-4 and 5-8
-  float rl, rr;         // GB: its columns 0 and 9 (the halo)
+  float4 gi4;           // GB: this lane's 16-B piece of its channel's block (row s / 2, columns 4 (s % 2) ..)
+  float gh;             // GB: its halo value (left (s < 4) / right block, row s % 4)
 
   // the j-th p1 piece of staging lane tid: the set past 256 goes to a wave without an item (waves
   // 4-6 hold the 160 items, the extra pieces go to wave 7)
@@ -468,30 +471,30 @@ struct BRStager {
         tds_buffer_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + R0) * P + (c0 - 2)) * 64, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t rp =
         tds_buffer_rsrc(reinterpret_cast<const char*>(a.p1) + ((img + R0) * P + (c0 - 2)) * 32, 0xFFFFFFF0u);
-    const int64_t gplane = (int64_t)Q * Q;
+    const int64_t gG = a.gG;
     const int py0 = R0 / 2, px0 = c0 / 2 - 1;
-    const __amdgpu_buffer_rsrc_t rg =
-        tds_buffer_rsrc(a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0, 0xFFFFFFF0u);
+    const float* gimg = a.g2m + (int64_t)b * 32 * gG;  // this image's 32 g2m planes
+    const __amdgpu_buffer_rsrc_t rg = tds_buffer_rsrc(gimg, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t ra = tds_buffer_rsrc(a.a2 + (((int64_t)b * Q + py0) * Q + px0) * 2, 0xFFFFFFF0u);
     if constexpr (GB) {
-      // the runs first: put_runs waits for them one tile before the rest of this set is needed
-      const int rt = tid - 128;  // lanes 128-255: channel rt & 31, pooled row rt >> 5
-      const int c = rt & 31, wy = (rt >> 5) & 3;
-      const bool row = (rt >= 0) & ((uint32_t)(py0 + wy) < (uint32_t)Q);
-      const bool lok = row & (px0 >= 0), rok = row & (px0 + 9 < Q);
-      const int64_t e0 = (int64_t)c * gplane + (int64_t)wy * Q;  // element of column 0, from rg's base
+      // the blocks first: put_runs waits for them one tile before the rest of this set is needed.
+      // Lane tid: channel c = tid / 8, s = tid % 8 -- piece s of block (R, tc) (row s / 2, columns
+      // 4 (s % 2) .. +3) and the halo value of row s % 4 from block tc - 1 (column 7, s < 4) or
+      // tc + 1 (column 0).  R = (py0 + 3) / 4 holds exactly pooled rows py0 .. py0 + 3 (py0 = R0 / 2
+      // = 4 tr + 1); blocks past the plane read zeros.
+      const int c = tid >> 3, sl = tid & 7;
+      const int R = (py0 + 3) >> 2, tc = (px0 + 1) >> 3;
+      const int hb = tc - 1 + 2 * (sl >> 2);
+      const bool rv = R < a.gNR;
+      const bool hv = rv & ((uint32_t)hb < (uint32_t)a.gQ8);
+      const int64_t ei = (int64_t)c * gG + ((int64_t)R * a.gQ8 + tc) * 32 + 4 * sl;
+      const int64_t eh = (int64_t)c * gG + ((int64_t)R * a.gQ8 + hb) * 32 + (sl & 3) * 8 + ((sl >> 2) ? 0 : 7);
       if constexpr (!BIG) {
-        const uint32_t o = (uint32_t)(e0 * 4);
-        rl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lok ? o : kBROob, 0, 0));
-        rm0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 4 : kBROob, 0, 0));
-        rm1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 20 : kBROob, 0, 0));
-        rr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, rok ? o + 36 : kBROob, 0, 0));
-      } else {
-        const float* gp = a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0 + (row ? e0 : 0);
-        rl = lok ? gp[0] : 0.f;  // (BIG: 64-bit loads; the rare >4 GiB-per-image shapes)
-        rm0 = *reinterpret_cast<const float4*>(gp + 1);
-        rm1 = *reinterpret_cast<const float4*>(gp + 5);
-        rr = rok ? gp[9] : 0.f;
+        gi4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, rv ? (uint32_t)(ei * 4) : kBROob, 0, 0));
+        gh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, hv ? (uint32_t)(eh * 4) : kBROob, 0, 0));
+      } else {  // (BIG: 64-bit loads; the rare >4 GiB-per-image shapes)
+        gi4 = rv ? *reinterpret_cast<const float4*>(gimg + ei) : make_float4(0.f, 0.f, 0.f, 0.f);
+        gh = hv ? gimg[eh] : 0.f;
       }
     }
     const int cb = (tid % BR_NCH) * BR_CW;  // the chunk's first channel (256 % BR_NCH == 0: every u)
@@ -514,17 +517,21 @@ struct BRStager {
       av[u] = __builtin_amdgcn_raw_buffer_load_b32(ra, pooled ? (uint32_t)(((wy * Q + wx) * 2 + (cb >> 4)) * 4) : kBROob, 0, 0);
       if constexpr (GB) {
         // (from the LDS tile in store())
-      } else if constexpr (!BIG) {
-        const uint32_t og = (uint32_t)(((int64_t)cb * gplane + (int64_t)wy * Q + wx) * 4);
-        const uint32_t gstep = (uint32_t)(gplane * 4);
-#pragma unroll
-        for (int k = 0; k < BR_CW; ++k)
-          gv[u][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
-                                                                                    0, 0));
       } else {
-        const float* gp = a.g2m + ((int64_t)b * 32 + cb) * gplane + (int64_t)(pooled ? py : 0) * Q + (pooled ? px : 0);
+        // (window (py, px) of channels cb .. cb+7: element (py, px) of 8 planes, G2MGeom)
+        const int pyc = pooled ? py : 0, pxc = pooled ? px : 0;
+        const int64_t eg = (int64_t)cb * gG + ((int64_t)((pyc + 3) >> 2) * a.gQ8 + (pxc >> 3)) * 32 + ((pyc + 3) & 3) * 8 +
+                           (pxc & 7);
+        if constexpr (!BIG) {
+          const uint32_t og = (uint32_t)(eg * 4), gstep = (uint32_t)(gG * 4);
 #pragma unroll
-        for (int k = 0; k < BR_CW; ++k) gv[u][k] = gp[k * gplane];  // masked at use (store: pooled)
+          for (int k = 0; k < BR_CW; ++k)
+            gv[u][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
+                                                                                      0, 0));
+        } else {
+#pragma unroll
+          for (int k = 0; k < BR_CW; ++k) gv[u][k] = gimg[eg + k * gG];  // masked at use (store: pooled)
+        }
       }
     }
 #pragma unroll
@@ -539,17 +546,17 @@ struct BRStager {
     }
   }
 
-  // GB: this set's runs into the LDS tile gb ([pooled row][col][channel])
+  // GB: this set's block pieces and halo values into the LDS tile gb ([pooled row][col 10][channel]:
+  // column 0 the left halo, 1..8 the block, 9 the right halo)
   __device__ __forceinline__ void put_runs(float* gb, int tid) const {
-    static_assert(GB, "runs only in the pipelined sets");
-    const int rt = tid - 128;
-    if (rt < 0) return;
-    const int c = rt & 31, wy = rt >> 5;
-    float* d = gb + wy * 10 * 32 + c;
-    d[0] = rl;
-    d[32] = rm0.x; d[64] = rm0.y; d[96] = rm0.z; d[128] = rm0.w;
-    d[160] = rm1.x; d[192] = rm1.y; d[224] = rm1.z; d[256] = rm1.w;
-    d[288] = rr;
+    static_assert(GB, "block pieces only in the pipelined sets");
+    const int c = tid >> 3, sl = tid & 7, r = sl >> 1, h = sl & 1;
+    float* d = gb + (r * 10 + 1 + 4 * h) * 32 + c;
+    d[0] = gi4.x;
+    d[32] = gi4.y;
+    d[64] = gi4.z;
+    d[96] = gi4.w;
+    gb[((sl & 3) * 10 + ((sl >> 2) ? 9 : 0)) * 32 + c] = gh;
   }
 
   // BN2 / ReLU / pool backward of the staged windows -> dy2 rows at dbase; p1 -> pbase;
@@ -807,6 +814,12 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
   BRArgs a;
   a.y2 = y2; a.a2 = a2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.walk = walk;
   a.B = B; a.P = P; a.Q = P / 2;
+  {
+    const G2MGeom gg = g2m_geom(P / 2);
+    a.gNR = gg.NR;
+    a.gQ8 = gg.Q8;
+    a.gG = gg.plane();
+  }
   a.sk = sk;
   a.w = xcd_remap(blockIdx.x, gridDim.x);  // this workgroup's list (XCD-contiguous: neighbouring columns)
   a.walk = walk + a.w * sw;
@@ -964,14 +977,14 @@ static int br_diag_env() {
 static int br_diag_env() { return 0; }
 #endif
 
-// g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
+// g2m: [B][32][G] (pooled_layout.h G2MGeom); walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
 // [nwg][rows] (fused_ops.cpp bwd_walk)
 void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const float* aff2, const float* kbuf,
                     const float* b2,
                     uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st) {
   const int Q = P / 2;
-  const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
+  const bool big = (int64_t)32 * g2m_geom(Q).plane() * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
 #define TDS_BR_LAUNCH_B(D, BG)                                                                                         \
   {                                                                                                                    \
     static bool set = false;                                                                                           \

@@ -323,7 +323,7 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const double* __restri
 }
 
 // Backward for images b0 .. b0+NB-1.
-//   g2m[b][c][py][px] = (sum_j dl[b][j] W[j][c][py][px]) * [a*ya + b > 0]   (planar [B][32][Q][Q])
+//   g2m[b][c][py][px] = (sum_j dl[b][j] W[j][c][py][px]) * [a*ya + b > 0]   ([B][32][G], G2MGeom)
 //   partial[c][pass*nblk + blk][2] = { sum g2m, sum g2m * ya }       (BN2 backward sums)
 //   dW[j][c][pos] (= or +=) scale * sum_b dl[b][j] X[b][c][pos]      (WITH_DW; ACC adds)
 //   Wupd = W - lr * dW                                               (UPD: SGD step fused)
@@ -374,6 +374,7 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   const float a = aff2[c], bb = aff2[32 + c];
   const int Q = g.Q;
   const int64_t plane = g.plane();
+  const G2MGeom gg = g2m_geom(Q);
   float sdz = 0.f, sdy = 0.f;
   uint32_t gmx = 0u;  // max |g2m| bits
   const int nch = (g.Q8 + 31) / 32;
@@ -413,8 +414,11 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
         sdz += gm[k];
         sdy = fmaf(gm[k], ok ? yy[k] : 0.f, sdy);
       }
-      // planar, like a weight plane
-      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]), true);
+      // row-shifted pooled-blocked (pooled_layout.h G2MGeom): the lane's 4 columns are one 16-B
+      // piece of a block (columns past Q as 0); rows past Q are not stored
+      if (rok)
+        st_stream(reinterpret_cast<float4*>(g2m + gg.index(b0 + b, c, py, px0)),
+                  make_float4(gm[0], gm[1], gm[2], gm[3]));
     }
     if constexpr (WITH_DW) {
       const HPRow& rw = rwg;
@@ -536,6 +540,7 @@ using namespace tds;
 int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // forward workgroups per channel
 int tds_head_bwd_pb_nblk(int Q) { return hp_grid_b(pb_geom(Q)).per_channel(); }  // backward workgroups per channel
 int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
+int64_t tds_g2m_plane(int Q) { return g2m_geom(Q).plane(); }
 
 // partial: double [32 * nblk + 32][B*NC] (the last 32 rows: the in-launch finalizer's channel sums);
 // sums: double [B*NC].  fused_fin = false: the separate head_logits launch (the A/B reference).
