@@ -105,7 +105,7 @@ def _parser():
                     help="send the activation exchange's fc input rows zero-suppressed (lossless, parallel/zs.py)")
     ap.add_argument("--exchange-groups", type=int, default=None,
                     help="column groups of the zero-suppressed activation exchange (one head launch, encode and "
-                         "gather pair each; default 4 at world > 1, 1 at world 1)
+                         "gather pair each; default 4 at world > 1, 1 at world 1)")
     ap.add_argument("--allreduce-chunks", type=int, default=None,
                     help="K-chunks of the fc weight gradient in the all-reduce regime (default 4 on GPU)")
     ap.add_argument("--reserve-cus", type=int, default=None,
@@ -538,8 +538,8 @@ def _tune_transport(args, store, rank: int, world: int) -> dict:
                                      store=dist.PrefixStore(f"tune{i}", store),
                                      timeout=datetime.timedelta(seconds=args.pg_timeout), device_id=local_rank,
                                      comm_cus=cfg.reserve_cus)
+            issue = []
             try:
-                issue = []
                 for kind, nbytes in colls:
                     n = max(1, nbytes // 4)
                     if kind == "all_gather":
@@ -567,8 +567,21 @@ def _tune_transport(args, store, rank: int, world: int) -> dict:
                     best = dt if best is None else min(best, dt)
                 g = torch.tensor([best], device=dev, dtype=torch.float64)
                 tdist.all_reduce(g, tdist.ReduceOp.MAX)
-                return float(g.item()) * 1e3
+                res_ms = float(g.item()) * 1e3
+                del g
+                return res_ms
             finally:
+                # the probe's buffers were used on the communicator's CU-masked stream: free them
+                # (the caching allocator records an event on every stream a block was used on)
+                # while that stream exists -- after the teardown releases it, that free is a
+                # use-after-free of the stream (r6_s4: a segfault in the second candidate)
+                issue.clear()
+                inp = out = sb = rb = t = None  # noqa: F841 -- (the loop's last buffers)
+                torch.cuda.synchronize(dev)
+                import gc
+
+                gc.collect()
+                torch.cuda.empty_cache()
                 _teardown(abort=False)
         finally:
             if saved is None:
