@@ -274,7 +274,7 @@ def test_bench_fallback_tiers_keep_the_exchange_cpu(world, phase):
     ops = [x["op"] for x in pf["collectives"]]
     assert "BN buffer broadcast (coalesced)" in ops and ops[-1] == "barrier"
     if world == 2:
-        assert "zs values all-gather (first-step capacity)" in ops
+        assert any(o.startswith("zs values all-gather") and o.endswith("(first-step capacity)") for o in ops)
     else:
         assert "X column-shard exchange (per peer)" in ops and "updated W shard exchange (per peer)" in ops
     assert all(x["ms"] >= 0 for x in pf["collectives"])

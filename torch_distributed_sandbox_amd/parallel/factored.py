@@ -314,11 +314,13 @@ class ActivationExchange:
         zs_ok = self.compress and n < (1 << 31)
         if path == "activations":
             if zs_ok:
-                for gi, (k0, k1) in enumerate(self.column_groups(in_f, self._planes_hint)):
+                groups = self.column_groups(in_f, self._planes_hint)
+                for gi, (k0, k1) in enumerate(groups):
                     ng = rows * (k1 - k0)
-                    gather(f"zs records all-gather, group {gi} (int32)", _meta_row(zs.meta_numel(ng)), torch.int32)
+                    tag = f", group {gi}" if len(groups) > 1 else ""
+                    gather(f"zs records all-gather{tag} (int32)", _meta_row(zs.meta_numel(ng)), torch.int32)
                     cap = self._cap.get(("activations", gi))
-                    gather(f"zs values all-gather, group {gi} (first-step capacity)", min(ng, cap) if cap else ng,
+                    gather(f"zs values all-gather{tag} (first-step capacity)", min(ng, cap) if cap else ng,
                            torch.float32)
             else:
                 gather("activation rows all-gather", n, torch.float32)
