@@ -407,7 +407,12 @@ def _make_store(args, rank: int, world: int):
     from torch_distributed_sandbox_amd.parallel.store import rendezvous
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    os.environ.setdefault("MASTER_PORT", "29533")
+    if "MASTER_PORT" not in os.environ:
+        # one process (a forced exchange at world 1): nobody else needs to agree on the port, so a
+        # free one -- a fixed default collided with the previous run's socket (EADDRINUSE, r6_s4)
+        from torch_distributed_sandbox_amd.parallel import launch
+
+        os.environ["MASTER_PORT"] = launch.find_free_port(os.environ["MASTER_ADDR"]) if world == 1 else "29533"
     store, kind = rendezvous(rank, world, timeout=datetime.timedelta(seconds=args.pg_timeout),
                              prefer=os.environ.get("TDS_STORE") or args.store)
     return store, kind, getattr(store, "_locator", store)
@@ -576,7 +581,9 @@ def _tune_transport(args, store, rank: int, world: int) -> dict:
                 # while that stream exists -- after the teardown releases it, that free is a
                 # use-after-free of the stream (r6_s4: a segfault in the second candidate)
                 issue.clear()
-                inp = out = sb = rb = t = None  # noqa: F841 -- (the loop's last buffers)
+                # (the loop's last buffers, and the last issued lambda's defaults: r6_s5's faulthandler
+                # trace put the crash at measure()'s return, where those locals are freed)
+                inp = out = sb = rb = t = f = None  # noqa: F841
                 torch.cuda.synchronize(dev)
                 import gc
 
