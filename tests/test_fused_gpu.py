@@ -376,10 +376,7 @@ def test_head_forward_backward(gpu, P, B):
     ypart(mag)[5, 3] = torch.tensor(2.5).view(torch.int32)  # a forward part: reduced per channel
     dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, True,
                                                              mag=mag)
-    from torch_distributed_sandbox_amd.ops.layouts import g2m_plane, g2m_to_planar
-
-    assert g2m.shape == (B, 32, g2m_plane(Q))  # row-shifted pooled-blocked (kernels/pooled_layout.h G2MGeom)
-    g2m_blk, g2m = g2m, g2m_to_planar(g2m, Q)
+    assert g2m.shape == (B, 32, Q, Q)
     assert mag_floats(mag)[32].item() == g2m.abs().max().item()  # max |g2m|: the conv2 backward's bound
     want = torch.zeros(32, device=gpu)
     want[5] = 2.5
@@ -392,8 +389,7 @@ def test_head_forward_backward(gpu, P, B):
     _check(g2m, pz.grad * mask, 1e-5, "g2m")
     # no-dW form (activation exchange) leaves the same g2m / BN2 gradients
     _, _, dg2b, dbe2b, g2mb, kbufb = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, False)
-    assert torch.equal(g2m_to_planar(g2mb, Q), g2m) and torch.equal(kbufb, kbuf) and torch.equal(dg2b, dg2)
-    del g2m_blk
+    assert torch.equal(g2mb, g2m) and torch.equal(kbufb, kbuf) and torch.equal(dg2b, dg2)
     if B <= 8:
         # SGD step fused into the backward: W <- W - lr dW (in place), dW still written
         w0 = wfc.clone()

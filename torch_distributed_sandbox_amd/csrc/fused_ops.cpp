@@ -5,7 +5,7 @@
 //               [B,P,P,16] travels to the layer-1 backward beside autograd, models/convnet_fused.py)
 //   y2          [B,P,P,32] f32
 //   ya          [B,32,PB] f32: pooled-blocked planes (kernels/pooled_layout.h)
-//   g2m         [B,32,G] f32: row-shifted pooled-blocked planes (kernels/pooled_layout.h G2MGeom)
+//   g2m         [B,32,Q,Q] f32: planar pooled gradient
 //   mag         int32 workspace [mag_numel(B, P)]: the step's magnitude bounds (float bits) behind
 //               the conv2 backward's fp16 gradient scale -- [0,32) max |y2 - b2| per channel, [32]
 //               max |g2m|, then per-workgroup maxima from the conv2 forward (ypart [32][nwg])
@@ -144,6 +144,7 @@ const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg
 int64_t pb_plane(int64_t P) { return tds_pb_plane((int)(P / 2)); }
 
 // ---------------------------------------------------------------- the step's magnitude-bound workspace
+constexpr int64_t kG2mSlack = 16;   // floats past g2m's end its allocations carry (conv2_bwd.hip GB runs)
 constexpr int64_t kMagParts = 64;   // ypart offset in the mag workspace
 constexpr int64_t kMagScales = 40;  // conv2 epilogue scales (csrc/kernels/conv2_common.h)
 int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
@@ -681,13 +682,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
               "fused_head_backward: update_lr needs compute_dw and a batch of <= 8 images");
   Tensor g2m;
   if (g2m_out.has_value() && g2m_out->defined()) {
-    need(*g2m_out, at::kFloat, {B, 32, tds_g2m_plane((int)Q)}, "g2m_out");
+    need(*g2m_out, at::kFloat, {B, 32, Q, Q}, "g2m_out");
     g2m = *g2m_out;
   } else {
     TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into g2m_out");
     // planar (the fc flatten order), with the 64 B of slack the conv2 backward's row loads may
     // touch past the last row (conv2_bwd.hip BRStager GB)
-    g2m = at::empty({B, 32, tds_g2m_plane((int)Q)}, ya.options());
+    g2m = at::empty({B * 32 * Q * Q + kG2mSlack}, ya.options()).narrow(0, 0, B * 32 * Q * Q).view({B, 32, Q, Q});
   }
   const int nblk = tds_head_bwd_pb_nblk((int)Q), npass = tds_head_bwd_pb_npass((int)B);
   Tensor partial;
@@ -764,7 +765,10 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   need(y2, at::kHalf, {B, P, P, 32}, "y2h (fused_conv2_forward's)");
   need(a2, at::kInt, {B, P / 2, P / 2, 2}, "a2 (fused_conv2_forward's pooling argmax codes)");
   need(b2, at::kFloat, {32}, "conv2.bias");
-  need(g2m, at::kFloat, {B, 32, tds_g2m_plane((int)(P / 2))}, "g2m (fused_head_backward's, G2MGeom)");
+  need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
+  TORCH_CHECK((int64_t)g2m.storage().nbytes() >= (g2m.storage_offset() + g2m.numel() + kG2mSlack) * 4,
+              "fused_conv2_backward_y2: g2m needs ", kG2mSlack, " floats of slack after it (as fused_head_backward "
+              "allocates it): the staging's row loads may read past the last row");
   need(aff2, at::kFloat, {64}, "aff2");
   need(kbuf, at::kFloat, {96}, "kbuf");
   need(wd, at::kShort, {25 * 4 * 16 * 8}, "conv2 dgrad pack");

@@ -103,14 +103,12 @@ __device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k,
 struct BRArgs {
   const uint2* __restrict__ y2;  // y2h [B][P][P][32] fp16 (conv2_common.h)
   const uint32_t* __restrict__ a2;  // the forward's pooling argmax codes [B][Q][Q][2] (conv2_common.h)
-  const float* __restrict__ g2m;  // [B][32][G] row-shifted pooled-blocked (pooled_layout.h G2MGeom)
+  const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
   const uint4* __restrict__ p1;
   uint2* __restrict__ dp1;  // dp1h (conv2_common.h)
   float* __restrict__ slab;
   const int* __restrict__ walk;
   int B, P, Q, sk, w;
-  int gNR, gQ8;  // g2m's block rows / columns per plane (G2MGeom)
-  int64_t gG;    // g2m floats per (image, channel) plane
 };
 
 // ---------------------------------------------------------------------------- dgrad
@@ -409,51 +407,34 @@ __device__ __forceinline__ BRY br_load_y(__amdgpu_buffer_rsrc_t r, uint32_t off)
 }
 
 // GB (the pipelined 8-row sets): the tile's pooled gradient g2m is not gathered per item (BR_CW
-// 4-B loads from as many channel planes) but per channel BLOCK: g2m is row-shifted pooled-blocked
-// (pooled_layout.h G2MGeom), so the tile's 4 pooled rows x 8 pooled columns of a channel are one
-// 128-B block -- every staging lane loads one 16-B piece of it (8 lanes per channel, a wave-
-// instruction 8 full lines) and one halo value (the column left / right of the block, from the
-// blocks beside it) -- and passed to the items through an LDS tile ([pooled row][col][channel]:
-// two 16-B reads per item) written one tile ahead (put_runs).  (Round 5 took (channel, pooled row)
-// runs of the planar g2m: 4 loads on each of 128 lanes, every lane on lines of its own -- at ~2
-// texture-path cycles per distinct line a wave-instruction touches, profiles/micro/
-// r6_s3_ta_pattern.txt, ~460 ns a tile against ~90 now.)
+// 4-B loads from as many channel planes) but per RUN -- one (channel, pooled row) of the tile's 10
+// pooled columns, on staging lanes 128-255: a 4-B load of the left halo column, two 16-B loads of
+// the 8 columns of the tile, a 4-B load of the right halo -- and passed to the items through an LDS
+// tile ([pooled row][col][channel]: two 16-B reads per item) written one tile ahead (put_runs).
+// Per tile 8 load instructions instead of 20 (r5_s14: the texture path, ~64 cycles per staging
+// load instruction, is the staging's limiter).  Mid loads past a row's end read the next row or,
+// for the tensor's last row, the 64 B of slack every g2m allocation carries (fused_ops.cpp): those
+// columns are never pooled.
 template <int NR, bool BIG, int DIAG, bool GB = false>
 struct BRStager {
-  // HALF-ITEMS: (window, 8-channel chunk, window column j): the two pixels (rows 0 and 1) of one
-  // column of a pooling window, 8 channels.  Lane order h = (window * 2 + j) * 4 + chunk, so the 8
-  // lanes of a window cover both its pixels' 64-B records of a row -- one full 128-B line -- and a
-  // wave's y2h load instruction 8 lines (round 5's (window, chunk) items put every instruction on
-  // 16 half-used lines: ~2x the texture-path time, profiles/micro/r6_s3_ta_pattern.txt).  A half-item
-  // needs only its own pixels, the window's argmax code and its pooled gradient.  The 320 of an 8-row
-  // set are one per staging lane plus 16 more per wave (every wave the same VALU share; round 5's
-  // 160 items sat on waves 4-6 only).
   static constexpr int NWIN = (NR / 2) * (BR_SC / 2);
-  static constexpr int HITEMS = NWIN * BR_NCH * 2;
-  static constexpr int HPER = HITEMS > 256 ? 2 : 1;
-  static_assert(HITEMS <= 256 + 4 * 16, "half-items: one per lane + 16 per wave at most");
+  static constexpr int ITEMS = NWIN * BR_NCH;
+  static constexpr int IPER = (ITEMS + 255) / 256;
   static constexpr int PIECES = NR * BR_SC * 2;  // 16-B p1 pieces (32-B fp16 records)
-  static constexpr int PPER = PIECES > 256 ? 2 : 1;
-  static_assert(PIECES <= 256 + 4 * 16, "p1 pieces: one per lane + 16 per wave at most");
-  BRY yv[HPER][2];      // y2h: BR_CW channels of the half-item's two pixels (window rows 0, 1)
-  float gv[HPER][BR_CW];
-  uint32_t av[HPER];    // a2: the window's argmax codes, 16 channels
+  static constexpr int PPER = (PIECES + 255) / 256;
+  BRY yv[IPER][4];      // y2h: BR_CW channels of each pixel of the window
+  float gv[IPER][BR_CW];
+  uint32_t av[IPER];    // a2: the window's argmax codes, 16 channels
   uint4 pr[PPER];
-  float4 gi4;           // GB: this lane's 16-B piece of its channel's block (row s / 2, columns 4 (s % 2) ..)
-  float gh;             // GB: its halo value (left (s < 4) / right block, row s % 4)
+  float4 rm0, rm1;      // GB: this lane's run, columns 1-4 and 5-8
+  float rl, rr;         // GB: its columns 0 and 9 (the halo)
 
-  // the u-th of a lane's (half-items / pieces): one per lane, then 16 per wave (lanes 0-15)
-  __device__ __forceinline__ static int slot(int tid, int u) {
-    return u == 0 ? tid : ((tid & 63) < 16 ? 256 + (tid >> 6) * 16 + (tid & 63) : 1 << 20);
-  }
-  __device__ __forceinline__ static int piece(int tid, int u) { return slot(tid, u); }
+  // the j-th p1 piece of staging lane tid: the set past 256 goes to a wave without an item (waves
+  // 4-6 hold the 160 items, the extra pieces go to wave 7)
+  __device__ __forceinline__ static int piece(int tid, int j) { return (j == 1 ? ((tid + 64) & 255) : tid) + 256 * j; }
 
-  // half-item h -> window row / column, window column j, chunk's first channel
-  __device__ __forceinline__ static void hitem_geom(int h, int& wy, int& wx, int& j, int& cb) {
-    const int hc = h < HITEMS ? h : 0;
-    cb = (hc & 3) * BR_CW;
-    j = (hc >> 2) & 1;
-    const int w = hc >> 3;
+  __device__ __forceinline__ static void item_geom(int it, int& wy, int& wx) {
+    const int w = (it < ITEMS ? it : 0) / BR_NCH;
     wy = w / (BR_SC / 2);
     wx = w - wy * (BR_SC / 2);
   }
@@ -468,16 +449,15 @@ struct BRStager {
   __device__ __forceinline__ void load(const BRArgs& a, int b, int R0, int c0, int tid) {
     if constexpr (br_no_gload(DIAG)) {
 #pragma unroll
-      for (int u = 0; u < HPER; ++u) {
+      for (int u = 0; u < IPER; ++u) {
 #pragma unroll
         for (int k = 0; k < BR_CW; ++k) gv[u][k] = 0.f;
         av[u] = 0u;
-        yv[u][0] = yv[u][1] = BRY{};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) yv[u][q] = BRY{};
       }
 #pragma unroll
-      for (int u = 0; u < PPER; ++u) pr[u] = make_uint4(0u, 0u, 0u, 0u);
-      gi4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      gh = 0.f;
+      for (int j = 0; j < PPER; ++j) pr[j] = make_uint4(0u, 0u, 0u, 0u);
       return;
     }
     const int P = a.P, Q = a.Q;
@@ -488,91 +468,88 @@ struct BRStager {
         tds_buffer_rsrc(reinterpret_cast<const char*>(a.y2) + ((img + R0) * P + (c0 - 2)) * 64, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t rp =
         tds_buffer_rsrc(reinterpret_cast<const char*>(a.p1) + ((img + R0) * P + (c0 - 2)) * 32, 0xFFFFFFF0u);
-    const int64_t gG = a.gG;
+    const int64_t gplane = (int64_t)Q * Q;
     const int py0 = R0 / 2, px0 = c0 / 2 - 1;
-    const float* gimg = a.g2m + (int64_t)b * 32 * gG;  // this image's 32 g2m planes
-    const __amdgpu_buffer_rsrc_t rg = tds_buffer_rsrc(gimg, 0xFFFFFFF0u);
+    const __amdgpu_buffer_rsrc_t rg =
+        tds_buffer_rsrc(a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0, 0xFFFFFFF0u);
     const __amdgpu_buffer_rsrc_t ra = tds_buffer_rsrc(a.a2 + (((int64_t)b * Q + py0) * Q + px0) * 2, 0xFFFFFFF0u);
     if constexpr (GB) {
-      // the blocks first: put_runs waits for them one tile before the rest of this set is needed.
-      // Lane tid: channel c = tid / 8, s = tid % 8 -- piece s of block (R, tc) (row s / 2, columns
-      // 4 (s % 2) .. +3) and the halo value of row s % 4 from block tc - 1 (column 7, s < 4) or
-      // tc + 1 (column 0).  R = (py0 + 3) / 4 holds exactly pooled rows py0 .. py0 + 3 (py0 = R0 / 2
-      // = 4 tr + 1); blocks past the plane read zeros.
-      const int c = tid >> 3, sl = tid & 7;
-      const int R = (py0 + 3) >> 2, tc = (px0 + 1) >> 3;
-      const int hb = tc - 1 + 2 * (sl >> 2);
-      const bool rv = R < a.gNR;
-      const bool hv = rv & ((uint32_t)hb < (uint32_t)a.gQ8);
-      const int64_t ei = (int64_t)c * gG + ((int64_t)R * a.gQ8 + tc) * 32 + 4 * sl;
-      const int64_t eh = (int64_t)c * gG + ((int64_t)R * a.gQ8 + hb) * 32 + (sl & 3) * 8 + ((sl >> 2) ? 0 : 7);
+      // the runs first: put_runs waits for them one tile before the rest of this set is needed
+      const int rt = tid - 128;  // lanes 128-255: channel rt & 31, pooled row rt >> 5
+      const int c = rt & 31, wy = (rt >> 5) & 3;
+      const bool row = (rt >= 0) & ((uint32_t)(py0 + wy) < (uint32_t)Q);
+      const bool lok = row & (px0 >= 0), rok = row & (px0 + 9 < Q);
+      const int64_t e0 = (int64_t)c * gplane + (int64_t)wy * Q;  // element of column 0, from rg's base
       if constexpr (!BIG) {
-        gi4 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, rv ? (uint32_t)(ei * 4) : kBROob, 0, 0));
-        gh = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, hv ? (uint32_t)(eh * 4) : kBROob, 0, 0));
-      } else {  // (BIG: 64-bit loads; the rare >4 GiB-per-image shapes)
-        gi4 = rv ? *reinterpret_cast<const float4*>(gimg + ei) : make_float4(0.f, 0.f, 0.f, 0.f);
-        gh = hv ? gimg[eh] : 0.f;
+        const uint32_t o = (uint32_t)(e0 * 4);
+        rl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lok ? o : kBROob, 0, 0));
+        rm0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 4 : kBROob, 0, 0));
+        rm1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 20 : kBROob, 0, 0));
+        rr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, rok ? o + 36 : kBROob, 0, 0));
+      } else {
+        const float* gp = a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0 + (row ? e0 : 0);
+        rl = lok ? gp[0] : 0.f;  // (BIG: 64-bit loads; the rare >4 GiB-per-image shapes)
+        rm0 = *reinterpret_cast<const float4*>(gp + 1);
+        rm1 = *reinterpret_cast<const float4*>(gp + 5);
+        rr = rok ? gp[9] : 0.f;
       }
     }
+    const int cb = (tid % BR_NCH) * BR_CW;  // the chunk's first channel (256 % BR_NCH == 0: every u)
 #pragma unroll
-    for (int u = 0; u < HPER; ++u) {
-      const int h = slot(tid, u);
-      int wy, wx, j, cb;
-      hitem_geom(h, wy, wx, j, cb);
-      const bool item = h < HITEMS;
-      const int lc = 2 * wx + j, gc = c0 - 2 + lc;
+    for (int u = 0; u < IPER; ++u) {
+      const int it = tid + 256 * u;
+      int wy, wx;
+      item_geom(it, wy, wx);
+      const bool item = it < ITEMS;
 #pragma unroll
-      for (int dr = 0; dr < 2; ++dr) {
-        const int lr = 2 * wy + dr, gr = R0 + lr;
+      for (int q = 0; q < 4; ++q) {
+        const int lr = 2 * wy + (q >> 1), lc = 2 * wx + (q & 1);
+        const int gr = R0 + lr, gc = c0 - 2 + lc;
         const bool ok = item & (in | (((uint32_t)gr < (uint32_t)P) & ((uint32_t)gc < (uint32_t)P)));
         const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 64 + cb * 2) : kBROob;
-        yv[u][dr] = br_load_y(ry, off);
+        yv[u][q] = br_load_y(ry, off);
       }
       const int py = py0 + wy, px = px0 + wx;
       const bool pooled = item & (in | (((uint32_t)py < (uint32_t)Q) & ((uint32_t)px < (uint32_t)Q)));
       av[u] = __builtin_amdgcn_raw_buffer_load_b32(ra, pooled ? (uint32_t)(((wy * Q + wx) * 2 + (cb >> 4)) * 4) : kBROob, 0, 0);
       if constexpr (GB) {
         // (from the LDS tile in store())
+      } else if constexpr (!BIG) {
+        const uint32_t og = (uint32_t)(((int64_t)cb * gplane + (int64_t)wy * Q + wx) * 4);
+        const uint32_t gstep = (uint32_t)(gplane * 4);
+#pragma unroll
+        for (int k = 0; k < BR_CW; ++k)
+          gv[u][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
+                                                                                    0, 0));
       } else {
-        // (window (py, px) of channels cb .. cb+7: element (py, px) of 8 planes, G2MGeom)
-        const int pyc = pooled ? py : 0, pxc = pooled ? px : 0;
-        const int64_t eg = (int64_t)cb * gG + ((int64_t)((pyc + 3) >> 2) * a.gQ8 + (pxc >> 3)) * 32 + ((pyc + 3) & 3) * 8 +
-                           (pxc & 7);
-        if constexpr (!BIG) {
-          const uint32_t og = (uint32_t)(eg * 4), gstep = (uint32_t)(gG * 4);
+        const float* gp = a.g2m + ((int64_t)b * 32 + cb) * gplane + (int64_t)(pooled ? py : 0) * Q + (pooled ? px : 0);
 #pragma unroll
-          for (int k = 0; k < BR_CW; ++k)
-            gv[u][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
-                                                                                      0, 0));
-        } else {
-#pragma unroll
-          for (int k = 0; k < BR_CW; ++k) gv[u][k] = gimg[eg + k * gG];  // masked at use (store: pooled)
-        }
+        for (int k = 0; k < BR_CW; ++k) gv[u][k] = gp[k * gplane];  // masked at use (store: pooled)
       }
     }
 #pragma unroll
-    for (int u = 0; u < PPER; ++u) {
-      const int e = piece(tid, u);
+    for (int j = 0; j < PPER; ++j) {
+      const int e = piece(tid, j);
       const int rec = (e < PIECES ? e : 0) >> 1, q = e & 1;
       const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
       const int gr = R0 + lr, gc = c0 - 2 + lc;
       const bool ok = (e < PIECES) & (in | (((uint32_t)gr < (uint32_t)P) & ((uint32_t)gc < (uint32_t)P)));
       const uint32_t off = ok ? (uint32_t)((lr * P + lc) * 32 + q * 16) : kBROob;
-      pr[u] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
+      pr[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rp, off, 0, 0));
     }
   }
 
-  // GB: this set's block pieces and halo values into the LDS tile gb ([pooled row][col 10][channel]:
-  // column 0 the left halo, 1..8 the block, 9 the right halo)
+  // GB: this set's runs into the LDS tile gb ([pooled row][col][channel])
   __device__ __forceinline__ void put_runs(float* gb, int tid) const {
-    static_assert(GB, "block pieces only in the pipelined sets");
-    const int c = tid >> 3, sl = tid & 7, r = sl >> 1, h = sl & 1;
-    float* d = gb + (r * 10 + 1 + 4 * h) * 32 + c;
-    d[0] = gi4.x;
-    d[32] = gi4.y;
-    d[64] = gi4.z;
-    d[96] = gi4.w;
-    gb[((sl & 3) * 10 + ((sl >> 2) ? 9 : 0)) * 32 + c] = gh;
+    static_assert(GB, "runs only in the pipelined sets");
+    const int rt = tid - 128;
+    if (rt < 0) return;
+    const int c = rt & 31, wy = rt >> 5;
+    float* d = gb + wy * 10 * 32 + c;
+    d[0] = rl;
+    d[32] = rm0.x; d[64] = rm0.y; d[96] = rm0.z; d[128] = rm0.w;
+    d[160] = rm1.x; d[192] = rm1.y; d[224] = rm1.z; d[256] = rm1.w;
+    d[288] = rr;
   }
 
   // BN2 / ReLU / pool backward of the staged windows -> dy2 rows at dbase; p1 -> pbase;
@@ -585,17 +562,18 @@ struct BRStager {
   template <bool MIRROR>
   __device__ __forceinline__ void store(const BRArgs& a, int R0, int c0, int tid, char* dbase, char* pbase,
                                         const float* kc, char* dmir, char* pmir, const float* gb = nullptr) {
-    // every register of the set is read here, on every path: the half-items / pieces past HITEMS /
+    if constexpr (DIAG == 3) {}
+    // every register of the set is read here, on every path: the items / pieces past ITEMS /
     // PIECES are skipped below under exec masks, and a load whose result was consumed only
     // under a branch stays "pending" at the merge for the compiler's waitcnt pass -- the next
     // write of that register (the look-ahead loads into this set) then got a vmcnt(0), draining
     // the OTHER set's look-ahead loads too
 #pragma unroll
-    for (int u = 0; u < HPER; ++u) {
+    for (int u = 0; u < IPER; ++u) {
 #pragma unroll
-      for (int dr = 0; dr < 2; ++dr)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int i = 0; i < BR_CW / 2; ++i) asm volatile("" ::"v"(br_word(yv[u][dr], i)));
+        for (int i = 0; i < BR_CW / 2; ++i) asm volatile("" ::"v"(br_word(yv[u][q], i)));
       if constexpr (!GB) {
 #pragma unroll
         for (int k = 0; k < BR_CW; ++k) asm volatile("" ::"v"(gv[u][k]));
@@ -603,94 +581,112 @@ struct BRStager {
       asm volatile("" ::"v"(av[u]));
     }
 #pragma unroll
-    for (int u = 0; u < PPER; ++u) asm volatile("" ::"v"(pr[u].x), "v"(pr[u].y), "v"(pr[u].z), "v"(pr[u].w));
+    for (int j = 0; j < PPER; ++j) asm volatile("" ::"v"(pr[j].x), "v"(pr[j].y), "v"(pr[j].z), "v"(pr[j].w));
+    const int cb = (tid % BR_NCH) * BR_CW;
     const int P = a.P, Q = a.Q;
-    const bool fast = interior(a, R0, c0);
-    // (a lane's chunk is the same in both of its half-items: slot(tid, u) % 4 == tid % 4)
-    const int cbl = (tid & 3) * BR_CW;
-    float k1[BR_CW], k2[BR_CW], k3[BR_CW];
+    if constexpr (GB) {  // the items' pooled gradients from the LDS tile (put_runs, a tile earlier)
 #pragma unroll
-    for (int hh = 0; hh < BR_CW / 4; ++hh) {
-      const float4 a1 = *reinterpret_cast<const float4*>(&kc[2 * 32 + cbl + 4 * hh]);
-      const float4 a2v = *reinterpret_cast<const float4*>(&kc[3 * 32 + cbl + 4 * hh]);
-      const float4 a3 = *reinterpret_cast<const float4*>(&kc[4 * 32 + cbl + 4 * hh]);
-      k1[4 * hh] = a1.x; k1[4 * hh + 1] = a1.y; k1[4 * hh + 2] = a1.z; k1[4 * hh + 3] = a1.w;
-      k2[4 * hh] = a2v.x; k2[4 * hh + 1] = a2v.y; k2[4 * hh + 2] = a2v.z; k2[4 * hh + 3] = a2v.w;
-      k3[4 * hh] = a3.x; k3[4 * hh + 1] = a3.y; k3[4 * hh + 2] = a3.z; k3[4 * hh + 3] = a3.w;
-    }
-#pragma unroll
-    for (int u = 0; u < HPER; ++u) {
-      const int h = slot(tid, u);
-      if (h >= HITEMS) continue;
-      int wy, wx, j, cb;
-      hitem_geom(h, wy, wx, j, cb);
-      if constexpr (GB) {  // the window's pooled gradients from the LDS tile (put_runs, a tile earlier)
+      for (int u = 0; u < IPER; ++u) {
+        int wy, wx;
+        item_geom(tid + 256 * u, wy, wx);
         const float4* gp = reinterpret_cast<const float4*>(gb + (wy * 10 + wx) * 32 + cb);
 #pragma unroll
-        for (int hh = 0; hh < BR_CW / 4; ++hh) {
-          const float4 v = gp[hh];
-          gv[u][4 * hh] = v.x; gv[u][4 * hh + 1] = v.y; gv[u][4 * hh + 2] = v.z; gv[u][4 * hh + 3] = v.w;
+        for (int h = 0; h < BR_CW / 4; ++h) {
+          const float4 v = gp[h];
+          gv[u][4 * h] = v.x; gv[u][4 * h + 1] = v.y; gv[u][4 * h + 2] = v.z; gv[u][4 * h + 3] = v.w;
         }
       }
-      float d[2][BR_CW];
-      // this chunk's channels' codes: bits (cb & 15) .. +BR_CW-1 and 16 + that of the window's word;
-      // this half-item's pixels are window pixels q = 2 dr + j
+    }
+    float k1[BR_CW], k2[BR_CW], k3[BR_CW];
+#pragma unroll
+    for (int h = 0; h < BR_CW / 4; ++h) {
+      const float4 a1 = *reinterpret_cast<const float4*>(&kc[2 * 32 + cb + 4 * h]);
+      const float4 a2v = *reinterpret_cast<const float4*>(&kc[3 * 32 + cb + 4 * h]);
+      const float4 a3 = *reinterpret_cast<const float4*>(&kc[4 * 32 + cb + 4 * h]);
+      k1[4 * h] = a1.x; k1[4 * h + 1] = a1.y; k1[4 * h + 2] = a1.z; k1[4 * h + 3] = a1.w;
+      k2[4 * h] = a2v.x; k2[4 * h + 1] = a2v.y; k2[4 * h + 2] = a2v.z; k2[4 * h + 3] = a2v.w;
+      k3[4 * h] = a3.x; k3[4 * h + 1] = a3.y; k3[4 * h + 2] = a3.z; k3[4 * h + 3] = a3.w;
+    }
+    const bool fast = interior(a, R0, c0);
+#pragma unroll
+    for (int u = 0; u < IPER; ++u) {
+      const int it = tid + 256 * u;
+      if (it >= ITEMS) continue;
+      int wy, wx;
+      item_geom(it, wy, wx);
+      float y[4][BR_CW];  // the stored values (ka, kb, k2, k3 carry the decode: kernel header)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int i = 0; i < BR_CW / 2; ++i) {
+          const uint32_t w = br_word(yv[u][q], i);
+          y[q][2 * i] = f16_val(w);
+          y[q][2 * i + 1] = f16_val(w >> 16);
+        }
+      float d[4][BR_CW];
+      // this item's channels' codes: bits (cb & 15) .. +BR_CW-1 and 16 + that of the window's word
       const uint32_t cw = av[u] >> (cb & 15);
       if constexpr (br_no_math(DIAG)) {  // timing only: no BN2 / pool backward math
 #pragma unroll
-        for (int dr = 0; dr < 2; ++dr)
+        for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int cc = 0; cc < BR_CW; ++cc) d[dr][cc] = f16_val(br_word(yv[u][dr], cc >> 1) >> (16 * (cc & 1))) + gv[u][cc];
+          for (int cc = 0; cc < BR_CW; ++cc) d[q][cc] = y[q][cc] + gv[u][cc];
       } else if (fast) {
 #pragma unroll
         for (int cc = 0; cc < BR_CW; ++cc) {
+          // y2h values straight into v_fma_mix_f32 (br_fma_y)
+          auto fy = [&](float k, int q, float c) { return br_fma_y(k, yv[u][q], cc, c); };
           const uint32_t code = ((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u);  // the forward's argmax
-          // the pooled gradient folded into the constant: select + FMA (v_fma_mix_f32 on the fp16
-          // y2h value, br_fma_y) per pixel; the 2 compares first (SGPR-pair masks: a VCC reused
-          // compare -> select -> compare costs an s_nop per pixel for the VALU-mask hazard)
+          // the pooled gradient folded into the constant: select + FMA per pixel.  The 4 compares
+          // go first (4 SGPR-pair masks): one VCC reused compare -> select -> compare cost an
+          // s_nop per pixel for the VALU-mask hazard
           const float k3g = fmaf(k1[cc], gv[u][cc], k3[cc]);
-          const bool e0 = code == (uint32_t)j, e1 = code == (uint32_t)(2 + j);
+          bool eq[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) eq[q] = code == (uint32_t)q;
           __builtin_amdgcn_sched_barrier(0);
-          d[0][cc] = br_fma_y(k2[cc], yv[u][0], cc, e0 ? k3g : k3[cc]);
-          d[1][cc] = br_fma_y(k2[cc], yv[u][1], cc, e1 ? k3g : k3[cc]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) d[q][cc] = fy(k2[cc], q, eq[q] ? k3g : k3[cc]);
         }
       } else {
         const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;
         const bool pooled = gy >= 0 && gx >= 0 && (gy >> 1) < Q && (gx >> 1) < Q;
-        const int c = gx + j;
 #pragma unroll
         for (int cc = 0; cc < BR_CW; ++cc) {
           const int am = pooled ? (int)(((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u)) : -1;
 #pragma unroll
-          for (int dr = 0; dr < 2; ++dr) {
-            const int r = gy + dr;
+          for (int q = 0; q < 4; ++q) {
+            const int r = gy + (q >> 1), c = gx + (q & 1);
             const bool inb = r >= 0 && r < P && c >= 0 && c < P;  // zero padding outside the image
-            const float dz = am == 2 * dr + j ? gv[u][cc] : 0.f;
-            const float yy = f16_val(br_word(yv[u][dr], cc >> 1) >> (16 * (cc & 1)));
-            d[dr][cc] = inb ? fmaf(k1[cc], dz, fmaf(k2[cc], yy, k3[cc])) : 0.f;
+            const float dz = am == q ? gv[u][cc] : 0.f;
+            d[q][cc] = inb ? fmaf(k1[cc], dz, fmaf(k2[cc], y[q][cc], k3[cc])) : 0.f;
           }
         }
       }
 #pragma unroll
-      for (int dr = 0; dr < 2; ++dr) {
-        uint32_t hw[BR_CW / 2];  // dy2 rounded once (TF32 class; k1..k3 carry the scale 2^e: d is dy2 * 2^e)
+      for (int q = 0; q < 4; ++q) {
+        uint32_t h[BR_CW / 2];  // dy2 rounded once (TF32 class; k1..k3 carry the scale 2^e: d is dy2 * 2^e)
 #pragma unroll
-        for (int i = 0; i < BR_CW / 2; ++i) hw[i] = cvt2_f16(d[dr][2 * i], d[dr][2 * i + 1]);
-        const int lr = 2 * wy + dr;
-        const int ro = (2 * wx + j) * 32 + (cb & 15) * 2 + (cb >> 4) * BR_DPL;
-        *reinterpret_cast<uint4*>(dbase + lr * BR_DROW + ro) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-        if (MIRROR && lr >= 4) *reinterpret_cast<uint4*>(dmir + (lr - 4) * BR_DROW + ro) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+        for (int i = 0; i < BR_CW / 2; ++i) h[i] = cvt2_f16(d[q][2 * i], d[q][2 * i + 1]);
+        const int lr = 2 * wy + (q >> 1);
+        const int ro = (2 * wx + (q & 1)) * 32 + (cb & 15) * 2;
+        char* rec = dbase + lr * BR_DROW + ro;
+        auto put = [&](char* r) {
+          *reinterpret_cast<uint4*>(r + (cb >> 4) * BR_DPL) = make_uint4(h[0], h[1], h[2], h[3]);
+        };
+        put(rec);
+        if (MIRROR && lr >= 4) put(dmir + (lr - 4) * BR_DROW + ro);
       }
     }
 #pragma unroll
-    for (int u = 0; u < PPER; ++u) {
-      const int e = piece(tid, u);
+    for (int j = 0; j < PPER; ++j) {
+      const int e = piece(tid, j);
       if (e < PIECES) {
         const int rec = e >> 1, q = e & 1;
         const int lr = rec / BR_SC, lc = rec - lr * BR_SC;
         const int po = lc * 32 + q * 16;
-        *reinterpret_cast<uint4*>(pbase + lr * BR_PROW + po) = pr[u];
-        if (MIRROR && lr >= 4) *reinterpret_cast<uint4*>(pmir + (lr - 4) * BR_PROW + po) = pr[u];
+        *reinterpret_cast<uint4*>(pbase + lr * BR_PROW + po) = pr[j];
+        if (MIRROR && lr >= 4) *reinterpret_cast<uint4*>(pmir + (lr - 4) * BR_PROW + po) = pr[j];
       }
     }
   }
@@ -811,12 +807,6 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
   BRArgs a;
   a.y2 = y2; a.a2 = a2; a.g2m = g2m; a.p1 = p1; a.dp1 = dp1; a.slab = slab; a.walk = walk;
   a.B = B; a.P = P; a.Q = P / 2;
-  {
-    const G2MGeom gg = g2m_geom(P / 2);
-    a.gNR = gg.NR;
-    a.gQ8 = gg.Q8;
-    a.gG = gg.plane();
-  }
   a.sk = sk;
   a.w = xcd_remap(blockIdx.x, gridDim.x);  // this workgroup's list (XCD-contiguous: neighbouring columns)
   a.walk = walk + a.w * sw;
@@ -974,14 +964,14 @@ static int br_diag_env() {
 static int br_diag_env() { return 0; }
 #endif
 
-// g2m: [B][32][G] (pooled_layout.h G2MGeom); walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
+// g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
 // [nwg][rows] (fused_ops.cpp bwd_walk)
 void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const float* aff2, const float* kbuf,
                     const float* b2,
                     uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st) {
   const int Q = P / 2;
-  const bool big = (int64_t)32 * g2m_geom(Q).plane() * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
+  const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
 #define TDS_BR_LAUNCH_B(D, BG)                                                                                         \
   {                                                                                                                    \
     static bool set = false;                                                                                           \

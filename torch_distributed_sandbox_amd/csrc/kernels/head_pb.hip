@@ -51,11 +51,7 @@ struct HPGrid {
 };
 
 __host__ __device__ inline HPGrid hp_grid(const PBGeom& g) { return HPGrid{(g.Q4 + HP_BAND - 1) / HP_BAND}; }
-// the backward walks g2m's row-shifted block rows (pooled_layout.h G2MGeom: NR of them), so the 4
-// waves of a workgroup write the 4 rows of the same g2m blocks in one iteration
-__host__ __device__ inline HPGrid hp_grid_b(const PBGeom& g) {
-  return HPGrid{(g2m_geom(g.Q).NR + HP_BAND_B - 1) / HP_BAND_B};
-}
+__host__ __device__ inline HPGrid hp_grid_b(const PBGeom& g) { return HPGrid{(g.Q4 + HP_BAND_B - 1) / HP_BAND_B}; }
 
 __device__ __forceinline__ float hp_relu(float z) { return z > 0.f ? z : (isnan(z) ? z : 0.f); }
 
@@ -99,12 +95,11 @@ __device__ __forceinline__ void hp_st4(float* p, int al, float4 v, bool nt = tru
 struct HPRow {
   int64_t off, ldoff;
   int al, nvalid, sh;
-  // pooled row py = 4 R + prow + shift (the backward walks g2m's row-shifted blocks: shift -3)
-  __device__ HPRow(const PBGeom& g, const HPThread& th, int c, int R, int shift = 0) {
+  __device__ HPRow(const PBGeom& g, const HPThread& th, int c, int R) {
     const int Q = g.Q;
-    const int py = 4 * R + th.prow + shift, px0 = th.blk * 8 + th.half * 4;
-    const int64_t rowbase = (int64_t)c * Q * Q + (int64_t)min(max(py, 0), Q - 1) * Q;
-    nvalid = (py >= 0 && py < Q && th.blk < g.Q8) ? max(0, min(4, Q - px0)) : 0;
+    const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
+    const int64_t rowbase = (int64_t)c * Q * Q + (int64_t)(py < Q ? py : Q - 1) * Q;
+    nvalid = (py < Q && th.blk < g.Q8) ? max(0, min(4, Q - px0)) : 0;
     al = __builtin_amdgcn_readfirstlane((int)(rowbase & 3));  // j*32*Q*Q % 4 == 0 for every class
     off = rowbase + px0;
     const int pxl = min(px0, max(0, Q - 4));  // Q >= 4 (supported(): H >= 16)
@@ -125,15 +120,13 @@ struct HPLoad {
   // for them is vmcnt(#loads of the NEXT chunk) -- an edge fix-up right after the loads made
   // it a vmcnt(0) on the prefetch and serialised every chunk on its own latency
   __device__ __forceinline__ void issue(const float* __restrict__ ya, const float* W, const PBGeom& g, const HPThread& th,
-                                        int c, int R, int b0, int NC, int shift = 0) {
+                                        int c, int R, int b0, int NC) {
     const int64_t plane = g.plane(), QQ = (int64_t)g.Q * g.Q;
     const int bc = th.blk < g.Q8 ? th.blk : g.Q8 - 1;  // idle lanes of the last chunk: a valid block
-    // ya at pooled row py = 4 R + prow + shift (rows outside the image: a valid row, masked)
-    const int py = min(max(4 * R + th.prow + shift, 0), g.Q - 1);
-    const int64_t yi = (((int64_t)c * g.Q4 + (py >> 2)) * g.Q8 + bc) * 32 + ((py & 3) * 2 + th.half) * 4;
+    const int64_t yi = (((int64_t)c * g.Q4 + R) * g.Q8 + bc) * 32 + th.part * 4;
 #pragma unroll
     for (int b = 0; b < NB; ++b) y[b] = *reinterpret_cast<const float4*>(ya + (int64_t)(b0 + b) * 32 * plane + yi);
-    const HPRow rw(g, th, c, R, shift);
+    const HPRow rw(g, th, c, R);
     sh = rw.sh;
     nvalid = rw.nvalid;
     // one dwordx4 per group at any dword alignment (global loads need only 4-B alignment;
@@ -330,7 +323,7 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const double* __restri
 }
 
 // Backward for images b0 .. b0+NB-1.
-//   g2m[b][c][py][px] = (sum_j dl[b][j] W[j][c][py][px]) * [a*ya + b > 0]   ([B][32][G], G2MGeom)
+//   g2m[b][c][py][px] = (sum_j dl[b][j] W[j][c][py][px]) * [a*ya + b > 0]   (planar [B][32][Q][Q])
 //   partial[c][pass*nblk + blk][2] = { sum g2m, sum g2m * ya }       (BN2 backward sums)
 //   dW[j][c][pos] (= or +=) scale * sum_b dl[b][j] X[b][c][pos]      (WITH_DW; ACC adds)
 //   Wupd = W - lr * dW                                               (UPD: SGD step fused)
@@ -381,26 +374,24 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   const float a = aff2[c], bb = aff2[32 + c];
   const int Q = g.Q;
   const int64_t plane = g.plane();
-  const G2MGeom gg = g2m_geom(Q);
   float sdz = 0.f, sdy = 0.f;
   uint32_t gmx = 0u;  // max |g2m| bits
   const int nch = (g.Q8 + 31) / 32;
-  // iteration i: g2m block row R = R0 + i / nch (pooled rows 4R - 3 .. 4R, one per wave), chunk i % nch
-  const int R0 = band * HP_BAND_B, nit = (min(gg.NR, R0 + HP_BAND_B) - R0) * nch;
+  const int R0 = band * HP_BAND_B, nit = (min(g.Q4, R0 + HP_BAND_B) - R0) * nch;
   // two load sets in alternation, as in the forward
   HPLoad<NB> ld0, ld1;
   auto issue = [&](HPLoad<NB>& L, int i) {
     const int ii = i < nit ? i : nit - 1;
-    L.issue(ya, W, g, HPThread(ii % nch), c, R0 + ii / nch, b0, NC, -3);
+    L.issue(ya, W, g, HPThread(ii % nch), c, R0 + ii / nch, b0, NC);
   };
   auto body = [&](HPLoad<NB>& cur, int i) {
     const int R = R0 + i / nch;
     const HPThread th(i % nch);
     cur.fix(NC);
     const bool bok = th.blk < g.Q8;
-    const int py = 4 * R + th.prow - 3, px0 = th.blk * 8 + th.half * 4;
-    const bool rok = bok && py >= 0 && py < Q;
-    const HPRow rwg(g, th, c, R, -3);
+    const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
+    const bool rok = bok && py < Q;
+    const HPRow rwg(g, th, c, R);
     float x[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -422,13 +413,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
         sdz += gm[k];
         sdy = fmaf(gm[k], ok ? yy[k] : 0.f, sdy);
       }
-      // row-shifted pooled-blocked (pooled_layout.h G2MGeom): the lane's 4 columns are one 16-B
-      // piece of a block (columns past Q as 0), the 4 waves the block's 4 rows in this iteration --
-      // plain stores, so the line is whole in L2 before it is written back (non-temporal 32-B
-      // pieces of lines went to HBM one by one: head backward 0.45 -> 0.80 ms, r6_s5); rows outside
-      // the image are not stored
-      if (rok)
-        *reinterpret_cast<float4*>(g2m + gg.index(b0 + b, c, py, px0)) = make_float4(gm[0], gm[1], gm[2], gm[3]);
+      // planar, like a weight plane
+      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]), true);
     }
     if constexpr (WITH_DW) {
       const HPRow& rw = rwg;
@@ -550,7 +536,6 @@ using namespace tds;
 int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // forward workgroups per channel
 int tds_head_bwd_pb_nblk(int Q) { return hp_grid_b(pb_geom(Q)).per_channel(); }  // backward workgroups per channel
 int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
-int64_t tds_g2m_plane(int Q) { return g2m_geom(Q).plane(); }
 
 // partial: double [32 * nblk + 32][B*NC] (the last 32 rows: the in-launch finalizer's channel sums);
 // sums: double [B*NC].  fused_fin = false: the separate head_logits launch (the A/B reference).

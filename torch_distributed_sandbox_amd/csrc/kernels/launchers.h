@@ -185,7 +185,6 @@ void tds_l1_finalize(const double* bwd_sum, const double* gram, int64_t n, const
 
 // ---- head_pb.hip (fc head on the pooled-blocked ya / g2m, pooled_layout.h)
 int64_t tds_pb_plane(int Q);  // floats per (image, channel) plane
-int64_t tds_g2m_plane(int Q);  // g2m floats per (image, channel) plane (pooled_layout.h G2MGeom)
 int tds_head_pb_nblk(int Q);  // workgroups per channel
 int tds_head_bwd_pb_nblk(int Q);  // the backward's workgroups per channel (its partial / gpart rows)
 // in-launch finalizer counters (launch_status.hip; common.h tds_arrive); nullptr: no fused finalize
