@@ -117,7 +117,54 @@ def _parser():
     ap.add_argument("--shared-device", action="store_true",
                     help="rehearsal: every rank on cuda:0 over gloo (plumbing only, not an OOM result)")
     ap.add_argument("--timeout", type=float, default=1800.0, help="--gpus > 1: terminate the ranks after this (s)")
+    ap.add_argument("--single-gpu-half", action="store_true",
+                    help="internal: run the calibration and the batch-%(default)s attempt, print their JSON, exit")
     return ap
+
+
+def single_gpu_half(args, device):
+    """Calibrate the memory model, pick the image size and try the failing batch on ONE GPU.
+    Runs in a process of its own (main() starts it before touching the GPU): a training step that
+    dies of out-of-memory part-way through the forward can leave tensors referenced from the
+    half-built autograd graph and the DDP hooks, and the batch-5 run must start on an empty GPU."""
+    total = torch.cuda.get_device_properties(device).total_memory
+    act, fixed, calib_runs = calibrate(args.calib_size, device)
+    gc.collect()
+    torch.cuda.empty_cache()
+    H = args.image_size
+    if H <= 0:
+        edge = (1.06 * total / (args.bs_fail * act + fixed)) ** 0.5
+        H = int(-(-edge // 500) * 500)
+    rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1),
+           "model": {"calibrated_at": args.calib_size, "calibration_runs": calib_runs,
+                     "act_bytes_per_px_per_image": round(act, 1),
+                     "fixed_bytes_per_px": round(fixed, 1),
+                     "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed) / 1e9, 1)
+                                      for b in (args.bs_fit, args.bs_fail)},
+                     "predicted_oom_edge_bs%d" % args.bs_fail:
+                         int((total / (args.bs_fail * act + fixed)) ** 0.5)}}
+    try:
+        r = run(H, args.bs_fail, 1, device, 1, 0)
+        rec["bs_fail_result"] = {"oom": False, **r}
+    except torch.cuda.OutOfMemoryError as e:
+        msg = str(e).split("\n")[0]
+        rec["bs_fail_result"] = {"oom": True, "error": msg[:300]}
+    return rec
+
+
+def _run_single_gpu_half(argv, local):
+    """The single-GPU half in a child process (this process has not touched the GPU yet)."""
+    import subprocess
+
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["LOCAL_RANK"] = str(local)
+    p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), *argv, "--gpus", "1", "--single-gpu-half"],
+                       env=env, stdout=subprocess.PIPE, text=True)
+    if p.returncode != 0:
+        raise SystemExit(f"oom_demo: the single-GPU half failed (exit {p.returncode})")
+    return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
 
 
 def _rank_entry(i, argv, world, addr, port):
@@ -141,41 +188,26 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.shared_device else int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    if args.single_gpu_half:
+        torch.cuda.set_device(local)
+        print(json.dumps(single_gpu_half(args, torch.device("cuda", local))), flush=True)
+        return
     H = args.image_size
     rec = None
     if H <= 0 and world > 1:
         raise SystemExit("oom_demo: --image-size 0 (auto) is for one process; give the size for --gpus > 1")
     if rank == 0:
-        # the single-GPU half runs on rank 0 BEFORE the process group exists (DDP at world size
-        # 1, no collective); the other ranks wait in the rendezvous meanwhile
-        total = torch.cuda.get_device_properties(device).total_memory
-        act, fixed, calib_runs = calibrate(args.calib_size, device)
-        gc.collect()
-        torch.cuda.empty_cache()
-        if H <= 0:
-            edge = (1.06 * total / (args.bs_fail * act + fixed)) ** 0.5
-            H = int(-(-edge // 500) * 500)
-        rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1), "world_size": world,
-               "model": {"calibrated_at": args.calib_size, "calibration_runs": calib_runs,
-                         "act_bytes_per_px_per_image": round(act, 1),
-                         "fixed_bytes_per_px": round(fixed, 1),
-                         "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed) / 1e9, 1)
-                                          for b in (args.bs_fit, args.bs_fail)},
-                         "predicted_oom_edge_bs%d" % args.bs_fail:
-                             int((total / (args.bs_fail * act + fixed)) ** 0.5)}}
+        # 1) calibration + batch 10 on ONE GPU, in a child process, BEFORE this rank touches the GPU
+        # or the process group exists; the other ranks wait in the rendezvous meanwhile
+        rec = _run_single_gpu_half(argv, local)
+        H = rec["image_size"]
+        rec["world_size"] = world
         if args.shared_device:
             rec["shared_device"] = True  # rehearsal: all ranks on one GPU
-        # 1) batch 10 on ONE GPU
-        try:
-            r = run(H, args.bs_fail, 1, device, 1, rank)
-            rec["bs_fail_result"] = {"oom": False, **r}
-        except torch.cuda.OutOfMemoryError as e:
-            msg = str(e).split("\n")[0]
-            rec["bs_fail_result"] = {"oom": True, "error": msg[:300]}
-        gc.collect()
-        torch.cuda.empty_cache()
+    elif H <= 0:
+        raise SystemExit("oom_demo: the ranks need --image-size")
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
     if world > 1:
         import datetime
 
