@@ -46,19 +46,24 @@ import torch  # noqa: E402
 # weight steps inside the head backward kernel and its 80 B/px gradient slot is never allocated
 # (parallel/ddp.py _lazy_from; round 4's record still carried it: 39.4 GiB at 23000^2).  The DDP
 # constructor holds the flat buffer and one original parameter at a time (2 x 80 B/px, before any
-# activation exists).
+# activation exists): its peak is modelled apart, peak(H, B) = max((act * B + fixed), ctor) * H^2.
 
 
 def calibrate(H, device):
+    """(act, fixed, ctor) bytes per input pixel: the training step's peak is (B * act + fixed) * H^2,
+    the DDP constructor's (before any activation exists) ctor * H^2.  The two peaks are measured
+    apart (r6: at 3000^2 the constructor's 2 x 80 B/px was above the batch-1 step, and fitting
+    the overall peaks at batch 1 and 2 made act far too small -- the auto size then OOMed at batch 5)."""
     ra, rb = run(H, 1, 1, device, 1, 0), run(H, 2, 1, device, 1, 0)
-    a, b = ra["peak_gb"] * 1e9, rb["peak_gb"] * 1e9
+    a, b = ra["step_peak_gb"] * 1e9, rb["step_peak_gb"] * 1e9
     act = (b - a) / (H * H)
     fixed = a / (H * H) - act
-    return act, fixed, [ra, rb]
+    ctor = max(ra["ctor_peak_gb"], rb["ctor_peak_gb"]) * 1e9 / (H * H)
+    return act, fixed, ctor, [ra, rb]
 
 
-def predicted_bytes(H, B, act, fixed):
-    return (B * act + fixed) * H * H
+def predicted_bytes(H, B, act, fixed, ctor=0.0):
+    return max(B * act + fixed, ctor) * H * H
 
 
 def run(H, B, steps, device, world, rank):
@@ -77,6 +82,8 @@ def run(H, B, steps, device, world, rank):
     opt = SGD(model.parameters(), 1e-4)
     ddp = DistributedDataParallel(model, device_ids=[device.index], overlap_optimizer=True)
     ddp.attach_optimizer(opt)
+    ctor_peak = torch.cuda.max_memory_allocated(device)
+    torch.cuda.reset_peak_memory_stats(device)
     crit = CrossEntropyLoss()
     src, lab = synthetic_batch(B, (H, H), device, seed=7 + rank)
     t0 = None
@@ -92,12 +99,14 @@ def run(H, B, steps, device, world, rank):
             t0 = time.perf_counter()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / max(1, steps - 1) if steps > 1 else None
-    peak = torch.cuda.max_memory_allocated(device)
+    step_peak = torch.cuda.max_memory_allocated(device)
+    peak = max(ctor_peak, step_peak)
     grad_gb = ddp.grad_storage_bytes() / 1e9
     del ddp, model, opt, images, loss
     gc.collect()
     torch.cuda.empty_cache()
     return {"batch_per_rank": B, "peak_gb": round((peak - base) / 1e9, 3), "base_gb": round(base / 1e9, 3),
+            "ctor_peak_gb": round((ctor_peak - base) / 1e9, 3), "step_peak_gb": round((step_peak - base) / 1e9, 3),
             "flat_grad_gb": round(grad_gb, 4),
             "ms_per_step": round(dt * 1e3, 2) if dt else None,
             "images_per_sec_node": round(world * B / dt, 2) if dt else None}
@@ -128,21 +137,22 @@ def single_gpu_half(args, device):
     dies of out-of-memory part-way through the forward can leave tensors referenced from the
     half-built autograd graph and the DDP hooks, and the batch-5 run must start on an empty GPU."""
     total = torch.cuda.get_device_properties(device).total_memory
-    act, fixed, calib_runs = calibrate(args.calib_size, device)
+    act, fixed, ctor, calib_runs = calibrate(args.calib_size, device)
     gc.collect()
     torch.cuda.empty_cache()
     H = args.image_size
     if H <= 0:
-        edge = (1.06 * total / (args.bs_fail * act + fixed)) ** 0.5
+        edge = (1.06 * total / max(args.bs_fail * act + fixed, ctor)) ** 0.5
         H = int(-(-edge // 500) * 500)
     rec = {"image_size": H, "gpu_total_gb": round(total / 1e9, 1),
            "model": {"calibrated_at": args.calib_size, "calibration_runs": calib_runs,
                      "act_bytes_per_px_per_image": round(act, 1),
                      "fixed_bytes_per_px": round(fixed, 1),
-                     "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed) / 1e9, 1)
+                     "ddp_constructor_bytes_per_px": round(ctor, 1),
+                     "predicted_gb": {str(b): round(predicted_bytes(H, b, act, fixed, ctor) / 1e9, 1)
                                       for b in (args.bs_fit, args.bs_fail)},
                      "predicted_oom_edge_bs%d" % args.bs_fail:
-                         int((total / (args.bs_fail * act + fixed)) ** 0.5)}}
+                         int((total / max(args.bs_fail * act + fixed, ctor)) ** 0.5)}}
     try:
         r = run(H, args.bs_fail, 1, device, 1, 0)
         rec["bs_fail_result"] = {"oom": False, **r}
@@ -215,7 +225,12 @@ def main(argv=None):
         tdist.init_process_group(backend, rank=rank, world_size=world, timeout=datetime.timedelta(hours=1),
                                  device_id=None if backend == "gloo" else local)
     # 2) batch 5 per rank: DDP over all ranks
-    fit = run(H, args.bs_fit, args.steps, device, world, rank)
+    try:
+        fit = run(H, args.bs_fit, args.steps, device, world, rank)
+    except torch.cuda.OutOfMemoryError as e:
+        if world > 1:
+            raise
+        fit = {"oom": True, "error": str(e).split("\n")[0][:300]}
     if rank == 0:
         rec["bs_fit_result"] = fit
         rec["effective_batch"] = args.bs_fit * world

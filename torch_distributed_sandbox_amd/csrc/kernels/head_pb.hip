@@ -31,9 +31,6 @@
 //   g2m : one float4 per image (same index as ya), dW / updated W: one 4-float group per class.
 // No LDS and no barriers in the stream: the next chunk's loads are issued before the current
 // one is reduced.  64-bit indexing throughout (no buffer descriptors).
-#include <cstdio>
-#include <cstdlib>
-
 #include "common.h"
 #include "ce_small.h"
 #include "launchers.h"
@@ -536,18 +533,6 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
 
 using namespace tds;
 
-// (A/B, r6: dynamic LDS requested only to cap the head kernels' workgroups per CU -- the HBM probe
-// moved a read + write stream at 5.6 TB/s with 4 waves per CU against 4.7-4.9 with 8 or more;
-// TDS_HEAD_LDS_PAD=<fwd bytes>,<bwd bytes>)
-static int hp_lds_pad(int which) {
-  static int pad[2] = {-1, -1};
-  if (pad[0] < 0) {
-    pad[0] = pad[1] = 0;
-    if (const char* e = std::getenv("TDS_HEAD_LDS_PAD")) std::sscanf(e, "%d,%d", &pad[0], &pad[1]);
-  }
-  return pad[which];
-}
-
 int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // forward workgroups per channel
 int tds_head_bwd_pb_nblk(int Q) { return hp_grid_b(pb_geom(Q)).per_channel(); }  // backward workgroups per channel
 int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
@@ -586,10 +571,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
 #define TDS_HPF(NBV)                                                                                                   \
   case NBV:                                                                                                            \
-    if (hp_lds_pad(0) > 65536)                                                                                         \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_fwd_pb_kernel<NBV>),                               \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, hp_lds_pad(0));                            \
-    hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), hp_lds_pad(0), st, ya, Wfc, aff2, partial, xout, g, \
+    hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
                        B, b0, NC, fin, c0, x_rs);                                                                      \
     TDS_LAUNCH_CHECK();                                                                                                \
     break;
@@ -638,10 +620,7 @@ int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const 
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
     const bool acc = pass > 0;
 #define TDS_HPB_E(NBV, WD, AC, UP, KP)                                                                             \
-  if (hp_lds_pad(1) > 65536)                                                                                       \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(head_bwd_pb_kernel<NBV, WD, AC, UP, KP>),               \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, hp_lds_pad(1));                          \
-  hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), hp_lds_pad(1), st, ya, Wfc, aff2, \
+  hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, \
                      dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gpart, fin);
 #define TDS_HPB(NBV)                                   \
   case NBV:                                            \

@@ -41,6 +41,7 @@ from __future__ import annotations
 
 import contextlib
 import hashlib
+import weakref
 from typing import List, Optional
 
 import torch
@@ -49,6 +50,21 @@ import torch.nn as nn
 from ..ops import grad_sink
 from . import distributed as tdist
 from . import factored
+
+def _weak_call(obj, name: str):
+    """``obj.<name>`` as a callable that holds ``obj`` weakly (a no-op once it is gone).  Hooks and
+    providers attached to parameters or to autograd nodes must not keep the wrapper alive: the
+    cycle parameter -> hook -> wrapper -> module -> parameter runs through C++ that Python's
+    collector cannot see, and every model built after it would find its predecessor's buffers
+    still allocated (round 6: 0.72 GB per ConvNet at 3000^2, tools/oom_demo.py)."""
+    ref = weakref.ref(obj)
+
+    def call(*args):
+        o = ref()
+        return None if o is None else getattr(o, name)(*args)
+
+    return call
+
 
 _ALIGN_ELEMS = 64  # 256-byte alignment of every parameter slot in the flat buffers
 
@@ -193,7 +209,7 @@ class DistributedDataParallel(nn.Module):
         self._callback_queued = False
         self._native = self._make_native_reducer(reducer)
         if self._native is None:
-            self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad_ready) for p in self._params]
+            self._hooks = [p.register_post_accumulate_grad_hook(_weak_call(self, "_on_grad_ready")) for p in self._params]
         else:
             self._hooks = []
             self._native.attach(self._params)
@@ -301,10 +317,13 @@ class DistributedDataParallel(nn.Module):
         return out
 
     def _make_skip_fn(self, b: _Bucket):
+        ref = weakref.ref(self)
+
         def set_skip(flag: bool):
             b.skip = bool(flag)
-            if self._native is not None:
-                self._native.set_bucket_skip(b.index, bool(flag))
+            s = ref()
+            if s is not None and s._native is not None:
+                s._native.set_bucket_skip(b.index, bool(flag))
 
         return set_skip
 
@@ -356,9 +375,11 @@ class DistributedDataParallel(nn.Module):
     def _make_view_fn(self, p):
         o, n = self._slots[id(p)]
         shape = p.shape
+        ref = weakref.ref(self)
 
-        def view():
-            return self._slot(o, n).view(shape)
+        def view():  # (None once the wrapper is gone: grad_sink.acquire then returns a plain tensor)
+            s = ref()
+            return None if s is None else s._slot(o, n).view(shape)
 
         return view
 
@@ -537,10 +558,12 @@ class DistributedDataParallel(nn.Module):
         backward kernel instead (ops/fused_update.py): nothing to average, and the
         kernel already holds the weight and its gradient."""
         if self.flat_param is not None and hasattr(optimizer, "set_flat_buffers"):
-            optimizer.set_flat_buffers(self.flat_param, lambda: self.flat_grad, self._params)
+            ref = weakref.ref(self)
+            optimizer.set_flat_buffers(self.flat_param, lambda: ref().flat_grad, self._params)
             if self._deferred and hasattr(optimizer, "set_deferred"):
-                optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred], self._run_deferred_update,
-                                       lambda p: id(p) in self._fused_done)
+                optimizer.set_deferred([(b.offset, b.numel) for b in self._deferred],
+                                       _weak_call(self, "_run_deferred_update"),
+                                       lambda p: ref() is not None and id(p) in ref()._fused_done)
                 if self.fuse_update_in_backward and (self.world_size == 1 or self._exchanges):
                     self._register_fused_updates(optimizer)
         return optimizer
@@ -558,12 +581,16 @@ class DistributedDataParallel(nn.Module):
                 return None
             return float(g["lr"])
 
+        ref = weakref.ref(self)
         for b in self._deferred:
             for p in b.params:
                 if p.dim() < 2:
                     continue  # biases: tiny, updated by the optimizer as usual
 
                 def provider(what, p=p):
+                    self = ref()  # (the provider lives on the parameter: no strong reference back)
+                    if self is None:
+                        return None
                     if what == "keep_grad":
                         return self.keep_fused_grads
                     if what in ("applied", "applied_no_grad"):
