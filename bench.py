@@ -164,10 +164,6 @@ def _parser():
     ap.add_argument("--preflight-timeout", type=float, default=60.0)
     ap.add_argument("--step-times", action="store_true",
                     help="record each timed step's GPU time with events (config.step_ms; diagnostics)")
-    ap.add_argument("--clock-warmup-ms", type=float, default=0.0,
-                    help="before the warmup steps, keep the GPU busy this long (a bf16 GEMM and a 256 MB copy, "
-                         "alternating) so the timed steps do not measure the clocks' ramp out of idle; recorded "
-                         "in config.clock_warmup_ms")
     ap.add_argument("--lr", type=float, default=1e-4, help="SGD learning rate (reference: 1e-4)")
     ap.add_argument("--transport-tune", action=argparse.BooleanOptionalAction, default=None,
                     help="before the model is built, time the fc exchange's collectives at each candidate "
@@ -612,28 +608,6 @@ def _tune_transport(args, store, rank: int, world: int) -> dict:
     return res
 
 
-def _clock_warmup(device, ms: float) -> None:
-    """Keep the GPU busy for ``ms`` of wall time before the warmup steps: an idle MI355X steps
-    up its clocks over tens of milliseconds, and the kernel traces of the driver's command show the
-    first ~20 steps 15 % slower than the steady ones (docs/KERNELS.md).  Neither a training step
-    nor part of the timed region."""
-    a = torch.randn(4096, 4096, device=device, dtype=torch.bfloat16)
-    b = torch.randn(4096, 4096, device=device, dtype=torch.bfloat16)
-    src = torch.empty(1 << 26, device=device, dtype=torch.float32)  # (below the step's own peak memory)
-    dst = torch.empty_like(src)
-    torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    gemm = os.environ.get("TDS_CLOCK_WARMUP", "mixed") != "copy"
-    while (time.perf_counter() - t0) * 1e3 < ms:
-        for _ in range(8):
-            if gemm:
-                torch.mm(a, b)
-            dst.copy_(src)
-        torch.cuda.synchronize(device)
-    del a, b, src, dst
-    torch.cuda.empty_cache()
-
-
 def _teardown(abort: bool) -> None:
     from torch_distributed_sandbox_amd.parallel import distributed as tdist
     from torch_distributed_sandbox_amd.parallel.rccl_backend import native_comm_of
@@ -859,9 +833,6 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             torch.cuda.synchronize()
 
     loss = None
-    if on_gpu and args.clock_warmup_ms > 0:
-        phase[0] = f"attempt {k} ({backend}): clock warm-up"
-        _clock_warmup(device, args.clock_warmup_ms)
     phase[0] = f"attempt {k} ({backend}): warmup"
     for i in range(args.warmup):
         fault.maybe_inject_bench(rank, "step")
@@ -922,7 +893,6 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
                       else "fp32 image"),
             "rccl_max_ctas": rccl_max_ctas or None,
             "optimizer": f"SGD(lr={args.lr:g})",
-            "clock_warmup_ms": args.clock_warmup_ms if on_gpu else None,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 3) if on_gpu else None,
             "final_loss": final_loss,
         }

@@ -1,25 +1,21 @@
-// Fused ConvNet kernels (everything except conv2, see conv2_bf16x3.hip).
-// Reference model: mnist_onegpu.py:11-31; SURVEY.md §2.4 K1-K4, K6-K18, K22-K25.
-//
+// Fused ConvNet kernels: layer 1 (forward and backward) and the small reductions around the conv2 /
+// head kernels (conv2: conv2_fwd2.hip, conv2_bwd.hip; head: head_pb.hip; the input op with the x
+// moments: ups_moments.hip).  Reference model: mnist_onegpu.py:11-31; SURVEY.md §2.4 K1-K4, K6, K22-K25.
 // Forward
-//   x_autocorr      : 9x9 autocorrelation + border strips of x -> Gram G = sum xpatch xpatch^T
-//                     and S = sum xpatch (l1_gram).  BN1 statistics follow in closed form
-//                     (sum y1 - b1 = w1.S, sum (y1 - b1)^2 = w1^T G w1), so conv1 runs ONCE;
-//                     G and S are reused by the closed-form conv1 weight gradient.
-//   l1_conv         : conv1 (bf16x3 MFMA), BN1 affine, ReLU, 2x2 max-pool -> p1 (fp16 NHWC, 32-B
-//                     records: conv2's single-rounded operand) and a 1-byte argmax per pooled
-//                     value; y1 is never written (2.88 GB saved).
-//   [conv2 fwd + BN2 stats]
-//   head_fwd        : BN2 affine + ReLU + 2x2 pool + fc, one pass over y2 and W (p2 never stored).
+//   l1_reduce_gram  : one launch after the input op: the x moments' column sums and border strips ->
+//                     Gram G = sum xpatch xpatch^T and S = sum xpatch; BN1's statistics in closed form
+//                     (sum y1 - b1 = w1.S, sum (y1 - b1)^2 = w1^T G w1), so conv1 runs ONCE; 64 more
+//                     workgroups pack conv2's weights (conv2_pack.h).
+//   l1_conv_bf3     : conv1 (bf16x2 MFMA on the uint8 levels, bf16x3 on an fp32 image), BN1 affine,
+//                     2x2 max-pool, ReLU -> p1 (fp16 NHWC, 32-B records: conv2's single-rounded
+//                     operand) and a 1-byte argmax per pooled value; y1 is never written.
 // Backward
-//   head_bwd        : recomputes p2; dW = dlogits^T p2 straight into the DDP bucket, g2 =
-//                     dlogits W masked by ReLU (pooled grad), BN2 reductions sum dz, sum dz*y.
-//   dy2_build       : max-pool/ReLU/BN2 backward -> dy2 = k1*dz + k2*y2 + k3 as bf16 hi|lo.
-//   [conv2 dgrad, conv2 wgrad]
-//   l1_bwd          : sparse layer-1 backward: dz1 is non-zero only at the argmax of each
-//                     pooled window with p1 > 0, so per (pooled pixel, channel) one y1 value
-//                     (25 FMA) and one rank-1 update of sum dz1 x xpatch (25 FMA).
-//   l1_finalize     : dW1 = a1*sum(dz1 xpatch) + a2*(W1 G + b1 S) + a3*S, db1, dgamma1, dbeta1.
+//   l1_bwd_mfma     : dz1 is non-zero only at the argmax of each pooled window with p1 > 0:
+//                     sum dz1 x xpatch as one MFMA product per tile (bf16x3 / bf16x2 split).
+//   l1_reduce_finalize : the per-workgroup partials' reduction and
+//                     dW1 = a1*sum(dz1 xpatch) + a2*(W1 G + b1 S) + a3*S, db1, dgamma1, dbeta1.
+// Separate-launch forms kept as ops (tests/test_fused_gpu.py, tools/micro; not in the default step):
+//   l1_gram, bn_finalize_shifted, bn_reduce_finalize, reduce_partials, bn_bwd_finalize2, l1_finalize.
 #include <cstdlib>
 
 #include "bf16x3.h"
@@ -118,19 +114,26 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
       tp = l1b_tap(g, j);
       koff[j] = tp >= 0 ? (tp / 5) * L1_XS + (tp % 5) : 1;  // pad: tap (0, 1) (odd word: opposite bank parity to g = 0 j = 7)
     }
-    const float wv = tp >= 0 ? w1[li * 25 + tp] : 0.f;
+    // channel li's weights carry the sign of its BN1 scale (below)
+    const float wv = tp >= 0 ? (aff[li] < 0.f ? -w1[li * 25 + tp] : w1[li * 25 + tp]) : 0.f;
     unsigned short h, l;
     split_bf16(wv, h, l);
     wah[j] = (short)h;
     wal[j] = (short)l;
   }
 
-  // per-lane epilogue constants for co = 4g + r: z = ea * (acc + b1) + eb = ea * acc + ebb
+  // per-lane epilogue constants for co = 4g + r: z = ea * (acc + b1) + eb = ea * acc + ebb.  The
+  // weights of a channel with ea < 0 are negated (exact), so acc holds -acc and z = |ea| * acc + ebb
+  // bit for bit: BN1's affine is then increasing in acc, the 2x2 max-pool picks the window's largest
+  // ACCUMULATOR and the affine runs once per pooled value instead of once per pixel (the epilogue's
+  // VALU bounds this kernel).  A window whose top two pixels round to one z keeps the larger acc
+  // (torch: the first in scan order) -- as the conv2 forward's pooling on y2 does.
   float ea[4], ebb[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    ea[r] = aff[4 * g + r];
-    ebb[r] = fmaf(ea[r], b1[4 * g + r], aff[16 + 4 * g + r]);
+    const float a = aff[4 * g + r];
+    ebb[r] = fmaf(a, b1[4 * g + r], aff[16 + 4 * g + r]);
+    ea[r] = fabsf(a);
   }
   bool fin = true;
 #pragma unroll
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
             else
               acc[a][c] = mfma_bf16x3(wah, wal, bh, bl, f32x4{0.f, 0.f, 0.f, 0.f});
           }
-        // BN1 affine -> 2x2 max-pool (first max in scan order) -> ReLU -> bf16 hi|lo record +
+        // BN1 affine -> 2x2 max-pool (first max in scan order) -> ReLU -> fp16 record +
         // argmax byte (bit 2 = ReLU passes the gradient) for channels 4g .. 4g+3
         const int prow = (r0 + 4 * wv + 2 * rp) >> 1;
         const int pcol = (c0 >> 1) + 16 * sp + li;
@@ -266,32 +269,31 @@ __global__ __launch_bounds__(256) void l1_conv_bf3_kernel(const void* __restrict
         uint32_t ixw = 0;
         // scan order: (row 0, col 0), (row 0, col 1), (row 1, col 0), (row 1, col 1)
         if (!slow) {  // every z finite (tile-uniform)
-          // the affine in packed fp32 (v_pk_fma_f32 on channel pairs r, r+1 of one accumulator:
-          // adjacent registers as the MFMA left them, no moves; this epilogue, not the MFMAs,
-          // bounds the kernel)
-          float z[2][2][4];
-#pragma unroll
-          for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int c = 0; c < 2; ++c)
-#pragma unroll
-              for (int r = 0; r < 4; r += 2) {
-                const f32x2 zz = __builtin_elementwise_fma(f32x2{acc[a][c][r], acc[a][c][r + 1]},
-                                                           f32x2{ea[r], ea[r + 1]}, f32x2{ebb[r], ebb[r + 1]});
-                z[a][c][r] = zz.x;
-                z[a][c][r + 1] = zz.y;
-              }
+          float mz[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float z0 = z[0][0][r], z1 = z[0][1][r], z2 = z[1][0][r], z3 = z[1][1][r];
-            const float m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(z0, z1),
-                                                          __builtin_elementwise_maximum(z2, z3));
+            const float a0 = acc[0][0][r], a1 = acc[0][1][r], a2 = acc[1][0][r], a3 = acc[1][1][r];
+            const float m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a0, a1),
+                                                          __builtin_elementwise_maximum(a2, a3));
             // first max, branch-free (the ?: chain compiled to exec-mask branches)
-            uint32_t am = z2 == m ? 2u : 3u;
-            am = z1 == m ? 1u : am;
-            am = z0 == m ? 0u : am;
-            pv[r] = fmaxf(m, 0.f);
-            ixw |= (am | (m > 0.f ? 4u : 0u)) << (8 * r);
+            uint32_t am = a2 == m ? 2u : 3u;
+            am = a1 == m ? 1u : am;
+            am = a0 == m ? 0u : am;
+            mz[r] = m;
+            ixw |= am << (8 * r);
+          }
+          // the affine on the pooled values only, in packed fp32 (channel pairs r, r + 1)
+#pragma unroll
+          for (int r = 0; r < 4; r += 2) {
+            const f32x2 zz = __builtin_elementwise_fma(f32x2{mz[r], mz[r + 1]}, f32x2{ea[r], ea[r + 1]},
+                                                       f32x2{ebb[r], ebb[r + 1]});
+            mz[r] = zz.x;
+            mz[r + 1] = zz.y;
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            pv[r] = fmaxf(mz[r], 0.f);
+            ixw |= (mz[r] > 0.f ? 4u : 0u) << (8 * r);
           }
         } else {  // torch's rule: update when (v > max || isnan(v)), relu(NaN) = NaN
 #pragma unroll
@@ -450,7 +452,7 @@ constexpr int LB_NP = LB_PR * LB_PC;                     // pooled pixels per ti
 constexpr int LB_V_DP = LB_NP * 2, LB_V_PH = 0, LB_V_ID = LB_NP, LB_V_X = LB_XR * 18;
 constexpr int LB_V = LB_V_DP + LB_V_PH + LB_V_ID + LB_V_X;  // 16-B vectors staged per tile
 // The argmax byte carries the ReLU mask in bit 2 (set by l1_conv: pooled max > 0), so the
-// backward never reads p1 (720 MB of 64-B hi|lo records at the bench shape).
+// backward never reads p1 (360 MB of 32-B fp16 records at the bench shape).
 constexpr int LB_PER = (LB_V + 255) / 256;
 static_assert(LB_V_PH == 0 && LB_V_DP % 256 == 0 && LB_V_ID % 256 == 0, "l1_bwd prefetch classes per vector");
 // fp16 bits (low half) -> float
