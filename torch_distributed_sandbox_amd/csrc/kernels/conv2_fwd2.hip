@@ -159,7 +159,9 @@ __device__ __forceinline__ float f2_ext4(float a, float b, float c, float d, boo
 // v_maximum_f32 (|v| as a source modifier; scaled by inv once per workgroup).  A wave64 VALU
 // instruction holds its SIMD for 4 cycles, and that issue competes with the same SIMD's MFMAs.
 typedef float f2v __attribute__((ext_vector_type(2)));
-template <bool EDGE>
+// PLAIN: every lane of the wave has gamma2 > 0 (wave-uniform, the usual case): the window extreme is
+// its maximum, no minimum / select / gamma2 == 0 case
+template <bool EDGE, bool PLAIN>
 __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x, char* stage, float* ystage, int P,
                                          int RH, int NT, int lane, float bco, float inv, float ksc, bool neg, bool zg,
                                          f2v& s_acc, f2v& q_acc, uint32_t& ymx, uint32_t* __restrict__ a2) {
@@ -212,11 +214,19 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
       // gamma2 == 0 (zg): every BN2 output of the window is beta2 and torch's max-pool keeps the
       // first position: code 0, and ya holds that position's value (the head backward's dgamma2
       // reads xhat there)
-      const float m = zg ? v0 : f2_ext4(v0, v1, v2, acc[2 * i + 1][2 * j + 1], neg);
+      const float v3 = acc[2 * i + 1][2 * j + 1];
+      float m;
+      if constexpr (PLAIN)
+        m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(v0, v1), __builtin_elementwise_maximum(v2, v3));
+      else
+        m = zg ? v0 : f2_ext4(v0, v1, v2, v3, neg);
       e[j] = fmaf(m, inv, bco);
-      const bool e0 = v0 == m, e1 = v1 == m, e2 = v2 == m;  // (a NaN window: code 3, unused)
-      cb0[2 * i + j] = __builtin_amdgcn_ballot_w64(!e0 & (e1 | !e2));  // code 1 or 3
-      cb1[2 * i + j] = __builtin_amdgcn_ballot_w64(!e0 & !e1);         // code 2 or 3
+      // (a NaN window: code 3, unused); the code bits from the three comparisons' ballots by
+      // scalar logic (as lane booleans the compiler formed them with ~4 VALU selects a window)
+      const uint64_t b0 = __builtin_amdgcn_ballot_w64(v0 == m), b1 = __builtin_amdgcn_ballot_w64(v1 == m),
+                     b2 = __builtin_amdgcn_ballot_w64(v2 == m);
+      cb0[2 * i + j] = ~b0 & (b1 | ~b2);  // code 1 or 3
+      cb1[2 * i + j] = ~b0 & ~b1;         // code 2 or 3
     }
     // pcols 2g, 2g+1 are adjacent floats of one swizzled chunk: one ds_write_b64
     *reinterpret_cast<float2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_float2(e[0], e[1]);
@@ -225,26 +235,28 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
   // (word = bits 16g .. 16g+15 of each code-bit ballot: channels 16NT + 0..15); f2_store_a2 writes
   // the tile's 32 windows as 4 rows of 64 B
   {
-    const uint32_t sh = 16u * (uint32_t)g;
     uint32_t* ab = reinterpret_cast<uint32_t*>(ystage + 32 * 32);
+    // group g's 16 bits of each ballot: the 32-bit half (g >= 2: upper), then one byte permute takes
+    // bits 16(g & 1) .. +15 of both code-bit words (a 64-bit shift by the per-lane 16g cost ~9 VALU a window)
+    const bool upper = g >= 2;
+    const uint32_t psel = (g & 1) ? 0x07060302u : 0x05040100u;
     if (li == 0) {
 #pragma unroll
-      for (int sl = 0; sl < 4; ++sl)
-        ab[((2 * RH + (sl >> 1)) * 8 + 2 * g + (sl & 1)) * 2 + NT] =
-            ((uint32_t)(cb0[sl] >> sh) & 0xFFFFu) | ((uint32_t)(cb1[sl] >> sh) << 16);
+      for (int sl = 0; sl < 4; ++sl) {
+        const uint32_t w0 = upper ? (uint32_t)(cb0[sl] >> 32) : (uint32_t)cb0[sl];
+        const uint32_t w1 = upper ? (uint32_t)(cb1[sl] >> 32) : (uint32_t)cb1[sl];
+        ab[((2 * RH + (sl >> 1)) * 8 + 2 * g + (sl & 1)) * 2 + NT] = __builtin_amdgcn_perm(w1, w0, psel);
+      }
     }
   }
-  // the y2h halves: even lanes join their odd neighbour's (channel co + 1) by a quad-permute DPP
-  // move and write the pair (row, px) of channels co, co + 1
+  // the y2h values: every lane writes its channel's half-word (no cross-lane pairing: the DPP move
+  // and the pack cost 2 VALU per value)
 #pragma unroll
   for (int o = 0; o < 4; ++o)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t nb = (uint32_t)__builtin_amdgcn_mov_dpp((int)h[o][r], 0xF5, 0xF, 0xF, false);  // quad [1,1,3,3]
-      if ((li & 1) == 0)
-        *reinterpret_cast<uint32_t*>(stage + (((4 * RH + o) * F2_TC + 4 * g + r) * F2_PXREC) + co * 2) =
-            (h[o][r] & 0xFFFFu) | (nb << 16);
-    }
+    for (int r = 0; r < 4; ++r)
+      *reinterpret_cast<unsigned short*>(stage + (((4 * RH + o) * F2_TC + 4 * g + r) * F2_PXREC) + co * 2) =
+          (unsigned short)h[o][r];
 }
 
 // the workgroup stores the staged pooled block: thread e -> channel e / 8, float4 e % 8
@@ -323,6 +335,7 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
   const float ksc = scales != nullptr ? __uint_as_float(scales[2]) : 1.f;  // y2h store factor
   const bool neg = gamma != nullptr && gamma[16 * NT + li] < 0.f;
   const bool zg = gamma != nullptr && gamma[16 * NT + li] == 0.f;
+  const bool plain = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_ballot_w64(neg || zg) == 0 ? 1 : 0) != 0;
   const PBGeom pg = pb_geom(P / 2);
   float* ys = reinterpret_cast<float*>(smem + F2_OFF_Y);
   // BN2 partials: each tile's sums in fp32 (<= 16 values per lane), accumulated across the
@@ -349,11 +362,14 @@ __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4
       f2_store_a2(ys + ((kk + 1) & 1) * (F2_YSTAGE / 4), prev, a2, P);
     }
     f2_compute<DIAG>(smem + (kk & 1) * F2_PBUF, W, acc, RH, lane);
-    if (cur.r0 + F2_TH <= P && cur.c0 + F2_TC <= P)  // tile-uniform
-      f2_stage<false>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
+    if (cur.r0 + F2_TH <= P && cur.c0 + F2_TC <= P && plain)  // tile- and wave-uniform
+      f2_stage<false, true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT,
+                            lane, bco, inv, ksc, neg, zg, s_acc, q_acc, ymx, a2);
+    else if (cur.r0 + F2_TH <= P && cur.c0 + F2_TC <= P)
+      f2_stage<false, false>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
                       bco, inv, ksc, neg, zg, s_acc, q_acc, ymx, a2);
     else
-      f2_stage<true>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
+      f2_stage<true, false>(acc, cur, smem + F2_OFF_S + (kk & 1) * F2_STAGE, ys + (kk & 1) * (F2_YSTAGE / 4), P, RH, NT, lane,
                      bco, inv, ksc, neg, zg, s_acc, q_acc, ymx, a2);
     s_d += (double)(s_acc.x + s_acc.y);
     q_d += (double)(q_acc.x + q_acc.y);
