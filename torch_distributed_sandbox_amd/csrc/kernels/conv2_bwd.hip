@@ -636,17 +636,22 @@ struct BRStager {
         for (int cc = 0; cc < BR_CW; ++cc) {
           // y2h values straight into v_fma_mix_f32 (br_fma_y)
           auto fy = [&](float k, int q, float c) { return br_fma_y(k, yv[u][q], cc, c); };
-          const uint32_t code = ((cw >> cc) & 1u) | ((cw >> (15 + cc)) & 2u);  // the forward's argmax
-          // the pooled gradient folded into the constant: select + FMA per pixel.  The 4 compares
-          // go first (4 SGPR-pair masks): one VCC reused compare -> select -> compare cost an
-          // s_nop per pixel for the VALU-mask hazard
+          // the pooled gradient folded into the constant: k3g at the window's argmax, k3 elsewhere
           const float k3g = fmaf(k1[cc], gv[u][cc], k3[cc]);
-          bool eq[4];
+          // by bit-field selects on the code's two bits sign-extended to masks (bit cc: column, bit
+          // 16 + cc: row of the argmax): 2 + 6 VALU a channel instead of the code, 4 compares and
+          // 4 selects (and no VALU-written lane masks)
+          const uint32_t mx = (uint32_t)__builtin_amdgcn_sbfe((int)cw, cc, 1);
+          const uint32_t my = (uint32_t)__builtin_amdgcn_sbfe((int)cw, 16 + cc, 1);
+          const uint32_t ug = __float_as_uint(k3g), u3 = __float_as_uint(k3[cc]);
+          // v_bitop3_b32 with truth table 0xCA = S0 ? S1 : S2 bitwise (the intrinsic keeps the
+          // optimizer from turning the masks back into compares and selects)
+          auto mux = [](uint32_t m, uint32_t x, uint32_t y) { return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA); };
+          const uint32_t t0 = mux(mx, u3, ug), t1 = mux(mx, ug, u3);  // row hit: column 0 / 1 is the argmax
+          const float c[4] = {__uint_as_float(mux(my, u3, t0)), __uint_as_float(mux(my, u3, t1)),
+                              __uint_as_float(mux(my, t0, u3)), __uint_as_float(mux(my, t1, u3))};
 #pragma unroll
-          for (int q = 0; q < 4; ++q) eq[q] = code == (uint32_t)q;
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) d[q][cc] = fy(k2[cc], q, eq[q] ? k3g : k3[cc]);
+          for (int q = 0; q < 4; ++q) d[q][cc] = fy(k2[cc], q, c[q]);
         }
       } else {
         const int gy = R0 + 2 * wy, gx = c0 - 2 + 2 * wx;
