@@ -51,19 +51,28 @@ from ..ops import grad_sink
 from . import distributed as tdist
 from . import factored
 
-def _weak_call(obj, name: str):
+class _weak_call:
     """``obj.<name>`` as a callable that holds ``obj`` weakly (a no-op once it is gone).  Hooks and
     providers attached to parameters or to autograd nodes must not keep the wrapper alive: the
     cycle parameter -> hook -> wrapper -> module -> parameter runs through C++ that Python's
     collector cannot see, and every model built after it would find its predecessor's buffers
-    still allocated (round 6: 0.72 GB per ConvNet at 3000^2, tools/oom_demo.py)."""
-    ref = weakref.ref(obj)
+    still allocated (round 6: 0.72 GB per ConvNet at 3000^2, tools/oom_demo.py).  ``__self__``
+    names the live owner as a bound method's does (ops/optim.py finds the deferred runner's owner
+    through it)."""
 
-    def call(*args):
-        o = ref()
-        return None if o is None else getattr(o, name)(*args)
+    __slots__ = ("_ref", "_name")
 
-    return call
+    def __init__(self, obj, name: str):
+        self._ref = weakref.ref(obj)
+        self._name = name
+
+    @property
+    def __self__(self):
+        return self._ref()
+
+    def __call__(self, *args):
+        o = self._ref()
+        return None if o is None else getattr(o, self._name)(*args)
 
 
 _ALIGN_ELEMS = 64  # 256-byte alignment of every parameter slot in the flat buffers
