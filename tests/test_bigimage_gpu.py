@@ -162,15 +162,26 @@ def test_one_step_beyond_2gib(gpu):
         sdzx += (dz * xh).sum((1, 2))
     dw2 = torch.zeros(32, 400, dtype=torch.float64, device=gpu)
     db2 = torch.zeros(32, dtype=torch.float64, device=gpu)
+    sady = torch.zeros(32, dtype=torch.float64, device=gpu)
     for r0 in range(0, P, ROWS):
         cols, dz, xh = chunk(r0, min(P, r0 + ROWS))
         dy = a2.view(-1, 1, 1) * (dz - (sdz / n2).view(-1, 1, 1) - xh * (sdzx / n2).view(-1, 1, 1))
         dw2 += dy.reshape(32, -1) @ cols.t()
         db2 += dy.sum((1, 2))
+        sady += dy.abs().sum((1, 2))
     rel = ((dw2_ours.double().view(32, 400) - dw2).norm() / dw2.norm()).item()
     # fp16x2-class rounding amplified by BN2's backward over 144 M positions (the 64^2 model test
     # measures 1.1e-2 for this gradient against 3.2e-2 for TF32 convolutions); an index wrap is O(1)
     print(f"fc tail max err {ft_err:.3e}, layer2.0.weight grad rel L2 err {rel:.3e}")
     assert rel <= 5e-2, f"layer2.0.weight grad rel L2 err {rel:.2e}"
-    # conv bias before BN: analytically zero, both sides rounding noise
-    assert (db2_ours.double() - db2).abs().max().item() <= 1e-3 * dw2.abs().max().item() + 1e-9
+    # conv bias before BN: analytically zero (and cancelled by BN2 in the forward), both sides rounding
+    # noise -- dy2 is rounded once to 11 significant bits per element (the TF32 class), so the sum is
+    # off by at most 2^-11 sum |dy2| per channel (as tests/test_fused_gpu.py's conv2 backward test);
+    # an index wrap gives O(sum |dy2|).  (Measured r6_s21: a max error of 2.7e-3 with g2m stored in
+    # fp16, 4.2e-4 with g2m in fp32 -- the pooled gradient's extra rounding at the windows' argmax
+    # shows in this sum of 144 M cancelling terms; the weight gradient above moved 2.30 -> 2.41e-2)
+    db2_err = (db2_ours.double() - db2).abs()
+    bound = sady * 2.0 ** -11 * 1.01 + 1e-9
+    print(f"conv2 bias grad max err {db2_err.max().item():.3e}, its bound min {bound.min().item():.3e}; "
+          f"ours max {db2_ours.abs().max().item():.3e}, ref max {db2.abs().max().item():.3e}")
+    assert bool((db2_err <= bound).all()), (db2_err.max().item(), bound.min().item())

@@ -1,11 +1,12 @@
 // Plan-level ops of the fused ConvNet execution (torch.ops.tdsa.fused_*).
 // Each op = a few kernel launches on the current stream, all shapes checked on
 // the host first.  Activation formats:
-//   p1          [B,P,P,16] fp16 (conv2's single-rounded fp16x2 operand; its fp32 gradient dp1
-//               [B,P,P,16] travels to the layer-1 backward beside autograd, models/convnet_fused.py)
-//   y2          [B,P,P,32] f32
+//   p1          [B,P,P,16] fp16 (conv2's single-rounded operand)
+//   y2h         [B,P,P,32] fp16 (the conv2 output the backward re-reads, bias-free, scaled)
 //   ya          [B,32,PB] f32: pooled-blocked planes (kernels/pooled_layout.h)
-//   g2m         [B,32,Q,Q] f32: planar pooled gradient
+//   g2m         [B,32,Q,Q] fp16: planar pooled gradient at a per-channel power-of-two scale 2^e_c
+//               bounded by the head forward's max |W| per channel and class (kernels/head_pb.hip);
+//               kbuf[96 + c] = 2^-e_c (kbuf = [k1 | k2 | k3 | g2m scales], 128 floats)
 //   mag         int32 workspace [mag_numel(B, P)]: the step's magnitude bounds (float bits) behind
 //               the conv2 backward's fp16 gradient scale -- [0,32) max |y2 - b2| per channel, [32]
 //               max |g2m|, then per-workgroup maxima from the conv2 forward (ypart [32][nwg])
@@ -144,7 +145,7 @@ const int* bwd_walk(const Tensor& like, int B, int tiles_r, int tiles_c, int nwg
 int64_t pb_plane(int64_t P) { return tds_pb_plane((int)(P / 2)); }
 
 // ---------------------------------------------------------------- the step's magnitude-bound workspace
-constexpr int64_t kG2mSlack = 16;   // floats past g2m's end its allocations carry (conv2_bwd.hip GB runs)
+constexpr int64_t kG2mSlack = 32;   // fp16 elements (64 B) past g2m's end its allocations carry (conv2_bwd.hip GB runs)
 constexpr int64_t kMagParts = 64;   // ypart offset in the mag workspace
 constexpr int64_t kMagScales = 40;  // conv2 epilogue scales (csrc/kernels/conv2_common.h)
 int64_t mag_ypart_count() { return (int64_t)tds_conv2_fwd2_num_wg(); }
@@ -635,9 +636,11 @@ Tensor conv2_bwd_clock_dump(int64_t nwg) {
   return t;
 }
 
+// the BN2 partials [32][npass * nblk][4] (fp32 dz / stored dz sums), then 16 doubles = g2m's 32 per-channel scales 2^-e_c (fp32)
+// for the K-chunked launches (the finalizing call copies them into kbuf[96..128))
 int64_t head_bwd_workspace(int64_t B, int64_t P) {
   const int Q = (int)(P / 2);
-  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_bwd_pb_nblk(Q) * 2;
+  return (int64_t)32 * tds_head_bwd_pb_npass((int)B) * tds_head_bwd_pb_nblk(Q) * 4 + 16;
 }
 
 // Channels [c_begin, c_end) of the head backward (K-chunked fc gradient): the caller passes the
@@ -682,13 +685,15 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
               "fused_head_backward: update_lr needs compute_dw and a batch of <= 8 images");
   Tensor g2m;
   if (g2m_out.has_value() && g2m_out->defined()) {
-    need(*g2m_out, at::kFloat, {B, 32, Q, Q}, "g2m_out");
+    need(*g2m_out, at::kHalf, {B, 32, Q, Q}, "g2m_out");
     g2m = *g2m_out;
   } else {
     TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into g2m_out");
     // planar (the fc flatten order), with the 64 B of slack the conv2 backward's row loads may
     // touch past the last row (conv2_bwd.hip BRStager GB)
-    g2m = at::empty({B * 32 * Q * Q + kG2mSlack}, ya.options()).narrow(0, 0, B * 32 * Q * Q).view({B, 32, Q, Q});
+    g2m = at::empty({B * 32 * Q * Q + kG2mSlack}, ya.options().dtype(at::kHalf))
+              .narrow(0, 0, B * 32 * Q * Q)
+              .view({B, 32, Q, Q});
   }
   const int nblk = tds_head_bwd_pb_nblk((int)Q), npass = tds_head_bwd_pb_npass((int)B);
   Tensor partial;
@@ -697,8 +702,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     partial = *partial_out;
   } else {
     TORCH_CHECK(whole, "fused_head_backward: a channel chunk writes into partial_out");
-    partial = at::empty({(int64_t)32 * npass * nblk * 2}, ya.options().dtype(at::kDouble));
+    partial = at::empty({head_bwd_workspace(B, P)}, ya.options().dtype(at::kDouble));
   }
+  // g2m's per-channel scales 2^-e_c: straight into kbuf[96..128) for a whole-weight call, into the
+  // workspace tail for the channel chunks (copied at the finalizing call)
+  auto kbuf = at::empty({128}, ya.options());
+  float* g2inv_tail = reinterpret_cast<float*>(partial.data_ptr<double>() + (int64_t)32 * npass * nblk * 4);
+  float* g2inv = whole ? kbuf.data_ptr<float>() + 96 : g2inv_tail;
+  auto* g2p = reinterpret_cast<unsigned short*>(g2m.data_ptr<at::Half>());
   uint32_t* gp = opt_mag(mag, mag_numel(B, P)) ? opt_mag(mag) + kMagParts + 32 * mag_ypart_count() : nullptr;
   // the BN2 backward finalize inside the head backward's launch (head_pb.hip HBFin): one pass over
   // all channels, with the conv2 forward having reduced its magnitude parts (ypart_done)
@@ -708,26 +719,25 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   if (fin_in) {
     auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
     auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");
-    auto kbuf = at::empty({96}, ya.options());
     auto dbfc = sink_or_empty(dbfc_out, {NC}, ya, "dbfc_out");
     auto cmax = at::empty({32}, ya.options().dtype(at::kInt));
     TdsHeadBwdFin hf{reinterpret_cast<uint32_t*>(cmax.data_ptr<int>()), stats2.data_ptr<float>(), g,
                      dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), dbfc.data_ptr<float>(),
                      opt_mag(mag, mag_numel(B, P))};
     const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
-                                   dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
+                                   dlogits.data_ptr<float>(), g2p, partial.data_ptr<double>(),
                                    compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                    upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
-                                   (float)scale, (float)update_lr, 0, 32, gp, st, &hf);
+                                   (float)scale, (float)update_lr, 0, 32, gp, g2inv, st, &hf);
     TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
     check_launches("fused_head_backward");
     return {dW, dbfc, dgamma, dbeta, g2m, kbuf};
   }
   const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
-                                 dlogits.data_ptr<float>(), g2m.data_ptr<float>(), partial.data_ptr<double>(),
+                                 dlogits.data_ptr<float>(), g2p, partial.data_ptr<double>(),
                                  compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                  upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
-                                 (float)scale, (float)update_lr, (int)c_begin, (int)c_end, gp, st);
+                                 (float)scale, (float)update_lr, (int)c_begin, (int)c_end, gp, g2inv, st);
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
   if (!finalize) {
     check_launches("fused_head_backward");
@@ -736,7 +746,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   }
   auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
   auto dbeta = sink_or_empty(dbe_out, {32}, ya, "dbeta2_out");
-  auto kbuf = at::empty({96}, ya.options());
+  if (!whole) kbuf.narrow(0, 96, 32).copy_(partial.narrow(0, (int64_t)32 * npass * nblk * 4, 16).view(at::kFloat));
   auto dbfc = sink_or_empty(dbfc_out, {NC}, ya, "dbfc_out");
   uint32_t* m = opt_mag(mag, mag_numel(B, P));
   tds_bn_bwd_finalize2(partial.data_ptr<double>(), 32, npass * nblk, B * P * P, g, stats2.data_ptr<float>(),
@@ -765,12 +775,12 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   need(y2, at::kHalf, {B, P, P, 32}, "y2h (fused_conv2_forward's)");
   need(a2, at::kInt, {B, P / 2, P / 2, 2}, "a2 (fused_conv2_forward's pooling argmax codes)");
   need(b2, at::kFloat, {32}, "conv2.bias");
-  need(g2m, at::kFloat, {B, 32, P / 2, P / 2}, "g2m");
-  TORCH_CHECK((int64_t)g2m.storage().nbytes() >= (g2m.storage_offset() + g2m.numel() + kG2mSlack) * 4,
-              "fused_conv2_backward_y2: g2m needs ", kG2mSlack, " floats of slack after it (as fused_head_backward "
-              "allocates it): the staging's row loads may read past the last row");
+  need(g2m, at::kHalf, {B, 32, P / 2, P / 2}, "g2m (fused_head_backward's, fp16 at the scales in kbuf[96..128))");
+  TORCH_CHECK((int64_t)g2m.storage().nbytes() >= (g2m.storage_offset() + g2m.numel() + kG2mSlack) * 2,
+              "fused_conv2_backward_y2: g2m needs ", kG2mSlack, " fp16 elements of slack after it (as "
+              "fused_head_backward allocates it): the staging's row loads may read past the last row");
   need(aff2, at::kFloat, {64}, "aff2");
-  need(kbuf, at::kFloat, {96}, "kbuf");
+  need(kbuf, at::kFloat, {128}, "kbuf");
   need(wd, at::kShort, {25 * 4 * 16 * 8}, "conv2 dgrad pack");
   TORCH_CHECK(B <= 63 && P >= 2, "fused_conv2_backward_y2: 1 <= batch <= 63 and P >= 2");
   c10::DeviceGuard guard(p1.device());
@@ -784,7 +794,8 @@ std::tuple<Tensor, Tensor, Tensor> fused_conv2_backward_y2(const Tensor& y2, con
   auto slab = at::empty({(int64_t)nwg * 26 * 512}, p1.options().dtype(at::kFloat));
   auto dw2 = sink_or_empty(dw_out, {32, 16, 5, 5}, p1, "dw2_out");
   auto db2 = sink_or_empty(db_out, {32}, p1, "db2_out");
-  tds_conv2_bwd3(y2.data_ptr(), reinterpret_cast<const uint32_t*>(a2.data_ptr<int>()), g2m.data_ptr<float>(), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
+  tds_conv2_bwd3(y2.data_ptr(), reinterpret_cast<const uint32_t*>(a2.data_ptr<int>()),
+                 reinterpret_cast<const unsigned short*>(g2m.data_ptr<at::Half>()), aff2.data_ptr<float>(), kbuf.data_ptr<float>(),
                  b2.data_ptr<float>(), reinterpret_cast<uint32_t*>(mag.data_ptr<int>()), p1.data_ptr(),
                  wd.data_ptr<int16_t>(),
                  dp1.data_ptr(), slab.data_ptr<float>(), order, nwg, sw, sk, (int)B, (int)P, st);

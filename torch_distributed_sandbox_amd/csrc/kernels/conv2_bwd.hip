@@ -103,7 +103,7 @@ __device__ __forceinline__ BRTile br_decode(const int* __restrict__ walk, int k,
 struct BRArgs {
   const uint2* __restrict__ y2;  // y2h [B][P][P][32] fp16 (conv2_common.h)
   const uint32_t* __restrict__ a2;  // the forward's pooling argmax codes [B][Q][Q][2] (conv2_common.h)
-  const float* __restrict__ g2m;  // planar [B][32][Q][Q] (the fc flatten order)
+  const unsigned short* __restrict__ g2m;  // fp16 planar [B][32][Q][Q] (the fc flatten order), scale 2^e_c
   const uint4* __restrict__ p1;
   uint2* __restrict__ dp1;  // dp1h (conv2_common.h)
   float* __restrict__ slab;
@@ -426,8 +426,8 @@ struct BRStager {
   float gv[IPER][BR_CW];
   uint32_t av[IPER];    // a2: the window's argmax codes, 16 channels
   uint4 pr[PPER];
-  float4 rm0, rm1;      // GB: this lane's run, columns 1-4 and 5-8
-  float rl, rr;         // GB: its columns 0 and 9 (the halo)
+  uint4 rm;             // GB: this lane's run, columns 1-8 (fp16)
+  uint32_t rl, rr;      // GB: its columns 0 and 9 (the halo; fp16 in the low half)
 
   // the j-th p1 piece of staging lane tid: the set past 256 goes to a wave without an item (waves
   // 4-6 hold the 160 items, the extra pieces go to wave 7)
@@ -481,17 +481,18 @@ struct BRStager {
       const bool lok = row & (px0 >= 0), rok = row & (px0 + 9 < Q);
       const int64_t e0 = (int64_t)c * gplane + (int64_t)wy * Q;  // element of column 0, from rg's base
       if constexpr (!BIG) {
-        const uint32_t o = (uint32_t)(e0 * 4);
-        rl = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, lok ? o : kBROob, 0, 0));
-        rm0 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 4 : kBROob, 0, 0));
-        rm1 = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 20 : kBROob, 0, 0));
-        rr = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, rok ? o + 36 : kBROob, 0, 0));
+        // fp16: the 8 inner columns in one (2-B aligned) 16-B load, the halo columns in 2-B loads
+        const uint32_t o = (uint32_t)(e0 * 2);
+        rl = __builtin_amdgcn_raw_buffer_load_b16(rg, lok ? o : kBROob, 0, 0);
+        rm = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rg, row ? o + 2 : kBROob, 0, 0));
+        rr = __builtin_amdgcn_raw_buffer_load_b16(rg, rok ? o + 18 : kBROob, 0, 0);
       } else {
-        const float* gp = a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0 + (row ? e0 : 0);
-        rl = lok ? gp[0] : 0.f;  // (BIG: 64-bit loads; the rare >4 GiB-per-image shapes)
-        rm0 = *reinterpret_cast<const float4*>(gp + 1);
-        rm1 = *reinterpret_cast<const float4*>(gp + 5);
-        rr = rok ? gp[9] : 0.f;
+        const unsigned short* gp = a.g2m + (int64_t)b * 32 * gplane + (int64_t)py0 * Q + px0 + (row ? e0 : 0);
+        rl = lok ? gp[0] : 0u;  // (BIG: 64-bit loads; the rare >4 GiB-per-image shapes)
+        const unsigned short* mp = gp + 1;
+        rm = make_uint4((uint32_t)mp[0] | ((uint32_t)mp[1] << 16), (uint32_t)mp[2] | ((uint32_t)mp[3] << 16),
+                        (uint32_t)mp[4] | ((uint32_t)mp[5] << 16), (uint32_t)mp[6] | ((uint32_t)mp[7] << 16));
+        rr = rok ? gp[9] : 0u;
       }
     }
     const int cb = (tid % BR_NCH) * BR_CW;  // the chunk's first channel (256 % BR_NCH == 0: every u)
@@ -515,16 +516,16 @@ struct BRStager {
       if constexpr (GB) {
         // (from the LDS tile in store())
       } else if constexpr (!BIG) {
-        const uint32_t og = (uint32_t)(((int64_t)cb * gplane + (int64_t)wy * Q + wx) * 4);
-        const uint32_t gstep = (uint32_t)(gplane * 4);
+        const uint32_t og = (uint32_t)(((int64_t)cb * gplane + (int64_t)wy * Q + wx) * 2);
+        const uint32_t gstep = (uint32_t)(gplane * 2);
 #pragma unroll
         for (int k = 0; k < BR_CW; ++k)
-          gv[u][k] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rg, pooled ? og + k * gstep : kBROob,
-                                                                                    0, 0));
+          gv[u][k] = f16_val(__builtin_amdgcn_raw_buffer_load_b16(rg, pooled ? og + k * gstep : kBROob, 0, 0));
       } else {
-        const float* gp = a.g2m + ((int64_t)b * 32 + cb) * gplane + (int64_t)(pooled ? py : 0) * Q + (pooled ? px : 0);
+        const unsigned short* gp =
+            a.g2m + ((int64_t)b * 32 + cb) * gplane + (int64_t)(pooled ? py : 0) * Q + (pooled ? px : 0);
 #pragma unroll
-        for (int k = 0; k < BR_CW; ++k) gv[u][k] = gp[k * gplane];  // masked at use (store: pooled)
+        for (int k = 0; k < BR_CW; ++k) gv[u][k] = f16_val(gp[k * gplane]);  // masked at use (store: pooled)
       }
     }
 #pragma unroll
@@ -546,10 +547,10 @@ struct BRStager {
     if (rt < 0) return;
     const int c = rt & 31, wy = rt >> 5;
     float* d = gb + wy * 10 * 32 + c;
-    d[0] = rl;
-    d[32] = rm0.x; d[64] = rm0.y; d[96] = rm0.z; d[128] = rm0.w;
-    d[160] = rm1.x; d[192] = rm1.y; d[224] = rm1.z; d[256] = rm1.w;
-    d[288] = rr;
+    d[0] = f16_val(rl);
+    d[32] = f16_val(rm.x); d[64] = f16_val(rm.x >> 16); d[96] = f16_val(rm.y); d[128] = f16_val(rm.y >> 16);
+    d[160] = f16_val(rm.z); d[192] = f16_val(rm.z >> 16); d[224] = f16_val(rm.w); d[256] = f16_val(rm.w >> 16);
+    d[288] = f16_val(rr);
   }
 
   // BN2 / ReLU / pool backward of the staged windows -> dy2 rows at dbase; p1 -> pbase;
@@ -800,7 +801,7 @@ __device__ __forceinline__ void br_stage(const BRArgs& a, char* smem) {
 
 template <int DIAG, bool BIG>
 __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
-    const uint2* __restrict__ y2, const uint32_t* __restrict__ a2, const float* __restrict__ g2m,
+    const uint2* __restrict__ y2, const uint32_t* __restrict__ a2, const unsigned short* __restrict__ g2m,
     const float* __restrict__ aff2, const float* __restrict__ kbuf, const float* __restrict__ b2,
     const uint32_t* __restrict__ mag,
     const uint4* __restrict__ p1,
@@ -840,7 +841,7 @@ __global__ __launch_bounds__(BR_THREADS, 2) void conv2_bwd_roll_kernel(
       const float ka = aff2[c], kb = aff2[32 + c], bc = b2[c];
       kc[c] = ka * d;
       kc[32 + c] = fmaf(ka, bc, kb);
-      kc[64 + c] = k1 * sc;
+      kc[64 + c] = k1 * sc * kbuf[96 + c];  // g2m is stored at 2^e_c: kbuf[96 + c] = 2^-e_c (head_pb.hip)
       kc[96 + c] = k2 * d * sc;
       kc[128 + c] = fmaf(k2, bc, k3) * sc;
     }
@@ -969,14 +970,14 @@ static int br_diag_env() {
 static int br_diag_env() { return 0; }
 #endif
 
-// g2m: planar [B][32][Q][Q]; walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
+// g2m: fp16 planar [B][32][Q][Q] (kbuf[96 + c] = its scale 2^-e_c); walk: tds_conv2_bwd_walk table for nwg workgroups, transposed to
 // [nwg][rows] (fused_ops.cpp bwd_walk)
-void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const float* aff2, const float* kbuf,
+void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const unsigned short* g2m, const float* aff2, const float* kbuf,
                     const float* b2,
                     uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st) {
   const int Q = P / 2;
-  const bool big = (int64_t)32 * Q * Q * 4 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
+  const bool big = (int64_t)32 * Q * Q * 2 >= 0xFFFFFF00LL;  // g2m image beyond a 4 GiB descriptor
 #define TDS_BR_LAUNCH_B(D, BG)                                                                                         \
   {                                                                                                                    \
     static bool set = false;                                                                                           \

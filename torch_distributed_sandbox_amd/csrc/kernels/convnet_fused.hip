@@ -378,7 +378,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
   if (threadIdx.x == 0) out[e] = s;
 }
 
-// BN backward finalize from (sum dz, sum dz*y) partials:
+// BN backward finalize from (sum dz, sum dz*y) partials (x2: fp32 dz / stored dz, below):
 //   dgamma = invstd*(sdzy - mean*sdz), dbeta = sdz,
 //   dy = k1*dz + k2*y + k3,  k1 = g*is, k2 = -g*is^3*(sdzy - mean*sdz)/n, k3 = -g*is*sdz/n - k2*mean
 // One workgroup per channel (the head backward leaves ~10^3 partials per channel: a serial
@@ -415,23 +415,31 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(const double* __r
     }
     return;
   }
-  double sdz = 0.0, sdzy = 0.0;
+  // partial[c][k][4]: (sum dz, sum dz*y) over the fp32 pooled gradient (dgamma, dbeta), then over
+  // the values the conv2 backward reads (its fp16 g2m, head_pb.hip: k2, k3)
+  double sdz = 0.0, sdzy = 0.0, sdr = 0.0, sdyr = 0.0;
   for (int k = threadIdx.x; k < nchunk; k += blockDim.x) {
-    const double2 v = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nchunk + k) * 2);
+    const double2 v = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nchunk + k) * 4);
+    const double2 vr = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nchunk + k) * 4 + 2);
     sdz += v.x;
     sdzy += v.y;
+    sdr += vr.x;
+    sdyr += vr.y;
   }
   sdz = block_sum(sdz, sh);
   sdzy = block_sum(sdzy, sh);
+  sdr = block_sum(sdr, sh);
+  sdyr = block_sum(sdyr, sh);
   if (threadIdx.x != 0) return;
   const double mean = stats[c], is = stats[C + c];
   const double gm = gamma ? gamma[c] : 1.0;
   const double sdxh = sdzy - mean * sdz;  // sum dz*(y-mean)
   if (dgamma) dgamma[c] = (float)(is * sdxh);
   if (dbeta) dbeta[c] = (float)sdz;
+  const double sdxr = sdyr - mean * sdr;
   const double k1 = gm * is;
-  const double k2 = -gm * is * is * is * sdxh / (double)n;
-  const double k3 = -gm * is * sdz / (double)n - k2 * mean;
+  const double k2 = -gm * is * is * is * sdxr / (double)n;
+  const double k3 = -gm * is * sdr / (double)n - k2 * mean;
   kbuf[c] = (float)k1;
   kbuf[C + c] = (float)k2;
   kbuf[2 * C + c] = (float)k3;

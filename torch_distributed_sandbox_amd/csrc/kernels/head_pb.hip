@@ -31,6 +31,7 @@
 //   g2m : one float4 per image (same index as ya), dW / updated W: one 4-float group per class.
 // No LDS and no barriers in the stream: the next chunk's loads are issued before the current
 // one is reduced.  64-bit indexing throughout (no buffer descriptors).
+#include "bf16x3.h"
 #include "common.h"
 #include "ce_small.h"
 #include "launchers.h"
@@ -169,6 +170,30 @@ __device__ __forceinline__ void hp_store4(float* out, const PBGeom& g, const HPR
   }
 }
 
+__device__ __forceinline__ float hp_f16(uint32_t h) {  // the low 16 bits as fp16
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(h & 0xFFFFu));
+}
+
+// 4 pooled-gradient values as fp16 bits (two packed pairs, element 0 low) at this thread's (row, 4
+// columns) of plane j: 8-B, 2 x 4-B or 2-B stores by the row's alignment class
+__device__ __forceinline__ void hp_store4h(unsigned short* out, const PBGeom& g, const HPRow& rw, int j, uint32_t lo,
+                                           uint32_t hi) {
+  if (rw.nvalid == 0) return;
+  unsigned short* p = out + (int64_t)j * 32 * g.Q * (int64_t)g.Q + rw.off;
+  if (rw.nvalid == 4 && rw.al == 0) {
+    st_stream(reinterpret_cast<uint2*>(p), make_uint2(lo, hi));
+  } else if (rw.nvalid == 4 && rw.al == 2) {
+    st_stream(reinterpret_cast<uint32_t*>(p), lo);
+    st_stream(reinterpret_cast<uint32_t*>(p + 2), hi);
+  } else {
+    const unsigned short e[4] = {(unsigned short)lo, (unsigned short)(lo >> 16), (unsigned short)hi,
+                                 (unsigned short)(hi >> 16)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < rw.nvalid) p[k] = e[k];
+  }
+}
+
 // Forward.  partial[blk][B*NC] (fp64): this workgroup's share of logits[b][j] for images
 // b0 .. b0+NB-1; xout (optional): X in the fc's flatten order, [B][32*Q*Q] -- or, for a launch over
 // channels [c0, c1) (the activation exchange's column groups, parallel/factored.py), that range's
@@ -196,8 +221,10 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
                                                                  const float* __restrict__ aff2,
                                                                  double* __restrict__ partial,
                                                                  float* __restrict__ xout, PBGeom g, int Btot, int b0,
-                                                                 int NC, HPFin fin, int c0, int64_t x_rs) {
+                                                                 int NC, HPFin fin, int c0, int64_t x_rs,
+                                                                 uint32_t* __restrict__ wmaxp) {
   __shared__ float red[HP_THREADS / 64][HP_MAXB * 10];
+  __shared__ uint32_t wred[HP_THREADS / 64][10];
   __shared__ int last_flag;
   __shared__ double wpart[256];
   const HPGrid hg = hp_grid(g);
@@ -207,6 +234,9 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
   const int Q = g.Q;
   const int64_t QQ = (int64_t)Q * Q;
   float acc[NB][10];
+  float wmx[10];  // max |W[j]| over this workgroup's weights (the backward's fp16 g2m scale)
+#pragma unroll
+  for (int j = 0; j < 10; ++j) wmx[j] = 0.f;
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll
@@ -256,6 +286,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
 #pragma unroll
       for (int b = 0; b < NB; ++b)
         acc[b][j] = fmaf(x[b][0], w4.x, fmaf(x[b][1], w4.y, fmaf(x[b][2], w4.z, fmaf(x[b][3], w4.w, acc[b][j]))));
+      // (fix() zeroed the lanes outside the image and the classes >= NC)
+      wmx[j] = fmaxf(fmaxf(wmx[j], fmaxf(fabsf(w4.x), fabsf(w4.y))), fmaxf(fabsf(w4.z), fabsf(w4.w)));
     }
   };
   if (nit > 0) issue(ld0, 0);
@@ -277,7 +309,16 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
         if (lane == 0) red[wv][b * 10 + j] = s;
       }
     }
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const uint32_t m = wave_max(__float_as_uint(wmx[j]));  // (non-negative: bits order as values)
+    if (lane == 0) wred[wv][j] = m;
+  }
   __syncthreads();
+  if (wmaxp != nullptr && (int)threadIdx.x < 10) {
+    const int j = threadIdx.x;
+    wmaxp[(int64_t)wg * 10 + j] = max(max(wred[0][j], wred[1][j]), max(wred[2][j], wred[3][j]));
+  }
   for (int i = threadIdx.x; i < NB * NC; i += HP_THREADS) {
     const int b = i / NC, j = i - b * NC;
     const double s = (((double)red[0][b * 10 + j] + (double)red[1][b * 10 + j]) + (double)red[2][b * 10 + j]) +
@@ -324,7 +365,8 @@ __global__ __launch_bounds__(256) void head_logits_kernel(const double* __restri
 
 // Backward for images b0 .. b0+NB-1.
 //   g2m[b][c][py][px] = (sum_j dl[b][j] W[j][c][py][px]) * [a*ya + b > 0]   (planar [B][32][Q][Q])
-//   partial[c][pass*nblk + blk][2] = { sum g2m, sum g2m * ya }       (BN2 backward sums)
+//   partial[c][pass*nblk + blk][4] = { sum g2m, sum g2m * ya } over the fp32 values (dgamma2,
+//                                    dbeta2), then the same over the stored fp16 values (k2, k3)
 //   dW[j][c][pos] (= or +=) scale * sum_b dl[b][j] X[b][c][pos]      (WITH_DW; ACC adds)
 //   Wupd = W - lr * dW                                               (UPD: SGD step fused)
 //   gpart (optional): this workgroup's max |g2m| as float bits (NaN-propagating as an unsigned
@@ -355,11 +397,14 @@ struct HBFin {
 template <int NB, bool WITH_DW, bool ACC, bool UPD, bool KEEP = true>
 __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     const float* __restrict__ ya, const float* W, const float* __restrict__ aff2, const float* __restrict__ dl,
-    float* __restrict__ g2m, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass, int npass,
-    int NC, float scale, float lr, int c0, uint32_t* __restrict__ gpart, HBFin fin) {
-  __shared__ float red[2][HP_THREADS / 64];
+    unsigned short* __restrict__ g2h, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass,
+    int npass, int NC, float scale, float lr, int c0, uint32_t* __restrict__ gpart, HBFin fin,
+    const uint32_t* __restrict__ wmaxp, int wrows, int Btot, float* __restrict__ g2inv) {
+  __shared__ float red[4][HP_THREADS / 64];
+  __shared__ uint32_t wms[10];
+  __shared__ float g2sc;
   __shared__ uint32_t gred[HP_THREADS / 64];
-  __shared__ double dred[2][HP_THREADS / 64];
+  __shared__ double dred[4][HP_THREADS / 64];
   __shared__ int last_flag;
   const HPGrid hg = hp_grid_b(g);
   // workgroups in the reverse of the forward's order: the backward starts on the channels the
@@ -371,10 +416,37 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   for (int b = 0; b < NB; ++b)
 #pragma unroll
     for (int j = 0; j < 10; ++j) dls[b * 10 + j] = j < NC ? dl[(b0 + b) * NC + j] : 0.f;
+  // g2m's fp16 scale for channel c: |g2m[b][c][.]| <= sum_j |dl[b][j]| max |W[j][c][.]| (the forward
+  // measured the maxima, wmaxp: wrows rows per channel); the power of two 2^e puts that bound below
+  // 2^14 (fp16 holds to 65504; ~28 binades of full precision below the bound).  Every workgroup of
+  // the channel forms the same e from the same data; the consumers get 2^-e (g2inv[c]).
+  if (threadIdx.x < 10) wms[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int i = threadIdx.x; i < wrows * 10; i += HP_THREADS)
+    atomicMax(&wms[i % 10], wmaxp[((int64_t)c * wrows + i / 10) * 10 + i % 10]);
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float s = 0.f;
+    if ((int)threadIdx.x < Btot)
+      for (int j = 0; j < NC; ++j) s = fmaf(fabsf(dl[threadIdx.x * NC + j]), __uint_as_float(wms[j]), s);
+    const float bound = __uint_as_float(wave_max(__float_as_uint(s)));  // (NaN: bits above inf -> no scale)
+    if (threadIdx.x == 0) {
+      int e = 0;
+      if (bound > 0.f && __builtin_isfinite(bound)) {
+        int x;
+        (void)frexpf(bound, &x);  // bound < 2^x
+        e = min(100, max(-100, 14 - x));
+      }
+      g2sc = ldexpf(1.f, e);
+      if (g2inv != nullptr && band == 0 && pass == 0) g2inv[c] = ldexpf(1.f, -e);
+    }
+  }
+  __syncthreads();
+  const float gsc = g2sc, ginv = 1.f / g2sc;  // (powers of two: exact)
   const float a = aff2[c], bb = aff2[32 + c];
   const int Q = g.Q;
   const int64_t plane = g.plane();
-  float sdz = 0.f, sdy = 0.f;
+  float sdz = 0.f, sdy = 0.f, sdzr = 0.f, sdyr = 0.f;  // (r: the stored values)
   uint32_t gmx = 0u;  // max |g2m| bits
   const int nch = (g.Q8 + 31) / 32;
   const int R0 = band * HP_BAND_B, nit = (min(g.Q4, R0 + HP_BAND_B) - R0) * nch;
@@ -408,13 +480,23 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
           gs = fmaf(dls[b * 10 + j], wk, gs);
         }
         gm[k] = (ok && z > 0.f) ? gs : 0.f;
-        gmx = max(gmx, __float_as_uint(gm[k]) & 0x7fffffffu);
         x[b][k] = ok ? hp_relu(z) : 0.f;
         sdz += gm[k];
         sdy = fmaf(gm[k], ok ? yy[k] : 0.f, sdy);
       }
-      // planar, like a weight plane
-      hp_store4(g2m, g, rwg, b0 + b, make_float4(gm[0], gm[1], gm[2], gm[3]), true);
+      // planar, like a weight plane, in fp16 at 2^e_c.  dy2's constants k2, k3 and the magnitude bound
+      // take the sums over the values as stored (the conv2 backward's dz): sum dy2 over the channel
+      // stays 0 in exact arithmetic, as torch's, instead of carrying k1 times the sum of g2m's rounding
+      // errors; dgamma2 / dbeta2 keep the fp32 values' sums
+      const uint32_t lo = cvt2_f16(gm[0] * gsc, gm[1] * gsc), hi = cvt2_f16(gm[2] * gsc, gm[3] * gsc);
+      hp_store4h(g2h, g, rwg, b0 + b, lo, hi);
+      const float gr[4] = {hp_f16(lo) * ginv, hp_f16(lo >> 16) * ginv, hp_f16(hi) * ginv, hp_f16(hi >> 16) * ginv};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        gmx = max(gmx, __float_as_uint(gr[k]) & 0x7fffffffu);
+        sdzr += gr[k];
+        sdyr = fmaf(gr[k], (rok && px0 + k < Q) ? yy[k] : 0.f, sdyr);
+      }
     }
     if constexpr (WITH_DW) {
       const HPRow& rw = rwg;
@@ -460,9 +542,13 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   gmx = wave_max(gmx);
   sdz = wave_sum(sdz);
   sdy = wave_sum(sdy);
+  sdzr = wave_sum(sdzr);
+  sdyr = wave_sum(sdyr);
   if (lane == 0) {
     red[0][wv] = sdz;
     red[1][wv] = sdy;
+    red[2][wv] = sdzr;
+    red[3][wv] = sdyr;
     gred[wv] = gmx;
   }
   __syncthreads();
@@ -472,46 +558,50 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     for (int i = 1; i < HP_THREADS / 64; ++i) m = max(m, gred[i]);
     st_agent(gpart + ((int64_t)c * npass + pass) * hg.per_channel() + band, m);  // (write-through: tds_arrive)
   }
-  if (threadIdx.x < 2) {
+  if (threadIdx.x < 4) {
     const int k = threadIdx.x;
     const double s = (((double)red[k][0] + (double)red[k][1]) + (double)red[k][2]) + (double)red[k][3];
     const int64_t nblk = (int64_t)hg.per_channel();
-    st_agent(partial + (((int64_t)c * npass + pass) * nblk + band) * 2 + k, s);
+    st_agent(partial + (((int64_t)c * npass + pass) * nblk + band) * 4 + k, s);
   }
   if (fin.sync == nullptr) return;
   const int nb = hg.per_channel();
   if (!tds_arrive(fin.sync + c, (uint32_t)nb, &last_flag)) return;
   {  // channel c: its bands in order (one pass: partial row = c * nb + band)
-    double sdz = 0.0, sdzy = 0.0;
+    double sd[4] = {0.0, 0.0, 0.0, 0.0};
     uint32_t m = 0u;
     for (int k = lane + 64 * wv; k < nb; k += HP_THREADS) {  // (nb <= 256 at Q <= 2044: one load each)
-      const double2 v = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nb + k) * 2);
-      sdz += v.x;
-      sdzy += v.y;
+      const double2 v = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nb + k) * 4);
+      const double2 vr = *reinterpret_cast<const double2*>(partial + ((int64_t)c * nb + k) * 4 + 2);
+      sd[0] += v.x;
+      sd[1] += v.y;
+      sd[2] += vr.x;
+      sd[3] += vr.y;
       if (gpart != nullptr) m = max(m, gpart[(int64_t)c * nb + k]);
     }
-    sdz = wave_sum(sdz);
-    sdzy = wave_sum(sdzy);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sd[i] = wave_sum(sd[i]);
     m = wave_max(m);
     if (lane == 0) {
-      dred[0][wv] = sdz;
-      dred[1][wv] = sdzy;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dred[i][wv] = sd[i];
       gred[wv] = m;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-      sdz = ((dred[0][0] + dred[0][1]) + dred[0][2]) + dred[0][3];
-      sdzy = ((dred[1][0] + dred[1][1]) + dred[1][2]) + dred[1][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sd[i] = ((dred[i][0] + dred[i][1]) + dred[i][2]) + dred[i][3];
       m = max(max(gred[0], gred[1]), max(gred[2], gred[3]));
       st_agent(fin.cmax + c, m);
       const double mean = fin.stats[c], is = fin.stats[32 + c];
       const double gm = fin.gamma ? fin.gamma[c] : 1.0;
-      const double sdxh = sdzy - mean * sdz;  // sum dz*(y-mean)
+      const double sdxh = sd[1] - mean * sd[0];  // sum dz*(y-mean), fp32 dz
       if (fin.dgamma) fin.dgamma[c] = (float)(is * sdxh);
-      if (fin.dbeta) fin.dbeta[c] = (float)sdz;
+      if (fin.dbeta) fin.dbeta[c] = (float)sd[0];
+      const double sdxr = sd[3] - mean * sd[2];  // the same over the stored dz
       const double k1 = gm * is;
-      const double k2 = -gm * is * is * is * sdxh / (double)fin.n;
-      const double k3 = -gm * is * sdz / (double)fin.n - k2 * mean;
+      const double k2 = -gm * is * is * is * sdxr / (double)fin.n;
+      const double k3 = -gm * is * sd[2] / (double)fin.n - k2 * mean;
       fin.kbuf[c] = (float)k1;
       fin.kbuf[32 + c] = (float)k2;
       fin.kbuf[64 + c] = (float)k3;
@@ -532,6 +622,15 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
 }  // namespace tds
 
 using namespace tds;
+
+// The forward's per-workgroup max |W[j]| ([32 * nblk][10] float bits), read by the next head backward
+// on the same stream for g2m's fp16 scale: one buffer per (device, stream), the forward and the
+// backward of one step see the same weight (the fused SGD step runs inside the backward, the
+// exchange's update before the forward)
+static uint32_t* hp_wmax_buf(int Q, hipStream_t st) {
+  const size_t n = (size_t)32 * hp_grid(pb_geom(Q)).per_channel() * 10;
+  return reinterpret_cast<uint32_t*>(tds_zeroed_u64(1, (n + 1) / 2, st));
+}
 
 int tds_head_pb_nblk(int Q) { return hp_grid(pb_geom(Q)).per_channel(); }  // forward workgroups per channel
 int tds_head_bwd_pb_nblk(int Q) { return hp_grid_b(pb_geom(Q)).per_channel(); }  // backward workgroups per channel
@@ -567,12 +666,14 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
     fin.inv_count = inv_count;
   }
   if (range && fin.sync == nullptr) return -1;
+  uint32_t* wmaxp = hp_wmax_buf(Q, st);
+  if (wmaxp == nullptr) return -2;
   for (int b0 = 0; b0 < B; b0 += HP_MAXB) {
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
 #define TDS_HPF(NBV)                                                                                                   \
   case NBV:                                                                                                            \
     hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
-                       B, b0, NC, fin, c0, x_rs);                                                                      \
+                       B, b0, NC, fin, c0, x_rs, wmaxp);                                                               \
     TDS_LAUNCH_CHECK();                                                                                                \
     break;
     switch (nb) {
@@ -590,10 +691,13 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 // partial: double [32][npass * nblk][2], npass = ceil(B / 8)
 int tds_head_bwd_pb_npass(int B) { return (B + HP_MAXB - 1) / HP_MAXB; }
 
-int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
+int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, unsigned short* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
-                    int c1, uint32_t* gpart, hipStream_t st, const TdsHeadBwdFin* hf) {
+                    int c1, uint32_t* gpart, float* g2inv, hipStream_t st, const TdsHeadBwdFin* hf) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1 || c0 < 0 || c1 > 32 || c0 >= c1) return -1;
+  const uint32_t* wmaxp = hp_wmax_buf(Q, st);
+  if (wmaxp == nullptr) return -5;
+  const int wrows = hp_grid(pb_geom(Q)).per_channel();
   const int npass = tds_head_bwd_pb_npass(B);
   if (Wupd && npass != 1) return -2;  // the fused SGD step needs the whole dW in one pass
   const PBGeom g = pb_geom(Q);
@@ -621,7 +725,8 @@ int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const 
     const bool acc = pass > 0;
 #define TDS_HPB_E(NBV, WD, AC, UP, KP)                                                                             \
   hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, \
-                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gpart, fin);
+                     dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gpart, fin, wmaxp, wrows, \
+                     B, g2inv);
 #define TDS_HPB(NBV)                                   \
   case NBV:                                            \
     if (!dW && Wupd) {                                 \

@@ -113,7 +113,7 @@ void tds_conv2_bwd3_tiles(int P, int* tiles_r, int* tiles_c);
 // decode (conv2_common.h); b2: conv2.bias (y2h is bias-free)
 // dp1h [B][P][ceil(P/4)][16][4] fp16 (conv2_common.h); its decode factor goes to mag[kMagScales + 4]
 // a2: the forward's pooling argmax codes (conv2_common.h)
-void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const float* g2m, const float* aff2, const float* kbuf, const float* b2,
+void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const unsigned short* g2m, const float* aff2, const float* kbuf, const float* b2,
                     uint32_t* mag, const void* p1, const short* wd, void* dp1h, float* slab, const int* walk,
                     int nwg, int sw, int sk, int B, int P, hipStream_t st);
 // host: per-workgroup tile lists of vertical segments of ~seg tiles; out == nullptr -> length
@@ -217,9 +217,11 @@ struct TdsHeadBwdFin {
   float* dbfc;     // [NC] or nullptr
   uint32_t* mag;   // mag[32] <- max |g2m|, or nullptr
 };
-int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, float* g2m,
+// g2m: fp16 [B][32][Q][Q] at a per-channel power-of-two scale 2^e_c (g2inv[c] <- 2^-e_c), bounded
+// by the max |W| per channel and class that the last head forward on this stream measured
+int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, unsigned short* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
-                    int c1, uint32_t* gpart, hipStream_t st, const TdsHeadBwdFin* hf = nullptr);
+                    int c1, uint32_t* gpart, float* g2inv, hipStream_t st, const TdsHeadBwdFin* hf = nullptr);
 
 // ---- zs_exchange.hip (zero-suppressed fc-input rows, parallel/zs.py)
 int64_t tds_zs_npages(int64_t n);

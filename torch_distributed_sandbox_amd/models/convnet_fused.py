@@ -376,8 +376,9 @@ class _Head(torch.autograd.Function):
             # group's dW columns all-reduced as soon as it lands; grads published by the exchange
             (dw, acc_w), (db, acc_b) = ex.chunk_targets()
             B, Q = ya.shape[0], P // 2
-            # (64 B of slack past the end: the conv2 backward's row loads, ops.fused_conv2_backward_y2)
-            g2m_buf = torch.empty(B * 32 * Q * Q + 16, device=ya.device, dtype=torch.float32)[:B * 32 * Q * Q].view(
+            # fp16 at per-channel scales (kernels/head_pb.hip), with 64 B of slack past the end: the conv2
+            # backward's row loads (ops.fused_conv2_backward_y2)
+            g2m_buf = torch.empty(B * 32 * Q * Q + 32, device=ya.device, dtype=torch.float16)[:B * 32 * Q * Q].view(
                 B, 32, Q, Q)
             part = torch.empty(ops.head_bwd_workspace(B, P), device=ya.device, dtype=torch.float64)
             _, dg_o, dbe_o = _sinks(ctx, ctx.small, (13, 5, 6))
