@@ -958,7 +958,7 @@ int64_t tds_conv2_bwd_walk(int* out, int B, int tiles_r, int tiles_c, int nwg, i
 }
 
 #ifdef TDS_DIAG
-// timing-only variants: 1 no MFMAs, 3 no global tile loads, 5 no staging, 7 no y2 loads, 9 no
+// timing-only variants: 1 no MFMAs, 3 no global tile loads, 5 no staging, 9 no
 // BN2 / pool backward math in the staging, 13 the full kernel with per-wave barrier-wait clocks,
 // 16..27 the flag sets of conv2_common.h (with clocks).  Compiled only into a -DTDS_DIAG build
 // (python -m torch_distributed_sandbox_amd._build --variant diag -D TDS_DIAG; TDS_CONV2_DIAG=N).
@@ -1001,7 +1001,6 @@ void tds_conv2_bwd3(const void* y2h, const uint32_t* a2, const unsigned short* g
     case 1: TDS_BR_LAUNCH(1) break;
     case 3: TDS_BR_LAUNCH(3) break;
     case 5: TDS_BR_LAUNCH(5) break;
-    case 7: TDS_BR_LAUNCH(7) break;
     case 9: TDS_BR_LAUNCH(9) break;
     case 13: TDS_BR_LAUNCH(13) break;
     // flag sets (conv2_common.h): 16 = full + clocks; +1 no staging, +2 no LDS operand reads,
