@@ -69,9 +69,10 @@ DTYPE_TF32 = ("fp32 (conv2 fwd+dgrad+wgrad: TF32-class -- one fp16 MFMA per prod
               "significant bits = TF32's significand, exact power-of-two range scaling, fp32 accumulate: the arithmetic "
               "of the reference's default cuDNN TF32 convolutions; conv1 fwd+wgrad: bf16x3 split MFMA (~2^-16); BN, fc, "
               "CE, SGD: fp32; stored in fp16 at exact power-of-two scales (11 significant bits): the conv2 output the "
-              "backward re-reads (y2h; BN2 statistics, pooled values and argmax from fp32), the pooled gradient "
+              "backward re-reads (y2h; BN2 statistics and argmax from fp32) and its value at each pooling window's argmax "
+              "that the head reads (ya, the same fp16 value), the pooled gradient "
               "entering the BN2 backward (g2m; its statistics from fp32) and the conv2 data gradient (dp1h) -- "
-              "docs/KERNELS.md 'y2h', 'g2m', 'dp1h')")
+              "docs/KERNELS.md 'y2h', 'ya', 'g2m', 'dp1h')")
 
 
 def _dtype(on_gpu: bool = True) -> str:

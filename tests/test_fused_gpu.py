@@ -280,11 +280,14 @@ def test_conv2_forward(gpu, P):
     yct = reft - b2.double().cpu().view(1, 32, 1, 1)
     _check_conv(s[:, 0], yc.sum((0, 2, 3)), yct.sum((0, 2, 3)), "sum")
     _check_conv(s[:, 1], (yc * yc).sum((0, 2, 3)), (yct * yct).sum((0, 2, 3)), "sumsq")
-    # ya: the fp32 window extremes; a2: each window's argmax pixel (first in scan order)
+    # ya: y2h at each window's extreme (fp16, decoded as y2h); rounding is monotone, so that is
+    # exactly the extreme of the window's stored values. a2: each window's argmax pixel (first in
+    # scan order)
     Q = P // 2
-    want = window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q].float(), (g2 < 0))
-    got = pb_to_planar(ya, Q)
-    assert ((got - want).abs() <= 2.0 ** -10 * vmax).all(), (got - want).abs().max()
+    assert ya.dtype == torch.float16
+    want = window_extreme(y2h.float().permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q], (g2 < 0))
+    got = pb_to_planar(ya, Q).float()
+    assert torch.equal(got, want), (got - want).abs().max()
     _check_argmax_kept(a2, reft, g2, Q)
 
 
@@ -331,19 +334,34 @@ def test_conv2_forward_argmax_codes_on_near_ties(gpu, P):
     _check_argmax_kept(a2, ref, g2, Q)
 
 
+def set_ya_scale(mag, d=1.0):
+    """ya's decode factor d = mag[40] * mag[41] / mag[42] (kernels/launchers.h TdsYaDec) in a
+    workspace no conv2 pack wrote"""
+    mag_floats(mag)[40:43] = torch.tensor([d, 1.0, 1.0])
+    return mag
+
+
+def ya_of(h, g2, Q):
+    """ya (fp16, pooled-blocked) of stored values h [B,P,P,32] (y2 = h d + b2): each window's extreme"""
+    return planar_to_pb(window_extreme(h.float().permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q], g2 < 0)).half()
+
+
 def _head_case(gpu, P, B, seed):
+    """A synthetic conv2 output y2 on ya's fp16 grid (decode d = 1: y2 = h + b2, h fp16), so the
+    fp64 references see the values the head kernels decode."""
     torch.manual_seed(seed)
     NC = 10
     Q = P // 2
-    y2 = torch.randn(B, P, P, 32, device=gpu)
     b2 = torch.randn(32, device=gpu) * 0.1
+    h = torch.randn(B, P, P, 32, device=gpu).half()
+    y2 = h.float() + b2
     g2 = torch.randn(32, device=gpu)  # negative gammas exercise the min windows
     be2 = torch.randn(32, device=gpu) * 0.1
     wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
     bfc = torch.randn(NC, device=gpu)
     yc = (y2 - b2).double()
     partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()  # [32][1][2]
-    ya = planar_to_pb(window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q], g2 < 0))
+    ya = ya_of(h, g2, Q)
     return y2, b2, g2, be2, wfc, bfc, partial2, ya
 
 
@@ -371,10 +389,10 @@ def test_head_forward_backward(gpu, P, B):
     _check(xo.view(B, 32, Q, Q), pz, 1e-5, "x_out (fc input rows)")
     dl = torch.randn(B, NC, device=gpu)
     ref.backward(dl.double().cpu())
-    mag = new_mag(gpu, B, P)
+    mag = set_ya_scale(new_mag(gpu, B, P))
     ypart(mag).zero_()
     ypart(mag)[5, 3] = torch.tensor(2.5).view(torch.int32)  # a forward part: reduced per channel
-    dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, True,
+    dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, b2, g2, wfc, P, None, 1.0, True,
                                                              mag=mag)
     # g2m: fp16 at a power-of-two scale per channel (kbuf[96 + c] = 2^-e_c), bounded by the forward's
     # max |W| per channel and class: below 2^14 by construction, 11 significant bits
@@ -395,13 +413,13 @@ def test_head_forward_backward(gpu, P, B):
     mask = (pz > 0).double()
     _check(g2f, pz.grad * mask, 2.0 ** -11 + 1e-5, "g2m (fp16, 2^-11 relative)")
     # no-dW form (activation exchange) leaves the same g2m / BN2 gradients
-    _, _, dg2b, dbe2b, g2mb, kbufb = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, False)
+    _, _, dg2b, dbe2b, g2mb, kbufb = ops.fused_head_backward(dl, ya, stats2, aff2, b2, g2, wfc, P, None, 1.0, False)
     assert torch.equal(g2mb, g2m) and torch.equal(kbufb, kbuf) and torch.equal(dg2b, dg2)
     if B <= 8:
         # SGD step fused into the backward: W <- W - lr dW (in place), dW still written
         w0 = wfc.clone()
         dW2 = torch.empty_like(wfc)
-        ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, dW2, 1.0, True, 0.5)
+        ops.fused_head_backward(dl, ya, stats2, aff2, b2, g2, wfc, P, dW2, 1.0, True, 0.5)
         assert torch.equal(dW2, dW)
         assert torch.allclose(wfc, w0 - 0.5 * dW, rtol=0, atol=1e-6)
 
@@ -426,12 +444,13 @@ def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     Q = P // 2
     yc = (y2 - b2).double()
     partial2 = torch.stack([yc.sum((0, 1, 2)), (yc * yc).sum((0, 1, 2))], dim=1).contiguous()
-    ya = planar_to_pb(window_extreme(y2.permute(0, 3, 1, 2)[:, :, :2 * Q, :2 * Q], g2 < 0))
-    _, stats2, aff2 = ops.fused_head_forward(ya, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, P)
+    ya = ya_of(y2h, g2, Q)
+    _, stats2, aff2 = ops.fused_head_forward(ya, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, P,
+                                             mag=mag)
     yp = ypart(mag)  # (the conv2 forward's per-workgroup bounds; y2 is synthetic here)
     yp.zero_()
     yp[:, 0] = (y2 - b2).abs().amax((0, 1, 2)).view(torch.int32)  # max |y2 - b2| per channel
-    _, _, _, _, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, True, mag=mag)
+    _, _, _, _, g2m, kbuf = ops.fused_head_backward(dl, ya, stats2, aff2, b2, g2, wfc, P, None, 1.0, True, mag=mag)
     dp1h, dw2, db2 = ops.fused_conv2_backward_y2(y2h, a2, g2m, aff2, kbuf, b2, mag, p, wd, 1.0)
     dp1 = dp1h_decode(dp1h, mag_floats(mag)[44].item(), P)
     # fp64 reference: dy2 from the head chain, then the conv2 backward with that dy2

@@ -32,7 +32,7 @@ def main():
         g = torch.Generator(device=dev).manual_seed(0)
         mk = (lambda *s: torch.randn(*s, device=dev, generator=g)) if fill == "random" else \
             (lambda *s: torch.zeros(*s, device=dev))
-        ya = mk(B, 32, Q4 * Q8 * 32)
+        ya = mk(B, 32, Q4 * Q8 * 32).half()  # fp16 as the conv2 forward stores it (d = 1: no mag)
         wfc = mk(10, 32 * Q * Q) * 0.01
         bfc = torch.zeros(10, device=dev)
         b2, g2, be2 = torch.zeros(32, device=dev), torch.ones(32, device=dev), torch.zeros(32, device=dev)
@@ -42,10 +42,10 @@ def main():
         dl = torch.randn(B, 10, device=dev)
         dw = torch.empty_like(wfc)
         tf = timeit(lambda: ops.fused_head_forward(ya, partial2, b2, g2, be2, None, None, None, 0.1, 1e-5, wfc, bfc, P))
-        tb = timeit(lambda: ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, dw, 1.0, True))
-        tu = timeit(lambda: ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, dw, 1.0, True, 1e-9))
-        tn = timeit(lambda: ops.fused_head_backward(dl, ya, stats2, aff2, g2, wfc, P, None, 1.0, False))
-        gb_f = (ya.numel() + wfc.numel()) * 4 / 1e9
+        tb = timeit(lambda: ops.fused_head_backward(dl, ya, stats2, aff2, b2, g2, wfc, P, dw, 1.0, True))
+        tu = timeit(lambda: ops.fused_head_backward(dl, ya, stats2, aff2, b2, g2, wfc, P, dw, 1.0, True, 1e-9))
+        tn = timeit(lambda: ops.fused_head_backward(dl, ya, stats2, aff2, b2, g2, wfc, P, None, 1.0, False))
+        gb_f = (ya.numel() * 2 + wfc.numel() * 4) / 1e9
         print(f"{fill:6s} head fwd op {tf:.3f} ms ({gb_f / tf:.2f} TB/s incl. small kernels) | bwd dW {tb:.3f} ms | "
               f"bwd dW+update {tu:.3f} ms | bwd no-dW {tn:.3f} ms", flush=True)
 

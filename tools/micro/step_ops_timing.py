@@ -72,19 +72,20 @@ def main():
             y2, partial2, ya = st["c2"][:3]
             st["hf"] = ops.fused_head_forward(ya, partial2, c2.bias, n2.weight, n2.bias, n2.running_mean,
                                               n2.running_var, n2.num_batches_tracked, 0.1, 1e-5, fc.weight,
-                                              fc.bias, P, None)
+                                              fc.bias, P, None, mag=st["mag"])
 
         dl = torch.randn(B, 10, device=dev) * 0.1
         dw = torch.empty_like(fc.weight)
 
         def hb():
             _, stats2, aff2 = st["hf"]
-            st["hb"] = ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, n2.weight, fc.weight, P, dw, 1.0, True,
+            st["hb"] = ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, c2.bias, n2.weight, fc.weight, P, dw, 1.0,
+                                               True,
                                                mag=st["mag"])
 
         def hb_nomag():  # A/B: the same launch without the |g2m| bound (atomic max)
             _, stats2, aff2 = st["hf"]
-            ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, n2.weight, fc.weight, P, dw, 1.0, True)
+            ops.fused_head_backward(dl, st["c2"][2], stats2, aff2, c2.bias, n2.weight, fc.weight, P, dw, 1.0, True)
 
         def c2b():
             y2 = st["c2"][0]
@@ -108,7 +109,7 @@ def main():
         vals = torch.empty(B * K, device=dev)
 
         def hf_x():
-            ops.fused_head_forward_aff(st["c2"][2], st["hf"][2], w2c, fc.bias, P, xo)
+            ops.fused_head_forward_aff(st["c2"][2], st["hf"][2], c2.bias, st["mag"], w2c, fc.bias, P, xo)
 
         def enc_x():
             st["nnz"] = zs.encode(xo, meta, vals)

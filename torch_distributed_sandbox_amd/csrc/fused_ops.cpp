@@ -3,7 +3,8 @@
 // the host first.  Activation formats:
 //   p1          [B,P,P,16] fp16 (conv2's single-rounded operand)
 //   y2h         [B,P,P,32] fp16 (the conv2 output the backward re-reads, bias-free, scaled)
-//   ya          [B,32,PB] f32: pooled-blocked planes (kernels/pooled_layout.h)
+//   ya          [B,32,PB] fp16: pooled-blocked planes (kernels/pooled_layout.h), the y2h value at
+//               each window's argmax: y2 = h d + b2 (kernels/launchers.h TdsYaDec)
 //   g2m         [B,32,Q,Q] fp16: planar pooled gradient at a per-channel power-of-two scale 2^e_c
 //               bounded by the head forward's max |W| per channel and class (kernels/head_pb.hip);
 //               kbuf[96 + c] = 2^-e_c (kbuf = [k1 | k2 | k3 | g2m scales], 128 floats)
@@ -339,8 +340,18 @@ std::tuple<Tensor, Tensor> conv2_pack(const Tensor& w2, const c10::optional<Tens
   return {wp, wd};
 }
 
+unsigned short* ya_out(const Tensor& ya) { return reinterpret_cast<unsigned short*>(ya.data_ptr<at::Half>()); }
+
+// ya's decode (kernels/launchers.h TdsYaDec): conv2.bias and the conv2 pack's scales in mag (none:
+// d = 1, as fused_conv2_forward stores ya without mag)
+TdsYaDec ya_dec(const Tensor& b2, const c10::optional<Tensor>& mag) {
+  need(b2, at::kFloat, {32}, "conv2.bias (ya's decode)");
+  uint32_t* m = opt_mag(mag, kMagScales + 3);
+  return TdsYaDec{b2.data_ptr<float>(), m ? m + kMagScales : nullptr};
+}
+
 // returns (y2h [B,P,P,32] fp16: the conv2 output bias-free at the y2h scale mag[kMagScales + 2]
-// (1 without mag; kernels/conv2_common.h), BN2 partials, ya [B,32,PB]: y2 at each 2x2 window's
+// (1 without mag; kernels/conv2_common.h), BN2 partials, ya [B,32,PB] fp16: y2h at each 2x2 window's
 // argmax of the BN2 output, resolved by the sign of gamma2, a2 [B,P/2,P/2,2] int32: those argmaxes
 // as 2-bit codes (kernels/conv2_common.h), for the backward)
 std::tuple<Tensor, Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1, const Tensor& wp, const Tensor& b2,
@@ -360,11 +371,11 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> fused_conv2_forward(const Tensor& p1,
   int sw = 0, sk = 0;
   const int* order = tile_order(p1, (int)B, tr, tc, nwg, &sw, &sk);
   auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kHalf));  // y2h (kernels/conv2_common.h)
-  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
+  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kHalf));
   auto partial = at::empty({32 * nwg * 2}, p1.options().dtype(at::kDouble));
   auto a2 = at::empty({B, P / 2, P / 2, 2}, p1.options().dtype(at::kInt));
   tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr(),
-                 ya.data_ptr<float>(), reinterpret_cast<uint32_t*>(a2.data_ptr<int>()), partial.data_ptr<double>(),
+                 ya_out(ya), reinterpret_cast<uint32_t*>(a2.data_ptr<int>()), partial.data_ptr<double>(),
                  opt_mag(mag, kMagParts + 32 * mag_ypart_count()) ? opt_mag(mag) + kMagParts : nullptr,
                  opt_mag(mag) ? opt_mag(mag) + kMagScales : nullptr, order, nwg, sw, sk, (int)B, (int)P, stream_of(p1));
   check_launches("fused_conv2_forward");
@@ -398,7 +409,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_conv2_forward_bn(
   int sw = 0, sk = 0;
   const int* order = tile_order(p1, (int)B, tr, tc, nwg, &sw, &sk);
   auto y2 = at::empty({B, P, P, 32}, p1.options().dtype(at::kHalf));
-  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kFloat));
+  auto ya = at::empty({B, 32, pb_plane(P)}, p1.options().dtype(at::kHalf));
   auto a2 = at::empty({B, P / 2, P / 2, 2}, p1.options().dtype(at::kInt));
   const int ndw = tds_conv2_fwd2_fin_doubles(nwg), nuw = tds_conv2_fwd2_fin_words(nwg);
   auto partial = at::empty({32 * nwg * 2 + ndw}, p1.options().dtype(at::kDouble));
@@ -418,7 +429,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_conv2_forward_bn(
   fin.mag = m;
   fin.dwork = partial.data_ptr<double>() + 32 * nwg * 2;
   fin.uwork = reinterpret_cast<uint32_t*>(uwork.data_ptr<int>());
-  tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr(), ya.data_ptr<float>(),
+  tds_conv2_fwd2(p1.data_ptr(), wp.data_ptr<int16_t>(), b2.data_ptr<float>(), g, y2.data_ptr(), ya_out(ya),
                  reinterpret_cast<uint32_t*>(a2.data_ptr<int>()), partial.data_ptr<double>(), m ? m + kMagParts : nullptr,
                  m ? m + kMagScales : nullptr, order, nwg, sw, sk, (int)B, (int)P, stream_of(p1), &fin);
   check_launches("fused_conv2_forward_bn");
@@ -427,12 +438,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> fused_conv2_forward_bn(
 
 // The head forward on a finished BN2 affine (fused_conv2_forward_bn's aff2): logits only, finished
 // inside the head's launch (head_pb.hip HPFin) for B <= 8
-Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor& wfc, const c10::optional<Tensor>& bfc,
-                              int64_t P, const c10::optional<Tensor>& x_out) {
+Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor& b2, const c10::optional<Tensor>& mag,
+                              const Tensor& wfc, const c10::optional<Tensor>& bfc, int64_t P,
+                              const c10::optional<Tensor>& x_out) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_aff: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_forward_aff: needs P/2 >= 4 pooled columns and B >= 1");
-  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(ya, at::kHalf, {B, 32, pb_plane(P)}, "ya (fp16)");
   need(aff2, at::kFloat, {64}, "aff2");
   TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
               "fc.weight must be [<=10, 32*Q*Q]");
@@ -448,8 +460,8 @@ Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor
   const int nblk = 32 * tds_head_pb_nblk((int)Q);
   auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
   auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
-  auto logits = at::empty({B, NC}, ya.options());
-  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
+  auto logits = at::empty({B, NC}, ya.options().dtype(at::kFloat));
+  const int rc = tds_head_fwd_pb(ya_out(ya), ya_dec(b2, mag), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
                                  part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
                                  (int)Q, (int)NC, stream_of(ya));
   TORCH_CHECK(rc == 0, "fused_head_forward_aff: unsupported shape");
@@ -461,13 +473,14 @@ Tensor fused_head_forward_aff(const Tensor& ya, const Tensor& aff2, const Tensor
 // CrossEntropyLoss defaults: ignore_index -100, no label smoothing) and dlogits formed by the
 // head forward's finalizing workgroup right after the logits (ce_small.h) -- one launch fewer than
 // logits then ops.cross_entropy, with the same arithmetic.  Returns (logits, loss, dlogits).
-std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, const Tensor& aff2, const Tensor& wfc,
+std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, const Tensor& aff2, const Tensor& b2,
+                                                             const c10::optional<Tensor>& mag, const Tensor& wfc,
                                                              const c10::optional<Tensor>& bfc, int64_t P,
                                                              const Tensor& labels, const c10::optional<Tensor>& x_out) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward_aff_ce: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_forward_aff_ce: needs P/2 >= 4 pooled columns and B >= 1");
-  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(ya, at::kHalf, {B, 32, pb_plane(P)}, "ya (fp16)");
   need(aff2, at::kFloat, {64}, "aff2");
   TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
               "fc.weight must be [<=10, 32*Q*Q]");
@@ -486,17 +499,17 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward_aff_ce(const Tensor& ya, c
   const int nblk = 32 * tds_head_pb_nblk((int)Q);
   auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
   auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
-  auto logits = at::empty({B, NC}, ya.options());
-  auto dlogits = at::empty({B, NC}, ya.options());
-  auto loss = at::empty({}, ya.options());
-  auto inv = at::empty({1}, ya.options());
-  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
+  auto logits = at::empty({B, NC}, ya.options().dtype(at::kFloat));
+  auto dlogits = at::empty({B, NC}, ya.options().dtype(at::kFloat));
+  auto loss = at::empty({}, ya.options().dtype(at::kFloat));
+  auto inv = at::empty({1}, ya.options().dtype(at::kFloat));
+  const int rc = tds_head_fwd_pb(ya_out(ya), ya_dec(b2, mag), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
                                  part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo,
                                  (int)B, (int)Q, (int)NC, st, true, labels.data_ptr<int64_t>(),
                                  dlogits.data_ptr<float>(), loss.data_ptr<float>(), inv.data_ptr<float>());
   TORCH_CHECK(rc >= 0, "fused_head_forward_aff_ce: unsupported shape");
   if (rc == 0) {  // (the finalizer was not in the launch: the separate CE)
-    auto row_loss = at::empty({B}, ya.options());
+    auto row_loss = at::empty({B}, ya.options().dtype(at::kFloat));
     tds_cross_entropy(logits.data_ptr<float>(), labels.data_ptr<int64_t>(), row_loss.data_ptr<float>(),
                       dlogits.data_ptr<float>(), loss.data_ptr<float>(), inv.data_ptr<float>(), (int)B, (int)NC, -100,
                       0.f, st);
@@ -515,12 +528,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> head_forward_range_ws
                                                                                  int64_t P) {
   const int64_t B = ya.size(0), Q = P / 2, NC = wfc.size(0);
   const int nblk = 32 * tds_head_pb_nblk((int)Q);
-  auto o = ya.options();
+  auto o = ya.options().dtype(at::kFloat);
   return {at::empty({(int64_t)(nblk + 32) * B * NC}, o.dtype(at::kDouble)), at::empty({B * NC}, o.dtype(at::kDouble)),
           at::empty({B, NC}, o), at::empty({B, NC}, o), at::empty({}, o), at::empty({1}, o)};
 }
 
-void fused_head_forward_range(const Tensor& ya, const Tensor& aff2, const Tensor& wfc, const c10::optional<Tensor>& bfc,
+void fused_head_forward_range(const Tensor& ya, const Tensor& aff2, const Tensor& b2, const c10::optional<Tensor>& mag,
+                              const Tensor& wfc, const c10::optional<Tensor>& bfc,
                               int64_t P, int64_t c0, int64_t c1, const Tensor& part, const Tensor& lsum,
                               const Tensor& logits, const Tensor& dlogits, const Tensor& loss, const Tensor& inv,
                               const c10::optional<Tensor>& labels, const c10::optional<Tensor>& x_out) {
@@ -528,7 +542,7 @@ void fused_head_forward_range(const Tensor& ya, const Tensor& aff2, const Tensor
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1 && B <= 8, "fused_head_forward_range: needs P/2 >= 4 and 1 <= B <= 8 (one pass)");
   TORCH_CHECK(0 <= c0 && c0 < c1 && c1 <= 32, "fused_head_forward_range: channels 0 <= c0 < c1 <= 32");
-  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(ya, at::kHalf, {B, 32, pb_plane(P)}, "ya (fp16)");
   need(aff2, at::kFloat, {64}, "aff2");
   TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
               "fc.weight must be [<=10, 32*Q*Q]");
@@ -553,7 +567,7 @@ void fused_head_forward_range(const Tensor& ya, const Tensor& aff2, const Tensor
     xo = x_out->data_ptr<float>();
   }
   c10::DeviceGuard guard(ya.device());
-  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
+  const int rc = tds_head_fwd_pb(ya_out(ya), ya_dec(b2, mag), wfc.data_ptr<float>(), bf, aff2.data_ptr<float>(),
                                  part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
                                  (int)Q, (int)NC, stream_of(ya), true, lab, dlogits.data_ptr<float>(),
                                  loss.data_ptr<float>(), inv.data_ptr<float>(), (int)c0, (int)c1);
@@ -567,11 +581,11 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
     const Tensor& ya, const Tensor& partial2, const Tensor& b2, const c10::optional<Tensor>& gamma2,
     const c10::optional<Tensor>& beta2, const c10::optional<Tensor>& rm2, const c10::optional<Tensor>& rv2,
     const c10::optional<Tensor>& nbt2, double momentum, double eps, const Tensor& wfc, const c10::optional<Tensor>& bfc,
-    int64_t P, const c10::optional<Tensor>& x_out) {
+    int64_t P, const c10::optional<Tensor>& x_out, const c10::optional<Tensor>& mag) {
   TORCH_CHECK(ya.dim() == 3 && ya.size(1) == 32, "fused_head_forward: ya must be [B,32,PB]");
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_forward: needs P/2 >= 4 pooled columns and B >= 1");
-  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(ya, at::kHalf, {B, 32, pb_plane(P)}, "ya (fp16)");
   TORCH_CHECK(partial2.is_cuda() && partial2.scalar_type() == at::kDouble && partial2.numel() % 64 == 0, "partial2");
   const int nch = (int)(partial2.numel() / 64);
   need(b2, at::kFloat, {32}, "conv2.bias");
@@ -596,15 +610,15 @@ std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
   }
   c10::DeviceGuard guard(ya.device());
   hipStream_t st = stream_of(ya);
-  auto stats = at::empty({64}, ya.options());
-  auto aff = at::empty({64}, ya.options());
+  auto stats = at::empty({64}, ya.options().dtype(at::kFloat));
+  auto aff = at::empty({64}, ya.options().dtype(at::kFloat));
   tds_bn_reduce_finalize(partial2.data_ptr<double>(), 32, nch, B * P * P, b2.data_ptr<float>(), (float)eps,
                          (float)momentum, g, be, stats.data_ptr<float>(), rm, rv, nb, aff.data_ptr<float>(), st);
   const int nblk = 32 * tds_head_pb_nblk((int)Q);
   auto part = at::empty({(int64_t)(nblk + 32) * B * NC}, ya.options().dtype(at::kDouble));
   auto lsum = at::empty({B * NC}, ya.options().dtype(at::kDouble));
-  auto logits = at::empty({B, NC}, ya.options());
-  const int rc = tds_head_fwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
+  auto logits = at::empty({B, NC}, ya.options().dtype(at::kFloat));
+  const int rc = tds_head_fwd_pb(ya_out(ya), ya_dec(b2, mag), wfc.data_ptr<float>(), bf, aff.data_ptr<float>(),
                                  part.data_ptr<double>(), lsum.data_ptr<double>(), logits.data_ptr<float>(), xo, (int)B,
                                  (int)Q, (int)NC, st);
   TORCH_CHECK(rc == 0, "fused_head_forward: unsupported shape");
@@ -647,7 +661,7 @@ int64_t head_bwd_workspace(int64_t B, int64_t P) {
 // same g2m_out / partial_out to every chunk and finalize=True on the last one, which then runs
 // the BN2 backward finalize and the bias gradient (outputs 1-3 and 5 are empty before that).
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
-    const Tensor& dlogits, const Tensor& ya, const Tensor& stats2, const Tensor& aff2,
+    const Tensor& dlogits, const Tensor& ya, const Tensor& stats2, const Tensor& aff2, const Tensor& b2,
     const c10::optional<Tensor>& gamma2, const Tensor& wfc, int64_t P, const c10::optional<Tensor>& dw_out,
     double scale, bool compute_dw, double update_lr, const c10::optional<Tensor>& dbfc_out,
     const c10::optional<Tensor>& dg_out, const c10::optional<Tensor>& dbe_out, bool keep_dw, int64_t c_begin,
@@ -657,13 +671,14 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   const int64_t B = ya.size(0), Q = P / 2;
   TORCH_CHECK(Q >= 4 && B >= 1, "fused_head_backward: needs P/2 >= 4 pooled columns and B >= 1");
   TORCH_CHECK(0 <= c_begin && c_begin < c_end && c_end <= 32, "fused_head_backward: bad channel range");
-  need(ya, at::kFloat, {B, 32, pb_plane(P)}, "ya");
+  need(ya, at::kHalf, {B, 32, pb_plane(P)}, "ya (fp16)");
   const int64_t NC = wfc.size(0);
   need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
   need(dlogits, at::kFloat, {B, NC}, "dlogits");
   need(stats2, at::kFloat, {64}, "stats2");
   need(aff2, at::kFloat, {64}, "aff2");
   const float* g = optf(gamma2, 32, "bn2.weight");
+  const TdsYaDec yd = ya_dec(b2, mag);
   c10::DeviceGuard guard(ya.device());
   hipStream_t st = stream_of(ya);
   const bool upd = update_lr > 0.0;
@@ -706,7 +721,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   }
   // g2m's per-channel scales 2^-e_c: straight into kbuf[96..128) for a whole-weight call, into the
   // workspace tail for the channel chunks (copied at the finalizing call)
-  auto kbuf = at::empty({128}, ya.options());
+  auto kbuf = at::empty({128}, ya.options().dtype(at::kFloat));
   float* g2inv_tail = reinterpret_cast<float*>(partial.data_ptr<double>() + (int64_t)32 * npass * nblk * 4);
   float* g2inv = whole ? kbuf.data_ptr<float>() + 96 : g2inv_tail;
   auto* g2p = reinterpret_cast<unsigned short*>(g2m.data_ptr<at::Half>());
@@ -724,7 +739,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     TdsHeadBwdFin hf{reinterpret_cast<uint32_t*>(cmax.data_ptr<int>()), stats2.data_ptr<float>(), g,
                      dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), kbuf.data_ptr<float>(), dbfc.data_ptr<float>(),
                      opt_mag(mag, mag_numel(B, P))};
-    const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
+    const int rc = tds_head_bwd_pb(ya_out(ya), yd, wfc.data_ptr<float>(), aff2.data_ptr<float>(),
                                    dlogits.data_ptr<float>(), g2p, partial.data_ptr<double>(),
                                    compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                    upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
@@ -733,7 +748,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
     check_launches("fused_head_backward");
     return {dW, dbfc, dgamma, dbeta, g2m, kbuf};
   }
-  const int rc = tds_head_bwd_pb(ya.data_ptr<float>(), wfc.data_ptr<float>(), aff2.data_ptr<float>(),
+  const int rc = tds_head_bwd_pb(ya_out(ya), yd, wfc.data_ptr<float>(), aff2.data_ptr<float>(),
                                  dlogits.data_ptr<float>(), g2p, partial.data_ptr<double>(),
                                  compute_dw && dW.defined() ? dW.data_ptr<float>() : nullptr,
                                  upd ? const_cast<float*>(wfc.data_ptr<float>()) : nullptr, (int)B, (int)Q, (int)NC,
@@ -741,7 +756,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> fused_head_backward(
   TORCH_CHECK(rc == 0, "fused_head_backward: unsupported shape (rc ", rc, ")");
   if (!finalize) {
     check_launches("fused_head_backward");
-    const Tensor none = at::empty({0}, ya.options());
+    const Tensor none = at::empty({0}, ya.options().dtype(at::kFloat));
     return {dW, none, none, none, g2m, none};
   }
   auto dgamma = sink_or_empty(dg_out, {32}, ya, "dgamma2_out");
@@ -1070,10 +1085,11 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
   m.def(
       "fused_head_forward(Tensor ya, Tensor partial2, Tensor b2, Tensor? gamma2, Tensor? beta2, Tensor(a!)? rm2, "
       "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor wfc, Tensor? bfc, int P, "
-      "Tensor(d!)? x_out=None) -> (Tensor, Tensor, Tensor)",
+      "Tensor(d!)? x_out=None, Tensor? mag=None) -> (Tensor, Tensor, Tensor)",
       &fused_head_forward);
   m.def(
-      "fused_head_backward(Tensor dlogits, Tensor ya, Tensor stats2, Tensor aff2, Tensor? gamma2, Tensor(e!) wfc, "
+      "fused_head_backward(Tensor dlogits, Tensor ya, Tensor stats2, Tensor aff2, Tensor b2, Tensor? gamma2, "
+      "Tensor(e!) wfc, "
       "int P, Tensor(a!)? dw_out, float scale, bool compute_dw=True, float update_lr=0.0, "
       "Tensor(b!)? dbfc_out=None, Tensor(c!)? dg_out=None, Tensor(d!)? dbe_out=None, bool keep_dw=True, "
       "int c_begin=0, int c_end=32, bool finalize=True, Tensor(f!)? g2m_out=None, Tensor(g!)? partial_out=None, "
@@ -1084,16 +1100,19 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor(b!)? rv2, Tensor(c!)? nbt2, float momentum, float eps, Tensor(d!)? mag=None) -> "
       "(Tensor, Tensor, Tensor, Tensor, Tensor)",
       &fused_conv2_forward_bn);
-  m.def("fused_head_forward_aff(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor(a!)? x_out=None) -> Tensor",
+  m.def("fused_head_forward_aff(Tensor ya, Tensor aff2, Tensor b2, Tensor? mag, Tensor wfc, Tensor? bfc, int P, "
+        "Tensor(a!)? x_out=None) -> Tensor",
         &fused_head_forward_aff);
-  m.def("fused_head_forward_aff_ce(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, Tensor labels, "
+  m.def("fused_head_forward_aff_ce(Tensor ya, Tensor aff2, Tensor b2, Tensor? mag, Tensor wfc, Tensor? bfc, int P, "
+        "Tensor labels, "
         "Tensor(a!)? x_out=None) -> (Tensor, Tensor, Tensor)",
         &fused_head_forward_aff_ce);
   m.def("head_bwd_workspace(int B, int P) -> int", &head_bwd_workspace);
   m.def("head_forward_range_ws(Tensor ya, Tensor wfc, int P) -> (Tensor, Tensor, Tensor, Tensor, Tensor, Tensor)",
         &head_forward_range_ws);
   m.def(
-      "fused_head_forward_range(Tensor ya, Tensor aff2, Tensor wfc, Tensor? bfc, int P, int c0, int c1, Tensor(a!) part, "
+      "fused_head_forward_range(Tensor ya, Tensor aff2, Tensor b2, Tensor? mag, Tensor wfc, Tensor? bfc, int P, int c0, "
+      "int c1, Tensor(a!) part, "
       "Tensor(b!) lsum, Tensor(c!) logits, Tensor(d!) dlogits, Tensor(e!) loss, Tensor(f!) inv, Tensor? labels=None, "
       "Tensor(g!)? x_out=None) -> ()",
       &fused_head_forward_range);

@@ -17,8 +17,9 @@
 //     monotone per channel with the sign of gamma (a = gamma * invstd), so the window's
 //     argmax value is max(y2) (gamma >= 0) or min(y2) (gamma < 0) -- known before the batch
 //     statistics are.  Every lane holds whole windows of its channel, the 4 x 8 pooled block
-//     of the tile is staged in LDS and stored as ya (pooled_layout.h): one 128-B line per
-//     channel.  The head then streams ya (72 MB per image at 3000^2) instead of y2 (288 MB).
+//     of the tile is staged in LDS and stored as ya (pooled_layout.h) in fp16: the y2h value at
+//     the window's argmax (y2 = h d + b2, launchers.h TdsYaDec), one 64-B run per channel.  The
+//     head then streams ya (36 MB per image at 3000^2) instead of y2 (288 MB in fp32).
 //   * max |y2 - b2| per channel and workgroup goes to ypart (a region of the step's magnitude-bound
 //     workspace, fused_ops.cpp "mag"); reduced with the head backward's max |g2m| by the BN2
 //     backward finalize, it bounds the conv2 output gradient, whose fp16 scale the backward
@@ -49,7 +50,7 @@ constexpr int F2_WG = 3;
 constexpr int F2_PXREC = 32 * 2 + 16;  // staged pixel record: 32 co fp16 + 16 B pad (banks)
 constexpr int F2_STAGE = F2_TH * F2_TC * F2_PXREC;           // a finished tile's padded staging buffer
 constexpr int F2_OFF_S = 2 * F2_PBUF;                  // p1 double buffer first (32 KiB)
-constexpr int F2_YSTAGE = 32 * 32 * 4 + 32 * 2 * 4;     // pooled block: 32 co x 4 x 8 fp32 = 4 KiB, + a2 words
+constexpr int F2_YSTAGE = 32 * 32 * 4 + 32 * 2 * 4;     // pooled block: 32 co x 4 x 8 words (fp16 bits) = 4 KiB, + a2 words
 constexpr int F2_OFF_Y = F2_OFF_S + 2 * F2_STAGE;
 constexpr int F2_LDS = F2_OFF_Y + 2 * F2_YSTAGE;       // + double-buffered output staging
 constexpr int F2_DMA_PER_WAVE = F2_PGROUPS / (F2_THREADS / 64);  // 2
@@ -200,14 +201,14 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
   }
   if constexpr (!EDGE) ymx = max(ymx, __float_as_uint(ymf));
   // pooled windows (rows 4RH + 2i + {0,1}, columns 4g + 2j + {0,1}) -> ya block entry
-  // (prow 2RH + i, pcol 2g + j); v -> v * inv + b2 is monotone (inv > 0) and rounds monotonically,
-  // so ext(v) * inv + b2 == ext(v * inv + b2)
+  // (prow 2RH + i, pcol 2g + j): the fp16 bits of the window's extreme as y2h stores it (v -> v *
+  // ksc is monotone and rounds monotonically, so this is y2h at the argmax pixel)
   // and the argmax codes (a2, conv2_common.h): the first extreme in scan order, two code bits per
   // channel gathered by ballots (lane = 16 g + li: channel 16NT + li of window column 2g + j)
   uint64_t cb0[4], cb1[4];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    float e[2];
+    uint32_t e[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const float v0 = acc[2 * i][2 * j], v1 = acc[2 * i][2 * j + 1], v2 = acc[2 * i + 1][2 * j];
@@ -220,7 +221,7 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
         m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(v0, v1), __builtin_elementwise_maximum(v2, v3));
       else
         m = zg ? v0 : f2_ext4(v0, v1, v2, v3, neg);
-      e[j] = fmaf(m, inv, bco);
+      e[j] = f16_bits(m * ksc);
       // (a NaN window: code 3, unused); the code bits from the three comparisons' ballots by
       // scalar logic (as lane booleans the compiler formed them with ~4 VALU selects a window)
       const uint64_t b0 = __builtin_amdgcn_ballot_w64(v0 == m), b1 = __builtin_amdgcn_ballot_w64(v1 == m),
@@ -228,8 +229,8 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
       cb0[2 * i + j] = ~b0 & (b1 | ~b2);  // code 1 or 3
       cb1[2 * i + j] = ~b0 & ~b1;         // code 2 or 3
     }
-    // pcols 2g, 2g+1 are adjacent floats of one swizzled chunk: one ds_write_b64
-    *reinterpret_cast<float2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_float2(e[0], e[1]);
+    // pcols 2g, 2g+1 are adjacent words of one swizzled chunk: one ds_write_b64
+    *reinterpret_cast<uint2*>(ystage + f2_ystage_off(co, (2 * RH + i) * 8 + 2 * g)) = make_uint2(e[0], e[1]);
   }
   // lane li = 0 of group g stages the 4 windows (2RH + i, 2g + j) in LDS after the pooled block
   // (word = bits 16g .. 16g+15 of each code-bit ballot: channels 16NT + 0..15); f2_store_a2 writes
@@ -259,14 +260,15 @@ __device__ __forceinline__ void f2_stage(const f32x4 (&acc)[4], const F2Tile& x,
           (unsigned short)h[o][r];
 }
 
-// the workgroup stores the staged pooled block: thread e -> channel e / 8, float4 e % 8
-__device__ __forceinline__ void f2_store_ya(const float* ystage, const F2Tile& x, float* __restrict__ ya,
+// the workgroup stores the staged pooled block: thread e -> channel e / 8, 4 values (8 B) e % 8
+__device__ __forceinline__ void f2_store_ya(const float* ystage, const F2Tile& x, unsigned short* __restrict__ ya,
                                             const PBGeom& pg) {
   const int tr = x.r0 / F2_TH, tc = x.c0 / F2_TC;  // = the tile's pooled block
   if (tr >= pg.Q4 || tc >= pg.Q8) return;          // (odd P: a last tile row beyond the pooled image)
   const int e = threadIdx.x, co = e >> 3, part = e & 7;
-  const float4 v = *reinterpret_cast<const float4*>(ystage + f2_ystage_off(co, part * 4));
-  st_stream(reinterpret_cast<float4*>(ya + ((((int64_t)x.b * 32 + co) * pg.Q4 + tr) * pg.Q8 + tc) * 32 + part * 4), v);
+  const uint4 v = *reinterpret_cast<const uint4*>(ystage + f2_ystage_off(co, part * 4));
+  st_stream(reinterpret_cast<uint2*>(ya + ((((int64_t)x.b * 32 + co) * pg.Q4 + tr) * pg.Q8 + tc) * 32 + part * 4),
+            make_uint2(__builtin_amdgcn_perm(v.y, v.x, 0x05040100u), __builtin_amdgcn_perm(v.w, v.z, 0x05040100u)));
 }
 
 // the tile's 32 pooling windows' argmax words (a2, conv2_common.h): thread e < 32 -> window e
@@ -304,7 +306,7 @@ __device__ __forceinline__ void f2_store(const char* stage, const F2Tile& x, uns
 template <int DIAG, int WV>
 __device__ __forceinline__ void f2_run(const uint4* __restrict__ p1, const uint4* __restrict__ wpack,
                                        const float* __restrict__ bias, const float* __restrict__ gamma,
-                                       unsigned short* __restrict__ y2, float* __restrict__ ya,
+                                       unsigned short* __restrict__ y2, unsigned short* __restrict__ ya,
                                        uint32_t* __restrict__ a2,
                                        double* __restrict__ partial, uint32_t* __restrict__ ypart,
                                        const uint32_t* __restrict__ scales,
@@ -478,7 +480,7 @@ __global__ __launch_bounds__(F2_THREADS, F2_WG) void conv2_fwd2_kernel(const uin
                                                                    const uint4* __restrict__ wpack,
                                                                    const float* __restrict__ bias,
                                                                    const float* __restrict__ gamma,
-                                                                   unsigned short* __restrict__ y2, float* __restrict__ ya,
+                                                                   unsigned short* __restrict__ y2, unsigned short* __restrict__ ya,
                                                                    uint32_t* __restrict__ a2,
                                                                    double* __restrict__ partial,
                                                                    uint32_t* __restrict__ ypart,
@@ -525,7 +527,7 @@ static int f2_diag_env() { return 0; }
 int tds_conv2_fwd2_fin_doubles(int nwg) { return ((nwg + F2_GROUP - 1) / F2_GROUP) * 32 * 2; }
 int tds_conv2_fwd2_fin_words(int nwg) { return ((nwg + F2_GROUP - 1) / F2_GROUP) * 32; }
 
-void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, unsigned short* ya,
                     uint32_t* a2, double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
                     int B, int P, hipStream_t st, const TdsBnFin* bn) {
   const dim3 grid(nwg), block(F2_THREADS);

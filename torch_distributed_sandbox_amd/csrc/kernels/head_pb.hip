@@ -9,6 +9,8 @@
 //
 //   forward : X = relu(a*ya + b);  logits[b][j] = sum X[b][k] W[j][k]           (+ X rows for
 //             DDP's activation exchange when asked)
+//             ya is fp16: the y2h value at each window's argmax, y2 = h d + b2 (launchers.h TdsYaDec);
+//             a*ya + b = (a d) h + (a b2 + b), one v_fma_mix_f32 per value (hp_fma_h)
 //   backward: g = dl W, g2m = g [z > 0] (planar, for the conv2 backward), BN2 sums
 //             (sum g2m, sum g2m*ya) per channel, dW = scale dl^T X and/or W -= lr dW (SGD
 //             step fused into the backward at world size 1)
@@ -20,7 +22,7 @@
 // 256 threads sweep a block row in chunks of 32 blocks (256 pooled columns): wave w takes
 // pooled row w of the block row, lane l block l/2 of the chunk, columns 4*(l%2) .. +3.  Per chunk
 // and thread:
-//   ya  : one float4 per image (the 4 waves together read one 4 KiB run per image),
+//   ya  : 4 fp16 values (8 B) per image (the 4 waves together read one 2 KiB run per image),
 //   W   : one 4-float group per class from the fc's own (c, h, w) layout at the same row and
 //         columns -- a wave-instruction covers one 1 KiB row run.  A row starts at a 16-B boundary
 //         only when (c*Q*Q + y*Q) % 4 == 0 (for Q = 750 every odd row is 8 B off).  Loads are
@@ -28,7 +30,7 @@
 //         the same bytes); stores of a misaligned group are moved as two float2 (or four floats),
 //         picked per wave, so no store straddles a 16-B granule -- misaligned dwordx4 stores of
 //         the weight update cost 14% of the backward,
-//   g2m : one float4 per image (same index as ya), dW / updated W: one 4-float group per class.
+//   g2m : 4 fp16 values per image (planar), dW / updated W: one 4-float group per class.
 // No LDS and no barriers in the stream: the next chunk's loads are issued before the current
 // one is reduced.  64-bit indexing throughout (no buffer descriptors).
 #include "bf16x3.h"
@@ -55,6 +57,31 @@ __host__ __device__ inline HPGrid hp_grid(const PBGeom& g) { return HPGrid{(g.Q4
 __host__ __device__ inline HPGrid hp_grid_b(const PBGeom& g) { return HPGrid{(g.Q4 + HP_BAND_B - 1) / HP_BAND_B}; }
 
 __device__ __forceinline__ float hp_relu(float z) { return z > 0.f ? z : (isnan(z) ? z : 0.f); }
+
+// fma(a, the fp16 value in half HI of w, c): one v_fma_mix_f32 (the fp16 operand converted exactly,
+// one rounding)
+template <int HI>
+__device__ __forceinline__ float hp_fma_h(float a, uint32_t w, float c) {
+  float d;
+  if constexpr (HI != 0)
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(w), "v"(c));
+  else
+    asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[0,1,0]" : "=v"(d) : "v"(a), "v"(w), "v"(c));
+  return d;
+}
+
+// the 4 values a * h_k + c of a loaded ya group (h_0 .. h_3 in y.x lo, y.x hi, y.y lo, y.y hi)
+__device__ __forceinline__ void hp_fma4(float a, uint2 y, float c, float (&o)[4]) {
+  o[0] = hp_fma_h<0>(a, y.x, c);
+  o[1] = hp_fma_h<1>(a, y.x, c);
+  o[2] = hp_fma_h<0>(a, y.y, c);
+  o[3] = hp_fma_h<1>(a, y.y, c);
+}
+
+// ya's decode factor d (launchers.h TdsYaDec; the conv2 backward forms it the same way)
+__device__ __forceinline__ float hp_ydec(const uint32_t* ysc) {
+  return ysc != nullptr ? __uint_as_float(ysc[0]) * __uint_as_float(ysc[1]) / __uint_as_float(ysc[2]) : 1.f;
+}
 
 struct HPThread {
   int blk, prow, half, part;  // block, pooled row in the block (= wave), column half, float4 in the block
@@ -112,21 +139,22 @@ struct HPRow {
 // 4 consecutive floats at any dword alignment (one global_load_dwordx4)
 __device__ __forceinline__ float4 hp_ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 
-// loads of one chunk: ya float4 per image, weight 4-groups per class (zeros outside the image)
+// loads of one chunk: ya 4 fp16 values per image, weight 4-groups per class (zeros outside the image)
 template <int NB>
 struct HPLoad {
-  float4 y[NB], w[10];
+  uint2 y[NB];
+  float4 w[10];
   int sh, nvalid;  // this lane's edge geometry for fix()
   // the loads only: their consumers (fix(), the reduction) run one iteration later, so the wait
   // for them is vmcnt(#loads of the NEXT chunk) -- an edge fix-up right after the loads made
   // it a vmcnt(0) on the prefetch and serialised every chunk on its own latency
-  __device__ __forceinline__ void issue(const float* __restrict__ ya, const float* W, const PBGeom& g, const HPThread& th,
+  __device__ __forceinline__ void issue(const unsigned short* __restrict__ ya, const float* W, const PBGeom& g, const HPThread& th,
                                         int c, int R, int b0, int NC) {
     const int64_t plane = g.plane(), QQ = (int64_t)g.Q * g.Q;
     const int bc = th.blk < g.Q8 ? th.blk : g.Q8 - 1;  // idle lanes of the last chunk: a valid block
     const int64_t yi = (((int64_t)c * g.Q4 + R) * g.Q8 + bc) * 32 + th.part * 4;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) y[b] = *reinterpret_cast<const float4*>(ya + (int64_t)(b0 + b) * 32 * plane + yi);
+    for (int b = 0; b < NB; ++b) y[b] = *reinterpret_cast<const uint2*>(ya + (int64_t)(b0 + b) * 32 * plane + yi);
     const HPRow rw(g, th, c, R);
     sh = rw.sh;
     nvalid = rw.nvalid;
@@ -216,8 +244,8 @@ struct HPFin {
   float* inv_count = nullptr;
 };
 template <int NB>
-__global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __restrict__ ya,
-                                                                 const float* __restrict__ W,
+__global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const unsigned short* __restrict__ ya,
+                                                                 TdsYaDec yd, const float* __restrict__ W,
                                                                  const float* __restrict__ aff2,
                                                                  double* __restrict__ partial,
                                                                  float* __restrict__ xout, PBGeom g, int Btot, int b0,
@@ -230,7 +258,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
   const HPGrid hg = hp_grid(g);
   const int c = c0 + (int)blockIdx.x / hg.per_channel(), band = (int)blockIdx.x - (c - c0) * hg.per_channel();
   const int wg = c * hg.per_channel() + band;  // this workgroup's partial row (all 32 channels' numbering)
-  const float a = aff2[c], bb = aff2[32 + c];
+  // z = a y + b on the stored h: (a d) h + (a b2 + b)
+  const float a = aff2[c], ad = a * hp_ydec(yd.ysc), bd = fmaf(a, yd.b2[c], aff2[32 + c]);
   const int Q = g.Q;
   const int64_t QQ = (int64_t)Q * Q;
   float acc[NB][10];
@@ -261,10 +290,11 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const float* __
     float x[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const float yy[4] = {cur.y[b].x, cur.y[b].y, cur.y[b].z, cur.y[b].w};
+      float zz[4];
+      hp_fma4(ad, cur.y[b], bd, zz);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float v = hp_relu(fmaf(a, yy[k], bb));
+        const float v = hp_relu(zz[k]);
         x[b][k] = (xfull || (rok && px0 + k < Q)) ? v : 0.f;
       }
     }
@@ -396,7 +426,8 @@ struct HBFin {
 
 template <int NB, bool WITH_DW, bool ACC, bool UPD, bool KEEP = true>
 __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
-    const float* __restrict__ ya, const float* W, const float* __restrict__ aff2, const float* __restrict__ dl,
+    const unsigned short* __restrict__ ya, TdsYaDec yd, const float* W, const float* __restrict__ aff2,
+    const float* __restrict__ dl,
     unsigned short* __restrict__ g2h, double* __restrict__ partial, float* dW, float* Wupd, PBGeom g, int b0, int pass,
     int npass, int NC, float scale, float lr, int c0, uint32_t* __restrict__ gpart, HBFin fin,
     const uint32_t* __restrict__ wmaxp, int wrows, int Btot, float* __restrict__ g2inv) {
@@ -443,7 +474,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   }
   __syncthreads();
   const float gsc = g2sc, ginv = 1.f / g2sc;  // (powers of two: exact)
-  const float a = aff2[c], bb = aff2[32 + c];
+  // z = a y + b on the stored h as in the forward; y = h d + b2 itself for the BN2 sums
+  const float a = aff2[c], yds = hp_ydec(yd.ysc), ad = a * yds, b2c = yd.b2[c], bd = fmaf(a, b2c, aff2[32 + c]);
   const int Q = g.Q;
   const int64_t plane = g.plane();
   float sdz = 0.f, sdy = 0.f, sdzr = 0.f, sdyr = 0.f;  // (r: the stored values)
@@ -467,12 +499,14 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
     float x[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const float yy[4] = {cur.y[b].x, cur.y[b].y, cur.y[b].z, cur.y[b].w};
+      float zz[4], yy[4];
+      hp_fma4(ad, cur.y[b], bd, zz);
+      hp_fma4(yds, cur.y[b], b2c, yy);
       float gm[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const bool ok = rok && px0 + k < Q;
-        const float z = fmaf(a, yy[k], bb);
+        const float z = zz[k];
         float gs = 0.f;
 #pragma unroll
         for (int j = 0; j < 10; ++j) {
@@ -641,7 +675,7 @@ int64_t tds_pb_plane(int Q) { return pb_geom(Q).plane(); }
 // [c0, c1) != [0, 32): this launch covers those channels only (in-launch finalize required: the
 // logits are finished by the launch that completes the 32nd channel, so a step's range launches
 // share partial / sums / logits and run on one stream); xout then holds the range's own rows.
-int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
+int tds_head_fwd_pb(const unsigned short* ya, TdsYaDec yd, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st, bool fused_fin,
                     const int64_t* labels, float* dlogits, float* loss, float* inv_count, int c0, int c1) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1 || c0 < 0 || c1 > 32 || c0 >= c1) return -1;
@@ -672,7 +706,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
 #define TDS_HPF(NBV)                                                                                                   \
   case NBV:                                                                                                            \
-    hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, partial, xout, g, \
+    hipLaunchKernelGGL((head_fwd_pb_kernel<NBV>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, yd, Wfc, aff2, partial, xout, g, \
                        B, b0, NC, fin, c0, x_rs, wmaxp);                                                               \
     TDS_LAUNCH_CHECK();                                                                                                \
     break;
@@ -691,7 +725,7 @@ int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const 
 // partial: double [32][npass * nblk][2], npass = ceil(B / 8)
 int tds_head_bwd_pb_npass(int B) { return (B + HP_MAXB - 1) / HP_MAXB; }
 
-int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, unsigned short* g2m,
+int tds_head_bwd_pb(const unsigned short* ya, TdsYaDec yd, const float* Wfc, const float* aff2, const float* dlogits, unsigned short* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
                     int c1, uint32_t* gpart, float* g2inv, hipStream_t st, const TdsHeadBwdFin* hf) {
   if (B < 1 || NC < 1 || NC > 10 || Q < 1 || c0 < 0 || c1 > 32 || c0 >= c1) return -1;
@@ -724,7 +758,7 @@ int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const 
     const int nb = B - b0 < HP_MAXB ? B - b0 : HP_MAXB;
     const bool acc = pass > 0;
 #define TDS_HPB_E(NBV, WD, AC, UP, KP)                                                                             \
-  hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, Wfc, aff2, \
+  hipLaunchKernelGGL((head_bwd_pb_kernel<NBV, WD, AC, UP, KP>), dim3(nwg), dim3(HP_THREADS), 0, st, ya, yd, Wfc, aff2, \
                      dlogits, g2m, partial, dW, Wupd, g, b0, pass, npass, NC, scale, lr, c0, gpart, fin, wmaxp, wrows, \
                      B, g2inv);
 #define TDS_HPB(NBV)                                   \

@@ -103,7 +103,7 @@ struct TdsBnFin {
 };
 int tds_conv2_fwd2_fin_doubles(int nwg);
 int tds_conv2_fwd2_fin_words(int nwg);
-void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, float* ya,
+void tds_conv2_fwd2(const void* p1, const short* wp, const float* bias, const float* gamma, void* y2h, unsigned short* ya,
                     uint32_t* a2, double* partial, uint32_t* ypart, const uint32_t* scales, const int* order, int nwg, int sw, int sk,
                     int B, int P, hipStream_t st, const TdsBnFin* bn = nullptr);
 int tds_conv2_bwd3_num_wg();  // slab rows the backward writes (workgroups it launches)
@@ -197,7 +197,13 @@ bool tds_fused_fin_enabled();  // TDS_FUSED_FIN=0: the separate finalize launche
 // labels (optional, int64 [B]): the cross-entropy loss / dlogits / 1/count formed in the same launch
 // (head_pb.hip HPFin) -- returns 1 when it did, 0 when the caller must run tds_cross_entropy, < 0 on
 // an unsupported shape
-int tds_head_fwd_pb(const float* ya, const float* Wfc, const float* bias, const float* aff2, double* partial,
+// ya: fp16 [B][32][PB] (conv2_fwd2.hip): y2 at each window's argmax = h d + b2[c], d = inv / 2^k
+// from the conv2 pack's scales (ysc = mag + kMagScales, 3 words; nullptr: d = 1)
+struct TdsYaDec {
+  const float* b2;     // [32]
+  const uint32_t* ysc;
+};
+int tds_head_fwd_pb(const unsigned short* ya, TdsYaDec yd, const float* Wfc, const float* bias, const float* aff2, double* partial,
                     double* sums, float* logits, float* xout, int B, int Q, int NC, hipStream_t st,
                     bool fused_fin = true, const int64_t* labels = nullptr, float* dlogits = nullptr,
                     float* loss = nullptr, float* inv_count = nullptr, int c0 = 0, int c1 = 32);
@@ -219,7 +225,7 @@ struct TdsHeadBwdFin {
 };
 // g2m: fp16 [B][32][Q][Q] at a per-channel power-of-two scale 2^e_c (g2inv[c] <- 2^-e_c), bounded
 // by the max |W| per channel and class that the last head forward on this stream measured
-int tds_head_bwd_pb(const float* ya, const float* Wfc, const float* aff2, const float* dlogits, unsigned short* g2m,
+int tds_head_bwd_pb(const unsigned short* ya, TdsYaDec yd, const float* Wfc, const float* aff2, const float* dlogits, unsigned short* g2m,
                     double* partial, float* dW, float* Wupd, int B, int Q, int NC, float scale, float lr, int c0,
                     int c1, uint32_t* gpart, float* g2inv, hipStream_t st, const TdsHeadBwdFin* hf = nullptr);
 

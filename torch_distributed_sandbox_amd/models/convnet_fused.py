@@ -8,7 +8,8 @@ autograd Functions over NHWC fp16 / uint8-level activations (kernels in
 ``_Layer1``  x -> p1            conv1 + BN1(batch stats) + ReLU + pool, conv1 never stored; p1 in fp16
 ``_Conv2``   p1 -> y2, ya       conv2 (TF32-class fp16 MFMA) with BN2 batch-stat partials and the 2x2
                                 max-pool (ya = y2 at each window's argmax, resolved by the sign
-                                of BN2's gamma) fused; its backward rebuilds dy2 from y2 in LDS
+                                of BN2's gamma, in fp16 as y2h stores it) fused; its backward
+                                rebuilds dy2 from y2 in LDS
                                 (BN2/pool backward fused)
 ``_Head``    ya -> logits       BN2 affine + ReLU + fc streamed over ya and the fc weight; fc
                                 grads into the DDP bucket (or the SGD step fused in)
@@ -285,7 +286,7 @@ class _Conv2(torch.autograd.Function):
         return dp1_ph, dw2, db2, None, None, None, None, None, None, None, None, None
 
 
-def _head_forward_grouped(ops, ya, aff2, wfc, bfc, P, ex, upd, link):
+def _head_forward_grouped(ops, ya, aff2, b2, wfc, bfc, P, ex, upd, link):
     """The head forward with the grouped zero-suppressed activation exchange (parallel/factored.py):
     one launch per column group (whole channel planes), each group's fc input rows handed to the
     exchange right after its launch is queued -- its encode and gathers start there, while the next
@@ -300,7 +301,7 @@ def _head_forward_grouped(ops, ya, aff2, wfc, bfc, P, ex, upd, link):
         if upd is not None:
             upd.run_until(k1)
         xg = torch.empty((B, k1 - k0), device=ya.device, dtype=torch.float32)
-        ops.fused_head_forward_range(ya, aff2, wfc, bfc, P, k0 // QQ, k1 // QQ, *ws, link.labels, xg)
+        ops.fused_head_forward_range(ya, aff2, b2, link.mag, wfc, bfc, P, k0 // QQ, k1 // QQ, *ws, link.labels, xg)
         ex.group_ready(gi, xg)
     if upd is not None:
         upd()  # (groups past the last range, had the geometry changed)
@@ -324,8 +325,8 @@ class _Head(torch.autograd.Function):
         B, K = ya.shape[0], wfc.shape[1]
         upd, link.fc_update = link.fc_update, None
         if link.bn_done and ex is not None and _FUSED_FIN and B <= 8 and ex.grouped(B, K):
-            logits = _head_forward_grouped(ops, ya, bn_b, wfc, bfc, P, ex, upd, link)
-            ctx.save_for_backward(ya, bn_a, bn_b, g2, wfc)
+            logits = _head_forward_grouped(ops, ya, bn_b, b2, wfc, bfc, P, ex, upd, link)
+            ctx.save_for_backward(ya, bn_a, bn_b, b2, g2, wfc)
             ctx.P = P
             ctx.y2_meta = (y2.shape, y2.dtype, y2.device)
             ctx.wfc_param = wfc
@@ -343,19 +344,20 @@ class _Head(torch.autograd.Function):
             stats2, aff2 = bn_a, bn_b
             if link.labels is not None:
                 # the loss and dlogits formed by the head forward's finalizing workgroup
-                logits, loss, dlogits = ops.fused_head_forward_aff_ce(ya, aff2, wfc, bfc, P, link.labels, x_out)
+                logits, loss, dlogits = ops.fused_head_forward_aff_ce(ya, aff2, b2, link.mag, wfc, bfc, P, link.labels,
+                                                                      x_out)
                 link.ce = (link.labels, loss, dlogits)
                 STATS["head_fused_ce"] += 1
             else:
-                logits = ops.fused_head_forward_aff(ya, aff2, wfc, bfc, P, x_out)
+                logits = ops.fused_head_forward_aff(ya, aff2, b2, link.mag, wfc, bfc, P, x_out)
         else:  # bn_a = the conv2 forward's BN2 partials
             logits, stats2, aff2 = ops.fused_head_forward(ya, bn_a, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
-                                                          bfc, P, x_out)
+                                                          bfc, P, x_out, mag=link.mag)
         if ex is not None:
             started = ex.begin(x_out, rows=B)
             if not started:
                 raise RuntimeError("fc gradient exchange refused to start after ready() agreed")
-        ctx.save_for_backward(ya, stats2, aff2, g2, wfc)
+        ctx.save_for_backward(ya, stats2, aff2, b2, g2, wfc)
         ctx.P = P
         ctx.y2_meta = (y2.shape, y2.dtype, y2.device)
         ctx.wfc_param = wfc
@@ -366,7 +368,7 @@ class _Head(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dlogits):
-        ya, stats2, aff2, g2, wfc = ctx.saved_tensors
+        ya, stats2, aff2, b2, g2, wfc = ctx.saved_tensors
         dlogits = dlogits.contiguous().float()
         ex = ctx.ex
         ops = _ext.ops()
@@ -387,7 +389,7 @@ class _Head(torch.autograd.Function):
             chunks = ex.column_chunks(wfc.shape[1], planes=32)
             for i, (k0, k1) in enumerate(chunks):
                 last = i == len(chunks) - 1
-                res = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, dst, 1.0, True, 0.0,
+                res = ops.fused_head_backward(dlogits, ya, stats2, aff2, b2, g2, wfc, P, dst, 1.0, True, 0.0,
                                               None, dg_o if last else None, dbe_o if last else None, True,
                                               k0 // (Q * Q), k1 // (Q * Q), last, g2m_buf, part, ctx.link.mag)
                 if acc_w:
@@ -400,7 +402,7 @@ class _Head(torch.autograd.Function):
             dW = dbfc = None
         elif ex is not None:
             # fc gradients come from the activation exchange (parallel/factored.py)
-            _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P, None, 1.0,
+            _, _, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, b2, g2, wfc, P, None, 1.0,
                                                                  False, mag=ctx.link.mag, ypart_done=ctx.link.bn_done)
             ex.defer(dlogits)
             dW = dbfc = None
@@ -415,7 +417,7 @@ class _Head(torch.autograd.Function):
             # update-only step never requests the slot, so DDP never allocates it (ddp.py _lazy_from)
             dw_out = grad_sink.acquire(ctx.wfc_param if ctx.needs_input_grad[12] and keep else None, wfc.shape, wfc)
             dbfc_o, dg_o, dbe_o = _sinks(ctx, ctx.small, (13, 5, 6))
-            dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, g2, wfc, P,
+            dW, dbfc, dg2, dbe2, g2m, kbuf = ops.fused_head_backward(dlogits, ya, stats2, aff2, b2, g2, wfc, P,
                                                                      dw_out if keep else None, 1.0, True,
                                                                      float(lr or 0.0), dbfc_o, dg_o, dbe_o, keep,
                                                                      mag=ctx.link.mag, ypart_done=ctx.link.bn_done)
