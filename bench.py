@@ -105,6 +105,9 @@ def _parser():
                     help="fc gradient path under DDP (parallel/factored.py); auto picks by the xGMI byte model")
     ap.add_argument("--exchange-compress", action=argparse.BooleanOptionalAction, default=True,
                     help="send the activation exchange's fc input rows zero-suppressed (lossless, parallel/zs.py)")
+    ap.add_argument("--exchange-source", choices=["pooled", "rows"], default="pooled",
+                    help="what the activation exchange gathers: the fused head's pooled input ya (fp16) and "
+                         "128 head constants per rank (pooled), or the fc input rows X (rows, zero-suppressed)")
     ap.add_argument("--exchange-groups", type=int, default=None,
                     help="column groups of the zero-suppressed activation exchange (one head launch, encode and "
                          "gather pair each; default 4 at world > 1, 1 at world 1)")
@@ -408,15 +411,25 @@ def _make_store(args, rank: int, world: int):
 
     from torch_distributed_sandbox_amd.parallel.store import rendezvous
 
+    from torch_distributed_sandbox_amd.parallel import launch
+
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    own_port = "MASTER_PORT" not in os.environ and world == 1
     if "MASTER_PORT" not in os.environ:
         # one process (a forced exchange at world 1): nobody else needs to agree on the port, so a
         # free one -- a fixed default collided with the previous run's socket (EADDRINUSE, r6_s4)
-        from torch_distributed_sandbox_amd.parallel import launch
-
         os.environ["MASTER_PORT"] = launch.find_free_port(os.environ["MASTER_ADDR"]) if world == 1 else "29533"
-    store, kind = rendezvous(rank, world, timeout=datetime.timedelta(seconds=args.pg_timeout),
-                             prefer=os.environ.get("TDS_STORE") or args.store)
+    for attempt in range(3):
+        try:
+            store, kind = rendezvous(rank, world, timeout=datetime.timedelta(seconds=args.pg_timeout),
+                                     prefer=os.environ.get("TDS_STORE") or args.store)
+            break
+        except Exception as e:  # noqa: BLE001 -- only a lost race for our own free port is retried
+            # the port found free was taken before the locator bound it (r6_s27: the native store's
+            # own ephemeral listener can draw the port just released): a world-1 run picks another
+            if not (own_port and attempt < 2 and "address already in use" in str(e).lower()):
+                raise
+            os.environ["MASTER_PORT"] = launch.find_free_port(os.environ["MASTER_ADDR"])
     return store, kind, getattr(store, "_locator", store)
 
 
@@ -714,7 +727,7 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
     ddp = DistributedDataParallel(model, device_ids=[local_rank] if on_gpu else None, bucket_cap_mb=args.bucket_mb,
                                   grad_exchange=grad_exchange, overlap_optimizer=args.overlap_optimizer,
                                   allreduce_chunks=args.allreduce_chunks, exchange_compress=args.exchange_compress,
-                                  exchange_groups=args.exchange_groups)
+                                  exchange_groups=args.exchange_groups, exchange_source=args.exchange_source)
 
     ddp.attach_optimizer(optimizer)
 
@@ -882,8 +895,8 @@ def _attempt(args, world, rank, backend, grad_exchange, reserve, backend_label, 
             "overlap_optimizer": ddp.overlap_optimizer,
             "fc_grad": ddp.fc_grad_path(),
             "allreduce_chunks": ddp.allreduce_chunks,
-            "x_exchange": [{"ratio": round(ex.x_ratio, 4), **ex.zs_stats} for ex in ddp.exchanges if ex.compress
-                           and ex.zs_stats["steps"]] or None,
+            "x_exchange": [{"source": ex.source, "last_path": ex.last_path, "ratio": round(ex.x_ratio, 4),
+                            **ex.zs_stats} for ex in ddp.exchanges if ex.steps_exchanged] or None,
             "reserve_cus": reserve,
             "prefetch": data_stream is not None,
             # where the batch's x moments (BN1's weight-independent half) are formed: in the upsample's pass

@@ -135,11 +135,12 @@ def test_linear_dw_kernel(gpu):
     assert (full[:, :3000] == 7).all() and (full[:, 6000:] == 7).all()
 
 
-@pytest.mark.parametrize("mode", ["activations", "sharded", "chunked"])
-def test_activation_exchange_fused_convnet(pg, gpu, mode):
-    """Forced activation exchange at world size 1 runs the whole GPU path (head
-    forward writing the fc input rows, head backward without dW, linear_dw into
-    the bucket) and must reproduce the plain fused gradients."""
+@pytest.mark.parametrize("mode,source", [("activations", "pooled"), ("activations", "rows"), ("sharded", "pooled"),
+                                         ("chunked", "pooled")])
+def test_activation_exchange_fused_convnet(pg, gpu, mode, source):
+    """Forced activation exchange at world size 1 runs the whole GPU path (the pooled input and the
+    head constants gathered, or the head forward writing the fc input rows; head backward without
+    dW; dW into the bucket) and must reproduce the plain fused gradients."""
     import copy
 
     from torch_distributed_sandbox_amd.models import ConvNet
@@ -150,7 +151,7 @@ def test_activation_exchange_fused_convnet(pg, gpu, mode):
     H = 256  # fc: 10 x 131072 (exchange candidate)
     m = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
     ref = copy.deepcopy(m)
-    ddp = DistributedDataParallel(m, grad_exchange=mode)
+    ddp = DistributedDataParallel(m, grad_exchange=mode, exchange_source=source)
     assert len(ddp.exchanges) == 1
     opt = ddp.attach_optimizer(SGD(m.parameters(), 0.01))
     x = torch.rand(3, 1, H, H, device=gpu)
@@ -172,11 +173,15 @@ def test_activation_exchange_fused_convnet(pg, gpu, mode):
             for p, q in zip(m.parameters(), ref.parameters()):
                 q.copy_(p)
     assert ddp.exchanges[0].steps_exchanged == 2
+    if mode == "activations":
+        assert ddp.fc_grad_path() == ("activation-exchange(pooled)" if source == "pooled" else
+                                      "activation-exchange(zs)")
 
 
 @pytest.mark.parametrize("exchange,fuse", [("allreduce", False), ("activations", False), ("sharded", False),
-                                           ("chunked", False),
-                                           ("allreduce", True), ("activations", True), ("sharded", True)])
+                                           ("chunked", False), ("activations:rows", False),
+                                           ("allreduce", True), ("activations", True), ("sharded", True),
+                                           ("activations:rows", True)])
 def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     """overlap_optimizer: the fc bucket's collective + SGD update run on a side stream
     and the next forward's head waits on a parameter fence; the trajectory must be
@@ -189,12 +194,16 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
     from torch_distributed_sandbox_amd.ops import SGD, CrossEntropyLoss, param_fence
     from torch_distributed_sandbox_amd.parallel import DistributedDataParallel
 
+    exchange, _, source = exchange.partition(":")
+    source = source or "pooled"  # activations: the pooled input (default) or the zero-suppressed rows
+    zs_path = exchange == "sharded" or (exchange == "activations" and source == "rows")
     torch.manual_seed(0)
     H = 256
     m1 = ConvNet(image_shape=(H, H), device=gpu, mode="fused")
     m2 = copy.deepcopy(m1)
-    d1 = DistributedDataParallel(m1, grad_exchange=exchange, overlap_optimizer=True, fuse_update_in_backward=fuse)
-    d2 = DistributedDataParallel(m2, grad_exchange=exchange)
+    d1 = DistributedDataParallel(m1, grad_exchange=exchange, overlap_optimizer=True, fuse_update_in_backward=fuse,
+                                 exchange_source=source)
+    d2 = DistributedDataParallel(m2, grad_exchange=exchange, exchange_source=source)
     assert d1.overlap_optimizer and len(d1._deferred) == 1
     o1 = d1.attach_optimizer(SGD(m1.parameters(), 1e-4))
     o2 = d2.attach_optimizer(SGD(m2.parameters(), 1e-4))
@@ -216,13 +225,15 @@ def test_overlap_optimizer_matches_sequential(pg, gpu, exchange, fuse):
         assert param_fence.pending(m1.fc.weight) or d1.last_deferred_inline
         if fuse and exchange == "allreduce":
             assert d1.last_deferred_inline and not param_fence.pending(m1.fc.bias)
-        if step == 0 and exchange in ("activations", "sharded") and d1.exchanges[0].compress:
+        if step == 0 and zs_path:
             assert d1.fc_grad_path().endswith("(zs)")  # tagged on the first step (its count check is deferred)
+        elif step == 0 and exchange == "activations":
+            assert d1.fc_grad_path().endswith("(pooled)")
         if fuse:
             assert not d1._fused_done  # consumed by the step: the bias was updated, the weight skipped
     d1.wait_pending_updates()
     torch.cuda.synchronize()
-    if exchange in ("activations", "sharded") and d1.exchanges[0].compress:
+    if zs_path:
         assert d1.exchanges[0].zs_stats["overflows"] >= 1  # step 2 went through the dense re-send
     for (n, p), q in zip(m1.named_parameters(), m2.parameters()):
         if fuse:  # same arithmetic (p - lr*g) in another kernel: equal up to fma contraction

@@ -532,3 +532,26 @@ def test_zs_codec_reference_roundtrip():
         out = torch.full((n,), 7.0)
         zs.decode(meta, vals, out)
         assert torch.equal(out.view(torch.int32), x.view(torch.int32))
+
+
+def test_pooled_exchange_geometry_and_pricing():
+    """The pooled activation-exchange source (parallel/factored.py): the pooled plane of the fused
+    head's fc inputs (csrc/kernels/pooled_layout.h: 4 x 8 blocks), and no pooled pricing for a layer
+    that cannot take it (CPU weight, or inputs that are not 32 square planes)."""
+    import torch
+
+    from torch_distributed_sandbox_amd.parallel import factored
+
+    assert factored.pooled_plane(32 * 747 * 747) == 748 * 752
+    assert factored.pooled_plane(32 * 64 * 64) == 64 * 64
+    assert factored.pooled_plane(32 * 10 * 11) is None and factored.pooled_plane(33) is None
+    w = torch.nn.Parameter(torch.zeros(10, 32 * 64 * 64))
+    ex = factored.ActivationExchange(w, None, None, 2, "auto", lambda on: None, lambda: None, None)
+    assert ex.source == "pooled" and not ex.pooled_capable()  # a CPU weight: the rows path prices it
+    ex.detach()
+    try:
+        factored.ActivationExchange(w, None, None, 2, "auto", lambda on: None, lambda: None, None, source="x")
+    except ValueError:
+        pass
+    else:
+        raise AssertionError("an unknown source must be refused")

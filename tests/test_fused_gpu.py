@@ -424,6 +424,50 @@ def test_head_forward_backward(gpu, P, B):
         assert torch.allclose(wfc, w0 - 0.5 * dW, rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("P,B,W", [(64, 3, 2), (38, 5, 1), (130, 2, 3)])
+def test_head_update_pooled(gpu, P, B, W):
+    """The pooled activation exchange's fc step (ops.head_update_pooled, parallel/factored.py "pooled")
+    from W ranks' ya and head records (each rank its own BN2 affine): the X it recomputes is bit for
+    bit the head forward's own X rows (x_out), and W -= lr*scale*dl^T X, dW = / += scale*dl^T X match
+    fp64 on those rows.  P = 38: odd pooled size (rows off the 16-B grid)."""
+    ops = _ops()
+    Q, NC = P // 2, 10
+    torch.manual_seed(P + 10 * B + W)
+    wfc = torch.randn(NC, 32 * Q * Q, device=gpu) * 0.01
+    bfc = torch.randn(NC, device=gpu)
+    b2 = torch.randn(32, device=gpu) * 0.1
+    mag = set_ya_scale(new_mag(gpu, B, P), 0.5)  # ya decode d = 0.5
+    yas, recs, xs = [], [], []
+    for _ in range(W):
+        h = torch.randn(B, P, P, 32, device=gpu).half()
+        ya = ya_of(h, torch.randn(32, device=gpu), Q)
+        aff2 = torch.cat([torch.randn(32, device=gpu), torch.randn(32, device=gpu) * 0.1])
+        xo = torch.empty(B, 32 * Q * Q, device=gpu)
+        ops.fused_head_forward_aff(ya, aff2, b2, mag, wfc, bfc, P, xo)
+        yas.append(ya)
+        recs.append(ops.head_pooled_record(aff2, b2, mag))
+        xs.append(xo)
+    ya_all, rec_all, x_all = torch.stack(yas), torch.stack(recs), torch.cat(xs)
+    M = W * B
+    # one-hot dl, scale 1: row j of the result is rank / image j's X itself (exact products and sums)
+    eye = torch.zeros(M, NC, device=gpu)
+    eye[torch.arange(M), torch.arange(M)] = 1.0
+    out = torch.full_like(wfc, 7.0)
+    ops.head_update_pooled(eye, ya_all, rec_all, wfc, out, P, 1.0, 0.0, 1)
+    assert torch.equal(out[:M], x_all), (out[:M] - x_all).abs().max()
+    assert (out[M:] == 0).all()
+    dl = torch.randn(M, NC, device=gpu)
+    scale, lr = 1.0 / W, 0.25
+    ref = (dl.double().t() @ x_all.double()) * scale
+    ops.head_update_pooled(dl, ya_all, rec_all, wfc, out, P, scale, 0.0, 1)
+    _check(out, ref, 1e-6, "dW (=)")
+    ops.head_update_pooled(dl, ya_all, rec_all, wfc, out, P, scale, 0.0, 2)
+    _check(out, 2 * ref, 1e-6, "dW (+=)")
+    w0 = wfc.double()
+    ops.head_update_pooled(dl, ya_all, rec_all, wfc, None, P, scale, lr, 0)
+    _check(wfc, w0 - lr * ref, 1e-6, "W update")
+
+
 @pytest.mark.parametrize("P,dscale", [(37, 1.0), (40, 1.0), (130, 1.0), (40, 1e-7), (40, 3e4)])
 def test_conv2_backward_fused_with_bn2_pool(gpu, P, dscale):
     """fused_conv2_backward_y2 (dy2 rebuilt in LDS from y2 + g2m + the BN2 constants) vs the fp64

@@ -110,7 +110,9 @@ def _check_two_ranks(tmp_path, mode, overlap, plan):
     launch.spawn(_worker, args=(world, launch.find_free_port(), mode, overlap, str(tmp_path), plan), nprocs=world,
                  timeout=240)
     recs = [torch.load(tmp_path / f"r{r}.pt", weights_only=True) for r in range(world)]
-    assert recs[0]["fc_grad"] == {"allreduce": "allreduce", "activations": "activation-exchange(zs)",
+    # (the fused head offers the exchange its pooled input; the generic plan's Linear sends its rows)
+    pooled = "activation-exchange(pooled)" if plan == "fused" else "activation-exchange(zs)"
+    assert recs[0]["fc_grad"] == {"allreduce": "allreduce", "activations": pooled,
                                   "sharded": "sharded-exchange(zs)", "chunked": "chunked-allreduce"}[mode]
     fused_expected = overlap and mode in ("activations", "sharded")
     assert (recs[0]["steps"][0]["grads"]["fc.weight"] is None) == fused_expected

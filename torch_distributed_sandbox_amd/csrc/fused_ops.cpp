@@ -575,6 +575,56 @@ void fused_head_forward_range(const Tensor& ya, const Tensor& aff2, const Tensor
   check_launches("fused_head_forward_range");
 }
 
+// The activation exchange's "pooled" source (parallel/factored.py): the ranks all-gather ya and a
+// 128-float record of the head constants their forward used (head_pooled_record: aff2 | the ya
+// scale words | b2), and every rank forms the fc step from them (head_update_pooled; kernels/
+// head_pb.hip head_upd_pb_kernel).  mode 0: wfc -= lr * scale * dl_all^T X (update only), 1: out =
+// scale * dl_all^T X, 2: out += scale * dl_all^T X; X recomputed from each rank's ya with that rank's
+// record, bitwise the rows its head forward used.
+Tensor head_pooled_record(const Tensor& aff2, const Tensor& b2, const c10::optional<Tensor>& mag) {
+  need(aff2, at::kFloat, {64}, "aff2");
+  need(b2, at::kFloat, {32}, "conv2.bias");
+  uint32_t* m = opt_mag(mag, kMagScales + 3);
+  c10::DeviceGuard guard(aff2.device());
+  auto rec = at::empty({128}, aff2.options());
+  tds_head_pooled_record(aff2.data_ptr<float>(), b2.data_ptr<float>(), m ? m + kMagScales : nullptr,
+                         rec.data_ptr<float>(), stream_of(aff2));
+  check_launches("head_pooled_record");
+  return rec;
+}
+
+void head_update_pooled(const Tensor& dl_all, const Tensor& ya_all, const Tensor& rec_all, const Tensor& wfc,
+                        const c10::optional<Tensor>& out, int64_t P, double scale, double lr, int64_t mode) {
+  TORCH_CHECK(ya_all.dim() == 4 && ya_all.size(2) == 32, "head_update_pooled: ya_all must be [W,B,32,PB]");
+  const int64_t Wr = ya_all.size(0), B = ya_all.size(1), Q = P / 2;
+  TORCH_CHECK(Q >= 4 && B >= 1 && B <= 8, "head_update_pooled: needs P/2 >= 4 and 1 <= B <= 8 images per rank");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "head_update_pooled: mode 0 (update), 1 (=) or 2 (+=)");
+  need(ya_all, at::kHalf, {Wr, B, 32, pb_plane(P)}, "ya_all");
+  need(rec_all, at::kFloat, {Wr, 128}, "rec_all");
+  TORCH_CHECK(wfc.dim() == 2 && wfc.size(1) == 32 * Q * Q && wfc.size(0) >= 1 && wfc.size(0) <= 10,
+              "fc.weight must be [<=10, 32*Q*Q]");
+  const int64_t NC = wfc.size(0);
+  need(wfc, at::kFloat, {NC, 32 * Q * Q}, "fc.weight");
+  need(dl_all, at::kFloat, {Wr * B, NC}, "dl_all");
+  float* o = wfc.data_ptr<float>();
+  if (mode != 0) {
+    TORCH_CHECK(out.has_value() && out->defined(), "head_update_pooled: modes 1 and 2 write into out");
+    need(*out, at::kFloat, {NC, 32 * Q * Q}, "out (dW)");
+    o = out->data_ptr<float>();
+  } else {
+    TORCH_CHECK(lr > 0.0, "head_update_pooled: mode 0 needs lr > 0");
+  }
+  // (the weight-layout stores pick their width from the row's alignment class: 16-B aligned bases)
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(o) % 16 == 0 && reinterpret_cast<uintptr_t>(wfc.data_ptr()) % 16 == 0,
+              "head_update_pooled: fc.weight and out must be 16-B aligned");
+  c10::DeviceGuard guard(wfc.device());
+  const int rc = tds_head_upd_pb(ya_out(ya_all), B * 32 * pb_plane(P), rec_all.data_ptr<float>(), (int)Wr,
+                                 dl_all.data_ptr<float>(), wfc.data_ptr<float>(), o, (int)B, (int)Q, (int)NC,
+                                 (float)scale, (float)lr, (int)mode, stream_of(wfc));
+  TORCH_CHECK(rc == 0, "head_update_pooled: unsupported shape");
+  check_launches("head_update_pooled");
+}
+
 // ---------------------------------------------------------------- head forward (BN2 finalize + fc)
 // returns (logits, stats2 [mean32|invstd32], aff2 [a32|b32])
 std::tuple<Tensor, Tensor, Tensor> fused_head_forward(
@@ -1116,6 +1166,11 @@ TORCH_LIBRARY_FRAGMENT(tdsa, m) {
       "Tensor(b!) lsum, Tensor(c!) logits, Tensor(d!) dlogits, Tensor(e!) loss, Tensor(f!) inv, Tensor? labels=None, "
       "Tensor(g!)? x_out=None) -> ()",
       &fused_head_forward_range);
+  m.def("head_pooled_record(Tensor aff2, Tensor b2, Tensor? mag=None) -> Tensor", &head_pooled_record);
+  m.def(
+      "head_update_pooled(Tensor dl_all, Tensor ya_all, Tensor rec_all, Tensor(a!) wfc, Tensor(b!)? out, int P, "
+      "float scale, float lr, int mode) -> ()",
+      &head_update_pooled);
   m.def("mag_numel(int B, int P) -> int", &mag_numel);
   m.def("mag_ypart_count() -> int", &mag_ypart_count);
   m.def("conv2_bwd_clock_dump(int nwg) -> Tensor", &conv2_bwd_clock_dump);

@@ -653,9 +653,147 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   }
 }
 
+// The activation exchange's fc step from every rank's POOLED input (parallel/factored.py, source
+// "pooled"): the ranks all-gather ya (fp16, 36 MB per image at 3000^2, half of X in fp32 and no
+// encode) and a 128-float record of the head constants their forward used; every rank then forms
+//   MODE 0: W -= lr * scale * sum_m dl[m] (x) X_m        (update only, the SGD step)
+//   MODE 1: out = scale * sum_m dl[m] (x) X_m             (dW)
+//   MODE 2: out += scale * sum_m dl[m] (x) X_m
+// with X_m recomputed from rank r's ya as its head forward did (m = r * NB + b; rec[r]: aff2 [64] |
+// ya scale words [3] | pad | b2 [32] | pad): the same v_fma_mix arithmetic on the same values, so
+// X is bitwise the rows that forward multiplied by the weight.  Workgroup = (channel, band of the
+// backward's HP_BAND_B block rows), 4 columns of one pooled row per thread as the head kernels;
+// per chunk the weight 4-groups are loaded once and every rank's images stream past them.
+constexpr int HP_REC = 128;  // floats per rank record
+
+template <int NB, int MODE>
+__global__ __launch_bounds__(HP_THREADS) void head_upd_pb_kernel(const unsigned short* __restrict__ ya_all,
+                                                                 int64_t ya_rs, const float* __restrict__ rec,
+                                                                 int nranks, const float* __restrict__ dl,
+                                                                 const float* W, float* out, PBGeom g, int NC,
+                                                                 float scale, float lr) {
+  const HPGrid hg = hp_grid_b(g);
+  const int c = (int)blockIdx.x / hg.per_channel(), band = (int)blockIdx.x - c * hg.per_channel();
+  const int Q = g.Q;
+  const int64_t plane = g.plane();
+  const int nch = (g.Q8 + 31) / 32;
+  const int R0 = band * HP_BAND_B, nit = (min(g.Q4, R0 + HP_BAND_B) - R0) * nch;
+#pragma unroll 1
+  for (int i = 0; i < nit; ++i) {
+    const int R = R0 + i / nch;
+    const HPThread th(i % nch);
+    HPLoad<NB> cur;  // the weight 4-groups and rank 0's images
+    cur.issue(ya_all, W, g, th, c, R, 0, NC);
+    cur.fix(NC);
+    const int py = 4 * R + th.prow, px0 = th.blk * 8 + th.half * 4;
+    const bool rok = th.blk < g.Q8 && py < Q;
+    const int64_t yi = (((int64_t)c * g.Q4 + R) * g.Q8 + (th.blk < g.Q8 ? th.blk : g.Q8 - 1)) * 32 + th.part * 4;
+    float acc[10][4];
+#pragma unroll
+    for (int j = 0; j < 10; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[j][k] = 0.f;
+#pragma unroll 1
+    for (int r = 0; r < nranks; ++r) {
+      uint2 y[NB];
+      if (r == 0) {
+#pragma unroll
+        for (int b = 0; b < NB; ++b) y[b] = cur.y[b];
+      } else {
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          y[b] = *reinterpret_cast<const uint2*>(ya_all + r * ya_rs + (int64_t)b * 32 * plane + yi);
+      }
+      // rank r's head constants, formed as its head kernels formed them (head_fwd_pb_kernel)
+      const float* rr = rec + (int64_t)r * HP_REC;
+      const TdsYaDec yd{rr + 68, reinterpret_cast<const uint32_t*>(rr + 64)};
+      const float a = rr[c], ad = a * hp_ydec(yd.ysc), bd = fmaf(a, yd.b2[c], rr[32 + c]);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float zz[4];
+        hp_fma4(ad, y[b], bd, zz);
+        float x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) x[k] = (rok && px0 + k < Q) ? hp_relu(zz[k]) : 0.f;
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          if (j < NC) {
+            const float dv = dl[(r * NB + b) * NC + j];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[j][k] = fmaf(dv, x[k], acc[j][k]);
+          }
+        }
+      }
+    }
+    const HPRow rw(g, th, c, R);
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+      if (j < NC) {
+        const float4 d = make_float4(scale * acc[j][0], scale * acc[j][1], scale * acc[j][2], scale * acc[j][3]);
+        if constexpr (MODE == 0) {
+          const float4 w = cur.w[j];
+          hp_store4(out, g, rw, j, make_float4(w.x - lr * d.x, w.y - lr * d.y, w.z - lr * d.z, w.w - lr * d.w));
+        } else if constexpr (MODE == 1) {
+          hp_store4(out, g, rw, j, d);
+        } else if (rw.nvalid > 0) {
+          float* p = out + (int64_t)j * 32 * Q * (int64_t)Q + rw.off;
+          const float e[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (k < rw.nvalid) p[k] += e[k];
+        }
+      }
+    }
+  }
+}
+
+// one rank's record (HP_REC floats): aff2 [64] | the ya scale words [3] (1, 1, 1 without) | 0 | b2 [32] | 0
+__global__ __launch_bounds__(HP_REC) void hp_record_kernel(const float* __restrict__ aff2, const float* __restrict__ b2,
+                                                          const uint32_t* __restrict__ ysc, float* __restrict__ rec) {
+  const int t = threadIdx.x;
+  float v = 0.f;
+  if (t < 64) v = aff2[t];
+  else if (t < 67) v = ysc != nullptr ? __uint_as_float(ysc[t - 64]) : 1.f;
+  else if (t >= 68 && t < 100) v = b2[t - 68];
+  rec[t] = v;
+}
+
 }  // namespace tds
 
 using namespace tds;
+
+void tds_head_pooled_record(const float* aff2, const float* b2, const uint32_t* ysc, float* rec, hipStream_t st) {
+  hipLaunchKernelGGL(hp_record_kernel, dim3(1), dim3(HP_REC), 0, st, aff2, b2, ysc, rec);
+  TDS_LAUNCH_CHECK();
+}
+
+int tds_head_upd_pb(const unsigned short* ya_all, int64_t ya_rs, const float* rec, int nranks, const float* dl,
+                    const float* W, float* out, int B, int Q, int NC, float scale, float lr, int mode, hipStream_t st) {
+  if (B < 1 || B > HP_MAXB || NC < 1 || NC > 10 || Q < 4 || nranks < 1 || mode < 0 || mode > 2) return -1;
+  const PBGeom g = pb_geom(Q);
+  const int nwg = 32 * hp_grid_b(g).per_channel();
+#define TDS_HPU_M(NBV, MD)                                                                                        \
+  hipLaunchKernelGGL((head_upd_pb_kernel<NBV, MD>), dim3(nwg), dim3(HP_THREADS), 0, st, ya_all, ya_rs, rec, nranks, \
+                     dl, W, out, g, NC, scale, lr);
+#define TDS_HPU(NBV)                                    \
+  case NBV:                                             \
+    if (mode == 0) {                                    \
+      TDS_HPU_M(NBV, 0)                                 \
+    } else if (mode == 1) {                             \
+      TDS_HPU_M(NBV, 1)                                 \
+    } else {                                            \
+      TDS_HPU_M(NBV, 2)                                 \
+    }                                                   \
+    break;
+  switch (B) {
+    TDS_HPU(1) TDS_HPU(2) TDS_HPU(3) TDS_HPU(4) TDS_HPU(5) TDS_HPU(6) TDS_HPU(7) TDS_HPU(8)
+    default: return -1;
+  }
+#undef TDS_HPU
+#undef TDS_HPU_M
+  TDS_LAUNCH_CHECK();
+  return 0;
+}
 
 // The forward's per-workgroup max |W[j]| ([32 * nblk][10] float bits), read by the next head backward
 // on the same stream for g2m's fp16 scale: one buffer per (device, stream), the forward and the

@@ -208,6 +208,14 @@ int tds_head_fwd_pb(const unsigned short* ya, TdsYaDec yd, const float* Wfc, con
                     bool fused_fin = true, const int64_t* labels = nullptr, float* dlogits = nullptr,
                     float* loss = nullptr, float* inv_count = nullptr, int c0 = 0, int c1 = 32);
 int tds_head_bwd_pb_npass(int B);
+// The activation exchange's fc step from the all-gathered pooled inputs (head_pb.hip head_upd_pb_kernel):
+// ya_all [nranks][B][32][PB] fp16 (ya_rs elements per rank), rec [nranks][128] (tds_head_pooled_record),
+// dl [nranks * B][NC]; mode 0: out = W - lr * scale * dl^T X (out may be W), 1: out = scale * dl^T X,
+// 2: out += scale * dl^T X
+int tds_head_upd_pb(const unsigned short* ya_all, int64_t ya_rs, const float* rec, int nranks, const float* dl,
+                    const float* W, float* out, int B, int Q, int NC, float scale, float lr, int mode, hipStream_t st);
+// a rank's record for tds_head_upd_pb: aff2 [64] | ya scale words [3] (ysc nullptr: 1, 1, 1) | 0 | b2 [32] | 0
+void tds_head_pooled_record(const float* aff2, const float* b2, const uint32_t* ysc, float* rec, hipStream_t st);
 // channels [c0, c1) only (K-chunked fc gradient: each chunk's dW columns can be all-reduced as
 // soon as its launch lands; the BN2 partials of the other channels are left untouched)
 // gpart (optional): max |g2m| per workgroup (float bits), [32][npass][nblk]

@@ -324,7 +324,12 @@ class _Head(torch.autograd.Function):
         P = y2.shape[1]
         B, K = ya.shape[0], wfc.shape[1]
         upd, link.fc_update = link.fc_update, None
-        if link.bn_done and ex is not None and _FUSED_FIN and B <= 8 and ex.grouped(B, K):
+        pooled = link.bn_done and ex is not None and B <= 8 and ex.pooled(B)
+        if pooled:
+            # the activation exchange from the pooled input (parallel/factored.py "pooled"): ya and
+            # this rank's head constants leave now, before the head forward; no X rows are written
+            ex.begin_pooled(ya, ops.head_pooled_record(bn_b, b2, link.mag), P)
+        elif link.bn_done and ex is not None and _FUSED_FIN and B <= 8 and ex.grouped(B, K):
             logits = _head_forward_grouped(ops, ya, bn_b, b2, wfc, bfc, P, ex, upd, link)
             ctx.save_for_backward(ya, bn_a, bn_b, b2, g2, wfc)
             ctx.P = P
@@ -338,7 +343,7 @@ class _Head(torch.autograd.Function):
             upd()  # the whole deferred update, before the weight is read
         x_out = None
         # the activation / sharded exchanges send the fc input rows X, which the head writes
-        if ex is not None and ex.planned(B) in ("activations", "sharded"):
+        if ex is not None and not pooled and ex.planned(B) in ("activations", "sharded"):
             x_out = torch.empty((B, K), device=ya.device, dtype=torch.float32)
         if link.bn_done:  # (bn_a, bn_b) = BN2's (stats, affine), finalized by the conv2 forward
             stats2, aff2 = bn_a, bn_b
@@ -353,7 +358,7 @@ class _Head(torch.autograd.Function):
         else:  # bn_a = the conv2 forward's BN2 partials
             logits, stats2, aff2 = ops.fused_head_forward(ya, bn_a, b2, g2, be2, rm2, rv2, nbt2, momentum, eps, wfc,
                                                           bfc, P, x_out, mag=link.mag)
-        if ex is not None:
+        if ex is not None and not pooled:
             started = ex.begin(x_out, rows=B)
             if not started:
                 raise RuntimeError("fc gradient exchange refused to start after ready() agreed")

@@ -103,7 +103,7 @@ class DistributedDataParallel(nn.Module):
                  reducer: str = "auto", grad_exchange: str = "auto", overlap_optimizer: bool = False,
                  fuse_update_in_backward: bool = True, keep_fused_grads: bool = False,
                  allreduce_chunks: Optional[int] = None, exchange_compress: bool = True,
-                 exchange_groups: Optional[int] = None):
+                 exchange_groups: Optional[int] = None, exchange_source: str = "pooled"):
         super().__init__()
         self.module = module
         self.device_ids = device_ids
@@ -237,7 +237,9 @@ class DistributedDataParallel(nn.Module):
                     # column groups of the zero-suppressed activation exchange: they start its gathers
                     # a group's head launch in (earlier window) for ~0.2 ms of launch and tail cost at
                     # the bench shape, worth it only when links carry the rows (world > 1)
-                    groups=exchange_groups if exchange_groups else (4 if self.world_size > 1 else 1)))
+                    groups=exchange_groups if exchange_groups else (4 if self.world_size > 1 else 1),
+                    # the fused head's pooled input instead of the fc rows X (factored.py "pooled")
+                    source=exchange_source))
 
         # ---- overlapped optimizer: the big layers' buckets finish (collective + SGD
         # update) on a side stream while the next forward's convolutions run

@@ -53,6 +53,15 @@ only when the step's gradient is formed (``defer``, after the head backward is q
 above the capacity sends the dense rows once more for that step.  The byte model takes the
 measured ratio: ``link_bytes("activations")`` = B·K·4·ratio.
 
+Pooled source (activation path, the fused ConvNet head; ``source="pooled"``, the default): the
+fc input X = relu(BN2(pooled conv2 output)) is a pointwise function of the head's pooled input ya
+(fp16, 2 bytes per column: half of X in fp32, and no encode) and of 128 head constants per rank (BN2's
+affine of that rank's batch, ya's decode, the conv bias).  The ranks all-gather ya and those
+constants right after the conv2 forward wrote them -- before the head forward starts -- and every
+rank forms the fc step from them (``ops.head_update_pooled``), recomputing each rank's X with that
+rank's constants and the head forward's own arithmetic: bitwise the rows the dense exchange would
+have sent.  ``link_bytes`` prices it at x_ratio 0.5.
+
 Column groups (activation path, zero-suppressed): the rows travel as ``groups`` column ranges
 (whole channel planes on the fused head), each encoded and gathered on its own.  The fused head
 forward runs one launch per group and hands each group's rows over as soon as its launch is
@@ -125,6 +134,19 @@ def choose_path(rows: int, out_f: int, in_f: int, world: int, x_ratio: float = 1
     return min(order, key=lambda p: (costs[p], order.index(p)))
 
 
+def pooled_plane(in_f: int, planes: int = 32) -> Optional[int]:
+    """Elements per (image, channel) of the fused head's pooled input for an fc layer of ``in_f``
+    inputs (csrc/kernels/pooled_layout.h: Q x Q padded to blocks of 4 rows x 8 columns), or None
+    when in_f is not ``planes`` square planes."""
+    if in_f % planes:
+        return None
+    qq = in_f // planes
+    q = int(round(qq ** 0.5))
+    if q * q != qq or q < 4:
+        return None
+    return ((q + 3) // 4 * 4) * ((q + 7) // 8 * 8)
+
+
 def shard_bounds(in_f: int, world: int) -> List[Tuple[int, int]]:
     per = -(-in_f // world)
     per = -(-per // _SHARD_ALIGN) * _SHARD_ALIGN
@@ -139,13 +161,19 @@ class ActivationExchange:
 
     def __init__(self, weight: torch.nn.Parameter, bias: Optional[torch.nn.Parameter], group, world: int,
                  mode: str, set_skip, weight_view, bias_view, chunks: int = 1, compress: bool = True,
-                 groups: int = 4):
+                 groups: int = 4, source: str = "pooled"):
         if mode not in ("auto", "activations", "sharded", "chunked", "allreduce"):
             raise ValueError(f"ActivationExchange mode must be auto|activations|sharded|chunked|allreduce, got {mode!r}")
         self.weight, self.bias = weight, bias
         self.group, self.world, self.mode = group, world, mode
         self.chunks = max(1, int(chunks))
         self.groups = max(1, int(groups))  # column groups of the zero-suppressed activation path
+        if source not in ("pooled", "rows"):
+            raise ValueError(f"ActivationExchange source must be pooled|rows, got {source!r}")
+        # "pooled": the activation path takes the fused head's pooled input when the layer offers
+        # it (begin_pooled); "rows": always the fc input rows X (begin / begin_groups)
+        self.source = source
+        self._pooled = None  # this step's pooled exchange (dict), or None
         self._works = []  # chunked: the per-chunk all-reduce works of this step
         self._set_skip, self._wview, self._bview = set_skip, weight_view, bias_view
         self.armed = False
@@ -185,7 +213,8 @@ class ActivationExchange:
         if self.world <= 1 or self.mode != "auto":
             return None
         out_f, in_f = self.weight.shape
-        p = choose_path(rows, out_f, in_f, self.world, x_ratio=self.x_ratio if self.compress else 1.0)
+        ratio = 0.5 if self.pooled_capable() else (self.x_ratio if self.compress else 1.0)
+        p = choose_path(rows, out_f, in_f, self.world, x_ratio=ratio)
         # auto's all-reduce regime is the plain bucket all-reduce: the chunked path costs more
         # compute than it saves on the links (W=1 forced: +4.4 ms/step, docs/DISTRIBUTED.md), so
         # it runs only when asked for
@@ -312,7 +341,12 @@ class ActivationExchange:
 
         n = rows * in_f
         zs_ok = self.compress and n < (1 << 31)
-        if path == "activations":
+        pb = pooled_plane(in_f) if self.pooled_capable() else None
+        if path == "activations" and pb is not None:
+            gather("head record all-gather", 128, torch.float32)
+            gather("pooled input (ya) all-gather (fp16)", rows * 32 * pb, torch.float16)
+            gather("dY all-gather", rows * out_f, torch.float32)
+        elif path == "activations":
             if zs_ok:
                 groups = self.column_groups(in_f, self._planes_hint)
                 for gi, (k0, k1) in enumerate(groups):
@@ -406,6 +440,52 @@ class ActivationExchange:
         """Would a forward with ``rows`` rows of ``in_f`` run the grouped zero-suppressed activation
         exchange (begin_groups / group_ready)?"""
         return self.compress and self._eligible(rows) == "activations" and rows * in_f < (1 << 31)
+
+    def pooled_capable(self) -> bool:
+        """Can this layer's activation exchange run from the pooled input (source "pooled", a GPU
+        weight whose inputs are the fused head's 32 square planes)?  The byte model and the preflight
+        price it so; the fused ConvNet head then takes it (a generic Linear still sends its rows)."""
+        return self.source == "pooled" and self.weight.is_cuda and pooled_plane(self.weight.shape[1]) is not None
+
+    def pooled(self, rows: int) -> bool:
+        """Would a forward with ``rows`` rows run the activation exchange from the pooled input
+        (``begin_pooled``)?"""
+        return self.source == "pooled" and self._eligible(rows) == "activations"
+
+    def begin_pooled(self, ya: torch.Tensor, rec: torch.Tensor, P: int) -> None:
+        """Start the activation exchange from the fused head's pooled input (module docstring): the
+        all-gathers of this rank's head record (128 floats, ``ops.head_pooled_record``) and of ya
+        ([rows, 32, PB] fp16), queued where the conv2 forward wrote ya, before the head forward."""
+        from . import distributed as tdist
+
+        ya = ya.detach().contiguous()
+        rec = rec.detach().contiguous().view(-1)
+        W = self.world
+        rec_all = torch.empty((W, rec.numel()), device=rec.device, dtype=rec.dtype)
+        w_rec = tdist.all_gather_into_tensor(rec_all.view(-1), rec, group=self.group, async_op=True)
+        ya_all = torch.empty((W,) + tuple(ya.shape), device=ya.device, dtype=ya.dtype)
+        w_ya = tdist.all_gather_into_tensor(ya_all.view(-1), ya.view(-1), group=self.group, async_op=True)
+        self._pooled = {"ya_all": ya_all, "rec_all": rec_all, "w_ya": w_ya, "w_rec": w_rec, "P": int(P),
+                        "keep": (ya, rec)}
+        self._zs = None
+        self._step_zs = False
+        self._x_local = ya  # keep alive until the exchange completes
+        self._x_work = None
+        out_f, in_f = self.weight.shape
+        self.x_ratio = (ya.numel() * ya.element_size() + rec.numel() * 4) / float(ya.shape[0] * in_f * 4)
+        self.active = "activations"
+        self._set_skip(True)
+
+    def _pooled_update(self, p, dy_all, out, scale: float, lr: float, acc: bool = False):
+        """The fc step from the gathered pooled inputs on the current stream, after both gathers:
+        lr > 0: the weight itself, W -= lr·scale·dy_allᵀX; else ``out`` (=/+=) scale·dy_allᵀX."""
+        from .. import _ext
+
+        p["w_rec"].wait()
+        p["w_ya"].wait()
+        mode = 0 if lr else (2 if acc else 1)
+        _ext.ops().head_update_pooled(dy_all, p["ya_all"], p["rec_all"], self.weight.data, None if lr else out,
+                                      p["P"], scale, float(lr or 0.0), mode)
 
     def begin_groups(self, rows: int, in_f: int, dev, planes: int = 0):
         """Start a grouped zero-suppressed activation exchange: returns the column groups; the caller
@@ -787,6 +867,8 @@ class ActivationExchange:
         keep = (self._dy, self._x_buf, self._x_local)  # used on the side stream
         keep = tuple(t for t in keep if not isinstance(t, list)) + tuple(self._x_local or ()) \
             if isinstance(self._x_local, list) else keep
+        if self._pooled is not None:
+            keep = keep + (self._pooled["ya_all"], self._pooled["rec_all"]) + self._pooled["keep"]
         z = getattr(self, "_zs_decode_pending", None)
         if isinstance(z, tuple):  # grouped activation step: every group's buffers
             for zg in z[1]:
@@ -848,6 +930,7 @@ class ActivationExchange:
             ev_dy = torch.cuda.Event()
             ev_dy.record(side)
         z, self._zs = self._zs, None
+        pooled, self._pooled = self._pooled, None
         x_work, x_dense = self._x_work, self._x_buf
         xl = self._x_local  # (captured: _done() below clears the attribute before update() runs)
         in_f = self.weight.shape[1]
@@ -902,6 +985,9 @@ class ActivationExchange:
                 from .. import _ext
 
                 x_buf = None
+                if pooled is not None:
+                    ex._pooled_update(pooled, dy_all, None, scale, lr)
+                    return
                 if z is not None:
                     if not ex._zs_check(z):
                         if ex._zs_fused(z, (weight.data,)):
@@ -923,6 +1009,7 @@ class ActivationExchange:
 
         param_fence.defer(weight, _Update())
         fused_update.applied(weight)
+        self._pooled_tag = pooled is not None
         self._done()
         return True
 
@@ -951,6 +1038,10 @@ class ActivationExchange:
         rows = dy.shape[0]
         dy_all = torch.empty((self.world * rows, dy.shape[1]), device=dy.device, dtype=dy.dtype)
         tdist.all_gather_into_tensor(dy_all, dy, group=self.group)
+        pooled, self._pooled = self._pooled, None
+        if pooled is not None:
+            self._finish_pooled(pooled, dy_all)
+            return
         zf = getattr(self, "_zs_decode_pending", None)
         # (the bucket slot dW may be written to is 256-byte aligned with rows of K % 4 == 0 floats,
         # which _zs_fused checks; it is not requested here, so the update-only path never allocates it)
@@ -1005,11 +1096,38 @@ class ActivationExchange:
             self.bias.grad = db
         self._done()
 
+    def _finish_pooled(self, pooled, dy_all):
+        """``_finish`` of a pooled step: the update-only step (optimizer-in-backward), or dW into
+        the bucket slot (accumulated under no_sync as ``_targets`` sets up) and db."""
+        from ..ops import fused_update
+
+        scale = 1.0 / self.world
+        lr = fused_update.take(self.weight, exchanged=True)
+        with torch.no_grad():
+            if lr:
+                (_, _), (db, acc_b) = self._targets(weight=False)
+                self._pooled_update(pooled, dy_all, None, scale, float(lr))
+            else:
+                (dw, acc_w), (db, acc_b) = self._targets()
+                self._pooled_update(pooled, dy_all, dw, scale, 0.0, acc_w)
+                self.weight.grad = dw
+            if db is not None:
+                s_b = dy_all.sum(0).mul_(scale)
+                db.add_(s_b) if acc_b else db.copy_(s_b)
+        if self.bias is not None:
+            self.bias.grad = db
+        if lr:
+            fused_update.applied(self.weight)
+        self._pooled_tag = True
+        self._done()
+
     def _done(self):
         self.last_path = "activation-exchange" if self.active == "activations" else "sharded-exchange"
         if self._step_zs:  # (under the deferred update the count check runs in the next forward)
             self.last_path += "(zs)"
-        self._step_zs = False
+        elif getattr(self, "_pooled_tag", False):
+            self.last_path += "(pooled)"
+        self._step_zs = self._pooled_tag = False
         self._x_buf = self._x_work = self._dy = self._x_local = None
         self.active = None
         self.steps_exchanged += 1
