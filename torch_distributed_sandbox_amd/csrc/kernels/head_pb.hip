@@ -4,7 +4,7 @@
 // max_pool2d_with_indices, addmm and their backward ops).
 //
 // The max-pool itself is resolved by the conv2 forward: it writes ya = y2 at each window's
-// argmax (conv2_fwd2.hip), so the head streams ya (B x 72 MB at 3000^2) instead of y2 (B x
+// argmax (conv2_fwd2.hip), so the head streams ya (B x 36 MB in fp16 at 3000^2) instead of y2 (B x
 // 288 MB) and both directions are pure streams over the fc weight (720 MB):
 //
 //   forward : X = relu(a*ya + b);  logits[b][j] = sum X[b][k] W[j][k]           (+ X rows for

@@ -220,7 +220,7 @@ class _Layer2Link:
     separate autograd nodes so the fc gradient's AccumulateGrad — and with it the DDP bucket
     all-reduce — fires before the conv2 backward runs."""
 
-    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update", "labels", "ce", "pack")
+    __slots__ = ("g2m", "kbuf", "aff2", "mag", "bn_done", "fc_update", "labels", "ce", "pack", "pooled")
 
     def __init__(self):
         self.fc_update = None  # the activation exchange's grouped deferred update, run range by range
@@ -228,6 +228,7 @@ class _Layer2Link:
         self.mag = None
         self.labels = None  # the batch's labels (attach_labels) -> ce = (labels, loss, dlogits) from the head
         self.ce = None
+        self.pooled = False  # the activation exchange started from the pooled input (forward below)
 
 
 # The small reductions behind BN2 (forward statistics, backward constants) and the logits run
@@ -324,11 +325,9 @@ class _Head(torch.autograd.Function):
         P = y2.shape[1]
         B, K = ya.shape[0], wfc.shape[1]
         upd, link.fc_update = link.fc_update, None
-        pooled = link.bn_done and ex is not None and B <= 8 and ex.pooled(B)
+        pooled = link.pooled  # (its gathers were started right after the conv2 forward: forward below)
         if pooled:
-            # the activation exchange from the pooled input (parallel/factored.py "pooled"): ya and
-            # this rank's head constants leave now, before the head forward; no X rows are written
-            ex.begin_pooled(ya, ops.head_pooled_record(bn_b, b2, link.mag), P)
+            pass
         elif link.bn_done and ex is not None and _FUSED_FIN and B <= 8 and ex.grouped(B, K):
             logits = _head_forward_grouped(ops, ya, bn_b, b2, wfc, bfc, P, ex, upd, link)
             ctx.save_for_backward(ya, bn_a, bn_b, b2, g2, wfc)
@@ -472,6 +471,15 @@ def forward(model, x):
     y2, ya, bn_a, bn_b = _Conv2.apply(p1, conv2.weight, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
                                       bn2.running_var, bn2.num_batches_tracked, float(bn2.momentum), float(bn2.eps),
                                       link, link1)
+    # the activation exchange from the pooled input (parallel/factored.py "pooled"): ya and this
+    # rank's head constants leave right here, after the conv2 forward and before the previous step's
+    # deferred fc update and the head forward, which then write no fc input rows
+    ex = factored.get(fc.weight)
+    B = x.shape[0]
+    if ex is not None and link.bn_done and B <= 8 and ex.ready(B) and ex.pooled(B):
+        ops = _ext.ops()
+        ex.begin_pooled(ya, ops.head_pooled_record(bn_b, conv2.bias, link.mag), y2.shape[1])
+        link.pooled = True
     # the fc update may still be running on DDP's side stream (overlap_optimizer), or deferred to
     # here (the activation exchange's update sweep, factored.py _Update): wait / queue it now, after
     # the convolutions were queued, not before.  A grouped update goes to the head forward, which
@@ -479,8 +487,7 @@ def forward(model, x):
     link.fc_update = param_fence.take(fc.weight, "groups")
     param_fence.wait(fc.weight)
     param_fence.wait(fc.bias)
-    ex = factored.get(fc.weight)
-    if ex is not None and not ex.ready(x.shape[0]):
+    if ex is not None and not link.pooled and not ex.ready(x.shape[0]):
         ex = None
     link.labels = _take_labels(x)
     logits = _Head.apply(y2, ya, bn_a, bn_b, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean, bn2.running_var,
