@@ -38,22 +38,26 @@ def test_bench_self_spawn_shared_device(gpu, exchange):
     assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 10
 
 
-@pytest.mark.parametrize("exchange", ["activations", "sharded"])
+@pytest.mark.parametrize("exchange", ["activations", "activations:rows", "sharded"])
 def test_bench_preflight_rccl_native_cu_split(gpu, exchange):
     """The multi-GPU default stack's preflight, at world 1 on the real communicator: rccl-native
     with 32 CUs split off (the comm stream confined to them, maxCTAs 32) and the fc exchange
     forced, so every collective the exchange uses runs once with a bounded wait before the
     warmup and reports its time."""
+    exchange, _, source = exchange.partition(":")
     r = _bench(["--image-size", "1000", "--steps", "2", "--warmup", "1", "--backend", "rccl-native",
-                "--reserve-cus", "32", "--grad-exchange", exchange])
+                "--reserve-cus", "32", "--grad-exchange", exchange, "--exchange-source", source or "pooled"])
     c = r["config"]
     assert c["reserve_cus"] == 32 and c["rccl_max_ctas"] == 32 and c["tier"] == "1/1"
     pf = c["preflight"]
     assert pf["fc_path"] == exchange
     ops = [x["op"] for x in pf["collectives"]]
-    if exchange == "activations":
+    if exchange == "activations" and source == "rows":
         assert ops[:3] == ["zs records all-gather (int32)", "zs values all-gather (first-step capacity)",
                            "dY all-gather"]
+    elif exchange == "activations":  # the pooled source (parallel/factored.py): head records, then ya
+        assert ops[:3] == ["head record all-gather", "pooled input (ya) all-gather (fp16)", "dY all-gather"]
+        assert c["fc_grad"] == "activation-exchange(pooled)"
     else:
         assert "zs segment counts all-gather (int64)" in ops and "updated W shard exchange (per peer)" in ops
     assert ops[-1] == "barrier" and all(x["ms"] > 0 for x in pf["collectives"])
