@@ -542,7 +542,9 @@ def _tune_transport(args, store, rank: int, world: int) -> dict:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dev = torch.device("cuda", local_rank)
     K = 32 * (args.image_size // 4) ** 2
-    path, colls = TT.step_collectives(max(2, world), args.batch_size, 10, K)
+    # (the pooled exchange moves ya in fp16: half the dense rows; the zero-suppressed rows ~0.6)
+    path, colls = TT.step_collectives(max(2, world), args.batch_size, 10, K,
+                                      x_ratio=0.5 if args.exchange_source == "pooled" else 0.6)
     n_probe = [0]
 
     def measure(cfg):

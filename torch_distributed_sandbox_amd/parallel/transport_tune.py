@@ -59,18 +59,20 @@ class StepModel:
                 "window_ms": self.window_ms, "interference": self.interference}
 
 
-# One-MI355X measurements at the bench shape (3000^2, batch 5), ms (docs/DISTRIBUTED.md):
-#  local 2.09: the driver's command at round-6 HEAD (r6_s8: 2.079 / 2.105; BENCH_r05.json 2.065);
-#  exchange 0.95: the forced activation exchange with no CU split minus local (r6_s8: 2.721 - 2.09),
-#    plus the 4 column groups' launches and tails at world > 1 (r6_s8 fx_g4 - fx_32: +0.31);
-#  split[32] 0.08, split[64] 0.30: the forced exchange at --reserve-cus 32 / 64 minus 0 (r6_s8
-#    fx_32 - fx_0; r6s2 fx_64 - fx_0; round 5: 0.09-0.14);
-#  window 2.8: with 4 column groups the first gathers leave ~1.05 ms into the ~3.1 ms step and must
-#    land before the next step's first group update at ~0.75 ms (profiles/r6_s10_forced_exchange_g4_*);
+# One-MI355X measurements at the bench shape (3000^2, batch 5), ms (docs/DISTRIBUTED.md "The pooled
+# source"), for the default activation exchange (the pooled input, round 6 end):
+#  local 1.93: the driver's command at round-6 HEAD (r6_s25 1.916-1.929, r6_s27 / r6_s28 1.927-1.949);
+#  exchange 0.35: the forced pooled exchange with no CU split minus local, same box (r6_s27 +0.30,
+#    r6_s28 +0.39, r6_s29 +0.36, r6_s31 +0.33);
+#  split[32] 0.14: the forced exchange at --reserve-cus 32 minus 0 (r6_s27 0.19, r6_s28 0.10,
+#    r6_s29 0.12, r6_s31 0.15); split[64] 0.30: the zero-suppressed rows' r6s2 fx_64 - fx_0 (not
+#    re-measured for the pooled source);
+#  window 2.4: the gathers leave ~0.70 ms into the ~2.4 ms step and must land before the next step's
+#    update at ~0.69 ms: about one step (profiles/r6_s29_forced_pooled_exchange_kernel_stats.md);
 #  interference 0.48: a 3 ms collective of 32 RCCL-sized workgroups beside the unsplit step
 #    added 1.44 ms (profiles/r2_cu_split.md).
-DEFAULT_MODEL = StepModel(local_ms=2.09, exchange_ms=0.95, split_ms={0: 0.0, 32: 0.08, 64: 0.30},
-                          window_ms=2.8, interference=0.48)
+DEFAULT_MODEL = StepModel(local_ms=1.93, exchange_ms=0.35, split_ms={0: 0.0, 32: 0.14, 64: 0.30},
+                          window_ms=2.4, interference=0.48)
 
 
 def predict_ms(cfg: TransportConfig, link_ms: float, model: StepModel = DEFAULT_MODEL) -> float:
