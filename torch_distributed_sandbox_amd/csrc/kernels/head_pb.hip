@@ -31,8 +31,11 @@
 //         picked per wave, so no store straddles a 16-B granule -- misaligned dwordx4 stores of
 //         the weight update cost 14% of the backward,
 //   g2m : 4 fp16 values per image (planar), dW / updated W: one 4-float group per class.
-// No LDS and no barriers in the stream: the next chunk's loads are issued before the current
-// one is reduced.  64-bit indexing throughout (no buffer descriptors).
+// No LDS and no barriers in the stream.  One load set per thread: a chunk's loads are issued right
+// before their use and the latency is left to occupancy -- two sets in alternation (the next chunk's
+// loads in flight while the current one is reduced) held 236 / 202 VGPRs in the forward / backward,
+// 2 waves per SIMD; one set holds 140 / 149, 3 waves, and measured 10 / 4 us faster in the step
+// (r6_s36, r6_s37).  64-bit indexing throughout (no buffer descriptors).
 #include "bf16x3.h"
 #include "common.h"
 #include "ce_small.h"
@@ -145,9 +148,7 @@ struct HPLoad {
   uint2 y[NB];
   float4 w[10];
   int sh, nvalid;  // this lane's edge geometry for fix()
-  // the loads only: their consumers (fix(), the reduction) run one iteration later, so the wait
-  // for them is vmcnt(#loads of the NEXT chunk) -- an edge fix-up right after the loads made
-  // it a vmcnt(0) on the prefetch and serialised every chunk on its own latency
+  // the loads only (fix() and the reduction consume them)
   __device__ __forceinline__ void issue(const unsigned short* __restrict__ ya, const float* W, const PBGeom& g, const HPThread& th,
                                         int c, int R, int b0, int NC) {
     const int64_t plane = g.plane(), QQ = (int64_t)g.Q * g.Q;
@@ -273,13 +274,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const unsigned 
   // iteration i: block row R0 + i / nch, chunk (32 blocks) i % nch of the row
   const int nch = (g.Q8 + 31) / 32;
   const int R0 = band * HP_BAND, nit = (min(g.Q4, R0 + HP_BAND) - R0) * nch;
-  // two load sets in alternation (no register copy): chunk i+1's loads are issued, into the other
-  // set, before chunk i is consumed, on every path (past the end: the last chunk again, unused)
-  HPLoad<NB> ld0, ld1;
-  auto issue = [&](HPLoad<NB>& L, int i) {
-    const int ii = i < nit ? i : nit - 1;
-    L.issue(ya, W, g, HPThread(ii % nch), c, R0 + ii / nch, b0, NC);
-  };
+  HPLoad<NB> ld;  // one load set (file header)
+  auto issue = [&](HPLoad<NB>& L, int i) { L.issue(ya, W, g, HPThread(i % nch), c, R0 + i / nch, b0, NC); };
   auto body = [&](HPLoad<NB>& cur, int i) {
     const int R = R0 + i / nch;
     const HPThread th(i % nch);
@@ -320,13 +316,10 @@ __global__ __launch_bounds__(HP_THREADS) void head_fwd_pb_kernel(const unsigned 
       wmx[j] = fmaxf(fmaxf(wmx[j], fmaxf(fabsf(w4.x), fabsf(w4.y))), fmaxf(fabsf(w4.z), fabsf(w4.w)));
     }
   };
-  if (nit > 0) issue(ld0, 0);
 #pragma unroll 1
-  for (int i = 0; i < nit; i += 2) {
-    issue(ld1, i + 1);
-    body(ld0, i);
-    issue(ld0, i + 2);
-    if (i + 1 < nit) body(ld1, i + 1);
+  for (int i = 0; i < nit; ++i) {
+    issue(ld, i);
+    body(ld, i);
   }
   // deterministic workgroup reduction: waves (DPP), then 4 wave partials in fixed order
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -482,12 +475,8 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
   uint32_t gmx = 0u;  // max |g2m| bits
   const int nch = (g.Q8 + 31) / 32;
   const int R0 = band * HP_BAND_B, nit = (min(g.Q4, R0 + HP_BAND_B) - R0) * nch;
-  // two load sets in alternation, as in the forward
-  HPLoad<NB> ld0, ld1;
-  auto issue = [&](HPLoad<NB>& L, int i) {
-    const int ii = i < nit ? i : nit - 1;
-    L.issue(ya, W, g, HPThread(ii % nch), c, R0 + ii / nch, b0, NC);
-  };
+  HPLoad<NB> ld;  // one load set, as in the forward
+  auto issue = [&](HPLoad<NB>& L, int i) { L.issue(ya, W, g, HPThread(i % nch), c, R0 + i / nch, b0, NC); };
   auto body = [&](HPLoad<NB>& cur, int i) {
     const int R = R0 + i / nch;
     const HPThread th(i % nch);
@@ -564,13 +553,10 @@ __global__ __launch_bounds__(HP_THREADS) void head_bwd_pb_kernel(
       }
     }
   };
-  if (nit > 0) issue(ld0, 0);
 #pragma unroll 1
-  for (int i = 0; i < nit; i += 2) {
-    issue(ld1, i + 1);
-    body(ld0, i);
-    issue(ld0, i + 2);
-    if (i + 1 < nit) body(ld1, i + 1);
+  for (int i = 0; i < nit; ++i) {
+    issue(ld, i);
+    body(ld, i);
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   gmx = wave_max(gmx);
