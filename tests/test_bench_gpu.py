@@ -13,8 +13,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _bench(args, timeout=240):
+    # a fresh rendezvous for the child: a MASTER_PORT left in this process's environment by another
+    # test's process group (tests/test_comm_gpu.py) is still bound by that group's store
+    env = {k: v for k, v in os.environ.items() if k not in ("MASTER_PORT", "MASTER_ADDR", "RANK", "WORLD_SIZE",
+                                                             "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
     p = subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, capture_output=True, text=True,
-                       timeout=timeout)
+                       timeout=timeout, env=env)
     assert p.returncode == 0, p.stderr[-4000:]
     recs = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(recs) == 1, p.stdout
